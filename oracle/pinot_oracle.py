@@ -1,0 +1,1072 @@
+"""CPU ORACLE for the pinot-core segment query hot path -- TEST INFRASTRUCTURE ONLY.
+
+This module is a literal CPU restatement of the reference's (Java) per-segment query algorithm.
+It exists to CHECK the MI355X path: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import it, and never as the thing measured or shipped.  The product path
+(pinot_amd + libpgx.so) never imports anything from oracle/.
+
+Parity of this oracle is PINNED by the reference's own known-answer tests, frozen as fixtures in
+tests/golden/ (see tests/golden/make_golden.py and tests/test_oracle_golden.py):
+  * AggregationSingleValueQueriesTest.java:43-221 on test_data-sv.avro (all 8 aggregation /
+    group-by cases, with and without the 5-clause filter, including ExecutionStatistics such as
+    numEntriesScannedInFilter=84134, which depends on the exact iterator algebra restated below);
+  * QueryExecutorTest.java:97-200 on simpleData200001.avro (2 segments, combine);
+  * the Java-written v1 segment starTreeSegment.tar.gz (fixed-bit MSB-first decode, dictionaries).
+
+All functions cite the reference file:line they restate.  Paths are relative to
+pinot-core/src/main/java/com/linkedin/pinot/core/.
+"""
+from __future__ import annotations
+
+import heapq
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+EOF = -2147483648  # Constants.EOF (core/common/Constants.java) == Integer.MIN_VALUE
+INT_MAX = 2147483647
+INT_MIN = -2147483648
+MAX_DOC_PER_CALL = 10000  # plan/DocIdSetPlanNode.java:33
+GROUP_BY_BLOCK = 5000  # plan/AggregationGroupByPlanNode.java:53
+MAX_INITIAL_RESULT_HOLDER_CAPACITY = 10000  # operator/aggregation/ResultHolderFactory.java:33
+LONG_MAX = (1 << 63) - 1
+
+
+# ------------------------------------------------------------------------------------------------
+# a-1: fixed-bit forward index decode
+# ------------------------------------------------------------------------------------------------
+def get_num_of_bits(card: int) -> int:
+    """SingleValueUnsortedForwardIndexCreator.getNumOfBits (segment/creator/impl/fwd/...:48-57)."""
+    if card < 2:
+        return 1
+    ret = int(math.ceil(math.log(card) / math.log(2)))
+    return 1 if ret == 0 else ret
+
+
+def _s32(x: int) -> int:
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x & 0x80000000 else x
+
+
+def read_int(buf: bytes, nr_bytes: int, start_bit: int, end_bit: int) -> int:
+    """Literal restatement of PinotDataCustomBitSet.readInt (util/PinotDataCustomBitSet.java:122-155).
+    buf is the big-endian forward-index byte buffer."""
+    bit_length = end_bit - start_bit
+    if bit_length < 16 and end_bit + 32 < nr_bytes * 8:
+        byte_pos = start_bit // 8
+        bit_off = start_bit % 8
+        shift = 32 - (bit_off + bit_length)
+        int_value = _s32(int.from_bytes(buf[byte_pos:byte_pos + 4], "big"))
+        mask = (1 << bit_length) - 1
+        return (int_value >> shift) & mask  # Java '>>' is arithmetic
+    byte_pos = start_bit >> 3
+    start_off = start_bit & 7
+    s = start_off + bit_length
+    end_off = (8 - (s & 7)) & 7
+    nbytes = (s + 7) >> 3
+    number = 0
+    i = -1
+    while True:
+        number |= buf[byte_pos] & 0xFF
+        i += 1
+        byte_pos += 1
+        if i == nbytes - 1:
+            break
+        number <<= 8
+    number >>= end_off
+    number &= (0xFFFFFFFF >> (32 - bit_length))
+    return _s32(number)
+
+
+def decode_fixed_bit(buf: bytes, num_rows: int, bits: int) -> np.ndarray:
+    """v1 FixedBitSingleValueReader.getInt for every row (io/reader/impl/v1/FixedBitSingleValueReader.java:30-58,
+    FixedBitSingleValueMultiColReader.java:87-130): row r occupies bits [r*b, r*b+b)."""
+    n = len(buf)
+    return np.array([read_int(buf, n, r * bits, r * bits + bits) for r in range(num_rows)], dtype=np.int64)
+
+
+def decode_fixed_bit_fast(buf: bytes, num_rows: int, bits: int) -> np.ndarray:
+    """Vectorised equivalent of decode_fixed_bit (checked against it in tests)."""
+    a = np.frombuffer(bytes(buf) + b"\0" * 8, dtype=np.uint8)
+    start = np.arange(num_rows, dtype=np.int64) * bits
+    byte = start >> 3
+    w = np.zeros(num_rows, dtype=np.uint64)
+    for k in range(5):
+        w = (w << np.uint64(8)) | a[byte + k].astype(np.uint64)
+    shift = (40 - (start & 7) - bits).astype(np.uint64)
+    return ((w >> shift) & np.uint64((1 << bits) - 1)).astype(np.int64)
+
+
+# ------------------------------------------------------------------------------------------------
+# Segment model (the oracle builds its own dictionaries from raw column values)
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class OColumn:
+    name: str
+    dtype: str  # INT, LONG, FLOAT, DOUBLE, STRING
+    dictionary: np.ndarray  # sorted distinct values (object array of str for STRING)
+    dict_ids: np.ndarray  # int64 per doc
+    is_sorted: bool
+    has_inverted: bool
+    bits: int
+
+    @property
+    def card(self) -> int:
+        return len(self.dictionary)
+
+    def index_of(self, raw: str) -> int:
+        """Dictionary.indexOf: binary search returning -(insertion)-1 when absent
+        (segment/index/readers/IntDictionary.java:28-37, StringDictionary.java:37-51)."""
+        if self.dtype == "STRING":
+            keys = list(self.dictionary)
+            v = raw
+        elif self.dtype in ("INT", "LONG"):
+            keys = self.dictionary
+            v = int(raw)
+        else:
+            keys = self.dictionary
+            v = float(raw)
+        pos = int(np.searchsorted(np.asarray(keys, dtype=object if self.dtype == "STRING" else None), v, side="left"))
+        if pos < self.card and keys[pos] == v:
+            return pos
+        return -(pos + 1)
+
+    def value_as_double(self, ids: np.ndarray) -> np.ndarray:
+        """Dictionary.readDoubleValues: (double) cast of the dictionary value (IntDictionary.java:50-52)."""
+        return self.dictionary[ids].astype(np.float64)
+
+    def string_of(self, dict_id: int) -> str:
+        """Dictionary.get(dictId).toString() used for string group keys."""
+        v = self.dictionary[dict_id]
+        if self.dtype == "STRING":
+            return v
+        if self.dtype in ("INT", "LONG"):
+            return str(int(v))
+        return repr(float(v))
+
+
+@dataclass
+class OSegment:
+    columns: Dict[str, OColumn]
+    total_docs: int
+    total_raw_docs: int
+
+    @staticmethod
+    def from_raw(raw: Dict[str, np.ndarray], inverted: Sequence[str] = (), dtypes: Dict[str, str] = None,
+                 sorted_override: Dict[str, bool] = None) -> "OSegment":
+        cols = {}
+        n = None
+        for name, vals in raw.items():
+            vals = np.asarray(vals)
+            n = len(vals) if n is None else n
+            dt = (dtypes or {}).get(name)
+            if dt is None:
+                dt = "STRING" if vals.dtype.kind in "SUO" else ("INT" if vals.dtype.kind in "iu" else "DOUBLE")
+            if dt == "STRING":
+                sv = np.array([v.decode() if isinstance(v, bytes) else str(v) for v in vals], dtype=object)
+                dictionary = np.array(sorted(set(sv.tolist())), dtype=object)
+                lookup = {v: i for i, v in enumerate(dictionary)}
+                ids = np.array([lookup[v] for v in sv], dtype=np.int64)
+            else:
+                dictionary, ids = np.unique(vals, return_inverse=True)
+                ids = ids.astype(np.int64)
+            is_sorted = bool(np.all(np.diff(ids) >= 0)) if n > 1 else True
+            if sorted_override and name in sorted_override:
+                is_sorted = sorted_override[name]
+            cols[name] = OColumn(name, dt, dictionary, ids, is_sorted,
+                                 name in inverted or is_sorted, get_num_of_bits(len(dictionary)))
+        return OSegment(cols, n, n)
+
+
+# ------------------------------------------------------------------------------------------------
+# a-4: predicates -> dictId space
+# ------------------------------------------------------------------------------------------------
+def parse_range(rng: str) -> Tuple[str, str, bool, bool]:
+    """RangePredicate (common/predicate/RangePredicate.java:31-57)."""
+    s = rng.strip()
+    lo_s, hi_s = s.split("\t\t")[0], s.split("\t\t")[1]
+    lower = lo_s[1:]
+    upper = hi_s[:-1]
+    inc_lower = (lower == "*") if s.startswith("(") else True
+    inc_upper = (upper == "*") if s.endswith(")") else True
+    return lower, upper, inc_lower, inc_upper
+
+
+@dataclass
+class Evaluator:
+    kind: str  # EQ NEQ IN NOT_IN RANGE
+    match: np.ndarray  # bool[card]: apply(dictId)
+    matching_ids: np.ndarray
+    non_matching_ids: Optional[np.ndarray]
+    always_false: bool
+
+
+def make_evaluator(col: OColumn, leaf: dict) -> Evaluator:
+    """PredicateEvaluatorProvider (operator/filter/predicate/PredicateEvaluatorProvider.java:31-54) and the
+    Equals/NotEquals/In/NotIn/RangeOffline evaluators in the same package."""
+    op = leaf["op"]
+    card = col.card
+    m = np.zeros(card, dtype=bool)
+    if op == "RANGE":
+        lower, upper, inc_lo, inc_hi = parse_range(leaf["values"][0])
+        # RangeOfflineDictionaryPredicateEvaluator.java:30-65
+        start = 0 if lower == "*" else col.index_of(lower)
+        end = card - 1 if upper == "*" else col.index_of(upper)
+        if start < 0:
+            start = -(start + 1)
+        elif not inc_lo and lower != "*":
+            start += 1
+        if end < 0:
+            end = -(end + 1) - 1
+        elif not inc_hi and upper != "*":
+            end -= 1
+        if end >= start:
+            m[start:end + 1] = True
+        ids = np.nonzero(m)[0]
+        return Evaluator(op, m, ids, None, (end - start + 1) <= 0)
+    if op == "EQ":
+        i = col.index_of(leaf["values"][0])
+        if i >= 0:
+            m[i] = True
+        return Evaluator(op, m, np.nonzero(m)[0], None, i < 0)
+    if op == "IN":
+        for v in leaf["values"]:
+            i = col.index_of(v)
+            if i >= 0:
+                m[i] = True
+        ids = np.nonzero(m)[0]
+        return Evaluator(op, m, ids, None, len(ids) == 0)
+    if op == "NEQ":
+        i = col.index_of(leaf["values"][0])
+        m[:] = True
+        non = np.array([i] if i >= 0 else [], dtype=np.int64)
+        if i >= 0:
+            m[i] = False
+        return Evaluator(op, m, np.nonzero(m)[0], non, False)
+    if op == "NOT_IN":
+        m[:] = True
+        non = set()
+        for v in leaf["values"]:
+            i = col.index_of(v)
+            if i >= 0:
+                non.add(i)
+        for i in non:
+            m[i] = False
+        return Evaluator(op, m, np.nonzero(m)[0], np.array(sorted(non), dtype=np.int64), False)
+    raise ValueError(op)
+
+
+# ------------------------------------------------------------------------------------------------
+# a-5..a-12: literal restatement of the filter DocIdSet / iterator algebra (for ExecutionStatistics)
+# ------------------------------------------------------------------------------------------------
+class _ScanSet:
+    """ScanBasedSingleValueDocIdSet + SVScanDocIdIterator (operator/docidsets/ScanBasedSingleValueDocIdSet.java:30-85,
+    operator/dociditerators/SVScanDocIdIterator.java:40-155)."""
+    kind = "scan"
+
+    def __init__(self, col: OColumn, ev: Evaluator, start: int, end: int):
+        self.ids = col.dict_ids
+        self.match = ev.match
+        self.ev = ev
+        self.scanned = 0
+        # The iterator's alwaysFalse EOF state (:42-45) is overwritten by the DocIdSet's setStartDocId/setEndDocId
+        # (ScanBasedFilterOperator.java:81-87); only applyAnd re-checks alwaysFalse.
+        self._set_start(start)
+        self.end = end
+
+    def _set_start(self, s):
+        self.cur = s - 1
+        self.start = s
+
+    # FilterBlockDocIdSet interface
+    def min_doc(self):
+        return self.start
+
+    def max_doc(self):
+        return self.end
+
+    def set_start(self, s):
+        self._set_start(s)
+
+    def set_end(self, e):
+        self.end = e
+
+    def iterator(self):
+        return self
+
+    def entries(self):
+        return self.scanned
+
+    # iterator
+    def is_match(self, doc):
+        if self.cur == EOF:
+            return False
+        self.scanned += 1
+        return bool(self.match[self.ids[doc]])
+
+    def advance(self, target):
+        if self.cur == EOF:
+            return EOF
+        if target < self.start:
+            target = self.start
+        elif target > self.end:
+            self.cur = EOF
+        if self.cur >= target:
+            return self.cur
+        self.cur = target - 1
+        return self.next()
+
+    def next(self):
+        if self.cur == EOF:
+            return EOF
+        n = len(self.ids)
+        while self.cur + 1 < n and self.cur < self.end:
+            self.cur += 1
+            self.scanned += 1
+            if self.match[self.ids[self.cur]]:
+                return self.cur
+        self.cur = EOF
+        return EOF
+
+    def apply_and(self, answer: List[int]) -> List[int]:
+        res = []
+        if self.ev.always_false:
+            return res
+        doc = -1
+        it = iter(answer)
+        for d in it:
+            if not doc < self.end:
+                break
+            doc = d
+            if doc >= self.start:
+                self.scanned += 1
+                if self.match[self.ids[doc]]:
+                    res.append(doc)
+        return res
+
+
+class _ListIter:
+    """BitmapDocIdIterator (clipped, operator/dociditerators/BitmapDocIdIterator.java:40-84) or
+    RangelessBitmapDocIdIterator (:30-80) over a sorted doc list."""
+
+    def __init__(self, docs: Sequence[int], start=None, end=None):
+        self.docs = docs
+        self.pos = 0
+        self.cur = -1
+        self.start = start
+        self.end = end
+
+    def _raw_next(self):
+        if self.pos >= len(self.docs):
+            return None
+        v = self.docs[self.pos]
+        self.pos += 1
+        return v
+
+    def next(self):
+        if self.cur == EOF or self.pos >= len(self.docs):
+            self.cur = EOF
+            return EOF
+        self.cur = self._raw_next()
+        if self.start is not None:
+            while self.cur < self.start and self.pos < len(self.docs):
+                self.cur = self._raw_next()
+            if self.cur < self.start or self.end < self.cur:
+                self.cur = EOF
+        return self.cur
+
+    def advance(self, target):
+        if self.cur == target:
+            return self.cur
+        c = self.next()
+        while c < target and c != EOF:
+            c = self.next()
+        return c
+
+
+class _BitmapSet:
+    """BitmapDocIdSet (operator/docidsets/BitmapDocIdSet.java:55-145)."""
+    kind = "bitmap"
+
+    def __init__(self, col: OColumn, ev: Evaluator, start: int, end: int):
+        if ev.kind in ("NEQ", "NOT_IN"):
+            ids, exclusion = ev.non_matching_ids, True
+        else:
+            ids, exclusion = ev.matching_ids, False
+        docs = np.nonzero(np.isin(col.dict_ids, ids))[0]
+        if exclusion:
+            inside = np.zeros(len(col.dict_ids), dtype=bool)
+            inside[start:end + 1] = True
+            m = np.zeros(len(col.dict_ids), dtype=bool)
+            m[docs] = True
+            m[inside] = ~m[inside]
+            docs = np.nonzero(m)[0]
+        self.answer = docs.tolist()
+        self.start, self.end = start, end
+
+    def min_doc(self):
+        return self.start
+
+    def max_doc(self):
+        return self.end
+
+    def set_start(self, s):
+        self.start = s
+
+    def set_end(self, e):
+        self.end = e
+
+    def iterator(self):
+        return _ListIter(self.answer, self.start, self.end)
+
+    def entries(self):
+        return 0
+
+
+class _SortedIter:
+    """SortedDocIdIterator (operator/dociditerators/SortedDocIdIterator.java:35-100)."""
+
+    def __init__(self, pairs):
+        self.pairs = pairs
+        self.pp = 0
+        self.cur = -1
+
+    def advance(self, target):
+        P = self.pairs
+        if self.pp == len(P) or target > P[-1][1]:
+            self.pp = len(P)
+            self.cur = EOF
+            return EOF
+        if self.cur >= target:
+            return self.cur
+        while self.pp < len(P):
+            if P[self.pp][0] > target:
+                self.cur = P[self.pp][0]
+                break
+            elif P[self.pp][0] <= target <= P[self.pp][1]:
+                self.cur = target
+                break
+            self.pp += 1
+        if self.pp == len(P):
+            self.cur = EOF
+        return self.cur
+
+    def next(self):
+        P = self.pairs
+        if self.pp == len(P) or self.cur > P[-1][1]:
+            self.pp = len(P)
+            self.cur = EOF
+            return EOF
+        self.cur += 1
+        if self.pp < len(P) and self.cur > P[self.pp][1]:
+            self.pp += 1
+            self.cur = EOF if self.pp == len(P) else P[self.pp][0]
+        elif self.cur < P[self.pp][0]:
+            self.cur = P[self.pp][0]
+        return self.cur
+
+
+class _EmptyIter:
+    def next(self):
+        return EOF
+
+    def advance(self, t):
+        return EOF
+
+
+class _SortedSet:
+    """SortedInvertedIndexBasedFilterOperator.nextFilterBlock (operator/filter/SortedInvertedIndexBasedFilterOperator.java:71-193)
+    + SortedDocIdSet (operator/docidsets/SortedDocIdSet.java:30-100)."""
+    kind = "sorted"
+
+    def __init__(self, col: OColumn, ev: Evaluator, start: int, end: int):
+        ids = col.dict_ids
+        # SortedInvertedIndexReader.getMinMaxRangeFor: per-dictId inclusive [first,last] doc
+        first = np.full(col.card, -1, dtype=np.int64)
+        last = np.full(col.card, -2, dtype=np.int64)
+        u, f = np.unique(ids, return_index=True)
+        first[u] = f
+        u2, l2 = np.unique(ids[::-1], return_index=True)
+        last[u2] = len(ids) - 1 - l2
+        additive = ev.kind in ("EQ", "IN", "RANGE")
+        d = np.sort(ev.matching_ids if additive else ev.non_matching_ids)
+        pairs = []
+        if len(d):
+            def clip(p):  # IntRanges.clip (operator/filter/IntRanges.java)
+                return [max(p[0], start), min(p[1], end)]
+
+            def invalid(p):
+                return p[1] < p[0]
+
+            lastp = clip([int(first[d[0]]), int(last[d[0]])])
+            for di in d[1:]:
+                cur = clip([int(first[di]), int(last[di])])
+                if invalid(lastp):
+                    lastp = cur
+                    continue
+                if cur[0] <= lastp[1] + 1 and lastp[0] <= cur[1] + 1:  # rangesAreMergeable
+                    lastp = [min(lastp[0], cur[0]), max(lastp[1], cur[1])]
+                else:
+                    if not invalid(lastp):
+                        pairs.append(lastp)
+                    lastp = cur
+            if not invalid(lastp):
+                pairs.append(lastp)
+        if not additive:
+            newp = []
+            if not pairs:
+                newp.append([start, end])
+            else:
+                r = [start, pairs[0][0] - 1]
+                if r[1] >= r[0]:
+                    newp.append(r)
+                for a, b in zip(pairs[:-1], pairs[1:]):
+                    r = [a[1] + 1, b[0] - 1]
+                    if r[1] >= r[0]:
+                        newp.append(r)
+                r = [pairs[-1][1] + 1, end]
+                if r[1] >= r[0]:
+                    newp.append(r)
+            pairs = newp
+        self.pairs = pairs
+
+    def min_doc(self):
+        return self.pairs[0][0] if self.pairs else 0
+
+    def max_doc(self):
+        return self.pairs[-1][1] if self.pairs else 0
+
+    def set_start(self, s):
+        pass
+
+    def set_end(self, e):
+        pass
+
+    def iterator(self):
+        return _SortedIter(self.pairs) if self.pairs else _EmptyIter()
+
+    def entries(self):
+        return 0
+
+    def docs(self):
+        out = []
+        for a, b in self.pairs:
+            out.extend(range(a, b + 1))
+        return out
+
+
+class _AndIter:
+    """AndDocIdIterator (operator/dociditerators/AndDocIdIterator.java:38-122)."""
+
+    def __init__(self, iters, scan_flags):
+        idx = sum(1 for f in scan_flags if f == "index")
+        sc = sum(1 for f in scan_flags if f == "scan")
+        if idx > 0 and sc > 0:
+            self.has_scan = True
+            self.iters = [it for it, f in zip(iters, scan_flags) if f != "scan"]
+            self.scans = [it for it, f in zip(iters, scan_flags) if f == "scan"]
+        else:
+            self.has_scan = False
+            self.iters = list(iters)
+            self.scans = []
+        self.cur = -1
+        self.cmax = -1
+
+    def advance(self, target):
+        if self.cur == EOF:
+            return EOF
+        if self.cur >= target:
+            return self.cur
+        self.cmax = target - 1
+        return self.next()
+
+    def next(self):
+        if self.cur == EOF:
+            return EOF
+        self.cmax += 1
+        i = 0
+        n = len(self.iters)
+        while i < n:
+            p = self.iters[i].advance(self.cmax)
+            if p == EOF:
+                self.cmax = EOF
+                break
+            if p > self.cmax:
+                self.cmax = p
+                if i > 0:
+                    i = -1
+            if self.has_scan and i == n - 1:
+                for s in self.scans:
+                    if not s.is_match(self.cmax):
+                        i = -1
+                        self.cmax += 1
+                        break
+            i += 1
+        self.cur = self.cmax
+        return self.cur
+
+
+class _OrIter:
+    """OrDocIdIterator (operator/dociditerators/OrDocIdIterator.java:30-153)."""
+
+    def __init__(self, iters, lo, hi):
+        self.iters = iters
+        self.inq = [False] * len(iters)
+        self.q = []  # heap of (doc, idx)
+        self.cur = -1
+        self.lo, self.hi = lo, hi
+
+    def advance(self, target):
+        if self.cur == EOF:
+            return EOF
+        if target < self.lo:
+            target = self.lo
+        elif target > self.hi:
+            self.cur = EOF
+            return EOF
+        keep = []
+        for d, i in self.q:
+            if d < target:
+                self.inq[i] = False
+            else:
+                keep.append((d, i))
+        self.q = keep
+        heapq.heapify(self.q)
+        for i, it in enumerate(self.iters):
+            if not self.inq[i]:
+                nd = it.advance(target)
+                if nd != EOF:
+                    heapq.heappush(self.q, (nd, i))
+                self.inq[i] = True
+        self.cur = self.q[0][0] if self.q else EOF
+        return self.cur
+
+    def next(self):
+        if self.cur == EOF:
+            return EOF
+        while self.q and self.q[0][0] <= self.cur:
+            d, i = heapq.heappop(self.q)
+            self.inq[i] = False
+        self.cur += 1
+        for i, it in enumerate(self.iters):
+            if not self.inq[i]:
+                nd = it.advance(self.cur)
+                if nd != EOF:
+                    heapq.heappush(self.q, (nd, i))
+                self.inq[i] = True
+        self.cur = self.q[0][0] if self.q else EOF
+        return self.cur
+
+
+class _AndSet:
+    """AndBlockDocIdSet (operator/docidsets/AndBlockDocIdSet.java:49-63,146-266)."""
+    kind = "and"
+
+    def __init__(self, children):
+        self.children = children
+        self.lo, self.hi = INT_MIN, INT_MAX
+        self._update()
+
+    def _update(self):
+        for c in self.children:
+            self.lo = max(self.lo, c.min_doc())
+            self.hi = min(self.hi, c.max_doc())
+        for c in self.children:
+            c.set_start(self.lo)
+            c.set_end(self.hi)
+
+    def min_doc(self):
+        return self.lo
+
+    def max_doc(self):
+        return self.hi
+
+    def set_start(self, s):
+        self.lo = max(self.lo, s)
+        self._update()
+
+    def set_end(self, e):
+        self.hi = min(self.hi, e)
+        self._update()
+
+    def entries(self):
+        return sum(c.entries() for c in self.children)
+
+    def iterator(self):
+        ranges, bitmaps, scans, rest = [], [], [], []
+        for c in self.children:
+            if c.kind == "sorted":
+                ranges.append(c)
+            elif c.kind == "bitmap":
+                bitmaps.append(c)
+            elif c.kind == "scan":
+                scans.append(c)
+            else:
+                rest.append(c.iterator())
+        if not bitmaps and not ranges:
+            its = [c.iterator() for c in self.children]
+            return _AndIter(its, [_flag(c) for c in self.children])
+        answer = None
+        if ranges:
+            # SortedRangeIntersection.intersectSortedRangeSets (util/SortedRangeIntersection.java:31)
+            sets = [set(r.docs()) for r in ranges]
+            answer = set.intersection(*sets) if sets else set()
+        for b in bitmaps:
+            answer = set(b.answer) if answer is None else (answer & set(b.answer))
+        answer = sorted(answer)
+        for s in scans:
+            it = s.iterator()
+            res = set(it.apply_and(answer))
+            answer = [d for d in answer if d in res]
+        ans_it = _ListIter(answer)
+        if not rest:
+            return ans_it
+        return _AndIter([ans_it] + rest, ["index"] + ["other"] * len(rest))
+
+
+class _OrSet:
+    """OrBlockDocIdSet (operator/docidsets/OrBlockDocIdSet.java:42-135)."""
+    kind = "or"
+
+    def __init__(self, children):
+        self.children = children
+        self.lo, self.hi = INT_MAX, INT_MIN
+        self._update()
+
+    def _update(self):
+        for c in self.children:
+            self.lo = min(self.lo, c.min_doc())
+            self.hi = max(self.hi, c.max_doc())
+        for c in self.children:
+            c.set_start(self.lo)
+            c.set_end(self.hi)
+
+    def min_doc(self):
+        return self.lo
+
+    def max_doc(self):
+        return self.hi
+
+    def set_start(self, s):
+        self.lo = min(self.lo, s)
+        self._update()
+
+    def set_end(self, e):
+        self.hi = max(self.hi, e)
+        self._update()
+
+    def entries(self):
+        return sum(c.entries() for c in self.children)
+
+    def iterator(self):
+        if any(c.kind == "bitmap" for c in self.children):
+            raw, allb = [], set()
+            for c in self.children:
+                if c.kind == "sorted":
+                    allb |= set(c.docs())
+                elif c.kind == "bitmap":
+                    allb |= set(c.answer)
+                else:
+                    raw.append(c.iterator())
+            raw.append(_ListIter(sorted(allb), self.lo, self.hi))
+            its = raw
+        else:
+            its = [c.iterator() for c in self.children]
+        return _OrIter(its, self.lo, self.hi)
+
+
+class _MatchAllSet:
+    """MatchEntireSegmentOperator / SizeBasedDocIdIterator (operator/filter/MatchEntireSegmentOperator.java:25-44)."""
+    kind = "all"
+
+    def __init__(self, n):
+        self.n = n
+        self.cur = -1
+
+    def iterator(self):
+        return self
+
+    def next(self):
+        self.cur += 1
+        if self.cur >= self.n:
+            self.cur = EOF
+        return self.cur
+
+    def entries(self):
+        return 0
+
+
+def _flag(c):
+    if c.kind == "scan":
+        return "scan"
+    if c.kind in ("bitmap", "sorted"):
+        return "index"
+    return "other"
+
+
+_PRIORITY = {"sorted": 0, "and": 1, "bitmap": 2, "scan": 3, "or": 4}
+
+
+def build_filter(seg: OSegment, tree: Optional[dict]):
+    """FilterPlanNode.constructPhysicalOperator + reorder (plan/FilterPlanNode.java:77-170)."""
+    if tree is None:
+        return _MatchAllSet(seg.total_raw_docs)
+    start, end = 0, seg.total_raw_docs - 1
+    op = tree["op"]
+    if op in ("AND", "OR"):
+        kids = [build_filter(seg, c) for c in tree["children"]]
+        kids = sorted(kids, key=lambda k: _PRIORITY[k.kind])  # Collections.sort is stable
+        return _AndSet(kids) if op == "AND" else _OrSet(kids)
+    col = seg.columns[tree["column"]]
+    ev = make_evaluator(col, tree)
+    if col.has_inverted and op != "RANGE":
+        if col.is_sorted:
+            return _SortedSet(col, ev, start, end)
+        return _BitmapSet(col, ev, start, end)
+    return _ScanSet(col, ev, start, end)
+
+
+def filter_docs(seg: OSegment, tree: Optional[dict]) -> Tuple[np.ndarray, int]:
+    """BReusableFilteredDocIdSetOperator (operator/BReusableFilteredDocIdSetOperator.java:68-109): the ascending
+    matching docIds and numEntriesScannedInFilter, via the literal iterator algebra."""
+    s = build_filter(seg, tree)
+    it = s.iterator()
+    out = []
+    while True:
+        d = it.next()
+        if d == EOF:
+            break
+        out.append(d)
+    return np.array(out, dtype=np.int64), int(s.entries())
+
+
+def filter_mask_vectorized(seg: OSegment, tree: Optional[dict]) -> np.ndarray:
+    """Set semantics of the same filter (docs in [0,totalRawDocs) satisfying the predicate tree)."""
+    n = seg.total_raw_docs
+    if tree is None:
+        return np.ones(n, dtype=bool)
+    op = tree["op"]
+    if op == "AND":
+        m = np.ones(n, dtype=bool)
+        for c in tree["children"]:
+            m &= filter_mask_vectorized(seg, c)
+        return m
+    if op == "OR":
+        m = np.zeros(n, dtype=bool)
+        for c in tree["children"]:
+            m |= filter_mask_vectorized(seg, c)
+        return m
+    col = seg.columns[tree["column"]]
+    ev = make_evaluator(col, tree)
+    return ev.match[col.dict_ids[:n]]
+
+
+# ------------------------------------------------------------------------------------------------
+# a-13..a-17, a-20: aggregation / group-by execution
+# ------------------------------------------------------------------------------------------------
+FN_DEFAULT = {"count": 0.0, "sum": 0.0, "min": math.inf, "max": -math.inf}
+
+
+def _projection_columns(q: dict) -> List[str]:
+    cols = []
+    for a in q["aggregations"]:
+        if a["fn"] != "count" and a["column"] not in cols:
+            cols.append(a["column"])
+    for g in (q.get("group_by") or {}).get("columns", []):
+        if g not in cols:
+            cols.append(g)
+    return cols
+
+
+def _blocks(docs: np.ndarray, size: int):
+    for i in range(0, len(docs), size):
+        yield docs[i:i + size]
+
+
+def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
+    """AggregationOperator.getNextBlock + DefaultAggregationExecutor (operator/aggregation/AggregationOperator.java:77-104,
+    DefaultAggregationExecutor.java:94-303) with Count/Sum/Min/Max/Avg.aggregate."""
+    if literal_filter:
+        docs, scanned = filter_docs(seg, q.get("filter"))
+    else:
+        docs, scanned = np.nonzero(filter_mask_vectorized(seg, q.get("filter")))[0], None
+    holders = []
+    for a in q["aggregations"]:
+        fn = a["fn"]
+        holders.append([0.0, 0] if fn == "avg" else FN_DEFAULT[fn])
+    for blk in _blocks(docs, MAX_DOC_PER_CALL):
+        for k, a in enumerate(q["aggregations"]):
+            fn = a["fn"]
+            if fn == "count":
+                holders[k] = holders[k] + float(len(blk))  # CountAggregationFunction.aggregate:43-48
+                continue
+            col = seg.columns[a["column"]]
+            v = col.value_as_double(col.dict_ids[blk])
+            if fn == "sum":  # SumAggregationFunction.aggregate:45-56 (sequential double sum)
+                s = float(np.cumsum(v)[-1]) if len(v) else 0.0
+                holders[k] = holders[k] + s
+            elif fn == "min":
+                mn = float(v.min()) if len(v) else math.inf
+                if mn < holders[k]:
+                    holders[k] = mn
+            elif fn == "max":
+                mx = float(v.max()) if len(v) else -math.inf
+                if mx > holders[k]:
+                    holders[k] = mx
+            elif fn == "avg":  # AvgAggregationFunction.aggregate:47-65
+                s = float(np.cumsum(v)[-1]) if len(v) else 0.0
+                holders[k] = [holders[k][0] + s, holders[k][1] + len(blk)]
+    results = []
+    for k, a in enumerate(q["aggregations"]):
+        if a["fn"] == "count":
+            results.append(int(holders[k]))  # MutableLongValue((long) double)
+        elif a["fn"] == "avg":
+            results.append((float(holders[k][0]), int(holders[k][1])))
+        else:
+            results.append(float(holders[k]))
+    n_proj = len(_projection_columns(q))
+    stats = [len(docs), scanned, len(docs) * n_proj, seg.total_raw_docs]
+    return {"results": results, "stats": stats}
+
+
+def group_key_mode(cards: Sequence[int]) -> Tuple[str, int]:
+    """DefaultGroupKeyGenerator storage-type choice (operator/aggregation/groupby/DefaultGroupKeyGenerator.java:131-186)."""
+    prod = 1
+    for c in cards:
+        if prod > LONG_MAX // c:
+            return "ARRAY_MAP_BASED", LONG_MAX
+        prod *= c
+    if prod > MAX_INITIAL_RESULT_HOLDER_CAPACITY:
+        return "LONG_MAP_BASED", prod
+    return "ARRAY_BASED", prod
+
+
+def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
+    """AggregationGroupByOperator + DefaultGroupByExecutor + DefaultGroupKeyGenerator + {fn}.aggregateGroupBySV
+    (operator/aggregation/groupby/AggregationGroupByOperator.java:81-106, DefaultGroupByExecutor.java:104-307,
+    DefaultGroupKeyGenerator.java:214-262, SumAggregationFunction.java:70-81, MinAggregationFunction.java:75-88,
+    AvgAggregationFunction.java:79-97).
+
+    Returns the per-segment map {tuple(dictIds): [result per function]} (order-free), the storage mode, the
+    ARRAY_BASED iteration order (ascending key), string keys and ExecutionStatistics."""
+    if literal_filter:
+        docs, scanned = filter_docs(seg, q.get("filter"))
+    else:
+        docs, scanned = np.nonzero(filter_mask_vectorized(seg, q.get("filter")))[0], None
+    gcols = [seg.columns[c] for c in q["group_by"]["columns"]]
+    cards = [c.card for c in gcols]
+    mode, prod = group_key_mode(cards)
+    # Raw key = sum_j dictId_j * prod_{i<j} card_i (column 0 least significant), :230-246
+    ids = np.stack([c.dict_ids[docs] for c in gcols], axis=1) if len(docs) else np.zeros((0, len(gcols)), np.int64)
+    keys = [tuple(int(x) for x in row) for row in ids]
+    uniq = {}
+    for k in keys:
+        if k not in uniq:
+            uniq[k] = len(uniq)  # first-seen dense group id (LONG/ARRAY_MAP modes)
+    gid = np.array([uniq[k] for k in keys], dtype=np.int64)
+    G = len(uniq)
+    out = {k: [] for k in uniq}
+    for a in q["aggregations"]:
+        fn = a["fn"]
+        if fn == "count":
+            acc = np.zeros(G)
+            np.add.at(acc, gid, 1.0)
+            vals = [int(x) for x in acc]
+        else:
+            col = seg.columns[a["column"]]
+            v = col.value_as_double(col.dict_ids[docs])
+            if fn == "sum":
+                acc = np.zeros(G)
+                np.add.at(acc, gid, v)  # unbuffered, in doc order == holder[key] += v sequentially
+                vals = [float(x) for x in acc]
+            elif fn == "min":
+                acc = np.full(G, math.inf)
+                np.minimum.at(acc, gid, v)
+                vals = [float(x) for x in acc]
+            elif fn == "max":
+                acc = np.full(G, -math.inf)
+                np.maximum.at(acc, gid, v)
+                vals = [float(x) for x in acc]
+            elif fn == "avg":
+                acc = np.zeros(G)
+                np.add.at(acc, gid, v)
+                cnt = np.bincount(gid, minlength=G)
+                vals = [(float(s), int(c)) for s, c in zip(acc, cnt)]
+        for k, i in uniq.items():
+            out[k].append(vals[i])
+
+    def raw_key(k):
+        r = 0
+        for j in range(len(k) - 1, -1, -1):
+            r = r * cards[j] + k[j]
+        return r
+
+    def string_key(k):  # DefaultGroupKeyGenerator.*ToStringGroupKey :711-773
+        return "\t".join(gcols[j].string_of(k[j]) for j in range(len(k)))
+
+    order = sorted(uniq.keys(), key=raw_key) if mode == "ARRAY_BASED" else None
+    n_proj = len(_projection_columns(q))
+    stats = [len(docs), scanned, len(docs) * n_proj, seg.total_raw_docs]
+    return {"mode": mode, "map": out, "order": order, "string_key": string_key, "stats": stats,
+            "empty": len(docs) == 0}
+
+
+# ------------------------------------------------------------------------------------------------
+# a-19: combine across segments
+# ------------------------------------------------------------------------------------------------
+def combine_two(fn: str, a, b):
+    """Legacy combineTwoValues (query/aggregation/function/{Sum,Count,Min,Max,Avg}AggregationFunction.java)."""
+    if fn == "count":
+        return a + b
+    if fn == "sum":
+        return a + b
+    if fn == "min":
+        return a if a < b else b
+    if fn == "max":
+        return a if a > b else b
+    if fn == "avg":
+        return (a[0] + b[0], a[1] + b[1])
+    raise ValueError(fn)
+
+
+def combine_aggregation(parts: List[dict], q: dict) -> dict:
+    """MCombineOperator + CombineService.mergeTwoBlocks (operator/MCombineOperator.java:84-199,
+    query/aggregation/CombineService.java:45-177)."""
+    res = list(parts[0]["results"])
+    for p in parts[1:]:
+        res = [combine_two(a["fn"], x, y) for a, x, y in zip(q["aggregations"], res, p["results"])]
+    stats = [sum(p["stats"][i] or 0 for p in parts) for i in range(4)]
+    return {"results": res, "stats": stats}
+
+
+def combine_group_by(parts: List[dict], q: dict) -> dict:
+    """MCombineGroupByOperator.combineBlocks (operator/MCombineGroupByOperator.java:139-233): merge per-segment maps
+    by STRING group key, then AggregationGroupByOperatorService.trimToSize (query/aggregation/groupby/
+    AggregationGroupByOperatorService.java:59-77,284-361).  Returns {string_key: [results]} untrimmed plus the trimmed
+    per-function maps."""
+    merged: Dict[str, list] = {}
+    fns = [a["fn"] for a in q["aggregations"]]
+    for p in parts:
+        if p["empty"]:
+            continue
+        for k, v in p["map"].items():
+            sk = p["string_key"](k)
+            if sk in merged:
+                merged[sk] = [combine_two(f, x, y) for f, x, y in zip(fns, merged[sk], v)]
+            else:
+                merged[sk] = list(v)
+    top_n = q["group_by"].get("top_n", 10)
+    min_trim = max(top_n, 1000)
+    threshold, size = min_trim * 20, min_trim * 5
+    trimmed = []
+    for i, f in enumerate(fns):
+        items = [(k, v[i]) for k, v in merged.items()]
+        if len(merged) > threshold:
+            keyf = (lambda kv: kv[1][0] / kv[1][1] if kv[1][1] else 0.0) if f == "avg" else (lambda kv: kv[1])
+            items.sort(key=keyf, reverse=(f != "min"))
+            items = items[:size]
+        trimmed.append(dict(items))
+    stats = [sum(p["stats"][i] or 0 for p in parts) for i in range(4)]
+    return {"merged": merged, "trimmed": trimmed, "stats": stats, "trim_threshold": threshold, "trim_size": size}
