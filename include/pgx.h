@@ -1,0 +1,226 @@
+/*
+ * pgx.h -- C ABI of the MI355X-native pinot-core segment query path (libpgx.so).
+ *
+ * This is the drop-in boundary a JNI shim binds.  It replaces, for immutable
+ * v1 segments and COUNT/SUM/MIN/MAX/AVG aggregation or group-by queries, the per-segment operator
+ * tree the reference builds behind its plan-maker API and the in-JVM combine of the per-segment
+ * results.  Reference interfaces replaced (pinot-core/src/main/java/com/linkedin/pinot/core/...):
+ *
+ *   pgx_segment_stage   <- segment/index/loader/Loaders.java:44-118 (Loaders.IndexSegment.load) +
+ *                          segment/index/column/ColumnIndexContainer.java:45-139 (reader per column kind)
+ *   pgx_execute         <- plan/maker/InstancePlanMakerImplV2.java:72-109 (makeInnerSegmentPlan /
+ *                          makeInterSegmentPlan) -> plan/CombinePlanNode.java:66-124 ->
+ *                          operator/MCombineOperator.java:84-199, operator/MCombineGroupByOperator.java:139-233
+ *                          over per-segment operator/aggregation/AggregationOperator.java:77-104 and
+ *                          operator/aggregation/groupby/AggregationGroupByOperator.java:81-106
+ *   pgx_result_*        <- operator/blocks/IntermediateResultsBlock.java:65-233 (aggregation result list,
+ *                          AggregationGroupByResult.getResultForKey, ExecutionStatistics)
+ *   pgx_leaf_binding    <- operator/filter/predicate/PredicateEvaluator.getMatchingDictionaryIds (the caller's
+ *                          PredicateEvaluatorProvider resolves each predicate to dictId space per segment)
+ *
+ * Conventions: every call returns pgx_status (0 = OK); no C++ exception crosses the ABI; on error
+ * pgx_last_error() returns a thread-local message.  Plain pointers and sizes only.  A pgx_ctx is
+ * bound to one device and is thread-safe; staged segments are immutable and may be shared by
+ * concurrent queries.  Host buffers passed in are only read during the call.
+ */
+#ifndef PGX_H_
+#define PGX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PGX_ABI_VERSION 1
+
+typedef enum {
+  PGX_OK = 0,
+  PGX_ERR_INVALID_ARG = 1,
+  PGX_ERR_UNSUPPORTED = 2, /* caller falls back to the Java operators */
+  PGX_ERR_OOM = 3,
+  PGX_ERR_DEVICE = 4,
+  PGX_ERR_TIMEOUT = 5,
+  PGX_ERR_INTERNAL = 6
+} pgx_status;
+
+typedef enum { PGX_INT = 0, PGX_LONG = 1, PGX_FLOAT = 2, PGX_DOUBLE = 3, PGX_STRING = 4 } pgx_data_type;
+
+typedef enum { PGX_COUNT = 0, PGX_SUM = 1, PGX_MIN = 2, PGX_MAX = 3, PGX_AVG = 4 } pgx_agg_fn;
+
+/* Predicate kinds (common/Predicate.java Type); they select the physical filter operator exactly as
+ * plan/FilterPlanNode.java:118-132 does and drive the numEntriesScannedInFilter statistic. */
+typedef enum { PGX_PRED_EQ = 0, PGX_PRED_NEQ = 1, PGX_PRED_IN = 2, PGX_PRED_NOT_IN = 3, PGX_PRED_RANGE = 4 } pgx_pred_kind;
+
+typedef enum { PGX_F_LEAF = 0, PGX_F_AND = 1, PGX_F_OR = 2 } pgx_filter_op;
+
+typedef enum { PGX_MEM_HOST = 0, PGX_MEM_DEVICE = 1 } pgx_mem_kind;
+
+typedef struct pgx_ctx pgx_ctx;
+typedef struct pgx_segment pgx_segment;
+typedef struct pgx_query pgx_query;
+typedef struct pgx_result pgx_result;
+
+typedef struct {
+  int32_t device;          /* HIP device ordinal */
+  uint32_t flags;          /* reserved, 0 */
+} pgx_ctx_opts;
+
+/* ---- context -------------------------------------------------------------------------------- */
+pgx_status pgx_ctx_create(const pgx_ctx_opts* opts, pgx_ctx** out);
+pgx_status pgx_ctx_destroy(pgx_ctx* ctx);
+const char* pgx_last_error(void);
+int32_t pgx_abi_version(void);
+
+/* ---- segments (staging into HBM) ---------------------------------------------------------------
+ * Buffers are the VERBATIM v1 file bytes (big-endian), see DESIGN.md "Data layout in HBM".
+ * mem == PGX_MEM_DEVICE means fwd/dict/... already live in HBM on the context's device (e.g. produced
+ * by pgx_synth_column); the library then references them without copying and the caller keeps them
+ * alive until pgx_segment_release. */
+typedef struct {
+  const char* name;
+  int32_t data_type;          /* pgx_data_type */
+  int32_t cardinality;
+  int32_t bits_per_element;   /* from metadata.properties, never recomputed */
+  int32_t is_sorted;
+  int32_t dict_width;         /* bytes per dictionary entry (lengthOfEachEntry for STRING) */
+  const void* fwd;            /* <col>.sv.unsorted.fwd, ceil(total_docs*bits/8) bytes (NULL if sorted) */
+  uint64_t fwd_len;
+  const void* sorted_pairs;   /* <col>.sv.sorted.fwd, card x (int32 BE start, int32 BE end) (NULL if unsorted) */
+  uint64_t sorted_len;
+  const void* dict;           /* <col>.dict */
+  uint64_t dict_len;
+  const void* inv;            /* <col>.bitmap.inv (optional, host memory) */
+  uint64_t inv_len;
+} pgx_column_desc;
+
+typedef struct {
+  const char* name;
+  int32_t total_docs;
+  int32_t total_raw_docs;
+  int32_t num_columns;
+  const pgx_column_desc* columns;
+  const void* star_tree;      /* star-tree.bin in OFF_HEAP format (optional, host memory) */
+  uint64_t star_tree_len;
+  int32_t mem;                /* pgx_mem_kind of fwd/sorted_pairs/dict */
+} pgx_segment_desc;
+
+pgx_status pgx_segment_stage(pgx_ctx* ctx, const pgx_segment_desc* desc, pgx_segment** out);
+pgx_status pgx_segment_release(pgx_segment* seg);
+/* HBM bytes held by the staged segment (forward indexes + dictionaries + inverted indexes). */
+pgx_status pgx_segment_device_bytes(const pgx_segment* seg, uint64_t* out);
+
+/* ---- query ---------------------------------------------------------------------------------- */
+typedef struct {
+  int32_t fn;                 /* pgx_agg_fn */
+  const char* column;         /* NULL or "*" for COUNT(*) */
+} pgx_agg;
+
+/* Filter tree in postfix order.  LEAF: arg = leaf index.  AND / OR: arg = number of children popped. */
+typedef struct {
+  int32_t op;                 /* pgx_filter_op */
+  int32_t arg;
+} pgx_filter_node;
+
+typedef struct {
+  const char* column;
+  int32_t kind;               /* pgx_pred_kind */
+} pgx_leaf;
+
+typedef struct {
+  int32_t num_aggs;
+  const pgx_agg* aggs;
+  int32_t num_group_cols;     /* 0 => aggregation-only query */
+  const char* const* group_cols;
+  int32_t top_n;              /* GROUP BY ... TOP n (reference default 10) */
+  int32_t num_filter_nodes;   /* 0 => MatchEntireSegment */
+  const pgx_filter_node* filter;
+  int32_t num_leaves;
+  const pgx_leaf* leaves;
+  uint32_t flags;             /* PGX_Q_* */
+} pgx_query_desc;
+
+#define PGX_Q_NO_STAR_TREE 0x1u /* debug option useStarTree=false (common/utils/request/RequestUtils.java:229-236) */
+
+pgx_status pgx_query_compile(pgx_ctx* ctx, const pgx_query_desc* desc, pgx_query** out);
+pgx_status pgx_query_release(pgx_query* q);
+
+/* Per-(segment, leaf) predicate in dictionary-id space, as produced by the caller's PredicateEvaluator:
+ * a doc matches iff its dictId d satisfies  (words ? bit d of words : lo <= d <= hi).
+ * For NEQ / NOT_IN the binding describes the MATCHING ids (the complement); the library derives the
+ * non-matching list for bitmap exclusion itself.  words has ceil(card/32) little-endian uint32. */
+typedef struct {
+  int32_t lo;
+  int32_t hi;
+  const uint32_t* words;      /* host memory, optional */
+} pgx_leaf_binding;
+
+typedef struct {
+  uint64_t stream;            /* hipStream_t (0 = the context's own stream) */
+  void* dense_out;            /* optional device buffer for the dense group table (multi-GPU merge) */
+  uint64_t dense_out_bytes;
+  uint32_t flags;             /* PGX_X_* */
+} pgx_exec_opts;
+
+#define PGX_X_KEEP_DENSE_ON_DEVICE 0x1u /* leave the dense table in dense_out; do not compact to host */
+#define PGX_X_FORCE_HASH 0x2u           /* testing: use the hash group-by path even for small key spaces */
+
+/* Execute the query over n segments on the context's device and merge the per-segment partials
+ * (the combine).  bindings is [n][num_leaves].  Synchronous w.r.t. the returned result. */
+pgx_status pgx_execute(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
+                       const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out);
+pgx_status pgx_result_release(pgx_result* r);
+
+/* ExecutionStatistics: numDocsScanned, numEntriesScannedInFilter, numEntriesScannedPostFilter, totalRawDocs
+ * (operator/ExecutionStatistics.java:21-74). */
+pgx_status pgx_result_stats(const pgx_result* r, int64_t out[4]);
+
+/* Aggregation-only results.  COUNT: *count. SUM/MIN/MAX: *value. AVG: *value = sum, *count = count.
+ * Empty input gives the reference defaults (MIN +inf, MAX -inf, AvgPair(0.0, 0)). */
+pgx_status pgx_result_agg(const pgx_result* r, int32_t fn_index, double* value, int64_t* count);
+
+/* Group-by results (combined over the segments, untrimmed). */
+pgx_status pgx_result_num_groups(const pgx_result* r, int64_t* n);
+/* For group-by column c: per group, the index (into the segs[] given to pgx_execute) of a segment that
+ * holds the group's value and that segment's local dictId for it. */
+pgx_status pgx_result_group_keys(const pgx_result* r, int32_t c, int32_t* seg_index, int32_t* dict_id);
+/* Per group: value (SUM/MIN/MAX; AVG sum) and count (COUNT; AVG count; for SUM/MIN/MAX the group's doc count). */
+pgx_status pgx_result_group_values(const pgx_result* r, int32_t fn_index, double* value, int64_t* count);
+/* Storage mode the reference would pick for a single segment: 0 ARRAY_BASED, 1 LONG_MAP_BASED, 2 ARRAY_MAP_BASED
+ * (operator/aggregation/groupby/DefaultGroupKeyGenerator.java:167-186). */
+pgx_status pgx_result_group_mode(const pgx_result* r, int32_t* mode);
+/* Combine trim (query/aggregation/groupby/AggregationGroupByOperatorService.java:59-77,284-361): if the number of
+ * groups exceeds 20*max(top_n,1000), the indices of the top 5*max(top_n,1000) groups for function fn (MIN ascending,
+ * AVG by sum/count, others descending), else all groups.  *n in: capacity, out: count written. */
+pgx_status pgx_result_trim(const pgx_result* r, int32_t fn_index, int64_t* group_index, int64_t* n);
+
+/* Dense-table layout for PGX_X_KEEP_DENSE_ON_DEVICE (multi-GPU RCCL merge):
+ * slots = product of group cardinalities; buffer = (1 + num_aggs) planes of slots x 8 bytes.
+ * plane 0: int64 doc count; plane 1+i: function i in its accumulator encoding (pgx_result_dense_plane_op). */
+pgx_status pgx_query_dense_slots(const pgx_query* q, pgx_segment* const* segs, int32_t n, int64_t* slots);
+/* For plane p: 0 = int64 add, 1 = double add, 2 = uint64 ordered-min, 3 = uint64 ordered-max. */
+pgx_status pgx_query_dense_plane_op(const pgx_query* q, pgx_segment* const* segs, int32_t n, int32_t plane, int32_t* op);
+/* Decode a (possibly RCCL-reduced) dense table living in device memory into a host-side result. */
+pgx_status pgx_result_from_dense(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
+                                 const void* dense_device, const int64_t stats[4], pgx_result** out);
+
+/* ---- synthetic data (benchmarks) ------------------------------------------------------------
+ * Fill a device buffer with the fixed-bit forward index of n rows whose dictId is
+ * pgx_synth_value(seed, row) = splitmix64(seed ^ (row * 0x9E3779B97F4A7C15)) % card  (DESIGN.md). */
+pgx_status pgx_synth_column(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
+                            uint64_t seed);
+pgx_status pgx_device_alloc(pgx_ctx* ctx, uint64_t bytes, void** out);
+pgx_status pgx_device_free(pgx_ctx* ctx, void* p);
+pgx_status pgx_copy_to_device(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+
+/* ---- timing (bench): run the query `iters` times back to back, returning per-launch kernel times of
+ * the dominant kernel measured with HIP events on the stream it is launched on. */
+pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
+                             const pgx_leaf_binding* bindings, int32_t iters, double* total_ms,
+                             double* kernel_ms, pgx_result** out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PGX_H_ */

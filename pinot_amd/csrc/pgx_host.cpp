@@ -1,0 +1,1330 @@
+// libpgx host side: the C ABI of include/pgx.h.
+//
+// Segment staging (Loaders / ColumnIndexContainer), per-query physical planning (FilterPlanNode's operator choice,
+// the AND/OR algebra as a postfix program, DefaultGroupKeyGenerator's key space), launch of the fused HIP kernel and
+// decoding of the combined result (MCombine*Operator + AggregationGroupByOperatorService.trimToSize).
+// Reference paths are relative to pinot-core/src/main/java/com/linkedin/pinot/core/.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/pgx.h"
+#include "pgx_internal.h"
+
+extern "C" hipError_t pgx_launch_scan(const pgx::KQuery* q, int grid, int64_t tiles_per_wg, size_t lds_bytes,
+                                      hipStream_t stream);
+extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t slots, int num_planes,
+                                             const pgx::KQuery* q, unsigned long long* keys, uint64_t key_words,
+                                             unsigned int* key_state, hipStream_t stream);
+extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
+                                         unsigned long long* counter, int64_t* out_slot,
+                                         unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
+extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
+                                       int64_t n_words, hipStream_t stream);
+
+using namespace pgx;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+struct PgxError {
+  pgx_status status;
+  std::string msg;
+};
+
+[[noreturn]] void fail(pgx_status s, const std::string& m) { throw PgxError{s, m}; }
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) fail(PGX_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename F>
+pgx_status guarded(F&& f) {
+  try {
+    f();
+    return PGX_OK;
+  } catch (const PgxError& e) {
+    g_last_error = e.msg;
+    return e.status;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host out of memory";
+    return PGX_ERR_OOM;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return PGX_ERR_INTERNAL;
+  }
+}
+
+inline uint32_t be32(const uint8_t* p) {
+  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
+}
+inline uint64_t be64(const uint8_t* p) { return (uint64_t(be32(p)) << 32) | be32(p + 4); }
+
+uint64_t fnv1a(const void* data, size_t n, uint64_t h = 1469598103934665603ull) {
+  const uint8_t* p = static_cast<const uint8_t*>(data);
+  for (size_t i = 0; i < n; ++i) {
+    h ^= p[i];
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+// Padded size of a fixed-bit forward index on device: whole tiles (each lane reads exactly `bits` dwords).
+uint64_t padded_fwd_bytes(int64_t total_docs, int bits) {
+  const int64_t tiles = (total_docs + kTileRows - 1) / kTileRows;
+  return static_cast<uint64_t>(std::max<int64_t>(tiles, 1)) * (kTileRows / 8) * bits + 64;
+}
+
+}  // namespace
+
+// =================================================================================================
+// Context
+// =================================================================================================
+struct pgx_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  // Simple size-bucketed device memory pool (avoids hipMalloc/hipFree on the query path).
+  std::multimap<size_t, void*> free_blocks;
+  std::unordered_map<void*, size_t> live;
+
+  void* alloc(size_t bytes) {
+    bytes = std::max<size_t>(256, (bytes + 255) & ~size_t(255));
+    std::lock_guard<std::mutex> g(mu);
+    auto it = free_blocks.lower_bound(bytes);
+    if (it != free_blocks.end() && it->first <= bytes * 2) {
+      void* p = it->second;
+      live[p] = it->first;
+      free_blocks.erase(it);
+      return p;
+    }
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess) {
+      // release cached blocks and retry once
+      for (auto& kv : free_blocks) (void)hipFree(kv.second);
+      free_blocks.clear();
+      e = hipMalloc(&p, bytes);
+      if (e != hipSuccess) fail(PGX_ERR_OOM, "hipMalloc(" + std::to_string(bytes) + ") failed");
+    }
+    live[p] = bytes;
+    return p;
+  }
+  void release(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = live.find(p);
+    if (it == live.end()) return;
+    free_blocks.emplace(it->second, p);
+    live.erase(it);
+  }
+};
+
+struct DevBuf {
+  pgx_ctx* ctx = nullptr;
+  void* p = nullptr;
+  DevBuf() = default;
+  DevBuf(pgx_ctx* c, size_t n) : ctx(c), p(c->alloc(n)) {}
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : ctx(o.ctx), p(o.p) { o.p = nullptr; }
+  DevBuf& operator=(DevBuf&& o) noexcept {
+    reset();
+    ctx = o.ctx;
+    p = o.p;
+    o.p = nullptr;
+    return *this;
+  }
+  ~DevBuf() { reset(); }
+  void reset() {
+    if (p && ctx) ctx->release(p);
+    p = nullptr;
+  }
+  template <typename T>
+  T* as() const { return static_cast<T*>(p); }
+};
+
+// =================================================================================================
+// Segments
+// =================================================================================================
+struct StagedColumn {
+  std::string name;
+  int data_type = 0;
+  int card = 0;
+  int bits = 0;
+  bool is_sorted = false;
+  int dict_width = 0;
+  bool has_inverted = false;
+  // device
+  const uint32_t* fwd = nullptr;  // packed fixed-bit (padded)
+  DevBuf fwd_owned;
+  const void* dict_dev = nullptr;  // int64 / double values per dictId
+  DevBuf dict_owned;
+  // host
+  std::vector<int32_t> sorted_first, sorted_last;  // sorted columns: inclusive doc range per dictId
+  std::vector<int64_t> ivals;                      // numeric dictionary values (INT/LONG)
+  std::vector<double> dvals;                       // FLOAT/DOUBLE dictionary values
+  std::vector<std::string> svals;                  // STRING dictionary values (unpadded)
+  uint64_t dict_hash = 0;
+  std::vector<uint8_t> inv;                        // bitmap inverted index bytes (host)
+};
+
+struct pgx_segment {
+  pgx_ctx* ctx = nullptr;
+  std::string name;
+  int32_t total_docs = 0, total_raw_docs = 0;
+  std::vector<StagedColumn> cols;
+  std::unordered_map<std::string, int> by_name;
+  std::vector<uint8_t> star_tree;
+  uint64_t device_bytes = 0;
+
+  const StagedColumn& col(const std::string& n) const {
+    auto it = by_name.find(n);
+    if (it == by_name.end()) fail(PGX_ERR_INVALID_ARG, "segment " + name + " has no column " + n);
+    return cols[it->second];
+  }
+};
+
+namespace {
+
+void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c) {
+  c.name = d.name ? d.name : "";
+  c.data_type = d.data_type;
+  c.card = d.cardinality;
+  c.bits = d.bits_per_element;
+  c.is_sorted = d.is_sorted != 0;
+  c.dict_width = d.dict_width;
+  if (c.card < 1) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": cardinality < 1");
+  if (c.bits < 1 || c.bits > 32) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": bitsPerElement out of [1,32]");
+  if (c.card > 1 && (c.bits < 32) && (int64_t(c.card) - 1) >> c.bits)
+    fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": cardinality does not fit bitsPerElement");
+  const int64_t n = seg->total_docs;
+  const uint64_t need = padded_fwd_bytes(n, c.bits);
+
+  // ---- dictionary (host copy always; device copy for numeric columns) ----
+  std::vector<uint8_t> dict_host;
+  if (device_mem) {
+    dict_host.resize(d.dict_len);
+    if (d.dict_len) hip_check(hipMemcpy(dict_host.data(), d.dict, d.dict_len, hipMemcpyDeviceToHost), "dict D2H");
+  } else {
+    const uint8_t* p = static_cast<const uint8_t*>(d.dict);
+    dict_host.assign(p, p + d.dict_len);
+  }
+  const int width = (c.data_type == PGX_INT || c.data_type == PGX_FLOAT) ? 4
+                    : (c.data_type == PGX_STRING)                          ? c.dict_width
+                                                                           : 8;
+  if (width <= 0 || dict_host.size() < uint64_t(width) * c.card)
+    fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": dictionary too short");
+  c.dict_hash = fnv1a(dict_host.data(), uint64_t(width) * c.card, fnv1a(&c.data_type, sizeof(int)));
+  if (c.data_type == PGX_STRING) {
+    c.svals.resize(c.card);
+    for (int i = 0; i < c.card; ++i) {
+      const char* s = reinterpret_cast<const char*>(dict_host.data()) + size_t(i) * width;
+      size_t len = width;
+      // StringDictionary.get: truncate at the first padding char ('\0' default, '%' legacy)
+      for (size_t k = 0; k < size_t(width); ++k)
+        if (s[k] == '\0') { len = k; break; }
+      c.svals[i].assign(s, len);
+    }
+  } else {
+    std::vector<uint64_t> enc(c.card);
+    if (c.data_type == PGX_INT || c.data_type == PGX_LONG) {
+      c.ivals.resize(c.card);
+      for (int i = 0; i < c.card; ++i) {
+        int64_t v = (c.data_type == PGX_INT) ? int64_t(int32_t(be32(&dict_host[size_t(i) * 4])))
+                                             : int64_t(be64(&dict_host[size_t(i) * 8]));
+        c.ivals[i] = v;
+        enc[i] = uint64_t(v);
+      }
+    } else {
+      c.dvals.resize(c.card);
+      for (int i = 0; i < c.card; ++i) {
+        double v;
+        if (c.data_type == PGX_FLOAT) {
+          uint32_t b = be32(&dict_host[size_t(i) * 4]);
+          float f;
+          std::memcpy(&f, &b, 4);
+          v = double(f);  // (double) widening as FloatDictionary.getDoubleValue
+        } else {
+          uint64_t b = be64(&dict_host[size_t(i) * 8]);
+          std::memcpy(&v, &b, 8);
+        }
+        c.dvals[i] = v;
+        std::memcpy(&enc[i], &v, 8);
+      }
+    }
+    c.dict_owned = DevBuf(ctx, enc.size() * 8);
+    hip_check(hipMemcpy(c.dict_owned.p, enc.data(), enc.size() * 8, hipMemcpyHostToDevice), "dict H2D");
+    c.dict_dev = c.dict_owned.p;
+    seg->device_bytes += enc.size() * 8;
+  }
+
+  // ---- forward index ----
+  if (c.is_sorted) {
+    // Sorted SV column: card x (start,end) BE int pairs (SortedForwardIndexReader / SortedInvertedIndexReader).
+    std::vector<uint8_t> pairs(d.sorted_len);
+    if (d.sorted_len < uint64_t(c.card) * 8) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": sorted index short");
+    if (device_mem) hip_check(hipMemcpy(pairs.data(), d.sorted_pairs, d.sorted_len, hipMemcpyDeviceToHost), "D2H");
+    else std::memcpy(pairs.data(), d.sorted_pairs, d.sorted_len);
+    c.sorted_first.resize(c.card);
+    c.sorted_last.resize(c.card);
+    for (int i = 0; i < c.card; ++i) {
+      c.sorted_first[i] = int32_t(be32(&pairs[size_t(i) * 8]));
+      c.sorted_last[i] = int32_t(be32(&pairs[size_t(i) * 8 + 4]));
+    }
+    // Materialise a packed fixed-bit view on device so group-by / value reads use the same unpack path.
+    std::vector<uint8_t> packed(need, 0);
+    for (int id = 0; id < c.card; ++id) {
+      for (int64_t r = std::max<int32_t>(0, c.sorted_first[id]); r <= c.sorted_last[id] && r < n; ++r) {
+        const int64_t bit0 = r * c.bits;
+        for (int k = 0; k < c.bits; ++k) {
+          if ((uint32_t(id) >> (c.bits - 1 - k)) & 1u) {
+            const int64_t bit = bit0 + k;
+            packed[bit >> 3] |= uint8_t(0x80u >> (bit & 7));
+          }
+        }
+      }
+    }
+    c.fwd_owned = DevBuf(ctx, need);
+    hip_check(hipMemcpy(c.fwd_owned.p, packed.data(), need, hipMemcpyHostToDevice), "fwd H2D");
+    c.fwd = c.fwd_owned.as<const uint32_t>();
+    seg->device_bytes += need;
+  } else {
+    const uint64_t file_bytes = (uint64_t(n) * c.bits + 7) / 8;
+    if (d.fwd_len < file_bytes) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": forward index short");
+    if (device_mem && d.fwd_len >= need && (reinterpret_cast<uintptr_t>(d.fwd) & 15) == 0) {
+      c.fwd = static_cast<const uint32_t*>(d.fwd);  // referenced in place (caller keeps it alive)
+    } else {
+      c.fwd_owned = DevBuf(ctx, need);
+      hip_check(hipMemset(c.fwd_owned.p, 0, need), "memset");
+      hip_check(hipMemcpy(c.fwd_owned.p, d.fwd, file_bytes, device_mem ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice),
+                "fwd copy");
+      c.fwd = c.fwd_owned.as<const uint32_t>();
+      seg->device_bytes += need;
+    }
+  }
+  if (d.inv && d.inv_len) {
+    const uint8_t* p = static_cast<const uint8_t*>(d.inv);
+    c.inv.assign(p, p + d.inv_len);
+    c.has_inverted = true;
+  }
+  if (c.is_sorted) c.has_inverted = true;  // ColumnDataSourceImpl: sorted columns report an inverted index
+}
+
+}  // namespace
+
+// =================================================================================================
+// Query
+// =================================================================================================
+struct pgx_query {
+  std::vector<int> agg_fn;
+  std::vector<std::string> agg_col;  // "" for COUNT(*)
+  std::vector<std::string> group_cols;
+  int top_n = 10;
+  std::vector<pgx_filter_node> filter;
+  std::vector<std::string> leaf_col;
+  std::vector<int> leaf_kind;
+  uint32_t flags = 0;
+};
+
+// =================================================================================================
+// Result
+// =================================================================================================
+struct pgx_result {
+  int64_t stats[4] = {0, 0, 0, 0};
+  int num_aggs = 0;
+  std::vector<int> agg_fn;
+  bool group_by = false;
+  int top_n = 10;
+  int mode = 0;
+  // aggregation-only
+  std::vector<double> agg_value;
+  std::vector<int64_t> agg_count;
+  // group-by (columnar)
+  int64_t num_groups = 0;
+  std::vector<std::vector<int32_t>> key_seg, key_id;  // [col][group]
+  std::vector<std::vector<double>> g_value;          // [fn][group]
+  std::vector<std::vector<int64_t>> g_count;         // [fn][group]
+};
+
+namespace {
+
+// ----- physical filter plan (FilterPlanNode.constructPhysicalOperator + reorder, plan/FilterPlanNode.java:77-170) -----
+enum PhysKind { PH_SORTED = 0, PH_AND = 1, PH_BITMAP = 2, PH_SCAN = 3, PH_OR = 4 };
+
+struct PNode {
+  int op;  // PGX_F_LEAF / AND / OR
+  int leaf = -1;
+  int phys = PH_SCAN;
+  std::vector<PNode> kids;
+};
+
+PNode build_tree(const pgx_query& q, const pgx_segment& seg0) {
+  std::vector<PNode> st;
+  for (const auto& n : q.filter) {
+    if (n.op == PGX_F_LEAF) {
+      if (n.arg < 0 || n.arg >= int(q.leaf_col.size())) fail(PGX_ERR_INVALID_ARG, "filter leaf index out of range");
+      PNode p;
+      p.op = PGX_F_LEAF;
+      p.leaf = n.arg;
+      const StagedColumn& c = seg0.col(q.leaf_col[n.arg]);
+      if (c.has_inverted && q.leaf_kind[n.arg] != PGX_PRED_RANGE) p.phys = c.is_sorted ? PH_SORTED : PH_BITMAP;
+      else p.phys = PH_SCAN;
+      st.push_back(std::move(p));
+    } else if (n.op == PGX_F_AND || n.op == PGX_F_OR) {
+      if (n.arg < 1 || n.arg > int(st.size())) fail(PGX_ERR_INVALID_ARG, "filter node arity");
+      PNode p;
+      p.op = n.op;
+      p.phys = n.op == PGX_F_AND ? PH_AND : PH_OR;
+      p.kids.assign(std::make_move_iterator(st.end() - n.arg), std::make_move_iterator(st.end()));
+      st.erase(st.end() - n.arg, st.end());
+      std::stable_sort(p.kids.begin(), p.kids.end(), [](const PNode& a, const PNode& b) { return a.phys < b.phys; });
+      st.push_back(std::move(p));
+    } else {
+      fail(PGX_ERR_INVALID_ARG, "bad filter op");
+    }
+  }
+  if (st.size() != 1) fail(PGX_ERR_INVALID_ARG, "filter postfix does not reduce to one tree");
+  return std::move(st.back());
+}
+
+// Emit the device program.  Evaluation order follows AndBlockDocIdSet.fastIterator (operator/docidsets/
+// AndBlockDocIdSet.java:146-229): sorted ranges and bitmaps first, then every scan child tested against the running
+// candidate set (applyAnd) -- an OP_STAT before each scan child records numEntriesScannedInFilter.  host_scan_leaves
+// counts scan leaves whose entries equal the whole scan range (a root scan leaf; scan children of a root OR, which
+// OrDocIdIterator advances doc by doc, operator/dociditerators/OrDocIdIterator.java:100-139).
+void emit(const PNode& n, std::vector<int8_t>& op, std::vector<int8_t>& arg, bool root, bool stats_inside,
+          int& host_scan_leaves) {
+  if (n.op == PGX_F_LEAF) {
+    op.push_back(OP_LEAF);
+    arg.push_back(int8_t(n.leaf));
+    if (root && n.phys == PH_SCAN) host_scan_leaves += 1;
+    return;
+  }
+  if (n.op == PGX_F_OR) {
+    for (size_t i = 0; i < n.kids.size(); ++i) {
+      const PNode& k = n.kids[i];
+      if (root && k.op == PGX_F_LEAF && k.phys == PH_SCAN) host_scan_leaves += 1;
+      emit(k, op, arg, false, false, host_scan_leaves);
+      if (i > 0) { op.push_back(OP_OR); arg.push_back(2); }
+    }
+    return;
+  }
+  // AND: index-based children first, then scans with statistics, then nested operators.
+  int pushed = 0;
+  auto fold = [&]() {
+    if (pushed > 1) { op.push_back(OP_AND); arg.push_back(2); }
+  };
+  for (const PNode& k : n.kids)
+    if (k.op == PGX_F_LEAF && (k.phys == PH_SORTED || k.phys == PH_BITMAP)) {
+      emit(k, op, arg, false, false, host_scan_leaves);
+      ++pushed;
+      fold();
+    }
+  const bool fast = pushed > 0;
+  for (const PNode& k : n.kids)
+    if (k.op == PGX_F_LEAF && k.phys == PH_SCAN) {
+      if (fast || pushed > 0) { op.push_back(OP_STAT); arg.push_back(0); }
+      else if (root) host_scan_leaves += 1;  // first scan of an all-scan AND walks the whole range
+      emit(k, op, arg, false, false, host_scan_leaves);
+      ++pushed;
+      fold();
+    }
+  for (const PNode& k : n.kids)
+    if (k.op != PGX_F_LEAF) {
+      emit(k, op, arg, false, stats_inside, host_scan_leaves);
+      ++pushed;
+      fold();
+    }
+}
+
+unsigned long long* devp(const DevBuf& b) { return b.as<unsigned long long>(); }
+
+double decode_plane(int op, bool fp, unsigned long long x, int fn) {
+  if (op == P_ADD_I64) return double(int64_t(x));
+  if (op == P_ADD_F64) {
+    double d;
+    std::memcpy(&d, &x, 8);
+    return d;
+  }
+  // ordered min/max
+  if (op == P_MIN_ORD && x == ~0ull) return std::numeric_limits<double>::infinity();
+  if (op == P_MAX_ORD && x == 0ull) return -std::numeric_limits<double>::infinity();
+  if (!fp) return double(int64_t(x ^ 0x8000000000000000ull));
+  uint64_t b = (x & 0x8000000000000000ull) ? (x & ~0x8000000000000000ull) : ~x;
+  double d;
+  std::memcpy(&d, &b, 8);
+  (void)fn;
+  return d;
+}
+
+// Global key identity for one group-by column over the executed segments (per-segment dictIds -> union
+// dictionary ids).  Identity when every segment holds the same dictionary bytes.
+struct GlobalDict {
+  int64_t card = 0;
+  bool identity = true;
+  std::vector<std::vector<int32_t>> remap;    // [seg][local] -> global
+  std::vector<int32_t> rep_seg, rep_id;        // [global] -> a (segment, local id) holding the value
+};
+
+GlobalDict build_global_dict(pgx_segment* const* segs, int n, const std::string& col) {
+  GlobalDict g;
+  const StagedColumn& c0 = segs[0]->col(col);
+  bool same = true;
+  for (int s = 1; s < n && same; ++s) {
+    const StagedColumn& c = segs[s]->col(col);
+    same = c.dict_hash == c0.dict_hash && c.card == c0.card && c.data_type == c0.data_type;
+  }
+  if (same) {
+    g.card = c0.card;
+    g.identity = true;
+    g.rep_seg.assign(g.card, 0);
+    g.rep_id.resize(g.card);
+    std::iota(g.rep_id.begin(), g.rep_id.end(), 0);
+    return g;
+  }
+  g.identity = false;
+  g.remap.resize(n);
+  // k-way merge of the sorted dictionaries by value.
+  struct Item { int seg; int id; };
+  std::vector<Item> all;
+  for (int s = 0; s < n; ++s) {
+    const StagedColumn& c = segs[s]->col(col);
+    if (c.data_type != c0.data_type) fail(PGX_ERR_INVALID_ARG, "column " + col + " has different types");
+    g.remap[s].resize(c.card);
+    for (int i = 0; i < c.card; ++i) all.push_back({s, i});
+  }
+  auto less = [&](const Item& a, const Item& b) {
+    const StagedColumn& ca = segs[a.seg]->col(col);
+    const StagedColumn& cb = segs[b.seg]->col(col);
+    if (c0.data_type == PGX_STRING) return ca.svals[a.id] < cb.svals[b.id];
+    if (c0.data_type == PGX_INT || c0.data_type == PGX_LONG) return ca.ivals[a.id] < cb.ivals[b.id];
+    return ca.dvals[a.id] < cb.dvals[b.id];
+  };
+  std::stable_sort(all.begin(), all.end(), less);
+  int64_t gid = -1;
+  for (size_t i = 0; i < all.size(); ++i) {
+    if (i == 0 || less(all[i - 1], all[i])) {
+      ++gid;
+      g.rep_seg.push_back(all[i].seg);
+      g.rep_id.push_back(all[i].id);
+    }
+    g.remap[all[i].seg][all[i].id] = int32_t(gid);
+  }
+  g.card = gid + 1;
+  return g;
+}
+
+int bits_for(int64_t card) {
+  int b = 1;
+  while ((int64_t(1) << b) < card) ++b;
+  return b;
+}
+
+struct ExecPlan {
+  KQuery kq{};
+  std::vector<KSeg> ksegs;
+  std::vector<int32_t> blob32;   // ranges / remaps / bitsets, uploaded as one buffer
+  struct Fix { size_t seg; int kind; int slot; size_t off; };  // pointer fixups into blob32
+  std::vector<Fix> fixes;
+  std::vector<std::string> qcols;
+  std::vector<GlobalDict> gdicts;
+  std::vector<int> gbits;
+  int64_t host_entries = 0;
+  int64_t total_raw = 0;
+  int n_proj = 0;
+  int mode_ref = 0;
+  uint64_t dense_slots = 0;
+  uint64_t hash_cap = 0;
+  int grid = 0;
+  int64_t tiles_per_wg = 0;
+  size_t lds_bytes = 0;
+};
+
+int qslot(ExecPlan& P, const std::string& name) {
+  for (size_t i = 0; i < P.qcols.size(); ++i)
+    if (P.qcols[i] == name) return int(i);
+  if (P.qcols.size() >= size_t(kMaxQCols)) fail(PGX_ERR_UNSUPPORTED, "query touches too many columns");
+  P.qcols.push_back(name);
+  return int(P.qcols.size() - 1);
+}
+
+void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
+                uint32_t xflags, ExecPlan& P) {
+  if (n < 1) fail(PGX_ERR_INVALID_ARG, "no segments");
+  if (q.agg_fn.size() > size_t(kMaxAggs)) fail(PGX_ERR_UNSUPPORTED, "too many aggregation functions");
+  if (q.group_cols.size() > size_t(kMaxGroupCols)) fail(PGX_ERR_UNSUPPORTED, "too many group-by columns");
+  if (q.leaf_col.size() > size_t(kMaxLeaves)) fail(PGX_ERR_UNSUPPORTED, "too many filter leaves");
+  KQuery& K = P.kq;
+  // query column slots
+  for (size_t l = 0; l < q.leaf_col.size(); ++l) K.leaf_col[l] = int8_t(qslot(P, q.leaf_col[l]));
+  K.num_aggs = int(q.agg_fn.size());
+  K.num_planes = K.num_aggs + 1;
+  K.plane_op[0] = P_ADD_I64;
+  std::vector<std::string> proj;
+  for (int a = 0; a < K.num_aggs; ++a) {
+    const int fn = q.agg_fn[a];
+    K.agg_kind[a] = int8_t(fn);
+    if (fn == PGX_COUNT) {
+      K.agg_col[a] = -1;
+      K.agg_fp[a] = 0;
+      K.plane_op[a + 1] = P_ADD_I64;
+      continue;
+    }
+    const StagedColumn& c = segs[0]->col(q.agg_col[a]);
+    if (c.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + c.name);
+    const bool fp = c.data_type == PGX_FLOAT || c.data_type == PGX_DOUBLE;
+    K.agg_col[a] = int8_t(qslot(P, q.agg_col[a]));
+    K.agg_fp[a] = fp;
+    K.plane_op[a + 1] = (fn == PGX_MIN) ? P_MIN_ORD : (fn == PGX_MAX) ? P_MAX_ORD : (fp ? P_ADD_F64 : P_ADD_I64);
+    if (std::find(proj.begin(), proj.end(), q.agg_col[a]) == proj.end()) proj.push_back(q.agg_col[a]);
+  }
+  for (const auto& g : q.group_cols)
+    if (std::find(proj.begin(), proj.end(), g) == proj.end()) proj.push_back(g);
+  P.n_proj = int(proj.size());
+
+  // group-by key space
+  K.num_gcols = int(q.group_cols.size());
+  K.group_mode = G_NONE;
+  if (K.num_gcols) {
+    uint64_t prod = 1;
+    bool overflow = false;
+    int total_bits = 0;
+    P.gdicts.clear();
+    for (int g = 0; g < K.num_gcols; ++g) {
+      K.gcol[g] = int8_t(qslot(P, q.group_cols[g]));
+      P.gdicts.push_back(build_global_dict(segs, n, q.group_cols[g]));
+      const int64_t gc = P.gdicts.back().card;
+      if (!overflow && prod > (uint64_t(1) << 62) / uint64_t(gc)) overflow = true;
+      if (!overflow) prod *= uint64_t(gc);
+      P.gbits.push_back(bits_for(gc));
+      total_bits += P.gbits.back();
+    }
+    // Reference storage mode of a single segment (DefaultGroupKeyGenerator.java:167-186)
+    {
+      int64_t p1 = 1;
+      bool ov = false;
+      for (const auto& g : q.group_cols) {
+        const int64_t cc = segs[0]->col(g).card;
+        if (!ov && p1 > std::numeric_limits<int64_t>::max() / cc) ov = true;
+        else if (!ov) p1 *= cc;
+      }
+      P.mode_ref = ov ? 2 : (p1 > 10000 ? 1 : 0);
+    }
+    const uint64_t kDenseMax = uint64_t(1) << 22;
+    if (!overflow && prod <= kDenseMax && !(xflags & PGX_X_FORCE_HASH)) {
+      uint64_t mul = 1;
+      for (int g = 0; g < K.num_gcols; ++g) {  // column 0 least significant (DefaultGroupKeyGenerator.java:230-237)
+        K.gmul[g] = mul;
+        mul *= uint64_t(P.gdicts[g].card);
+      }
+      P.dense_slots = prod;
+      const size_t lds = size_t(prod) * K.num_planes * 8;
+      K.group_mode = (lds <= 48 * 1024) ? G_DENSE_LDS : G_DENSE_GLOBAL;
+      if (K.group_mode == G_DENSE_LDS) P.lds_bytes = lds;
+    } else if (total_bits <= 126) {
+      int sh = 0;
+      bool hi = false;
+      for (int g = 0; g < K.num_gcols; ++g) {
+        if (!hi && sh + P.gbits[g] > 63) {
+          hi = true;
+          sh = 0;
+        }
+        K.gshift[g] = sh;
+        K.ghi[g] = hi;
+        sh += P.gbits[g];
+      }
+      K.group_mode = hi ? G_HASH128 : G_HASH64;
+    } else {
+      fail(PGX_ERR_UNSUPPORTED, "group key wider than 126 bits");
+    }
+  }
+  K.num_qcols = int(P.qcols.size());
+
+  // filter program
+  P.host_entries = 0;
+  int host_scan_leaves = 0;
+  std::vector<int8_t> pop, parg;
+  if (!q.filter.empty()) {
+    PNode root = build_tree(q, *segs[0]);
+    emit(root, pop, parg, true, false, host_scan_leaves);
+  }
+  if (pop.size() > size_t(kMaxProg)) fail(PGX_ERR_UNSUPPORTED, "filter program too long");
+  K.prog_len = int(pop.size());
+  for (size_t i = 0; i < pop.size(); ++i) {
+    K.prog_op[i] = pop[i];
+    K.prog_arg[i] = parg[i];
+  }
+
+  // per-segment descriptors
+  P.ksegs.assign(n, KSeg{});
+  int64_t tiles = 0;
+  P.total_raw = 0;
+  for (int s = 0; s < n; ++s) {
+    const pgx_segment& seg = *segs[s];
+    KSeg& S = P.ksegs[s];
+    S.tile_begin = tiles;
+    S.num_docs = seg.total_raw_docs;  // MatchEntireSegment / FilterPlanNode scan range [0, totalRawDocs)
+    S.num_tiles = int32_t((int64_t(S.num_docs) + kTileRows - 1) / kTileRows);
+    tiles += S.num_tiles;
+    P.total_raw += seg.total_raw_docs;
+    P.host_entries += int64_t(host_scan_leaves) * seg.total_raw_docs;
+    for (size_t c = 0; c < P.qcols.size(); ++c) {
+      const StagedColumn& col = seg.col(P.qcols[c]);
+      S.fwd[c] = col.fwd;
+      S.bits[c] = int8_t(col.bits);
+      S.dict[c] = col.dict_dev;
+      S.remap[c] = nullptr;
+    }
+    for (int g = 0; g < K.num_gcols; ++g) {
+      if (!P.gdicts[g].identity) {
+        const auto& rm = P.gdicts[g].remap[s];
+        P.fixes.push_back({size_t(s), 0, K.gcol[g], P.blob32.size()});
+        P.blob32.insert(P.blob32.end(), rm.begin(), rm.end());
+      }
+    }
+    // leaves
+    for (size_t l = 0; l < q.leaf_col.size(); ++l) {
+      const StagedColumn& col = seg.col(q.leaf_col[l]);
+      const pgx_leaf_binding& b = bindings[size_t(s) * q.leaf_col.size() + l];
+      KLeaf& L = S.leaf[l];
+      L.lo = b.lo;
+      L.hi = b.hi;
+      L.bitset = nullptr;
+      L.ranges = nullptr;
+      L.nranges = 0;
+      // matching dictIds
+      auto matches = [&](int id) -> bool {
+        if (b.words) return (b.words[id >> 5] >> (id & 31)) & 1u;
+        return id >= b.lo && id <= b.hi;
+      };
+      if (col.is_sorted) {
+        // SortedInvertedIndexBasedFilterOperator (additive ranges, merged), clipped to [0, totalRawDocs-1]
+        std::vector<int32_t> r;
+        for (int id = 0; id < col.card; ++id) {
+          if (!matches(id)) continue;
+          int32_t a = std::max(col.sorted_first[id], 0);
+          int32_t e = std::min(col.sorted_last[id], seg.total_raw_docs - 1);
+          if (e < a) continue;
+          if (!r.empty() && a <= r.back() + 1) r.back() = std::max(r.back(), e);
+          else { r.push_back(a); r.push_back(e); }
+        }
+        if (r.empty()) { L.mode = LEAF_NONE; continue; }
+        L.mode = LEAF_RANGES;
+        L.nranges = int32_t(r.size() / 2);
+        P.fixes.push_back({size_t(s), 1, int(l), P.blob32.size()});
+        P.blob32.insert(P.blob32.end(), r.begin(), r.end());
+      } else if (b.words) {
+        bool any = false;
+        const int nw = (col.card + 31) / 32;
+        for (int w = 0; w < nw && !any; ++w) any = b.words[w] != 0;
+        if (!any) { L.mode = LEAF_NONE; continue; }
+        L.mode = LEAF_SCAN_BITSET;
+        P.fixes.push_back({size_t(s), 2, int(l), P.blob32.size()});
+        for (int w = 0; w < nw; ++w) P.blob32.push_back(int32_t(b.words[w]));
+      } else {
+        L.mode = (b.hi < b.lo) ? LEAF_NONE : LEAF_SCAN_INTERVAL;
+      }
+    }
+  }
+  K.total_tiles = tiles;
+  K.num_segs = n;
+
+  // grid: persistent, contiguous tile ranges per workgroup
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
+    cus = prop.multiProcessorCount;
+  const int wgs_per_cu = (K.group_mode == G_NONE) ? 8 : 4;
+  const int64_t max_grid = int64_t(cus) * wgs_per_cu;
+  P.tiles_per_wg = std::max<int64_t>(1, (tiles + max_grid - 1) / max_grid);
+  P.grid = int(std::max<int64_t>(1, (tiles + P.tiles_per_wg - 1) / P.tiles_per_wg));
+}
+
+struct ExecBuffers {
+  DevBuf segs, blob, agg_out, stats, table, keys, key_state, overflow;
+};
+
+void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
+  B.blob = DevBuf(ctx, std::max<size_t>(16, P.blob32.size() * 4));
+  if (!P.blob32.empty())
+    hip_check(hipMemcpyAsync(B.blob.p, P.blob32.data(), P.blob32.size() * 4, hipMemcpyHostToDevice, st), "blob");
+  const int32_t* base = B.blob.as<int32_t>();
+  for (const auto& f : P.fixes) {
+    KSeg& S = P.ksegs[f.seg];
+    if (f.kind == 0) S.remap[f.slot] = base + f.off;
+    else if (f.kind == 1) S.leaf[f.slot].ranges = base + f.off;
+    else S.leaf[f.slot].bitset = reinterpret_cast<const uint32_t*>(base + f.off);
+  }
+  B.segs = DevBuf(ctx, P.ksegs.size() * sizeof(KSeg));
+  hip_check(hipMemcpyAsync(B.segs.p, P.ksegs.data(), P.ksegs.size() * sizeof(KSeg), hipMemcpyHostToDevice, st), "segs");
+  P.kq.segs = B.segs.as<KSeg>();
+}
+
+void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, uint64_t dense_out_bytes) {
+  KQuery& K = P.kq;
+  B.agg_out = DevBuf(ctx, 8 * (kMaxAggs + 1));
+  B.stats = DevBuf(ctx, 64);
+  B.overflow = DevBuf(ctx, 64);
+  K.agg_out = devp(B.agg_out);
+  K.stats = devp(B.stats);
+  K.overflow = devp(B.overflow);
+  K.table = nullptr;
+  K.keys = nullptr;
+  K.key_state = nullptr;
+  if (K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL) {
+    K.dense_slots = P.dense_slots;
+    const uint64_t bytes = P.dense_slots * K.num_planes * 8;
+    if (dense_out) {
+      if (dense_out_bytes < bytes) fail(PGX_ERR_INVALID_ARG, "dense_out too small");
+      K.table = static_cast<unsigned long long*>(dense_out);
+    } else {
+      B.table = DevBuf(ctx, bytes);
+      K.table = devp(B.table);
+    }
+  } else if (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) {
+    K.hash_cap = P.hash_cap;
+    B.table = DevBuf(ctx, P.hash_cap * K.num_planes * 8);
+    K.table = devp(B.table);
+    const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : P.hash_cap;
+    B.keys = DevBuf(ctx, kw * 8);
+    K.keys = devp(B.keys);
+    if (K.group_mode == G_HASH128) {
+      B.key_state = DevBuf(ctx, P.hash_cap * 4);
+      K.key_state = B.key_state.as<unsigned int>();
+    }
+  }
+}
+
+void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st) {
+  KQuery& K = P.kq;
+  std::vector<unsigned long long> init(kMaxAggs + 1, 0ull);
+  for (int p = 1; p < K.num_planes; ++p) init[p] = (K.plane_op[p] == P_MIN_ORD) ? ~0ull : 0ull;
+  hip_check(hipMemcpyAsync(B.agg_out.p, init.data(), init.size() * 8, hipMemcpyHostToDevice, st), "init");
+  hip_check(hipMemsetAsync(B.stats.p, 0, 64, st), "memset");
+  hip_check(hipMemsetAsync(B.overflow.p, 0, 64, st), "memset");
+  if (K.group_mode != G_NONE) {
+    const uint64_t slots = (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) ? P.hash_cap : P.dense_slots;
+    const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : (K.group_mode == G_HASH64 ? P.hash_cap : 0);
+    hip_check(pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
+  }
+}
+
+void launch_scan(ExecPlan& P, hipStream_t st) {
+  if (P.kq.total_tiles == 0) return;
+  hip_check(pgx_launch_scan(&P.kq, P.grid, P.tiles_per_wg, P.lds_bytes, st), "scan kernel launch");
+}
+
+void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, pgx_segment* const* segs, int n,
+                   hipStream_t st, pgx_result* R, const unsigned long long* dense_host_override) {
+  KQuery& K = P.kq;
+  unsigned long long stats[2] = {0, 0};
+  hip_check(hipMemcpyAsync(stats, B.stats.p, 16, hipMemcpyDeviceToHost, st), "stats D2H");
+  hip_check(hipStreamSynchronize(st), "sync");
+  R->stats[0] = int64_t(stats[0]);
+  R->stats[1] = int64_t(stats[1]) + P.host_entries;
+  R->stats[2] = int64_t(stats[0]) * P.n_proj;
+  R->stats[3] = P.total_raw;
+  R->num_aggs = K.num_aggs;
+  R->agg_fn = q.agg_fn;
+  R->top_n = q.top_n;
+  R->group_by = K.num_gcols > 0;
+  R->mode = P.mode_ref;
+  if (!R->group_by) {
+    unsigned long long acc[kMaxAggs + 1];
+    hip_check(hipMemcpy(acc, B.agg_out.p, 8 * (kMaxAggs + 1), hipMemcpyDeviceToHost), "agg D2H");
+    R->agg_value.assign(K.num_aggs, 0.0);
+    R->agg_count.assign(K.num_aggs, 0);
+    for (int a = 0; a < K.num_aggs; ++a) {
+      const int fn = K.agg_kind[a];
+      if (fn == A_COUNT) {
+        R->agg_count[a] = int64_t(acc[0]);
+        R->agg_value[a] = double(int64_t(acc[0]));
+      } else {
+        R->agg_value[a] = decode_plane(K.plane_op[a + 1], K.agg_fp[a], acc[a + 1], fn);
+        R->agg_count[a] = int64_t(acc[0]);
+      }
+    }
+    return;
+  }
+  // group-by: compact occupied slots
+  const bool hash = K.group_mode == G_HASH64 || K.group_mode == G_HASH128;
+  const uint64_t slots = hash ? P.hash_cap : P.dense_slots;
+  std::vector<int64_t> slot_ids;
+  std::vector<unsigned long long> planes;  // [plane][group]
+  uint64_t ng = 0;
+  if (dense_host_override) {
+    for (uint64_t s = 0; s < slots; ++s)
+      if (dense_host_override[s]) slot_ids.push_back(int64_t(s));
+    ng = slot_ids.size();
+    planes.resize(ng * K.num_planes);
+    for (int p = 0; p < K.num_planes; ++p)
+      for (uint64_t i = 0; i < ng; ++i) planes[p * ng + i] = dense_host_override[p * slots + slot_ids[i]];
+  } else {
+    DevBuf counter(ctx, 64);
+    hip_check(hipMemsetAsync(counter.p, 0, 8, st), "memset");
+    const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(slots, uint64_t(std::max<int64_t>(stats[0], 1))));
+    DevBuf oslot(ctx, cap * 8), oplanes(ctx, cap * K.num_planes * 8);
+    hip_check(pgx_launch_compact(K.table, slots, K.num_planes, devp(counter), oslot.as<int64_t>(), devp(oplanes), cap,
+                                 st),
+              "compact");
+    unsigned long long cnt = 0;
+    hip_check(hipMemcpyAsync(&cnt, counter.p, 8, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    ng = std::min<uint64_t>(cnt, cap);
+    slot_ids.resize(ng);
+    std::vector<unsigned long long> pl(cap * K.num_planes);
+    if (ng) {
+      hip_check(hipMemcpy(slot_ids.data(), oslot.p, ng * 8, hipMemcpyDeviceToHost), "D2H");
+      hip_check(hipMemcpy(pl.data(), oplanes.p, cap * K.num_planes * 8, hipMemcpyDeviceToHost), "D2H");
+    }
+    planes.resize(ng * K.num_planes);
+    for (int p = 0; p < K.num_planes; ++p)
+      for (uint64_t i = 0; i < ng; ++i) planes[p * ng + i] = pl[p * cap + i];
+  }
+  // keys
+  std::vector<unsigned long long> keys_lo, keys_hi;
+  if (hash && ng) {
+    const uint64_t kw = (K.group_mode == G_HASH128) ? 2 : 1;
+    std::vector<unsigned long long> all(slots * kw);
+    hip_check(hipMemcpy(all.data(), K.keys, slots * kw * 8, hipMemcpyDeviceToHost), "keys D2H");
+    keys_lo.resize(ng);
+    keys_hi.resize(ng, 0);
+    for (uint64_t i = 0; i < ng; ++i) {
+      keys_lo[i] = all[uint64_t(slot_ids[i]) * kw];
+      if (kw == 2) keys_hi[i] = all[uint64_t(slot_ids[i]) * 2 + 1];
+    }
+  }
+  // ARRAY_BASED iteration order is ascending raw key (DefaultGroupKeyGenerator.java:613-644): sort dense slots.
+  std::vector<uint64_t> order(ng);
+  std::iota(order.begin(), order.end(), 0);
+  if (!hash) std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return slot_ids[a] < slot_ids[b]; });
+  R->num_groups = int64_t(ng);
+  R->key_seg.assign(K.num_gcols, std::vector<int32_t>(ng));
+  R->key_id.assign(K.num_gcols, std::vector<int32_t>(ng));
+  for (uint64_t oi = 0; oi < ng; ++oi) {
+    const uint64_t i = order[oi];
+    for (int g = 0; g < K.num_gcols; ++g) {
+      int64_t gid;
+      if (!hash) {
+        gid = int64_t((uint64_t(slot_ids[i]) / K.gmul[g]) % uint64_t(P.gdicts[g].card));
+      } else {
+        const unsigned long long w = K.ghi[g] ? keys_hi[i] : keys_lo[i];
+        gid = int64_t((w >> K.gshift[g]) & ((1ull << P.gbits[g]) - 1ull));
+      }
+      R->key_seg[g][oi] = P.gdicts[g].rep_seg[gid];
+      R->key_id[g][oi] = P.gdicts[g].rep_id[gid];
+    }
+  }
+  R->g_value.assign(K.num_aggs, std::vector<double>(ng));
+  R->g_count.assign(K.num_aggs, std::vector<int64_t>(ng));
+  for (int a = 0; a < K.num_aggs; ++a) {
+    for (uint64_t oi = 0; oi < ng; ++oi) {
+      const uint64_t i = order[oi];
+      const int64_t cnt = int64_t(planes[i]);
+      R->g_count[a][oi] = cnt;
+      if (K.agg_kind[a] == A_COUNT) R->g_value[a][oi] = double(cnt);
+      else R->g_value[a][oi] = decode_plane(K.plane_op[a + 1], K.agg_fp[a], planes[(a + 1) * ng + i], K.agg_kind[a]);
+    }
+  }
+}
+
+uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {
+  uint64_t docs = 0;
+  for (int s = 0; s < n; ++s) docs += uint64_t(segs[s]->total_raw_docs);
+  uint64_t prod = 1;
+  bool big = false;
+  for (const auto& g : P.gdicts) {
+    if (prod > (uint64_t(1) << 40) / uint64_t(g.card)) big = true;
+    else prod *= uint64_t(g.card);
+  }
+  uint64_t want = std::max<uint64_t>(1024, std::min<uint64_t>(big ? docs : std::min(prod, docs), uint64_t(1) << 25));
+  uint64_t cap = 1;
+  while (cap < want * 2) cap <<= 1;
+  return cap;
+}
+
+void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
+               const pgx_exec_opts* opts, pgx_result* R) {
+  hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
+  const uint32_t xflags = opts ? opts->flags : 0;
+  ExecPlan P;
+  plan_query(ctx, q, segs, n, bindings, xflags, P);
+  ExecBuffers B;
+  upload_plan(ctx, P, B, st);
+  const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
+  if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
+  for (int attempt = 0; attempt < 6; ++attempt) {
+    alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
+    reset_outputs(P, B, st);
+    launch_scan(P, st);
+    if (!hash) break;
+    unsigned long long ovf = 0;
+    hip_check(hipMemcpyAsync(&ovf, B.overflow.p, 8, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    if (ovf == 0) break;
+    P.hash_cap *= 4;  // table full: grow and rerun
+    if (attempt == 5) fail(PGX_ERR_OOM, "group-by hash table overflow");
+  }
+  if (opts && (opts->flags & PGX_X_KEEP_DENSE_ON_DEVICE)) {
+    unsigned long long stats[2] = {0, 0};
+    hip_check(hipMemcpyAsync(stats, B.stats.p, 16, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    R->stats[0] = int64_t(stats[0]);
+    R->stats[1] = int64_t(stats[1]) + P.host_entries;
+    R->stats[2] = int64_t(stats[0]) * P.n_proj;
+    R->stats[3] = P.total_raw;
+    R->group_by = true;
+    R->num_aggs = P.kq.num_aggs;
+    R->agg_fn = q.agg_fn;
+    return;
+  }
+  finish_result(ctx, q, P, B, segs, n, st, R, nullptr);
+}
+
+}  // namespace
+
+// =================================================================================================
+// C ABI
+// =================================================================================================
+extern "C" {
+
+const char* pgx_last_error(void) { return g_last_error.c_str(); }
+int32_t pgx_abi_version(void) { return PGX_ABI_VERSION; }
+
+pgx_status pgx_ctx_create(const pgx_ctx_opts* opts, pgx_ctx** out) {
+  return guarded([&] {
+    if (!out) fail(PGX_ERR_INVALID_ARG, "out is NULL");
+    int ndev = 0;
+    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    const int dev = opts ? opts->device : 0;
+    if (dev < 0 || dev >= ndev) fail(PGX_ERR_DEVICE, "no HIP device " + std::to_string(dev));
+    hip_check(hipSetDevice(dev), "hipSetDevice");
+    auto* c = new pgx_ctx();
+    c->device = dev;
+    hip_check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+    *out = c;
+  });
+}
+
+pgx_status pgx_ctx_destroy(pgx_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->free_blocks) (void)hipFree(kv.second);
+    for (auto& kv : ctx->live) (void)hipFree(kv.first);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+  });
+}
+
+pgx_status pgx_segment_stage(pgx_ctx* ctx, const pgx_segment_desc* d, pgx_segment** out) {
+  return guarded([&] {
+    if (!ctx || !d || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    if (d->total_docs < 0 || d->total_raw_docs < 0 || d->total_raw_docs > d->total_docs)
+      fail(PGX_ERR_INVALID_ARG, "bad doc counts");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    auto seg = std::make_unique<pgx_segment>();
+    seg->ctx = ctx;
+    seg->name = d->name ? d->name : "";
+    seg->total_docs = d->total_docs;
+    seg->total_raw_docs = d->total_raw_docs;
+    seg->cols.resize(d->num_columns);
+    for (int i = 0; i < d->num_columns; ++i) {
+      stage_column(ctx, seg.get(), d->columns[i], d->mem == PGX_MEM_DEVICE, seg->cols[i]);
+      seg->by_name[seg->cols[i].name] = i;
+    }
+    if (d->star_tree && d->star_tree_len) {
+      const uint8_t* p = static_cast<const uint8_t*>(d->star_tree);
+      seg->star_tree.assign(p, p + d->star_tree_len);
+    }
+    *out = seg.release();
+  });
+}
+
+pgx_status pgx_segment_release(pgx_segment* seg) {
+  return guarded([&] { delete seg; });
+}
+
+pgx_status pgx_segment_device_bytes(const pgx_segment* seg, uint64_t* out) {
+  return guarded([&] {
+    if (!seg || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    *out = seg->device_bytes;
+  });
+}
+
+pgx_status pgx_query_compile(pgx_ctx* ctx, const pgx_query_desc* d, pgx_query** out) {
+  return guarded([&] {
+    if (!ctx || !d || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    auto q = std::make_unique<pgx_query>();
+    for (int a = 0; a < d->num_aggs; ++a) {
+      const int fn = d->aggs[a].fn;
+      if (fn < PGX_COUNT || fn > PGX_AVG) fail(PGX_ERR_UNSUPPORTED, "aggregation function not on the GPU path");
+      q->agg_fn.push_back(fn);
+      const char* c = d->aggs[a].column;
+      std::string col = (c && std::strcmp(c, "*") != 0) ? c : "";
+      if (fn != PGX_COUNT && col.empty()) fail(PGX_ERR_INVALID_ARG, "aggregation without column");
+      q->agg_col.push_back(fn == PGX_COUNT ? "" : col);
+    }
+    for (int g = 0; g < d->num_group_cols; ++g) q->group_cols.push_back(d->group_cols[g]);
+    q->top_n = d->top_n;
+    q->filter.assign(d->filter, d->filter + d->num_filter_nodes);
+    for (int l = 0; l < d->num_leaves; ++l) {
+      q->leaf_col.push_back(d->leaves[l].column);
+      q->leaf_kind.push_back(d->leaves[l].kind);
+    }
+    q->flags = d->flags;
+    *out = q.release();
+  });
+}
+
+pgx_status pgx_query_release(pgx_query* q) {
+  return guarded([&] { delete q; });
+}
+
+pgx_status pgx_execute(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
+                       const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out) {
+  return guarded([&] {
+    if (!ctx || !q || !segs || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    if (!q->leaf_col.empty() && !bindings) fail(PGX_ERR_INVALID_ARG, "filter leaves need bindings");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    auto R = std::make_unique<pgx_result>();
+    run_query(ctx, *q, segs, n, bindings, opts, R.get());
+    *out = R.release();
+  });
+}
+
+pgx_status pgx_result_release(pgx_result* r) {
+  return guarded([&] { delete r; });
+}
+
+pgx_status pgx_result_stats(const pgx_result* r, int64_t out[4]) {
+  return guarded([&] {
+    if (!r || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    for (int i = 0; i < 4; ++i) out[i] = r->stats[i];
+  });
+}
+
+pgx_status pgx_result_agg(const pgx_result* r, int32_t fn, double* value, int64_t* count) {
+  return guarded([&] {
+    if (!r) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    if (r->group_by) fail(PGX_ERR_INVALID_ARG, "group-by result");
+    if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
+    if (value) *value = r->agg_value[fn];
+    if (count) *count = r->agg_count[fn];
+  });
+}
+
+pgx_status pgx_result_num_groups(const pgx_result* r, int64_t* n) {
+  return guarded([&] {
+    if (!r || !n) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    *n = r->num_groups;
+  });
+}
+
+pgx_status pgx_result_group_keys(const pgx_result* r, int32_t c, int32_t* seg_index, int32_t* dict_id) {
+  return guarded([&] {
+    if (!r || !r->group_by) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
+    if (c < 0 || c >= int(r->key_seg.size())) fail(PGX_ERR_INVALID_ARG, "group column index");
+    if (seg_index) std::memcpy(seg_index, r->key_seg[c].data(), r->num_groups * 4);
+    if (dict_id) std::memcpy(dict_id, r->key_id[c].data(), r->num_groups * 4);
+  });
+}
+
+pgx_status pgx_result_group_values(const pgx_result* r, int32_t fn, double* value, int64_t* count) {
+  return guarded([&] {
+    if (!r || !r->group_by) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
+    if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
+    if (value) std::memcpy(value, r->g_value[fn].data(), r->num_groups * 8);
+    if (count) std::memcpy(count, r->g_count[fn].data(), r->num_groups * 8);
+  });
+}
+
+pgx_status pgx_result_group_mode(const pgx_result* r, int32_t* mode) {
+  return guarded([&] {
+    if (!r || !mode) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    *mode = r->mode;
+  });
+}
+
+pgx_status pgx_result_trim(const pgx_result* r, int32_t fn, int64_t* idx, int64_t* n) {
+  return guarded([&] {
+    if (!r || !r->group_by || !n) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
+    if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
+    const int64_t min_trim = std::max<int64_t>(r->top_n, 1000);
+    const int64_t threshold = min_trim * 20, size = min_trim * 5;
+    std::vector<int64_t> order(r->num_groups);
+    std::iota(order.begin(), order.end(), 0);
+    if (r->num_groups > threshold) {
+      const int f = r->agg_fn[fn];
+      const auto& v = r->g_value[fn];
+      const auto& c = r->g_count[fn];
+      auto key = [&](int64_t i) -> double {
+        if (f == PGX_AVG) return c[i] ? v[i] / double(c[i]) : 0.0;  // AvgPair compares by ratio
+        return v[i];
+      };
+      auto cmp = [&](int64_t a, int64_t b) { return (f == PGX_MIN) ? key(a) < key(b) : key(a) > key(b); };
+      std::nth_element(order.begin(), order.begin() + size, order.end(), cmp);
+      order.resize(size);
+      std::sort(order.begin(), order.end(), cmp);
+    }
+    if (idx) {
+      if (*n < int64_t(order.size())) fail(PGX_ERR_INVALID_ARG, "trim output capacity too small");
+      std::memcpy(idx, order.data(), order.size() * 8);
+    }
+    *n = int64_t(order.size());
+  });
+}
+
+pgx_status pgx_query_dense_slots(const pgx_query* q, pgx_segment* const* segs, int32_t n, int64_t* slots) {
+  return guarded([&] {
+    if (!q || !segs || !slots) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    uint64_t prod = 1;
+    for (const auto& g : q->group_cols) prod *= uint64_t(build_global_dict(segs, n, g).card);
+    *slots = int64_t(prod);
+  });
+}
+
+pgx_status pgx_query_dense_plane_op(const pgx_query* q, pgx_segment* const* segs, int32_t n, int32_t plane,
+                                    int32_t* op) {
+  return guarded([&] {
+    if (!q || !segs || !op) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    if (plane == 0) { *op = P_ADD_I64; return; }
+    if (plane < 1 || plane > int(q->agg_fn.size())) fail(PGX_ERR_INVALID_ARG, "plane");
+    const int fn = q->agg_fn[plane - 1];
+    if (fn == PGX_COUNT) { *op = P_ADD_I64; return; }
+    const StagedColumn& c = segs[0]->col(q->agg_col[plane - 1]);
+    const bool fp = c.data_type == PGX_FLOAT || c.data_type == PGX_DOUBLE;
+    *op = (fn == PGX_MIN) ? P_MIN_ORD : (fn == PGX_MAX) ? P_MAX_ORD : (fp ? P_ADD_F64 : P_ADD_I64);
+  });
+}
+
+pgx_status pgx_result_from_dense(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
+                                 const void* dense_device, const int64_t stats[4], pgx_result** out) {
+  return guarded([&] {
+    if (!ctx || !q || !segs || !dense_device || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    ExecPlan P;
+    std::vector<pgx_leaf_binding> none(size_t(n) * q->leaf_col.size(), pgx_leaf_binding{0, -1, nullptr});
+    plan_query(ctx, *q, segs, n, none.data(), 0, P);
+    if (!(P.kq.group_mode == G_DENSE_LDS || P.kq.group_mode == G_DENSE_GLOBAL))
+      fail(PGX_ERR_INVALID_ARG, "query is not dense");
+    const uint64_t total = P.dense_slots * P.kq.num_planes;
+    std::vector<unsigned long long> host(total);
+    hip_check(hipMemcpy(host.data(), dense_device, total * 8, hipMemcpyDeviceToHost), "dense D2H");
+    auto R = std::make_unique<pgx_result>();
+    ExecBuffers B;
+    B.stats = DevBuf(ctx, 64);
+    unsigned long long s2[2] = {static_cast<unsigned long long>(stats[0]), 0ull};
+    hip_check(hipMemcpy(B.stats.p, s2, 16, hipMemcpyHostToDevice), "H2D");
+    P.host_entries = stats[1];
+    finish_result(ctx, *q, P, B, segs, n, ctx->stream, R.get(), host.data());
+    R->stats[0] = stats[0];
+    R->stats[1] = stats[1];
+    R->stats[2] = stats[2];
+    R->stats[3] = stats[3];
+    *out = R.release();
+  });
+}
+
+pgx_status pgx_device_alloc(pgx_ctx* ctx, uint64_t bytes, void** out) {
+  return guarded([&] {
+    if (!ctx || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    void* p = nullptr;
+    if (hipMalloc(&p, std::max<uint64_t>(bytes, 256)) != hipSuccess) fail(PGX_ERR_OOM, "hipMalloc failed");
+    *out = p;
+  });
+}
+
+pgx_status pgx_device_free(pgx_ctx* ctx, void* p) {
+  return guarded([&] {
+    if (!ctx) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    if (p) hip_check(hipFree(p), "hipFree");
+  });
+}
+
+pgx_status pgx_copy_to_device(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+  return guarded([&] {
+    if (!ctx || !dst || !src) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    hip_check(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "H2D");
+  });
+}
+
+pgx_status pgx_synth_column(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
+                            uint64_t seed) {
+  return guarded([&] {
+    if (!ctx || !device_fwd) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    if (bits < 1 || bits > 32 || card < 1) fail(PGX_ERR_INVALID_ARG, "bits/card");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    const int64_t n_words = int64_t(padded_fwd_bytes(n_rows, bits) / 4);
+    hip_check(pgx_launch_synth(static_cast<uint32_t*>(device_fwd), n_rows, bits, uint32_t(card), seed, n_words,
+                               ctx->stream),
+              "synth launch");
+    hip_check(hipStreamSynchronize(ctx->stream), "sync");
+  });
+}
+
+pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
+                             const pgx_leaf_binding* bindings, int32_t iters, double* total_ms, double* kernel_ms,
+                             pgx_result** out) {
+  return guarded([&] {
+    if (!ctx || !q || !segs || iters < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t st = ctx->stream;
+    ExecPlan P;
+    plan_query(ctx, *q, segs, n, bindings, 0, P);
+    ExecBuffers B;
+    upload_plan(ctx, P, B, st);
+    const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
+    if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
+    alloc_outputs(ctx, P, B, nullptr, 0);
+    std::vector<hipEvent_t> ev(2 * iters);
+    for (auto& e : ev) hip_check(hipEventCreate(&e), "event");
+    hipEvent_t t0, t1;
+    hip_check(hipEventCreate(&t0), "event");
+    hip_check(hipEventCreate(&t1), "event");
+    hip_check(hipEventRecord(t0, st), "record");
+    for (int i = 0; i < iters; ++i) {
+      reset_outputs(P, B, st);
+      hip_check(hipEventRecord(ev[2 * i], st), "record");
+      launch_scan(P, st);
+      hip_check(hipEventRecord(ev[2 * i + 1], st), "record");
+    }
+    hip_check(hipEventRecord(t1, st), "record");
+    hip_check(hipEventSynchronize(t1), "sync");
+    float tot = 0, k = 0;
+    hip_check(hipEventElapsedTime(&tot, t0, t1), "elapsed");
+    for (int i = 0; i < iters; ++i) {
+      float x = 0;
+      hip_check(hipEventElapsedTime(&x, ev[2 * i], ev[2 * i + 1]), "elapsed");
+      k += x;
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(t0);
+    (void)hipEventDestroy(t1);
+    if (total_ms) *total_ms = tot;
+    if (kernel_ms) *kernel_ms = k / iters;
+    if (out) {
+      auto R = std::make_unique<pgx_result>();
+      finish_result(ctx, *q, P, B, segs, n, st, R.get(), nullptr);
+      *out = R.release();
+    }
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,89 @@
+// Internal host/device structures of libpgx (not part of the ABI).
+#pragma once
+#include <stdint.h>
+
+namespace pgx {
+
+constexpr int kTileRows = 8192;        // rows per workgroup tile = 256 lanes x 32 rows
+constexpr int kLaneRows = 32;          // rows owned by one lane: exactly one 32-bit mask word
+constexpr int kBlock = 256;            // threads per workgroup
+constexpr int kMaxQCols = 16;          // distinct columns a query touches
+constexpr int kMaxLeaves = 16;
+constexpr int kMaxAggs = 8;
+constexpr int kMaxGroupCols = 10;
+constexpr int kMaxProg = 64;
+constexpr int kStackDepth = 8;
+constexpr uint64_t kEmptyKey = ~0ull;
+
+enum LeafMode : int8_t {
+  LEAF_SCAN_INTERVAL = 0,  // decode + lo <= id <= hi
+  LEAF_SCAN_BITSET = 1,    // decode + bitset lookup
+  LEAF_RANGES = 2,         // sorted doc ranges
+  LEAF_NONE = 3,           // always false (empty binding)
+};
+
+enum ProgOp : int8_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_STAT = 3, OP_TRUE = 4 };
+
+enum AggKind : int8_t { A_COUNT = 0, A_SUM = 1, A_MIN = 2, A_MAX = 3, A_AVG = 4 };
+
+// Accumulator plane ops (pgx.h pgx_query_dense_plane_op)
+enum PlaneOp : int8_t { P_ADD_I64 = 0, P_ADD_F64 = 1, P_MIN_ORD = 2, P_MAX_ORD = 3 };
+
+enum GroupMode : int8_t { G_NONE = 0, G_DENSE_LDS = 1, G_DENSE_GLOBAL = 2, G_HASH64 = 3, G_HASH128 = 4 };
+
+struct KLeaf {
+  int32_t lo, hi;
+  const uint32_t* bitset;      // device, ceil(card/32) words (LEAF_SCAN_BITSET)
+  const int32_t* ranges;       // device, 2*nranges inclusive [a,b] pairs, sorted (LEAF_RANGES)
+  int32_t nranges;
+  int8_t mode;
+  int8_t pad[3];
+};
+
+struct KSeg {
+  int64_t tile_begin;          // global tile index of this segment's first tile
+  int32_t num_docs;            // rows scanned: [0, num_docs)
+  int32_t num_tiles;
+  const uint32_t* fwd[kMaxQCols];     // packed big-endian fixed-bit forward index (padded)
+  const void* dict[kMaxQCols];        // value columns: int64 (INT/LONG) or double (FLOAT/DOUBLE) per dictId
+  const int32_t* remap[kMaxQCols];    // group columns: dictId -> global id (nullptr = identity)
+  int8_t bits[kMaxQCols];
+  KLeaf leaf[kMaxLeaves];
+};
+
+struct KQuery {
+  const KSeg* segs;
+  int32_t num_segs;
+  int32_t num_qcols;
+  int64_t total_tiles;
+  // filter program (postfix, stack machine)
+  int32_t prog_len;
+  int8_t prog_op[kMaxProg];
+  int8_t prog_arg[kMaxProg];
+  int8_t leaf_col[kMaxLeaves];
+  // value columns decoded for aggregation (distinct), and aggs
+  int32_t num_aggs;
+  int8_t agg_kind[kMaxAggs];
+  int8_t agg_col[kMaxAggs];      // query-column slot (-1 for COUNT)
+  int8_t agg_fp[kMaxAggs];       // value column is FLOAT/DOUBLE
+  int8_t plane_op[kMaxAggs + 1]; // plane 0 = count
+  int32_t num_planes;            // 1 + num_aggs
+  // group-by
+  int8_t group_mode;
+  int32_t num_gcols;
+  int8_t gcol[kMaxGroupCols];
+  uint64_t gmul[kMaxGroupCols];  // dense: mixed-radix multiplier; hash: bit shift
+  int32_t gshift[kMaxGroupCols];
+  int32_t ghi[kMaxGroupCols];    // 128-bit keys: field goes to the high word
+  uint64_t dense_slots;          // dense key space
+  uint64_t hash_cap;             // power of two
+  // outputs
+  unsigned long long* agg_out;   // aggregation-only: num_planes accumulators (plane encodings)
+  unsigned long long* stats;     // [0] docs matched, [1] entries scanned in filter (kernel part)
+  unsigned long long* table;     // dense: planes x dense_slots ; hash: planes x hash_cap
+  unsigned long long* keys;      // hash: hash_cap (64-bit) or 2*hash_cap (128-bit: lo, hi)
+  unsigned int* key_state;       // hash128: 0 empty, 1 busy, 2 ready
+  unsigned long long* overflow;  // hash insert failures (table full) -> host retries bigger
+};
+
+}  // namespace pgx

@@ -1,0 +1,614 @@
+// MI355X (gfx950) kernels of the pinot-core segment query hot path.
+//
+// One fused kernel (pgx_scan_kernel) replaces the reference's per-doc Java loops for a whole query:
+//   a-1  fixed-bit forward-index decode     (util/PinotDataCustomBitSet.java:122-155)        -> decode32<B>
+//   a-6  scan predicates                    (operator/dociditerators/SVScanDocIdIterator.java) -> leaf words
+//   a-8  sorted-index ranges                (operator/filter/SortedInvertedIndexBasedFilterOperator.java) -> leaf words
+//   a-9/a-10 AND / OR doc-set algebra       (operator/docidsets/{And,Or}BlockDocIdSet.java)    -> bitwise ops on words
+//   a-12 doc-id compaction into blocks      (operator/BReusableFilteredDocIdSetOperator.java)  -> 32-row mask words
+//   a-13/a-3 projection + dictionary decode (operator/aggregation/DataBlockCache.java, Dictionary.readDoubleValues)
+//   a-14 aggregation                        (operator/aggregation/DefaultAggregationExecutor.java)
+//   a-15..a-17 group-by                     (operator/aggregation/groupby/DefaultGroupByExecutor.java,
+//                                            DefaultGroupKeyGenerator.java, DoubleGroupByResultHolder.java)
+//   a-19 combine over segments              (operator/MCombine*Operator.java): every segment accumulates into the
+//                                            same query-wide accumulators (global key ids), so the combine is free.
+//
+// Execution model: a workgroup (256 lanes = 4 waves) owns a TILE of 8192 consecutive rows of one segment; lane l owns
+// rows [32l, 32l+32) of the tile, i.e. exactly one 32-bit doc mask word and exactly B dwords of a B-bit forward index
+// (32*B bits), so no value straddles two lanes and every lane decodes from its own registers.  Workgroups walk a
+// contiguous range of tiles (persistent grid) so per-workgroup accumulators (registers / LDS tables) are flushed once.
+// The whole path is HBM-bound integer work: no MFMA.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "pgx_internal.h"
+
+namespace pgx {
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// ---------------------------------------------------------------------------------------------
+// K1: fixed-bit unpack.  The lane's 32 rows occupy B dwords starting at dword (row0/32)*B of the (big-endian,
+// MSB-first) forward index.  Loads are as wide as the lane chunk's alignment allows.
+// ---------------------------------------------------------------------------------------------
+template <int B>
+__device__ __forceinline__ void decode32(const uint32_t* __restrict__ p, uint32_t (&v)[32]) {
+  uint32_t w[B + 1];
+  if constexpr (B % 4 == 0) {
+#pragma unroll
+    for (int i = 0; i < B / 4; ++i) {
+      u32x4 q = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + i);
+      w[4 * i] = q.x; w[4 * i + 1] = q.y; w[4 * i + 2] = q.z; w[4 * i + 3] = q.w;
+    }
+  } else if constexpr (B % 2 == 0) {
+#pragma unroll
+    for (int i = 0; i < B / 2; ++i) {
+      u32x2 q = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p) + i);
+      w[2 * i] = q.x; w[2 * i + 1] = q.y;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < B; ++i) w[i] = __builtin_nontemporal_load(p + i);
+  }
+  w[B] = 0;
+#pragma unroll
+  for (int i = 0; i < B; ++i) w[i] = bswap32(w[i]);
+  constexpr uint32_t MASK = (B == 32) ? 0xFFFFFFFFu : ((1u << (B & 31)) - 1u);
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const int o = j * B;
+    const int k = o >> 5;
+    const int s = o & 31;
+    if (s + B <= 32) {
+      v[j] = (w[k] >> (32 - s - B)) & MASK;
+    } else {
+      const uint64_t win = (static_cast<uint64_t>(w[k]) << 32) | w[k + 1];
+      v[j] = static_cast<uint32_t>(win >> (64 - s - B)) & MASK;
+    }
+  }
+}
+
+#define PGX_DECODE_CASES(X) \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) \
+  X(17) X(18) X(19) X(20) X(21) X(22) X(23) X(24) X(25) X(26) X(27) X(28) X(29) X(30) X(31) X(32)
+
+__device__ __forceinline__ void decode_dyn(int bits, const uint32_t* __restrict__ fwd, int64_t lane_chunk,
+                                           uint32_t (&v)[32]) {
+  const uint32_t* p = fwd + lane_chunk * bits;
+  switch (bits) {
+#define PGX_CASE(b) \
+  case b:           \
+    decode32<b>(p, v); \
+    break;
+    PGX_DECODE_CASES(PGX_CASE)
+#undef PGX_CASE
+    default:
+#pragma unroll
+      for (int j = 0; j < 32; ++j) v[j] = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Accumulator encodings
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long ord_i64(int64_t x) {
+  return static_cast<unsigned long long>(x) ^ 0x8000000000000000ull;
+}
+__device__ __forceinline__ unsigned long long ord_f64(double d) {
+  unsigned long long b = __double_as_longlong(d);
+  return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Filter leaves
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t ranges_word(const KLeaf& L, int32_t row0) {
+  // Sorted-index doc ranges (inclusive, ascending, disjoint) -> this lane's 32-doc word.
+  const int32_t* r = L.ranges;
+  int lo = 0, hi = L.nranges;  // first range with end >= row0
+  while (lo < hi) {
+    int mid = (lo + hi) >> 1;
+    if (r[2 * mid + 1] < row0) lo = mid + 1; else hi = mid;
+  }
+  uint32_t word = 0;
+  const int32_t last = row0 + 31;
+  for (int i = lo; i < L.nranges; ++i) {
+    int32_t a = r[2 * i], b = r[2 * i + 1];
+    if (a > last) break;
+    int s = max(a, row0) - row0, e = min(b, last) - row0;
+    uint32_t m = (e - s == 31) ? 0xFFFFFFFFu : (((1u << (e - s + 1)) - 1u) << s);
+    word |= m;
+  }
+  return word;
+}
+
+__device__ __forceinline__ uint32_t leaf_word(const KSeg& S, const KQuery& Q, int leaf, int32_t row0,
+                                              int64_t lane_chunk) {
+  const KLeaf& L = S.leaf[leaf];
+  if (L.mode == LEAF_NONE) return 0u;
+  if (L.mode == LEAF_RANGES) return ranges_word(L, row0);
+  const int c = Q.leaf_col[leaf];
+  uint32_t v[32];
+  decode_dyn(S.bits[c], S.fwd[c], lane_chunk, v);
+  uint32_t word = 0;
+  if (L.mode == LEAF_SCAN_INTERVAL) {
+    const uint32_t lo = static_cast<uint32_t>(L.lo);
+    const uint32_t span = static_cast<uint32_t>(L.hi - L.lo);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) word |= static_cast<uint32_t>((v[j] - lo) <= span) << j;
+  } else {
+    const uint32_t* bs = L.bitset;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) word |= ((bs[v[j] >> 5] >> (v[j] & 31)) & 1u) << j;
+  }
+  return word;
+}
+
+// Stack machine over 32-bit doc words, registers only (no runtime-indexed arrays -> no scratch).
+struct WordStack {
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0, s4 = 0, s5 = 0, s6 = 0, s7 = 0;
+  __device__ __forceinline__ void push(uint32_t x) {
+    s7 = s6; s6 = s5; s5 = s4; s4 = s3; s3 = s2; s2 = s1; s1 = s0; s0 = x;
+  }
+  __device__ __forceinline__ void fold(bool is_and) {
+    s0 = is_and ? (s0 & s1) : (s0 | s1);
+    s1 = s2; s2 = s3; s3 = s4; s4 = s5; s5 = s6; s6 = s7; s7 = 0;
+  }
+};
+
+__device__ __forceinline__ uint32_t run_filter(const KSeg& S, const KQuery& Q, int32_t row0, int64_t lane_chunk,
+                                               uint32_t valid, unsigned long long& entries) {
+  if (Q.prog_len == 0) return valid;
+  WordStack st;
+  for (int pc = 0; pc < Q.prog_len; ++pc) {
+    const int op = Q.prog_op[pc];
+    const int arg = Q.prog_arg[pc];
+    if (op == OP_LEAF) {
+      st.push(leaf_word(S, Q, arg, row0, lane_chunk) & valid);
+    } else if (op == OP_AND) {
+      for (int k = 1; k < arg; ++k) st.fold(true);
+    } else if (op == OP_OR) {
+      for (int k = 1; k < arg; ++k) st.fold(false);
+    } else if (op == OP_STAT) {
+      entries += __popc(st.s0);
+    } else if (op == OP_TRUE) {
+      st.push(valid);
+    }
+  }
+  return st.s0 & valid;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Hash table (LONG_MAP / ARRAY_MAP group keys): open addressing, linear probing.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return x;
+}
+
+__device__ __forceinline__ int64_t hash_slot64(const KQuery& Q, uint64_t key) {
+  const uint64_t mask = Q.hash_cap - 1;
+  uint64_t h = mix64(key) & mask;
+  for (uint64_t probe = 0; probe < Q.hash_cap; ++probe) {
+    unsigned long long prev = atomicCAS(Q.keys + h, kEmptyKey, static_cast<unsigned long long>(key));
+    if (prev == kEmptyKey || prev == key) return static_cast<int64_t>(h);
+    h = (h + 1) & mask;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int64_t hash_slot128(const KQuery& Q, uint64_t klo, uint64_t khi) {
+  const uint64_t mask = Q.hash_cap - 1;
+  uint64_t h = mix64(klo ^ mix64(khi)) & mask;
+  uint64_t probes = 0;
+  // Every loop iteration makes progress for every lane (no divergent spin on another lane's write).
+  while (probes < Q.hash_cap) {
+    unsigned int st = atomicCAS(Q.key_state + h, 0u, 1u);
+    if (st == 0u) {
+      __hip_atomic_store(Q.keys + 2 * h, klo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(Q.keys + 2 * h + 1, khi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+      atomicExch(Q.key_state + h, 2u);
+      return static_cast<int64_t>(h);
+    }
+    if (st == 2u) {
+      unsigned long long a = __hip_atomic_load(Q.keys + 2 * h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long b = __hip_atomic_load(Q.keys + 2 * h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a == klo && b == khi) return static_cast<int64_t>(h);
+      h = (h + 1) & mask;
+      ++probes;
+    }
+    // st == 1: another lane is publishing this slot; re-read next iteration.
+  }
+  return -1;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Plane updates (LDS or global; the pointer's address space is known at each call site)
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void plane_update_global(unsigned long long* p, int op, unsigned long long enc) {
+  switch (op) {
+    case P_ADD_I64: atomicAdd(p, enc); break;
+    case P_ADD_F64: atomicAdd(reinterpret_cast<double*>(p), __longlong_as_double(static_cast<long long>(enc))); break;
+    case P_MIN_ORD: atomicMin(p, enc); break;
+    case P_MAX_ORD: atomicMax(p, enc); break;
+  }
+}
+
+__device__ __forceinline__ unsigned long long value_enc(const void* dict, bool fp, int kind, uint32_t id) {
+  if (fp) {
+    const double d = static_cast<const double*>(dict)[id];
+    if (kind == A_MIN || kind == A_MAX) return ord_f64(d);
+    return static_cast<unsigned long long>(__double_as_longlong(d));
+  }
+  const int64_t x = static_cast<const int64_t*>(dict)[id];
+  if (kind == A_MIN || kind == A_MAX) return ord_i64(x);
+  return static_cast<unsigned long long>(x);
+}
+
+__device__ __forceinline__ unsigned long long combine_enc(int op, unsigned long long x, unsigned long long y) {
+  if (op == P_ADD_I64) return x + y;
+  if (op == P_ADD_F64)
+    return static_cast<unsigned long long>(__double_as_longlong(__longlong_as_double(static_cast<long long>(x)) +
+                                                                __longlong_as_double(static_cast<long long>(y))));
+  if (op == P_MIN_ORD) return x < y ? x : y;
+  return x > y ? x : y;
+}
+
+__device__ __forceinline__ unsigned long long wave_reduce(int op, unsigned long long x) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) x = combine_enc(op, x, __shfl_xor(x, off));
+  return x;
+}
+
+__device__ __forceinline__ unsigned long long plane_identity(int op) { return op == P_MIN_ORD ? ~0ull : 0ull; }
+
+// ---------------------------------------------------------------------------------------------
+// The fused scan kernel.  GM selects the group-by storage at compile time:
+//   G_NONE aggregation-only | G_DENSE_LDS | G_DENSE_GLOBAL | G_HASH64 | G_HASH128
+// ---------------------------------------------------------------------------------------------
+template <int GM>
+__global__ void __launch_bounds__(kBlock) pgx_scan_kernel(const KQuery Q, int64_t tiles_per_wg) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long lds_table[];
+  __shared__ unsigned long long s_acc[kMaxAggs + 1];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int64_t t_begin = static_cast<int64_t>(blockIdx.x) * tiles_per_wg;
+  const int64_t t_end = min(t_begin + tiles_per_wg, Q.total_tiles);
+  if (t_begin >= t_end) return;
+
+  if (tid <= kMaxAggs) s_acc[tid] = (tid >= 1 && tid <= Q.num_aggs) ? plane_identity(Q.plane_op[tid]) : 0ull;
+  if constexpr (GM == G_DENSE_LDS) {
+    const uint64_t n = Q.dense_slots * Q.num_planes;
+    for (uint64_t i = tid; i < n; i += kBlock)
+      lds_table[i] = plane_identity(Q.plane_op[static_cast<int>(i / Q.dense_slots)]);
+  }
+  __syncthreads();
+
+  unsigned long long entries = 0;
+  unsigned long long docs = 0;
+
+  // Locate the first tile's segment (binary search, wave-uniform), then walk forward.
+  int seg;
+  {
+    int lo = 0, hi = Q.num_segs - 1;
+    while (lo < hi) {
+      int mid = (lo + hi + 1) >> 1;
+      if (Q.segs[mid].tile_begin <= t_begin) lo = mid; else hi = mid - 1;
+    }
+    seg = lo;
+  }
+
+  for (int64_t t = t_begin; t < t_end; ++t) {
+    while (seg + 1 < Q.num_segs && Q.segs[seg + 1].tile_begin <= t) ++seg;
+    const KSeg& S = Q.segs[seg];
+    const int64_t local_tile = t - S.tile_begin;
+    const int32_t row0 = static_cast<int32_t>(local_tile * kTileRows + tid * kLaneRows);
+    const int64_t lane_chunk = local_tile * kBlock + tid;  // lane chunk index within the segment
+    uint32_t valid;
+    if (row0 >= S.num_docs) valid = 0u;
+    else if (row0 + 32 <= S.num_docs) valid = 0xFFFFFFFFu;
+    else valid = (1u << (S.num_docs - row0)) - 1u;
+
+    uint32_t mask = 0;
+    if (valid) mask = run_filter(S, Q, row0, lane_chunk, valid, entries);
+    docs += __popc(mask);
+
+    if constexpr (GM == G_NONE) {
+      // ---- aggregation-only (a-14) ----
+      for (int a = 0; a < Q.num_aggs; ++a) {
+        const int kind = Q.agg_kind[a];
+        if (kind == A_COUNT) continue;
+        const int op = Q.plane_op[a + 1];
+        unsigned long long x = plane_identity(op);
+        if (mask) {
+          const int c = Q.agg_col[a];
+          uint32_t v[32];
+          decode_dyn(S.bits[c], S.fwd[c], lane_chunk, v);
+          const bool fp = Q.agg_fp[a];
+          if (kind == A_MIN || kind == A_MAX) {
+            // Dictionaries are sorted ascending (SegmentDictionaryCreator.build), so the extreme value is the value
+            // of the extreme dictId: one dictionary read per lane per tile instead of one per row.
+            uint32_t best = (kind == A_MIN) ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+            for (int j = 0; j < 32; ++j)
+              if ((mask >> j) & 1u) best = (kind == A_MIN) ? min(best, v[j]) : max(best, v[j]);
+            x = value_enc(S.dict[c], fp, kind, best);
+          } else if (fp) {
+            const double* d = static_cast<const double*>(S.dict[c]);
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < 32; ++j)
+              if ((mask >> j) & 1u) s += d[v[j]];
+            x = static_cast<unsigned long long>(__double_as_longlong(s));
+          } else {
+            const int64_t* d = static_cast<const int64_t*>(S.dict[c]);
+            int64_t s = 0;
+#pragma unroll
+            for (int j = 0; j < 32; ++j)
+              if ((mask >> j) & 1u) s += d[v[j]];
+            x = static_cast<unsigned long long>(s);
+          }
+        }
+        x = wave_reduce(op, x);
+        if (lane == 0) {
+          if (op == P_ADD_I64) atomicAdd(&s_acc[a + 1], x);
+          else if (op == P_ADD_F64) atomicAdd(reinterpret_cast<double*>(&s_acc[a + 1]),
+                                              __longlong_as_double(static_cast<long long>(x)));
+          else if (op == P_MIN_ORD) atomicMin(&s_acc[a + 1], x);
+          else atomicMax(&s_acc[a + 1], x);
+        }
+      }
+    } else {
+      // ---- group-by (a-15..a-17) ----
+      if (!mask) continue;
+      using KeyT = typename std::conditional<(GM == G_DENSE_LDS || GM == G_DENSE_GLOBAL), uint32_t, uint64_t>::type;
+      KeyT klo[32];
+      uint64_t khi[(GM == G_HASH128) ? 32 : 1];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) klo[j] = 0;
+      if constexpr (GM == G_HASH128) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) khi[j] = 0;
+      }
+      for (int g = 0; g < Q.num_gcols; ++g) {
+        const int c = Q.gcol[g];
+        uint32_t v[32];
+        decode_dyn(S.bits[c], S.fwd[c], lane_chunk, v);
+        const int32_t* rm = S.remap[c];
+        if (rm) {
+#pragma unroll
+          for (int j = 0; j < 32; ++j)
+            if ((mask >> j) & 1u) v[j] = static_cast<uint32_t>(rm[v[j]]);
+        }
+        if constexpr (GM == G_DENSE_LDS || GM == G_DENSE_GLOBAL) {
+          const uint32_t mul = static_cast<uint32_t>(Q.gmul[g]);
+#pragma unroll
+          for (int j = 0; j < 32; ++j) klo[j] += v[j] * mul;
+        } else {
+          const int sh = Q.gshift[g];
+          if (GM == G_HASH128 && Q.ghi[g]) {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) khi[(GM == G_HASH128) ? j : 0] |= static_cast<uint64_t>(v[j]) << sh;
+          } else {
+#pragma unroll
+            for (int j = 0; j < 32; ++j) klo[j] |= static_cast<uint64_t>(v[j]) << sh;
+          }
+        }
+      }
+      // Resolve hash slots in place (klo becomes the slot index).
+      uint32_t live = mask;
+      if constexpr (GM == G_HASH64 || GM == G_HASH128) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          if ((mask >> j) & 1u) {
+            int64_t s;
+            if constexpr (GM == G_HASH64) s = hash_slot64(Q, klo[j]);
+            else s = hash_slot128(Q, klo[j], khi[j]);
+            if (s < 0) live &= ~(1u << j);
+            klo[j] = static_cast<uint64_t>(s);
+          }
+        }
+        if (live != mask) atomicAdd(Q.overflow, static_cast<unsigned long long>(__popc(mask & ~live)));
+      }
+      const uint64_t stride = (GM == G_DENSE_LDS || GM == G_DENSE_GLOBAL) ? Q.dense_slots : Q.hash_cap;
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if ((live >> j) & 1u) {
+          if constexpr (GM == G_DENSE_LDS) atomicAdd(&lds_table[klo[j]], 1ull);
+          else atomicAdd(&Q.table[klo[j]], 1ull);
+        }
+      for (int a = 0; a < Q.num_aggs; ++a) {
+        const int kind = Q.agg_kind[a];
+        if (kind == A_COUNT) continue;
+        const int c = Q.agg_col[a];
+        uint32_t v[32];
+        decode_dyn(S.bits[c], S.fwd[c], lane_chunk, v);
+        const bool fp = Q.agg_fp[a];
+        const int op = Q.plane_op[a + 1];
+        const uint64_t pbase = static_cast<uint64_t>(a + 1) * stride;
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if ((live >> j) & 1u) {
+            const unsigned long long e = value_enc(S.dict[c], fp, kind, v[j]);
+            if constexpr (GM == G_DENSE_LDS) {
+              unsigned long long* p = &lds_table[pbase + klo[j]];
+              if (op == P_ADD_I64) atomicAdd(p, e);
+              else if (op == P_ADD_F64) atomicAdd(reinterpret_cast<double*>(p), __longlong_as_double(static_cast<long long>(e)));
+              else if (op == P_MIN_ORD) atomicMin(p, e);
+              else atomicMax(p, e);
+            } else {
+              plane_update_global(&Q.table[pbase + klo[j]], op, e);
+            }
+          }
+      }
+    }
+  }
+
+  // ---- flush: statistics, aggregation-only accumulators, LDS group table ----
+  unsigned long long d = wave_reduce(P_ADD_I64, docs);
+  unsigned long long e = wave_reduce(P_ADD_I64, entries);
+  if (lane == 0) {
+    if (d) atomicAdd(Q.stats + 0, d);
+    if (e) atomicAdd(Q.stats + 1, e);
+    if (GM == G_NONE && d) atomicAdd(&s_acc[0], d);
+  }
+  __syncthreads();
+  if constexpr (GM == G_NONE) {
+    if (tid < Q.num_planes) {
+      const int op = (tid == 0) ? P_ADD_I64 : Q.plane_op[tid];
+      if (tid == 0 || Q.agg_kind[tid - 1] != A_COUNT) plane_update_global(Q.agg_out + tid, op, s_acc[tid]);
+    }
+  }
+  if constexpr (GM == G_DENSE_LDS) {
+    const uint64_t n = Q.dense_slots * Q.num_planes;
+    for (uint64_t i = tid; i < n; i += kBlock) {
+      const uint64_t plane = i / Q.dense_slots;
+      const uint64_t s = i - plane * Q.dense_slots;
+      if (lds_table[s] == 0) continue;  // slot untouched by this workgroup
+      plane_update_global(Q.table + i, Q.plane_op[plane], lds_table[i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Table initialisation and compaction
+// ---------------------------------------------------------------------------------------------
+__global__ void pgx_init_planes(unsigned long long* table, uint64_t slots, int num_planes, const KQuery Q,
+                               unsigned long long* keys, uint64_t key_words, unsigned int* key_state) {
+  const uint64_t n = slots * num_planes;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const int plane = static_cast<int>(i / slots);
+    table[i] = (Q.plane_op[plane] == P_MIN_ORD) ? ~0ull : 0ull;
+  }
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < key_words; i += (uint64_t)gridDim.x * blockDim.x)
+    keys[i] = kEmptyKey;
+  if (key_state)
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < slots; i += (uint64_t)gridDim.x * blockDim.x)
+      key_state[i] = 0u;
+}
+
+// Emit occupied slots: out_slot[i] = slot index, out_planes[p*cap_out + i] = plane value.
+__global__ void pgx_compact(const unsigned long long* table, uint64_t slots, int num_planes,
+                            unsigned long long* counter, int64_t* out_slot, unsigned long long* out_planes,
+                            uint64_t cap_out) {
+  for (uint64_t s = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; s < slots; s += (uint64_t)gridDim.x * blockDim.x) {
+    const unsigned long long cnt = table[s];
+    if (cnt == 0) continue;
+    const unsigned long long i = atomicAdd(counter, 1ull);
+    if (i >= cap_out) continue;
+    out_slot[i] = static_cast<int64_t>(s);
+    for (int p = 0; p < num_planes; ++p) out_planes[p * cap_out + i] = table[p * slots + s];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Synthetic forward-index generator (benchmarks): dictId(row) = splitmix64(seed ^ row*golden) % card, packed
+// MSB-first big-endian.  One thread writes one 32-bit big-endian word = the 32 rows' bits that fall in it.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ uint32_t synth_value(uint64_t seed, int64_t row, uint32_t card) {
+  return static_cast<uint32_t>(splitmix64(seed ^ (static_cast<uint64_t>(row) * 0x9E3779B97F4A7C15ull)) % card);
+}
+
+__global__ void pgx_synth_kernel(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
+                                 int64_t n_words) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bit0 = w * 32;
+    const int64_t r_first = bit0 / bits;
+    const int64_t r_last = (bit0 + 31) / bits;
+    uint32_t word = 0;
+    for (int64_t r = r_first; r <= r_last; ++r) {
+      if (r >= n_rows) break;
+      const uint64_t v = synth_value(seed, r, card);
+      // bits of row r occupy [r*bits, r*bits+bits); MSB-first.
+      const int64_t rs = r * bits;
+      // position of row's MSB relative to word start
+      const int64_t off = rs - bit0;  // may be negative
+      // shift so that the row's bits land in the word (bit 31 = first bit of the word)
+      const int64_t sh = 32 - off - bits;  // left shift amount (may be negative)
+      uint64_t placed;
+      if (sh >= 0) placed = v << sh;
+      else placed = v >> (-sh);
+      word |= static_cast<uint32_t>(placed & 0xFFFFFFFFull);
+    }
+    out_words[w] = bswap32(word);
+  }
+}
+
+}  // namespace pgx
+
+// ---------------------------------------------------------------------------------------------
+// Host-side launchers (called from pgx_host.cpp)
+// ---------------------------------------------------------------------------------------------
+extern "C" hipError_t pgx_launch_scan(const pgx::KQuery* q, int grid, int64_t tiles_per_wg, size_t lds_bytes,
+                                      hipStream_t stream) {
+  switch (q->group_mode) {
+    case pgx::G_NONE:
+      hipLaunchKernelGGL(pgx::pgx_scan_kernel<pgx::G_NONE>, dim3(grid), dim3(pgx::kBlock), lds_bytes, stream, *q,
+                         tiles_per_wg);
+      break;
+    case pgx::G_DENSE_LDS:
+      hipLaunchKernelGGL(pgx::pgx_scan_kernel<pgx::G_DENSE_LDS>, dim3(grid), dim3(pgx::kBlock), lds_bytes, stream, *q,
+                         tiles_per_wg);
+      break;
+    case pgx::G_DENSE_GLOBAL:
+      hipLaunchKernelGGL(pgx::pgx_scan_kernel<pgx::G_DENSE_GLOBAL>, dim3(grid), dim3(pgx::kBlock), lds_bytes, stream,
+                         *q, tiles_per_wg);
+      break;
+    case pgx::G_HASH64:
+      hipLaunchKernelGGL(pgx::pgx_scan_kernel<pgx::G_HASH64>, dim3(grid), dim3(pgx::kBlock), lds_bytes, stream, *q,
+                         tiles_per_wg);
+      break;
+    case pgx::G_HASH128:
+      hipLaunchKernelGGL(pgx::pgx_scan_kernel<pgx::G_HASH128>, dim3(grid), dim3(pgx::kBlock), lds_bytes, stream, *q,
+                         tiles_per_wg);
+      break;
+    default:
+      return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t slots, int num_planes,
+                                             const pgx::KQuery* q, unsigned long long* keys, uint64_t key_words,
+                                             unsigned int* key_state, hipStream_t stream) {
+  uint64_t n = slots * num_planes;
+  if (key_words > n) n = key_words;
+  int grid = static_cast<int>(std::min<uint64_t>((n + 255) / 256, 8192));
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(pgx::pgx_init_planes, dim3(grid), dim3(256), 0, stream, table, slots, num_planes, *q, keys,
+                     key_words, key_state);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
+                                         unsigned long long* counter, int64_t* out_slot,
+                                         unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream) {
+  int grid = static_cast<int>(std::min<uint64_t>((slots + 255) / 256, 8192));
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(pgx::pgx_compact, dim3(grid), dim3(256), 0, stream, table, slots, num_planes, counter, out_slot,
+                     out_planes, cap_out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
+                                       int64_t n_words, hipStream_t stream) {
+  int grid = static_cast<int>(std::min<int64_t>((n_words + 255) / 256, 65536));
+  if (grid < 1) grid = 1;
+  hipLaunchKernelGGL(pgx::pgx_synth_kernel, dim3(grid), dim3(256), 0, stream, out_words, n_rows, bits, card, seed,
+                     n_words);
+  return hipGetLastError();
+}

@@ -1,0 +1,596 @@
+"""Host-side mirror of the reference's plan-maker / operator API over libpgx (the MI355X path).
+
+Names and argument meaning follow pinot-core (paths relative to pinot-core/src/main/java/com/linkedin/pinot/core/):
+
+  InstancePlanMakerImplV2.make_inner_segment_plan(segment, broker_request) -> PlanNode   (plan/maker/InstancePlanMakerImplV2.java:72-82)
+  InstancePlanMakerImplV2.make_inter_segment_plan(segments, broker_request) -> Plan      (:93-109, plan/CombinePlanNode.java)
+  PlanNode.run() -> Operator ; Operator.next_block() -> IntermediateResultsBlock          (plan/PlanNode.java:31, common/Operator.java:25-48)
+  Operator.get_execution_statistics() -> ExecutionStatistics                              (operator/ExecutionStatistics.java:21-74)
+  AggregationGroupByResult.get_group_key_iterator() / get_result_for_key(key, i)          (operator/aggregation/groupby/AggregationGroupByResult.java:56-113)
+
+The per-segment predicate -> dictId resolution (a-4, operator/filter/predicate/*PredicateEvaluator.java) runs here on the
+host, exactly where the Java caller would run its PredicateEvaluatorProvider before crossing the JNI boundary; every
+doc-level step runs in the HIP kernel.  Unsupported shapes raise PgxError(PGX_ERR_UNSUPPORTED) so a caller can fall back
+to the Java operators; nothing here computes results on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import native as N
+from .segment import Column, SegmentData
+
+_DT = {"INT": N.PGX_INT, "LONG": N.PGX_LONG, "FLOAT": N.PGX_FLOAT, "DOUBLE": N.PGX_DOUBLE, "STRING": N.PGX_STRING}
+_FN = {"count": N.PGX_COUNT, "sum": N.PGX_SUM, "min": N.PGX_MIN, "max": N.PGX_MAX, "avg": N.PGX_AVG}
+
+
+# ------------------------------------------------------------------------------------------------
+# Context / staged segments
+# ------------------------------------------------------------------------------------------------
+class Context:
+    """One pgx_ctx bound to one HIP device (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        L = N.lib()
+        h = C.c_void_p()
+        N.check(L.pgx_ctx_create(C.byref(N.CtxOpts(device, 0)), C.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            N.lib().pgx_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _java_double_str(x: float) -> str:
+    """Double.toString formatting for FLOAT/DOUBLE group keys."""
+    if x != x:
+        return "NaN"
+    if math.isinf(x):
+        return "Infinity" if x > 0 else "-Infinity"
+    if x == 0:
+        return "-0.0" if math.copysign(1, x) < 0 else "0.0"
+    a = abs(x)
+    if 1e-3 <= a < 1e7:
+        s = repr(float(x))
+        if "e" in s or "E" in s:
+            s = "%f" % x
+        return s if "." in s else s + ".0"
+    m, e = ("%.17e" % x).split("e")
+    r = repr(float(x))
+    digits = r.replace("-", "").replace(".", "").split("e")[0].lstrip("0") or "0"
+    exp = int(e)
+    mant = digits[0] + "." + (digits[1:].rstrip("0") or "0")
+    return ("-" if x < 0 else "") + mant + "E" + str(exp)
+
+
+@dataclass
+class _ColInfo:
+    meta: Column
+    values: object  # numpy array (numeric) or list of str
+
+    def index_of(self, raw: str) -> int:
+        """Dictionary.indexOf: binary search, -(insertion point)-1 when absent (segment/index/readers/*Dictionary.java)."""
+        dt = self.meta.data_type
+        if dt == "STRING":
+            width = self.meta.dict_width
+            pad = self.meta.pad_char
+            b = raw.encode("utf-8")
+            key = raw if len(b) >= width else raw + pad * (width - len(b))
+            padded = [v + pad * (width - len(v.encode("utf-8"))) for v in self.values]
+            lo, hi = 0, len(padded)
+            while lo < hi:
+                mid = (lo + hi) // 2
+                if padded[mid] < key:
+                    lo = mid + 1
+                else:
+                    hi = mid
+            return lo if lo < len(padded) and padded[lo] == key else -(lo + 1)
+        if dt in ("INT", "LONG"):
+            v = int(raw)  # Integer.parseInt / Long.parseLong semantics (raises on non-integers)
+        else:
+            v = float(raw)
+        arr = self.values
+        pos = int(np.searchsorted(arr, v, side="left"))
+        return pos if pos < len(arr) and arr[pos] == v else -(pos + 1)
+
+    def string_of(self, dict_id: int) -> str:
+        dt = self.meta.data_type
+        v = self.values[dict_id]
+        if dt == "STRING":
+            return v
+        if dt in ("INT", "LONG"):
+            return str(int(v))
+        if dt == "FLOAT":
+            return _java_double_str(float(np.float32(v)))
+        return _java_double_str(float(v))
+
+
+class IndexSegment:
+    """A segment staged into HBM (Loaders.IndexSegment.load equivalent)."""
+
+    def __init__(self, ctx: Context, seg: SegmentData, device_buffers: Optional[Dict[str, int]] = None):
+        self.ctx = ctx
+        self.data = seg
+        self.name = seg.name
+        self._cols: Dict[str, _ColInfo] = {}
+        descs = (N.ColumnDesc * len(seg.columns))()
+        keep = []
+        for i, (name, c) in enumerate(seg.columns.items()):
+            d = descs[i]
+            nb = name.encode()
+            keep.append(nb)
+            d.name = nb
+            d.data_type = _DT[c.data_type]
+            d.cardinality = c.cardinality
+            d.bits_per_element = c.bits
+            d.is_sorted = int(c.is_sorted)
+            d.dict_width = c.dict_width
+            for attr, data in (("fwd", c.fwd_bytes), ("sorted_pairs", c.sorted_bytes), ("dict", c.dict_bytes),
+                               ("inv", c.inv_bytes)):
+                if data is None:
+                    setattr(d, attr, None)
+                    continue
+                buf = C.create_string_buffer(bytes(data), len(data))
+                keep.append(buf)
+                setattr(d, attr, C.cast(buf, C.c_void_p))
+            d.fwd_len = len(c.fwd_bytes) if c.fwd_bytes is not None else 0
+            d.sorted_len = len(c.sorted_bytes) if c.sorted_bytes is not None else 0
+            d.dict_len = len(c.dict_bytes)
+            d.inv_len = len(c.inv_bytes) if c.inv_bytes is not None else 0
+        sd = N.SegmentDesc()
+        sd.name = seg.name.encode()
+        sd.total_docs = seg.total_docs
+        sd.total_raw_docs = seg.total_raw_docs
+        sd.num_columns = len(seg.columns)
+        sd.columns = descs
+        if seg.star_tree is not None:
+            st = C.create_string_buffer(bytes(seg.star_tree), len(seg.star_tree))
+            keep.append(st)
+            sd.star_tree = C.cast(st, C.c_void_p)
+            sd.star_tree_len = len(seg.star_tree)
+        sd.mem = N.PGX_MEM_HOST
+        h = C.c_void_p()
+        N.check(N.lib().pgx_segment_stage(ctx.handle, C.byref(sd), C.byref(h)))
+        self.handle = h
+        del keep  # the library copied every host buffer during staging
+
+    @classmethod
+    def from_device(cls, ctx: Context, seg: SegmentData, fwd_device: Dict[str, int]):
+        """Stage a segment whose forward indexes already live in HBM (synthetic benchmark data)."""
+        self = cls.__new__(cls)
+        self.ctx = ctx
+        self.data = seg
+        self.name = seg.name
+        self._cols = {}
+        descs = (N.ColumnDesc * len(seg.columns))()
+        keep = []
+        dict_dev = []
+        for i, (name, c) in enumerate(seg.columns.items()):
+            d = descs[i]
+            nb = name.encode()
+            keep.append(nb)
+            d.name = nb
+            d.data_type = _DT[c.data_type]
+            d.cardinality = c.cardinality
+            d.bits_per_element = c.bits
+            d.is_sorted = 0
+            d.dict_width = c.dict_width
+            d.fwd = C.c_void_p(fwd_device[name][0])
+            d.fwd_len = fwd_device[name][1]
+            p = C.c_void_p()
+            N.check(N.lib().pgx_device_alloc(ctx.handle, len(c.dict_bytes), C.byref(p)))
+            N.check(N.lib().pgx_copy_to_device(ctx.handle, p, c.dict_bytes, len(c.dict_bytes)))
+            dict_dev.append(p)
+            d.dict = p
+            d.dict_len = len(c.dict_bytes)
+        sd = N.SegmentDesc()
+        sd.name = seg.name.encode()
+        sd.total_docs = seg.total_docs
+        sd.total_raw_docs = seg.total_raw_docs
+        sd.num_columns = len(seg.columns)
+        sd.columns = descs
+        sd.mem = N.PGX_MEM_DEVICE
+        h = C.c_void_p()
+        N.check(N.lib().pgx_segment_stage(ctx.handle, C.byref(sd), C.byref(h)))
+        for p in dict_dev:
+            N.lib().pgx_device_free(ctx.handle, p)
+        self.handle = h
+        return self
+
+    def column(self, name: str) -> _ColInfo:
+        if name not in self._cols:
+            c = self.data.columns.get(name)
+            if c is None:
+                raise KeyError("segment %s has no column %s" % (self.name, name))
+            vals = c.dictionary_values()
+            if c.data_type != "STRING":
+                vals = np.asarray(vals).astype(vals.dtype.newbyteorder("="))
+            self._cols[name] = _ColInfo(c, vals)
+        return self._cols[name]
+
+    def device_bytes(self) -> int:
+        v = C.c_uint64()
+        N.check(N.lib().pgx_segment_device_bytes(self.handle, C.byref(v)))
+        return v.value
+
+    def destroy(self):
+        if getattr(self, "handle", None):
+            N.lib().pgx_segment_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.destroy()
+        except Exception:
+            pass
+
+
+# ------------------------------------------------------------------------------------------------
+# a-4: predicate -> dictId binding (PredicateEvaluatorProvider and the evaluators, operator/filter/predicate/)
+# ------------------------------------------------------------------------------------------------
+def _parse_range(rng: str):
+    """RangePredicate (common/predicate/RangePredicate.java:31-57)."""
+    s = rng.strip()
+    a, b = s.split("\t\t")[0], s.split("\t\t")[1]
+    lower, upper = a[1:], b[:-1]
+    inc_lo = (lower == "*") if s.startswith("(") else True
+    inc_hi = (upper == "*") if s.endswith(")") else True
+    return lower, upper, inc_lo, inc_hi
+
+
+def resolve_leaf(col: _ColInfo, leaf: dict):
+    """Returns (lo, hi, words|None): docs match iff dictId in [lo,hi] (words None) or bit set in words."""
+    card = col.meta.cardinality
+    op = leaf["op"]
+    if op == "RANGE":  # RangeOfflineDictionaryPredicateEvaluator.java:30-65
+        lower, upper, inc_lo, inc_hi = _parse_range(leaf["values"][0])
+        start = 0 if lower == "*" else col.index_of(lower)
+        end = card - 1 if upper == "*" else col.index_of(upper)
+        if start < 0:
+            start = -(start + 1)
+        elif not inc_lo and lower != "*":
+            start += 1
+        if end < 0:
+            end = -(end + 1) - 1
+        elif not inc_hi and upper != "*":
+            end -= 1
+        return (start, end, None) if end >= start else (0, -1, None)
+    if op == "EQ":  # EqualsPredicateEvaluator.java:28-42
+        i = col.index_of(leaf["values"][0])
+        return (i, i, None) if i >= 0 else (0, -1, None)
+    m = np.zeros(card, dtype=bool)
+    if op == "IN":
+        for v in leaf["values"]:
+            i = col.index_of(v)
+            if i >= 0:
+                m[i] = True
+    elif op in ("NEQ", "NOT_IN"):
+        m[:] = True
+        for v in leaf["values"]:
+            i = col.index_of(v)
+            if i >= 0:
+                m[i] = False
+    else:
+        raise ValueError("unsupported predicate " + op)
+    ids = np.nonzero(m)[0]
+    if len(ids) == 0:
+        return (0, -1, None)
+    if ids[-1] - ids[0] + 1 == len(ids):
+        return (int(ids[0]), int(ids[-1]), None)
+    words = np.packbits(np.pad(m, (0, (-card) % 32)).reshape(-1, 32)[:, ::-1], axis=1,
+                        bitorder="big").view(">u4").astype(np.uint32).reshape(-1)
+    return (0, -1, np.ascontiguousarray(words))
+
+
+def _flatten_filter(tree):
+    """FilterQueryTree -> postfix nodes + leaf list."""
+    nodes, leaves = [], []
+
+    def walk(t):
+        if t["op"] in ("AND", "OR"):
+            for c in t["children"]:
+                walk(c)
+            nodes.append((N.PGX_F_AND if t["op"] == "AND" else N.PGX_F_OR, len(t["children"])))
+        else:
+            nodes.append((N.PGX_F_LEAF, len(leaves)))
+            leaves.append(t)
+
+    if tree is not None:
+        walk(tree)
+    return nodes, leaves
+
+
+# ------------------------------------------------------------------------------------------------
+# Results
+# ------------------------------------------------------------------------------------------------
+@dataclass
+class ExecutionStatistics:
+    num_docs_scanned: int = 0
+    num_entries_scanned_in_filter: int = 0
+    num_entries_scanned_post_filter: int = 0
+    num_total_raw_docs: int = 0
+
+    def as_list(self):
+        return [self.num_docs_scanned, self.num_entries_scanned_in_filter, self.num_entries_scanned_post_filter,
+                self.num_total_raw_docs]
+
+
+@dataclass
+class GroupKey:
+    group_id: int
+    string_key: str
+
+
+class AggregationGroupByResult:
+    """operator/aggregation/groupby/AggregationGroupByResult.java:56-113 over the columnar pgx result."""
+
+    def __init__(self, keys: List[str], values: List[list], fns: List[str], mode: str, raw_keys=None):
+        self._keys = keys
+        self._values = values  # [group][fn]
+        self.fns = fns
+        self.storage_mode = mode
+        self.raw_keys = raw_keys
+
+    def get_group_key_iterator(self):
+        for i, k in enumerate(self._keys):
+            yield GroupKey(i, k)
+
+    def get_result_for_key(self, key: GroupKey, fn_index: int):
+        return self._values[key.group_id][fn_index]
+
+    def num_groups(self):
+        return len(self._keys)
+
+    def as_map(self) -> Dict[str, list]:
+        return {k: v for k, v in zip(self._keys, self._values)}
+
+
+@dataclass
+class IntermediateResultsBlock:
+    aggregation_result: Optional[list] = None
+    aggregation_group_by_result: Optional[AggregationGroupByResult] = None
+    trimmed: Optional[List[Dict[str, object]]] = None  # combine output after trimToSize (one map per function)
+    stats: ExecutionStatistics = field(default_factory=ExecutionStatistics)
+
+    def get_aggregation_result(self):
+        return self.aggregation_result
+
+    def get_aggregation_group_by_result(self):
+        return self.aggregation_group_by_result
+
+
+_MODES = {0: "ARRAY_BASED", 1: "LONG_MAP_BASED", 2: "ARRAY_MAP_BASED"}
+
+
+class _Query:
+    """A compiled pgx_query for one broker request."""
+
+    def __init__(self, ctx: Context, request: dict):
+        self.ctx = ctx
+        self.request = request
+        aggs = request["aggregations"]
+        self.fns = [a["fn"] for a in aggs]
+        self._keep = []
+        agg_arr = (N.Agg * len(aggs))()
+        for i, a in enumerate(aggs):
+            agg_arr[i].fn = _FN[a["fn"]]
+            col = None if a["column"] == "*" else a["column"].encode()
+            self._keep.append(col)
+            agg_arr[i].column = col
+        gb = request.get("group_by")
+        gcols = gb["columns"] if gb else []
+        garr = (C.c_char_p * max(1, len(gcols)))(*[g.encode() for g in gcols])
+        nodes, leaves = _flatten_filter(request.get("filter"))
+        self.leaves = leaves
+        narr = (N.FilterNode * max(1, len(nodes)))()
+        for i, (op, arg) in enumerate(nodes):
+            narr[i].op, narr[i].arg = op, arg
+        larr = (N.Leaf * max(1, len(leaves)))()
+        for i, lf in enumerate(leaves):
+            cb = lf["column"].encode()
+            self._keep.append(cb)
+            larr[i].column = cb
+            larr[i].kind = N.PGX_PRED[lf["op"]]
+        qd = N.QueryDesc(len(aggs), agg_arr, len(gcols), garr, gb["top_n"] if gb else 10, len(nodes), narr,
+                         len(leaves), larr, 0)
+        self._keep += [agg_arr, garr, narr, larr]
+        h = C.c_void_p()
+        N.check(N.lib().pgx_query_compile(ctx.handle, C.byref(qd), C.byref(h)))
+        self.handle = h
+        self.group_cols = gcols
+
+    def bindings(self, segments: Sequence[IndexSegment]):
+        nl = len(self.leaves)
+        arr = (N.LeafBinding * max(1, len(segments) * nl))()
+        keep = []
+        for s, seg in enumerate(segments):
+            for l, leaf in enumerate(self.leaves):
+                lo, hi, words = resolve_leaf(seg.column(leaf["column"]), leaf)
+                b = arr[s * nl + l]
+                b.lo, b.hi = lo, hi
+                if words is not None:
+                    keep.append(words)
+                    b.words = words.ctypes.data_as(C.POINTER(C.c_uint32))
+                else:
+                    b.words = None
+        return arr, keep
+
+    def execute(self, segments: Sequence[IndexSegment], flags: int = 0, dense_out=None, dense_out_bytes: int = 0):
+        segs = (C.c_void_p * len(segments))(*[s.handle.value for s in segments])
+        binds, keep = self.bindings(segments)
+        opts = N.ExecOpts(0, dense_out, dense_out_bytes, flags)
+        r = C.c_void_p()
+        N.check(N.lib().pgx_execute(self.ctx.handle, self.handle, segs, len(segments), binds, C.byref(opts),
+                                    C.byref(r)))
+        return r
+
+    def close(self):
+        if getattr(self, "handle", None):
+            N.lib().pgx_query_release(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def decode_result(q: _Query, r, segments: Sequence[IndexSegment], trim: bool = False) -> IntermediateResultsBlock:
+    L = N.lib()
+    st = (C.c_int64 * 4)()
+    N.check(L.pgx_result_stats(r, st))
+    blk = IntermediateResultsBlock(stats=ExecutionStatistics(*list(st)))
+    if not q.group_cols:
+        out = []
+        for i, fn in enumerate(q.fns):
+            v, c = C.c_double(), C.c_int64()
+            N.check(L.pgx_result_agg(r, i, C.byref(v), C.byref(c)))
+            if fn == "count":
+                out.append(int(c.value))  # MutableLongValue
+            elif fn == "avg":
+                out.append((v.value, int(c.value)))  # AvgPair(sum, count)
+            else:
+                out.append(v.value)
+        blk.aggregation_result = out
+        return blk
+    ng = C.c_int64()
+    N.check(L.pgx_result_num_groups(r, C.byref(ng)))
+    n = ng.value
+    mode = C.c_int32()
+    N.check(L.pgx_result_group_mode(r, C.byref(mode)))
+    key_parts = []
+    raw = []
+    for g, col in enumerate(q.group_cols):
+        si = np.zeros(max(n, 1), dtype=np.int32)
+        di = np.zeros(max(n, 1), dtype=np.int32)
+        N.check(L.pgx_result_group_keys(r, g, si.ctypes.data, di.ctypes.data))
+        infos = [seg.column(col) for seg in segments]
+        key_parts.append([infos[si[i]].string_of(int(di[i])) for i in range(n)])
+        raw.append(di[:n].copy())
+    keys = ["\t".join(p[i] for p in key_parts) for i in range(n)]
+    vals = []
+    for i, fn in enumerate(q.fns):
+        v = np.zeros(max(n, 1), dtype=np.float64)
+        c = np.zeros(max(n, 1), dtype=np.int64)
+        N.check(L.pgx_result_group_values(r, i, v.ctypes.data, c.ctypes.data))
+        if fn == "count":
+            vals.append([int(x) for x in c[:n]])
+        elif fn == "avg":
+            vals.append([(float(a), int(b)) for a, b in zip(v[:n], c[:n])])
+        else:
+            vals.append([float(x) for x in v[:n]])
+    per_group = [[vals[f][i] for f in range(len(q.fns))] for i in range(n)]
+    blk.aggregation_group_by_result = AggregationGroupByResult(keys, per_group, q.fns, _MODES[mode.value],
+                                                               raw_keys=raw)
+    if trim:
+        trimmed = []
+        for i in range(len(q.fns)):
+            cap = C.c_int64(n)
+            idx = np.zeros(max(n, 1), dtype=np.int64)
+            N.check(L.pgx_result_trim(r, i, idx.ctypes.data, C.byref(cap)))
+            trimmed.append({keys[j]: per_group[j][i] for j in idx[:cap.value]})
+        blk.trimmed = trimmed
+    return blk
+
+
+# ------------------------------------------------------------------------------------------------
+# Operators / plan nodes / plan maker
+# ------------------------------------------------------------------------------------------------
+class _GpuOperator:
+    """Gpu{Aggregation,AggregationGroupBy}Operator: returns exactly one IntermediateResultsBlock (blockId 0), then None
+    (operator/aggregation/groupby/AggregationGroupByOperator.java:81-85)."""
+
+    def __init__(self, ctx, request, segments, combine: bool):
+        self.ctx = ctx
+        self.request = request
+        self.segments = list(segments)
+        self.combine = combine
+        self._done = False
+        self._stats = None
+
+    def open(self):
+        return True
+
+    def close(self):
+        return True
+
+    def next_block(self):
+        if self._done:
+            return None
+        q = _Query(self.ctx, self.request)
+        r = q.execute(self.segments)
+        try:
+            blk = decode_result(q, r, self.segments, trim=self.combine and bool(q.group_cols))
+        finally:
+            N.lib().pgx_result_release(r)
+            q.close()
+        if q.group_cols and blk.aggregation_group_by_result.num_groups() == 0 and not self.combine:
+            blk.aggregation_group_by_result = None  # DefaultGroupByExecutor.java:221-224: no blocks -> null result
+        self._stats = blk.stats
+        self._done = True
+        return blk
+
+    nextBlock = next_block
+
+    def get_execution_statistics(self) -> ExecutionStatistics:
+        return self._stats
+
+
+class AggregationOperator(_GpuOperator):
+    pass
+
+
+class AggregationGroupByOperator(_GpuOperator):
+    pass
+
+
+class PlanNode:
+    def __init__(self, op_factory):
+        self._f = op_factory
+
+    def run(self):
+        return self._f()
+
+
+class Plan:
+    """GlobalPlanImplV0 over InstanceResponsePlanNode(CombinePlanNode(...)) (plan/GlobalPlanImplV0.java:52-75)."""
+
+    def __init__(self, op):
+        self._op = op
+        self.result = None
+
+    def execute(self):
+        self.result = self._op.next_block()
+        return self.result
+
+
+class InstancePlanMakerImplV2:
+    """plan/maker/InstancePlanMakerImplV2.java:72-109 for aggregation and aggregation-group-by queries."""
+
+    def __init__(self, ctx: Context):
+        self.ctx = ctx
+
+    def make_inner_segment_plan(self, segment: IndexSegment, broker_request: dict) -> PlanNode:
+        cls = AggregationGroupByOperator if broker_request.get("group_by") else AggregationOperator
+        return PlanNode(lambda: cls(self.ctx, broker_request, [segment], combine=False))
+
+    def make_inter_segment_plan(self, segments: Sequence[IndexSegment], broker_request: dict) -> Plan:
+        cls = AggregationGroupByOperator if broker_request.get("group_by") else AggregationOperator
+        return Plan(cls(self.ctx, broker_request, segments, combine=True))
+
+    makeInnerSegmentPlan = make_inner_segment_plan
+    makeInterSegmentPlan = make_inter_segment_plan
