@@ -1,0 +1,260 @@
+"""Benchmark of the MI355X segment query hot path (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c5]
+  (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+
+A "step" is one execution of the compiled query over all of this rank's segments resident in HBM (filter + decode +
+aggregate in the fused HIP kernel, the on-device combine, result back to the host) plus, for N>1, the cross-GPU merge
+(RCCL all-reduce of the partial aggregates / dense group tables).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "rows/sec for filter+group-by SUM at 1/2/4/8 GPUs; % of HBM roofline"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default=os.environ.get("PGX_WORKLOAD", "c2"))
+    ap.add_argument("--rows", type=int, default=0, help="override rows per segment (smoke/debug only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--profile-iters", type=int, default=0, help="only run K kernel launches (for rocprofv3)")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier_sync(world):
+    import torch
+    torch.cuda.synchronize()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        torch.cuda.synchronize()
+
+
+def cpu_baseline_c2(wl, seg_rows, nseg, threads):
+    """The oracle's C twin (one thread per segment, per-row readInt, 10000-doc blocks, double SUM) on a bounded sample
+    of the same workload, timed on this host's cores: best of 5 after 2 warm-ups."""
+    import numpy as np
+    from oracle import c_oracle
+    from pinot_amd import synth
+    dicts = {c.name: synth.make_dictionary(c.dict_kind, c.card).astype(np.float64) for c in wl.columns}
+    segs = [None] * nseg
+
+    def gen(s):
+        cols = {}
+        for ci, c in enumerate(wl.columns):
+            fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), seg_rows, c.bits, c.card)
+            cols[c.name] = (fwd, c.bits, dicts[c.name], c.card)
+        segs[s] = c_oracle.Segment(seg_rows, cols)
+
+    ths = [threading.Thread(target=gen, args=(s,)) for s in range(nseg)]
+    [t.start() for t in ths]
+    [t.join() for t in ths]
+    times = []
+    out = None
+    for it in range(7):
+        t0 = time.perf_counter()
+        out = c_oracle.run(segs, filter_col="dA", lo=64, hi=191, metric="m", threads=threads)
+        dt = time.perf_counter() - t0
+        if it >= 2:
+            times.append(dt)
+    best = min(times)
+    return {"value": nseg * seg_rows / best, "unit": "rows/s", "cores": threads, "kind": "port",
+            "sample": "%d segments x %d rows of the same synthetic c2 data (host-generated bit-identically), "
+                      "oracle/pinot_oracle_c.c one thread per segment, best of 5 after 2 warm-ups; %.3f s per query"
+                      % (nseg, seg_rows, best),
+            "result_count": int(sum(r["count"] for r in out))}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    import ctypes as C
+
+    import numpy as np
+    import torch
+
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    from pinot_amd import pql, synth
+
+    wl = synth.WORKLOADS[args.workload]
+    rows = args.rows or wl.rows
+    ctx = E.Context(local)
+    if wl.scaling == "weak":
+        seg_ids = [rank * wl.segments + i for i in range(wl.segments)]
+    else:
+        seg_ids = list(range(rank, wl.segments, world))
+    t_gen = time.perf_counter()
+    data = synth.DeviceSegments(ctx, wl, seg_ids, rows=rows)
+    t_gen = time.perf_counter() - t_gen
+    req = pql.compile(wl.query)
+    q = E._Query(ctx, req)
+    segs = data.segments
+    seg_arr = (C.c_void_p * len(segs))(*[s.handle.value for s in segs])
+    binds, keep = q.bindings(segs)
+    L = N.lib()
+
+    dense = bool(req.get("group_by"))
+    dense_t = None
+    plane_ops = []
+    if dense:
+        slots = C.c_int64()
+        N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
+        nplanes = 1 + len(req["aggregations"])
+        for p in range(nplanes):
+            op = C.c_int32()
+            N.check(L.pgx_query_dense_plane_op(q.handle, seg_arr, len(segs), p, C.byref(op)))
+            plane_ops.append(op.value)
+        dense_t = torch.zeros(nplanes * slots.value, dtype=torch.int64, device="cuda:%d" % local)
+
+    if args.profile_iters:
+        tot, kern = C.c_double(), C.c_double()
+        N.check(L.pgx_execute_timed(ctx.handle, q.handle, seg_arr, len(segs), binds, args.profile_iters,
+                                    C.byref(tot), C.byref(kern), None))
+        if rank == 0:
+            print(json.dumps({"profile_iters": args.profile_iters, "kernel_ms": kern.value}))
+        return
+
+    def step():
+        r = C.c_void_p()
+        if dense and world > 1:
+            opts = N.ExecOpts(0, C.c_void_p(dense_t.data_ptr()), dense_t.numel() * 8, N.PGX_X_KEEP_DENSE_ON_DEVICE)
+            N.check(L.pgx_execute(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
+            st = (C.c_int64 * 4)()
+            N.check(L.pgx_result_stats(r, st))
+            L.pgx_result_release(r)
+            merge_dense(dense_t, plane_ops, world)
+            stats_t = torch.tensor(list(st), dtype=torch.int64, device=dense_t.device)
+            torch.distributed.all_reduce(stats_t)
+            out = C.c_void_p()
+            s4 = (C.c_int64 * 4)(*stats_t.tolist())
+            N.check(L.pgx_result_from_dense(ctx.handle, q.handle, seg_arr, len(segs),
+                                            C.c_void_p(dense_t.data_ptr()), s4, C.byref(out)))
+            return out
+        opts = N.ExecOpts(0, None, 0, 0)
+        N.check(L.pgx_execute(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
+        if world > 1:  # aggregation-only: combine the scalar partials across GPUs
+            vals = []
+            for i in range(len(req["aggregations"])):
+                v, c = C.c_double(), C.c_int64()
+                N.check(L.pgx_result_agg(r, i, C.byref(v), C.byref(c)))
+                vals += [v.value, float(c.value)]
+            t = torch.tensor(vals, dtype=torch.float64, device="cuda:%d" % local)
+            torch.distributed.all_reduce(t)
+        return r
+
+    for _ in range(args.warmup):
+        L.pgx_result_release(step())
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    last = None
+    for i in range(args.steps):
+        r = step()
+        if i == args.steps - 1:
+            last = r
+        else:
+            L.pgx_result_release(r)
+    barrier_sync(world)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+
+    # result summary (for the log) and kernel roofline on rank 0
+    st = (C.c_int64 * 4)()
+    N.check(L.pgx_result_stats(last, st))
+    blk = E.decode_result(q, last, segs) if rank == 0 else None
+    L.pgx_result_release(last)
+    total_rows = rows * (wl.segments * world if wl.scaling == "weak" else wl.segments)
+    value = total_rows / (elapsed / args.steps)
+
+    if rank != 0:
+        return
+    tot, kern = C.c_double(), C.c_double()
+    N.check(L.pgx_execute_timed(ctx.handle, q.handle, seg_arr, len(segs), binds, 10, C.byref(tot), C.byref(kern),
+                                None))
+    used = sorted({lf["column"] for lf in q.leaves} | {a["column"] for a in req["aggregations"] if a["column"] != "*"}
+                  | set((req.get("group_by") or {}).get("columns", [])))
+    dict_cols = sorted({a["column"] for a in req["aggregations"] if a["column"] != "*"})
+    algo_bytes = data.algorithmic_bytes(used, dict_cols)
+    achieved = algo_bytes / (kern.value * 1e-3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.workload)
+    if os.path.exists(tf):
+        tj = json.load(open(tf))
+        if tj.get("rows") == rows:
+            traffic = tj.get("hbm_bytes_per_launch")
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline and wl.name == "c2":
+        cpu = cpu_baseline_c2(wl, min(rows, 32_000_000), 8, 8)
+    summary = blk.get_aggregation_result() if blk.aggregation_result is not None else \
+        {"groups": blk.get_aggregation_group_by_result().num_groups()}
+    line = {
+        "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+        "scaling": wl.scaling, "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic: device-generated v1 fixed-bit segments (seed %d), dictionaries per SURVEY 8d" % wl.seed,
+        "config": {"workload": wl.name + ": " + wl.description, "query": wl.query,
+                   "rows_per_segment": rows, "segments": len(segs) * (world if wl.scaling == "weak" else 1),
+                   "rows_total": total_rows, "parallelism": "dp%d (segment sharding)" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "pgx_scan_kernel", "kernel_ms": kern.value, "algorithmic_bytes": algo_bytes},
+        "cpu_baseline": cpu,
+        "result": summary, "stats": list(st), "gen_s": t_gen,
+    }
+    print(json.dumps(line))
+    data.free()
+
+
+def merge_dense(t, plane_ops, world):
+    """Cross-GPU merge of the dense partial group tables over RCCL: one all-reduce per plane kind."""
+    import torch
+    import torch.distributed as dist
+    nplanes = len(plane_ops)
+    planes = t.view(nplanes, -1)
+    sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=t.device)
+    adds = [p for p, op in enumerate(plane_ops) if op == 0]
+    if adds:
+        if len(adds) == nplanes:
+            dist.all_reduce(t)
+        else:
+            for p in adds:
+                dist.all_reduce(planes[p])
+    for p, op in enumerate(plane_ops):
+        if op == 1:
+            dist.all_reduce(planes[p].view(torch.float64))
+        elif op in (2, 3):
+            x = planes[p] ^ sign  # ordered-unsigned -> ordered-signed
+            dist.all_reduce(x, op=dist.ReduceOp.MIN if op == 2 else dist.ReduceOp.MAX)
+            planes[p].copy_(x ^ sign)
+
+
+if __name__ == "__main__":
+    main()

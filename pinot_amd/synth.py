@@ -1,0 +1,139 @@
+"""Synthetic benchmark segments generated directly in HBM (BASELINE.json configs; SURVEY.md 8d "Configs as concrete
+synthetic inputs").  Forward indexes are the v1 fixed-bit bytes produced on the device by pgx_synth_column:
+
+    dictId(row) = splitmix64(column_seed ^ row * 0x9E3779B97F4A7C15) % cardinality
+
+The oracle's C twin (oracle/pinot_oracle_c.c: pgo_synth_fwd) regenerates the identical bytes on the host for the CPU
+baseline and for full-size spot checks.  Dictionaries are small and built on the host:
+    "ids"    dict[i] = i                                    (dimension columns)
+    "metric" dict[i] = 16*i + splitmix64(0xD1C7 ^ i) % 16    (sorted, distinct, in [0, 2^20) for card <= 65536)
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List
+
+import numpy as np
+
+from . import native as N
+from .segment import Column, SegmentData, num_bits
+
+M64 = (1 << 64) - 1
+TILE_ROWS = 8192
+
+
+def splitmix64_np(x: np.ndarray) -> np.ndarray:
+    x = (x.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15))
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def column_seed(cfg_seed: int, seg: int, col: int) -> int:
+    return (cfg_seed * 0x100000001B3 + seg * 0x9E3779B1 + col * 0x85EBCA77 + 1) & M64
+
+
+def make_dictionary(kind: str, card: int) -> np.ndarray:
+    i = np.arange(card, dtype=np.uint64)
+    if kind == "ids":
+        return i.astype(np.int64)
+    if kind == "metric":
+        with np.errstate(over="ignore"):
+            jitter = splitmix64_np(np.uint64(0xD1C7) ^ i) % np.uint64(16)
+        return (i * np.uint64(16) + jitter).astype(np.int64)
+    raise ValueError(kind)
+
+
+@dataclass
+class ColSpec:
+    name: str
+    card: int
+    dict_kind: str = "ids"
+
+    @property
+    def bits(self):
+        return num_bits(self.card)
+
+
+@dataclass
+class Workload:
+    name: str
+    description: str
+    segments: int
+    rows: int
+    columns: List[ColSpec]
+    query: str
+    seed: int
+    scaling: str  # "weak" (every rank holds `segments` segments) or "strong" (segments sharded over ranks)
+
+
+WORKLOADS: Dict[str, Workload] = {
+    "c2": Workload("c2", "BASELINE configs[1]: 1B rows (8 x 125M), 8-bit filter dim + 16-bit metric, "
+                   "count(*)+sum(metric) with a 50% range filter, 1 MI355X per 1B rows",
+                   8, 125_000_000, [ColSpec("dA", 256), ColSpec("m", 65536, "metric")],
+                   "SELECT COUNT(*), SUM(m) FROM T WHERE dA BETWEEN 64 AND 191", 2, "weak"),
+    "c5": Workload("c5", "BASELINE configs[4]: 4096 x 2M rows sharded over the GPUs, (f1 IN 32 ids OR f2=7) AND "
+                   "f3<>3, group by gk (card 1000), sum(m)",
+                   4096, 2_000_000,
+                   [ColSpec("f1", 1000), ColSpec("f2", 100), ColSpec("f3", 10), ColSpec("gk", 1000),
+                    ColSpec("m", 65536, "metric")],
+                   "SELECT SUM(m) FROM T WHERE (f1 IN (%s) OR f2 = 7) AND f3 <> 3 GROUP BY gk TOP 10"
+                   % ",".join(str(v) for v in range(3, 1000, 31)[:32]), 5, "strong"),
+}
+
+
+def padded_fwd_bytes(rows: int, bits: int) -> int:
+    tiles = max(1, (rows + TILE_ROWS - 1) // TILE_ROWS)
+    return tiles * (TILE_ROWS // 8) * bits + 64
+
+
+class DeviceSegments:
+    """Synthetic segments resident in HBM, staged through the C-ABI (pgx_segment_stage with PGX_MEM_DEVICE)."""
+
+    def __init__(self, ctx, wl: Workload, seg_ids: List[int], rows: int = None):
+        from .engine import IndexSegment
+        self.ctx = ctx
+        self.wl = wl
+        self.rows = rows or wl.rows
+        self.seg_ids = list(seg_ids)
+        self.buffers = []
+        self.segments = []
+        dicts = {c.name: make_dictionary(c.dict_kind, c.card) for c in wl.columns}
+        L = N.lib()
+        for s in self.seg_ids:
+            cols = []
+            fwd_dev = {}
+            for ci, c in enumerate(wl.columns):
+                nbytes = padded_fwd_bytes(self.rows, c.bits)
+                p = C.c_void_p()
+                N.check(L.pgx_device_alloc(ctx.handle, nbytes, C.byref(p)))
+                self.buffers.append(p)
+                N.check(L.pgx_synth_column(ctx.handle, p, self.rows, c.bits, c.card,
+                                           column_seed(wl.seed, s, ci)))
+                fwd_dev[c.name] = (p.value, nbytes)
+                dict_bytes = dicts[c.name].astype(">i4").tobytes()
+                cols.append(Column(c.name, "INT", "DIMENSION", c.card, c.bits, self.rows, self.rows, False, False,
+                                   dict_bytes, 4, None, None, None))
+            seg = SegmentData("%s_%d" % (wl.name, s), self.rows, self.rows, {c.name: c for c in cols})
+            self.segments.append(IndexSegment.from_device(ctx, seg, fwd_dev))
+
+    def algorithmic_bytes(self, used_columns: List[str], dict_columns: List[str]) -> int:
+        """per segment, ceil(N*b/8) per distinct column read + card*width per dictionary used."""
+        total = 0
+        for _ in self.segments:
+            for c in self.wl.columns:
+                if c.name in used_columns:
+                    total += (self.rows * c.bits + 7) // 8
+                if c.name in dict_columns:
+                    total += c.card * 4
+        return total
+
+    def free(self):
+        for s in self.segments:
+            s.destroy()
+        L = N.lib()
+        for p in self.buffers:
+            L.pgx_device_free(self.ctx.handle, p)
+        self.buffers = []
+        self.segments = []
