@@ -2,21 +2,29 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-function -Wno-unused-variable
-SRC = pinot_amd/csrc/pgx_host.cpp pinot_amd/csrc/pgx_kernels.hip
-HDR = include/pgx.h pinot_amd/csrc/pgx_internal.h
+CSRC = pinot_amd/csrc
+HDR = include/pgx.h $(CSRC)/pgx_internal.h $(CSRC)/pgx_jit_abi.h
 
 all: pinot_amd/libpgx.so
 
-build/pgx_host.o: pinot_amd/csrc/pgx_host.cpp $(HDR)
+# The query compiler pastes these headers in front of every generated kernel: embed them as raw string literals.
+build/%.inc: $(CSRC)/%.h
+	@mkdir -p build
+	@(echo 'R"PGXSRC('; cat $<; echo ')PGXSRC"') > $@
+
+build/pgx_host.o: $(CSRC)/pgx_host.cpp $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-build/pgx_kernels.o: pinot_amd/csrc/pgx_kernels.hip $(HDR)
+build/pgx_jit.o: $(CSRC)/pgx_jit.cpp $(HDR) build/pgx_jit_abi.inc build/pgx_jit_device.inc
+	$(HIPCC) $(HIPFLAGS) -Ibuild -c $< -o $@
+
+build/pgx_kernels.o: $(CSRC)/pgx_kernels.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-pinot_amd/libpgx.so: build/pgx_host.o build/pgx_kernels.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@
+pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 
 clean:
 	rm -rf build pinot_amd/libpgx.so

@@ -220,6 +220,13 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
                              const pgx_leaf_binding* bindings, int32_t iters, double* total_ms,
                              double* kernel_ms, pgx_result** out);
 
+/* ---- query compiler build checks (no device needed) ---------------------------------------------
+ * The scan/aggregate kernels are generated per query shape and compiled by hiprtc for gfx950.
+ * pgx_jit_compile_check compiles one generated source; pgx_jit_selftest generates and compiles a representative set
+ * of shapes and returns the number that failed (*n_total = number tried), with the compiler log in log. */
+int pgx_jit_compile_check(const char* source, char* log, unsigned long log_cap);
+int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <map>
@@ -21,6 +22,7 @@
 
 #include "../../include/pgx.h"
 #include "pgx_internal.h"
+#include "pgx_jit_abi.h"
 
 extern "C" hipError_t pgx_launch_scan(const pgx::KQuery* q, int grid, int64_t tiles_per_wg, size_t lds_bytes,
                                       hipStream_t stream);
@@ -179,6 +181,13 @@ struct StagedColumn {
   std::vector<std::string> svals;                  // STRING dictionary values (unpadded)
   uint64_t dict_hash = 0;
   std::vector<uint8_t> inv;                        // bitmap inverted index bytes (host)
+  // LDS value image (pgx_jit.cpp): the dictionary re-encoded so a whole column's values fit one workgroup's LDS
+  int img_kind = IMG_NONE;
+  int img_sh = 0;
+  int img_words = 0;
+  int64_t vbase = 0;       // integer images hold value - vbase
+  uint64_t vrange = 0;     // max(value) - vbase
+  DevBuf img_owned;
 };
 
 struct pgx_segment {
@@ -198,6 +207,72 @@ struct pgx_segment {
 };
 
 namespace {
+
+// Re-encode a numeric dictionary into an LDS image (DESIGN.md "LDS value images"): the sum of a column over a scan
+// is a per-row dictionary lookup (ImmutableDictionaryReader.readValues), which from HBM/L2 is a random 8-byte gather
+// per row.  The image makes it an LDS read.  INT/LONG: u32 (value - min) when the card fits 144 KiB, else 64 block
+// bases + u16 offsets (frame of reference; exact, checked per block).  FLOAT/DOUBLE: doubles when they fit.
+void build_value_image(pgx_ctx* ctx, pgx_segment* seg, StagedColumn& c) {
+  const int64_t card = c.card;
+  const int64_t kMax = 144 * 1024;
+  std::vector<uint32_t> img;
+  if (c.data_type == PGX_INT || c.data_type == PGX_LONG) {
+    const int64_t vmin = *std::min_element(c.ivals.begin(), c.ivals.end());
+    const int64_t vmax = *std::max_element(c.ivals.begin(), c.ivals.end());
+    const uint64_t range = uint64_t(vmax) - uint64_t(vmin);
+    if (range > 0xFFFFFFFFull) return;
+    c.vbase = vmin;
+    c.vrange = range;
+    if (card * 4 <= kMax) {
+      img.resize(card);
+      for (int64_t i = 0; i < card; ++i) img[i] = uint32_t(uint64_t(c.ivals[i]) - uint64_t(vmin));
+      c.img_kind = IMG_U32;
+    } else if (card * 2 + 4 * kImgFor16Blocks <= kMax) {
+      int sh = 0;
+      while ((card + (int64_t(1) << sh) - 1) >> sh > 32) ++sh;  // <= 32 blocks: base reads are bank-conflict free
+      bool ok = false;
+      std::vector<uint32_t> base;
+      for (int tries = 0; tries < 2 && !ok; ++tries, --sh) {
+        if (sh < 0 || ((card + (int64_t(1) << sh) - 1) >> sh) > kImgFor16Blocks) break;
+        const int64_t nblk = (card + (int64_t(1) << sh) - 1) >> sh;
+        base.assign(kImgFor16Blocks, 0);
+        ok = true;
+        for (int64_t b = 0; b < nblk && ok; ++b) {
+          uint64_t lo = ~0ull, hi = 0;
+          for (int64_t i = b << sh; i < std::min(card, (b + 1) << sh); ++i) {
+            const uint64_t x = uint64_t(c.ivals[i]) - uint64_t(vmin);
+            lo = std::min(lo, x);
+            hi = std::max(hi, x);
+          }
+          if (hi - lo > 0xFFFF) ok = false;
+          base[b] = uint32_t(lo);
+        }
+        if (ok) c.img_sh = sh;
+      }
+      if (!ok) return;
+      img.assign(kImgFor16Blocks + (card + 1) / 2, 0);
+      std::copy(base.begin(), base.end(), img.begin());
+      uint16_t* off = reinterpret_cast<uint16_t*>(img.data() + kImgFor16Blocks);
+      for (int64_t i = 0; i < card; ++i)
+        off[i] = uint16_t(uint64_t(c.ivals[i]) - uint64_t(vmin) - base[i >> c.img_sh]);
+      c.img_kind = IMG_FOR16;
+    } else {
+      return;
+    }
+  } else if (c.data_type == PGX_FLOAT || c.data_type == PGX_DOUBLE) {
+    if (card * 8 > kMax) return;
+    img.resize(card * 2);
+    std::memcpy(img.data(), c.dvals.data(), card * 8);
+    c.img_kind = IMG_F64;
+  } else {
+    return;
+  }
+  c.img_words = int(img.size());
+  img.resize((img.size() + 3) & ~size_t(3), 0);  // whole 16-B chunks for the LDS staging copy
+  c.img_owned = DevBuf(ctx, img.size() * 4);
+  hip_check(hipMemcpy(c.img_owned.p, img.data(), img.size() * 4, hipMemcpyHostToDevice), "image H2D");
+  seg->device_bytes += img.size() * 4;
+}
 
 void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c) {
   c.name = d.name ? d.name : "";
@@ -269,6 +344,7 @@ void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool
     hip_check(hipMemcpy(c.dict_owned.p, enc.data(), enc.size() * 8, hipMemcpyHostToDevice), "dict H2D");
     c.dict_dev = c.dict_owned.p;
     seg->device_bytes += enc.size() * 8;
+    build_value_image(ctx, seg, c);
   }
 
   // ---- forward index ----
@@ -551,6 +627,16 @@ struct ExecPlan {
   int grid = 0;
   int64_t tiles_per_wg = 0;
   size_t lds_bytes = 0;
+  // query-specialised kernels (pgx_jit.cpp): one launch per group of segments sharing a shape
+  struct JitGroup {
+    void* fn = nullptr;
+    int T = 256;
+    int grid = 1;
+    JArgs args{};
+    std::vector<JSeg> segs;
+  };
+  std::vector<JitGroup> jit;
+  std::vector<DevBuf> jit_bufs;
 };
 
 int qslot(ExecPlan& P, const std::string& name) {
@@ -822,7 +908,189 @@ void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st) {
   }
 }
 
+// Build the query-specialised launch groups (pgx_jit.cpp) for plans the generated kernels cover: aggregation-only
+// and dense group-by over at most PGX_J_MAX_COLS columns.  Hash group-by keeps the generic kernel.  PGX_JIT=0 forces
+// the generic kernel (A/B timing); both are HIP paths with identical accumulator encodings.
+bool jit_enabled() {
+  const char* e = std::getenv("PGX_JIT");
+  return !(e && e[0] == '0');
+}
+
+void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, hipStream_t st) {
+  P.jit.clear();
+  const KQuery& K = P.kq;
+  if (!jit_enabled()) return;
+  if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL)) return;
+  const int nc = K.num_qcols;
+  if (nc > PGX_J_MAX_COLS) return;
+  const bool grouped = K.group_mode != G_NONE;
+  // which columns are decoded, which carry value images
+  std::vector<bool> decode(nc, false), want_img(nc, false);
+  const int nleaves = int(q.leaf_col.size());
+  for (int a = 0; a < K.num_aggs; ++a) {
+    if (K.agg_kind[a] == A_COUNT) continue;
+    decode[K.agg_col[a]] = true;
+    if (grouped || K.agg_kind[a] == A_SUM || K.agg_kind[a] == A_AVG) want_img[K.agg_col[a]] = true;
+  }
+  for (int g = 0; g < K.num_gcols; ++g) decode[K.gcol[g]] = true;
+  // signature per segment -> groups
+  std::map<std::string, std::vector<int>> groups;
+  std::vector<std::string> order;
+  for (int s = 0; s < n; ++s) {
+    const KSeg& S = P.ksegs[s];
+    std::string sig;
+    for (int l = 0; l < nleaves; ++l) sig += char('a' + S.leaf[l].mode);
+    sig += '|';
+    for (int c = 0; c < nc; ++c) {
+      const StagedColumn& col = segs[s]->col(P.qcols[c]);
+      sig += std::to_string(S.bits[c]) + (S.remap[c] ? "r" : "") + ",";
+      if (want_img[c]) sig += "i" + std::to_string(col.img_kind) + "." + std::to_string(col.img_sh) + ",";
+    }
+    if (!groups.count(sig)) order.push_back(sig);
+    groups[sig].push_back(s);
+  }
+  int cus = 256;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
+    cus = prop.multiProcessorCount;
+  for (const std::string& sig : order) {
+    const std::vector<int>& members = groups[sig];
+    const KSeg& S0 = P.ksegs[members[0]];
+    JitShape J;
+    J.cols.resize(nc);
+    std::vector<bool> dec = decode;
+    for (int l = 0; l < nleaves; ++l)
+      if (S0.leaf[l].mode == LEAF_SCAN_INTERVAL || S0.leaf[l].mode == LEAF_SCAN_BITSET) dec[K.leaf_col[l]] = true;
+    int R = 8;
+    for (int c = 0; c < nc; ++c) {
+      JitCol& C = J.cols[c];
+      C.bits = S0.bits[c];
+      C.decode = dec[c];
+      C.remap = S0.remap[c] != nullptr;
+      const StagedColumn& col0 = segs[members[0]]->col(P.qcols[c]);
+      C.fp = col0.data_type == PGX_FLOAT || col0.data_type == PGX_DOUBLE;
+      if (C.decode) {
+        int g = 1;
+        while (g < 32 && (C.bits % (g * 2)) == 0) g *= 2;  // largest power of two dividing bits (<= 32)
+        R = std::max(R, 32 / g);
+      }
+      if (want_img[c]) {
+        C.img = col0.img_kind;
+        C.img_sh = col0.img_sh;
+        uint64_t range = 0;
+        for (int s : members) {
+          const StagedColumn& col = segs[s]->col(P.qcols[c]);
+          C.img_words = std::max(C.img_words, col.img_words);
+          range = std::max(range, col.vrange);
+        }
+        C.acc32 = range * 32 < 0xFFFFFFFFull;
+      }
+    }
+    J.R = R;
+    // LDS budget: drop the largest images until everything fits
+    auto lds_need = [&]() {
+      int64_t b = 0;
+      for (const JitCol& C : J.cols)
+        if (C.img != IMG_NONE) b += ((int64_t(C.img_words) * 4 + 15) / 16) * 16;
+      if (K.group_mode == G_DENSE_LDS) b += int64_t(P.dense_slots) * K.num_planes * 8;
+      return b;
+    };
+    while (lds_need() > kLdsBudget) {
+      int big = -1;
+      for (int c = 0; c < nc; ++c)
+        if (J.cols[c].img != IMG_NONE && (big < 0 || J.cols[c].img_words > J.cols[big].img_words)) big = c;
+      if (big < 0) return;  // the dense LDS table alone does not fit: generic kernel
+      J.cols[big].img = IMG_NONE;
+    }
+    const int64_t lds = lds_need();
+    J.T = lds <= 20 * 1024 ? 256 : (lds <= 40 * 1024 ? 512 : 1024);
+    for (int l = 0; l < nleaves; ++l) {
+      J.leaf_col.push_back(K.leaf_col[l]);
+      J.leaf_mode.push_back(S0.leaf[l].mode);
+    }
+    for (int i = 0; i < K.prog_len; ++i) {
+      J.prog_op.push_back(K.prog_op[i]);
+      J.prog_arg.push_back(K.prog_arg[i]);
+    }
+    for (int a = 0; a < K.num_aggs; ++a) {
+      J.agg_kind.push_back(K.agg_kind[a]);
+      J.agg_col.push_back(K.agg_col[a]);
+    }
+    for (int p = 0; p < K.num_planes; ++p) J.plane_op.push_back(K.plane_op[p]);
+    J.num_planes = K.num_planes;
+    J.group_mode = K.group_mode;
+    for (int g = 0; g < K.num_gcols; ++g) {
+      J.gcol.push_back(K.gcol[g]);
+      J.gmul.push_back(K.gmul[g]);
+    }
+    J.dense_slots = P.dense_slots;
+
+    ExecPlan::JitGroup G;
+    G.T = J.T;
+    int lds_bytes = 0;
+    std::string err;
+    G.fn = jit_function(J, ctx->device, &lds_bytes, &err);
+    if (!G.fn) fail(PGX_ERR_INTERNAL, "query kernel compile: " + err);
+    // per-segment arguments
+    const int64_t tile_rows = int64_t(J.T) * 32;
+    int64_t tiles = 0;
+    for (int s : members) {
+      const KSeg& S = P.ksegs[s];
+      JSeg js{};
+      js.tile_begin = tiles;
+      js.num_docs = S.num_docs;
+      tiles += (int64_t(S.num_docs) + tile_rows - 1) / tile_rows;
+      for (int c = 0; c < nc; ++c) {
+        const StagedColumn& col = segs[s]->col(P.qcols[c]);
+        js.fwd[c] = S.fwd[c];
+        js.dict[c] = S.dict[c];
+        js.remap[c] = S.remap[c];
+        js.img[c] = J.cols[c].img != IMG_NONE ? col.img_owned.p : nullptr;
+        js.img_words[c] = J.cols[c].img != IMG_NONE ? col.img_words : 0;
+        js.vbase[c] = col.vbase;
+      }
+      for (int l = 0; l < nleaves; ++l) {
+        const KLeaf& L = S.leaf[l];
+        js.lbits[l] = L.bitset;
+        js.lranges[l] = L.ranges;
+        js.lnr[l] = L.nranges;
+        js.llo[l] = uint32_t(L.lo);
+        js.lspan[l] = uint32_t(L.hi) - uint32_t(L.lo);
+      }
+      G.segs.push_back(js);
+    }
+    const int waves = J.T / 64;
+    int per_cu = std::max(1, 32 / waves);
+    if (lds > 0) per_cu = std::min<int64_t>(per_cu, std::max<int64_t>(1, (160 * 1024) / (lds + 256)));
+    const int64_t max_grid = int64_t(cus) * per_cu;
+    const int64_t tpw = std::max<int64_t>(1, (tiles + max_grid - 1) / max_grid);
+    G.grid = int(std::max<int64_t>(1, (tiles + tpw - 1) / tpw));
+    DevBuf buf(ctx, G.segs.size() * sizeof(JSeg));
+    hip_check(hipMemcpyAsync(buf.p, G.segs.data(), G.segs.size() * sizeof(JSeg), hipMemcpyHostToDevice, st), "jseg");
+    G.args.segs = buf.as<JSeg>();
+    G.args.num_segs = int(G.segs.size());
+    G.args.total_tiles = tiles;
+    G.args.tiles_per_wg = tpw;
+    P.jit_bufs.push_back(std::move(buf));
+    if (tiles > 0) P.jit.push_back(std::move(G));
+  }
+  if (P.jit.empty()) P.jit.push_back(ExecPlan::JitGroup{});  // every segment empty: nothing to launch
+}
+
 void launch_scan(ExecPlan& P, hipStream_t st) {
+  if (!P.jit.empty()) {
+    for (auto& G : P.jit) {
+      if (!G.fn) continue;
+      G.args.agg_out = P.kq.agg_out;
+      G.args.stats = P.kq.stats;
+      G.args.table = P.kq.table;
+      void* params[] = {&G.args};
+      hip_check(hipModuleLaunchKernel(static_cast<hipFunction_t>(G.fn), G.grid, 1, 1, G.T, 1, 1, 0, st, params,
+                                      nullptr),
+                "query kernel launch");
+    }
+    return;
+  }
   if (P.kq.total_tiles == 0) return;
   hip_check(pgx_launch_scan(&P.kq, P.grid, P.tiles_per_wg, P.lds_bytes, st), "scan kernel launch");
 }
@@ -964,6 +1232,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   plan_query(ctx, q, segs, n, bindings, xflags, P);
   ExecBuffers B;
   upload_plan(ctx, P, B, st);
+  plan_jit(ctx, q, segs, n, P, st);
   const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
   if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
   for (int attempt = 0; attempt < 6; ++attempt) {
@@ -1290,6 +1559,7 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     plan_query(ctx, *q, segs, n, bindings, 0, P);
     ExecBuffers B;
     upload_plan(ctx, P, B, st);
+    plan_jit(ctx, *q, segs, n, P, st);
     const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
     if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
     alloc_outputs(ctx, P, B, nullptr, 0);

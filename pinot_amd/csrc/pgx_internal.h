@@ -87,3 +87,53 @@ struct KQuery {
 };
 
 }  // namespace pgx
+
+// =================================================================================================
+// Query-specialised kernels (pgx_jit.cpp): the shape of one launch group, from which a kernel is generated and
+// compiled by hiprtc once per distinct shape (cached per process and device).
+// =================================================================================================
+#include <string>
+#include <vector>
+
+namespace pgx {
+
+// Value images staged in LDS for aggregated columns (built once per column at staging time, pgx_host.cpp).
+enum ImgKind : int8_t {
+  IMG_NONE = 0,   // no image: values are gathered from the HBM value table (int64 / double per dictId)
+  IMG_U32 = 1,    // u32 (value - vbase) per dictId
+  IMG_FOR16 = 2,  // 64 x u32 block bases (relative to vbase) then u16 offset per dictId; block = 1 << sh dictIds
+  IMG_F64 = 3,    // double per dictId
+};
+constexpr int kImgFor16Blocks = 64;
+constexpr int kLdsBudget = 160 * 1024 - 256;  // static LDS of one workgroup, minus the per-plane accumulators
+
+struct JitCol {
+  int bits = 0;
+  bool decode = false;   // read by a scan leaf, an aggregation or a group key
+  int img = IMG_NONE;    // value image kind (aggregated columns)
+  int img_sh = 0;        // IMG_FOR16 block shift
+  int img_words = 0;     // LDS dwords reserved for the image (max over the group's segments)
+  bool acc32 = false;    // R rows of (value - vbase) always fit a u32 partial sum
+  bool fp = false;       // FLOAT/DOUBLE values
+  bool remap = false;    // group column with a local->global dictId remap table
+};
+
+struct JitShape {
+  int T = 256;           // threads per workgroup
+  int R = 8;             // rows per lane per sub-step (R * bits % 32 == 0 for every decoded column)
+  std::vector<JitCol> cols;
+  std::vector<int> leaf_col, leaf_mode;
+  std::vector<int> prog_op, prog_arg;
+  std::vector<int> agg_kind, agg_col, plane_op;
+  int group_mode = G_NONE;
+  std::vector<int> gcol;
+  std::vector<uint64_t> gmul;
+  uint64_t dense_slots = 0;
+  int num_planes = 1;
+};
+
+std::string jit_source(const JitShape& s, int* lds_bytes);
+// Compile (or fetch from the cache) the kernel for shape s on the current device.  Returns the hipFunction_t as void*.
+void* jit_function(const JitShape& s, int device, int* lds_bytes, std::string* err);
+
+}  // namespace pgx

@@ -1,0 +1,675 @@
+// Query compiler of libpgx: generates one HIP kernel per query SHAPE and compiles it for gfx950 with hiprtc.
+//
+// The reference interprets every query through a tree of virtual iterators (operator/dociditerators/*,
+// operator/aggregation/*Executor.java): per doc a chain of next()/apply()/readInt() calls.  Here the operator tree
+// of one query over one group of segments (plan/maker/InstancePlanMakerImplV2.java:72-109) is flattened into a
+// single fused kernel whose loops are specialised to the query's shape:
+//   * the bit width of every column (fixed-bit decode, util/PinotDataCustomBitSet.java:122-155) is a constant, so the
+//     unpack of a lane's rows is straight-line shifts / byte-permutes on registers;
+//   * the physical filter program (plan/FilterPlanNode.java:77-170, AndBlockDocIdSet / OrBlockDocIdSet) becomes
+//     bitwise logic on per-lane doc-mask words;
+//   * the aggregation list (operator/aggregation/DefaultAggregationExecutor.java, DefaultGroupByExecutor.java)
+//     becomes per-lane register accumulators (aggregation-only) or LDS / global atomics (dense group-by);
+//   * SUM/AVG values are read from an LDS-resident image of the column's dictionary (Dictionary.readDoubleValues,
+//     segment/index/readers/ImmutableDictionaryReader.java:107-155) instead of HBM/L2 gathers.
+// Everything else (segment pointers, dictId intervals, bitsets, doc ranges) is a kernel argument, so one compiled
+// kernel serves every query and segment set with the same shape.  Results use the same accumulator planes as the
+// generic interpreter kernel (pgx_kernels.hip), so the host decodes them identically.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "pgx_internal.h"
+
+extern "C" int pgx_jit_compile_check(const char* source, char* log, unsigned long log_cap);
+
+namespace pgx {
+
+namespace {
+
+const char* kAbiSrc =
+#include "pgx_jit_abi.inc"
+    ;
+const char* kDevSrc =
+#include "pgx_jit_device.inc"
+    ;
+
+struct Emitter {
+  std::ostringstream o;
+  int ind = 0;
+  template <typename... Ts>
+  Emitter& ln(Ts&&... xs) {
+    for (int i = 0; i < ind; ++i) o << "  ";
+    (o << ... << xs);
+    o << "\n";
+    return *this;
+  }
+};
+
+int dwords_per(const JitShape& s, int c) { return s.R * s.cols[c].bits / 32; }
+
+std::string plane_atomic(int op, const std::string& ptr, const std::string& val) {
+  switch (op) {
+    case P_ADD_I64: return "atomicAdd(" + ptr + ", " + val + ");";
+    case P_ADD_F64: return "atomicAdd((double*)(" + ptr + "), pgx_bits_f64(" + val + "));";
+    case P_MIN_ORD: return "atomicMin(" + ptr + ", " + val + ");";
+    default: return "atomicMax(" + ptr + ", " + val + ");";
+  }
+}
+
+// Expression (u32) for the value image of column c at dictId expression v, relative to vbase.
+std::string img_value(const JitShape& s, int c, const std::vector<int>& img_off, const std::string& v) {
+  const JitCol& C = s.cols[c];
+  const int off = img_off[c];  // byte offset in lds
+  if (C.img == IMG_U32) return "lds[" + std::to_string(off / 4) + " + " + v + "]";
+  // FOR16: bases first (64 x u32), then u16 offsets
+  return "(lds[" + std::to_string(off / 4) + " + (" + v + " >> " + std::to_string(C.img_sh) + ")] + (u32)lds16[" +
+         std::to_string((off + 4 * kImgFor16Blocks) / 2) + " + " + v + "])";
+}
+
+}  // namespace
+
+std::string jit_source(const JitShape& s, int* lds_bytes_out) {
+  const int ncols = int(s.cols.size());
+  const int U = 32 / s.R;
+  const bool grouped = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL;
+  // ---- LDS layout: images, then the dense group table ----
+  std::vector<int> img_off(ncols, -1);
+  int lds = 0;
+  for (int c = 0; c < ncols; ++c) {
+    if (s.cols[c].img == IMG_NONE) continue;
+    img_off[c] = lds;
+    lds += ((s.cols[c].img_words * 4 + 15) / 16) * 16;
+  }
+  int tab_off = -1;
+  if (s.group_mode == G_DENSE_LDS) {
+    tab_off = lds;
+    lds += int(s.dense_slots) * s.num_planes * 8;
+  }
+  if (lds_bytes_out) *lds_bytes_out = lds;
+  const bool any_img = lds > 0 && (tab_off != 0 || s.group_mode != G_DENSE_LDS);
+
+  Emitter e;
+  e.o << kAbiSrc << "\n" << kDevSrc << "\n";
+  e.ln("#define PT ", s.T);
+  e.ln("#define PR ", s.R);
+  e.ln("extern \"C\" __global__ void __launch_bounds__(PT) pgxq(const JArgs A) {");
+  e.ind = 1;
+  if (lds > 0) {
+    e.ln("__shared__ __attribute__((aligned(16))) u32 lds[", (lds + 3) / 4, "];");
+    e.ln("const unsigned short* lds16 = (const unsigned short*)lds;");
+    e.ln("(void)lds16;");
+  }
+  e.ln("__shared__ u64 s_acc[", s.num_planes, "];");
+  e.ln("const int tid = threadIdx.x;");
+  e.ln("const int lane = tid & 63;");
+  e.ln("const long long tb = (long long)blockIdx.x * A.tiles_per_wg;");
+  e.ln("const long long te = (tb + A.tiles_per_wg < A.total_tiles) ? tb + A.tiles_per_wg : A.total_tiles;");
+  e.ln("if (tb >= te) return;");
+  // accumulator init
+  {
+    std::string init = "0ull";
+    e.ln("if (tid < ", s.num_planes, ") {");
+    e.ind++;
+    e.ln("u64 z = 0ull;");
+    for (int p = 1; p < s.num_planes; ++p)
+      if (s.plane_op[p] == P_MIN_ORD) e.ln("if (tid == ", p, ") z = ~0ull;");
+    e.ln("s_acc[tid] = z;");
+    e.ind--;
+    e.ln("}");
+  }
+  if (s.group_mode == G_DENSE_LDS) {
+    e.ln("{");
+    e.ind++;
+    e.ln("u64* tab = (u64*)(lds + ", tab_off / 4, ");");
+    e.ln("for (int i = tid; i < ", s.dense_slots * s.num_planes, "; i += PT) {");
+    e.ind++;
+    e.ln("const int p = i / ", s.dense_slots, ";");
+    e.ln("u64 z = 0ull;");
+    for (int p = 1; p < s.num_planes; ++p)
+      if (s.plane_op[p] == P_MIN_ORD) e.ln("if (p == ", p, ") z = ~0ull;");
+    e.ln("tab[i] = z;");
+    e.ind--;
+    e.ln("}");
+    e.ind--;
+    e.ln("}");
+  }
+  e.ln("__syncthreads();");
+  if (s.group_mode == G_DENSE_LDS) e.ln("u64* const tab = (u64*)(lds + ", tab_off / 4, ");");
+  if (s.group_mode == G_DENSE_GLOBAL) e.ln("u64* const tab = A.table;");
+  e.ln("u64 st_docs = 0, st_ent = 0;");
+  e.ln("int seg = pgx_find_seg(A.segs, A.num_segs, tb);");
+  e.ln("long long t = tb;");
+  e.ln("while (t < te) {");
+  e.ind = 2;
+  e.ln("const JSeg* __restrict__ S = A.segs + seg;");
+  e.ln("const long long tse = (seg + 1 < A.num_segs) ? A.segs[seg + 1].tile_begin : A.total_tiles;");
+  e.ln("const long long t2 = (te < tse) ? te : tse;");
+  e.ln("const int nd = S->num_docs;");
+  e.ln("const long long tile0 = S->tile_begin;");
+  // stage this segment's value images into LDS
+  bool has_img = false;
+  for (int c = 0; c < ncols; ++c) has_img |= s.cols[c].img != IMG_NONE;
+  (void)any_img;
+  if (has_img) {
+    e.ln("__syncthreads();");
+    for (int c = 0; c < ncols; ++c) {
+      if (s.cols[c].img == IMG_NONE) continue;
+      e.ln("{");
+      e.ind++;
+      e.ln("const pgx_u32x4* __restrict__ src = (const pgx_u32x4*)S->img[", c, "];");
+      e.ln("pgx_u32x4* dst = (pgx_u32x4*)(lds + ", img_off[c] / 4, ");");
+      e.ln("const int nq = (S->img_words[", c, "] + 3) >> 2;");
+      e.ln("for (int i = tid; i < nq; i += PT) dst[i] = src[i];");
+      e.ind--;
+      e.ln("}");
+    }
+    e.ln("__syncthreads();");
+  }
+  // per-segment pointers and leaf parameters
+  for (int c = 0; c < ncols; ++c)
+    if (s.cols[c].decode) e.ln("const u32* __restrict__ f", c, " = S->fwd[", c, "];");
+  const int nleaves = int(s.leaf_col.size());
+  for (int l = 0; l < nleaves; ++l) {
+    switch (s.leaf_mode[l]) {
+      case LEAF_SCAN_INTERVAL:
+        e.ln("const u32 lo", l, " = S->llo[", l, "], sp", l, " = S->lspan[", l, "];");
+        break;
+      case LEAF_SCAN_BITSET:
+        e.ln("const u32* __restrict__ bs", l, " = S->lbits[", l, "];");
+        break;
+      case LEAF_RANGES:
+        e.ln("const int* __restrict__ rg", l, " = S->lranges[", l, "];");
+        e.ln("const int nr", l, " = S->lnr[", l, "];");
+        e.ln("int cur", l, " = pgx_ranges_seek(rg", l, ", nr", l, ", (int)((t - tile0) * (PT * 32)));");
+        break;
+      default:
+        break;
+    }
+  }
+  // group columns: remap tables
+  if (grouped)
+    for (size_t g = 0; g < s.gcol.size(); ++g)
+      if (s.cols[s.gcol[g]].remap) e.ln("const int* __restrict__ rm", g, " = S->remap[", s.gcol[g], "];");
+  // value bases / dictionaries used by the aggregations
+  const int naggs = int(s.agg_kind.size());
+  std::vector<bool> need_vb(ncols, false), need_dict(ncols, false);
+  for (int a = 0; a < naggs; ++a) {
+    const int k = s.agg_kind[a];
+    if (k == A_COUNT) continue;
+    const int c = s.agg_col[a];
+    const JitCol& C = s.cols[c];
+    if (!grouped) {
+      if (k == A_SUM || k == A_AVG) {
+        if (C.img == IMG_U32 || C.img == IMG_FOR16) need_vb[c] = true;
+        else if (C.img == IMG_NONE) need_dict[c] = true;
+      } else {
+        need_dict[c] = true;  // MIN/MAX: one value lookup per lane at flush
+      }
+    } else {
+      if (C.img == IMG_U32 || C.img == IMG_FOR16) need_vb[c] = true;
+      else if (C.img == IMG_NONE) need_dict[c] = true;
+    }
+  }
+  for (int c = 0; c < ncols; ++c) {
+    if (need_vb[c]) e.ln("const i64 vb", c, " = S->vbase[", c, "];");
+    if (need_dict[c]) {
+      if (s.cols[c].fp) e.ln("const double* __restrict__ dd", c, " = (const double*)S->dict[", c, "];");
+      else e.ln("const i64* __restrict__ di", c, " = (const i64*)S->dict[", c, "];");
+    }
+  }
+  // lane accumulators (aggregation-only)
+  e.ln("u64 scnt = 0;");
+  if (!grouped) {
+    for (int a = 0; a < naggs; ++a) {
+      const int k = s.agg_kind[a];
+      const int c = s.agg_col[a];
+      if (k == A_SUM || k == A_AVG) {
+        if (s.cols[c].fp) e.ln("double acc", a, " = 0.0;");
+        else if (s.cols[c].img == IMG_NONE) e.ln("i64 acc", a, " = 0;");
+        else e.ln("u64 acc", a, " = 0;");
+      } else if (k == A_MIN) {
+        e.ln("u32 mn", a, " = 0xFFFFFFFFu;");
+      } else if (k == A_MAX) {
+        e.ln("u32 mx", a, " = 0u;");
+      }
+    }
+  }
+  // software-pipelined tile loop: raw words of tile tt+1 are loaded while tile tt is computed
+  auto emit_loads = [&](const std::string& tile, const std::string& dst) {
+    e.ln("{");
+    e.ind++;
+    e.ln("const int rb = (int)((", tile, " - tile0) * (PT * 32));");
+    e.ln("const bool full = rb + PT * 32 <= nd;");
+    for (int u = 0; u < U; ++u) {
+      e.ln("{");
+      e.ind++;
+      e.ln("const int r0 = rb + ", u * s.R, " * PT + tid * PR;");
+      for (int c = 0; c < ncols; ++c) {
+        if (!s.cols[c].decode) continue;
+        const int D = dwords_per(s, c);
+        e.ln("if (full || r0 < nd) pgx_ld<", D, ">(f", c, " + (long long)(r0 / PR) * ", D, ", &", dst, c, "[", u * D,
+             "]); else pgx_zero<", D, ">(&", dst, c, "[", u * D, "]);");
+      }
+      e.ind--;
+      e.ln("}");
+    }
+    e.ind--;
+    e.ln("}");
+  };
+  for (int c = 0; c < ncols; ++c)
+    if (s.cols[c].decode) e.ln("u32 n", c, "[", U * dwords_per(s, c), "];");
+  emit_loads("t", "n");
+  e.ln("for (long long tt = t; tt < t2; ++tt) {");
+  e.ind = 3;
+  for (int c = 0; c < ncols; ++c) {
+    if (!s.cols[c].decode) continue;
+    const int n = U * dwords_per(s, c);
+    e.ln("u32 c", c, "[", n, "];");
+    e.ln("#pragma unroll");
+    e.ln("for (int i = 0; i < ", n, "; ++i) c", c, "[i] = n", c, "[i];");
+  }
+  e.ln("if (tt + 1 < t2) ");
+  emit_loads("tt + 1", "n");
+  e.ln("const int rb = (int)((tt - tile0) * (PT * 32));");
+  for (int u = 0; u < U; ++u) {
+    e.ln("{");
+    e.ind = 4;
+    e.ln("const int r0 = rb + ", u * s.R, " * PT + tid * PR;");
+    e.ln("const u32 valid = pgx_valid_bits(r0, nd, PR);");
+    for (int c = 0; c < ncols; ++c) {
+      if (!s.cols[c].decode) continue;
+      e.ln("u32 v", c, "[PR];");
+      e.ln("pgx_unpack<", s.cols[c].bits, ", PR>(&c", c, "[", u * dwords_per(s, c), "], v", c, ");");
+    }
+    // filter program
+    std::vector<std::string> st;
+    int tmp = 0;
+    std::string mask = "valid";
+    for (size_t pc = 0; pc < s.prog_op.size(); ++pc) {
+      const int op = s.prog_op[pc], arg = s.prog_arg[pc];
+      if (op == OP_LEAF) {
+        const int l = arg, c = s.leaf_col[l];
+        const std::string L = "L" + std::to_string(tmp++);
+        switch (s.leaf_mode[l]) {
+          case LEAF_SCAN_INTERVAL:
+            e.ln("u32 ", L, " = 0u;");
+            e.ln("#pragma unroll");
+            e.ln("for (int j = 0; j < PR; ++j) ", L, " |= (u32)((v", c, "[j] - lo", l, ") <= sp", l, ") << j;");
+            break;
+          case LEAF_SCAN_BITSET:
+            e.ln("u32 ", L, " = 0u;");
+            e.ln("#pragma unroll");
+            e.ln("for (int j = 0; j < PR; ++j) ", L, " |= ((bs", l, "[v", c, "[j] >> 5] >> (v", c,
+                 "[j] & 31u)) & 1u) << j;");
+            break;
+          case LEAF_RANGES:
+            e.ln("const u32 ", L, " = pgx_ranges_bits(rg", l, ", nr", l, ", cur", l, ", r0, PR);");
+            break;
+          default:
+            e.ln("const u32 ", L, " = 0u;");
+            break;
+        }
+        st.push_back("(" + L + " & valid)");
+      } else if (op == OP_AND || op == OP_OR) {
+        for (int k = 1; k < arg; ++k) {
+          const std::string b = st.back();
+          st.pop_back();
+          const std::string a = st.back();
+          st.pop_back();
+          const std::string X = "X" + std::to_string(tmp++);
+          e.ln("const u32 ", X, " = ", a, op == OP_AND ? " & " : " | ", b, ";");
+          st.push_back(X);
+        }
+      } else if (op == OP_STAT) {
+        e.ln("st_ent += __popc(", st.back(), ");");
+      } else if (op == OP_TRUE) {
+        st.push_back("valid");
+      }
+    }
+    if (!st.empty()) mask = "(" + st.back() + " & valid)";
+    e.ln("const u32 mask = ", mask, ";");
+    e.ln("scnt += __popc(mask);");
+    if (!grouped) {
+      for (int a = 0; a < naggs; ++a) {
+        const int k = s.agg_kind[a];
+        if (k == A_COUNT) continue;
+        const int c = s.agg_col[a];
+        const JitCol& C = s.cols[c];
+        const std::string va = "v" + std::to_string(c);
+        if (k == A_MIN) {
+          e.ln("#pragma unroll");
+          e.ln("for (int j = 0; j < PR; ++j) mn", a, " = min(mn", a, ", ((mask >> j) & 1u) ? ", va, "[j] : 0xFFFFFFFFu);");
+        } else if (k == A_MAX) {
+          e.ln("#pragma unroll");
+          e.ln("for (int j = 0; j < PR; ++j) mx", a, " = max(mx", a, ", ((mask >> j) & 1u) ? ", va, "[j] : 0u);");
+        } else if (C.fp) {
+          const std::string val = (C.img == IMG_F64)
+                                      ? "((const double*)lds)[" + std::to_string(img_off[c] / 8) + " + " + va + "[j]]"
+                                      : "dd" + std::to_string(c) + "[" + va + "[j]]";
+          e.ln("#pragma unroll");
+          e.ln("for (int j = 0; j < PR; ++j) if ((mask >> j) & 1u) acc", a, " += ", val, ";");
+        } else if (C.img == IMG_NONE) {
+          e.ln("#pragma unroll");
+          e.ln("for (int j = 0; j < PR; ++j) if ((mask >> j) & 1u) acc", a, " += di", c, "[", va, "[j]];");
+        } else if (C.acc32) {
+          e.ln("{");
+          e.ln("  u32 p = 0u;");
+          e.ln("  #pragma unroll");
+          e.ln("  for (int j = 0; j < PR; ++j) { const u32 x = ", img_value(s, c, img_off, va + "[j]"),
+               "; p += ((mask >> j) & 1u) ? x : 0u; }");
+          e.ln("  acc", a, " += p;");
+          e.ln("}");
+        } else {
+          e.ln("#pragma unroll");
+          e.ln("for (int j = 0; j < PR; ++j) { const u32 x = ", img_value(s, c, img_off, va + "[j]"), "; acc", a,
+               " += ((mask >> j) & 1u) ? (u64)x : 0ull; }");
+        }
+      }
+    } else {
+      // dense group-by: key = sum_g id_g * mul_g (column 0 least significant, DefaultGroupKeyGenerator.java:230-237)
+      e.ln("#pragma unroll");
+      e.ln("for (int j = 0; j < PR; ++j) {");
+      e.ind++;
+      e.ln("if (!((mask >> j) & 1u)) continue;");
+      std::string key;
+      for (size_t g = 0; g < s.gcol.size(); ++g) {
+        const int c = s.gcol[g];
+        std::string id = "v" + std::to_string(c) + "[j]";
+        if (s.cols[c].remap) id = "(u32)rm" + std::to_string(g) + "[" + id + "]";
+        if (!key.empty()) key += " + ";
+        key += id + " * " + std::to_string(s.gmul[g]) + "u";
+      }
+      e.ln("const u32 key = ", key.empty() ? "0u" : key, ";");
+      e.ln("atomicAdd(&tab[key], 1ull);");
+      for (int a = 0; a < naggs; ++a) {
+        const int k = s.agg_kind[a];
+        if (k == A_COUNT) continue;
+        const int c = s.agg_col[a];
+        const JitCol& C = s.cols[c];
+        const std::string id = "v" + std::to_string(c) + "[j]";
+        std::string val;  // i64 or double expression
+        if (C.fp) val = (C.img == IMG_F64) ? "((const double*)lds)[" + std::to_string(img_off[c] / 8) + " + " + id + "]"
+                                            : "dd" + std::to_string(c) + "[" + id + "]";
+        else if (C.img == IMG_NONE) val = "di" + std::to_string(c) + "[" + id + "]";
+        else val = "(vb" + std::to_string(c) + " + (i64)" + img_value(s, c, img_off, id) + ")";
+        std::string enc;
+        if (k == A_MIN || k == A_MAX) enc = C.fp ? "pgx_ord_f64(" + val + ")" : "pgx_ord_i64(" + val + ")";
+        else enc = C.fp ? "pgx_f64_bits(" + val + ")" : "(u64)" + val;
+        e.ln(plane_atomic(s.plane_op[a + 1], "&tab[" + std::to_string((a + 1) * s.dense_slots) + " + key]", enc));
+      }
+      e.ind--;
+      e.ln("}");
+    }
+    e.ind = 3;
+    e.ln("}");
+  }
+  e.ind = 2;
+  e.ln("}");
+  // per-segment flush of the lane accumulators (values depend on this segment's dictionaries)
+  e.ln("st_docs += scnt;");
+  if (!grouped) {
+    for (int a = 0; a < naggs; ++a) {
+      const int k = s.agg_kind[a];
+      if (k == A_COUNT) continue;
+      const int c = s.agg_col[a];
+      const JitCol& C = s.cols[c];
+      e.ln("{");
+      e.ind++;
+      if (k == A_SUM || k == A_AVG) {
+        if (C.fp) {
+          e.ln("const double x = pgx_wsum_f64(acc", a, ");");
+          e.ln("if (lane == 0) atomicAdd((double*)&s_acc[", a + 1, "], x);");
+        } else if (C.img == IMG_NONE) {
+          e.ln("const u64 x = pgx_wsum_u64((u64)acc", a, ");");
+          e.ln("if (lane == 0) atomicAdd(&s_acc[", a + 1, "], x);");
+        } else {
+          e.ln("const u64 x = pgx_wsum_u64(acc", a, " + scnt * (u64)vb", c, ");");
+          e.ln("if (lane == 0) atomicAdd(&s_acc[", a + 1, "], x);");
+        }
+      } else {
+        const bool mn = k == A_MIN;
+        const std::string id = (mn ? "mn" : "mx") + std::to_string(a);
+        const std::string v = C.fp ? "pgx_ord_f64(dd" + std::to_string(c) + "[" + id + "])"
+                                   : "pgx_ord_i64(di" + std::to_string(c) + "[" + id + "])";
+        e.ln("u64 x = ", mn ? "~0ull" : "0ull", ";");
+        e.ln("if (scnt) x = ", v, ";");
+        e.ln("x = ", mn ? "pgx_wmin_u64(x)" : "pgx_wmax_u64(x)", ";");
+        e.ln("if (lane == 0) ", mn ? "atomicMin" : "atomicMax", "(&s_acc[", a + 1, "], x);");
+      }
+      e.ind--;
+      e.ln("}");
+    }
+  }
+  e.ln("t = t2;");
+  e.ln("++seg;");
+  e.ind = 1;
+  e.ln("}");
+  e.ln("{");
+  e.ln("  const u64 d = pgx_wsum_u64(st_docs), x = pgx_wsum_u64(st_ent);");
+  e.ln("  if (lane == 0) {");
+  e.ln("    if (d) atomicAdd(A.stats, d);");
+  e.ln("    if (x) atomicAdd(A.stats + 1, x);");
+  if (!grouped) e.ln("    if (d) atomicAdd(&s_acc[0], d);");
+  e.ln("  }");
+  e.ln("}");
+  e.ln("__syncthreads();");
+  if (!grouped) {
+    e.ln("if (tid < ", s.num_planes, ") {");
+    e.ind++;
+    for (int p = 0; p < s.num_planes; ++p) {
+      if (p > 0 && s.agg_kind[p - 1] == A_COUNT) continue;
+      const int op = p == 0 ? P_ADD_I64 : s.plane_op[p];
+      e.ln("if (tid == ", p, ") ", plane_atomic(op, "A.agg_out + " + std::to_string(p), "s_acc[" + std::to_string(p) + "]"));
+    }
+    e.ind--;
+    e.ln("}");
+  }
+  if (s.group_mode == G_DENSE_LDS) {
+    e.ln("for (int i = tid; i < ", s.dense_slots * s.num_planes, "; i += PT) {");
+    e.ind++;
+    e.ln("const int p = i / ", s.dense_slots, ";");
+    e.ln("const int sl = i - p * ", s.dense_slots, ";");
+    e.ln("if (tab[sl] == 0ull) continue;");
+    e.ln("u64* g = A.table + i;");
+    e.ln("const u64 x = tab[i];");
+    for (int p = 0; p < s.num_planes; ++p)
+      e.ln("if (p == ", p, ") ", plane_atomic(p == 0 ? P_ADD_I64 : s.plane_op[p], "g", "x"));
+    e.ind--;
+    e.ln("}");
+  }
+  e.ind = 0;
+  e.ln("}");
+  return e.o.str();
+}
+
+namespace {
+
+struct JitEntry {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  int lds = 0;
+};
+
+std::mutex g_jit_mu;
+std::map<std::pair<int, std::string>, JitEntry> g_jit_cache;
+
+}  // namespace
+
+void* jit_function(const JitShape& s, int device, int* lds_bytes, std::string* err) {
+  int lds = 0;
+  const std::string src = jit_source(s, &lds);
+  if (lds_bytes) *lds_bytes = lds;
+  std::lock_guard<std::mutex> g(g_jit_mu);
+  auto key = std::make_pair(device, src);
+  auto it = g_jit_cache.find(key);
+  if (it != g_jit_cache.end()) return it->second.fn;
+  if (const char* dump = std::getenv("PGX_JIT_DUMP")) {  // debugging: keep every generated kernel's source
+    const std::string path = std::string(dump) + "/pgxq_" + std::to_string(g_jit_cache.size()) + ".hip";
+    if (FILE* f = std::fopen(path.c_str(), "w")) {
+      std::fputs(src.c_str(), f);
+      std::fclose(f);
+    }
+  }
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, src.c_str(), "pgx_query.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+    if (err) *err = "hiprtcCreateProgram failed";
+    return nullptr;
+  }
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+  if (rc != HIPRTC_SUCCESS) {
+    size_t n = 0;
+    hiprtcGetProgramLogSize(prog, &n);
+    std::string log(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &log[0]);
+    hiprtcDestroyProgram(&prog);
+    if (err) *err = "hiprtc compile failed: " + log.substr(0, 4000);
+    return nullptr;
+  }
+  size_t code_size = 0;
+  hiprtcGetCodeSize(prog, &code_size);
+  std::string code(code_size, '\0');
+  hiprtcGetCode(prog, &code[0]);
+  hiprtcDestroyProgram(&prog);
+  JitEntry ent;
+  ent.lds = lds;
+  if (hipModuleLoadData(&ent.mod, code.data()) != hipSuccess ||
+      hipModuleGetFunction(&ent.fn, ent.mod, "pgxq") != hipSuccess) {
+    if (err) *err = "hipModuleLoadData / hipModuleGetFunction failed";
+    return nullptr;
+  }
+  g_jit_cache.emplace(key, ent);
+  return ent.fn;
+}
+
+}  // namespace pgx
+
+// Debug / build-check entry: compile the kernel source of a shape without a device (declared in include/pgx.h).
+extern "C" int pgx_jit_compile_check(const char* source, char* log, unsigned long log_cap) {
+  hiprtcProgram prog;
+  if (hiprtcCreateProgram(&prog, source, "pgx_query.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return -1;
+  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+  size_t n = 0;
+  hiprtcGetProgramLogSize(prog, &n);
+  if (log && log_cap) {
+    std::string l(n, '\0');
+    if (n) hiprtcGetProgramLog(prog, &l[0]);
+    std::snprintf(log, log_cap, "%s", l.c_str());
+  }
+  hiprtcDestroyProgram(&prog);
+  return rc == HIPRTC_SUCCESS ? 0 : 1;
+}
+
+// Build check without a device: generate and compile a representative set of query shapes (every bit width, every
+// leaf kind, AND/OR/STAT programs, every aggregation, dense LDS / global group-by, every value-image kind).
+// Returns the number of shapes that failed; *n_total receives the number tried.  Declared in include/pgx.h.
+extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) {
+  using namespace pgx;
+  std::vector<JitShape> shapes;
+  auto base = [](int bits_f, int bits_m, int img, int sh) {
+    JitShape s;
+    s.cols.resize(2);
+    s.cols[0].bits = bits_f;
+    s.cols[0].decode = true;
+    s.cols[1].bits = bits_m;
+    s.cols[1].decode = true;
+    s.cols[1].img = img;
+    s.cols[1].img_sh = sh;
+    s.cols[1].img_words = img == IMG_FOR16 ? kImgFor16Blocks + (1 << 15) : (img == IMG_NONE ? 0 : 1024);
+    s.cols[1].acc32 = true;
+    int R = 8;
+    for (int b : {bits_f, bits_m}) {
+      int g = 1;
+      while (g < 32 && b % (g * 2) == 0) g *= 2;
+      R = std::max(R, 32 / g);
+    }
+    s.R = R;
+    s.T = img == IMG_FOR16 ? 1024 : 256;
+    s.leaf_col = {0};
+    s.leaf_mode = {LEAF_SCAN_INTERVAL};
+    s.prog_op = {OP_LEAF};
+    s.prog_arg = {0};
+    s.agg_kind = {A_COUNT, A_SUM, A_MIN, A_MAX, A_AVG};
+    s.agg_col = {-1, 1, 1, 1, 1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64, P_ADD_I64, P_MIN_ORD, P_MAX_ORD, P_ADD_I64};
+    s.num_planes = 6;
+    return s;
+  };
+  for (int b = 1; b <= 32; b += 3) shapes.push_back(base(b, 33 - b, IMG_U32, 0));
+  shapes.push_back(base(8, 16, IMG_FOR16, 11));
+  shapes.push_back(base(8, 16, IMG_NONE, 0));
+  {
+    JitShape s = base(10, 16, IMG_F64, 0);
+    s.cols[1].fp = true;
+    s.plane_op = {P_ADD_I64, P_ADD_I64, P_ADD_F64, P_MIN_ORD, P_MAX_ORD, P_ADD_F64};
+    s.leaf_mode = {LEAF_SCAN_BITSET};
+    shapes.push_back(s);
+  }
+  {
+    JitShape s = base(7, 12, IMG_U32, 0);
+    s.cols.push_back(JitCol{});
+    s.cols[2].bits = 4;
+    s.cols[2].decode = false;
+    s.leaf_col = {0, 2, 0};
+    s.leaf_mode = {LEAF_SCAN_INTERVAL, LEAF_RANGES, LEAF_NONE};
+    s.prog_op = {OP_LEAF, OP_STAT, OP_LEAF, OP_AND, OP_LEAF, OP_OR};
+    s.prog_arg = {1, 0, 0, 2, 2, 2};
+    s.cols[1].acc32 = false;
+    shapes.push_back(s);
+  }
+  for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {
+    JitShape s = base(8, 16, IMG_U32, 0);
+    s.cols.push_back(JitCol{});
+    s.cols[2].bits = 10;
+    s.cols[2].decode = true;
+    s.cols[2].remap = gm == G_DENSE_GLOBAL;
+    s.R = 16;
+    s.group_mode = gm;
+    s.gcol = {2, 0};
+    s.gmul = {1, 1000};
+    s.dense_slots = gm == G_DENSE_LDS ? 1000 : 256000;
+    s.agg_kind = {A_SUM, A_MIN, A_MAX, A_COUNT};
+    s.agg_col = {1, 1, 1, -1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64, P_MIN_ORD, P_MAX_ORD, P_ADD_I64};
+    s.num_planes = 5;
+    shapes.push_back(s);
+  }
+  {
+    JitShape s = base(8, 16, IMG_U32, 0);
+    s.prog_op.clear();
+    s.prog_arg.clear();
+    s.leaf_col.clear();
+    s.leaf_mode.clear();
+    s.agg_kind = {A_COUNT};
+    s.agg_col = {-1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64};
+    s.num_planes = 2;
+    s.cols[1].decode = false;
+    s.cols[1].img = IMG_NONE;
+    shapes.push_back(s);
+  }
+  int failed = 0;
+  std::string all;
+  for (size_t i = 0; i < shapes.size(); ++i) {
+    const std::string src = jit_source(shapes[i], nullptr);
+    char buf[4096];
+    if (pgx_jit_compile_check(src.c_str(), buf, sizeof(buf)) != 0) {
+      ++failed;
+      all += "shape " + std::to_string(i) + ": " + buf + "\n";
+    }
+  }
+  if (n_total) *n_total = int(shapes.size());
+  if (log && log_cap) std::snprintf(log, log_cap, "%s", all.c_str());
+  return failed;
+}
+

@@ -1,0 +1,40 @@
+// Argument block shared by the host (pgx_jit.cpp) and the query kernels it generates at run time (hiprtc).
+// Plain builtin types only, no includes: this file is compiled by hipcc for the host AND pasted verbatim in front of
+// every generated kernel, so both sides see the same layout.
+#ifndef PGX_JIT_ABI_H_
+#define PGX_JIT_ABI_H_
+
+#define PGX_J_MAX_COLS 8     // distinct columns one generated kernel reads
+#define PGX_J_MAX_LEAVES 16  // filter leaves (== kMaxLeaves)
+#define PGX_J_MAX_AGGS 8     // aggregation functions (== kMaxAggs)
+
+// Per-segment arguments of one launch group (segments whose columns share bit widths and value-image kinds).
+struct JSeg {
+  long long tile_begin;                          // first tile of this segment inside the launch group
+  int num_docs;                                  // rows scanned: [0, num_docs)
+  int pad0;
+  const unsigned int* fwd[PGX_J_MAX_COLS];       // packed big-endian fixed-bit forward index
+  const void* img[PGX_J_MAX_COLS];               // value image (LDS-staged) of SUM/AVG columns
+  const void* dict[PGX_J_MAX_COLS];              // full value table per dictId: int64 (INT/LONG) or double
+  const int* remap[PGX_J_MAX_COLS];              // group columns: local dictId -> global id (0 = identity)
+  long long vbase[PGX_J_MAX_COLS];               // integer images store value - vbase
+  const unsigned int* lbits[PGX_J_MAX_LEAVES];   // scan-bitset leaves: ceil(card/32) words
+  const int* lranges[PGX_J_MAX_LEAVES];          // sorted leaves: inclusive [a,b] doc ranges, ascending
+  int lnr[PGX_J_MAX_LEAVES];                     // number of ranges
+  unsigned int llo[PGX_J_MAX_LEAVES];            // scan-interval leaves: lo <= id <= lo + lspan
+  unsigned int lspan[PGX_J_MAX_LEAVES];
+  int img_words[PGX_J_MAX_COLS];                 // dwords of img to stage into LDS
+};
+
+struct JArgs {
+  const struct JSeg* segs;
+  int num_segs;
+  int pad0;
+  long long total_tiles;
+  long long tiles_per_wg;
+  unsigned long long* agg_out;   // aggregation-only: plane accumulators (plane 0 = matched docs)
+  unsigned long long* stats;     // [0] docs matched, [1] entries scanned in filter
+  unsigned long long* table;     // dense group-by: planes x slots
+};
+
+#endif  // PGX_JIT_ABI_H_

@@ -71,6 +71,8 @@ class ExecOpts(C.Structure):
 _lib = None
 
 EXPORTS = {
+    "pgx_jit_compile_check": (C.c_int, [C.c_char_p, C.c_char_p, C.c_ulong]),
+    "pgx_jit_selftest": (C.c_int, [C.POINTER(C.c_int), C.c_char_p, C.c_ulong]),
     "pgx_last_error": (C.c_char_p, []),
     "pgx_abi_version": (C.c_int32, []),
     "pgx_ctx_create": (C.c_int, [C.POINTER(CtxOpts), C.POINTER(C.c_void_p)]),

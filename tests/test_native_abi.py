@@ -37,3 +37,15 @@ def test_binding_table_matches_header():
     from pinot_amd import native
     assert set(native.EXPORTS) <= set(declared_symbols())
     assert set(declared_symbols()) <= set(native.EXPORTS)
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpgx.so not built")
+def test_query_compiler_shapes_compile_for_gfx950():
+    """The query compiler's generated kernels (every bit width, leaf kind, program op, aggregation, group mode and
+    value-image kind) compile with hiprtc for gfx950 -- checked here without a device."""
+    from pinot_amd import native
+    n = ctypes.c_int()
+    log = ctypes.create_string_buffer(1 << 16)
+    failed = native.lib().pgx_jit_selftest(ctypes.byref(n), log, len(log))
+    assert n.value >= 15
+    assert failed == 0, log.value.decode(errors="replace")
