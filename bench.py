@@ -203,9 +203,11 @@ def main():
                   | set((req.get("group_by") or {}).get("columns", [])))
     dict_cols = sorted({a["column"] for a in req["aggregations"] if a["column"] != "*"})
     algo_bytes = data.algorithmic_bytes(used, dict_cols)
+    # the query-specialised kernel (hiprtc, pgx_jit.cpp) unless PGX_JIT=0 selects the generic interpreter kernel
+    kernel_name = "pgxq (generated per query shape)" if os.environ.get("PGX_JIT", "1") != "0" else "pgx_scan_kernel"
     achieved = algo_bytes / (kern.value * 1e-3) / 1e9
     traffic = None
-    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.workload)
+    tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % wl.name)
     if os.path.exists(tf):
         tj = json.load(open(tf))
         if tj.get("rows") == rows:
@@ -225,7 +227,8 @@ def main():
                    "rows_total": total_rows, "parallelism": "dp%d (segment sharding)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "pgx_scan_kernel", "kernel_ms": kern.value, "algorithmic_bytes": algo_bytes},
+                     "kernel": kernel_name, "kernel_ms": kern.value, "algorithmic_bytes": algo_bytes,
+                     "host_ms_per_step": 1e3 * elapsed / args.steps - kern.value},
         "cpu_baseline": cpu,
         "result": summary, "stats": list(st), "gen_s": t_gen,
     }

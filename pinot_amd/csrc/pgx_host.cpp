@@ -96,8 +96,36 @@ uint64_t padded_fwd_bytes(int64_t total_docs, int bits) {
 // =================================================================================================
 struct pgx_ctx {
   int device = 0;
+  int num_cus = 256;
   hipStream_t stream = nullptr;
   std::mutex mu;
+  // Pinned host blocks for the per-query argument arena (one H2D copy per query) and result read-back.
+  std::multimap<size_t, void*> pinned_free;
+  std::unordered_map<void*, size_t> pinned_live;
+
+  void* pinned_alloc(size_t bytes) {
+    bytes = std::max<size_t>(4096, (bytes + 4095) & ~size_t(4095));
+    std::lock_guard<std::mutex> g(mu);
+    auto it = pinned_free.lower_bound(bytes);
+    if (it != pinned_free.end() && it->first <= bytes * 4) {
+      void* p = it->second;
+      pinned_live[p] = it->first;
+      pinned_free.erase(it);
+      return p;
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) fail(PGX_ERR_OOM, "hipHostMalloc failed");
+    pinned_live[p] = bytes;
+    return p;
+  }
+  void pinned_release(void* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> g(mu);
+    auto it = pinned_live.find(p);
+    if (it == pinned_live.end()) return;
+    pinned_free.emplace(it->second, p);
+    pinned_live.erase(it);
+  }
   // Simple size-bucketed device memory pool (avoids hipMalloc/hipFree on the query path).
   std::multimap<size_t, void*> free_blocks;
   std::unordered_map<void*, size_t> live;
@@ -132,6 +160,29 @@ struct pgx_ctx {
     free_blocks.emplace(it->second, p);
     live.erase(it);
   }
+};
+
+struct PinnedBuf {
+  pgx_ctx* ctx = nullptr;
+  void* p = nullptr;
+  PinnedBuf() = default;
+  PinnedBuf(pgx_ctx* c, size_t n) : ctx(c), p(c->pinned_alloc(n)) {}
+  PinnedBuf(const PinnedBuf&) = delete;
+  PinnedBuf& operator=(const PinnedBuf&) = delete;
+  PinnedBuf(PinnedBuf&& o) noexcept : ctx(o.ctx), p(o.p) { o.p = nullptr; }
+  PinnedBuf& operator=(PinnedBuf&& o) noexcept {
+    reset();
+    ctx = o.ctx;
+    p = o.p;
+    o.p = nullptr;
+    return *this;
+  }
+  ~PinnedBuf() { reset(); }
+  void reset() {
+    if (p && ctx) ctx->pinned_release(p);
+    p = nullptr;
+  }
+  uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
 };
 
 struct DevBuf {
@@ -636,7 +687,6 @@ struct ExecPlan {
     std::vector<JSeg> segs;
   };
   std::vector<JitGroup> jit;
-  std::vector<DevBuf> jit_bufs;
 };
 
 int qslot(ExecPlan& P, const std::string& name) {
@@ -829,44 +879,53 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   K.num_segs = n;
 
   // grid: persistent, contiguous tile ranges per workgroup
-  int cus = 256;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
-    cus = prop.multiProcessorCount;
+  const int cus = ctx->num_cus;
   const int wgs_per_cu = (K.group_mode == G_NONE) ? 8 : 4;
   const int64_t max_grid = int64_t(cus) * wgs_per_cu;
   P.tiles_per_wg = std::max<int64_t>(1, (tiles + max_grid - 1) / max_grid);
   P.grid = int(std::max<int64_t>(1, (tiles + P.tiles_per_wg - 1) / P.tiles_per_wg));
 }
 
+// Per-query device arguments live in ONE arena, written on the host into pinned memory and sent with ONE copy:
+//   [blob (ranges / bitsets / remaps) | KSeg x n | JSeg x n | outputs (agg planes, stats, overflow)]
+constexpr size_t kOutsBytes = 256;  // agg planes [0, 72), stats [128, 144), overflow [192, 200)
 struct ExecBuffers {
-  DevBuf segs, blob, agg_out, stats, table, keys, key_state, overflow;
+  DevBuf arena;
+  PinnedBuf host;
+  size_t off_ksegs = 0, off_jsegs = 0, off_outs = 0, size = 0;
+  DevBuf table, keys, key_state;
+  uint8_t* dev() const { return arena.as<uint8_t>(); }
 };
 
+size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
+
 void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
-  B.blob = DevBuf(ctx, std::max<size_t>(16, P.blob32.size() * 4));
-  if (!P.blob32.empty())
-    hip_check(hipMemcpyAsync(B.blob.p, P.blob32.data(), P.blob32.size() * 4, hipMemcpyHostToDevice, st), "blob");
-  const int32_t* base = B.blob.as<int32_t>();
+  (void)st;
+  const size_t n = P.ksegs.size();
+  B.off_ksegs = align_up(P.blob32.size() * 4, 256);
+  B.off_jsegs = align_up(B.off_ksegs + n * sizeof(KSeg), 256);
+  B.off_outs = align_up(B.off_jsegs + n * sizeof(JSeg), 256);
+  B.size = B.off_outs + kOutsBytes;
+  B.arena = DevBuf(ctx, B.size);
+  B.host = PinnedBuf(ctx, B.size);
+  if (!P.blob32.empty()) std::memcpy(B.host.bytes(), P.blob32.data(), P.blob32.size() * 4);
+  const int32_t* base = reinterpret_cast<const int32_t*>(B.dev());
   for (const auto& f : P.fixes) {
     KSeg& S = P.ksegs[f.seg];
     if (f.kind == 0) S.remap[f.slot] = base + f.off;
     else if (f.kind == 1) S.leaf[f.slot].ranges = base + f.off;
     else S.leaf[f.slot].bitset = reinterpret_cast<const uint32_t*>(base + f.off);
   }
-  B.segs = DevBuf(ctx, P.ksegs.size() * sizeof(KSeg));
-  hip_check(hipMemcpyAsync(B.segs.p, P.ksegs.data(), P.ksegs.size() * sizeof(KSeg), hipMemcpyHostToDevice, st), "segs");
-  P.kq.segs = B.segs.as<KSeg>();
+  if (n) std::memcpy(B.host.bytes() + B.off_ksegs, P.ksegs.data(), n * sizeof(KSeg));
+  P.kq.segs = reinterpret_cast<const KSeg*>(B.dev() + B.off_ksegs);
+  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.dev() + B.off_outs);
+  P.kq.agg_out = outs;
+  P.kq.stats = outs + 16;
+  P.kq.overflow = outs + 24;
 }
 
 void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, uint64_t dense_out_bytes) {
   KQuery& K = P.kq;
-  B.agg_out = DevBuf(ctx, 8 * (kMaxAggs + 1));
-  B.stats = DevBuf(ctx, 64);
-  B.overflow = DevBuf(ctx, 64);
-  K.agg_out = devp(B.agg_out);
-  K.stats = devp(B.stats);
-  K.overflow = devp(B.overflow);
   K.table = nullptr;
   K.keys = nullptr;
   K.key_state = nullptr;
@@ -895,12 +954,12 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
 }
 
 void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st) {
+  // (re)sends the whole argument arena with initialised output planes
   KQuery& K = P.kq;
-  std::vector<unsigned long long> init(kMaxAggs + 1, 0ull);
-  for (int p = 1; p < K.num_planes; ++p) init[p] = (K.plane_op[p] == P_MIN_ORD) ? ~0ull : 0ull;
-  hip_check(hipMemcpyAsync(B.agg_out.p, init.data(), init.size() * 8, hipMemcpyHostToDevice, st), "init");
-  hip_check(hipMemsetAsync(B.stats.p, 0, 64, st), "memset");
-  hip_check(hipMemsetAsync(B.overflow.p, 0, 64, st), "memset");
+  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+  std::memset(outs, 0, kOutsBytes);
+  for (int p = 1; p < K.num_planes; ++p) outs[p] = (K.plane_op[p] == P_MIN_ORD) ? ~0ull : 0ull;
+  hip_check(hipMemcpyAsync(B.arena.p, B.host.p, B.size, hipMemcpyHostToDevice, st), "argument arena H2D");
   if (K.group_mode != G_NONE) {
     const uint64_t slots = (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) ? P.hash_cap : P.dense_slots;
     const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : (K.group_mode == G_HASH64 ? P.hash_cap : 0);
@@ -916,7 +975,7 @@ bool jit_enabled() {
   return !(e && e[0] == '0');
 }
 
-void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, hipStream_t st) {
+void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
   P.jit.clear();
   const KQuery& K = P.kq;
   if (!jit_enabled()) return;
@@ -949,10 +1008,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     if (!groups.count(sig)) order.push_back(sig);
     groups[sig].push_back(s);
   }
-  int cus = 256;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, ctx->device) == hipSuccess && prop.multiProcessorCount > 0)
-    cus = prop.multiProcessorCount;
+  const int cus = ctx->num_cus;
+  size_t jidx = 0;  // next free JSeg slot of the arena
   for (const std::string& sig : order) {
     const std::vector<int>& members = groups[sig];
     const KSeg& S0 = P.ksegs[members[0]];
@@ -1065,13 +1122,12 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     const int64_t max_grid = int64_t(cus) * per_cu;
     const int64_t tpw = std::max<int64_t>(1, (tiles + max_grid - 1) / max_grid);
     G.grid = int(std::max<int64_t>(1, (tiles + tpw - 1) / tpw));
-    DevBuf buf(ctx, G.segs.size() * sizeof(JSeg));
-    hip_check(hipMemcpyAsync(buf.p, G.segs.data(), G.segs.size() * sizeof(JSeg), hipMemcpyHostToDevice, st), "jseg");
-    G.args.segs = buf.as<JSeg>();
+    std::memcpy(B.host.bytes() + B.off_jsegs + jidx * sizeof(JSeg), G.segs.data(), G.segs.size() * sizeof(JSeg));
+    G.args.segs = reinterpret_cast<const JSeg*>(B.dev() + B.off_jsegs + jidx * sizeof(JSeg));
+    jidx += G.segs.size();
     G.args.num_segs = int(G.segs.size());
     G.args.total_tiles = tiles;
     G.args.tiles_per_wg = tpw;
-    P.jit_bufs.push_back(std::move(buf));
     if (tiles > 0) P.jit.push_back(std::move(G));
   }
   if (P.jit.empty()) P.jit.push_back(ExecPlan::JitGroup{});  // every segment empty: nothing to launch
@@ -1098,9 +1154,12 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
 void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, pgx_segment* const* segs, int n,
                    hipStream_t st, pgx_result* R, const unsigned long long* dense_host_override) {
   KQuery& K = P.kq;
-  unsigned long long stats[2] = {0, 0};
-  hip_check(hipMemcpyAsync(stats, B.stats.p, 16, hipMemcpyDeviceToHost, st), "stats D2H");
-  hip_check(hipStreamSynchronize(st), "sync");
+  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+  if (!dense_host_override) {  // one read-back of every output plane and statistic
+    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+  }
+  const unsigned long long* stats = outs + 16;
   R->stats[0] = int64_t(stats[0]);
   R->stats[1] = int64_t(stats[1]) + P.host_entries;
   R->stats[2] = int64_t(stats[0]) * P.n_proj;
@@ -1111,8 +1170,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
   R->group_by = K.num_gcols > 0;
   R->mode = P.mode_ref;
   if (!R->group_by) {
-    unsigned long long acc[kMaxAggs + 1];
-    hip_check(hipMemcpy(acc, B.agg_out.p, 8 * (kMaxAggs + 1), hipMemcpyDeviceToHost), "agg D2H");
+    const unsigned long long* acc = outs;
     R->agg_value.assign(K.num_aggs, 0.0);
     R->agg_count.assign(K.num_aggs, 0);
     for (int a = 0; a < K.num_aggs; ++a) {
@@ -1232,7 +1290,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   plan_query(ctx, q, segs, n, bindings, xflags, P);
   ExecBuffers B;
   upload_plan(ctx, P, B, st);
-  plan_jit(ctx, q, segs, n, P, st);
+  plan_jit(ctx, q, segs, n, P, B);
   const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
   if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
   for (int attempt = 0; attempt < 6; ++attempt) {
@@ -1240,17 +1298,18 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     reset_outputs(P, B, st);
     launch_scan(P, st);
     if (!hash) break;
-    unsigned long long ovf = 0;
-    hip_check(hipMemcpyAsync(&ovf, B.overflow.p, 8, hipMemcpyDeviceToHost, st), "D2H");
+    unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
     hip_check(hipStreamSynchronize(st), "sync");
-    if (ovf == 0) break;
+    if (outs[24] == 0) break;
     P.hash_cap *= 4;  // table full: grow and rerun
     if (attempt == 5) fail(PGX_ERR_OOM, "group-by hash table overflow");
   }
   if (opts && (opts->flags & PGX_X_KEEP_DENSE_ON_DEVICE)) {
-    unsigned long long stats[2] = {0, 0};
-    hip_check(hipMemcpyAsync(stats, B.stats.p, 16, hipMemcpyDeviceToHost, st), "D2H");
+    unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
     hip_check(hipStreamSynchronize(st), "sync");
+    const unsigned long long* stats = outs + 16;
     R->stats[0] = int64_t(stats[0]);
     R->stats[1] = int64_t(stats[1]) + P.host_entries;
     R->stats[2] = int64_t(stats[0]) * P.n_proj;
@@ -1283,6 +1342,9 @@ pgx_status pgx_ctx_create(const pgx_ctx_opts* opts, pgx_ctx** out) {
     hip_check(hipSetDevice(dev), "hipSetDevice");
     auto* c = new pgx_ctx();
     c->device = dev;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+      c->num_cus = prop.multiProcessorCount;
     hip_check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
     *out = c;
   });
@@ -1295,6 +1357,8 @@ pgx_status pgx_ctx_destroy(pgx_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->free_blocks) (void)hipFree(kv.second);
     for (auto& kv : ctx->live) (void)hipFree(kv.first);
+    for (auto& kv : ctx->pinned_free) (void)hipHostFree(kv.second);
+    for (auto& kv : ctx->pinned_live) (void)hipHostFree(kv.first);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
   });
@@ -1496,9 +1560,10 @@ pgx_status pgx_result_from_dense(pgx_ctx* ctx, const pgx_query* q, pgx_segment* 
     hip_check(hipMemcpy(host.data(), dense_device, total * 8, hipMemcpyDeviceToHost), "dense D2H");
     auto R = std::make_unique<pgx_result>();
     ExecBuffers B;
-    B.stats = DevBuf(ctx, 64);
-    unsigned long long s2[2] = {static_cast<unsigned long long>(stats[0]), 0ull};
-    hip_check(hipMemcpy(B.stats.p, s2, 16, hipMemcpyHostToDevice), "H2D");
+    B.host = PinnedBuf(ctx, kOutsBytes);
+    B.off_outs = 0;
+    std::memset(B.host.p, 0, kOutsBytes);
+    reinterpret_cast<unsigned long long*>(B.host.p)[16] = static_cast<unsigned long long>(stats[0]);
     P.host_entries = stats[1];
     finish_result(ctx, *q, P, B, segs, n, ctx->stream, R.get(), host.data());
     R->stats[0] = stats[0];
@@ -1559,7 +1624,7 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     plan_query(ctx, *q, segs, n, bindings, 0, P);
     ExecBuffers B;
     upload_plan(ctx, P, B, st);
-    plan_jit(ctx, *q, segs, n, P, st);
+    plan_jit(ctx, *q, segs, n, P, B);
     const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
     if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
     alloc_outputs(ctx, P, B, nullptr, 0);

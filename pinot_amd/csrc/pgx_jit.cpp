@@ -165,7 +165,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       if (s.cols[c].img == IMG_NONE) continue;
       e.ln("{");
       e.ind++;
-      e.ln("const pgx_u32x4* __restrict__ src = (const pgx_u32x4*)S->img[", c, "];");
+      e.ln("const PGX_G pgx_u32x4* __restrict__ src = (const PGX_G pgx_u32x4*)S->img[", c, "];");
       e.ln("pgx_u32x4* dst = (pgx_u32x4*)(lds + ", img_off[c] / 4, ");");
       e.ln("const int nq = (S->img_words[", c, "] + 3) >> 2;");
       e.ln("for (int i = tid; i < nq; i += PT) dst[i] = src[i];");
@@ -184,10 +184,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         e.ln("const u32 lo", l, " = S->llo[", l, "], sp", l, " = S->lspan[", l, "];");
         break;
       case LEAF_SCAN_BITSET:
-        e.ln("const u32* __restrict__ bs", l, " = S->lbits[", l, "];");
+        e.ln("const PGX_G u32* __restrict__ bs", l, " = (const PGX_G u32*)S->lbits[", l, "];");
         break;
       case LEAF_RANGES:
-        e.ln("const int* __restrict__ rg", l, " = S->lranges[", l, "];");
+        e.ln("const PGX_G int* __restrict__ rg", l, " = (const PGX_G int*)S->lranges[", l, "];");
         e.ln("const int nr", l, " = S->lnr[", l, "];");
         e.ln("int cur", l, " = pgx_ranges_seek(rg", l, ", nr", l, ", (int)((t - tile0) * (PT * 32)));");
         break;
@@ -198,7 +198,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // group columns: remap tables
   if (grouped)
     for (size_t g = 0; g < s.gcol.size(); ++g)
-      if (s.cols[s.gcol[g]].remap) e.ln("const int* __restrict__ rm", g, " = S->remap[", s.gcol[g], "];");
+      if (s.cols[s.gcol[g]].remap) e.ln("const PGX_G int* __restrict__ rm", g, " = (const PGX_G int*)S->remap[", s.gcol[g], "];");
   // value bases / dictionaries used by the aggregations
   const int naggs = int(s.agg_kind.size());
   std::vector<bool> need_vb(ncols, false), need_dict(ncols, false);
@@ -222,12 +222,12 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   for (int c = 0; c < ncols; ++c) {
     if (need_vb[c]) e.ln("const i64 vb", c, " = S->vbase[", c, "];");
     if (need_dict[c]) {
-      if (s.cols[c].fp) e.ln("const double* __restrict__ dd", c, " = (const double*)S->dict[", c, "];");
-      else e.ln("const i64* __restrict__ di", c, " = (const i64*)S->dict[", c, "];");
+      if (s.cols[c].fp) e.ln("const PGX_G double* __restrict__ dd", c, " = (const PGX_G double*)S->dict[", c, "];");
+      else e.ln("const PGX_G i64* __restrict__ di", c, " = (const PGX_G i64*)S->dict[", c, "];");
     }
   }
   // lane accumulators (aggregation-only)
-  e.ln("u64 scnt = 0;");
+  e.ln("u64 wcnt = 0;  // selected rows of this wave in this segment (wave-uniform)");
   if (!grouped) {
     for (int a = 0; a < naggs; ++a) {
       const int k = s.agg_kind[a];
@@ -280,106 +280,103 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("if (tt + 1 < t2) ");
   emit_loads("tt + 1", "n");
   e.ln("const int rb = (int)((tt - tile0) * (PT * 32));");
+  // The tile body is instantiated twice: for whole tiles (no per-row bound check) and for a segment's last tile.
+  e.ln("auto body = [&](auto FT) {");
+  e.ind = 4;
+  e.ln("constexpr bool FULL = decltype(FT)::value;");
   for (int u = 0; u < U; ++u) {
     e.ln("{");
-    e.ind = 4;
+    e.ind = 5;
     e.ln("const int r0 = rb + ", u * s.R, " * PT + tid * PR;");
-    e.ln("const u32 valid = pgx_valid_bits(r0, nd, PR);");
     for (int c = 0; c < ncols; ++c) {
       if (!s.cols[c].decode) continue;
       e.ln("u32 v", c, "[PR];");
       e.ln("pgx_unpack<", s.cols[c].bits, ", PR>(&c", c, "[", u * dwords_per(s, c), "], v", c, ");");
     }
-    // filter program
+    for (int l = 0; l < nleaves; ++l)
+      if (s.leaf_mode[l] == LEAF_RANGES) e.ln("const u32 W", l, " = pgx_ranges_bits(rg", l, ", nr", l, ", cur", l, ", r0, PR);");
+    // per-aggregation sub-step partials
+    if (!grouped)
+      for (int a = 0; a < naggs; ++a) {
+        const int k = s.agg_kind[a];
+        if ((k == A_SUM || k == A_AVG) && !s.cols[s.agg_col[a]].fp && s.cols[s.agg_col[a]].img != IMG_NONE &&
+            s.cols[s.agg_col[a]].acc32)
+          e.ln("u32 p", a, " = 0u;");
+      }
+    e.ln("#pragma unroll");
+    e.ln("for (int j = 0; j < PR; ++j) {");
+    e.ind = 6;
+    e.ln("const bool vj = FULL || (r0 + j < nd);");
+    // filter program over per-row predicates (lane masks: AND/OR become scalar ops on the wave's masks)
     std::vector<std::string> st;
     int tmp = 0;
-    std::string mask = "valid";
     for (size_t pc = 0; pc < s.prog_op.size(); ++pc) {
       const int op = s.prog_op[pc], arg = s.prog_arg[pc];
       if (op == OP_LEAF) {
         const int l = arg, c = s.leaf_col[l];
-        const std::string L = "L" + std::to_string(tmp++);
+        const std::string B = "b" + std::to_string(tmp++);
+        const std::string v = "v" + std::to_string(c) + "[j]";
         switch (s.leaf_mode[l]) {
           case LEAF_SCAN_INTERVAL:
-            e.ln("u32 ", L, " = 0u;");
-            e.ln("#pragma unroll");
-            e.ln("for (int j = 0; j < PR; ++j) ", L, " |= (u32)((v", c, "[j] - lo", l, ") <= sp", l, ") << j;");
+            e.ln("const bool ", B, " = vj && ((", v, " - lo", l, ") <= sp", l, ");");
             break;
           case LEAF_SCAN_BITSET:
-            e.ln("u32 ", L, " = 0u;");
-            e.ln("#pragma unroll");
-            e.ln("for (int j = 0; j < PR; ++j) ", L, " |= ((bs", l, "[v", c, "[j] >> 5] >> (v", c,
-                 "[j] & 31u)) & 1u) << j;");
+            e.ln("const bool ", B, " = vj && ((bs", l, "[", v, " >> 5] >> (", v, " & 31u)) & 1u);");
             break;
           case LEAF_RANGES:
-            e.ln("const u32 ", L, " = pgx_ranges_bits(rg", l, ", nr", l, ", cur", l, ", r0, PR);");
+            e.ln("const bool ", B, " = vj && ((W", l, " >> j) & 1u);");
             break;
           default:
-            e.ln("const u32 ", L, " = 0u;");
+            e.ln("const bool ", B, " = false;");
             break;
         }
-        st.push_back("(" + L + " & valid)");
+        st.push_back(B);
       } else if (op == OP_AND || op == OP_OR) {
         for (int k = 1; k < arg; ++k) {
           const std::string b = st.back();
           st.pop_back();
           const std::string a = st.back();
           st.pop_back();
-          const std::string X = "X" + std::to_string(tmp++);
-          e.ln("const u32 ", X, " = ", a, op == OP_AND ? " & " : " | ", b, ";");
+          const std::string X = "x" + std::to_string(tmp++);
+          e.ln("const bool ", X, " = ", a, op == OP_AND ? " & " : " | ", b, ";");
           st.push_back(X);
         }
       } else if (op == OP_STAT) {
-        e.ln("st_ent += __popc(", st.back(), ");");
+        e.ln("st_ent += __popcll(__ballot(", st.back(), "));");
       } else if (op == OP_TRUE) {
-        st.push_back("valid");
+        st.push_back("vj");
       }
     }
-    if (!st.empty()) mask = "(" + st.back() + " & valid)";
-    e.ln("const u32 mask = ", mask, ";");
-    e.ln("scnt += __popc(mask);");
+    e.ln("const bool m = ", st.empty() ? std::string("vj") : st.back(), ";");
+    e.ln("wcnt += __popcll(__ballot(m));");
     if (!grouped) {
       for (int a = 0; a < naggs; ++a) {
         const int k = s.agg_kind[a];
         if (k == A_COUNT) continue;
         const int c = s.agg_col[a];
         const JitCol& C = s.cols[c];
-        const std::string va = "v" + std::to_string(c);
+        const std::string v = "v" + std::to_string(c) + "[j]";
         if (k == A_MIN) {
-          e.ln("#pragma unroll");
-          e.ln("for (int j = 0; j < PR; ++j) mn", a, " = min(mn", a, ", ((mask >> j) & 1u) ? ", va, "[j] : 0xFFFFFFFFu);");
+          e.ln("mn", a, " = min(mn", a, ", m ? ", v, " : 0xFFFFFFFFu);");
         } else if (k == A_MAX) {
-          e.ln("#pragma unroll");
-          e.ln("for (int j = 0; j < PR; ++j) mx", a, " = max(mx", a, ", ((mask >> j) & 1u) ? ", va, "[j] : 0u);");
+          e.ln("mx", a, " = max(mx", a, ", m ? ", v, " : 0u);");
         } else if (C.fp) {
           const std::string val = (C.img == IMG_F64)
-                                      ? "((const double*)lds)[" + std::to_string(img_off[c] / 8) + " + " + va + "[j]]"
-                                      : "dd" + std::to_string(c) + "[" + va + "[j]]";
-          e.ln("#pragma unroll");
-          e.ln("for (int j = 0; j < PR; ++j) if ((mask >> j) & 1u) acc", a, " += ", val, ";");
+                                      ? "((const double*)lds)[" + std::to_string(img_off[c] / 8) + " + " + v + "]"
+                                      : "dd" + std::to_string(c) + "[" + v + "]";
+          e.ln("if (m) acc", a, " += ", val, ";");
         } else if (C.img == IMG_NONE) {
-          e.ln("#pragma unroll");
-          e.ln("for (int j = 0; j < PR; ++j) if ((mask >> j) & 1u) acc", a, " += di", c, "[", va, "[j]];");
+          e.ln("if (m) acc", a, " += di", c, "[", v, "];");
         } else if (C.acc32) {
-          e.ln("{");
-          e.ln("  u32 p = 0u;");
-          e.ln("  #pragma unroll");
-          e.ln("  for (int j = 0; j < PR; ++j) { const u32 x = ", img_value(s, c, img_off, va + "[j]"),
-               "; p += ((mask >> j) & 1u) ? x : 0u; }");
-          e.ln("  acc", a, " += p;");
-          e.ln("}");
+          e.ln("{ const u32 x = ", img_value(s, c, img_off, v), "; p", a, " += m ? x : 0u; }");
         } else {
-          e.ln("#pragma unroll");
-          e.ln("for (int j = 0; j < PR; ++j) { const u32 x = ", img_value(s, c, img_off, va + "[j]"), "; acc", a,
-               " += ((mask >> j) & 1u) ? (u64)x : 0ull; }");
+          e.ln("{ const u32 x = ", img_value(s, c, img_off, v), "; acc", a, " += m ? (u64)x : 0ull; }");
         }
       }
     } else {
       // dense group-by: key = sum_g id_g * mul_g (column 0 least significant, DefaultGroupKeyGenerator.java:230-237)
-      e.ln("#pragma unroll");
-      e.ln("for (int j = 0; j < PR; ++j) {");
-      e.ind++;
-      e.ln("if (!((mask >> j) & 1u)) continue;");
+      e.ln("if (m) {");
+      e.ind = 7;
       std::string key;
       for (size_t g = 0; g < s.gcol.size(); ++g) {
         const int c = s.gcol[g];
@@ -406,16 +403,28 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         else enc = C.fp ? "pgx_f64_bits(" + val + ")" : "(u64)" + val;
         e.ln(plane_atomic(s.plane_op[a + 1], "&tab[" + std::to_string((a + 1) * s.dense_slots) + " + key]", enc));
       }
-      e.ind--;
+      e.ind = 6;
       e.ln("}");
     }
-    e.ind = 3;
+    e.ind = 5;
+    e.ln("}");
+    if (!grouped)
+      for (int a = 0; a < naggs; ++a) {
+        const int k = s.agg_kind[a];
+        if ((k == A_SUM || k == A_AVG) && !s.cols[s.agg_col[a]].fp && s.cols[s.agg_col[a]].img != IMG_NONE &&
+            s.cols[s.agg_col[a]].acc32)
+          e.ln("acc", a, " += p", a, ";");
+      }
+    e.ind = 4;
     e.ln("}");
   }
+  e.ind = 3;
+  e.ln("};");
+  e.ln("if (rb + PT * 32 <= nd) body(pgx_bool<true>{}); else body(pgx_bool<false>{});");
   e.ind = 2;
   e.ln("}");
   // per-segment flush of the lane accumulators (values depend on this segment's dictionaries)
-  e.ln("st_docs += scnt;");
+  e.ln("st_docs += wcnt;");
   if (!grouped) {
     for (int a = 0; a < naggs; ++a) {
       const int k = s.agg_kind[a];
@@ -432,8 +441,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
           e.ln("const u64 x = pgx_wsum_u64((u64)acc", a, ");");
           e.ln("if (lane == 0) atomicAdd(&s_acc[", a + 1, "], x);");
         } else {
-          e.ln("const u64 x = pgx_wsum_u64(acc", a, " + scnt * (u64)vb", c, ");");
-          e.ln("if (lane == 0) atomicAdd(&s_acc[", a + 1, "], x);");
+          e.ln("const u64 x = pgx_wsum_u64(acc", a, ");");
+          e.ln("if (lane == 0) atomicAdd(&s_acc[", a + 1, "], x + wcnt * (u64)vb", c, ");");
         }
       } else {
         const bool mn = k == A_MIN;
@@ -441,7 +450,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         const std::string v = C.fp ? "pgx_ord_f64(dd" + std::to_string(c) + "[" + id + "])"
                                    : "pgx_ord_i64(di" + std::to_string(c) + "[" + id + "])";
         e.ln("u64 x = ", mn ? "~0ull" : "0ull", ";");
-        e.ln("if (scnt) x = ", v, ";");
+        e.ln("if (", mn ? "mn" + std::to_string(a) + " != 0xFFFFFFFFu" : std::string("wcnt"), ") x = ", v, ";");
         e.ln("x = ", mn ? "pgx_wmin_u64(x)" : "pgx_wmax_u64(x)", ";");
         e.ln("if (lane == 0) ", mn ? "atomicMin" : "atomicMax", "(&s_acc[", a + 1, "], x);");
       }
@@ -454,7 +463,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ind = 1;
   e.ln("}");
   e.ln("{");
-  e.ln("  const u64 d = pgx_wsum_u64(st_docs), x = pgx_wsum_u64(st_ent);");
+  e.ln("  const u64 d = st_docs, x = st_ent;  // wave-uniform counts");
   e.ln("  if (lane == 0) {");
   e.ln("    if (d) atomicAdd(A.stats, d);");
   e.ln("    if (x) atomicAdd(A.stats + 1, x);");
@@ -566,6 +575,18 @@ extern "C" int pgx_jit_compile_check(const char* source, char* log, unsigned lon
     if (n) hiprtcGetProgramLog(prog, &l[0]);
     std::snprintf(log, log_cap, "%s", l.c_str());
   }
+  // debugging: PGX_JIT_CODE=<path> keeps the code object of the last compile (for llvm-objdump)
+  if (rc == HIPRTC_SUCCESS)
+    if (const char* path = std::getenv("PGX_JIT_CODE")) {
+      size_t cs = 0;
+      hiprtcGetCodeSize(prog, &cs);
+      std::string code(cs, '\0');
+      hiprtcGetCode(prog, &code[0]);
+      if (FILE* f = std::fopen(path, "wb")) {
+        std::fwrite(code.data(), 1, cs, f);
+        std::fclose(f);
+      }
+    }
   hiprtcDestroyProgram(&prog);
   return rc == HIPRTC_SUCCESS ? 0 : 1;
 }
@@ -607,6 +628,14 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
   };
   for (int b = 1; b <= 32; b += 3) shapes.push_back(base(b, 33 - b, IMG_U32, 0));
   shapes.push_back(base(8, 16, IMG_FOR16, 11));
+  {  // the C2 benchmark shape: COUNT(*), SUM(m) WHERE dA BETWEEN lo AND hi
+    JitShape s = base(8, 16, IMG_FOR16, 11);
+    s.agg_kind = {A_COUNT, A_SUM};
+    s.agg_col = {-1, 1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64, P_ADD_I64};
+    s.num_planes = 3;
+    shapes.push_back(s);
+  }
   shapes.push_back(base(8, 16, IMG_NONE, 0));
   {
     JitShape s = base(10, 16, IMG_F64, 0);
@@ -662,6 +691,13 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
   std::string all;
   for (size_t i = 0; i < shapes.size(); ++i) {
     const std::string src = jit_source(shapes[i], nullptr);
+    if (const char* dump = std::getenv("PGX_JIT_DUMP")) {
+      const std::string path = std::string(dump) + "/selftest_" + std::to_string(i) + ".hip";
+      if (FILE* f = std::fopen(path.c_str(), "w")) {
+        std::fputs(src.c_str(), f);
+        std::fclose(f);
+      }
+    }
     char buf[4096];
     if (pgx_jit_compile_check(src.c_str(), buf, sizeof(buf)) != 0) {
       ++failed;
