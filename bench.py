@@ -104,10 +104,8 @@ def main():
     wl = synth.WORKLOADS[args.workload]
     rows = args.rows or wl.rows
     ctx = E.Context(local)
-    if wl.scaling == "weak":
-        seg_ids = [rank * wl.segments + i for i in range(wl.segments)]
-    else:
-        seg_ids = list(range(rank, wl.segments, world))
+    from pinot_amd import multigpu
+    seg_ids = multigpu.shard(wl.segments, world, rank, wl.scaling)
     t_gen = time.perf_counter()
     data = synth.DeviceSegments(ctx, wl, seg_ids, rows=rows)
     t_gen = time.perf_counter() - t_gen
@@ -139,6 +137,8 @@ def main():
             print(json.dumps({"profile_iters": args.profile_iters, "kernel_ms": kern.value}))
         return
 
+    merged = [None]
+
     def step():
         r = C.c_void_p()
         if dense and world > 1:
@@ -147,7 +147,7 @@ def main():
             st = (C.c_int64 * 4)()
             N.check(L.pgx_result_stats(r, st))
             L.pgx_result_release(r)
-            merge_dense(dense_t, plane_ops, world)
+            multigpu.merge_dense_planes(dense_t, plane_ops)
             stats_t = torch.tensor(list(st), dtype=torch.int64, device=dense_t.device)
             torch.distributed.all_reduce(stats_t)
             out = C.c_void_p()
@@ -162,9 +162,9 @@ def main():
             for i in range(len(req["aggregations"])):
                 v, c = C.c_double(), C.c_int64()
                 N.check(L.pgx_result_agg(r, i, C.byref(v), C.byref(c)))
-                vals += [v.value, float(c.value)]
-            t = torch.tensor(vals, dtype=torch.float64, device="cuda:%d" % local)
-            torch.distributed.all_reduce(t)
+                vals.append((v.value, c.value))
+            merged[0] = multigpu.merge_aggregation([a["fn"] for a in req["aggregations"]], vals,
+                                                   device="cuda:%d" % local)
         return r
 
     for _ in range(args.warmup):
@@ -217,6 +217,8 @@ def main():
         cpu = cpu_baseline_c2(wl, min(rows, 32_000_000), 8, 8)
     summary = blk.get_aggregation_result() if blk.aggregation_result is not None else \
         {"groups": blk.get_aggregation_group_by_result().num_groups()}
+    if merged[0] is not None:
+        summary = {"local": summary, "merged_over_gpus": merged[0]}
     line = {
         "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
@@ -234,29 +236,6 @@ def main():
     }
     print(json.dumps(line))
     data.free()
-
-
-def merge_dense(t, plane_ops, world):
-    """Cross-GPU merge of the dense partial group tables over RCCL: one all-reduce per plane kind."""
-    import torch
-    import torch.distributed as dist
-    nplanes = len(plane_ops)
-    planes = t.view(nplanes, -1)
-    sign = torch.tensor(-(1 << 63), dtype=torch.int64, device=t.device)
-    adds = [p for p, op in enumerate(plane_ops) if op == 0]
-    if adds:
-        if len(adds) == nplanes:
-            dist.all_reduce(t)
-        else:
-            for p in adds:
-                dist.all_reduce(planes[p])
-    for p, op in enumerate(plane_ops):
-        if op == 1:
-            dist.all_reduce(planes[p].view(torch.float64))
-        elif op in (2, 3):
-            x = planes[p] ^ sign  # ordered-unsigned -> ordered-signed
-            dist.all_reduce(x, op=dist.ReduceOp.MIN if op == 2 else dist.ReduceOp.MAX)
-            planes[p].copy_(x ^ sign)
 
 
 if __name__ == "__main__":

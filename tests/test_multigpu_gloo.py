@@ -1,0 +1,118 @@
+"""World-size-2 gloo tests (CPU) of the multi-GPU layer (pinot_amd/multigpu.py): segment sharding and the
+cross-rank merge of partials, checked against a single-process merge of the same rows.
+
+The per-rank partials are built here in the library's own plane encodings (pgx.h pgx_query_dense_plane_op) from raw
+rows, exactly as the GPU would leave them in HBM; the GPU side of the same path runs in bench.py --gpus N."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from pinot_amd import multigpu  # noqa: E402
+
+SIGN = np.uint64(1 << 63)
+
+
+def _ord_i64(x):
+    return (x.astype(np.int64).view(np.uint64) ^ SIGN).view(np.int64)
+
+
+def _rows(seed, n, card):
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, card, n), rng.integers(-(1 << 20), 1 << 20, n), rng.random(n) * 1e6
+
+
+def dense_table(keys, iv, fv, slots):
+    """planes: 0 count (i64 add) | sum(iv) i64 add | min(iv) ord | max(iv) ord | sum(fv) f64 add"""
+    t = np.zeros((5, slots), dtype=np.int64)
+    t[2] = -1  # ~0: MIN identity
+    np.add.at(t[0], keys, 1)
+    np.add.at(t[1], keys, iv)
+    mn = np.full(slots, np.iinfo(np.int64).max)
+    np.minimum.at(mn, keys, iv)
+    mx = np.full(slots, np.iinfo(np.int64).min)
+    np.maximum.at(mx, keys, iv)
+    has = t[0] > 0
+    t[2][has] = _ord_i64(mn[has])
+    t[3][has] = _ord_i64(mx[has])
+    f = np.zeros(slots)
+    np.add.at(f, keys, fv)
+    t[4] = f.view(np.int64)
+    return t
+
+
+OPS = [multigpu.PLANE_ADD_I64, multigpu.PLANE_ADD_I64, multigpu.PLANE_MIN_ORD, multigpu.PLANE_MAX_ORD,
+       multigpu.PLANE_ADD_F64]
+NSEG, ROWS, SLOTS = 6, 5000, 97
+
+
+def _worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = multigpu.shard(NSEG, world, rank, "strong")
+        parts = [_rows(s, ROWS, SLOTS) for s in mine]
+        k = np.concatenate([p[0] for p in parts])
+        iv = np.concatenate([p[1] for p in parts])
+        fv = np.concatenate([p[2] for p in parts])
+        t = torch.from_numpy(dense_table(k, iv, fv, SLOTS).reshape(-1).copy())
+        multigpu.merge_dense_planes(t, OPS)
+        fns = ["count", "sum", "min", "max", "avg"]
+        vals = [(float(len(iv)), len(iv)), (float(iv.sum()), len(iv)), (float(iv.min()), len(iv)),
+                (float(iv.max()), len(iv)), (float(iv.sum()), len(iv))]
+        agg = multigpu.merge_aggregation(fns, vals)
+        q.put((rank, mine, t.numpy().copy(), agg))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_covers_every_segment_once():
+    for world in (1, 2, 3, 8):
+        got = sorted(s for r in range(world) for s in multigpu.shard(4096, world, r, "strong"))
+        assert got == list(range(4096))
+        weak = [multigpu.shard(8, world, r, "weak") for r in range(world)]
+        assert all(len(w) == 8 for w in weak) and len({s for w in weak for s in w}) == 8 * world
+
+
+def test_two_rank_merge_matches_single_process():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    assert sorted(res[0][1] + res[1][1]) == list(range(NSEG))
+    allp = [_rows(s, ROWS, SLOTS) for s in range(NSEG)]
+    k = np.concatenate([p[0] for p in allp])
+    iv = np.concatenate([p[1] for p in allp])
+    fv = np.concatenate([p[2] for p in allp])
+    exp = dense_table(k, iv, fv, SLOTS).reshape(-1)
+    for rank, _, t, agg in res:
+        t2 = t.reshape(5, SLOTS)
+        e2 = exp.reshape(5, SLOTS)
+        assert np.array_equal(t2[:4], e2[:4]), "integer / ordered planes must merge bit-exactly"
+        np.testing.assert_allclose(t2[4].view(np.float64), e2[4].view(np.float64), rtol=1e-9)
+        assert agg[0] == (float(len(iv)), len(iv))
+        assert agg[1][0] == float(iv.sum()) and agg[2][0] == float(iv.min()) and agg[3][0] == float(iv.max())
+        assert agg[4] == (float(iv.sum()), len(iv))
