@@ -199,10 +199,15 @@ def main():
     tot, kern = C.c_double(), C.c_double()
     N.check(L.pgx_execute_timed(ctx.handle, q.handle, seg_arr, len(segs), binds, 10, C.byref(tot), C.byref(kern),
                                 None))
-    used = sorted({lf["column"] for lf in q.leaves} | {a["column"] for a in req["aggregations"] if a["column"] != "*"}
+    # forward-index bytes of every column the kernel decodes, serialized roaring bytes of every bitmap a
+    # bitmap-index leaf ORs (inverted columns, non-RANGE predicates: FilterPlanNode.java:118-132), dictionaries.
+    bitmap_leaves = [(lf, np.nonzero(E.leaf_matching_ids(segs[0].column(lf["column"]), lf))[0])
+                     for lf in q.leaves if data.is_inverted(lf["column"]) and lf["op"] != "RANGE"]
+    scan_cols = {lf["column"] for lf in q.leaves} - {lf["column"] for lf, _ in bitmap_leaves}
+    used = sorted(scan_cols | {a["column"] for a in req["aggregations"] if a["column"] != "*"}
                   | set((req.get("group_by") or {}).get("columns", [])))
     dict_cols = sorted({a["column"] for a in req["aggregations"] if a["column"] != "*"})
-    algo_bytes = data.algorithmic_bytes(used, dict_cols)
+    algo_bytes = data.algorithmic_bytes(used, dict_cols, bitmap_leaves)
     # the query-specialised kernel (hiprtc, pgx_jit.cpp) unless PGX_JIT=0 selects the generic interpreter kernel
     kernel_name = "pgxq (generated per query shape)" if os.environ.get("PGX_JIT", "1") != "0" else "pgx_scan_kernel"
     achieved = algo_bytes / (kern.value * 1e-3) / 1e9

@@ -210,6 +210,12 @@ pgx_status pgx_result_from_dense(pgx_ctx* ctx, const pgx_query* q, pgx_segment* 
  * pgx_synth_value(seed, row) = splitmix64(seed ^ (row * 0x9E3779B97F4A7C15)) % card  (DESIGN.md). */
 pgx_status pgx_synth_column(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
                             uint64_t seed);
+/* Host twin of pgx_synth_column's dictIds (int32 per row). */
+pgx_status pgx_synth_dict_ids(uint64_t seed, int64_t n_rows, int32_t card, int32_t* out);
+/* Segment creation: the <col>.bitmap.inv bytes of a column (HeapBitmapInvertedIndexCreator.java:42-81 layout, roaring
+ * portable format).  out == NULL or cap too small: *len receives the size only. */
+pgx_status pgx_inverted_index_build(const int32_t* ids, int64_t n, int32_t card, uint8_t* out, uint64_t cap,
+                                    uint64_t* len);
 pgx_status pgx_device_alloc(pgx_ctx* ctx, uint64_t bytes, void** out);
 pgx_status pgx_device_free(pgx_ctx* ctx, void* p);
 pgx_status pgx_copy_to_device(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes);

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -32,6 +33,7 @@ extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t
 extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
                                          unsigned long long* counter, int64_t* out_slot,
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
+extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
 extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
                                        int64_t n_words, hipStream_t stream);
 
@@ -95,6 +97,7 @@ uint64_t padded_fwd_bytes(int64_t total_docs, int bits) {
 // Context
 // =================================================================================================
 struct pgx_ctx {
+  std::atomic<int> refs{1};  // the caller's handle + one per staged segment
   int device = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
@@ -232,6 +235,8 @@ struct StagedColumn {
   std::vector<std::string> svals;                  // STRING dictionary values (unpadded)
   uint64_t dict_hash = 0;
   std::vector<uint8_t> inv;                        // bitmap inverted index bytes (host)
+  std::vector<uint32_t> inv_off;                   // (card+1) byte offsets of the per-dictId roaring bitmaps
+  DevBuf inv_dev;                                  // device copy (expanded by pgx_roaring_expand); null if unusable
   // LDS value image (pgx_jit.cpp): the dictionary re-encoded so a whole column's values fit one workgroup's LDS
   int img_kind = IMG_NONE;
   int img_sh = 0;
@@ -443,9 +448,32 @@ void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool
     }
   }
   if (d.inv && d.inv_len) {
+    // <col>.bitmap.inv: (card+1) BE int offsets, then concatenated portable roaring bitmaps
+    // (segment/creator/impl/inv/HeapBitmapInvertedIndexCreator.java:74-81, BitmapInvertedIndexReader.java:91-117)
     const uint8_t* p = static_cast<const uint8_t*>(d.inv);
     c.inv.assign(p, p + d.inv_len);
     c.has_inverted = true;
+    if (d.inv_len < uint64_t(c.card + 1) * 4) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": inverted index short");
+    c.inv_off.resize(c.card + 1);
+    bool device_ok = true;
+    for (int i = 0; i <= c.card; ++i) {
+      c.inv_off[i] = be32(p + 4 * size_t(i));
+      if (c.inv_off[i] > d.inv_len || (i && c.inv_off[i] < c.inv_off[i - 1]))
+        fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": inverted index offsets out of order");
+      // The device expansion reads RoaringBitmap 0.5.10's portable no-run format (cookie 12346), all the reference
+      // writes (no runOptimize); anything else keeps this column on the dictId-bitset scan path.
+      if (i < c.card) {
+        const uint32_t o = c.inv_off[i];
+        if ((o & 1u) || uint64_t(o) + 8 > d.inv_len) device_ok = false;
+        else if ((uint32_t(p[o]) | uint32_t(p[o + 1]) << 8 | uint32_t(p[o + 2]) << 16 | uint32_t(p[o + 3]) << 24) != 12346u)
+          device_ok = false;
+      }
+    }
+    if (device_ok) {
+      c.inv_dev = DevBuf(ctx, d.inv_len + 16);
+      hip_check(hipMemcpy(c.inv_dev.p, p, d.inv_len, hipMemcpyHostToDevice), "inverted index H2D");
+      seg->device_bytes += d.inv_len;
+    }
   }
   if (c.is_sorted) c.has_inverted = true;  // ColumnDataSourceImpl: sorted columns report an inverted index
 }
@@ -671,6 +699,23 @@ struct ExecPlan {
   std::vector<int> gbits;
   int64_t host_entries = 0;
   int64_t total_raw = 0;
+  // bitmap inverted-index leaves expanded on device for the query kernels (a-7)
+  bool use_docmask = false;
+  std::vector<int> leaf_phys;                      // physical operator kind per leaf (FilterPlanNode choice)
+  struct RoarItem {
+    int seg, leaf;
+    bool neg;
+    size_t blob_off;
+    int nb, nchunks;
+    uint64_t mask_off;
+    const void* inv;
+  };
+  std::vector<RoarItem> roar;
+  std::vector<std::vector<int>> roar_index;        // [seg][leaf] -> index into roar or -1
+  uint64_t mask_words = 0;
+  const RDesc* rdesc_dev = nullptr;
+  int roar_maxchunks = 0;
+  uint32_t* masks_dev = nullptr;
   int n_proj = 0;
   int mode_ref = 0;
   uint64_t dense_slots = 0;
@@ -688,6 +733,11 @@ struct ExecPlan {
   };
   std::vector<JitGroup> jit;
 };
+
+bool jit_enabled() {
+  const char* e = std::getenv("PGX_JIT");
+  return !(e && e[0] == '0');
+}
 
 int qslot(ExecPlan& P, const std::string& name) {
   for (size_t i = 0; i < P.qcols.size(); ++i)
@@ -796,7 +846,21 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   if (!q.filter.empty()) {
     PNode root = build_tree(q, *segs[0]);
     emit(root, pop, parg, true, false, host_scan_leaves);
+    P.leaf_phys.assign(q.leaf_col.size(), PH_SCAN);
+    std::vector<const PNode*> todo{&root};
+    while (!todo.empty()) {
+      const PNode* x = todo.back();
+      todo.pop_back();
+      if (x->op == PGX_F_LEAF) P.leaf_phys[x->leaf] = x->phys;
+      for (const PNode& k : x->kids) todo.push_back(&k);
+    }
   }
+  P.use_docmask = jit_enabled() && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
+                                    K.group_mode == G_DENSE_GLOBAL) && K.num_qcols <= PGX_J_MAX_COLS;
+  P.roar.clear();
+  P.roar_index.assign(n, std::vector<int>(q.leaf_col.size(), -1));
+  P.mask_words = 0;
+  P.roar_maxchunks = 0;
   if (pop.size() > size_t(kMaxProg)) fail(PGX_ERR_UNSUPPORTED, "filter program too long");
   K.prog_len = int(pop.size());
   for (size_t i = 0; i < pop.size(); ++i) {
@@ -873,6 +937,22 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       } else {
         L.mode = (b.hi < b.lo) ? LEAF_NONE : LEAF_SCAN_INTERVAL;
       }
+      if (P.use_docmask && L.mode != LEAF_NONE && P.leaf_phys[l] == PH_BITMAP && col.inv_dev.p) {
+        // BitmapBasedFilterOperator (operator/filter/BitmapBasedFilterOperator.java:62-92): OR the roaring bitmaps of
+        // the matching dictIds; NEQ / NOT_IN OR the NON-matching ones and flip over the scanned doc range.
+        const bool neg = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
+        ExecPlan::RoarItem it{s, int(l), neg, P.blob32.size(), 0, int((int64_t(seg.total_docs) + 65535) >> 16),
+                              P.mask_words, col.inv_dev.p};
+        for (int id = 0; id < col.card; ++id)
+          if (matches(id) != neg) {
+            P.blob32.push_back(int32_t(col.inv_off[id]));
+            ++it.nb;
+          }
+        P.mask_words += uint64_t(it.nchunks) * 2048;
+        P.roar_maxchunks = std::max(P.roar_maxchunks, it.nchunks);
+        P.roar_index[s][l] = int(P.roar.size());
+        P.roar.push_back(it);
+      }
     }
   }
   K.total_tiles = tiles;
@@ -892,8 +972,8 @@ constexpr size_t kOutsBytes = 256;  // agg planes [0, 72), stats [128, 144), ove
 struct ExecBuffers {
   DevBuf arena;
   PinnedBuf host;
-  size_t off_ksegs = 0, off_jsegs = 0, off_outs = 0, size = 0;
-  DevBuf table, keys, key_state;
+  size_t off_ksegs = 0, off_jsegs = 0, off_rdesc = 0, off_outs = 0, size = 0;
+  DevBuf table, keys, key_state, masks;
   uint8_t* dev() const { return arena.as<uint8_t>(); }
 };
 
@@ -904,7 +984,8 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
   const size_t n = P.ksegs.size();
   B.off_ksegs = align_up(P.blob32.size() * 4, 256);
   B.off_jsegs = align_up(B.off_ksegs + n * sizeof(KSeg), 256);
-  B.off_outs = align_up(B.off_jsegs + n * sizeof(JSeg), 256);
+  B.off_rdesc = align_up(B.off_jsegs + n * sizeof(JSeg), 256);
+  B.off_outs = align_up(B.off_rdesc + P.roar.size() * sizeof(RDesc), 256);
   B.size = B.off_outs + kOutsBytes;
   B.arena = DevBuf(ctx, B.size);
   B.host = PinnedBuf(ctx, B.size);
@@ -922,6 +1003,23 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
   P.kq.agg_out = outs;
   P.kq.stats = outs + 16;
   P.kq.overflow = outs + 24;
+  // bitmap inverted-index expansion descriptors + the per-(segment, leaf) doc masks they fill
+  P.rdesc_dev = nullptr;
+  P.masks_dev = nullptr;
+  if (!P.roar.empty()) {
+    B.masks = DevBuf(ctx, P.mask_words * 4);
+    P.masks_dev = B.masks.as<uint32_t>();
+    RDesc* rd = reinterpret_cast<RDesc*>(B.host.bytes() + B.off_rdesc);
+    for (size_t i = 0; i < P.roar.size(); ++i) {
+      const auto& it = P.roar[i];
+      rd[i].mask = P.masks_dev + it.mask_off;
+      rd[i].inv = static_cast<const uint8_t*>(it.inv);
+      rd[i].offs = reinterpret_cast<const uint32_t*>(base + it.blob_off);
+      rd[i].nb = it.nb;
+      rd[i].nchunks = it.nchunks;
+    }
+    P.rdesc_dev = reinterpret_cast<const RDesc*>(B.dev() + B.off_rdesc);
+  }
 }
 
 void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, uint64_t dense_out_bytes) {
@@ -970,10 +1068,6 @@ void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st) {
 // Build the query-specialised launch groups (pgx_jit.cpp) for plans the generated kernels cover: aggregation-only
 // and dense group-by over at most PGX_J_MAX_COLS columns.  Hash group-by keeps the generic kernel.  PGX_JIT=0 forces
 // the generic kernel (A/B timing); both are HIP paths with identical accumulator encodings.
-bool jit_enabled() {
-  const char* e = std::getenv("PGX_JIT");
-  return !(e && e[0] == '0');
-}
 
 void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
   P.jit.clear();
@@ -998,7 +1092,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
   for (int s = 0; s < n; ++s) {
     const KSeg& S = P.ksegs[s];
     std::string sig;
-    for (int l = 0; l < nleaves; ++l) sig += char('a' + S.leaf[l].mode);
+    for (int l = 0; l < nleaves; ++l)
+      sig += P.roar_index[s][l] >= 0 ? (P.roar[P.roar_index[s][l]].neg ? 'F' : 'E') : char('a' + S.leaf[l].mode);
     sig += '|';
     for (int c = 0; c < nc; ++c) {
       const StagedColumn& col = segs[s]->col(P.qcols[c]);
@@ -1017,7 +1112,9 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     J.cols.resize(nc);
     std::vector<bool> dec = decode;
     for (int l = 0; l < nleaves; ++l)
-      if (S0.leaf[l].mode == LEAF_SCAN_INTERVAL || S0.leaf[l].mode == LEAF_SCAN_BITSET) dec[K.leaf_col[l]] = true;
+      if ((S0.leaf[l].mode == LEAF_SCAN_INTERVAL || S0.leaf[l].mode == LEAF_SCAN_BITSET) &&
+          P.roar_index[members[0]][l] < 0)
+        dec[K.leaf_col[l]] = true;
     int R = 8;
     for (int c = 0; c < nc; ++c) {
       JitCol& C = J.cols[c];
@@ -1063,7 +1160,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     J.T = lds <= 20 * 1024 ? 256 : (lds <= 40 * 1024 ? 512 : 1024);
     for (int l = 0; l < nleaves; ++l) {
       J.leaf_col.push_back(K.leaf_col[l]);
-      J.leaf_mode.push_back(S0.leaf[l].mode);
+      const int ri = P.roar_index[members[0]][l];
+      J.leaf_mode.push_back(ri >= 0 ? (P.roar[ri].neg ? LEAF_DOCMASK_NOT : LEAF_DOCMASK) : S0.leaf[l].mode);
     }
     for (int i = 0; i < K.prog_len; ++i) {
       J.prog_op.push_back(K.prog_op[i]);
@@ -1108,7 +1206,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       }
       for (int l = 0; l < nleaves; ++l) {
         const KLeaf& L = S.leaf[l];
-        js.lbits[l] = L.bitset;
+        const int ri = P.roar_index[s][l];
+        js.lbits[l] = ri >= 0 ? P.masks_dev + P.roar[ri].mask_off : L.bitset;
         js.lranges[l] = L.ranges;
         js.lnr[l] = L.nranges;
         js.llo[l] = uint32_t(L.lo);
@@ -1135,6 +1234,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
 
 void launch_scan(ExecPlan& P, hipStream_t st) {
   if (!P.jit.empty()) {
+    if (P.rdesc_dev)
+      hip_check(pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
     for (auto& G : P.jit) {
       if (!G.fn) continue;
       G.args.agg_out = P.kq.agg_out;
@@ -1350,17 +1451,25 @@ pgx_status pgx_ctx_create(const pgx_ctx_opts* opts, pgx_ctx** out) {
   });
 }
 
+// A context outlives its staged segments: pgx_ctx_destroy with segments still staged only drops the caller's
+// reference, and the last pgx_segment_release frees the device memory (a JVM finaliser may release a segment after
+// the context was closed).
+void ctx_unref(pgx_ctx* ctx) {
+  if (ctx->refs.fetch_sub(1) != 1) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->free_blocks) (void)hipFree(kv.second);
+  for (auto& kv : ctx->live) (void)hipFree(kv.first);
+  for (auto& kv : ctx->pinned_free) (void)hipHostFree(kv.second);
+  for (auto& kv : ctx->pinned_live) (void)hipHostFree(kv.first);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
 pgx_status pgx_ctx_destroy(pgx_ctx* ctx) {
   return guarded([&] {
     if (!ctx) return;
-    (void)hipSetDevice(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
-    for (auto& kv : ctx->free_blocks) (void)hipFree(kv.second);
-    for (auto& kv : ctx->live) (void)hipFree(kv.first);
-    for (auto& kv : ctx->pinned_free) (void)hipHostFree(kv.second);
-    for (auto& kv : ctx->pinned_live) (void)hipHostFree(kv.first);
-    (void)hipStreamDestroy(ctx->stream);
-    delete ctx;
+    ctx_unref(ctx);
   });
 }
 
@@ -1384,12 +1493,18 @@ pgx_status pgx_segment_stage(pgx_ctx* ctx, const pgx_segment_desc* d, pgx_segmen
       const uint8_t* p = static_cast<const uint8_t*>(d->star_tree);
       seg->star_tree.assign(p, p + d->star_tree_len);
     }
+    ctx->refs.fetch_add(1);  // released by pgx_segment_release
     *out = seg.release();
   });
 }
 
 pgx_status pgx_segment_release(pgx_segment* seg) {
-  return guarded([&] { delete seg; });
+  return guarded([&] {
+    if (!seg) return;
+    pgx_ctx* ctx = seg->ctx;
+    delete seg;
+    if (ctx) ctx_unref(ctx);
+  });
 }
 
 pgx_status pgx_segment_device_bytes(const pgx_segment* seg, uint64_t* out) {
@@ -1610,6 +1725,109 @@ pgx_status pgx_synth_column(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int3
                                ctx->stream),
               "synth launch");
     hip_check(hipStreamSynchronize(ctx->stream), "sync");
+  });
+}
+
+// ---- segment-creation helpers (benchmark data and fixtures; not on the query path) ----------------------------------
+
+// dictId(row) = splitmix64(seed ^ row * 0x9E3779B97F4A7C15) % card: the same sequence pgx_synth_column packs on device.
+pgx_status pgx_synth_dict_ids(uint64_t seed, int64_t n_rows, int32_t card, int32_t* out) {
+  return guarded([&] {
+    if (!out || n_rows < 0 || card < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    for (int64_t r = 0; r < n_rows; ++r) {
+      uint64_t x = seed ^ (static_cast<uint64_t>(r) * 0x9E3779B97F4A7C15ull);
+      x += 0x9E3779B97F4A7C15ull;
+      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+      x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+      x ^= x >> 31;
+      out[r] = static_cast<int32_t>(x % static_cast<uint64_t>(card));
+    }
+  });
+}
+
+// <col>.bitmap.inv of a column (segment/creator/impl/inv/HeapBitmapInvertedIndexCreator.java:42-81): (card+1) BE int
+// offsets, then per dictId the RoaringBitmap 0.5.10 portable serialisation of its doc ids (cookie 12346, no run
+// containers; array containers up to 4096 docs, bitmap containers above).  out == NULL (or cap too small) only
+// reports the size in *len.
+pgx_status pgx_inverted_index_build(const int32_t* ids, int64_t n, int32_t card, uint8_t* out, uint64_t cap,
+                                    uint64_t* len) {
+  return guarded([&] {
+    if (!ids || !len || n < 0 || card < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    // counting sort of doc ids by dictId
+    std::vector<int64_t> start(size_t(card) + 1, 0);
+    for (int64_t i = 0; i < n; ++i) {
+      if (ids[i] < 0 || ids[i] >= card) fail(PGX_ERR_INVALID_ARG, "dictId out of range");
+      ++start[size_t(ids[i]) + 1];
+    }
+    for (int32_t v = 0; v < card; ++v) start[v + 1] += start[v];
+    std::vector<int32_t> docs(static_cast<size_t>(n));
+    {
+      std::vector<int64_t> pos(start.begin(), start.end() - 1);
+      for (int64_t i = 0; i < n; ++i) docs[size_t(pos[ids[i]]++)] = int32_t(i);
+    }
+    // sizes
+    auto bitmap_bytes = [&](int32_t v, std::vector<std::pair<int, int>>* conts) {
+      uint64_t b = 8;
+      const int64_t a = start[v], e = start[v + 1];
+      int64_t i = a;
+      while (i < e) {
+        const int key = docs[size_t(i)] >> 16;
+        int64_t j = i;
+        while (j < e && (docs[size_t(j)] >> 16) == key) ++j;
+        const int c = int(j - i);
+        b += 8 + (c > 4096 ? 8192 : 2 * uint64_t(c));
+        if (conts) conts->push_back({key, c});
+        i = j;
+      }
+      return b;
+    };
+    uint64_t total = 4 * (uint64_t(card) + 1);
+    for (int32_t v = 0; v < card; ++v) total += bitmap_bytes(v, nullptr);
+    *len = total;
+    if (!out || cap < total) return;
+    if (total > 0x7FFFFFFFull) fail(PGX_ERR_UNSUPPORTED, "inverted index over 2 GiB");
+    auto put32be = [&](uint64_t o, uint32_t x) {
+      out[o] = uint8_t(x >> 24); out[o + 1] = uint8_t(x >> 16); out[o + 2] = uint8_t(x >> 8); out[o + 3] = uint8_t(x);
+    };
+    auto put32le = [&](uint64_t o, uint32_t x) { std::memcpy(out + o, &x, 4); };
+    auto put16le = [&](uint64_t o, uint16_t x) { std::memcpy(out + o, &x, 2); };
+    uint64_t o = 4 * (uint64_t(card) + 1);
+    std::vector<std::pair<int, int>> conts;
+    for (int32_t v = 0; v < card; ++v) {
+      put32be(4 * uint64_t(v), uint32_t(o));
+      conts.clear();
+      bitmap_bytes(v, &conts);
+      const uint64_t b0 = o;
+      const int nc = int(conts.size());
+      put32le(o, 12346u);
+      put32le(o + 4, uint32_t(nc));
+      uint64_t payload = 8 + 8 * uint64_t(nc);
+      for (int k = 0; k < nc; ++k) {
+        put16le(o + 8 + 4 * k, uint16_t(conts[k].first));
+        put16le(o + 8 + 4 * k + 2, uint16_t(conts[k].second - 1));
+        put32le(o + 8 + 4 * uint64_t(nc) + 4 * k, uint32_t(payload));
+        payload += conts[k].second > 4096 ? 8192 : 2 * uint64_t(conts[k].second);
+      }
+      uint64_t p = o + 8 + 8 * uint64_t(nc);
+      int64_t i = start[v];
+      for (int k = 0; k < nc; ++k) {
+        const int c = conts[k].second;
+        if (c > 4096) {
+          std::memset(out + p, 0, 8192);
+          for (int t = 0; t < c; ++t) {
+            const uint32_t lo = uint32_t(docs[size_t(i + t)]) & 0xFFFFu;
+            out[p + (lo >> 3)] |= uint8_t(1u << (lo & 7));
+          }
+          p += 8192;
+        } else {
+          for (int t = 0; t < c; ++t) put16le(p + 2 * uint64_t(t), uint16_t(uint32_t(docs[size_t(i + t)]) & 0xFFFFu));
+          p += 2 * uint64_t(c);
+        }
+        i += c;
+      }
+      o = b0 + (p - b0);
+    }
+    put32be(4 * uint64_t(card), uint32_t(o));
   });
 }
 

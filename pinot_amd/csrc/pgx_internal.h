@@ -20,6 +20,17 @@ enum LeafMode : int8_t {
   LEAF_SCAN_BITSET = 1,    // decode + bitset lookup
   LEAF_RANGES = 2,         // sorted doc ranges
   LEAF_NONE = 3,           // always false (empty binding)
+  LEAF_DOCMASK = 4,        // query kernels: bitmap inverted-index leaf expanded to a per-segment doc mask
+  LEAF_DOCMASK_NOT = 5,    // ... NEQ / NOT_IN: OR of the non-matching bitmaps, flipped (BitmapBasedFilterOperator)
+};
+
+// Bitmap inverted-index expansion (pgx_kernels.hip pgx_roaring_expand): one descriptor per (segment, leaf).
+struct RDesc {
+  uint32_t* mask;              // nchunks x 2048 words: bit (doc & 31) of word (doc >> 5)
+  const uint8_t* inv;          // device copy of <col>.bitmap.inv
+  const uint32_t* offs;        // byte offsets (into inv) of the roaring bitmaps to OR
+  int32_t nb;                  // number of bitmaps
+  int32_t nchunks;             // ceil(total_docs / 65536)
 };
 
 enum ProgOp : int8_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_STAT = 3, OP_TRUE = 4 };
@@ -122,7 +133,7 @@ struct JitShape {
   int T = 256;           // threads per workgroup
   int R = 8;             // rows per lane per sub-step (R * bits % 32 == 0 for every decoded column)
   std::vector<JitCol> cols;
-  std::vector<int> leaf_col, leaf_mode;
+  std::vector<int> leaf_col, leaf_mode;   // leaf_col -1: doc-range leaf with no column (star-tree node ranges)
   std::vector<int> prog_op, prog_arg;
   std::vector<int> agg_kind, agg_col, plane_op;
   int group_mode = G_NONE;

@@ -55,6 +55,7 @@ struct Emitter {
 };
 
 int dwords_per(const JitShape& s, int c) { return s.R * s.cols[c].bits / 32; }
+bool is_docmask(int mode) { return mode == LEAF_DOCMASK || mode == LEAF_DOCMASK_NOT; }
 
 std::string plane_atomic(int op, const std::string& ptr, const std::string& val) {
   switch (op) {
@@ -186,6 +187,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       case LEAF_SCAN_BITSET:
         e.ln("const PGX_G u32* __restrict__ bs", l, " = (const PGX_G u32*)S->lbits[", l, "];");
         break;
+      case LEAF_DOCMASK:
+      case LEAF_DOCMASK_NOT:
+        e.ln("const PGX_G u32* __restrict__ dm", l, " = (const PGX_G u32*)S->lbits[", l, "];");
+        break;
       case LEAF_RANGES:
         e.ln("const PGX_G int* __restrict__ rg", l, " = (const PGX_G int*)S->lranges[", l, "];");
         e.ln("const int nr", l, " = S->lnr[", l, "];");
@@ -259,6 +264,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         e.ln("if (full || r0 < nd) pgx_ld<", D, ">(f", c, " + (long long)(r0 / PR) * ", D, ", &", dst, c, "[", u * D,
              "]); else pgx_zero<", D, ">(&", dst, c, "[", u * D, "]);");
       }
+      for (int l = 0; l < nleaves; ++l)
+        if (is_docmask(s.leaf_mode[l]))
+          e.ln(dst, "q", l, "[", u, "] = (full || r0 < nd) ? dm", l, "[r0 >> 5] : 0u;");
       e.ind--;
       e.ln("}");
     }
@@ -267,6 +275,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   };
   for (int c = 0; c < ncols; ++c)
     if (s.cols[c].decode) e.ln("u32 n", c, "[", U * dwords_per(s, c), "];");
+  for (int l = 0; l < nleaves; ++l)
+    if (is_docmask(s.leaf_mode[l])) e.ln("u32 nq", l, "[", U, "];");
   emit_loads("t", "n");
   e.ln("for (long long tt = t; tt < t2; ++tt) {");
   e.ind = 3;
@@ -277,6 +287,12 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ln("#pragma unroll");
     e.ln("for (int i = 0; i < ", n, "; ++i) c", c, "[i] = n", c, "[i];");
   }
+  for (int l = 0; l < nleaves; ++l)
+    if (is_docmask(s.leaf_mode[l])) {
+      e.ln("u32 cq", l, "[", U, "];");
+      e.ln("#pragma unroll");
+      e.ln("for (int i = 0; i < ", U, "; ++i) cq", l, "[i] = nq", l, "[i];");
+    }
   e.ln("if (tt + 1 < t2) ");
   emit_loads("tt + 1", "n");
   e.ln("const int rb = (int)((tt - tile0) * (PT * 32));");
@@ -293,8 +309,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("u32 v", c, "[PR];");
       e.ln("pgx_unpack<", s.cols[c].bits, ", PR>(&c", c, "[", u * dwords_per(s, c), "], v", c, ");");
     }
-    for (int l = 0; l < nleaves; ++l)
+    for (int l = 0; l < nleaves; ++l) {
       if (s.leaf_mode[l] == LEAF_RANGES) e.ln("const u32 W", l, " = pgx_ranges_bits(rg", l, ", nr", l, ", cur", l, ", r0, PR);");
+      if (is_docmask(s.leaf_mode[l])) e.ln("const u32 W", l, " = cq", l, "[", u, "] >> (r0 & 31);");
+    }
     // per-aggregation sub-step partials
     if (!grouped)
       for (int a = 0; a < naggs; ++a) {
@@ -324,7 +342,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
             e.ln("const bool ", B, " = vj && ((bs", l, "[", v, " >> 5] >> (", v, " & 31u)) & 1u);");
             break;
           case LEAF_RANGES:
+          case LEAF_DOCMASK:
             e.ln("const bool ", B, " = vj && ((W", l, " >> j) & 1u);");
+            break;
+          case LEAF_DOCMASK_NOT:  // BitmapBasedFilterOperator NEQ / NOT_IN: flip of the OR of the non-matching bitmaps
+            e.ln("const bool ", B, " = vj && !((W", l, " >> j) & 1u);");
             break;
           default:
             e.ln("const bool ", B, " = false;");
@@ -654,6 +676,16 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.prog_op = {OP_LEAF, OP_STAT, OP_LEAF, OP_AND, OP_LEAF, OP_OR};
     s.prog_arg = {1, 0, 0, 2, 2, 2};
     s.cols[1].acc32 = false;
+    shapes.push_back(s);
+  }
+  {  // bitmap inverted-index leaves (doc masks), one of them negated, OR / AND with a scan leaf
+    JitShape s = base(10, 16, IMG_FOR16, 11);
+    s.cols[0].decode = true;
+    s.leaf_col = {0, 0, 0};
+    s.leaf_mode = {LEAF_DOCMASK, LEAF_DOCMASK_NOT, LEAF_SCAN_INTERVAL};
+    s.prog_op = {OP_LEAF, OP_LEAF, OP_OR, OP_LEAF, OP_AND};
+    s.prog_arg = {0, 1, 2, 2, 2};
+    s.R = 16;
     shapes.push_back(s);
   }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {

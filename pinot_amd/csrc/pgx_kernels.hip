@@ -508,6 +508,79 @@ __global__ void pgx_compact(const unsigned long long* table, uint64_t slots, int
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// a-7: bitmap inverted-index leaves.  The reference ORs the RoaringBitmap of every matching dictId
+// (operator/filter/BitmapBasedFilterOperator.java:62-92, segment/index/readers/BitmapInvertedIndexReader.java:91-117;
+// RoaringBitmap 0.5.10 portable format without run containers: cookie 12346, container count, (key, card-1) u16
+// pairs, u32 offsets, then array (<= 4096 u16) or bitmap (1024 u64) containers).  One workgroup expands one
+// 65536-doc chunk of one (segment, leaf): each lane binary-searches one bitmap's container keys for the chunk, then
+// the workgroup ORs the found containers into an 8 KiB LDS mask (array containers bit by bit with LDS atomics, bitmap
+// containers word by word) and writes the 2048 mask words to HBM with coalesced stores.  Roaring bytes are only
+// 2-byte aligned inside the inverted-index file, so multi-byte fields are read as u16 pairs.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rd16(const uint8_t* p) { return *reinterpret_cast<const uint16_t*>(p); }
+__device__ __forceinline__ uint32_t rd32(const uint8_t* p) { return rd16(p) | (rd16(p + 2) << 16); }
+
+constexpr int kRoarBatch = 256;
+
+__global__ void __launch_bounds__(256) pgx_roaring_expand(const RDesc* __restrict__ descs, int npairs, int maxchunks) {
+  const int pair = static_cast<int>(blockIdx.x / maxchunks);
+  const int chunk = static_cast<int>(blockIdx.x - static_cast<unsigned>(pair) * maxchunks);
+  if (pair >= npairs) return;
+  const RDesc D = descs[pair];
+  if (chunk >= D.nchunks) return;
+  __shared__ uint32_t m[2048];
+  __shared__ const uint8_t* cptr[kRoarBatch];
+  __shared__ int ccard[kRoarBatch];
+  __shared__ int ncont;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < 2048; i += 256) m[i] = 0u;
+  for (int b0 = 0; b0 < D.nb; b0 += kRoarBatch) {
+    if (tid == 0) ncont = 0;
+    __syncthreads();
+    const int b = b0 + tid;
+    if (b < D.nb) {
+      const uint8_t* base = D.inv + D.offs[b];
+      const int n = static_cast<int>(rd32(base + 4));
+      int lo = 0, hi = n - 1, found = -1;
+      while (lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const int k = static_cast<int>(rd16(base + 8 + 4 * mid));
+        if (k == chunk) { found = mid; break; }
+        if (k < chunk) lo = mid + 1; else hi = mid - 1;
+      }
+      if (found >= 0) {
+        const int card = static_cast<int>(rd16(base + 8 + 4 * found + 2)) + 1;
+        const uint32_t off = rd32(base + 8 + 4 * n + 4 * found);
+        const int slot = atomicAdd(&ncont, 1);
+        cptr[slot] = base + off;
+        ccard[slot] = card;
+      }
+    }
+    __syncthreads();
+    const int nc = ncont;
+    for (int k = 0; k < nc; ++k) {
+      const uint8_t* c = cptr[k];
+      const int card = ccard[k];
+      if (card > 4096) {  // bitmap container: 1024 x u64 little-endian == 2048 x u32, bit j of word w = doc 32w + j
+        for (int w = tid; w < 2048; w += 256) {
+          const uint32_t x = rd32(c + 4 * w);
+          if (x) atomicOr(&m[w], x);
+        }
+      } else {            // array container: sorted u16 low bits
+        for (int i = tid; i < card; i += 256) {
+          const uint32_t v = rd16(c + 2 * i);
+          atomicOr(&m[v >> 5], 1u << (v & 31u));
+        }
+      }
+    }
+    __syncthreads();
+  }
+  uint32_t* out = D.mask + static_cast<size_t>(chunk) * 2048;
+  for (int i = tid; i < 2048; i += 256) out[i] = m[i];
+}
+
 // ---------------------------------------------------------------------------------------------
 // Synthetic forward-index generator (benchmarks): dictId(row) = splitmix64(seed ^ row*golden) % card, packed
 // MSB-first big-endian.  One thread writes one 32-bit big-endian word = the 32 rows' bits that fall in it.
@@ -610,5 +683,14 @@ extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int 
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(pgx::pgx_synth_kernel, dim3(grid), dim3(256), 0, stream, out_words, n_rows, bits, card, seed,
                      n_words);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream) {
+  if (npairs <= 0 || maxchunks <= 0) return hipSuccess;
+  const long long blocks = static_cast<long long>(npairs) * maxchunks;
+  if (blocks > 0x7FFFFFFFll) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pgx::pgx_roaring_expand, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, descs, npairs,
+                     maxchunks);
   return hipGetLastError();
 }

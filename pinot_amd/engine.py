@@ -196,7 +196,11 @@ class IndexSegment:
             dict_dev.append(p)
             d.dict = p
             d.dict_len = len(c.dict_bytes)
-        sd = N.SegmentDesc()
+            if c.inv_bytes is not None:  # inverted index bytes are host memory in either mode (pgx.h)
+                ib = C.create_string_buffer(bytes(c.inv_bytes), len(c.inv_bytes))
+                keep.append(ib)
+                d.inv = C.cast(ib, C.c_void_p)
+                d.inv_len = len(c.inv_bytes)
         sd.name = seg.name.encode()
         sd.total_docs = seg.total_docs
         sd.total_raw_docs = seg.total_raw_docs
@@ -293,6 +297,19 @@ def resolve_leaf(col: _ColInfo, leaf: dict):
     words = np.packbits(np.pad(m, (0, (-card) % 32)).reshape(-1, 32)[:, ::-1], axis=1,
                         bitorder="big").view(">u4").astype(np.uint32).reshape(-1)
     return (0, -1, np.ascontiguousarray(words))
+
+
+def leaf_matching_ids(col: _ColInfo, leaf: dict) -> np.ndarray:
+    """Boolean mask over dictIds of the ids the leaf's evaluator matches (PredicateEvaluator.getMatchingDictionaryIds)."""
+    lo, hi, words = resolve_leaf(col, leaf)
+    card = col.meta.cardinality
+    if words is None:
+        m = np.zeros(card, dtype=bool)
+        if hi >= lo:
+            m[lo:hi + 1] = True
+        return m
+    bits = np.unpackbits(words.astype(">u4").view(np.uint8), bitorder="big").reshape(-1, 32)[:, ::-1].reshape(-1)
+    return bits[:card].astype(bool)
 
 
 def _flatten_filter(tree):

@@ -73,6 +73,9 @@ _lib = None
 EXPORTS = {
     "pgx_jit_compile_check": (C.c_int, [C.c_char_p, C.c_char_p, C.c_ulong]),
     "pgx_jit_selftest": (C.c_int, [C.POINTER(C.c_int), C.c_char_p, C.c_ulong]),
+    "pgx_synth_dict_ids": (C.c_int, [C.c_uint64, C.c_int64, C.c_int32, C.c_void_p]),
+    "pgx_inverted_index_build": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_uint64,
+                                           C.POINTER(C.c_uint64)]),
     "pgx_last_error": (C.c_char_p, []),
     "pgx_abi_version": (C.c_int32, []),
     "pgx_ctx_create": (C.c_int, [C.POINTER(CtxOpts), C.POINTER(C.c_void_p)]),

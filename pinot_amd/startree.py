@@ -1,0 +1,243 @@
+"""Star-tree index builder (segment creation side of SURVEY 8a row a-18), writing the reference's OFF_HEAP format.
+
+Restates core/startree/OffHeapStarTreeBuilder.java (paths relative to pinot-core/src/main/java/com/linkedin/pinot/):
+  * default split order = dimensions by cardinality, descending, stable (computeDefaultSplitOrder, :535-555);
+  * raw records sorted by the split order then the remaining dimensions (getSortOrder, :585-601);
+  * constructStarTree (:620-711): per level, one child per value of the split dimension; a child whose range holds
+    more than maxLeafRecords docs is split further; then a STAR child whose docs are the unique combinations of the
+    range with the split dimension set to ALL (uniqueCombinations, :724-800: metrics summed), split further when
+    rowsAdded >= maxLeafRecords;
+  * createAggDocForAllNodes (:365-410): post-order, every node gets one aggregated doc (sum over its non-star
+    children, or over its leaf range), dimension values = the node's path, ALL elsewhere;
+and core/startree/StarTreeSerDe.java:183-328 for the OFF_HEAP bytes: header (magic, version, header size, dimension
+name map, node count) then 7 x int32 per node in BFS order, children sorted by value (ALL = -1 first), native (LE)
+byte order.
+
+One deliberate difference: the reference builder sorts by its own first-seen value ids and re-maps the tree to segment
+dictIds afterwards (segment/creator/impl/SegmentIndexCreationDriverImpl.java:291-347); here records are sorted by
+segment dictIds directly.  That changes the order of docs inside a node's range, never which docs a node covers.
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+ALL = -1
+MAGIC = 0xBADDA55B00DAD00D
+VERSION = 1
+DEFAULT_MAX_LEAF_RECORDS = 100000  # common/data/StarTreeIndexSpec.java:25-26
+INT_DEFAULT_NULL = -(1 << 31)      # FieldSpec default null for INT dimensions = the star value (:210-225)
+
+
+@dataclass
+class Node:
+    dim: int
+    value: int
+    level: int
+    start: int = -1
+    end: int = -1
+    agg: int = -1
+    children: Optional[Dict[int, "Node"]] = None
+    path: Dict[int, int] = field(default_factory=dict)
+
+
+class _Table:
+    """Growable record table: dims int32 (ALL = -1 for star), metrics int64."""
+
+    def __init__(self, dims: np.ndarray, mets: np.ndarray):
+        self.dims = [dims]
+        self.mets = [mets]
+        self.n = len(dims)
+        self._cd = None
+
+    def append(self, d: np.ndarray, m: np.ndarray) -> int:
+        start = self.n
+        self.dims.append(d)
+        self.mets.append(m)
+        self.n += len(d)
+        self._cd = None
+        return start
+
+    def compact(self):
+        if len(self.dims) > 1:
+            self.dims = [np.concatenate(self.dims)]
+            self.mets = [np.concatenate(self.mets)]
+
+    def rows(self, a, b):
+        self.compact()
+        return self.dims[0][a:b], self.mets[0][a:b]
+
+    def set_rows(self, a, d, m):
+        self.compact()
+        self.dims[0][a:a + len(d)] = d
+        self.mets[0][a:a + len(m)] = m
+
+
+def _lexsort(d: np.ndarray, order: Sequence[int]) -> np.ndarray:
+    return np.lexsort(tuple(d[:, k] for k in reversed(order))) if len(d) else np.zeros(0, dtype=np.int64)
+
+
+def build(dim_ids: np.ndarray, metrics: np.ndarray, cards: Sequence[int], max_leaf_records: int = DEFAULT_MAX_LEAF_RECORDS,
+          split_order: Optional[Sequence[int]] = None):
+    """dim_ids: (N, D) int dictIds (no star values); metrics: (N, M) int64.
+    Returns (tree_root, all_dims (T, D) with ALL=-1 for star, all_metrics (T, M), split_order, num_raw)."""
+    n, ndim = dim_ids.shape
+    if split_order is None:
+        split_order = sorted(range(ndim), key=lambda k: -cards[k])  # stable: ties keep schema order
+    sort_order = list(split_order) + [k for k in range(ndim) if k not in split_order]
+    perm = _lexsort(dim_ids, sort_order)
+    tab = _Table(np.ascontiguousarray(dim_ids[perm]).astype(np.int32), np.ascontiguousarray(metrics[perm]).astype(np.int64))
+    root = Node(ALL, ALL, 0)
+
+    def unique_combinations(a, b, split_dim):
+        d, m = tab.rows(a, b)
+        d = d.copy()
+        d[:, split_dim] = ALL
+        o = _lexsort(d, sort_order)
+        d, m = d[o], m[o]
+        if len(d) == 0:
+            return d, m
+        brk = np.ones(len(d), dtype=bool)
+        brk[1:] = np.any(d[1:] != d[:-1], axis=1)
+        starts = np.nonzero(brk)[0]
+        return d[starts], np.add.reduceat(m, starts, axis=0)
+
+    def construct(node: Node, a: int, b: int, level: int) -> int:
+        if level == len(split_order):
+            return 0
+        sd = split_order[level]
+        d, _ = tab.rows(a, b)
+        col = d[:, sd]
+        vals, first = np.unique(col, return_index=True)  # range is sorted by the sort order: groups are contiguous
+        bounds = list(first) + [len(col)]
+        node.children = {}
+        added = 0
+        for i, v in enumerate(vals.tolist()):
+            child = Node(sd, int(v), node.level + 1, path=dict(node.path, **{sd: int(v)}))
+            node.children[int(v)] = child
+            ca, cb = a + int(bounds[i]), a + int(bounds[i + 1])
+            cdocs = 0
+            if cb - ca > max_leaf_records:
+                cdocs = construct(child, ca, cb, level + 1)
+                added += cdocs
+            if cdocs == 0:
+                child.start, child.end = ca, cb
+        star = Node(sd, ALL, node.level + 1, path=dict(node.path))
+        node.children[ALL] = star
+        ud, um = unique_combinations(a, b, sd)
+        so = tab.append(ud, um)
+        rows_added = len(ud)
+        added += rows_added
+        cdocs = 0
+        if rows_added >= max_leaf_records:
+            cdocs = construct(star, so, so + rows_added, level + 1)
+            added += cdocs
+        if cdocs == 0:
+            star.start, star.end = so, so + rows_added
+        return added
+
+    construct(root, 0, n, 0)
+
+    def agg_docs(node: Node) -> np.ndarray:
+        if node.children is None:
+            _, m = tab.rows(node.start, node.end)
+            acc = m.sum(axis=0)
+        else:
+            acc = None
+            for v, child in node.children.items():
+                cm = agg_docs(child)
+                if v == ALL:
+                    continue  # the star child does not feed its parent's aggregate
+                acc = cm.copy() if acc is None else acc + cm
+        dims = np.full((1, ndim), ALL, dtype=np.int32)
+        for k, v in node.path.items():
+            dims[0, k] = v
+        node.agg = tab.append(dims, acc.reshape(1, -1).astype(np.int64))
+        return acc
+
+    agg_docs(root)
+    tab.compact()
+    return root, tab.dims[0], tab.mets[0], list(split_order), n
+
+
+def serialize(root: Node, dim_names: Sequence[str]) -> bytes:
+    """StarTreeSerDe.writeTreeOffHeapFormat: header + BFS nodes (7 x int32, native LE)."""
+    nodes = []
+    q = [root]
+    while q:
+        nodes.append(q.pop(0))
+        ch = sorted((nodes[-1].children or {}).values(), key=lambda c: c.value)
+        q.extend(ch)
+    index = {id(x): i for i, x in enumerate(nodes)}
+    names = b""
+    for i, nm in enumerate(dim_names):
+        e = nm.encode("utf-8")
+        names += struct.pack("<ii", i, len(e)) + e
+    header_size = 8 + 4 + 4 + 4 + len(names) + 4
+    out = [struct.pack("<QiIi", MAGIC, VERSION, header_size, len(dim_names)), names, struct.pack("<i", len(nodes))]
+    for x in nodes:
+        ch = sorted((x.children or {}).values(), key=lambda c: c.value)
+        cs = index[id(ch[0])] if ch else -1
+        ce = index[id(ch[-1])] if ch else -1
+        out.append(struct.pack("<7i", x.dim, x.value, x.start, x.end, x.agg, cs, ce))
+    return b"".join(out)
+
+
+def parse(buf: bytes):
+    """StarTreeOffHeap.readHeader (core/startree/StarTreeOffHeap.java:95-150) -> (dim names by index, nodes array)."""
+    magic, version, header_size, nd = struct.unpack_from("<QiIi", buf, 0)
+    if magic != MAGIC:
+        raise ValueError("not an OFF_HEAP star tree")
+    pos = 20
+    names = {}
+    for _ in range(nd):
+        i, ln = struct.unpack_from("<ii", buf, pos)
+        names[i] = buf[pos + 8:pos + 8 + ln].decode("utf-8")
+        pos += 8 + ln
+    (nn,) = struct.unpack_from("<i", buf, pos)
+    pos += 4
+    nodes = np.frombuffer(buf, dtype="<i4", count=7 * nn, offset=pos).reshape(nn, 7)
+    return names, nodes
+
+
+def make_star_tree_segment(name: str, dims: Dict[str, np.ndarray], metrics: Dict[str, np.ndarray],
+                           max_leaf_records: int = DEFAULT_MAX_LEAF_RECORDS, inverted: Sequence[str] = ()):
+    """Build a v1 star-tree segment from raw INT dimension and metric values (SegmentIndexCreationDriverImpl.buildStarTree,
+    :193-289): docs = raw docs in star-tree order, then the aggregated docs; star dimension values are the INT default
+    null (Integer.MIN_VALUE), which therefore sits in every dimension dictionary."""
+    from .segment import make_column, SegmentData
+    dnames = list(dims)
+    mnames = list(metrics)
+    dicts, ids = [], []
+    for k in dnames:
+        v = np.asarray(dims[k], dtype=np.int64)
+        dv = np.unique(np.concatenate([v, [INT_DEFAULT_NULL]]))
+        dicts.append(dv)
+        ids.append(np.searchsorted(dv, v))
+    dim_ids = np.stack(ids, axis=1)
+    mets = np.stack([np.asarray(metrics[k], dtype=np.int64) for k in mnames], axis=1)
+    cards = [len(np.unique(dim_ids[:, i])) for i in range(len(dnames))]
+    root, all_d, all_m, order, nraw = build(dim_ids, mets, cards, max_leaf_records)
+    total = len(all_d)
+    cols = []
+    for i, k in enumerate(dnames):
+        col_ids = all_d[:, i].astype(np.int64)
+        col_ids[col_ids == ALL] = 0  # dictId of Integer.MIN_VALUE (smallest value)
+        c = make_column(k, None, "INT", "DIMENSION", inverted=k in inverted, dictionary=dicts[i], dict_ids=col_ids)
+        c.total_raw_docs = nraw
+        cols.append(c)
+    for j, k in enumerate(mnames):
+        mv = all_m[:, j]
+        md, mid = np.unique(mv, return_inverse=True)
+        c = make_column(k, None, "INT" if md.max(initial=0) < (1 << 31) else "LONG", "METRIC", dictionary=md,
+                        dict_ids=mid)
+        c.total_raw_docs = nraw
+        cols.append(c)
+    seg = SegmentData(name, total, nraw, {c.name: c for c in cols})
+    seg.star_tree = serialize(root, dnames)
+    seg.metadata["startree.split.order"] = ",".join(dnames[k] for k in order)
+    seg.metadata["startree.maxLeafRecords"] = str(max_leaf_records)
+    return seg

@@ -11,6 +11,7 @@ baseline and for full-size spot checks.  Dictionaries are small and built on the
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import Dict, List
 
@@ -50,6 +51,7 @@ class ColSpec:
     name: str
     card: int
     dict_kind: str = "ids"
+    inverted: bool = False  # build <col>.bitmap.inv (roaring) for the segment, like a Pinot invertedIndexColumns entry
 
     @property
     def bits(self):
@@ -76,8 +78,8 @@ WORKLOADS: Dict[str, Workload] = {
     "c5": Workload("c5", "BASELINE configs[4]: 4096 x 2M rows sharded over the GPUs, (f1 IN 32 ids OR f2=7) AND "
                    "f3<>3, group by gk (card 1000), sum(m)",
                    4096, 2_000_000,
-                   [ColSpec("f1", 1000), ColSpec("f2", 100), ColSpec("f3", 10), ColSpec("gk", 1000),
-                    ColSpec("m", 65536, "metric")],
+                   [ColSpec("f1", 1000, inverted=True), ColSpec("f2", 100, inverted=True),
+                    ColSpec("f3", 10, inverted=True), ColSpec("gk", 1000), ColSpec("m", 65536, "metric")],
                    "SELECT SUM(m) FROM T WHERE (f1 IN (%s) OR f2 = 7) AND f3 <> 3 GROUP BY gk TOP 10"
                    % ",".join(str(v) for v in range(3, 1000, 31)[:32]), 5, "strong"),
 }
@@ -99,8 +101,10 @@ class DeviceSegments:
         self.seg_ids = list(seg_ids)
         self.buffers = []
         self.segments = []
+        self.inv_offsets = {}
         dicts = {c.name: make_dictionary(c.dict_kind, c.card) for c in wl.columns}
         L = N.lib()
+        inv = self._inverted_indexes()
         for s in self.seg_ids:
             cols = []
             fwd_dev = {}
@@ -113,20 +117,59 @@ class DeviceSegments:
                                            column_seed(wl.seed, s, ci)))
                 fwd_dev[c.name] = (p.value, nbytes)
                 dict_bytes = dicts[c.name].astype(">i4").tobytes()
-                cols.append(Column(c.name, "INT", "DIMENSION", c.card, c.bits, self.rows, self.rows, False, False,
-                                   dict_bytes, 4, None, None, None))
+                inv_bytes = inv.pop((s, ci), None)
+                if inv_bytes is not None:
+                    self.inv_offsets[(s, c.name)] = np.frombuffer(inv_bytes, dtype=">u4", count=c.card + 1).astype(
+                        np.int64)
+                cols.append(Column(c.name, "INT", "DIMENSION", c.card, c.bits, self.rows, self.rows, False,
+                                   inv_bytes is not None, dict_bytes, 4, None, None, inv_bytes))
             seg = SegmentData("%s_%d" % (wl.name, s), self.rows, self.rows, {c.name: c for c in cols})
             self.segments.append(IndexSegment.from_device(ctx, seg, fwd_dev))
 
-    def algorithmic_bytes(self, used_columns: List[str], dict_columns: List[str]) -> int:
-        """per segment, ceil(N*b/8) per distinct column read + card*width per dictionary used."""
+    def _inverted_indexes(self):
+        """Roaring inverted indexes of the workload's inverted columns, built on host threads from the same dictIds
+        the device generator packs (pgx_synth_dict_ids + pgx_inverted_index_build, both release the GIL)."""
+        from concurrent.futures import ThreadPoolExecutor
+        jobs = [(s, ci, c) for s in self.seg_ids for ci, c in enumerate(self.wl.columns) if c.inverted]
+        if not jobs:
+            return {}
+        L = N.lib()
+
+        def build(job):
+            s, ci, c = job
+            ids = np.empty(self.rows, dtype=np.int32)
+            N.check(L.pgx_synth_dict_ids(column_seed(self.wl.seed, s, ci), self.rows, c.card, ids.ctypes.data))
+            ln = C.c_uint64()
+            N.check(L.pgx_inverted_index_build(ids.ctypes.data, self.rows, c.card, None, 0, C.byref(ln)))
+            buf = bytearray(ln.value)
+            out = (C.c_uint8 * ln.value).from_buffer(buf)
+            N.check(L.pgx_inverted_index_build(ids.ctypes.data, self.rows, c.card, out, ln.value, C.byref(ln)))
+            del out
+            return (s, ci), bytes(buf)
+
+        with ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 1)) as ex:
+            return dict(ex.map(build, jobs))
+
+    def is_inverted(self, name: str) -> bool:
+        return any(c.name == name and c.inverted for c in self.wl.columns)
+
+    def algorithmic_bytes(self, used_columns: List[str], dict_columns: List[str], bitmap_leaves=()) -> int:
+        """per segment, ceil(N*b/8) per distinct column read + card*width per dictionary used + the
+        serialized bytes of every roaring bitmap a bitmap-index leaf reads (NEQ / NOT_IN read the non-matching ones)."""
         total = 0
-        for _ in self.segments:
+        for s in self.seg_ids:
             for c in self.wl.columns:
                 if c.name in used_columns:
                     total += (self.rows * c.bits + 7) // 8
                 if c.name in dict_columns:
                     total += c.card * 4
+            for leaf, ids in bitmap_leaves:
+                off = self.inv_offsets[(s, leaf["column"])]
+                sel = np.zeros(len(off) - 1, dtype=bool)
+                sel[ids] = True
+                if leaf["op"] in ("NEQ", "NOT_IN"):
+                    sel = ~sel
+                total += int((off[1:] - off[:-1])[sel].sum())
         return total
 
     def free(self):
