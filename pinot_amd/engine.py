@@ -201,6 +201,7 @@ class IndexSegment:
                 keep.append(ib)
                 d.inv = C.cast(ib, C.c_void_p)
                 d.inv_len = len(c.inv_bytes)
+        sd = N.SegmentDesc()
         sd.name = seg.name.encode()
         sd.total_docs = seg.total_docs
         sd.total_raw_docs = seg.total_raw_docs
