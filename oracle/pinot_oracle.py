@@ -1070,3 +1070,86 @@ def combine_group_by(parts: List[dict], q: dict) -> dict:
         trimmed.append(dict(items))
     stats = [sum(p["stats"][i] or 0 for p in parts) for i in range(4)]
     return {"merged": merged, "trimmed": trimmed, "stats": stats, "trim_threshold": threshold, "trim_size": size}
+
+
+# ------------------------------------------------------------------------------------------------
+# a-18: star-tree traversal (test oracle)
+# ------------------------------------------------------------------------------------------------
+def parse_star_tree_off_heap(buf: bytes):
+    """StarTreeOffHeap.readHeader (core/startree/StarTreeOffHeap.java:95-150): dimension names by index and the node
+    table (7 x int32 per node, native LE: dimName, dimValue, startDoc, endDoc (exclusive), aggDocId, childStart,
+    childEnd)."""
+    import struct
+    magic, _version, _hsize, nd = struct.unpack_from("<QiIi", buf, 0)
+    assert magic == 0xBADDA55B00DAD00D
+    pos, names = 20, {}
+    for _ in range(nd):
+        i, ln = struct.unpack_from("<ii", buf, pos)
+        names[i] = buf[pos + 8:pos + 8 + ln].decode("utf-8")
+        pos += 8 + ln
+    (nn,) = struct.unpack_from("<i", buf, pos)
+    nodes = np.frombuffer(buf, dtype="<i4", count=7 * nn, offset=pos + 4).reshape(nn, 7).astype(np.int64)
+    return names, nodes
+
+
+def star_tree_docs(seg: OSegment, tree_bytes: bytes, q: dict, num_raw: int) -> np.ndarray:
+    """Doc ids StarTreeIndexOperator selects (operator/filter/StarTreeIndexOperator.java:134-478): BFS that follows the
+    matching children of predicate columns (getMatchingDictionaryIds + getChildForDimensionValue), every non-star child
+    of group-by columns (or when no star child exists) and the star child otherwise; matched entries contribute their
+    aggregated doc, their range, or their range filtered by the remaining predicates."""
+    from collections import deque
+    names, nodes = parse_star_tree_off_heap(tree_bytes)
+    tree = q.get("filter")
+    leaves = [] if tree is None else ([tree] if tree["op"] not in ("AND", "OR") else tree["children"])
+    preds = {lf["column"]: make_evaluator(seg.columns[lf["column"]], lf) for lf in leaves}
+    if any(ev.always_false for ev in preds.values()):
+        return np.zeros(0, dtype=np.int64)
+    gb = set(q["group_by"]["columns"]) if q.get("group_by") else set()
+    queue = deque([(0, frozenset(preds), frozenset(gb))])
+    matched = []
+    while queue:
+        node, rp, rg = queue.popleft()
+        _, _, st, en, agg, cs, ce = nodes[node]
+        if cs == -1 or (not rp and not rg and agg >= num_raw):
+            matched.append((node, rp, rg))
+            continue
+        col = names[int(nodes[cs][0])]
+        children = range(int(cs), int(ce) + 1)
+        if col in preds:
+            nrp, nrg = rp - {col}, rg - {col}
+            by_value = {int(nodes[c][1]): c for c in children}
+            for did in preds[col].matching_ids:
+                if int(did) in by_value:
+                    queue.append((by_value[int(did)], nrp, nrg))
+        elif col in gb or int(nodes[cs][1]) != -1:
+            real = [c for c in children if int(nodes[c][1]) != -1]
+            nrg = rg - {col} if real else rg
+            for c in real:
+                queue.append((c, rp, nrg))
+        else:
+            queue.append((int(cs), rp, rg))
+    out = []
+    for node, rp, rg in matched:
+        _, _, st, en, agg, _, _ = nodes[node]
+        if not rp:
+            out.append(np.array([agg]) if (agg >= num_raw and not rg) else np.arange(st, en))
+        else:
+            r = np.arange(st, en)
+            keep = np.ones(len(r), dtype=bool)
+            for c in rp:
+                keep &= preds[c].match[seg.columns[c].dict_ids[r]]
+            out.append(r[keep])
+    return np.sort(np.concatenate(out)).astype(np.int64) if out else np.zeros(0, dtype=np.int64)
+
+
+def sum_by_group(seg: OSegment, docs: np.ndarray, metrics: Sequence[str], group_cols: Sequence[str]) -> dict:
+    """BaseSumStarTreeIndexTest.computeSum (pinot-core/src/test/.../startree/BaseSumStarTreeIndexTest.java:145-195):
+    per group key (dictionary values joined), the double sums of the metric columns over the given docs."""
+    res = {}
+    for d in docs.tolist():
+        key = "\t".join(seg.columns[g].string_of(int(seg.columns[g].dict_ids[d])) for g in group_cols)
+        acc = res.setdefault(key, [0.0] * len(metrics))
+        for i, m in enumerate(metrics):
+            c = seg.columns[m]
+            acc[i] += float(c.dictionary[c.dict_ids[d]])
+    return res

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <limits>
 #include <map>
 #include <memory>
@@ -253,6 +254,12 @@ struct pgx_segment {
   std::vector<StagedColumn> cols;
   std::unordered_map<std::string, int> by_name;
   std::vector<uint8_t> star_tree;
+  // OFF_HEAP star tree (core/startree/StarTreeOffHeap.java:95-150, StarTreeIndexNodeOffHeap.java): BFS nodes of
+  // {dimName, dimValue, startDoc, endDoc (exclusive), aggDocId, childStart, childEnd}, children sorted by value.
+  struct StarNode { int32_t dim, value, start, end, agg, cbeg, cend; };
+  bool st_ok = false;
+  std::vector<StarNode> st_nodes;
+  std::vector<std::string> st_dim_name;          // dimension index -> column name
   uint64_t device_bytes = 0;
 
   const StagedColumn& col(const std::string& n) const {
@@ -328,6 +335,44 @@ void build_value_image(pgx_ctx* ctx, pgx_segment* seg, StagedColumn& c) {
   c.img_owned = DevBuf(ctx, img.size() * 4);
   hip_check(hipMemcpy(c.img_owned.p, img.data(), img.size() * 4, hipMemcpyHostToDevice), "image H2D");
   seg->device_bytes += img.size() * 4;
+}
+
+// StarTreeSerDe.writeTreeOffHeapFormat (core/startree/StarTreeSerDe.java:183-328), native (LE) byte order: u64 magic,
+// i32 version, i32 header size, i32 #dims, #dims x {i32 index, i32 len, bytes}, i32 #nodes, #nodes x 7 x i32.
+// Other star-tree formats (the Java-serialised ON_HEAP tree) leave st_ok false: queries then scan the raw docs.
+void parse_star_tree(pgx_segment& seg) {
+  const std::vector<uint8_t>& b = seg.star_tree;
+  auto rd32 = [&](size_t o) {
+    if (o + 4 > b.size()) fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": star tree truncated");
+    int32_t x;
+    std::memcpy(&x, &b[o], 4);
+    return x;
+  };
+  if (b.size() < 24) return;
+  uint64_t magic;
+  std::memcpy(&magic, b.data(), 8);
+  if (magic != 0xBADDA55B00DAD00Dull) return;
+  size_t o = 16;
+  const int nd = rd32(o);
+  o += 4;
+  if (nd < 0 || nd > 4096) fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": bad star tree header");
+  seg.st_dim_name.assign(nd, "");
+  for (int i = 0; i < nd; ++i) {
+    const int idx = rd32(o), len = rd32(o + 4);
+    if (idx < 0 || idx >= nd || len < 0 || o + 8 + size_t(len) > b.size())
+      fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": bad star tree dimension map");
+    seg.st_dim_name[idx].assign(reinterpret_cast<const char*>(&b[o + 8]), size_t(len));
+    o += 8 + size_t(len);
+  }
+  const int nn = rd32(o);
+  o += 4;
+  if (nn < 1 || o + size_t(nn) * 28 > b.size()) fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": bad star tree");
+  seg.st_nodes.resize(nn);
+  std::memcpy(seg.st_nodes.data(), &b[o], size_t(nn) * 28);
+  for (const auto& x : seg.st_nodes)
+    if ((x.cbeg != -1 && (x.cbeg < 1 || x.cend < x.cbeg || x.cend >= nn)) || x.dim >= nd)
+      fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": star tree node out of range");
+  seg.st_ok = true;
 }
 
 void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c) {
@@ -712,6 +757,14 @@ struct ExecPlan {
   };
   std::vector<RoarItem> roar;
   std::vector<std::vector<int>> roar_index;        // [seg][leaf] -> index into roar or -1
+  std::vector<std::vector<const StagedColumn*>> segcols;  // [seg][query column slot]
+  // star-tree segments (a-18): a per-segment filter program over the query's leaves plus doc-range leaves
+  struct StarPlan {
+    bool on = false;
+    std::vector<int> op, arg;                      // postfix program (OP_*)
+    std::vector<std::pair<size_t, int>> ranges;    // extra range leaves: (blob offset, number of [a,b] pairs)
+  };
+  std::vector<StarPlan> star;
   uint64_t mask_words = 0;
   const RDesc* rdesc_dev = nullptr;
   int roar_maxchunks = 0;
@@ -745,6 +798,159 @@ int qslot(ExecPlan& P, const std::string& name) {
   if (P.qcols.size() >= size_t(kMaxQCols)) fail(PGX_ERR_UNSUPPORTED, "query touches too many columns");
   P.qcols.push_back(name);
   return int(P.qcols.size() - 1);
+}
+
+// RequestUtils.isFitForStarTreeIndex (pinot-common/.../common/utils/request/RequestUtils.java:128-220): aggregations
+// only SUM, filter a single predicate or an AND of predicates on distinct star-tree dimensions.
+bool star_fit(const pgx_query& q, const pgx_segment& seg) {
+  if (!seg.st_ok || (q.flags & PGX_Q_NO_STAR_TREE) || q.agg_fn.empty()) return false;
+  for (int fn : q.agg_fn)
+    if (fn != PGX_SUM) return false;
+  const size_t nl = q.leaf_col.size();
+  if (!q.filter.empty()) {
+    if (q.filter.size() == 1) {
+      if (q.filter[0].op != PGX_F_LEAF) return false;
+    } else {
+      if (q.filter.back().op != PGX_F_AND || q.filter.back().arg != int(nl) || q.filter.size() != nl + 1) return false;
+      for (size_t i = 0; i + 1 < q.filter.size(); ++i)
+        if (q.filter[i].op != PGX_F_LEAF) return false;
+    }
+  }
+  for (size_t i = 0; i < nl; ++i) {
+    if (std::find(seg.st_dim_name.begin(), seg.st_dim_name.end(), q.leaf_col[i]) == seg.st_dim_name.end()) return false;
+    for (size_t j = 0; j < i; ++j)
+      if (q.leaf_col[j] == q.leaf_col[i]) return false;
+  }
+  return true;
+}
+
+// StarTreeIndexOperator (operator/filter/StarTreeIndexOperator.java:134-478) for one segment: BFS from the root; at a
+// node splitting on a predicate column follow the children of the matching dictIds; on a group-by column (or with no
+// star child) follow every non-star child; otherwise take the star child.  An entry matches at a leaf, or once no
+// predicate / group-by column remains and the node has an aggregated doc.  Matched entries become: the aggregated doc
+// (nothing left to apply), the node's doc range, or the range AND the remaining predicates (createChildOperator).
+// The result is expressed as a filter program: OR(exact ranges, range_m AND preds(m) for each remaining-set m).
+void plan_star_segment(const pgx_query& q, const pgx_segment& seg, const KSeg& S, const pgx_leaf_binding* b,
+                       const std::vector<int>& leaf_phys, std::vector<int32_t>& blob, ExecPlan::StarPlan& sp) {
+  const auto& nodes = seg.st_nodes;
+  const int nl = int(q.leaf_col.size());
+  const int ng = int(q.group_cols.size());
+  sp.on = true;
+  sp.op.clear();
+  sp.arg.clear();
+  sp.ranges.clear();
+  bool empty = false;
+  for (int l = 0; l < nl; ++l)
+    if (S.leaf[l].mode == LEAF_NONE) empty = true;  // PredicateEvaluator.alwaysFalse -> emptyResult
+  std::map<uint32_t, std::vector<std::pair<int32_t, int32_t>>> groups;  // remaining-predicate mask -> [a, b] ranges
+  std::vector<std::pair<int32_t, int32_t>>& exact = groups[0];
+  if (!empty) {
+    std::vector<int> dim_leaf(seg.st_dim_name.size(), -1), dim_group(seg.st_dim_name.size(), -1);
+    for (size_t d = 0; d < seg.st_dim_name.size(); ++d) {
+      for (int l = 0; l < nl; ++l)
+        if (q.leaf_col[l] == seg.st_dim_name[d]) dim_leaf[d] = l;
+      for (int g = 0; g < ng; ++g)
+        if (q.group_cols[g] == seg.st_dim_name[d]) dim_group[d] = g;
+    }
+    auto matches = [&](int l, int id) -> bool {
+      const pgx_leaf_binding& x = b[l];
+      if (x.words) return (x.words[id >> 5] >> (id & 31)) & 1u;
+      return id >= x.lo && id <= x.hi;
+    };
+    struct Entry { int node; uint32_t pred, gb; };
+    std::deque<Entry> queue;
+    queue.push_back({0, nl ? (uint32_t(1) << nl) - 1u : 0u, ng ? (uint32_t(1) << ng) - 1u : 0u});
+    const int32_t num_raw = seg.total_raw_docs;
+    while (!queue.empty()) {
+      const Entry e = queue.front();
+      queue.pop_front();
+      const auto& cur = nodes[e.node];
+      const bool leaf = cur.cbeg == -1;
+      if (leaf || (e.pred == 0 && e.gb == 0 && cur.agg >= num_raw)) {
+        const bool agg_ok = cur.agg >= num_raw;
+        if (e.pred == 0) {
+          if (agg_ok && e.gb == 0) exact.push_back({cur.agg, cur.agg});
+          else if (cur.end > cur.start) exact.push_back({cur.start, cur.end - 1});
+        } else if (cur.end > cur.start) {
+          groups[e.pred].push_back({cur.start, cur.end - 1});
+        }
+        continue;
+      }
+      const int cdim = nodes[cur.cbeg].dim;  // StarTreeIndexNodeOffHeap.getChildDimensionName: first child's dimension
+      const int l = (cdim >= 0 && cdim < int(dim_leaf.size())) ? dim_leaf[cdim] : -1;
+      const int g = (cdim >= 0 && cdim < int(dim_group.size())) ? dim_group[cdim] : -1;
+      Entry ne{0, e.pred, e.gb};
+      if (l >= 0) {
+        ne.pred &= ~(uint32_t(1) << l);
+        if (g >= 0) ne.gb &= ~(uint32_t(1) << g);
+        // children sorted by value: each matching dictId is a binary search (getChildForDimensionValue)
+        const int card = seg.col(q.leaf_col[l]).card;
+        for (int id = 0; id < card; ++id) {
+          if (!matches(l, id)) continue;
+          int lo = cur.cbeg, hi = cur.cend;
+          while (lo <= hi) {
+            const int mid = lo + ((hi - lo) >> 1);
+            if (nodes[mid].value == id) { ne.node = mid; queue.push_back(ne); break; }
+            if (nodes[mid].value < id) lo = mid + 1; else hi = mid - 1;
+          }
+        }
+      } else {
+        const bool has_star = nodes[cur.cbeg].value == -1;
+        if (g >= 0 || !has_star) {
+          for (int c = cur.cbeg; c <= cur.cend; ++c) {
+            if (nodes[c].value == -1) continue;
+            if (g >= 0) ne.gb &= ~(uint32_t(1) << g);
+            ne.node = c;
+            queue.push_back(ne);
+          }
+        } else {
+          ne.node = cur.cbeg;
+          queue.push_back(ne);
+        }
+      }
+    }
+  }
+  // ranges -> blob (sorted, merged), program
+  auto put_ranges = [&](std::vector<std::pair<int32_t, int32_t>>& r) {
+    std::sort(r.begin(), r.end());
+    std::vector<int32_t> m;
+    for (const auto& x : r) {
+      if (!m.empty() && x.first <= m.back() + 1) m.back() = std::max(m.back(), x.second);
+      else { m.push_back(x.first); m.push_back(x.second); }
+    }
+    sp.ranges.push_back({blob.size(), int(m.size() / 2)});
+    blob.insert(blob.end(), m.begin(), m.end());
+    return nl + int(sp.ranges.size()) - 1;  // leaf index of this range leaf
+  };
+  int terms = 0;
+  for (auto& kv : groups) {
+    if (kv.second.empty()) continue;
+    const int rl = put_ranges(kv.second);
+    sp.op.push_back(OP_LEAF);
+    sp.arg.push_back(rl);
+    int pushed = 1;
+    for (int pass = 0; pass < 2; ++pass)  // index-based children first, then scans (AndBlockDocIdSet)
+      for (int l = 0; l < nl; ++l) {
+        if (!((kv.first >> l) & 1u)) continue;
+        const bool scan = leaf_phys[l] == PH_SCAN;
+        if (scan != (pass == 1)) continue;
+        if (scan) { sp.op.push_back(OP_STAT); sp.arg.push_back(0); }
+        sp.op.push_back(OP_LEAF);
+        sp.arg.push_back(l);
+        sp.op.push_back(OP_AND);
+        sp.arg.push_back(2);
+        ++pushed;
+      }
+    ++terms;
+  }
+  if (terms == 0) {
+    std::vector<std::pair<int32_t, int32_t>> none;
+    const int rl = put_ranges(none);
+    sp.op.push_back(OP_LEAF);
+    sp.arg.push_back(rl);
+    terms = 1;
+  }
+  if (terms > 1) { sp.op.push_back(OP_OR); sp.arg.push_back(terms); }
 }
 
 void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
@@ -870,6 +1076,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
 
   // per-segment descriptors
   P.ksegs.assign(n, KSeg{});
+  P.segcols.assign(n, {});
   int64_t tiles = 0;
   P.total_raw = 0;
   for (int s = 0; s < n; ++s) {
@@ -881,8 +1088,11 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     tiles += S.num_tiles;
     P.total_raw += seg.total_raw_docs;
     P.host_entries += int64_t(host_scan_leaves) * seg.total_raw_docs;
+    auto& segcols = P.segcols[s];
+    segcols.resize(P.qcols.size());
     for (size_t c = 0; c < P.qcols.size(); ++c) {
       const StagedColumn& col = seg.col(P.qcols[c]);
+      segcols[c] = &col;
       S.fwd[c] = col.fwd;
       S.bits[c] = int8_t(col.bits);
       S.dict[c] = col.dict_dev;
@@ -897,7 +1107,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     }
     // leaves
     for (size_t l = 0; l < q.leaf_col.size(); ++l) {
-      const StagedColumn& col = seg.col(q.leaf_col[l]);
+      const StagedColumn& col = *segcols[K.leaf_col[l]];
       const pgx_leaf_binding& b = bindings[size_t(s) * q.leaf_col.size() + l];
       KLeaf& L = S.leaf[l];
       L.lo = b.lo;
@@ -943,16 +1153,52 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         const bool neg = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
         ExecPlan::RoarItem it{s, int(l), neg, P.blob32.size(), 0, int((int64_t(seg.total_docs) + 65535) >> 16),
                               P.mask_words, col.inv_dev.p};
-        for (int id = 0; id < col.card; ++id)
-          if (matches(id) != neg) {
-            P.blob32.push_back(int32_t(col.inv_off[id]));
-            ++it.nb;
+        auto take = [&](int id) {
+          P.blob32.push_back(int32_t(col.inv_off[id]));
+          ++it.nb;
+        };
+        if (b.words) {  // walk the set (or, negated, the clear) bits of the dictId bitset
+          const int nw = (col.card + 31) / 32;
+          for (int w = 0; w < nw; ++w) {
+            uint32_t x = neg ? ~b.words[w] : b.words[w];
+            if (w == nw - 1 && (col.card & 31)) x &= (1u << (col.card & 31)) - 1u;
+            while (x) {
+              take(w * 32 + __builtin_ctz(x));
+              x &= x - 1u;
+            }
           }
+        } else if (!neg) {
+          for (int id = std::max(0, b.lo); id <= std::min(b.hi, col.card - 1); ++id) take(id);
+        } else {
+          for (int id = 0; id < col.card; ++id)
+            if (id < b.lo || id > b.hi) take(id);
+        }
         P.mask_words += uint64_t(it.nchunks) * 2048;
         P.roar_maxchunks = std::max(P.roar_maxchunks, it.nchunks);
         P.roar_index[s][l] = int(P.roar.size());
         P.roar.push_back(it);
       }
+    }
+  }
+  // star-tree segments (query kernels only: the per-segment program needs the generated kernels)
+  P.star.assign(n, ExecPlan::StarPlan{});
+  if (P.use_docmask && int(q.leaf_col.size()) + 8 <= PGX_J_MAX_LEAVES) {
+    tiles = 0;
+    for (int s = 0; s < n; ++s) {
+      KSeg& S = P.ksegs[s];
+      if (star_fit(q, *segs[s])) {
+        plan_star_segment(q, *segs[s], S, bindings + size_t(s) * q.leaf_col.size(), P.leaf_phys, P.blob32, P.star[s]);
+        if (int(q.leaf_col.size() + P.star[s].ranges.size()) > PGX_J_MAX_LEAVES) {
+          P.star[s] = ExecPlan::StarPlan{};
+        } else {
+          // StarTreeIndexOperator reaches aggregated docs: scan [0, totalDocs); no root scan leaf
+          P.host_entries -= int64_t(host_scan_leaves) * segs[s]->total_raw_docs;
+          S.num_docs = segs[s]->total_docs;
+        }
+      }
+      S.tile_begin = tiles;
+      S.num_tiles = int32_t((int64_t(S.num_docs) + kTileRows - 1) / kTileRows);
+      tiles += S.num_tiles;
     }
   }
   K.total_tiles = tiles;
@@ -1094,9 +1340,14 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     std::string sig;
     for (int l = 0; l < nleaves; ++l)
       sig += P.roar_index[s][l] >= 0 ? (P.roar[P.roar_index[s][l]].neg ? 'F' : 'E') : char('a' + S.leaf[l].mode);
+    if (P.star[s].on) {
+      sig += "|star";
+      for (size_t i = 0; i < P.star[s].op.size(); ++i)
+        sig += "," + std::to_string(P.star[s].op[i]) + ":" + std::to_string(P.star[s].arg[i]);
+    }
     sig += '|';
     for (int c = 0; c < nc; ++c) {
-      const StagedColumn& col = segs[s]->col(P.qcols[c]);
+      const StagedColumn& col = *P.segcols[s][c];
       sig += std::to_string(S.bits[c]) + (S.remap[c] ? "r" : "") + ",";
       if (want_img[c]) sig += "i" + std::to_string(col.img_kind) + "." + std::to_string(col.img_sh) + ",";
     }
@@ -1133,7 +1384,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         C.img_sh = col0.img_sh;
         uint64_t range = 0;
         for (int s : members) {
-          const StagedColumn& col = segs[s]->col(P.qcols[c]);
+          const StagedColumn& col = *P.segcols[s][c];
           C.img_words = std::max(C.img_words, col.img_words);
           range = std::max(range, col.vrange);
         }
@@ -1163,9 +1414,19 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       const int ri = P.roar_index[members[0]][l];
       J.leaf_mode.push_back(ri >= 0 ? (P.roar[ri].neg ? LEAF_DOCMASK_NOT : LEAF_DOCMASK) : S0.leaf[l].mode);
     }
-    for (int i = 0; i < K.prog_len; ++i) {
-      J.prog_op.push_back(K.prog_op[i]);
-      J.prog_arg.push_back(K.prog_arg[i]);
+    const ExecPlan::StarPlan& SP = P.star[members[0]];
+    if (SP.on) {
+      for (size_t k = 0; k < SP.ranges.size(); ++k) {
+        J.leaf_col.push_back(-1);
+        J.leaf_mode.push_back(LEAF_RANGES);
+      }
+      J.prog_op = SP.op;
+      J.prog_arg = SP.arg;
+    } else {
+      for (int i = 0; i < K.prog_len; ++i) {
+        J.prog_op.push_back(K.prog_op[i]);
+        J.prog_arg.push_back(K.prog_arg[i]);
+      }
     }
     for (int a = 0; a < K.num_aggs; ++a) {
       J.agg_kind.push_back(K.agg_kind[a]);
@@ -1196,7 +1457,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       js.num_docs = S.num_docs;
       tiles += (int64_t(S.num_docs) + tile_rows - 1) / tile_rows;
       for (int c = 0; c < nc; ++c) {
-        const StagedColumn& col = segs[s]->col(P.qcols[c]);
+        const StagedColumn& col = *P.segcols[s][c];
         js.fwd[c] = S.fwd[c];
         js.dict[c] = S.dict[c];
         js.remap[c] = S.remap[c];
@@ -1213,6 +1474,11 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         js.llo[l] = uint32_t(L.lo);
         js.lspan[l] = uint32_t(L.hi) - uint32_t(L.lo);
       }
+      if (P.star[s].on)
+        for (size_t k = 0; k < P.star[s].ranges.size(); ++k) {
+          js.lranges[nleaves + k] = reinterpret_cast<const int*>(B.dev()) + P.star[s].ranges[k].first;
+          js.lnr[nleaves + k] = P.star[s].ranges[k].second;
+        }
       G.segs.push_back(js);
     }
     const int waves = J.T / 64;
@@ -1492,6 +1758,7 @@ pgx_status pgx_segment_stage(pgx_ctx* ctx, const pgx_segment_desc* d, pgx_segmen
     if (d->star_tree && d->star_tree_len) {
       const uint8_t* p = static_cast<const uint8_t*>(d->star_tree);
       seg->star_tree.assign(p, p + d->star_tree_len);
+      parse_star_tree(*seg);
     }
     ctx->refs.fetch_add(1);  // released by pgx_segment_release
     *out = seg.release();

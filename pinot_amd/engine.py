@@ -422,8 +422,10 @@ class _Query:
             self._keep.append(cb)
             larr[i].column = cb
             larr[i].kind = N.PGX_PRED[lf["op"]]
+        # BrokerRequest debug option useStarTree=false (common/utils/request/RequestUtils.java:229-236)
+        use_st = str((request.get("debug_options") or {}).get("useStarTree", "true")).lower() != "false"
         qd = N.QueryDesc(len(aggs), agg_arr, len(gcols), garr, gb["top_n"] if gb else 10, len(nodes), narr,
-                         len(leaves), larr, 0)
+                         len(leaves), larr, 0 if use_st else N.PGX_Q_NO_STAR_TREE)
         self._keep += [agg_arr, garr, narr, larr]
         h = C.c_void_p()
         N.check(N.lib().pgx_query_compile(ctx.handle, C.byref(qd), C.byref(h)))

@@ -116,7 +116,7 @@ def build(dim_ids: np.ndarray, metrics: np.ndarray, cards: Sequence[int], max_le
         node.children = {}
         added = 0
         for i, v in enumerate(vals.tolist()):
-            child = Node(sd, int(v), node.level + 1, path=dict(node.path, **{sd: int(v)}))
+            child = Node(sd, int(v), node.level + 1, path={**node.path, sd: int(v)})
             node.children[int(v)] = child
             ca, cb = a + int(bounds[i]), a + int(bounds[i + 1])
             cdocs = 0
