@@ -101,13 +101,26 @@ def main():
     from pinot_amd import native as N
     from pinot_amd import pql, synth
 
-    wl = synth.WORKLOADS[args.workload]
-    rows = args.rows or wl.rows
     ctx = E.Context(local)
     from pinot_amd import multigpu
-    seg_ids = multigpu.shard(wl.segments, world, rank, wl.scaling)
     t_gen = time.perf_counter()
-    data = synth.DeviceSegments(ctx, wl, seg_ids, rows=rows)
+    if args.workload == "c1":  # baseball quick-start shape, one 100k-row segment (latency-bound)
+        data = synth.BaseballSegments(ctx, rows=args.rows or None)
+        wl = synth.Workload("c1", "BASELINE configs[0]: baseballStats quick-start shape (100k rows, synthetic), "
+                            "sum(runs) where yearID>=2000 group by playerName", 1, data.rows, [], synth.C1_QUERY, 1,
+                            "weak")
+        rows = data.rows
+    elif args.workload == "c4":  # star-tree segment (weak scaling: one segment per GPU)
+        data = synth.StarTreeSegments(ctx, rows=args.rows or None)
+        wl = synth.Workload("c4", "BASELINE configs[3]: star-tree over 6 dims (cards %s) + 3 metrics, %d raw rows "
+                            "per segment, maxLeafRecords 100000, filtered group-by served from pre-aggregated docs"
+                            % (synth.C4_CARDS, data.rows), 1, data.rows, [], synth.C4_QUERY, 4, "weak")
+        rows = data.rows
+    else:
+        wl = synth.WORKLOADS[args.workload]
+        rows = args.rows or wl.rows
+        seg_ids = multigpu.shard(wl.segments, world, rank, wl.scaling)
+        data = synth.DeviceSegments(ctx, wl, seg_ids, rows=rows)
     t_gen = time.perf_counter() - t_gen
     req = pql.compile(wl.query)
     q = E._Query(ctx, req)
@@ -202,12 +215,16 @@ def main():
     # forward-index bytes of every column the kernel decodes, serialized roaring bytes of every bitmap a
     # bitmap-index leaf ORs (inverted columns, non-RANGE predicates: FilterPlanNode.java:118-132), dictionaries.
     bitmap_leaves = [(lf, np.nonzero(E.leaf_matching_ids(segs[0].column(lf["column"]), lf))[0])
-                     for lf in q.leaves if data.is_inverted(lf["column"]) and lf["op"] != "RANGE"]
+                     for lf in q.leaves if wl.name != "c4" and data.is_inverted(lf["column"]) and lf["op"] != "RANGE"]
     scan_cols = {lf["column"] for lf in q.leaves} - {lf["column"] for lf, _ in bitmap_leaves}
     used = sorted(scan_cols | {a["column"] for a in req["aggregations"] if a["column"] != "*"}
                   | set((req.get("group_by") or {}).get("columns", [])))
     dict_cols = sorted({a["column"] for a in req["aggregations"] if a["column"] != "*"})
-    algo_bytes = data.algorithmic_bytes(used, dict_cols, bitmap_leaves)
+    if wl.name == "c4":
+        from pinot_amd import startree as ST
+        algo_bytes = data.algorithmic_bytes(used, dict_cols, int(st[0]), len(ST.parse(data.seg_data.star_tree)[1]))
+    else:
+        algo_bytes = data.algorithmic_bytes(used, dict_cols, bitmap_leaves)
     # the query-specialised kernel (hiprtc, pgx_jit.cpp) unless PGX_JIT=0 selects the generic interpreter kernel
     kernel_name = "pgxq (generated per query shape)" if os.environ.get("PGX_JIT", "1") != "0" else "pgx_scan_kernel"
     achieved = algo_bytes / (kern.value * 1e-3) / 1e9

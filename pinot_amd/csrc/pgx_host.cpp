@@ -765,6 +765,8 @@ struct ExecPlan {
     std::vector<std::pair<size_t, int>> ranges;    // extra range leaves: (blob offset, number of [a,b] pairs)
   };
   std::vector<StarPlan> star;
+  std::vector<std::vector<int32_t>> star_tiles;   // per star segment: local tile ids intersecting its ranges
+  size_t star_tile_cap = 0;                       // arena int32 slots reserved for them
   uint64_t mask_words = 0;
   const RDesc* rdesc_dev = nullptr;
   int roar_maxchunks = 0;
@@ -1218,7 +1220,7 @@ constexpr size_t kOutsBytes = 256;  // agg planes [0, 72), stats [128, 144), ove
 struct ExecBuffers {
   DevBuf arena;
   PinnedBuf host;
-  size_t off_ksegs = 0, off_jsegs = 0, off_rdesc = 0, off_outs = 0, size = 0;
+  size_t off_ksegs = 0, off_jsegs = 0, off_tiles = 0, off_rdesc = 0, off_outs = 0, size = 0;
   DevBuf table, keys, key_state, masks;
   uint8_t* dev() const { return arena.as<uint8_t>(); }
 };
@@ -1230,7 +1232,11 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
   const size_t n = P.ksegs.size();
   B.off_ksegs = align_up(P.blob32.size() * 4, 256);
   B.off_jsegs = align_up(B.off_ksegs + n * sizeof(KSeg), 256);
-  B.off_rdesc = align_up(B.off_jsegs + n * sizeof(JSeg), 256);
+  P.star_tile_cap = 0;
+  for (int s = 0; s < int(n); ++s)
+    if (!P.star.empty() && P.star[s].on) P.star_tile_cap += size_t(P.ksegs[s].num_docs) / 8192 + 2;
+  B.off_tiles = align_up(B.off_jsegs + n * sizeof(JSeg), 256);
+  B.off_rdesc = align_up(B.off_tiles + P.star_tile_cap * 4, 256);
   B.off_outs = align_up(B.off_rdesc + P.roar.size() * sizeof(RDesc), 256);
   B.size = B.off_outs + kOutsBytes;
   B.arena = DevBuf(ctx, B.size);
@@ -1356,6 +1362,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
   }
   const int cus = ctx->num_cus;
   size_t jidx = 0;  // next free JSeg slot of the arena
+  size_t star_tile_off = 0;
+  P.star_tiles.assign(n, {});
   for (const std::string& sig : order) {
     const std::vector<int>& members = groups[sig];
     const KSeg& S0 = P.ksegs[members[0]];
@@ -1455,7 +1463,27 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       JSeg js{};
       js.tile_begin = tiles;
       js.num_docs = S.num_docs;
-      tiles += (int64_t(S.num_docs) + tile_rows - 1) / tile_rows;
+      if (P.star[s].on) {
+        // visit only the tiles that intersect a star-tree range: every selected doc lies in one
+        auto& tl = P.star_tiles[s];
+        tl.clear();
+        for (const auto& r : P.star[s].ranges)
+          for (int k = 0; k < r.second; ++k) {
+            const int32_t a = P.blob32[r.first + 2 * k], b = P.blob32[r.first + 2 * k + 1];
+            for (int64_t t = a / tile_rows; t <= b / tile_rows; ++t)
+              if (tl.empty() || tl.back() != int32_t(t)) tl.push_back(int32_t(t));
+          }
+        std::sort(tl.begin(), tl.end());
+        tl.erase(std::unique(tl.begin(), tl.end()), tl.end());
+        const size_t off = star_tile_off;
+        star_tile_off += tl.size();
+        if (star_tile_off > P.star_tile_cap) fail(PGX_ERR_INTERNAL, "star tile list overflow");
+        std::memcpy(B.host.bytes() + B.off_tiles + off * 4, tl.data(), tl.size() * 4);
+        js.tiles = reinterpret_cast<const int*>(B.dev() + B.off_tiles + off * 4);
+        tiles += int64_t(tl.size());
+      } else {
+        tiles += (int64_t(S.num_docs) + tile_rows - 1) / tile_rows;
+      }
       for (int c = 0; c < nc; ++c) {
         const StagedColumn& col = *P.segcols[s][c];
         js.fwd[c] = S.fwd[c];

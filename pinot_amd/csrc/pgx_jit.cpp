@@ -156,6 +156,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("const long long t2 = (te < tse) ? te : tse;");
   e.ln("const int nd = S->num_docs;");
   e.ln("const long long tile0 = S->tile_begin;");
+  e.ln("const PGX_G int* __restrict__ tl = (const PGX_G int*)S->tiles;  // tile skipping (star-tree ranges)");
   // stage this segment's value images into LDS
   bool has_img = false;
   for (int c = 0; c < ncols; ++c) has_img |= s.cols[c].img != IMG_NONE;
@@ -194,7 +195,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       case LEAF_RANGES:
         e.ln("const PGX_G int* __restrict__ rg", l, " = (const PGX_G int*)S->lranges[", l, "];");
         e.ln("const int nr", l, " = S->lnr[", l, "];");
-        e.ln("int cur", l, " = pgx_ranges_seek(rg", l, ", nr", l, ", (int)((t - tile0) * (PT * 32)));");
+        e.ln("int cur", l, " = pgx_ranges_seek(rg", l, ", nr", l, ", (int)((tl ? (long long)tl[t - tile0] : (t - tile0)) * (PT * 32)));");
         break;
       default:
         break;
@@ -252,7 +253,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   auto emit_loads = [&](const std::string& tile, const std::string& dst) {
     e.ln("{");
     e.ind++;
-    e.ln("const int rb = (int)((", tile, " - tile0) * (PT * 32));");
+    e.ln("const int rb = (int)((tl ? (long long)tl[", tile, " - tile0] : (", tile, " - tile0)) * (PT * 32));");
     e.ln("const bool full = rb + PT * 32 <= nd;");
     for (int u = 0; u < U; ++u) {
       e.ln("{");
@@ -295,7 +296,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     }
   e.ln("if (tt + 1 < t2) ");
   emit_loads("tt + 1", "n");
-  e.ln("const int rb = (int)((tt - tile0) * (PT * 32));");
+  e.ln("const int rb = (int)((tl ? (long long)tl[tt - tile0] : (tt - tile0)) * (PT * 32));");
   // The tile body is instantiated twice: for whole tiles (no per-row bound check) and for a segment's last tile.
   e.ln("auto body = [&](auto FT) {");
   e.ind = 4;

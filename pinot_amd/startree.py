@@ -45,35 +45,28 @@ class Node:
 
 
 class _Table:
-    """Growable record table: dims int32 (ALL = -1 for star), metrics int64."""
+    """Record table grown by appends (star-node rows, aggregated docs): dims int32 (ALL = -1), metrics int64.  Kept as
+    a list of contiguous blocks; every range the builder reads lies inside one block, so no re-concatenation."""
 
     def __init__(self, dims: np.ndarray, mets: np.ndarray):
-        self.dims = [dims]
-        self.mets = [mets]
+        self.blocks = [(0, dims, mets)]
         self.n = len(dims)
-        self._cd = None
 
     def append(self, d: np.ndarray, m: np.ndarray) -> int:
         start = self.n
-        self.dims.append(d)
-        self.mets.append(m)
+        self.blocks.append((start, d, m))
         self.n += len(d)
-        self._cd = None
         return start
 
-    def compact(self):
-        if len(self.dims) > 1:
-            self.dims = [np.concatenate(self.dims)]
-            self.mets = [np.concatenate(self.mets)]
-
     def rows(self, a, b):
-        self.compact()
-        return self.dims[0][a:b], self.mets[0][a:b]
+        import bisect
+        i = bisect.bisect_right([blk[0] for blk in self.blocks], a) - 1
+        s0, d, m = self.blocks[i]
+        assert b - s0 <= len(d), "range spans two blocks"
+        return d[a - s0:b - s0], m[a - s0:b - s0]
 
-    def set_rows(self, a, d, m):
-        self.compact()
-        self.dims[0][a:a + len(d)] = d
-        self.mets[0][a:a + len(m)] = m
+    def all(self):
+        return (np.concatenate([b[1] for b in self.blocks]), np.concatenate([b[2] for b in self.blocks]))
 
 
 def _lexsort(d: np.ndarray, order: Sequence[int]) -> np.ndarray:
@@ -159,8 +152,8 @@ def build(dim_ids: np.ndarray, metrics: np.ndarray, cards: Sequence[int], max_le
         return acc
 
     agg_docs(root)
-    tab.compact()
-    return root, tab.dims[0], tab.mets[0], list(split_order), n
+    all_d, all_m = tab.all()
+    return root, all_d, all_m, list(split_order), n
 
 
 def serialize(root: Node, dim_names: Sequence[str]) -> bytes:

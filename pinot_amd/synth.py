@@ -85,6 +85,78 @@ WORKLOADS: Dict[str, Workload] = {
 }
 
 
+# C4 (BASELINE configs[3]): star-tree segment over 6 dims + 3 metrics.  Built by the Python restatement of the
+# reference builder (pinot_amd/startree.py), which takes ~50 s at 10M raw rows; the SURVEY's 100M-row instance would take
+# ~8 min per bench run, so the bench uses 10M raw rows per segment (same dims, metrics, maxLeafRecords and query).
+C4_CARDS = [8, 16, 32, 64, 128, 1000]
+C4_ROWS = 10_000_000
+C4_QUERY = "SELECT SUM(m1), SUM(m2), SUM(m3) FROM T WHERE d2 = 3 AND d4 IN (1, 2, 3) GROUP BY d1 TOP 10"
+
+
+class StarTreeSegments:
+    """One C4 star-tree segment staged from host bytes (synthetic, seed 4)."""
+
+    def __init__(self, ctx, rows: int = None, seed: int = 4):
+        from . import startree as ST
+        from .engine import IndexSegment
+        self.rows = rows or C4_ROWS
+        rng = np.random.default_rng(seed)
+        dims = {"d%d" % (i + 1): rng.integers(0, c, self.rows) for i, c in enumerate(C4_CARDS)}
+        mets = {"m%d" % (i + 1): rng.integers(0, 1 << 16, self.rows) for i in range(3)}
+        self.seg_data = ST.make_star_tree_segment("c4_0", dims, mets, max_leaf_records=ST.DEFAULT_MAX_LEAF_RECORDS)
+        self.segments = [IndexSegment(ctx, self.seg_data)]
+        self.seg_ids = [0]
+
+    def algorithmic_bytes(self, used_columns, dict_columns, docs_scanned: int, nodes_visited: int) -> int:
+        """docs scanned x (bits of the columns read)/8 + dictionaries + 28 B per star-tree node."""
+        cols = self.seg_data.columns
+        b = docs_scanned * sum(cols[c].bits for c in used_columns) // 8
+        b += sum(cols[c].cardinality * 4 for c in dict_columns)
+        return b + 28 * nodes_visited
+
+    def free(self):
+        for s in self.segments:
+            s.destroy()
+        self.segments = []
+
+
+# C1 (BASELINE configs[0]): the baseball quick-start shape (baseball.csv is not in the reference tree, so the data is
+# synthetic per SURVEY 8d: yearID uniform 1871..2013, playerName 17,000 distinct strings, runs 0..177; seed 1).
+C1_ROWS = 100_000
+C1_QUERY = "SELECT SUM(runs) FROM T WHERE yearID >= 2000 GROUP BY playerName TOP 10"
+
+
+class BaseballSegments:
+    """One C1 segment built on the host (v1 format) and staged through pgx_segment_stage."""
+
+    def __init__(self, ctx, rows: int = None, seed: int = 1):
+        from .engine import IndexSegment
+        from .segment import make_column, make_segment
+        self.rows = rows or C1_ROWS
+        rng = np.random.default_rng(seed)
+        names = np.array(["player%05d" % i for i in range(17000)])
+        raw = {"yearID": rng.integers(1871, 2014, self.rows).astype(np.int32),
+               "playerName": names[rng.integers(0, len(names), self.rows)],
+               "runs": rng.integers(0, 178, self.rows).astype(np.int32)}
+        self.raw = raw
+        self.seg_data = make_segment("baseballStats_0", [make_column(k, v) for k, v in raw.items()])
+        self.segments = [IndexSegment(ctx, self.seg_data)]
+        self.seg_ids = [0]
+
+    def is_inverted(self, name):
+        return False
+
+    def algorithmic_bytes(self, used_columns, dict_columns, bitmap_leaves=()) -> int:
+        cols = self.seg_data.columns
+        b = sum((self.rows * cols[c].bits + 7) // 8 for c in used_columns)
+        return b + sum(cols[c].cardinality * 4 for c in dict_columns)
+
+    def free(self):
+        for s in self.segments:
+            s.destroy()
+        self.segments = []
+
+
 def padded_fwd_bytes(rows: int, bits: int) -> int:
     tiles = max(1, (rows + TILE_ROWS - 1) // TILE_ROWS)
     return tiles * (TILE_ROWS // 8) * bits + 64
