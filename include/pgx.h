@@ -210,6 +210,10 @@ pgx_status pgx_result_from_dense(pgx_ctx* ctx, const pgx_query* q, pgx_segment* 
  * pgx_synth_value(seed, row) = splitmix64(seed ^ (row * 0x9E3779B97F4A7C15)) % card  (DESIGN.md). */
 pgx_status pgx_synth_column(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
                             uint64_t seed);
+/* Joint columns: the row first draws pair = pgx_synth_value(pair_seed, row) % npairs, the dictId is then
+ * pgx_synth_value(seed, pair) % card; columns sharing pair_seed / npairs take values from npairs fixed combinations. */
+pgx_status pgx_synth_column_paired(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
+                                   uint64_t seed, uint64_t pair_seed, uint32_t npairs);
 /* Host twin of pgx_synth_column's dictIds (int32 per row). */
 pgx_status pgx_synth_dict_ids(uint64_t seed, int64_t n_rows, int32_t card, int32_t* out);
 /* Segment creation: the <col>.bitmap.inv bytes of a column (HeapBitmapInvertedIndexCreator.java:42-81 layout, roaring

@@ -36,7 +36,7 @@ extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
 extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
-                                       int64_t n_words, hipStream_t stream);
+                                       int64_t n_words, uint64_t pair_seed, uint32_t npairs, hipStream_t stream);
 
 using namespace pgx;
 
@@ -2009,18 +2009,23 @@ pgx_status pgx_copy_to_device(pgx_ctx* ctx, void* dst, const void* src, uint64_t
   });
 }
 
-pgx_status pgx_synth_column(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
-                            uint64_t seed) {
+pgx_status pgx_synth_column_paired(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
+                                   uint64_t seed, uint64_t pair_seed, uint32_t npairs) {
   return guarded([&] {
     if (!ctx || !device_fwd) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     if (bits < 1 || bits > 32 || card < 1) fail(PGX_ERR_INVALID_ARG, "bits/card");
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     const int64_t n_words = int64_t(padded_fwd_bytes(n_rows, bits) / 4);
-    hip_check(pgx_launch_synth(static_cast<uint32_t*>(device_fwd), n_rows, bits, uint32_t(card), seed, n_words,
+    hip_check(pgx_launch_synth(static_cast<uint32_t*>(device_fwd), n_rows, bits, uint32_t(card), seed, n_words, pair_seed, npairs,
                                ctx->stream),
               "synth launch");
     hip_check(hipStreamSynchronize(ctx->stream), "sync");
   });
+}
+
+pgx_status pgx_synth_column(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
+                            uint64_t seed) {
+  return pgx_synth_column_paired(ctx, device_fwd, n_rows, bits, card, seed, 0, 0);
 }
 
 // ---- segment-creation helpers (benchmark data and fixtures; not on the query path) ----------------------------------

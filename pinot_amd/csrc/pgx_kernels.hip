@@ -596,8 +596,10 @@ __device__ __forceinline__ uint32_t synth_value(uint64_t seed, int64_t row, uint
   return static_cast<uint32_t>(splitmix64(seed ^ (static_cast<uint64_t>(row) * 0x9E3779B97F4A7C15ull)) % card);
 }
 
+// npairs > 0: the row first draws a pair index from pair_seed, and the value is a function of that index, so two
+// columns generated with the same pair_seed / npairs take their values jointly from npairs fixed combinations.
 __global__ void pgx_synth_kernel(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
-                                 int64_t n_words) {
+                                 int64_t n_words, uint64_t pair_seed, uint32_t npairs) {
   for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * blockDim.x) {
     const int64_t bit0 = w * 32;
     const int64_t r_first = bit0 / bits;
@@ -605,7 +607,8 @@ __global__ void pgx_synth_kernel(uint32_t* out_words, int64_t n_rows, int bits, 
     uint32_t word = 0;
     for (int64_t r = r_first; r <= r_last; ++r) {
       if (r >= n_rows) break;
-      const uint64_t v = synth_value(seed, r, card);
+      const int64_t src = npairs ? static_cast<int64_t>(synth_value(pair_seed, r, npairs)) : r;
+      const uint64_t v = synth_value(seed, src, card);
       // bits of row r occupy [r*bits, r*bits+bits); MSB-first.
       const int64_t rs = r * bits;
       // position of row's MSB relative to word start
@@ -678,11 +681,11 @@ extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64
 }
 
 extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
-                                       int64_t n_words, hipStream_t stream) {
+                                       int64_t n_words, uint64_t pair_seed, uint32_t npairs, hipStream_t stream) {
   int grid = static_cast<int>(std::min<int64_t>((n_words + 255) / 256, 65536));
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(pgx::pgx_synth_kernel, dim3(grid), dim3(256), 0, stream, out_words, n_rows, bits, card, seed,
-                     n_words);
+                     n_words, pair_seed, npairs);
   return hipGetLastError();
 }
 

@@ -74,6 +74,8 @@ _lib = None
 EXPORTS = {
     "pgx_jit_compile_check": (C.c_int, [C.c_char_p, C.c_char_p, C.c_ulong]),
     "pgx_jit_selftest": (C.c_int, [C.POINTER(C.c_int), C.c_char_p, C.c_ulong]),
+    "pgx_synth_column_paired": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_uint64,
+                                          C.c_uint64, C.c_uint32]),
     "pgx_synth_dict_ids": (C.c_int, [C.c_uint64, C.c_int64, C.c_int32, C.c_void_p]),
     "pgx_inverted_index_build": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_uint64,
                                            C.POINTER(C.c_uint64)]),

@@ -52,6 +52,7 @@ class ColSpec:
     card: int
     dict_kind: str = "ids"
     inverted: bool = False  # build <col>.bitmap.inv (roaring) for the segment, like a Pinot invertedIndexColumns entry
+    paired: bool = False    # value drawn jointly with the workload's other paired columns from `npairs` fixed combos
 
     @property
     def bits(self):
@@ -68,6 +69,7 @@ class Workload:
     query: str
     seed: int
     scaling: str  # "weak" (every rank holds `segments` segments) or "strong" (segments sharded over ranks)
+    npairs: int = 0
 
 
 WORKLOADS: Dict[str, Workload] = {
@@ -75,6 +77,11 @@ WORKLOADS: Dict[str, Workload] = {
                    "count(*)+sum(metric) with a 50% range filter, 1 MI355X per 1B rows",
                    8, 125_000_000, [ColSpec("dA", 256), ColSpec("m", 65536, "metric")],
                    "SELECT COUNT(*), SUM(m) FROM T WHERE dA BETWEEN 64 AND 191", 2, "weak"),
+    "c3": Workload("c3", "BASELINE configs[2]: 1B rows (8 x 125M), group by g1 (card 10k) x g2 (card 1M) drawn from "
+                   "2^24 fixed pairs (high-cardinality LONG_MAP path), sum/min/max(m)",
+                   8, 125_000_000, [ColSpec("g1", 10000, paired=True), ColSpec("g2", 1_000_000, paired=True),
+                                    ColSpec("m", 65536, "metric")],
+                   "SELECT SUM(m), MIN(m), MAX(m) FROM T GROUP BY g1, g2 TOP 10", 3, "weak", npairs=1 << 24),
     "c5": Workload("c5", "BASELINE configs[4]: 4096 x 2M rows sharded over the GPUs, (f1 IN 32 ids OR f2=7) AND "
                    "f3<>3, group by gk (card 1000), sum(m)",
                    4096, 2_000_000,
@@ -185,8 +192,13 @@ class DeviceSegments:
                 p = C.c_void_p()
                 N.check(L.pgx_device_alloc(ctx.handle, nbytes, C.byref(p)))
                 self.buffers.append(p)
-                N.check(L.pgx_synth_column(ctx.handle, p, self.rows, c.bits, c.card,
-                                           column_seed(wl.seed, s, ci)))
+                if c.paired:  # the pair -> value map is global; the row -> pair draw is per segment
+                    N.check(L.pgx_synth_column_paired(ctx.handle, p, self.rows, c.bits, c.card,
+                                                      column_seed(wl.seed, 0, ci), column_seed(wl.seed, s, 99),
+                                                      wl.npairs))
+                else:
+                    N.check(L.pgx_synth_column(ctx.handle, p, self.rows, c.bits, c.card,
+                                               column_seed(wl.seed, s, ci)))
                 fwd_dev[c.name] = (p.value, nbytes)
                 dict_bytes = dicts[c.name].astype(">i4").tobytes()
                 inv_bytes = inv.pop((s, ci), None)
