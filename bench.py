@@ -129,12 +129,16 @@ def main():
     binds, keep = q.bindings(segs)
     L = N.lib()
 
-    dense = bool(req.get("group_by"))
+    dense = False
     dense_t = None
     plane_ops = []
-    if dense:
+    if req.get("group_by") and world > 1:
         slots = C.c_int64()
         N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
+        dense = slots.value <= (1 << 22)  # dense key space: RCCL all-reduce of the tables
+        if not dense:
+            raise SystemExit("sparse group-by across GPUs (hash-partitioned exchange) is not implemented; run N=1")
+    if dense:
         nplanes = 1 + len(req["aggregations"])
         for p in range(nplanes):
             op = C.c_int32()

@@ -55,22 +55,25 @@ def merge_dense_planes(t, plane_ops: Sequence[int]) -> None:
 
 
 def merge_aggregation(fns: Sequence[str], values: Sequence[Tuple[float, int]], device=None) -> List[Tuple[float, int]]:
-    """Merge aggregation-only partials (value, count) per function across ranks."""
+    """Merge aggregation-only partials (value, count) per function across ranks: ONE all-reduce (sum) carries every
+    count and every SUM/AVG value (doubles: counts are exact below 2^53); MIN and MAX get one collective each only
+    when the query has them (they are latency-bound 8-byte messages on xGMI)."""
     import torch
     import torch.distributed as dist
-    n = len(fns)
-    v = torch.tensor([x[0] for x in values], dtype=torch.float64, device=device)
-    c = torch.tensor([x[1] for x in values], dtype=torch.int64, device=device)
-    dist.all_reduce(c)
-    add = torch.tensor([f in ("count", "sum", "avg") for f in fns], device=device)
-    s = torch.where(add, v, torch.zeros_like(v))
-    dist.all_reduce(s)
-    mn = torch.where(torch.tensor([f == "min" for f in fns], device=device), v, torch.full_like(v, float("inf")))
-    dist.all_reduce(mn, op=dist.ReduceOp.MIN)
-    mx = torch.where(torch.tensor([f == "max" for f in fns], device=device), v, torch.full_like(v, float("-inf")))
-    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-    out = []
+    adds = [float(x[1]) for x in values] + [float(x[0]) for f, x in zip(fns, values) if f in ("count", "sum", "avg")]
+    t = torch.tensor(adds, dtype=torch.float64, device=device)
+    dist.all_reduce(t)
+    counts = [int(v) for v in t[:len(fns)].tolist()]
+    sums = iter(t[len(fns):].tolist())
+    out = [None] * len(fns)
     for i, f in enumerate(fns):
-        val = {"min": mn[i], "max": mx[i]}.get(f, s[i]).item()
-        out.append((val, int(c[i].item())))
+        if f in ("count", "sum", "avg"):
+            out[i] = (next(sums), counts[i])
+    for f, op in (("min", dist.ReduceOp.MIN), ("max", dist.ReduceOp.MAX)):
+        idx = [i for i, g in enumerate(fns) if g == f]
+        if idx:
+            m = torch.tensor([values[i][0] for i in idx], dtype=torch.float64, device=device)
+            dist.all_reduce(m, op=op)
+            for i, v in zip(idx, m.tolist()):
+                out[i] = (v, counts[i])
     return out
