@@ -1338,34 +1338,41 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     if (grouped || K.agg_kind[a] == A_SUM || K.agg_kind[a] == A_AVG) want_img[K.agg_col[a]] = true;
   }
   for (int g = 0; g < K.num_gcols; ++g) decode[K.gcol[g]] = true;
-  // signature per segment -> groups
-  std::map<std::string, std::vector<int>> groups;
-  std::vector<std::string> order;
+  // signature per segment -> groups (a flat int vector per segment, compared whole; one std::map lookup each)
+  std::map<std::vector<int32_t>, std::vector<int>> groups;
+  std::vector<const std::vector<int32_t>*> order;
+  std::vector<int32_t> sig;
   for (int s = 0; s < n; ++s) {
     const KSeg& S = P.ksegs[s];
-    std::string sig;
+    sig.clear();
     for (int l = 0; l < nleaves; ++l)
-      sig += P.roar_index[s][l] >= 0 ? (P.roar[P.roar_index[s][l]].neg ? 'F' : 'E') : char('a' + S.leaf[l].mode);
+      sig.push_back(P.roar_index[s][l] >= 0 ? (P.roar[P.roar_index[s][l]].neg ? 101 : 100) : S.leaf[l].mode);
     if (P.star[s].on) {
-      sig += "|star";
-      for (size_t i = 0; i < P.star[s].op.size(); ++i)
-        sig += "," + std::to_string(P.star[s].op[i]) + ":" + std::to_string(P.star[s].arg[i]);
+      sig.push_back(-7);
+      for (size_t i = 0; i < P.star[s].op.size(); ++i) {
+        sig.push_back(P.star[s].op[i]);
+        sig.push_back(P.star[s].arg[i]);
+      }
     }
-    sig += '|';
+    sig.push_back(-1);
     for (int c = 0; c < nc; ++c) {
       const StagedColumn& col = *P.segcols[s][c];
-      sig += std::to_string(S.bits[c]) + (S.remap[c] ? "r" : "") + ",";
-      if (want_img[c]) sig += "i" + std::to_string(col.img_kind) + "." + std::to_string(col.img_sh) + ",";
+      sig.push_back(S.bits[c] | (S.remap[c] ? 256 : 0));
+      if (want_img[c]) sig.push_back(col.img_kind * 64 + col.img_sh);
     }
-    if (!groups.count(sig)) order.push_back(sig);
-    groups[sig].push_back(s);
+    auto it = groups.find(sig);
+    if (it == groups.end()) {
+      it = groups.emplace(sig, std::vector<int>{}).first;
+      order.push_back(&it->first);
+    }
+    it->second.push_back(s);
   }
   const int cus = ctx->num_cus;
   size_t jidx = 0;  // next free JSeg slot of the arena
   size_t star_tile_off = 0;
   P.star_tiles.assign(n, {});
-  for (const std::string& sig : order) {
-    const std::vector<int>& members = groups[sig];
+  for (const std::vector<int32_t>* key : order) {
+    const std::vector<int>& members = groups[*key];
     const KSeg& S0 = P.ksegs[members[0]];
     JitShape J;
     J.cols.resize(nc);

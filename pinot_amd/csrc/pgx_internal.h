@@ -40,7 +40,8 @@ enum AggKind : int8_t { A_COUNT = 0, A_SUM = 1, A_MIN = 2, A_MAX = 3, A_AVG = 4 
 // Accumulator plane ops (pgx.h pgx_query_dense_plane_op)
 enum PlaneOp : int8_t { P_ADD_I64 = 0, P_ADD_F64 = 1, P_MIN_ORD = 2, P_MAX_ORD = 3 };
 
-enum GroupMode : int8_t { G_NONE = 0, G_DENSE_LDS = 1, G_DENSE_GLOBAL = 2, G_HASH64 = 3, G_HASH128 = 4 };
+enum GroupMode : int8_t { G_NONE = 0, G_DENSE_LDS = 1, G_DENSE_GLOBAL = 2, G_HASH64 = 3, G_HASH128 = 4,
+                          G_EMIT = 5 /* query kernels: emit key|value records for the partitioned group-by */ };
 
 struct KLeaf {
   int32_t lo, hi;
@@ -141,6 +142,10 @@ struct JitShape {
   std::vector<uint64_t> gmul;
   uint64_t dense_slots = 0;
   int num_planes = 1;
+  // G_EMIT: record = key (group ids at gshift) | value offset << keybits; emit_col = value column (-1: none)
+  std::vector<int> gshift;
+  int keybits = 0;
+  int emit_col = -1;
 };
 
 std::string jit_source(const JitShape& s, int* lds_bytes);

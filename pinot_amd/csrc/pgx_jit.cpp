@@ -81,7 +81,8 @@ std::string img_value(const JitShape& s, int c, const std::vector<int>& img_off,
 std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const int ncols = int(s.cols.size());
   const int U = 32 / s.R;
-  const bool grouped = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL;
+  const bool emit = s.group_mode == G_EMIT;
+  const bool grouped = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL || emit;
   // ---- LDS layout: images, then the dense group table ----
   std::vector<int> img_off(ncols, -1);
   int lds = 0;
@@ -397,6 +398,28 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         }
       }
     } else {
+      if (emit) {
+        // partitioned group-by: one record per row (~0 = not selected); key packing as the LONG_MAP raw key
+        // (DefaultGroupKeyGenerator.java:239-246: dictIds at fixed bit offsets)
+        e.ln("if (vj) {");
+        e.ind = 7;
+        e.ln("u64 rec = ~0ull;");
+        e.ln("if (m) {");
+        std::string key = "0ull";
+        for (size_t g = 0; g < s.gcol.size(); ++g) {
+          const int c = s.gcol[g];
+          std::string id = "v" + std::to_string(c) + "[j]";
+          if (s.cols[c].remap) id = "(u32)rm" + std::to_string(g) + "[" + id + "]";
+          key += " | ((u64)" + id + " << " + std::to_string(s.gshift[g]) + ")";
+        }
+        const std::string x = s.emit_col >= 0 ? img_value(s, s.emit_col, img_off, "v" + std::to_string(s.emit_col) + "[j]")
+                                              : std::string("0u");
+        e.ln("  rec = (", key, ") | ((u64)(", x, ") << ", s.keybits, ");");
+        e.ln("}");
+        e.ln("A.table[S->rec_base + r0 + j] = rec;");
+        e.ind = 6;
+        e.ln("}");
+      } else {
       // dense group-by: key = sum_g id_g * mul_g (column 0 least significant, DefaultGroupKeyGenerator.java:230-237)
       e.ln("if (m) {");
       e.ind = 7;
@@ -428,6 +451,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       }
       e.ind = 6;
       e.ln("}");
+      }
     }
     e.ind = 5;
     e.ln("}");
@@ -687,6 +711,27 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.prog_op = {OP_LEAF, OP_LEAF, OP_OR, OP_LEAF, OP_AND};
     s.prog_arg = {0, 1, 2, 2, 2};
     s.R = 16;
+    shapes.push_back(s);
+  }
+  {  // partitioned group-by records (C3 shape: g1 14 bits, g2 20 bits, value offsets of m)
+    JitShape s = base(14, 16, IMG_FOR16, 11);
+    s.cols.push_back(JitCol{});
+    s.cols[2].bits = 20;
+    s.cols[2].decode = true;
+    s.leaf_col.clear();
+    s.leaf_mode.clear();
+    s.prog_op.clear();
+    s.prog_arg.clear();
+    s.R = 8;
+    s.group_mode = G_EMIT;
+    s.gcol = {0, 2};
+    s.gshift = {0, 14};
+    s.keybits = 34;
+    s.emit_col = 1;
+    s.agg_kind = {A_SUM, A_MIN, A_MAX};
+    s.agg_col = {1, 1, 1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64, P_MIN_ORD, P_MAX_ORD};
+    s.num_planes = 4;
     shapes.push_back(s);
   }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {

@@ -24,6 +24,7 @@ struct JSeg {
   unsigned int llo[PGX_J_MAX_LEAVES];            // scan-interval leaves: lo <= id <= lo + lspan
   unsigned int lspan[PGX_J_MAX_LEAVES];
   int img_words[PGX_J_MAX_COLS];                 // dwords of img to stage into LDS
+  long long rec_base;                            // G_EMIT: index of this segment's row 0 in the record array
   const int* tiles;                              // optional: ascending local tile ids to visit (others hold no
                                                  // selected doc, e.g. outside every star-tree node range); 0 = all
 };

@@ -581,6 +581,156 @@ __global__ void __launch_bounds__(256) pgx_roaring_expand(const RDesc* __restric
   for (int i = tid; i < 2048; i += 256) out[i] = m[i];
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// High-cardinality group-by (LONG_MAP semantics, DefaultGroupKeyGenerator.java:239-246 / :429-441): the reference
+// probes a Long2IntOpenHashMap per doc; at 10^7 groups a device-wide hash table turns every row into random HBM atomics.
+// Instead the generated scan kernel emits one packed record per selected row (key | value << keybits), two radix
+// passes split the records into 64 x 128 partitions by hash bits, and one workgroup per partition aggregates it in an
+// LDS hash table, then appends its groups to compact output arrays.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t part_mix(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return x;
+}
+
+constexpr int kPartChunk = 8192;   // records per partitioning workgroup (64 KiB LDS staging)
+constexpr uint64_t kNoRecord = ~0ull;
+
+// Records of region r live at in + in_off[r], in_cnt[r] of them (in_cnt may be a device counter array); region r's
+// partition b goes to out + (r * nb + b) * cap, appended at cursor[r * nb + b].
+__global__ void __launch_bounds__(256) pgx_partition(const uint64_t* __restrict__ in, const int64_t* __restrict__ in_off,
+                                                     const unsigned long long* __restrict__ in_cnt, int nreg,
+                                                     int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
+                                                     int nbits, uint64_t* __restrict__ out, int64_t cap,
+                                                     unsigned long long* __restrict__ cursor,
+                                                     unsigned long long* __restrict__ overflow) {
+  const int r = static_cast<int>(blockIdx.x / chunks_per_reg);
+  const int64_t chunk = static_cast<int64_t>(blockIdx.x % chunks_per_reg);
+  if (r >= nreg) return;
+  const int64_t n = min(static_cast<int64_t>(in_cnt[r]), in_cap);
+  const int64_t c0 = chunk * kPartChunk;
+  if (c0 >= n) return;
+  const int cn = static_cast<int>(min<int64_t>(kPartChunk, n - c0));
+  const int nb = 1 << nbits;
+  __shared__ uint64_t stage[kPartChunk];
+  __shared__ uint8_t sb[kPartChunk];   // bucket of input record i (255: no record)
+  __shared__ uint8_t sbs[kPartChunk];  // bucket of staged (bucket-sorted) record i
+  __shared__ int hist[128], offs[128], fill[128];
+  __shared__ unsigned long long gpos[128];
+  const int tid = threadIdx.x;
+  if (tid < nb) { hist[tid] = 0; fill[tid] = 0; }
+  __syncthreads();
+  const uint64_t* src = in + in_off[r] + c0;
+  for (int i = tid; i < cn; i += 256) {
+    const uint64_t rec = src[i];
+    int b = -1;
+    if (rec != kNoRecord) {
+      b = static_cast<int>((part_mix(rec & keymask) >> shift) & static_cast<uint64_t>(nb - 1));
+      atomicAdd(&hist[b], 1);
+    }
+    sb[i] = static_cast<uint8_t>(b < 0 ? 255 : b);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int b = 0; b < nb; ++b) { offs[b] = acc; acc += hist[b]; }
+  }
+  if (tid < nb && hist[tid]) {
+    gpos[tid] = atomicAdd(&cursor[r * nb + tid], static_cast<unsigned long long>(hist[tid]));
+    if (gpos[tid] + hist[tid] > static_cast<unsigned long long>(cap)) atomicAdd(overflow, 1ull);
+  }
+  __syncthreads();
+  for (int i = tid; i < cn; i += 256) {
+    const int b = sb[i];
+    if (b == 255) continue;
+    const int pos = offs[b] + atomicAdd(&fill[b], 1);
+    stage[pos] = src[i];
+    sbs[pos] = static_cast<uint8_t>(b);
+  }
+  __syncthreads();
+  // copy out bucket runs: consecutive staged records of one bucket go to consecutive output words
+  int total = 0;
+  for (int b = 0; b < nb; ++b) total += hist[b];
+  for (int i = tid; i < total; i += 256) {
+    const int b = sbs[i];
+    const unsigned long long p = gpos[b] + static_cast<unsigned long long>(i - offs[b]);
+    if (p < static_cast<unsigned long long>(cap)) out[(static_cast<int64_t>(r) * nb + b) * cap + static_cast<int64_t>(p)] = stage[i];
+  }
+}
+
+// One workgroup aggregates one partition in an LDS hash table (linear probing, 64-bit CAS on the key) and appends its
+// groups to the output: okey[g] = packed key, oplane[p * ocap + g] = plane p in the library's plane encodings.
+constexpr int kAggSlots = 4096;
+
+__global__ void __launch_bounds__(512) pgx_part_aggregate(const uint64_t* __restrict__ in,
+                                                          const unsigned long long* __restrict__ in_cnt, int64_t cap,
+                                                          uint64_t keymask, int keybits, int64_t vbase, int need_sum,
+                                                          int need_min, int need_max, uint64_t* __restrict__ okey,
+                                                          uint64_t* __restrict__ oplane, int64_t ocap,
+                                                          unsigned long long* __restrict__ ocount,
+                                                          unsigned long long* __restrict__ overflow) {
+  __shared__ uint64_t tkey[kAggSlots];
+  __shared__ unsigned int tcnt[kAggSlots];
+  __shared__ unsigned long long tsum[kAggSlots];
+  __shared__ unsigned int tmin[kAggSlots], tmax[kAggSlots];
+  __shared__ int nfound;
+  __shared__ unsigned long long obase;
+  const int tid = threadIdx.x;
+  const int part = blockIdx.x;
+  for (int i = tid; i < kAggSlots; i += 512) {
+    tkey[i] = kNoRecord; tcnt[i] = 0u; tsum[i] = 0ull; tmin[i] = 0xFFFFFFFFu; tmax[i] = 0u;
+  }
+  if (tid == 0) nfound = 0;
+  __syncthreads();
+  const int64_t n = min(static_cast<int64_t>(in_cnt[part]), cap);
+  const uint64_t* src = in + static_cast<int64_t>(part) * cap;
+  bool lost = false;
+  for (int64_t i = tid; i < n; i += 512) {
+    const uint64_t rec = src[i];
+    const uint64_t key = rec & keymask;
+    const unsigned int v = static_cast<unsigned int>(rec >> keybits);
+    unsigned int h = static_cast<unsigned int>(part_mix(key)) & (kAggSlots - 1);
+    int probes = 0;
+    for (; probes < kAggSlots; ++probes) {
+      const uint64_t k = tkey[h];
+      if (k == key) break;
+      if (k == kNoRecord) {
+        const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[h]), kNoRecord, key);
+        if (prev == kNoRecord || prev == key) break;
+      }
+      h = (h + 1) & (kAggSlots - 1);
+    }
+    if (probes == kAggSlots) { lost = true; continue; }
+    atomicAdd(&tcnt[h], 1u);
+    if (need_sum) atomicAdd(&tsum[h], static_cast<unsigned long long>(v));
+    if (need_min) atomicMin(&tmin[h], v);
+    if (need_max) atomicMax(&tmax[h], v);
+  }
+  if (lost) atomicAdd(overflow, 1ull);
+  __syncthreads();
+  // compact: count, reserve once, write
+  int mine = 0;
+  for (int i = tid; i < kAggSlots; i += 512) mine += tkey[i] != kNoRecord;
+  const int before = atomicAdd(&nfound, mine);
+  __syncthreads();
+  if (tid == 0) obase = atomicAdd(ocount, static_cast<unsigned long long>(nfound));
+  __syncthreads();
+  unsigned long long o = obase + static_cast<unsigned long long>(before);
+  for (int i = tid; i < kAggSlots; i += 512) {
+    if (tkey[i] == kNoRecord) continue;
+    if (o >= static_cast<unsigned long long>(ocap)) { atomicAdd(overflow, 1ull); continue; }
+    okey[o] = tkey[i];
+    const unsigned long long c = tcnt[i];
+    oplane[o] = c;  // plane 0: doc count
+    // planes 1..3: sum (int64), min, max (ordered encodings of the int64 value), in this fixed order
+    oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(tsum[i]) + static_cast<int64_t>(c) * vbase);
+    oplane[2 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(tmin[i])) ^ 0x8000000000000000ull;
+    oplane[3 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(tmax[i])) ^ 0x8000000000000000ull;
+    ++o;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Synthetic forward-index generator (benchmarks): dictId(row) = splitmix64(seed ^ row*golden) % card, packed
 // MSB-first big-endian.  One thread writes one 32-bit big-endian word = the 32 rows' bits that fall in it.
@@ -695,5 +845,28 @@ extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, in
   if (blocks > 0x7FFFFFFFll) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pgx::pgx_roaring_expand, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, descs, npairs,
                      maxchunks);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
+                                           int nreg, int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
+                                           int nbits, uint64_t* out, int64_t cap, unsigned long long* cursor,
+                                           unsigned long long* overflow, hipStream_t stream) {
+  const long long blocks = static_cast<long long>(nreg) * chunks_per_reg;
+  if (blocks <= 0) return hipSuccess;
+  if (blocks > 0x7FFFFFFFll || nbits > 7) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pgx::pgx_partition, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, in, in_off, in_cnt,
+                     nreg, in_cap, chunks_per_reg, keymask, shift, nbits, out, cap, cursor, overflow);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int nparts,
+                                                int64_t cap, uint64_t keymask, int keybits, int64_t vbase, int need_sum,
+                                                int need_min, int need_max, uint64_t* okey, uint64_t* oplane,
+                                                int64_t ocap, unsigned long long* ocount,
+                                                unsigned long long* overflow, hipStream_t stream) {
+  if (nparts <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pgx::pgx_part_aggregate, dim3(nparts), dim3(512), 0, stream, in, in_cnt, cap, keymask, keybits,
+                     vbase, need_sum, need_min, need_max, okey, oplane, ocap, ocount, overflow);
   return hipGetLastError();
 }
