@@ -165,6 +165,8 @@ typedef struct {
 
 #define PGX_X_KEEP_DENSE_ON_DEVICE 0x1u /* leave the dense table in dense_out; do not compact to host */
 #define PGX_X_FORCE_HASH 0x2u           /* testing: use the hash group-by path even for small key spaces */
+#define PGX_X_NO_PARTITION 0x4u         /* testing: sparse group-by through the global hash table, not the partitioned
+                                           record path (pgx_host.cpp run_partitioned) */
 
 /* Execute the query over n segments on the context's device and merge the per-segment partials
  * (the combine).  bindings is [n][num_leaves].  Synchronous w.r.t. the returned result. */

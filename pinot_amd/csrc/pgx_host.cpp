@@ -37,6 +37,17 @@ extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64
 extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
 extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
                                        int64_t n_words, uint64_t pair_seed, uint32_t npairs, hipStream_t stream);
+extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
+                                           int nreg, int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
+                                           int nbits, uint64_t* out, int64_t cap, unsigned long long* cursor,
+                                           unsigned long long* overflow, hipStream_t stream);
+extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int nparts,
+                                                int64_t cap, uint64_t keymask, int keybits, int64_t vbase, int need_sum,
+                                                int need_min, int need_max, uint64_t* okey, uint64_t* oplane,
+                                                int64_t ocap, unsigned long long* ocount,
+                                                unsigned long long* overflow, hipStream_t stream);
+struct pgx_ctx;
+extern "C" void ctx_unref(pgx_ctx* ctx);
 
 using namespace pgx;
 
@@ -557,6 +568,22 @@ struct pgx_result {
   std::vector<std::vector<int32_t>> key_seg, key_id;  // [col][group]
   std::vector<std::vector<double>> g_value;          // [fn][group]
   std::vector<std::vector<int64_t>> g_count;         // [fn][group]
+  // Partitioned group-by (run_partitioned): the groups stay in device memory until an accessor needs them.
+  struct Lazy {
+    pgx_ctx* ctx = nullptr;      // holds a context reference (the result may outlive the caller's handle)
+    DevBuf okey, oplane;         // packed keys; planes [count, sum, min, max] x ocap
+    int64_t ocap = 0;
+    std::vector<int> gshift, gbits;
+    std::vector<std::vector<int32_t>> rep_seg, rep_id;  // [col][global id]
+    std::vector<int> agg_kind;
+    ~Lazy() {
+      okey.reset();
+      oplane.reset();
+      if (ctx) ctx_unref(ctx);
+    }
+  };
+  std::unique_ptr<Lazy> lazy;
+  void materialize();
 };
 
 namespace {
@@ -779,6 +806,15 @@ struct ExecPlan {
   int64_t tiles_per_wg = 0;
   size_t lds_bytes = 0;
   // query-specialised kernels (pgx_jit.cpp): one launch per group of segments sharing a shape
+  // partitioned group-by (G_HASH64 keys, one integer value column; run_partitioned)
+  bool use_part = false;
+  int part_vcol = -1;            // query column slot of the aggregated value (-1: COUNT only)
+  int part_keybits = 0;
+  int part_vbits = 0;
+  int64_t part_vbase = 0;
+  bool part_sum = false, part_min = false, part_max = false;
+  std::vector<int64_t> rec_base; // per segment: index of its row 0 in the record array
+  int64_t rec_total = 0;
   struct JitGroup {
     void* fn = nullptr;
     int T = 256;
@@ -791,6 +827,11 @@ struct ExecPlan {
 
 bool jit_enabled() {
   const char* e = std::getenv("PGX_JIT");
+  return !(e && e[0] == '0');
+}
+
+bool part_enabled() {
+  const char* e = std::getenv("PGX_PART");
   return !(e && e[0] == '0');
 }
 
@@ -1047,6 +1088,57 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   }
   K.num_qcols = int(P.qcols.size());
 
+  // Partitioned group-by: sparse 64-bit keys go through record-emitting query kernels, radix partitioning and LDS
+  // aggregation (run_partitioned) instead of one global hash table.  Eligible when every non-COUNT function reads the
+  // same INT/LONG column whose dictionary is identical in every segment (one value base), with a value range of at
+  // most 32 bits, and key + value fit 63 bits.
+  P.use_part = false;
+  if (K.group_mode == G_HASH64 && jit_enabled() && part_enabled() && !(xflags & PGX_X_NO_PARTITION) &&
+      K.num_qcols <= PGX_J_MAX_COLS) {
+    int vc = -1;
+    bool ok = true;
+    bool need_sum = false, need_min = false, need_max = false;
+    for (int a = 0; a < K.num_aggs && ok; ++a) {
+      const int k = K.agg_kind[a];
+      if (k == A_COUNT) continue;
+      if (K.agg_fp[a] || (vc >= 0 && vc != K.agg_col[a])) ok = false;
+      vc = K.agg_col[a];
+      need_sum |= k == A_SUM || k == A_AVG;
+      need_min |= k == A_MIN;
+      need_max |= k == A_MAX;
+    }
+    int keybits = 0;
+    for (int g = 0; g < K.num_gcols; ++g) keybits = std::max(keybits, K.gshift[g] + P.gbits[g]);
+    int vbits = 0;
+    int64_t vbase = 0;
+    if (ok && vc >= 0) {
+      const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
+      ok = (c0.data_type == PGX_INT || c0.data_type == PGX_LONG) && !c0.ivals.empty();
+      for (int s = 1; s < n && ok; ++s) {
+        const StagedColumn& c = segs[s]->col(P.qcols[vc]);
+        ok = c.dict_hash == c0.dict_hash && c.card == c0.card && c.data_type == c0.data_type;
+      }
+      if (ok) {
+        const int64_t vmin = *std::min_element(c0.ivals.begin(), c0.ivals.end());
+        const int64_t vmax = *std::max_element(c0.ivals.begin(), c0.ivals.end());
+        const uint64_t range = uint64_t(vmax) - uint64_t(vmin);
+        ok = range <= 0xFFFFFFFFull && c0.vbase == vmin;
+        vbase = vmin;
+        vbits = ok ? bits_for(int64_t(range) + 1) : 64;
+      }
+    }
+    if (ok && keybits + vbits <= 63) {
+      P.use_part = true;
+      P.part_vcol = vc;
+      P.part_keybits = keybits;
+      P.part_vbits = vbits;
+      P.part_vbase = vbase;
+      P.part_sum = need_sum;
+      P.part_min = need_min;
+      P.part_max = need_max;
+    }
+  }
+
   // filter program
   P.host_entries = 0;
   int host_scan_leaves = 0;
@@ -1064,7 +1156,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     }
   }
   P.use_docmask = jit_enabled() && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
-                                    K.group_mode == G_DENSE_GLOBAL) && K.num_qcols <= PGX_J_MAX_COLS;
+                                    K.group_mode == G_DENSE_GLOBAL || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS;
   P.roar.clear();
   P.roar_index.assign(n, std::vector<int>(q.leaf_col.size(), -1));
   P.mask_words = 0;
@@ -1184,7 +1276,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   }
   // star-tree segments (query kernels only: the per-segment program needs the generated kernels)
   P.star.assign(n, ExecPlan::StarPlan{});
-  if (P.use_docmask && int(q.leaf_col.size()) + 8 <= PGX_J_MAX_LEAVES) {
+  if (P.use_docmask && !P.use_part && int(q.leaf_col.size()) + 8 <= PGX_J_MAX_LEAVES) {
     tiles = 0;
     for (int s = 0; s < n; ++s) {
       KSeg& S = P.ksegs[s];
@@ -1205,6 +1297,12 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   }
   K.total_tiles = tiles;
   K.num_segs = n;
+  P.rec_base.assign(n, 0);
+  P.rec_total = 0;
+  for (int s = 0; s < n; ++s) {
+    P.rec_base[s] = P.rec_total;
+    P.rec_total += P.ksegs[s].num_docs;
+  }
 
   // grid: persistent, contiguous tile ranges per workgroup
   const int cus = ctx->num_cus;
@@ -1289,6 +1387,9 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
       B.table = DevBuf(ctx, bytes);
       K.table = devp(B.table);
     }
+  } else if (P.use_part) {
+    B.table = DevBuf(ctx, std::max<int64_t>(P.rec_total, 1) * 8);  // one key|value record per scanned row
+    K.table = devp(B.table);
   } else if (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) {
     K.hash_cap = P.hash_cap;
     B.table = DevBuf(ctx, P.hash_cap * K.num_planes * 8);
@@ -1310,7 +1411,7 @@ void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st) {
   std::memset(outs, 0, kOutsBytes);
   for (int p = 1; p < K.num_planes; ++p) outs[p] = (K.plane_op[p] == P_MIN_ORD) ? ~0ull : 0ull;
   hip_check(hipMemcpyAsync(B.arena.p, B.host.p, B.size, hipMemcpyHostToDevice, st), "argument arena H2D");
-  if (K.group_mode != G_NONE) {
+  if (K.group_mode != G_NONE && !P.use_part) {
     const uint64_t slots = (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) ? P.hash_cap : P.dense_slots;
     const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : (K.group_mode == G_HASH64 ? P.hash_cap : 0);
     hip_check(pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
@@ -1325,7 +1426,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
   P.jit.clear();
   const KQuery& K = P.kq;
   if (!jit_enabled()) return;
-  if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL)) return;
+  if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL || P.use_part)) return;
   const int nc = K.num_qcols;
   if (nc > PGX_J_MAX_COLS) return;
   const bool grouped = K.group_mode != G_NONE;
@@ -1449,10 +1550,15 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     }
     for (int p = 0; p < K.num_planes; ++p) J.plane_op.push_back(K.plane_op[p]);
     J.num_planes = K.num_planes;
-    J.group_mode = K.group_mode;
+    J.group_mode = P.use_part ? int(G_EMIT) : int(K.group_mode);
     for (int g = 0; g < K.num_gcols; ++g) {
       J.gcol.push_back(K.gcol[g]);
       J.gmul.push_back(K.gmul[g]);
+      J.gshift.push_back(K.gshift[g]);
+    }
+    if (P.use_part) {
+      J.keybits = P.part_keybits;
+      J.emit_col = P.part_vcol;
     }
     J.dense_slots = P.dense_slots;
 
@@ -1470,6 +1576,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       JSeg js{};
       js.tile_begin = tiles;
       js.num_docs = S.num_docs;
+      js.rec_base = P.rec_base[s];
       if (P.star[s].on) {
         // visit only the tiles that intersect a star-tree range: every selected doc lies in one
         auto& tl = P.star_tiles[s];
@@ -1684,6 +1791,209 @@ uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {
   return cap;
 }
 
+// -------------------------------------------------------------------------------------------------
+// Partitioned group-by (DESIGN.md "Sparse group-by").  The query kernel writes one 8-byte record per scanned row,
+// key | (value - vbase) << keybits (~0: row not selected).  Two radix passes on independent bits of a 64-bit mix of
+// the key (64 buckets, then 2^nbits2 per bucket) split the records into partitions whose groups fit one workgroup's
+// LDS hash table; pgx_part_aggregate aggregates each partition and appends its groups.  Each pass reads the previous
+// pass's cursors on the device, so the chain runs without a host round trip until the final counters.
+// Replaces, for sparse keys, the reference's per-segment MAP-based group-key holders
+// (DefaultGroupKeyGenerator.java:239-343 LONG_MAP / ARRAY_MAP) with a layout that streams HBM instead of probing it.
+// -------------------------------------------------------------------------------------------------
+constexpr int kPart1Bits = 6;           // first pass: 64 buckets (top bits of the mix)
+constexpr int64_t kPartGroupsPerWg = 2800;  // groups one pgx_part_aggregate workgroup holds comfortably (4096 slots)
+constexpr uint64_t kPartMaxBytes = uint64_t(96) << 30;  // partition buffers beyond this: fall back to the hash table
+
+struct PartBuffers {
+  int nbits2 = 7;                       // second pass: 2^nbits2 buckets per first-pass bucket (0: no second pass)
+  int64_t cap1 = 0, cap2 = 0, ocap = 0;
+  DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[64] | cursors2[nparts] | ocount | overflow[3]
+  int64_t nparts() const { return int64_t(1) << (kPart1Bits + nbits2); }
+  size_t ctr_words() const { return size_t(64 + (nbits2 ? nparts() : 0) + 4); }
+};
+
+// PGX_PART_DEBUG=1 (tests): start from undersized buckets and one pass, and allow at most one refinement, so the
+// resize, re-split and hash-table fallback branches run at small row counts.
+bool part_debug() {
+  const char* e = std::getenv("PGX_PART_DEBUG");
+  return e && e[0] == '1';
+}
+
+void part_size(const ExecPlan& P, PartBuffers& PB) {
+  const int64_t N = P.rec_total;
+  double ub = double(N);  // groups: at most the rows and the product of the key cardinalities
+  double prod = 1;
+  for (const auto& g : P.gdicts) prod *= double(g.card);
+  ub = std::min(ub, prod);
+  PB.nbits2 = 0;
+  while (PB.nbits2 < 7 && double(int64_t(1) << (kPart1Bits + PB.nbits2)) * kPartGroupsPerWg < ub) ++PB.nbits2;
+  PB.cap1 = N / 64 + N / 512 + 65536;
+  const int64_t np = PB.nparts();
+  PB.cap2 = N / np + N / np / 4 + 16384;
+  if (part_debug()) {
+    PB.nbits2 = 0;
+    PB.cap1 = N / 256 + 1;
+    PB.cap2 = 1;
+  }
+}
+
+bool part_alloc(pgx_ctx* ctx, const ExecPlan& P, PartBuffers& PB) {
+  const int64_t np = PB.nparts();
+  PB.ocap = std::max<int64_t>(1, std::min<int64_t>(P.rec_total, np * 4096));
+  const uint64_t bytes = uint64_t(64) * PB.cap1 * 8 + (PB.nbits2 ? uint64_t(np) * PB.cap2 * 8 : 0) + uint64_t(PB.ocap) * 40;
+  if (bytes > kPartMaxBytes) return false;
+  PB.out1 = DevBuf(ctx, size_t(64) * PB.cap1 * 8);
+  if (PB.nbits2) PB.out2 = DevBuf(ctx, size_t(np) * PB.cap2 * 8);
+  PB.okey = DevBuf(ctx, size_t(PB.ocap) * 8);
+  PB.oplane = DevBuf(ctx, size_t(PB.ocap) * 4 * 8);
+  PB.ctr = DevBuf(ctx, PB.ctr_words() * 8);
+  return true;
+}
+
+void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
+  const int64_t N = P.rec_total;
+  unsigned long long* ctr = devp(PB.ctr);
+  const int64_t np = PB.nparts();
+  unsigned long long* c1 = ctr;
+  unsigned long long* c2 = ctr + 64;
+  unsigned long long* tail = ctr + PB.ctr_words() - 4;  // ocount, overflow[3]
+  hip_check(hipMemsetAsync(ctr, 0, PB.ctr_words() * 8, st), "partition counters");
+  if (N == 0) return;
+  const uint64_t keymask = (uint64_t(1) << P.part_keybits) - 1u;
+  const uint64_t* recs = reinterpret_cast<const uint64_t*>(P.kq.table);
+  const int64_t chunks1 = (N + 8191) / 8192;
+  if (chunks1 > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
+  hip_check(pgx_launch_partition(recs, nullptr, nullptr, 1, N, int(chunks1), keymask, 64 - kPart1Bits, kPart1Bits,
+                                 PB.out1.as<uint64_t>(), PB.cap1, c1, tail + 1, st),
+            "partition pass 1");
+  const uint64_t* ain = PB.out1.as<uint64_t>();
+  const unsigned long long* acnt = c1;
+  int64_t acap = PB.cap1;
+  int aparts = 64;
+  if (PB.nbits2) {
+    const int64_t chunks2 = (PB.cap1 + 8191) / 8192;
+    hip_check(pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, 64, PB.cap1, int(chunks2), keymask,
+                                   64 - kPart1Bits - PB.nbits2, PB.nbits2, PB.out2.as<uint64_t>(), PB.cap2, c2,
+                                   tail + 2, st),
+              "partition pass 2");
+    ain = PB.out2.as<uint64_t>();
+    acnt = c2;
+    acap = PB.cap2;
+    aparts = int(np);
+  }
+  hip_check(pgx_launch_part_aggregate(ain, acnt, aparts, acap, keymask, P.part_keybits, P.part_vbase, P.part_sum,
+                                      P.part_min, P.part_max, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(),
+                                      PB.ocap, tail, tail + 3, st),
+            "partition aggregate");
+}
+
+// Scan (records), partition passes and aggregation; grows the buffers to the measured bucket sizes when a pass
+// overflowed.  False: the groups do not fit the partitioned layout (the caller uses the global hash table).
+bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB, hipStream_t st) {
+  alloc_outputs(ctx, P, B, nullptr, 0);
+  reset_outputs(P, B, st);
+  launch_scan(P, st);
+  part_size(P, PB);
+  for (int attempt = 0; attempt < 12; ++attempt) {
+    if (!part_alloc(ctx, P, PB)) return false;
+    part_enqueue(P, PB, st);
+    unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
+    unsigned long long* tail = outs + 28;  // spare words of the outputs block
+    hip_check(hipMemcpyAsync(tail, devp(PB.ctr) + PB.ctr_words() - 4, 32, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    if (!tail[1] && !tail[2] && !tail[3]) return true;
+    std::vector<unsigned long long> c(PB.ctr_words());
+    hip_check(hipMemcpy(c.data(), PB.ctr.p, c.size() * 8, hipMemcpyDeviceToHost), "counters D2H");
+    if (tail[1]) {  // a first-pass bucket overflowed: size to the largest (cursors count every record)
+      PB.cap1 = int64_t(*std::max_element(c.begin(), c.begin() + 64)) + 1024;
+      continue;
+    }
+    if (tail[2]) {
+      PB.cap2 = int64_t(*std::max_element(c.begin() + 64, c.begin() + 64 + PB.nparts())) + 1024;
+      continue;
+    }
+    if (PB.nbits2 == (part_debug() ? 1 : 7)) return false;  // an LDS table overflowed at the finest split
+    ++PB.nbits2;
+    const int64_t np = PB.nparts();
+    PB.cap2 = P.rec_total / np + P.rec_total / np / 4 + (part_debug() ? 1 : 16384);
+  }
+  return false;
+}
+
+}  // namespace
+
+// Read the partitioned group-by's groups back and decode them into the columnar host result.
+void pgx_result::materialize() {
+  if (!lazy) return;
+  std::unique_ptr<Lazy> L = std::move(lazy);
+  const int64_t ng = num_groups;
+  hip_check(hipSetDevice(L->ctx->device), "hipSetDevice");
+  std::vector<uint64_t> keys(ng), pl(size_t(4) * ng);
+  if (ng) {
+    hip_check(hipMemcpy(keys.data(), L->okey.p, ng * 8, hipMemcpyDeviceToHost), "group keys D2H");
+    for (int p = 0; p < 4; ++p)
+      hip_check(hipMemcpy(pl.data() + p * ng, L->oplane.as<uint64_t>() + p * L->ocap, ng * 8, hipMemcpyDeviceToHost),
+                "group planes D2H");
+  }
+  const int ncols = int(L->gshift.size());
+  key_seg.assign(ncols, std::vector<int32_t>(ng));
+  key_id.assign(ncols, std::vector<int32_t>(ng));
+  for (int g = 0; g < ncols; ++g) {
+    const uint64_t mask = (uint64_t(1) << L->gbits[g]) - 1u;
+    for (int64_t i = 0; i < ng; ++i) {
+      const uint64_t gid = (keys[i] >> L->gshift[g]) & mask;
+      key_seg[g][i] = L->rep_seg[g][gid];
+      key_id[g][i] = L->rep_id[g][gid];
+    }
+  }
+  const int na = int(L->agg_kind.size());
+  g_value.assign(na, std::vector<double>(ng));
+  g_count.assign(na, std::vector<int64_t>(ng));
+  for (int a = 0; a < na; ++a) {
+    const int k = L->agg_kind[a];
+    // planes: 0 count, 1 int64 sum, 2 ordered min, 3 ordered max (pgx_part_aggregate)
+    const int p = k == A_COUNT ? 0 : (k == A_MIN ? 2 : (k == A_MAX ? 3 : 1));
+    const int op = k == A_MIN ? P_MIN_ORD : (k == A_MAX ? P_MAX_ORD : P_ADD_I64);
+    for (int64_t i = 0; i < ng; ++i) {
+      g_count[a][i] = int64_t(pl[i]);
+      g_value[a][i] = decode_plane(op, false, pl[size_t(p) * ng + i], k);
+    }
+  }
+}
+
+namespace {
+
+void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, PartBuffers& PB, pgx_result* R) {
+  const unsigned long long* outs = reinterpret_cast<const unsigned long long*>(B.host.bytes() + B.off_outs);
+  const unsigned long long* stats = outs + 16;
+  const KQuery& K = P.kq;
+  R->stats[0] = int64_t(stats[0]);
+  R->stats[1] = int64_t(stats[1]) + P.host_entries;
+  R->stats[2] = int64_t(stats[0]) * P.n_proj;
+  R->stats[3] = P.total_raw;
+  R->num_aggs = K.num_aggs;
+  R->agg_fn = q.agg_fn;
+  R->top_n = q.top_n;
+  R->group_by = true;
+  R->mode = P.mode_ref;
+  R->num_groups = int64_t(std::min<unsigned long long>(outs[28], uint64_t(PB.ocap)));
+  auto L = std::make_unique<pgx_result::Lazy>();
+  L->okey = std::move(PB.okey);
+  L->oplane = std::move(PB.oplane);
+  L->ocap = PB.ocap;
+  for (int g = 0; g < K.num_gcols; ++g) {
+    L->gshift.push_back(K.gshift[g]);
+    L->gbits.push_back(P.gbits[g]);
+    L->rep_seg.push_back(std::move(P.gdicts[g].rep_seg));
+    L->rep_id.push_back(std::move(P.gdicts[g].rep_id));
+  }
+  for (int a = 0; a < K.num_aggs; ++a) L->agg_kind.push_back(K.agg_kind[a]);
+  ctx->refs.fetch_add(1);
+  L->ctx = ctx;
+  R->lazy = std::move(L);
+}
+
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                const pgx_exec_opts* opts, pgx_result* R) {
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
@@ -1693,6 +2003,15 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   ExecBuffers B;
   upload_plan(ctx, P, B, st);
   plan_jit(ctx, q, segs, n, P, B);
+  if (P.use_part) {
+    PartBuffers PB;
+    if (run_partitioned(ctx, P, B, PB, st)) {
+      part_result(ctx, q, P, B, PB, R);
+      return;
+    }
+    P.use_part = false;  // groups too many or too skewed for the partitions: global hash table, generic kernel
+    P.jit.clear();
+  }
   const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
   if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
   for (int attempt = 0; attempt < 6; ++attempt) {
@@ -1888,6 +2207,7 @@ pgx_status pgx_result_num_groups(const pgx_result* r, int64_t* n) {
 pgx_status pgx_result_group_keys(const pgx_result* r, int32_t c, int32_t* seg_index, int32_t* dict_id) {
   return guarded([&] {
     if (!r || !r->group_by) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
+    const_cast<pgx_result*>(r)->materialize();
     if (c < 0 || c >= int(r->key_seg.size())) fail(PGX_ERR_INVALID_ARG, "group column index");
     if (seg_index) std::memcpy(seg_index, r->key_seg[c].data(), r->num_groups * 4);
     if (dict_id) std::memcpy(dict_id, r->key_id[c].data(), r->num_groups * 4);
@@ -1898,6 +2218,7 @@ pgx_status pgx_result_group_values(const pgx_result* r, int32_t fn, double* valu
   return guarded([&] {
     if (!r || !r->group_by) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
     if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
+    const_cast<pgx_result*>(r)->materialize();
     if (value) std::memcpy(value, r->g_value[fn].data(), r->num_groups * 8);
     if (count) std::memcpy(count, r->g_count[fn].data(), r->num_groups * 8);
   });
@@ -1914,6 +2235,7 @@ pgx_status pgx_result_trim(const pgx_result* r, int32_t fn, int64_t* idx, int64_
   return guarded([&] {
     if (!r || !r->group_by || !n) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
     if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
+    const_cast<pgx_result*>(r)->materialize();
     const int64_t min_trim = std::max<int64_t>(r->top_n, 1000);
     const int64_t threshold = min_trim * 20, size = min_trim * 5;
     std::vector<int64_t> order(r->num_groups);
@@ -2150,9 +2472,14 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     ExecBuffers B;
     upload_plan(ctx, P, B, st);
     plan_jit(ctx, *q, segs, n, P, B);
+    PartBuffers PB;
+    if (P.use_part && !run_partitioned(ctx, P, B, PB, st)) {  // untimed: settles the partition sizes
+      P.use_part = false;
+      P.jit.clear();
+    }
     const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
-    if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
-    alloc_outputs(ctx, P, B, nullptr, 0);
+    if (hash && !P.use_part) P.hash_cap = initial_hash_cap(segs, n, P);
+    if (!P.use_part) alloc_outputs(ctx, P, B, nullptr, 0);
     std::vector<hipEvent_t> ev(2 * iters);
     for (auto& e : ev) hip_check(hipEventCreate(&e), "event");
     hipEvent_t t0, t1;
@@ -2163,6 +2490,7 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
       reset_outputs(P, B, st);
       hip_check(hipEventRecord(ev[2 * i], st), "record");
       launch_scan(P, st);
+      if (P.use_part) part_enqueue(P, PB, st);
       hip_check(hipEventRecord(ev[2 * i + 1], st), "record");
     }
     hip_check(hipEventRecord(t1, st), "record");
@@ -2181,7 +2509,15 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     if (kernel_ms) *kernel_ms = k / iters;
     if (out) {
       auto R = std::make_unique<pgx_result>();
-      finish_result(ctx, *q, P, B, segs, n, st, R.get(), nullptr);
+      if (P.use_part) {
+        unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+        hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
+        hip_check(hipMemcpyAsync(outs + 28, devp(PB.ctr) + PB.ctr_words() - 4, 32, hipMemcpyDeviceToHost, st), "D2H");
+        hip_check(hipStreamSynchronize(st), "sync");
+        part_result(ctx, *q, P, B, PB, R.get());
+      } else {
+        finish_result(ctx, *q, P, B, segs, n, st, R.get(), nullptr);
+      }
       *out = R.release();
     }
   });

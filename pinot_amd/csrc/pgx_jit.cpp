@@ -412,8 +412,12 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
           if (s.cols[c].remap) id = "(u32)rm" + std::to_string(g) + "[" + id + "]";
           key += " | ((u64)" + id + " << " + std::to_string(s.gshift[g]) + ")";
         }
-        const std::string x = s.emit_col >= 0 ? img_value(s, s.emit_col, img_off, "v" + std::to_string(s.emit_col) + "[j]")
-                                              : std::string("0u");
+        std::string x = "0u";
+        if (s.emit_col >= 0) {
+          const std::string ec = std::to_string(s.emit_col);
+          x = s.cols[s.emit_col].img != IMG_NONE ? img_value(s, s.emit_col, img_off, "v" + ec + "[j]")
+                                                 : "(u32)(di" + ec + "[v" + ec + "[j]] - S->vbase[" + ec + "])";
+        }
         e.ln("  rec = (", key, ") | ((u64)(", x, ") << ", s.keybits, ");");
         e.ln("}");
         e.ln("A.table[S->rec_base + r0 + j] = rec;");
@@ -732,6 +736,9 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.agg_col = {1, 1, 1};
     s.plane_op = {P_ADD_I64, P_ADD_I64, P_MIN_ORD, P_MAX_ORD};
     s.num_planes = 4;
+    shapes.push_back(s);
+    s.cols[1].img = IMG_NONE;  // value image demoted (LDS budget): values from the HBM dictionary
+    s.cols[2].remap = true;
     shapes.push_back(s);
   }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {

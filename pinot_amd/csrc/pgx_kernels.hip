@@ -597,7 +597,8 @@ __device__ __forceinline__ uint64_t part_mix(uint64_t x) {
 constexpr int kPartChunk = 8192;   // records per partitioning workgroup (64 KiB LDS staging)
 constexpr uint64_t kNoRecord = ~0ull;
 
-// Records of region r live at in + in_off[r], in_cnt[r] of them (in_cnt may be a device counter array); region r's
+// Records of region r live at in + in_off[r] (in_off null: r * in_cap), in_cnt[r] of them (in_cnt null: in_cap; else
+// typically the previous pass's cursors, read on the device, so passes chain without a host round trip); region r's
 // partition b goes to out + (r * nb + b) * cap, appended at cursor[r * nb + b].
 __global__ void __launch_bounds__(256) pgx_partition(const uint64_t* __restrict__ in, const int64_t* __restrict__ in_off,
                                                      const unsigned long long* __restrict__ in_cnt, int nreg,
@@ -608,7 +609,7 @@ __global__ void __launch_bounds__(256) pgx_partition(const uint64_t* __restrict_
   const int r = static_cast<int>(blockIdx.x / chunks_per_reg);
   const int64_t chunk = static_cast<int64_t>(blockIdx.x % chunks_per_reg);
   if (r >= nreg) return;
-  const int64_t n = min(static_cast<int64_t>(in_cnt[r]), in_cap);
+  const int64_t n = in_cnt ? min(static_cast<int64_t>(in_cnt[r]), in_cap) : in_cap;
   const int64_t c0 = chunk * kPartChunk;
   if (c0 >= n) return;
   const int cn = static_cast<int>(min<int64_t>(kPartChunk, n - c0));
@@ -621,7 +622,7 @@ __global__ void __launch_bounds__(256) pgx_partition(const uint64_t* __restrict_
   const int tid = threadIdx.x;
   if (tid < nb) { hist[tid] = 0; fill[tid] = 0; }
   __syncthreads();
-  const uint64_t* src = in + in_off[r] + c0;
+  const uint64_t* src = in + (in_off ? in_off[r] : static_cast<int64_t>(r) * in_cap) + c0;
   for (int i = tid; i < cn; i += 256) {
     const uint64_t rec = src[i];
     int b = -1;

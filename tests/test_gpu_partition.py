@@ -1,0 +1,159 @@
+"""GPU parity of the partitioned sparse group-by (pgx_host.cpp run_partitioned: record-emitting query kernel, two
+radix passes, per-partition LDS aggregation) for LONG_MAP-sized key spaces: against the oracle, against the global
+hash-table path (PGX_X_NO_PARTITION), across segments with different group dictionaries, and through its resize /
+re-split / fallback branches (PGX_PART_DEBUG=1 starts from undersized buckets and a single pass)."""
+import numpy as np
+import pytest
+
+from pinot_amd import pql
+from tests import helpers as H
+from tests.test_gpu_parity import FILTERS, _rand_segment, _run_inner
+
+pytestmark = pytest.mark.gpu
+
+AGGS = "SELECT COUNT(*), SUM(m), MIN(m), MAX(m), AVG(m) FROM t"
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from pinot_amd import engine as E
+    c = E.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def seg(ctx):
+    from pinot_amd import engine as E
+    rng = np.random.default_rng(21)
+    n = 8192 * 5 + 333
+    raw = _rand_segment(rng, n, {"a": 3000, "b": 40, "c": 700, "s": 6, "g1": 13, "g2": 900, "m": 5000}, "p",
+                        sorted_col="s")
+    seg, oseg = H.build_pair("p", raw, inverted=("b", "c"))
+    fmt = {"b0": int(np.unique(raw["b"])[0]), "b1": int(np.unique(raw["b"])[5]), "b2": int(np.unique(raw["b"])[9]),
+           "s0": int(np.unique(raw["s"])[1]), "s1": int(np.unique(raw["s"])[4])}
+    return E.IndexSegment(ctx, seg), oseg, fmt
+
+
+def _map(blk):
+    g = blk.get_aggregation_group_by_result()
+    return g.as_map() if g is not None else {}
+
+
+def _execute(ctx, segs, q, flags):
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    qq = E._Query(ctx, q)
+    r = qq.execute(segs, flags=flags)
+    try:
+        return E.decode_result(qq, r, segs)
+    finally:
+        N.lib().pgx_result_release(r)
+
+
+@pytest.mark.parametrize("flt", FILTERS)
+@pytest.mark.parametrize("group", [" GROUP BY g2, a, c", " GROUP BY a, c, g1", " GROUP BY c, g2, s, g1"])
+def test_partitioned_matches_oracle(ctx, seg, flt, group):
+    gseg, oseg, fmt = seg
+    q = pql.compile(AGGS + (flt % fmt) + group)
+    blk, st = _run_inner(ctx, gseg, q)
+    o = H.oracle_answer([oseg], q, literal=True)
+    s = st.as_list()
+    assert s[0] == o["stats"][0] and s[2] == o["stats"][2] and s[3] == o["stats"][3]
+    gr = blk.get_aggregation_group_by_result()
+    m = gr.as_map() if gr is not None else {}
+    assert set(m) == set(o["map"])
+    fns = [a["fn"] for a in q["aggregations"]]
+    for k, v in o["map"].items():
+        H.assert_values_equal(m[k], v, fns)
+    if gr is not None:
+        assert gr.storage_mode == o["mode"]
+
+
+@pytest.mark.parametrize("text", [
+    AGGS + " GROUP BY g2, a, c",
+    "SELECT COUNT(*) FROM t WHERE a > 0 GROUP BY a, c",
+    "SELECT MAX(m), COUNT(*) FROM t WHERE b IN (%(b0)s, %(b2)s) GROUP BY g1, s",
+])
+@pytest.mark.parametrize("force_hash", [False, True])
+def test_partitioned_equals_hash_table(ctx, seg, text, force_hash):
+    from pinot_amd import native as N
+    gseg, _, fmt = seg
+    q = pql.compile(text % fmt)
+    base = N.PGX_X_FORCE_HASH if force_hash else 0
+    part = _execute(ctx, [gseg], q, base)
+    table = _execute(ctx, [gseg], q, base | N.PGX_X_NO_PARTITION)
+    assert _map(part) == _map(table)
+    assert part.stats.as_list() == table.stats.as_list()
+
+
+def test_partitioned_multi_segment_remap(ctx):
+    """Group columns with a different dictionary per segment (keys merged by value through the remap tables), one
+    shared dictionary for the aggregated column (one value base: the partitioned path's precondition)."""
+    from pinot_amd import engine as E
+    rng = np.random.default_rng(5)
+    mdom = np.sort(rng.choice(np.arange(-10 ** 6, 10 ** 6), size=300, replace=False)).astype(np.int32)
+    gsegs, osegs = [], []
+    for i in range(3):
+        n = 20000 + 7001 * i
+        mid = rng.integers(0, len(mdom), size=n)
+        mid[:len(mdom)] = np.arange(len(mdom))
+        raw = {"k": (rng.integers(0, 3000 + 500 * i, size=n) * 7).astype(np.int32),
+               "x": np.array(["v%d" % v for v in rng.integers(0, 2000 + 100 * i, size=n)]),
+               "m": mdom[rng.permutation(mid)]}
+        s, o = H.build_pair("ps%d" % i, raw)
+        gsegs.append(E.IndexSegment(ctx, s))
+        osegs.append(o)
+    q = pql.compile(AGGS + " WHERE m > -500000 GROUP BY x, k")
+    blk = E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute()
+    o = H.oracle_answer(osegs, q, literal=False)
+    m = blk.get_aggregation_group_by_result().as_map()
+    assert set(m) == set(o["map"])
+    fns = [a["fn"] for a in q["aggregations"]]
+    for k, v in o["map"].items():
+        H.assert_values_equal(m[k], v, fns)
+
+
+def _pairs_segment(ctx, n, card, seed):
+    from pinot_amd import engine as E
+    rng = np.random.default_rng(seed)
+    raw = {"ga": rng.integers(0, card, size=n).astype(np.int32),
+           "gb": rng.integers(0, card, size=n).astype(np.int32) * 3,
+           "m": rng.integers(-5000, 5000, size=n).astype(np.int32)}
+    raw["ga"][:card] = np.arange(card)
+    raw["gb"][:card] = np.arange(card) * 3
+    raw["m"][:2] = [-5000, 4999]
+    s, _ = H.build_pair("pp%d" % seed, raw)
+    return E.IndexSegment(ctx, s), raw
+
+
+def _expected(raw):
+    key = raw["ga"].astype(np.int64) * (1 << 32) + raw["gb"].astype(np.int64)
+    u, inv = np.unique(key, return_inverse=True)
+    m = raw["m"].astype(np.int64)
+    cnt = np.bincount(inv)
+    sm = np.bincount(inv, weights=m)
+    mn = np.full(len(u), np.iinfo(np.int64).max)
+    mx = np.full(len(u), np.iinfo(np.int64).min)
+    np.minimum.at(mn, inv, m)
+    np.maximum.at(mx, inv, m)
+    out = {}
+    for i, k in enumerate(u.tolist()):
+        out["%d\t%d" % (k >> 32, k & 0xFFFFFFFF)] = (int(cnt[i]), float(sm[i]), float(mn[i]), float(mx[i]))
+    return out
+
+
+@pytest.mark.parametrize("n,card", [(400000, 1000), (1200000, 2000)])
+def test_partitioned_debug_resize_and_fallback(ctx, monkeypatch, n, card):
+    """PGX_PART_DEBUG=1: pass-1 buckets start at 1/4 of their expected size (resize from the measured cursors), one
+    pass of 64 partitions (~n distinct groups overflow the 4096-slot LDS tables: re-split to 128), and at most one
+    re-split: the 1.2M-row case still overflows and falls back to the global hash table.  Both must be exact."""
+    monkeypatch.setenv("PGX_PART_DEBUG", "1")
+    gseg, raw = _pairs_segment(ctx, n, card, seed=card)
+    q = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY ga, gb")
+    got = _map(_execute(ctx, [gseg], q, 0))
+    exp = _expected(raw)
+    assert len(got) == len(exp)
+    for k, (c, s, lo, hi) in exp.items():
+        g = got[k]
+        assert (int(g[0]), float(g[1]), float(g[2]), float(g[3])) == (c, s, lo, hi)
