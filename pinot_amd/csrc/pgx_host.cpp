@@ -40,12 +40,13 @@ extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int 
 extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
                                            int nreg, int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
                                            int nbits, uint64_t* out, int64_t cap, unsigned long long* cursor,
-                                           unsigned long long* overflow, hipStream_t stream);
-extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int nparts,
-                                                int64_t cap, uint64_t keymask, int keybits, int64_t vbase, int need_sum,
-                                                int need_min, int need_max, uint64_t* okey, uint64_t* oplane,
-                                                int64_t ocap, unsigned long long* ocount,
-                                                unsigned long long* overflow, hipStream_t stream);
+                                           int cstride, unsigned long long* overflow, hipStream_t stream);
+extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
+                                                int nparts, int64_t cap, uint64_t keymask, int keybits, int64_t vbase,
+                                                int need_sum, int need_min, int need_max, int pack_shift,
+                                                uint64_t* okey, uint64_t* oplane, int64_t ocap,
+                                                unsigned long long* ocount, unsigned long long* overflow,
+                                                hipStream_t stream);
 struct pgx_ctx;
 extern "C" void ctx_unref(pgx_ctx* ctx);
 
@@ -1525,6 +1526,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     }
     const int64_t lds = lds_need();
     J.T = lds <= 20 * 1024 ? 256 : (lds <= 40 * 1024 ? 512 : 1024);
+    if (P.use_part) J.T = std::min(J.T, 512);  // record-emitting kernels hold R 64-bit records per lane: 256 VGPRs
     for (int l = 0; l < nleaves; ++l) {
       J.leaf_col.push_back(K.leaf_col[l]);
       const int ri = P.roar_index[members[0]][l];
@@ -1625,7 +1627,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     }
     const int waves = J.T / 64;
     int per_cu = std::max(1, 32 / waves);
-    if (lds > 0) per_cu = std::min<int64_t>(per_cu, std::max<int64_t>(1, (160 * 1024) / (lds + 256)));
+    const int64_t lds_all = std::max<int64_t>(lds, lds_bytes);  // incl. record staging (G_EMIT)
+    if (lds_all > 0) per_cu = std::min<int64_t>(per_cu, std::max<int64_t>(1, (160 * 1024) / (lds_all + 256)));
     const int64_t max_grid = int64_t(cus) * per_cu;
     const int64_t tpw = std::max<int64_t>(1, (tiles + max_grid - 1) / max_grid);
     G.grid = int(std::max<int64_t>(1, (tiles + tpw - 1) / tpw));
@@ -1803,13 +1806,15 @@ uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {
 constexpr int kPart1Bits = 6;           // first pass: 64 buckets (top bits of the mix)
 constexpr int64_t kPartGroupsPerWg = 2800;  // groups one pgx_part_aggregate workgroup holds comfortably (4096 slots)
 constexpr uint64_t kPartMaxBytes = uint64_t(96) << 30;  // partition buffers beyond this: fall back to the hash table
+constexpr int kPartChunkRecs = 4096;    // records per pgx_partition workgroup
+constexpr int kCursorStride = 16;       // u64 words between cursors: one 128-B line each
 
 struct PartBuffers {
   int nbits2 = 7;                       // second pass: 2^nbits2 buckets per first-pass bucket (0: no second pass)
   int64_t cap1 = 0, cap2 = 0, ocap = 0;
-  DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[64] | cursors2[nparts] | ocount | overflow[3]
+  DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[64] | cursors2[nparts] (kCursorStride apart) | ocount | ovf[3]
   int64_t nparts() const { return int64_t(1) << (kPart1Bits + nbits2); }
-  size_t ctr_words() const { return size_t(64 + (nbits2 ? nparts() : 0) + 4); }
+  size_t ctr_words() const { return size_t(64 + (nbits2 ? nparts() : 0)) * kCursorStride + 4; }
 };
 
 // PGX_PART_DEBUG=1 (tests): start from undersized buckets and one pass, and allow at most one refinement, so the
@@ -1855,35 +1860,39 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   unsigned long long* ctr = devp(PB.ctr);
   const int64_t np = PB.nparts();
   unsigned long long* c1 = ctr;
-  unsigned long long* c2 = ctr + 64;
+  unsigned long long* c2 = ctr + 64 * kCursorStride;
   unsigned long long* tail = ctr + PB.ctr_words() - 4;  // ocount, overflow[3]
   hip_check(hipMemsetAsync(ctr, 0, PB.ctr_words() * 8, st), "partition counters");
   if (N == 0) return;
   const uint64_t keymask = (uint64_t(1) << P.part_keybits) - 1u;
   const uint64_t* recs = reinterpret_cast<const uint64_t*>(P.kq.table);
-  const int64_t chunks1 = (N + 8191) / 8192;
+  const int64_t chunks1 = (N + kPartChunkRecs - 1) / kPartChunkRecs;
   if (chunks1 > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
   hip_check(pgx_launch_partition(recs, nullptr, nullptr, 1, N, int(chunks1), keymask, 64 - kPart1Bits, kPart1Bits,
-                                 PB.out1.as<uint64_t>(), PB.cap1, c1, tail + 1, st),
+                                 PB.out1.as<uint64_t>(), PB.cap1, c1, kCursorStride, tail + 1, st),
             "partition pass 1");
   const uint64_t* ain = PB.out1.as<uint64_t>();
   const unsigned long long* acnt = c1;
   int64_t acap = PB.cap1;
   int aparts = 64;
   if (PB.nbits2) {
-    const int64_t chunks2 = (PB.cap1 + 8191) / 8192;
+    const int64_t chunks2 = (PB.cap1 + kPartChunkRecs - 1) / kPartChunkRecs;
+    if (chunks2 * 64 > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
     hip_check(pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, 64, PB.cap1, int(chunks2), keymask,
                                    64 - kPart1Bits - PB.nbits2, PB.nbits2, PB.out2.as<uint64_t>(), PB.cap2, c2,
-                                   tail + 2, st),
+                                   kCursorStride, tail + 2, st),
               "partition pass 2");
     ain = PB.out2.as<uint64_t>();
     acnt = c2;
     acap = PB.cap2;
     aparts = int(np);
   }
-  hip_check(pgx_launch_part_aggregate(ain, acnt, aparts, acap, keymask, P.part_keybits, P.part_vbase, P.part_sum,
-                                      P.part_min, P.part_max, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(),
-                                      PB.ocap, tail, tail + 3, st),
+  // count and sum share one LDS add when a partition's count and value sum both fit their bit fields
+  const int cbits = bits_for(acap + 1);
+  const int pack_shift = (2 * cbits + P.part_vbits <= 64) ? 64 - cbits : 0;
+  hip_check(pgx_launch_part_aggregate(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits, P.part_vbase,
+                                      P.part_sum, P.part_min, P.part_max, pack_shift, PB.okey.as<uint64_t>(),
+                                      PB.oplane.as<uint64_t>(), PB.ocap, tail, tail + 3, st),
             "partition aggregate");
 }
 
@@ -1905,12 +1914,17 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
     if (!tail[1] && !tail[2] && !tail[3]) return true;
     std::vector<unsigned long long> c(PB.ctr_words());
     hip_check(hipMemcpy(c.data(), PB.ctr.p, c.size() * 8, hipMemcpyDeviceToHost), "counters D2H");
+    auto max_cursor = [&](size_t first, int64_t count) {
+      unsigned long long m = 0;
+      for (int64_t i = 0; i < count; ++i) m = std::max(m, c[first + size_t(i) * kCursorStride]);
+      return int64_t(m);
+    };
     if (tail[1]) {  // a first-pass bucket overflowed: size to the largest (cursors count every record)
-      PB.cap1 = int64_t(*std::max_element(c.begin(), c.begin() + 64)) + 1024;
+      PB.cap1 = max_cursor(0, 64) + 1024;
       continue;
     }
     if (tail[2]) {
-      PB.cap2 = int64_t(*std::max_element(c.begin() + 64, c.begin() + 64 + PB.nparts())) + 1024;
+      PB.cap2 = max_cursor(64 * kCursorStride, PB.nparts()) + 1024;
       continue;
     }
     if (PB.nbits2 == (part_debug() ? 1 : 7)) return false;  // an LDS table overflowed at the finest split

@@ -96,6 +96,23 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     tab_off = lds;
     lds += int(s.dense_slots) * s.num_planes * 8;
   }
+  // G_EMIT: per-wave LDS staging of the records, so that they leave as 64 lanes x 8 contiguous bytes per store
+  // instead of R-strided 8-byte stores (each lane owns R consecutive rows).  A lane's R records sit at a pitch of
+  // R + 2 words (conflict-free 16-byte LDS writes); rounds of stg_recs records when the budget is tight.
+  int stg_off = -1, stg_recs = 0;
+  const int stg_pitch = s.R + 2;
+  if (emit) {
+    const int waves = s.T / 64;
+    for (int r = 64 * s.R; r >= std::max(64, s.R); r /= 2)
+      if (lds + (r / s.R) * stg_pitch * 8 * waves <= kLdsBudget) {
+        stg_recs = r;
+        break;
+      }
+    if (stg_recs) {
+      stg_off = lds;
+      lds += (stg_recs / s.R) * stg_pitch * 8 * waves;
+    }
+  }
   if (lds_bytes_out) *lds_bytes_out = lds;
   const bool any_img = lds > 0 && (tab_off != 0 || s.group_mode != G_DENSE_LDS);
 
@@ -323,6 +340,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
             s.cols[s.agg_col[a]].acc32)
           e.ln("u32 p", a, " = 0u;");
       }
+    if (emit) e.ln("u64 recs[PR];");
     e.ln("#pragma unroll");
     e.ln("for (int j = 0; j < PR; ++j) {");
     e.ind = 6;
@@ -401,8 +419,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       if (emit) {
         // partitioned group-by: one record per row (~0 = not selected); key packing as the LONG_MAP raw key
         // (DefaultGroupKeyGenerator.java:239-246: dictIds at fixed bit offsets)
-        e.ln("if (vj) {");
-        e.ind = 7;
         e.ln("u64 rec = ~0ull;");
         e.ln("if (m) {");
         std::string key = "0ull";
@@ -420,9 +436,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         }
         e.ln("  rec = (", key, ") | ((u64)(", x, ") << ", s.keybits, ");");
         e.ln("}");
-        e.ln("A.table[S->rec_base + r0 + j] = rec;");
-        e.ind = 6;
-        e.ln("}");
+        e.ln("recs[j] = rec;");
       } else {
       // dense group-by: key = sum_g id_g * mul_g (column 0 least significant, DefaultGroupKeyGenerator.java:230-237)
       e.ln("if (m) {");
@@ -466,6 +480,39 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
             s.cols[s.agg_col[a]].acc32)
           e.ln("acc", a, " += p", a, ";");
       }
+    if (emit && stg_recs) {
+      const int L = stg_recs / s.R;  // lanes whose records fill one round
+      int lg = 0;
+      while ((1 << lg) < L) ++lg;
+      e.ln("{");
+      e.ln("  u64* stg = (u64*)(lds + ", stg_off / 4, ") + (tid >> 6) * ", L * stg_pitch, ";");
+      e.ln("  const int w0 = r0 - lane * PR;  // first row of this wave's slice");
+      e.ln("  PGX_G u64* out = (PGX_G u64*)A.table + S->rec_base + w0;");
+      e.ln("  #pragma unroll");
+      e.ln("  for (int rd = 0; rd < ", 64 * s.R / stg_recs, "; ++rd) {");
+      e.ln("    if ((lane >> ", lg, ") == rd) {");
+      e.ln("      u64* d = stg + (lane & ", L - 1, ") * ", stg_pitch, ";");
+      e.ln("      #pragma unroll");
+      e.ln("      for (int j = 0; j < PR; ++j) d[j] = recs[j];");
+      e.ln("    }");
+      e.ln("    __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");");
+      e.ln("    __builtin_amdgcn_wave_barrier();");
+      e.ln("    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");");
+      e.ln("    #pragma unroll");
+      e.ln("    for (int k = 0; k < ", stg_recs / 64, "; ++k) {");
+      e.ln("      const int i = k * 64 + lane;");
+      e.ln("      const int row = rd * ", stg_recs, " + i;");
+      e.ln("      if (FULL || w0 + row < nd) __builtin_nontemporal_store(stg[(i / PR) * ", stg_pitch, " + (i % PR)], out + row);");
+      e.ln("    }");
+      e.ln("    __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");");
+      e.ln("    __builtin_amdgcn_wave_barrier();");
+      e.ln("    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");");
+      e.ln("  }");
+      e.ln("}");
+    } else if (emit) {
+      e.ln("#pragma unroll");
+      e.ln("for (int j = 0; j < PR; ++j) if (FULL || r0 + j < nd) A.table[S->rec_base + r0 + j] = recs[j];");
+    }
     e.ind = 4;
     e.ln("}");
   }
@@ -726,7 +773,8 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.leaf_mode.clear();
     s.prog_op.clear();
     s.prog_arg.clear();
-    s.R = 8;
+    s.R = 16;
+    s.T = 512;
     s.group_mode = G_EMIT;
     s.gcol = {0, 2};
     s.gshift = {0, 14};

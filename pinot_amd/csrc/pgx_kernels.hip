@@ -589,143 +589,191 @@ __global__ void __launch_bounds__(256) pgx_roaring_expand(const RDesc* __restric
 // passes split the records into 64 x 128 partitions by hash bits, and one workgroup per partition aggregates it in an
 // LDS hash table, then appends its groups to compact output arrays.
 // ---------------------------------------------------------------------------------------------
+#define PGX_GLOBAL __attribute__((address_space(1)))
+
 __device__ __forceinline__ uint64_t part_mix(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
   return x;
 }
 
-constexpr int kPartChunk = 8192;   // records per partitioning workgroup (64 KiB LDS staging)
+constexpr int kPartThreads = 512;
+constexpr int kPartPer = 8;                             // records per thread, held in registers
+constexpr int kPartChunk = kPartThreads * kPartPer;     // records per partitioning workgroup (32 KiB LDS staging)
 constexpr uint64_t kNoRecord = ~0ull;
+
+// Exclusive scan of hist[0, nb) (nb <= 128) by wave 0: offs[b] = sum of hist[< b]; *total = sum of all.
+__device__ __forceinline__ void part_scan128(const int* hist, int* offs, int* total, int nb, int tid) {
+  if (tid >= 64) return;
+  const int a = 2 * tid < nb ? hist[2 * tid] : 0;
+  const int b = 2 * tid + 1 < nb ? hist[2 * tid + 1] : 0;
+  int x = a + b;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d, 64);
+    if (tid >= d) x += y;
+  }
+  const int excl = x - a - b;
+  if (2 * tid < nb) offs[2 * tid] = excl;
+  if (2 * tid + 1 < nb) offs[2 * tid + 1] = excl + a;
+  if (tid == 63) *total = x;
+}
 
 // Records of region r live at in + in_off[r] (in_off null: r * in_cap), in_cnt[r] of them (in_cnt null: in_cap; else
 // typically the previous pass's cursors, read on the device, so passes chain without a host round trip); region r's
-// partition b goes to out + (r * nb + b) * cap, appended at cursor[r * nb + b].
-__global__ void __launch_bounds__(256) pgx_partition(const uint64_t* __restrict__ in, const int64_t* __restrict__ in_off,
-                                                     const unsigned long long* __restrict__ in_cnt, int nreg,
-                                                     int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
-                                                     int nbits, uint64_t* __restrict__ out, int64_t cap,
-                                                     unsigned long long* __restrict__ cursor,
-                                                     unsigned long long* __restrict__ overflow) {
+// partition b goes to out + (r * nb + b) * cap, appended at cursor[(r * nb + b) * cstride] (cursors spread over
+// separate cache lines: every workgroup of a pass reserves its runs there).
+__global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __restrict__ in,
+                                                              const int64_t* __restrict__ in_off,
+                                                              const unsigned long long* __restrict__ in_cnt, int nreg,
+                                                              int64_t in_cap, int chunks_per_reg, uint64_t keymask,
+                                                              int shift, int nbits, uint64_t* __restrict__ out,
+                                                              int64_t cap, unsigned long long* __restrict__ cursor,
+                                                              int cstride, unsigned long long* __restrict__ overflow) {
   const int r = static_cast<int>(blockIdx.x / chunks_per_reg);
   const int64_t chunk = static_cast<int64_t>(blockIdx.x % chunks_per_reg);
   if (r >= nreg) return;
-  const int64_t n = in_cnt ? min(static_cast<int64_t>(in_cnt[r]), in_cap) : in_cap;
+  const int64_t n = in_cnt ? min(static_cast<int64_t>(in_cnt[r * cstride]), in_cap) : in_cap;
   const int64_t c0 = chunk * kPartChunk;
   if (c0 >= n) return;
   const int cn = static_cast<int>(min<int64_t>(kPartChunk, n - c0));
   const int nb = 1 << nbits;
   __shared__ uint64_t stage[kPartChunk];
-  __shared__ uint8_t sb[kPartChunk];   // bucket of input record i (255: no record)
   __shared__ uint8_t sbs[kPartChunk];  // bucket of staged (bucket-sorted) record i
-  __shared__ int hist[128], offs[128], fill[128];
+  __shared__ int hist[128], offs[128], fill[128], total;
   __shared__ unsigned long long gpos[128];
   const int tid = threadIdx.x;
   if (tid < nb) { hist[tid] = 0; fill[tid] = 0; }
-  __syncthreads();
-  const uint64_t* src = in + (in_off ? in_off[r] : static_cast<int64_t>(r) * in_cap) + c0;
-  for (int i = tid; i < cn; i += 256) {
-    const uint64_t rec = src[i];
-    int b = -1;
-    if (rec != kNoRecord) {
-      b = static_cast<int>((part_mix(rec & keymask) >> shift) & static_cast<uint64_t>(nb - 1));
-      atomicAdd(&hist[b], 1);
-    }
-    sb[i] = static_cast<uint8_t>(b < 0 ? 255 : b);
+  const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) +
+                                   (in_off ? in_off[r] : static_cast<int64_t>(r) * in_cap) + c0;
+  uint64_t rec[kPartPer];
+#pragma unroll
+  for (int k = 0; k < kPartPer; ++k) {
+    const int i = k * kPartThreads + tid;
+    rec[k] = i < cn ? __builtin_nontemporal_load(src + i) : kNoRecord;
   }
   __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int b = 0; b < nb; ++b) { offs[b] = acc; acc += hist[b]; }
+  int bk[kPartPer];
+#pragma unroll
+  for (int k = 0; k < kPartPer; ++k) {
+    bk[k] = rec[k] == kNoRecord ? -1 : static_cast<int>((part_mix(rec[k] & keymask) >> shift) & static_cast<uint64_t>(nb - 1));
+    if (bk[k] >= 0) atomicAdd(&hist[bk[k]], 1);
   }
+  __syncthreads();
+  part_scan128(hist, offs, &total, nb, tid);
   if (tid < nb && hist[tid]) {
-    gpos[tid] = atomicAdd(&cursor[r * nb + tid], static_cast<unsigned long long>(hist[tid]));
-    if (gpos[tid] + hist[tid] > static_cast<unsigned long long>(cap)) atomicAdd(overflow, 1ull);
+    const unsigned long long g = atomicAdd(&cursor[static_cast<int64_t>(r * nb + tid) * cstride],
+                                           static_cast<unsigned long long>(hist[tid]));
+    gpos[tid] = g;
+    if (g + hist[tid] > static_cast<unsigned long long>(cap)) atomicAdd(overflow, 1ull);
   }
   __syncthreads();
-  for (int i = tid; i < cn; i += 256) {
-    const int b = sb[i];
-    if (b == 255) continue;
-    const int pos = offs[b] + atomicAdd(&fill[b], 1);
-    stage[pos] = src[i];
-    sbs[pos] = static_cast<uint8_t>(b);
+#pragma unroll
+  for (int k = 0; k < kPartPer; ++k) {
+    if (bk[k] < 0) continue;
+    const int pos = offs[bk[k]] + atomicAdd(&fill[bk[k]], 1);
+    stage[pos] = rec[k];
+    sbs[pos] = static_cast<uint8_t>(bk[k]);
   }
   __syncthreads();
   // copy out bucket runs: consecutive staged records of one bucket go to consecutive output words
-  int total = 0;
-  for (int b = 0; b < nb; ++b) total += hist[b];
-  for (int i = tid; i < total; i += 256) {
+  PGX_GLOBAL uint64_t* dst = (PGX_GLOBAL uint64_t*)(out);
+  const int tot = total;
+  for (int i = tid; i < tot; i += kPartThreads) {
     const int b = sbs[i];
     const unsigned long long p = gpos[b] + static_cast<unsigned long long>(i - offs[b]);
-    if (p < static_cast<unsigned long long>(cap)) out[(static_cast<int64_t>(r) * nb + b) * cap + static_cast<int64_t>(p)] = stage[i];
+    if (p < static_cast<unsigned long long>(cap))
+      __builtin_nontemporal_store(stage[i], dst + (static_cast<int64_t>(r) * nb + b) * cap + static_cast<int64_t>(p));
   }
 }
 
 // One workgroup aggregates one partition in an LDS hash table (linear probing, 64-bit CAS on the key) and appends its
-// groups to the output: okey[g] = packed key, oplane[p * ocap + g] = plane p in the library's plane encodings.
+// groups to the output: okey[g] = packed key, oplane[p * ocap + g] = plane p (count, int64 sum, ordered min, ordered
+// max).  pack_shift > 0: count and sum share one 64-bit LDS add ((1 << pack_shift) + value; the host checks that a
+// partition's value sum stays below bit pack_shift and its count below bit 64 - pack_shift).
 constexpr int kAggSlots = 4096;
+constexpr int kAggThreads = 1024;
+constexpr int kAggPer = 8;
 
-__global__ void __launch_bounds__(512) pgx_part_aggregate(const uint64_t* __restrict__ in,
-                                                          const unsigned long long* __restrict__ in_cnt, int64_t cap,
-                                                          uint64_t keymask, int keybits, int64_t vbase, int need_sum,
-                                                          int need_min, int need_max, uint64_t* __restrict__ okey,
-                                                          uint64_t* __restrict__ oplane, int64_t ocap,
-                                                          unsigned long long* __restrict__ ocount,
-                                                          unsigned long long* __restrict__ overflow) {
+__global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t* __restrict__ in,
+                                                                  const unsigned long long* __restrict__ in_cnt,
+                                                                  int cstride, int64_t cap, uint64_t keymask,
+                                                                  int keybits, int64_t vbase, int need_sum,
+                                                                  int need_min, int need_max, int pack_shift,
+                                                                  uint64_t* __restrict__ okey,
+                                                                  uint64_t* __restrict__ oplane, int64_t ocap,
+                                                                  unsigned long long* __restrict__ ocount,
+                                                                  unsigned long long* __restrict__ overflow) {
   __shared__ uint64_t tkey[kAggSlots];
+  __shared__ unsigned long long tsum[kAggSlots];   // sum, or (count << pack_shift) + sum
   __shared__ unsigned int tcnt[kAggSlots];
-  __shared__ unsigned long long tsum[kAggSlots];
   __shared__ unsigned int tmin[kAggSlots], tmax[kAggSlots];
   __shared__ int nfound;
   __shared__ unsigned long long obase;
   const int tid = threadIdx.x;
   const int part = blockIdx.x;
-  for (int i = tid; i < kAggSlots; i += 512) {
+  for (int i = tid; i < kAggSlots; i += kAggThreads) {
     tkey[i] = kNoRecord; tcnt[i] = 0u; tsum[i] = 0ull; tmin[i] = 0xFFFFFFFFu; tmax[i] = 0u;
   }
   if (tid == 0) nfound = 0;
   __syncthreads();
-  const int64_t n = min(static_cast<int64_t>(in_cnt[part]), cap);
-  const uint64_t* src = in + static_cast<int64_t>(part) * cap;
+  const int64_t n = min(static_cast<int64_t>(in_cnt[static_cast<int64_t>(part) * cstride]), cap);
+  const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) + static_cast<int64_t>(part) * cap;
+  const unsigned long long one = pack_shift ? (1ull << pack_shift) : 0ull;
   bool lost = false;
-  for (int64_t i = tid; i < n; i += 512) {
-    const uint64_t rec = src[i];
-    const uint64_t key = rec & keymask;
-    const unsigned int v = static_cast<unsigned int>(rec >> keybits);
-    unsigned int h = static_cast<unsigned int>(part_mix(key)) & (kAggSlots - 1);
-    int probes = 0;
-    for (; probes < kAggSlots; ++probes) {
-      const uint64_t k = tkey[h];
-      if (k == key) break;
-      if (k == kNoRecord) {
-        const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[h]), kNoRecord, key);
-        if (prev == kNoRecord || prev == key) break;
-      }
-      h = (h + 1) & (kAggSlots - 1);
+  for (int64_t base = 0; base < n; base += kAggThreads * kAggPer) {
+    uint64_t rec[kAggPer];
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) {
+      const int64_t i = base + k * kAggThreads + tid;
+      rec[k] = i < n ? __builtin_nontemporal_load(src + i) : kNoRecord;
     }
-    if (probes == kAggSlots) { lost = true; continue; }
-    atomicAdd(&tcnt[h], 1u);
-    if (need_sum) atomicAdd(&tsum[h], static_cast<unsigned long long>(v));
-    if (need_min) atomicMin(&tmin[h], v);
-    if (need_max) atomicMax(&tmax[h], v);
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) {
+      if (rec[k] == kNoRecord) continue;
+      const uint64_t key = rec[k] & keymask;
+      const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);
+      unsigned int h = static_cast<unsigned int>(part_mix(key)) & (kAggSlots - 1);
+      int probes = 0;
+      for (; probes < kAggSlots; ++probes) {
+        const uint64_t kk = tkey[h];
+        if (kk == key) break;
+        if (kk == kNoRecord) {
+          const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[h]), kNoRecord, key);
+          if (prev == kNoRecord || prev == key) break;
+        }
+        h = (h + 1) & (kAggSlots - 1);
+      }
+      if (probes == kAggSlots) { lost = true; continue; }
+      if (pack_shift) {
+        atomicAdd(&tsum[h], one + v);
+      } else {
+        atomicAdd(&tcnt[h], 1u);
+        if (need_sum) atomicAdd(&tsum[h], static_cast<unsigned long long>(v));
+      }
+      if (need_min) atomicMin(&tmin[h], v);
+      if (need_max) atomicMax(&tmax[h], v);
+    }
   }
   if (lost) atomicAdd(overflow, 1ull);
   __syncthreads();
   // compact: count, reserve once, write
   int mine = 0;
-  for (int i = tid; i < kAggSlots; i += 512) mine += tkey[i] != kNoRecord;
+  for (int i = tid; i < kAggSlots; i += kAggThreads) mine += tkey[i] != kNoRecord;
   const int before = atomicAdd(&nfound, mine);
   __syncthreads();
   if (tid == 0) obase = atomicAdd(ocount, static_cast<unsigned long long>(nfound));
   __syncthreads();
   unsigned long long o = obase + static_cast<unsigned long long>(before);
-  for (int i = tid; i < kAggSlots; i += 512) {
+  const unsigned long long smask = pack_shift ? (1ull << pack_shift) - 1ull : ~0ull;
+  for (int i = tid; i < kAggSlots; i += kAggThreads) {
     if (tkey[i] == kNoRecord) continue;
     if (o >= static_cast<unsigned long long>(ocap)) { atomicAdd(overflow, 1ull); continue; }
     okey[o] = tkey[i];
-    const unsigned long long c = tcnt[i];
+    const unsigned long long c = pack_shift ? (tsum[i] >> pack_shift) : tcnt[i];
+    const unsigned long long sm = tsum[i] & smask;
     oplane[o] = c;  // plane 0: doc count
-    // planes 1..3: sum (int64), min, max (ordered encodings of the int64 value), in this fixed order
-    oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(tsum[i]) + static_cast<int64_t>(c) * vbase);
+    // planes 1..3: sum (int64 incl. vbase * count), min, max (ordered encodings of the int64 value)
+    oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(sm) + static_cast<int64_t>(c) * vbase);
     oplane[2 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(tmin[i])) ^ 0x8000000000000000ull;
     oplane[3 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(tmax[i])) ^ 0x8000000000000000ull;
     ++o;
@@ -852,22 +900,25 @@ extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, in
 extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
                                            int nreg, int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
                                            int nbits, uint64_t* out, int64_t cap, unsigned long long* cursor,
-                                           unsigned long long* overflow, hipStream_t stream) {
+                                           int cstride, unsigned long long* overflow, hipStream_t stream) {
   const long long blocks = static_cast<long long>(nreg) * chunks_per_reg;
   if (blocks <= 0) return hipSuccess;
-  if (blocks > 0x7FFFFFFFll || nbits > 7) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pgx::pgx_partition, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, in, in_off, in_cnt,
-                     nreg, in_cap, chunks_per_reg, keymask, shift, nbits, out, cap, cursor, overflow);
+  if (blocks > 0x7FFFFFFFll || nbits > 7 || nbits < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pgx::pgx_partition, dim3(static_cast<unsigned>(blocks)), dim3(pgx::kPartThreads), 0, stream, in,
+                     in_off, in_cnt, nreg, in_cap, chunks_per_reg, keymask, shift, nbits, out, cap, cursor, cstride,
+                     overflow);
   return hipGetLastError();
 }
 
-extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int nparts,
-                                                int64_t cap, uint64_t keymask, int keybits, int64_t vbase, int need_sum,
-                                                int need_min, int need_max, uint64_t* okey, uint64_t* oplane,
-                                                int64_t ocap, unsigned long long* ocount,
-                                                unsigned long long* overflow, hipStream_t stream) {
+extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
+                                                int nparts, int64_t cap, uint64_t keymask, int keybits, int64_t vbase,
+                                                int need_sum, int need_min, int need_max, int pack_shift,
+                                                uint64_t* okey, uint64_t* oplane, int64_t ocap,
+                                                unsigned long long* ocount, unsigned long long* overflow,
+                                                hipStream_t stream) {
   if (nparts <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pgx::pgx_part_aggregate, dim3(nparts), dim3(512), 0, stream, in, in_cnt, cap, keymask, keybits,
-                     vbase, need_sum, need_min, need_max, okey, oplane, ocap, ocount, overflow);
+  hipLaunchKernelGGL(pgx::pgx_part_aggregate, dim3(nparts), dim3(pgx::kAggThreads), 0, stream, in, in_cnt, cstride,
+                     cap, keymask, keybits, vbase, need_sum, need_min, need_max, pack_shift, okey, oplane, ocap,
+                     ocount, overflow);
   return hipGetLastError();
 }
