@@ -1797,24 +1797,25 @@ uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {
 // -------------------------------------------------------------------------------------------------
 // Partitioned group-by (DESIGN.md "Sparse group-by").  The query kernel writes one 8-byte record per scanned row,
 // key | (value - vbase) << keybits (~0: row not selected).  Two radix passes on independent bits of a 64-bit mix of
-// the key (64 buckets, then 2^nbits2 per bucket) split the records into partitions whose groups fit one workgroup's
+// the key (128 buckets, then 2^nbits2 per bucket) split the records into partitions whose groups fit one workgroup's
 // LDS hash table; pgx_part_aggregate aggregates each partition and appends its groups.  Each pass reads the previous
 // pass's cursors on the device, so the chain runs without a host round trip until the final counters.
 // Replaces, for sparse keys, the reference's per-segment MAP-based group-key holders
 // (DefaultGroupKeyGenerator.java:239-343 LONG_MAP / ARRAY_MAP) with a layout that streams HBM instead of probing it.
 // -------------------------------------------------------------------------------------------------
-constexpr int kPart1Bits = 6;           // first pass: 64 buckets (top bits of the mix)
-constexpr int64_t kPartGroupsPerWg = 2800;  // groups one pgx_part_aggregate workgroup holds comfortably (4096 slots)
+constexpr int kPart1Bits = 7;           // first pass: 128 buckets (top bits of the mix)
+constexpr int kPart1N = 1 << kPart1Bits;
+constexpr int64_t kPartGroupsPerWg = 1400;  // groups per pgx_part_aggregate workgroup: LDS table load <= ~1/3 (4096 slots)
 constexpr uint64_t kPartMaxBytes = uint64_t(96) << 30;  // partition buffers beyond this: fall back to the hash table
-constexpr int kPartChunkRecs = 4096;    // records per pgx_partition workgroup
+constexpr int kPartChunkRecs = 8192;    // records per pgx_partition workgroup (pgx_kernels.hip kPartChunk)
 constexpr int kCursorStride = 16;       // u64 words between cursors: one 128-B line each
 
 struct PartBuffers {
   int nbits2 = 7;                       // second pass: 2^nbits2 buckets per first-pass bucket (0: no second pass)
   int64_t cap1 = 0, cap2 = 0, ocap = 0;
-  DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[64] | cursors2[nparts] (kCursorStride apart) | ocount | ovf[3]
+  DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[kPart1N] | cursors2[nparts] (kCursorStride apart) | ocount | ovf[3]
   int64_t nparts() const { return int64_t(1) << (kPart1Bits + nbits2); }
-  size_t ctr_words() const { return size_t(64 + (nbits2 ? nparts() : 0)) * kCursorStride + 4; }
+  size_t ctr_words() const { return size_t(kPart1N + (nbits2 ? nparts() : 0)) * kCursorStride + 4; }
 };
 
 // PGX_PART_DEBUG=1 (tests): start from undersized buckets and one pass, and allow at most one refinement, so the
@@ -1832,7 +1833,7 @@ void part_size(const ExecPlan& P, PartBuffers& PB) {
   ub = std::min(ub, prod);
   PB.nbits2 = 0;
   while (PB.nbits2 < 7 && double(int64_t(1) << (kPart1Bits + PB.nbits2)) * kPartGroupsPerWg < ub) ++PB.nbits2;
-  PB.cap1 = N / 64 + N / 512 + 65536;
+  PB.cap1 = N / kPart1N + N / 512 + 65536;
   const int64_t np = PB.nparts();
   PB.cap2 = N / np + N / np / 4 + 16384;
   if (part_debug()) {
@@ -1845,9 +1846,9 @@ void part_size(const ExecPlan& P, PartBuffers& PB) {
 bool part_alloc(pgx_ctx* ctx, const ExecPlan& P, PartBuffers& PB) {
   const int64_t np = PB.nparts();
   PB.ocap = std::max<int64_t>(1, std::min<int64_t>(P.rec_total, np * 4096));
-  const uint64_t bytes = uint64_t(64) * PB.cap1 * 8 + (PB.nbits2 ? uint64_t(np) * PB.cap2 * 8 : 0) + uint64_t(PB.ocap) * 40;
+  const uint64_t bytes = uint64_t(kPart1N) * PB.cap1 * 8 + (PB.nbits2 ? uint64_t(np) * PB.cap2 * 8 : 0) + uint64_t(PB.ocap) * 40;
   if (bytes > kPartMaxBytes) return false;
-  PB.out1 = DevBuf(ctx, size_t(64) * PB.cap1 * 8);
+  PB.out1 = DevBuf(ctx, size_t(kPart1N) * PB.cap1 * 8);
   if (PB.nbits2) PB.out2 = DevBuf(ctx, size_t(np) * PB.cap2 * 8);
   PB.okey = DevBuf(ctx, size_t(PB.ocap) * 8);
   PB.oplane = DevBuf(ctx, size_t(PB.ocap) * 4 * 8);
@@ -1860,7 +1861,7 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   unsigned long long* ctr = devp(PB.ctr);
   const int64_t np = PB.nparts();
   unsigned long long* c1 = ctr;
-  unsigned long long* c2 = ctr + 64 * kCursorStride;
+  unsigned long long* c2 = ctr + kPart1N * kCursorStride;
   unsigned long long* tail = ctr + PB.ctr_words() - 4;  // ocount, overflow[3]
   hip_check(hipMemsetAsync(ctr, 0, PB.ctr_words() * 8, st), "partition counters");
   if (N == 0) return;
@@ -1874,11 +1875,11 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   const uint64_t* ain = PB.out1.as<uint64_t>();
   const unsigned long long* acnt = c1;
   int64_t acap = PB.cap1;
-  int aparts = 64;
+  int aparts = kPart1N;
   if (PB.nbits2) {
     const int64_t chunks2 = (PB.cap1 + kPartChunkRecs - 1) / kPartChunkRecs;
-    if (chunks2 * 64 > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
-    hip_check(pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, 64, PB.cap1, int(chunks2), keymask,
+    if (chunks2 * kPart1N > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
+    hip_check(pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, kPart1N, PB.cap1, int(chunks2), keymask,
                                    64 - kPart1Bits - PB.nbits2, PB.nbits2, PB.out2.as<uint64_t>(), PB.cap2, c2,
                                    kCursorStride, tail + 2, st),
               "partition pass 2");
@@ -1920,11 +1921,11 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
       return int64_t(m);
     };
     if (tail[1]) {  // a first-pass bucket overflowed: size to the largest (cursors count every record)
-      PB.cap1 = max_cursor(0, 64) + 1024;
+      PB.cap1 = max_cursor(0, kPart1N) + 1024;
       continue;
     }
     if (tail[2]) {
-      PB.cap2 = max_cursor(64 * kCursorStride, PB.nparts()) + 1024;
+      PB.cap2 = max_cursor(kPart1N * kCursorStride, PB.nparts()) + 1024;
       continue;
     }
     if (PB.nbits2 == (part_debug() ? 1 : 7)) return false;  // an LDS table overflowed at the finest split

@@ -596,9 +596,9 @@ __device__ __forceinline__ uint64_t part_mix(uint64_t x) {
   return x;
 }
 
-constexpr int kPartThreads = 512;
+constexpr int kPartThreads = 1024;
 constexpr int kPartPer = 8;                             // records per thread, held in registers
-constexpr int kPartChunk = kPartThreads * kPartPer;     // records per partitioning workgroup (32 KiB LDS staging)
+constexpr int kPartChunk = kPartThreads * kPartPer;     // records per partitioning workgroup (64 KiB LDS staging)
 constexpr uint64_t kNoRecord = ~0ull;
 
 // Exclusive scan of hist[0, nb) (nb <= 128) by wave 0: offs[b] = sum of hist[< b]; *total = sum of all.
@@ -681,8 +681,9 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
   for (int i = tid; i < tot; i += kPartThreads) {
     const int b = sbs[i];
     const unsigned long long p = gpos[b] + static_cast<unsigned long long>(i - offs[b]);
-    if (p < static_cast<unsigned long long>(cap))
-      __builtin_nontemporal_store(stage[i], dst + (static_cast<int64_t>(r) * nb + b) * cap + static_cast<int64_t>(p));
+    // plain (not streaming) stores: a bucket run's first and last lines are completed by other workgroups' runs,
+    // which L2 merges before write-back
+    if (p < static_cast<unsigned long long>(cap)) dst[(static_cast<int64_t>(r) * nb + b) * cap + static_cast<int64_t>(p)] = stage[i];
   }
 }
 
@@ -727,31 +728,45 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
       const int64_t i = base + k * kAggThreads + tid;
       rec[k] = i < n ? __builtin_nontemporal_load(src + i) : kNoRecord;
     }
+    // home-slot reads of all kAggPer records first (independent LDS reads in flight); most keys sit at home
+    unsigned int h[kAggPer];
+    uint64_t kk[kAggPer];
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) {
+      h[k] = static_cast<unsigned int>(part_mix(rec[k] & keymask)) & (kAggSlots - 1);
+      kk[k] = tkey[h[k]];
+    }
 #pragma unroll
     for (int k = 0; k < kAggPer; ++k) {
       if (rec[k] == kNoRecord) continue;
       const uint64_t key = rec[k] & keymask;
       const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);
-      unsigned int h = static_cast<unsigned int>(part_mix(key)) & (kAggSlots - 1);
-      int probes = 0;
-      for (; probes < kAggSlots; ++probes) {
-        const uint64_t kk = tkey[h];
-        if (kk == key) break;
-        if (kk == kNoRecord) {
-          const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[h]), kNoRecord, key);
-          if (prev == kNoRecord || prev == key) break;
+      unsigned int hh = h[k];
+      if (kk[k] != key) {  // linear probing from the home slot; CAS claims an empty slot
+        uint64_t cur = kk[k];
+        int probes = 0;
+        while (true) {
+          if (cur == kNoRecord) {
+            const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[hh]), kNoRecord, key);
+            if (prev == kNoRecord || prev == key) break;
+            cur = prev;
+            continue;  // lost the race for this slot to another key: keep probing
+          }
+          if (cur == key) break;
+          if (++probes == kAggSlots) break;
+          hh = (hh + 1) & (kAggSlots - 1);
+          cur = tkey[hh];
         }
-        h = (h + 1) & (kAggSlots - 1);
+        if (probes == kAggSlots) { lost = true; continue; }
       }
-      if (probes == kAggSlots) { lost = true; continue; }
       if (pack_shift) {
-        atomicAdd(&tsum[h], one + v);
+        atomicAdd(&tsum[hh], one + v);
       } else {
-        atomicAdd(&tcnt[h], 1u);
-        if (need_sum) atomicAdd(&tsum[h], static_cast<unsigned long long>(v));
+        atomicAdd(&tcnt[hh], 1u);
+        if (need_sum) atomicAdd(&tsum[hh], static_cast<unsigned long long>(v));
       }
-      if (need_min) atomicMin(&tmin[h], v);
-      if (need_max) atomicMax(&tmax[h], v);
+      if (need_min) atomicMin(&tmin[hh], v);
+      if (need_max) atomicMax(&tmax[hh], v);
     }
   }
   if (lost) atomicAdd(overflow, 1ull);
