@@ -23,7 +23,11 @@ build/pgx_kernels.o: $(CSRC)/pgx_kernels.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o
+build/pgx_trim.o: $(CSRC)/pgx_trim.hip
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o build/pgx_trim.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 
 clean:

@@ -171,9 +171,12 @@ def main():
             s4 = (C.c_int64 * 4)(*stats_t.tolist())
             N.check(L.pgx_result_from_dense(ctx.handle, q.handle, seg_arr, len(segs),
                                             C.c_void_p(dense_t.data_ptr()), s4, C.byref(out)))
+            E.trim_and_gather(q, out)
             return out
         opts = N.ExecOpts(0, None, 0, 0)
         N.check(L.pgx_execute(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
+        if req.get("group_by"):  # the server's combine output: trimToSize, kept groups read back (a-19)
+            E.trim_and_gather(q, r)
         if world > 1:  # aggregation-only: combine the scalar partials across GPUs
             vals = []
             for i in range(len(req["aggregations"])):
@@ -206,7 +209,18 @@ def main():
     # result summary (for the log) and kernel roofline on rank 0
     st = (C.c_int64 * 4)()
     N.check(L.pgx_result_stats(last, st))
-    blk = E.decode_result(q, last, segs) if rank == 0 else None
+    summary = None
+    ngroups = 0
+    if rank == 0:
+        if req.get("group_by"):  # do not read a sparse result back whole: group count + the top of the trim
+            ng = C.c_int64()
+            N.check(L.pgx_result_num_groups(last, C.byref(ng)))
+            ngroups = ng.value
+            top = E.trimmed_maps(q, last, segs)[0]
+            best = sorted(top.items(), key=lambda kv: kv[1], reverse=q.fns[0] != "min")[:3]
+            summary = {"groups": ngroups, "top3_" + q.fns[0]: best}
+        else:
+            summary = E.decode_result(q, last, segs).get_aggregation_result()
     L.pgx_result_release(last)
     total_rows = rows * (wl.segments * world if wl.scaling == "weak" else wl.segments)
     value = total_rows / (elapsed / args.steps)
@@ -229,6 +243,8 @@ def main():
         algo_bytes = data.algorithmic_bytes(used, dict_cols, int(st[0]), len(ST.parse(data.seg_data.star_tree)[1]))
     else:
         algo_bytes = data.algorithmic_bytes(used, dict_cols, bitmap_leaves)
+    # + output_bytes of the final partial table: key + one 8-byte value per function per group
+    algo_bytes += ngroups * 8 * (1 + len(req["aggregations"]))
     # the query-specialised kernel (hiprtc, pgx_jit.cpp) unless PGX_JIT=0 selects the generic interpreter kernel
     kernel_name = "pgxq (generated per query shape)" if os.environ.get("PGX_JIT", "1") != "0" else "pgx_scan_kernel"
     achieved = algo_bytes / (kern.value * 1e-3) / 1e9
@@ -241,8 +257,6 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline and wl.name == "c2":
         cpu = cpu_baseline_c2(wl, min(rows, 32_000_000), 8, 8)
-    summary = blk.get_aggregation_result() if blk.aggregation_result is not None else \
-        {"groups": blk.get_aggregation_group_by_result().num_groups()}
     if merged[0] is not None:
         summary = {"local": summary, "merged_over_gpus": merged[0]}
     line = {

@@ -196,6 +196,12 @@ pgx_status pgx_result_group_mode(const pgx_result* r, int32_t* mode);
  * groups exceeds 20*max(top_n,1000), the indices of the top 5*max(top_n,1000) groups for function fn (MIN ascending,
  * AVG by sum/count, others descending), else all groups.  *n in: capacity, out: count written. */
 pgx_status pgx_result_trim(const pgx_result* r, int32_t fn_index, int64_t* group_index, int64_t* n);
+/* Keys and values of selected groups only (e.g. the indices pgx_result_trim returned): for group-by column c,
+ * seg_index[c*n + j] / dict_id[c*n + j] as pgx_result_group_keys; for function f, value[f*n + j] / count[f*n + j] as
+ * pgx_result_group_values.  Results that stay in device memory (sparse group-by) gather on the device and read back
+ * only these n groups.  Any output may be NULL. */
+pgx_status pgx_result_gather(const pgx_result* r, const int64_t* group_index, int64_t n, int32_t* seg_index,
+                             int32_t* dict_id, double* value, int64_t* count);
 
 /* Dense-table layout for PGX_X_KEEP_DENSE_ON_DEVICE (multi-GPU RCCL merge):
  * slots = product of group cardinalities; buffer = (1 + num_aggs) planes of slots x 8 bytes.

@@ -47,6 +47,11 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
                                                 uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream);
+extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, int kind, void* state,
+                                      int64_t* idx, uint64_t* keys, int64_t cap, int grid, hipStream_t stream);
+extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
+                                              const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
+extern "C" size_t pgx_trim_state_bytes(void);
 struct pgx_ctx;
 extern "C" void ctx_unref(pgx_ctx* ctx);
 
@@ -577,6 +582,7 @@ struct pgx_result {
     std::vector<int> gshift, gbits;
     std::vector<std::vector<int32_t>> rep_seg, rep_id;  // [col][global id]
     std::vector<int> agg_kind;
+    std::vector<std::vector<int64_t>> trims;  // per function: the device-selected trim, best first
     ~Lazy() {
       okey.reset();
       oplane.reset();
@@ -585,6 +591,9 @@ struct pgx_result {
   };
   std::unique_ptr<Lazy> lazy;
   void materialize();
+  const std::vector<int64_t>& device_trim(int fn, int64_t size);
+  void decode_lazy(const uint64_t* keys, const uint64_t* planes, int64_t n, int64_t out_stride, int32_t* seg_index,
+                   int32_t* dict_id, double* value, int64_t* count) const;
 };
 
 namespace {
@@ -1938,43 +1947,99 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
 
 }  // namespace
 
+// Decode n groups of a device-resident result (packed keys; planes p at planes[p * n], p = 0 count, 1 int64 sum,
+// 2 ordered min, 3 ordered max: pgx_part_aggregate) into column / function-major outputs of stride out_stride.
+void pgx_result::decode_lazy(const uint64_t* keys, const uint64_t* planes, int64_t n, int64_t out_stride,
+                             int32_t* seg_index, int32_t* dict_id, double* value, int64_t* count) const {
+  const Lazy& L = *lazy;
+  const int ncols = int(L.gshift.size());
+  for (int g = 0; g < ncols; ++g) {
+    const uint64_t mask = (uint64_t(1) << L.gbits[g]) - 1u;
+    for (int64_t i = 0; i < n; ++i) {
+      const uint64_t gid = (keys[i] >> L.gshift[g]) & mask;
+      if (seg_index) seg_index[g * out_stride + i] = L.rep_seg[g][gid];
+      if (dict_id) dict_id[g * out_stride + i] = L.rep_id[g][gid];
+    }
+  }
+  for (int a = 0; a < int(L.agg_kind.size()); ++a) {
+    const int k = L.agg_kind[a];
+    const int p = k == A_COUNT ? 0 : (k == A_MIN ? 2 : (k == A_MAX ? 3 : 1));
+    const int op = k == A_MIN ? P_MIN_ORD : (k == A_MAX ? P_MAX_ORD : P_ADD_I64);
+    for (int64_t i = 0; i < n; ++i) {
+      if (count) count[a * out_stride + i] = int64_t(planes[i]);
+      if (value) value[a * out_stride + i] = decode_plane(op, false, planes[size_t(p) * n + i], k);
+    }
+  }
+}
+
 // Read the partitioned group-by's groups back and decode them into the columnar host result.
 void pgx_result::materialize() {
   if (!lazy) return;
-  std::unique_ptr<Lazy> L = std::move(lazy);
   const int64_t ng = num_groups;
-  hip_check(hipSetDevice(L->ctx->device), "hipSetDevice");
+  hip_check(hipSetDevice(lazy->ctx->device), "hipSetDevice");
   std::vector<uint64_t> keys(ng), pl(size_t(4) * ng);
   if (ng) {
-    hip_check(hipMemcpy(keys.data(), L->okey.p, ng * 8, hipMemcpyDeviceToHost), "group keys D2H");
+    hip_check(hipMemcpy(keys.data(), lazy->okey.p, ng * 8, hipMemcpyDeviceToHost), "group keys D2H");
     for (int p = 0; p < 4; ++p)
-      hip_check(hipMemcpy(pl.data() + p * ng, L->oplane.as<uint64_t>() + p * L->ocap, ng * 8, hipMemcpyDeviceToHost),
+      hip_check(hipMemcpy(pl.data() + p * ng, lazy->oplane.as<uint64_t>() + p * lazy->ocap, ng * 8,
+                          hipMemcpyDeviceToHost),
                 "group planes D2H");
   }
-  const int ncols = int(L->gshift.size());
-  key_seg.assign(ncols, std::vector<int32_t>(ng));
-  key_id.assign(ncols, std::vector<int32_t>(ng));
+  const int ncols = int(lazy->gshift.size()), na = int(lazy->agg_kind.size());
+  std::vector<int32_t> seg(size_t(ncols) * ng), id(size_t(ncols) * ng);
+  std::vector<double> val(size_t(na) * ng);
+  std::vector<int64_t> cnt(size_t(na) * ng);
+  decode_lazy(keys.data(), pl.data(), ng, ng, seg.data(), id.data(), val.data(), cnt.data());
+  key_seg.assign(ncols, {});
+  key_id.assign(ncols, {});
   for (int g = 0; g < ncols; ++g) {
-    const uint64_t mask = (uint64_t(1) << L->gbits[g]) - 1u;
-    for (int64_t i = 0; i < ng; ++i) {
-      const uint64_t gid = (keys[i] >> L->gshift[g]) & mask;
-      key_seg[g][i] = L->rep_seg[g][gid];
-      key_id[g][i] = L->rep_id[g][gid];
-    }
+    key_seg[g].assign(seg.begin() + g * ng, seg.begin() + (g + 1) * ng);
+    key_id[g].assign(id.begin() + g * ng, id.begin() + (g + 1) * ng);
   }
-  const int na = int(L->agg_kind.size());
-  g_value.assign(na, std::vector<double>(ng));
-  g_count.assign(na, std::vector<int64_t>(ng));
+  g_value.assign(na, {});
+  g_count.assign(na, {});
   for (int a = 0; a < na; ++a) {
-    const int k = L->agg_kind[a];
-    // planes: 0 count, 1 int64 sum, 2 ordered min, 3 ordered max (pgx_part_aggregate)
-    const int p = k == A_COUNT ? 0 : (k == A_MIN ? 2 : (k == A_MAX ? 3 : 1));
-    const int op = k == A_MIN ? P_MIN_ORD : (k == A_MAX ? P_MAX_ORD : P_ADD_I64);
-    for (int64_t i = 0; i < ng; ++i) {
-      g_count[a][i] = int64_t(pl[i]);
-      g_value[a][i] = decode_plane(op, false, pl[size_t(p) * ng + i], k);
-    }
+    g_value[a].assign(val.begin() + a * ng, val.begin() + (a + 1) * ng);
+    g_count[a].assign(cnt.begin() + a * ng, cnt.begin() + (a + 1) * ng);
   }
+  lazy.reset();
+}
+
+// Combine trim of a device-resident result (pgx_trim.hip): indices of the `size` best groups for function fn, best
+// first (ties in index order).  Computed once per function and kept with the result.
+const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
+  Lazy& L = *lazy;
+  if (L.trims.size() < L.agg_kind.size()) L.trims.resize(L.agg_kind.size());
+  std::vector<int64_t>& out = L.trims[fn];
+  if (!out.empty()) return out;
+  hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
+  hipStream_t st = L.ctx->stream;
+  const int k = L.agg_kind[fn];
+  const int kind = k == A_COUNT ? 0 : k == A_SUM ? 1 : k == A_MIN ? 2 : k == A_MAX ? 3 : 4;
+  const size_t sb = pgx_trim_state_bytes();
+  std::vector<uint8_t> init(sb, 0);
+  const int64_t want = size;
+  const int32_t shift = 56;
+  std::memcpy(init.data() + 16, &want, 8);  // TrimState.k
+  std::memcpy(init.data() + 24, &shift, 4); // TrimState.shift
+  DevBuf state(L.ctx, sb), idx(L.ctx, size_t(size) * 8), keys(L.ctx, size_t(size) * 8);
+  hip_check(hipMemcpyAsync(state.p, init.data(), sb, hipMemcpyHostToDevice, st), "trim state H2D");
+  const int grid = int(std::max<int64_t>(1, std::min<int64_t>((num_groups + 255) / 256, int64_t(L.ctx->num_cus) * 8)));
+  hip_check(pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kind, state.p, idx.as<int64_t>(),
+                            keys.as<uint64_t>(), size, grid, st),
+            "trim launch");
+  std::vector<int64_t> ix(size);
+  std::vector<uint64_t> ky(size);
+  hip_check(hipMemcpyAsync(ix.data(), idx.p, size_t(size) * 8, hipMemcpyDeviceToHost, st), "trim D2H");
+  hip_check(hipMemcpyAsync(ky.data(), keys.p, size_t(size) * 8, hipMemcpyDeviceToHost, st), "trim D2H");
+  hip_check(hipStreamSynchronize(st), "sync");
+  std::vector<int64_t> order(size);
+  std::iota(order.begin(), order.end(), 0);
+  std::sort(order.begin(), order.end(),
+            [&](int64_t a, int64_t b) { return ky[a] != ky[b] ? ky[a] > ky[b] : ix[a] < ix[b]; });
+  out.resize(size);
+  for (int64_t i = 0; i < size; ++i) out[i] = ix[order[i]];
+  return out;
 }
 
 namespace {
@@ -2250,12 +2315,16 @@ pgx_status pgx_result_trim(const pgx_result* r, int32_t fn, int64_t* idx, int64_
   return guarded([&] {
     if (!r || !r->group_by || !n) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
     if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
-    const_cast<pgx_result*>(r)->materialize();
     const int64_t min_trim = std::max<int64_t>(r->top_n, 1000);
     const int64_t threshold = min_trim * 20, size = min_trim * 5;
-    std::vector<int64_t> order(r->num_groups);
-    std::iota(order.begin(), order.end(), 0);
-    if (r->num_groups > threshold) {
+    std::vector<int64_t> order;
+    const std::vector<int64_t>* sel = &order;
+    if (r->lazy && r->num_groups > threshold) {
+      sel = &const_cast<pgx_result*>(r)->device_trim(fn, size);  // groups stay on the device
+    } else if (r->num_groups <= threshold) {
+      order.resize(r->num_groups);
+      std::iota(order.begin(), order.end(), 0);
+    } else {
       const int f = r->agg_fn[fn];
       const auto& v = r->g_value[fn];
       const auto& c = r->g_count[fn];
@@ -2264,15 +2333,52 @@ pgx_status pgx_result_trim(const pgx_result* r, int32_t fn, int64_t* idx, int64_
         return v[i];
       };
       auto cmp = [&](int64_t a, int64_t b) { return (f == PGX_MIN) ? key(a) < key(b) : key(a) > key(b); };
+      order.resize(r->num_groups);
+      std::iota(order.begin(), order.end(), 0);
       std::nth_element(order.begin(), order.begin() + size, order.end(), cmp);
       order.resize(size);
       std::sort(order.begin(), order.end(), cmp);
     }
     if (idx) {
-      if (*n < int64_t(order.size())) fail(PGX_ERR_INVALID_ARG, "trim output capacity too small");
-      std::memcpy(idx, order.data(), order.size() * 8);
+      if (*n < int64_t(sel->size())) fail(PGX_ERR_INVALID_ARG, "trim output capacity too small");
+      std::memcpy(idx, sel->data(), sel->size() * 8);
     }
-    *n = int64_t(order.size());
+    *n = int64_t(sel->size());
+  });
+}
+
+pgx_status pgx_result_gather(const pgx_result* r, const int64_t* gi, int64_t n, int32_t* seg_index, int32_t* dict_id,
+                             double* value, int64_t* count) {
+  return guarded([&] {
+    if (!r || !r->group_by || (n > 0 && !gi) || n < 0) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    for (int64_t j = 0; j < n; ++j)
+      if (gi[j] < 0 || gi[j] >= r->num_groups) fail(PGX_ERR_INVALID_ARG, "group index out of range");
+    if (n == 0) return;
+    if (r->lazy) {
+      const auto& L = *r->lazy;
+      hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
+      hipStream_t st = L.ctx->stream;
+      DevBuf di(L.ctx, size_t(n) * 8), out(L.ctx, size_t(n) * 5 * 8);
+      std::vector<uint64_t> h(size_t(n) * 5);
+      hip_check(hipMemcpyAsync(di.p, gi, size_t(n) * 8, hipMemcpyHostToDevice, st), "gather H2D");
+      hip_check(pgx_launch_group_gather(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, di.as<int64_t>(), n,
+                                        out.as<uint64_t>(), st),
+                "gather launch");
+      hip_check(hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, st), "gather D2H");
+      hip_check(hipStreamSynchronize(st), "sync");
+      r->decode_lazy(h.data(), h.data() + n, n, n, seg_index, dict_id, value, count);
+      return;
+    }
+    for (size_t c = 0; c < r->key_seg.size(); ++c)
+      for (int64_t j = 0; j < n; ++j) {
+        if (seg_index) seg_index[c * n + j] = r->key_seg[c][gi[j]];
+        if (dict_id) dict_id[c * n + j] = r->key_id[c][gi[j]];
+      }
+    for (int a = 0; a < r->num_aggs; ++a)
+      for (int64_t j = 0; j < n; ++j) {
+        if (value) value[a * n + j] = r->g_value[a][gi[j]];
+        if (count) count[a * n + j] = r->g_count[a][gi[j]];
+      }
   });
 }
 

@@ -687,39 +687,47 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
   }
 }
 
-// One workgroup aggregates one partition in an LDS hash table (linear probing, 64-bit CAS on the key) and appends its
-// groups to the output: okey[g] = packed key, oplane[p * ocap + g] = plane p (count, int64 sum, ordered min, ordered
-// max).  pack_shift > 0: count and sum share one 64-bit LDS add ((1 << pack_shift) + value; the host checks that a
-// partition's value sum stays below bit pack_shift and its count below bit 64 - pack_shift).
-constexpr int kAggSlots = 4096;
+// One workgroup aggregates one partition in an LDS hash table and appends its groups to the output: okey[g] = packed
+// key, oplane[p * ocap + g] = plane p (count, int64 sum, ordered min, ordered max).  The table is bucketised: a key
+// hashes to a bucket of 4 slots (32 contiguous bytes, read with two 16-byte LDS loads and compared in registers), so a
+// lookup is straight-line code; a full bucket continues in the next one (rare at the planned load <= 1/3).
+// PACK: count and sum share one 64-bit LDS add ((1 << pack_shift) + value; the host checks that a partition's value
+// sum stays below bit pack_shift and its count below bit 64 - pack_shift).
+constexpr int kAggWays = 4;
+constexpr int kAggBuckets = 1024;
+constexpr int kAggSlots = kAggBuckets * kAggWays;
 constexpr int kAggThreads = 1024;
 constexpr int kAggPer = 8;
 
+template <bool PACK, bool MN, bool MX>
 __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t* __restrict__ in,
                                                                   const unsigned long long* __restrict__ in_cnt,
                                                                   int cstride, int64_t cap, uint64_t keymask,
-                                                                  int keybits, int64_t vbase, int need_sum,
-                                                                  int need_min, int need_max, int pack_shift,
+                                                                  int keybits, int64_t vbase, int pack_shift,
                                                                   uint64_t* __restrict__ okey,
                                                                   uint64_t* __restrict__ oplane, int64_t ocap,
                                                                   unsigned long long* __restrict__ ocount,
                                                                   unsigned long long* __restrict__ overflow) {
-  __shared__ uint64_t tkey[kAggSlots];
+  __shared__ __attribute__((aligned(16))) uint64_t tkey[kAggSlots];
   __shared__ unsigned long long tsum[kAggSlots];   // sum, or (count << pack_shift) + sum
-  __shared__ unsigned int tcnt[kAggSlots];
-  __shared__ unsigned int tmin[kAggSlots], tmax[kAggSlots];
+  __shared__ unsigned int tcnt[PACK ? 1 : kAggSlots];
+  __shared__ unsigned int tmin[MN ? kAggSlots : 1], tmax[MX ? kAggSlots : 1];
   __shared__ int nfound;
   __shared__ unsigned long long obase;
   const int tid = threadIdx.x;
   const int part = blockIdx.x;
   for (int i = tid; i < kAggSlots; i += kAggThreads) {
-    tkey[i] = kNoRecord; tcnt[i] = 0u; tsum[i] = 0ull; tmin[i] = 0xFFFFFFFFu; tmax[i] = 0u;
+    tkey[i] = kNoRecord;
+    tsum[i] = 0ull;
+    if (!PACK) tcnt[i] = 0u;
+    if (MN) tmin[i] = 0xFFFFFFFFu;
+    if (MX) tmax[i] = 0u;
   }
   if (tid == 0) nfound = 0;
   __syncthreads();
   const int64_t n = min(static_cast<int64_t>(in_cnt[static_cast<int64_t>(part) * cstride]), cap);
   const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) + static_cast<int64_t>(part) * cap;
-  const unsigned long long one = pack_shift ? (1ull << pack_shift) : 0ull;
+  const unsigned long long one = PACK ? (1ull << pack_shift) : 0ull;
   bool lost = false;
   for (int64_t base = 0; base < n; base += kAggThreads * kAggPer) {
     uint64_t rec[kAggPer];
@@ -728,45 +736,37 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
       const int64_t i = base + k * kAggThreads + tid;
       rec[k] = i < n ? __builtin_nontemporal_load(src + i) : kNoRecord;
     }
-    // home-slot reads of all kAggPer records first (independent LDS reads in flight); most keys sit at home
-    unsigned int h[kAggPer];
-    uint64_t kk[kAggPer];
-#pragma unroll
-    for (int k = 0; k < kAggPer; ++k) {
-      h[k] = static_cast<unsigned int>(part_mix(rec[k] & keymask)) & (kAggSlots - 1);
-      kk[k] = tkey[h[k]];
-    }
 #pragma unroll
     for (int k = 0; k < kAggPer; ++k) {
       if (rec[k] == kNoRecord) continue;
       const uint64_t key = rec[k] & keymask;
       const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);
-      unsigned int hh = h[k];
-      if (kk[k] != key) {  // linear probing from the home slot; CAS claims an empty slot
-        uint64_t cur = kk[k];
-        int probes = 0;
-        while (true) {
-          if (cur == kNoRecord) {
-            const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[hh]), kNoRecord, key);
-            if (prev == kNoRecord || prev == key) break;
-            cur = prev;
-            continue;  // lost the race for this slot to another key: keep probing
-          }
-          if (cur == key) break;
-          if (++probes == kAggSlots) break;
-          hh = (hh + 1) & (kAggSlots - 1);
-          cur = tkey[hh];
+      unsigned int bk = static_cast<unsigned int>(part_mix(key)) & (kAggBuckets - 1);
+      int slot = -1;
+      for (int t = 0; t < kAggBuckets;) {
+        const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(&tkey[bk * kAggWays]);
+        const ulonglong2 a = bp[0], c = bp[1];
+        const int m = a.x == key ? 0 : a.y == key ? 1 : c.x == key ? 2 : c.y == key ? 3 : -1;
+        if (m >= 0) { slot = static_cast<int>(bk) * kAggWays + m; break; }
+        const int e = a.x == kNoRecord ? 0 : a.y == kNoRecord ? 1 : c.x == kNoRecord ? 2 : c.y == kNoRecord ? 3 : -1;
+        if (e >= 0) {
+          const int cand = static_cast<int>(bk) * kAggWays + e;
+          const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[cand]), kNoRecord, key);
+          if (prev == kNoRecord || prev == key) { slot = cand; break; }
+          continue;  // another key took that slot first: re-read this bucket
         }
-        if (probes == kAggSlots) { lost = true; continue; }
+        bk = (bk + 1) & (kAggBuckets - 1);
+        ++t;
       }
-      if (pack_shift) {
-        atomicAdd(&tsum[hh], one + v);
+      if (slot < 0) { lost = true; continue; }
+      if (PACK) {
+        atomicAdd(&tsum[slot], one + v);
       } else {
-        atomicAdd(&tcnt[hh], 1u);
-        if (need_sum) atomicAdd(&tsum[hh], static_cast<unsigned long long>(v));
+        atomicAdd(&tcnt[slot], 1u);
+        atomicAdd(&tsum[slot], static_cast<unsigned long long>(v));
       }
-      if (need_min) atomicMin(&tmin[hh], v);
-      if (need_max) atomicMax(&tmax[hh], v);
+      if (MN) atomicMin(&tmin[slot], v);
+      if (MX) atomicMax(&tmax[slot], v);
     }
   }
   if (lost) atomicAdd(overflow, 1ull);
@@ -779,18 +779,19 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
   if (tid == 0) obase = atomicAdd(ocount, static_cast<unsigned long long>(nfound));
   __syncthreads();
   unsigned long long o = obase + static_cast<unsigned long long>(before);
-  const unsigned long long smask = pack_shift ? (1ull << pack_shift) - 1ull : ~0ull;
+  const unsigned long long smask = PACK ? (1ull << pack_shift) - 1ull : ~0ull;
   for (int i = tid; i < kAggSlots; i += kAggThreads) {
     if (tkey[i] == kNoRecord) continue;
     if (o >= static_cast<unsigned long long>(ocap)) { atomicAdd(overflow, 1ull); continue; }
     okey[o] = tkey[i];
-    const unsigned long long c = pack_shift ? (tsum[i] >> pack_shift) : tcnt[i];
+    const unsigned long long c = PACK ? (tsum[i] >> pack_shift) : tcnt[i];
     const unsigned long long sm = tsum[i] & smask;
+    const unsigned int lo = MN ? tmin[i] : 0u, hi = MX ? tmax[i] : 0u;
     oplane[o] = c;  // plane 0: doc count
     // planes 1..3: sum (int64 incl. vbase * count), min, max (ordered encodings of the int64 value)
     oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(sm) + static_cast<int64_t>(c) * vbase);
-    oplane[2 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(tmin[i])) ^ 0x8000000000000000ull;
-    oplane[3 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(tmax[i])) ^ 0x8000000000000000ull;
+    oplane[2 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(lo)) ^ 0x8000000000000000ull;
+    oplane[3 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(hi)) ^ 0x8000000000000000ull;
     ++o;
   }
 }
@@ -931,9 +932,25 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
                                                 uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream) {
+  (void)need_sum;  // sums are always accumulated (one add)
   if (nparts <= 0) return hipSuccess;
-  hipLaunchKernelGGL(pgx::pgx_part_aggregate, dim3(nparts), dim3(pgx::kAggThreads), 0, stream, in, in_cnt, cstride,
-                     cap, keymask, keybits, vbase, need_sum, need_min, need_max, pack_shift, okey, oplane, ocap,
-                     ocount, overflow);
+  const int sel = (pack_shift ? 4 : 0) | (need_min ? 2 : 0) | (need_max ? 1 : 0);
+#define PGX_AGG_CASE(K, A, B, C)                                                                                   \
+  case K:                                                                                                           \
+    hipLaunchKernelGGL((pgx::pgx_part_aggregate<A, B, C>), dim3(nparts), dim3(pgx::kAggThreads), 0, stream, in,     \
+                       in_cnt, cstride, cap, keymask, keybits, vbase, pack_shift, okey, oplane, ocap, ocount,       \
+                       overflow);                                                                                   \
+    break;
+  switch (sel) {
+    PGX_AGG_CASE(0, false, false, false)
+    PGX_AGG_CASE(1, false, false, true)
+    PGX_AGG_CASE(2, false, true, false)
+    PGX_AGG_CASE(3, false, true, true)
+    PGX_AGG_CASE(4, true, false, false)
+    PGX_AGG_CASE(5, true, false, true)
+    PGX_AGG_CASE(6, true, true, false)
+    PGX_AGG_CASE(7, true, true, true)
+  }
+#undef PGX_AGG_CASE
   return hipGetLastError();
 }

@@ -527,6 +527,44 @@ def decode_result(q: _Query, r, segments: Sequence[IndexSegment], trim: bool = F
     return blk
 
 
+def trim_and_gather(q: _Query, r):
+    """Combine trim of a group-by result (pgx_result_trim, AggregationGroupByOperatorService.trimToSize) and the
+    kept groups only (pgx_result_gather): per function (seg_index[ncols, n], dict_id[ncols, n], value[n], count[n]).
+    For results that stay in device memory neither call reads the other groups back."""
+    L = N.lib()
+    ncols, nf = len(q.group_cols), len(q.fns)
+    out = []
+    for i in range(nf):
+        cap = C.c_int64(0)
+        N.check(L.pgx_result_trim(r, i, None, C.byref(cap)))
+        n = cap.value
+        idx = np.zeros(max(n, 1), dtype=np.int64)
+        N.check(L.pgx_result_trim(r, i, idx.ctypes.data, C.byref(cap)))
+        si = np.zeros(max(n * ncols, 1), dtype=np.int32)
+        di = np.zeros(max(n * ncols, 1), dtype=np.int32)
+        v = np.zeros(max(n * nf, 1), dtype=np.float64)
+        c = np.zeros(max(n * nf, 1), dtype=np.int64)
+        N.check(L.pgx_result_gather(r, idx.ctypes.data, n, si.ctypes.data, di.ctypes.data, v.ctypes.data,
+                                    c.ctypes.data))
+        out.append((si[:n * ncols].reshape(ncols, n), di[:n * ncols].reshape(ncols, n), v[i * n:(i + 1) * n],
+                    c[i * n:(i + 1) * n]))
+    return out
+
+
+def trimmed_maps(q: _Query, r, segments: Sequence[IndexSegment]) -> List[Dict[str, object]]:
+    """trim_and_gather rendered like the reference's trimmed combine output: one {string key: value} map per
+    function (count -> int, avg -> (sum, count), others -> float)."""
+    maps = []
+    for fn, (si, di, v, c) in zip(q.fns, trim_and_gather(q, r)):
+        infos = [[seg.column(col) for seg in segments] for col in q.group_cols]
+        m = {}
+        for j in range(len(v)):
+            key = "\t".join(infos[g][si[g, j]].string_of(int(di[g, j])) for g in range(len(q.group_cols)))
+            m[key] = int(c[j]) if fn == "count" else ((float(v[j]), int(c[j])) if fn == "avg" else float(v[j]))
+        maps.append(m)
+    return maps
+
+
 # ------------------------------------------------------------------------------------------------
 # Operators / plan nodes / plan maker
 # ------------------------------------------------------------------------------------------------

@@ -99,6 +99,8 @@ EXPORTS = {
     "pgx_result_group_values": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     "pgx_result_group_mode": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "pgx_result_trim": (C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.POINTER(C.c_int64)]),
+    "pgx_result_gather": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p]),
     "pgx_query_dense_slots": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(C.c_int64)]),
     "pgx_query_dense_plane_op": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.c_int32,
                                            C.POINTER(C.c_int32)]),

@@ -157,3 +157,50 @@ def test_partitioned_debug_resize_and_fallback(ctx, monkeypatch, n, card):
     for k, (c, s, lo, hi) in exp.items():
         g = got[k]
         assert (int(g[0]), float(g[1]), float(g[2]), float(g[3])) == (c, s, lo, hi)
+
+
+def _trim_expect(exp, fn, size=5000):
+    rows = list(exp.values())
+    if fn == "count":
+        vals = sorted((r[0] for r in rows), reverse=True)
+    elif fn == "sum":
+        vals = sorted((r[1] for r in rows), reverse=True)
+    elif fn == "min":
+        vals = sorted(r[2] for r in rows)
+    elif fn == "max":
+        vals = sorted((r[3] for r in rows), reverse=True)
+    else:
+        vals = sorted((r[1] / r[0] for r in rows), reverse=True)
+    return vals[:size]
+
+
+@pytest.mark.parametrize("flags", [0, "table"])
+def test_combine_trim_on_device(ctx, flags):
+    """Combine trim (a-19) over more than 20,000 groups: the 5,000 best groups per function (MIN ascending, AVG by
+    sum/count).  Sparse results trim on the device (radix select) and read back only the kept groups; the hash-table
+    path trims on the host.  Kept values must equal the expected top values (ties at the threshold are unpinned, so
+    values are compared as sorted lists) and every kept group must carry its own untrimmed value."""
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    gseg, raw = _pairs_segment(ctx, 300000, 700, seed=77)
+    exp = _expected(raw)
+    assert len(exp) > 20000
+    q = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m), AVG(m) FROM t GROUP BY ga, gb")
+    qq = E._Query(ctx, q)
+    r = qq.execute([gseg], flags=N.PGX_X_NO_PARTITION if flags == "table" else 0)
+    try:
+        maps = E.trimmed_maps(qq, r, [gseg])
+    finally:
+        N.lib().pgx_result_release(r)
+    for i, fn in enumerate(qq.fns):
+        m = maps[i]
+        assert len(m) == 5000
+        if fn == "avg":
+            got = sorted((s / c for s, c in m.values()), reverse=True)
+        else:
+            got = sorted(m.values(), reverse=(fn != "min"))
+        assert got == _trim_expect(exp, fn), fn
+        col = {"count": 0, "sum": 1, "min": 2, "max": 3}.get(fn)
+        for k, v in m.items():
+            e = exp[k]
+            assert (v == (float(e[1]), e[0])) if fn == "avg" else (v == e[col]), (fn, k, v, e)
