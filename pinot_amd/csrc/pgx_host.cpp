@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -2074,15 +2075,43 @@ void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, 
   R->lazy = std::move(L);
 }
 
+// PGX_HOST_PROFILE=1: per-phase host wall time of every pgx_execute on stderr (host overhead hunting).
+struct HostProf {
+  bool on = false;
+  std::chrono::steady_clock::time_point t0, last;
+  std::string line;
+  HostProf() {
+    const char* e = std::getenv("PGX_HOST_PROFILE");
+    on = e && e[0] == '1';
+    if (on) t0 = last = std::chrono::steady_clock::now();
+  }
+  void mark(const char* what) {
+    if (!on) return;
+    const auto t = std::chrono::steady_clock::now();
+    line += std::string(" ") + what + "=" + std::to_string(std::chrono::duration<double, std::micro>(t - last).count());
+    last = t;
+  }
+  ~HostProf() {
+    if (on)
+      std::fprintf(stderr, "[pgx host us] total=%.1f%s\n",
+                   std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count(),
+                   line.c_str());
+  }
+};
+
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                const pgx_exec_opts* opts, pgx_result* R) {
+  HostProf hp;
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
   const uint32_t xflags = opts ? opts->flags : 0;
   ExecPlan P;
   plan_query(ctx, q, segs, n, bindings, xflags, P);
+  hp.mark("plan");
   ExecBuffers B;
   upload_plan(ctx, P, B, st);
+  hp.mark("upload");
   plan_jit(ctx, q, segs, n, P, B);
+  hp.mark("jit");
   if (P.use_part) {
     PartBuffers PB;
     if (run_partitioned(ctx, P, B, PB, st)) {
@@ -2098,6 +2127,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
     reset_outputs(P, B, st);
     launch_scan(P, st);
+    hp.mark("launch");
     if (!hash) break;
     unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
     hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
@@ -2121,6 +2151,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     return;
   }
   finish_result(ctx, q, P, B, segs, n, st, R, nullptr);
+  hp.mark("finish");
 }
 
 }  // namespace
