@@ -9,6 +9,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <exception>
+#include <functional>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -115,8 +119,83 @@ uint64_t padded_fwd_bytes(int64_t total_docs, int bits) {
 // =================================================================================================
 // Context
 // =================================================================================================
+// Host worker pool of a context: per-segment query planning of large segment lists runs on it (C5: 4096 segments).
+// run(n, f) calls f(i) for i in [0, n) on the workers and the caller; the first exception is rethrown to the caller.
+struct WorkerPool {
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv, done_cv;
+  const std::function<void(int)>* job = nullptr;
+  int njobs = 0, pending = 0;
+  std::atomic<int> next{0};
+  uint64_t gen = 0;
+  bool stop = false;
+  std::exception_ptr err;
+
+  void work() {
+    for (int i; (i = next.fetch_add(1)) < njobs;) {
+      try {
+        (*job)(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(m);
+        if (!err) err = std::current_exception();
+      }
+    }
+  }
+  void start(int nthreads) {
+    for (int t = 0; t < nthreads; ++t)
+      th.emplace_back([this] {
+        uint64_t seen = 0;
+        for (;;) {
+          {
+            std::unique_lock<std::mutex> g(m);
+            cv.wait(g, [&] { return stop || gen != seen; });
+            if (stop) return;
+            seen = gen;
+          }
+          work();
+          std::lock_guard<std::mutex> g(m);
+          if (--pending == 0) done_cv.notify_all();
+        }
+      });
+  }
+  void run(int n, const std::function<void(int)>& f) {
+    std::unique_lock<std::mutex> g(m);
+    job = &f;
+    njobs = n;
+    next = 0;
+    err = nullptr;
+    pending = int(th.size());
+    ++gen;
+    cv.notify_all();
+    g.unlock();
+    work();
+    g.lock();
+    done_cv.wait(g, [&] { return pending == 0; });
+    job = nullptr;
+    if (err) std::rethrow_exception(err);
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+};
+
 struct pgx_ctx {
   std::atomic<int> refs{1};  // the caller's handle + one per staged segment
+  WorkerPool pool;           // started lazily (first large query)
+  std::once_flag pool_once;
+  void parallel_for(int n, const std::function<void(int)>& f) {
+    std::call_once(pool_once, [this] {
+      const unsigned hc = std::thread::hardware_concurrency();
+      pool.start(int(std::min<unsigned>(15, hc > 1 ? hc - 1 : 1)));  // + the caller: 16 (the box's CPU share)
+    });
+    pool.run(n, f);
+  }
   int device = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
@@ -1179,111 +1258,148 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     K.prog_arg[i] = parg[i];
   }
 
-  // per-segment descriptors
+  // per-segment descriptors: planned in chunks of segments (in parallel for long segment lists); each chunk keeps its
+  // blob words, pointer fixups and bitmap items with chunk-local offsets, concatenated in segment order afterwards.
   P.ksegs.assign(n, KSeg{});
   P.segcols.assign(n, {});
+  struct ChunkOut {
+    std::vector<int32_t> blob;
+    std::vector<ExecPlan::Fix> fixes;
+    std::vector<ExecPlan::RoarItem> roar;
+    int64_t total_raw = 0, host_entries = 0;
+    uint64_t mask_words = 0;
+    int maxchunks = 0;
+  };
+  const int kSegsPerChunk = 64;
+  const int nchunk = (n + kSegsPerChunk - 1) / kSegsPerChunk;
+  std::vector<ChunkOut> chunks(nchunk);
+  auto plan_chunk = [&](int ci) {
+    ChunkOut& o = chunks[ci];
+    for (int s = ci * kSegsPerChunk; s < std::min(n, (ci + 1) * kSegsPerChunk); ++s) {
+      const pgx_segment& seg = *segs[s];
+      KSeg& S = P.ksegs[s];
+      S.num_docs = seg.total_raw_docs;  // MatchEntireSegment / FilterPlanNode scan range [0, totalRawDocs)
+      S.num_tiles = int32_t((int64_t(S.num_docs) + kTileRows - 1) / kTileRows);
+      o.total_raw += seg.total_raw_docs;
+      o.host_entries += int64_t(host_scan_leaves) * seg.total_raw_docs;
+      auto& segcols = P.segcols[s];
+      segcols.resize(P.qcols.size());
+      for (size_t c = 0; c < P.qcols.size(); ++c) {
+        const StagedColumn& col = seg.col(P.qcols[c]);
+        segcols[c] = &col;
+        S.fwd[c] = col.fwd;
+        S.bits[c] = int8_t(col.bits);
+        S.dict[c] = col.dict_dev;
+        S.remap[c] = nullptr;
+      }
+      for (int g = 0; g < K.num_gcols; ++g) {
+        if (!P.gdicts[g].identity) {
+          const auto& rm = P.gdicts[g].remap[s];
+          o.fixes.push_back({size_t(s), 0, K.gcol[g], o.blob.size()});
+          o.blob.insert(o.blob.end(), rm.begin(), rm.end());
+        }
+      }
+      // leaves
+      for (size_t l = 0; l < q.leaf_col.size(); ++l) {
+        const StagedColumn& col = *segcols[K.leaf_col[l]];
+        const pgx_leaf_binding& b = bindings[size_t(s) * q.leaf_col.size() + l];
+        KLeaf& L = S.leaf[l];
+        L.lo = b.lo;
+        L.hi = b.hi;
+        L.bitset = nullptr;
+        L.ranges = nullptr;
+        L.nranges = 0;
+        // matching dictIds
+        auto matches = [&](int id) -> bool {
+          if (b.words) return (b.words[id >> 5] >> (id & 31)) & 1u;
+          return id >= b.lo && id <= b.hi;
+        };
+        if (col.is_sorted) {
+          // SortedInvertedIndexBasedFilterOperator (additive ranges, merged), clipped to [0, totalRawDocs-1]
+          std::vector<int32_t> r;
+          for (int id = 0; id < col.card; ++id) {
+            if (!matches(id)) continue;
+            int32_t a = std::max(col.sorted_first[id], 0);
+            int32_t e = std::min(col.sorted_last[id], seg.total_raw_docs - 1);
+            if (e < a) continue;
+            if (!r.empty() && a <= r.back() + 1) r.back() = std::max(r.back(), e);
+            else { r.push_back(a); r.push_back(e); }
+          }
+          if (r.empty()) { L.mode = LEAF_NONE; continue; }
+          L.mode = LEAF_RANGES;
+          L.nranges = int32_t(r.size() / 2);
+          o.fixes.push_back({size_t(s), 1, int(l), o.blob.size()});
+          o.blob.insert(o.blob.end(), r.begin(), r.end());
+        } else if (b.words) {
+          bool any = false;
+          const int nw = (col.card + 31) / 32;
+          for (int w = 0; w < nw && !any; ++w) any = b.words[w] != 0;
+          if (!any) { L.mode = LEAF_NONE; continue; }
+          L.mode = LEAF_SCAN_BITSET;
+          o.fixes.push_back({size_t(s), 2, int(l), o.blob.size()});
+          for (int w = 0; w < nw; ++w) o.blob.push_back(int32_t(b.words[w]));
+        } else {
+          L.mode = (b.hi < b.lo) ? LEAF_NONE : LEAF_SCAN_INTERVAL;
+        }
+        if (P.use_docmask && L.mode != LEAF_NONE && P.leaf_phys[l] == PH_BITMAP && col.inv_dev.p) {
+          // BitmapBasedFilterOperator (operator/filter/BitmapBasedFilterOperator.java:62-92): OR the roaring bitmaps
+          // of the matching dictIds; NEQ / NOT_IN OR the NON-matching ones and flip over the scanned doc range.
+          const bool neg = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
+          ExecPlan::RoarItem it{s, int(l), neg, o.blob.size(), 0, int((int64_t(seg.total_docs) + 65535) >> 16),
+                                o.mask_words, col.inv_dev.p};
+          auto take = [&](int id) {
+            o.blob.push_back(int32_t(col.inv_off[id]));
+            ++it.nb;
+          };
+          if (b.words) {  // walk the set (or, negated, the clear) bits of the dictId bitset
+            const int nw = (col.card + 31) / 32;
+            for (int w = 0; w < nw; ++w) {
+              uint32_t x = neg ? ~b.words[w] : b.words[w];
+              if (w == nw - 1 && (col.card & 31)) x &= (1u << (col.card & 31)) - 1u;
+              while (x) {
+                take(w * 32 + __builtin_ctz(x));
+                x &= x - 1u;
+              }
+            }
+          } else if (!neg) {
+            for (int id = std::max(0, b.lo); id <= std::min(b.hi, col.card - 1); ++id) take(id);
+          } else {
+            for (int id = 0; id < col.card; ++id)
+              if (id < b.lo || id > b.hi) take(id);
+          }
+          o.mask_words += uint64_t(it.nchunks) * 2048;
+          o.maxchunks = std::max(o.maxchunks, it.nchunks);
+          o.roar.push_back(it);
+        }
+      }
+    }
+  };
+  if (nchunk > 1) ctx->parallel_for(nchunk, plan_chunk);
+  else if (nchunk == 1) plan_chunk(0);
   int64_t tiles = 0;
   P.total_raw = 0;
   for (int s = 0; s < n; ++s) {
-    const pgx_segment& seg = *segs[s];
-    KSeg& S = P.ksegs[s];
-    S.tile_begin = tiles;
-    S.num_docs = seg.total_raw_docs;  // MatchEntireSegment / FilterPlanNode scan range [0, totalRawDocs)
-    S.num_tiles = int32_t((int64_t(S.num_docs) + kTileRows - 1) / kTileRows);
-    tiles += S.num_tiles;
-    P.total_raw += seg.total_raw_docs;
-    P.host_entries += int64_t(host_scan_leaves) * seg.total_raw_docs;
-    auto& segcols = P.segcols[s];
-    segcols.resize(P.qcols.size());
-    for (size_t c = 0; c < P.qcols.size(); ++c) {
-      const StagedColumn& col = seg.col(P.qcols[c]);
-      segcols[c] = &col;
-      S.fwd[c] = col.fwd;
-      S.bits[c] = int8_t(col.bits);
-      S.dict[c] = col.dict_dev;
-      S.remap[c] = nullptr;
+    P.ksegs[s].tile_begin = tiles;
+    tiles += P.ksegs[s].num_tiles;
+  }
+  for (ChunkOut& o : chunks) {
+    const size_t base = P.blob32.size();
+    const uint64_t mbase = P.mask_words;
+    P.blob32.insert(P.blob32.end(), o.blob.begin(), o.blob.end());
+    for (auto f : o.fixes) {
+      f.off += base;
+      P.fixes.push_back(f);
     }
-    for (int g = 0; g < K.num_gcols; ++g) {
-      if (!P.gdicts[g].identity) {
-        const auto& rm = P.gdicts[g].remap[s];
-        P.fixes.push_back({size_t(s), 0, K.gcol[g], P.blob32.size()});
-        P.blob32.insert(P.blob32.end(), rm.begin(), rm.end());
-      }
+    for (auto it : o.roar) {
+      it.blob_off += base;
+      it.mask_off += mbase;
+      P.roar_index[it.seg][it.leaf] = int(P.roar.size());
+      P.roar.push_back(it);
     }
-    // leaves
-    for (size_t l = 0; l < q.leaf_col.size(); ++l) {
-      const StagedColumn& col = *segcols[K.leaf_col[l]];
-      const pgx_leaf_binding& b = bindings[size_t(s) * q.leaf_col.size() + l];
-      KLeaf& L = S.leaf[l];
-      L.lo = b.lo;
-      L.hi = b.hi;
-      L.bitset = nullptr;
-      L.ranges = nullptr;
-      L.nranges = 0;
-      // matching dictIds
-      auto matches = [&](int id) -> bool {
-        if (b.words) return (b.words[id >> 5] >> (id & 31)) & 1u;
-        return id >= b.lo && id <= b.hi;
-      };
-      if (col.is_sorted) {
-        // SortedInvertedIndexBasedFilterOperator (additive ranges, merged), clipped to [0, totalRawDocs-1]
-        std::vector<int32_t> r;
-        for (int id = 0; id < col.card; ++id) {
-          if (!matches(id)) continue;
-          int32_t a = std::max(col.sorted_first[id], 0);
-          int32_t e = std::min(col.sorted_last[id], seg.total_raw_docs - 1);
-          if (e < a) continue;
-          if (!r.empty() && a <= r.back() + 1) r.back() = std::max(r.back(), e);
-          else { r.push_back(a); r.push_back(e); }
-        }
-        if (r.empty()) { L.mode = LEAF_NONE; continue; }
-        L.mode = LEAF_RANGES;
-        L.nranges = int32_t(r.size() / 2);
-        P.fixes.push_back({size_t(s), 1, int(l), P.blob32.size()});
-        P.blob32.insert(P.blob32.end(), r.begin(), r.end());
-      } else if (b.words) {
-        bool any = false;
-        const int nw = (col.card + 31) / 32;
-        for (int w = 0; w < nw && !any; ++w) any = b.words[w] != 0;
-        if (!any) { L.mode = LEAF_NONE; continue; }
-        L.mode = LEAF_SCAN_BITSET;
-        P.fixes.push_back({size_t(s), 2, int(l), P.blob32.size()});
-        for (int w = 0; w < nw; ++w) P.blob32.push_back(int32_t(b.words[w]));
-      } else {
-        L.mode = (b.hi < b.lo) ? LEAF_NONE : LEAF_SCAN_INTERVAL;
-      }
-      if (P.use_docmask && L.mode != LEAF_NONE && P.leaf_phys[l] == PH_BITMAP && col.inv_dev.p) {
-        // BitmapBasedFilterOperator (operator/filter/BitmapBasedFilterOperator.java:62-92): OR the roaring bitmaps of
-        // the matching dictIds; NEQ / NOT_IN OR the NON-matching ones and flip over the scanned doc range.
-        const bool neg = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
-        ExecPlan::RoarItem it{s, int(l), neg, P.blob32.size(), 0, int((int64_t(seg.total_docs) + 65535) >> 16),
-                              P.mask_words, col.inv_dev.p};
-        auto take = [&](int id) {
-          P.blob32.push_back(int32_t(col.inv_off[id]));
-          ++it.nb;
-        };
-        if (b.words) {  // walk the set (or, negated, the clear) bits of the dictId bitset
-          const int nw = (col.card + 31) / 32;
-          for (int w = 0; w < nw; ++w) {
-            uint32_t x = neg ? ~b.words[w] : b.words[w];
-            if (w == nw - 1 && (col.card & 31)) x &= (1u << (col.card & 31)) - 1u;
-            while (x) {
-              take(w * 32 + __builtin_ctz(x));
-              x &= x - 1u;
-            }
-          }
-        } else if (!neg) {
-          for (int id = std::max(0, b.lo); id <= std::min(b.hi, col.card - 1); ++id) take(id);
-        } else {
-          for (int id = 0; id < col.card; ++id)
-            if (id < b.lo || id > b.hi) take(id);
-        }
-        P.mask_words += uint64_t(it.nchunks) * 2048;
-        P.roar_maxchunks = std::max(P.roar_maxchunks, it.nchunks);
-        P.roar_index[s][l] = int(P.roar.size());
-        P.roar.push_back(it);
-      }
-    }
+    P.mask_words += o.mask_words;
+    P.roar_maxchunks = std::max(P.roar_maxchunks, o.maxchunks);
+    P.total_raw += o.total_raw;
+    P.host_entries += o.host_entries;
   }
   // star-tree segments (query kernels only: the per-segment program needs the generated kernels)
   P.star.assign(n, ExecPlan::StarPlan{});
@@ -1677,7 +1793,41 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
                    hipStream_t st, pgx_result* R, const unsigned long long* dense_host_override) {
   KQuery& K = P.kq;
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
-  if (!dense_host_override) {  // one read-back of every output plane and statistic
+  const bool hash = K.group_mode == G_HASH64 || K.group_mode == G_HASH128;
+  const bool dense_dev = K.num_gcols > 0 && !hash && !dense_host_override;
+  // group-by compaction (occupied slots -> columnar), read back together with the outputs block: ONE sync
+  const uint64_t slots = hash ? P.hash_cap : P.dense_slots;
+  std::vector<int64_t> slot_ids;
+  std::vector<unsigned long long> planes;  // [plane][group]
+  uint64_t ng = 0;
+  if (dense_dev) {
+    uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(slots, uint64_t(1) << 16));
+    for (;;) {
+      const size_t bytes = 256 + size_t(cap) * 8 * (1 + K.num_planes);
+      DevBuf res(ctx, bytes);
+      PinnedBuf hres(ctx, bytes);
+      hip_check(hipMemsetAsync(res.p, 0, 8, st), "memset");
+      unsigned long long* rb = devp(res);
+      hip_check(pgx_launch_compact(K.table, slots, K.num_planes, rb, reinterpret_cast<int64_t*>(rb + 32), rb + 32 + cap,
+                                   cap, st),
+                "compact");
+      hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
+      hip_check(hipMemcpyAsync(hres.p, res.p, bytes, hipMemcpyDeviceToHost, st), "groups D2H");
+      hip_check(hipStreamSynchronize(st), "sync");
+      const unsigned long long* h = reinterpret_cast<const unsigned long long*>(hres.p);
+      const uint64_t cnt = h[0];
+      if (cnt > cap) {  // more groups than the first guess: once more at the exact size
+        cap = cnt;
+        continue;
+      }
+      ng = cnt;
+      slot_ids.assign(reinterpret_cast<const int64_t*>(h + 32), reinterpret_cast<const int64_t*>(h + 32) + ng);
+      planes.resize(ng * K.num_planes);
+      for (int p = 0; p < K.num_planes; ++p)
+        std::memcpy(planes.data() + p * ng, h + 32 + cap + p * cap, ng * 8);
+      break;
+    }
+  } else if (!dense_host_override) {  // one read-back of every output plane and statistic
     hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
     hip_check(hipStreamSynchronize(st), "sync");
   }
@@ -1707,12 +1857,6 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     }
     return;
   }
-  // group-by: compact occupied slots
-  const bool hash = K.group_mode == G_HASH64 || K.group_mode == G_HASH128;
-  const uint64_t slots = hash ? P.hash_cap : P.dense_slots;
-  std::vector<int64_t> slot_ids;
-  std::vector<unsigned long long> planes;  // [plane][group]
-  uint64_t ng = 0;
   if (dense_host_override) {
     for (uint64_t s = 0; s < slots; ++s)
       if (dense_host_override[s]) slot_ids.push_back(int64_t(s));
@@ -1720,7 +1864,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     planes.resize(ng * K.num_planes);
     for (int p = 0; p < K.num_planes; ++p)
       for (uint64_t i = 0; i < ng; ++i) planes[p * ng + i] = dense_host_override[p * slots + slot_ids[i]];
-  } else {
+  } else if (hash) {
     DevBuf counter(ctx, 64);
     hip_check(hipMemsetAsync(counter.p, 0, 8, st), "memset");
     const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(slots, uint64_t(std::max<int64_t>(stats[0], 1))));
