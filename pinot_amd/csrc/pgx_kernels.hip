@@ -519,10 +519,110 @@ __global__ void pgx_compact(const unsigned long long* table, uint64_t slots, int
 // containers word by word) and writes the 2048 mask words to HBM with coalesced stores.  Roaring bytes are only
 // 2-byte aligned inside the inverted-index file, so multi-byte fields are read as u16 pairs.
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rd16(const uint8_t* p) { return *reinterpret_cast<const uint16_t*>(p); }
+#define PGX_GLOBAL __attribute__((address_space(1)))
+// Global-address-space loads: flat loads would share the LDS counter with the mask atomics and serialise them.
+__device__ __forceinline__ uint32_t rd16(const uint8_t* p) { return *(const PGX_GLOBAL uint16_t*)(p); }
 __device__ __forceinline__ uint32_t rd32(const uint8_t* p) { return rd16(p) | (rd16(p + 2) << 16); }
 
 constexpr int kRoarBatch = 256;
+
+// ORs the containers of D's bitmaps for one chunk into the LDS mask m (2048 words, zeroed by the caller).  Every
+// thread of the 256-lane workgroup must call it (it synchronises).
+__device__ void roar_or_chunk(const RDesc& D, int chunk, uint32_t* m, const uint8_t** cptr, int* ccard, int* cpre,
+                              int* ncont, int* celems) {
+  const int tid = threadIdx.x;
+  for (int b0 = 0; b0 < D.nb; b0 += kRoarBatch) {
+    if (tid == 0) *ncont = 0;
+    __syncthreads();
+    const int b = b0 + tid;
+    if (b < D.nb) {
+      const uint8_t* base = D.inv + D.offs[b];
+      const int n = static_cast<int>(rd32(base + 4));
+      // keys are sorted and distinct, so a bitmap with a container in every chunk holds chunk c at index c: probe
+      // there first (one load for dense bitmaps), then binary-search the rest of the range
+      int lo = 0, hi = n - 1, found = -1;
+      const int g = min(chunk, n - 1);
+      if (g >= 0) {
+        const uint32_t kv = rd32(base + 8 + 4 * g);  // key | (card - 1) << 16
+        const int k = static_cast<int>(kv & 0xFFFFu);
+        if (k == chunk) found = g;
+        else if (k < chunk) lo = g + 1;
+        else hi = g - 1;
+      }
+      while (found < 0 && lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const int k = static_cast<int>(rd16(base + 8 + 4 * mid));
+        if (k == chunk) { found = mid; break; }
+        if (k < chunk) lo = mid + 1; else hi = mid - 1;
+      }
+      if (found >= 0) {
+        const int card = static_cast<int>(rd16(base + 8 + 4 * found + 2)) + 1;
+        const uint32_t off = rd32(base + 8 + 4 * n + 4 * found);
+        const int slot = atomicAdd(ncont, 1);
+        cptr[slot] = base + off;
+        ccard[slot] = card;
+      }
+    }
+    __syncthreads();
+    const int nc = *ncont;
+    // array containers: exclusive prefix of their cardinalities (wave 0, 4 entries per lane), then every lane takes
+    // elements of any container with 4 loads in flight before the LDS atomics (a loop over containers would chain one
+    // global-load latency per container)
+    if (tid < 64) {
+      int v[4], x = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = tid * 4 + j;
+        v[j] = (k < nc && ccard[k] <= 4096) ? ccard[k] : 0;
+        x += v[j];
+      }
+      int incl = x;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (tid >= d) incl += y;
+      }
+      int e = incl - x;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        cpre[tid * 4 + j] = e;
+        e += v[j];
+      }
+      if (tid == 63) *celems = incl;
+    }
+    __syncthreads();
+    const int ne = *celems;
+    for (int e0 = 0; e0 < ne; e0 += 4 * 256) {
+      uint32_t val[4];
+      bool ok[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int e = e0 + j * 256 + tid;
+        ok[j] = e < ne;
+        if (ok[j]) {
+          int lo = 0, hi = nc - 1;  // the last container with cpre <= e holds element e (empty parts repeat cpre)
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cpre[mid] <= e) lo = mid; else hi = mid - 1;
+          }
+          val[j] = rd16(cptr[lo] + 2 * (e - cpre[lo]));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (ok[j]) atomicOr(&m[val[j] >> 5], 1u << (val[j] & 31u));
+    }
+    for (int k = 0; k < nc; ++k) {  // bitmap containers: 1024 x u64 LE == 2048 x u32, bit j of word w = doc 32w + j
+      if (ccard[k] <= 4096) continue;
+      const uint8_t* c = cptr[k];
+      for (int w = tid; w < 2048; w += 256) {
+        const uint32_t x = rd32(c + 4 * w);
+        if (x) atomicOr(&m[w], x);
+      }
+    }
+    __syncthreads();
+  }
+}
 
 __global__ void __launch_bounds__(256) pgx_roaring_expand(const RDesc* __restrict__ descs, int npairs, int maxchunks) {
   const int pair = static_cast<int>(blockIdx.x / maxchunks);
@@ -532,55 +632,14 @@ __global__ void __launch_bounds__(256) pgx_roaring_expand(const RDesc* __restric
   if (chunk >= D.nchunks) return;
   __shared__ uint32_t m[2048];
   __shared__ const uint8_t* cptr[kRoarBatch];
-  __shared__ int ccard[kRoarBatch];
-  __shared__ int ncont;
+  __shared__ int ccard[kRoarBatch], cpre[kRoarBatch];
+  __shared__ int ncont, celems;
   const int tid = threadIdx.x;
   for (int i = tid; i < 2048; i += 256) m[i] = 0u;
-  for (int b0 = 0; b0 < D.nb; b0 += kRoarBatch) {
-    if (tid == 0) ncont = 0;
-    __syncthreads();
-    const int b = b0 + tid;
-    if (b < D.nb) {
-      const uint8_t* base = D.inv + D.offs[b];
-      const int n = static_cast<int>(rd32(base + 4));
-      int lo = 0, hi = n - 1, found = -1;
-      while (lo <= hi) {
-        const int mid = (lo + hi) >> 1;
-        const int k = static_cast<int>(rd16(base + 8 + 4 * mid));
-        if (k == chunk) { found = mid; break; }
-        if (k < chunk) lo = mid + 1; else hi = mid - 1;
-      }
-      if (found >= 0) {
-        const int card = static_cast<int>(rd16(base + 8 + 4 * found + 2)) + 1;
-        const uint32_t off = rd32(base + 8 + 4 * n + 4 * found);
-        const int slot = atomicAdd(&ncont, 1);
-        cptr[slot] = base + off;
-        ccard[slot] = card;
-      }
-    }
-    __syncthreads();
-    const int nc = ncont;
-    for (int k = 0; k < nc; ++k) {
-      const uint8_t* c = cptr[k];
-      const int card = ccard[k];
-      if (card > 4096) {  // bitmap container: 1024 x u64 little-endian == 2048 x u32, bit j of word w = doc 32w + j
-        for (int w = tid; w < 2048; w += 256) {
-          const uint32_t x = rd32(c + 4 * w);
-          if (x) atomicOr(&m[w], x);
-        }
-      } else {            // array container: sorted u16 low bits
-        for (int i = tid; i < card; i += 256) {
-          const uint32_t v = rd16(c + 2 * i);
-          atomicOr(&m[v >> 5], 1u << (v & 31u));
-        }
-      }
-    }
-    __syncthreads();
-  }
+  roar_or_chunk(D, chunk, m, cptr, ccard, cpre, &ncont, &celems);
   uint32_t* out = D.mask + static_cast<size_t>(chunk) * 2048;
   for (int i = tid; i < 2048; i += 256) out[i] = m[i];
 }
-
 
 // ---------------------------------------------------------------------------------------------
 // High-cardinality group-by (LONG_MAP semantics, DefaultGroupKeyGenerator.java:239-246 / :429-441): the reference
@@ -589,8 +648,6 @@ __global__ void __launch_bounds__(256) pgx_roaring_expand(const RDesc* __restric
 // passes split the records into 64 x 128 partitions by hash bits, and one workgroup per partition aggregates it in an
 // LDS hash table, then appends its groups to compact output arrays.
 // ---------------------------------------------------------------------------------------------
-#define PGX_GLOBAL __attribute__((address_space(1)))
-
 __device__ __forceinline__ uint64_t part_mix(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
   return x;

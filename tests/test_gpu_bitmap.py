@@ -47,6 +47,11 @@ QUERIES = [
     "SELECT COUNT(*), SUM(m) FROM t WHERE x <> 0 AND y <> 5 AND g = 3",
     "SELECT SUM(m), COUNT(*) FROM t WHERE (x IN (1, 2) OR y = 9) AND x <> 2 GROUP BY g",
     "SELECT SUM(m) FROM t WHERE y = 123456 GROUP BY g",
+    # all-bitmap filters: one combined doc mask per segment (pgx_roaring_program), incl. empty and flipped leaves
+    "SELECT COUNT(*), SUM(m) FROM t WHERE x = 1 OR y IN (3, 4, 5)",
+    "SELECT COUNT(*), SUM(m) FROM t WHERE (y = 123456 OR x = 2) AND x <> 7",
+    "SELECT COUNT(*), MIN(m), MAX(m) FROM t WHERE (x IN (0, 4) OR y IN (10, 20, 30)) AND y NOT IN (20, 21) AND g <> 5",
+    "SELECT SUM(m), COUNT(*) FROM t WHERE (x = 3 OR g IN (1, 2)) AND (y <> 8 OR x = 0) GROUP BY g",
 ]
 
 
@@ -74,3 +79,24 @@ def test_bitmap_leaves_match_oracle_and_scan(ctx, segs, text):
     else:
         H.assert_values_equal(blk.get_aggregation_result(), o["results"], fns)
         assert blk.get_aggregation_result() == blk_scan.get_aggregation_result()
+
+
+@pytest.mark.parametrize("text", QUERIES[5:])
+def test_mixed_bitmap_and_scan_segments_in_one_query(ctx, segs, text):
+    """One launch over an inverted segment (combined bitmap program or per-leaf masks) and a scan-only segment: the
+    combine over both equals the oracle's combine of the two identical segments."""
+    from pinot_amd import engine as E
+    inv, scan, oseg = segs
+    q = pql.compile(text)
+    pm = E.InstancePlanMakerImplV2(ctx)
+    blk = pm.make_inter_segment_plan([inv, scan, inv], q).execute()
+    o = H.oracle_answer([oseg, oseg, oseg], q, literal=True)
+    fns = [a["fn"] for a in q["aggregations"]]
+    if q.get("group_by"):
+        m = blk.get_aggregation_group_by_result()
+        m = m.as_map() if m is not None else {}
+        assert set(m) == set(o["map"])
+        for k, v in o["map"].items():
+            H.assert_values_equal(m[k], v, fns)
+    else:
+        H.assert_values_equal(blk.get_aggregation_result(), o["results"], fns)
