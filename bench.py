@@ -40,8 +40,14 @@ def dist_setup(args):
     if world > 1:
         import torch
         import torch.distributed as dist
+        backend = os.environ.get("PGX_DIST_BACKEND", "nccl")  # "gloo": rehearse N ranks on fewer GPUs (box has 1)
+        if backend != "nccl":
+            local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -135,9 +141,8 @@ def main():
     if req.get("group_by") and world > 1:
         slots = C.c_int64()
         N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
-        dense = slots.value <= (1 << 22)  # dense key space: RCCL all-reduce of the tables
-        if not dense:
-            raise SystemExit("sparse group-by across GPUs (hash-partitioned exchange) is not implemented; run N=1")
+        dense = slots.value <= (1 << 22)  # dense key space: RCCL all-reduce of the tables; else the
+        # sparse groups are gathered to rank 0 by key value, merged and trimmed there (multigpu.merge_group_partials)
     if dense:
         nplanes = 1 + len(req["aggregations"])
         for p in range(nplanes):
@@ -175,9 +180,16 @@ def main():
             return out
         opts = N.ExecOpts(0, None, 0, 0)
         N.check(L.pgx_execute(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
-        if req.get("group_by"):  # the server's combine output: trimToSize, kept groups read back (a-19)
+        if req.get("group_by") and world > 1:  # sparse keys: host merge of every rank's groups, then trimToSize
+            fns = [a["fn"] for a in req["aggregations"]]
+            parts = multigpu.gather_group_partials(*E.group_partials(q, r, segs))
+            if rank == 0:
+                cols, vals, cnts = multigpu.merge_group_partials(fns, parts)
+                kept = multigpu.trim_to_size(fns, vals, cnts, req["group_by"].get("top_n", 10))
+                merged[0] = E.render_group_maps(q, segs, cols, vals, cnts, kept)
+        elif req.get("group_by"):  # the server's combine output: trimToSize, kept groups read back (a-19)
             E.trim_and_gather(q, r)
-        if world > 1:  # aggregation-only: combine the scalar partials across GPUs
+        if world > 1 and not req.get("group_by"):  # aggregation-only: combine the scalar partials across GPUs
             vals = []
             for i in range(len(req["aggregations"])):
                 v, c = C.c_double(), C.c_int64()
@@ -257,7 +269,11 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline and wl.name == "c2":
         cpu = cpu_baseline_c2(wl, min(rows, 32_000_000), 8, 8)
-    if merged[0] is not None:
+    if merged[0] is not None and req.get("group_by"):
+        top = merged[0][0]
+        best = sorted(top.items(), key=lambda kv: kv[1], reverse=q.fns[0] != "min")[:3]
+        summary = {"local": summary, "merged_over_gpus": {"top3_" + q.fns[0]: best}}
+    elif merged[0] is not None:
         summary = {"local": summary, "merged_over_gpus": merged[0]}
     line = {
         "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,

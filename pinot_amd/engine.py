@@ -565,6 +565,66 @@ def trimmed_maps(q: _Query, r, segments: Sequence[IndexSegment]) -> List[Dict[st
     return maps
 
 
+def _column_values(segments: Sequence[IndexSegment], col: str, si: np.ndarray, di: np.ndarray) -> np.ndarray:
+    """Values of (segment index, dictId) pairs of one group column, vectorised per distinct segment dictionary."""
+    infos = [seg.column(col) for seg in segments]
+    strings = infos[0].meta.data_type == "STRING"
+    out = np.empty(len(si), dtype=object if strings else np.float64 if infos[0].meta.data_type in ("FLOAT", "DOUBLE")
+                   else np.int64)
+    for s in np.unique(si):
+        m = si == s
+        vals = infos[int(s)].values
+        out[m] = (np.asarray(vals, dtype=object) if strings else np.asarray(vals))[di[m]]
+    return out.astype(str) if strings else out
+
+
+def group_partials(q: _Query, r, segments: Sequence[IndexSegment]):
+    """Every group of a group-by result as (key_cols: one array of group-column VALUES per column, vals float64
+    [nf, n], cnts int64 [nf, n]): the per-GPU partial of the cross-GPU sparse merge (multigpu.merge_group_partials)."""
+    L = N.lib()
+    ng = C.c_int64()
+    N.check(L.pgx_result_num_groups(r, C.byref(ng)))
+    n = ng.value
+    cols = []
+    for g, col in enumerate(q.group_cols):
+        si = np.zeros(max(n, 1), dtype=np.int32)
+        di = np.zeros(max(n, 1), dtype=np.int32)
+        N.check(L.pgx_result_group_keys(r, g, si.ctypes.data, di.ctypes.data))
+        cols.append(_column_values(segments, col, si[:n], di[:n]))
+    nf = len(q.fns)
+    vals = np.zeros((nf, max(n, 1)))
+    cnts = np.zeros((nf, max(n, 1)), dtype=np.int64)
+    for i in range(nf):
+        N.check(L.pgx_result_group_values(r, i, vals[i].ctypes.data, cnts[i].ctypes.data))
+    return cols, vals[:, :n], cnts[:, :n]
+
+
+def render_group_maps(q: _Query, segments: Sequence[IndexSegment], key_cols, vals, cnts, kept) -> List[Dict[str, object]]:
+    """Merged (and trimmed: `kept` = group indices per function) groups as the reference's trimmed combine output:
+    one {string key: value} map per function, keys rendered like Dictionary.getStringValue (values joined by tab)."""
+    infos = [segments[0].column(col) for col in q.group_cols]
+
+    def render(info, v):
+        dt = info.meta.data_type
+        if dt == "STRING":
+            return str(v)
+        if dt in ("INT", "LONG"):
+            return str(int(v))
+        if dt == "FLOAT":
+            return _java_double_str(float(np.float32(v)))
+        return _java_double_str(float(v))
+
+    maps = []
+    for i, fn in enumerate(q.fns):
+        m = {}
+        for j in kept[i]:
+            key = "\t".join(render(info, c[j]) for info, c in zip(infos, key_cols))
+            m[key] = int(cnts[i, j]) if fn == "count" else (
+                (float(vals[i, j]), int(cnts[i, j])) if fn == "avg" else float(vals[i, j]))
+        maps.append(m)
+    return maps
+
+
 # ------------------------------------------------------------------------------------------------
 # Operators / plan nodes / plan maker
 # ------------------------------------------------------------------------------------------------

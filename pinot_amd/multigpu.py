@@ -7,11 +7,15 @@ operator/MCombineGroupByOperator.java:139-233) for partials that live on differe
   * aggregation-only: COUNT/SUM/AVG add, MIN/MAX take min/max (query/aggregation/function/*.combineTwoValues);
   * dense group-by: every rank holds the same dense table layout (pgx_query_dense_slots / pgx_query_dense_plane_op:
     plane 0 = int64 doc count, then one plane per function: 0 int64 add, 1 double add, 2 ordered-u64 min,
-    3 ordered-u64 max) -> one all-reduce per plane kind, min/max on sign-flipped ordered encodings.
+    3 ordered-u64 max) -> one all-reduce per plane kind, min/max on sign-flipped ordered encodings;
+  * sparse group-by (key spaces too wide for a dense table): groups gathered to rank 0 by key value and merged there
+    (gather_group_partials / merge_group_partials / trim_to_size).
 """
 from __future__ import annotations
 
 from typing import List, Sequence, Tuple
+
+import numpy as np
 
 PLANE_ADD_I64, PLANE_ADD_F64, PLANE_MIN_ORD, PLANE_MAX_ORD = range(4)
 SIGN64 = -(1 << 63)
@@ -76,4 +80,83 @@ def merge_aggregation(fns: Sequence[str], values: Sequence[Tuple[float, int]], d
             dist.all_reduce(m, op=op)
             for i, v in zip(idx, m.tolist()):
                 out[i] = (v, counts[i])
+    return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Sparse (high-cardinality) group-by partials across GPUs ("hipMemcpy to host with a host hash-merge"):
+# every rank compacts its groups to (key values per group column, one (value, count) pair per function), rank 0 gathers
+# them, merges equal keys with the combine semantics of query/aggregation/function/*.combineTwoValues
+# (CountAggregationFunction.java:79-87 long add, SumAggregationFunction.java:168-176 double add, Min/Max extremes,
+# AvgAggregationFunction.java:116-125 pair add) and applies AggregationGroupByOperatorService.trimToSize
+# (query/aggregation/groupby/AggregationGroupByOperatorService.java:59-77,284-361) to the merged groups.
+# Keys are the group columns' VALUES, not dictIds: the segments of different GPUs have their own dictionaries, and the
+# reference's combine is keyed by the value string (MCombineGroupByOperator.java:139-233).
+# ------------------------------------------------------------------------------------------------
+def gather_group_partials(key_cols, vals, cnts, root: int = 0):
+    """Gather every rank's partial (key_cols: list of 1-D arrays, vals: float64 [nf, n], cnts: int64 [nf, n]) to
+    `root`.  Returns the list of per-rank partials on the root, None elsewhere."""
+    import torch.distributed as dist
+    mine = ([np.ascontiguousarray(k) for k in key_cols], np.ascontiguousarray(vals), np.ascontiguousarray(cnts))
+    world = dist.get_world_size()
+    out = [None] * world if dist.get_rank() == root else None
+    dist.gather_object(mine, out, dst=root)
+    return out
+
+
+def merge_group_partials(fns: Sequence[str], parts):
+    """Merge partials with equal keys (sort-based: lexsort over the key columns, then reduceat per function).  Returns
+    (key_cols, vals, cnts) with one row per distinct key, keys in ascending order."""
+    parts = [p for p in parts if p is not None and len(p[0]) and len(p[0][0])]
+    nf = len(fns)
+    if not parts:
+        return [], np.zeros((nf, 0)), np.zeros((nf, 0), dtype=np.int64)
+    ncols = len(parts[0][0])
+    cols = [np.concatenate([p[0][c] for p in parts]) for c in range(ncols)]
+    vals = np.concatenate([p[1] for p in parts], axis=1)
+    cnts = np.concatenate([p[2] for p in parts], axis=1)
+    order = np.lexsort(tuple(reversed(cols)))  # lexsort: the LAST key is primary
+    cols = [c[order] for c in cols]
+    vals, cnts = vals[:, order], cnts[:, order]
+    n = len(order)
+    change = np.zeros(n, dtype=bool)
+    change[0] = True
+    for c in cols:
+        change[1:] |= c[1:] != c[:-1]
+    starts = np.flatnonzero(change)
+    out_v = np.empty((nf, len(starts)))
+    out_c = np.add.reduceat(cnts, starts, axis=1)
+    for i, f in enumerate(fns):
+        if f == "min":
+            out_v[i] = np.minimum.reduceat(vals[i], starts)
+        elif f == "max":
+            out_v[i] = np.maximum.reduceat(vals[i], starts)
+        else:  # count (value unused), sum, avg: add
+            out_v[i] = np.add.reduceat(vals[i], starts)
+    return [c[starts] for c in cols], out_v, out_c
+
+
+def trim_to_size(fns: Sequence[str], vals, cnts, top_n: int) -> List[np.ndarray]:
+    """AggregationGroupByOperatorService.trimToSize over merged groups: above 20 x max(topN, 1000) groups keep, per
+    function, the 5 x max(topN, 1000) best (MIN ascending, others descending, AVG by sum / count); otherwise every
+    group.  Ties at the threshold are arbitrary, as in the reference's MinMaxPriorityQueue.  Returns the kept group
+    indices per function."""
+    n = vals.shape[1]
+    min_trim = max(top_n, 1000)
+    threshold, size = min_trim * 20, min_trim * 5
+    out = []
+    for i, f in enumerate(fns):
+        if n <= threshold:
+            out.append(np.arange(n))
+            continue
+        if f == "count":
+            score = cnts[i].astype(np.float64)
+        elif f == "avg":
+            c = cnts[i].astype(np.float64)
+            score = np.divide(vals[i], c, out=np.zeros(n), where=c != 0)
+        else:
+            score = vals[i]
+        if f != "min":
+            score = -score
+        out.append(np.argpartition(score, size - 1)[:size])
     return out

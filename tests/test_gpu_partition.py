@@ -204,3 +204,40 @@ def test_combine_trim_on_device(ctx, flags):
         for k, v in m.items():
             e = exp[k]
             assert (v == (float(e[1]), e[0])) if fn == "avg" else (v == e[col]), (fn, k, v, e)
+
+
+def test_group_partials_split_then_merged_equal_one_launch(ctx):
+    """The cross-GPU sparse merge (multigpu.merge_group_partials over engine.group_partials): segments split over two
+    'ranks' with different dictionaries, each rank's groups read back by VALUE, merged on the host, equal the groups
+    of one launch over all segments."""
+    from pinot_amd import engine as E
+    from pinot_amd import multigpu as MG
+    from pinot_amd import native as N
+    rng = np.random.default_rng(8)
+    mdom = np.sort(rng.choice(np.arange(-10 ** 6, 10 ** 6), size=300, replace=False)).astype(np.int32)
+    gsegs = []
+    for i in range(3):
+        n = 30000 + 5003 * i
+        raw = {"k": (rng.integers(0, 2500 + 400 * i, size=n) * 3).astype(np.int32),
+               "x": np.array(["w%d" % v for v in rng.integers(0, 1500 + 90 * i, size=n)]),
+               "m": mdom[rng.integers(0, len(mdom), size=n)]}
+        s, _ = H.build_pair("gp%d" % i, raw)
+        gsegs.append(E.IndexSegment(ctx, s))
+    q = pql.compile(AGGS + " GROUP BY x, k")
+    fns = [a["fn"] for a in q["aggregations"]]
+    whole = _map(_execute(ctx, gsegs, q, 0))
+    parts = []
+    for part in (gsegs[:2], gsegs[2:]):
+        qq = E._Query(ctx, q)
+        r = qq.execute(part)
+        try:
+            parts.append(E.group_partials(qq, r, part))
+        finally:
+            N.lib().pgx_result_release(r)
+    cols, vals, cnts = MG.merge_group_partials(fns, parts)
+    everything = [np.arange(vals.shape[1])] * len(fns)
+    maps = E.render_group_maps(E._Query(ctx, q), gsegs, cols, vals, cnts, everything)
+    merged = {k: [maps[i][k] for i in range(len(fns))] for k in maps[0]}
+    assert set(merged) == set(whole) and len(whole) > 20000
+    for k, v in whole.items():
+        H.assert_values_equal(merged[k], v, fns)

@@ -116,3 +116,106 @@ def test_two_rank_merge_matches_single_process():
         assert agg[0] == (float(len(iv)), len(iv))
         assert agg[1][0] == float(iv.sum()) and agg[2][0] == float(iv.min()) and agg[3][0] == float(iv.max())
         assert agg[4] == (float(iv.sum()), len(iv))
+
+
+# ------------------------------------------------------------------------------------------------
+# Sparse group-by across ranks (multigpu.gather_group_partials / merge_group_partials / trim_to_size): every rank
+# combines its segments with the oracle, hands its groups over as value-keyed arrays, rank 0 merges and trims; the
+# result must equal the oracle's combine (MCombineGroupByOperator + trimToSize) over ALL segments.
+# ------------------------------------------------------------------------------------------------
+SP_NSEG, SP_ROWS = 4, 12000
+SP_QUERY = "SELECT SUM(m), MIN(m), MAX(m), COUNT(*), AVG(m) FROM t GROUP BY g1, g2 TOP 10"
+
+
+def _sparse_segments():
+    from oracle import pinot_oracle as O
+    segs = []
+    for s in range(SP_NSEG):
+        rng = np.random.default_rng(100 + s)
+        # per-segment value domains differ (different dictionaries on different ranks); ~40k distinct keys overall
+        raw = {"g1": rng.integers(0, 200, SP_ROWS).astype(np.int32) * 7 + s,
+               "g2": rng.integers(-100, 100, SP_ROWS).astype(np.int32),
+               "m": rng.integers(0, 1 << 20, SP_ROWS).astype(np.int32)}
+        segs.append(O.OSegment.from_raw(raw))
+    return segs
+
+
+def _partial_arrays(merged, fns):
+    keys = list(merged)
+    cols = [np.array([int(k.split("\t")[c]) for k in keys], dtype=np.int64) for c in range(2)]
+    vals = np.zeros((len(fns), len(keys)))
+    cnts = np.zeros((len(fns), len(keys)), dtype=np.int64)
+    for j, k in enumerate(keys):
+        for i, f in enumerate(fns):
+            v = merged[k][i]
+            if f == "count":
+                cnts[i, j] = v
+            elif f == "avg":
+                vals[i, j], cnts[i, j] = v[0], v[1]
+            else:
+                vals[i, j] = v
+    return cols, vals, cnts
+
+
+def _sparse_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oracle import pinot_oracle as O
+    from pinot_amd import pql
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        req = pql.compile(SP_QUERY)
+        fns = [a["fn"] for a in req["aggregations"]]
+        segs = _sparse_segments()
+        mine = multigpu.shard(SP_NSEG, world, rank, "strong")
+        local = O.combine_group_by([O.run_group_by(segs[s], req) for s in mine], req)["merged"]
+        parts = multigpu.gather_group_partials(*_partial_arrays(local, fns))
+        out = None
+        if rank == 0:
+            cols, vals, cnts = multigpu.merge_group_partials(fns, parts)
+            kept = multigpu.trim_to_size(fns, vals, cnts, req["group_by"].get("top_n", 10))
+            out = (cols, vals, cnts, kept)
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sparse_group_merge_and_trim_match_oracle_combine():
+    import torch.multiprocessing as mp
+    from oracle import pinot_oracle as O
+    from pinot_amd import pql
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sparse_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    cols, vals, cnts, kept = res[0]
+    req = pql.compile(SP_QUERY)
+    fns = [a["fn"] for a in req["aggregations"]]
+    exp = O.combine_group_by([O.run_group_by(s, req) for s in _sparse_segments()], req)
+    keys = ["%d\t%d" % (a, b) for a, b in zip(cols[0], cols[1])]
+    assert len(keys) == len(exp["merged"]) > 20000  # the trim engages
+    assert set(keys) == set(exp["merged"])
+    for j, k in enumerate(keys):
+        e = exp["merged"][k]
+        for i, f in enumerate(fns):
+            if f == "count":
+                assert cnts[i, j] == e[i]
+            elif f == "avg":
+                assert cnts[i, j] == e[i][1] and abs(vals[i, j] - e[i][0]) <= 1e-9 * abs(e[i][0])
+            elif f == "sum":
+                assert abs(vals[i, j] - e[i]) <= 1e-9 * abs(e[i])
+            else:
+                assert vals[i, j] == e[i]  # MIN / MAX bit-exact
+    for i, f in enumerate(fns):  # trimmed: same size and the same multiset of kept values (ties are arbitrary)
+        got = sorted(float(cnts[i, j]) if f == "count" else
+                     (vals[i, j] / cnts[i, j] if f == "avg" else vals[i, j]) for j in kept[i])
+        want = sorted(float(v) if f == "count" else (v[0] / v[1] if f == "avg" else v)
+                      for v in exp["trimmed"][i].values())
+        assert len(got) == len(want) == exp["trim_size"]
+        np.testing.assert_allclose(got, want, rtol=1e-9)
