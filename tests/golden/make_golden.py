@@ -203,7 +203,10 @@ EXPECTED = {
     },
     "broker_reduce": {
         "source": "pinot-core/src/test/java/com/linkedin/pinot/query/executor/BrokerReduceServiceTest.java",
-        "servers_2": {"count": 800004}, "servers_10": {"count": 4000020},
+        "lines": "163,287,397-413",
+        "servers_2": {"count_star": 800004, "avg_met": 100000.0},
+        "servers_10": {"count_star": 4000020, "sum_met": 400002000000.0, "max_met": 200000.0, "min_met": 0.0,
+                       "avg_met": 100000.0},
     },
 }
 
