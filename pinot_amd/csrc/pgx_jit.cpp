@@ -175,11 +175,13 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("const int nd = S->num_docs;");
   e.ln("const long long tile0 = S->tile_begin;");
   e.ln("const PGX_G int* __restrict__ tl = (const PGX_G int*)S->tiles;  // tile skipping (star-tree ranges)");
-  // stage this segment's value images into LDS
+  // stage this segment's value images into LDS (emitted after the first tile's loads are in flight, below): four
+  // 16-byte loads per thread are issued before their LDS stores, so a 128 KiB image costs two load latencies, not eight
   bool has_img = false;
   for (int c = 0; c < ncols; ++c) has_img |= s.cols[c].img != IMG_NONE;
   (void)any_img;
-  if (has_img) {
+  auto emit_images = [&]() {
+    if (!has_img) return;
     e.ln("__syncthreads();");
     for (int c = 0; c < ncols; ++c) {
       if (s.cols[c].img == IMG_NONE) continue;
@@ -188,12 +190,18 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("const PGX_G pgx_u32x4* __restrict__ src = (const PGX_G pgx_u32x4*)S->img[", c, "];");
       e.ln("pgx_u32x4* dst = (pgx_u32x4*)(lds + ", img_off[c] / 4, ");");
       e.ln("const int nq = (S->img_words[", c, "] + 3) >> 2;");
-      e.ln("for (int i = tid; i < nq; i += PT) dst[i] = src[i];");
+      e.ln("for (int i0 = 0; i0 < nq; i0 += 4 * PT) {");
+      e.ln("  pgx_u32x4 x[4];");
+      e.ln("  #pragma unroll");
+      e.ln("  for (int k = 0; k < 4; ++k) if (i0 + k * PT + tid < nq) x[k] = src[i0 + k * PT + tid];");
+      e.ln("  #pragma unroll");
+      e.ln("  for (int k = 0; k < 4; ++k) if (i0 + k * PT + tid < nq) dst[i0 + k * PT + tid] = x[k];");
+      e.ln("}");
       e.ind--;
       e.ln("}");
     }
     e.ln("__syncthreads();");
-  }
+  };
   // per-segment pointers and leaf parameters
   for (int c = 0; c < ncols; ++c)
     if (s.cols[c].decode) e.ln("const u32* __restrict__ f", c, " = S->fwd[", c, "];");
@@ -297,6 +305,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   for (int l = 0; l < nleaves; ++l)
     if (is_docmask(s.leaf_mode[l])) e.ln("u32 nq", l, "[", U, "];");
   emit_loads("t", "n");
+  emit_images();
   e.ln("for (long long tt = t; tt < t2; ++tt) {");
   e.ind = 3;
   for (int c = 0; c < ncols; ++c) {
