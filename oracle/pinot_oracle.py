@@ -895,7 +895,9 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
     holders = []
     for a in q["aggregations"]:
         fn = a["fn"]
-        holders.append([0.0, 0] if fn == "avg" else FN_DEFAULT[fn])
+        holders.append([0.0, 0] if fn == "avg" else set() if fn == "distinctcount" else
+                       [math.inf, -math.inf] if fn == "minmaxrange" else [] if fn.startswith("percentile") else
+                       FN_DEFAULT[fn])
     for blk in _blocks(docs, MAX_DOC_PER_CALL):
         for k, a in enumerate(q["aggregations"]):
             fn = a["fn"]
@@ -918,12 +920,25 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
             elif fn == "avg":  # AvgAggregationFunction.aggregate:47-65
                 s = float(np.cumsum(v)[-1]) if len(v) else 0.0
                 holders[k] = [holders[k][0] + s, holders[k][1] + len(blk)]
+            elif fn == "distinctcount":  # DistinctCountAggregationFunction.aggregate: IntOpenHashSet of (int) value
+                holders[k].update(java_int_cast(x) for x in v.tolist())
+            elif fn == "minmaxrange":  # MinMaxRangeAggregationFunction.aggregate: block min / max into the pair
+                if len(v):
+                    holders[k] = [min(holders[k][0], float(v.min())), max(holders[k][1], float(v.max()))]
+            elif fn.startswith("percentile"):  # PercentileAggregationFunction.aggregate: DoubleArrayList of values
+                holders[k].extend(v.tolist())
     results = []
     for k, a in enumerate(q["aggregations"]):
         if a["fn"] == "count":
             results.append(int(holders[k]))  # MutableLongValue((long) double)
         elif a["fn"] == "avg":
             results.append((float(holders[k][0]), int(holders[k][1])))
+        elif a["fn"] == "distinctcount":
+            results.append(set(holders[k]))
+        elif a["fn"] == "minmaxrange":
+            results.append((float(holders[k][0]), float(holders[k][1])))
+        elif a["fn"].startswith("percentile"):
+            results.append(sorted(holders[k]))
         else:
             results.append(float(holders[k]))
     n_proj = len(_projection_columns(q))
@@ -1028,7 +1043,36 @@ def combine_two(fn: str, a, b):
         return a if a > b else b
     if fn == "avg":
         return (a[0] + b[0], a[1] + b[1])
+    if fn == "distinctcount":  # DistinctCountAggregationFunction.combineTwoValues: set union
+        return set(a) | set(b)
+    if fn == "minmaxrange":  # MinMaxRangeAggregationFunction.combineTwoValues
+        return (min(a[0], b[0]), max(a[1], b[1]))
+    if fn.startswith("percentile"):  # PercentileAggregationFunction.combineTwoValues: list concatenation
+        return sorted(list(a) + list(b))
     raise ValueError(fn)
+
+
+def java_int_cast(x: float) -> int:
+    """Java (int) of a double: truncation toward zero, saturating at the int range, NaN -> 0 (JLS 5.1.3)."""
+    if x != x:
+        return 0
+    if x >= 2147483647.0:
+        return 2147483647
+    if x <= -2147483648.0:
+        return -2147483648
+    return int(x)
+
+
+def reduce_extended(fn: str, v) -> float:
+    """Final value of the extended functions (query/aggregation/function/DistinctCountAggregationFunction.java:136-145,
+    MinMaxRangeAggregationFunction.java:129-146, quantile/PercentileUtil.java:40-52: sorted list, element
+    (int)(size * p / 100))."""
+    if fn == "distinctcount":
+        return len(v)
+    if fn == "minmaxrange":
+        return v[1] - v[0] if v[0] != math.inf and v[1] != -math.inf else -1.0  # DEFAULT_MIN_MAX_RANGE_VALUE
+    p = int(fn[len("percentile"):])
+    return float(sorted(v)[int(len(v) * (p / 100.0))])
 
 
 def combine_aggregation(parts: List[dict], q: dict) -> dict:

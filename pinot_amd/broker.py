@@ -24,12 +24,21 @@ from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
 from . import engine as E
+from . import extended as X
+from .pql import EXT_FUNCTIONS
+
+
+_NAMES = {"distinctcount": "distinctCount", "minmaxrange": "minMaxRange"}
 
 
 def function_name(agg: dict) -> str:
-    """AggregationFunction.getFunctionName: count_star, sum_<col>, min_<col>, max_<col>, avg_<col>
-    (query/aggregation/function/CountAggregationFunction.java:118-120, SumAggregationFunction.java:207-209, ...)."""
-    return "count_star" if agg["fn"] == "count" else "%s_%s" % (agg["fn"], agg["column"])
+    """AggregationFunction.getFunctionName: count_star, sum_<col>, min_<col>, max_<col>, avg_<col>, distinctCount_<col>,
+    minMaxRange_<col>, percentileNN_<col> (query/aggregation/function/CountAggregationFunction.java:118-120,
+    SumAggregationFunction.java:207-209, DistinctCountAggregationFunction.java:165, MinMaxRangeAggregationFunction
+    .java:170, quantile/PercentileAggregationFunction.java:171)."""
+    if agg["fn"] == "count":
+        return "count_star"
+    return "%s_%s" % (_NAMES.get(agg["fn"], agg["fn"]), agg["column"])
 
 
 def java_format_5f(x: float) -> str:
@@ -53,6 +62,8 @@ def _combine_two(fn: str, a, b):
         return b
     if b is None:
         return a
+    if fn in EXT_FUNCTIONS:
+        return X.combine_two(fn, a, b)
     if fn == "count":
         return int(a) + int(b)
     if fn == "sum":
@@ -67,6 +78,13 @@ def _combine_two(fn: str, a, b):
 def _reduce(fn: str, values: Sequence):
     """AggregationFunction.reduce: count -> long sum; sum -> double sum; min / max over the default +/-inf; avg -> sum /
     count, 0.0 when no docs (AvgAggregationFunction.java:128-143)."""
+    if fn in EXT_FUNCTIONS:  # combine the intermediates, then the function's final value
+        acc = None
+        for v in values:
+            acc = v if acc is None else X.combine_two(fn, acc, v)
+        if acc is None:
+            return 0 if fn == "distinctcount" else (-1.0 if fn == "minmaxrange" else 0.0)
+        return X.reduce_value(fn, acc)
     if fn == "count":
         return sum(int(v) for v in values)
     if fn == "sum":
@@ -94,7 +112,8 @@ def _reduce(fn: str, values: Sequence):
 
 
 def _format(fn: str, v) -> str:
-    return str(int(v)) if fn == "count" else java_format_5f(float(v))
+    """Long / Integer (count, distinctcount) -> toString; doubles -> %1.5f (BrokerReduceService.formatValue)."""
+    return str(int(v)) if fn in ("count", "distinctcount") else java_format_5f(float(v))
 
 
 @dataclass

@@ -649,6 +649,12 @@ class _GpuOperator:
     def next_block(self):
         if self._done:
             return None
+        from . import extended
+        if extended.has_extended(self.request):  # decomposed into GPU sub-queries on the host (extended.py)
+            blk = extended.run(self.ctx, self.request, self.segments)
+            self._stats = blk.stats
+            self._done = True
+            return blk
         q = _Query(self.ctx, self.request)
         r = q.execute(self.segments)
         try:

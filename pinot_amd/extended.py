@@ -1,0 +1,147 @@
+"""DISTINCTCOUNT, MINMAXRANGE and PERCENTILE{50,90,95,99} for aggregation-only requests,
+decomposed on the host into GPU sub-queries the fused scan kernels already run:
+
+* MINMAXRANGE(c) -> MIN(c) and MAX(c) in the base query; intermediate (min, max)
+  (core/operator/aggregation/function/MinMaxRangeAggregationFunction.java aggregate: a Pair of block extremes);
+* DISTINCTCOUNT(c) -> ``GROUP BY c`` with COUNT(*) under the same filter; intermediate the set of (int) values
+  (DistinctCountAggregationFunction.java aggregate: IntOpenHashSet.add((int) value));
+* PERCENTILEnn(c) -> the same ``GROUP BY c`` histogram; intermediate the (value, count) pairs in value order, i.e. the
+  reference's DoubleArrayList of every selected value (PercentileAggregationFunction.java aggregate) held as a multiset.
+
+One histogram sub-query serves every DISTINCTCOUNT / PERCENTILE over the same column.  Statistics are the base query's,
+with numEntriesScannedPostFilter counted over the ORIGINAL projection columns (AggregationOperator.java:93-98).
+Group-by requests with these functions are not decomposed: ``PgxError(UNSUPPORTED)`` lets the caller fall back.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Sequence
+
+import numpy as np
+
+from . import engine as E
+from . import native as N
+from .pql import EXT_FUNCTIONS
+
+
+def has_extended(request: dict) -> bool:
+    return any(a["fn"] in EXT_FUNCTIONS for a in request["aggregations"])
+
+
+def java_int_cast(x) -> int:
+    """Java (int) of a double: truncation toward zero, saturating at the int range, NaN -> 0 (JLS 5.1.3)."""
+    x = float(x)
+    if x != x:
+        return 0
+    if x >= 2147483647.0:
+        return 2147483647
+    if x <= -2147483648.0:
+        return -2147483648
+    return int(x)
+
+
+def percentile_of_histogram(fn: str, hist: Sequence) -> float:
+    """quantile/PercentileUtil.getValueOnQuantile over the multiset: element (int)(size * p / 100) of the sorted
+    values (query/aggregation/function/quantile/PercentileUtil.java:40-52)."""
+    p = int(fn[len("percentile"):])
+    total = sum(int(c) for _, c in hist)
+    idx = int(total * (p / 100.0))
+    if idx >= total:
+        raise IndexError("percentile of an empty value list")
+    for v, c in hist:
+        if idx < c:
+            return float(v)
+        idx -= int(c)
+    raise AssertionError("unreachable")
+
+
+def merge_histograms(a: Sequence, b: Sequence) -> List:
+    d: Dict[float, int] = {}
+    for v, c in list(a) + list(b):
+        d[v] = d.get(v, 0) + int(c)
+    return sorted(d.items())
+
+
+def _projection_count(request: dict) -> int:
+    cols = []
+    for a in request["aggregations"]:
+        if a["fn"] != "count" and a["column"] not in cols:
+            cols.append(a["column"])
+    return len(cols)
+
+
+def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment]) -> E.IntermediateResultsBlock:
+    if request.get("group_by"):
+        raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "distinctcount / minmaxrange / percentile in a group-by request")
+    aggs = request["aggregations"]
+    base = [{"fn": "count", "column": "*"}]
+    slot = []  # per original aggregation: index (or (min, max) indices) into the base results
+    for a in aggs:
+        fn = a["fn"]
+        if fn == "minmaxrange":
+            base += [{"fn": "min", "column": a["column"]}, {"fn": "max", "column": a["column"]}]
+            slot.append((len(base) - 2, len(base) - 1))
+        elif fn in ("distinctcount",) or fn.startswith("percentile"):
+            slot.append(None)
+        else:
+            base.append(dict(a))
+            slot.append(len(base) - 1)
+    bq = E._Query(ctx, {"aggregations": base, "group_by": None, "filter": request.get("filter")})
+    r = bq.execute(segments)
+    try:
+        bblk = E.decode_result(bq, r, segments)
+    finally:
+        N.lib().pgx_result_release(r)
+        bq.close()
+    hists = {}
+    for a in aggs:
+        c = a["column"]
+        if (a["fn"] == "distinctcount" or a["fn"].startswith("percentile")) and c not in hists:
+            if segments and segments[0].column(c).meta.data_type == "STRING":
+                raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a STRING column" % a["fn"])
+            hq = E._Query(ctx, {"aggregations": [{"fn": "count", "column": "*"}],
+                                "group_by": {"columns": [c], "top_n": 10}, "filter": request.get("filter")})
+            r = hq.execute(segments)
+            try:
+                cols, _, cnts = E.group_partials(hq, r, segments)
+            finally:
+                N.lib().pgx_result_release(r)
+                hq.close()
+            order = np.argsort(cols[0], kind="stable")
+            hists[c] = [(float(cols[0][i]), int(cnts[0][i])) for i in order]
+    base_res = bblk.get_aggregation_result()
+    out = []
+    for a, s in zip(aggs, slot):
+        fn = a["fn"]
+        if fn == "minmaxrange":
+            out.append((float(base_res[s[0]]), float(base_res[s[1]])))
+        elif fn == "distinctcount":
+            out.append({java_int_cast(v) for v, _ in hists[a["column"]]})
+        elif fn.startswith("percentile"):
+            out.append(list(hists[a["column"]]))
+        else:
+            out.append(base_res[s])
+    st = bblk.stats
+    docs = st.num_docs_scanned
+    stats = E.ExecutionStatistics(docs, st.num_entries_scanned_in_filter, docs * _projection_count(request),
+                                  st.num_total_raw_docs)
+    return E.IntermediateResultsBlock(aggregation_result=out, stats=stats)
+
+
+def reduce_value(fn: str, v):
+    """Final value of an extended function's (combined) intermediate (DistinctCountAggregationFunction.java:136-145,
+    MinMaxRangeAggregationFunction.java:129-146 with DEFAULT_MIN_MAX_RANGE_VALUE = -1, PercentileUtil)."""
+    if fn == "distinctcount":
+        return len(v)
+    if fn == "minmaxrange":
+        return v[1] - v[0] if v[0] != math.inf and v[1] != -math.inf else -1.0
+    return percentile_of_histogram(fn, v)
+
+
+def combine_two(fn: str, a, b):
+    """combineTwoValues: set union, pair extremes, list concatenation (histogram merge)."""
+    if fn == "distinctcount":
+        return set(a) | set(b)
+    if fn == "minmaxrange":
+        return (min(a[0], b[0]), max(a[1], b[1]))
+    return merge_histograms(a, b)

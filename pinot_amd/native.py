@@ -7,6 +7,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PGX_LIB", os.path.join(_HERE, "libpgx.so"))
 
 
+PGX_ERR_UNSUPPORTED = 2  # pgx.h pgx_status: the caller falls back to the Java operators
+
+
 class PgxError(RuntimeError):
     def __init__(self, status, msg):
         super().__init__("pgx error %d: %s" % (status, msg))

@@ -22,6 +22,8 @@ _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(
                     r"(?P<op><=|>=|<>|!=|=|<|>|\(|\)|,|\*)|(?P<id>[A-Za-z_][A-Za-z0-9_.$]*))")
 
 AGG_FUNCTIONS = ("count", "sum", "min", "max", "avg")
+# distinctcount / minmaxrange / percentileNN (AggregationFunctionFactory.java:84-107): aggregation-only requests
+EXT_FUNCTIONS = ("distinctcount", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
 
 
 class PqlError(ValueError):
@@ -136,7 +138,7 @@ def compile(pql: str) -> dict:  # noqa: A001 - mirrors Pql2Compiler.compileToBro
     aggs = []
     while True:
         fn = p.take("id").lower()
-        if fn not in AGG_FUNCTIONS:
+        if fn not in AGG_FUNCTIONS and fn not in EXT_FUNCTIONS:
             raise PqlError("unsupported aggregation function " + fn)
         p.take("op", "(")
         k, v = p.peek()

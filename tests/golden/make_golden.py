@@ -203,10 +203,10 @@ EXPECTED = {
     },
     "broker_reduce": {
         "source": "pinot-core/src/test/java/com/linkedin/pinot/query/executor/BrokerReduceServiceTest.java",
-        "lines": "163,287,397-413",
-        "servers_2": {"count_star": 800004, "avg_met": 100000.0},
+        "lines": "163,287,321,356,397-421",
+        "servers_2": {"count_star": 800004, "avg_met": 100000.0, "distinctCount_dim0": 10, "distinctCount_dim1": 100},
         "servers_10": {"count_star": 4000020, "sum_met": 400002000000.0, "max_met": 200000.0, "min_met": 0.0,
-                       "avg_met": 100000.0},
+                       "avg_met": 100000.0, "distinctCount_dim0": 10, "distinctCount_dim1": 100},
     },
 }
 

@@ -12,7 +12,9 @@ from pinot_amd import broker as B
 from pinot_amd import pql
 from tests import helpers as H
 
-MULTI = "SELECT COUNT(*), SUM(met), MAX(met), MIN(met), AVG(met) FROM midas"
+MULTI = ("SELECT COUNT(*), SUM(met), MAX(met), MIN(met), AVG(met), DISTINCTCOUNT(dim0), DISTINCTCOUNT(dim1) "
+         "FROM midas")
+BASIC = "SELECT COUNT(*), SUM(met), MAX(met), MIN(met), AVG(met) FROM midas"
 GROUPED = "SELECT SUM(met), COUNT(*), MIN(met), AVG(met) FROM midas GROUP BY dim0 TOP 4"
 
 
@@ -21,7 +23,13 @@ def _oracle_response(q, osegs):
     if q.get("group_by"):
         return B.InstanceResponse(group_by=[{k: v[i] for k, v in a["map"].items()} for i in range(len(q["aggregations"]))],
                                   stats=a["stats"])
-    return B.InstanceResponse(aggregation=list(a["results"]), stats=a["stats"])
+    res = []
+    for agg, v in zip(q["aggregations"], a["results"]):
+        if agg["fn"].startswith("percentile"):  # the oracle's DoubleArrayList -> the (value, count) multiset
+            vals, cnts = np.unique(np.asarray(v, dtype=np.float64), return_counts=True)
+            v = [(float(x), int(c)) for x, c in zip(vals, cnts)]
+        res.append(v)
+    return B.InstanceResponse(aggregation=res, stats=a["stats"])
 
 
 @pytest.fixture(scope="module")
@@ -67,7 +75,7 @@ def test_group_by_reduce_top_n_and_rendering(osegs):
 
 
 def test_exception_responses_and_stats():
-    q = pql.compile(MULTI)
+    q = pql.compile(BASIC)
     ok = B.InstanceResponse(aggregation=[3, 6.0, 3.0, 1.0, (6.0, 3)], stats=[3, 1, 12, 10])
     bad = B.InstanceResponse(exceptions={B.QUERY_EXECUTION_ERROR_CODE: "segment failed"})
     resp = B.BrokerReduceService().reduce_on_data_table(q, {"s1": ok, "s2": bad, "s3": None})

@@ -1,0 +1,77 @@
+"""GPU parity of DISTINCTCOUNT / MINMAXRANGE / PERCENTILEnn (pinot_amd/extended.py): aggregation-only
+requests decomposed into GPU sub-queries (MIN/MAX in the base query, a GROUP BY <column> histogram) against the CPU
+oracle's literal restatement of the reference functions (IntOpenHashSet of (int) values, Pair of extremes,
+DoubleArrayList + PercentileUtil), over several segments with different dictionaries."""
+import numpy as np
+import pytest
+
+from oracle import pinot_oracle as O
+from pinot_amd import pql
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def env():
+    from pinot_amd import engine as E
+    ctx = E.Context(0)
+    rng = np.random.default_rng(17)
+    gsegs, osegs = [], []
+    for i in range(3):
+        n = 40000 + 9000 * i
+        raw = {"d": rng.integers(0, 50 + 10 * i, n).astype(np.int32),
+               "v": rng.integers(-(1 << 20), 1 << 20, n).astype(np.int32) // (i + 1),
+               "w": (rng.integers(0, 3000, n) * 0.37 - 300.0).astype(np.float32),
+               "m": rng.integers(0, 5000, n).astype(np.int32)}
+        s, o = H.build_pair("ext%d" % i, raw, types={"w": "FLOAT"})
+        gsegs.append(E.IndexSegment(ctx, s))
+        osegs.append(o)
+    yield ctx, gsegs, osegs
+    ctx.close()
+
+
+QUERIES = [
+    "SELECT DISTINCTCOUNT(d), MINMAXRANGE(v), PERCENTILE50(v), PERCENTILE90(m), COUNT(*) FROM t",
+    "SELECT SUM(m), DISTINCTCOUNT(w), PERCENTILE95(w), PERCENTILE99(w), MINMAXRANGE(w) FROM t WHERE d < 20",
+    "SELECT MINMAXRANGE(m), DISTINCTCOUNT(v), AVG(m), PERCENTILE50(d) FROM t WHERE v > 1000 AND m IN (1, 2, 3, 4000)",
+    "SELECT COUNT(*), MINMAXRANGE(m), DISTINCTCOUNT(d) FROM t WHERE d = 123456",
+]
+
+
+@pytest.mark.parametrize("text", QUERIES)
+def test_extended_functions_match_oracle(env, text):
+    from pinot_amd import engine as E
+    from pinot_amd import extended as X
+    ctx, gsegs, osegs = env
+    q = pql.compile(text)
+    blk = E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute()
+    got = blk.get_aggregation_result()
+    parts = [O.run_aggregation(s, q, literal_filter=False) for s in osegs]
+    exp = O.combine_aggregation(parts, q)
+    fns = [a["fn"] for a in q["aggregations"]]
+    for fn, g, e in zip(fns, got, exp["results"]):
+        if fn == "distinctcount":
+            assert g == e
+        elif fn == "minmaxrange":
+            assert tuple(g) == tuple(e)
+            assert X.reduce_value(fn, g) == O.reduce_extended(fn, e)
+        elif fn.startswith("percentile"):
+            vals, cnts = np.unique(np.asarray(e, dtype=np.float64), return_counts=True)
+            assert g == [(float(x), int(c)) for x, c in zip(vals, cnts)]
+            if e:
+                assert X.reduce_value(fn, g) == O.reduce_extended(fn, e)
+        else:
+            H.assert_values_equal([g], [e], [fn])
+    st = blk.stats.as_list()
+    assert st[0] == exp["stats"][0] and st[2] == exp["stats"][2] and st[3] == exp["stats"][3]
+
+
+def test_extended_function_in_group_by_is_unsupported(env):
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    ctx, gsegs, _ = env
+    q = pql.compile("SELECT DISTINCTCOUNT(v) FROM t GROUP BY d")
+    with pytest.raises(N.PgxError) as ei:
+        E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute()
+    assert ei.value.status == N.PGX_ERR_UNSUPPORTED
