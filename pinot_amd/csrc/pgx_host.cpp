@@ -886,6 +886,7 @@ struct ExecPlan {
   size_t star_tile_cap = 0;                       // arena int32 slots reserved for them
   uint64_t mask_words = 0;
   const RDesc* rdesc_dev = nullptr;
+  bool roar_early = false;  // the expansion was launched by upload_plan (before the query kernels are planned)
   int roar_maxchunks = 0;
   uint32_t* masks_dev = nullptr;
   int n_proj = 0;
@@ -1086,6 +1087,12 @@ void plan_star_segment(const pgx_query& q, const pgx_segment& seg, const KSeg& S
   if (terms > 1) { sp.op.push_back(OP_OR); sp.arg.push_back(terms); }
 }
 
+// PGX_HOST_PROFILE=1: sub-phase marks of the planner (appended to the running pgx_execute's profile line).
+thread_local std::function<void(const char*)> g_prof_mark;
+void prof_mark(const char* what) {
+  if (g_prof_mark) g_prof_mark(what);
+}
+
 void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                 uint32_t xflags, ExecPlan& P) {
   if (n < 1) fail(PGX_ERR_INVALID_ARG, "no segments");
@@ -1258,6 +1265,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     K.prog_arg[i] = parg[i];
   }
 
+  prof_mark("p.head");
   // per-segment descriptors: planned in chunks of segments (in parallel for long segment lists); each chunk keeps its
   // blob words, pointer fixups and bitmap items with chunk-local offsets, concatenated in segment order afterwards.
   P.ksegs.assign(n, KSeg{});
@@ -1382,6 +1390,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     P.ksegs[s].tile_begin = tiles;
     tiles += P.ksegs[s].num_tiles;
   }
+  prof_mark("p.chunks");
   for (ChunkOut& o : chunks) {
     const size_t base = P.blob32.size();
     const uint64_t mbase = P.mask_words;
@@ -1401,6 +1410,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     P.total_raw += o.total_raw;
     P.host_entries += o.host_entries;
   }
+  prof_mark("p.merge");
   // star-tree segments (query kernels only: the per-segment program needs the generated kernels)
   P.star.assign(n, ExecPlan::StarPlan{});
   if (P.use_docmask && !P.use_part && int(q.leaf_col.size()) + 8 <= PGX_J_MAX_LEAVES) {
@@ -1453,7 +1463,6 @@ struct ExecBuffers {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 
 void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
-  (void)st;
   const size_t n = P.ksegs.size();
   B.off_ksegs = align_up(P.blob32.size() * 4, 256);
   B.off_jsegs = align_up(B.off_ksegs + n * sizeof(KSeg), 256);
@@ -1496,6 +1505,13 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
       rd[i].nchunks = it.nchunks;
     }
     P.rdesc_dev = reinterpret_cast<const RDesc*>(B.dev() + B.off_rdesc);
+    // Expand the bitmaps now: send the blob (roaring offsets) and the descriptors ahead of the rest of the arena and
+    // launch, so the expansion runs on the GPU while the host plans the query kernels (plan_jit).
+    hip_check(hipMemcpyAsync(B.arena.p, B.host.p, P.blob32.size() * 4, hipMemcpyHostToDevice, st), "blob H2D");
+    hip_check(hipMemcpyAsync(B.dev() + B.off_rdesc, B.host.bytes() + B.off_rdesc, P.roar.size() * sizeof(RDesc),
+                             hipMemcpyHostToDevice, st), "bitmap descriptors H2D");
+    hip_check(pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
+    P.roar_early = true;
   }
 }
 
@@ -1595,6 +1611,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     }
     it->second.push_back(s);
   }
+  prof_mark("j.sig");
   const int cus = ctx->num_cus;
   size_t jidx = 0;  // next free JSeg slot of the arena
   size_t star_tile_off = 0;
@@ -1771,8 +1788,9 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
 
 void launch_scan(ExecPlan& P, hipStream_t st) {
   if (!P.jit.empty()) {
-    if (P.rdesc_dev)
+    if (P.rdesc_dev && !P.roar_early)
       hip_check(pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
+    P.roar_early = false;  // relaunches (hash-table retries, timed iterations) expand again
     for (auto& G : P.jit) {
       if (!G.fn) continue;
       G.args.agg_out = P.kq.agg_out;
@@ -2246,6 +2264,8 @@ struct HostProf {
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                const pgx_exec_opts* opts, pgx_result* R) {
   HostProf hp;
+  if (hp.on) g_prof_mark = [&hp](const char* w) { hp.mark(w); };
+  struct Unmark { ~Unmark() { g_prof_mark = nullptr; } } unmark;
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
   const uint32_t xflags = opts ? opts->flags : 0;
   ExecPlan P;
@@ -2768,6 +2788,7 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     ExecBuffers B;
     upload_plan(ctx, P, B, st);
     plan_jit(ctx, *q, segs, n, P, B);
+    P.roar_early = false;  // every timed iteration includes the bitmap expansion
     PartBuffers PB;
     if (P.use_part && !run_partitioned(ctx, P, B, PB, st)) {  // untimed: settles the partition sizes
       P.use_part = false;
