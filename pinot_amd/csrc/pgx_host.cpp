@@ -52,7 +52,8 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
                                                 uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream);
-extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, int kind, void* state,
+extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
+                                      void* states,
                                       int64_t* idx, uint64_t* keys, int64_t cap, int grid, hipStream_t stream);
 extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
                                               const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
@@ -663,6 +664,7 @@ struct pgx_result {
     std::vector<std::vector<int32_t>> rep_seg, rep_id;  // [col][global id]
     std::vector<int> agg_kind;
     std::vector<std::vector<int64_t>> trims;  // per function: the device-selected trim, best first
+    int64_t trim_size = 0;                    // the size those selections were made for
     ~Lazy() {
       okey.reset();
       oplane.reset();
@@ -2169,40 +2171,52 @@ void pgx_result::materialize() {
 }
 
 // Combine trim of a device-resident result (pgx_trim.hip): indices of the `size` best groups for function fn, best
-// first (ties in index order).  Computed once per function and kept with the result.
+// first (ties in index order).  The first call selects for EVERY function of the result in one set of launches (one
+// range pass, <= 8 histogram passes, one select, all functions side by side) and keeps the selections.
 const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
   Lazy& L = *lazy;
-  if (L.trims.size() < L.agg_kind.size()) L.trims.resize(L.agg_kind.size());
-  std::vector<int64_t>& out = L.trims[fn];
-  if (!out.empty()) return out;
+  const int nf = int(L.agg_kind.size());
+  if (int(L.trims.size()) < nf) L.trims.resize(nf);
+  if (!L.trims[fn].empty() && L.trim_size == size) return L.trims[fn];
   hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
   hipStream_t st = L.ctx->stream;
-  const int k = L.agg_kind[fn];
-  const int kind = k == A_COUNT ? 0 : k == A_SUM ? 1 : k == A_MIN ? 2 : k == A_MAX ? 3 : 4;
+  std::vector<int> kinds(nf);
+  for (int f = 0; f < nf; ++f) {
+    const int k = L.agg_kind[f];
+    kinds[f] = k == A_COUNT ? 0 : k == A_SUM ? 1 : k == A_MIN ? 2 : k == A_MAX ? 3 : 4;
+  }
   const size_t sb = pgx_trim_state_bytes();
-  std::vector<uint8_t> init(sb, 0);
+  std::vector<uint8_t> init(sb * nf, 0);
   const int64_t want = size;
-  const int32_t shift = 56;
-  std::memcpy(init.data() + 16, &want, 8);  // TrimState.k
-  std::memcpy(init.data() + 24, &shift, 4); // TrimState.shift
-  DevBuf state(L.ctx, sb), idx(L.ctx, size_t(size) * 8), keys(L.ctx, size_t(size) * 8);
-  hip_check(hipMemcpyAsync(state.p, init.data(), sb, hipMemcpyHostToDevice, st), "trim state H2D");
+  const uint64_t kmin0 = ~0ull;
+  for (int f = 0; f < nf; ++f) {
+    std::memcpy(init.data() + f * sb + 16, &want, 8);   // TrimState.k
+    std::memcpy(init.data() + f * sb + 48, &kmin0, 8);  // TrimState.kmin
+  }
+  DevBuf state(L.ctx, sb * nf), idx(L.ctx, size_t(size) * 8 * nf), keys(L.ctx, size_t(size) * 8 * nf);
+  hip_check(hipMemcpyAsync(state.p, init.data(), init.size(), hipMemcpyHostToDevice, st), "trim state H2D");
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((num_groups + 255) / 256, int64_t(L.ctx->num_cus) * 8)));
-  hip_check(pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kind, state.p, idx.as<int64_t>(),
-                            keys.as<uint64_t>(), size, grid, st),
+  hip_check(pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kinds.data(), nf, state.p,
+                            idx.as<int64_t>(), keys.as<uint64_t>(), size, grid, st),
             "trim launch");
-  std::vector<int64_t> ix(size);
-  std::vector<uint64_t> ky(size);
-  hip_check(hipMemcpyAsync(ix.data(), idx.p, size_t(size) * 8, hipMemcpyDeviceToHost, st), "trim D2H");
-  hip_check(hipMemcpyAsync(ky.data(), keys.p, size_t(size) * 8, hipMemcpyDeviceToHost, st), "trim D2H");
+  std::vector<int64_t> ix(size_t(size) * nf);
+  std::vector<uint64_t> ky(size_t(size) * nf);
+  hip_check(hipMemcpyAsync(ix.data(), idx.p, ix.size() * 8, hipMemcpyDeviceToHost, st), "trim D2H");
+  hip_check(hipMemcpyAsync(ky.data(), keys.p, ky.size() * 8, hipMemcpyDeviceToHost, st), "trim D2H");
   hip_check(hipStreamSynchronize(st), "sync");
-  std::vector<int64_t> order(size);
-  std::iota(order.begin(), order.end(), 0);
-  std::sort(order.begin(), order.end(),
-            [&](int64_t a, int64_t b) { return ky[a] != ky[b] ? ky[a] > ky[b] : ix[a] < ix[b]; });
-  out.resize(size);
-  for (int64_t i = 0; i < size; ++i) out[i] = ix[order[i]];
-  return out;
+  L.trim_size = size;
+  for (int f = 0; f < nf; ++f) {
+    const int64_t* fi = ix.data() + size_t(f) * size;
+    const uint64_t* fk = ky.data() + size_t(f) * size;
+    std::vector<int64_t> order(size);
+    std::iota(order.begin(), order.end(), 0);
+    std::sort(order.begin(), order.end(),
+              [&](int64_t a, int64_t b) { return fk[a] != fk[b] ? fk[a] > fk[b] : fi[a] < fi[b]; });
+    std::vector<int64_t>& out = L.trims[f];
+    out.resize(size);
+    for (int64_t i = 0; i < size; ++i) out[i] = fi[order[i]];
+  }
+  return L.trims[fn];
 }
 
 namespace {

@@ -19,16 +19,24 @@ namespace pgx {
 // 2 ordered min, 3 ordered max.
 enum TrimKind : int { TK_COUNT = 0, TK_SUM = 1, TK_MIN = 2, TK_MAX = 3, TK_AVG = 4 };
 
-// Layout shared with pgx_host.cpp (device_trim writes prefix / mask / k / shift before the launch).
+// Layout shared with pgx_host.cpp (device_trims writes k, kmin = ~0 and zeros before the launch).  One state per
+// function: every kernel below takes an array of states and the function slot is blockIdx.y.
 struct TrimState {
   unsigned long long prefix;   // selected high bits of the threshold key          (offset 0)
   unsigned long long mask;     // which bits of prefix are fixed                   (8)
   long long k;                 // groups still to take among those matching prefix (16)
   int shift;                   // bit position of the digit of the next pass       (24)
-  int pad;
+  int done;                    // threshold complete (no more histogram passes)   (28)
   unsigned long long n_sel;    // compaction cursors                               (32)
   unsigned long long n_tie;    //                                                  (40)
-  unsigned int hist[256];      //                                                  (48)
+  unsigned long long kmin;     // key range of the groups                          (48)
+  unsigned long long kmax;     //                                                  (56)
+  unsigned int hist[256];      //                                                  (64)
+};
+
+constexpr int kTrimMaxFns = 8;
+struct TrimKinds {             // function slot -> trim key kind
+  int kind[kTrimMaxFns];
 };
 
 // Larger key = better group.
@@ -51,10 +59,67 @@ __device__ __forceinline__ uint64_t trim_key(const PGX_GLOBAL uint64_t* pl, int6
   }
 }
 
+// Key range per function: the digits above the highest bit in which the smallest and largest keys differ are the
+// same for every group, so the radix passes start below them (C3's sums span ~27 bits: 4 passes instead of 8).
+__global__ void __launch_bounds__(256) pgx_trim_range(const uint64_t* __restrict__ oplane, int64_t ocap, int64_t n,
+                                                      const TrimKinds K, TrimState* __restrict__ sts) {
+  __shared__ unsigned long long wmin[4], wmax[4];
+  TrimState* st = sts + blockIdx.y;
+  const int kind = K.kind[blockIdx.y];
+  const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)oplane;
+  unsigned long long lo = ~0ull, hi = 0ull;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * 256) {
+    const uint64_t key = trim_key(pl, ocap, i, kind);
+    lo = key < lo ? key : lo;
+    hi = key > hi ? key : hi;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const unsigned long long a = __shfl_xor(lo, d, 64), b = __shfl_xor(hi, d, 64);
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    wmin[threadIdx.x >> 6] = lo;
+    wmax[threadIdx.x >> 6] = hi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) {
+      lo = wmin[w] < lo ? wmin[w] : lo;
+      hi = wmax[w] > hi ? wmax[w] : hi;
+    }
+    atomicMin(&st->kmin, lo);
+    atomicMax(&st->kmax, hi);
+  }
+}
+
+// One lane per function: fix the bits above the highest differing bit, first digit just below them.
+__global__ void pgx_trim_begin(TrimState* __restrict__ sts) {
+  if (threadIdx.x != 0) return;
+  TrimState* st = sts + blockIdx.x;
+  const unsigned long long x = st->kmin ^ st->kmax;
+  if (st->kmin > st->kmax || x == 0ull) {  // no groups, or every key equal: all ties at kmin
+    st->prefix = st->kmin;
+    st->mask = ~0ull;
+    st->done = 1;
+    return;
+  }
+  const int hb = 64 - __clzll(static_cast<long long>(x));  // bits [0, hb) vary
+  st->mask = hb == 64 ? 0ull : ~((1ull << hb) - 1ull);
+  st->prefix = st->kmin & st->mask;
+  st->shift = hb > 8 ? hb - 8 : 0;
+  st->done = 0;
+}
+
 __global__ void __launch_bounds__(256) pgx_trim_hist(const uint64_t* __restrict__ oplane, int64_t ocap, int64_t n,
-                                                     int kind, TrimState* __restrict__ st) {
+                                                     const TrimKinds K, TrimState* __restrict__ sts) {
+  TrimState* st = sts + blockIdx.y;
+  if (st->done) return;
   __shared__ unsigned int lh[256];
   const int tid = threadIdx.x;
+  const int kind = K.kind[blockIdx.y];
   lh[tid] = 0u;
   __syncthreads();
   const unsigned long long prefix = st->prefix, mask = st->mask;
@@ -68,10 +133,13 @@ __global__ void __launch_bounds__(256) pgx_trim_hist(const uint64_t* __restrict_
   if (lh[tid]) atomicAdd(&st->hist[tid], lh[tid]);
 }
 
-// One lane: fix the next digit of the threshold from the histogram (the largest digit d whose bins >= d hold at
-// least k groups), then clear the histogram for the next pass.
-__global__ void pgx_trim_step(TrimState* __restrict__ st) {
+// One lane per function: fix the next digit of the threshold from the histogram (the largest digit d whose bins >= d
+// hold at least k groups), then clear the histogram for the next pass.  Digits may overlap bits fixed before (the
+// last one ends at bit 0): those bits are equal in every key matching the prefix, so OR-ing them in changes nothing.
+__global__ void pgx_trim_step(TrimState* __restrict__ sts) {
   if (threadIdx.x != 0) return;
+  TrimState* st = sts + blockIdx.x;
+  if (st->done) return;
   long long above = 0;
   int d = 255;
   for (; d > 0; --d) {
@@ -82,23 +150,49 @@ __global__ void pgx_trim_step(TrimState* __restrict__ st) {
   st->prefix |= static_cast<unsigned long long>(d) << st->shift;
   st->mask |= 255ull << st->shift;
   st->k -= above;
-  st->shift -= 8;
+  if (st->shift == 0) st->done = 1;
+  else st->shift = st->shift > 8 ? st->shift - 8 : 0;
   for (int b = 0; b < 256; ++b) st->hist[b] = 0u;
 }
 
+// Function slot y writes its selection to idx / keys + y * cap.  Cursor reservations are wave-aggregated (one atomic
+// per wave and kind): at a MIN threshold tens of thousands of groups can tie, and per-lane atomics on one address
+// serialise.
 __global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restrict__ oplane, int64_t ocap, int64_t n,
-                                                       int kind, TrimState* __restrict__ st, int64_t* __restrict__ idx,
-                                                       uint64_t* __restrict__ keys, int64_t cap) {
+                                                       const TrimKinds K, TrimState* __restrict__ sts,
+                                                       int64_t* __restrict__ idx, uint64_t* __restrict__ keys,
+                                                       int64_t cap) {
+  TrimState* st = sts + blockIdx.y;
+  const int kind = K.kind[blockIdx.y];
+  idx += static_cast<int64_t>(blockIdx.y) * cap;
+  keys += static_cast<int64_t>(blockIdx.y) * cap;
   const unsigned long long thr = st->prefix;
   const long long ties = st->k;
   const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)oplane;
-  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
-       i += static_cast<int64_t>(gridDim.x) * 256) {
-    const uint64_t key = trim_key(pl, ocap, i, kind);
-    bool take = key > thr;
-    if (!take && key == thr) take = static_cast<long long>(atomicAdd(&st->n_tie, 1ull)) < ties;
+  const int lane = threadIdx.x & 63;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  for (int64_t b = static_cast<int64_t>(blockIdx.x) * 256 + (threadIdx.x & ~63); b < n; b += stride) {
+    const int64_t i = b + lane;
+    const bool valid = i < n;
+    const uint64_t key = valid ? trim_key(pl, ocap, i, kind) : 0ull;
+    const bool eq = valid && key == thr;
+    const unsigned long long em = __ballot(eq);
+    long long tbase = 0;
+    if (em) {
+      if (lane == __ffsll(static_cast<long long>(em)) - 1)
+        tbase = static_cast<long long>(atomicAdd(&st->n_tie, static_cast<unsigned long long>(__popcll(em))));
+      tbase = __shfl(tbase, __ffsll(static_cast<long long>(em)) - 1, 64);
+    }
+    const bool take = (valid && key > thr) || (eq && tbase + __popcll(em & below) < ties);
+    const unsigned long long tm = __ballot(take);
+    if (!tm) continue;
+    unsigned long long sbase = 0;
+    const int leader = __ffsll(static_cast<long long>(tm)) - 1;
+    if (lane == leader) sbase = atomicAdd(&st->n_sel, static_cast<unsigned long long>(__popcll(tm)));
+    sbase = __shfl(sbase, leader, 64);
     if (take) {
-      const unsigned long long p = atomicAdd(&st->n_sel, 1ull);
+      const unsigned long long p = sbase + __popcll(tm & below);
       if (p < static_cast<unsigned long long>(cap)) {
         idx[p] = i;
         keys[p] = key;
@@ -122,17 +216,24 @@ __global__ void __launch_bounds__(256) pgx_group_gather(const uint64_t* __restri
 
 }  // namespace pgx
 
-// Host launchers (pgx_host.cpp).  The state block is prepared by the caller: prefix = mask = 0, k = groups wanted,
-// shift = 56, everything else zero.
-extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, int kind, void* state,
-                                      int64_t* idx, uint64_t* keys, int64_t cap, int grid, hipStream_t stream) {
-  pgx::TrimState* st = static_cast<pgx::TrimState*>(state);
+// Host launchers (pgx_host.cpp).  The nf state blocks are prepared by the caller: k = groups wanted, kmin = ~0,
+// everything else zero.  kinds[f]: TrimKind of function slot f.  At most 8 histogram passes (8-bit digits); passes after
+// a function's threshold is complete return at once.
+extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
+                                      void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
+                                      hipStream_t stream) {
+  if (nf < 1 || nf > pgx::kTrimMaxFns) return hipErrorInvalidValue;
+  pgx::TrimKinds K{};
+  for (int f = 0; f < nf; ++f) K.kind[f] = kinds[f];
+  pgx::TrimState* st = static_cast<pgx::TrimState*>(states);
+  const dim3 g(grid, nf);
+  hipLaunchKernelGGL(pgx::pgx_trim_range, g, dim3(256), 0, stream, oplane, ocap, n, K, st);
+  hipLaunchKernelGGL(pgx::pgx_trim_begin, dim3(nf), dim3(64), 0, stream, st);
   for (int pass = 0; pass < 8; ++pass) {
-    hipLaunchKernelGGL(pgx::pgx_trim_hist, dim3(grid), dim3(256), 0, stream, oplane, ocap, n, kind, st);
-    hipLaunchKernelGGL(pgx::pgx_trim_step, dim3(1), dim3(64), 0, stream, st);
+    hipLaunchKernelGGL(pgx::pgx_trim_hist, g, dim3(256), 0, stream, oplane, ocap, n, K, st);
+    hipLaunchKernelGGL(pgx::pgx_trim_step, dim3(nf), dim3(64), 0, stream, st);
   }
-  hipLaunchKernelGGL(pgx::pgx_trim_select, dim3(grid), dim3(256), 0, stream, oplane, ocap, n, kind, st, idx, keys,
-                     cap);
+  hipLaunchKernelGGL(pgx::pgx_trim_select, g, dim3(256), 0, stream, oplane, ocap, n, K, st, idx, keys, cap);
   return hipGetLastError();
 }
 
