@@ -867,6 +867,7 @@ def filter_mask_vectorized(seg: OSegment, tree: Optional[dict]) -> np.ndarray:
 # a-13..a-17, a-20: aggregation / group-by execution
 # ------------------------------------------------------------------------------------------------
 FN_DEFAULT = {"count": 0.0, "sum": 0.0, "min": math.inf, "max": -math.inf}
+EXT_FUNCTIONS = ("distinctcount", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
 
 
 def _projection_columns(q: dict) -> List[str]:
@@ -1009,6 +1010,21 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
                 np.add.at(acc, gid, v)
                 cnt = np.bincount(gid, minlength=G)
                 vals = [(float(s), int(c)) for s, c in zip(acc, cnt)]
+            elif fn == "distinctcount":  # DistinctCountAggregationFunction.aggregateGroupBySV: a set per group
+                vals = [set() for _ in range(G)]
+                for i, x in zip(gid.tolist(), v.tolist()):
+                    vals[i].add(java_int_cast(x))
+            elif fn == "minmaxrange":  # MinMaxRangeAggregationFunction.aggregateGroupBySV: a (min, max) pair
+                mn = np.full(G, math.inf)
+                mx = np.full(G, -math.inf)
+                np.minimum.at(mn, gid, v)
+                np.maximum.at(mx, gid, v)
+                vals = [(float(a_), float(b_)) for a_, b_ in zip(mn, mx)]
+            elif fn.startswith("percentile"):  # PercentileAggregationFunction.aggregateGroupBySV: a list per group
+                vals = [[] for _ in range(G)]
+                for i, x in zip(gid.tolist(), v.tolist()):
+                    vals[i].append(x)
+                vals = [sorted(x) for x in vals]
         for k, i in uniq.items():
             out[k].append(vals[i])
 
@@ -1107,7 +1123,12 @@ def combine_group_by(parts: List[dict], q: dict) -> dict:
     trimmed = []
     for i, f in enumerate(fns):
         items = [(k, v[i]) for k, v in merged.items()]
-        if len(merged) > threshold:
+        # getMinMaxPriorityQueue returns null for intermediates that are not Comparable (IntOpenHashSet,
+        # MinMaxRangePair): those functions keep every group (AggregationGroupByOperatorService.java:336-349).
+        # PERCENTILE's DoubleArrayList IS Comparable (lexicographic, over values in merge order, which depends on
+        # thread timing): that trim is not reproducible, so every group is kept here too (parity unpinned above the
+        # threshold; tests stay below it).
+        if len(merged) > threshold and f not in EXT_FUNCTIONS:
             keyf = (lambda kv: kv[1][0] / kv[1][1] if kv[1][1] else 0.0) if f == "avg" else (lambda kv: kv[1])
             items.sort(key=keyf, reverse=(f != "min"))
             items = items[:size]

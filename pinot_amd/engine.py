@@ -651,7 +651,9 @@ class _GpuOperator:
             return None
         from . import extended
         if extended.has_extended(self.request):  # decomposed into GPU sub-queries on the host (extended.py)
-            blk = extended.run(self.ctx, self.request, self.segments)
+            blk = extended.run(self.ctx, self.request, self.segments, combine=self.combine)
+            if self.request.get("group_by") and blk.aggregation_group_by_result.num_groups() == 0 and not self.combine:
+                blk.aggregation_group_by_result = None
             self._stats = blk.stats
             self._done = True
             return blk

@@ -10,7 +10,9 @@ decomposed on the host into GPU sub-queries the fused scan kernels already run:
 
 One histogram sub-query serves every DISTINCTCOUNT / PERCENTILE over the same column.  Statistics are the base query's,
 with numEntriesScannedPostFilter counted over the ORIGINAL projection columns (AggregationOperator.java:93-98).
-Group-by requests with these functions are not decomposed: ``PgxError(UNSUPPORTED)`` lets the caller fall back.
+Group-by requests keep their GROUP BY columns in the base query, and the histograms group by those columns plus c
+(``_run_group_by``).  A STRING column under DISTINCTCOUNT / PERCENTILE raises ``PgxError(UNSUPPORTED)`` (the reference
+reads it through getDoubleValue, which STRING dictionaries do not support).
 """
 from __future__ import annotations
 
@@ -67,25 +69,109 @@ def _projection_count(request: dict) -> int:
     for a in request["aggregations"]:
         if a["fn"] != "count" and a["column"] not in cols:
             cols.append(a["column"])
+    for g in (request.get("group_by") or {}).get("columns", []):
+        if g not in cols:
+            cols.append(g)
     return len(cols)
 
 
-def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment]) -> E.IntermediateResultsBlock:
-    if request.get("group_by"):
-        raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "distinctcount / minmaxrange / percentile in a group-by request")
-    aggs = request["aggregations"]
+def _base_request(request: dict):
+    """The base GPU request (COUNT(*), the standard functions, MIN + MAX for each MINMAXRANGE) and, per original
+    function, its base slot: an index, a (min, max) index pair, or None (histogram functions)."""
     base = [{"fn": "count", "column": "*"}]
-    slot = []  # per original aggregation: index (or (min, max) indices) into the base results
-    for a in aggs:
+    slot = []
+    for a in request["aggregations"]:
         fn = a["fn"]
         if fn == "minmaxrange":
             base += [{"fn": "min", "column": a["column"]}, {"fn": "max", "column": a["column"]}]
             slot.append((len(base) - 2, len(base) - 1))
-        elif fn in ("distinctcount",) or fn.startswith("percentile"):
+        elif fn == "distinctcount" or fn.startswith("percentile"):
             slot.append(None)
         else:
             base.append(dict(a))
             slot.append(len(base) - 1)
+    return base, slot
+
+
+def _hist_columns(request: dict, segments) -> List[str]:
+    cols = []
+    for a in request["aggregations"]:
+        if (a["fn"] == "distinctcount" or a["fn"].startswith("percentile")) and a["column"] not in cols:
+            if segments and segments[0].column(a["column"]).meta.data_type == "STRING":
+                raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a STRING column" % a["fn"])
+            cols.append(a["column"])
+    return cols
+
+
+def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock:
+    """Group-by: the base request keeps the GROUP BY columns; each histogram column c runs ``GROUP BY <columns>, c``
+    with COUNT(*), and its groups are folded back per leading key (the group string minus its last field).  The
+    combine trim keeps the base request's trimmed maps for the standard functions; functions whose intermediates the
+    reference cannot order keep every group (AggregationGroupByOperatorService.java:336-349)."""
+    gb = request["group_by"]
+    base, slot = _base_request(request)
+    bq = E._Query(ctx, {"aggregations": base, "group_by": dict(gb), "filter": request.get("filter")})
+    r = bq.execute(segments)
+    try:
+        bblk = E.decode_result(bq, r, segments, trim=combine)
+    finally:
+        N.lib().pgx_result_release(r)
+        bq.close()
+    bmap = bblk.get_aggregation_group_by_result().as_map()
+    hists: Dict[str, Dict[str, List]] = {}
+    for c in _hist_columns(request, segments):
+        hq = E._Query(ctx, {"aggregations": [{"fn": "count", "column": "*"}],
+                            "group_by": {"columns": list(gb["columns"]) + [c], "top_n": gb.get("top_n", 10)},
+                            "filter": request.get("filter")})
+        r = hq.execute(segments)
+        try:
+            hmap = E.decode_result(hq, r, segments).get_aggregation_group_by_result().as_map()
+        finally:
+            N.lib().pgx_result_release(r)
+            hq.close()
+        per: Dict[str, Dict[float, int]] = {}
+        for key, (cnt,) in hmap.items():
+            g, v = key.rsplit("\t", 1)
+            d = per.setdefault(g, {})
+            d[float(v)] = d.get(float(v), 0) + int(cnt)
+        hists[c] = {g: sorted(d.items()) for g, d in per.items()}
+    aggs = request["aggregations"]
+
+    def value(a, s, key, bvals):
+        fn = a["fn"]
+        if fn == "minmaxrange":
+            return (float(bvals[s[0]]), float(bvals[s[1]]))
+        if fn == "distinctcount":
+            return {java_int_cast(v) for v, _ in hists[a["column"]].get(key, [])}
+        if fn.startswith("percentile"):
+            return list(hists[a["column"]].get(key, []))
+        return bvals[s]
+
+    keys = list(bmap)
+    per_group = [[value(a, s, k, bmap[k]) for a, s in zip(aggs, slot)] for k in keys]
+    res = E.AggregationGroupByResult(keys, per_group, [a["fn"] for a in aggs],
+                                     bblk.get_aggregation_group_by_result().storage_mode)
+    st = bblk.stats
+    docs = st.num_docs_scanned
+    blk = E.IntermediateResultsBlock(aggregation_group_by_result=res, stats=E.ExecutionStatistics(
+        docs, st.num_entries_scanned_in_filter, docs * _projection_count(request), st.num_total_raw_docs))
+    if combine:
+        trimmed = []
+        for i, (a, s) in enumerate(zip(aggs, slot)):
+            if a["fn"] in EXT_FUNCTIONS:
+                trimmed.append({k: per_group[j][i] for j, k in enumerate(keys)})
+            else:
+                trimmed.append(dict(bblk.trimmed[s]))
+        blk.trimmed = trimmed
+    return blk
+
+
+def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment],
+        combine: bool = True) -> E.IntermediateResultsBlock:
+    if request.get("group_by"):
+        return _run_group_by(ctx, request, segments, combine)
+    aggs = request["aggregations"]
+    base, slot = _base_request(request)
     bq = E._Query(ctx, {"aggregations": base, "group_by": None, "filter": request.get("filter")})
     r = bq.execute(segments)
     try:
@@ -94,21 +180,17 @@ def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment]) -> E.
         N.lib().pgx_result_release(r)
         bq.close()
     hists = {}
-    for a in aggs:
-        c = a["column"]
-        if (a["fn"] == "distinctcount" or a["fn"].startswith("percentile")) and c not in hists:
-            if segments and segments[0].column(c).meta.data_type == "STRING":
-                raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a STRING column" % a["fn"])
-            hq = E._Query(ctx, {"aggregations": [{"fn": "count", "column": "*"}],
-                                "group_by": {"columns": [c], "top_n": 10}, "filter": request.get("filter")})
-            r = hq.execute(segments)
-            try:
-                cols, _, cnts = E.group_partials(hq, r, segments)
-            finally:
-                N.lib().pgx_result_release(r)
-                hq.close()
-            order = np.argsort(cols[0], kind="stable")
-            hists[c] = [(float(cols[0][i]), int(cnts[0][i])) for i in order]
+    for c in _hist_columns(request, segments):
+        hq = E._Query(ctx, {"aggregations": [{"fn": "count", "column": "*"}],
+                            "group_by": {"columns": [c], "top_n": 10}, "filter": request.get("filter")})
+        r = hq.execute(segments)
+        try:
+            cols, _, cnts = E.group_partials(hq, r, segments)
+        finally:
+            N.lib().pgx_result_release(r)
+            hq.close()
+        order = np.argsort(cols[0], kind="stable")
+        hists[c] = [(float(cols[0][i]), int(cnts[0][i])) for i in order]
     base_res = bblk.get_aggregation_result()
     out = []
     for a, s in zip(aggs, slot):

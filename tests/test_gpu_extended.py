@@ -67,11 +67,47 @@ def test_extended_functions_match_oracle(env, text):
     assert st[0] == exp["stats"][0] and st[2] == exp["stats"][2] and st[3] == exp["stats"][3]
 
 
-def test_extended_function_in_group_by_is_unsupported(env):
+GROUPED = [
+    "SELECT DISTINCTCOUNT(v), MINMAXRANGE(m), SUM(m), PERCENTILE50(m), COUNT(*) FROM t GROUP BY d",
+    "SELECT PERCENTILE90(w), DISTINCTCOUNT(w), MAX(v) FROM t WHERE m < 2500 GROUP BY d TOP 5",
+    "SELECT MINMAXRANGE(v), AVG(m), DISTINCTCOUNT(m) FROM t WHERE d IN (1, 2, 3) GROUP BY d, m",
+]
+
+
+@pytest.mark.parametrize("text", GROUPED)
+def test_extended_functions_group_by_match_oracle(env, text):
+    from pinot_amd import engine as E
+    ctx, gsegs, osegs = env
+    q = pql.compile(text)
+    blk = E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute()
+    got = blk.get_aggregation_group_by_result().as_map()
+    exp = O.combine_group_by([O.run_group_by(s, q, literal_filter=False) for s in osegs], q)
+    fns = [a["fn"] for a in q["aggregations"]]
+    assert set(got) == set(exp["merged"])
+    for k, e in exp["merged"].items():
+        for fn, g, x in zip(fns, got[k], e):
+            if fn == "distinctcount":
+                assert g == x
+            elif fn == "minmaxrange":
+                assert tuple(g) == tuple(x)
+            elif fn.startswith("percentile"):
+                vals, cnts = np.unique(np.asarray(x, dtype=np.float64), return_counts=True)
+                assert g == [(float(a), int(c)) for a, c in zip(vals, cnts)]
+            else:
+                H.assert_values_equal([g], [x], [fn])
+    for i, fn in enumerate(fns):  # combine output: every group for the extended functions, trimmed maps otherwise
+        assert set(blk.trimmed[i]) == set(exp["trimmed"][i])
+    st = blk.stats.as_list()
+    assert st[0] == exp["stats"][0] and st[2] == exp["stats"][2] and st[3] == exp["stats"][3]
+
+
+def test_extended_over_string_column_is_unsupported(env):
     from pinot_amd import engine as E
     from pinot_amd import native as N
-    ctx, gsegs, _ = env
-    q = pql.compile("SELECT DISTINCTCOUNT(v) FROM t GROUP BY d")
+    ctx, _, _ = env
+    raw = {"s": np.array(["a", "b", "c", "a"]), "m": np.array([1, 2, 3, 4], dtype=np.int32)}
+    seg, _ = H.build_pair("strx", raw)
+    g = E.IndexSegment(ctx, seg)
     with pytest.raises(N.PgxError) as ei:
-        E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute()
+        E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan([g], pql.compile("SELECT DISTINCTCOUNT(s) FROM t")).execute()
     assert ei.value.status == N.PGX_ERR_UNSUPPORTED
