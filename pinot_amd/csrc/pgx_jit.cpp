@@ -620,14 +620,52 @@ std::map<std::pair<int, std::string>, JitEntry> g_jit_cache;
 
 }  // namespace
 
+// Every field of a shape that the generated source depends on, flattened: the per-query lookup key (generating the
+// source text to find a cached kernel cost ~14 us per query).
+std::vector<int64_t> shape_key(const JitShape& s, int device) {
+  std::vector<int64_t> k{device, s.T, s.R, s.group_mode, int64_t(s.dense_slots), s.num_planes, s.keybits, s.emit_col,
+                         int64_t(s.cols.size())};
+  for (const JitCol& c : s.cols)
+    k.insert(k.end(), {c.bits, c.decode, c.img, c.img_sh, c.img_words, c.acc32, c.fp, c.remap});
+  auto add = [&](const auto& v) {
+    k.push_back(-int64_t(v.size()) - 1);
+    for (auto x : v) k.push_back(int64_t(x));
+  };
+  add(s.leaf_col);
+  add(s.leaf_mode);
+  add(s.prog_op);
+  add(s.prog_arg);
+  add(s.agg_kind);
+  add(s.agg_col);
+  add(s.plane_op);
+  add(s.gcol);
+  add(s.gmul);
+  add(s.gshift);
+  return k;
+}
+
+std::map<std::vector<int64_t>, JitEntry> g_jit_shapes;  // shape key -> compiled entry (same entries as g_jit_cache)
+
 void* jit_function(const JitShape& s, int device, int* lds_bytes, std::string* err) {
+  const std::vector<int64_t> skey = shape_key(s, device);
+  {
+    std::lock_guard<std::mutex> g(g_jit_mu);
+    auto it = g_jit_shapes.find(skey);
+    if (it != g_jit_shapes.end()) {
+      if (lds_bytes) *lds_bytes = it->second.lds;
+      return it->second.fn;
+    }
+  }
   int lds = 0;
   const std::string src = jit_source(s, &lds);
   if (lds_bytes) *lds_bytes = lds;
   std::lock_guard<std::mutex> g(g_jit_mu);
   auto key = std::make_pair(device, src);
   auto it = g_jit_cache.find(key);
-  if (it != g_jit_cache.end()) return it->second.fn;
+  if (it != g_jit_cache.end()) {
+    g_jit_shapes.emplace(skey, it->second);
+    return it->second.fn;
+  }
   if (const char* dump = std::getenv("PGX_JIT_DUMP")) {  // debugging: keep every generated kernel's source
     const std::string path = std::string(dump) + "/pgxq_" + std::to_string(g_jit_cache.size()) + ".hip";
     if (FILE* f = std::fopen(path.c_str(), "w")) {
@@ -664,6 +702,7 @@ void* jit_function(const JitShape& s, int device, int* lds_bytes, std::string* e
     return nullptr;
   }
   g_jit_cache.emplace(key, ent);
+  g_jit_shapes.emplace(skey, ent);
   return ent.fn;
 }
 
