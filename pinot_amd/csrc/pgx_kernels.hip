@@ -695,11 +695,11 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
   const int cn = static_cast<int>(min<int64_t>(kPartChunk, n - c0));
   const int nb = 1 << nbits;
   __shared__ uint64_t stage[kPartChunk];
-  __shared__ uint8_t sbs[kPartChunk];  // bucket of staged (bucket-sorted) record i
-  __shared__ int hist[128], offs[128], fill[128], total;
+  __shared__ int hist[128], offs[128], total;
   __shared__ unsigned long long gpos[128];
   const int tid = threadIdx.x;
-  if (tid < nb) { hist[tid] = 0; fill[tid] = 0; }
+  const uint64_t bmask = static_cast<uint64_t>(nb - 1);
+  if (tid < nb) hist[tid] = 0;
   const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) +
                                    (in_off ? in_off[r] : static_cast<int64_t>(r) * in_cap) + c0;
   uint64_t rec[kPartPer];
@@ -709,11 +709,12 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
     rec[k] = i < cn ? __builtin_nontemporal_load(src + i) : kNoRecord;
   }
   __syncthreads();
-  int bk[kPartPer];
+  // the histogram atomic returns the record's rank within its bucket, so staging needs no second atomic
+  int bk[kPartPer], rk[kPartPer];
 #pragma unroll
   for (int k = 0; k < kPartPer; ++k) {
-    bk[k] = rec[k] == kNoRecord ? -1 : static_cast<int>((part_mix(rec[k] & keymask) >> shift) & static_cast<uint64_t>(nb - 1));
-    if (bk[k] >= 0) atomicAdd(&hist[bk[k]], 1);
+    bk[k] = rec[k] == kNoRecord ? -1 : static_cast<int>((part_mix(rec[k] & keymask) >> shift) & bmask);
+    rk[k] = bk[k] >= 0 ? atomicAdd(&hist[bk[k]], 1) : 0;
   }
   __syncthreads();
   part_scan128(hist, offs, &total, nb, tid);
@@ -726,21 +727,19 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kPartPer; ++k) {
-    if (bk[k] < 0) continue;
-    const int pos = offs[bk[k]] + atomicAdd(&fill[bk[k]], 1);
-    stage[pos] = rec[k];
-    sbs[pos] = static_cast<uint8_t>(bk[k]);
+    if (bk[k] >= 0) stage[offs[bk[k]] + rk[k]] = rec[k];
   }
   __syncthreads();
   // copy out bucket runs: consecutive staged records of one bucket go to consecutive output words
   PGX_GLOBAL uint64_t* dst = (PGX_GLOBAL uint64_t*)(out);
   const int tot = total;
   for (int i = tid; i < tot; i += kPartThreads) {
-    const int b = sbs[i];
+    const uint64_t v = stage[i];
+    const int b = static_cast<int>((part_mix(v & keymask) >> shift) & bmask);  // recomputed: cheaper than an LDS byte array
     const unsigned long long p = gpos[b] + static_cast<unsigned long long>(i - offs[b]);
     // plain (not streaming) stores: a bucket run's first and last lines are completed by other workgroups' runs,
     // which L2 merges before write-back
-    if (p < static_cast<unsigned long long>(cap)) dst[(static_cast<int64_t>(r) * nb + b) * cap + static_cast<int64_t>(p)] = stage[i];
+    if (p < static_cast<unsigned long long>(cap)) dst[(static_cast<int64_t>(r) * nb + b) * cap + static_cast<int64_t>(p)] = v;
   }
 }
 
