@@ -867,7 +867,61 @@ def filter_mask_vectorized(seg: OSegment, tree: Optional[dict]) -> np.ndarray:
 # a-13..a-17, a-20: aggregation / group-by execution
 # ------------------------------------------------------------------------------------------------
 FN_DEFAULT = {"count": 0.0, "sum": 0.0, "min": math.inf, "max": -math.inf}
-EXT_FUNCTIONS = ("distinctcount", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
+EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
+
+
+# DISTINCTCOUNTHLL: stream-lib 2.7.0 HyperLogLog(log2m = HllConstants.DEFAULT_LOG2M = 8) (third-party, not vendored;
+# com.clearspring.analytics:stream, pom.xml:525-527), restated scalar and per offer.
+HLL_LOG2M = 8
+
+
+def _i32(x: int) -> int:
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x & 0x80000000 else x
+
+
+def murmur_hash_long(data: int) -> int:
+    """MurmurHash.hashLong(long) in Java int arithmetic (>>> = logical shift of the 32-bit pattern)."""
+    m, r = 0x5BD1E995, 24
+    h = 0
+    k = _i32(_i32(data) * m)
+    k ^= (k & 0xFFFFFFFF) >> r
+    h ^= _i32(k * m)
+    k = _i32(_i32(data >> 32) * m)
+    k ^= (k & 0xFFFFFFFF) >> r
+    h = _i32(h * m)
+    h ^= _i32(k * m)
+    h ^= (h & 0xFFFFFFFF) >> 13
+    h = _i32(h * m)
+    h ^= (h & 0xFFFFFFFF) >> 15
+    return _i32(h)
+
+
+def hll_offer(regs: List[int], value: int) -> None:
+    """HyperLogLog.offer(Integer) -> offerHashed(MurmurHash.hash(o)): j = x >>> (32 - log2m),
+    r = numberOfLeadingZeros((x << log2m) | (1 << (log2m - 1)) + 1) + 1, RegisterSet.updateIfGreater(j, r)."""
+    x = murmur_hash_long(value) & 0xFFFFFFFF
+    j = x >> (32 - HLL_LOG2M)
+    w = ((x << HLL_LOG2M) & 0xFFFFFFFF) | ((1 << (HLL_LOG2M - 1)) + 1)
+    r = 32 - w.bit_length() + 1
+    if r > regs[j]:
+        regs[j] = r
+
+
+def hll_cardinality(regs: List[int]) -> int:
+    """HyperLogLog.cardinality(): harmonic mean estimate, linear counting at or below 2.5 m, Math.round."""
+    m = 1 << HLL_LOG2M
+    total, zeros = 0.0, 0.0
+    for v in regs:
+        total += 1.0 / (1 << v)
+        if v == 0:
+            zeros += 1.0
+    est = (0.7213 / (1 + 1.079 / m)) * m * m * (1 / total)
+    if est <= 2.5 * m:
+        est = m * math.log(m / zeros) if zeros else math.inf
+    if est == math.inf:
+        return (1 << 63) - 1
+    return int(math.floor(est + 0.5))
 
 
 def _projection_columns(q: dict) -> List[str]:
@@ -897,6 +951,7 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
     for a in q["aggregations"]:
         fn = a["fn"]
         holders.append([0.0, 0] if fn == "avg" else set() if fn == "distinctcount" else
+                       [0] * (1 << HLL_LOG2M) if fn == "distinctcounthll" else
                        [math.inf, -math.inf] if fn == "minmaxrange" else [] if fn.startswith("percentile") else
                        FN_DEFAULT[fn])
     for blk in _blocks(docs, MAX_DOC_PER_CALL):
@@ -923,6 +978,9 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
                 holders[k] = [holders[k][0] + s, holders[k][1] + len(blk)]
             elif fn == "distinctcount":  # DistinctCountAggregationFunction.aggregate: IntOpenHashSet of (int) value
                 holders[k].update(java_int_cast(x) for x in v.tolist())
+            elif fn == "distinctcounthll":  # DistinctCountHLLAggregationFunction.aggregate: hll.offer((int) value)
+                for x in v.tolist():
+                    hll_offer(holders[k], java_int_cast(x))
             elif fn == "minmaxrange":  # MinMaxRangeAggregationFunction.aggregate: block min / max into the pair
                 if len(v):
                     holders[k] = [min(holders[k][0], float(v.min())), max(holders[k][1], float(v.max()))]
@@ -936,6 +994,8 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
             results.append((float(holders[k][0]), int(holders[k][1])))
         elif a["fn"] == "distinctcount":
             results.append(set(holders[k]))
+        elif a["fn"] == "distinctcounthll":
+            results.append(list(holders[k]))
         elif a["fn"] == "minmaxrange":
             results.append((float(holders[k][0]), float(holders[k][1])))
         elif a["fn"].startswith("percentile"):
@@ -1014,6 +1074,10 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
                 vals = [set() for _ in range(G)]
                 for i, x in zip(gid.tolist(), v.tolist()):
                     vals[i].add(java_int_cast(x))
+            elif fn == "distinctcounthll":  # DistinctCountHLLAggregationFunction.aggregateGroupBySV: an HLL per group
+                vals = [[0] * (1 << HLL_LOG2M) for _ in range(G)]
+                for i, x in zip(gid.tolist(), v.tolist()):
+                    hll_offer(vals[i], java_int_cast(x))
             elif fn == "minmaxrange":  # MinMaxRangeAggregationFunction.aggregateGroupBySV: a (min, max) pair
                 mn = np.full(G, math.inf)
                 mx = np.full(G, -math.inf)
@@ -1061,6 +1125,8 @@ def combine_two(fn: str, a, b):
         return (a[0] + b[0], a[1] + b[1])
     if fn == "distinctcount":  # DistinctCountAggregationFunction.combineTwoValues: set union
         return set(a) | set(b)
+    if fn == "distinctcounthll":  # DistinctCountHLLAggregationFunction.combineTwoValues: HyperLogLog.addAll
+        return [max(x, y) for x, y in zip(a, b)]
     if fn == "minmaxrange":  # MinMaxRangeAggregationFunction.combineTwoValues
         return (min(a[0], b[0]), max(a[1], b[1]))
     if fn.startswith("percentile"):  # PercentileAggregationFunction.combineTwoValues: list concatenation
@@ -1085,6 +1151,8 @@ def reduce_extended(fn: str, v) -> float:
     (int)(size * p / 100))."""
     if fn == "distinctcount":
         return len(v)
+    if fn == "distinctcounthll":  # DistinctCountHLLAggregationFunction.reduce: cardinality()
+        return hll_cardinality(v)
     if fn == "minmaxrange":
         return v[1] - v[0] if v[0] != math.inf and v[1] != -math.inf else -1.0  # DEFAULT_MIN_MAX_RANGE_VALUE
     p = int(fn[len("percentile"):])

@@ -6,7 +6,10 @@ decomposed on the host into GPU sub-queries the fused scan kernels already run:
 * DISTINCTCOUNT(c) -> ``GROUP BY c`` with COUNT(*) under the same filter; intermediate the set of (int) values
   (DistinctCountAggregationFunction.java aggregate: IntOpenHashSet.add((int) value));
 * PERCENTILEnn(c) -> the same ``GROUP BY c`` histogram; intermediate the (value, count) pairs in value order, i.e. the
-  reference's DoubleArrayList of every selected value (PercentileAggregationFunction.java aggregate) held as a multiset.
+  reference's DoubleArrayList of every selected value (PercentileAggregationFunction.java aggregate) held as a multiset;
+* DISTINCTCOUNTHLL(c) -> the same histogram; intermediate the HyperLogLog registers of the distinct (int) values
+  (operator/aggregation/function/DistinctCountHLLAggregationFunction.java aggregate: hll.offer((int) value)), which
+  depend only on that set (hll.py).
 
 One histogram sub-query serves every DISTINCTCOUNT / PERCENTILE over the same column.  Statistics are the base query's,
 with numEntriesScannedPostFilter counted over the ORIGINAL projection columns (AggregationOperator.java:93-98).
@@ -22,8 +25,12 @@ from typing import Dict, List, Sequence
 import numpy as np
 
 from . import engine as E
+from . import hll as HLL
 from . import native as N
 from .pql import EXT_FUNCTIONS
+
+
+_HIST_FNS = ("distinctcount", "distinctcounthll")
 
 
 def has_extended(request: dict) -> bool:
@@ -85,7 +92,7 @@ def _base_request(request: dict):
         if fn == "minmaxrange":
             base += [{"fn": "min", "column": a["column"]}, {"fn": "max", "column": a["column"]}]
             slot.append((len(base) - 2, len(base) - 1))
-        elif fn == "distinctcount" or fn.startswith("percentile"):
+        elif fn in _HIST_FNS or fn.startswith("percentile"):
             slot.append(None)
         else:
             base.append(dict(a))
@@ -96,7 +103,7 @@ def _base_request(request: dict):
 def _hist_columns(request: dict, segments) -> List[str]:
     cols = []
     for a in request["aggregations"]:
-        if (a["fn"] == "distinctcount" or a["fn"].startswith("percentile")) and a["column"] not in cols:
+        if (a["fn"] in _HIST_FNS or a["fn"].startswith("percentile")) and a["column"] not in cols:
             if segments and segments[0].column(a["column"]).meta.data_type == "STRING":
                 raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a STRING column" % a["fn"])
             cols.append(a["column"])
@@ -143,6 +150,8 @@ def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock
             return (float(bvals[s[0]]), float(bvals[s[1]]))
         if fn == "distinctcount":
             return {java_int_cast(v) for v, _ in hists[a["column"]].get(key, [])}
+        if fn == "distinctcounthll":
+            return HLL.from_ints({java_int_cast(v) for v, _ in hists[a["column"]].get(key, [])})
         if fn.startswith("percentile"):
             return list(hists[a["column"]].get(key, []))
         return bvals[s]
@@ -199,6 +208,8 @@ def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment],
             out.append((float(base_res[s[0]]), float(base_res[s[1]])))
         elif fn == "distinctcount":
             out.append({java_int_cast(v) for v, _ in hists[a["column"]]})
+        elif fn == "distinctcounthll":
+            out.append(HLL.from_ints({java_int_cast(v) for v, _ in hists[a["column"]]}))
         elif fn.startswith("percentile"):
             out.append(list(hists[a["column"]]))
         else:
@@ -215,6 +226,8 @@ def reduce_value(fn: str, v):
     MinMaxRangeAggregationFunction.java:129-146 with DEFAULT_MIN_MAX_RANGE_VALUE = -1, PercentileUtil)."""
     if fn == "distinctcount":
         return len(v)
+    if fn == "distinctcounthll":  # query/aggregation/function/DistinctCountHLLAggregationFunction.java reduce
+        return HLL.cardinality(v)
     if fn == "minmaxrange":
         return v[1] - v[0] if v[0] != math.inf and v[1] != -math.inf else -1.0
     return percentile_of_histogram(fn, v)
@@ -224,6 +237,8 @@ def combine_two(fn: str, a, b):
     """combineTwoValues: set union, pair extremes, list concatenation (histogram merge)."""
     if fn == "distinctcount":
         return set(a) | set(b)
+    if fn == "distinctcounthll":  # HyperLogLog.addAll
+        return HLL.merge(a, b)
     if fn == "minmaxrange":
         return (min(a[0], b[0]), max(a[1], b[1]))
     return merge_histograms(a, b)

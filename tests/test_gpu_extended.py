@@ -36,6 +36,8 @@ QUERIES = [
     "SELECT SUM(m), DISTINCTCOUNT(w), PERCENTILE95(w), PERCENTILE99(w), MINMAXRANGE(w) FROM t WHERE d < 20",
     "SELECT MINMAXRANGE(m), DISTINCTCOUNT(v), AVG(m), PERCENTILE50(d) FROM t WHERE v > 1000 AND m IN (1, 2, 3, 4000)",
     "SELECT COUNT(*), MINMAXRANGE(m), DISTINCTCOUNT(d) FROM t WHERE d = 123456",
+    "SELECT DISTINCTCOUNTHLL(v), DISTINCTCOUNT(v), DISTINCTCOUNTHLL(w), DISTINCTCOUNTHLL(d) FROM t WHERE m < 4000",
+    "SELECT DISTINCTCOUNTHLL(m), COUNT(*) FROM t WHERE d = 123456",
 ]
 
 
@@ -53,6 +55,9 @@ def test_extended_functions_match_oracle(env, text):
     for fn, g, e in zip(fns, got, exp["results"]):
         if fn == "distinctcount":
             assert g == e
+        elif fn == "distinctcounthll":  # HyperLogLog registers bit-exact, then the same cardinality()
+            assert list(g) == list(e)
+            assert X.reduce_value(fn, g) == O.reduce_extended(fn, e)
         elif fn == "minmaxrange":
             assert tuple(g) == tuple(e)
             assert X.reduce_value(fn, g) == O.reduce_extended(fn, e)
@@ -71,6 +76,7 @@ GROUPED = [
     "SELECT DISTINCTCOUNT(v), MINMAXRANGE(m), SUM(m), PERCENTILE50(m), COUNT(*) FROM t GROUP BY d",
     "SELECT PERCENTILE90(w), DISTINCTCOUNT(w), MAX(v) FROM t WHERE m < 2500 GROUP BY d TOP 5",
     "SELECT MINMAXRANGE(v), AVG(m), DISTINCTCOUNT(m) FROM t WHERE d IN (1, 2, 3) GROUP BY d, m",
+    "SELECT DISTINCTCOUNTHLL(v), SUM(m), DISTINCTCOUNTHLL(w) FROM t WHERE m > 100 GROUP BY d",
 ]
 
 
@@ -88,6 +94,8 @@ def test_extended_functions_group_by_match_oracle(env, text):
         for fn, g, x in zip(fns, got[k], e):
             if fn == "distinctcount":
                 assert g == x
+            elif fn == "distinctcounthll":
+                assert list(g) == list(x)
             elif fn == "minmaxrange":
                 assert tuple(g) == tuple(x)
             elif fn.startswith("percentile"):

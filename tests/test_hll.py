@@ -1,0 +1,58 @@
+"""DISTINCTCOUNTHLL host logic (pinot_amd/hll.py, vectorised) against the oracle's scalar per-offer restatement of
+stream-lib 2.7.0 HyperLogLog(log2m = 8) / MurmurHash.hashLong, and the reference's own accuracy contract
+(query/aggregation/DistinctCountHLLTest.java:145-171 with TestUtils.assertApproximation: relative error < 0.1 at
+cardinalities >= 1000).  Parity of the hash itself is unpinned: stream-lib is a third-party jar absent from the
+reference and no test there holds literal HLL registers or hashes."""
+import numpy as np
+
+from oracle import pinot_oracle as O
+from pinot_amd import hll
+
+
+def _oracle_regs(values):
+    regs = [0] * 256
+    for v in values:
+        O.hll_offer(regs, int(v))
+    return regs
+
+
+def test_hash_matches_oracle_on_edge_and_random_ints():
+    rng = np.random.default_rng(3)
+    vals = [0, 1, -1, 2147483647, -2147483648, 12345, -54321] + rng.integers(-2**31, 2**31, 4000).tolist()
+    got = hll.hash_long(np.array(vals, dtype=np.int64)).view(np.int32).tolist()
+    assert got == [O.murmur_hash_long(v) for v in vals]
+
+
+def test_registers_match_oracle_and_depend_only_on_the_set():
+    rng = np.random.default_rng(4)
+    for n in (0, 1, 7, 300, 5000):
+        vals = rng.integers(-1000000, 1000000, n).tolist()
+        exp = _oracle_regs(vals)  # per-doc offers, duplicates and order as drawn
+        got = hll.from_ints(sorted(set(vals)))  # the distinct set, as the GPU histogram yields it
+        assert list(got) == exp
+        assert hll.cardinality(got) == O.hll_cardinality(exp)
+
+
+def test_merge_is_union():
+    a, b = list(range(0, 3000)), list(range(2000, 9000))
+    assert list(hll.merge(hll.from_ints(a), hll.from_ints(b))) == list(hll.from_ints(a + b))
+    assert O.combine_two("distinctcounthll", _oracle_regs(a), _oracle_regs(b)) == _oracle_regs(a + b)
+
+
+def test_small_cardinalities_use_linear_counting():
+    for n in (0, 1, 2, 10):
+        assert hll.cardinality(hll.from_ints(range(n))) == n
+    for n in (50, 200):  # m * ln(m / zeros): register collisions only
+        assert abs(hll.cardinality(hll.from_ints(range(n))) - n) <= 0.05 * n
+
+
+def test_accuracy_contract_of_the_reference():
+    rng = np.random.default_rng(5)
+    errs = []
+    for _ in range(40):
+        n = int(rng.integers(1000, 60000))
+        xs = np.unique(rng.integers(-2**31, 2**31, n))
+        errs.append(hll.cardinality(hll.from_ints(xs.tolist())) / len(xs) - 1.0)
+    errs = np.abs(np.array(errs))
+    assert np.mean(errs < 0.1) >= 0.8  # 1.04 / sqrt(256) = 6.5% standard error per estimate
+    assert errs.mean() < 0.07
