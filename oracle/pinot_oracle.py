@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import heapq
 import math
+import struct
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -924,6 +925,32 @@ def hll_cardinality(regs: List[int]) -> int:
     return int(math.floor(est + 0.5))
 
 
+def java_hash_code(col: OColumn, dict_id: int) -> int:
+    """common/DataFetcher.java:242-248 fetchSingleHashCodes: dictionary.get(dictId).hashCode() of the boxed value
+    (Integer, Long, Float, Double, String), the values DISTINCTCOUNT / DISTINCTCOUNTHLL receive
+    (operator/aggregation/DefaultAggregationExecutor.java:135-139)."""
+    v = col.dictionary[dict_id]
+    if col.dtype == "INT":
+        return _i32(int(v))
+    if col.dtype == "LONG":  # Long.hashCode: (int)(value ^ (value >>> 32))
+        u = int(v) & 0xFFFFFFFFFFFFFFFF
+        return _i32(u ^ (u >> 32))
+    if col.dtype == "FLOAT":  # Float.hashCode: floatToIntBits (NaN -> 0x7fc00000)
+        f = float(v)
+        return 0x7FC00000 if f != f else _i32(struct.unpack(">I", struct.pack(">f", f))[0])
+    if col.dtype == "DOUBLE":  # Double.hashCode: bits ^ (bits >>> 32) of doubleToLongBits
+        d = float(v)
+        u = 0x7FF8000000000000 if d != d else struct.unpack(">Q", struct.pack(">d", d))[0]
+        return _i32(u ^ (u >> 32))
+    h = 0  # String.hashCode over UTF-16 code units
+    for ch in str(v):
+        cp = ord(ch)
+        units = [cp] if cp < 0x10000 else [0xD800 + ((cp - 0x10000) >> 10), 0xDC00 + ((cp - 0x10000) & 0x3FF)]
+        for u16 in units:
+            h = (31 * h + u16) & 0xFFFFFFFF
+    return _i32(h)
+
+
 def _projection_columns(q: dict) -> List[str]:
     cols = []
     for a in q["aggregations"]:
@@ -961,6 +988,16 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
                 holders[k] = holders[k] + float(len(blk))  # CountAggregationFunction.aggregate:43-48
                 continue
             col = seg.columns[a["column"]]
+            if fn in ("distinctcount", "distinctcounthll"):  # getSVHashCodeArray: (int) of each value's hashCode()
+                hc = [java_hash_code(col, int(i)) for i in col.dict_ids[blk]]
+                if fn == "distinctcount":
+                    holders[k].update(hc)
+                else:
+                    for x in hc:
+                        hll_offer(holders[k], x)
+                continue
+            if col.dtype == "STRING":  # String[] values where aggregate() requires double[]
+                raise ValueError("%s over a STRING column" % fn)
             v = col.value_as_double(col.dict_ids[blk])
             if fn == "sum":  # SumAggregationFunction.aggregate:45-56 (sequential double sum)
                 s = float(np.cumsum(v)[-1]) if len(v) else 0.0
@@ -976,11 +1013,6 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
             elif fn == "avg":  # AvgAggregationFunction.aggregate:47-65
                 s = float(np.cumsum(v)[-1]) if len(v) else 0.0
                 holders[k] = [holders[k][0] + s, holders[k][1] + len(blk)]
-            elif fn == "distinctcount":  # DistinctCountAggregationFunction.aggregate: IntOpenHashSet of (int) value
-                holders[k].update(java_int_cast(x) for x in v.tolist())
-            elif fn == "distinctcounthll":  # DistinctCountHLLAggregationFunction.aggregate: hll.offer((int) value)
-                for x in v.tolist():
-                    hll_offer(holders[k], java_int_cast(x))
             elif fn == "minmaxrange":  # MinMaxRangeAggregationFunction.aggregate: block min / max into the pair
                 if len(v):
                     holders[k] = [min(holders[k][0], float(v.min())), max(holders[k][1], float(v.max()))]
@@ -1052,7 +1084,10 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
             vals = [int(x) for x in acc]
         else:
             col = seg.columns[a["column"]]
-            v = col.value_as_double(col.dict_ids[docs])
+            if fn in ("distinctcount", "distinctcounthll"):
+                v = [java_hash_code(col, int(i)) for i in col.dict_ids[docs]]
+            else:
+                v = col.value_as_double(col.dict_ids[docs])
             if fn == "sum":
                 acc = np.zeros(G)
                 np.add.at(acc, gid, v)  # unbuffered, in doc order == holder[key] += v sequentially
@@ -1072,12 +1107,12 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
                 vals = [(float(s), int(c)) for s, c in zip(acc, cnt)]
             elif fn == "distinctcount":  # DistinctCountAggregationFunction.aggregateGroupBySV: a set per group
                 vals = [set() for _ in range(G)]
-                for i, x in zip(gid.tolist(), v.tolist()):
-                    vals[i].add(java_int_cast(x))
+                for i, x in zip(gid.tolist(), v):
+                    vals[i].add(x)
             elif fn == "distinctcounthll":  # DistinctCountHLLAggregationFunction.aggregateGroupBySV: an HLL per group
                 vals = [[0] * (1 << HLL_LOG2M) for _ in range(G)]
-                for i, x in zip(gid.tolist(), v.tolist()):
-                    hll_offer(vals[i], java_int_cast(x))
+                for i, x in zip(gid.tolist(), v):
+                    hll_offer(vals[i], x)
             elif fn == "minmaxrange":  # MinMaxRangeAggregationFunction.aggregateGroupBySV: a (min, max) pair
                 mn = np.full(G, math.inf)
                 mx = np.full(G, -math.inf)

@@ -3,19 +3,22 @@ decomposed on the host into GPU sub-queries the fused scan kernels already run:
 
 * MINMAXRANGE(c) -> MIN(c) and MAX(c) in the base query; intermediate (min, max)
   (core/operator/aggregation/function/MinMaxRangeAggregationFunction.java aggregate: a Pair of block extremes);
-* DISTINCTCOUNT(c) -> ``GROUP BY c`` with COUNT(*) under the same filter; intermediate the set of (int) values
-  (DistinctCountAggregationFunction.java aggregate: IntOpenHashSet.add((int) value));
+* DISTINCTCOUNT(c) -> ``GROUP BY c`` with COUNT(*) under the same filter; intermediate the set of the values' Java
+  hashCode()s: the executor hands DISTINCTCOUNT / DISTINCTCOUNTHLL ``getSVHashCodeArray()``
+  (operator/aggregation/DefaultAggregationExecutor.java:135-139, common/DataFetcher.java:242-248:
+  ``dictionary.get(dictId).hashCode()``), and the function adds ``(int) hash`` (operator/aggregation/function/
+  DistinctCountAggregationFunction.java aggregate), so STRING columns are supported and FLOAT 0.25 / 0.75 stay distinct;
 * PERCENTILEnn(c) -> the same ``GROUP BY c`` histogram; intermediate the (value, count) pairs in value order, i.e. the
   reference's DoubleArrayList of every selected value (PercentileAggregationFunction.java aggregate) held as a multiset;
-* DISTINCTCOUNTHLL(c) -> the same histogram; intermediate the HyperLogLog registers of the distinct (int) values
-  (operator/aggregation/function/DistinctCountHLLAggregationFunction.java aggregate: hll.offer((int) value)), which
+* DISTINCTCOUNTHLL(c) -> the same histogram; intermediate the HyperLogLog registers of the distinct hash codes
+  (operator/aggregation/function/DistinctCountHLLAggregationFunction.java aggregate: hll.offer((int) hash)), which
   depend only on that set (hll.py).
 
 One histogram sub-query serves every DISTINCTCOUNT / PERCENTILE over the same column.  Statistics are the base query's,
 with numEntriesScannedPostFilter counted over the ORIGINAL projection columns (AggregationOperator.java:93-98).
 Group-by requests keep their GROUP BY columns in the base query, and the histograms group by those columns plus c
-(``_run_group_by``).  A STRING column under DISTINCTCOUNT / PERCENTILE raises ``PgxError(UNSUPPORTED)`` (the reference
-reads it through getDoubleValue, which STRING dictionaries do not support).
+(``_run_group_by``).  A STRING column under PERCENTILE / MINMAXRANGE raises ``PgxError(UNSUPPORTED)`` (the executor
+hands those functions String[] values and their aggregate() requires double[]).
 """
 from __future__ import annotations
 
@@ -47,6 +50,42 @@ def java_int_cast(x) -> int:
     if x <= -2147483648.0:
         return -2147483648
     return int(x)
+
+
+def java_hash_code(dtype: str, v) -> int:
+    """Boxed dictionary value's hashCode(): Integer -> value; Long -> (int)(v ^ v >>> 32); Float -> floatToIntBits;
+    Double -> (int)(bits ^ bits >>> 32) of doubleToLongBits (NaN canonical); String -> s[0]*31^(n-1) + ... over UTF-16
+    code units; all in Java int arithmetic."""
+    def i32(x: int) -> int:
+        x &= 0xFFFFFFFF
+        return x - (1 << 32) if x & 0x80000000 else x
+    if dtype == "INT":
+        return i32(int(v))
+    if dtype == "LONG":
+        u = int(v) & 0xFFFFFFFFFFFFFFFF
+        return i32(u ^ (u >> 32))
+    if dtype == "FLOAT":
+        f = np.float32(v)
+        return 0x7FC00000 if f != f else int(np.array([f], dtype=np.float32).view(np.int32)[0])
+    if dtype == "DOUBLE":
+        d = float(v)
+        u = 0x7FF8000000000000 if d != d else int(np.array([d]).view(np.uint64)[0])
+        return i32(u ^ (u >> 32))
+    h = 0
+    b = str(v).encode("utf-16-be", "surrogatepass")
+    for i in range(0, len(b), 2):
+        h = (31 * h + (b[i] << 8 | b[i + 1])) & 0xFFFFFFFF
+    return i32(h)
+
+
+def _parse_value(dtype: str, s: str):
+    """A group-key field back to the column's value (keys render INT/LONG as integers, FLOAT/DOUBLE as Double.toString,
+    which identifies the value exactly)."""
+    if dtype in ("INT", "LONG"):
+        return int(s)
+    if dtype == "STRING":
+        return s
+    return float(np.float32(float(s))) if dtype == "FLOAT" else float(s)
 
 
 def percentile_of_histogram(fn: str, hist: Sequence) -> float:
@@ -100,14 +139,29 @@ def _base_request(request: dict):
     return base, slot
 
 
+def _dtype(segments, col: str) -> str:
+    return segments[0].column(col).meta.data_type if segments else "INT"
+
+
 def _hist_columns(request: dict, segments) -> List[str]:
     cols = []
     for a in request["aggregations"]:
-        if (a["fn"] in _HIST_FNS or a["fn"].startswith("percentile")) and a["column"] not in cols:
-            if segments and segments[0].column(a["column"]).meta.data_type == "STRING":
-                raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a STRING column" % a["fn"])
+        fn = a["fn"]
+        if fn not in _HIST_FNS and fn != "minmaxrange" and not fn.startswith("percentile"):
+            continue
+        if fn not in _HIST_FNS and _dtype(segments, a["column"]) == "STRING":
+            raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a STRING column" % fn)
+        if fn != "minmaxrange" and a["column"] not in cols:
             cols.append(a["column"])
     return cols
+
+
+def _hash_set(dtype: str, hist) -> set:
+    return {java_hash_code(dtype, v) for v, _ in hist}
+
+
+def _numeric(hist) -> List:
+    return [(float(v), c) for v, c in hist]
 
 
 def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock:
@@ -125,6 +179,7 @@ def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock
         N.lib().pgx_result_release(r)
         bq.close()
     bmap = bblk.get_aggregation_group_by_result().as_map()
+    ng = len(gb["columns"])
     hists: Dict[str, Dict[str, List]] = {}
     for c in _hist_columns(request, segments):
         hq = E._Query(ctx, {"aggregations": [{"fn": "count", "column": "*"}],
@@ -136,11 +191,13 @@ def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock
         finally:
             N.lib().pgx_result_release(r)
             hq.close()
-        per: Dict[str, Dict[float, int]] = {}
+        dt = _dtype(segments, c)
+        per: Dict[str, Dict[object, int]] = {}
         for key, (cnt,) in hmap.items():
-            g, v = key.rsplit("\t", 1)
+            f = key.split("\t", ng)  # the value field is last and may itself hold tabs (STRING)
+            g, v = "\t".join(f[:ng]), _parse_value(dt, f[ng])
             d = per.setdefault(g, {})
-            d[float(v)] = d.get(float(v), 0) + int(cnt)
+            d[v] = d.get(v, 0) + int(cnt)
         hists[c] = {g: sorted(d.items()) for g, d in per.items()}
     aggs = request["aggregations"]
 
@@ -149,11 +206,11 @@ def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock
         if fn == "minmaxrange":
             return (float(bvals[s[0]]), float(bvals[s[1]]))
         if fn == "distinctcount":
-            return {java_int_cast(v) for v, _ in hists[a["column"]].get(key, [])}
+            return _hash_set(_dtype(segments, a["column"]), hists[a["column"]].get(key, []))
         if fn == "distinctcounthll":
-            return HLL.from_ints({java_int_cast(v) for v, _ in hists[a["column"]].get(key, [])})
+            return HLL.from_ints(_hash_set(_dtype(segments, a["column"]), hists[a["column"]].get(key, [])))
         if fn.startswith("percentile"):
-            return list(hists[a["column"]].get(key, []))
+            return _numeric(hists[a["column"]].get(key, []))
         return bvals[s]
 
     keys = list(bmap)
@@ -199,7 +256,7 @@ def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment],
             N.lib().pgx_result_release(r)
             hq.close()
         order = np.argsort(cols[0], kind="stable")
-        hists[c] = [(float(cols[0][i]), int(cnts[0][i])) for i in order]
+        hists[c] = [(cols[0][i], int(cnts[0][i])) for i in order]
     base_res = bblk.get_aggregation_result()
     out = []
     for a, s in zip(aggs, slot):
@@ -207,11 +264,11 @@ def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment],
         if fn == "minmaxrange":
             out.append((float(base_res[s[0]]), float(base_res[s[1]])))
         elif fn == "distinctcount":
-            out.append({java_int_cast(v) for v, _ in hists[a["column"]]})
+            out.append(_hash_set(_dtype(segments, a["column"]), hists[a["column"]]))
         elif fn == "distinctcounthll":
-            out.append(HLL.from_ints({java_int_cast(v) for v, _ in hists[a["column"]]}))
+            out.append(HLL.from_ints(_hash_set(_dtype(segments, a["column"]), hists[a["column"]])))
         elif fn.startswith("percentile"):
-            out.append(list(hists[a["column"]]))
+            out.append(_numeric(hists[a["column"]]))
         else:
             out.append(base_res[s])
     st = bblk.stats

@@ -109,13 +109,32 @@ def test_extended_functions_group_by_match_oracle(env, text):
     assert st[0] == exp["stats"][0] and st[2] == exp["stats"][2] and st[3] == exp["stats"][3]
 
 
-def test_extended_over_string_column_is_unsupported(env):
+def test_extended_over_string_column(env):
+    """DISTINCTCOUNT / DISTINCTCOUNTHLL take String.hashCode() of STRING values (getSVHashCodeArray); PERCENTILE gets
+    String[] where its aggregate() requires double[], which the reference rejects."""
     from pinot_amd import engine as E
     from pinot_amd import native as N
     ctx, _, _ = env
-    raw = {"s": np.array(["a", "b", "c", "a"]), "m": np.array([1, 2, 3, 4], dtype=np.int32)}
-    seg, _ = H.build_pair("strx", raw)
+    words = np.array(["a", "b", "c", "a", "hello", "Aa", "BB", "\u00e9t\u00e9", "x\ty"])  # "Aa"/"BB" share a hash
+    raw = {"s": words, "m": np.arange(len(words), dtype=np.int32)}
+    seg, o = H.build_pair("strx", raw)
     g = E.IndexSegment(ctx, seg)
+    pm = E.InstancePlanMakerImplV2(ctx)
+    for text in ("SELECT DISTINCTCOUNT(s), DISTINCTCOUNTHLL(s) FROM t WHERE m < 8",
+                 "SELECT DISTINCTCOUNT(s), DISTINCTCOUNTHLL(s) FROM t GROUP BY m"):
+        q = pql.compile(text)
+        blk = pm.make_inter_segment_plan([g], q).execute()
+        if q.get("group_by"):
+            got = blk.get_aggregation_group_by_result().as_map()
+            exp = O.combine_group_by([O.run_group_by(o, q, literal_filter=False)], q)["merged"]
+            assert set(got) == set(exp)
+            for k in exp:
+                assert got[k][0] == exp[k][0] and list(got[k][1]) == list(exp[k][1])
+        else:
+            got = blk.get_aggregation_result()
+            exp = O.combine_aggregation([O.run_aggregation(o, q, literal_filter=False)], q)["results"]
+            assert got[0] == exp[0] and list(got[1]) == list(exp[1])
+            assert len(got[0]) == 6  # a b c hello Aa|BB ete
     with pytest.raises(N.PgxError) as ei:
-        E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan([g], pql.compile("SELECT DISTINCTCOUNT(s) FROM t")).execute()
+        pm.make_inter_segment_plan([g], pql.compile("SELECT PERCENTILE50(s) FROM t")).execute()
     assert ei.value.status == N.PGX_ERR_UNSUPPORTED

@@ -56,3 +56,19 @@ def test_accuracy_contract_of_the_reference():
     errs = np.abs(np.array(errs))
     assert np.mean(errs < 0.1) >= 0.8  # 1.04 / sqrt(256) = 6.5% standard error per estimate
     assert errs.mean() < 0.07
+
+
+def test_java_hash_codes_known_answers():
+    """Values the JDK defines: "a".hashCode() = 97, "hello".hashCode() = 99162322, "Aa" and "BB" collide (2112),
+    Long.hashCode(1L << 32) = 1, Long.hashCode(-1L) = 0, Float.hashCode(1.0f) = 0x3f800000,
+    Double.hashCode(1.0) = 0x3ff00000, Double.hashCode(-0.0) = 0x80000000 (as int)."""
+    from pinot_amd.extended import java_hash_code as P
+    cases = [("STRING", "a", 97), ("STRING", "hello", 99162322), ("STRING", "Aa", 2112), ("STRING", "BB", 2112),
+             ("STRING", "", 0), ("LONG", 1 << 32, 1), ("LONG", -1, 0), ("INT", -5, -5),
+             ("FLOAT", 1.0, 0x3F800000), ("DOUBLE", 1.0, 0x3FF00000), ("DOUBLE", -0.0, -0x80000000),
+             ("FLOAT", float("nan"), 0x7FC00000)]
+    for dt, v, h in cases:
+        assert P(dt, v) == h, (dt, v)
+        col = O.OColumn("c", dt, np.array([v], dtype=object if dt == "STRING" else None), np.zeros(1, np.int64),
+                        True, False, 1)
+        assert O.java_hash_code(col, 0) == h, (dt, v)
