@@ -868,7 +868,7 @@ def filter_mask_vectorized(seg: OSegment, tree: Optional[dict]) -> np.ndarray:
 # a-13..a-17, a-20: aggregation / group-by execution
 # ------------------------------------------------------------------------------------------------
 FN_DEFAULT = {"count": 0.0, "sum": 0.0, "min": math.inf, "max": -math.inf}
-EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
+EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
 
 
 # DISTINCTCOUNTHLL: stream-lib 2.7.0 HyperLogLog(log2m = HllConstants.DEFAULT_LOG2M = 8) (third-party, not vendored;
@@ -907,6 +907,24 @@ def hll_offer(regs: List[int], value: int) -> None:
     r = 32 - w.bit_length() + 1
     if r > regs[j]:
         regs[j] = r
+
+
+def hll_from_string(s: str) -> List[int]:
+    """HllUtil.convertStringToHll (core/startree/hll/HllUtil.java:58-60, SerializationConverter :146-175: byte =
+    (byte)(char - 129)) then HyperLogLog.Builder.build: readInt log2m, readInt size, size bytes of big-endian int
+    RegisterSet words, register i = (word[i / 6] >>> 5 * (i % 6)) & 0x1f."""
+    b = bytes(((ord(c) - 129) & 0xFF) for c in s)
+    log2m, size = struct.unpack_from(">ii", b, 0)
+    if log2m != HLL_LOG2M:  # HyperLogLog.addAll into HyperLogLog(8): "Cannot merge estimators of different sizes"
+        raise ValueError("Cannot merge estimators of different sizes")
+    words = struct.unpack_from(">%dI" % (size // 4), b, 8)
+    return [(words[i // 6] >> (5 * (i % 6))) & 0x1F for i in range(1 << HLL_LOG2M)]
+
+
+def hll_add_all(regs: List[int], other: List[int]) -> None:
+    for i, v in enumerate(other):
+        if v > regs[i]:
+            regs[i] = v
 
 
 def hll_cardinality(regs: List[int]) -> int:
@@ -978,7 +996,7 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
     for a in q["aggregations"]:
         fn = a["fn"]
         holders.append([0.0, 0] if fn == "avg" else set() if fn == "distinctcount" else
-                       [0] * (1 << HLL_LOG2M) if fn == "distinctcounthll" else
+                       [0] * (1 << HLL_LOG2M) if fn in ("distinctcounthll", "fasthll") else
                        [math.inf, -math.inf] if fn == "minmaxrange" else [] if fn.startswith("percentile") else
                        FN_DEFAULT[fn])
     for blk in _blocks(docs, MAX_DOC_PER_CALL):
@@ -995,6 +1013,12 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
                 else:
                     for x in hc:
                         hll_offer(holders[k], x)
+                continue
+            if fn == "fasthll":  # FastHllAggregationFunction.aggregate: addAll(convertStringToHll(value)) per doc
+                if col.dtype != "STRING":
+                    raise ValueError("fasthll over a non-STRING column")
+                for i in col.dict_ids[blk]:
+                    hll_add_all(holders[k], hll_from_string(col.dictionary[int(i)]))
                 continue
             if col.dtype == "STRING":  # String[] values where aggregate() requires double[]
                 raise ValueError("%s over a STRING column" % fn)
@@ -1026,7 +1050,7 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
             results.append((float(holders[k][0]), int(holders[k][1])))
         elif a["fn"] == "distinctcount":
             results.append(set(holders[k]))
-        elif a["fn"] == "distinctcounthll":
+        elif a["fn"] in ("distinctcounthll", "fasthll"):
             results.append(list(holders[k]))
         elif a["fn"] == "minmaxrange":
             results.append((float(holders[k][0]), float(holders[k][1])))
@@ -1086,6 +1110,8 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
             col = seg.columns[a["column"]]
             if fn in ("distinctcount", "distinctcounthll"):
                 v = [java_hash_code(col, int(i)) for i in col.dict_ids[docs]]
+            elif fn == "fasthll":
+                v = [col.dictionary[int(i)] for i in col.dict_ids[docs]]
             else:
                 v = col.value_as_double(col.dict_ids[docs])
             if fn == "sum":
@@ -1113,6 +1139,10 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
                 vals = [[0] * (1 << HLL_LOG2M) for _ in range(G)]
                 for i, x in zip(gid.tolist(), v):
                     hll_offer(vals[i], x)
+            elif fn == "fasthll":  # FastHllAggregationFunction.aggregateGroupBySV: addAll per doc into its group's HLL
+                vals = [[0] * (1 << HLL_LOG2M) for _ in range(G)]
+                for i, x in zip(gid.tolist(), v):
+                    hll_add_all(vals[i], hll_from_string(x))
             elif fn == "minmaxrange":  # MinMaxRangeAggregationFunction.aggregateGroupBySV: a (min, max) pair
                 mn = np.full(G, math.inf)
                 mx = np.full(G, -math.inf)
@@ -1160,7 +1190,7 @@ def combine_two(fn: str, a, b):
         return (a[0] + b[0], a[1] + b[1])
     if fn == "distinctcount":  # DistinctCountAggregationFunction.combineTwoValues: set union
         return set(a) | set(b)
-    if fn == "distinctcounthll":  # DistinctCountHLLAggregationFunction.combineTwoValues: HyperLogLog.addAll
+    if fn in ("distinctcounthll", "fasthll"):  # {DistinctCountHLL,FastHll}AggregationFunction.combineTwoValues: addAll
         return [max(x, y) for x, y in zip(a, b)]
     if fn == "minmaxrange":  # MinMaxRangeAggregationFunction.combineTwoValues
         return (min(a[0], b[0]), max(a[1], b[1]))
@@ -1186,7 +1216,7 @@ def reduce_extended(fn: str, v) -> float:
     (int)(size * p / 100))."""
     if fn == "distinctcount":
         return len(v)
-    if fn == "distinctcounthll":  # DistinctCountHLLAggregationFunction.reduce: cardinality()
+    if fn in ("distinctcounthll", "fasthll"):  # {DistinctCountHLL,FastHll}AggregationFunction.reduce: cardinality()
         return hll_cardinality(v)
     if fn == "minmaxrange":
         return v[1] - v[0] if v[0] != math.inf and v[1] != -math.inf else -1.0  # DEFAULT_MIN_MAX_RANGE_VALUE

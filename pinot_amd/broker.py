@@ -28,7 +28,7 @@ from . import extended as X
 from .pql import EXT_FUNCTIONS
 
 
-_NAMES = {"distinctcount": "distinctCount", "distinctcounthll": "distinctCountHLL", "minmaxrange": "minMaxRange"}
+_NAMES = {"distinctcount": "distinctCount", "distinctcounthll": "distinctCountHLL", "fasthll": "fasthll", "minmaxrange": "minMaxRange"}
 
 
 def function_name(agg: dict) -> str:
@@ -83,7 +83,7 @@ def _reduce(fn: str, values: Sequence):
         for v in values:
             acc = v if acc is None else X.combine_two(fn, acc, v)
         if acc is None:
-            return 0 if fn in ("distinctcount", "distinctcounthll") else (-1.0 if fn == "minmaxrange" else 0.0)
+            return 0 if fn in ("distinctcount", "distinctcounthll", "fasthll") else (-1.0 if fn == "minmaxrange" else 0.0)
         return X.reduce_value(fn, acc)
     if fn == "count":
         return sum(int(v) for v in values)
@@ -113,7 +113,7 @@ def _reduce(fn: str, values: Sequence):
 
 def _format(fn: str, v) -> str:
     """Long / Integer (count, distinctcount) -> toString; doubles -> %1.5f (BrokerReduceService.formatValue)."""
-    return str(int(v)) if fn in ("count", "distinctcount", "distinctcounthll") else java_format_5f(float(v))
+    return str(int(v)) if fn in ("count", "distinctcount", "distinctcounthll", "fasthll") else java_format_5f(float(v))
 
 
 @dataclass

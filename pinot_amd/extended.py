@@ -33,7 +33,7 @@ from . import native as N
 from .pql import EXT_FUNCTIONS
 
 
-_HIST_FNS = ("distinctcount", "distinctcounthll")
+_HIST_FNS = ("distinctcount", "distinctcounthll", "fasthll")
 
 
 def has_extended(request: dict) -> bool:
@@ -151,6 +151,8 @@ def _hist_columns(request: dict, segments) -> List[str]:
             continue
         if fn not in _HIST_FNS and _dtype(segments, a["column"]) == "STRING":
             raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a STRING column" % fn)
+        if fn == "fasthll" and _dtype(segments, a["column"]) != "STRING":  # aggregate() requires String[]
+            raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "fasthll over a non-STRING column")
         if fn != "minmaxrange" and a["column"] not in cols:
             cols.append(a["column"])
     return cols
@@ -158,6 +160,19 @@ def _hist_columns(request: dict, segments) -> List[str]:
 
 def _hash_set(dtype: str, hist) -> set:
     return {java_hash_code(dtype, v) for v, _ in hist}
+
+
+def _fast_hll(hist) -> np.ndarray:
+    """FastHllAggregationFunction.aggregate: addAll of every selected doc's deserialized HLL into a fresh HyperLogLog(8)
+    (operator/aggregation/function/FastHllAggregationFunction.java aggregate); max is idempotent, so each distinct
+    serialized value is merged once."""
+    regs = HLL.empty()
+    for v, _ in hist:
+        try:
+            regs = HLL.merge(regs, HLL.from_string(v))
+        except ValueError as e:
+            raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "fasthll: %s" % e)
+    return regs
 
 
 def _numeric(hist) -> List:
@@ -209,6 +224,8 @@ def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock
             return _hash_set(_dtype(segments, a["column"]), hists[a["column"]].get(key, []))
         if fn == "distinctcounthll":
             return HLL.from_ints(_hash_set(_dtype(segments, a["column"]), hists[a["column"]].get(key, [])))
+        if fn == "fasthll":
+            return _fast_hll(hists[a["column"]].get(key, []))
         if fn.startswith("percentile"):
             return _numeric(hists[a["column"]].get(key, []))
         return bvals[s]
@@ -267,6 +284,8 @@ def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment],
             out.append(_hash_set(_dtype(segments, a["column"]), hists[a["column"]]))
         elif fn == "distinctcounthll":
             out.append(HLL.from_ints(_hash_set(_dtype(segments, a["column"]), hists[a["column"]])))
+        elif fn == "fasthll":
+            out.append(_fast_hll(hists[a["column"]]))
         elif fn.startswith("percentile"):
             out.append(_numeric(hists[a["column"]]))
         else:
@@ -283,7 +302,7 @@ def reduce_value(fn: str, v):
     MinMaxRangeAggregationFunction.java:129-146 with DEFAULT_MIN_MAX_RANGE_VALUE = -1, PercentileUtil)."""
     if fn == "distinctcount":
         return len(v)
-    if fn == "distinctcounthll":  # query/aggregation/function/DistinctCountHLLAggregationFunction.java reduce
+    if fn in ("distinctcounthll", "fasthll"):  # query/aggregation/function/{DistinctCountHLL,FastHll}... reduce
         return HLL.cardinality(v)
     if fn == "minmaxrange":
         return v[1] - v[0] if v[0] != math.inf and v[1] != -math.inf else -1.0
@@ -294,7 +313,7 @@ def combine_two(fn: str, a, b):
     """combineTwoValues: set union, pair extremes, list concatenation (histogram merge)."""
     if fn == "distinctcount":
         return set(a) | set(b)
-    if fn == "distinctcounthll":  # HyperLogLog.addAll
+    if fn in ("distinctcounthll", "fasthll"):  # HyperLogLog.addAll
         return HLL.merge(a, b)
     if fn == "minmaxrange":
         return (min(a[0], b[0]), max(a[1], b[1]))

@@ -1,6 +1,6 @@
-"""DISTINCTCOUNTHLL intermediates: HyperLogLog(log2m = 8) register sets, vectorised over numpy.
+"""DISTINCTCOUNTHLL / FASTHLL intermediates: HyperLogLog(log2m = 8) register sets, vectorised over numpy.
 
-The hot path offers ``(int) value`` of every selected doc (core/operator/aggregation/function/
+The hot path offers ``(int) hashCode`` of every selected doc's value (core/operator/aggregation/function/
 DistinctCountHLLAggregationFunction.java:51-62 aggregate, :80-92 aggregateGroupBySV; log2m = HllConstants.DEFAULT_LOG2M,
 core/startree/hll/HllConstants.java:19).  The HyperLogLog and its hash live in the third-party stream-lib
 (com.clearspring.analytics:stream 2.7.0, pom.xml:525-527, not vendored in the reference); their published algorithm is
@@ -111,3 +111,48 @@ def _java_round(x: float) -> int:
     if x >= 9.223372036854775807e18:
         return (1 << 63) - 1
     return int(math.floor(x + 0.5))
+
+
+# ---- serialized form (FASTHLL columns) --------------------------------------------------------------------------
+# HyperLogLog.getBytes(): writeInt(log2m), writeInt(4 * words), then the RegisterSet words big-endian; a word holds 6
+# registers of 5 bits (register i: word i / 6, shift 5 * (i % 6)); 2^8 registers -> 43 words -> 180 bytes
+# (HllUtil.LOG2M_TO_SIZE_IN_BYTES, core/startree/hll/HllUtil.java:38-39).  The segment stores it as a STRING whose chars
+# are byte + 129 (HllUtil.SerializationConverter, :146-175).
+_PER_WORD = 6
+_CHAR_OFFSET = 129
+
+
+def _words_for(count: int) -> int:
+    bits = count // _PER_WORD  # RegisterSet.getSizeForCount
+    return 1 if bits == 0 else bits if bits % 32 == 0 else bits + 1
+
+
+def to_bytes(regs: np.ndarray, log2m: int = LOG2M) -> bytes:
+    n = 1 << log2m
+    words = np.zeros(_words_for(n), dtype=np.uint32)
+    pos = np.arange(n)
+    np.bitwise_or.at(words, pos // _PER_WORD,
+                     regs[:n].astype(np.uint32) << (5 * (pos % _PER_WORD)).astype(np.uint32))
+    head = np.array([log2m, 4 * len(words)], dtype=">i4").tobytes()
+    return head + words.astype(">u4").tobytes()
+
+
+def from_bytes(b: bytes) -> np.ndarray:
+    """HyperLogLog.Builder.build: the registers (log2m must be this module's: addAll of estimators of different sizes
+    throws in the reference)."""
+    log2m, nbytes = (int(x) for x in np.frombuffer(b[:8], dtype=">i4"))
+    if log2m != LOG2M:
+        raise ValueError("Cannot merge estimators of different sizes (log2m %d)" % log2m)
+    words = np.frombuffer(b[8:8 + nbytes], dtype=">u4").astype(np.uint32)
+    pos = np.arange(M)
+    return ((words[pos // _PER_WORD] >> (5 * (pos % _PER_WORD)).astype(np.uint32)) & 0x1F).astype(np.uint8)
+
+
+def to_string(regs: np.ndarray) -> str:
+    """HllUtil.convertHllToString: one char per (signed) byte, char = byte + 129."""
+    return "".join(chr(((x - 256) if x > 127 else x) + _CHAR_OFFSET) for x in to_bytes(regs))
+
+
+def from_string(s: str) -> np.ndarray:
+    """HllUtil.convertStringToHll: byte = (byte) (char - 129)."""
+    return from_bytes(bytes(((ord(c) - _CHAR_OFFSET) & 0xFF) for c in s))

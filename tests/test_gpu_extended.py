@@ -138,3 +138,39 @@ def test_extended_over_string_column(env):
     with pytest.raises(N.PgxError) as ei:
         pm.make_inter_segment_plan([g], pql.compile("SELECT PERCENTILE50(s) FROM t")).execute()
     assert ei.value.status == N.PGX_ERR_UNSUPPORTED
+
+
+def test_fasthll_over_serialized_hll_column(env):
+    """FASTHLL over a STRING column of serialized HyperLogLogs (the star-tree HLL derived field: HllUtil
+    .convertHllToString, char = byte + 129): addAll of every selected doc's estimator, aggregation-only and group-by,
+    registers bit-exact against the oracle's per-doc restatement; FASTHLL over a numeric column is rejected."""
+    from pinot_amd import engine as E
+    from pinot_amd import hll
+    from pinot_amd import native as N
+    ctx, _, _ = env
+    rng = np.random.default_rng(23)
+    pool = [hll.to_string(hll.from_ints(rng.integers(0, 1 << 20, int(rng.integers(1, 400))).tolist()))
+            for _ in range(60)]
+    gsegs, osegs = [], []
+    for i in range(2):
+        n = 3000 + 500 * i
+        raw = {"h": np.array([pool[j] for j in rng.integers(0, len(pool), n)], dtype=object),
+               "d": rng.integers(0, 12, n).astype(np.int32)}
+        s, o = H.build_pair("fhll%d" % i, raw)
+        gsegs.append(E.IndexSegment(ctx, s))
+        osegs.append(o)
+    pm = E.InstancePlanMakerImplV2(ctx)
+    q = pql.compile("SELECT FASTHLL(h), COUNT(*) FROM t WHERE d < 7")
+    got = pm.make_inter_segment_plan(gsegs, q).execute().get_aggregation_result()
+    exp = O.combine_aggregation([O.run_aggregation(o, q, literal_filter=False) for o in osegs], q)["results"]
+    assert list(got[0]) == list(exp[0]) and int(got[1]) == int(exp[1])
+    assert hll.cardinality(got[0]) == O.reduce_extended("fasthll", exp[0])
+    q = pql.compile("SELECT FASTHLL(h) FROM t GROUP BY d")
+    got = pm.make_inter_segment_plan(gsegs, q).execute().get_aggregation_group_by_result().as_map()
+    exp = O.combine_group_by([O.run_group_by(o, q, literal_filter=False) for o in osegs], q)["merged"]
+    assert set(got) == set(exp)
+    for k in exp:
+        assert list(got[k][0]) == list(exp[k][0])
+    with pytest.raises(N.PgxError) as ei:
+        pm.make_inter_segment_plan(gsegs, pql.compile("SELECT FASTHLL(d) FROM t")).execute()
+    assert ei.value.status == N.PGX_ERR_UNSUPPORTED

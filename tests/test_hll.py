@@ -72,3 +72,17 @@ def test_java_hash_codes_known_answers():
         col = O.OColumn("c", dt, np.array([v], dtype=object if dt == "STRING" else None), np.zeros(1, np.int64),
                         True, False, 1)
         assert O.java_hash_code(col, 0) == h, (dt, v)
+
+
+def test_serialized_form_size_and_round_trip():
+    """HllFieldSizeTest: getBytes() of a log2m = 8 estimator is HllUtil.getHllFieldSizeFromLog2m(8) = 180 bytes; the
+    STRING form (char = byte + 129) round-trips through the oracle's independent decoder."""
+    rng = np.random.default_rng(6)
+    for n in (0, 1, 50, 20000):
+        regs = hll.from_ints(rng.integers(-2**31, 2**31, n).tolist())
+        b = hll.to_bytes(regs)
+        assert len(b) == 180 and b[:8] == bytes([0, 0, 0, 8, 0, 0, 0, 172])
+        s = hll.to_string(regs)
+        assert all(1 <= ord(c) <= 256 for c in s)
+        assert list(hll.from_string(s)) == list(regs)
+        assert O.hll_from_string(s) == list(regs)
