@@ -1979,7 +1979,7 @@ uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {
 // -------------------------------------------------------------------------------------------------
 constexpr int kPart1Bits = 7;           // first pass: 128 buckets (top bits of the mix)
 constexpr int kPart1N = 1 << kPart1Bits;
-constexpr int64_t kPartGroupsPerWg = 1400;  // groups per pgx_part_aggregate workgroup: LDS table load <= ~1/3 (4096 slots)
+constexpr int64_t kPartGroupsPerWg = 700;   // groups per pgx_part_aggregate workgroup: LDS table load <= ~1/3 (2048 slots)
 constexpr uint64_t kPartMaxBytes = uint64_t(96) << 30;  // partition buffers beyond this: fall back to the hash table
 constexpr int kPartChunkRecs = 8192;    // records per pgx_partition workgroup (pgx_kernels.hip kPartChunk)
 constexpr int kCursorStride = 16;       // u64 words between cursors: one 128-B line each

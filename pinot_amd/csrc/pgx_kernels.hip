@@ -750,7 +750,7 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
 // PACK: count and sum share one 64-bit LDS add ((1 << pack_shift) + value; the host checks that a partition's value
 // sum stays below bit pack_shift and its count below bit 64 - pack_shift).
 constexpr int kAggWays = 4;
-constexpr int kAggBuckets = 1024;
+constexpr int kAggBuckets = 512;
 constexpr int kAggSlots = kAggBuckets * kAggWays;
 constexpr int kAggThreads = 1024;
 constexpr int kAggPer = 8;
