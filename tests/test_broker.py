@@ -125,3 +125,21 @@ def test_gpu_servers_match_reference_goldens():
         assert gpu == cpu
     finally:
         ctx.close()
+
+
+def test_hll_functions_reduce_and_render(osegs):
+    """DISTINCTCOUNTHLL across servers: HyperLogLog.addAll of the server estimators, cardinality() rendered as a long
+    (query/aggregation/function/DistinctCountHLLAggregationFunction.java combine / reduce / getFunctionName), equal to
+    the estimate over all servers' distinct hash codes."""
+    from pinot_amd import hll
+    q = pql.compile("SELECT DISTINCTCOUNTHLL(dim0), DISTINCTCOUNT(dim0) FROM midas")
+    one = _oracle_response(q, osegs)
+    resp = B.BrokerReduceService().reduce_on_data_table(q, {"s1": one, "s2": one, "s3": one})
+    got = _by_fn(resp)
+    assert set(got) == {"distinctCountHLL_dim0", "distinctCount_dim0"}
+    regs = np.array(one.aggregation[0], dtype=np.uint8)
+    assert got["distinctCountHLL_dim0"] == str(hll.cardinality(regs))
+    assert list(hll.from_ints(one.aggregation[1])) == list(regs)  # registers are a function of the hash-code set
+    empty = B.BrokerReduceService().reduce_on_data_table(pql.compile("SELECT FASTHLL(dim0) FROM midas"),
+                                                          {"s": B.InstanceResponse(aggregation=[None])})
+    assert _by_fn(empty) == {"fasthll_dim0": "0"}
