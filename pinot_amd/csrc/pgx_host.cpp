@@ -1064,7 +1064,6 @@ void plan_star_segment(const pgx_query& q, const pgx_segment& seg, const KSeg& S
     const int rl = put_ranges(kv.second);
     sp.op.push_back(OP_LEAF);
     sp.arg.push_back(rl);
-    int pushed = 1;
     for (int pass = 0; pass < 2; ++pass)  // index-based children first, then scans (AndBlockDocIdSet)
       for (int l = 0; l < nl; ++l) {
         if (!((kv.first >> l) & 1u)) continue;
@@ -1075,7 +1074,6 @@ void plan_star_segment(const pgx_query& q, const pgx_segment& seg, const KSeg& S
         sp.arg.push_back(l);
         sp.op.push_back(OP_AND);
         sp.arg.push_back(2);
-        ++pushed;
       }
     ++terms;
   }
