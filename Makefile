@@ -23,11 +23,15 @@ build/pgx_kernels.o: $(CSRC)/pgx_kernels.hip $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+build/pgx_stats.o: $(CSRC)/pgx_stats.cpp $(CSRC)/pgx_internal.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
 build/pgx_trim.o: $(CSRC)/pgx_trim.hip
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o build/pgx_trim.o
+pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o build/pgx_trim.o build/pgx_stats.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 
 clean:

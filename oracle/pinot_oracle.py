@@ -245,7 +245,8 @@ def make_evaluator(col: OColumn, leaf: dict) -> Evaluator:
         non = np.array([i] if i >= 0 else [], dtype=np.int64)
         if i >= 0:
             m[i] = False
-        return Evaluator(op, m, np.nonzero(m)[0], non, False)
+        # NotEqualsPredicateEvaluator.alwaysFalse (:102-104): every dictId excluded
+        return Evaluator(op, m, np.nonzero(m)[0], non, len(non) == card)
     if op == "NOT_IN":
         m[:] = True
         non = set()
@@ -255,7 +256,8 @@ def make_evaluator(col: OColumn, leaf: dict) -> Evaluator:
                 non.add(i)
         for i in non:
             m[i] = False
-        return Evaluator(op, m, np.nonzero(m)[0], np.array(sorted(non), dtype=np.int64), False)
+        # NotInPredicateEvaluator.alwaysFalse (:98-100): the excluded id set covers the dictionary
+        return Evaluator(op, m, np.nonzero(m)[0], np.array(sorted(non), dtype=np.int64), len(non) == card)
     raise ValueError(op)
 
 
@@ -668,6 +670,7 @@ class _AndSet:
     def __init__(self, children):
         self.children = children
         self.lo, self.hi = INT_MIN, INT_MAX
+        self.answer = None  # the `answer` FIELD (:46): it survives between iterator() calls
         self._update()
 
     def _update(self):
@@ -696,6 +699,10 @@ class _AndSet:
         return sum(c.entries() for c in self.children)
 
     def iterator(self):
+        """fastIterator (:146-229).  The classification loop already calls iterator() on every nested operator child
+        (:166-168) and the no-index branch calls it on every child again (:171-178), so an AND without sorted/bitmap
+        children builds its nested operators' iterators twice; a nested AND with bitmap children but no sorted child
+        then re-uses its `answer` field (:192-203), already reduced by the first call's applyAnd."""
         ranges, bitmaps, scans, rest = [], [], [], []
         for c in self.children:
             if c.kind == "sorted":
@@ -709,18 +716,21 @@ class _AndSet:
         if not bitmaps and not ranges:
             its = [c.iterator() for c in self.children]
             return _AndIter(its, [_flag(c) for c in self.children])
-        answer = None
         if ranges:
             # SortedRangeIntersection.intersectSortedRangeSets (util/SortedRangeIntersection.java:31)
             sets = [set(r.docs()) for r in ranges]
-            answer = set.intersection(*sets) if sets else set()
-        for b in bitmaps:
-            answer = set(b.answer) if answer is None else (answer & set(b.answer))
-        answer = sorted(answer)
+            self.answer = set.intersection(*sets) if sets else set()
+        for i, b in enumerate(bitmaps):
+            if self.answer is None:
+                self.answer = set(b.answer)
+            else:
+                self.answer &= set(b.answer)
+        answer = sorted(self.answer)
         for s in scans:
             it = s.iterator()
             res = set(it.apply_and(answer))
             answer = [d for d in answer if d in res]
+        self.answer = set(answer)
         ans_it = _ListIter(answer)
         if not rest:
             return ans_it

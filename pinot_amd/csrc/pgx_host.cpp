@@ -58,6 +58,9 @@ extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int6
 extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
                                               const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
 extern "C" size_t pgx_trim_state_bytes(void);
+extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
+                                     int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
+                                     uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream);
 struct pgx_ctx;
 extern "C" void ctx_unref(pgx_ctx* ctx);
 
@@ -916,6 +919,18 @@ struct ExecPlan {
     std::vector<JSeg> segs;
   };
   std::vector<JitGroup> jit;
+  // numEntriesScannedInFilter automaton (pgx_stats.cpp) for filter trees whose statistic has no closed form
+  bool fsm_on = false;
+  FsmPlan fsm;
+  std::vector<int64_t> sorted_span;     // [seg * L + leaf] -> (first << 32 | last) doc of a sorted leaf (0 = empty)
+  std::vector<int64_t> lmask_off;       // [seg] word offset of its leaf masks (-1: no automaton for this segment)
+  std::vector<int64_t> lmask_words;     // [seg] words per leaf
+  uint64_t lmask_total = 0;
+  uint32_t* lmask_dev = nullptr;
+  std::vector<FsmSeg> fsm_segs;
+  int64_t fsm_chunks = 0;
+  DevBuf fsm_table, fsm_segbuf, fsm_cnt, fsm_stv, fsm_pcount, fsm_pstate, lmask_buf;
+  int fsm_T = 1;
 };
 
 bool jit_enabled() {
@@ -1087,6 +1102,56 @@ void plan_star_segment(const pgx_query& q, const pgx_segment& seg, const KSeg& S
   if (terms > 1) { sp.op.push_back(OP_OR); sp.arg.push_back(terms); }
 }
 
+// Does numEntriesScannedInFilter have a closed form the query kernels compute on the fly?  Yes for: no scan leaf at
+// all (0); a root scan leaf or a root OR of leaves (SVScanDocIdIterator.next walks its whole [start, end] range,
+// OrDocIdIterator.next re-targets a child right after each of its matches); a root AND of leaves with at least one
+// sorted / bitmap leaf (AndBlockDocIdSet.fastIterator: each scan's applyAnd tests the running answer -- OP_STAT
+// popcounts -- unless its evaluator is alwaysFalse, SVScanDocIdIterator.java:133-135).  Every other tree goes through
+// the statistics automaton (pgx_stats.cpp).
+bool has_scan_leaf(const PNode& n) {
+  if (n.op == PGX_F_LEAF) return n.phys == PH_SCAN;
+  for (const PNode& k : n.kids)
+    if (has_scan_leaf(k)) return true;
+  return false;
+}
+
+bool binding_empty(const pgx_leaf_binding& b, int card) {
+  if (b.words) {
+    const int nw = (card + 31) / 32;
+    for (int w = 0; w < nw; ++w)
+      if (b.words[w]) return false;
+    return true;
+  }
+  return b.hi < b.lo;
+}
+
+bool stats_closed_form(const PNode& root, const pgx_query& q, pgx_segment* const* segs, int n,
+                       const pgx_leaf_binding* bindings) {
+  if (!has_scan_leaf(root)) return true;
+  if (root.op == PGX_F_LEAF) return true;
+  for (const PNode& k : root.kids)
+    if (k.op != PGX_F_LEAF) return false;
+  if (root.op == PGX_F_OR) return true;
+  bool index = false;
+  for (const PNode& k : root.kids) index |= k.phys == PH_SORTED || k.phys == PH_BITMAP;
+  if (!index) return false;
+  const size_t L = q.leaf_col.size();
+  for (const PNode& k : root.kids)
+    if (k.phys == PH_SCAN)
+      for (int s = 0; s < n; ++s)
+        if (binding_empty(bindings[size_t(s) * L + k.leaf], segs[s]->col(q.leaf_col[k.leaf]).card)) return false;
+  return true;
+}
+
+FsmTreeNode fsm_tree(const PNode& n) {
+  FsmTreeNode t;
+  t.op = n.op == PGX_F_LEAF ? 0 : (n.op == PGX_F_AND ? 1 : 2);
+  t.leaf = n.leaf;
+  t.phys = n.phys;
+  for (const PNode& k : n.kids) t.kids.push_back(fsm_tree(k));
+  return t;
+}
+
 // PGX_HOST_PROFILE=1: sub-phase marks of the planner (appended to the running pgx_execute's profile line).
 thread_local std::function<void(const char*)> g_prof_mark;
 void prof_mark(const char* what) {
@@ -1240,9 +1305,25 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   P.host_entries = 0;
   int host_scan_leaves = 0;
   std::vector<int8_t> pop, parg;
+  PNode froot;
+  P.fsm_on = false;
   if (!q.filter.empty()) {
     PNode root = build_tree(q, *segs[0]);
     emit(root, pop, parg, true, false, host_scan_leaves);
+    if (!stats_closed_form(root, q, segs, n, bindings)) {
+      // the automaton counts every entry: no OP_STAT popcounts, no whole-range host terms
+      P.fsm_on = true;
+      host_scan_leaves = 0;
+      std::vector<int8_t> o2, a2;
+      for (size_t i = 0; i < pop.size(); ++i)
+        if (pop[i] != OP_STAT) {
+          o2.push_back(pop[i]);
+          a2.push_back(parg[i]);
+        }
+      pop.swap(o2);
+      parg.swap(a2);
+      froot = root;
+    }
     P.leaf_phys.assign(q.leaf_col.size(), PH_SCAN);
     std::vector<const PNode*> todo{&root};
     while (!todo.empty()) {
@@ -1270,6 +1351,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   // blob words, pointer fixups and bitmap items with chunk-local offsets, concatenated in segment order afterwards.
   P.ksegs.assign(n, KSeg{});
   P.segcols.assign(n, {});
+  P.sorted_span.assign(size_t(n) * q.leaf_col.size(), 0);
   struct ChunkOut {
     std::vector<int32_t> blob;
     std::vector<ExecPlan::Fix> fixes;
@@ -1334,6 +1416,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
             else { r.push_back(a); r.push_back(e); }
           }
           if (r.empty()) { L.mode = LEAF_NONE; continue; }
+          P.sorted_span[size_t(s) * q.leaf_col.size() + l] = (int64_t(r.front()) << 32) | int64_t(uint32_t(r.back()));
           L.mode = LEAF_RANGES;
           L.nranges = int32_t(r.size() / 2);
           o.fixes.push_back({size_t(s), 1, int(l), o.blob.size()});
@@ -1434,6 +1517,56 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   }
   K.total_tiles = tiles;
   K.num_segs = n;
+  P.lmask_off.assign(n, -1);
+  P.lmask_words.assign(n, 0);
+  P.lmask_total = 0;
+  P.fsm_segs.clear();
+  P.fsm_chunks = 0;
+  if (P.fsm_on) {
+    const int L = int(q.leaf_col.size());
+    std::vector<FsmSegInfo> infos;
+    std::vector<int> fsegs;
+    for (int s = 0; s < n; ++s) {
+      if (!P.star.empty() && P.star[s].on) continue;  // star-tree plans count their own statistic
+      FsmSegInfo si;
+      si.num_docs = P.ksegs[s].num_docs;
+      si.sorted_first.assign(L, 0);
+      si.sorted_last.assign(L, 0);
+      for (int l = 0; l < L; ++l) {
+        const int64_t sp = P.sorted_span[size_t(s) * L + l];
+        if (sp) {
+          si.sorted_first[l] = sp >> 32;
+          si.sorted_last[l] = int32_t(uint32_t(sp));
+        }
+        if (P.ksegs[s].leaf[l].mode == LEAF_NONE && P.leaf_phys[l] == PH_SCAN) si.always_false |= 1u << l;
+      }
+      infos.push_back(std::move(si));
+      fsegs.push_back(s);
+    }
+    std::string err;
+    if (!fsegs.empty() && !fsm_build(fsm_tree(froot), L, infos, P.fsm, &err)) fail(PGX_ERR_UNSUPPORTED, err);
+    for (size_t i = 0; i < fsegs.size(); ++i) {
+      const int s = fsegs[i];
+      const int64_t nd = P.ksegs[s].num_docs;
+      P.lmask_words[s] = (nd + 31) / 32 + 1;
+      P.lmask_off[s] = int64_t(P.lmask_total);
+      P.lmask_total += uint64_t(P.lmask_words[s]) * L;
+      FsmSeg g{};
+      g.words = P.lmask_words[s];
+      g.num_docs = int32_t(nd);
+      g.chunk0 = P.fsm_chunks;
+      P.fsm_chunks += (nd + kFsmChunkRows - 1) / kFsmChunkRows;
+      const auto& iv = P.fsm.seg_intervals[i];
+      if (iv.size() > size_t(kFsmMaxIntervals)) fail(PGX_ERR_INTERNAL, "statistics automaton intervals");
+      g.nint = int32_t(iv.size());
+      for (size_t k = 0; k < iv.size(); ++k) {
+        g.ibeg[k] = iv[k].first;
+        g.itab[k] = iv[k].second;
+      }
+      P.fsm_segs.push_back(g);
+    }
+    if (P.fsm_segs.empty()) P.fsm_on = false;
+  }
   P.rec_base.assign(n, 0);
   P.rec_total = 0;
   for (int s = 0; s < n; ++s) {
@@ -1482,6 +1615,34 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
     if (f.kind == 0) S.remap[f.slot] = base + f.off;
     else if (f.kind == 1) S.leaf[f.slot].ranges = base + f.off;
     else S.leaf[f.slot].bitset = reinterpret_cast<const uint32_t*>(base + f.off);
+  }
+  P.lmask_dev = nullptr;
+  if (P.fsm_on) {
+    const int L = P.fsm.num_leaves, S = P.fsm.num_states;
+    P.lmask_buf = DevBuf(ctx, std::max<uint64_t>(P.lmask_total, 1) * 4);
+    P.lmask_dev = P.lmask_buf.as<uint32_t>();
+    size_t fi = 0;
+    for (size_t s = 0; s < n; ++s) {
+      if (P.lmask_off[s] < 0) continue;
+      P.ksegs[s].lmask = P.lmask_dev + P.lmask_off[s];
+      P.ksegs[s].lmask_words = P.lmask_words[s];
+      P.fsm_segs[fi++].lmask = P.lmask_dev + P.lmask_off[s];
+    }
+    P.fsm_table = DevBuf(ctx, P.fsm.table.size() * 4);
+    hip_check(hipMemcpyAsync(P.fsm_table.p, P.fsm.table.data(), P.fsm.table.size() * 4, hipMemcpyHostToDevice, st),
+              "automaton tables H2D");
+    P.fsm_segbuf = DevBuf(ctx, P.fsm_segs.size() * sizeof(FsmSeg));
+    hip_check(hipMemcpyAsync(P.fsm_segbuf.p, P.fsm_segs.data(), P.fsm_segs.size() * sizeof(FsmSeg),
+                             hipMemcpyHostToDevice, st),
+              "automaton segments H2D");
+    const uint64_t ent = std::max<uint64_t>(uint64_t(P.fsm_chunks) * S, 1);
+    P.fsm_cnt = DevBuf(ctx, ent * 4);
+    P.fsm_stv = DevBuf(ctx, ent * 2);
+    P.fsm_T = std::max(1, std::min(64, 512 / S));
+    const uint64_t pe = uint64_t(P.fsm_segs.size()) * P.fsm_T * S;
+    P.fsm_pcount = DevBuf(ctx, pe * 8);
+    P.fsm_pstate = DevBuf(ctx, pe * 2);
+    (void)L;
   }
   if (n) std::memcpy(B.host.bytes() + B.off_ksegs, P.ksegs.data(), n * sizeof(KSeg));
   P.kq.segs = reinterpret_cast<const KSeg*>(B.dev() + B.off_ksegs);
@@ -1706,6 +1867,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       J.emit_col = P.part_vcol;
     }
     J.dense_slots = P.dense_slots;
+    J.leafmask = P.fsm_on && P.lmask_off[members[0]] >= 0;
 
     ExecPlan::JitGroup G;
     G.T = J.T;
@@ -1722,6 +1884,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       js.tile_begin = tiles;
       js.num_docs = S.num_docs;
       js.rec_base = P.rec_base[s];
+      js.lmask = S.lmask;
+      js.lmask_words = S.lmask_words;
       if (P.star[s].on) {
         // visit only the tiles that intersect a star-tree range: every selected doc lies in one
         auto& tl = P.star_tiles[s];
@@ -1786,6 +1950,15 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
   if (P.jit.empty()) P.jit.push_back(ExecPlan::JitGroup{});  // every segment empty: nothing to launch
 }
 
+void launch_fsm(ExecPlan& P, hipStream_t st) {
+  if (!P.fsm_on) return;
+  hip_check(pgx_launch_fsm(P.fsm_segbuf.as<FsmSeg>(), int(P.fsm_segs.size()), P.fsm_table.as<uint32_t>(),
+                           P.fsm.num_states, P.fsm.num_leaves, P.fsm_chunks, P.fsm_cnt.as<uint32_t>(),
+                           P.fsm_stv.as<uint16_t>(), P.fsm_pcount.as<unsigned long long>(), P.fsm_pstate.as<uint16_t>(),
+                           P.fsm_T, P.kq.stats, st),
+            "statistics automaton launch");
+}
+
 void launch_scan(ExecPlan& P, hipStream_t st) {
   if (!P.jit.empty()) {
     if (P.rdesc_dev && !P.roar_early)
@@ -1801,10 +1974,12 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
                                       nullptr),
                 "query kernel launch");
     }
+    launch_fsm(P, st);
     return;
   }
   if (P.kq.total_tiles == 0) return;
   hip_check(pgx_launch_scan(&P.kq, P.grid, P.tiles_per_wg, P.lds_bytes, st), "scan kernel launch");
+  launch_fsm(P, st);
 }
 
 void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, pgx_segment* const* segs, int n,

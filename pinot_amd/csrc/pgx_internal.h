@@ -35,6 +35,17 @@ struct RDesc {
 
 enum ProgOp : int8_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_STAT = 3, OP_TRUE = 4 };
 
+// Statistics automaton over one segment's leaf masks (pgx_kernels.hip pgx_fsm_chunks / pgx_fsm_compose).
+struct FsmSeg {
+  const uint32_t* lmask;       // leaf l, row r: bit (r & 31) of word [l * words + (r >> 5)]
+  int64_t words;               // words per leaf
+  int32_t num_docs;
+  int32_t nint;                // intervals of constant range position
+  int64_t chunk0;              // first chunk of this segment in the launch
+  int32_t ibeg[3 * 10 + 2];    // interval first rows (ascending, ibeg[0] = 0)
+  int32_t itab[3 * 10 + 2];    // interval transition table
+};
+
 enum AggKind : int8_t { A_COUNT = 0, A_SUM = 1, A_MIN = 2, A_MAX = 3, A_AVG = 4 };
 
 // Accumulator plane ops (pgx.h pgx_query_dense_plane_op)
@@ -61,6 +72,8 @@ struct KSeg {
   const int32_t* remap[kMaxQCols];    // group columns: dictId -> global id (nullptr = identity)
   int8_t bits[kMaxQCols];
   KLeaf leaf[kMaxLeaves];
+  uint32_t* lmask;                    // statistics automaton input: leaf l, row r -> bit (r & 31) of
+  int64_t lmask_words;                // word [l * lmask_words + (r >> 5)] (nullptr: not requested)
 };
 
 struct KQuery {
@@ -146,7 +159,34 @@ struct JitShape {
   std::vector<int> gshift;
   int keybits = 0;
   int emit_col = -1;
+  bool leafmask = false;  // write every leaf's per-row predicate bit (statistics automaton input, pgx_stats.cpp)
 };
+
+// ----- numEntriesScannedInFilter automaton (pgx_stats.cpp builds it, pgx_kernels.hip pgx_fsm_* runs it) -----
+constexpr int kFsmMaxLeaves = 10;                // transition tables are indexed by every leaf's membership bit
+constexpr int kFsmMaxStates = 4096;
+constexpr uint64_t kFsmMaxTable = 1ull << 22;    // u32 entries over all tables
+constexpr int kFsmChunkRows = 1024;              // rows one thread runs from every start state
+constexpr int kFsmMaxIntervals = 3 * kFsmMaxLeaves + 2;
+
+struct FsmTreeNode {             // the physical filter tree after FilterPlanNode.reorder
+  int op = 0;                    // 0 leaf, 1 AND, 2 OR
+  int leaf = -1;
+  int phys = 3;                  // leaf: 0 sorted, 2 bitmap, 3 scan
+  std::vector<FsmTreeNode> kids;
+};
+struct FsmSegInfo {
+  int32_t num_docs = 0;
+  std::vector<int64_t> sorted_first, sorted_last;  // per leaf: first / last doc of a sorted leaf's ranges (0, 0 empty)
+  uint32_t always_false = 0;                       // scan leaves whose predicate evaluator is alwaysFalse
+};
+struct FsmPlan {
+  int num_states = 0, num_leaves = 0, num_tables = 0;
+  std::vector<uint32_t> table;   // [(t * S + q) << L | input] = next_state << 16 | entries counted
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> seg_intervals;  // per segment: (first row, table)
+};
+bool fsm_build(const FsmTreeNode& tree, int num_leaves, const std::vector<FsmSegInfo>& segs, FsmPlan& out,
+               std::string* err);
 
 std::string jit_source(const JitShape& s, int* lds_bytes);
 // Compile (or fetch from the cache) the kernel for shape s on the current device.  Returns the hipFunction_t as void*.

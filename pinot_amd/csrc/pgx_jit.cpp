@@ -350,6 +350,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
           e.ln("u32 p", a, " = 0u;");
       }
     if (emit) e.ln("u64 recs[PR];");
+    if (s.leafmask)
+      for (int l = 0; l < nleaves; ++l) e.ln("u32 lw", l, " = 0u;");
     e.ln("#pragma unroll");
     e.ln("for (int j = 0; j < PR; ++j) {");
     e.ind = 6;
@@ -381,6 +383,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
             e.ln("const bool ", B, " = false;");
             break;
         }
+        if (s.leafmask) e.ln("lw", l, " |= (u32)", B, " << j;");
         st.push_back(B);
       } else if (op == OP_AND || op == OP_OR) {
         for (int k = 1; k < arg; ++k) {
@@ -489,6 +492,14 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
             s.cols[s.agg_col[a]].acc32)
           e.ln("acc", a, " += p", a, ";");
       }
+    if (s.leafmask) {
+      // the lane's PR rows are PR consecutive bits of the leaf's mask (r0 is a multiple of PR, PR divides 32)
+      const char* ty = s.R == 8 ? "unsigned char" : (s.R == 16 ? "unsigned short" : "unsigned int");
+      e.ln("if (FULL || r0 < nd) {");
+      for (int l = 0; l < nleaves; ++l)
+        e.ln("  ((PGX_G ", ty, "*)(S->lmask + ", l, " * S->lmask_words))[r0 / PR] = (", ty, ")lw", l, ";");
+      e.ln("}");
+    }
     if (emit && stg_recs) {
       const int L = stg_recs / s.R;  // lanes whose records fill one round
       int lg = 0;
@@ -624,7 +635,7 @@ std::map<std::pair<int, std::string>, JitEntry> g_jit_cache;
 // source text to find a cached kernel cost ~14 us per query).
 std::vector<int64_t> shape_key(const JitShape& s, int device) {
   std::vector<int64_t> k{device, s.T, s.R, s.group_mode, int64_t(s.dense_slots), s.num_planes, s.keybits, s.emit_col,
-                         int64_t(s.cols.size())};
+                         int64_t(s.cols.size()), s.leafmask};
   for (const JitCol& c : s.cols)
     k.insert(k.end(), {c.bits, c.decode, c.img, c.img_sh, c.img_words, c.acc32, c.fp, c.remap});
   auto add = [&](const auto& v) {
@@ -810,6 +821,18 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.prog_op = {OP_LEAF, OP_LEAF, OP_OR, OP_LEAF, OP_AND};
     s.prog_arg = {0, 1, 2, 2, 2};
     s.R = 16;
+    shapes.push_back(s);
+  }
+  for (int R : {8, 16, 32}) {  // statistics automaton input: every leaf's predicate bits written per lane
+    JitShape s = base(R == 8 ? 8 : (R == 16 ? 10 : 7), 16, IMG_FOR16, 11);
+    s.cols.push_back(JitCol{});
+    s.cols[2].bits = 4;
+    s.leaf_col = {0, 2, 0};
+    s.leaf_mode = {LEAF_SCAN_INTERVAL, LEAF_RANGES, LEAF_DOCMASK_NOT};
+    s.prog_op = {OP_LEAF, OP_LEAF, OP_LEAF, OP_OR, OP_AND};
+    s.prog_arg = {0, 1, 2, 2, 2};
+    s.R = R;
+    s.leafmask = true;
     shapes.push_back(s);
   }
   {  // partitioned group-by records (C3 shape: g1 14 bits, g2 20 bits, value offsets of m)

@@ -27,6 +27,8 @@ struct JSeg {
   long long rec_base;                            // G_EMIT: index of this segment's row 0 in the record array
   const int* tiles;                              // optional: ascending local tile ids to visit (others hold no
                                                  // selected doc, e.g. outside every star-tree node range); 0 = all
+  unsigned int* lmask;                           // statistics automaton: leaf l's predicate bit of row r goes to bit
+  long long lmask_words;                         // (r & 31) of word [l * lmask_words + (r >> 5)]
 };
 
 struct JArgs {

@@ -170,7 +170,9 @@ __device__ __forceinline__ uint32_t run_filter(const KSeg& S, const KQuery& Q, i
     const int op = Q.prog_op[pc];
     const int arg = Q.prog_arg[pc];
     if (op == OP_LEAF) {
-      st.push(leaf_word(S, Q, arg, row0, lane_chunk) & valid);
+      const uint32_t w = leaf_word(S, Q, arg, row0, lane_chunk) & valid;
+      if (S.lmask) S.lmask[arg * S.lmask_words + lane_chunk] = w;  // statistics automaton input
+      st.push(w);
     } else if (op == OP_AND) {
       for (int k = 1; k < arg; ++k) st.fold(true);
     } else if (op == OP_OR) {
@@ -895,6 +897,94 @@ __global__ void pgx_synth_kernel(uint32_t* out_words, int64_t n_rows, int bits, 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// numEntriesScannedInFilter automaton (pgx_stats.cpp): the reference's iterator algebra restated as a finite automaton
+// over each row's leaf-membership bits.  Pass 1: one thread per (1024-row chunk, start state) runs the chunk; pass 2:
+// per segment, the chunk transitions are composed (threads over chunk ranges x start states, then one lane walks the
+// range results from the initial state) and the total is added to stats[1].
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) pgx_fsm_chunks(const FsmSeg* __restrict__ segs, int nsegs,
+                                                      const uint32_t* __restrict__ table, int S, int L,
+                                                      int64_t total_chunks, uint32_t* __restrict__ out_count,
+                                                      uint16_t* __restrict__ out_state) {
+  const int64_t gid = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (gid >= total_chunks * S) return;
+  const int64_t chunk = gid / S;
+  uint32_t state = static_cast<uint32_t>(gid - chunk * S);
+  int lo = 0, hi = nsegs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].chunk0 <= chunk) lo = mid; else hi = mid - 1;
+  }
+  const FsmSeg& G = segs[lo];
+  const int32_t r0 = static_cast<int32_t>((chunk - G.chunk0) * kFsmChunkRows);
+  const int32_t r1 = min(r0 + kFsmChunkRows, G.num_docs);
+  int iv = 0;
+  while (iv + 1 < G.nint && G.ibeg[iv + 1] <= r0) ++iv;
+  int32_t cut = iv + 1 < G.nint ? G.ibeg[iv + 1] : 0x7FFFFFFF;
+  const uint32_t* tab = table + (static_cast<uint64_t>(G.itab[iv]) * S << L);
+  uint32_t count = 0;
+  for (int32_t w = r0 >> 5; (w << 5) < r1; ++w) {
+    uint32_t m[kFsmMaxLeaves];
+#pragma unroll
+    for (int l = 0; l < kFsmMaxLeaves; ++l) m[l] = l < L ? G.lmask[l * G.words + w] : 0u;
+    const int jn = min(32, r1 - (w << 5));
+    for (int j = 0; j < jn; ++j) {
+      const int32_t r = (w << 5) + j;
+      if (r >= cut) {
+        ++iv;
+        cut = iv + 1 < G.nint ? G.ibeg[iv + 1] : 0x7FFFFFFF;
+        tab = table + (static_cast<uint64_t>(G.itab[iv]) * S << L);
+      }
+      uint32_t in = 0;
+#pragma unroll
+      for (int l = 0; l < kFsmMaxLeaves; ++l) in |= ((m[l] >> j) & 1u) << l;
+      const uint32_t e = tab[(static_cast<uint64_t>(state) << L) | in];
+      count += e & 0xFFFFu;
+      state = e >> 16;
+    }
+  }
+  out_count[gid] = count;
+  out_state[gid] = static_cast<uint16_t>(state);
+}
+
+__global__ void __launch_bounds__(256) pgx_fsm_compose(const FsmSeg* __restrict__ segs, int S, int T,
+                                                       const uint32_t* __restrict__ cnt,
+                                                       const uint16_t* __restrict__ stv,
+                                                       unsigned long long* __restrict__ pcount,
+                                                       uint16_t* __restrict__ pstate,
+                                                       unsigned long long* __restrict__ stats) {
+  const FsmSeg& G = segs[blockIdx.x];
+  const int64_t nch = (static_cast<int64_t>(G.num_docs) + kFsmChunkRows - 1) / kFsmChunkRows;
+  const int64_t per = (nch + T - 1) / T;
+  unsigned long long* pc = pcount + static_cast<int64_t>(blockIdx.x) * T * S;
+  uint16_t* ps = pstate + static_cast<int64_t>(blockIdx.x) * T * S;
+  for (int i = threadIdx.x; i < T * S; i += blockDim.x) {
+    const int t = i / S;
+    uint32_t q = static_cast<uint32_t>(i - t * S);
+    unsigned long long c = 0;
+    const int64_t c0 = t * per, c1 = min(nch, c0 + per);
+    for (int64_t ch = c0; ch < c1; ++ch) {
+      const int64_t e = (G.chunk0 + ch) * S + q;
+      c += cnt[e];
+      q = stv[e];
+    }
+    pc[i] = c;
+    ps[i] = static_cast<uint16_t>(q);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long total = 0;
+    uint32_t q = 0;  // the initial state: every iterator idle, the root's first next() pending
+    for (int t = 0; t < T; ++t) {
+      total += pc[t * S + q];
+      q = ps[t * S + q];
+    }
+    if (total) atomicAdd(stats + 1, total);
+  }
+}
+
 }  // namespace pgx
 
 // ---------------------------------------------------------------------------------------------
@@ -1008,5 +1098,20 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
     PGX_AGG_CASE(7, true, true, true)
   }
 #undef PGX_AGG_CASE
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
+                                     int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
+                                     uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream) {
+  const int64_t threads = total_chunks * S;
+  if (threads > 0) {
+    const unsigned grid = static_cast<unsigned>((threads + 255) / 256);
+    hipLaunchKernelGGL(pgx::pgx_fsm_chunks, dim3(grid), dim3(256), 0, stream, segs, nsegs, table, S, L, total_chunks,
+                       cnt, stv);
+  }
+  if (nsegs > 0)
+    hipLaunchKernelGGL(pgx::pgx_fsm_compose, dim3(nsegs), dim3(256), 0, stream, segs, S, T, cnt, stv, pcount, pstate,
+                       stats);
   return hipGetLastError();
 }

@@ -64,3 +64,10 @@ def _close(a, b, rel):
         assert a == b, (a, b)
     else:
         assert abs(a - b) <= rel * max(1.0, abs(b)), (a, b)
+
+
+def literal_entries(osegs, q):
+    """numEntriesScannedInFilter summed over segments, from the oracle's literal iterator algebra."""
+    if not q.get("filter"):
+        return 0
+    return int(sum(O.filter_docs(s, q["filter"])[1] for s in osegs))

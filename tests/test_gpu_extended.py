@@ -70,6 +70,7 @@ def test_extended_functions_match_oracle(env, text):
             H.assert_values_equal([g], [e], [fn])
     st = blk.stats.as_list()
     assert st[0] == exp["stats"][0] and st[2] == exp["stats"][2] and st[3] == exp["stats"][3]
+    assert st[1] == H.literal_entries(osegs, q)
 
 
 GROUPED = [
@@ -107,6 +108,7 @@ def test_extended_functions_group_by_match_oracle(env, text):
         assert set(blk.trimmed[i]) == set(exp["trimmed"][i])
     st = blk.stats.as_list()
     assert st[0] == exp["stats"][0] and st[2] == exp["stats"][2] and st[3] == exp["stats"][3]
+    assert st[1] == H.literal_entries(osegs, q)
 
 
 def test_extended_over_string_column(env):
