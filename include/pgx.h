@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGX_ABI_VERSION 1
+#define PGX_ABI_VERSION 2
 
 typedef enum {
   PGX_OK = 0,
@@ -93,6 +93,9 @@ typedef struct {
   uint64_t dict_len;
   const void* inv;            /* <col>.bitmap.inv (optional, host memory) */
   uint64_t inv_len;
+  int32_t pad_char;           /* STRING padding byte: metadata "segment.padding.character" ('\0'), '%' when the key
+                                 is absent (legacy segments, ColumnMetadata.java:93-98); StringDictionary.get cuts at
+                                 its first occurrence (StringDictionary.java:53-66) */
 } pgx_column_desc;
 
 typedef struct {
@@ -104,6 +107,8 @@ typedef struct {
   const void* star_tree;      /* star-tree.bin in OFF_HEAP format (optional, host memory) */
   uint64_t star_tree_len;
   int32_t mem;                /* pgx_mem_kind of fwd/sorted_pairs/dict */
+  int32_t num_star_skip_dims; /* metadata "star.tree.skip.materialization.for.dimensions": dimensions the star tree */
+  const char* const* star_skip_dims;  /* does not materialise (RequestUtils.isFitForStarTreeIndex:149-163) */
 } pgx_segment_desc;
 
 pgx_status pgx_segment_stage(pgx_ctx* ctx, const pgx_segment_desc* desc, pgx_segment** out);

@@ -663,6 +663,68 @@ class _OrIter:
         return self.cur
 
 
+def intersect_sorted_range_sets(sets: List[List[List[int]]]) -> List[List[int]]:
+    """SortedRangeIntersection.intersectSortedRangeSets (core/util/SortedRangeIntersection.java:31-120), literally:
+    pointer per range set, chase the max head, emit the overlap, merge contiguous results."""
+    if not sets:
+        return []
+    if len(sets) == 1:
+        return [list(p) for p in sets[0]]
+    if any(len(s) == 0 for s in sets):
+        return []
+    cur = [0] * len(sets)
+    max_head, max_idx = -1, -1
+    result: List[List[int]] = []
+    reached_end = False
+    while not reached_end:
+        for i, s in enumerate(sets):
+            head = s[cur[i]][0]
+            if head > max_head:
+                max_head, max_idx = head, i
+        i = 0
+        while i < len(sets):
+            if i == max_idx:
+                i += 1
+                continue
+            found = False
+            restart = False
+            while not found and cur[i] < len(sets[i]):
+                lo, hi = sets[i][cur[i]]
+                if lo <= max_head <= hi:
+                    found = True
+                    break
+                if lo > max_head:
+                    max_head, max_idx = lo, i
+                    restart = True
+                    break
+                cur[i] += 1
+            if restart:
+                i = 0
+                continue
+            if not found:
+                reached_end = True
+                break
+            i += 1
+        if reached_end:
+            break
+        a, b = sets[0][cur[0]]
+        inter = [a, b]
+        for i in range(1, len(sets)):
+            lo, hi = sets[i][cur[i]]
+            inter = [max(inter[0], lo), min(inter[1], hi)]
+        if result and inter[0] == result[-1][1] + 1:
+            result[-1][1] = inter[1]
+        else:
+            result.append(inter)
+        for i in range(len(sets)):
+            if sets[i][cur[i]][1] == inter[1]:
+                cur[i] += 1
+                if cur[i] == len(sets[i]):
+                    reached_end = True
+                    break
+    return result
+
+
 class _AndSet:
     """AndBlockDocIdSet (operator/docidsets/AndBlockDocIdSet.java:49-63,146-266)."""
     kind = "and"
@@ -718,8 +780,8 @@ class _AndSet:
             return _AndIter(its, [_flag(c) for c in self.children])
         if ranges:
             # SortedRangeIntersection.intersectSortedRangeSets (util/SortedRangeIntersection.java:31)
-            sets = [set(r.docs()) for r in ranges]
-            self.answer = set.intersection(*sets) if sets else set()
+            pairs = intersect_sorted_range_sets([r.pairs for r in ranges])
+            self.answer = {d for a, b in pairs for d in range(a, b + 1)}
         for i, b in enumerate(bitmaps):
             if self.answer is None:
                 self.answer = set(b.answer)

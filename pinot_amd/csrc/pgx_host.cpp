@@ -335,6 +335,7 @@ struct StagedColumn {
   std::vector<int64_t> ivals;                      // numeric dictionary values (INT/LONG)
   std::vector<double> dvals;                       // FLOAT/DOUBLE dictionary values
   std::vector<std::string> svals;                  // STRING dictionary values (unpadded)
+  int pad_char = 0;                                // STRING padding byte
   uint64_t dict_hash = 0;
   std::vector<uint8_t> inv;                        // bitmap inverted index bytes (host)
   std::vector<uint32_t> inv_off;                   // (card+1) byte offsets of the per-dictId roaring bitmaps
@@ -361,6 +362,7 @@ struct pgx_segment {
   bool st_ok = false;
   std::vector<StarNode> st_nodes;
   std::vector<std::string> st_dim_name;          // dimension index -> column name
+  std::vector<std::string> st_skip;              // star.tree.skip.materialization.for.dimensions
   uint64_t device_bytes = 0;
 
   const StagedColumn& col(const std::string& n) const {
@@ -483,6 +485,7 @@ void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool
   c.bits = d.bits_per_element;
   c.is_sorted = d.is_sorted != 0;
   c.dict_width = d.dict_width;
+  c.pad_char = d.pad_char & 0xFF;
   if (c.card < 1) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": cardinality < 1");
   if (c.bits < 1 || c.bits > 32) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": bitsPerElement out of [1,32]");
   if (c.card > 1 && (c.bits < 32) && (int64_t(c.card) - 1) >> c.bits)
@@ -510,9 +513,9 @@ void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool
     for (int i = 0; i < c.card; ++i) {
       const char* s = reinterpret_cast<const char*>(dict_host.data()) + size_t(i) * width;
       size_t len = width;
-      // StringDictionary.get: truncate at the first padding char ('\0' default, '%' legacy)
+      // StringDictionary.get: truncate at the first padding char (metadata; '\0' default, '%' legacy)
       for (size_t k = 0; k < size_t(width); ++k)
-        if (s[k] == '\0') { len = k; break; }
+        if (s[k] == char(c.pad_char)) { len = k; break; }
       c.svals[i].assign(s, len);
     }
   } else {
@@ -955,6 +958,15 @@ int qslot(ExecPlan& P, const std::string& name) {
 // only SUM, filter a single predicate or an AND of predicates on distinct star-tree dimensions.
 bool star_fit(const pgx_query& q, const pgx_segment& seg) {
   if (!seg.st_ok || (q.flags & PGX_Q_NO_STAR_TREE) || q.agg_fn.empty()) return false;
+  // group-by and predicate columns must be materialised (:149-163, :195-198, :209-211): a skipped dimension holds the
+  // star value in every aggregated doc, so only a raw scan answers for it
+  auto skipped = [&](const std::string& c) {
+    return std::find(seg.st_skip.begin(), seg.st_skip.end(), c) != seg.st_skip.end();
+  };
+  for (const auto& g : q.group_cols)
+    if (skipped(g)) return false;
+  for (const auto& c : q.leaf_col)
+    if (skipped(c)) return false;
   for (int fn : q.agg_fn)
     if (fn != PGX_SUM) return false;
   const size_t nl = q.leaf_col.size();
@@ -2571,6 +2583,8 @@ pgx_status pgx_segment_stage(pgx_ctx* ctx, const pgx_segment_desc* d, pgx_segmen
       stage_column(ctx, seg.get(), d->columns[i], d->mem == PGX_MEM_DEVICE, seg->cols[i]);
       seg->by_name[seg->cols[i].name] = i;
     }
+    for (int i = 0; i < d->num_star_skip_dims; ++i)
+      if (d->star_skip_dims && d->star_skip_dims[i]) seg->st_skip.emplace_back(d->star_skip_dims[i]);
     if (d->star_tree && d->star_tree_len) {
       const uint8_t* p = static_cast<const uint8_t*>(d->star_tree);
       seg->star_tree.assign(p, p + d->star_tree_len);

@@ -118,6 +118,15 @@ class _ColInfo:
         return _java_double_str(float(v))
 
 
+STAR_SKIP_KEY = "star.tree.skip.materialization.for.dimensions"  # V1Constants.MetadataKeys.StarTree (:104-105)
+
+
+def star_skip_dims(seg: SegmentData):
+    """SegmentMetadataImpl reads the skip list as a PropertiesConfiguration list (comma separated, :345-355)."""
+    v = (seg.metadata or {}).get(STAR_SKIP_KEY, "")
+    return [x.strip() for x in v.split(",") if x.strip()]
+
+
 class IndexSegment:
     """A segment staged into HBM (Loaders.IndexSegment.load equivalent)."""
 
@@ -138,6 +147,7 @@ class IndexSegment:
             d.bits_per_element = c.bits
             d.is_sorted = int(c.is_sorted)
             d.dict_width = c.dict_width
+            d.pad_char = ord(c.pad_char) if c.data_type == "STRING" else 0
             for attr, data in (("fwd", c.fwd_bytes), ("sorted_pairs", c.sorted_bytes), ("dict", c.dict_bytes),
                                ("inv", c.inv_bytes)):
                 if data is None:
@@ -162,6 +172,12 @@ class IndexSegment:
             sd.star_tree = C.cast(st, C.c_void_p)
             sd.star_tree_len = len(seg.star_tree)
         sd.mem = N.PGX_MEM_HOST
+        skip = star_skip_dims(seg)
+        if skip:
+            arr = (C.c_char_p * len(skip))(*[x.encode() for x in skip])
+            keep.append(arr)
+            sd.num_star_skip_dims = len(skip)
+            sd.star_skip_dims = arr
         h = C.c_void_p()
         N.check(N.lib().pgx_segment_stage(ctx.handle, C.byref(sd), C.byref(h)))
         self.handle = h

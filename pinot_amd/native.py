@@ -36,13 +36,15 @@ class ColumnDesc(C.Structure):
     _fields_ = [("name", C.c_char_p), ("data_type", C.c_int32), ("cardinality", C.c_int32),
                 ("bits_per_element", C.c_int32), ("is_sorted", C.c_int32), ("dict_width", C.c_int32),
                 ("fwd", C.c_void_p), ("fwd_len", C.c_uint64), ("sorted_pairs", C.c_void_p), ("sorted_len", C.c_uint64),
-                ("dict", C.c_void_p), ("dict_len", C.c_uint64), ("inv", C.c_void_p), ("inv_len", C.c_uint64)]
+                ("dict", C.c_void_p), ("dict_len", C.c_uint64), ("inv", C.c_void_p), ("inv_len", C.c_uint64),
+                ("pad_char", C.c_int32)]
 
 
 class SegmentDesc(C.Structure):
     _fields_ = [("name", C.c_char_p), ("total_docs", C.c_int32), ("total_raw_docs", C.c_int32),
                 ("num_columns", C.c_int32), ("columns", C.POINTER(ColumnDesc)), ("star_tree", C.c_void_p),
-                ("star_tree_len", C.c_uint64), ("mem", C.c_int32)]
+                ("star_tree_len", C.c_uint64), ("mem", C.c_int32), ("num_star_skip_dims", C.c_int32),
+                ("star_skip_dims", C.POINTER(C.c_char_p))]
 
 
 class Agg(C.Structure):

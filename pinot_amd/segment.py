@@ -26,6 +26,36 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 
 DEFAULT_PAD = "\0"  # V1Constants.Str.DEFAULT_STRING_PAD_CHAR (segment/creator/impl/V1Constants.java:51)
+LEGACY_PAD = "%"    # V1Constants.Str.LEGACY_STRING_PAD_CHAR (:52): segments whose metadata has no padding key
+PAD_KEY = "segment.padding.character"  # V1Constants.MetadataKeys.Segment.SEGMENT_PADDING_CHARACTER (:127)
+
+
+def java_escape(ch: str) -> str:
+    """StringEscapeUtils.escapeJava of one char, as SegmentColumnarIndexCreator writes the padding key (:216-217)."""
+    if ch == "\\":
+        return "\\\\"
+    if " " <= ch <= "~":
+        return ch
+    return "\\u%04X" % ord(ch)
+
+
+def java_unescape(s: str) -> str:
+    """StringEscapeUtils.unescapeJava (ColumnMetadata.java:93-98 takes charAt(0) of the result)."""
+    out, i = [], 0
+    while i < len(s):
+        c = s[i]
+        if c == "\\" and i + 1 < len(s):
+            n = s[i + 1]
+            if n == "u" and i + 6 <= len(s):
+                out.append(chr(int(s[i + 2:i + 6], 16)))
+                i += 6
+                continue
+            out.append({"t": "\t", "n": "\n", "r": "\r", "0": "\0", "\\": "\\"}.get(n, n))
+            i += 2
+            continue
+        out.append(c)
+        i += 1
+    return "".join(out)
 ROARING_COOKIE_NO_RUN = 12346
 DTYPES = ("INT", "LONG", "FLOAT", "DOUBLE", "STRING")
 _DICT_NP = {"INT": ">i4", "LONG": ">i8", "FLOAT": ">f4", "DOUBLE": ">f8"}
@@ -273,6 +303,10 @@ def write_segment(seg: SegmentData, out_dir: str) -> str:
              "segment.total.docs = %d" % seg.total_docs]
     if seg.star_tree is not None:
         lines.append("startree.enabled = true")
+    pads = {c.pad_char for c in seg.columns.values() if c.data_type == "STRING"} or {DEFAULT_PAD}
+    assert len(pads) == 1, "one padding character per segment"
+    if PAD_KEY not in seg.metadata:
+        lines.append("%s = %s" % (PAD_KEY, java_escape(pads.pop()).replace("\\", "\\\\")))
     for k, v in seg.metadata.items():
         lines.append("%s = %s" % (k, v))
     for c in seg.columns.values():
@@ -306,13 +340,15 @@ def write_segment(seg: SegmentData, out_dir: str) -> str:
 
 
 def _read_props(path):
+    """metadata.properties as commons-configuration PropertiesConfiguration reads it: `key = value`, with the file's
+    backslash escapes undone (the padding key is written as \\\\u0000, read back as the 6-char string \\u0000)."""
     props = {}
     for line in open(path, encoding="utf-8"):
         line = line.rstrip("\n")
         if not line or line.startswith("#") or "=" not in line:
             continue
         k, v = line.split("=", 1)
-        props[k.strip()] = v.strip()
+        props[k.strip()] = v.strip().replace("\\\\", "\\")
     return props
 
 
@@ -335,7 +371,7 @@ def load_segment(seg_dir: str) -> SegmentData:
         card = int(g("cardinality"))
         width = int(g("lengthOfEachEntry", "0")) if dt == "STRING" else int(_DICT_NP[dt][-1])
         is_sorted = g("isSorted") == "true"
-        pad = DEFAULT_PAD
+        pad = java_unescape(props[PAD_KEY])[0] if PAD_KEY in props else LEGACY_PAD
 
         def rd(suffix):
             f = os.path.join(seg_dir, c + suffix)
@@ -344,10 +380,6 @@ def load_segment(seg_dir: str) -> SegmentData:
         col = Column(c, dt, g("columnType"), card, int(g("bitsPerElement")), int(g("totalDocs")),
                      int(g("totalRawDocs", g("totalDocs"))), is_sorted, g("hasInvertedIndex") == "true",
                      rd(".dict"), width, rd(".sv.unsorted.fwd"), rd(".sv.sorted.fwd"), rd(".bitmap.inv"), pad)
-        if dt == "STRING":
-            # Legacy segments pad with '%' (V1Constants.Str.LEGACY_STRING_PAD_CHAR); detect from the dictionary bytes.
-            if b"\0" not in col.dict_bytes and b"%" in col.dict_bytes:
-                col.pad_char = "%"
         seg.columns[c] = col
     st = os.path.join(seg_dir, "star-tree.bin")
     if os.path.exists(st):

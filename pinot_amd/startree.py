@@ -29,6 +29,9 @@ ALL = -1
 MAGIC = 0xBADDA55B00DAD00D
 VERSION = 1
 DEFAULT_MAX_LEAF_RECORDS = 100000  # common/data/StarTreeIndexSpec.java:25-26
+DEFAULT_SKIP_MATERIALIZATION_CARDINALITY = 10000  # StarTreeIndexSpec.DEFAULT_SKIP_MATERIALIZATION_CARDINALITY_THRESHOLD
+SKIP_KEY = "star.tree.skip.materialization.for.dimensions"  # V1Constants.MetadataKeys.StarTree (:104-107)
+SKIP_CARD_KEY = "star.tree.skip.materialization.cardinality"
 INT_DEFAULT_NULL = -(1 << 31)      # FieldSpec default null for INT dimensions = the star value (:210-225)
 
 
@@ -74,12 +77,20 @@ def _lexsort(d: np.ndarray, order: Sequence[int]) -> np.ndarray:
 
 
 def build(dim_ids: np.ndarray, metrics: np.ndarray, cards: Sequence[int], max_leaf_records: int = DEFAULT_MAX_LEAF_RECORDS,
-          split_order: Optional[Sequence[int]] = None):
+          split_order: Optional[Sequence[int]] = None, skip: Optional[Sequence[int]] = None,
+          skip_cardinality: int = DEFAULT_SKIP_MATERIALIZATION_CARDINALITY):
     """dim_ids: (N, D) int dictIds (no star values); metrics: (N, M) int64.
-    Returns (tree_root, all_dims (T, D) with ALL=-1 for star, all_metrics (T, M), split_order, num_raw)."""
+    Returns (tree_root, all_dims (T, D) with ALL=-1 for star, all_metrics (T, M), split_order, num_raw, skip).
+
+    skipMaterializationForDimensions (OffHeapStarTreeBuilder.build :308-322): by default every dimension whose
+    cardinality exceeds the threshold (computeDefaultDimensionsToSkipMaterialization :557-565); they leave the default
+    split order, and the star-node rows hold ALL for them (uniqueCombinations :738-745)."""
     n, ndim = dim_ids.shape
+    skip = set(skip) if skip else {k for k in range(ndim) if cards[k] > skip_cardinality}
     if split_order is None:
-        split_order = sorted(range(ndim), key=lambda k: -cards[k])  # stable: ties keep schema order
+        split_order = [k for k in sorted(range(ndim), key=lambda k: -cards[k]) if k not in skip]  # stable
+    else:
+        skip -= set(split_order)
     sort_order = list(split_order) + [k for k in range(ndim) if k not in split_order]
     perm = _lexsort(dim_ids, sort_order)
     tab = _Table(np.ascontiguousarray(dim_ids[perm]).astype(np.int32), np.ascontiguousarray(metrics[perm]).astype(np.int64))
@@ -89,6 +100,8 @@ def build(dim_ids: np.ndarray, metrics: np.ndarray, cards: Sequence[int], max_le
         d, m = tab.rows(a, b)
         d = d.copy()
         d[:, split_dim] = ALL
+        for k in skip:
+            d[:, k] = ALL
         o = _lexsort(d, sort_order)
         d, m = d[o], m[o]
         if len(d) == 0:
@@ -153,7 +166,7 @@ def build(dim_ids: np.ndarray, metrics: np.ndarray, cards: Sequence[int], max_le
 
     agg_docs(root)
     all_d, all_m = tab.all()
-    return root, all_d, all_m, list(split_order), n
+    return root, all_d, all_m, list(split_order), n, sorted(skip)
 
 
 def serialize(root: Node, dim_names: Sequence[str]) -> bytes:
@@ -197,7 +210,9 @@ def parse(buf: bytes):
 
 
 def make_star_tree_segment(name: str, dims: Dict[str, np.ndarray], metrics: Dict[str, np.ndarray],
-                           max_leaf_records: int = DEFAULT_MAX_LEAF_RECORDS, inverted: Sequence[str] = ()):
+                           max_leaf_records: int = DEFAULT_MAX_LEAF_RECORDS, inverted: Sequence[str] = (),
+                           skip_materialization: Optional[Sequence[str]] = None,
+                           skip_cardinality: int = DEFAULT_SKIP_MATERIALIZATION_CARDINALITY):
     """Build a v1 star-tree segment from raw INT dimension and metric values (SegmentIndexCreationDriverImpl.buildStarTree,
     :193-289): docs = raw docs in star-tree order, then the aggregated docs; star dimension values are the INT default
     null (Integer.MIN_VALUE), which therefore sits in every dimension dictionary."""
@@ -213,7 +228,9 @@ def make_star_tree_segment(name: str, dims: Dict[str, np.ndarray], metrics: Dict
     dim_ids = np.stack(ids, axis=1)
     mets = np.stack([np.asarray(metrics[k], dtype=np.int64) for k in mnames], axis=1)
     cards = [len(np.unique(dim_ids[:, i])) for i in range(len(dnames))]
-    root, all_d, all_m, order, nraw = build(dim_ids, mets, cards, max_leaf_records)
+    skip_idx = [dnames.index(k) for k in skip_materialization] if skip_materialization else None
+    root, all_d, all_m, order, nraw, skipped = build(dim_ids, mets, cards, max_leaf_records, skip=skip_idx,
+                                                     skip_cardinality=skip_cardinality)
     total = len(all_d)
     cols = []
     for i, k in enumerate(dnames):
@@ -233,4 +250,7 @@ def make_star_tree_segment(name: str, dims: Dict[str, np.ndarray], metrics: Dict
     seg.star_tree = serialize(root, dnames)
     seg.metadata["startree.split.order"] = ",".join(dnames[k] for k in order)
     seg.metadata["startree.maxLeafRecords"] = str(max_leaf_records)
+    seg.metadata[SKIP_CARD_KEY] = str(skip_cardinality)
+    if skipped:
+        seg.metadata[SKIP_KEY] = ",".join(dnames[k] for k in skipped)
     return seg

@@ -223,7 +223,26 @@ def main():
     with open(os.path.join(OUT, "expected_sv_queries.json"), "w") as f:
         json.dump(EXPECTED, f, indent=1, sort_keys=True)
     shutil.copy(os.path.join(REF, "starTreeSegment.tar.gz"), os.path.join(OUT, "starTreeSegment.tar.gz"))
+    for name in ("paddingOld", "paddingPercent", "paddingNull"):  # LoadersTest.testPadding fixtures (data files)
+        shutil.copy(os.path.join(REF, name + ".tar.gz"), os.path.join(OUT, name + ".tar.gz"))
+    make_sorted_range_vectors()
     print("wrote fixtures to", OUT)
+
+
+def make_sorted_range_vectors():
+    """The fixed range sets of SortedRangeIntersectionTest.testSimple / testComplex (:45-80), as JSON data."""
+    import re
+    src = open(os.path.join(REF, "..", "..", "java", "com", "linkedin", "pinot", "core", "util",
+                            "SortedRangeIntersectionTest.java")).read()
+    body = re.search(r"public void testComplex\(\)(.*?)\n  }\n", src, re.S).group(1)
+    lit = lambda decl: json.loads("".join(re.findall(r'"(.*?)"', decl, re.S)))
+    sets = [lit(x) for x in re.findall(r'String rangeSet\d = (".*?");', body, re.S)]
+    exp = lit(re.search(r'String expectedOutputRangeSet = (".*?");', body, re.S).group(1))
+    out = {"source": "pinot-core/src/test/java/com/linkedin/pinot/core/util/SortedRangeIntersectionTest.java:45-80",
+           "simple": {"sets": [[[0, 4], [6, 10]], [[4, 7], [8, 14]]], "expected": [[4, 4], [6, 10]]},
+           "complex": {"sets": sets, "expected": exp}}
+    with open(os.path.join(OUT, "sorted_range_intersection.json"), "w") as f:
+        json.dump(out, f)
 
 
 if __name__ == "__main__":

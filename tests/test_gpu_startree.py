@@ -68,3 +68,36 @@ def test_star_tree_query(ctx, staged, text):
     assert st[0] == len(docs)
     assert st_raw[0] == len(raw_docs)
     assert st[3] == st_raw[3] == seg.total_raw_docs
+
+
+@pytest.fixture(scope="module")
+def staged_skip(ctx):
+    """d4 skipped for materialization (OffHeapStarTreeBuilder: cardinality above the threshold): the star-node rows and
+    every aggregated doc hold the star value for it, so RequestUtils.isFitForStarTreeIndex (:149-163, :195-198)
+    sends a query grouping or filtering on d4 to the raw docs."""
+    from pinot_amd import engine as E
+    dims, mets = make_raw(30000, seed=11)
+    seg = ST.make_star_tree_segment("stskip", dims, mets, max_leaf_records=300, skip_cardinality=20)
+    assert seg.metadata[ST.SKIP_KEY] == "d4"
+    return E.IndexSegment(ctx, seg), seg, oseg_of(seg)
+
+
+@pytest.mark.parametrize("text", [
+    "select sum(m1), sum(m2) from T group by d4",
+    "select sum(m1), sum(m2) from T where d4 in (3, 7, 11) group by d1",
+    "select sum(m1), sum(m2) from T where d4 = 5",
+    "select sum(m1), sum(m2) from T where d1 = 2 group by d2",  # fits: served from the star tree
+])
+def test_star_tree_skipped_dimension(ctx, staged_skip, text):
+    gseg, seg, os_ = staged_skip
+    q = pql.compile(text)
+    blk, st = _run(ctx, gseg, q)
+    gcols = q["group_by"]["columns"] if q.get("group_by") else []
+    raw_docs = np.nonzero(O.filter_mask_vectorized(os_, q.get("filter")))[0]
+    exp = O.sum_by_group(os_, raw_docs, METRICS, gcols)
+    assert {k: [float(x) for x in v] for k, v in _as_map(blk, q).items()} == exp
+    uses_d4 = "d4" in text
+    if uses_d4:
+        assert st[0] == len(raw_docs)  # raw scan
+    else:
+        assert st[0] == len(O.star_tree_docs(os_, seg.star_tree, q, seg.total_raw_docs))

@@ -111,3 +111,24 @@ def test_star_tree_docs_sum_equals_raw_scan(star_seg, text):
     assert got == exp
     if not q.get("filter") and not gcols:
         assert len(docs) == 1  # the root's aggregated doc
+
+
+def test_skip_materialization_dimension():
+    """OffHeapStarTreeBuilder skipMaterializationForDimensions (:308-322, :738-745): a dimension above the cardinality
+    threshold leaves the split order and holds ALL in every star-node row and aggregated doc."""
+    dims, mets = make_raw(6000, seed=5)
+    seg = ST.make_star_tree_segment("sk", dims, mets, max_leaf_records=100, skip_cardinality=20)
+    assert seg.metadata[ST.SKIP_KEY] == "d4"
+    assert "d4" not in seg.metadata["startree.split.order"].split(",")
+    names, nodes = ST.parse(seg.star_tree)
+    assert all(names[int(x[0])] != "d4" for x in nodes[1:])
+    d4 = seg.columns["d4"]
+    ids = d4.dict_ids()
+    assert np.all(ids[seg.total_raw_docs:] == 0)  # dictId 0 = Integer.MIN_VALUE, the star value
+    # star-tree sums still equal raw sums for queries that do not touch d4
+    os_ = oseg_of(seg)
+    for text in QUERIES[:6]:
+        q = pql.compile(text)
+        raw_docs = np.nonzero(O.filter_mask_vectorized(os_, q.get("filter")))[0]
+        docs = O.star_tree_docs(os_, seg.star_tree, q, seg.total_raw_docs)
+        assert O.sum_by_group(os_, docs, METRICS, []) == O.sum_by_group(os_, raw_docs, METRICS, [])
