@@ -18,11 +18,16 @@ class PgoCol(C.Structure):
 
 class PgoSegQuery(C.Structure):
     _fields_ = [("num_docs", C.c_int32), ("num_cols", C.c_int32), ("cols", C.POINTER(PgoCol)),
-                ("filter_col", C.c_int32), ("lo", C.c_int32), ("hi", C.c_int32), ("metric_col", C.c_int32),
+                ("filter_col", C.c_int32), ("lo", C.c_int32), ("hi", C.c_int32),
+                ("num_leaves", C.c_int32), ("leaf_col", C.POINTER(C.c_int32)),
+                ("leaf_bits", C.POINTER(C.POINTER(C.c_uint32))), ("prog_len", C.c_int32),
+                ("prog", C.POINTER(C.c_int32)), ("metric_col", C.c_int32),
                 ("num_group_cols", C.c_int32), ("group_cols", C.POINTER(C.c_int32)),
-                ("count", C.c_int64), ("sum", C.c_double), ("entries_scanned", C.c_int64),
+                ("count", C.c_int64), ("sum", C.c_double), ("vmin", C.c_double), ("vmax", C.c_double),
+                ("entries_scanned", C.c_int64),
                 ("num_groups", C.c_int64), ("g_keys", C.POINTER(C.c_int64)), ("g_sums", C.POINTER(C.c_double)),
-                ("g_counts", C.POINTER(C.c_int64)), ("g_cap", C.c_int64)]
+                ("g_counts", C.POINTER(C.c_int64)), ("g_mins", C.POINTER(C.c_double)),
+                ("g_maxs", C.POINTER(C.c_double)), ("g_cap", C.c_int64)]
 
 
 def lib():
@@ -32,6 +37,8 @@ def lib():
             subprocess.check_call(["make", "-C", _HERE])
         L = C.CDLL(_LIB)
         L.pgo_synth_fwd.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_uint32, C.c_void_p, C.c_int64]
+        L.pgo_synth_fwd_paired.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_uint32, C.c_void_p, C.c_int64,
+                                           C.c_uint64, C.c_uint32]
         L.pgo_synth_value.argtypes = [C.c_uint64, C.c_int64, C.c_uint32]
         L.pgo_synth_value.restype = C.c_uint32
         L.pgo_run.argtypes = [C.POINTER(PgoSegQuery), C.c_int, C.c_int]
@@ -43,12 +50,19 @@ def lib():
     return _lib
 
 
-def synth_fwd(seed, n, bits, card):
-    """Packed fixed-bit forward index of synthetic dictIds (bit-identical to libpgx's pgx_synth_column)."""
+def synth_fwd(seed, n, bits, card, pair_seed=0, npairs=0):
+    """Packed fixed-bit forward index of synthetic dictIds (bit-identical to libpgx's pgx_synth_column, and with
+    npairs > 0 to pgx_synth_column_paired)."""
     nbytes = (n * bits + 7) // 8 + 8
     out = np.zeros(nbytes, dtype=np.uint8)
-    lib().pgo_synth_fwd(seed, n, bits, card, out.ctypes.data, nbytes)
+    lib().pgo_synth_fwd_paired(seed, n, bits, card, out.ctypes.data, nbytes, pair_seed, npairs)
     return out
+
+
+def dict_ids(fwd, n, bits):
+    """Decode a packed forward index (numpy, MSB-first big-endian; oracle decode_fixed_bit_fast)."""
+    from oracle import pinot_oracle as O
+    return O.decode_fixed_bit_fast(bytes(fwd), n, bits)
 
 
 class Segment:
@@ -60,7 +74,9 @@ class Segment:
         self.columns = columns
 
 
-def run(segments, filter_col=None, lo=0, hi=-1, metric="m", group_cols=(), threads=1, collect_groups=False):
+def run(segments, filter_col=None, lo=0, hi=-1, metric="m", group_cols=(), threads=1, collect_groups=False,
+        leaves=None, prog=None):
+    """leaves = [(column, dictId bitset uint32 array)], prog = postfix ints (>= 0 leaf, -1 AND, -2 OR)."""
     L = lib()
     qs = (PgoSegQuery * len(segments))()
     keep = []
@@ -81,27 +97,40 @@ def run(segments, filter_col=None, lo=0, hi=-1, metric="m", group_cols=(), threa
         q.cols = cols
         q.filter_col = s.names.index(filter_col) if filter_col else -1
         q.lo, q.hi = lo, hi
+        if leaves:
+            lc = (C.c_int32 * len(leaves))(*[s.names.index(c) for c, _ in leaves])
+            bits = [np.ascontiguousarray(b, dtype=np.uint32) for _, b in leaves]
+            lb = (C.POINTER(C.c_uint32) * len(leaves))(*[b.ctypes.data_as(C.POINTER(C.c_uint32)) for b in bits])
+            pg = (C.c_int32 * len(prog))(*prog)
+            keep += [lc, bits, lb, pg]
+            q.num_leaves = len(leaves)
+            q.leaf_col = lc
+            q.leaf_bits = lb
+            q.prog_len = len(prog)
+            q.prog = pg
         q.metric_col = s.names.index(metric)
         q.num_group_cols = len(group_cols)
         q.group_cols = gc
         if collect_groups:
             cap = s.num_docs
-            arrs = (np.zeros(cap, np.int64), np.zeros(cap, np.float64), np.zeros(cap, np.int64))
+            arrs = (np.zeros(cap, np.int64), np.zeros(cap, np.float64), np.zeros(cap, np.int64),
+                    np.zeros(cap, np.float64), np.zeros(cap, np.float64))
             keep.append(arrs)
             q.g_keys = arrs[0].ctypes.data_as(C.POINTER(C.c_int64))
             q.g_sums = arrs[1].ctypes.data_as(C.POINTER(C.c_double))
             q.g_counts = arrs[2].ctypes.data_as(C.POINTER(C.c_int64))
+            q.g_mins = arrs[3].ctypes.data_as(C.POINTER(C.c_double))
+            q.g_maxs = arrs[4].ctypes.data_as(C.POINTER(C.c_double))
             q.g_cap = cap
     L.pgo_run(qs, len(segments), threads)
     out = []
     for i in range(len(segments)):
         q = qs[i]
-        r = {"count": q.count, "sum": q.sum, "entries": q.entries_scanned, "num_groups": q.num_groups}
+        r = {"count": q.count, "sum": q.sum, "min": q.vmin, "max": q.vmax, "entries": q.entries_scanned,
+             "num_groups": q.num_groups}
         if collect_groups:
             ng = q.num_groups
-            arrs = keep[-len(segments) + i] if False else None
-            r["groups"] = (np.ctypeslib.as_array(q.g_keys, shape=(ng,)).copy(),
-                           np.ctypeslib.as_array(q.g_sums, shape=(ng,)).copy(),
-                           np.ctypeslib.as_array(q.g_counts, shape=(ng,)).copy())
+            r["groups"] = tuple(np.ctypeslib.as_array(p, shape=(ng,)).copy()
+                                for p in (q.g_keys, q.g_sums, q.g_counts, q.g_mins, q.g_maxs))
         out.append(r)
     return out

@@ -41,15 +41,22 @@ uint32_t pgo_synth_value(uint64_t seed, int64_t row, uint32_t card) {
   return (uint32_t)(splitmix64(seed ^ ((uint64_t)row * 0x9E3779B97F4A7C15ull)) % card);
 }
 
-/* Fixed-bit writer (io/writer/impl/FixedBitSingleValueMultiColWriter.java:86-130): MSB-first, big-endian. */
-void pgo_synth_fwd(uint64_t seed, int64_t n, int bits, uint32_t card, uint8_t* out, int64_t out_len) {
+/* Fixed-bit writer (io/writer/impl/FixedBitSingleValueMultiColWriter.java:86-130): MSB-first, big-endian.
+   npairs > 0: the row's value is a function of a pair index drawn from pair_seed (libpgx pgx_synth_column_paired). */
+void pgo_synth_fwd_paired(uint64_t seed, int64_t n, int bits, uint32_t card, uint8_t* out, int64_t out_len,
+                          uint64_t pair_seed, uint32_t npairs) {
   memset(out, 0, (size_t)out_len);
   for (int64_t r = 0; r < n; ++r) {
-    uint32_t v = pgo_synth_value(seed, r, card);
+    const int64_t src = npairs ? (int64_t)pgo_synth_value(pair_seed, r, npairs) : r;
+    uint32_t v = pgo_synth_value(seed, src, card);
     int64_t bit = r * bits;
     for (int k = bits - 1; k >= 0; --k, ++bit)
       if ((v >> k) & 1u) out[bit >> 3] |= (uint8_t)(0x80u >> (bit & 7));
   }
+}
+
+void pgo_synth_fwd(uint64_t seed, int64_t n, int bits, uint32_t card, uint8_t* out, int64_t out_len) {
+  pgo_synth_fwd_paired(seed, n, bits, card, out, out_len, 0, 0);
 }
 
 /* PinotDataCustomBitSet.readInt (util/PinotDataCustomBitSet.java:122-155), literal. */
@@ -97,20 +104,48 @@ typedef struct {
   const pgo_col* cols;
   /* filter: scan leaf on column filter_col, dictId in [lo, hi]; filter_col < 0 = match all */
   int32_t filter_col, lo, hi;
-  int32_t metric_col;       /* SUM(metric) */
+  /* or, when num_leaves > 0: a postfix program over leaves (prog[i] >= 0: leaf; -1: AND; -2: OR of the top two),
+     leaf l matching a row iff the row's dictId of column leaf_col[l] has its bit set in leaf_bits[l] (the dictId
+     sets the reference's predicate evaluators resolve, evaluated per row) */
+  int32_t num_leaves;
+  const int32_t* leaf_col;
+  const uint32_t* const* leaf_bits;
+  int32_t prog_len;
+  const int32_t* prog;
+  int32_t metric_col;       /* SUM / MIN / MAX (metric) */
   int32_t num_group_cols;   /* 0 = aggregation only */
   const int32_t* group_cols;
   /* outputs */
   int64_t count;
-  double sum;
+  double sum, vmin, vmax;
   int64_t entries_scanned;
   /* group-by output: dense table (if card product small) or hash map */
   int64_t num_groups;
   int64_t* g_keys;
   double* g_sums;
   int64_t* g_counts;
+  double* g_mins;           /* optional, MIN / MAX per group (+inf / -inf defaults, MinAggregationFunction) */
+  double* g_maxs;
   int64_t g_cap;
 } pgo_segment_query;
+
+static int row_matches(const pgo_segment_query* q, int64_t d) {
+  int stack[32];
+  int sp = 0;
+  for (int i = 0; i < q->prog_len; ++i) {
+    const int op = q->prog[i];
+    if (op >= 0) {
+      const int32_t id = read_int(q->cols[q->leaf_col[op]].fwd, q->cols[q->leaf_col[op]].nbytes,
+                                  d * q->cols[q->leaf_col[op]].bits,
+                                  d * q->cols[q->leaf_col[op]].bits + q->cols[q->leaf_col[op]].bits);
+      stack[sp++] = (q->leaf_bits[op][id >> 5] >> (id & 31)) & 1u;
+    } else {
+      const int b = stack[--sp], a = stack[--sp];
+      stack[sp++] = op == -1 ? (a & b) : (a | b);
+    }
+  }
+  return sp ? stack[0] : 1;
+}
 
 static inline int32_t col_id(const pgo_col* c, int64_t row) {
   return read_int(c->fwd, c->nbytes, row * c->bits, row * c->bits + c->bits);
@@ -180,7 +215,7 @@ static void run_segment(pgo_segment_query* q) {
   int32_t* gkeys = (int32_t*)malloc(sizeof(int32_t) * block);
   const pgo_col* fc = q->filter_col >= 0 ? &q->cols[q->filter_col] : NULL;
   const pgo_col* mc = &q->cols[q->metric_col];
-  double holder = 0.0;
+  double holder = 0.0, vmin = 1.0 / 0.0, vmax = -1.0 / 0.0;
   int64_t count = 0, scanned = 0;
   int64_t next = 0;
   /* group-by state */
@@ -194,6 +229,7 @@ static void run_segment(pgo_segment_query* q) {
   const int array_based = q->num_group_cols && !overflow && prod <= 10000;
   double* dsum = NULL;
   int64_t* dcnt = NULL;
+  double *dmin = NULL, *dmax = NULL, *mmin = NULL, *mmax = NULL;
   lmap map = {0};
   double* msum = NULL;
   int64_t* mcnt = NULL;
@@ -202,11 +238,17 @@ static void run_segment(pgo_segment_query* q) {
     if (array_based) {
       dsum = (double*)calloc((size_t)prod, sizeof(double));
       dcnt = (int64_t*)calloc((size_t)prod, sizeof(int64_t));
+      dmin = (double*)malloc(sizeof(double) * (size_t)prod);
+      dmax = (double*)malloc(sizeof(double) * (size_t)prod);
+      for (int64_t k = 0; k < prod; ++k) { dmin[k] = 1.0 / 0.0; dmax[k] = -1.0 / 0.0; }
     } else {
       lmap_init(&map, 1024);
       mcap = 1024;
       msum = (double*)calloc((size_t)mcap, sizeof(double));
       mcnt = (int64_t*)calloc((size_t)mcap, sizeof(int64_t));
+      mmin = (double*)malloc(sizeof(double) * (size_t)mcap);
+      mmax = (double*)malloc(sizeof(double) * (size_t)mcap);
+      for (int64_t k = 0; k < mcap; ++k) { mmin[k] = 1.0 / 0.0; mmax[k] = -1.0 / 0.0; }
     }
   }
   for (;;) {
@@ -214,7 +256,10 @@ static void run_segment(pgo_segment_query* q) {
     int n = 0;
     while (n < block && next < q->num_docs) {
       int64_t d = next++;
-      if (fc) {
+      if (q->num_leaves > 0) {
+        scanned += q->num_leaves;
+        if (!row_matches(q, d)) continue;
+      } else if (fc) {
         scanned++;
         int32_t id = col_id(fc, d);
         if (id < q->lo || id > q->hi) continue;
@@ -226,9 +271,15 @@ static void run_segment(pgo_segment_query* q) {
     for (int i = 0; i < n; ++i) dict_ids[i] = col_id(mc, doc_ids[i]);
     for (int i = 0; i < n; ++i) values[i] = mc->dict[dict_ids[i]];
     if (!q->num_group_cols) {
-      double s = 0.0;
-      for (int i = 0; i < n; ++i) s += values[i];
+      double s = 0.0, lo = 1.0 / 0.0, hi = -1.0 / 0.0;
+      for (int i = 0; i < n; ++i) {
+        s += values[i];
+        if (values[i] < lo) lo = values[i];
+        if (values[i] > hi) hi = values[i];
+      }
       holder += s;
+      if (lo < vmin) vmin = lo;
+      if (hi > vmax) vmax = hi;
       count += n;
     } else {
       for (int i = 0; i < n; ++i) {
@@ -245,22 +296,34 @@ static void run_segment(pgo_segment_query* q) {
             int64_t nc = mcap * 2;
             msum = (double*)realloc(msum, sizeof(double) * nc);
             mcnt = (int64_t*)realloc(mcnt, sizeof(int64_t) * nc);
+            mmin = (double*)realloc(mmin, sizeof(double) * nc);
+            mmax = (double*)realloc(mmax, sizeof(double) * nc);
             memset(msum + mcap, 0, sizeof(double) * (nc - mcap));
             memset(mcnt + mcap, 0, sizeof(int64_t) * (nc - mcap));
+            for (int64_t k = mcap; k < nc; ++k) { mmin[k] = 1.0 / 0.0; mmax[k] = -1.0 / 0.0; }
             mcap = nc;
           }
           gkeys[i] = id;
         }
       }
-      if (array_based)
-        for (int i = 0; i < n; ++i) { dsum[gkeys[i]] += values[i]; dcnt[gkeys[i]] += 1; }
-      else
-        for (int i = 0; i < n; ++i) { msum[gkeys[i]] += values[i]; mcnt[gkeys[i]] += 1; }
+      double* S_ = array_based ? dsum : msum;
+      int64_t* C_ = array_based ? dcnt : mcnt;
+      double* L_ = array_based ? dmin : mmin;
+      double* H_ = array_based ? dmax : mmax;
+      for (int i = 0; i < n; ++i) {  /* per doc in doc order (Sum/Min/MaxAggregationFunction.aggregateGroupBySV) */
+        const int32_t k = gkeys[i];
+        S_[k] += values[i];
+        C_[k] += 1;
+        if (values[i] < L_[k]) L_[k] = values[i];
+        if (values[i] > H_[k]) H_[k] = values[i];
+      }
       count += n;
     }
   }
   q->count = count;
   q->sum = holder;
+  q->vmin = vmin;
+  q->vmax = vmax;
   q->entries_scanned = scanned;
   q->num_groups = 0;
   if (q->num_group_cols) {
@@ -275,7 +338,14 @@ static void run_segment(pgo_segment_query* q) {
       int64_t j = 0;
       if (array_based) {
         for (int64_t k = 0; k < prod; ++k)
-          if (dcnt[k]) { q->g_keys[j] = k; q->g_sums[j] = dsum[k]; q->g_counts[j] = dcnt[k]; ++j; }
+          if (dcnt[k]) {
+            q->g_keys[j] = k;
+            q->g_sums[j] = dsum[k];
+            q->g_counts[j] = dcnt[k];
+            if (q->g_mins) q->g_mins[j] = dmin[k];
+            if (q->g_maxs) q->g_maxs[j] = dmax[k];
+            ++j;
+          }
       } else {
         for (int64_t h = 0; h < map.cap; ++h)
           if (map.keys[h] != -1) {
@@ -283,11 +353,13 @@ static void run_segment(pgo_segment_query* q) {
             q->g_keys[id] = map.keys[h];
             q->g_sums[id] = msum[id];
             q->g_counts[id] = mcnt[id];
+            if (q->g_mins) q->g_mins[id] = mmin[id];
+            if (q->g_maxs) q->g_maxs[id] = mmax[id];
           }
       }
     }
-    if (array_based) { free(dsum); free(dcnt); }
-    else { free(map.keys); free(map.ids); free(msum); free(mcnt); }
+    if (array_based) { free(dsum); free(dcnt); free(dmin); free(dmax); }
+    else { free(map.keys); free(map.ids); free(msum); free(mcnt); free(mmin); free(mmax); }
   }
   free(doc_ids);
   free(dict_ids);

@@ -42,7 +42,6 @@ def _run_inner(ctx, seg, q):
     return blk, op.get_execution_statistics()
 
 
-@pytest.mark.parametrize("filtered", [False, True])
 def _golden_stats(exp_stats, loaded, filtered):
     e = list(exp_stats)
     if filtered and loaded == "bitmaps_loaded":
@@ -50,6 +49,7 @@ def _golden_stats(exp_stats, loaded, filtered):
     return e
 
 
+@pytest.mark.parametrize("filtered", [False, True])
 def test_golden_aggregation_only(ctx, sv, filtered):
     gseg, oseg, exp, loaded = sv
     q = pql.compile("SELECT" + exp["aggregation"] + " FROM testTable" + (exp["filter"]["text"] if filtered else ""))
