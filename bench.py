@@ -1,11 +1,13 @@
 """Benchmark of the MI355X segment query hot path (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c2|c5]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c2|c3|c1|c4]
   (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
-A "step" is one execution of the compiled query over all of this rank's segments resident in HBM (filter + decode +
-aggregate in the fused HIP kernel, the on-device combine, result back to the host) plus, for N>1, the cross-GPU merge
-(RCCL all-reduce of the partial aggregates / dense group tables).  Rank 0 prints one JSON line.
+The default workload is c5, BASELINE configs[4] -- the metric's own shape: bitmap inverted-index AND/OR filter +
+group-by SUM over 4096 x 2M-row segments, sharded over the GPUs.  A "step" is one execution of the query over all of
+this rank's segments resident in HBM: predicate values resolved to dictId space for every segment (a-4, in the
+library), bitmap sub-tree expansion, filter + decode + aggregate in the fused HIP kernel, the on-device combine, the
+result back to the host, and for N>1 the cross-GPU merge.  Rank 0 prints one JSON line.
 """
 import argparse
 import json
@@ -19,6 +21,8 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "rows/sec for filter+group-by SUM at 1/2/4/8 GPUs; % of HBM roofline"
+# bounded CPU-baseline samples (segments, rows per segment): ~10-30 s of single-core work over 8 threads in total
+CPU_SAMPLE = {"c2": (8, 32_000_000), "c5": (64, 2_000_000), "c3": (8, 16_000_000)}
 
 
 def parse():
@@ -26,7 +30,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default=os.environ.get("PGX_WORKLOAD", "c2"))
+    ap.add_argument("--workload", default=os.environ.get("PGX_WORKLOAD", "c5"))
     ap.add_argument("--rows", type=int, default=0, help="override rows per segment (smoke/debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-iters", type=int, default=0, help="only run K kernel launches (for rocprofv3)")
@@ -60,9 +64,11 @@ def barrier_sync(world):
         torch.cuda.synchronize()
 
 
-def cpu_baseline_c2(wl, seg_rows, nseg, threads):
-    """The oracle's C twin (one thread per segment, per-row readInt, 10000-doc blocks, double SUM) on a bounded sample
-    of the same workload, timed on this host's cores: best of 5 after 2 warm-ups."""
+def cpu_baseline(wl, query, seg_rows, nseg, threads):
+    """The oracle's C twin (oracle/pinot_oracle_c.c: one thread per segment, per-row readInt, 10000 / 5000-doc blocks,
+    double SUM, hash-map group keys) on a bounded sample of the same workload, generated bit-identically on the host and
+    timed on this host's cores: best of 5 after 2 warm-ups.  Filters with several leaves are evaluated per
+    row on the leaves' dictId sets (the reference's bitmap iterators are not restated in C)."""
     import numpy as np
     from oracle import c_oracle
     from pinot_amd import synth
@@ -72,26 +78,48 @@ def cpu_baseline_c2(wl, seg_rows, nseg, threads):
     def gen(s):
         cols = {}
         for ci, c in enumerate(wl.columns):
-            fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), seg_rows, c.bits, c.card)
+            if c.paired:
+                fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, 0, ci), seg_rows, c.bits, c.card,
+                                         pair_seed=synth.column_seed(wl.seed, s, 99), npairs=wl.npairs)
+            else:
+                fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), seg_rows, c.bits, c.card)
             cols[c.name] = (fwd, c.bits, dicts[c.name], c.card)
         segs[s] = c_oracle.Segment(seg_rows, cols)
 
     ths = [threading.Thread(target=gen, args=(s,)) for s in range(nseg)]
     [t.start() for t in ths]
     [t.join() for t in ths]
+    kw = {"threads": threads, "metric": "m"}
+    if wl.name == "c2":
+        kw.update(filter_col="dA", lo=64, hi=191)
+    elif wl.name == "c3":
+        kw.update(group_cols=("g1", "g2"))
+    elif wl.name == "c5":  # (f1 IN (...) OR f2 = 7) AND f3 <> 3 GROUP BY gk: leaves as dictId bitsets
+        f1 = [int(v) for v in query["filter"]["children"][0]["children"][0]["values"]]
+
+        def bits(card, ids):
+            w = np.zeros((card + 31) // 32, dtype=np.uint32)
+            for i in ids:
+                w[i >> 5] |= np.uint32(1 << (i & 31))
+            return w
+        kw.update(group_cols=("gk",), leaves=[("f1", bits(1000, f1)), ("f2", bits(100, [7])),
+                                              ("f3", bits(10, [i for i in range(10) if i != 3]))],
+                  prog=[0, 1, -2, 2, -1])
+    else:
+        return None
     times = []
     out = None
     for it in range(7):
         t0 = time.perf_counter()
-        out = c_oracle.run(segs, filter_col="dA", lo=64, hi=191, metric="m", threads=threads)
+        out = c_oracle.run(segs, **kw)
         dt = time.perf_counter() - t0
         if it >= 2:
             times.append(dt)
     best = min(times)
     return {"value": nseg * seg_rows / best, "unit": "rows/s", "cores": threads, "kind": "port",
-            "sample": "%d segments x %d rows of the same synthetic c2 data (host-generated bit-identically), "
-                      "oracle/pinot_oracle_c.c one thread per segment, best of 5 after 2 warm-ups; %.3f s per query"
-                      % (nseg, seg_rows, best),
+            "sample": "%d segments x %d rows of the same synthetic %s data (host-generated bit-identically), "
+                      "oracle/pinot_oracle_c.c one thread per segment on %d threads, best of 5 after 2 warm-ups; "
+                      "%.3f s per query" % (nseg, seg_rows, wl.name, threads, best),
             "result_count": int(sum(r["count"] for r in out))}
 
 
@@ -132,7 +160,7 @@ def main():
     q = E._Query(ctx, req)
     segs = data.segments
     seg_arr = (C.c_void_p * len(segs))(*[s.handle.value for s in segs])
-    binds, keep = q.bindings(segs)
+    binds, keep = q.bindings(segs)  # for the untimed profiling / timing calls only; steps bind their own
     L = N.lib()
 
     dense = False
@@ -162,6 +190,7 @@ def main():
     merged = [None]
 
     def step():
+        binds, _owner = q.bindings(segs)  # a-4 per segment, inside the timed step
         r = C.c_void_p()
         if dense and world > 1:
             opts = N.ExecOpts(0, C.c_void_p(dense_t.data_ptr()), dense_t.numel() * 8, N.PGX_X_KEEP_DENSE_ON_DEVICE)
@@ -259,16 +288,19 @@ def main():
     algo_bytes += ngroups * 8 * (1 + len(req["aggregations"]))
     # the query-specialised kernel (hiprtc, pgx_jit.cpp) unless PGX_JIT=0 selects the generic interpreter kernel
     kernel_name = "pgxq (generated per query shape)" if os.environ.get("PGX_JIT", "1") != "0" else "pgx_scan_kernel"
+    if bitmap_leaves:  # the timed span covers the bitmap expansion too (pgx_execute_timed brackets both launches)
+        kernel_name = "pgx_roaring_program + " + kernel_name
     achieved = algo_bytes / (kern.value * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % wl.name)
     if os.path.exists(tf):
         tj = json.load(open(tf))
         if tj.get("rows") == rows:
-            traffic = tj.get("hbm_bytes_per_launch")
+            traffic = tj.get("hbm_bytes_per_launch")  # PMC FETCH/WRITE of the same command (tools/profile_wl.sh)
     cpu = None
-    if world == 1 and not args.no_cpu_baseline and wl.name == "c2":
-        cpu = cpu_baseline_c2(wl, min(rows, 32_000_000), 8, 8)
+    if world == 1 and not args.no_cpu_baseline and wl.name in CPU_SAMPLE:
+        nseg, seg_rows = CPU_SAMPLE[wl.name]
+        cpu = cpu_baseline(wl, req, min(rows, seg_rows), nseg, 8)
     if merged[0] is not None and req.get("group_by"):
         top = merged[0][0]
         best = sorted(top.items(), key=lambda kv: kv[1], reverse=q.fns[0] != "min")[:3]

@@ -161,6 +161,25 @@ typedef struct {
   const uint32_t* words;      /* host memory, optional */
 } pgx_leaf_binding;
 
+/* a-4 inside the library: resolve each leaf's raw predicate values against every segment's dictionary, as
+ * PredicateEvaluatorProvider (operator/filter/predicate/PredicateEvaluatorProvider.java:31-54) and the Equals /
+ * NotEquals / In / NotIn / RangeOffline evaluators do per segment; Dictionary.indexOf parses the value with the column's
+ * type (Integer.parseInt, Long.parseLong, Float.parseFloat, Double.parseDouble; STRING padded with the padding char,
+ * StringDictionary.java:37-51).  Segments whose dictionaries are byte-identical share one resolution. */
+typedef struct {
+  int32_t num_values;         /* EQ / NEQ 1, IN / NOT_IN n, RANGE 2 (lower, upper; "*" = unbounded) */
+  const char* const* values;
+  int32_t lower_inclusive;    /* RANGE only (RangePredicate.java:31-57) */
+  int32_t upper_inclusive;
+} pgx_predicate;
+
+typedef struct pgx_bindings pgx_bindings;
+/* preds[num_leaves] in the query's leaf order; the result holds bindings[n][num_leaves] for pgx_execute. */
+pgx_status pgx_bind_predicates(const pgx_query* q, pgx_segment* const* segs, int32_t n, const pgx_predicate* preds,
+                               pgx_bindings** out);
+const pgx_leaf_binding* pgx_bindings_array(const pgx_bindings* b);
+pgx_status pgx_bindings_release(pgx_bindings* b);
+
 typedef struct {
   uint64_t stream;            /* hipStream_t (0 = the context's own stream) */
   void* dense_out;            /* optional device buffer for the dense group table (multi-GPU merge) */

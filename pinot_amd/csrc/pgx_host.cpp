@@ -13,7 +13,10 @@
 #include <exception>
 #include <functional>
 #include <thread>
+#include <cctype>
+#include <cerrno>
 #include <cmath>
+#include <tuple>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,6 +43,8 @@ extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64
                                          unsigned long long* counter, int64_t* out_slot,
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
+extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
+                                                 int maxchunks, hipStream_t stream);
 extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
                                        int64_t n_words, uint64_t pair_seed, uint32_t npairs, hipStream_t stream);
 extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
@@ -646,6 +651,11 @@ struct pgx_query {
 // =================================================================================================
 // Result
 // =================================================================================================
+struct pgx_bindings {
+  std::vector<pgx_leaf_binding> arr;
+  std::vector<std::vector<uint32_t>> words;  // owned bitsets (arr[i].words points into these)
+};
+
 struct pgx_result {
   int64_t stats[4] = {0, 0, 0, 0};
   int num_aggs = 0;
@@ -922,6 +932,14 @@ struct ExecPlan {
     std::vector<JSeg> segs;
   };
   std::vector<JitGroup> jit;
+  // bitmap sub-trees evaluated by pgx_roaring_program into one mask each (JIT leaf L + k for program k)
+  bool rprog_on = false;
+  struct DmProg {
+    std::vector<int> op, arg;  // RP_*; RP_LEAF arg = query leaf index
+  };
+  std::vector<DmProg> dm_progs;
+  std::vector<RProg> rprogs;              // [seg * nprogs + k]
+  const RProg* rprog_dev = nullptr;
   // numEntriesScannedInFilter automaton (pgx_stats.cpp) for filter trees whose statistic has no closed form
   bool fsm_on = false;
   FsmPlan fsm;
@@ -1155,6 +1173,149 @@ bool stats_closed_form(const PNode& root, const pgx_query& q, pgx_segment* const
   return true;
 }
 
+// Bitmap sub-trees: a node whose leaves are all bitmap inverted-index leaves (and the bitmap / all-bitmap children of
+// any AND / OR) is evaluated per 65536-doc chunk by pgx_roaring_program into ONE doc mask.
+struct FusePlan {
+  std::map<const PNode*, int> full;   // node evaluated whole by program k
+  std::map<const PNode*, int> group;  // AND / OR whose all-bitmap children are program k
+  std::vector<ExecPlan::DmProg> progs;
+};
+
+bool all_bitmap(const PNode& n) {
+  if (n.op == PGX_F_LEAF) return n.phys == PH_BITMAP;
+  for (const PNode& k : n.kids)
+    if (!all_bitmap(k)) return false;
+  return true;
+}
+
+void bitmap_prog(const PNode& n, const pgx_query& q, ExecPlan::DmProg& p) {
+  if (n.op == PGX_F_LEAF) {
+    p.op.push_back(RP_LEAF);
+    p.arg.push_back(n.leaf);
+    // BitmapBasedFilterOperator NEQ / NOT_IN: OR of the non-matching bitmaps, then flip (BitmapDocIdSet.java:60-73)
+    if (q.leaf_kind[n.leaf] == PGX_PRED_NEQ || q.leaf_kind[n.leaf] == PGX_PRED_NOT_IN) {
+      p.op.push_back(RP_NOT);
+      p.arg.push_back(0);
+    }
+    return;
+  }
+  for (size_t i = 0; i < n.kids.size(); ++i) {
+    bitmap_prog(n.kids[i], q, p);
+    if (i > 0) {
+      p.op.push_back(n.op == PGX_F_AND ? RP_AND : RP_OR);
+      p.arg.push_back(0);
+    }
+  }
+}
+
+void plan_fuse(const PNode& n, const pgx_query& q, FusePlan& F) {
+  if (n.op == PGX_F_LEAF) {
+    if (n.phys == PH_BITMAP) {
+      F.full[&n] = int(F.progs.size());
+      F.progs.emplace_back();
+      bitmap_prog(n, q, F.progs.back());
+    }
+    return;
+  }
+  if (all_bitmap(n)) {
+    F.full[&n] = int(F.progs.size());
+    F.progs.emplace_back();
+    bitmap_prog(n, q, F.progs.back());
+    return;
+  }
+  std::vector<const PNode*> fk;
+  for (const PNode& k : n.kids) {
+    if (all_bitmap(k)) fk.push_back(&k);
+    else plan_fuse(k, q, F);
+  }
+  if (fk.empty()) return;
+  ExecPlan::DmProg p;
+  for (size_t i = 0; i < fk.size(); ++i) {
+    bitmap_prog(*fk[i], q, p);
+    if (i > 0) {
+      p.op.push_back(n.op == PGX_F_AND ? RP_AND : RP_OR);
+      p.arg.push_back(0);
+    }
+  }
+  F.group[&n] = int(F.progs.size());
+  F.progs.push_back(std::move(p));
+}
+
+int prog_depth(const ExecPlan::DmProg& p) {
+  int d = 0, mx = 0;
+  for (int op : p.op) {
+    if (op == RP_LEAF) mx = std::max(mx, ++d);
+    else if (op == RP_AND || op == RP_OR) --d;
+  }
+  return mx;
+}
+
+// emit() with bitmap programs: a fused node is one doc-mask leaf (query leaf L + k); an AND / OR puts its fused group
+// where its bitmap children were (AND: after the sorted ranges, before the scan children and their OP_STATs).
+void emit_fused(const PNode& n, const FusePlan& F, int L, std::vector<int8_t>& op, std::vector<int8_t>& arg, bool root,
+                int& host_scan_leaves) {
+  auto f = F.full.find(&n);
+  if (f != F.full.end()) {
+    op.push_back(OP_LEAF);
+    arg.push_back(int8_t(L + f->second));
+    return;
+  }
+  if (n.op == PGX_F_LEAF) {
+    op.push_back(OP_LEAF);
+    arg.push_back(int8_t(n.leaf));
+    if (root && n.phys == PH_SCAN) host_scan_leaves += 1;
+    return;
+  }
+  auto g = F.group.find(&n);
+  int pushed = 0;
+  auto fold = [&](int opc) {
+    if (pushed > 1) { op.push_back(int8_t(opc)); arg.push_back(2); }
+  };
+  if (n.op == PGX_F_OR) {
+    for (const PNode& k : n.kids) {
+      if (all_bitmap(k)) continue;
+      if (root && k.op == PGX_F_LEAF && k.phys == PH_SCAN) host_scan_leaves += 1;
+      emit_fused(k, F, L, op, arg, false, host_scan_leaves);
+      ++pushed;
+      fold(OP_OR);
+    }
+    if (g != F.group.end()) {
+      op.push_back(OP_LEAF);
+      arg.push_back(int8_t(L + g->second));
+      ++pushed;
+      fold(OP_OR);
+    }
+    return;
+  }
+  for (const PNode& k : n.kids)
+    if (k.op == PGX_F_LEAF && k.phys == PH_SORTED) {
+      emit_fused(k, F, L, op, arg, false, host_scan_leaves);
+      ++pushed;
+      fold(OP_AND);
+    }
+  if (g != F.group.end()) {
+    op.push_back(OP_LEAF);
+    arg.push_back(int8_t(L + g->second));
+    ++pushed;
+    fold(OP_AND);
+  }
+  const bool fast = pushed > 0;
+  for (const PNode& k : n.kids)
+    if (k.op == PGX_F_LEAF && k.phys == PH_SCAN) {
+      if (fast || pushed > 0) { op.push_back(OP_STAT); arg.push_back(0); }
+      else if (root) host_scan_leaves += 1;
+      emit_fused(k, F, L, op, arg, false, host_scan_leaves);
+      ++pushed;
+      fold(OP_AND);
+    }
+  for (const PNode& k : n.kids)
+    if (k.op != PGX_F_LEAF && !all_bitmap(k)) {
+      emit_fused(k, F, L, op, arg, false, host_scan_leaves);
+      ++pushed;
+      fold(OP_AND);
+    }
+}
+
 FsmTreeNode fsm_tree(const PNode& n) {
   FsmTreeNode t;
   t.op = n.op == PGX_F_LEAF ? 0 : (n.op == PGX_F_AND ? 1 : 2);
@@ -1163,6 +1324,118 @@ FsmTreeNode fsm_tree(const PNode& n) {
   for (const PNode& k : n.kids) t.kids.push_back(fsm_tree(k));
   return t;
 }
+
+
+// ----- a-4: predicate values -> dictId space (per segment, memoised per distinct dictionary) -----
+
+namespace {
+
+std::string trim_ws(const std::string& v) {
+  size_t a = 0, b = v.size();
+  while (a < b && (unsigned char)v[a] <= ' ') ++a;
+  while (b > a && (unsigned char)v[b - 1] <= ' ') --b;
+  return v.substr(a, b - a);
+}
+
+// Dictionary.indexOf (segment/index/readers/{Int,Long,Float,Double,String}Dictionary.java): binary search, -(insertion
+// point) - 1 when absent.
+int dict_index_of(const StagedColumn& c, const std::string& raw) {
+  auto search = [&](auto less, auto eq) {
+    int lo = 0, hi = c.card - 1;
+    while (lo <= hi) {
+      const int mid = (lo + hi) >> 1;
+      if (eq(mid)) return mid;
+      if (less(mid)) lo = mid + 1;
+      else hi = mid - 1;
+    }
+    return -(lo + 1);
+  };
+  switch (c.data_type) {
+    case PGX_INT:
+    case PGX_LONG: {  // Integer.parseInt / Long.parseLong: optional sign, digits only
+      const char* s = raw.c_str();
+      char* end = nullptr;
+      errno = 0;
+      const long long v = std::strtoll(s, &end, 10);
+      const bool ok = !raw.empty() && *end == '\0' && errno == 0 && !std::isspace((unsigned char)raw[0]) &&
+                      (c.data_type == PGX_LONG || (v >= INT32_MIN && v <= INT32_MAX));
+      if (!ok) fail(PGX_ERR_INVALID_ARG, "NumberFormatException: For input string: \"" + raw + "\"");
+      return search([&](int i) { return c.ivals[i] < v; }, [&](int i) { return c.ivals[i] == v; });
+    }
+    case PGX_FLOAT:
+    case PGX_DOUBLE: {  // Float.parseFloat / Double.parseDouble: surrounding whitespace and a trailing f/F/d/D allowed
+      std::string t = trim_ws(raw);
+      if (!t.empty() && std::strchr("fFdD", t.back())) t.pop_back();
+      char* end = nullptr;
+      const double d = c.data_type == PGX_FLOAT ? double(std::strtof(t.c_str(), &end)) : std::strtod(t.c_str(), &end);
+      if (t.empty() || *end != '\0') fail(PGX_ERR_INVALID_ARG, "NumberFormatException: For input string: \"" + raw + "\"");
+      return search([&](int i) { return c.dvals[i] < d; }, [&](int i) { return c.dvals[i] == d; });
+    }
+    default: {  // StringDictionary.indexOf: pad the lookup to the entry width unless it is at least that long
+      const size_t w = size_t(c.dict_width);
+      const char pad = char(c.pad_char);
+      const std::string key = raw.size() >= w ? raw : raw + std::string(w - raw.size(), pad);
+      auto entry = [&](int i) {
+        const std::string& v = c.svals[i];
+        return v.size() >= w ? v : v + std::string(w - v.size(), pad);
+      };
+      return search([&](int i) { return entry(i) < key; }, [&](int i) { return entry(i) == key; });
+    }
+  }
+}
+
+void resolve_binding(const StagedColumn& c, int kind, const pgx_predicate& p, int32_t& lo, int32_t& hi,
+                     std::vector<uint32_t>& words) {
+  const int card = c.card;
+  auto val = [&](int i) { return std::string(p.values[i] ? p.values[i] : ""); };
+  words.clear();
+  lo = 0;
+  hi = -1;
+  if (kind == PGX_PRED_RANGE) {  // RangeOfflineDictionaryPredicateEvaluator.java:30-65
+    if (p.num_values != 2) fail(PGX_ERR_INVALID_ARG, "RANGE needs (lower, upper)");
+    const std::string a = val(0), b = val(1);
+    int start = a == "*" ? 0 : dict_index_of(c, a);
+    int end = b == "*" ? card - 1 : dict_index_of(c, b);
+    if (start < 0) start = -(start + 1);
+    else if (!p.lower_inclusive && a != "*") start += 1;
+    if (end < 0) end = -(end + 1) - 1;
+    else if (!p.upper_inclusive && b != "*") end -= 1;
+    if (end >= start) {
+      lo = start;
+      hi = end;
+    }
+    return;
+  }
+  if (kind == PGX_PRED_EQ) {  // EqualsPredicateEvaluator.java:28-42
+    if (p.num_values < 1) fail(PGX_ERR_INVALID_ARG, "EQ needs a value");
+    const int i = dict_index_of(c, val(0));
+    if (i >= 0) lo = hi = i;
+    return;
+  }
+  std::vector<uint8_t> m(card, kind == PGX_PRED_IN ? 0 : 1);  // In / NotIn / NotEquals evaluators
+  for (int k = 0; k < p.num_values; ++k) {
+    const int i = dict_index_of(c, val(k));
+    if (i >= 0) m[i] = kind == PGX_PRED_IN ? 1 : 0;
+  }
+  int first = -1, last = -1, cnt = 0;
+  for (int i = 0; i < card; ++i)
+    if (m[i]) {
+      if (first < 0) first = i;
+      last = i;
+      ++cnt;
+    }
+  if (cnt == 0) return;
+  if (last - first + 1 == cnt) {
+    lo = first;
+    hi = last;
+    return;
+  }
+  words.assign((card + 31) / 32, 0u);
+  for (int i = 0; i < card; ++i)
+    if (m[i]) words[i >> 5] |= 1u << (i & 31);
+}
+
+}  // namespace
 
 // PGX_HOST_PROFILE=1: sub-phase marks of the planner (appended to the running pgx_execute's profile line).
 thread_local std::function<void(const char*)> g_prof_mark;
@@ -1319,9 +1592,40 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   std::vector<int8_t> pop, parg;
   PNode froot;
   P.fsm_on = false;
+  P.rprog_on = false;
+  P.dm_progs.clear();
+  P.use_docmask = jit_enabled() && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
+                                    K.group_mode == G_DENSE_GLOBAL || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS;
   if (!q.filter.empty()) {
     PNode root = build_tree(q, *segs[0]);
-    emit(root, pop, parg, true, false, host_scan_leaves);
+    const size_t L = q.leaf_col.size();
+    bool fuse = P.use_docmask && stats_closed_form(root, q, segs, n, bindings) && !std::getenv("PGX_NO_RPROG");
+    for (int s = 0; s < n && fuse; ++s) {
+      if (star_fit(q, *segs[s])) fuse = false;
+      for (size_t l = 0; l < L && fuse; ++l) {
+        const StagedColumn& c = segs[s]->col(q.leaf_col[l]);
+        const bool bitmap = c.has_inverted && !c.is_sorted && q.leaf_kind[l] != PGX_PRED_RANGE;
+        if (bitmap != (!segs[0]->col(q.leaf_col[l]).is_sorted && segs[0]->col(q.leaf_col[l]).has_inverted &&
+                       q.leaf_kind[l] != PGX_PRED_RANGE))
+          fuse = false;  // index kinds differ across segments
+        else if (bitmap && !c.inv_dev.p && !binding_empty(bindings[size_t(s) * L + l], c.card))
+          fuse = false;
+      }
+    }
+    FusePlan F;
+    if (fuse) {
+      plan_fuse(root, q, F);
+      if (F.progs.empty() || L + F.progs.size() > size_t(PGX_J_MAX_LEAVES)) fuse = false;
+      for (const auto& p : F.progs)
+        if (prog_depth(p) > 4 || p.op.size() > size_t(kMaxRProg)) fuse = false;
+    }
+    if (fuse) {
+      emit_fused(root, F, int(L), pop, parg, true, host_scan_leaves);
+      P.rprog_on = true;
+      P.dm_progs = F.progs;
+    } else {
+      emit(root, pop, parg, true, false, host_scan_leaves);
+    }
     if (!stats_closed_form(root, q, segs, n, bindings)) {
       // the automaton counts every entry: no OP_STAT popcounts, no whole-range host terms
       P.fsm_on = true;
@@ -1345,8 +1649,6 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       for (const PNode& k : x->kids) todo.push_back(&k);
     }
   }
-  P.use_docmask = jit_enabled() && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
-                                    K.group_mode == G_DENSE_GLOBAL || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS;
   P.roar.clear();
   P.roar_index.assign(n, std::vector<int>(q.leaf_col.size(), -1));
   P.mask_words = 0;
@@ -1470,7 +1772,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
             for (int id = 0; id < col.card; ++id)
               if (id < b.lo || id > b.hi) take(id);
           }
-          o.mask_words += uint64_t(it.nchunks) * 2048;
+          if (!P.rprog_on) o.mask_words += uint64_t(it.nchunks) * 2048;
           o.maxchunks = std::max(o.maxchunks, it.nchunks);
           o.roar.push_back(it);
         }
@@ -1504,6 +1806,39 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     P.roar_maxchunks = std::max(P.roar_maxchunks, o.maxchunks);
     P.total_raw += o.total_raw;
     P.host_entries += o.host_entries;
+  }
+  // per (segment, bitmap program): the program over that segment's leaf descriptors and its output mask
+  P.rprogs.clear();
+  if (P.rprog_on) {
+    const size_t np = P.dm_progs.size();
+    P.rprogs.resize(size_t(n) * np);
+    for (int s = 0; s < n; ++s) {
+      const int nchunks = int((int64_t(segs[s]->total_docs) + 65535) >> 16);
+      P.roar_maxchunks = std::max(P.roar_maxchunks, nchunks);
+      for (size_t k = 0; k < np; ++k) {
+        const auto& dp = P.dm_progs[k];
+        RProg& r = P.rprogs[size_t(s) * np + k];
+        r = RProg{};
+        r.nchunks = nchunks;
+        r.num_docs = P.ksegs[s].num_docs;
+        r.mask = reinterpret_cast<uint32_t*>(uintptr_t(P.mask_words));  // word offset until the buffer exists
+        P.mask_words += uint64_t(nchunks) * 2048;
+        int o = 0;
+        for (size_t i = 0; i < dp.op.size(); ++i) {
+          if (dp.op[i] == RP_LEAF) {
+            const int ri = P.roar_index[s][dp.arg[i]];
+            r.op[o] = RP_LEAF;
+            r.arg[o++] = int16_t(ri);
+            // a leaf without matching dictIds (alwaysFalse) is empty, negated or not
+            if (ri < 0 && i + 1 < dp.op.size() && dp.op[i + 1] == RP_NOT) ++i;
+          } else {
+            r.op[o] = int8_t(dp.op[i]);
+            r.arg[o++] = 0;
+          }
+        }
+        r.nops = o;
+      }
+    }
   }
   prof_mark("p.merge");
   // star-tree segments (query kernels only: the per-segment program needs the generated kernels)
@@ -1600,12 +1935,23 @@ constexpr size_t kOutsBytes = 256;  // agg planes [0, 72), stats [128, 144), ove
 struct ExecBuffers {
   DevBuf arena;
   PinnedBuf host;
-  size_t off_ksegs = 0, off_jsegs = 0, off_tiles = 0, off_rdesc = 0, off_outs = 0, size = 0;
+  size_t off_ksegs = 0, off_jsegs = 0, off_tiles = 0, off_rdesc = 0, off_rprog = 0, off_outs = 0, size = 0;
   DevBuf table, keys, key_state, masks;
   uint8_t* dev() const { return arena.as<uint8_t>(); }
 };
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
+
+// Bitmap inverted-index leaves: one mask per (segment, leaf) (pgx_roaring_expand), or one mask per (segment, bitmap
+// program) with the sub-tree's AND / OR / NOT applied in the same pass (pgx_roaring_program).
+void launch_bitmaps(ExecPlan& P, hipStream_t st) {
+  if (P.rprog_on) {
+    const int np = int(P.rprogs.size());
+    hip_check(pgx_launch_roaring_program(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, st), "bitmap program launch");
+  } else if (P.rdesc_dev) {
+    hip_check(pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
+  }
+}
 
 void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
   const size_t n = P.ksegs.size();
@@ -1616,7 +1962,8 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
     if (!P.star.empty() && P.star[s].on) P.star_tile_cap += size_t(P.ksegs[s].num_docs) / 8192 + 2;
   B.off_tiles = align_up(B.off_jsegs + n * sizeof(JSeg), 256);
   B.off_rdesc = align_up(B.off_tiles + P.star_tile_cap * 4, 256);
-  B.off_outs = align_up(B.off_rdesc + P.roar.size() * sizeof(RDesc), 256);
+  B.off_rprog = align_up(B.off_rdesc + P.roar.size() * sizeof(RDesc), 256);
+  B.off_outs = align_up(B.off_rprog + P.rprogs.size() * sizeof(RProg), 256);
   B.size = B.off_outs + kOutsBytes;
   B.arena = DevBuf(ctx, B.size);
   B.host = PinnedBuf(ctx, B.size);
@@ -1665,25 +2012,32 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
   // bitmap inverted-index expansion descriptors + the per-(segment, leaf) doc masks they fill
   P.rdesc_dev = nullptr;
   P.masks_dev = nullptr;
-  if (!P.roar.empty()) {
-    B.masks = DevBuf(ctx, P.mask_words * 4);
+  P.rprog_dev = nullptr;
+  if (!P.roar.empty() || !P.rprogs.empty()) {
+    B.masks = DevBuf(ctx, std::max<uint64_t>(P.mask_words, 1) * 4);
     P.masks_dev = B.masks.as<uint32_t>();
     RDesc* rd = reinterpret_cast<RDesc*>(B.host.bytes() + B.off_rdesc);
     for (size_t i = 0; i < P.roar.size(); ++i) {
       const auto& it = P.roar[i];
-      rd[i].mask = P.masks_dev + it.mask_off;
+      rd[i].mask = P.rprog_on ? nullptr : P.masks_dev + it.mask_off;
       rd[i].inv = static_cast<const uint8_t*>(it.inv);
       rd[i].offs = reinterpret_cast<const uint32_t*>(base + it.blob_off);
       rd[i].nb = it.nb;
       rd[i].nchunks = it.nchunks;
     }
     P.rdesc_dev = reinterpret_cast<const RDesc*>(B.dev() + B.off_rdesc);
+    RProg* rp = reinterpret_cast<RProg*>(B.host.bytes() + B.off_rprog);
+    for (size_t i = 0; i < P.rprogs.size(); ++i) {
+      rp[i] = P.rprogs[i];
+      rp[i].mask = P.masks_dev + uintptr_t(P.rprogs[i].mask);  // word offset -> device pointer
+    }
+    P.rprog_dev = reinterpret_cast<const RProg*>(B.dev() + B.off_rprog);
     // Expand the bitmaps now: send the blob (roaring offsets) and the descriptors ahead of the rest of the arena and
     // launch, so the expansion runs on the GPU while the host plans the query kernels (plan_jit).
     hip_check(hipMemcpyAsync(B.arena.p, B.host.p, P.blob32.size() * 4, hipMemcpyHostToDevice, st), "blob H2D");
-    hip_check(hipMemcpyAsync(B.dev() + B.off_rdesc, B.host.bytes() + B.off_rdesc, P.roar.size() * sizeof(RDesc),
-                             hipMemcpyHostToDevice, st), "bitmap descriptors H2D");
-    hip_check(pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
+    hip_check(hipMemcpyAsync(B.dev() + B.off_rdesc, B.host.bytes() + B.off_rdesc,
+                             B.off_outs - B.off_rdesc, hipMemcpyHostToDevice, st), "bitmap descriptors H2D");
+    launch_bitmaps(P, st);
     P.roar_early = true;
   }
 }
@@ -1846,8 +2200,14 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     for (int l = 0; l < nleaves; ++l) {
       J.leaf_col.push_back(K.leaf_col[l]);
       const int ri = P.roar_index[members[0]][l];
-      J.leaf_mode.push_back(ri >= 0 ? (P.roar[ri].neg ? LEAF_DOCMASK_NOT : LEAF_DOCMASK) : S0.leaf[l].mode);
+      if (P.rprog_on && P.leaf_phys[l] == PH_BITMAP) J.leaf_mode.push_back(LEAF_NONE);  // read via its program
+      else J.leaf_mode.push_back(ri >= 0 ? (P.roar[ri].neg ? LEAF_DOCMASK_NOT : LEAF_DOCMASK) : S0.leaf[l].mode);
     }
+    if (P.rprog_on)
+      for (size_t k = 0; k < P.dm_progs.size(); ++k) {
+        J.leaf_col.push_back(-1);
+        J.leaf_mode.push_back(LEAF_DOCMASK);
+      }
     const ExecPlan::StarPlan& SP = P.star[members[0]];
     if (SP.on) {
       for (size_t k = 0; k < SP.ranges.size(); ++k) {
@@ -1928,10 +2288,13 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         js.img_words[c] = J.cols[c].img != IMG_NONE ? col.img_words : 0;
         js.vbase[c] = col.vbase;
       }
+      if (P.rprog_on)
+        for (size_t k = 0; k < P.dm_progs.size(); ++k)
+          js.lbits[nleaves + k] = P.masks_dev + uintptr_t(P.rprogs[size_t(s) * P.dm_progs.size() + k].mask);
       for (int l = 0; l < nleaves; ++l) {
         const KLeaf& L = S.leaf[l];
         const int ri = P.roar_index[s][l];
-        js.lbits[l] = ri >= 0 ? P.masks_dev + P.roar[ri].mask_off : L.bitset;
+        js.lbits[l] = (ri >= 0 && !P.rprog_on) ? P.masks_dev + P.roar[ri].mask_off : L.bitset;
         js.lranges[l] = L.ranges;
         js.lnr[l] = L.nranges;
         js.llo[l] = uint32_t(L.lo);
@@ -1973,8 +2336,7 @@ void launch_fsm(ExecPlan& P, hipStream_t st) {
 
 void launch_scan(ExecPlan& P, hipStream_t st) {
   if (!P.jit.empty()) {
-    if (P.rdesc_dev && !P.roar_early)
-      hip_check(pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
+    if (P.rdesc_dev && !P.roar_early) launch_bitmaps(P, st);
     P.roar_early = false;  // relaunches (hash-table retries, timed iterations) expand again
     for (auto& G : P.jit) {
       if (!G.fn) continue;
@@ -1990,6 +2352,7 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
     return;
   }
   if (P.kq.total_tiles == 0) return;
+  if (P.rprog_on) fail(PGX_ERR_INTERNAL, "bitmap programs need the query kernels");
   hip_check(pgx_launch_scan(&P.kq, P.grid, P.tiles_per_wg, P.lds_bytes, st), "scan kernel launch");
   launch_fsm(P, st);
 }
@@ -2975,6 +3338,45 @@ pgx_status pgx_inverted_index_build(const int32_t* ids, int64_t n, int32_t card,
     }
     put32be(4 * uint64_t(card), uint32_t(o));
   });
+}
+
+pgx_status pgx_bind_predicates(const pgx_query* q, pgx_segment* const* segs, int32_t n, const pgx_predicate* preds,
+                               pgx_bindings** out) {
+  return guarded([&] {
+    if (!q || (!segs && n) || (!preds && !q->leaf_col.empty()) || !out || n < 0) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    auto B = std::make_unique<pgx_bindings>();
+    const size_t L = q->leaf_col.size();
+    B->arr.assign(size_t(n) * L, pgx_leaf_binding{0, -1, nullptr});
+    B->words.reserve(size_t(n) * L);
+    // one resolution per (leaf, distinct dictionary)
+    std::map<std::tuple<size_t, uint64_t, int, int, int>, size_t> memo;
+    for (int s = 0; s < n; ++s)
+      for (size_t l = 0; l < L; ++l) {
+        const StagedColumn& c = segs[s]->col(q->leaf_col[l]);
+        const auto key = std::make_tuple(l, c.dict_hash, c.card, c.data_type, c.pad_char);
+        pgx_leaf_binding& b = B->arr[size_t(s) * L + l];
+        auto it = memo.find(key);
+        if (it != memo.end()) {
+          b = B->arr[it->second];
+          continue;
+        }
+        std::vector<uint32_t> w;
+        resolve_binding(c, q->leaf_kind[l], preds[l], b.lo, b.hi, w);
+        if (!w.empty()) {
+          B->words.push_back(std::move(w));
+          b.words = B->words.back().data();
+        }
+        memo.emplace(key, size_t(s) * L + l);
+      }
+    *out = B.release();
+  });
+}
+
+const pgx_leaf_binding* pgx_bindings_array(const pgx_bindings* b) { return b ? b->arr.data() : nullptr; }
+
+pgx_status pgx_bindings_release(pgx_bindings* b) {
+  delete b;
+  return PGX_OK;
 }
 
 pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,

@@ -33,6 +33,19 @@ struct RDesc {
   int32_t nchunks;             // ceil(total_docs / 65536)
 };
 
+// A sub-tree of the filter whose leaves are all bitmap inverted-index leaves, evaluated per 65536-doc chunk by
+// pgx_roaring_program into ONE doc mask (the query kernel then reads one mask word per 32 rows for the whole sub-tree).
+constexpr int kMaxRProg = 24;
+enum RProgOp : int8_t { RP_LEAF = 0, RP_AND = 1, RP_OR = 2, RP_NOT = 3 };
+struct RProg {
+  uint32_t* mask;              // nchunks x 2048 words
+  int32_t nchunks;
+  int32_t num_docs;            // NOT flips inside [0, num_docs) (BitmapDocIdSet: flip(startDocId, endDocId + 1))
+  int32_t nops;
+  int8_t op[kMaxRProg];
+  int16_t arg[kMaxRProg];      // RP_LEAF: index into the RDesc array (-1: empty leaf, no matching dictId)
+};
+
 enum ProgOp : int8_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_STAT = 3, OP_TRUE = 4 };
 
 // Statistics automaton over one segment's leaf masks (pgx_kernels.hip pgx_fsm_chunks / pgx_fsm_compose).

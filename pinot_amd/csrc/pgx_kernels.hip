@@ -643,6 +643,54 @@ __global__ void __launch_bounds__(256) pgx_roaring_expand(const RDesc* __restric
   for (int i = tid; i < 2048; i += 256) out[i] = m[i];
 }
 
+// AND / OR / NOT over bitmap leaves for one 65536-doc chunk (AndBlockDocIdSet.fastIterator's bitmap AND,
+// OrBlockDocIdSet's bitmap OR, BitmapDocIdSet's exclusion flip): a stack of LDS masks, each leaf expanded with
+// roar_or_chunk, the result written once.  One workgroup per (program, chunk).
+constexpr int kRProgStack = 4;
+__global__ void __launch_bounds__(256) pgx_roaring_program(const RProg* __restrict__ progs, const RDesc* __restrict__ descs,
+                                                           int nprogs, int maxchunks) {
+  const int pi = static_cast<int>(blockIdx.x / maxchunks);
+  const int chunk = static_cast<int>(blockIdx.x - static_cast<unsigned>(pi) * maxchunks);
+  if (pi >= nprogs) return;
+  const RProg& P = progs[pi];
+  if (chunk >= P.nchunks) return;
+  __shared__ uint32_t stk[kRProgStack][2048];
+  __shared__ const uint8_t* cptr[kRoarBatch];
+  __shared__ int ccard[kRoarBatch], cpre[kRoarBatch];
+  __shared__ int ncont, celems;
+  const int tid = threadIdx.x;
+  const int64_t doc0 = static_cast<int64_t>(chunk) << 16;
+  int sp = 0;
+  for (int i = 0; i < P.nops; ++i) {
+    const int op = P.op[i];
+    if (op == RP_LEAF) {
+      uint32_t* m = stk[sp];
+      for (int w = tid; w < 2048; w += 256) m[w] = 0u;
+      __syncthreads();
+      const int a = P.arg[i];
+      if (a >= 0) roar_or_chunk(descs[a], chunk, m, cptr, ccard, cpre, &ncont, &celems);
+      ++sp;
+    } else if (op == RP_NOT) {
+      uint32_t* m = stk[sp - 1];
+      for (int w = tid; w < 2048; w += 256) {
+        const int64_t d = doc0 + 32 * w;  // first doc of the word
+        uint32_t keep = 0xFFFFFFFFu;       // bits inside [0, num_docs)
+        if (d >= P.num_docs) keep = 0u;
+        else if (d + 32 > P.num_docs) keep = (1u << (P.num_docs - d)) - 1u;
+        m[w] = ~m[w] & keep;
+      }
+    } else {
+      uint32_t* a = stk[sp - 2];
+      const uint32_t* b = stk[sp - 1];
+      for (int w = tid; w < 2048; w += 256) a[w] = op == RP_AND ? (a[w] & b[w]) : (a[w] | b[w]);
+      --sp;
+    }
+    __syncthreads();
+  }
+  uint32_t* out = P.mask + static_cast<size_t>(chunk) * 2048;
+  for (int w = tid; w < 2048; w += 256) out[w] = stk[0][w];
+}
+
 // ---------------------------------------------------------------------------------------------
 // High-cardinality group-by (LONG_MAP semantics, DefaultGroupKeyGenerator.java:239-246 / :429-441): the reference
 // probes a Long2IntOpenHashMap per doc; at 10^7 groups a device-wide hash table turns every row into random HBM atomics.
@@ -1113,5 +1161,14 @@ extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const u
   if (nsegs > 0)
     hipLaunchKernelGGL(pgx::pgx_fsm_compose, dim3(nsegs), dim3(256), 0, stream, segs, S, T, cnt, stv, pcount, pstate,
                        stats);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
+                                                 int maxchunks, hipStream_t stream) {
+  if (nprogs <= 0 || maxchunks <= 0) return hipSuccess;
+  const long long blocks = static_cast<long long>(nprogs) * maxchunks;
+  hipLaunchKernelGGL(pgx::pgx_roaring_program, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, progs, descs,
+                     nprogs, maxchunks);
   return hipGetLastError();
 }

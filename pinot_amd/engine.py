@@ -100,6 +100,8 @@ class _ColInfo:
             return lo if lo < len(padded) and padded[lo] == key else -(lo + 1)
         if dt in ("INT", "LONG"):
             v = int(raw)  # Integer.parseInt / Long.parseLong semantics (raises on non-integers)
+        elif dt == "FLOAT":
+            v = float(np.float32(float(raw)))  # Float.parseFloat: the lookup is a float
         else:
             v = float(raw)
         arr = self.values
@@ -448,21 +450,33 @@ class _Query:
         self.handle = h
         self.group_cols = gcols
 
-    def bindings(self, segments: Sequence[IndexSegment]):
-        nl = len(self.leaves)
-        arr = (N.LeafBinding * max(1, len(segments) * nl))()
-        keep = []
-        for s, seg in enumerate(segments):
+    def predicates(self):
+        """The leaves' raw predicate values for pgx_bind_predicates (a-4 runs inside the library)."""
+        if getattr(self, "_preds", None) is None:
+            keep = []
+            arr = (N.Predicate * max(1, len(self.leaves)))()
             for l, leaf in enumerate(self.leaves):
-                lo, hi, words = resolve_leaf(seg.column(leaf["column"]), leaf)
-                b = arr[s * nl + l]
-                b.lo, b.hi = lo, hi
-                if words is not None:
-                    keep.append(words)
-                    b.words = words.ctypes.data_as(C.POINTER(C.c_uint32))
+                if leaf["op"] == "RANGE":
+                    lower, upper, inc_lo, inc_hi = _parse_range(leaf["values"][0])
+                    vals = [lower, upper]
+                    arr[l].lower_inclusive, arr[l].upper_inclusive = int(inc_lo), int(inc_hi)
                 else:
-                    b.words = None
-        return arr, keep
+                    vals = list(leaf["values"])
+                cv = (C.c_char_p * max(1, len(vals)))(*[v.encode("utf-8") for v in vals])
+                keep.append(cv)
+                arr[l].num_values = len(vals)
+                arr[l].values = cv
+            self._preds = (arr, keep)
+        return self._preds[0]
+
+    def bindings(self, segments: Sequence[IndexSegment]):
+        """[segment][leaf] dictId-space bindings (PredicateEvaluatorProvider per segment), resolved by the library.
+        Returns (binding array, owner): keep the owner alive while the array is in use."""
+        segs = (C.c_void_p * max(1, len(segments)))(*[s.handle.value for s in segments])
+        h = C.c_void_p()
+        N.check(N.lib().pgx_bind_predicates(self.handle, segs, len(segments), self.predicates(), C.byref(h)))
+        owner = _Bindings(h)
+        return N.lib().pgx_bindings_array(h), owner
 
     def execute(self, segments: Sequence[IndexSegment], flags: int = 0, dense_out=None, dense_out_bytes: int = 0):
         segs = (C.c_void_p * len(segments))(*[s.handle.value for s in segments])
@@ -483,6 +497,18 @@ class _Query:
             self.close()
         except Exception:
             pass
+
+
+class _Bindings:
+    """Owner of a pgx_bindings handle."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        if self.h:
+            N.lib().pgx_bindings_release(self.h)
+            self.h = None
 
 
 def decode_result(q: _Query, r, segments: Sequence[IndexSegment], trim: bool = False) -> IntermediateResultsBlock:

@@ -70,6 +70,11 @@ class LeafBinding(C.Structure):
     _fields_ = [("lo", C.c_int32), ("hi", C.c_int32), ("words", C.POINTER(C.c_uint32))]
 
 
+class Predicate(C.Structure):
+    _fields_ = [("num_values", C.c_int32), ("values", C.POINTER(C.c_char_p)), ("lower_inclusive", C.c_int32),
+                ("upper_inclusive", C.c_int32)]
+
+
 class ExecOpts(C.Structure):
     _fields_ = [("stream", C.c_uint64), ("dense_out", C.c_void_p), ("dense_out_bytes", C.c_uint64),
                 ("flags", C.c_uint32)]
@@ -115,6 +120,10 @@ EXPORTS = {
     "pgx_device_alloc": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "pgx_device_free": (C.c_int, [C.c_void_p, C.c_void_p]),
     "pgx_copy_to_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "pgx_bind_predicates": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(Predicate),
+                                      C.POINTER(C.c_void_p)]),
+    "pgx_bindings_array": (C.POINTER(LeafBinding), [C.c_void_p]),
+    "pgx_bindings_release": (C.c_int, [C.c_void_p]),
     "pgx_execute_timed": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(LeafBinding),
                                     C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_void_p)]),
 }
