@@ -169,8 +169,11 @@ def main():
     if req.get("group_by") and world > 1:
         slots = C.c_int64()
         N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
-        dense = slots.value <= (1 << 22)  # dense key space: RCCL all-reduce of the tables; else the
-        # sparse groups are gathered to rank 0 by key value, merged and trimmed there (multigpu.merge_group_partials)
+        # dense key space on every rank with identical dictionaries: RCCL all-reduce of the tables; else
+        # the groups merge by key VALUE (multigpu.merge_group_partials)
+        fps = multigpu.dictionary_fingerprint([[s.column(c).values for s in segs] for c in q.group_cols])
+        agree = multigpu.dense_layout_agrees(slots.value, fps, device="cuda:%d" % local)
+        dense = slots.value <= (1 << 22) and agree
     if dense:
         nplanes = 1 + len(req["aggregations"])
         for p in range(nplanes):

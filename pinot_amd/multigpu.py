@@ -29,6 +29,40 @@ def shard(num_segments: int, world: int, rank: int, scaling: str) -> List[int]:
     return list(range(rank, num_segments, world))
 
 
+def dictionary_fingerprint(columns_values: Sequence[Sequence]) -> List[int]:
+    """Per group-by column: a 63-bit fingerprint of the union of this rank's dictionary values for the column (the
+    rank-local global dictionary build_global_dict builds: sorted distinct values)."""
+    import hashlib
+    out = []
+    for values in columns_values:
+        parts = [np.asarray(v) for v in values if len(v)]
+        if not parts:
+            u = np.zeros(0)
+        elif parts[0].dtype.kind in "OSU":
+            u = np.array(sorted({str(x) for p in parts for x in p.tolist()}), dtype=object)
+        else:
+            u = np.unique(np.concatenate(parts).astype(np.float64 if parts[0].dtype.kind == "f" else np.int64))
+        h = hashlib.blake2b(digest_size=8)
+        h.update(str(u.dtype).encode())
+        h.update("\x1f".join(map(str, u.tolist())).encode("utf-8") if u.dtype == object else u.tobytes())
+        out.append(int.from_bytes(h.digest(), "little") >> 1)
+    return out
+
+
+def dense_layout_agrees(slots: int, fingerprints: Sequence[int], device=None) -> bool:
+    """True iff every rank has the same dense slot count and the same per-column dictionaries, i.e. slot i means the
+    same group on every GPU and the tables can be all-reduced plane by plane.  Otherwise (different value sets across
+    GPUs) the group-by must merge by key VALUE (MCombineGroupByOperator.java:166-191 keys the combine by the value
+    string): the sparse path.  Two tiny all-reduces (MIN and MAX) decide it identically on every rank."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([int(slots)] + [int(f) for f in fingerprints], dtype=torch.int64, device=device)
+    lo, hi = t.clone(), t.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+    return bool(torch.equal(lo, hi))
+
+
 def merge_dense_planes(t, plane_ops: Sequence[int]) -> None:
     """In-place all-reduce of a dense partial group table `t` (int64 tensor, len(plane_ops) planes x slots)."""
     import torch

@@ -142,7 +142,8 @@ def _sparse_segments():
 
 def _partial_arrays(merged, fns):
     keys = list(merged)
-    cols = [np.array([int(k.split("\t")[c]) for k in keys], dtype=np.int64) for c in range(2)]
+    ncols = len(keys[0].split("\t")) if keys else 2
+    cols = [np.array([int(k.split("\t")[c]) for k in keys], dtype=np.int64) for c in range(ncols)]
     vals = np.zeros((len(fns), len(keys)))
     cnts = np.zeros((len(fns), len(keys)), dtype=np.int64)
     for j, k in enumerate(keys):
@@ -219,3 +220,67 @@ def test_two_rank_sparse_group_merge_and_trim_match_oracle_combine():
                       for v in exp["trimmed"][i].values())
         assert len(got) == len(want) == exp["trim_size"]
         np.testing.assert_allclose(got, want, rtol=1e-9)
+
+
+# ------------------------------------------------------------------------------------------------
+# Dense key identity across ranks: slot i of a dense table means the same group on every GPU only
+# when every rank built the same global dictionaries; otherwise the merge goes by key value.
+# ------------------------------------------------------------------------------------------------
+def _dict_segments(rank):
+    """Rank-specific value sets: rank 1's group column holds values rank 0 never sees (and misses some of rank 0's)."""
+    from oracle import pinot_oracle as O
+    rng = np.random.default_rng(40 + rank)
+    segs = []
+    for s in range(2):
+        n = 3000
+        g = rng.choice(np.arange(rank * 7, rank * 7 + 40), n)  # rank 0: 0..39, rank 1: 7..46
+        segs.append(O.OSegment.from_raw({"g": g.astype(np.int32), "m": rng.integers(0, 1000, n).astype(np.int32)}))
+    return segs
+
+
+def _dict_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oracle import pinot_oracle as O
+    from pinot_amd import pql
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        segs = _dict_segments(rank)
+        same = multigpu.dictionary_fingerprint([[np.arange(40)]])
+        differ = multigpu.dictionary_fingerprint([[s.columns["g"].dictionary for s in segs]])
+        checks = (multigpu.dense_layout_agrees(40, same),          # identical dictionaries, same slots
+                  multigpu.dense_layout_agrees(40 + rank, same),   # slot counts differ
+                  multigpu.dense_layout_agrees(40, differ))        # same slot count, different values
+        req = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY g")
+        fns = [a["fn"] for a in req["aggregations"]]
+        local = O.combine_group_by([O.run_group_by(s, req) for s in segs], req)["merged"]
+        parts = multigpu.gather_group_partials(*_partial_arrays(local, fns))
+        out = multigpu.merge_group_partials(fns, parts) if rank == 0 else None
+        q.put((rank, (checks, out)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_dense_layout_agreement_and_value_keyed_merge():
+    import torch.multiprocessing as mp
+    from oracle import pinot_oracle as O
+    from pinot_amd import pql
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dict_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in (0, 1):
+        assert res[r][0] == (True, False, False)  # every rank takes the same decision
+    cols, vals, cnts = res[0][1]
+    req = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY g")
+    exp = O.combine_group_by([O.run_group_by(s, req) for r in (0, 1) for s in _dict_segments(r)], req)["merged"]
+    got = {str(int(k)): [int(cnts[0, j]), vals[1, j], vals[2, j], vals[3, j]] for j, k in enumerate(cols[0])}
+    assert set(got) == set(exp) and len(got) == 47
+    for k, e in exp.items():
+        assert got[k] == [e[0], e[1], e[2], e[3]]
