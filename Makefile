@@ -31,7 +31,11 @@ build/pgx_trim.o: $(CSRC)/pgx_trim.hip
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o build/pgx_trim.o build/pgx_stats.o
+build/pgx_merge.o: $(CSRC)/pgx_merge.hip
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o build/pgx_trim.o build/pgx_stats.o build/pgx_merge.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 
 clean:

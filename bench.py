@@ -164,6 +164,7 @@ def main():
     L = N.lib()
 
     dense = False
+    agree = False
     dense_t = None
     plane_ops = []
     if req.get("group_by") and world > 1:
@@ -212,13 +213,23 @@ def main():
             return out
         opts = N.ExecOpts(0, None, 0, 0)
         N.check(L.pgx_execute(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
-        if req.get("group_by") and world > 1:  # sparse keys: host merge of every rank's groups, then trimToSize
-            fns = [a["fn"] for a in req["aggregations"]]
-            parts = multigpu.gather_group_partials(*E.group_partials(q, r, segs))
-            if rank == 0:
-                cols, vals, cnts = multigpu.merge_group_partials(fns, parts)
-                kept = multigpu.trim_to_size(fns, vals, cnts, req["group_by"].get("top_n", 10))
-                merged[0] = E.render_group_maps(q, segs, cols, vals, cnts, kept)
+        if req.get("group_by") and world > 1:  # sparse keys
+            dev = "cuda:%d" % local
+            n = C.c_int64()
+            resident = L.pgx_result_device_groups(r, C.byref(n), None) == 0
+            flag = torch.tensor([int(agree and resident)], dtype=torch.int64, device=dev)
+            torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
+            if flag.item():  # one key space, groups in HBM: all-to-all by key hash + device merge + device trim
+                maps, _total, _st = multigpu.device_sparse_merge(ctx, q, r, segs, dev)
+                if rank == 0:
+                    merged[0] = maps
+            else:  # dictionaries differ across ranks: host merge of every rank's groups by VALUE, then trimToSize
+                fns = [a["fn"] for a in req["aggregations"]]
+                parts = multigpu.gather_group_partials(*E.group_partials(q, r, segs))
+                if rank == 0:
+                    cols, vals, cnts = multigpu.merge_group_partials(fns, parts)
+                    kept = multigpu.trim_to_size(fns, vals, cnts, req["group_by"].get("top_n", 10))
+                    merged[0] = E.render_group_maps(q, segs, cols, vals, cnts, kept)
         elif req.get("group_by"):  # the server's combine output: trimToSize, kept groups read back (a-19)
             E.trim_and_gather(q, r)
         if world > 1 and not req.get("group_by"):  # aggregation-only: combine the scalar partials across GPUs

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGX_ABI_VERSION 2
+#define PGX_ABI_VERSION 3
 
 typedef enum {
   PGX_OK = 0,
@@ -196,7 +196,40 @@ typedef struct {
  * (the combine).  bindings is [n][num_leaves].  Synchronous w.r.t. the returned result. */
 pgx_status pgx_execute(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
                        const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out);
-pgx_status pgx_result_release(pgx_result* r);
+pgx_status pgx_result_release(pgx_result* r);  /* an async result waits for its execution first */
+
+/* Asynchronous execute (SURVEY 8b "async on the stream, then pgx_result_wait"): returns at once with a pending result
+ * while the query plans, launches on the context's stream (or opts->stream) and reads back on a library thread.  The
+ * segment list, the bindings (including their bitsets) and opts are copied before the call returns; the query and the
+ * segments must stay alive until the result is complete.  Every pgx_result_* accessor waits for completion first.
+ * Replaces the per-query task the reference submits to its executor (query/executor/ServerQueryExecutorV1Impl.java:
+ * 118-134 -> plan/CombinePlanNode.java:66-124 futures). */
+pgx_status pgx_execute_async(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
+                             const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out);
+/* timeout_ms < 0: wait until done.  PGX_ERR_TIMEOUT if still running; otherwise the execution's own status. */
+pgx_status pgx_result_wait(pgx_result* r, int64_t timeout_ms);
+
+/* Multi-GPU in one process (SURVEY 8b/8e pgx_execute_multi): ctxs[k] is the context of one device; every segment runs
+ * on the device it was staged on (segments never move per query).  The per-device executions run concurrently and
+ * their partials merge on ctxs[0]'s device: one key space over ALL segments (the union dictionary per group-by
+ * column), dense tables copied over xGMI (hipMemcpyPeerAsync) and reduced plane by plane, device-resident sparse groups
+ * copied and merged by a device hash merge (pgx_merge.hip), the rest by key on the host.  Group keys of the result
+ * index into THIS segs[] list.  opts: flags only (stream / dense_out must be 0).  Replaces the reference server's one
+ * combine over all of its segments (operator/MCombineOperator.java:84-199, MCombineGroupByOperator.java:139-233). */
+pgx_status pgx_execute_multi(pgx_ctx* const* ctxs, int32_t nctx, const pgx_query* q, pgx_segment* const* segs,
+                             int32_t n, const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out);
+
+/* Cross-process merge of sparse group-by results (one process per GPU; the caller exchanges the groups, e.g. an RCCL
+ * all-to-all by key hash).  A group travels as a record of 5 uint64: packed group key, doc count, int64 sum, ordered
+ * min, ordered max (the layout of the partitioned sparse group-by).  pgx_result_device_groups: *n = the number of
+ * groups of a result whose groups stay in device memory (PGX_ERR_UNSUPPORTED otherwise) and, when records is
+ * non-NULL, the records written to that device buffer (n x 40 bytes, on the result's device).
+ * pgx_result_merge_groups: merge n records (equal keys combine) into a device-resident result decoded with `like`'s
+ * key tables -- valid when every source planned the same key space (identical dictionaries on all ranks); stats
+ * (may be NULL: like's) become the result's ExecutionStatistics. */
+pgx_status pgx_result_device_groups(const pgx_result* r, int64_t* n, void* records);
+pgx_status pgx_result_merge_groups(pgx_ctx* ctx, const pgx_result* like, const void* records, int64_t n,
+                                   const int64_t stats[4], pgx_result** out);
 
 /* ExecutionStatistics: numDocsScanned, numEntriesScannedInFilter, numEntriesScannedPostFilter, totalRawDocs
  * (operator/ExecutionStatistics.java:21-74). */
@@ -255,6 +288,7 @@ pgx_status pgx_inverted_index_build(const int32_t* ids, int64_t n, int32_t card,
 pgx_status pgx_device_alloc(pgx_ctx* ctx, uint64_t bytes, void** out);
 pgx_status pgx_device_free(pgx_ctx* ctx, void* p);
 pgx_status pgx_copy_to_device(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+pgx_status pgx_copy_to_host(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 
 /* ---- timing (bench): run the query `iters` times back to back, returning per-launch kernel times of
  * the dominant kernel measured with HIP events on the stream it is launched on. */

@@ -66,6 +66,16 @@ extern "C" size_t pgx_trim_state_bytes(void);
 extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
                                      int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
                                      uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream);
+extern "C" hipError_t pgx_launch_dense_reduce(unsigned long long* dst, const unsigned long long* src, uint64_t slots,
+                                              int nplanes, uint64_t ops, hipStream_t stream);
+extern "C" hipError_t pgx_launch_group_merge(const uint64_t* key, const uint64_t* pl, int64_t es, int64_t ps,
+                                             int64_t n, unsigned long long* tkey, unsigned long long* tpl,
+                                             uint64_t cap, unsigned long long* overflow, hipStream_t stream);
+extern "C" hipError_t pgx_launch_group_pack(const uint64_t* okey, const uint64_t* opl, int64_t ocap, int64_t n,
+                                            uint64_t* rec, hipStream_t stream);
+extern "C" hipError_t pgx_launch_group_compact(const unsigned long long* tkey, const unsigned long long* tpl,
+                                               uint64_t cap, uint64_t* okey, uint64_t* opl, int64_t ocap,
+                                               unsigned long long* counter, hipStream_t stream);
 struct pgx_ctx;
 extern "C" void ctx_unref(pgx_ctx* ctx);
 
@@ -168,7 +178,9 @@ struct WorkerPool {
         }
       });
   }
+  std::mutex run_mu;  // one job at a time: concurrent pgx_execute calls on one context take turns here
   void run(int n, const std::function<void(int)>& f) {
+    std::lock_guard<std::mutex> one(run_mu);
     std::unique_lock<std::mutex> g(m);
     job = &f;
     njobs = n;
@@ -656,6 +668,28 @@ struct pgx_bindings {
   std::vector<std::vector<uint32_t>> words;  // owned bitsets (arr[i].words points into these)
 };
 
+// pgx_execute_async: the query runs on a host thread of its own (planning, the launches on the context's stream, the
+// read-back); the submitting thread returns at once.  The inputs the caller owns only for the duration of the call (the
+// segment list, the bindings and their bitsets, the options) are copied here first.
+struct AsyncState {
+  std::thread th;
+  std::mutex m, join_mu;
+  std::condition_variable cv;
+  bool done = false;
+  pgx_status status = PGX_OK;
+  std::string msg;
+  std::vector<pgx_segment*> segs;
+  std::vector<pgx_leaf_binding> binds;
+  std::vector<std::vector<uint32_t>> words;
+  pgx_exec_opts opts{};
+  bool has_opts = false;
+  void join() {
+    std::lock_guard<std::mutex> g(join_mu);
+    if (th.joinable()) th.join();
+  }
+  ~AsyncState() { join(); }
+};
+
 struct pgx_result {
   int64_t stats[4] = {0, 0, 0, 0};
   int num_aggs = 0;
@@ -688,6 +722,8 @@ struct pgx_result {
     }
   };
   std::unique_ptr<Lazy> lazy;
+  std::unique_ptr<AsyncState> async;  // declared last: destroyed (joined) before the fields its thread writes
+  void ready() const;                 // waits for an async execution; throws its error
   void materialize();
   const std::vector<int64_t>& device_trim(int fn, int64_t size);
   void decode_lazy(const uint64_t* keys, const uint64_t* planes, int64_t n, int64_t out_stride, int32_t* seg_index,
@@ -860,6 +896,41 @@ GlobalDict build_global_dict(pgx_segment* const* segs, int n, const std::string&
   }
   g.card = gid + 1;
   return g;
+}
+
+// Reference storage mode of a single segment (DefaultGroupKeyGenerator.java:167-186): 0 ARRAY_BASED, 1 LONG_MAP_BASED,
+// 2 ARRAY_MAP_BASED.
+int reference_mode(const pgx_query& q, const pgx_segment* seg) {
+  int64_t p1 = 1;
+  bool ov = false;
+  for (const auto& g : q.group_cols) {
+    const int64_t cc = seg->col(g).card;
+    if (!ov && p1 > std::numeric_limits<int64_t>::max() / cc) ov = true;
+    else if (!ov) p1 *= cc;
+  }
+  return ov ? 2 : (p1 > 10000 ? 1 : 0);
+}
+
+// Key identity of a query whose segments run on several devices (pgx_execute_multi): the global dictionaries are built
+// once over ALL segments, and each device's plan takes its segments' rows of them, so a packed key or dense slot
+// means the same group on every device and the per-device partials merge without a remap.
+struct Domain {
+  const std::vector<GlobalDict>* g = nullptr;  // per group column, over the full segment list
+  std::vector<int> index;                      // this device's segment i -> position in the full list
+};
+
+GlobalDict domain_dict(const Domain& d, int col, int n) {
+  const GlobalDict& full = (*d.g)[col];
+  GlobalDict r;
+  r.card = full.card;
+  r.identity = full.identity;
+  r.rep_seg = full.rep_seg;  // positions in the FULL segment list: the merged result is decoded against it
+  r.rep_id = full.rep_id;
+  if (!full.identity) {
+    r.remap.resize(n);
+    for (int s = 0; s < n; ++s) r.remap[s] = full.remap[d.index[s]];
+  }
+  return r;
 }
 
 int bits_for(int64_t card) {
@@ -1444,7 +1515,7 @@ void prof_mark(const char* what) {
 }
 
 void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
-                uint32_t xflags, ExecPlan& P) {
+                uint32_t xflags, ExecPlan& P, const Domain* dom = nullptr) {
   if (n < 1) fail(PGX_ERR_INVALID_ARG, "no segments");
   if (q.agg_fn.size() > size_t(kMaxAggs)) fail(PGX_ERR_UNSUPPORTED, "too many aggregation functions");
   if (q.group_cols.size() > size_t(kMaxGroupCols)) fail(PGX_ERR_UNSUPPORTED, "too many group-by columns");
@@ -1487,24 +1558,14 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     P.gdicts.clear();
     for (int g = 0; g < K.num_gcols; ++g) {
       K.gcol[g] = int8_t(qslot(P, q.group_cols[g]));
-      P.gdicts.push_back(build_global_dict(segs, n, q.group_cols[g]));
+      P.gdicts.push_back(dom ? domain_dict(*dom, g, n) : build_global_dict(segs, n, q.group_cols[g]));
       const int64_t gc = P.gdicts.back().card;
       if (!overflow && prod > (uint64_t(1) << 62) / uint64_t(gc)) overflow = true;
       if (!overflow) prod *= uint64_t(gc);
       P.gbits.push_back(bits_for(gc));
       total_bits += P.gbits.back();
     }
-    // Reference storage mode of a single segment (DefaultGroupKeyGenerator.java:167-186)
-    {
-      int64_t p1 = 1;
-      bool ov = false;
-      for (const auto& g : q.group_cols) {
-        const int64_t cc = segs[0]->col(g).card;
-        if (!ov && p1 > std::numeric_limits<int64_t>::max() / cc) ov = true;
-        else if (!ov) p1 *= cc;
-      }
-      P.mode_ref = ov ? 2 : (p1 > 10000 ? 1 : 0);
-    }
+    P.mode_ref = reference_mode(q, segs[0]);
     const uint64_t kDenseMax = uint64_t(1) << 22;
     if (!overflow && prod <= kDenseMax && !(xflags & PGX_X_FORCE_HASH)) {
       uint64_t mul = 1;
@@ -2824,14 +2885,14 @@ struct HostProf {
 };
 
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
-               const pgx_exec_opts* opts, pgx_result* R) {
+               const pgx_exec_opts* opts, pgx_result* R, const Domain* dom = nullptr) {
   HostProf hp;
   if (hp.on) g_prof_mark = [&hp](const char* w) { hp.mark(w); };
   struct Unmark { ~Unmark() { g_prof_mark = nullptr; } } unmark;
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
   const uint32_t xflags = opts ? opts->flags : 0;
   ExecPlan P;
-  plan_query(ctx, q, segs, n, bindings, xflags, P);
+  plan_query(ctx, q, segs, n, bindings, xflags, P, dom);
   hp.mark("plan");
   ExecBuffers B;
   upload_plan(ctx, P, B, st);
@@ -2880,7 +2941,268 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   hp.mark("finish");
 }
 
+// -------------------------------------------------------------------------------------------------
+// Merging group-by partials of different devices (MCombineGroupByOperator.java:166-191 semantics: equal
+// keys combine with each function's combineTwoValues).
+// -------------------------------------------------------------------------------------------------
+// Sparse groups resident in device memory (packed keys; planes count / int64 sum / ordered min / ordered max: group i
+// key keys[i * es], plane p planes[p * ps + i * es]) -> one device-resident result decoded with `like`'s key tables
+// (pgx_merge.hip).
+void merge_device_groups(pgx_ctx* ctx, hipStream_t st, const uint64_t* keys, const uint64_t* planes, int64_t es,
+                         int64_t ps, int64_t n, const pgx_result::Lazy& like, pgx_result* R) {
+  uint64_t cap = 1024;
+  while (cap < uint64_t(std::max<int64_t>(n, 1)) * 2) cap <<= 1;
+  DevBuf tkey(ctx, cap * 8), tpl(ctx, cap * 4 * 8), ctr(ctx, 64);
+  const int64_t ocap = std::max<int64_t>(n, 1);
+  DevBuf okey(ctx, size_t(ocap) * 8), oplane(ctx, size_t(ocap) * 4 * 8);
+  unsigned long long* tp = tpl.as<unsigned long long>();
+  hip_check(hipMemsetAsync(tkey.p, 0xFF, cap * 8, st), "merge table");
+  hip_check(hipMemsetAsync(tp, 0, cap * 2 * 8, st), "merge table");          // count, sum
+  hip_check(hipMemsetAsync(tp + 2 * cap, 0xFF, cap * 8, st), "merge table"); // ordered min
+  hip_check(hipMemsetAsync(tp + 3 * cap, 0, cap * 8, st), "merge table");    // ordered max
+  hip_check(hipMemsetAsync(ctr.p, 0, 16, st), "merge counters");
+  unsigned long long* c = ctr.as<unsigned long long>();
+  hip_check(pgx_launch_group_merge(keys, planes, es, ps, n, tkey.as<unsigned long long>(), tp, cap, c + 1, st),
+            "group merge");
+  hip_check(pgx_launch_group_compact(tkey.as<unsigned long long>(), tp, cap, okey.as<uint64_t>(),
+                                     oplane.as<uint64_t>(), ocap, c, st),
+            "group compact");
+  unsigned long long h[2] = {0, 0};
+  hip_check(hipMemcpyAsync(h, c, 16, hipMemcpyDeviceToHost, st), "merge counters D2H");
+  hip_check(hipStreamSynchronize(st), "sync");
+  if (h[1]) fail(PGX_ERR_INTERNAL, "group merge table overflow");
+  R->group_by = true;
+  R->num_groups = int64_t(std::min<unsigned long long>(h[0], uint64_t(ocap)));
+  auto L = std::make_unique<pgx_result::Lazy>();
+  L->okey = std::move(okey);
+  L->oplane = std::move(oplane);
+  L->ocap = ocap;
+  L->gshift = like.gshift;
+  L->gbits = like.gbits;
+  L->rep_seg = like.rep_seg;
+  L->rep_id = like.rep_id;
+  L->agg_kind = like.agg_kind;
+  ctx->refs.fetch_add(1);
+  L->ctx = ctx;
+  R->lazy = std::move(L);
+}
+
+// Combine of one function's partial (value, count) into an accumulated one (the host-side combineTwoValues).
+void combine_partial(int fn, double& v, int64_t& c, double v2, int64_t c2) {
+  if (fn == PGX_MIN) v = std::min(v, v2);
+  else if (fn == PGX_MAX) v = std::max(v, v2);
+  else if (fn == PGX_COUNT) v = double(c + c2);
+  else v += v2;  // SUM, AVG sum
+  c += c2;
+}
+
+// Host merge of materialised group-by results whose keys come from one Domain (equal global ids <=> equal
+// (rep segment, rep dictId) pairs, so the pairs key the merge).
+void merge_host_groups(std::vector<std::unique_ptr<pgx_result>>& parts, pgx_result* R) {
+  const int ncols = int(parts[0]->key_seg.size()), na = parts[0]->num_aggs;
+  std::unordered_map<std::string, int64_t> where;
+  R->key_seg.assign(ncols, {});
+  R->key_id.assign(ncols, {});
+  R->g_value.assign(na, {});
+  R->g_count.assign(na, {});
+  std::string k(size_t(ncols) * 8, '\0');
+  for (auto& p : parts) {
+    for (int64_t i = 0; i < p->num_groups; ++i) {
+      for (int g = 0; g < ncols; ++g) {
+        std::memcpy(&k[size_t(g) * 8], &p->key_seg[g][i], 4);
+        std::memcpy(&k[size_t(g) * 8 + 4], &p->key_id[g][i], 4);
+      }
+      auto it = where.find(k);
+      if (it == where.end()) {
+        where.emplace(k, R->num_groups);
+        for (int g = 0; g < ncols; ++g) {
+          R->key_seg[g].push_back(p->key_seg[g][i]);
+          R->key_id[g].push_back(p->key_id[g][i]);
+        }
+        for (int a = 0; a < na; ++a) {
+          R->g_value[a].push_back(p->g_value[a][i]);
+          R->g_count[a].push_back(p->g_count[a][i]);
+        }
+        ++R->num_groups;
+      } else {
+        for (int a = 0; a < na; ++a)
+          combine_partial(R->agg_fn[a], R->g_value[a][it->second], R->g_count[a][it->second], p->g_value[a][i],
+                          p->g_count[a][i]);
+      }
+    }
+  }
+}
+
+// pgx_execute_multi: the segments run where they are staged (one thread per context, concurrently), then the partials
+// merge on the first context's device: aggregation-only on the host; dense tables over the shared key space are copied
+// to that device (hipMemcpyPeerAsync, xGMI between GPUs) and reduced plane by plane; sparse groups still in device
+// memory are copied there and merged by pgx_group_merge; anything else merges on the host by key.
+void run_multi(pgx_ctx* const* ctxs, int nctx, const pgx_query& q, pgx_segment* const* segs, int n,
+               const pgx_leaf_binding* bindings, uint32_t xflags, pgx_result* R) {
+  if (n < 1) fail(PGX_ERR_INVALID_ARG, "no segments");
+  std::vector<std::vector<int>> part(nctx);
+  for (int i = 0; i < n; ++i) {
+    int k = 0;
+    while (k < nctx && segs[i]->ctx != ctxs[k]) ++k;
+    if (k == nctx) fail(PGX_ERR_INVALID_ARG, "segment " + segs[i]->name + " is not staged on any of the contexts");
+    part[k].push_back(i);
+  }
+  std::vector<int> active;
+  for (int k = 0; k < nctx; ++k)
+    if (!part[k].empty()) active.push_back(k);
+  const size_t L = q.leaf_col.size();
+  std::vector<GlobalDict> gd;
+  for (const auto& g : q.group_cols) gd.push_back(build_global_dict(segs, n, g));
+  uint64_t slots = 1;
+  bool dense = !q.group_cols.empty() && !(xflags & PGX_X_FORCE_HASH);
+  for (const auto& g : gd) {
+    if (slots > (uint64_t(1) << 22) / uint64_t(std::max<int64_t>(g.card, 1))) dense = false;
+    else slots *= uint64_t(g.card);
+  }
+  const int nplanes = 1 + int(q.agg_fn.size());
+  const int na = int(q.agg_fn.size());
+  uint64_t ops = 0;  // dense plane ops, 2 bits per plane (pgx_query_dense_plane_op)
+  for (int a = 0; a < na; ++a) {
+    const int fn = q.agg_fn[a];
+    int op = P_ADD_I64;
+    if (fn != PGX_COUNT) {
+      const StagedColumn& c = segs[0]->col(q.agg_col[a]);
+      const bool fp = c.data_type == PGX_FLOAT || c.data_type == PGX_DOUBLE;
+      op = fn == PGX_MIN ? P_MIN_ORD : fn == PGX_MAX ? P_MAX_ORD : (fp ? P_ADD_F64 : P_ADD_I64);
+    }
+    ops |= uint64_t(op) << (2 * (a + 1));
+  }
+  const int na_ctx = int(active.size());
+  std::vector<Domain> dom(na_ctx);
+  std::vector<std::vector<pgx_segment*>> sub(na_ctx);
+  std::vector<std::vector<pgx_leaf_binding>> sb(na_ctx);
+  std::vector<std::unique_ptr<pgx_result>> res(na_ctx);
+  std::vector<DevBuf> tables(na_ctx);
+  std::vector<std::exception_ptr> errs(na_ctx);
+  const uint64_t tbytes = slots * uint64_t(nplanes) * 8;
+  for (int j = 0; j < na_ctx; ++j) {
+    const int k = active[j];
+    dom[j].g = &gd;
+    dom[j].index = part[k];
+    for (int i : part[k]) {
+      sub[j].push_back(segs[i]);
+      if (L) sb[j].insert(sb[j].end(), bindings + size_t(i) * L, bindings + size_t(i + 1) * L);
+    }
+    res[j] = std::make_unique<pgx_result>();
+  }
+  auto run_one = [&](int j) {
+    pgx_ctx* c = ctxs[active[j]];
+    hip_check(hipSetDevice(c->device), "hipSetDevice");
+    pgx_exec_opts o{};
+    o.flags = xflags & ~uint32_t(PGX_X_KEEP_DENSE_ON_DEVICE);
+    if (dense) {
+      tables[j] = DevBuf(c, tbytes);
+      o.dense_out = tables[j].p;
+      o.dense_out_bytes = tbytes;
+      o.flags |= PGX_X_KEEP_DENSE_ON_DEVICE;
+    }
+    run_query(c, q, sub[j].data(), int(sub[j].size()), L ? sb[j].data() : nullptr, &o, res[j].get(), &dom[j]);
+  };
+  {
+    std::vector<std::thread> th;
+    for (int j = 1; j < na_ctx; ++j)
+      th.emplace_back([&, j] {
+        try {
+          run_one(j);
+        } catch (...) {
+          errs[j] = std::current_exception();
+        }
+      });
+    try {
+      run_one(0);
+    } catch (...) {
+      errs[0] = std::current_exception();
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+  }
+  pgx_ctx* c0 = ctxs[active[0]];
+  hip_check(hipSetDevice(c0->device), "hipSetDevice");
+  hipStream_t st = c0->stream;
+  int64_t stats[4] = {0, 0, 0, 0};
+  for (auto& r : res)
+    for (int i = 0; i < 4; ++i) stats[i] += r->stats[i];
+  if (q.group_cols.empty()) {
+    *R = std::move(*res[0]);
+    for (int j = 1; j < na_ctx; ++j)
+      for (int a = 0; a < na; ++a)
+        combine_partial(q.agg_fn[a], R->agg_value[a], R->agg_count[a], res[j]->agg_value[a], res[j]->agg_count[a]);
+  } else if (dense) {
+    unsigned long long* t0 = tables[0].as<unsigned long long>();
+    DevBuf stage;
+    for (int j = 1; j < na_ctx; ++j) {
+      const unsigned long long* src = tables[j].as<unsigned long long>();
+      if (tables[j].ctx->device != c0->device) {
+        if (!stage.p) stage = DevBuf(c0, tbytes);
+        hip_check(hipMemcpyPeerAsync(stage.p, c0->device, tables[j].p, tables[j].ctx->device, tbytes, st),
+                  "dense table peer copy");
+        src = stage.as<unsigned long long>();
+      }
+      hip_check(pgx_launch_dense_reduce(t0, src, slots, nplanes, ops, st), "dense reduce");
+    }
+    std::vector<unsigned long long> host(slots * nplanes);
+    hip_check(hipMemcpyAsync(host.data(), t0, tbytes, hipMemcpyDeviceToHost, st), "dense D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    ExecPlan P;
+    std::vector<pgx_leaf_binding> none(sub[0].size() * L, pgx_leaf_binding{0, -1, nullptr});
+    plan_query(c0, q, sub[0].data(), int(sub[0].size()), none.data(), xflags, P, &dom[0]);
+    ExecBuffers B;
+    B.host = PinnedBuf(c0, kOutsBytes);
+    B.off_outs = 0;
+    std::memset(B.host.p, 0, kOutsBytes);
+    reinterpret_cast<unsigned long long*>(B.host.p)[16] = static_cast<unsigned long long>(stats[0]);
+    finish_result(c0, q, P, B, sub[0].data(), int(sub[0].size()), st, R, host.data());
+  } else {
+    bool all_lazy = true;
+    for (auto& r : res) all_lazy = all_lazy && r->lazy;
+    *R = pgx_result();
+    R->num_aggs = na;
+    R->agg_fn = q.agg_fn;
+    R->group_by = true;
+    if (all_lazy) {
+      int64_t total = 0;
+      for (auto& r : res) total += r->num_groups;
+      DevBuf keys(c0, size_t(std::max<int64_t>(total, 1)) * 8), pl(c0, size_t(std::max<int64_t>(total, 1)) * 32);
+      int64_t off = 0;
+      for (auto& r : res) {
+        const auto& Lz = *r->lazy;
+        const int64_t ng = r->num_groups;
+        if (!ng) continue;
+        hip_check(hipMemcpyPeerAsync(keys.as<uint64_t>() + off, c0->device, Lz.okey.p, Lz.ctx->device, ng * 8, st),
+                  "group keys peer copy");
+        for (int p = 0; p < 4; ++p)
+          hip_check(hipMemcpyPeerAsync(pl.as<uint64_t>() + p * total + off, c0->device,
+                                       Lz.oplane.as<uint64_t>() + p * Lz.ocap, Lz.ctx->device, ng * 8, st),
+                    "group planes peer copy");
+        off += ng;
+      }
+      merge_device_groups(c0, st, keys.as<uint64_t>(), pl.as<uint64_t>(), 1, total, total, *res[0]->lazy, R);
+    } else {
+      for (auto& r : res) r->materialize();
+      merge_host_groups(res, R);
+    }
+  }
+  for (int i = 0; i < 4; ++i) R->stats[i] = stats[i];
+  R->num_aggs = na;
+  R->agg_fn = q.agg_fn;
+  R->top_n = q.top_n;
+  R->group_by = !q.group_cols.empty();
+  if (R->group_by) R->mode = reference_mode(q, segs[0]);
+}
+
 }  // namespace
+
+void pgx_result::ready() const {
+  if (!async) return;
+  async->join();
+  if (async->status != PGX_OK) fail(async->status, async->msg);
+}
 
 // =================================================================================================
 // C ABI
@@ -3016,11 +3338,127 @@ pgx_status pgx_execute(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* seg
 }
 
 pgx_status pgx_result_release(pgx_result* r) {
-  return guarded([&] { delete r; });
+  return guarded([&] { delete r; });  // an async result joins its execution first (~AsyncState)
+}
+
+pgx_status pgx_execute_async(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
+                             const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out) {
+  return guarded([&] {
+    if (!ctx || !q || !segs || !out || n < 0) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    const size_t L = q->leaf_col.size();
+    if (L && !bindings) fail(PGX_ERR_INVALID_ARG, "filter leaves need bindings");
+    auto R = std::make_unique<pgx_result>();
+    R->async = std::make_unique<AsyncState>();
+    AsyncState& A = *R->async;
+    A.segs.assign(segs, segs + n);
+    if (L) {
+      A.binds.assign(bindings, bindings + size_t(n) * L);
+      A.words.reserve(A.binds.size());
+      for (size_t i = 0; i < A.binds.size(); ++i) {
+        pgx_leaf_binding& b = A.binds[i];
+        if (!b.words) continue;
+        const int card = segs[i / L]->col(q->leaf_col[i % L]).card;
+        A.words.emplace_back(b.words, b.words + (card + 31) / 32);
+        b.words = A.words.back().data();
+      }
+    }
+    if (opts) {
+      A.opts = *opts;
+      A.has_opts = true;
+    }
+    pgx_result* r = R.get();
+    A.th = std::thread([ctx, q, r] {
+      AsyncState& S = *r->async;
+      const pgx_status st = guarded([&] {
+        hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+        run_query(ctx, *q, S.segs.data(), int(S.segs.size()), S.binds.empty() ? nullptr : S.binds.data(),
+                  S.has_opts ? &S.opts : nullptr, r);
+      });
+      std::lock_guard<std::mutex> g(S.m);
+      S.status = st;
+      if (st != PGX_OK) S.msg = g_last_error;
+      S.done = true;
+      S.cv.notify_all();
+    });
+    *out = R.release();
+  });
+}
+
+pgx_status pgx_result_wait(pgx_result* r, int64_t timeout_ms) {
+  if (!r) {
+    g_last_error = "NULL argument";
+    return PGX_ERR_INVALID_ARG;
+  }
+  if (!r->async) return PGX_OK;
+  AsyncState& A = *r->async;
+  {
+    std::unique_lock<std::mutex> g(A.m);
+    if (timeout_ms < 0) {
+      A.cv.wait(g, [&] { return A.done; });
+    } else if (!A.cv.wait_for(g, std::chrono::milliseconds(timeout_ms), [&] { return A.done; })) {
+      g_last_error = "query still running";
+      return PGX_ERR_TIMEOUT;
+    }
+  }
+  A.join();
+  if (A.status != PGX_OK) g_last_error = A.msg;
+  return A.status;
+}
+
+pgx_status pgx_execute_multi(pgx_ctx* const* ctxs, int32_t nctx, const pgx_query* q, pgx_segment* const* segs,
+                             int32_t n, const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out) {
+  return guarded([&] {
+    if (!ctxs || nctx < 1 || !q || !segs || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    for (int k = 0; k < nctx; ++k)
+      if (!ctxs[k]) fail(PGX_ERR_INVALID_ARG, "NULL context");
+    if (!q->leaf_col.empty() && !bindings) fail(PGX_ERR_INVALID_ARG, "filter leaves need bindings");
+    if (opts && (opts->stream || opts->dense_out || (opts->flags & PGX_X_KEEP_DENSE_ON_DEVICE)))
+      fail(PGX_ERR_INVALID_ARG, "pgx_execute_multi takes flags only (each context runs on its own stream)");
+    auto R = std::make_unique<pgx_result>();
+    run_multi(ctxs, nctx, *q, segs, n, bindings, opts ? opts->flags : 0, R.get());
+    *out = R.release();
+  });
+}
+
+pgx_status pgx_result_device_groups(const pgx_result* r, int64_t* n, void* records) {
+  return guarded([&] {
+    if (!r || !n) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    r->ready();
+    if (!r->group_by || !r->lazy) fail(PGX_ERR_UNSUPPORTED, "the groups of this result are not in device memory");
+    *n = r->num_groups;
+    if (!records || !r->num_groups) return;
+    const auto& L = *r->lazy;
+    hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
+    hipStream_t st = L.ctx->stream;
+    hip_check(pgx_launch_group_pack(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, r->num_groups,
+                                    static_cast<uint64_t*>(records), st),
+              "group pack");
+    hip_check(hipStreamSynchronize(st), "sync");
+  });
+}
+
+pgx_status pgx_result_merge_groups(pgx_ctx* ctx, const pgx_result* like, const void* records, int64_t n,
+                                   const int64_t stats[4], pgx_result** out) {
+  return guarded([&] {
+    if (!ctx || !like || !out || n < 0 || (n && !records)) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    like->ready();
+    if (!like->group_by || !like->lazy) fail(PGX_ERR_UNSUPPORTED, "template result has no device-resident groups");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    auto R = std::make_unique<pgx_result>();
+    const uint64_t* rec = static_cast<const uint64_t*>(records);
+    merge_device_groups(ctx, ctx->stream, rec, rec + 1, 5, 1, n, *like->lazy, R.get());
+    R->num_aggs = like->num_aggs;
+    R->agg_fn = like->agg_fn;
+    R->top_n = like->top_n;
+    R->mode = like->mode;
+    for (int i = 0; i < 4; ++i) R->stats[i] = stats ? stats[i] : like->stats[i];
+    *out = R.release();
+  });
 }
 
 pgx_status pgx_result_stats(const pgx_result* r, int64_t out[4]) {
   return guarded([&] {
+    if (r) r->ready();
     if (!r || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     for (int i = 0; i < 4; ++i) out[i] = r->stats[i];
   });
@@ -3028,6 +3466,7 @@ pgx_status pgx_result_stats(const pgx_result* r, int64_t out[4]) {
 
 pgx_status pgx_result_agg(const pgx_result* r, int32_t fn, double* value, int64_t* count) {
   return guarded([&] {
+    if (r) r->ready();
     if (!r) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     if (r->group_by) fail(PGX_ERR_INVALID_ARG, "group-by result");
     if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
@@ -3038,6 +3477,7 @@ pgx_status pgx_result_agg(const pgx_result* r, int32_t fn, double* value, int64_
 
 pgx_status pgx_result_num_groups(const pgx_result* r, int64_t* n) {
   return guarded([&] {
+    if (r) r->ready();
     if (!r || !n) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     *n = r->num_groups;
   });
@@ -3045,6 +3485,7 @@ pgx_status pgx_result_num_groups(const pgx_result* r, int64_t* n) {
 
 pgx_status pgx_result_group_keys(const pgx_result* r, int32_t c, int32_t* seg_index, int32_t* dict_id) {
   return guarded([&] {
+    if (r) r->ready();
     if (!r || !r->group_by) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
     const_cast<pgx_result*>(r)->materialize();
     if (c < 0 || c >= int(r->key_seg.size())) fail(PGX_ERR_INVALID_ARG, "group column index");
@@ -3055,6 +3496,7 @@ pgx_status pgx_result_group_keys(const pgx_result* r, int32_t c, int32_t* seg_in
 
 pgx_status pgx_result_group_values(const pgx_result* r, int32_t fn, double* value, int64_t* count) {
   return guarded([&] {
+    if (r) r->ready();
     if (!r || !r->group_by) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
     if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
     const_cast<pgx_result*>(r)->materialize();
@@ -3065,6 +3507,7 @@ pgx_status pgx_result_group_values(const pgx_result* r, int32_t fn, double* valu
 
 pgx_status pgx_result_group_mode(const pgx_result* r, int32_t* mode) {
   return guarded([&] {
+    if (r) r->ready();
     if (!r || !mode) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     *mode = r->mode;
   });
@@ -3072,6 +3515,7 @@ pgx_status pgx_result_group_mode(const pgx_result* r, int32_t* mode) {
 
 pgx_status pgx_result_trim(const pgx_result* r, int32_t fn, int64_t* idx, int64_t* n) {
   return guarded([&] {
+    if (r) r->ready();
     if (!r || !r->group_by || !n) fail(PGX_ERR_INVALID_ARG, "not a group-by result");
     if (fn < 0 || fn >= r->num_aggs) fail(PGX_ERR_INVALID_ARG, "function index");
     const int64_t min_trim = std::max<int64_t>(r->top_n, 1000);
@@ -3109,6 +3553,7 @@ pgx_status pgx_result_trim(const pgx_result* r, int32_t fn, int64_t* idx, int64_
 pgx_status pgx_result_gather(const pgx_result* r, const int64_t* gi, int64_t n, int32_t* seg_index, int32_t* dict_id,
                              double* value, int64_t* count) {
   return guarded([&] {
+    if (r) r->ready();
     if (!r || !r->group_by || (n > 0 && !gi) || n < 0) fail(PGX_ERR_INVALID_ARG, "bad argument");
     for (int64_t j = 0; j < n; ++j)
       if (gi[j] < 0 || gi[j] >= r->num_groups) fail(PGX_ERR_INVALID_ARG, "group index out of range");
@@ -3215,6 +3660,14 @@ pgx_status pgx_copy_to_device(pgx_ctx* ctx, void* dst, const void* src, uint64_t
     if (!ctx || !dst || !src) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     hip_check(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "H2D");
+  });
+}
+
+pgx_status pgx_copy_to_host(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
+  return guarded([&] {
+    if (!ctx || (bytes && (!dst || !src))) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    hip_check(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "D2H");
   });
 }
 

@@ -1,0 +1,153 @@
+// Cross-GPU merge of per-device group-by partials, the device-side counterpart of the reference's
+// combine over segments served by different executors: operator/MCombineGroupByOperator.java:166-191 merges equal
+// group keys with each function's combineTwoValues (CountAggregationFunction.java:79-87 long add,
+// SumAggregationFunction.java:168-176 double add, Min/Max extremes, AvgAggregationFunction.java:116-125 pair add).
+//
+// * pgx_dense_reduce: dst op= src over dense tables of the same layout (slot s = the same group on every device: the
+//   plan's key space is the union dictionary of ALL segments of the query), one plane op per plane.  Streams both
+//   tables once (16 B read + 8 B written per slot and plane), HBM-bound.
+// * pgx_group_merge: sparse groups (packed key + planes count / int64 sum / ordered min / ordered max, the layout
+//   pgx_part_aggregate writes) from any number of devices, copied side by side into one buffer, are inserted into an
+//   open-addressing table in HBM (linear probing on a 64-bit mix of the key, one CAS per new key, then one atomic per
+//   plane), and pgx_group_compact appends the occupied slots to okey / oplane again (wave-aggregated cursor).  A group
+//   moves 40 B in, ~5 random 8-B atomics, 40 B out: bound by the atomics' 64-B granules, not by arithmetic.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace pgx {
+
+constexpr unsigned long long kMergeEmpty = ~0ull;  // packed keys use < 64 bits (pgx_host.cpp part_keybits <= 63)
+
+__device__ __forceinline__ uint64_t merge_mix(uint64_t x) {
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return x;
+}
+
+// op: 0 int64 add, 1 double add, 2 ordered-u64 min, 3 ordered-u64 max (PlaneOp); ops packs 2 bits per plane.
+__global__ void pgx_dense_reduce(unsigned long long* __restrict__ dst, const unsigned long long* __restrict__ src,
+                                 uint64_t slots, int nplanes, uint64_t ops) {
+  const uint64_t n = slots * static_cast<uint64_t>(nplanes);
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const int op = static_cast<int>((ops >> (2 * (i / slots))) & 3u);
+    const unsigned long long a = dst[i], b = src[i];
+    unsigned long long r;
+    if (op == 0) r = a + b;
+    else if (op == 1)
+      r = static_cast<unsigned long long>(__double_as_longlong(__longlong_as_double(static_cast<long long>(a)) +
+                                                              __longlong_as_double(static_cast<long long>(b))));
+    else if (op == 2) r = a < b ? a : b;
+    else r = a > b ? a : b;
+    dst[i] = r;
+  }
+}
+
+// Table: tkey[cap] (kMergeEmpty = free), tpl[p * cap + slot] for p = 0 count, 1 sum, 2 min (init ~0), 3 max (init 0).
+// Input group i: key[i * es], plane p at pl[p * ps + i * es] (columnar: es = 1, ps = n; records of 5 words: key = rec,
+// pl = rec + 1, es = 5, ps = 1).  A group whose probe sequence finds no slot counts in *overflow.
+__global__ void __launch_bounds__(256) pgx_group_merge(const uint64_t* __restrict__ key,
+                                                       const uint64_t* __restrict__ pl, int64_t es, int64_t ps,
+                                                       int64_t n, unsigned long long* __restrict__ tkey,
+                                                       unsigned long long* __restrict__ tpl, uint64_t cap,
+                                                       unsigned long long* __restrict__ overflow) {
+  const uint64_t mask = cap - 1;  // cap is a power of two
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const unsigned long long k = key[i * es];
+    uint64_t h = merge_mix(k) & mask;
+    int64_t slot = -1;
+    for (uint64_t probe = 0; probe < cap; ++probe) {
+      const unsigned long long prev = atomicCAS(tkey + h, kMergeEmpty, k);
+      if (prev == kMergeEmpty || prev == k) {
+        slot = static_cast<int64_t>(h);
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+    if (slot < 0) {
+      atomicAdd(overflow, 1ull);
+      continue;
+    }
+    const uint64_t* g = pl + i * es;
+    atomicAdd(tpl + slot, static_cast<unsigned long long>(g[0]));
+    atomicAdd(tpl + cap + slot, static_cast<unsigned long long>(g[ps]));
+    atomicMin(tpl + 2 * cap + slot, static_cast<unsigned long long>(g[2 * ps]));
+    atomicMax(tpl + 3 * cap + slot, static_cast<unsigned long long>(g[3 * ps]));
+  }
+}
+
+__global__ void __launch_bounds__(256) pgx_group_compact(const unsigned long long* __restrict__ tkey,
+                                                         const unsigned long long* __restrict__ tpl, uint64_t cap,
+                                                         uint64_t* __restrict__ okey, uint64_t* __restrict__ opl,
+                                                         int64_t ocap, unsigned long long* __restrict__ counter) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t base = blockIdx.x * static_cast<uint64_t>(blockDim.x) + (threadIdx.x & ~63u); base < cap;
+       base += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t s = base + static_cast<uint64_t>(lane);
+    const bool live = s < cap && tkey[s] != kMergeEmpty;
+    const unsigned long long bal = __ballot(live);
+    if (!bal) continue;
+    unsigned long long o = 0;
+    if (lane == 0) o = atomicAdd(counter, static_cast<unsigned long long>(__popcll(bal)));
+    o = __shfl(o, 0);
+    if (!live) continue;
+    const unsigned long long j = o + __popcll(bal & ((1ull << lane) - 1ull));
+    if (j >= static_cast<unsigned long long>(ocap)) continue;  // the host sized ocap from the table; cannot happen
+    okey[j] = tkey[s];
+    for (int p = 0; p < 4; ++p) opl[p * ocap + j] = tpl[p * cap + s];
+  }
+}
+
+// Columnar groups (okey, oplane[p * ocap + i]) -> records of 5 words (key, count, sum, min, max) for an exchange.
+__global__ void __launch_bounds__(256) pgx_group_pack(const uint64_t* __restrict__ okey,
+                                                      const uint64_t* __restrict__ opl, int64_t ocap, int64_t n,
+                                                      uint64_t* __restrict__ rec) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    uint64_t* r = rec + 5 * i;
+    r[0] = okey[i];
+    for (int p = 0; p < 4; ++p) r[1 + p] = opl[p * ocap + i];
+  }
+}
+
+}  // namespace pgx
+
+extern "C" hipError_t pgx_launch_dense_reduce(unsigned long long* dst, const unsigned long long* src, uint64_t slots,
+                                              int nplanes, uint64_t ops, hipStream_t stream) {
+  const uint64_t n = slots * static_cast<uint64_t>(nplanes);
+  if (n == 0) return hipSuccess;
+  if (nplanes > 32) return hipErrorInvalidValue;
+  const unsigned grid = static_cast<unsigned>(n / 256 + 1 < 16384 ? n / 256 + 1 : 16384);
+  hipLaunchKernelGGL(pgx::pgx_dense_reduce, dim3(grid), dim3(256), 0, stream, dst, src, slots, nplanes, ops);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_group_merge(const uint64_t* key, const uint64_t* pl, int64_t es, int64_t ps,
+                                             int64_t n, unsigned long long* tkey, unsigned long long* tpl,
+                                             uint64_t cap, unsigned long long* overflow, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (cap == 0 || (cap & (cap - 1)) != 0) return hipErrorInvalidValue;
+  const int64_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(pgx::pgx_group_merge, dim3(static_cast<unsigned>(g < 65536 ? g : 65536)), dim3(256), 0, stream,
+                     key, pl, es, ps, n, tkey, tpl, cap, overflow);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_group_pack(const uint64_t* okey, const uint64_t* opl, int64_t ocap, int64_t n,
+                                            uint64_t* rec, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int64_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(pgx::pgx_group_pack, dim3(static_cast<unsigned>(g < 65536 ? g : 65536)), dim3(256), 0, stream,
+                     okey, opl, ocap, n, rec);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_group_compact(const unsigned long long* tkey, const unsigned long long* tpl,
+                                               uint64_t cap, uint64_t* okey, uint64_t* opl, int64_t ocap,
+                                               unsigned long long* counter, hipStream_t stream) {
+  if (cap == 0) return hipSuccess;
+  const uint64_t g = (cap + 255) / 256;
+  hipLaunchKernelGGL(pgx::pgx_group_compact, dim3(static_cast<unsigned>(g < 65536 ? g : 65536)), dim3(256), 0, stream,
+                     tkey, tpl, cap, okey, opl, ocap, counter);
+  return hipGetLastError();
+}

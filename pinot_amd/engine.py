@@ -487,6 +487,35 @@ class _Query:
                                     C.byref(r)))
         return r
 
+    def execute_async(self, segments: Sequence[IndexSegment], flags: int = 0):
+        """pgx_execute_async: returns the pending result at once (the library copied the bindings); every accessor,
+        or pgx_result_wait, waits for it."""
+        segs = (C.c_void_p * len(segments))(*[s.handle.value for s in segments])
+        binds, keep = self.bindings(segments)
+        opts = N.ExecOpts(0, None, 0, flags)
+        r = C.c_void_p()
+        N.check(N.lib().pgx_execute_async(self.ctx.handle, self.handle, segs, len(segments), binds, C.byref(opts),
+                                          C.byref(r)))
+        return r
+
+    def execute_multi(self, segments: Sequence[IndexSegment], contexts: Optional[Sequence[Context]] = None,
+                      flags: int = 0):
+        """pgx_execute_multi over segments staged on several contexts (one per device); the merged result lives on
+        the first context's device and its group keys index into `segments`."""
+        if contexts is None:
+            contexts = []
+            for s in segments:
+                if all(s.ctx is not c for c in contexts):
+                    contexts.append(s.ctx)
+        ctxs = (C.c_void_p * len(contexts))(*[c.handle.value for c in contexts])
+        segs = (C.c_void_p * len(segments))(*[s.handle.value for s in segments])
+        binds, keep = self.bindings(segments)
+        opts = N.ExecOpts(0, None, 0, flags)
+        r = C.c_void_p()
+        N.check(N.lib().pgx_execute_multi(ctxs, len(contexts), self.handle, segs, len(segments), binds,
+                                          C.byref(opts), C.byref(r)))
+        return r
+
     def close(self):
         if getattr(self, "handle", None):
             N.lib().pgx_query_release(self.handle)

@@ -170,17 +170,19 @@ def merge_group_partials(fns: Sequence[str], parts):
     return [c[starts] for c in cols], out_v, out_c
 
 
-def trim_to_size(fns: Sequence[str], vals, cnts, top_n: int) -> List[np.ndarray]:
+def trim_to_size(fns: Sequence[str], vals, cnts, top_n: int, total: int = None) -> List[np.ndarray]:
     """AggregationGroupByOperatorService.trimToSize over merged groups: above 20 x max(topN, 1000) groups keep, per
     function, the 5 x max(topN, 1000) best (MIN ascending, others descending, AVG by sum / count); otherwise every
-    group.  Ties at the threshold are arbitrary, as in the reference's MinMaxPriorityQueue.  Returns the kept group
-    indices per function."""
+    group.  Ties at the threshold are arbitrary, as in the reference's MinMaxPriorityQueue.  `total` is the number of
+    merged groups the threshold applies to when `vals` holds only candidates (the per-rank trims of disjoint key
+    partitions).  Returns the kept group indices per function."""
     n = vals.shape[1]
     min_trim = max(top_n, 1000)
     threshold, size = min_trim * 20, min_trim * 5
+    total = n if total is None else total
     out = []
     for i, f in enumerate(fns):
-        if n <= threshold:
+        if total <= threshold or n <= size:
             out.append(np.arange(n))
             continue
         if f == "count":
@@ -194,3 +196,112 @@ def trim_to_size(fns: Sequence[str], vals, cnts, top_n: int) -> List[np.ndarray]
             score = -score
         out.append(np.argpartition(score, size - 1)[:size])
     return out
+
+
+# ------------------------------------------------------------------------------------------------
+# Device-side sparse merge (ranks planned the same key space: identical dictionaries, dense_layout_agrees's fingerprint
+# check).  Every rank's groups stay in HBM as 5-word records (packed key, count, sum, min, max: pgx_result_device_groups),
+# are routed to rank hash(key) mod world with ONE all_to_all_single (RCCL send/recv over xGMI), merged there by the
+# library's device hash merge (pgx_result_merge_groups), trimmed on the device (pgx_result_trim: the key partitions are
+# disjoint, so the union of the per-partition top-K holds the global top-K), and only the kept groups -- as VALUES --
+# go to rank 0, which applies trimToSize once more with the global group count.
+# ------------------------------------------------------------------------------------------------
+_GOLDEN = -7046029254386353131  # 0x9E3779B97F4A7C15 as a signed 64-bit constant
+
+
+def group_destination(keys, world: int):
+    """Destination rank of each packed group key: high bits of a multiplicative hash (identical on every rank)."""
+    return ((keys * _GOLDEN) >> 40) % world
+
+
+def _all_to_all(out, inp, out_splits, in_splits):
+    import torch.distributed as dist
+    if dist.get_backend() == "gloo" and inp.is_cuda:  # gloo rehearsal on a 1-GPU box: exchange through host memory
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits)
+
+
+def exchange_group_records(recs, world: int):
+    """all_to_all of [n, 5] int64 group records by destination rank: returns this rank's [m, 5] records."""
+    import torch
+    import torch.distributed as dist
+    dest = group_destination(recs[:, 0], world)
+    order = torch.argsort(dest, stable=True)
+    recs = recs[order]
+    send = torch.bincount(dest, minlength=world).to(torch.int64)
+    recv = torch.empty_like(send)
+    if dist.get_backend() == "gloo" and send.is_cuda:
+        r = recv.cpu()
+        dist.all_to_all_single(r, send.cpu())
+        recv.copy_(r)
+    else:
+        dist.all_to_all_single(recv, send)
+    in_splits, out_splits = send.tolist(), recv.tolist()
+    out = torch.empty((sum(out_splits), 5), dtype=torch.int64, device=recs.device)
+    _all_to_all(out, recs, out_splits, in_splits)
+    return out
+
+
+def device_sparse_merge(ctx, q, r, segments, device):
+    """Merge a device-resident sparse group-by result across ranks (see above).  Returns (maps, total_groups, stats):
+    on rank 0 one {rendered key: value} map per function after trimToSize (None elsewhere)."""
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    L = N.lib()
+    world = dist.get_world_size()
+    n = C.c_int64()
+    N.check(L.pgx_result_device_groups(r, C.byref(n), None))
+    recs = torch.empty((max(n.value, 1), 5), dtype=torch.int64, device=device)
+    N.check(L.pgx_result_device_groups(r, C.byref(n), C.c_void_p(recs.data_ptr())))
+    mine = exchange_group_records(recs[:n.value], world)
+    st = (C.c_int64 * 4)()
+    N.check(L.pgx_result_stats(r, st))
+    stats = torch.tensor(list(st), dtype=torch.int64, device=device)
+    dist.all_reduce(stats)
+    s4 = (C.c_int64 * 4)(*stats.tolist())
+    merged = C.c_void_p()
+    torch.cuda.synchronize(device)
+    N.check(L.pgx_result_merge_groups(ctx.handle, r, C.c_void_p(mine.data_ptr()), mine.shape[0], s4,
+                                      C.byref(merged)))
+    try:
+        ng = C.c_int64()
+        N.check(L.pgx_result_num_groups(merged, C.byref(ng)))
+        total = torch.tensor([ng.value], dtype=torch.int64, device=device)
+        dist.all_reduce(total)
+        # union over the functions of the device trim's kept groups, then every function's value of each
+        nf, ncols = len(q.fns), len(q.group_cols)
+        idx = set()
+        for i in range(nf):
+            cap = C.c_int64(0)
+            N.check(L.pgx_result_trim(merged, i, None, C.byref(cap)))
+            sel = np.zeros(max(cap.value, 1), dtype=np.int64)
+            N.check(L.pgx_result_trim(merged, i, sel.ctypes.data, C.byref(cap)))
+            idx.update(sel[:cap.value].tolist())
+        idx = np.array(sorted(idx), dtype=np.int64)
+        m = len(idx)
+        si = np.zeros(max(m * ncols, 1), dtype=np.int32)
+        di = np.zeros(max(m * ncols, 1), dtype=np.int32)
+        v = np.zeros(max(m * nf, 1))
+        c = np.zeros(max(m * nf, 1), dtype=np.int64)
+        N.check(L.pgx_result_gather(merged, idx.ctypes.data, m, si.ctypes.data, di.ctypes.data, v.ctypes.data,
+                                    c.ctypes.data))
+    finally:
+        L.pgx_result_release(merged)
+    fns = q.fns
+    si, di = si[:m * ncols].reshape(ncols, m), di[:m * ncols].reshape(ncols, m)
+    cols = [E._column_values(segments, col, si[g], di[g]) for g, col in enumerate(q.group_cols)]
+    vals, cnts = v[:m * nf].reshape(nf, m), c[:m * nf].reshape(nf, m)
+    parts = gather_group_partials(cols, vals, cnts)  # kept groups only, as key values
+    if dist.get_rank() != 0:
+        return None, int(total.item()), list(s4)
+    cols, vals, cnts = merge_group_partials(fns, parts)  # partitions are disjoint: this only concatenates
+    keep = trim_to_size(fns, vals, cnts, q.request["group_by"].get("top_n", 10), total=int(total.item()))
+    return E.render_group_maps(q, segments, cols, vals, cnts, keep), int(total.item()), list(s4)

@@ -26,6 +26,7 @@ PGX_X_FORCE_HASH = 0x2
 PGX_X_NO_PARTITION = 0x4
 PGX_Q_NO_STAR_TREE = 0x1
 ERR_UNSUPPORTED = 2
+PGX_ERR_TIMEOUT = 5
 
 
 class CtxOpts(C.Structure):
@@ -124,6 +125,15 @@ EXPORTS = {
                                       C.POINTER(C.c_void_p)]),
     "pgx_bindings_array": (C.POINTER(LeafBinding), [C.c_void_p]),
     "pgx_bindings_release": (C.c_int, [C.c_void_p]),
+    "pgx_execute_async": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(LeafBinding),
+                                    C.POINTER(ExecOpts), C.POINTER(C.c_void_p)]),
+    "pgx_result_wait": (C.c_int, [C.c_void_p, C.c_int64]),
+    "pgx_execute_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
+                                    C.POINTER(LeafBinding), C.POINTER(ExecOpts), C.POINTER(C.c_void_p)]),
+    "pgx_result_device_groups": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_void_p]),
+    "pgx_result_merge_groups": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
+                                          C.POINTER(C.c_void_p)]),
+    "pgx_copy_to_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     "pgx_execute_timed": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(LeafBinding),
                                     C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_void_p)]),
 }

@@ -284,3 +284,60 @@ def test_two_rank_dense_layout_agreement_and_value_keyed_merge():
     assert set(got) == set(exp) and len(got) == 47
     for k, e in exp.items():
         assert got[k] == [e[0], e[1], e[2], e[3]]
+
+
+# ------------------------------------------------------------------------------------------------
+# Device-side sparse merge plumbing (multigpu.exchange_group_records): group records routed by key hash with one
+# all_to_all_single; every key lands on exactly one rank, every record arrives once.
+# ------------------------------------------------------------------------------------------------
+def _a2a_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        g = torch.Generator().manual_seed(rank)
+        n = 5000 + 777 * rank
+        keys = torch.randint(0, 1 << 40, (n,), generator=g, dtype=torch.int64)
+        keys[:100] = torch.arange(100)  # keys present on every rank
+        recs = torch.stack([keys, torch.ones(n, dtype=torch.int64), keys % 97, keys % 13, keys % 7], dim=1)
+        out = multigpu.exchange_group_records(recs, world)
+        q.put((rank, (recs.numpy(), out.numpy())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_three_rank_group_record_exchange():
+    import torch
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_a2a_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    sent = np.concatenate([res[r][0] for r in range(3)])
+    got = np.concatenate([res[r][1] for r in range(3)])
+    assert sorted(map(tuple, sent.tolist())) == sorted(map(tuple, got.tolist()))
+    for r in range(3):
+        out = res[r][1]
+        dest = multigpu.group_destination(torch.from_numpy(out[:, 0]), 3).numpy()
+        assert np.all(dest == r)
+    # the shared keys 0..99 are each on exactly one rank, all three copies together
+    for k in range(100):
+        holders = [r for r in range(3) if np.any(res[r][1][:, 0] == k)]
+        assert len(holders) == 1 and np.sum(res[holders[0]][1][:, 0] == k) == 3
+
+
+def test_trim_to_size_with_global_total():
+    """Candidates = per-partition top-K of disjoint partitions: the threshold applies to the global group count."""
+    rng = np.random.default_rng(0)
+    vals = rng.permutation(12000).astype(np.float64)[None, :]
+    cnts = np.ones((1, 12000), dtype=np.int64)
+    kept = multigpu.trim_to_size(["sum"], vals, cnts, 10, total=50000)[0]  # 50000 > 20000: keep the best 5000
+    assert len(kept) == 5000 and set(vals[0, kept]) == set(range(7000, 12000))
+    assert len(multigpu.trim_to_size(["sum"], vals, cnts, 10, total=15000)[0]) == 12000  # below the threshold: all
