@@ -283,6 +283,9 @@ pgx_status pgx_synth_column_paired(pgx_ctx* ctx, void* device_fwd, int64_t n_row
 pgx_status pgx_synth_dict_ids(uint64_t seed, int64_t n_rows, int32_t card, int32_t* out);
 /* Segment creation: the <col>.bitmap.inv bytes of a column (HeapBitmapInvertedIndexCreator.java:42-81 layout, roaring
  * portable format).  out == NULL or cap too small: *len receives the size only. */
+/* Segment creation: the <col>.sv.unsorted.fwd bytes of n dictIds at `bits` per value (FixedBitSingleValueWriter:
+ * MSB-first, big-endian, values back to back); out holds ceil(n * bits / 8) bytes. */
+pgx_status pgx_pack_fixed_bit(const int32_t* ids, int64_t n, int32_t bits, uint8_t* out);
 pgx_status pgx_inverted_index_build(const int32_t* ids, int64_t n, int32_t card, uint8_t* out, uint64_t cap,
                                     uint64_t* len);
 pgx_status pgx_device_alloc(pgx_ctx* ctx, uint64_t bytes, void** out);

@@ -3711,6 +3711,38 @@ pgx_status pgx_synth_dict_ids(uint64_t seed, int64_t n_rows, int32_t card, int32
 // offsets, then per dictId the RoaringBitmap 0.5.10 portable serialisation of its doc ids (cookie 12346, no run
 // containers; array containers up to 4096 docs, bitmap containers above).  out == NULL (or cap too small) only
 // reports the size in *len.
+// Segment creation: FixedBitSingleValueWriter's packing (MSB-first, big-endian, no padding between values), 64 bits
+// at a time.  out holds ceil(n * bits / 8) bytes.
+pgx_status pgx_pack_fixed_bit(const int32_t* ids, int64_t n, int32_t bits, uint8_t* out) {
+  return guarded([&] {
+    if (bits < 1 || bits > 32 || n < 0 || (n && (!ids || !out))) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    const uint64_t nbytes = (uint64_t(n) * uint64_t(bits) + 7) / 8;
+    uint64_t acc = 0;  // pending bits, left-aligned count `have`
+    int have = 0;
+    uint64_t o = 0;
+    const uint64_t mask = bits == 32 ? 0xFFFFFFFFull : ((uint64_t(1) << bits) - 1);
+    for (int64_t i = 0; i < n; ++i) {
+      const uint64_t v = uint64_t(uint32_t(ids[i])) & mask;
+      if (have + bits <= 64) {
+        acc |= v << (64 - have - bits);
+        have += bits;
+      } else {
+        const int fit = 64 - have;
+        acc |= v >> (bits - fit);
+        for (int b = 0; b < 8; ++b) out[o++] = uint8_t(acc >> (56 - 8 * b));
+        acc = v << (64 - (bits - fit));
+        have = bits - fit;
+      }
+      if (have == 64) {
+        for (int b = 0; b < 8; ++b) out[o++] = uint8_t(acc >> (56 - 8 * b));
+        acc = 0;
+        have = 0;
+      }
+    }
+    for (int b = 0; o < nbytes; ++b) out[o++] = uint8_t(acc >> (56 - 8 * b));
+  });
+}
+
 pgx_status pgx_inverted_index_build(const int32_t* ids, int64_t n, int32_t card, uint8_t* out, uint64_t cap,
                                     uint64_t* len) {
   return guarded([&] {

@@ -17,6 +17,8 @@
 // generic interpreter kernel (pgx_kernels.hip), so the host decodes them identically.
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -657,6 +659,77 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
 
 std::map<std::vector<int64_t>, JitEntry> g_jit_shapes;  // shape key -> compiled entry (same entries as g_jit_cache)
 
+// Persistent code-object cache (opt-in): with PGX_JIT_CACHE=<directory> a server restart (or a new process on the same
+// host) reuses the kernels earlier processes compiled instead of paying hiprtc (~0.4 s per new query shape).  Unset:
+// no file is read or written.  File name: FNV-1a of the source and the compile options; the file starts with a second,
+// independent hash of the same text, checked on load.
+constexpr const char* kJitOpts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
+
+std::string jit_cache_dir() {
+  const char* d = std::getenv("PGX_JIT_CACHE");
+  return d && *d ? d : "";
+}
+
+uint64_t text_hash(const std::string& t, uint64_t h, uint64_t mul) {
+  for (unsigned char c : t) {
+    h ^= c;
+    h *= mul;
+  }
+  return h;
+}
+
+std::string cache_text(const std::string& src) {
+  std::string t = src;
+  for (const char* o : kJitOpts) t += std::string("\n//") + o;
+  return t;
+}
+
+std::string cache_path(const std::string& dir, const std::string& text) {
+  char name[64];
+  std::snprintf(name, sizeof name, "/pgxq_%016llx.co",
+                static_cast<unsigned long long>(text_hash(text, 1469598103934665603ull, 1099511628211ull)));
+  return dir + name;
+}
+
+bool cache_load(const std::string& src, std::string* code) {
+  const std::string dir = jit_cache_dir();
+  if (dir.empty()) return false;
+  const std::string text = cache_text(src);
+  FILE* f = std::fopen(cache_path(dir, text).c_str(), "rb");
+  if (!f) return false;
+  uint64_t check = 0;
+  bool ok = std::fread(&check, 8, 1, f) == 1 && check == text_hash(text, 0x9E3779B97F4A7C15ull, 0x100000001B3ull);
+  if (ok) {
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f) - 8;
+    ok = n > 0;
+    if (ok) {
+      code->resize(size_t(n));
+      std::fseek(f, 8, SEEK_SET);
+      ok = std::fread(&(*code)[0], 1, size_t(n), f) == size_t(n);
+    }
+  }
+  std::fclose(f);
+  return ok;
+}
+
+void cache_store(const std::string& src, const std::string& code) {
+  const std::string dir = jit_cache_dir();
+  if (dir.empty()) return;
+  std::string cmd_dir = dir;  // create the directory chain
+  for (size_t i = 1; i <= cmd_dir.size(); ++i)
+    if (i == cmd_dir.size() || cmd_dir[i] == '/') mkdir(cmd_dir.substr(0, i).c_str(), 0755);
+  const std::string text = cache_text(src);
+  const std::string path = cache_path(dir, text);
+  const std::string tmp = path + ".tmp" + std::to_string(getpid());
+  FILE* f = std::fopen(tmp.c_str(), "wb");
+  if (!f) return;
+  const uint64_t check = text_hash(text, 0x9E3779B97F4A7C15ull, 0x100000001B3ull);
+  const bool ok = std::fwrite(&check, 8, 1, f) == 1 && std::fwrite(code.data(), 1, code.size(), f) == code.size();
+  std::fclose(f);
+  if (!ok || std::rename(tmp.c_str(), path.c_str()) != 0) std::remove(tmp.c_str());
+}
+
 void* jit_function(const JitShape& s, int device, int* lds_bytes, std::string* err) {
   const std::vector<int64_t> skey = shape_key(s, device);
   {
@@ -684,27 +757,30 @@ void* jit_function(const JitShape& s, int device, int* lds_bytes, std::string* e
       std::fclose(f);
     }
   }
-  hiprtcProgram prog;
-  if (hiprtcCreateProgram(&prog, src.c_str(), "pgx_query.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
-    if (err) *err = "hiprtcCreateProgram failed";
-    return nullptr;
-  }
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
-  if (rc != HIPRTC_SUCCESS) {
-    size_t n = 0;
-    hiprtcGetProgramLogSize(prog, &n);
-    std::string log(n, '\0');
-    if (n) hiprtcGetProgramLog(prog, &log[0]);
+  std::string code;
+  if (!cache_load(src, &code)) {
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "pgx_query.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) {
+      if (err) *err = "hiprtcCreateProgram failed";
+      return nullptr;
+    }
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 3, const_cast<const char**>(pgx::kJitOpts));
+    if (rc != HIPRTC_SUCCESS) {
+      size_t n = 0;
+      hiprtcGetProgramLogSize(prog, &n);
+      std::string log(n, '\0');
+      if (n) hiprtcGetProgramLog(prog, &log[0]);
+      hiprtcDestroyProgram(&prog);
+      if (err) *err = "hiprtc compile failed: " + log.substr(0, 4000);
+      return nullptr;
+    }
+    size_t code_size = 0;
+    hiprtcGetCodeSize(prog, &code_size);
+    code.assign(code_size, '\0');
+    hiprtcGetCode(prog, &code[0]);
     hiprtcDestroyProgram(&prog);
-    if (err) *err = "hiprtc compile failed: " + log.substr(0, 4000);
-    return nullptr;
+    cache_store(src, code);
   }
-  size_t code_size = 0;
-  hiprtcGetCodeSize(prog, &code_size);
-  std::string code(code_size, '\0');
-  hiprtcGetCode(prog, &code[0]);
-  hiprtcDestroyProgram(&prog);
   JitEntry ent;
   ent.lds = lds;
   if (hipModuleLoadData(&ent.mod, code.data()) != hipSuccess ||
@@ -723,8 +799,7 @@ void* jit_function(const JitShape& s, int device, int* lds_bytes, std::string* e
 extern "C" int pgx_jit_compile_check(const char* source, char* log, unsigned long log_cap) {
   hiprtcProgram prog;
   if (hiprtcCreateProgram(&prog, source, "pgx_query.hip", 0, nullptr, nullptr) != HIPRTC_SUCCESS) return -1;
-  const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17"};
-  const hiprtcResult rc = hiprtcCompileProgram(prog, 3, opts);
+  const hiprtcResult rc = hiprtcCompileProgram(prog, 3, const_cast<const char**>(pgx::kJitOpts));
   size_t n = 0;
   hiprtcGetProgramLogSize(prog, &n);
   if (log && log_cap) {

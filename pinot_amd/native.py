@@ -89,6 +89,7 @@ EXPORTS = {
     "pgx_synth_column_paired": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_int32, C.c_uint64,
                                           C.c_uint64, C.c_uint32]),
     "pgx_synth_dict_ids": (C.c_int, [C.c_uint64, C.c_int64, C.c_int32, C.c_void_p]),
+    "pgx_pack_fixed_bit": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]),
     "pgx_inverted_index_build": (C.c_int, [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_uint64,
                                            C.POINTER(C.c_uint64)]),
     "pgx_last_error": (C.c_char_p, []),

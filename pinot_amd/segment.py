@@ -91,9 +91,26 @@ def pack_fixed_bit(values, bits: int) -> bytes:
     return out.tobytes()[:nbytes].ljust(nbytes, b"\0")
 
 
+def _native_pack(v: np.ndarray, bits: int):
+    """pgx_pack_fixed_bit (libpgx host code, no device needed); None when the library is not built."""
+    import ctypes as C
+    from . import native as N
+    if not os.path.exists(N.LIB_PATH) or v.size == 0 or int(v.max()) >= (1 << 31) or int(v.min()) < 0:
+        return None
+    ids = np.ascontiguousarray(v, dtype=np.int32)
+    out = np.zeros((len(ids) * bits + 7) // 8, dtype=np.uint8)
+    N.check(N.lib().pgx_pack_fixed_bit(ids.ctypes.data, len(ids), bits, out.ctypes.data))
+    return out.tobytes()
+
+
 def pack_fixed_bit_chunked(values, bits: int, chunk: int = 1 << 22) -> bytes:
-    """pack_fixed_bit for large arrays, chunked on byte boundaries (chunk rows multiple of 8)."""
+    """pack_fixed_bit for large arrays: the library's packer, else numpy chunked on byte boundaries (chunk rows a
+    multiple of 8)."""
     v = np.asarray(values)
+    if len(v) > 65536:
+        out = _native_pack(v, bits)
+        if out is not None:
+            return out
     if len(v) <= chunk:
         return pack_fixed_bit(v, bits)
     assert chunk % 8 == 0

@@ -92,11 +92,12 @@ WORKLOADS: Dict[str, Workload] = {
 }
 
 
-# C4 (BASELINE configs[3]): star-tree segment over 6 dims + 3 metrics.  Built by the Python restatement of the
-# reference builder (pinot_amd/startree.py), which takes ~50 s at 10M raw rows; the SURVEY's 100M-row instance would take
-# ~8 min per bench run, so the bench uses 10M raw rows per segment (same dims, metrics, maxLeafRecords and query).
+# C4 (BASELINE configs[3]): star-tree segment over 6 dims + 3 metrics, SURVEY 8d's 100M raw rows (same dims, metrics,
+# maxLeafRecords and query).  Built on the host by pinot_amd/startree.py (one int64 sort key per row, hash-based
+# dictionaries); the GPU parity test uses a 10M-row instance (C4_TEST_ROWS) so the oracle stays quick.
 C4_CARDS = [8, 16, 32, 64, 128, 1000]
-C4_ROWS = 10_000_000
+C4_ROWS = 100_000_000
+C4_TEST_ROWS = 10_000_000
 C4_QUERY = "SELECT SUM(m1), SUM(m2), SUM(m3) FROM T WHERE d2 = 3 AND d4 IN (1, 2, 3) GROUP BY d1 TOP 10"
 
 
@@ -106,11 +107,18 @@ class StarTreeSegments:
     def __init__(self, ctx, rows: int = None, seed: int = 4):
         from . import startree as ST
         from .engine import IndexSegment
+        import sys
+        import time
         self.rows = rows or C4_ROWS
+        t0 = time.time()
         rng = np.random.default_rng(seed)
         dims = {"d%d" % (i + 1): rng.integers(0, c, self.rows) for i, c in enumerate(C4_CARDS)}
         mets = {"m%d" % (i + 1): rng.integers(0, 1 << 16, self.rows) for i in range(3)}
+        print("[c4] building the star tree over %d raw rows" % self.rows, file=sys.stderr, flush=True)
         self.seg_data = ST.make_star_tree_segment("c4_0", dims, mets, max_leaf_records=ST.DEFAULT_MAX_LEAF_RECORDS)
+        del dims, mets
+        print("[c4] built in %.1f s (%d docs); staging" % (time.time() - t0, self.seg_data.total_docs), file=sys.stderr,
+              flush=True)
         self.segments = [IndexSegment(ctx, self.seg_data)]
         self.seg_ids = [0]
 

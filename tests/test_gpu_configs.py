@@ -4,7 +4,7 @@
 * C3 one full 125M-row segment (10k x 1M key space, 2^24 pairs): every group's count / sum / min / max == the
   oracle's C twin over the regenerated (bit-identical) forward indexes; two segments combined == the merge of their
   per-segment results (combine linearity).
-* C4 star tree over 6 dims + 3 metrics, the bench's 10M raw rows: star-tree result == raw-scan result == oracle, and
+* C4 star tree over 6 dims + 3 metrics at 10M raw rows (the bench builds SURVEY's 100M): star-tree result == raw-scan result == oracle, and
   numDocsScanned == the oracle's StarTreeIndexOperator traversal.
 * C5 8 segments x 2M rows with roaring inverted indexes on f1 / f2 / f3: the merged group map == the oracle's
   vectorised filter + group sums over the regenerated columns; numEntriesScannedInFilter == 0 (bitmap leaves only).
@@ -126,7 +126,7 @@ def test_c4_star_tree_bench_size(ctx):
     import copy
 
     from tests.test_startree import oseg_of
-    data = synth.StarTreeSegments(ctx)
+    data = synth.StarTreeSegments(ctx, rows=synth.C4_TEST_ROWS)
     try:
         seg = data.seg_data
         q = pql.compile(synth.C4_QUERY)
@@ -144,7 +144,7 @@ def test_c4_star_tree_bench_size(ctx):
         assert {k: [float(x) for x in v] for k, v in raw.items()} == exp
         assert st_raw[0] == len(raw_docs)
         assert st[0] == len(O.star_tree_docs(os_, seg.star_tree, q, seg.total_raw_docs)) < st_raw[0]
-        assert st[3] == st_raw[3] == seg.total_raw_docs == synth.C4_ROWS
+        assert st[3] == st_raw[3] == seg.total_raw_docs == synth.C4_TEST_ROWS
     finally:
         data.free()
 

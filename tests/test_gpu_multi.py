@@ -122,17 +122,17 @@ def _pairs_raw(n, card, seed):
     raw = {"ga": rng.integers(0, card, size=n).astype(np.int32),
            "gb": rng.integers(0, card, size=n).astype(np.int32) * 3,
            "m": rng.integers(-5000, 5000, size=n).astype(np.int32)}
-    raw["ga"][:card] = np.arange(card)  # every segment holds the full dictionaries: one key space everywhere
+    raw["ga"][:card] = np.arange(card)  # every segment holds the full dictionaries: one key space everywhere (9M keys:
+    # beyond the 2^22-slot dense limit, so the sparse partitioned path runs)
     raw["gb"][:card] = np.arange(card) * 3
-    raw["m"][:2] = [-5000, 4999]
-    raw["m"][2:10000] = np.arange(-5000, 4999 + 1)[:9998]
+    raw["m"][:10000] = np.arange(-5000, 5000)  # one metric dictionary in every segment (one value base)
     return raw
 
 
 @pytest.fixture(scope="module")
 def pair_segs(ctxs):
     from pinot_amd import engine as E
-    built = [H.build_pair("pq%d" % i, _pairs_raw(150000 + 10000 * i, 400, 90 + i))[0] for i in range(4)]
+    built = [H.build_pair("pq%d" % i, _pairs_raw(150000 + 10000 * i, 3000, 90 + i))[0] for i in range(4)]
     multi = [E.IndexSegment(ctxs[i % 2], s) for i, s in enumerate(built)]
     single = [E.IndexSegment(ctxs[2], s) for s in built]
     return multi, single
