@@ -44,7 +44,7 @@ extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
-                                                 int maxchunks, hipStream_t stream);
+                                                 int maxchunks, int maxleaves, hipStream_t stream);
 extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
                                        int64_t n_words, uint64_t pair_seed, uint32_t npairs, hipStream_t stream);
 extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
@@ -382,7 +382,13 @@ struct pgx_segment {
   std::vector<std::string> st_skip;              // star.tree.skip.materialization.for.dimensions
   uint64_t device_bytes = 0;
 
+  std::vector<std::string> names;  // column names, contiguous: planning looks columns up per segment and query column
   const StagedColumn& col(const std::string& n) const {
+    if (names.size() <= 24) {  // a short scan over one or two cache lines beats hashing the name
+      for (size_t i = 0; i < names.size(); ++i)
+        if (names[i].size() == n.size() && std::memcmp(names[i].data(), n.data(), n.size()) == 0) return cols[i];
+      fail(PGX_ERR_INVALID_ARG, "segment " + name + " has no column " + n);
+    }
     auto it = by_name.find(n);
     if (it == by_name.end()) fail(PGX_ERR_INVALID_ARG, "segment " + name + " has no column " + n);
     return cols[it->second];
@@ -1595,6 +1601,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     }
   }
   K.num_qcols = int(P.qcols.size());
+  prof_mark("p.keys");
 
   // Partitioned group-by: sparse 64-bit keys go through record-emitting query kernels, radix partitioning and LDS
   // aggregation (run_partitioned) instead of one global hash table.  Eligible when every non-COUNT function reads the
@@ -1673,6 +1680,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           fuse = false;
       }
     }
+    prof_mark("p.fusechk");
     FusePlan F;
     if (fuse) {
       plan_fuse(root, q, F);
@@ -2008,7 +2016,15 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 void launch_bitmaps(ExecPlan& P, hipStream_t st) {
   if (P.rprog_on) {
     const int np = int(P.rprogs.size());
-    hip_check(pgx_launch_roaring_program(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, st), "bitmap program launch");
+    int maxleaves = 0;  // leaf masks the wide kernel keeps in LDS (PGX_RPROG_NARROW=1: the stack kernel)
+    for (const auto& dp : P.dm_progs) {
+      int nl = 0;
+      for (int8_t o : dp.op) nl += o == RP_LEAF;
+      maxleaves = std::max(maxleaves, nl);
+    }
+    if (std::getenv("PGX_RPROG_NARROW")) maxleaves = 0;
+    hip_check(pgx_launch_roaring_program(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, maxleaves, st),
+              "bitmap program launch");
   } else if (P.rdesc_dev) {
     hip_check(pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
   }
@@ -3267,6 +3283,7 @@ pgx_status pgx_segment_stage(pgx_ctx* ctx, const pgx_segment_desc* d, pgx_segmen
     for (int i = 0; i < d->num_columns; ++i) {
       stage_column(ctx, seg.get(), d->columns[i], d->mem == PGX_MEM_DEVICE, seg->cols[i]);
       seg->by_name[seg->cols[i].name] = i;
+      seg->names.push_back(seg->cols[i].name);
     }
     for (int i = 0; i < d->num_star_skip_dims; ++i)
       if (d->star_skip_dims && d->star_skip_dims[i]) seg->st_skip.emplace_back(d->star_skip_dims[i]);

@@ -691,6 +691,160 @@ __global__ void __launch_bounds__(256) pgx_roaring_program(const RProg* __restri
   for (int w = tid; w < 2048; w += 256) out[w] = stk[0][w];
 }
 
+// The same program with every leaf expanded at once: one container search over ALL bitmaps of ALL leaves (a lane per
+// bitmap), one pass over all their array-container elements (4 loads in flight per lane, LDS atomics into the leaf's
+// own mask), the bitmap containers, then the AND / OR / NOT program evaluated per mask word in registers and written
+// straight out.  The dependent global-load chain is that of ONE leaf, not one per leaf (C5: 3 leaves, 34 bitmaps), and
+// the LDS holds exactly the program's leaf masks (dynamic LDS, nleaves x 8 KiB).
+constexpr int kRProgMaxLeaves = 8;
+__global__ void __launch_bounds__(256) pgx_roaring_program_wide(const RProg* __restrict__ progs,
+                                                                const RDesc* __restrict__ descs, int nprogs,
+                                                                int maxchunks) {
+  const int pi = static_cast<int>(blockIdx.x / maxchunks);
+  const int chunk = static_cast<int>(blockIdx.x - static_cast<unsigned>(pi) * maxchunks);
+  if (pi >= nprogs) return;
+  const RProg& P = progs[pi];
+  if (chunk >= P.nchunks) return;
+  extern __shared__ uint32_t lmask[];  // [leaf][2048]
+  __shared__ const uint8_t* cptr[kRoarBatch];
+  __shared__ int ccard[kRoarBatch], cpre[kRoarBatch], cleaf[kRoarBatch];
+  __shared__ int ncont, celems;
+  __shared__ int leaf_desc[kRProgMaxLeaves], leaf_b0[kRProgMaxLeaves + 1];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    int nl = 0, tot = 0;
+    for (int i = 0; i < P.nops; ++i)
+      if (P.op[i] == RP_LEAF) {
+        const int a = P.arg[i];
+        leaf_desc[nl] = a;
+        leaf_b0[nl] = tot;
+        tot += a >= 0 ? descs[a].nb : 0;
+        ++nl;
+      }
+    leaf_b0[nl] = tot;
+    ncont = nl;  // leaves, read below before the first batch reuses ncont
+  }
+  __syncthreads();
+  const int nl = ncont;
+  const int total_b = leaf_b0[nl];
+  for (int i = tid; i < nl * 2048; i += 256) lmask[i] = 0u;
+  for (int b0 = 0; b0 < total_b; b0 += kRoarBatch) {
+    __syncthreads();
+    if (tid == 0) ncont = 0;
+    __syncthreads();
+    const int b = b0 + tid;
+    if (b < total_b) {
+      int j = 0;
+      while (leaf_b0[j + 1] <= b) ++j;  // the leaf this bitmap belongs to (<= 8 leaves)
+      const RDesc& D = descs[leaf_desc[j]];
+      const uint8_t* base = D.inv + D.offs[b - leaf_b0[j]];
+      const int n = static_cast<int>(rd32(base + 4));
+      int lo = 0, hi = n - 1, found = -1;
+      const int g = min(chunk, n - 1);
+      if (g >= 0) {
+        const uint32_t kv = rd32(base + 8 + 4 * g);
+        const int k = static_cast<int>(kv & 0xFFFFu);
+        if (k == chunk) found = g;
+        else if (k < chunk) lo = g + 1;
+        else hi = g - 1;
+      }
+      while (found < 0 && lo <= hi) {
+        const int mid = (lo + hi) >> 1;
+        const int k = static_cast<int>(rd16(base + 8 + 4 * mid));
+        if (k == chunk) { found = mid; break; }
+        if (k < chunk) lo = mid + 1; else hi = mid - 1;
+      }
+      if (found >= 0) {
+        const int card = static_cast<int>(rd16(base + 8 + 4 * found + 2)) + 1;
+        const uint32_t off = rd32(base + 8 + 4 * n + 4 * found);
+        const int slot = atomicAdd(&ncont, 1);
+        cptr[slot] = base + off;
+        ccard[slot] = card;
+        cleaf[slot] = j;
+      }
+    }
+    __syncthreads();
+    const int nc = ncont;
+    if (tid < 64) {
+      int v[4], x = 0;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = tid * 4 + q;
+        v[q] = (k < nc && ccard[k] <= 4096) ? ccard[k] : 0;
+        x += v[q];
+      }
+      int incl = x;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (tid >= d) incl += y;
+      }
+      int e = incl - x;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        cpre[tid * 4 + q] = e;
+        e += v[q];
+      }
+      if (tid == 63) celems = incl;
+    }
+    __syncthreads();
+    const int ne = celems;
+    for (int e0 = 0; e0 < ne; e0 += 4 * 256) {
+      uint32_t val[4];
+      int dst[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = e0 + q * 256 + tid;
+        dst[q] = -1;
+        if (e < ne) {
+          int lo = 0, hi = nc - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cpre[mid] <= e) lo = mid; else hi = mid - 1;
+          }
+          val[q] = rd16(cptr[lo] + 2 * (e - cpre[lo]));
+          dst[q] = cleaf[lo] * 2048;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (dst[q] >= 0) atomicOr(&lmask[dst[q] + (val[q] >> 5)], 1u << (val[q] & 31u));
+    }
+    for (int k = 0; k < nc; ++k) {
+      if (ccard[k] <= 4096) continue;
+      const uint8_t* c = cptr[k];
+      uint32_t* m = lmask + cleaf[k] * 2048;
+      for (int w = tid; w < 2048; w += 256) {
+        const uint32_t x = rd32(c + 4 * w);
+        if (x) atomicOr(&m[w], x);
+      }
+    }
+  }
+  __syncthreads();
+  // the program, per mask word, in registers
+  const int64_t doc0 = static_cast<int64_t>(chunk) << 16;
+  uint32_t* out = P.mask + static_cast<size_t>(chunk) * 2048;
+  for (int w = tid; w < 2048; w += 256) {
+    uint32_t st[kRProgStack + 4];
+    int sp = 0, leaf = 0;
+    const int64_t d = doc0 + 32 * w;
+    const uint32_t keep = d >= P.num_docs ? 0u : (d + 32 > P.num_docs ? (1u << (P.num_docs - d)) - 1u : 0xFFFFFFFFu);
+    for (int i = 0; i < P.nops; ++i) {
+      const int op = P.op[i];
+      if (op == RP_LEAF) {
+        st[sp++] = lmask[leaf * 2048 + w];
+        ++leaf;
+      } else if (op == RP_NOT) {
+        st[sp - 1] = ~st[sp - 1] & keep;
+      } else {
+        st[sp - 2] = op == RP_AND ? (st[sp - 2] & st[sp - 1]) : (st[sp - 2] | st[sp - 1]);
+        --sp;
+      }
+    }
+    out[w] = st[0];
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // High-cardinality group-by (LONG_MAP semantics, DefaultGroupKeyGenerator.java:239-246 / :429-441): the reference
 // probes a Long2IntOpenHashMap per doc; at 10^7 groups a device-wide hash table turns every row into random HBM atomics.
@@ -1165,9 +1319,14 @@ extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const u
 }
 
 extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
-                                                 int maxchunks, hipStream_t stream) {
+                                                 int maxchunks, int maxleaves, hipStream_t stream) {
   if (nprogs <= 0 || maxchunks <= 0) return hipSuccess;
   const long long blocks = static_cast<long long>(nprogs) * maxchunks;
+  if (maxleaves >= 1 && maxleaves <= pgx::kRProgMaxLeaves) {
+    hipLaunchKernelGGL(pgx::pgx_roaring_program_wide, dim3(static_cast<unsigned>(blocks)), dim3(256),
+                       static_cast<size_t>(maxleaves) * 2048 * 4, stream, progs, descs, nprogs, maxchunks);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(pgx::pgx_roaring_program, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, progs, descs,
                      nprogs, maxchunks);
   return hipGetLastError();

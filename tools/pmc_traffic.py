@@ -12,13 +12,17 @@ import sys
 def main():
     path, kname, workload, rows = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
     out = sys.argv[5] if len(sys.argv) > 5 else "profiles/traffic_%s.json" % workload
-    fetch, write = {}, {}
+    knames = kname.split("+")  # several kernels per query (e.g. pgx_roaring_program+pgxq): bytes summed per query
     rows_all = []
     for p in path.split(","):
         rows_all += list(csv.DictReader(open(p)))
+    per = {k: ({}, {}) for k in knames}
     for r in rows_all:
-        if kname not in r.get("Kernel_Name", ""):
+        name_k = r.get("Kernel_Name", "")
+        ks = [k for k in knames if k in name_k]
+        if not ks:
             continue
+        fetch, write = per[ks[0]]
         d = r.get("Dispatch_Id") or r.get("Correlation_Id")
         name = r.get("Counter_Name")
         v = float(r.get("Counter_Value", 0))
@@ -26,14 +30,21 @@ def main():
             fetch[d] = fetch.get(d, 0.0) + v
         elif name == "WRITE_SIZE":
             write[d] = write.get(d, 0.0) + v
-    if not fetch and not write:
+    if not any(f or w for f, w in per.values()):
         sys.exit("no %s dispatches in %s" % (kname, path))
-    f = sorted(fetch.values())
-    w = sorted(write.values())
-    med = lambda xs: xs[len(xs) // 2] if xs else 0.0
-    res = {"workload": workload, "rows": rows, "kernel": kname, "dispatches": max(len(f), len(w)),
-           "fetch_size_kib_median": med(f), "write_size_kib_median": med(w),
-           "hbm_bytes_per_launch": 2 * med(f) * 1024 + med(w) * 1024,
+    med = lambda xs: sorted(xs)[len(xs) // 2] if xs else 0.0
+    f0, w0 = per[knames[0]]
+    nq = max(len(f0), len(w0), 1)
+    breakdown = {}
+    total = 0.0
+    for k in knames:
+        f, w = per[k]
+        b = 2 * med(list(f.values())) * 1024 + med(list(w.values())) * 1024  # each kernel launches once per query
+        breakdown[k] = {"dispatches": max(len(f), len(w)), "hbm_bytes_per_query": b}
+        total += b
+    res = {"workload": workload, "rows": rows, "kernel": kname, "dispatches": nq,
+           "fetch_size_kib_median": med(list(f0.values())), "write_size_kib_median": med(list(w0.values())),
+           "hbm_bytes_per_launch": total, "per_kernel": breakdown,
            "correction": "read bytes = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write bytes = WRITE_SIZE x 1024"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))

@@ -17,4 +17,4 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o $WL --output
   python3 bench.py --workload $WL --profile-iters 5 "$@" > $OUT/pmc_write.log 2>&1
 ROWS=$(python3 -c "import json; print(json.load(open('$OUT/bench.json'))['config']['rows_per_segment'])")
 python3 tools/pmc_traffic.py $OUT/pmc_fetch/${WL}_counter_collection.csv,$OUT/pmc_write/${WL}_counter_collection.csv \
-  pgxq $WL $ROWS $OUT/traffic_$WL.json
+  ${PGX_PMC_KERNELS:-pgxq} $WL $ROWS $OUT/traffic_$WL.json
