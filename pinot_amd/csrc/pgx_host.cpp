@@ -966,6 +966,7 @@ struct ExecPlan {
     int nb, nchunks;
     uint64_t mask_off;
     const void* inv;
+    uint64_t bytes = 0;  // serialized bytes of its bitmaps (selectivity estimate)
   };
   std::vector<RoarItem> roar;
   std::vector<std::vector<int>> roar_index;        // [seg][leaf] -> index into roar or -1
@@ -1011,6 +1012,7 @@ struct ExecPlan {
   std::vector<JitGroup> jit;
   // bitmap sub-trees evaluated by pgx_roaring_program into one mask each (JIT leaf L + k for program k)
   bool rprog_on = false;
+  bool rchunk = false;   // ... evaluated per chunk inside the query kernels (LEAF_RCHUNK), not by a separate pass
   struct DmProg {
     std::vector<int> op, arg;  // RP_*; RP_LEAF arg = query leaf index
   };
@@ -1030,6 +1032,10 @@ struct ExecPlan {
   DevBuf fsm_table, fsm_segbuf, fsm_cnt, fsm_stv, fsm_pcount, fsm_pstate, lmask_buf;
   int fsm_T = 1;
 };
+
+// Estimated filter selectivity below which bitmap programs run inside the query kernels (LEAF_RCHUNK).  0: only when
+// forced with PGX_RCHUNK=1 (measured slower at C5 so far: the per-chunk container search stalls its workgroup).
+constexpr double kRchunkMaxSel = 0.0;
 
 bool jit_enabled() {
   const char* e = std::getenv("PGX_JIT");
@@ -1823,6 +1829,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
                                 o.mask_words, col.inv_dev.p};
           auto take = [&](int id) {
             o.blob.push_back(int32_t(col.inv_off[id]));
+            it.bytes += col.inv_off[id + 1] - col.inv_off[id];
             ++it.nb;
           };
           if (b.words) {  // walk the set (or, negated, the clear) bits of the dictId bitset
@@ -1876,6 +1883,37 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     P.total_raw += o.total_raw;
     P.host_entries += o.host_entries;
   }
+  // Bitmap programs inside the query kernels (LEAF_RCHUNK) when the filter is selective: the kernel then needs no
+  // value image (selected rows gather their values from the dictionary in HBM/L2), leaving LDS for the chunk masks and
+  // several workgroups per CU.  Selectivity estimate: segment 0's leaves, 2 serialized bytes per doc (array
+  // containers), AND / OR / NOT as independent events.  PGX_RCHUNK=0/1 forces the choice.
+  P.rchunk = false;
+  if (P.rprog_on && !P.use_part) {
+    double est = 1.0;
+    const double nd0 = std::max(1, segs[0]->total_raw_docs);
+    for (const auto& dp : P.dm_progs) {
+      std::vector<double> st;
+      for (size_t i = 0; i < dp.op.size(); ++i) {
+        if (dp.op[i] == RP_LEAF) {
+          const int ri = P.roar_index[0][dp.arg[i]];
+          double f = ri >= 0 ? std::min(1.0, double(P.roar[ri].bytes) / 2.0 / nd0) : 0.0;
+          if (ri >= 0 && P.roar[ri].neg) f = 1.0 - f;
+          st.push_back(f);
+        } else if (dp.op[i] == RP_NOT) {
+          st.back() = 1.0 - st.back();
+        } else {
+          const double b = st.back();
+          st.pop_back();
+          st.back() = dp.op[i] == RP_AND ? st.back() * b : st.back() + b - st.back() * b;
+        }
+      }
+      if (!st.empty()) est = std::min(est, st.back());  // the programs are ANDed or ORed into the tree: a bound
+    }
+    P.rchunk = est <= kRchunkMaxSel;
+    if (const char* e = std::getenv("PGX_RCHUNK")) P.rchunk = e[0] == '1';
+    for (int s = 0; s < n && P.rchunk; ++s)
+      if (star_fit(q, *segs[s])) P.rchunk = false;
+  }
   // per (segment, bitmap program): the program over that segment's leaf descriptors and its output mask
   P.rprogs.clear();
   if (P.rprog_on) {
@@ -1891,13 +1929,15 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         r.nchunks = nchunks;
         r.num_docs = P.ksegs[s].num_docs;
         r.mask = reinterpret_cast<uint32_t*>(uintptr_t(P.mask_words));  // word offset until the buffer exists
-        P.mask_words += uint64_t(nchunks) * 2048;
-        int o = 0;
+        if (!P.rchunk) P.mask_words += uint64_t(nchunks) * 2048;
+        int o = 0, nl = 0;
         for (size_t i = 0; i < dp.op.size(); ++i) {
           if (dp.op[i] == RP_LEAF) {
             const int ri = P.roar_index[s][dp.arg[i]];
             r.op[o] = RP_LEAF;
             r.arg[o++] = int16_t(ri);
+            if (nl < PGX_J_MAX_RLEAVES) r.ldesc[nl] = int16_t(ri);
+            ++nl;
             // a leaf without matching dictIds (alwaysFalse) is empty, negated or not
             if (ri < 0 && i + 1 < dp.op.size() && dp.op[i + 1] == RP_NOT) ++i;
           } else {
@@ -2014,6 +2054,7 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 // Bitmap inverted-index leaves: one mask per (segment, leaf) (pgx_roaring_expand), or one mask per (segment, bitmap
 // program) with the sub-tree's AND / OR / NOT applied in the same pass (pgx_roaring_program).
 void launch_bitmaps(ExecPlan& P, hipStream_t st) {
+  if (P.rchunk) return;  // the query kernels evaluate the bitmap programs per chunk themselves
   if (P.rprog_on) {
     const int np = int(P.rprogs.size());
     int maxleaves = 0;  // leaf masks the wide kernel keeps in LDS (PGX_RPROG_NARROW=1: the stack kernel)
@@ -2115,7 +2156,7 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
     hip_check(hipMemcpyAsync(B.dev() + B.off_rdesc, B.host.bytes() + B.off_rdesc,
                              B.off_outs - B.off_rdesc, hipMemcpyHostToDevice, st), "bitmap descriptors H2D");
     launch_bitmaps(P, st);
-    P.roar_early = true;
+    P.roar_early = !P.rchunk;
   }
 }
 
@@ -2151,14 +2192,14 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
   }
 }
 
-void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st) {
+void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table = true) {
   // (re)sends the whole argument arena with initialised output planes
   KQuery& K = P.kq;
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
   std::memset(outs, 0, kOutsBytes);
   for (int p = 1; p < K.num_planes; ++p) outs[p] = (K.plane_op[p] == P_MIN_ORD) ? ~0ull : 0ull;
   hip_check(hipMemcpyAsync(B.arena.p, B.host.p, B.size, hipMemcpyHostToDevice, st), "argument arena H2D");
-  if (K.group_mode != G_NONE && !P.use_part) {
+  if (init_table && K.group_mode != G_NONE && !P.use_part) {
     const uint64_t slots = (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) ? P.hash_cap : P.dense_slots;
     const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : (K.group_mode == G_HASH64 ? P.hash_cap : 0);
     hip_check(pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
@@ -2168,6 +2209,22 @@ void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st) {
 // Build the query-specialised launch groups (pgx_jit.cpp) for plans the generated kernels cover: aggregation-only
 // and dense group-by over at most PGX_J_MAX_COLS columns.  Hash group-by keeps the generic kernel.  PGX_JIT=0 forces
 // the generic kernel (A/B timing); both are HIP paths with identical accumulator encodings.
+
+// Workgroups of a generated kernel resident per CU (LDS, registers, waves), cached per kernel.  The persistent grids
+// are sized to exactly one round: a second, partial round of workgroups would run the tail at a fraction of the chip.
+int jit_occupancy(void* fn, int threads) {
+  static std::mutex mu;
+  static std::map<void*, int> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(fn);
+  if (it != cache.end()) return it->second;
+  int occ = 0;
+  if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&occ, static_cast<hipFunction_t>(fn), threads, 0) !=
+          hipSuccess || occ < 1)
+    occ = 1;
+  cache.emplace(fn, occ);
+  return occ;
+}
 
 void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
   P.jit.clear();
@@ -2256,23 +2313,42 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       }
     }
     J.R = R;
-    // LDS budget: drop the largest images until everything fits
+    // LDS budget: drop the largest images until everything fits (LEAF_RCHUNK: a budget for three workgroups per CU)
+    int64_t rch_bytes = 0;
+    if (P.rchunk) {
+      const size_t np = P.dm_progs.size();
+      for (size_t k = 0; k < np; ++k) {
+        const RProg& r0 = P.rprogs[size_t(members[0]) * np + k];
+        std::vector<int> ops(r0.op, r0.op + r0.nops);
+        int nl = 0;
+        for (int op : ops) nl += op == RP_LEAF;
+        if (nl > PGX_J_MAX_RLEAVES) fail(PGX_ERR_UNSUPPORTED, "bitmap program with too many leaves");
+        rch_bytes += int64_t(nl) * 8192;
+        J.rprog_ops.push_back(std::move(ops));
+      }
+      rch_bytes += 5152;  // container-search scratch
+    }
+    const int64_t lds_budget = P.rchunk ? 52 * 1024 : kLdsBudget;
     auto lds_need = [&]() {
-      int64_t b = 0;
+      int64_t b = rch_bytes;
       for (const JitCol& C : J.cols)
         if (C.img != IMG_NONE) b += ((int64_t(C.img_words) * 4 + 15) / 16) * 16;
       if (K.group_mode == G_DENSE_LDS) b += int64_t(P.dense_slots) * K.num_planes * 8;
       return b;
     };
-    while (lds_need() > kLdsBudget) {
+    while (lds_need() > lds_budget) {
       int big = -1;
       for (int c = 0; c < nc; ++c)
         if (J.cols[c].img != IMG_NONE && (big < 0 || J.cols[c].img_words > J.cols[big].img_words)) big = c;
-      if (big < 0) return;  // the dense LDS table alone does not fit: generic kernel
+      if (big < 0) {
+        if (P.rchunk) fail(PGX_ERR_INTERNAL, "bitmap-program kernel LDS budget");
+        return;  // the dense LDS table alone does not fit: generic kernel
+      }
       J.cols[big].img = IMG_NONE;
     }
     const int64_t lds = lds_need();
     J.T = lds <= 20 * 1024 ? 256 : (lds <= 40 * 1024 ? 512 : 1024);
+    if (P.rchunk) J.T = 512;  // three 512-thread workgroups per CU, four tiles per chunk
     if (P.use_part) J.T = std::min(J.T, 512);  // record-emitting kernels hold R 64-bit records per lane: 256 VGPRs
     for (int l = 0; l < nleaves; ++l) {
       J.leaf_col.push_back(K.leaf_col[l]);
@@ -2283,7 +2359,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     if (P.rprog_on)
       for (size_t k = 0; k < P.dm_progs.size(); ++k) {
         J.leaf_col.push_back(-1);
-        J.leaf_mode.push_back(LEAF_DOCMASK);
+        J.leaf_mode.push_back(P.rchunk ? LEAF_RCHUNK : LEAF_DOCMASK);
       }
     const ExecPlan::StarPlan& SP = P.star[members[0]];
     if (SP.on) {
@@ -2367,7 +2443,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       }
       if (P.rprog_on)
         for (size_t k = 0; k < P.dm_progs.size(); ++k)
-          js.lbits[nleaves + k] = P.masks_dev + uintptr_t(P.rprogs[size_t(s) * P.dm_progs.size() + k].mask);
+          js.lbits[nleaves + k] = P.rchunk ? reinterpret_cast<const uint32_t*>(P.rprog_dev + s * P.dm_progs.size() + k)
+                                           : P.masks_dev + uintptr_t(P.rprogs[size_t(s) * P.dm_progs.size() + k].mask);
       for (int l = 0; l < nleaves; ++l) {
         const KLeaf& L = S.leaf[l];
         const int ri = P.roar_index[s][l];
@@ -2388,6 +2465,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     int per_cu = std::max(1, 32 / waves);
     const int64_t lds_all = std::max<int64_t>(lds, lds_bytes);  // incl. record staging (G_EMIT)
     if (lds_all > 0) per_cu = std::min<int64_t>(per_cu, std::max<int64_t>(1, (160 * 1024) / (lds_all + 256)));
+    per_cu = std::min(per_cu, jit_occupancy(G.fn, J.T));  // registers too: a persistent grid one round deep
     const int64_t max_grid = int64_t(cus) * per_cu;
     const int64_t tpw = std::max<int64_t>(1, (tiles + max_grid - 1) / max_grid);
     G.grid = int(std::max<int64_t>(1, (tiles + tpw - 1) / tpw));
@@ -2395,6 +2473,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     G.args.segs = reinterpret_cast<const JSeg*>(B.dev() + B.off_jsegs + jidx * sizeof(JSeg));
     jidx += G.segs.size();
     G.args.num_segs = int(G.segs.size());
+    G.args.rdesc = P.rdesc_dev;
     G.args.total_tiles = tiles;
     G.args.tiles_per_wg = tpw;
     if (tiles > 0) P.jit.push_back(std::move(G));
@@ -2900,6 +2979,81 @@ struct HostProf {
   }
 };
 
+// Long segment lists (C5: 4096 segments) are planned and launched in batches on one stream: the host plans batch k + 1
+// while the GPU runs batch k, instead of planning every segment before the first launch.  Every batch decodes its
+// group keys against global dictionaries built over the WHOLE list (Domain), accumulates into batch 0's dense table
+// and writes its statistics / aggregation planes into batch 0's output block, so the combine stays on the device and
+// the result is read back once.  Aggregation-only and dense group-by plans only (sparse / hash plans size their
+// tables from the whole list); false before anything was launched when the plan does not qualify.
+bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
+                 const pgx_exec_opts* opts, pgx_result* R, hipStream_t st, uint32_t xflags, HostProf& hp) {
+  int bs = 512;
+  if (const char* e = std::getenv("PGX_BATCH_SEGS")) bs = std::atoi(e);
+  if (bs <= 0 || n < 2 * bs || !jit_enabled()) return false;
+  const size_t L = q.leaf_col.size();
+  std::vector<GlobalDict> full;
+  for (const auto& g : q.group_cols) full.push_back(build_global_dict(segs, n, g));
+  const int nb = (n + bs - 1) / bs;
+  bs = (n + nb - 1) / nb;  // even batches
+  std::vector<std::unique_ptr<ExecPlan>> plans;
+  std::vector<std::unique_ptr<ExecBuffers>> bufs;
+  int64_t host_entries = 0, total_raw = 0;
+  for (int b = 0; b < nb; ++b) {
+    const int s0 = b * bs, cnt = std::min(bs, n - s0);
+    Domain d;
+    d.g = &full;
+    d.index.resize(cnt);
+    std::iota(d.index.begin(), d.index.end(), s0);
+    auto P = std::make_unique<ExecPlan>();
+    plan_query(ctx, q, segs + s0, cnt, bindings ? bindings + size_t(s0) * L : nullptr, xflags, *P, &d);
+    const int gm = P->kq.group_mode;
+    if (b == 0 && (P->use_part || !(gm == G_NONE || gm == G_DENSE_LDS || gm == G_DENSE_GLOBAL))) return false;
+    auto B = std::make_unique<ExecBuffers>();
+    upload_plan(ctx, *P, *B, st);
+    plan_jit(ctx, q, segs + s0, cnt, *P, *B);
+    if (b == 0) {
+      alloc_outputs(ctx, *P, *B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
+      reset_outputs(*P, *B, st);
+    } else {
+      const KQuery& K0 = plans[0]->kq;
+      if (P->kq.group_mode != K0.group_mode || P->dense_slots != plans[0]->dense_slots ||
+          P->kq.num_planes != K0.num_planes)
+        fail(PGX_ERR_INTERNAL, "batched plans disagree");
+      alloc_outputs(ctx, *P, *B, K0.table, plans[0]->dense_slots * uint64_t(K0.num_planes) * 8);
+      reset_outputs(*P, *B, st, false);
+      P->kq.agg_out = K0.agg_out;  // one output block for the whole query
+      P->kq.stats = K0.stats;
+      P->kq.overflow = K0.overflow;
+    }
+    launch_scan(*P, st);
+    host_entries += P->host_entries;
+    total_raw += P->total_raw;
+    plans.push_back(std::move(P));
+    bufs.push_back(std::move(B));
+  }
+  hp.mark("batches");
+  ExecPlan& P0 = *plans[0];
+  P0.host_entries = host_entries;
+  P0.total_raw = total_raw;
+  if (opts && (opts->flags & PGX_X_KEEP_DENSE_ON_DEVICE)) {
+    unsigned long long* outs = reinterpret_cast<unsigned long long*>(bufs[0]->host.bytes() + bufs[0]->off_outs);
+    hip_check(hipMemcpyAsync(outs, bufs[0]->dev() + bufs[0]->off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    const unsigned long long* stats = outs + 16;
+    R->stats[0] = int64_t(stats[0]);
+    R->stats[1] = int64_t(stats[1]) + P0.host_entries;
+    R->stats[2] = int64_t(stats[0]) * P0.n_proj;
+    R->stats[3] = P0.total_raw;
+    R->group_by = true;
+    R->num_aggs = P0.kq.num_aggs;
+    R->agg_fn = q.agg_fn;
+    return true;
+  }
+  finish_result(ctx, q, P0, *bufs[0], segs, n, st, R, nullptr);
+  hp.mark("finish");
+  return true;
+}
+
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                const pgx_exec_opts* opts, pgx_result* R, const Domain* dom = nullptr) {
   HostProf hp;
@@ -2907,6 +3061,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   struct Unmark { ~Unmark() { g_prof_mark = nullptr; } } unmark;
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
   const uint32_t xflags = opts ? opts->flags : 0;
+  if (!dom && run_batched(ctx, q, segs, n, bindings, opts, R, st, xflags, hp)) return;
   ExecPlan P;
   plan_query(ctx, q, segs, n, bindings, xflags, P, dom);
   hp.mark("plan");

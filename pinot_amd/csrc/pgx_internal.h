@@ -2,6 +2,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "pgx_jit_abi.h"
+
 namespace pgx {
 
 constexpr int kTileRows = 8192;        // rows per workgroup tile = 256 lanes x 32 rows
@@ -22,29 +24,21 @@ enum LeafMode : int8_t {
   LEAF_NONE = 3,           // always false (empty binding)
   LEAF_DOCMASK = 4,        // query kernels: bitmap inverted-index leaf expanded to a per-segment doc mask
   LEAF_DOCMASK_NOT = 5,    // ... NEQ / NOT_IN: OR of the non-matching bitmaps, flipped (BitmapBasedFilterOperator)
+  LEAF_RCHUNK = 6,         // query kernels: a bitmap program evaluated per 65536-doc chunk into LDS by the kernel
 };
 
-// Bitmap inverted-index expansion (pgx_kernels.hip pgx_roaring_expand): one descriptor per (segment, leaf).
-struct RDesc {
-  uint32_t* mask;              // nchunks x 2048 words: bit (doc & 31) of word (doc >> 5)
-  const uint8_t* inv;          // device copy of <col>.bitmap.inv
-  const uint32_t* offs;        // byte offsets (into inv) of the roaring bitmaps to OR
-  int32_t nb;                  // number of bitmaps
-  int32_t nchunks;             // ceil(total_docs / 65536)
-};
+// Bitmap inverted-index expansion (pgx_kernels.hip pgx_roaring_expand): one descriptor per (segment, leaf).  The
+// layout is shared with the generated query kernels (pgx_jit_abi.h JRDesc), which evaluate bitmap programs per chunk
+// themselves (LEAF_RCHUNK).
+//   mask: nchunks x 2048 words: bit (doc & 31) of word (doc >> 5); inv: device copy of <col>.bitmap.inv;
+//   offs: byte offsets (into inv) of the roaring bitmaps to OR; nb: their number; nchunks: ceil(total_docs / 65536)
+using RDesc = ::JRDesc;
 
-// A sub-tree of the filter whose leaves are all bitmap inverted-index leaves, evaluated per 65536-doc chunk by
-// pgx_roaring_program into ONE doc mask (the query kernel then reads one mask word per 32 rows for the whole sub-tree).
-constexpr int kMaxRProg = 24;
+// A sub-tree of the filter whose leaves are all bitmap inverted-index leaves, evaluated per 65536-doc chunk into ONE
+// doc mask: by pgx_roaring_program into HBM, or inside the query kernel into LDS (LEAF_RCHUNK).  pgx_jit_abi.h JRProg.
+constexpr int kMaxRProg = PGX_J_MAX_RPROG;
 enum RProgOp : int8_t { RP_LEAF = 0, RP_AND = 1, RP_OR = 2, RP_NOT = 3 };
-struct RProg {
-  uint32_t* mask;              // nchunks x 2048 words
-  int32_t nchunks;
-  int32_t num_docs;            // NOT flips inside [0, num_docs) (BitmapDocIdSet: flip(startDocId, endDocId + 1))
-  int32_t nops;
-  int8_t op[kMaxRProg];
-  int16_t arg[kMaxRProg];      // RP_LEAF: index into the RDesc array (-1: empty leaf, no matching dictId)
-};
+using RProg = ::JRProg;
 
 enum ProgOp : int8_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_STAT = 3, OP_TRUE = 4 };
 
@@ -173,6 +167,8 @@ struct JitShape {
   int keybits = 0;
   int emit_col = -1;
   bool leafmask = false;  // write every leaf's per-row predicate bit (statistics automaton input, pgx_stats.cpp)
+  // LEAF_RCHUNK leaves, in leaf order: the bitmap program's postfix ops (RP_*), identical for the group's segments
+  std::vector<std::vector<int>> rprog_ops;
 };
 
 // ----- numEntriesScannedInFilter automaton (pgx_stats.cpp builds it, pgx_kernels.hip pgx_fsm_* runs it) -----

@@ -115,6 +115,24 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       lds += (stg_recs / s.R) * stg_pitch * 8 * waves;
     }
   }
+  // LEAF_RCHUNK: one 2048-word mask per leaf of each bitmap program, plus the container-search scratch
+  const int nleaves_all = int(s.leaf_col.size());
+  std::vector<int> rch_off(nleaves_all, -1), rch_nl(nleaves_all, 0);
+  int scr_off = -1;
+  {
+    size_t k = 0;
+    for (int l = 0; l < nleaves_all; ++l) {
+      if (s.leaf_mode[l] != LEAF_RCHUNK) continue;
+      const std::vector<int>& ops = s.rprog_ops.at(k++);
+      for (int op : ops) rch_nl[l] += op == RP_LEAF;
+      rch_off[l] = lds;
+      lds += rch_nl[l] * 2048 * 4;
+    }
+    if (k) {
+      scr_off = lds;
+      lds += (int(sizeof(void*)) * 256 + 3 * 4 * 256 + 16 + 15) / 16 * 16;
+    }
+  }
   if (lds_bytes_out) *lds_bytes_out = lds;
   const bool any_img = lds > 0 && (tab_off != 0 || s.group_mode != G_DENSE_LDS);
 
@@ -166,6 +184,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("__syncthreads();");
   if (s.group_mode == G_DENSE_LDS) e.ln("u64* const tab = (u64*)(lds + ", tab_off / 4, ");");
   if (s.group_mode == G_DENSE_GLOBAL) e.ln("u64* const tab = A.table;");
+  if (scr_off >= 0) e.ln("PgxRScratch& rscr = *(PgxRScratch*)(lds + ", scr_off / 4, ");");
   e.ln("u64 st_docs = 0, st_ent = 0;");
   e.ln("int seg = pgx_find_seg(A.segs, A.num_segs, tb);");
   e.ln("long long t = tb;");
@@ -184,7 +203,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   (void)any_img;
   auto emit_images = [&]() {
     if (!has_img) return;
-    e.ln("__syncthreads();");
+    e.ln("pgx_lds_barrier();");
     for (int c = 0; c < ncols; ++c) {
       if (s.cols[c].img == IMG_NONE) continue;
       e.ln("{");
@@ -202,7 +221,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ind--;
       e.ln("}");
     }
-    e.ln("__syncthreads();");
+    e.ln("pgx_lds_barrier();");
   };
   // per-segment pointers and leaf parameters
   for (int c = 0; c < ncols; ++c)
@@ -219,6 +238,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       case LEAF_DOCMASK:
       case LEAF_DOCMASK_NOT:
         e.ln("const PGX_G u32* __restrict__ dm", l, " = (const PGX_G u32*)S->lbits[", l, "];");
+        break;
+      case LEAF_RCHUNK:
+        e.ln("const PGX_G JRProg* __restrict__ rp", l, " = (const PGX_G JRProg*)S->lbits[", l, "];");
+        e.ln("u32* const rlm", l, " = lds + ", rch_off[l] / 4, ";");
         break;
       case LEAF_RANGES:
         e.ln("const PGX_G int* __restrict__ rg", l, " = (const PGX_G int*)S->lranges[", l, "];");
@@ -260,6 +283,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       else e.ln("const PGX_G i64* __restrict__ di", c, " = (const PGX_G i64*)S->dict[", c, "];");
     }
   }
+  if (scr_off >= 0) e.ln("int rc_cur = -1;  // chunk whose bitmap-program masks are in LDS");
   // lane accumulators (aggregation-only)
   e.ln("u64 wcnt = 0;  // selected rows of this wave in this segment (wave-uniform)");
   if (!grouped) {
@@ -326,6 +350,49 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("if (tt + 1 < t2) ");
   emit_loads("tt + 1", "n");
   e.ln("const int rb = (int)((tl ? (long long)tl[tt - tile0] : (tt - tile0)) * (PT * 32));");
+  if (scr_off >= 0) {
+    // a tile (PT * 32 rows) lies inside one 65536-doc chunk: build that chunk's program masks when it changes (the next
+    // tile's forward-index loads are already in flight)
+    e.ln("if ((rb >> 16) != rc_cur) {");
+    e.ln("  rc_cur = rb >> 16;");
+    e.ln("  pgx_lds_barrier();");
+    size_t k = 0;
+    for (int l = 0; l < nleaves_all; ++l) {
+      if (s.leaf_mode[l] != LEAF_RCHUNK) continue;
+      const std::vector<int>& ops = s.rprog_ops[k++];
+      e.ln("  pgx_rchunk_leaves<PT, ", rch_nl[l], ">(rp", l, ", (const PGX_G JRDesc*)A.rdesc, rc_cur, rlm", l, ", rscr);");
+      e.ln("  pgx_lds_barrier();");
+      bool has_not = false;
+      for (int op : ops) has_not |= op == RP_NOT;
+      e.ln("  for (int w = tid; w < 2048; w += PT) {");
+      if (has_not) {
+        e.ln("    const long long dw = ((long long)rc_cur << 16) + 32 * w;");
+        e.ln("    const u32 keep = dw >= nd ? 0u : (dw + 32 > nd ? (1u << (nd - dw)) - 1u : 0xFFFFFFFFu);");
+      }
+      std::vector<std::string> st;
+      int leaf = 0, tmp = 0;
+      for (int op : ops) {
+        const std::string X = "y" + std::to_string(tmp++);
+        if (op == RP_LEAF) {
+          e.ln("    const u32 ", X, " = rlm", l, "[", leaf++ * 2048, " + w];");
+        } else if (op == RP_NOT) {
+          e.ln("    const u32 ", X, " = ~", st.back(), " & keep;");
+          st.pop_back();
+        } else {
+          const std::string b = st.back();
+          st.pop_back();
+          const std::string a = st.back();
+          st.pop_back();
+          e.ln("    const u32 ", X, " = ", a, op == RP_AND ? " & " : " | ", b, ";");
+        }
+        st.push_back(X);
+      }
+      e.ln("    rlm", l, "[w] = ", st.empty() ? std::string("0u") : st.back(), ";");
+      e.ln("  }");
+    }
+    e.ln("  pgx_lds_barrier();");
+    e.ln("}");
+  }
   // The tile body is instantiated twice: for whole tiles (no per-row bound check) and for a segment's last tile.
   e.ln("auto body = [&](auto FT) {");
   e.ind = 4;
@@ -342,6 +409,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     for (int l = 0; l < nleaves; ++l) {
       if (s.leaf_mode[l] == LEAF_RANGES) e.ln("const u32 W", l, " = pgx_ranges_bits(rg", l, ", nr", l, ", cur", l, ", r0, PR);");
       if (is_docmask(s.leaf_mode[l])) e.ln("const u32 W", l, " = cq", l, "[", u, "] >> (r0 & 31);");
+      if (s.leaf_mode[l] == LEAF_RCHUNK) e.ln("const u32 W", l, " = rlm", l, "[(r0 & 0xFFFF) >> 5] >> (r0 & 31);");
     }
     // per-aggregation sub-step partials
     if (!grouped)
@@ -376,6 +444,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
             break;
           case LEAF_RANGES:
           case LEAF_DOCMASK:
+          case LEAF_RCHUNK:
             e.ln("const bool ", B, " = vj && ((W", l, " >> j) & 1u);");
             break;
           case LEAF_DOCMASK_NOT:  // BitmapBasedFilterOperator NEQ / NOT_IN: flip of the OR of the non-matching bitmaps
@@ -654,6 +723,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   add(s.gcol);
   add(s.gmul);
   add(s.gshift);
+  for (const auto& ops : s.rprog_ops) add(ops);
   return k;
 }
 
@@ -896,6 +966,28 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.prog_op = {OP_LEAF, OP_LEAF, OP_OR, OP_LEAF, OP_AND};
     s.prog_arg = {0, 1, 2, 2, 2};
     s.R = 16;
+    shapes.push_back(s);
+  }
+  {  // C5 shape: (L0 OR L1) AND NOT L2 over bitmap leaves evaluated per chunk in LDS, dense LDS group-by, no image
+    JitShape s = base(10, 16, IMG_NONE, 0);
+    s.cols.push_back(JitCol{});
+    s.cols[2].bits = 10;
+    s.cols[2].decode = false;
+    s.leaf_col = {2, 2, 2, -1};
+    s.leaf_mode = {LEAF_NONE, LEAF_NONE, LEAF_NONE, LEAF_RCHUNK};
+    s.prog_op = {OP_LEAF, OP_STAT};
+    s.prog_arg = {3, 0};
+    s.rprog_ops = {{RP_LEAF, RP_LEAF, RP_OR, RP_LEAF, RP_NOT, RP_AND}};
+    s.R = 16;
+    s.T = 512;
+    s.group_mode = G_DENSE_LDS;
+    s.gcol = {0};
+    s.gmul = {1};
+    s.dense_slots = 1000;
+    s.agg_kind = {A_SUM};
+    s.agg_col = {1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64};
+    s.num_planes = 2;
     shapes.push_back(s);
   }
   for (int R : {8, 16, 32}) {  // statistics automaton input: every leaf's predicate bits written per lane

@@ -8,6 +8,28 @@
 #define PGX_J_MAX_LEAVES 16  // filter leaves (== kMaxLeaves)
 #define PGX_J_MAX_AGGS 8     // aggregation functions (== kMaxAggs)
 
+// Bitmap inverted-index leaf of one segment: the roaring bitmaps (byte offsets into the staged .bitmap.inv) whose OR
+// is the leaf's doc set (BitmapBasedFilterOperator.java:62-92).  pgx::RDesc on the host side.
+#define PGX_J_MAX_RPROG 24   // ops of one bitmap program (== kMaxRProg)
+#define PGX_J_MAX_RLEAVES 8  // leaves of one bitmap program (== kRProgMaxLeaves)
+struct JRDesc {
+  unsigned int* mask;            // separate-expansion path only: nchunks x 2048 words
+  const unsigned char* inv;      // device copy of <col>.bitmap.inv
+  const unsigned int* offs;      // byte offsets (into inv) of the roaring bitmaps to OR
+  int nb;                        // number of bitmaps
+  int nchunks;                   // ceil(total_docs / 65536)
+};
+// A filter sub-tree whose leaves are all bitmap leaves (AND / OR / NOT, postfix), for one segment.  pgx::RProg.
+struct JRProg {
+  unsigned int* mask;            // separate-expansion path only: nchunks x 2048 words
+  int nchunks;
+  int num_docs;                  // NOT flips inside [0, num_docs) (BitmapDocIdSet: flip(startDocId, endDocId + 1))
+  int nops;
+  signed char op[PGX_J_MAX_RPROG];   // 0 leaf, 1 AND, 2 OR, 3 NOT
+  short arg[PGX_J_MAX_RPROG];        // leaf: index into the JRDesc array (-1: empty leaf)
+  short ldesc[PGX_J_MAX_RLEAVES];    // the leaves' arg values in program order (LEAF_RCHUNK)
+};
+
 // Per-segment arguments of one launch group (segments whose columns share bit widths and value-image kinds).
 struct JSeg {
   long long tile_begin;                          // first tile of this segment inside the launch group
@@ -40,6 +62,7 @@ struct JArgs {
   unsigned long long* agg_out;   // aggregation-only: plane accumulators (plane 0 = matched docs)
   unsigned long long* stats;     // [0] docs matched, [1] entries scanned in filter
   unsigned long long* table;     // dense group-by: planes x slots
+  const struct JRDesc* rdesc;    // LEAF_RCHUNK leaves: the bitmap descriptors their programs index
 };
 
 #endif  // PGX_JIT_ABI_H_

@@ -100,3 +100,37 @@ def test_mixed_bitmap_and_scan_segments_in_one_query(ctx, segs, text):
             H.assert_values_equal(m[k], v, fns)
     else:
         H.assert_values_equal(blk.get_aggregation_result(), o["results"], fns)
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("text", QUERIES[9:])
+def test_bitmap_program_in_kernel_vs_separate_pass(ctx, segs, text, mode, monkeypatch):
+    """All-bitmap filter sub-trees evaluated per 65536-doc chunk inside the query kernel (LEAF_RCHUNK, PGX_RCHUNK=1)
+    or by the separate expansion pass (PGX_RCHUNK=0): both equal the oracle, statistics included, alone and in a
+    multi-segment launch whose workgroups start mid-chunk."""
+    from pinot_amd import engine as E
+    monkeypatch.setenv("PGX_RCHUNK", mode)
+    inv, scan, oseg = segs
+    q = pql.compile(text)
+    pm = E.InstancePlanMakerImplV2(ctx)
+    op = pm.make_inner_segment_plan(inv, q).run()
+    blk = op.next_block()
+    o = H.oracle_answer([oseg], q, literal=True)
+    fns = [a["fn"] for a in q["aggregations"]]
+    assert op.get_execution_statistics().as_list() == list(o["stats"])
+    blk3 = pm.make_inter_segment_plan([inv, scan, inv], q).execute()
+    o3 = H.oracle_answer([oseg, oseg, oseg], q, literal=True)
+    if q.get("group_by"):
+        m = blk.get_aggregation_group_by_result()
+        m = m.as_map() if m is not None else {}
+        assert set(m) == set(o["map"])
+        for k, v in o["map"].items():
+            H.assert_values_equal(m[k], v, fns)
+        m3 = blk3.get_aggregation_group_by_result()
+        m3 = m3.as_map() if m3 is not None else {}
+        assert set(m3) == set(o3["map"])
+        for k, v in o3["map"].items():
+            H.assert_values_equal(m3[k], v, fns)
+    else:
+        H.assert_values_equal(blk.get_aggregation_result(), o["results"], fns)
+        H.assert_values_equal(blk3.get_aggregation_result(), o3["results"], fns)

@@ -149,8 +149,12 @@ def test_c4_star_tree_bench_size(ctx):
         data.free()
 
 
-def test_c5_eight_segments(ctx):
+@pytest.mark.parametrize("rchunk", ["1", "0"])
+def test_c5_eight_segments(ctx, rchunk, monkeypatch):
+    """C5 at 8 x 2M rows, bitmap program evaluated inside the query kernel (the planner's choice at this selectivity)
+    and by the separate expansion pass."""
     from pinot_amd import engine as E
+    monkeypatch.setenv("PGX_RCHUNK", rchunk)
     wl = synth.WORKLOADS["c5"]
     seg_ids = list(range(8))
     data = synth.DeviceSegments(ctx, wl, seg_ids)
