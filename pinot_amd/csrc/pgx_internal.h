@@ -169,6 +169,11 @@ struct JitShape {
   bool leafmask = false;  // write every leaf's per-row predicate bit (statistics automaton input, pgx_stats.cpp)
   // LEAF_RCHUNK leaves, in leaf order: the bitmap program's postfix ops (RP_*), identical for the group's segments
   std::vector<std::vector<int>> rprog_ops;
+  // G_EMIT: records split 2^part_bits ways inside the kernel (first radix pass fused; 0 = row-order records), and the
+  // record's value field is the value column's dictId (sorted dictionary) instead of its offset from vbase
+  int part_bits = 0;
+  bool emit_dictid = false;
+  bool compact = false;   // pack each sub-step's selected rows into consecutive lanes before aggregating (selective)
 };
 
 // ----- numEntriesScannedInFilter automaton (pgx_stats.cpp builds it, pgx_kernels.hip pgx_fsm_* runs it) -----

@@ -103,7 +103,19 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // R + 2 words (conflict-free 16-byte LDS writes); rounds of stg_recs records when the budget is tight.
   int stg_off = -1, stg_recs = 0;
   const int stg_pitch = s.R + 2;
-  if (emit) {
+  // G_EMIT with part_bits: the sub-step's PT * PR records are split 2^part_bits ways in LDS (histogram, scan, one
+  // global cursor reservation per bucket, bucket-sorted staging) and leave as per-bucket runs: the first radix pass of
+  // the partitioned group-by, fused into the scan
+  const bool epart = emit && s.part_bits > 0;
+  const int pnb = 1 << s.part_bits;
+  int pst_off = -1, phist_off = -1;
+  if (epart) {
+    pst_off = lds;
+    lds += s.T * s.R * 8;
+    phist_off = lds;
+    lds += pnb * 16 + 16;  // hist (u32), offs (u32), gpos (u64), total
+  }
+  if (emit && !epart) {
     const int waves = s.T / 64;
     for (int r = 64 * s.R; r >= std::max(64, s.R); r /= 2)
       if (lds + (r / s.R) * stg_pitch * 8 * waves <= kLdsBudget) {
@@ -132,6 +144,22 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       scr_off = lds;
       lds += (int(sizeof(void*)) * 256 + 3 * 4 * 256 + 16 + 15) / 16 * 16;
     }
+  }
+  // compact: the selected rows of a sub-step are packed into consecutive lanes (wave prefix of the per-lane selection
+  // counts, the rows' dictIds staged in LDS) before values are looked up and aggregated, so a selective filter costs
+  // one gather / atomic wave-instruction per 64 SELECTED rows instead of PR mostly-idle ones per sub-step
+  std::vector<int> ccols;  // columns whose dictIds are staged: group columns, then aggregated value columns
+  int cst_off = -1;
+  const bool compact = s.compact && !emit && s.group_mode != G_HASH64 && s.group_mode != G_HASH128;
+  if (compact) {
+    if (grouped)
+      for (int c : s.gcol)
+        if (std::find(ccols.begin(), ccols.end(), c) == ccols.end()) ccols.push_back(c);
+    for (size_t a = 0; a < s.agg_kind.size(); ++a)
+      if (s.agg_kind[a] != A_COUNT && std::find(ccols.begin(), ccols.end(), s.agg_col[a]) == ccols.end())
+        ccols.push_back(s.agg_col[a]);
+    cst_off = lds;
+    lds += (s.T / 64) * 64 * std::max<int>(1, int(ccols.size())) * 4;
   }
   if (lds_bytes_out) *lds_bytes_out = lds;
   const bool any_img = lds > 0 && (tab_off != 0 || s.group_mode != G_DENSE_LDS);
@@ -185,6 +213,16 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   if (s.group_mode == G_DENSE_LDS) e.ln("u64* const tab = (u64*)(lds + ", tab_off / 4, ");");
   if (s.group_mode == G_DENSE_GLOBAL) e.ln("u64* const tab = A.table;");
   if (scr_off >= 0) e.ln("PgxRScratch& rscr = *(PgxRScratch*)(lds + ", scr_off / 4, ");");
+  if (compact) e.ln("u32* const cstg = lds + ", cst_off / 4, " + (tid >> 6) * ", 64 * std::max<size_t>(1, ccols.size()), ";");
+  if (epart) {
+    e.ln("u64* const pstage = (u64*)(lds + ", pst_off / 4, ");");
+    e.ln("u32* const phist = lds + ", phist_off / 4, ";");
+    e.ln("u32* const poffs = phist + ", pnb, ";");
+    e.ln("u64* const pgpos = (u64*)(phist + ", 2 * pnb, ");");
+    e.ln("u32* const ptotal = phist + ", 4 * pnb, ";");
+    e.ln("for (int i = tid; i < ", pnb, "; i += PT) phist[i] = 0u;");
+    e.ln("__syncthreads();");
+  }
   e.ln("u64 st_docs = 0, st_ent = 0;");
   e.ln("int seg = pgx_find_seg(A.segs, A.num_segs, tb);");
   e.ln("long long t = tb;");
@@ -275,6 +313,23 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       if (C.img == IMG_U32 || C.img == IMG_FOR16) need_vb[c] = true;
       else if (C.img == IMG_NONE) need_dict[c] = true;
     }
+  }
+  // Values gathered per selected row (no LDS image: HBM/L2 dictionary; group-key remaps): the row loop is split into a
+  // filter pass (selection bits), a gather pass that issues every selected row's loads back to back, and the
+  // aggregation pass; a gather inside the filtered row loop would wait for its load before the next row's.
+  std::vector<bool> gcolv(ncols, false), gremap(s.gcol.size(), false);
+  bool split = compact;
+  if (!emit) {
+    for (int c = 0; c < ncols; ++c)
+      if (need_dict[c]) {
+        bool summed = false;
+        for (int a = 0; a < naggs; ++a)
+          if (s.agg_col[a] == c && (grouped || s.agg_kind[a] == A_SUM || s.agg_kind[a] == A_AVG)) summed = true;
+        if (summed) gcolv[c] = split = true;
+      }
+    if (grouped)
+      for (size_t g = 0; g < s.gcol.size(); ++g)
+        if (s.cols[s.gcol[g]].remap) gremap[g] = split = true;
   }
   for (int c = 0; c < ncols; ++c) {
     if (need_vb[c]) e.ln("const i64 vb", c, " = S->vbase[", c, "];");
@@ -420,6 +475,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
           e.ln("u32 p", a, " = 0u;");
       }
     if (emit) e.ln("u64 recs[PR];");
+    if (split) e.ln("u32 msk = 0u;");
     if (s.leafmask)
       for (int l = 0; l < nleaves; ++l) e.ln("u32 lw", l, " = 0u;");
     e.ln("#pragma unroll");
@@ -474,6 +530,65 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     }
     e.ln("const bool m = ", st.empty() ? std::string("vj") : st.back(), ";");
     e.ln("wcnt += __popcll(__ballot(m));");
+    if (compact) {
+      const int ncw = int(std::max<size_t>(1, ccols.size()));
+      e.ln("msk |= (u32)m << j;");
+      e.ind = 5;
+      e.ln("}");
+      e.ln("const u32 ccnt = __popc(msk);");
+      e.ln("u32 cinc = ccnt;");
+      e.ln("#pragma unroll");
+      e.ln("for (int d = 1; d < 64; d <<= 1) { const u32 y = __shfl_up(cinc, d, 64); if (lane >= d) cinc += y; }");
+      e.ln("const u32 cexc = cinc - ccnt;");
+      e.ln("const u32 ctot = __shfl(cinc, 63, 64);");
+      e.ln("for (u32 cb = 0; cb < ctot; cb += 64) {");
+      e.ind = 6;
+      e.ln("u32 ck = cexc;");
+      e.ln("#pragma unroll");
+      e.ln("for (int j = 0; j < PR; ++j)");
+      e.ln("  if ((msk >> j) & 1u) {");
+      e.ln("    const u32 sl = ck - cb;");
+      e.ln("    if (sl < 64u) {");
+      for (size_t i = 0; i < ccols.size(); ++i) e.ln("      cstg[sl * ", ncw, " + ", i, "] = v", ccols[i], "[j];");
+      e.ln("    }");
+      e.ln("    ++ck;");
+      e.ln("  }");
+      e.ln("pgx_wave_lds_sync();");
+      e.ln("const bool m = (u32)lane < ((ctot - cb) < 64u ? (ctot - cb) : 64u);");
+      e.ln("{");
+      e.ind = 7;
+      e.ln("const int j = 0;");
+      for (size_t i = 0; i < ccols.size(); ++i)
+        e.ln("u32 v", ccols[i], "[1] = {m ? cstg[lane * ", ncw, " + ", i, "] : 0u};");
+      for (int c = 0; c < ncols; ++c)
+        if (gcolv[c]) e.ln(s.cols[c].fp ? "double" : "i64", " gv", c, "[1] = {m ? ", s.cols[c].fp ? "dd" : "di", c,
+                           "[v", c, "[0]] : 0};");
+      for (size_t g = 0; g < s.gcol.size(); ++g)
+        if (gremap[g]) e.ln("u32 gr", g, "[1] = {m ? (u32)rm", g, "[v", s.gcol[g], "[0]] : 0u};");
+    } else if (split) {
+      e.ln("msk |= (u32)m << j;");
+      e.ind = 5;
+      e.ln("}");
+      for (int c = 0; c < ncols; ++c)
+        if (gcolv[c]) {
+          const bool fp = s.cols[c].fp;
+          e.ln(fp ? "double" : "i64", " gv", c, "[PR];");
+          e.ln("#pragma unroll");
+          e.ln("for (int j = 0; j < PR; ++j) gv", c, "[j] = ((msk >> j) & 1u) ? ", fp ? "dd" : "di", c, "[v", c,
+               "[j]] : 0;");
+        }
+      for (size_t g = 0; g < s.gcol.size(); ++g)
+        if (gremap[g]) {
+          const int c = s.gcol[g];
+          e.ln("u32 gr", g, "[PR];");
+          e.ln("#pragma unroll");
+          e.ln("for (int j = 0; j < PR; ++j) gr", g, "[j] = ((msk >> j) & 1u) ? (u32)rm", g, "[v", c, "[j]] : 0u;");
+        }
+      e.ln("#pragma unroll");
+      e.ln("for (int j = 0; j < PR; ++j) {");
+      e.ind = 6;
+      e.ln("const bool m = (msk >> j) & 1u;");
+    }
     if (!grouped) {
       for (int a = 0; a < naggs; ++a) {
         const int k = s.agg_kind[a];
@@ -488,10 +603,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         } else if (C.fp) {
           const std::string val = (C.img == IMG_F64)
                                       ? "((const double*)lds)[" + std::to_string(img_off[c] / 8) + " + " + v + "]"
-                                      : "dd" + std::to_string(c) + "[" + v + "]";
+                                      : (gcolv[c] ? "gv" + std::to_string(c) + "[j]" : "dd" + std::to_string(c) + "[" + v + "]");
           e.ln("if (m) acc", a, " += ", val, ";");
         } else if (C.img == IMG_NONE) {
-          e.ln("if (m) acc", a, " += di", c, "[", v, "];");
+          if (gcolv[c]) e.ln("acc", a, " += gv", c, "[j];");  // 0 for unselected rows
+          else e.ln("if (m) acc", a, " += di", c, "[", v, "];");
         } else if (C.acc32) {
           e.ln("{ const u32 x = ", img_value(s, c, img_off, v), "; p", a, " += m ? x : 0u; }");
         } else {
@@ -514,8 +630,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         std::string x = "0u";
         if (s.emit_col >= 0) {
           const std::string ec = std::to_string(s.emit_col);
-          x = s.cols[s.emit_col].img != IMG_NONE ? img_value(s, s.emit_col, img_off, "v" + ec + "[j]")
-                                                 : "(u32)(di" + ec + "[v" + ec + "[j]] - S->vbase[" + ec + "])";
+          if (s.emit_dictid) x = "v" + ec + "[j]";  // the value's dictId (sorted dictionary): looked up at aggregation
+          else x = s.cols[s.emit_col].img != IMG_NONE ? img_value(s, s.emit_col, img_off, "v" + ec + "[j]")
+                                                      : "(u32)(di" + ec + "[v" + ec + "[j]] - S->vbase[" + ec + "])";
         }
         e.ln("  rec = (", key, ") | ((u64)(", x, ") << ", s.keybits, ");");
         e.ln("}");
@@ -528,7 +645,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       for (size_t g = 0; g < s.gcol.size(); ++g) {
         const int c = s.gcol[g];
         std::string id = "v" + std::to_string(c) + "[j]";
-        if (s.cols[c].remap) id = "(u32)rm" + std::to_string(g) + "[" + id + "]";
+        if (s.cols[c].remap) id = gremap[g] ? "gr" + std::to_string(g) + "[j]" : "(u32)rm" + std::to_string(g) + "[" + id + "]";
         if (!key.empty()) key += " + ";
         key += id + " * " + std::to_string(s.gmul[g]) + "u";
       }
@@ -542,8 +659,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         const std::string id = "v" + std::to_string(c) + "[j]";
         std::string val;  // i64 or double expression
         if (C.fp) val = (C.img == IMG_F64) ? "((const double*)lds)[" + std::to_string(img_off[c] / 8) + " + " + id + "]"
-                                            : "dd" + std::to_string(c) + "[" + id + "]";
-        else if (C.img == IMG_NONE) val = "di" + std::to_string(c) + "[" + id + "]";
+                                            : (gcolv[c] ? "gv" + std::to_string(c) + "[j]" : "dd" + std::to_string(c) + "[" + id + "]");
+        else if (C.img == IMG_NONE) val = gcolv[c] ? "gv" + std::to_string(c) + "[j]" : "di" + std::to_string(c) + "[" + id + "]";
         else val = "(vb" + std::to_string(c) + " + (i64)" + img_value(s, c, img_off, id) + ")";
         std::string enc;
         if (k == A_MIN || k == A_MAX) enc = C.fp ? "pgx_ord_f64(" + val + ")" : "pgx_ord_i64(" + val + ")";
@@ -556,6 +673,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     }
     e.ind = 5;
     e.ln("}");
+    if (compact) {
+      e.ln("  pgx_wave_lds_sync();");
+      e.ln("}");
+    }
     if (!grouped)
       for (int a = 0; a < naggs; ++a) {
         const int k = s.agg_kind[a];
@@ -571,7 +692,43 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         e.ln("  ((PGX_G ", ty, "*)(S->lmask + ", l, " * S->lmask_words))[r0 / PR] = (", ty, ")lw", l, ";");
       e.ln("}");
     }
-    if (emit && stg_recs) {
+    if (epart) {
+      const std::string KM = std::to_string((1ull << s.keybits) - 1ull) + "ull";
+      const std::string SH = std::to_string(64 - s.part_bits);
+      e.ln("{");
+      e.ln("  u32 rk[PR];");
+      e.ln("  #pragma unroll");
+      e.ln("  for (int j = 0; j < PR; ++j)");
+      e.ln("    rk[j] = recs[j] != ~0ull ? atomicAdd(&phist[(u32)(pgx_part_mix(recs[j] & ", KM, ") >> ", SH,
+           ")], 1u) : 0u;");
+      e.ln("  pgx_lds_barrier();");
+      e.ln("  pgx_scan_buckets<", pnb, ">(phist, poffs, ptotal, tid);");
+      e.ln("  pgx_lds_barrier();");
+      e.ln("  if (tid < ", pnb, ") {");
+      e.ln("    const u32 h = phist[tid];");
+      e.ln("    if (h) {");
+      e.ln("      const u64 g = atomicAdd(A.part_cursor + (long long)tid * A.part_cstride, (u64)h);");
+      e.ln("      pgpos[tid] = g;");
+      e.ln("      if (g + h > (u64)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
+      e.ln("    }");
+      e.ln("    phist[tid] = 0u;  // ready for the next sub-step (its atomics follow two barriers)");
+      e.ln("  }");
+      e.ln("  pgx_lds_barrier();");
+      e.ln("  #pragma unroll");
+      e.ln("  for (int j = 0; j < PR; ++j)");
+      e.ln("    if (recs[j] != ~0ull) pstage[poffs[(u32)(pgx_part_mix(recs[j] & ", KM, ") >> ", SH, ")] + rk[j]] = recs[j];");
+      e.ln("  pgx_lds_barrier();");
+      e.ln("  const int tot = (int)*ptotal;");
+      e.ln("  PGX_G u64* const pout = (PGX_G u64*)A.table;");
+      e.ln("  for (int i = tid; i < tot; i += PT) {");
+      e.ln("    const u64 v = pstage[i];");
+      e.ln("    const u32 b = (u32)(pgx_part_mix(v & ", KM, ") >> ", SH, ");");
+      e.ln("    const u64 pos = pgpos[b] + (u64)(i - (int)poffs[b]);");
+      e.ln("    if (pos < (u64)A.part_cap) pout[(long long)b * A.part_cap + (long long)pos] = v;");
+      e.ln("  }");
+      e.ln("  pgx_lds_barrier();");
+      e.ln("}");
+    } else if (emit && stg_recs) {
       const int L = stg_recs / s.R;  // lanes whose records fill one round
       int lg = 0;
       while ((1 << lg) < L) ++lg;
@@ -724,6 +881,9 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   add(s.gmul);
   add(s.gshift);
   for (const auto& ops : s.rprog_ops) add(ops);
+  k.push_back(s.part_bits);
+  k.push_back(s.emit_dictid);
+  k.push_back(s.compact);
   return k;
 }
 
@@ -989,6 +1149,19 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.plane_op = {P_ADD_I64, P_ADD_I64};
     s.num_planes = 2;
     shapes.push_back(s);
+    s.compact = true;  // selected rows packed into consecutive lanes before the gathers and atomics
+    shapes.push_back(s);
+    s.group_mode = G_NONE;  // aggregation-only, compacted, every function
+    s.gcol.clear();
+    s.gmul.clear();
+    s.agg_kind = {A_COUNT, A_SUM, A_MIN, A_MAX, A_AVG};
+    s.agg_col = {-1, 1, 1, 1, 1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64, P_ADD_I64, P_MIN_ORD, P_MAX_ORD, P_ADD_I64};
+    s.num_planes = 6;
+    shapes.push_back(s);
+    s.cols[1].img = IMG_U32;  // ... with a value image
+    s.cols[1].img_words = 1024;
+    shapes.push_back(s);
   }
   for (int R : {8, 16, 32}) {  // statistics automaton input: every leaf's predicate bits written per lane
     JitShape s = base(R == 8 ? 8 : (R == 16 ? 10 : 7), 16, IMG_FOR16, 11);
@@ -1025,6 +1198,9 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     shapes.push_back(s);
     s.cols[1].img = IMG_NONE;  // value image demoted (LDS budget): values from the HBM dictionary
     s.cols[2].remap = true;
+    shapes.push_back(s);
+    s.part_bits = 7;           // first radix pass fused, dictId records (the C3 path)
+    s.emit_dictid = true;
     shapes.push_back(s);
   }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {

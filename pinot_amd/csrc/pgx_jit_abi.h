@@ -63,6 +63,10 @@ struct JArgs {
   unsigned long long* stats;     // [0] docs matched, [1] entries scanned in filter
   unsigned long long* table;     // dense group-by: planes x slots
   const struct JRDesc* rdesc;    // LEAF_RCHUNK leaves: the bitmap descriptors their programs index
+  unsigned long long* part_cursor;   // G_EMIT with part_bits: bucket b appends at part_cursor[b * part_cstride]
+  unsigned long long* part_overflow; // ... counts buckets that ran past part_cap records
+  long long part_cap;                // records per bucket; bucket b's records at table + b * part_cap
+  long long part_cstride;
 };
 
 #endif  // PGX_JIT_ABI_H_

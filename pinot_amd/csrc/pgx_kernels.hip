@@ -963,7 +963,8 @@ template <bool PACK, bool MN, bool MX>
 __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t* __restrict__ in,
                                                                   const unsigned long long* __restrict__ in_cnt,
                                                                   int cstride, int64_t cap, uint64_t keymask,
-                                                                  int keybits, int64_t vbase, int pack_shift,
+                                                                  int keybits, int64_t vbase,
+                                                                  const int64_t* __restrict__ vdict, int pack_shift,
                                                                   uint64_t* __restrict__ okey,
                                                                   uint64_t* __restrict__ oplane, int64_t ocap,
                                                                   unsigned long long* __restrict__ ocount,
@@ -988,6 +989,7 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
   const int64_t n = min(static_cast<int64_t>(in_cnt[static_cast<int64_t>(part) * cstride]), cap);
   const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) + static_cast<int64_t>(part) * cap;
   const unsigned long long one = PACK ? (1ull << pack_shift) : 0ull;
+  const PGX_GLOBAL int64_t* vd = (const PGX_GLOBAL int64_t*)vdict;  // dictId records: value = vd[id] (sorted dictionary)
   bool lost = false;
   for (int64_t base = 0; base < n; base += kAggThreads * kAggPer) {
     uint64_t rec[kAggPer];
@@ -996,11 +998,17 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
       const int64_t i = base + k * kAggThreads + tid;
       rec[k] = i < n ? __builtin_nontemporal_load(src + i) : kNoRecord;
     }
+    unsigned int sv[kAggPer];  // the values to sum: the record's offset, or (dictId records) gathered, all in flight
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) {
+      const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);
+      sv[k] = vd ? (rec[k] != kNoRecord ? static_cast<unsigned int>(vd[v] - vbase) : 0u) : v;
+    }
 #pragma unroll
     for (int k = 0; k < kAggPer; ++k) {
       if (rec[k] == kNoRecord) continue;
       const uint64_t key = rec[k] & keymask;
-      const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);
+      const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);  // value offset, or dictId (vd)
       unsigned int bk = static_cast<unsigned int>(part_mix(key)) & (kAggBuckets - 1);
       int slot = -1;
       for (int t = 0; t < kAggBuckets;) {
@@ -1020,10 +1028,10 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
       }
       if (slot < 0) { lost = true; continue; }
       if (PACK) {
-        atomicAdd(&tsum[slot], one + v);
+        atomicAdd(&tsum[slot], one + sv[k]);
       } else {
         atomicAdd(&tcnt[slot], 1u);
-        atomicAdd(&tsum[slot], static_cast<unsigned long long>(v));
+        atomicAdd(&tsum[slot], static_cast<unsigned long long>(sv[k]));
       }
       if (MN) atomicMin(&tmin[slot], v);
       if (MX) atomicMax(&tmax[slot], v);
@@ -1050,8 +1058,10 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
     oplane[o] = c;  // plane 0: doc count
     // planes 1..3: sum (int64 incl. vbase * count), min, max (ordered encodings of the int64 value)
     oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(sm) + static_cast<int64_t>(c) * vbase);
-    oplane[2 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(lo)) ^ 0x8000000000000000ull;
-    oplane[3 * ocap + o] = static_cast<unsigned long long>(vbase + static_cast<int64_t>(hi)) ^ 0x8000000000000000ull;
+    const int64_t vlo = vd ? (MN ? vd[lo] : 0) : vbase + static_cast<int64_t>(lo);  // min / max of dictIds -> values
+    const int64_t vhi = vd ? (MX ? vd[hi] : 0) : vbase + static_cast<int64_t>(hi);
+    oplane[2 * ocap + o] = static_cast<unsigned long long>(vlo) ^ 0x8000000000000000ull;
+    oplane[3 * ocap + o] = static_cast<unsigned long long>(vhi) ^ 0x8000000000000000ull;
     ++o;
   }
 }
@@ -1276,7 +1286,7 @@ extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in
 
 extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
                                                 int nparts, int64_t cap, uint64_t keymask, int keybits, int64_t vbase,
-                                                int need_sum, int need_min, int need_max, int pack_shift,
+                                                const int64_t* vdict, int need_sum, int need_min, int need_max, int pack_shift,
                                                 uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream) {
@@ -1286,7 +1296,7 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
 #define PGX_AGG_CASE(K, A, B, C)                                                                                   \
   case K:                                                                                                           \
     hipLaunchKernelGGL((pgx::pgx_part_aggregate<A, B, C>), dim3(nparts), dim3(pgx::kAggThreads), 0, stream, in,     \
-                       in_cnt, cstride, cap, keymask, keybits, vbase, pack_shift, okey, oplane, ocap, ocount,       \
+                       in_cnt, cstride, cap, keymask, keybits, vbase, vdict, pack_shift, okey, oplane, ocap, ocount, \
                        overflow);                                                                                   \
     break;
   switch (sel) {

@@ -24,8 +24,15 @@ def main():
     queries = {"c5": wl.query,
                "c5_count": "SELECT COUNT(*) FROM T WHERE (%s OR f2 = 7) AND f3 <> 3 GROUP BY gk TOP 10" % f1,
                "c5_nogroup": "SELECT SUM(m) FROM T WHERE (%s OR f2 = 7) AND f3 <> 3" % f1,
-               "scan_only": "SELECT SUM(m) FROM T GROUP BY gk TOP 10"}
-    variants = [("sep", {"PGX_RCHUNK": "0"}), ("rchunk", {"PGX_RCHUNK": "1"})]
+               "scan_only": "SELECT SUM(m) FROM T GROUP BY gk TOP 10",
+               "c2like": "SELECT COUNT(*), SUM(m) FROM T WHERE gk BETWEEN 0 AND 499",
+               "c2like_f1": "SELECT COUNT(*), SUM(m) FROM T WHERE f1 BETWEEN 0 AND 499"}
+    only = os.environ.get("VARIANT_QUERIES")
+    if only:
+        queries = {k: v for k, v in queries.items() if k in only.split(",")}
+    variants = [("sep", {"PGX_RCHUNK": "0", "PGX_COMPACT": "0"}), ("sep+compact", {"PGX_RCHUNK": "0", "PGX_COMPACT": "1"}),
+                ("rchunk", {"PGX_RCHUNK": "1", "PGX_COMPACT": "0"}),
+                ("rchunk+compact", {"PGX_RCHUNK": "1", "PGX_COMPACT": "1"})]
     for qn, text in queries.items():
         q = E._Query(ctx, pql.compile(text))
         binds, keep = q.bindings(segs)
