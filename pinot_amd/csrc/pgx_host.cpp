@@ -2131,6 +2131,17 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
       maxleaves = std::max(maxleaves, nl);
     }
     if (std::getenv("PGX_RPROG_NARROW")) maxleaves = 0;
+    // per-segment container walk when every program's bitmaps fit one lane each (PGX_RPROG_SEG=0: per-chunk kernels)
+    bool seg_walk = maxleaves >= 1;
+    if (const char* e = std::getenv("PGX_RPROG_SEG")) seg_walk = seg_walk && e[0] == '1';
+    for (size_t i = 0; i < P.rprogs.size() && seg_walk; ++i) {
+      int nb = 0;
+      const RProg& r = P.rprogs[i];
+      for (int k = 0; k < r.nops; ++k)
+        if (r.op[k] == RP_LEAF && r.arg[k] >= 0) nb += P.roar[r.arg[k]].nb;
+      if (nb > 512) seg_walk = false;
+    }
+    if (seg_walk) maxleaves = -maxleaves;
     hip_check(pgx_launch_roaring_program(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, maxleaves, st),
               "bitmap program launch");
   } else if (P.rdesc_dev) {

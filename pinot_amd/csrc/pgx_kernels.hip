@@ -845,6 +845,157 @@ __global__ void __launch_bounds__(256) pgx_roaring_program_wide(const RProg* __r
   }
 }
 
+// One workgroup per (segment, program), walking the segment's 65536-doc chunks in order.  Every bitmap of the program
+// (<= kSegRBitmaps, one lane each) keeps a cursor into its sorted container keys, and the key / cardinality / offset of
+// its NEXT container are loaded while the current chunk is expanded, so a chunk costs the element and bitmap-word loads
+// only (the per-chunk kernels above pay a container search of four dependent loads per chunk).  Array elements spread
+// over all lanes (4 loads in flight each), bitmap-container words too; the AND / OR / NOT program is evaluated per mask
+// word in registers and the chunk's mask written out.
+constexpr int kSegRThreads = 512;
+constexpr int kSegRBitmaps = 512;
+__global__ void __launch_bounds__(kSegRThreads) pgx_roaring_program_seg(const RProg* __restrict__ progs,
+                                                                        const RDesc* __restrict__ descs, int nprogs) {
+  const int pi = static_cast<int>(blockIdx.x);
+  if (pi >= nprogs) return;
+  const RProg& P = progs[pi];
+  extern __shared__ uint32_t lmask[];  // [leaf][2048]
+  __shared__ const uint8_t* cptr[kSegRBitmaps];
+  __shared__ int ccard[kSegRBitmaps], cpre[kSegRBitmaps + 1], cleaf[kSegRBitmaps];
+  __shared__ int ncont;
+  const int tid = threadIdx.x;
+  // leaves in program order (uniform loads)
+  int leaf_desc[kRProgMaxLeaves], leaf_b0[kRProgMaxLeaves + 1];
+  int nl = 0, tot = 0;
+  for (int i = 0; i < P.nops; ++i)
+    if (P.op[i] == RP_LEAF && nl < kRProgMaxLeaves) {
+      const int a = P.arg[i];
+      leaf_desc[nl] = a;
+      leaf_b0[nl] = tot;
+      tot += a >= 0 ? descs[a].nb : 0;
+      ++nl;
+    }
+  leaf_b0[nl] = tot;
+  const int total_b = tot;  // the host launches this kernel only when total_b <= kSegRBitmaps
+  // this lane's bitmap: header, container count and the fields of its first container
+  const uint8_t* base = nullptr;
+  int n = 0, cur = 0, key = 1 << 30, card = 0, leaf = 0;
+  uint32_t off = 0;
+  if (tid < total_b) {
+    int j = 0;
+    while (leaf_b0[j + 1] <= tid) ++j;
+    leaf = j;
+    const RDesc& D = descs[leaf_desc[j]];
+    base = D.inv + D.offs[tid - leaf_b0[j]];
+    n = static_cast<int>(rd32(base + 4));
+    if (n > 0) {
+      key = static_cast<int>(rd16(base + 8));
+      card = static_cast<int>(rd16(base + 10)) + 1;
+      off = rd32(base + 8 + 4 * n);
+    }
+  }
+  for (int chunk = 0; chunk < P.nchunks; ++chunk) {
+    for (int i = tid; i < nl * 2048; i += kSegRThreads) lmask[i] = 0u;
+    if (tid == 0) ncont = 0;
+    __syncthreads();
+    if (key == chunk) {
+      const int slot = atomicAdd(&ncont, 1);
+      cptr[slot] = base + off;
+      ccard[slot] = card;
+      cleaf[slot] = leaf;
+      // advance the cursor and prefetch the next container's fields (consumed at a later chunk)
+      ++cur;
+      if (cur < n) {
+        key = static_cast<int>(rd16(base + 8 + 4 * cur));
+        card = static_cast<int>(rd16(base + 8 + 4 * cur + 2)) + 1;
+        off = rd32(base + 8 + 4 * n + 4 * cur);
+      } else {
+        key = 1 << 30;
+      }
+    }
+    __syncthreads();
+    const int nc = ncont;
+    if (tid < 64) {  // exclusive prefix of the array containers' cardinalities (8 per lane)
+      int v[8], x = 0;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = tid * 8 + q;
+        v[q] = (k < nc && ccard[k] <= 4096) ? ccard[k] : 0;
+        x += v[q];
+      }
+      int incl = x;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (tid >= d) incl += y;
+      }
+      int e = incl - x;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (tid * 8 + q < kSegRBitmaps) cpre[tid * 8 + q] = e;
+        e += v[q];
+      }
+      if (tid == 63) cpre[kSegRBitmaps] = incl;
+    }
+    __syncthreads();
+    const int ne = cpre[kSegRBitmaps];
+    for (int e0 = 0; e0 < ne; e0 += 4 * kSegRThreads) {
+      uint32_t val[4];
+      int dst[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int e = e0 + q * kSegRThreads + tid;
+        dst[q] = -1;
+        if (e < ne) {
+          int lo = 0, hi = nc - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (cpre[mid] <= e) lo = mid; else hi = mid - 1;
+          }
+          val[q] = rd16(cptr[lo] + 2 * (e - cpre[lo]));
+          dst[q] = cleaf[lo] * 2048;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if (dst[q] >= 0) atomicOr(&lmask[dst[q] + (val[q] >> 5)], 1u << (val[q] & 31u));
+    }
+    for (int k = 0; k < nc; ++k) {  // bitmap containers: all words in flight, then the ORs
+      if (ccard[k] <= 4096) continue;
+      const uint8_t* c = cptr[k];
+      uint32_t* m = lmask + cleaf[k] * 2048;
+      uint32_t x[2048 / kSegRThreads];
+#pragma unroll
+      for (int q = 0; q < 2048 / kSegRThreads; ++q) x[q] = rd32(c + 4 * (q * kSegRThreads + tid));
+#pragma unroll
+      for (int q = 0; q < 2048 / kSegRThreads; ++q)
+        if (x[q]) atomicOr(&m[q * kSegRThreads + tid], x[q]);
+    }
+    __syncthreads();
+    const int64_t doc0 = static_cast<int64_t>(chunk) << 16;
+    uint32_t* out = P.mask + static_cast<size_t>(chunk) * 2048;
+    for (int w = tid; w < 2048; w += kSegRThreads) {
+      uint32_t st[kRProgStack + 4];
+      int sp = 0, lf = 0;
+      const int64_t d = doc0 + 32 * w;
+      const uint32_t keep = d >= P.num_docs ? 0u : (d + 32 > P.num_docs ? (1u << (P.num_docs - d)) - 1u : 0xFFFFFFFFu);
+      for (int i = 0; i < P.nops; ++i) {
+        const int op = P.op[i];
+        if (op == RP_LEAF) {
+          st[sp++] = lmask[lf * 2048 + w];
+          ++lf;
+        } else if (op == RP_NOT) {
+          st[sp - 1] = ~st[sp - 1] & keep;
+        } else {
+          st[sp - 2] = op == RP_AND ? (st[sp - 2] & st[sp - 1]) : (st[sp - 2] | st[sp - 1]);
+          --sp;
+        }
+      }
+      out[w] = st[0];
+    }
+    __syncthreads();  // lmask is zeroed for the next chunk
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // High-cardinality group-by (LONG_MAP semantics, DefaultGroupKeyGenerator.java:239-246 / :429-441): the reference
 // probes a Long2IntOpenHashMap per doc; at 10^7 groups a device-wide hash table turns every row into random HBM atomics.
@@ -1332,6 +1483,11 @@ extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const 
                                                  int maxchunks, int maxleaves, hipStream_t stream) {
   if (nprogs <= 0 || maxchunks <= 0) return hipSuccess;
   const long long blocks = static_cast<long long>(nprogs) * maxchunks;
+  if (maxleaves < 0 && -maxleaves <= pgx::kRProgMaxLeaves) {  // per-segment walk (host: every program <= 512 bitmaps)
+    hipLaunchKernelGGL(pgx::pgx_roaring_program_seg, dim3(static_cast<unsigned>(nprogs)), dim3(pgx::kSegRThreads),
+                       static_cast<size_t>(-maxleaves) * 2048 * 4, stream, progs, descs, nprogs);
+    return hipGetLastError();
+  }
   if (maxleaves >= 1 && maxleaves <= pgx::kRProgMaxLeaves) {
     hipLaunchKernelGGL(pgx::pgx_roaring_program_wide, dim3(static_cast<unsigned>(blocks)), dim3(256),
                        static_cast<size_t>(maxleaves) * 2048 * 4, stream, progs, descs, nprogs, maxchunks);

@@ -102,14 +102,17 @@ def test_mixed_bitmap_and_scan_segments_in_one_query(ctx, segs, text):
         H.assert_values_equal(blk.get_aggregation_result(), o["results"], fns)
 
 
-@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("mode", ["0", "0chunk", "1"])
 @pytest.mark.parametrize("text", QUERIES[9:])
 def test_bitmap_program_in_kernel_vs_separate_pass(ctx, segs, text, mode, monkeypatch):
     """All-bitmap filter sub-trees evaluated per 65536-doc chunk inside the query kernel (LEAF_RCHUNK, PGX_RCHUNK=1)
-    or by the separate expansion pass (PGX_RCHUNK=0): both equal the oracle, statistics included, alone and in a
-    multi-segment launch whose workgroups start mid-chunk."""
+    or by the separate expansion pass (PGX_RCHUNK=0): one workgroup per segment walking every bitmap's containers in
+    key order (default), or one workgroup per (segment, chunk) with a container search ("0chunk", PGX_RPROG_SEG=0).
+    All equal the oracle, statistics included, alone and in a multi-segment launch whose workgroups start
+    mid-chunk."""
     from pinot_amd import engine as E
-    monkeypatch.setenv("PGX_RCHUNK", mode)
+    monkeypatch.setenv("PGX_RCHUNK", mode[0])
+    monkeypatch.setenv("PGX_RPROG_SEG", "0" if mode == "0chunk" else "1")
     inv, scan, oseg = segs
     q = pql.compile(text)
     pm = E.InstancePlanMakerImplV2(ctx)

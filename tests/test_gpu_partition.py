@@ -241,3 +241,24 @@ def test_group_partials_split_then_merged_equal_one_launch(ctx):
     assert set(merged) == set(whole) and len(whole) > 20000
     for k, v in whole.items():
         H.assert_values_equal(merged[k], v, fns)
+
+
+@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("text", [AGGS + " GROUP BY g2, a, c", "SELECT COUNT(*) FROM t WHERE a > 0 GROUP BY a, c",
+                                  "SELECT MIN(m), MAX(m) FROM t WHERE b <> %(b1)s GROUP BY c, g2, s, g1"])
+def test_fused_first_pass_equals_oracle(ctx, seg, text, fused, monkeypatch):
+    """PGX_PART_FUSED=1: the scan kernel splits its records 128 ways itself (LDS histogram, per-bucket cursor
+    reservation, bucket-sorted staging) and the records carry the value's dictId (sorted dictionary: MIN / MAX of ids,
+    SUM by lookup while aggregating); =0: row-order records and a separate first pass.  COUNT-only keys always take
+    the fused pass.  Both against the oracle."""
+    monkeypatch.setenv("PGX_PART_FUSED", fused)
+    gseg, oseg, fmt = seg
+    q = pql.compile(text % fmt)
+    blk, st = _run_inner(ctx, gseg, q)
+    o = H.oracle_answer([oseg], q, literal=True)
+    assert st.as_list() == list(o["stats"])
+    m = _map(blk)
+    assert set(m) == set(o["map"])
+    fns = [a["fn"] for a in q["aggregations"]]
+    for k, v in o["map"].items():
+        H.assert_values_equal(m[k], v, fns)
