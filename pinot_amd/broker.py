@@ -9,7 +9,8 @@ core/query/reduce/BrokerReduceService.java:62-256).  Here:
   path) and wraps the combined block in an ``InstanceResponse``: the aggregation intermediates (count as int, sum / min /
   max as double, avg as (sum, count)) or, for group-by, the trimmed combine maps (one {group string: intermediate} per
   function), plus the four execution statistics and any processing exception (ServerQueryExecutorV1Impl.java:118-176).
-  The response is an in-process object; the DataTable byte format (common/utils/DataTable.java:315-482) is not produced.
+  ``datatable.response_to_datatable`` serializes it as the reference's DataTable bytes (version 2, custom ser/de;
+  common/utils/DataTable.java:315-482) and the reduce accepts either form.
 * ``BrokerReduceService.reduce_on_data_table`` sums the statistics, turns exception responses into processing
   exceptions, reduces aggregation results with each function's ``reduce`` and group-by maps with ``combineTwoValues``
   + ``reduce`` (query/aggregation/groupby/AggregationGroupByOperatorService.java:93-129), keeps the top N groups per
@@ -194,6 +195,9 @@ class BrokerReduceService:
         for server, resp in responses.items():
             if resp is None:
                 continue
+            if isinstance(resp, (bytes, bytearray)):  # a serialized DataTable (pinot_amd/datatable.py)
+                from .datatable import datatable_to_response
+                resp = datatable_to_response(broker_request, bytes(resp))
             if resp.aggregation is None and resp.group_by is None:  # schema-less: exception metadata only
                 for code, msg in resp.exceptions.items():
                     out.processing_exceptions.append(QueryProcessingException(int(code), msg))
