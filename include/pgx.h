@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGX_ABI_VERSION 3
+#define PGX_ABI_VERSION 4
 
 typedef enum {
   PGX_OK = 0,
@@ -47,7 +47,10 @@ typedef enum {
 
 typedef enum { PGX_INT = 0, PGX_LONG = 1, PGX_FLOAT = 2, PGX_DOUBLE = 3, PGX_STRING = 4 } pgx_data_type;
 
-typedef enum { PGX_COUNT = 0, PGX_SUM = 1, PGX_MIN = 2, PGX_MAX = 3, PGX_AVG = 4 } pgx_agg_fn;
+/* The *MV functions aggregate every value of a multi-value column in the selected docs
+ * (operator/aggregation/function/{Count,Sum,Min,Max,Avg}MVAggregationFunction.java); aggregation-only queries. */
+typedef enum { PGX_COUNT = 0, PGX_SUM = 1, PGX_MIN = 2, PGX_MAX = 3, PGX_AVG = 4,
+               PGX_COUNTMV = 5, PGX_SUMMV = 6, PGX_MINMV = 7, PGX_MAXMV = 8, PGX_AVGMV = 9 } pgx_agg_fn;
 
 /* Predicate kinds (common/Predicate.java Type); they select the physical filter operator exactly as
  * plan/FilterPlanNode.java:118-132 does and drive the numEntriesScannedInFilter statistic. */
@@ -96,6 +99,9 @@ typedef struct {
   int32_t pad_char;           /* STRING padding byte: metadata "segment.padding.character" ('\0'), '%' when the key
                                  is absent (legacy segments, ColumnMetadata.java:93-98); StringDictionary.get cuts at
                                  its first occurrence (StringDictionary.java:53-66) */
+  int32_t is_multi_value;     /* 1: fwd holds <col>.mv.fwd (io/writer/impl/v1/FixedBitMultiValueWriter.java: chunk
+                                 offsets, doc-start bitset, fixed-bit values; ColumnIndexContainer.java:78) */
+  int32_t total_entries;      /* metadata totalNumberOfEntries (multi-value columns) */
 } pgx_column_desc;
 
 typedef struct {

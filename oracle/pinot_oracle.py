@@ -112,6 +112,7 @@ class OColumn:
     is_sorted: bool
     has_inverted: bool
     bits: int
+    mv_ids: Optional[List[np.ndarray]] = None  # multi-value column: the dictIds of every doc (dict_ids: all values)
 
     @property
     def card(self) -> int:
@@ -160,6 +161,18 @@ class OSegment:
         cols = {}
         n = None
         for name, vals in raw.items():
+            if isinstance(vals, list) and vals and isinstance(vals[0], (list, tuple, np.ndarray)):
+                # multi-value column: one dictionary over every value (SegmentDictionaryCreator), per-doc id arrays
+                n = len(vals) if n is None else n
+                lens = [len(v) for v in vals]
+                flat = np.concatenate([np.asarray(v) for v in vals])
+                dt = (dtypes or {}).get(name) or ("INT" if flat.dtype.kind in "iu" else "DOUBLE")
+                dictionary, ids = np.unique(flat, return_inverse=True)
+                starts = np.concatenate([[0], np.cumsum(lens)])
+                per = [ids[starts[d]:starts[d + 1]].astype(np.int64) for d in range(n)]
+                cols[name] = OColumn(name, dt, dictionary, ids.astype(np.int64), False, name in inverted,
+                                     get_num_of_bits(len(dictionary)), per)
+                continue
             vals = np.asarray(vals)
             n = len(vals) if n is None else n
             dt = (dtypes or {}).get(name)
@@ -882,6 +895,20 @@ def _flag(c):
 _PRIORITY = {"sorted": 0, "and": 1, "bitmap": 2, "scan": 3, "or": 4}
 
 
+def mv_doc_view(col: OColumn, ev: Evaluator):
+    """A multi-value leaf as a per-doc predicate: the evaluators' apply(int[]) (operator/filter/predicate/
+    {Equals,In,RangeOffline}PredicateEvaluator.java: ANY value matches; NotEquals / NotIn: NO value is excluded) driven
+    by MVScanDocIdIterator (operator/dociditerators/MVScanDocIdIterator.java:78-121, one entry scanned per doc), or
+    the bitmap of every doc holding a matching (excluded) value, flipped for NEQ / NOT_IN (BitmapBasedFilterOperator).
+    Returned as a pseudo single-value column whose dictId of doc d is d, so the iterator algebra applies unchanged."""
+    neg = ev.kind in ("NEQ", "NOT_IN")
+    doc = np.array([bool(ev.match[v].all()) if neg else bool(ev.match[v].any()) for v in col.mv_ids], dtype=bool)
+    n = len(col.mv_ids)
+    pcol = OColumn(col.name, col.dtype, col.dictionary, np.arange(n, dtype=np.int64), False, col.has_inverted, col.bits)
+    pev = Evaluator(ev.kind, doc, np.nonzero(doc)[0], np.nonzero(~doc)[0] if neg else None, ev.always_false)
+    return pcol, pev
+
+
 def build_filter(seg: OSegment, tree: Optional[dict]):
     """FilterPlanNode.constructPhysicalOperator + reorder (plan/FilterPlanNode.java:77-170)."""
     if tree is None:
@@ -894,6 +921,8 @@ def build_filter(seg: OSegment, tree: Optional[dict]):
         return _AndSet(kids) if op == "AND" else _OrSet(kids)
     col = seg.columns[tree["column"]]
     ev = make_evaluator(col, tree)
+    if col.mv_ids is not None:
+        col, ev = mv_doc_view(col, ev)
     if col.has_inverted and op != "RANGE":
         if col.is_sorted:
             return _SortedSet(col, ev, start, end)
@@ -933,13 +962,17 @@ def filter_mask_vectorized(seg: OSegment, tree: Optional[dict]) -> np.ndarray:
         return m
     col = seg.columns[tree["column"]]
     ev = make_evaluator(col, tree)
+    if col.mv_ids is not None:
+        col, ev = mv_doc_view(col, ev)
     return ev.match[col.dict_ids[:n]]
 
 
 # ------------------------------------------------------------------------------------------------
 # a-13..a-17, a-20: aggregation / group-by execution
 # ------------------------------------------------------------------------------------------------
-FN_DEFAULT = {"count": 0.0, "sum": 0.0, "min": math.inf, "max": -math.inf}
+FN_DEFAULT = {"count": 0.0, "sum": 0.0, "min": math.inf, "max": -math.inf,
+              "countmv": 0.0, "summv": 0.0, "minmv": math.inf, "maxmv": -math.inf}
+MV_FUNCTIONS = ("countmv", "summv", "minmv", "maxmv", "avgmv")
 EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
 
 
@@ -1067,7 +1100,7 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
     holders = []
     for a in q["aggregations"]:
         fn = a["fn"]
-        holders.append([0.0, 0] if fn == "avg" else set() if fn == "distinctcount" else
+        holders.append([0.0, 0] if fn in ("avg", "avgmv") else set() if fn == "distinctcount" else
                        [0] * (1 << HLL_LOG2M) if fn in ("distinctcounthll", "fasthll") else
                        [math.inf, -math.inf] if fn == "minmaxrange" else [] if fn.startswith("percentile") else
                        FN_DEFAULT[fn])
@@ -1078,6 +1111,25 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
                 holders[k] = holders[k] + float(len(blk))  # CountAggregationFunction.aggregate:43-48
                 continue
             col = seg.columns[a["column"]]
+            if fn in MV_FUNCTIONS:  # {Count,Sum,Min,Max,Avg}MVAggregationFunction.aggregate: every value of every doc
+                if col.mv_ids is None:
+                    raise ValueError("%s over a single-value column" % fn)
+                vals = [col.value_as_double(col.mv_ids[int(d)]) for d in blk]
+                flat = np.concatenate(vals) if vals else np.zeros(0)
+                if fn == "countmv":
+                    holders[k] = holders[k] + float(len(flat))
+                elif fn == "summv":
+                    holders[k] = holders[k] + (float(np.cumsum(flat)[-1]) if len(flat) else 0.0)
+                elif fn == "minmv":
+                    holders[k] = min(holders[k], float(flat.min())) if len(flat) else holders[k]
+                elif fn == "maxmv":
+                    holders[k] = max(holders[k], float(flat.max())) if len(flat) else holders[k]
+                else:
+                    holders[k] = [holders[k][0] + (float(np.cumsum(flat)[-1]) if len(flat) else 0.0),
+                                  holders[k][1] + len(flat)]
+                continue
+            if col.mv_ids is not None:
+                raise ValueError("%s over a multi-value column" % fn)
             if fn in ("distinctcount", "distinctcounthll"):  # getSVHashCodeArray: (int) of each value's hashCode()
                 hc = [java_hash_code(col, int(i)) for i in col.dict_ids[blk]]
                 if fn == "distinctcount":
@@ -1116,9 +1168,9 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
                 holders[k].extend(v.tolist())
     results = []
     for k, a in enumerate(q["aggregations"]):
-        if a["fn"] == "count":
+        if a["fn"] in ("count", "countmv"):
             results.append(int(holders[k]))  # MutableLongValue((long) double)
-        elif a["fn"] == "avg":
+        elif a["fn"] in ("avg", "avgmv"):
             results.append((float(holders[k][0]), int(holders[k][1])))
         elif a["fn"] == "distinctcount":
             results.append(set(holders[k]))
@@ -1250,8 +1302,14 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
 # ------------------------------------------------------------------------------------------------
 def combine_two(fn: str, a, b):
     """Legacy combineTwoValues (query/aggregation/function/{Sum,Count,Min,Max,Avg}AggregationFunction.java)."""
-    if fn == "count":
+    if fn in ("count", "countmv", "summv"):
         return a + b
+    if fn == "minmv":
+        return a if a < b else b
+    if fn == "maxmv":
+        return a if a > b else b
+    if fn == "avgmv":
+        return (a[0] + b[0], a[1] + b[1])
     if fn == "sum":
         return a + b
     if fn == "min":

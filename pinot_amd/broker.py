@@ -55,6 +55,11 @@ def java_format_5f(x: float) -> str:
     return "-0.00000" if s == "0.00000" and math.copysign(1.0, x) < 0 else s
 
 
+# {Count,Sum,Min,Max,Avg}MVAggregationFunction combine / reduce like their single-value counterparts (the values of
+# every doc fold into the same intermediates: count, double sum, min, max, AvgPair)
+_MV_BASE = {"countmv": "count", "summv": "sum", "minmv": "min", "maxmv": "max", "avgmv": "avg"}
+
+
 def _combine_two(fn: str, a, b):
     """combineTwoValues of the legacy functions (CountAggregationFunction.java:79-87 long add, SumAggregationFunction
     .java:168-176 double add, MinAggregationFunction.java:112-120, Max..., AvgAggregationFunction.java:116-125 pair add);
@@ -63,6 +68,7 @@ def _combine_two(fn: str, a, b):
         return b
     if b is None:
         return a
+    fn = _MV_BASE.get(fn, fn)
     if fn in EXT_FUNCTIONS:
         return X.combine_two(fn, a, b)
     if fn == "count":
@@ -79,6 +85,7 @@ def _combine_two(fn: str, a, b):
 def _reduce(fn: str, values: Sequence):
     """AggregationFunction.reduce: count -> long sum; sum -> double sum; min / max over the default +/-inf; avg -> sum /
     count, 0.0 when no docs (AvgAggregationFunction.java:128-143)."""
+    fn = _MV_BASE.get(fn, fn)
     if fn in EXT_FUNCTIONS:  # combine the intermediates, then the function's final value
         acc = None
         for v in values:
@@ -114,7 +121,8 @@ def _reduce(fn: str, values: Sequence):
 
 def _format(fn: str, v) -> str:
     """Long / Integer (count, distinctcount) -> toString; doubles -> %1.5f (BrokerReduceService.formatValue)."""
-    return str(int(v)) if fn in ("count", "distinctcount", "distinctcounthll", "fasthll") else java_format_5f(float(v))
+    return str(int(v)) if fn in ("count", "countmv", "distinctcount", "distinctcounthll", "fasthll") \
+        else java_format_5f(float(v))
 
 
 @dataclass

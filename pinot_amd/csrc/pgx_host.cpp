@@ -51,6 +51,8 @@ extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in
                                            int nreg, int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
                                            int nbits, uint64_t* out, int64_t cap, unsigned long long* cursor,
                                            int cstride, unsigned long long* overflow, hipStream_t stream);
+extern "C" hipError_t pgx_launch_mv_leaf_mask(const pgx::MvLeaf* items, int nitems, int max_words, hipStream_t stream);
+extern "C" hipError_t pgx_launch_mv_aggregate(const pgx::MvAgg* items, int nitems, int max_words, hipStream_t stream);
 extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
                                                 int nparts, int64_t cap, uint64_t keymask, int keybits, int64_t vbase,
                                                 const int64_t* vdict, int need_sum, int need_min, int need_max, int pack_shift,
@@ -382,6 +384,11 @@ struct StagedColumn {
   int64_t vbase = 0;       // integer images hold value - vbase
   uint64_t vrange = 0;     // max(value) - vbase
   const void* img_dev = nullptr;  // shared->img
+  // multi-value columns (<col>.mv.fwd): fwd holds the raw value section; doc d owns values [mv_start[d], mv_start[d+1])
+  bool is_mv = false;
+  int64_t total_entries = 0;
+  DevBuf mv_start;
+  int max_mv = 0;
 };
 
 struct pgx_segment {
@@ -616,7 +623,43 @@ void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool
   }
 
   // ---- forward index ----
-  if (c.is_sorted) {
+  if (d.is_multi_value) {
+    // FixedBitMultiValueWriter / FixedBitMultiValueReader (io/*/impl/v1/FixedBitMultiValue*.java): numChunks BE int
+    // chunk offsets, a totalNumValues-bit MSB-first bitset marking every doc's first value, then the values fixed-bit.
+    // docsPerChunk = ceil(2048 / (float)(totalNumValues / numDocs)) with the integer division of the reference.
+    c.is_mv = true;
+    c.is_sorted = false;
+    const int64_t tv = d.total_entries;
+    if (tv < n || n < 1) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": totalNumberOfEntries < docs");
+    c.total_entries = tv;
+    const float avg = float(tv / n);
+    const int64_t dpc = int64_t(std::ceil(2048.0f / avg));
+    const int64_t nchunks = (n + dpc - 1) / dpc;
+    const uint64_t head = uint64_t(nchunks) * 4, bs = uint64_t(tv + 7) / 8, raw = (uint64_t(tv) * c.bits + 7) / 8;
+    if (d.fwd_len < head + bs + raw) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": multi-value index short");
+    std::vector<uint8_t> f(head + bs + raw);
+    if (device_mem) hip_check(hipMemcpy(f.data(), d.fwd, f.size(), hipMemcpyDeviceToHost), "mv fwd D2H");
+    else std::memcpy(f.data(), d.fwd, f.size());
+    std::vector<int32_t> start;
+    start.reserve(size_t(n) + 1);
+    for (int64_t i = 0; i < tv; ++i)
+      if ((f[head + size_t(i >> 3)] >> (7 - (i & 7))) & 1u) start.push_back(int32_t(i));
+    if (int64_t(start.size()) != n || start[0] != 0)
+      fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": multi-value doc bitset does not mark one start per doc");
+    for (int64_t k = 0; k < nchunks; ++k)
+      if (int64_t(be32(&f[size_t(k) * 4])) != start[size_t(k * dpc)])
+        fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": multi-value chunk offset mismatch");
+    start.push_back(int32_t(tv));
+    for (int64_t dd = 0; dd < n; ++dd) c.max_mv = std::max<int>(c.max_mv, start[dd + 1] - start[dd]);
+    c.mv_start = DevBuf(ctx, start.size() * 4);
+    hip_check(hipMemcpy(c.mv_start.p, start.data(), start.size() * 4, hipMemcpyHostToDevice), "mv starts H2D");
+    const uint64_t vneed = padded_fwd_bytes(tv, c.bits);
+    c.fwd_owned = DevBuf(ctx, vneed);
+    hip_check(hipMemset(c.fwd_owned.p, 0, vneed), "memset");
+    hip_check(hipMemcpy(c.fwd_owned.p, f.data() + head + bs, raw, hipMemcpyHostToDevice), "mv values H2D");
+    c.fwd = c.fwd_owned.as<const uint32_t>();
+    seg->device_bytes += vneed + start.size() * 4;
+  } else if (c.is_sorted) {
     // Sorted SV column: card x (start,end) BE int pairs (SortedForwardIndexReader / SortedInvertedIndexReader).
     std::vector<uint8_t> pairs(d.sorted_len);
     if (d.sorted_len < uint64_t(c.card) * 8) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": sorted index short");
@@ -1063,6 +1106,17 @@ struct ExecPlan {
   // bitmap sub-trees evaluated by pgx_roaring_program into one mask each (JIT leaf L + k for program k)
   bool rprog_on = false;
   bool rchunk = false;   // ... evaluated per chunk inside the query kernels (LEAF_RCHUNK), not by a separate pass
+  // multi-value scan leaves (pgx_mv_leaf_mask writes one doc mask per (segment, leaf), read as LEAF_DOCMASK)
+  struct MvItem { int seg, leaf; };
+  std::vector<MvItem> mv_items;
+  std::vector<int> mv_neg;                 // [leaf] NEQ / NOT_IN
+  std::vector<std::vector<int>> mv_index;  // [seg][leaf] -> index into mv_items or -1
+  DevBuf mv_masks, mv_descs;
+  int mv_max_words = 0;
+  // selection masks for the multi-value functions (one bit per scanned row, per segment)
+  bool want_selmask = false;
+  DevBuf sel_buf;
+  std::vector<int64_t> sel_off;       // [seg] word offset in sel_buf
   struct DmProg {
     std::vector<int> op, arg;  // RP_*; RP_LEAF arg = query leaf index
   };
@@ -1600,6 +1654,10 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     }
     const StagedColumn& c = segs[0]->col(q.agg_col[a]);
     if (c.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + c.name);
+    if (fn >= PGX_COUNTMV) fail(PGX_ERR_INTERNAL, "multi-value function in the single-value plan");
+    for (int s = 0; s < n; ++s)
+      if (segs[s]->col(q.agg_col[a]).is_mv)
+        fail(PGX_ERR_UNSUPPORTED, "single-value aggregation on multi-value column " + c.name);
     const bool fp = c.data_type == PGX_FLOAT || c.data_type == PGX_DOUBLE;
     K.agg_col[a] = int8_t(qslot(P, q.agg_col[a]));
     K.agg_fp[a] = fp;
@@ -1619,6 +1677,9 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     int total_bits = 0;
     P.gdicts.clear();
     for (int g = 0; g < K.num_gcols; ++g) {
+      for (int s = 0; s < n; ++s)
+        if (segs[s]->col(q.group_cols[g]).is_mv)
+          fail(PGX_ERR_UNSUPPORTED, "GROUP BY on multi-value column " + q.group_cols[g]);
       K.gcol[g] = int8_t(qslot(P, q.group_cols[g]));
       P.gdicts.push_back(dom ? domain_dict(*dom, g, n) : build_global_dict(segs, n, q.group_cols[g]));
       const int64_t gc = P.gdicts.back().card;
@@ -1812,6 +1873,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     std::vector<int32_t> blob;
     std::vector<ExecPlan::Fix> fixes;
     std::vector<ExecPlan::RoarItem> roar;
+    std::vector<ExecPlan::MvItem> mv;
     int64_t total_raw = 0, host_entries = 0;
     uint64_t mask_words = 0;
     int maxchunks = 0;
@@ -1918,12 +1980,26 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           if (!P.rprog_on) o.mask_words += uint64_t(it.nchunks) * 2048;
           o.maxchunks = std::max(o.maxchunks, it.nchunks);
           o.roar.push_back(it);
+        } else if (col.is_mv && L.mode != LEAF_NONE) {
+          // MVScanDocIdIterator: the query kernel reads the doc mask pgx_mv_leaf_mask derives from the values
+          if (!P.use_docmask) fail(PGX_ERR_UNSUPPORTED, "multi-value filter needs the query kernels");
+          o.mv.push_back({s, int(l)});
         }
       }
     }
   };
   if (nchunk > 1) ctx->parallel_for(nchunk, plan_chunk);
   else if (nchunk == 1) plan_chunk(0);
+  P.mv_items.clear();
+  P.mv_index.assign(n, std::vector<int>(q.leaf_col.size(), -1));
+  P.mv_neg.assign(q.leaf_col.size(), 0);
+  for (size_t l = 0; l < q.leaf_col.size(); ++l)
+    P.mv_neg[l] = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
+  for (ChunkOut& o : chunks)
+    for (const auto& it : o.mv) {
+      P.mv_index[it.seg][it.leaf] = int(P.mv_items.size());
+      P.mv_items.push_back(it);
+    }
   int64_t tiles = 0;
   P.total_raw = 0;
   for (int s = 0; s < n; ++s) {
@@ -2199,6 +2275,41 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
     P.fsm_pstate = DevBuf(ctx, pe * 2);
     (void)L;
   }
+  if (!P.mv_items.empty()) {  // multi-value scan leaves: descriptors + one doc mask per (segment, leaf)
+    std::vector<MvLeaf> items(P.mv_items.size());
+    std::vector<int64_t> off(P.mv_items.size());
+    int64_t words = 0;
+    P.mv_max_words = 0;
+    for (size_t i = 0; i < items.size(); ++i) {
+      const int w = (P.ksegs[P.mv_items[i].seg].num_docs + 31) / 32 + 1;
+      off[i] = words;
+      words += w;
+      P.mv_max_words = std::max(P.mv_max_words, w);
+    }
+    P.mv_masks = DevBuf(ctx, size_t(std::max<int64_t>(words, 1)) * 4);
+    for (size_t i = 0; i < items.size(); ++i) {
+      const auto& it = P.mv_items[i];
+      const KSeg& S = P.ksegs[it.seg];
+      const KLeaf& L = S.leaf[it.leaf];
+      const StagedColumn& col = *P.segcols[it.seg][P.kq.leaf_col[it.leaf]];
+      MvLeaf& m = items[i];
+      m.vals = col.fwd;
+      m.start = col.mv_start.as<const int32_t>();
+      m.bitset = L.mode == LEAF_SCAN_BITSET ? L.bitset : nullptr;
+      m.mask = P.mv_masks.as<uint32_t>() + off[i];
+      m.bits = col.bits;
+      m.num_docs = S.num_docs;
+      m.lo = uint32_t(L.lo);
+      m.span = uint32_t(L.hi) - uint32_t(L.lo);
+      m.neg = 0;
+      P.ksegs[it.seg].leaf[it.leaf].bitset = m.mask;  // the query kernel's LEAF_DOCMASK word source
+    }
+    P.mv_descs = DevBuf(ctx, items.size() * sizeof(MvLeaf));
+    for (size_t i = 0; i < items.size(); ++i) items[i].neg = P.mv_neg.empty() ? 0 : P.mv_neg[P.mv_items[i].leaf];
+    hip_check(hipMemcpyAsync(P.mv_descs.p, items.data(), items.size() * sizeof(MvLeaf), hipMemcpyHostToDevice, st),
+              "multi-value leaf descriptors H2D");
+    hip_check(hipStreamSynchronize(st), "sync");  // the host vector goes out of scope
+  }
   if (n) std::memcpy(B.host.bytes() + B.off_ksegs, P.ksegs.data(), n * sizeof(KSeg));
   P.kq.segs = reinterpret_cast<const KSeg*>(B.dev() + B.off_ksegs);
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.dev() + B.off_outs);
@@ -2329,7 +2440,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     const KSeg& S = P.ksegs[s];
     sig.clear();
     for (int l = 0; l < nleaves; ++l)
-      sig.push_back(P.roar_index[s][l] >= 0 ? (P.roar[P.roar_index[s][l]].neg ? 101 : 100) : S.leaf[l].mode);
+      sig.push_back(P.roar_index[s][l] >= 0 ? (P.roar[P.roar_index[s][l]].neg ? 101 : 100)
+                                            : (P.mv_index[s][l] >= 0 ? 102 : S.leaf[l].mode));
     if (P.star[s].on) {
       sig.push_back(-7);
       for (size_t i = 0; i < P.star[s].op.size(); ++i) {
@@ -2363,7 +2475,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     std::vector<bool> dec = decode;
     for (int l = 0; l < nleaves; ++l)
       if ((S0.leaf[l].mode == LEAF_SCAN_INTERVAL || S0.leaf[l].mode == LEAF_SCAN_BITSET) &&
-          P.roar_index[members[0]][l] < 0)
+          P.roar_index[members[0]][l] < 0 && P.mv_index[members[0]][l] < 0)
         dec[K.leaf_col[l]] = true;
     int R = 8;
     for (int c = 0; c < nc; ++c) {
@@ -2432,6 +2544,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       J.leaf_col.push_back(K.leaf_col[l]);
       const int ri = P.roar_index[members[0]][l];
       if (P.rprog_on && P.leaf_phys[l] == PH_BITMAP) J.leaf_mode.push_back(LEAF_NONE);  // read via its program
+      else if (P.mv_index[members[0]][l] >= 0) J.leaf_mode.push_back(LEAF_DOCMASK);  // pgx_mv_leaf_mask's doc mask
       else J.leaf_mode.push_back(ri >= 0 ? (P.roar[ri].neg ? LEAF_DOCMASK_NOT : LEAF_DOCMASK) : S0.leaf[l].mode);
     }
     if (P.rprog_on)
@@ -2475,6 +2588,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     J.leafmask = P.fsm_on && P.lmask_off[members[0]] >= 0;
     J.compact = P.rchunk && !P.use_part;  // selective bitmap filters: aggregate the selected rows packed
     if (const char* e = std::getenv("PGX_COMPACT")) J.compact = e[0] == '1' && !P.use_part;
+    J.selmask = P.want_selmask;
 
     ExecPlan::JitGroup G;
     G.T = J.T;
@@ -2493,6 +2607,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       js.rec_base = P.rec_base[s];
       js.lmask = S.lmask;
       js.lmask_words = S.lmask_words;
+      js.selmask = P.want_selmask ? P.sel_buf.as<unsigned int>() + P.sel_off[s] : nullptr;
       if (P.star[s].on) {
         // visit only the tiles that intersect a star-tree range: every selected doc lies in one
         auto& tl = P.star_tiles[s];
@@ -2573,6 +2688,11 @@ void launch_fsm(ExecPlan& P, hipStream_t st) {
 }
 
 void launch_scan(ExecPlan& P, hipStream_t st) {
+  if (!P.mv_items.empty()) {
+    if (P.jit.empty() || !P.jit[0].fn) fail(PGX_ERR_UNSUPPORTED, "multi-value filter needs the query kernels");
+    hip_check(pgx_launch_mv_leaf_mask(P.mv_descs.as<MvLeaf>(), int(P.mv_items.size()), P.mv_max_words, st),
+              "multi-value leaf masks");
+  }
   if (!P.jit.empty()) {
     if (P.rdesc_dev && !P.roar_early) launch_bitmaps(P, st);
     P.roar_early = false;  // relaunches (hash-table retries, timed iterations) expand again
@@ -3154,6 +3274,126 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   return true;
 }
 
+// Multi-value functions (Count/Sum/Min/Max/AvgMVAggregationFunction, operator/aggregation/function/*MV*.java),
+// aggregation-only: the single-value part of the query (its filter and SV functions, or COUNT(*) alone) runs through
+// the query kernels, which also write every scanned row's selection bit; pgx_mv_aggregate then folds every value of
+// every selected doc of each MV column (count, int64 / f64 sum, min / max over the sorted dictionary's ids).
+void run_mv(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
+            uint32_t xflags, pgx_result* R, hipStream_t st) {
+  if (!q.group_cols.empty()) fail(PGX_ERR_UNSUPPORTED, "multi-value functions with GROUP BY");
+  if (!jit_enabled()) fail(PGX_ERR_UNSUPPORTED, "multi-value functions need the query kernels");
+  pgx_query qs = q;
+  qs.flags |= PGX_Q_NO_STAR_TREE;  // every raw row gets its selection bit
+  qs.agg_fn.clear();
+  qs.agg_col.clear();
+  std::vector<int> sv_pos(q.agg_fn.size(), -1), mv_pos(q.agg_fn.size(), -1);
+  std::vector<std::string> mv_cols;
+  for (size_t a = 0; a < q.agg_fn.size(); ++a) {
+    if (q.agg_fn[a] >= PGX_COUNTMV) {
+      const std::string& c = q.agg_col[a];
+      for (int s = 0; s < n; ++s) {
+        const StagedColumn& col = segs[s]->col(c);
+        if (!col.is_mv) fail(PGX_ERR_UNSUPPORTED, "multi-value function on single-value column " + c);
+        if (col.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + c);
+      }
+      auto it = std::find(mv_cols.begin(), mv_cols.end(), c);
+      mv_pos[a] = int(it - mv_cols.begin());
+      if (it == mv_cols.end()) mv_cols.push_back(c);
+    } else {
+      sv_pos[a] = int(qs.agg_fn.size());
+      qs.agg_fn.push_back(q.agg_fn[a]);
+      qs.agg_col.push_back(q.agg_col[a]);
+    }
+  }
+  if (qs.agg_fn.empty()) {
+    qs.agg_fn.push_back(PGX_COUNT);
+    qs.agg_col.push_back("");
+  }
+  ExecPlan P;
+  P.want_selmask = true;
+  plan_query(ctx, qs, segs, n, bindings, xflags, P);
+  P.sel_off.assign(n, 0);
+  int64_t words = 0;
+  int max_words = 0;
+  for (int s = 0; s < n; ++s) {
+    P.sel_off[s] = words;
+    const int w = (P.ksegs[s].num_docs + 31) / 32 + 1;
+    words += w;
+    max_words = std::max(max_words, w);
+  }
+  P.sel_buf = DevBuf(ctx, size_t(std::max<int64_t>(words, 1)) * 4);
+  hip_check(hipMemsetAsync(P.sel_buf.p, 0, size_t(std::max<int64_t>(words, 1)) * 4, st), "selection masks");
+  ExecBuffers B;
+  upload_plan(ctx, P, B, st);
+  plan_jit(ctx, qs, segs, n, P, B);
+  if (P.jit.empty()) fail(PGX_ERR_UNSUPPORTED, "multi-value functions need the query kernels");
+  alloc_outputs(ctx, P, B, nullptr, 0);
+  reset_outputs(P, B, st);
+  launch_scan(P, st);
+  // one item per (segment, MV column); outputs [count, sum, ordered min, ordered max] per column
+  std::vector<unsigned long long> init(mv_cols.size() * 4, 0ull);
+  for (size_t k = 0; k < mv_cols.size(); ++k) init[4 * k + 2] = ~0ull;
+  DevBuf outs(ctx, init.size() * 8);
+  hip_check(hipMemcpy(outs.p, init.data(), init.size() * 8, hipMemcpyHostToDevice), "MV outputs init");
+  std::vector<MvAgg> items;
+  std::vector<int> fp(mv_cols.size(), 0);
+  for (size_t k = 0; k < mv_cols.size(); ++k)
+    for (int s = 0; s < n; ++s) {
+      const StagedColumn& col = segs[s]->col(mv_cols[k]);
+      fp[k] = col.data_type == PGX_FLOAT || col.data_type == PGX_DOUBLE;
+      MvAgg m{};
+      m.vals = col.fwd;
+      m.start = col.mv_start.as<const int32_t>();
+      m.sel = P.sel_buf.as<uint32_t>() + P.sel_off[s];
+      m.dict = col.dict_dev;
+      m.out = outs.as<unsigned long long>() + 4 * k;
+      m.bits = col.bits;
+      m.num_docs = P.ksegs[s].num_docs;
+      m.fp = fp[k];
+      items.push_back(m);
+    }
+  DevBuf idev(ctx, std::max<size_t>(1, items.size()) * sizeof(MvAgg));
+  hip_check(hipMemcpy(idev.p, items.data(), items.size() * sizeof(MvAgg), hipMemcpyHostToDevice), "MV items H2D");
+  hip_check(pgx_launch_mv_aggregate(idev.as<MvAgg>(), int(items.size()), max_words, st), "multi-value aggregation");
+  pgx_result Rs;
+  finish_result(ctx, qs, P, B, segs, n, st, &Rs, nullptr);
+  std::vector<unsigned long long> res(init.size());
+  hip_check(hipMemcpy(res.data(), outs.p, res.size() * 8, hipMemcpyDeviceToHost), "MV outputs D2H");
+  // assemble in the request's order; numEntriesScannedPostFilter counts the MV columns among the projected ones
+  int extra = 0;
+  for (const auto& c : mv_cols)
+    if (std::find(qs.agg_col.begin(), qs.agg_col.end(), c) == qs.agg_col.end()) ++extra;
+  for (int i = 0; i < 4; ++i) R->stats[i] = Rs.stats[i];
+  R->stats[2] = Rs.stats[0] * (P.n_proj + extra);
+  R->num_aggs = int(q.agg_fn.size());
+  R->agg_fn = q.agg_fn;
+  R->top_n = q.top_n;
+  R->group_by = false;
+  R->mode = Rs.mode;
+  R->agg_value.assign(q.agg_fn.size(), 0.0);
+  R->agg_count.assign(q.agg_fn.size(), 0);
+  for (size_t a = 0; a < q.agg_fn.size(); ++a) {
+    if (sv_pos[a] >= 0) {
+      R->agg_value[a] = Rs.agg_value[sv_pos[a]];
+      R->agg_count[a] = Rs.agg_count[sv_pos[a]];
+      continue;
+    }
+    const int k = mv_pos[a];
+    const unsigned long long* o = &res[4 * size_t(k)];
+    const int64_t cnt = int64_t(o[0]);
+    double sum;
+    if (fp[k]) std::memcpy(&sum, &o[1], 8);
+    else sum = double(int64_t(o[1]));
+    R->agg_count[a] = cnt;
+    switch (q.agg_fn[a]) {
+      case PGX_COUNTMV: R->agg_value[a] = double(cnt); break;
+      case PGX_MINMV: R->agg_value[a] = decode_plane(P_MIN_ORD, fp[k], o[2], PGX_MIN); break;
+      case PGX_MAXMV: R->agg_value[a] = decode_plane(P_MAX_ORD, fp[k], o[3], PGX_MAX); break;
+      default: R->agg_value[a] = sum; break;  // SUMMV; AVGMV: (sum, value count) like AvgPair
+    }
+  }
+}
+
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                const pgx_exec_opts* opts, pgx_result* R, const Domain* dom = nullptr) {
   HostProf hp;
@@ -3161,6 +3401,12 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   struct Unmark { ~Unmark() { g_prof_mark = nullptr; } } unmark;
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
   const uint32_t xflags = opts ? opts->flags : 0;
+  for (int fn : q.agg_fn)
+    if (fn >= PGX_COUNTMV) {
+      if (dom || (opts && opts->dense_out)) fail(PGX_ERR_UNSUPPORTED, "multi-value functions across devices");
+      run_mv(ctx, q, segs, n, bindings, xflags, R, st);
+      return;
+    }
   if (!dom && run_batched(ctx, q, segs, n, bindings, opts, R, st, xflags, hp)) return;
   ExecPlan P;
   plan_query(ctx, q, segs, n, bindings, xflags, P, dom);
@@ -3574,7 +3820,7 @@ pgx_status pgx_query_compile(pgx_ctx* ctx, const pgx_query_desc* d, pgx_query** 
     auto q = std::make_unique<pgx_query>();
     for (int a = 0; a < d->num_aggs; ++a) {
       const int fn = d->aggs[a].fn;
-      if (fn < PGX_COUNT || fn > PGX_AVG) fail(PGX_ERR_UNSUPPORTED, "aggregation function not on the GPU path");
+      if (fn < PGX_COUNT || fn > PGX_AVGMV) fail(PGX_ERR_UNSUPPORTED, "aggregation function not on the GPU path");
       q->agg_fn.push_back(fn);
       const char* c = d->aggs[a].column;
       std::string col = (c && std::strcmp(c, "*") != 0) ? c : "";

@@ -42,6 +42,35 @@ using RProg = ::JRProg;
 
 enum ProgOp : int8_t { OP_LEAF = 0, OP_AND = 1, OP_OR = 2, OP_STAT = 3, OP_TRUE = 4 };
 
+// Multi-value columns (pgx_kernels.hip).  Values are the .mv.fwd raw section (value i at bits [i*B, i*B+B), MSB-first
+// big-endian, like a single-value forward index over value positions); doc d owns values [start[d], start[d+1]).
+// MV scan leaf (MVScanDocIdIterator + the evaluators' apply(int[]), operator/filter/predicate/*PredicateEvaluator
+// .java): a doc matches when ANY value is in the matching set (EQ / IN / RANGE), or, for NEQ / NOT_IN, when NO value is
+// outside it; one output bit per doc.
+struct MvLeaf {
+  const uint32_t* vals;
+  const int32_t* start;        // num_docs + 1
+  const uint32_t* bitset;      // matching dictIds (null: lo <= id <= lo + span)
+  uint32_t* mask;              // out: bit (d & 31) of word d >> 5
+  int32_t bits;
+  int32_t num_docs;
+  uint32_t lo, span;
+  int32_t neg;
+  int32_t pad;
+};
+// MV aggregation (Count/Sum/Min/Max/AvgMVAggregationFunction): every value of every selected doc of one segment.
+struct MvAgg {
+  const uint32_t* vals;
+  const int32_t* start;
+  const uint32_t* sel;         // selected docs: bit (d & 31) of word d >> 5 (written by the query kernel)
+  const void* dict;            // int64 or double per dictId
+  unsigned long long* out;     // [count, sum (int64 or f64 bits), ordered min, ordered max]
+  int32_t bits;
+  int32_t num_docs;
+  int32_t fp;
+  int32_t pad;
+};
+
 // Statistics automaton over one segment's leaf masks (pgx_kernels.hip pgx_fsm_chunks / pgx_fsm_compose).
 struct FsmSeg {
   const uint32_t* lmask;       // leaf l, row r: bit (r & 31) of word [l * words + (r >> 5)]
@@ -174,6 +203,7 @@ struct JitShape {
   int part_bits = 0;
   bool emit_dictid = false;
   bool compact = false;   // pack each sub-step's selected rows into consecutive lanes before aggregating (selective)
+  bool selmask = false;   // write every row's selection bit (multi-value aggregations read it)
 };
 
 // ----- numEntriesScannedInFilter automaton (pgx_stats.cpp builds it, pgx_kernels.hip pgx_fsm_* runs it) -----

@@ -476,6 +476,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       }
     if (emit) e.ln("u64 recs[PR];");
     if (split) e.ln("u32 msk = 0u;");
+    if (s.selmask) e.ln("u32 smk = 0u;");
     if (s.leafmask)
       for (int l = 0; l < nleaves; ++l) e.ln("u32 lw", l, " = 0u;");
     e.ln("#pragma unroll");
@@ -530,6 +531,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     }
     e.ln("const bool m = ", st.empty() ? std::string("vj") : st.back(), ";");
     e.ln("wcnt += __popcll(__ballot(m));");
+    if (s.selmask) e.ln("smk |= (u32)m << j;");
     if (compact) {
       const int ncw = int(std::max<size_t>(1, ccols.size()));
       e.ln("msk |= (u32)m << j;");
@@ -684,6 +686,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
             s.cols[s.agg_col[a]].acc32)
           e.ln("acc", a, " += p", a, ";");
       }
+    if (s.selmask) {  // the lane's PR selection bits (r0 is a multiple of PR, PR divides 32)
+      const char* ty = s.R == 8 ? "unsigned char" : (s.R == 16 ? "unsigned short" : "unsigned int");
+      e.ln("if (FULL || r0 < nd) ((PGX_G ", ty, "*)S->selmask)[r0 / PR] = (", ty, ")smk;");
+    }
     if (s.leafmask) {
       // the lane's PR rows are PR consecutive bits of the leaf's mask (r0 is a multiple of PR, PR divides 32)
       const char* ty = s.R == 8 ? "unsigned char" : (s.R == 16 ? "unsigned short" : "unsigned int");
@@ -884,6 +890,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.part_bits);
   k.push_back(s.emit_dictid);
   k.push_back(s.compact);
+  k.push_back(s.selmask);
   return k;
 }
 
@@ -1161,6 +1168,9 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     shapes.push_back(s);
     s.cols[1].img = IMG_U32;  // ... with a value image
     s.cols[1].img_words = 1024;
+    shapes.push_back(s);
+    s.compact = false;  // selection bits written for the multi-value aggregation pass
+    s.selmask = true;
     shapes.push_back(s);
   }
   for (int R : {8, 16, 32}) {  // statistics automaton input: every leaf's predicate bits written per lane

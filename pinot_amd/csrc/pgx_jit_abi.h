@@ -51,6 +51,7 @@ struct JSeg {
                                                  // selected doc, e.g. outside every star-tree node range); 0 = all
   unsigned int* lmask;                           // statistics automaton: leaf l's predicate bit of row r goes to bit
   long long lmask_words;                         // (r & 31) of word [l * lmask_words + (r >> 5)]
+  unsigned int* selmask;                         // selection bit of row r: bit (r & 31) of word r >> 5 (MV functions)
 };
 
 struct JArgs {

@@ -997,6 +997,101 @@ __global__ void __launch_bounds__(kSegRThreads) pgx_roaring_program_seg(const RP
 }
 
 // ---------------------------------------------------------------------------------------------
+// Multi-value columns.  One thread owns 32 consecutive docs (one mask word); their values are consecutive in the raw
+// section, so neighbouring threads read neighbouring bytes.  A value is cut out of the big-endian bit stream with one
+// 64-bit window (two byte-swapped dwords; the staged buffer is padded past the last value).
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mv_value(const uint32_t* __restrict__ vals, int64_t i, int bits) {
+  const int64_t o = i * bits;
+  const PGX_GLOBAL uint32_t* w = (const PGX_GLOBAL uint32_t*)(vals) + (o >> 5);
+  const uint64_t x = (static_cast<uint64_t>(__builtin_bswap32(w[0])) << 32) | __builtin_bswap32(w[1]);
+  return static_cast<uint32_t>(x >> (64 - (o & 31) - bits)) & (bits == 32 ? 0xFFFFFFFFu : ((1u << bits) - 1u));
+}
+
+__global__ void __launch_bounds__(256) pgx_mv_leaf_mask(const MvLeaf* __restrict__ items, int nitems, int max_words) {
+  const int it = static_cast<int>(blockIdx.y);
+  if (it >= nitems) return;
+  const MvLeaf& L = items[it];
+  const int w = static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x);
+  const int words = (L.num_docs + 31) >> 5;
+  if (w >= words) return;
+  (void)max_words;
+  uint32_t out = 0u;
+  const int d0 = w * 32;
+  const int dn = min(32, L.num_docs - d0);
+  for (int k = 0; k < dn; ++k) {
+    const int s = L.start[d0 + k], e = L.start[d0 + k + 1];
+    bool hit = false;  // any value in the matching set (EQ / IN / RANGE) or outside it (NEQ / NOT_IN)
+    for (int i = s; i < e && !hit; ++i) {
+      const uint32_t v = mv_value(L.vals, i, L.bits);
+      const bool in = L.bitset ? ((L.bitset[v >> 5] >> (v & 31u)) & 1u) : (v - L.lo <= L.span);
+      hit = in != (L.neg != 0);
+    }
+    if (hit != (L.neg != 0)) out |= 1u << k;
+  }
+  L.mask[w] = out;
+}
+
+__device__ __forceinline__ uint64_t mv_ord_i64(int64_t x) { return static_cast<uint64_t>(x) ^ 0x8000000000000000ull; }
+__device__ __forceinline__ uint64_t mv_ord_f64(double d) {
+  const uint64_t b = static_cast<uint64_t>(__double_as_longlong(d));
+  return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+}
+
+__global__ void __launch_bounds__(256) pgx_mv_aggregate(const MvAgg* __restrict__ items, int nitems) {
+  const int it = static_cast<int>(blockIdx.y);
+  if (it >= nitems) return;
+  const MvAgg& A = items[it];
+  const int w = static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x);
+  const int words = (A.num_docs + 31) >> 5;
+  uint64_t cnt = 0;
+  int64_t isum = 0;
+  double dsum = 0.0;
+  uint32_t mn = 0xFFFFFFFFu, mx = 0u;  // dictIds: numeric dictionaries are sorted (SegmentDictionaryCreator)
+  if (w < words) {
+    uint32_t sel = A.sel[w];
+    const int d0 = w * 32;
+    if (d0 + 32 > A.num_docs) sel &= (1u << (A.num_docs - d0)) - 1u;
+    while (sel) {
+      const int k = __builtin_ctz(sel);
+      sel &= sel - 1u;
+      const int s = A.start[d0 + k], e = A.start[d0 + k + 1];
+      for (int i = s; i < e; ++i) {
+        const uint32_t v = mv_value(A.vals, i, A.bits);
+        ++cnt;
+        if (A.fp) dsum += ((const PGX_GLOBAL double*)A.dict)[v];
+        else isum += ((const PGX_GLOBAL int64_t*)A.dict)[v];
+        mn = min(mn, v);
+        mx = max(mx, v);
+      }
+    }
+  }
+  uint64_t omin = ~0ull, omax = 0ull;
+  if (cnt) {
+    omin = A.fp ? mv_ord_f64(((const PGX_GLOBAL double*)A.dict)[mn])
+                : mv_ord_i64(((const PGX_GLOBAL int64_t*)A.dict)[mn]);
+    omax = A.fp ? mv_ord_f64(((const PGX_GLOBAL double*)A.dict)[mx])
+                : mv_ord_i64(((const PGX_GLOBAL int64_t*)A.dict)[mx]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    cnt += __shfl_xor(cnt, off);
+    isum += __shfl_xor(isum, off);
+    dsum += __shfl_xor(dsum, off);
+    const uint64_t a = __shfl_xor(omin, off), b = __shfl_xor(omax, off);
+    omin = a < omin ? a : omin;
+    omax = b > omax ? b : omax;
+  }
+  if ((threadIdx.x & 63) == 0 && cnt) {
+    atomicAdd(A.out, static_cast<unsigned long long>(cnt));
+    if (A.fp) atomicAdd(reinterpret_cast<double*>(A.out + 1), dsum);
+    else atomicAdd(A.out + 1, static_cast<unsigned long long>(isum));
+    atomicMin(A.out + 2, static_cast<unsigned long long>(omin));
+    atomicMax(A.out + 3, static_cast<unsigned long long>(omax));
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // High-cardinality group-by (LONG_MAP semantics, DefaultGroupKeyGenerator.java:239-246 / :429-441): the reference
 // probes a Long2IntOpenHashMap per doc; at 10^7 groups a device-wide hash table turns every row into random HBM atomics.
 // Instead the generated scan kernel emits one packed record per selected row (key | value << keybits), two radix
@@ -1110,7 +1205,7 @@ constexpr int kAggSlots = kAggBuckets * kAggWays;
 constexpr int kAggThreads = 1024;
 constexpr int kAggPer = 8;
 
-template <bool PACK, bool MN, bool MX>
+template <bool PACK, bool MN, bool MX, bool IDV>
 __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t* __restrict__ in,
                                                                   const unsigned long long* __restrict__ in_cnt,
                                                                   int cstride, int64_t cap, uint64_t keymask,
@@ -1153,7 +1248,7 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
 #pragma unroll
     for (int k = 0; k < kAggPer; ++k) {
       const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);
-      sv[k] = vd ? (rec[k] != kNoRecord ? static_cast<unsigned int>(vd[v] - vbase) : 0u) : v;
+      sv[k] = IDV ? (rec[k] != kNoRecord ? static_cast<unsigned int>(vd[v] - vbase) : 0u) : v;
     }
 #pragma unroll
     for (int k = 0; k < kAggPer; ++k) {
@@ -1209,8 +1304,8 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
     oplane[o] = c;  // plane 0: doc count
     // planes 1..3: sum (int64 incl. vbase * count), min, max (ordered encodings of the int64 value)
     oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(sm) + static_cast<int64_t>(c) * vbase);
-    const int64_t vlo = vd ? (MN ? vd[lo] : 0) : vbase + static_cast<int64_t>(lo);  // min / max of dictIds -> values
-    const int64_t vhi = vd ? (MX ? vd[hi] : 0) : vbase + static_cast<int64_t>(hi);
+    const int64_t vlo = IDV ? (MN ? vd[lo] : 0) : vbase + static_cast<int64_t>(lo);  // min / max of dictIds -> values
+    const int64_t vhi = IDV ? (MX ? vd[hi] : 0) : vbase + static_cast<int64_t>(hi);
     oplane[2 * ocap + o] = static_cast<unsigned long long>(vlo) ^ 0x8000000000000000ull;
     oplane[3 * ocap + o] = static_cast<unsigned long long>(vhi) ^ 0x8000000000000000ull;
     ++o;
@@ -1446,9 +1541,14 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
   const int sel = (pack_shift ? 4 : 0) | (need_min ? 2 : 0) | (need_max ? 1 : 0);
 #define PGX_AGG_CASE(K, A, B, C)                                                                                   \
   case K:                                                                                                           \
-    hipLaunchKernelGGL((pgx::pgx_part_aggregate<A, B, C>), dim3(nparts), dim3(pgx::kAggThreads), 0, stream, in,     \
-                       in_cnt, cstride, cap, keymask, keybits, vbase, vdict, pack_shift, okey, oplane, ocap, ocount, \
-                       overflow);                                                                                   \
+    if (vdict)                                                                                                      \
+      hipLaunchKernelGGL((pgx::pgx_part_aggregate<A, B, C, true>), dim3(nparts), dim3(pgx::kAggThreads), 0, stream, \
+                         in, in_cnt, cstride, cap, keymask, keybits, vbase, vdict, pack_shift, okey, oplane, ocap,  \
+                         ocount, overflow);                                                                         \
+    else                                                                                                            \
+      hipLaunchKernelGGL((pgx::pgx_part_aggregate<A, B, C, false>), dim3(nparts), dim3(pgx::kAggThreads), 0,       \
+                         stream, in, in_cnt, cstride, cap, keymask, keybits, vbase, vdict, pack_shift, okey, oplane,\
+                         ocap, ocount, overflow);                                                                   \
     break;
   switch (sel) {
     PGX_AGG_CASE(0, false, false, false)
@@ -1495,5 +1595,21 @@ extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const 
   }
   hipLaunchKernelGGL(pgx::pgx_roaring_program, dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, progs, descs,
                      nprogs, maxchunks);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_mv_leaf_mask(const pgx::MvLeaf* items, int nitems, int max_words, hipStream_t stream) {
+  if (nitems <= 0 || max_words <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pgx::pgx_mv_leaf_mask, dim3(static_cast<unsigned>((max_words + 255) / 256),
+                                                   static_cast<unsigned>(nitems)),
+                     dim3(256), 0, stream, items, nitems, max_words);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_mv_aggregate(const pgx::MvAgg* items, int nitems, int max_words, hipStream_t stream) {
+  if (nitems <= 0 || max_words <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pgx::pgx_mv_aggregate, dim3(static_cast<unsigned>((max_words + 255) / 256),
+                                                   static_cast<unsigned>(nitems)),
+                     dim3(256), 0, stream, items, nitems);
   return hipGetLastError();
 }

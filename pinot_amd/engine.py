@@ -26,7 +26,8 @@ from . import native as N
 from .segment import Column, SegmentData
 
 _DT = {"INT": N.PGX_INT, "LONG": N.PGX_LONG, "FLOAT": N.PGX_FLOAT, "DOUBLE": N.PGX_DOUBLE, "STRING": N.PGX_STRING}
-_FN = {"count": N.PGX_COUNT, "sum": N.PGX_SUM, "min": N.PGX_MIN, "max": N.PGX_MAX, "avg": N.PGX_AVG}
+_FN = {"count": N.PGX_COUNT, "sum": N.PGX_SUM, "min": N.PGX_MIN, "max": N.PGX_MAX, "avg": N.PGX_AVG,
+       "countmv": N.PGX_COUNTMV, "summv": N.PGX_SUMMV, "minmv": N.PGX_MINMV, "maxmv": N.PGX_MAXMV, "avgmv": N.PGX_AVGMV}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -150,6 +151,8 @@ class IndexSegment:
             d.is_sorted = int(c.is_sorted)
             d.dict_width = c.dict_width
             d.pad_char = ord(c.pad_char) if c.data_type == "STRING" else 0
+            d.is_multi_value = int(c.is_mv)
+            d.total_entries = c.total_entries
             for attr, data in (("fwd", c.fwd_bytes), ("sorted_pairs", c.sorted_bytes), ("dict", c.dict_bytes),
                                ("inv", c.inv_bytes)):
                 if data is None:
@@ -550,10 +553,10 @@ def decode_result(q: _Query, r, segments: Sequence[IndexSegment], trim: bool = F
         for i, fn in enumerate(q.fns):
             v, c = C.c_double(), C.c_int64()
             N.check(L.pgx_result_agg(r, i, C.byref(v), C.byref(c)))
-            if fn == "count":
+            if fn in ("count", "countmv"):
                 out.append(int(c.value))  # MutableLongValue
-            elif fn == "avg":
-                out.append((v.value, int(c.value)))  # AvgPair(sum, count)
+            elif fn in ("avg", "avgmv"):
+                out.append((v.value, int(c.value)))  # AvgPair(sum, count): count = values for AVGMV
             else:
                 out.append(v.value)
         blk.aggregation_result = out

@@ -17,7 +17,7 @@ class PgxError(RuntimeError):
 
 
 PGX_INT, PGX_LONG, PGX_FLOAT, PGX_DOUBLE, PGX_STRING = range(5)
-PGX_COUNT, PGX_SUM, PGX_MIN, PGX_MAX, PGX_AVG = range(5)
+PGX_COUNT, PGX_SUM, PGX_MIN, PGX_MAX, PGX_AVG, PGX_COUNTMV, PGX_SUMMV, PGX_MINMV, PGX_MAXMV, PGX_AVGMV = range(10)
 PGX_PRED = {"EQ": 0, "NEQ": 1, "IN": 2, "NOT_IN": 3, "RANGE": 4}
 PGX_F_LEAF, PGX_F_AND, PGX_F_OR = 0, 1, 2
 PGX_MEM_HOST, PGX_MEM_DEVICE = 0, 1
@@ -38,7 +38,7 @@ class ColumnDesc(C.Structure):
                 ("bits_per_element", C.c_int32), ("is_sorted", C.c_int32), ("dict_width", C.c_int32),
                 ("fwd", C.c_void_p), ("fwd_len", C.c_uint64), ("sorted_pairs", C.c_void_p), ("sorted_len", C.c_uint64),
                 ("dict", C.c_void_p), ("dict_len", C.c_uint64), ("inv", C.c_void_p), ("inv_len", C.c_uint64),
-                ("pad_char", C.c_int32)]
+                ("pad_char", C.c_int32), ("is_multi_value", C.c_int32), ("total_entries", C.c_int32)]
 
 
 class SegmentDesc(C.Structure):

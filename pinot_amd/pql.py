@@ -21,7 +21,7 @@ import re
 _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(?:[^']|'')*'|\"(?:[^\"])*\")|"
                     r"(?P<op><=|>=|<>|!=|=|<|>|\(|\)|,|\*)|(?P<id>[A-Za-z_][A-Za-z0-9_.$]*))")
 
-AGG_FUNCTIONS = ("count", "sum", "min", "max", "avg")
+AGG_FUNCTIONS = ("count", "sum", "min", "max", "avg", "countmv", "summv", "minmv", "maxmv", "avgmv")
 # distinctcount / minmaxrange / percentileNN (AggregationFunctionFactory.java:84-107): aggregation-only requests
 EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
 

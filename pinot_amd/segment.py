@@ -218,6 +218,9 @@ class Column:
     sorted_bytes: Optional[bytes]  # sorted forward index pairs
     inv_bytes: Optional[bytes]  # bitmap inverted index
     pad_char: str = DEFAULT_PAD
+    is_mv: bool = False          # multi-value column: fwd_bytes holds <col>.mv.fwd
+    total_entries: int = 0       # totalNumberOfEntries
+    max_mv: int = 0              # maxNumberOfMultiValues
 
     def dictionary_values(self):
         if self.data_type == "STRING":
@@ -232,6 +235,8 @@ class Column:
         return np.frombuffer(self.dict_bytes, dtype=_DICT_NP[self.data_type], count=self.cardinality)
 
     def dict_ids(self) -> np.ndarray:
+        if self.is_mv:
+            raise ValueError("multi-value column: use mv_dict_ids()")
         if self.is_sorted and self.sorted_bytes is not None:
             pairs = np.frombuffer(self.sorted_bytes, dtype=">i4").reshape(-1, 2)
             out = np.zeros(self.total_docs, dtype=np.int64)
@@ -239,6 +244,52 @@ class Column:
                 out[a:b + 1] = d
             return out
         return unpack_fixed_bit(self.fwd_bytes, self.total_docs, self.bits)
+
+
+    def mv_dict_ids(self) -> List[np.ndarray]:
+        """FixedBitMultiValueReader.getIntArray for every doc (io/reader/impl/v1/FixedBitMultiValueReader.java)."""
+        starts, raw_off = mv_layout(self.fwd_bytes, self.total_docs, self.total_entries)
+        vals = unpack_fixed_bit(self.fwd_bytes[raw_off:], self.total_entries, self.bits)
+        return [vals[starts[d]:starts[d + 1]] for d in range(self.total_docs)]
+
+
+def mv_docs_per_chunk(num_docs: int, total_values: int) -> int:
+    """FixedBitMultiValueWriter: float averageValuesPerDoc = totalNumValues / numDocs (an INTEGER division, then
+    widened); docsPerChunk = (int) Math.ceil(2048 / averageValuesPerDoc) in float arithmetic."""
+    avg = np.float32(total_values // num_docs)
+    return int(math.ceil(float(np.float32(2048) / avg)))
+
+
+def pack_mv_fwd(doc_ids: Sequence[Sequence[int]], bits: int) -> bytes:
+    """<col>.mv.fwd (io/writer/impl/v1/FixedBitMultiValueWriter.java): numChunks big-endian int chunk offsets (the
+    value index of every docsPerChunk-th doc), a totalNumValues-bit MSB-first bitset with the first value of every doc
+    set, then all values fixed-bit (MSB-first, as a single-value forward index over value positions)."""
+    n = len(doc_ids)
+    lens = np.array([len(v) for v in doc_ids], dtype=np.int64)
+    assert n > 0 and lens.min() >= 1, "every doc holds at least one value"
+    starts = np.concatenate([[0], np.cumsum(lens)])
+    tv = int(starts[-1])
+    dpc = mv_docs_per_chunk(n, tv)
+    nchunks = (n + dpc - 1) // dpc
+    head = starts[np.arange(nchunks) * dpc].astype(">i4").tobytes()
+    bitset = np.zeros((tv + 7) // 8 * 8, dtype=np.uint8)
+    bitset[starts[:-1]] = 1
+    bs = np.packbits(bitset).tobytes()[:(tv + 7) // 8]
+    flat = np.concatenate([np.asarray(v, dtype=np.int64) for v in doc_ids])
+    raw = pack_fixed_bit(flat, bits)[:(tv * bits + 7) // 8]
+    return head + bs + raw
+
+
+def mv_layout(buf: bytes, num_docs: int, total_values: int):
+    """(doc start offsets [num_docs + 1], byte offset of the raw values) of a <col>.mv.fwd."""
+    dpc = mv_docs_per_chunk(num_docs, total_values)
+    nchunks = (num_docs + dpc - 1) // dpc
+    head = nchunks * 4
+    nbs = (total_values + 7) // 8
+    bits = np.unpackbits(np.frombuffer(buf, dtype=np.uint8, count=nbs, offset=head))[:total_values]
+    starts = np.concatenate([np.nonzero(bits)[0], [total_values]]).astype(np.int64)
+    assert len(starts) == num_docs + 1
+    return starts, head + nbs
 
 
 @dataclass
@@ -299,6 +350,32 @@ def make_column(name: str, values, data_type: str = None, column_type: str = "DI
                   dict_bytes, width, fwd, sorted_b, inv, pad)
 
 
+def make_mv_column(name: str, doc_values: Sequence[Sequence], data_type: str = "INT", column_type: str = "DIMENSION",
+                   inverted: bool = False) -> Column:
+    """A v1 multi-value column from per-doc value lists (SegmentDictionaryCreator over all values; MV forward index;
+    the inverted index holds every doc under each of its values, HeapBitmapInvertedIndexCreator.add(int, int[]))."""
+    flat = np.concatenate([np.asarray(v) for v in doc_values])
+    dictionary, ids = np.unique(flat.astype(_DICT_NP[data_type].replace(">", "<")), return_inverse=True)
+    card = len(dictionary)
+    bits = num_bits(card)
+    lens = [len(v) for v in doc_values]
+    starts = np.concatenate([[0], np.cumsum(lens)])
+    doc_ids = [ids[starts[d]:starts[d + 1]] for d in range(len(doc_values))]
+    fwd = pack_mv_fwd(doc_ids, bits)
+    inv = None
+    if inverted:
+        docs = np.repeat(np.arange(len(doc_values)), lens)
+        per = [np.unique(docs[ids == k]) for k in range(card)]
+        blobs = [roaring_serialize(p) for p in per]
+        offs = np.concatenate([[0], np.cumsum([len(b) for b in blobs])]) + 4 * (card + 1)
+        inv = offs.astype(">i4").tobytes() + b"".join(blobs)
+    width = int(_DICT_NP[data_type][-1])
+    dict_bytes = np.asarray(dictionary).astype(_DICT_NP[data_type]).tobytes()
+    n = len(doc_values)
+    return Column(name, data_type, column_type, card, bits, n, n, False, inverted, dict_bytes, width, fwd, None, inv,
+                  DEFAULT_PAD, True, int(starts[-1]), int(max(lens)))
+
+
 def make_segment(name: str, columns: Sequence[Column]) -> SegmentData:
     n = columns[0].total_docs
     seg = SegmentData(name, n, n)
@@ -335,11 +412,15 @@ def write_segment(seg: SegmentData, out_dir: str) -> str:
                   p + "lengthOfEachEntry = %d" % (c.dict_width if c.data_type == "STRING" else 0),
                   p + "columnType = %s" % c.column_type, p + "isSorted = %s" % str(c.is_sorted).lower(),
                   p + "hasNullValue = false", p + "hasDictionary = true",
-                  p + "hasInvertedIndex = %s" % str(c.has_inverted).lower(), p + "isSingleValues = true",
-                  p + "maxNumberOfMultiValues = 0", p + "totalNumberOfEntries = 0"]
+                  p + "hasInvertedIndex = %s" % str(c.has_inverted).lower(),
+                  p + "isSingleValues = %s" % str(not c.is_mv).lower(),
+                  p + "maxNumberOfMultiValues = %d" % c.max_mv, p + "totalNumberOfEntries = %d" % c.total_entries]
         with open(os.path.join(d, c.name + ".dict"), "wb") as f:
             f.write(c.dict_bytes)
-        if c.is_sorted:
+        if c.is_mv:
+            with open(os.path.join(d, c.name + ".mv.fwd"), "wb") as f:
+                f.write(c.fwd_bytes)
+        elif c.is_sorted:
             with open(os.path.join(d, c.name + ".sv.sorted.fwd"), "wb") as f:
                 f.write(c.sorted_bytes)
         else:
@@ -394,9 +475,12 @@ def load_segment(seg_dir: str) -> SegmentData:
             f = os.path.join(seg_dir, c + suffix)
             return open(f, "rb").read() if os.path.exists(f) else None
 
+        mv = g("isSingleValues", "true") == "false"
         col = Column(c, dt, g("columnType"), card, int(g("bitsPerElement")), int(g("totalDocs")),
                      int(g("totalRawDocs", g("totalDocs"))), is_sorted, g("hasInvertedIndex") == "true",
-                     rd(".dict"), width, rd(".sv.unsorted.fwd"), rd(".sv.sorted.fwd"), rd(".bitmap.inv"), pad)
+                     rd(".dict"), width, rd(".mv.fwd") if mv else rd(".sv.unsorted.fwd"), rd(".sv.sorted.fwd"),
+                     rd(".bitmap.inv"), pad, mv, int(g("totalNumberOfEntries", "0")),
+                     int(g("maxNumberOfMultiValues", "0")))
         seg.columns[c] = col
     st = os.path.join(seg_dir, "star-tree.bin")
     if os.path.exists(st):

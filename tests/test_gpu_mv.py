@@ -1,0 +1,101 @@
+"""GPU parity of multi-value columns: v1 .mv.fwd staged into HBM (doc starts + fixed-bit values),
+MV filter leaves (pgx_mv_leaf_mask: ANY value matches for EQ / IN / RANGE, NO value excluded for NEQ / NOT_IN, one
+entry scanned per doc like MVScanDocIdIterator; bitmap inverted indexes hold every doc under each of its values) and
+the MV aggregation functions COUNTMV / SUMMV / MINMV / MAXMV / AVGMV (pgx_mv_aggregate over the query kernel's
+selection bits).  Against the oracle's literal restatement, statistics included, on one and several segments."""
+import numpy as np
+import pytest
+
+from oracle import pinot_oracle as O
+from pinot_amd import pql
+from pinot_amd import segment as S
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from pinot_amd import engine as E
+    c = E.Context(0)
+    yield c
+    c.close()
+
+
+def _segment(name, seed, n, inverted):
+    rng = np.random.default_rng(seed)
+    tags = [rng.integers(0, 40, rng.integers(1, 6)).tolist() for _ in range(n)]
+    vals = [np.round(rng.normal(0, 100, rng.integers(1, 4)), 3).tolist() for _ in range(n)]
+    raw_sv = {"d": rng.integers(0, 60, n).astype(np.int32), "m": rng.integers(0, 1000, n).astype(np.int32)}
+    cols = [S.make_mv_column("tags", tags, "INT", inverted=inverted),
+            S.make_mv_column("vals", vals, "DOUBLE"),
+            S.make_column("d", raw_sv["d"]), S.make_column("m", raw_sv["m"])]
+    seg = S.make_segment(name, cols)
+    oseg = O.OSegment.from_raw({"tags": tags, "vals": vals, **raw_sv}, inverted=("tags",) if inverted else ())
+    return seg, oseg
+
+
+@pytest.fixture(scope="module", params=[False, True], ids=["scan", "inverted"])
+def segs(ctx, request):
+    from pinot_amd import engine as E
+    out = []
+    for i in range(2):
+        seg, oseg = _segment("mv%d" % i, 40 + i, 70000 + 13 * i, request.param)
+        out.append((E.IndexSegment(ctx, seg), oseg))
+    return out
+
+
+QUERIES = [
+    "SELECT COUNTMV(tags), SUMMV(tags), MINMV(tags), MAXMV(tags), AVGMV(tags) FROM t",
+    "SELECT COUNTMV(tags), SUMMV(vals), MINMV(vals), MAXMV(vals), AVGMV(vals) FROM t WHERE d > 30",
+    "SELECT COUNT(*), SUM(m), SUMMV(tags) FROM t WHERE tags IN (3, 5)",
+    "SELECT COUNT(*), MAX(m) FROM t WHERE tags <> 3 AND d < 50",
+    "SELECT COUNT(*), SUM(m), COUNTMV(tags) FROM t WHERE tags NOT IN (1, 2, 39) OR m > 900",
+    "SELECT COUNT(*), AVGMV(vals) FROM t WHERE tags BETWEEN 2 AND 4",
+    "SELECT SUM(m), COUNT(*) FROM t WHERE tags = 7 GROUP BY d",
+    "SELECT COUNT(*) FROM t WHERE tags = 12345",
+]
+
+
+def _check(blk, o, q):
+    fns = [a["fn"] for a in q["aggregations"]]
+    if q.get("group_by"):
+        m = blk.get_aggregation_group_by_result()
+        m = m.as_map() if m is not None else {}
+        assert set(m) == set(o["map"])
+        for k, v in o["map"].items():
+            H.assert_values_equal(m[k], v, fns, rel=1e-9)
+    else:
+        H.assert_values_equal(blk.get_aggregation_result(), o["results"], fns, rel=1e-9)
+
+
+@pytest.mark.parametrize("text", QUERIES)
+def test_mv_inner_segment_matches_oracle(ctx, segs, text):
+    from pinot_amd import engine as E
+    q = pql.compile(text)
+    gseg, oseg = segs[0]
+    op = E.InstancePlanMakerImplV2(ctx).make_inner_segment_plan(gseg, q).run()
+    blk = op.next_block()
+    o = H.oracle_answer([oseg], q, literal=True)
+    assert op.get_execution_statistics().as_list() == list(o["stats"])
+    _check(blk, o, q)
+
+
+@pytest.mark.parametrize("text", QUERIES)
+def test_mv_combine_matches_oracle(ctx, segs, text):
+    from pinot_amd import engine as E
+    q = pql.compile(text)
+    blk = E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan([g for g, _ in segs], q).execute()
+    o = H.oracle_answer([o for _, o in segs], q, literal=True)
+    assert blk.stats.as_list() == list(o["stats"])
+    _check(blk, o, q)
+
+
+def test_mv_unsupported_shapes_fail_loudly(ctx, segs):
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    gseg, _ = segs[0]
+    for text in ("SELECT SUM(tags) FROM t", "SELECT COUNT(*) FROM t GROUP BY tags",
+                 "SELECT SUMMV(tags) FROM t GROUP BY d", "SELECT SUMMV(m) FROM t"):
+        with pytest.raises(N.PgxError):
+            E.InstancePlanMakerImplV2(ctx).make_inner_segment_plan(gseg, pql.compile(text)).run().next_block()
