@@ -973,7 +973,8 @@ def filter_mask_vectorized(seg: OSegment, tree: Optional[dict]) -> np.ndarray:
 FN_DEFAULT = {"count": 0.0, "sum": 0.0, "min": math.inf, "max": -math.inf,
               "countmv": 0.0, "summv": 0.0, "minmv": math.inf, "maxmv": -math.inf}
 MV_FUNCTIONS = ("countmv", "summv", "minmv", "maxmv", "avgmv")
-EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
+EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95",
+                 "percentile99", "percentileest50", "percentileest90", "percentileest95", "percentileest99")
 
 
 # DISTINCTCOUNTHLL: stream-lib 2.7.0 HyperLogLog(log2m = HllConstants.DEFAULT_LOG2M = 8) (third-party, not vendored;
@@ -1102,7 +1103,8 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
         fn = a["fn"]
         holders.append([0.0, 0] if fn in ("avg", "avgmv") else set() if fn == "distinctcount" else
                        [0] * (1 << HLL_LOG2M) if fn in ("distinctcounthll", "fasthll") else
-                       [math.inf, -math.inf] if fn == "minmaxrange" else [] if fn.startswith("percentile") else
+                       [math.inf, -math.inf] if fn == "minmaxrange" else _qdigest() if fn.startswith("percentileest")
+                       else [] if fn.startswith("percentile") else
                        FN_DEFAULT[fn])
     for blk in _blocks(docs, MAX_DOC_PER_CALL):
         for k, a in enumerate(q["aggregations"]):
@@ -1164,6 +1166,9 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
             elif fn == "minmaxrange":  # MinMaxRangeAggregationFunction.aggregate: block min / max into the pair
                 if len(v):
                     holders[k] = [min(holders[k][0], float(v.min())), max(holders[k][1], float(v.max()))]
+            elif fn.startswith("percentileest"):  # PercentileestAggregationFunction.aggregate: add((long) v) per doc
+                for x in v.tolist():
+                    holders[k].add(int(x))
             elif fn.startswith("percentile"):  # PercentileAggregationFunction.aggregate: DoubleArrayList of values
                 holders[k].extend(v.tolist())
     results = []
@@ -1178,6 +1183,8 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
             results.append(list(holders[k]))
         elif a["fn"] == "minmaxrange":
             results.append((float(holders[k][0]), float(holders[k][1])))
+        elif a["fn"].startswith("percentileest"):
+            results.append(holders[k])
         elif a["fn"].startswith("percentile"):
             results.append(sorted(holders[k]))
         else:
@@ -1273,6 +1280,10 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
                 np.minimum.at(mn, gid, v)
                 np.maximum.at(mx, gid, v)
                 vals = [(float(a_), float(b_)) for a_, b_ in zip(mn, mx)]
+            elif fn.startswith("percentileest"):  # PercentileestAggregationFunction.aggregateGroupBySV: per doc
+                vals = [_qdigest() for _ in range(G)]
+                for i, x in zip(gid.tolist(), v.tolist()):
+                    vals[i].add(int(x))
             elif fn.startswith("percentile"):  # PercentileAggregationFunction.aggregateGroupBySV: a list per group
                 vals = [[] for _ in range(G)]
                 for i, x in zip(gid.tolist(), v.tolist()):
@@ -1300,6 +1311,14 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
 # ------------------------------------------------------------------------------------------------
 # a-19: combine across segments
 # ------------------------------------------------------------------------------------------------
+def _qdigest():
+    """QuantileDigest(0.05) as vendored by the reference (quantile/digest/QuantileDigest.java).  The data structure is
+    shared with the product's host code (pinot_amd/qdigest.py restates it); what the oracle checks independently is the
+    per-doc insertion in doc order, as PercentileestAggregationFunction does, against the GPU's value histogram."""
+    from pinot_amd.qdigest import QuantileDigest
+    return QuantileDigest(0.05)
+
+
 def combine_two(fn: str, a, b):
     """Legacy combineTwoValues (query/aggregation/function/{Sum,Count,Min,Max,Avg}AggregationFunction.java)."""
     if fn in ("count", "countmv", "summv"):
@@ -1324,6 +1343,8 @@ def combine_two(fn: str, a, b):
         return [max(x, y) for x, y in zip(a, b)]
     if fn == "minmaxrange":  # MinMaxRangeAggregationFunction.combineTwoValues
         return (min(a[0], b[0]), max(a[1], b[1]))
+    if fn.startswith("percentileest"):  # DigestAggregationFunction.combineTwoValues: merge (a copy of) the first
+        return _qdigest().merge(a).merge(b)
     if fn.startswith("percentile"):  # PercentileAggregationFunction.combineTwoValues: list concatenation
         return sorted(list(a) + list(b))
     raise ValueError(fn)
@@ -1350,6 +1371,8 @@ def reduce_extended(fn: str, v) -> float:
         return hll_cardinality(v)
     if fn == "minmaxrange":
         return v[1] - v[0] if v[0] != math.inf and v[1] != -math.inf else -1.0  # DEFAULT_MIN_MAX_RANGE_VALUE
+    if fn.startswith("percentileest"):  # DigestAggregationFunction.reduce: getQuantile of the merged digest
+        return v.get_quantile(int(fn[len("percentileest"):]) / 100.0)
     p = int(fn[len("percentile"):])
     return float(sorted(v)[int(len(v) * (p / 100.0))])
 

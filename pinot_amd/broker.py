@@ -39,6 +39,8 @@ def function_name(agg: dict) -> str:
     .java:170, quantile/PercentileAggregationFunction.java:171)."""
     if agg["fn"] == "count":
         return "count_star"
+    if agg["fn"].startswith("percentileest"):  # DigestAggregationFunction.getFunctionName (:161-163)
+        return "percentileEst%s_%s" % (agg["fn"][len("percentileest"):], agg["column"])
     return "%s_%s" % (_NAMES.get(agg["fn"], agg["fn"]), agg["column"])
 
 
@@ -122,6 +124,7 @@ def _reduce(fn: str, values: Sequence):
 def _format(fn: str, v) -> str:
     """Long / Integer (count, distinctcount) -> toString; doubles -> %1.5f (BrokerReduceService.formatValue)."""
     return str(int(v)) if fn in ("count", "countmv", "distinctcount", "distinctcounthll", "fasthll") \
+        or fn.startswith("percentileest") \
         else java_format_5f(float(v))
 
 

@@ -34,6 +34,7 @@ import struct
 from typing import Dict, List, Optional, Sequence
 
 from . import hll as HLL
+from . import qdigest as QD
 
 V1, V2 = 1, 2
 HEADER_BYTES = 52
@@ -111,6 +112,8 @@ def object_type(v) -> int:
         return T_MIN_MAX_RANGE
     if isinstance(v, HyperLogLogRegs):
         return T_HLL
+    if isinstance(v, QD.QuantileDigest):
+        return T_QDIGEST
     if isinstance(v, dict):
         return T_HASHMAP
     if isinstance(v, (set, frozenset)):
@@ -139,6 +142,8 @@ def serialize_object(v) -> bytes:
         return _i32(len(v)) + b"".join(_i32(int(x)) for x in sorted(v))
     if t == T_HLL:
         return HLL.to_bytes(v.regs)
+    if t == T_QDIGEST:
+        return v.serialize()
     # HashMap: size, then (key type, value type) before the first entry, then length-prefixed key / value bytes
     out = [_i32(len(v))]
     keys = java_hashmap_order(list(v.keys())) if all(isinstance(k, str) for k in v) else list(v.keys())
@@ -174,6 +179,8 @@ def deserialize_object(b: bytes, t: int):
         return set(struct.unpack_from(">%di" % n, b, 4))
     if t == T_HLL:
         return HyperLogLogRegs(HLL.from_bytes(b))
+    if t == T_QDIGEST:
+        return QD.QuantileDigest.deserialize(b)
     if t == T_HASHMAP:
         if not b:
             return {}
@@ -363,6 +370,8 @@ def _to_object(fn: str, v):
     if fn in ("distinctcounthll", "fasthll"):
         import numpy as np
         return HyperLogLogRegs(HLL.empty() if v is None else np.asarray(v, dtype=np.uint8))  # None: a fresh estimator
+    if fn.startswith("percentileest"):
+        return v if v is not None else QD.QuantileDigest()
     if fn.startswith("percentile"):
         out = []
         for value, count in v:
@@ -380,6 +389,8 @@ def _from_object(fn: str, o):
         return set(o)
     if fn in ("distinctcounthll", "fasthll"):
         return o.regs
+    if fn.startswith("percentileest"):
+        return o
     if fn.startswith("percentile"):
         hist: Dict[float, int] = {}
         for x in o:

@@ -29,6 +29,7 @@ import numpy as np
 
 from . import engine as E
 from . import hll as HLL
+from . import qdigest as QD
 from . import native as N
 from .pql import EXT_FUNCTIONS
 
@@ -226,6 +227,8 @@ def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock
             return HLL.from_ints(_hash_set(_dtype(segments, a["column"]), hists[a["column"]].get(key, [])))
         if fn == "fasthll":
             return _fast_hll(hists[a["column"]].get(key, []))
+        if fn.startswith("percentileest"):
+            return QD.from_histogram(_numeric(hists[a["column"]].get(key, [])))
         if fn.startswith("percentile"):
             return _numeric(hists[a["column"]].get(key, []))
         return bvals[s]
@@ -286,6 +289,8 @@ def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment],
             out.append(HLL.from_ints(_hash_set(_dtype(segments, a["column"]), hists[a["column"]])))
         elif fn == "fasthll":
             out.append(_fast_hll(hists[a["column"]]))
+        elif fn.startswith("percentileest"):  # QuantileDigest of the selected values (pinot_amd/qdigest.py)
+            out.append(QD.from_histogram(_numeric(hists[a["column"]])))
         elif fn.startswith("percentile"):
             out.append(_numeric(hists[a["column"]]))
         else:
@@ -306,6 +311,8 @@ def reduce_value(fn: str, v):
         return HLL.cardinality(v)
     if fn == "minmaxrange":
         return v[1] - v[0] if v[0] != math.inf and v[1] != -math.inf else -1.0
+    if fn.startswith("percentileest"):  # DigestAggregationFunction.reduce (quantile/digest/...:134-141): a long
+        return 0 if v is None else v.get_quantile(int(fn[len("percentileest"):]) / 100.0)
     return percentile_of_histogram(fn, v)
 
 
@@ -317,4 +324,6 @@ def combine_two(fn: str, a, b):
         return HLL.merge(a, b)
     if fn == "minmaxrange":
         return (min(a[0], b[0]), max(a[1], b[1]))
+    if fn.startswith("percentileest"):  # DigestAggregationFunction.combineTwoValues: merge into the first
+        return QD.merge_all([QD.QuantileDigest.deserialize(a.serialize()), b])
     return merge_histograms(a, b)

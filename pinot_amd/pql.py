@@ -23,7 +23,8 @@ _TOKEN = re.compile(r"\s*(?:(?P<num>-?\d+(?:\.\d+)?(?:[eE][-+]?\d+)?)|(?P<str>'(
 
 AGG_FUNCTIONS = ("count", "sum", "min", "max", "avg", "countmv", "summv", "minmv", "maxmv", "avgmv")
 # distinctcount / minmaxrange / percentileNN (AggregationFunctionFactory.java:84-107): aggregation-only requests
-EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95", "percentile99")
+EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95",
+                 "percentile99", "percentileest50", "percentileest90", "percentileest95", "percentileest99")
 
 
 class PqlError(ValueError):

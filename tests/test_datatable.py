@@ -118,9 +118,10 @@ def test_group_by_reduce_same_through_the_wire(osegs):  # noqa: F811
 
 @pytest.mark.parametrize("text", ["SELECT DISTINCTCOUNT(dim0), DISTINCTCOUNTHLL(dim0), MINMAXRANGE(met), "
                                   "PERCENTILE90(met) FROM midas",
-                                  "SELECT DISTINCTCOUNT(dim1), MINMAXRANGE(met) FROM midas GROUP BY dim0 TOP 3"])
+                                  "SELECT DISTINCTCOUNT(dim1), MINMAXRANGE(met) FROM midas GROUP BY dim0 TOP 3",
+                                  "SELECT PERCENTILEEST90(met), PERCENTILEEST50(met) FROM midas"])
 def test_extended_intermediates_round_trip(osegs, text):  # noqa: F811
-    """IntOpenHashSet, HyperLogLog (stream-lib bytes), MinMaxRangePair and DoubleArrayList objects."""
+    """IntOpenHashSet, HyperLogLog (stream-lib bytes), MinMaxRangePair, DoubleArrayList and QuantileDigest objects."""
     q = pql.compile(text)
     obj = _oracle_response(q, osegs)
     wire = D.response_to_datatable(q, obj)

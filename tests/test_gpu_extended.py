@@ -38,6 +38,7 @@ QUERIES = [
     "SELECT COUNT(*), MINMAXRANGE(m), DISTINCTCOUNT(d) FROM t WHERE d = 123456",
     "SELECT DISTINCTCOUNTHLL(v), DISTINCTCOUNT(v), DISTINCTCOUNTHLL(w), DISTINCTCOUNTHLL(d) FROM t WHERE m < 4000",
     "SELECT DISTINCTCOUNTHLL(m), COUNT(*) FROM t WHERE d = 123456",
+    "SELECT PERCENTILEEST50(v), PERCENTILEEST90(m), PERCENTILEEST99(w), COUNT(*) FROM t WHERE d < 40",
 ]
 
 
@@ -61,6 +62,8 @@ def test_extended_functions_match_oracle(env, text):
         elif fn == "minmaxrange":
             assert tuple(g) == tuple(e)
             assert X.reduce_value(fn, g) == O.reduce_extended(fn, e)
+        elif fn.startswith("percentileest"):  # both digests answer within the rank-error guarantee
+            _assert_qdigest_bound(fn, X.reduce_value(fn, g), O.reduce_extended(fn, e), _selected(osegs, q, fn, fns))
         elif fn.startswith("percentile"):
             vals, cnts = np.unique(np.asarray(e, dtype=np.float64), return_counts=True)
             assert g == [(float(x), int(c)) for x, c in zip(vals, cnts)]
@@ -73,12 +76,46 @@ def test_extended_functions_match_oracle(env, text):
     assert st[1] == H.literal_entries(osegs, q)
 
 
+def _selected(osegs, q, fn, fns):
+    """The (long) values PERCENTILEEST offers: the column's selected values over every segment."""
+    col = q["aggregations"][fns.index(fn)]["column"]
+    out = []
+    for s in osegs:
+        m = O.filter_mask_vectorized(s, q.get("filter"))
+        c = s.columns[col]
+        out += [int(x) for x in c.dictionary[c.dict_ids[np.nonzero(m)[0]]].astype(np.float64)]
+    return np.sort(np.array(out, dtype=np.int64))
+
+
+def _assert_qdigest_bound(fn, got, exp, values):
+    """QuantileDigest(maxError = 0.05): the answer's rank lies within maxError * N of q * N (getQuantile contract)."""
+    qq = int(fn[len("percentileest"):]) / 100.0
+    n = len(values)
+    for x in (got, exp):
+        lo, hi = np.searchsorted(values, x, side="left"), np.searchsorted(values, x, side="right")
+        assert lo - 0.05 * n - 1 <= qq * n <= hi + 0.05 * n + 1, (fn, x, qq, n)
+
+
 GROUPED = [
     "SELECT DISTINCTCOUNT(v), MINMAXRANGE(m), SUM(m), PERCENTILE50(m), COUNT(*) FROM t GROUP BY d",
     "SELECT PERCENTILE90(w), DISTINCTCOUNT(w), MAX(v) FROM t WHERE m < 2500 GROUP BY d TOP 5",
     "SELECT MINMAXRANGE(v), AVG(m), DISTINCTCOUNT(m) FROM t WHERE d IN (1, 2, 3) GROUP BY d, m",
     "SELECT DISTINCTCOUNTHLL(v), SUM(m), DISTINCTCOUNTHLL(w) FROM t WHERE m > 100 GROUP BY d",
+    "SELECT PERCENTILEEST90(m), SUM(m) FROM t WHERE d < 10 GROUP BY d",
 ]
+
+
+def _group_values(osegs, q, key, fn, fns):
+    col = q["aggregations"][fns.index(fn)]["column"]
+    gcols = q["group_by"]["columns"]
+    out = []
+    for s in osegs:
+        m = O.filter_mask_vectorized(s, q.get("filter"))
+        for d in np.nonzero(m)[0]:
+            if "\t".join(s.columns[g].string_of(int(s.columns[g].dict_ids[d])) for g in gcols) == key:
+                c = s.columns[col]
+                out.append(float(c.dictionary[c.dict_ids[d]]))
+    return out
 
 
 @pytest.mark.parametrize("text", GROUPED)
@@ -99,6 +136,11 @@ def test_extended_functions_group_by_match_oracle(env, text):
                 assert list(g) == list(x)
             elif fn == "minmaxrange":
                 assert tuple(g) == tuple(x)
+            elif fn.startswith("percentileest"):  # same multiset offered: same count, quantiles within the bound
+                assert g.count == x.count
+                vals = np.sort(np.array([int(v) for v in _group_values(osegs, q, k, fn, fns)], dtype=np.int64))
+                _assert_qdigest_bound(fn, g.get_quantile(int(fn[13:]) / 100.0), x.get_quantile(int(fn[13:]) / 100.0),
+                                      vals)
             elif fn.startswith("percentile"):
                 vals, cnts = np.unique(np.asarray(x, dtype=np.float64), return_counts=True)
                 assert g == [(float(a), int(c)) for a, c in zip(vals, cnts)]
