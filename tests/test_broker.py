@@ -26,7 +26,7 @@ def _oracle_response(q, osegs):
                                   stats=a["stats"])
     res = []
     for agg, v in zip(q["aggregations"], a["results"]):
-        if agg["fn"].startswith("percentile"):  # the oracle's DoubleArrayList -> the (value, count) multiset
+        if agg["fn"].startswith("percentile") and not agg["fn"].startswith("percentileest"):  # the oracle's DoubleArrayList -> the (value, count) multiset
             vals, cnts = np.unique(np.asarray(v, dtype=np.float64), return_counts=True)
             v = [(float(x), int(c)) for x, c in zip(vals, cnts)]
         res.append(v)
