@@ -194,7 +194,7 @@ def main():
     merged = [None]
 
     def step():
-        binds, _owner = q.bindings(segs)  # a-4 per segment, inside the timed step
+        binds, _owner = q.bindings(segs, seg_arr)  # a-4 per segment, inside the timed step
         r = C.c_void_p()
         if dense and world > 1:
             opts = N.ExecOpts(0, C.c_void_p(dense_t.data_ptr()), dense_t.numel() * 8, N.PGX_X_KEEP_DENSE_ON_DEVICE)

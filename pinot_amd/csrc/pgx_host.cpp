@@ -230,6 +230,7 @@ struct pgx_ctx {
   int device = 0;
   int num_cus = 256;
   hipStream_t stream = nullptr;
+  hipStream_t side = nullptr;  // batched queries: argument uploads + bitmap programs run ahead of the query kernels
   std::mutex mu;
   // Pinned host blocks for the per-query argument arena (one H2D copy per query) and result read-back.
   std::multimap<size_t, void*> pinned_free;
@@ -3217,6 +3218,33 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   bs = (n + nb - 1) / nb;  // even batches
   std::vector<std::unique_ptr<ExecPlan>> plans;
   std::vector<std::unique_ptr<ExecBuffers>> bufs;
+  // Two streams: each batch's argument arena and bitmap programs go on the side stream, and the query stream waits
+  // for them with an event.  The copies' SDMA latency and the bitmap programs of batch k + 1 then run while batch k's
+  // query kernel streams the forward indexes, instead of between the query kernels.  Declared after the buffers:
+  // on any exit both streams drain before the buffers return to the pool.
+  const bool two = std::getenv("PGX_BATCH_ONE_STREAM") == nullptr;
+  hipStream_t ss = two ? ctx->side : st;
+  struct Events {
+    hipStream_t a, b;
+    std::vector<hipEvent_t> ev;
+    hipEvent_t make() {
+      hipEvent_t e = nullptr;
+      hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+      ev.push_back(e);
+      return e;
+    }
+    ~Events() {
+      if (ev.empty()) return;
+      (void)hipStreamSynchronize(a);
+      (void)hipStreamSynchronize(b);
+      for (auto e : ev) (void)hipEventDestroy(e);
+    }
+  } evs{st, ss, {}};
+  if (two) {  // the side stream starts after the work already queued on the query stream (a caller's stream)
+    hipEvent_t e = evs.make();
+    hip_check(hipEventRecord(e, st), "record");
+    hip_check(hipStreamWaitEvent(ss, e, 0), "wait");
+  }
   int64_t host_entries = 0, total_raw = 0;
   for (int b = 0; b < nb; ++b) {
     const int s0 = b * bs, cnt = std::min(bs, n - s0);
@@ -3229,21 +3257,26 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
     const int gm = P->kq.group_mode;
     if (b == 0 && (P->use_part || !(gm == G_NONE || gm == G_DENSE_LDS || gm == G_DENSE_GLOBAL))) return false;
     auto B = std::make_unique<ExecBuffers>();
-    upload_plan(ctx, *P, *B, st);
+    upload_plan(ctx, *P, *B, ss);
     plan_jit(ctx, q, segs + s0, cnt, *P, *B);
     if (b == 0) {
       alloc_outputs(ctx, *P, *B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
-      reset_outputs(*P, *B, st);
+      reset_outputs(*P, *B, ss);
     } else {
       const KQuery& K0 = plans[0]->kq;
       if (P->kq.group_mode != K0.group_mode || P->dense_slots != plans[0]->dense_slots ||
           P->kq.num_planes != K0.num_planes)
         fail(PGX_ERR_INTERNAL, "batched plans disagree");
       alloc_outputs(ctx, *P, *B, K0.table, plans[0]->dense_slots * uint64_t(K0.num_planes) * 8);
-      reset_outputs(*P, *B, st, false);
+      reset_outputs(*P, *B, ss, false);
       P->kq.agg_out = K0.agg_out;  // one output block for the whole query
       P->kq.stats = K0.stats;
       P->kq.overflow = K0.overflow;
+    }
+    if (two) {
+      hipEvent_t e = evs.make();
+      hip_check(hipEventRecord(e, ss), "record");
+      hip_check(hipStreamWaitEvent(st, e, 0), "wait");
     }
     launch_scan(*P, st);
     host_entries += P->host_entries;
@@ -3743,6 +3776,7 @@ pgx_status pgx_ctx_create(const pgx_ctx_opts* opts, pgx_ctx** out) {
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
       c->num_cus = prop.multiProcessorCount;
     hip_check(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking), "hipStreamCreate");
+    hip_check(hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking), "hipStreamCreate");
     *out = c;
   });
 }
@@ -3754,11 +3788,13 @@ void ctx_unref(pgx_ctx* ctx) {
   if (ctx->refs.fetch_sub(1) != 1) return;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->side);
   for (auto& kv : ctx->free_blocks) (void)hipFree(kv.second);
   for (auto& kv : ctx->live) (void)hipFree(kv.first);
   for (auto& kv : ctx->pinned_free) (void)hipHostFree(kv.second);
   for (auto& kv : ctx->pinned_live) (void)hipHostFree(kv.first);
   (void)hipStreamDestroy(ctx->stream);
+  (void)hipStreamDestroy(ctx->side);
   delete ctx;
 }
 
@@ -4351,13 +4387,25 @@ pgx_status pgx_bind_predicates(const pgx_query* q, pgx_segment* const* segs, int
     const size_t L = q->leaf_col.size();
     B->arr.assign(size_t(n) * L, pgx_leaf_binding{0, -1, nullptr});
     B->words.reserve(size_t(n) * L);
-    // one resolution per (leaf, distinct dictionary)
-    std::map<std::tuple<size_t, uint64_t, int, int, int>, size_t> memo;
+    // one resolution per (leaf, distinct dictionary); consecutive segments usually share a dictionary, so each leaf
+    // first compares with the previous segment's column before the map lookup
+    using Key = std::tuple<size_t, uint64_t, int, int, int>;
+    std::map<Key, size_t> memo;
+    std::vector<const StagedColumn*> prev(L, nullptr);
+    std::vector<size_t> prev_at(L, 0);
     for (int s = 0; s < n; ++s)
       for (size_t l = 0; l < L; ++l) {
         const StagedColumn& c = segs[s]->col(q->leaf_col[l]);
-        const auto key = std::make_tuple(l, c.dict_hash, c.card, c.data_type, c.pad_char);
         pgx_leaf_binding& b = B->arr[size_t(s) * L + l];
+        const StagedColumn* p = prev[l];
+        if (p && p->dict_hash == c.dict_hash && p->card == c.card && p->data_type == c.data_type &&
+            p->pad_char == c.pad_char) {
+          b = B->arr[prev_at[l]];
+          continue;
+        }
+        prev[l] = &c;
+        prev_at[l] = size_t(s) * L + l;
+        const Key key = std::make_tuple(l, c.dict_hash, c.card, c.data_type, c.pad_char);
         auto it = memo.find(key);
         if (it != memo.end()) {
           b = B->arr[it->second];

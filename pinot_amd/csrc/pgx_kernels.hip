@@ -853,50 +853,79 @@ __global__ void __launch_bounds__(256) pgx_roaring_program_wide(const RProg* __r
 // word in registers and the chunk's mask written out.
 constexpr int kSegRThreads = 512;
 constexpr int kSegRBitmaps = 512;
-__global__ void __launch_bounds__(kSegRThreads) pgx_roaring_program_seg(const RProg* __restrict__ progs,
-                                                                        const RDesc* __restrict__ descs, int nprogs) {
-  const int pi = static_cast<int>(blockIdx.x);
+// Workgroup barrier that orders LDS only: no s_waitcnt vmcnt(0), so global loads issued before it (next container's
+// fields) and the mask stores of the previous chunk are not drained at every phase of the chunk loop.  Global memory
+// is never communicated between the workgroup's threads here.
+__device__ __forceinline__ void seg_lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+__global__ void __launch_bounds__(kSegRThreads, 8) pgx_roaring_program_seg(const RProg* __restrict__ progs,
+                                                                        const RDesc* __restrict__ descs, int nprogs,
+                                                                        int parts) {
+  // `parts` workgroups per segment, each walking a contiguous range of its chunks: short segment lists (a batch of a
+  // long query) still put enough workgroups on the chip
+  const int pi = static_cast<int>(blockIdx.x) / parts;
   if (pi >= nprogs) return;
   const RProg& P = progs[pi];
+  const int per = (P.nchunks + parts - 1) / parts;
+  const int c0 = (static_cast<int>(blockIdx.x) % parts) * per;
+  const int c1 = min(P.nchunks, c0 + per);
+  if (c0 >= c1) return;
   extern __shared__ uint32_t lmask[];  // [leaf][2048]
   __shared__ const uint8_t* cptr[kSegRBitmaps];
   __shared__ int ccard[kSegRBitmaps], cpre[kSegRBitmaps + 1], cleaf[kSegRBitmaps];
   __shared__ int ncont;
   const int tid = threadIdx.x;
-  // leaves in program order (uniform loads)
-  int leaf_desc[kRProgMaxLeaves], leaf_b0[kRProgMaxLeaves + 1];
-  int nl = 0, tot = 0;
+  // leaves in program order (uniform loads); lane tid < total bitmaps owns bitmap (tid - first) of leaf `leaf`
+  int nl = 0, tot = 0, leaf = 0, my_desc = -1, my_first = 0;
   for (int i = 0; i < P.nops; ++i)
     if (P.op[i] == RP_LEAF && nl < kRProgMaxLeaves) {
       const int a = P.arg[i];
-      leaf_desc[nl] = a;
-      leaf_b0[nl] = tot;
-      tot += a >= 0 ? descs[a].nb : 0;
+      const int nb = a >= 0 ? descs[a].nb : 0;
+      if (tid >= tot && tid < tot + nb) {
+        leaf = nl;
+        my_desc = a;
+        my_first = tot;
+      }
+      tot += nb;
       ++nl;
     }
-  leaf_b0[nl] = tot;
-  const int total_b = tot;  // the host launches this kernel only when total_b <= kSegRBitmaps
-  // this lane's bitmap: header, container count and the fields of its first container
+  // this lane's bitmap: header, container count and the fields of its first container (the host launches this
+  // kernel only when the program's bitmaps number <= kSegRBitmaps)
   const uint8_t* base = nullptr;
-  int n = 0, cur = 0, key = 1 << 30, card = 0, leaf = 0;
+  int n = 0, cur = 0, key = 1 << 30, card = 0;
   uint32_t off = 0;
-  if (tid < total_b) {
-    int j = 0;
-    while (leaf_b0[j + 1] <= tid) ++j;
-    leaf = j;
-    const RDesc& D = descs[leaf_desc[j]];
-    base = D.inv + D.offs[tid - leaf_b0[j]];
+  if (my_desc >= 0) {
+    const RDesc& D = descs[my_desc];
+    base = D.inv + D.offs[tid - my_first];
     n = static_cast<int>(rd32(base + 4));
-    if (n > 0) {
-      key = static_cast<int>(rd16(base + 8));
-      card = static_cast<int>(rd16(base + 10)) + 1;
-      off = rd32(base + 8 + 4 * n);
+    if (c0 > 0 && n > 0) {  // first container with key >= c0: keys are strictly increasing, so key[c0] == c0 settles it
+      if (n > c0 && static_cast<int>(rd16(base + 8 + 4 * c0)) == c0) {
+        cur = c0;
+      } else {
+        int lo = 0, hi = n;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (static_cast<int>(rd16(base + 8 + 4 * mid)) < c0) lo = mid + 1; else hi = mid;
+        }
+        cur = lo;
+      }
+    }
+    if (cur < n) {
+      key = static_cast<int>(rd16(base + 8 + 4 * cur));
+      card = static_cast<int>(rd16(base + 8 + 4 * cur + 2)) + 1;
+      off = rd32(base + 8 + 4 * n + 4 * cur);
     }
   }
-  for (int chunk = 0; chunk < P.nchunks; ++chunk) {
+  __shared__ int bidx[kSegRBitmaps], nbm;
+  constexpr int kPer = 4;  // array elements in flight per lane (8 costs a quarter of the workgroups per CU)
+  for (int chunk = c0; chunk < c1; ++chunk) {
     for (int i = tid; i < nl * 2048; i += kSegRThreads) lmask[i] = 0u;
     if (tid == 0) ncont = 0;
-    __syncthreads();
+    // LDS-only barriers: the container-field prefetches and the previous chunk's mask stores stay in flight
+    seg_lds_barrier();
     if (key == chunk) {
       const int slot = atomicAdd(&ncont, 1);
       cptr[slot] = base + off;
@@ -912,37 +941,57 @@ __global__ void __launch_bounds__(kSegRThreads) pgx_roaring_program_seg(const RP
         key = 1 << 30;
       }
     }
-    __syncthreads();
+    seg_lds_barrier();
     const int nc = ncont;
-    if (tid < 64) {  // exclusive prefix of the array containers' cardinalities (8 per lane)
-      int v[8], x = 0;
+    if (tid < 64) {  // exclusive prefix of the array containers' cardinalities (8 per lane); bitmap containers listed
+      int v[8], x = 0, nb = 0;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int k = tid * 8 + q;
-        v[q] = (k < nc && ccard[k] <= 4096) ? ccard[k] : 0;
+        const bool in = k < nc;
+        v[q] = (in && ccard[k] <= 4096) ? ccard[k] : 0;
+        nb += (in && ccard[k] > 4096) ? 1 : 0;
         x += v[q];
       }
-      int incl = x;
+      int incl = x, binc = nb;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const int y = __shfl_up(incl, d, 64);
-        if (tid >= d) incl += y;
+        const int z = __shfl_up(binc, d, 64);
+        if (tid >= d) {
+          incl += y;
+          binc += z;
+        }
       }
-      int e = incl - x;
+      int e = incl - x, b = binc - nb;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
-        if (tid * 8 + q < kSegRBitmaps) cpre[tid * 8 + q] = e;
+        const int k = tid * 8 + q;
+        if (k < kSegRBitmaps) cpre[k] = e;
         e += v[q];
+        if (k < nc && ccard[k] > 4096) bidx[b++] = k;
       }
-      if (tid == 63) cpre[kSegRBitmaps] = incl;
+      if (tid == 63) {
+        cpre[kSegRBitmaps] = incl;
+        nbm = binc;
+      }
     }
-    __syncthreads();
+    seg_lds_barrier();
     const int ne = cpre[kSegRBitmaps];
-    for (int e0 = 0; e0 < ne; e0 += 4 * kSegRThreads) {
-      uint32_t val[4];
-      int dst[4];
+    const int nbc = nbm;
+    // the first bitmap container's words are requested before the array elements, so both round trips overlap
+    constexpr int kWords = 2048 / kSegRThreads;
+    uint32_t bw[kWords];
+    if (nbc > 0) {
+      const uint8_t* c = cptr[bidx[0]];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < kWords; ++q) bw[q] = rd32(c + 4 * (q * kSegRThreads + tid));
+    }
+    for (int e0 = 0; e0 < ne; e0 += kPer * kSegRThreads) {
+      uint32_t val[kPer];
+      int dst[kPer];
+#pragma unroll
+      for (int q = 0; q < kPer; ++q) {
         const int e = e0 + q * kSegRThreads + tid;
         dst[q] = -1;
         if (e < ne) {
@@ -956,21 +1005,22 @@ __global__ void __launch_bounds__(kSegRThreads) pgx_roaring_program_seg(const RP
         }
       }
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < kPer; ++q)
         if (dst[q] >= 0) atomicOr(&lmask[dst[q] + (val[q] >> 5)], 1u << (val[q] & 31u));
     }
-    for (int k = 0; k < nc; ++k) {  // bitmap containers: all words in flight, then the ORs
-      if (ccard[k] <= 4096) continue;
-      const uint8_t* c = cptr[k];
+    for (int i = 0; i < nbc; ++i) {  // bitmap containers: all words in flight, then the ORs
+      const int k = bidx[i];
+      if (i > 0) {
+        const uint8_t* c = cptr[k];
+#pragma unroll
+        for (int q = 0; q < kWords; ++q) bw[q] = rd32(c + 4 * (q * kSegRThreads + tid));
+      }
       uint32_t* m = lmask + cleaf[k] * 2048;
-      uint32_t x[2048 / kSegRThreads];
 #pragma unroll
-      for (int q = 0; q < 2048 / kSegRThreads; ++q) x[q] = rd32(c + 4 * (q * kSegRThreads + tid));
-#pragma unroll
-      for (int q = 0; q < 2048 / kSegRThreads; ++q)
-        if (x[q]) atomicOr(&m[q * kSegRThreads + tid], x[q]);
+      for (int q = 0; q < kWords; ++q)
+        if (bw[q]) atomicOr(&m[q * kSegRThreads + tid], bw[q]);
     }
-    __syncthreads();
+    seg_lds_barrier();
     const int64_t doc0 = static_cast<int64_t>(chunk) << 16;
     uint32_t* out = P.mask + static_cast<size_t>(chunk) * 2048;
     for (int w = tid; w < 2048; w += kSegRThreads) {
@@ -992,7 +1042,7 @@ __global__ void __launch_bounds__(kSegRThreads) pgx_roaring_program_seg(const RP
       }
       out[w] = st[0];
     }
-    __syncthreads();  // lmask is zeroed for the next chunk
+    seg_lds_barrier();  // lmask is zeroed for the next chunk
   }
 }
 
@@ -1584,8 +1634,12 @@ extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const 
   if (nprogs <= 0 || maxchunks <= 0) return hipSuccess;
   const long long blocks = static_cast<long long>(nprogs) * maxchunks;
   if (maxleaves < 0 && -maxleaves <= pgx::kRProgMaxLeaves) {  // per-segment walk (host: every program <= 512 bitmaps)
-    hipLaunchKernelGGL(pgx::pgx_roaring_program_seg, dim3(static_cast<unsigned>(nprogs)), dim3(pgx::kSegRThreads),
-                       static_cast<size_t>(-maxleaves) * 2048 * 4, stream, progs, descs, nprogs);
+    // at least ~2048 workgroups (two full rounds at 4 resident per CU on 256 CUs), at most 8 parts per segment
+    int parts = std::max(1, std::min(std::min(maxchunks, 8), (2048 + nprogs - 1) / nprogs));
+    if (const char* e = std::getenv("PGX_RPROG_PARTS")) parts = std::max(1, std::atoi(e));
+    hipLaunchKernelGGL(pgx::pgx_roaring_program_seg, dim3(static_cast<unsigned>(nprogs * parts)),
+                       dim3(pgx::kSegRThreads), static_cast<size_t>(-maxleaves) * 2048 * 4, stream, progs, descs,
+                       nprogs, parts);
     return hipGetLastError();
   }
   if (maxleaves >= 1 && maxleaves <= pgx::kRProgMaxLeaves) {

@@ -472,10 +472,12 @@ class _Query:
             self._preds = (arr, keep)
         return self._preds[0]
 
-    def bindings(self, segments: Sequence[IndexSegment]):
+    def bindings(self, segments: Sequence[IndexSegment], seg_array=None):
         """[segment][leaf] dictId-space bindings (PredicateEvaluatorProvider per segment), resolved by the library.
-        Returns (binding array, owner): keep the owner alive while the array is in use."""
-        segs = (C.c_void_p * max(1, len(segments)))(*[s.handle.value for s in segments])
+        `seg_array`: the segments' handles as a ctypes array when the caller already holds one (the Java side passes
+        its long[] as is).  Returns (binding array, owner): keep the owner alive while the array is in use."""
+        segs = seg_array if seg_array is not None else \
+            (C.c_void_p * max(1, len(segments)))(*[s.handle.value for s in segments])
         h = C.c_void_p()
         N.check(N.lib().pgx_bind_predicates(self.handle, segs, len(segments), self.predicates(), C.byref(h)))
         owner = _Bindings(h)

@@ -24,10 +24,18 @@ def main():
     arr = (C.c_void_p * len(segs))(*[s.handle.value for s in segs])
     L = N.lib()
     q = E._Query(ctx, pql.compile(wl.query))
+    for bs in os.environ.get("BREAKDOWN_BATCH", "512").split(","):
+        os.environ["PGX_BATCH_SEGS"] = bs
+        run(ctx, q, segs, arr, L, nseg, steps, bs)
+    data.free()
+    ctx.close()
+
+
+def run(ctx, q, segs, arr, L, nseg, steps, bs):
     parts = {"bind": 0.0, "execute": 0.0, "trim": 0.0, "release": 0.0}
     for i in range(steps + 3):
         t0 = time.perf_counter()
-        binds, _own = q.bindings(segs)
+        binds, _own = q.bindings(segs, arr)
         t1 = time.perf_counter()
         r = C.c_void_p()
         opts = N.ExecOpts(0, None, 0, 0)
@@ -44,11 +52,9 @@ def main():
     binds, keep = q.bindings(segs)
     tot, kern = C.c_double(), C.c_double()
     N.check(L.pgx_execute_timed(ctx.handle, q.handle, arr, len(segs), binds, 10, C.byref(tot), C.byref(kern), None))
-    print(json.dumps({"segments": nseg, "step_parts_ms": {k: round(v, 3) for k, v in parts.items()},
+    print(json.dumps({"segments": nseg, "batch_segs": bs, "step_parts_ms": {k: round(v, 3) for k, v in parts.items()},
                       "step_ms": round(sum(parts.values()), 3), "timed_total_ms": round(tot.value, 3),
                       "timed_kernel_ms": round(kern.value, 3)}), flush=True)
-    data.free()
-    ctx.close()
 
 
 if __name__ == "__main__":

@@ -33,6 +33,8 @@ def main():
     variants = [("sep", {"PGX_RCHUNK": "0", "PGX_COMPACT": "0"}), ("sep+compact", {"PGX_RCHUNK": "0", "PGX_COMPACT": "1"}),
                 ("rchunk", {"PGX_RCHUNK": "1", "PGX_COMPACT": "0"}),
                 ("rchunk+compact", {"PGX_RCHUNK": "1", "PGX_COMPACT": "1"})]
+    if os.environ.get("VARIANTS_JSON"):  # [[name, {env}], ...]
+        variants = [tuple(v) for v in json.loads(os.environ["VARIANTS_JSON"])]
     for qn, text in queries.items():
         q = E._Query(ctx, pql.compile(text))
         binds, keep = q.bindings(segs)
