@@ -3214,8 +3214,15 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   const size_t L = q.leaf_col.size();
   std::vector<GlobalDict> full;
   for (const auto& g : q.group_cols) full.push_back(build_global_dict(segs, n, g));
-  const int nb = (n + bs - 1) / bs;
-  bs = (n + nb - 1) / nb;  // even batches
+  // batch 0 is a quarter batch: the GPU idles until it is planned; the rest split evenly
+  std::vector<int> start{0};
+  int first = bs / 4;
+  if (const char* e = std::getenv("PGX_BATCH_FIRST")) first = std::atoi(e);
+  first = std::max(1, std::min(first, bs));
+  start.push_back(first);
+  const int rest = (n - first + bs - 1) / bs;
+  for (int b = 1; b <= rest; ++b) start.push_back(first + int(int64_t(n - first) * b / rest));
+  const int nb = int(start.size()) - 1;
   std::vector<std::unique_ptr<ExecPlan>> plans;
   std::vector<std::unique_ptr<ExecBuffers>> bufs;
   // Two streams: each batch's argument arena and bitmap programs go on the side stream, and the query stream waits
@@ -3247,7 +3254,7 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   }
   int64_t host_entries = 0, total_raw = 0;
   for (int b = 0; b < nb; ++b) {
-    const int s0 = b * bs, cnt = std::min(bs, n - s0);
+    const int s0 = start[b], cnt = start[b + 1] - s0;
     Domain d;
     d.g = &full;
     d.index.resize(cnt);
