@@ -43,6 +43,8 @@ extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64
                                          unsigned long long* counter, int64_t* out_slot,
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
+extern "C" hipError_t pgx_launch_roaring_program_wave(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
+                                                      int maxchunks, int nslots, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
                                                  int maxchunks, int maxleaves, hipStream_t stream);
 extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
@@ -2197,10 +2199,53 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 
 // Bitmap inverted-index leaves: one mask per (segment, leaf) (pgx_roaring_expand), or one mask per (segment, bitmap
 // program) with the sub-tree's AND / OR / NOT applied in the same pass (pgx_roaring_program).
+// Mask slots the wave-per-chunk kernel (pgx_roaring_program_wave) needs for one program: a leaf directly followed by
+// OR whose left operand is still a pure OR of leaves shares that operand's slot; every other leaf takes a new one.
+int rprog_slots(const RProg& r) {
+  std::vector<bool> pure;  // the operand stack's "pure OR of leaves" flags
+  int ns = 0;
+  for (int i = 0; i < r.nops; ++i) {
+    const int op = r.op[i];
+    if (op == RP_LEAF) {
+      const bool fuse = i + 1 < r.nops && r.op[i + 1] == RP_OR && !pure.empty() && pure.back();
+      if (fuse) {
+        ++i;
+      } else {
+        pure.push_back(true);
+        ++ns;
+      }
+    } else if (op == RP_NOT) {
+      if (!pure.empty()) pure.back() = false;
+    } else if (pure.size() >= 2) {
+      pure.pop_back();
+      pure.back() = false;
+    }
+  }
+  return ns;
+}
+
 void launch_bitmaps(ExecPlan& P, hipStream_t st) {
   if (P.rchunk) return;  // the query kernels evaluate the bitmap programs per chunk themselves
   if (P.rprog_on) {
     const int np = int(P.rprogs.size());
+    // wave-per-chunk kernel when every program has <= 64 bitmaps (one lane each) and <= 3 mask slots
+    bool wave = true;
+    int nslots = 1;
+    if (const char* e = std::getenv("PGX_RPROG_WAVE")) wave = e[0] == '1';
+    for (size_t i = 0; i < P.rprogs.size() && wave; ++i) {
+      const RProg& r = P.rprogs[i];
+      int nb = 0;
+      for (int k = 0; k < r.nops; ++k)
+        if (r.op[k] == RP_LEAF && r.arg[k] >= 0) nb += P.roar[r.arg[k]].nb;
+      const int ns = rprog_slots(r);
+      if (nb > 64 || ns > 3) wave = false;
+      nslots = std::max(nslots, ns);
+    }
+    if (wave) {
+      hip_check(pgx_launch_roaring_program_wave(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, nslots, st),
+                "bitmap program launch");
+      return;
+    }
     int maxleaves = 0;  // leaf masks the wide kernel keeps in LDS (PGX_RPROG_NARROW=1: the stack kernel)
     for (const auto& dp : P.dm_progs) {
       int nl = 0;

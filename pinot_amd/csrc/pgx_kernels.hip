@@ -1046,6 +1046,232 @@ __global__ void __launch_bounds__(kSegRThreads, 8) pgx_roaring_program_seg(const
   }
 }
 
+// Wave-per-chunk form of the bitmap programs: every wavefront walks its own range of one segment's chunks with its own
+// LDS masks, and the workgroup never synchronises (the workgroup kernel above spends most of a chunk waiting at five
+// barriers for its slowest wave).  Lane b owns bitmap b of the program (<= 64 bitmaps) and its container cursor.  Leaves
+// share mask "slots": a leaf directly followed by OR, whose left operand is still an untouched OR of leaves, is ORed
+// into that operand's slot (C5's (f1 IN .. OR f2 = 7) AND NOT f3 = 3 needs two slots), so a wave holds NS x 8 KiB.
+// The postfix program is then evaluated over the slots and the chunk's mask written.  The slot plan is a walk of the
+// program with a 4-bit-per-entry stack in one 64-bit word (slot in bits 0-2, "pure OR of leaves" in bit 3); the host
+// applies the same rule (rprog_slots) to pick NS.
+#ifndef PGX_WAVE_ELEMS
+#define PGX_WAVE_ELEMS 8  // array elements per lane in flight (measured: 8 beat 32 with per-element searches)
+#endif
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int NS, int WPB>
+__global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg* __restrict__ progs,
+                                                                    const RDesc* __restrict__ descs, int nprogs,
+                                                                    int parts) {
+  extern __shared__ uint32_t wmask[];  // [wave][NS][2048]
+  __shared__ int wpre[WPB][65];
+  __shared__ const uint8_t* wptr[WPB][64];
+  __shared__ int wslot[WPB][64];
+  const int lane = static_cast<int>(threadIdx.x) & 63, wv = static_cast<int>(threadIdx.x) >> 6;
+  const int gw = static_cast<int>(blockIdx.x) * WPB + wv;
+  const int pi = gw / parts;
+  if (pi >= nprogs) return;  // per wave: nothing below synchronises the workgroup
+  const RProg& P = progs[pi];
+  const int per = (P.nchunks + parts - 1) / parts;
+  const int c0 = (gw % parts) * per;
+  const int c1 = min(P.nchunks, c0 + per);
+  if (c0 >= c1) return;
+  uint32_t* sm = wmask + wv * NS * 2048;
+  int* pre = wpre[wv];
+  const uint8_t** ptrs = wptr[wv];
+  int* slots = wslot[wv];
+  // slot plan: this lane's bitmap, its leaf's slot
+  int my_desc = -1, my_first = 0, my_slot = 0;
+  {
+    uint64_t stk = 0;
+    int ns = 0, tot = 0;
+    for (int i = 0; i < P.nops; ++i) {
+      const int op = P.op[i];
+      if (op == RP_LEAF) {
+        const int a = P.arg[i];
+        const int nb = a >= 0 ? descs[a].nb : 0;
+        const bool fuse = i + 1 < P.nops && P.op[i + 1] == RP_OR && (stk & 8u);
+        const int slot = fuse ? static_cast<int>(stk & 7u) : ns;
+        if (!fuse) {
+          stk = (stk << 4) | 8u | static_cast<uint64_t>(ns);
+          ++ns;
+        }
+        if (lane >= tot && lane < tot + nb) {
+          my_desc = a;
+          my_first = tot;
+          my_slot = slot;
+        }
+        tot += nb;
+        if (fuse) ++i;  // the OR is done by the expansion itself
+      } else if (op == RP_NOT) {
+        stk &= ~uint64_t(8);
+      } else {
+        stk >>= 4;  // drop the right operand; the left one holds the result, no longer a pure OR of leaves
+        stk &= ~uint64_t(8);
+      }
+    }
+  }
+  const uint8_t* base = nullptr;
+  int n = 0, cur = 0, key = 1 << 30, card = 0;
+  uint32_t off = 0;
+  if (my_desc >= 0) {
+    const RDesc& D = descs[my_desc];
+    base = D.inv + D.offs[lane - my_first];
+    n = static_cast<int>(rd32(base + 4));
+    if (c0 > 0 && n > 0) {
+      if (n > c0 && static_cast<int>(rd16(base + 8 + 4 * c0)) == c0) {
+        cur = c0;
+      } else {
+        int lo = 0, hi = n;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (static_cast<int>(rd16(base + 8 + 4 * mid)) < c0) lo = mid + 1; else hi = mid;
+        }
+        cur = lo;
+      }
+    }
+    if (cur < n) {
+      key = static_cast<int>(rd16(base + 8 + 4 * cur));
+      card = static_cast<int>(rd16(base + 8 + 4 * cur + 2)) + 1;
+      off = rd32(base + 8 + 4 * n + 4 * cur);
+    }
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+    for (int j = 0; j < 32; ++j) sm[s * 2048 + j * 64 + lane] = 0u;
+  for (int chunk = c0; chunk < c1; ++chunk) {
+    const bool act = key == chunk;
+    const bool arr = act && card <= 4096;
+    const int v = arr ? card : 0;
+    int incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    const int total = __shfl(incl, 63, 64);
+    pre[lane] = incl - v;
+    if (lane == 63) pre[64] = incl;
+    ptrs[lane] = act ? base + off : nullptr;
+    slots[lane] = my_slot;
+    uint64_t bm = __ballot(act && card > 4096);
+    if (act) {  // advance the cursor; the next container's fields are consumed at a later chunk
+      ++cur;
+      if (cur < n) {
+        key = static_cast<int>(rd16(base + 8 + 4 * cur));
+        card = static_cast<int>(rd16(base + 8 + 4 * cur + 2)) + 1;
+        off = rd32(base + 8 + 4 * n + 4 * cur);
+      } else {
+        key = 1 << 30;
+      }
+    }
+    wave_lds_sync();
+    // array containers: element e of the chunk's concatenated containers, container k with pre[k] <= e < pre[k + 1]
+    if (total > 0) {
+      // lane's first element: its container by one search over pre[]; later elements (64 apart) advance from there
+      // (containers hold ~64+ elements, so about one step each).  B elements per lane in flight.
+      int k = 0;
+#pragma unroll
+      for (int step = 32; step > 0; step >>= 1)
+        if (pre[k + step] <= lane) k += step;  // largest k <= 63 with pre[k] <= lane
+      int kend = pre[k + 1], kbeg = pre[k];
+      const uint8_t* kp = ptrs[k];
+      int ks = slots[k];
+      constexpr int B = PGX_WAVE_ELEMS;
+      for (int e0 = lane; e0 < total; e0 += 64 * B) {
+        uint32_t val[B];
+        int dst[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const int e = e0 + 64 * q;
+          dst[q] = -1;
+          if (e < total) {
+            while (kend <= e) {
+              ++k;
+              kbeg = kend;
+              kend = pre[k + 1];
+              kp = ptrs[k];
+              ks = slots[k];
+            }
+            val[q] = rd16(kp + 2 * (e - kbeg));
+            dst[q] = ks * 2048;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+          if (dst[q] >= 0) atomicOr(&sm[dst[q] + (val[q] >> 5)], 1u << (val[q] & 31u));
+      }
+    }
+    // bitmap containers: 32 words per lane, all in flight, then ORed into the leaf's slot
+    while (bm) {
+      const int src = __builtin_ctzll(bm);
+      bm &= bm - 1;
+      const uint8_t* c = ptrs[src];
+      uint32_t* m = sm + slots[src] * 2048;
+      uint32_t x[32];
+      if ((reinterpret_cast<uintptr_t>(c) & 3u) == 0) {
+        const PGX_GLOBAL uint32_t* c32 = (const PGX_GLOBAL uint32_t*)(c);
+#pragma unroll
+        for (int j = 0; j < 32; ++j) x[j] = c32[j * 64 + lane];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) x[j] = rd32(c + 4 * (j * 64 + lane));
+      }
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if (x[j]) atomicOr(&m[j * 64 + lane], x[j]);
+    }
+    wave_lds_sync();
+    // the program over the slots (same walk as the plan), word j * 64 + lane; result written, slots cleared
+    const int64_t doc0 = static_cast<int64_t>(chunk) << 16;
+    uint32_t* out = P.mask + static_cast<size_t>(chunk) * 2048;
+    uint64_t stk = 0;
+    int ns = 0;
+    for (int i = 0; i < P.nops; ++i) {
+      const int op = P.op[i];
+      if (op == RP_LEAF) {
+        const bool fuse = i + 1 < P.nops && P.op[i + 1] == RP_OR && (stk & 8u);
+        if (!fuse) {
+          stk = (stk << 4) | 8u | static_cast<uint64_t>(ns);
+          ++ns;
+        } else {
+          ++i;
+        }
+      } else if (op == RP_NOT) {
+        uint32_t* a = sm + static_cast<int>(stk & 7u) * 2048;
+        for (int j = 0; j < 32; ++j) {
+          const int w = j * 64 + lane;
+          const int64_t d = doc0 + 32 * w;
+          const uint32_t keep =
+              d >= P.num_docs ? 0u : (d + 32 > P.num_docs ? (1u << (P.num_docs - d)) - 1u : 0xFFFFFFFFu);
+          a[w] = ~a[w] & keep;
+        }
+        stk &= ~uint64_t(8);
+      } else {
+        const uint32_t* b = sm + static_cast<int>(stk & 7u) * 2048;
+        stk >>= 4;
+        uint32_t* a = sm + static_cast<int>(stk & 7u) * 2048;
+        if (op == RP_AND) {
+          for (int j = 0; j < 32; ++j) a[j * 64 + lane] &= b[j * 64 + lane];
+        } else {
+          for (int j = 0; j < 32; ++j) a[j * 64 + lane] |= b[j * 64 + lane];
+        }
+        stk &= ~uint64_t(8);
+      }
+    }
+    const uint32_t* r = sm + static_cast<int>(stk & 7u) * 2048;
+    for (int j = 0; j < 32; ++j) out[j * 64 + lane] = r[j * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+      for (int j = 0; j < 32; ++j) sm[s * 2048 + j * 64 + lane] = 0u;
+    wave_lds_sync();
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Multi-value columns.  One thread owns 32 consecutive docs (one mask word); their values are consecutive in the raw
 // section, so neighbouring threads read neighbouring bytes.  A value is cut out of the big-endian bit stream with one
@@ -1626,6 +1852,24 @@ extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const u
   if (nsegs > 0)
     hipLaunchKernelGGL(pgx::pgx_fsm_compose, dim3(nsegs), dim3(256), 0, stream, segs, S, T, cnt, stv, pcount, pstate,
                        stats);
+  return hipGetLastError();
+}
+
+// Wave-per-chunk bitmap programs (host: every program <= 64 bitmaps and <= 3 slots).
+extern "C" hipError_t pgx_launch_roaring_program_wave(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
+                                                      int maxchunks, int nslots, hipStream_t stream) {
+  if (nprogs <= 0 || maxchunks <= 0) return hipSuccess;
+  // ~8192 waves (four rounds of 256 CUs x 8 resident), at most one per chunk
+  int parts = std::max(1, std::min(maxchunks, (8192 + nprogs - 1) / nprogs));
+  if (const char* e = std::getenv("PGX_RPROG_PARTS")) parts = std::max(1, std::atoi(e));
+  const long long waves = static_cast<long long>(nprogs) * parts;
+#define PGX_WAVE_LAUNCH(NS, WPB)                                                                                   \
+  hipLaunchKernelGGL((pgx::pgx_roaring_program_wave<NS, WPB>), dim3(static_cast<unsigned>((waves + WPB - 1) / WPB)), \
+                     dim3(64 * WPB), static_cast<size_t>(NS) * WPB * 2048 * 4, stream, progs, descs, nprogs, parts)
+  if (nslots <= 1) PGX_WAVE_LAUNCH(1, 4);
+  else if (nslots == 2) PGX_WAVE_LAUNCH(2, 2);
+  else PGX_WAVE_LAUNCH(3, 2);
+#undef PGX_WAVE_LAUNCH
   return hipGetLastError();
 }
 
