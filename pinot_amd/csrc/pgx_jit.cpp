@@ -224,6 +224,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ln("__syncthreads();");
   }
   e.ln("u64 st_docs = 0, st_ent = 0;");
+  // value images already in LDS (segments sharing one dictionary share one image: not restaged per segment)
+  for (int c = 0; c < ncols; ++c)
+    if (s.cols[c].img != IMG_NONE) e.ln("const void* imgp", c, " = nullptr;");
   e.ln("int seg = pgx_find_seg(A.segs, A.num_segs, tb);");
   e.ln("long long t = tb;");
   e.ln("while (t < te) {");
@@ -241,9 +244,17 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   (void)any_img;
   auto emit_images = [&]() {
     if (!has_img) return;
+    // uniform: every thread reads the same segment descriptor
+    std::string same;
+    for (int c = 0; c < ncols; ++c)
+      if (s.cols[c].img != IMG_NONE) same += std::string(same.empty() ? "" : " && ") + "S->img[" + std::to_string(c) +
+                                             "] == imgp" + std::to_string(c);
+    e.ln("if (!(", same, ")) {");
+    e.ind++;
     e.ln("pgx_lds_barrier();");
     for (int c = 0; c < ncols; ++c) {
       if (s.cols[c].img == IMG_NONE) continue;
+      e.ln("imgp", c, " = S->img[", c, "];");
       e.ln("{");
       e.ind++;
       e.ln("const PGX_G pgx_u32x4* __restrict__ src = (const PGX_G pgx_u32x4*)S->img[", c, "];");
@@ -260,6 +271,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("}");
     }
     e.ln("pgx_lds_barrier();");
+    e.ind--;
+    e.ln("}");
   };
   // per-segment pointers and leaf parameters
   for (int c = 0; c < ncols; ++c)
