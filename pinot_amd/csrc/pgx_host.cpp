@@ -1633,6 +1633,8 @@ void prof_mark(const char* what) {
   if (g_prof_mark) g_prof_mark(what);
 }
 
+void canon_rprog(std::vector<int>& op, std::vector<int>& arg);
+
 void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                 uint32_t xflags, ExecPlan& P, const Domain* dom = nullptr) {
   if (n < 1) fail(PGX_ERR_INVALID_ARG, "no segments");
@@ -1829,6 +1831,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       emit_fused(root, F, int(L), pop, parg, true, host_scan_leaves);
       P.rprog_on = true;
       P.dm_progs = F.progs;
+      for (auto& p : P.dm_progs) canon_rprog(p.op, p.arg);
     } else {
       emit(root, pop, parg, true, false, host_scan_leaves);
     }
@@ -2199,17 +2202,66 @@ size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 
 // Bitmap inverted-index leaves: one mask per (segment, leaf) (pgx_roaring_expand), or one mask per (segment, bitmap
 // program) with the sub-tree's AND / OR / NOT applied in the same pass (pgx_roaring_program).
-// Mask slots the wave-per-chunk kernel (pgx_roaring_program_wave) needs for one program: a leaf directly followed by
-// OR whose left operand is still a pure OR of leaves shares that operand's slot; every other leaf takes a new one.
+// Bitmap programs are pure mask algebra (the statistics come from the filter tree, not from here), so AND's operands
+// commute: an AND whose left operand is NOT(leaf) gets it as its right operand instead, which turns
+// "NOT c, (a OR b), AND" into "(a OR b), c, NOT, AND": the form the wave kernel folds into one mask slot (AND-NOT).
+void canon_rprog(std::vector<int>& op, std::vector<int>& arg) {
+  struct Node { int op, arg, l, r; };
+  std::vector<Node> nodes;
+  std::vector<int> st;
+  for (size_t i = 0; i < op.size(); ++i) {
+    Node nd{op[i], arg[i], -1, -1};
+    if (op[i] == RP_NOT) {
+      if (st.empty()) return;  // malformed: leave as is
+      nd.l = st.back();
+      st.pop_back();
+    } else if (op[i] != RP_LEAF) {
+      if (st.size() < 2) return;
+      nd.r = st.back();
+      st.pop_back();
+      nd.l = st.back();
+      st.pop_back();
+    }
+    nodes.push_back(nd);
+    st.push_back(int(nodes.size()) - 1);
+  }
+  if (st.size() != 1) return;
+  auto neg_leaf = [&](int x) { return nodes[x].op == RP_NOT && nodes[nodes[x].l].op == RP_LEAF; };
+  std::vector<int> o2, a2;
+  std::function<void(int)> out = [&](int x) {
+    const Node& nd = nodes[x];
+    if (nd.op == RP_NOT) {
+      out(nd.l);
+    } else if (nd.op != RP_LEAF) {
+      const bool swap = nd.op == RP_AND && neg_leaf(nd.l) && !neg_leaf(nd.r);
+      out(swap ? nd.r : nd.l);
+      out(swap ? nd.l : nd.r);
+    }
+    o2.push_back(nd.op);
+    a2.push_back(nd.arg);
+  };
+  out(st[0]);
+  op.swap(o2);
+  arg.swap(a2);
+}
+
+// Mask slots the wave-per-chunk kernel (pgx_roaring_program_wave) needs for one program.  While the top operand is
+// "pure" (an OR of leaves, nothing applied yet), a leaf directly followed by OR is ORed into its slot, and a leaf
+// directly followed by NOT, AND is cleared out of it (which ends its purity); every other leaf takes a new slot.
 int rprog_slots(const RProg& r) {
   std::vector<bool> pure;  // the operand stack's "pure OR of leaves" flags
   int ns = 0;
   for (int i = 0; i < r.nops; ++i) {
     const int op = r.op[i];
     if (op == RP_LEAF) {
-      const bool fuse = i + 1 < r.nops && r.op[i + 1] == RP_OR && !pure.empty() && pure.back();
-      if (fuse) {
+      const bool top = !pure.empty() && pure.back();
+      const bool f_or = top && i + 1 < r.nops && r.op[i + 1] == RP_OR;
+      const bool f_andnot = top && !f_or && i + 2 < r.nops && r.op[i + 1] == RP_NOT && r.op[i + 2] == RP_AND;
+      if (f_or) {
         ++i;
+      } else if (f_andnot) {
+        pure.back() = false;
+        i += 2;
       } else {
         pure.push_back(true);
         ++ns;

@@ -1048,12 +1048,14 @@ __global__ void __launch_bounds__(kSegRThreads, 8) pgx_roaring_program_seg(const
 
 // Wave-per-chunk form of the bitmap programs: every wavefront walks its own range of one segment's chunks with its own
 // LDS masks, and the workgroup never synchronises (the workgroup kernel above spends most of a chunk waiting at five
-// barriers for its slowest wave).  Lane b owns bitmap b of the program (<= 64 bitmaps) and its container cursor.  Leaves
-// share mask "slots": a leaf directly followed by OR, whose left operand is still an untouched OR of leaves, is ORed
-// into that operand's slot (C5's (f1 IN .. OR f2 = 7) AND NOT f3 = 3 needs two slots), so a wave holds NS x 8 KiB.
-// The postfix program is then evaluated over the slots and the chunk's mask written.  The slot plan is a walk of the
-// program with a 4-bit-per-entry stack in one 64-bit word (slot in bits 0-2, "pure OR of leaves" in bit 3); the host
-// applies the same rule (rprog_slots) to pick NS.
+// barriers for its slowest wave).  Lane b owns bitmap b of the program (<= 64 bitmaps) and its container cursor.
+// Leaves share mask "slots" while the slot's operand is still "pure" (an OR of leaves, nothing applied to it yet):
+//   * a leaf directly followed by OR is ORed into the pure top operand's slot (phase 0);
+//   * a leaf directly followed by NOT, AND is cleared out of the pure top operand's slot (phase 1: AND-NOT, after
+//     every phase-0 container of the chunk), which leaves the slot impure.
+// C5's (f1 IN .. OR f2 = 7) AND NOT f3 = 3 thus needs ONE 8 KiB slot per wave.  The rest of the postfix program is
+// evaluated over the slots and the chunk's mask written.  The plan is a walk of the program with a 4-bit-per-entry
+// stack in one 64-bit word (slot in bits 0-2, "pure" in bit 3); the host applies the same rule (rprog_slots).
 #ifndef PGX_WAVE_ELEMS
 #define PGX_WAVE_ELEMS 8  // array elements per lane in flight (measured: 8 beat 32 with per-element searches)
 #endif
@@ -1063,10 +1065,18 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int NS, int WPB>
-__global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg* __restrict__ progs,
-                                                                    const RDesc* __restrict__ descs, int nprogs,
-                                                                    int parts) {
+// Fusion of the leaf at op i into the top operand: 0 none, 1 OR (skips op i + 1), 2 AND-NOT (skips ops i + 1, i + 2).
+__device__ __forceinline__ int rprog_fusion(const RProg& P, int i, uint64_t stk) {
+  if (!(stk & 8u)) return 0;
+  if (i + 1 < P.nops && P.op[i + 1] == RP_OR) return 1;
+  if (i + 2 < P.nops && P.op[i + 1] == RP_NOT && P.op[i + 2] == RP_AND) return 2;
+  return 0;
+}
+
+template <int NS, int WPB, int MINW>
+__global__ void __launch_bounds__(64 * WPB, MINW) pgx_roaring_program_wave(const RProg* __restrict__ progs,
+                                                                          const RDesc* __restrict__ descs, int nprogs,
+                                                                          int parts) {
   extern __shared__ uint32_t wmask[];  // [wave][NS][2048]
   __shared__ int wpre[WPB][65];
   __shared__ const uint8_t* wptr[WPB][64];
@@ -1084,8 +1094,9 @@ __global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg
   int* pre = wpre[wv];
   const uint8_t** ptrs = wptr[wv];
   int* slots = wslot[wv];
-  // slot plan: this lane's bitmap, its leaf's slot
-  int my_desc = -1, my_first = 0, my_slot = 0;
+  // slot plan: this lane's bitmap, its leaf's slot and phase
+  int my_desc = -1, my_first = 0, my_slot = 0, my_phase = 0;
+  bool any_andnot = false;
   {
     uint64_t stk = 0;
     int ns = 0, tot = 0;
@@ -1094,9 +1105,9 @@ __global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg
       if (op == RP_LEAF) {
         const int a = P.arg[i];
         const int nb = a >= 0 ? descs[a].nb : 0;
-        const bool fuse = i + 1 < P.nops && P.op[i + 1] == RP_OR && (stk & 8u);
-        const int slot = fuse ? static_cast<int>(stk & 7u) : ns;
-        if (!fuse) {
+        const int f = rprog_fusion(P, i, stk);
+        const int slot = f ? static_cast<int>(stk & 7u) : ns;
+        if (!f) {
           stk = (stk << 4) | 8u | static_cast<uint64_t>(ns);
           ++ns;
         }
@@ -1104,13 +1115,18 @@ __global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg
           my_desc = a;
           my_first = tot;
           my_slot = slot;
+          my_phase = f == 2 ? 1 : 0;
         }
         tot += nb;
-        if (fuse) ++i;  // the OR is done by the expansion itself
+        if (f == 2) {
+          stk &= ~uint64_t(8);
+          any_andnot = true;
+        }
+        i += f;  // the fused OR / NOT, AND are done by the expansion itself
       } else if (op == RP_NOT) {
         stk &= ~uint64_t(8);
       } else {
-        stk >>= 4;  // drop the right operand; the left one holds the result, no longer a pure OR of leaves
+        stk >>= 4;  // drop the right operand; the left one holds the result, no longer pure
         stk &= ~uint64_t(8);
       }
     }
@@ -1145,21 +1161,9 @@ __global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg
     for (int j = 0; j < 32; ++j) sm[s * 2048 + j * 64 + lane] = 0u;
   for (int chunk = c0; chunk < c1; ++chunk) {
     const bool act = key == chunk;
-    const bool arr = act && card <= 4096;
-    const int v = arr ? card : 0;
-    int incl = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const int y = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += y;
-    }
-    const int total = __shfl(incl, 63, 64);
-    pre[lane] = incl - v;
-    if (lane == 63) pre[64] = incl;
-    ptrs[lane] = act ? base + off : nullptr;
-    slots[lane] = my_slot;
-    uint64_t bm = __ballot(act && card > 4096);
-    if (act) {  // advance the cursor; the next container's fields are consumed at a later chunk
+    const uint8_t* cptr = base + off;
+    const int ccard = card;
+    if (act) {  // advance the cursor now; the next container's fields are consumed at a later chunk
       ++cur;
       if (cur < n) {
         key = static_cast<int>(rd16(base + 8 + 4 * cur));
@@ -1169,64 +1173,90 @@ __global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg
         key = 1 << 30;
       }
     }
-    wave_lds_sync();
-    // array containers: element e of the chunk's concatenated containers, container k with pre[k] <= e < pre[k + 1]
-    if (total > 0) {
-      // lane's first element: its container by one search over pre[]; later elements (64 apart) advance from there
-      // (containers hold ~64+ elements, so about one step each).  B elements per lane in flight.
-      int k = 0;
+    for (int ph = 0; ph < (any_andnot ? 2 : 1); ++ph) {
+      const bool mine = act && my_phase == ph;
+      const bool arr = mine && ccard <= 4096;
+      const int v = arr ? ccard : 0;
+      int incl = v;
 #pragma unroll
-      for (int step = 32; step > 0; step >>= 1)
-        if (pre[k + step] <= lane) k += step;  // largest k <= 63 with pre[k] <= lane
-      int kend = pre[k + 1], kbeg = pre[k];
-      const uint8_t* kp = ptrs[k];
-      int ks = slots[k];
-      constexpr int B = PGX_WAVE_ELEMS;
-      for (int e0 = lane; e0 < total; e0 += 64 * B) {
-        uint32_t val[B];
-        int dst[B];
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      const int total = __shfl(incl, 63, 64);
+      pre[lane] = incl - v;
+      if (lane == 63) pre[64] = incl;
+      ptrs[lane] = mine ? cptr : nullptr;
+      slots[lane] = my_slot;
+      uint64_t bm = __ballot(mine && ccard > 4096);
+      wave_lds_sync();
+      // array containers: element e of the chunk's concatenated containers, container k with pre[k] <= e < pre[k + 1];
+      // the lane's first element by one search, later ones (64 apart) by stepping forward (about one step each)
+      if (total > 0) {
+        int k = 0;
 #pragma unroll
-        for (int q = 0; q < B; ++q) {
-          const int e = e0 + 64 * q;
-          dst[q] = -1;
-          if (e < total) {
-            while (kend <= e) {
-              ++k;
-              kbeg = kend;
-              kend = pre[k + 1];
-              kp = ptrs[k];
-              ks = slots[k];
+        for (int step = 32; step > 0; step >>= 1)
+          if (pre[k + step] <= lane) k += step;  // largest k <= 63 with pre[k] <= lane
+        int kend = pre[k + 1], kbeg = pre[k];
+        const uint8_t* kp = ptrs[k];
+        int ks = slots[k];
+        constexpr int B = PGX_WAVE_ELEMS;
+        for (int e0 = lane; e0 < total; e0 += 64 * B) {
+          uint32_t val[B];
+          int dst[B];
+#pragma unroll
+          for (int q = 0; q < B; ++q) {
+            const int e = e0 + 64 * q;
+            dst[q] = -1;
+            if (e < total) {
+              while (kend <= e) {
+                ++k;
+                kbeg = kend;
+                kend = pre[k + 1];
+                kp = ptrs[k];
+                ks = slots[k];
+              }
+              val[q] = rd16(kp + 2 * (e - kbeg));
+              dst[q] = ks * 2048;
             }
-            val[q] = rd16(kp + 2 * (e - kbeg));
-            dst[q] = ks * 2048;
           }
+#pragma unroll
+          for (int q = 0; q < B; ++q)
+            if (dst[q] >= 0) {
+              if (ph == 0) atomicOr(&sm[dst[q] + (val[q] >> 5)], 1u << (val[q] & 31u));
+              else atomicAnd(&sm[dst[q] + (val[q] >> 5)], ~(1u << (val[q] & 31u)));
+            }
         }
-#pragma unroll
-        for (int q = 0; q < B; ++q)
-          if (dst[q] >= 0) atomicOr(&sm[dst[q] + (val[q] >> 5)], 1u << (val[q] & 31u));
       }
-    }
-    // bitmap containers: 32 words per lane, all in flight, then ORed into the leaf's slot
-    while (bm) {
-      const int src = __builtin_ctzll(bm);
-      bm &= bm - 1;
-      const uint8_t* c = ptrs[src];
-      uint32_t* m = sm + slots[src] * 2048;
-      uint32_t x[32];
-      if ((reinterpret_cast<uintptr_t>(c) & 3u) == 0) {
-        const PGX_GLOBAL uint32_t* c32 = (const PGX_GLOBAL uint32_t*)(c);
+      // bitmap containers: 16 words per lane in flight at a time, ORed into (or cleared out of) the leaf's slot
+      while (bm) {
+        const int src = __builtin_ctzll(bm);
+        bm &= bm - 1;
+        const uint8_t* c = ptrs[src];
+        uint32_t* m = sm + slots[src] * 2048;
+        const bool al = (reinterpret_cast<uintptr_t>(c) & 3u) == 0;
+#pragma unroll 1
+        for (int h = 0; h < 2; ++h) {
+          uint32_t x[16];
+          if (al) {
+            const PGX_GLOBAL uint32_t* c32 = (const PGX_GLOBAL uint32_t*)(c);
 #pragma unroll
-        for (int j = 0; j < 32; ++j) x[j] = c32[j * 64 + lane];
-      } else {
+            for (int j = 0; j < 16; ++j) x[j] = c32[(h * 16 + j) * 64 + lane];
+          } else {
 #pragma unroll
-        for (int j = 0; j < 32; ++j) x[j] = rd32(c + 4 * (j * 64 + lane));
+            for (int j = 0; j < 16; ++j) x[j] = rd32(c + 4 * ((h * 16 + j) * 64 + lane));
+          }
+#pragma unroll
+          for (int j = 0; j < 16; ++j)
+            if (x[j]) {
+              if (ph == 0) atomicOr(&m[(h * 16 + j) * 64 + lane], x[j]);
+              else atomicAnd(&m[(h * 16 + j) * 64 + lane], ~x[j]);
+            }
+        }
       }
-#pragma unroll
-      for (int j = 0; j < 32; ++j)
-        if (x[j]) atomicOr(&m[j * 64 + lane], x[j]);
+      wave_lds_sync();
     }
-    wave_lds_sync();
-    // the program over the slots (same walk as the plan), word j * 64 + lane; result written, slots cleared
+    // the rest of the program over the slots (same walk as the plan), word j * 64 + lane; result written, slots cleared
     const int64_t doc0 = static_cast<int64_t>(chunk) << 16;
     uint32_t* out = P.mask + static_cast<size_t>(chunk) * 2048;
     uint64_t stk = 0;
@@ -1234,15 +1264,16 @@ __global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg
     for (int i = 0; i < P.nops; ++i) {
       const int op = P.op[i];
       if (op == RP_LEAF) {
-        const bool fuse = i + 1 < P.nops && P.op[i + 1] == RP_OR && (stk & 8u);
-        if (!fuse) {
+        const int f = rprog_fusion(P, i, stk);
+        if (!f) {
           stk = (stk << 4) | 8u | static_cast<uint64_t>(ns);
           ++ns;
-        } else {
-          ++i;
         }
+        if (f == 2) stk &= ~uint64_t(8);
+        i += f;
       } else if (op == RP_NOT) {
         uint32_t* a = sm + static_cast<int>(stk & 7u) * 2048;
+#pragma unroll 4
         for (int j = 0; j < 32; ++j) {
           const int w = j * 64 + lane;
           const int64_t d = doc0 + 32 * w;
@@ -1256,17 +1287,20 @@ __global__ void __launch_bounds__(64 * WPB) pgx_roaring_program_wave(const RProg
         stk >>= 4;
         uint32_t* a = sm + static_cast<int>(stk & 7u) * 2048;
         if (op == RP_AND) {
+#pragma unroll 8
           for (int j = 0; j < 32; ++j) a[j * 64 + lane] &= b[j * 64 + lane];
         } else {
+#pragma unroll 8
           for (int j = 0; j < 32; ++j) a[j * 64 + lane] |= b[j * 64 + lane];
         }
         stk &= ~uint64_t(8);
       }
     }
     const uint32_t* r = sm + static_cast<int>(stk & 7u) * 2048;
+#pragma unroll 8
     for (int j = 0; j < 32; ++j) out[j * 64 + lane] = r[j * 64 + lane];
-#pragma unroll
     for (int s = 0; s < NS; ++s)
+#pragma unroll 8
       for (int j = 0; j < 32; ++j) sm[s * 2048 + j * 64 + lane] = 0u;
     wave_lds_sync();
   }
@@ -1863,12 +1897,14 @@ extern "C" hipError_t pgx_launch_roaring_program_wave(const pgx::RProg* progs, c
   int parts = std::max(1, std::min(maxchunks, (8192 + nprogs - 1) / nprogs));
   if (const char* e = std::getenv("PGX_RPROG_PARTS")) parts = std::max(1, std::atoi(e));
   const long long waves = static_cast<long long>(nprogs) * parts;
-#define PGX_WAVE_LAUNCH(NS, WPB)                                                                                   \
-  hipLaunchKernelGGL((pgx::pgx_roaring_program_wave<NS, WPB>), dim3(static_cast<unsigned>((waves + WPB - 1) / WPB)), \
-                     dim3(64 * WPB), static_cast<size_t>(NS) * WPB * 2048 * 4, stream, progs, descs, nprogs, parts)
-  if (nslots <= 1) PGX_WAVE_LAUNCH(1, 4);
-  else if (nslots == 2) PGX_WAVE_LAUNCH(2, 2);
-  else PGX_WAVE_LAUNCH(3, 2);
+  // waves per SIMD the LDS allows (NS x 8 KiB per wave) bound the registers: 1 slot -> 4, 2 -> 2, 3 -> 1
+#define PGX_WAVE_LAUNCH(NS, WPB, MINW)                                                                             \
+  hipLaunchKernelGGL((pgx::pgx_roaring_program_wave<NS, WPB, MINW>),                                              \
+                     dim3(static_cast<unsigned>((waves + WPB - 1) / WPB)), dim3(64 * WPB),                        \
+                     static_cast<size_t>(NS) * WPB * 2048 * 4, stream, progs, descs, nprogs, parts)
+  if (nslots <= 1) PGX_WAVE_LAUNCH(1, 4, 4);
+  else if (nslots == 2) PGX_WAVE_LAUNCH(2, 2, 2);
+  else PGX_WAVE_LAUNCH(3, 2, 1);
 #undef PGX_WAVE_LAUNCH
   return hipGetLastError();
 }
