@@ -164,17 +164,16 @@ def main():
     L = N.lib()
 
     dense = False
-    agree = False
     dense_t = None
     plane_ops = []
     if req.get("group_by") and world > 1:
+        # one key space on every rank: the union of all ranks' group-column dictionaries, set once per query
+        # shape (segment metadata, like staging); dense tables then all-reduce by slot over RCCL, sparse groups merge
+        # on the device by packed key
+        multigpu.union_key_domains(q, segs)
         slots = C.c_int64()
         N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
-        # dense key space on every rank with identical dictionaries: RCCL all-reduce of the tables; else
-        # the groups merge by key VALUE (multigpu.merge_group_partials)
-        fps = multigpu.dictionary_fingerprint([[s.column(c).values for s in segs] for c in q.group_cols])
-        agree = multigpu.dense_layout_agrees(slots.value, fps, device="cuda:%d" % local)
-        dense = slots.value <= (1 << 22) and agree
+        dense = slots.value <= (1 << 22)
     if dense:
         nplanes = 1 + len(req["aggregations"])
         for p in range(nplanes):
@@ -217,13 +216,13 @@ def main():
             dev = "cuda:%d" % local
             n = C.c_int64()
             resident = L.pgx_result_device_groups(r, C.byref(n), None) == 0
-            flag = torch.tensor([int(agree and resident)], dtype=torch.int64, device=dev)
+            flag = torch.tensor([int(resident)], dtype=torch.int64, device=dev)
             torch.distributed.all_reduce(flag, op=torch.distributed.ReduceOp.MIN)
             if flag.item():  # one key space, groups in HBM: all-to-all by key hash + device merge + device trim
                 maps, _total, _st = multigpu.device_sparse_merge(ctx, q, r, segs, dev)
                 if rank == 0:
                     merged[0] = maps
-            else:  # dictionaries differ across ranks: host merge of every rank's groups by VALUE, then trimToSize
+            else:  # groups not device-resident (global hash table): host merge of every rank's groups by VALUE
                 fns = [a["fn"] for a in req["aggregations"]]
                 parts = multigpu.gather_group_partials(*E.group_partials(q, r, segs))
                 if rank == 0:

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGX_ABI_VERSION 4
+#define PGX_ABI_VERSION 5
 
 typedef enum {
   PGX_OK = 0,
@@ -155,6 +155,16 @@ typedef struct {
 #define PGX_Q_NO_STAR_TREE 0x1u /* debug option useStarTree=false (common/utils/request/RequestUtils.java:229-236) */
 
 pgx_status pgx_query_compile(pgx_ctx* ctx, const pgx_query_desc* desc, pgx_query** out);
+/* Cross-process key identity (SURVEY 8e "a host-side global dictionary per group-by column"; ABI 5): the key space of
+ * group-by column group_col becomes the caller's sorted distinct values (type PGX_INT / PGX_LONG -> ivals, PGX_FLOAT /
+ * PGX_DOUBLE -> dvals, PGX_STRING -> svals, compared bytewise) instead of the union of the executed segments'
+ * dictionaries.  Processes that set the same domains plan the same dense slots / packed keys, so their partials merge
+ * by slot (RCCL all-reduce) or by packed key (all-to-all + pgx_result_merge_groups) -- the value-keyed merge of
+ * MCombineGroupByOperator.java:166-191 without shipping strings.  Results of such a query report seg_index -1 and
+ * dict_id = the index into the domain for that column (pgx_result_group_keys / pgx_result_gather).  Every segment value
+ * must be in the domain (PGX_ERR_INVALID_ARG otherwise).  num_values 0 clears it. */
+pgx_status pgx_query_set_key_domain(pgx_query* q, int32_t group_col, int32_t type, int64_t num_values,
+                                    const int64_t* ivals, const double* dvals, const char* const* svals);
 pgx_status pgx_query_release(pgx_query* q);
 
 /* Per-(segment, leaf) predicate in dictionary-id space, as produced by the caller's PredicateEvaluator:

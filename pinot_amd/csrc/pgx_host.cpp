@@ -210,6 +210,48 @@ struct WorkerPool {
   }
 };
 
+// Persistent host threads for independent tasks (batched plans: every batch of a long segment list is planned on its own
+// thread while the submitting thread launches the batches in order).  Unlike WorkerPool (one parallel loop at a time,
+// the caller blocks), submit() returns at once.
+struct TaskTeam {
+  std::vector<std::thread> th;
+  std::mutex m;
+  std::condition_variable cv;
+  std::deque<std::function<void()>> q;
+  bool stop = false;
+  void start(int n) {
+    for (int t = 0; t < n; ++t)
+      th.emplace_back([this] {
+        for (;;) {
+          std::function<void()> f;
+          {
+            std::unique_lock<std::mutex> g(m);
+            cv.wait(g, [&] { return stop || !q.empty(); });
+            if (q.empty()) return;  // stop, nothing left
+            f = std::move(q.front());
+            q.pop_front();
+          }
+          f();  // tasks catch their own exceptions
+        }
+      });
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m);
+      q.push_back(std::move(f));
+    }
+    cv.notify_one();
+  }
+  ~TaskTeam() {
+    {
+      std::lock_guard<std::mutex> g(m);
+      stop = true;
+    }
+    cv.notify_all();
+    for (auto& t : th) t.join();
+  }
+};
+
 struct DevBuf;
 struct SharedDict;
 
@@ -222,6 +264,15 @@ struct pgx_ctx {
   std::unordered_map<uint64_t, std::weak_ptr<SharedDict>> dicts;
   WorkerPool pool;           // started lazily (first large query)
   std::once_flag pool_once;
+  TaskTeam plan_team;        // batched plans (run_batched), started lazily
+  std::once_flag plan_once;
+  void plan_submit(std::function<void()> f) {
+    std::call_once(plan_once, [this] {
+      const unsigned hc = std::thread::hardware_concurrency();
+      plan_team.start(int(std::min<unsigned>(8, hc > 2 ? hc - 2 : 1)));
+    });
+    plan_team.submit(std::move(f));
+  }
   void parallel_for(int n, const std::function<void(int)>& f) {
     std::call_once(pool_once, [this] {
       const unsigned hc = std::thread::hardware_concurrency();
@@ -741,6 +792,17 @@ void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool
 // =================================================================================================
 // Query
 // =================================================================================================
+// A caller-given key space for one group-by column (pgx_query_set_key_domain): the sorted distinct values of the column
+// over every process's segments, so that every rank plans the same dense slots / packed keys.
+struct KeyDomain {
+  bool set = false;
+  int type = PGX_INT;                 // PGX_INT / PGX_LONG -> iv, PGX_FLOAT / PGX_DOUBLE -> dv, PGX_STRING -> sv
+  std::vector<int64_t> iv;
+  std::vector<double> dv;
+  std::vector<std::string> sv;
+  int64_t size() const { return type == PGX_STRING ? int64_t(sv.size()) : (iv.empty() ? int64_t(dv.size()) : int64_t(iv.size())); }
+};
+
 struct pgx_query {
   std::vector<int> agg_fn;
   std::vector<std::string> agg_col;  // "" for COUNT(*)
@@ -750,6 +812,7 @@ struct pgx_query {
   std::vector<std::string> leaf_col;
   std::vector<int> leaf_kind;
   uint32_t flags = 0;
+  std::vector<KeyDomain> key_domain;  // [group column]
 };
 
 // =================================================================================================
@@ -938,18 +1001,30 @@ double decode_plane(int op, bool fp, unsigned long long x, int fn) {
 struct GlobalDict {
   int64_t card = 0;
   bool identity = true;
-  std::vector<std::vector<int32_t>> remap;    // [seg][local] -> global
-  std::vector<int32_t> rep_seg, rep_id;        // [global] -> a (segment, local id) holding the value
+  // [seg][local] -> global; segments with byte-identical dictionaries share one table (and one blob copy)
+  std::vector<std::shared_ptr<const std::vector<int32_t>>> remap;
+  // [global] -> a (segment, local id) holding the value; rep_seg -1: the caller's key domain, rep_id = domain index
+  std::vector<int32_t> rep_seg, rep_id;
 };
 
 GlobalDict build_global_dict(pgx_segment* const* segs, int n, const std::string& col) {
   GlobalDict g;
   const StagedColumn& c0 = segs[0]->col(col);
-  bool same = true;
-  for (int s = 1; s < n && same; ++s) {
-    const StagedColumn& c = segs[s]->col(col);
-    same = c.dict_hash == c0.dict_hash && c.card == c0.card && c.data_type == c0.data_type;
-  }
+  // every segment holds the same dictionary?  (long lists: chunks on the context's pool -- the loop is bound by cache
+  // misses on the segments' column records, ~45 ns per segment)
+  std::atomic<bool> same{true};
+  auto check = [&](int lo, int hi) {
+    for (int s = lo; s < hi && same.load(std::memory_order_relaxed); ++s) {
+      const StagedColumn& c = segs[s]->col(col);
+      if (!(c.dict_hash == c0.dict_hash && c.card == c0.card && c.data_type == c0.data_type)) same = false;
+    }
+  };
+  constexpr int kChunk = 256;
+  if (n >= 4 * kChunk) segs[0]->ctx->parallel_for((n + kChunk - 1) / kChunk, [&](int i) {
+      check(std::max(1, i * kChunk), std::min(n, (i + 1) * kChunk));
+    });
+  else
+    check(1, n);
   if (same) {
     g.card = c0.card;
     g.identity = true;
@@ -960,13 +1035,19 @@ GlobalDict build_global_dict(pgx_segment* const* segs, int n, const std::string&
   }
   g.identity = false;
   g.remap.resize(n);
-  // k-way merge of the sorted dictionaries by value.
+  // k-way merge of the sorted dictionaries by value, one representative segment per distinct dictionary
   struct Item { int seg; int id; };
   std::vector<Item> all;
+  std::map<std::pair<uint64_t, int>, int> first;  // (dict hash, card) -> representative segment
+  std::vector<int> rep(n);
+  std::vector<std::vector<int32_t>> tabs(n);
   for (int s = 0; s < n; ++s) {
     const StagedColumn& c = segs[s]->col(col);
     if (c.data_type != c0.data_type) fail(PGX_ERR_INVALID_ARG, "column " + col + " has different types");
-    g.remap[s].resize(c.card);
+    auto it = first.emplace(std::make_pair(c.dict_hash, c.card), s).first;
+    rep[s] = it->second;
+    if (rep[s] != s) continue;
+    tabs[s].resize(c.card);
     for (int i = 0; i < c.card; ++i) all.push_back({s, i});
   }
   auto less = [&](const Item& a, const Item& b) {
@@ -984,10 +1065,65 @@ GlobalDict build_global_dict(pgx_segment* const* segs, int n, const std::string&
       g.rep_seg.push_back(all[i].seg);
       g.rep_id.push_back(all[i].id);
     }
-    g.remap[all[i].seg][all[i].id] = int32_t(gid);
+    tabs[all[i].seg][all[i].id] = int32_t(gid);
+  }
+  std::vector<std::shared_ptr<const std::vector<int32_t>>> shared(n);
+  for (int s = 0; s < n; ++s) {
+    if (rep[s] == s) shared[s] = std::make_shared<const std::vector<int32_t>>(std::move(tabs[s]));
+    g.remap[s] = shared[rep[s]];
   }
   g.card = gid + 1;
   return g;
+}
+
+// Key space from the caller's domain (pgx_query_set_key_domain): each distinct segment dictionary is remapped by value
+// into the domain's sorted values; a value outside the domain is a caller error.
+GlobalDict domain_global_dict(const KeyDomain& D, pgx_segment* const* segs, int n, const std::string& col) {
+  GlobalDict g;
+  g.card = D.size();
+  g.identity = false;
+  g.remap.resize(n);
+  g.rep_seg.assign(size_t(g.card), -1);
+  g.rep_id.resize(size_t(g.card));
+  std::iota(g.rep_id.begin(), g.rep_id.end(), 0);
+  std::map<std::pair<uint64_t, int>, std::shared_ptr<const std::vector<int32_t>>> memo;
+  bool ident = true;
+  for (int s = 0; s < n; ++s) {
+    const StagedColumn& c = segs[s]->col(col);
+    const bool str = c.data_type == PGX_STRING, integral = c.data_type == PGX_INT || c.data_type == PGX_LONG;
+    if (str != (D.type == PGX_STRING) || integral != (D.type == PGX_INT || D.type == PGX_LONG))
+      fail(PGX_ERR_INVALID_ARG, "key domain type differs from column " + col);
+    auto& m = memo[std::make_pair(c.dict_hash, c.card)];
+    if (!m) {
+      std::vector<int32_t> t(c.card);
+      for (int i = 0; i < c.card; ++i) {
+        int64_t pos;
+        if (str) pos = std::lower_bound(D.sv.begin(), D.sv.end(), c.svals[i]) - D.sv.begin();
+        else if (integral) pos = std::lower_bound(D.iv.begin(), D.iv.end(), c.ivals[i]) - D.iv.begin();
+        else pos = std::lower_bound(D.dv.begin(), D.dv.end(), c.dvals[i]) - D.dv.begin();
+        const bool hit = pos < g.card && (str ? D.sv[pos] == c.svals[i]
+                                              : integral ? D.iv[pos] == c.ivals[i] : D.dv[pos] == c.dvals[i]);
+        if (!hit) fail(PGX_ERR_INVALID_ARG, "a value of column " + col + " is not in its key domain");
+        t[i] = int32_t(pos);
+        ident = ident && pos == i;
+      }
+      ident = ident && c.card == g.card;
+      m = std::make_shared<const std::vector<int32_t>>(std::move(t));
+    }
+    g.remap[s] = m;
+  }
+  if (ident) {  // every segment holds exactly the domain: no remap tables (rep_seg stays -1: keys are domain indices)
+    g.identity = true;
+    g.remap.clear();
+  }
+  return g;
+}
+
+// The key space of group-by column g: the caller's domain when one is set, else the union of the segments' dictionaries.
+GlobalDict group_dict(const pgx_query& q, pgx_segment* const* segs, int n, int g) {
+  if (size_t(g) < q.key_domain.size() && q.key_domain[g].set)
+    return domain_global_dict(q.key_domain[g], segs, n, q.group_cols[g]);
+  return build_global_dict(segs, n, q.group_cols[g]);
 }
 
 // Reference storage mode of a single segment (DefaultGroupKeyGenerator.java:167-186): 0 ARRAY_BASED, 1 LONG_MAP_BASED,
@@ -1036,6 +1172,7 @@ constexpr int kPart1N = 1 << kPart1Bits;
 constexpr int kCursorStride = 16;       // u64 words between partition cursors: one 128-B line each
 
 struct ExecPlan {
+  bool serial = false;            // planned on a planner thread: no nested parallel_for on the context's pool
   KQuery kq{};
   std::vector<KSeg> ksegs;
   std::vector<int32_t> blob32;   // ranges / remaps / bitsets, uploaded as one buffer
@@ -1115,6 +1252,7 @@ struct ExecPlan {
   std::vector<int> mv_neg;                 // [leaf] NEQ / NOT_IN
   std::vector<std::vector<int>> mv_index;  // [seg][leaf] -> index into mv_items or -1
   DevBuf mv_masks, mv_descs;
+  std::vector<MvLeaf> mv_host;             // their descriptors (host copy, sent by send_arena)
   int mv_max_words = 0;
   // selection masks for the multi-value functions (one bit per scanned row, per segment)
   bool want_selmask = false;
@@ -1686,7 +1824,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         if (segs[s]->col(q.group_cols[g]).is_mv)
           fail(PGX_ERR_UNSUPPORTED, "GROUP BY on multi-value column " + q.group_cols[g]);
       K.gcol[g] = int8_t(qslot(P, q.group_cols[g]));
-      P.gdicts.push_back(dom ? domain_dict(*dom, g, n) : build_global_dict(segs, n, q.group_cols[g]));
+      P.gdicts.push_back(dom ? domain_dict(*dom, g, n) : group_dict(q, segs, n, g));
       const int64_t gc = P.gdicts.back().card;
       if (!overflow && prod > (uint64_t(1) << 62) / uint64_t(gc)) overflow = true;
       if (!overflow) prod *= uint64_t(gc);
@@ -1875,8 +2013,20 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   P.ksegs.assign(n, KSeg{});
   P.segcols.assign(n, {});
   P.sorted_span.assign(size_t(n) * q.leaf_col.size(), 0);
+  // Per distinct (leaf, binding, cardinality) in a chunk: the leaf mode, ONE blob copy of its dictId bitset and ONE list
+  // of the dictIds whose bitmaps a bitmap leaf ORs.  Segments sharing a dictionary share their bindings
+  // (pgx_bind_predicates), so a chunk usually resolves each leaf once, whatever its segment count.
+  struct LeafMemo {
+    int8_t mode = LEAF_NONE;
+    int64_t bits_off = -1;  // chunk blob offset of the bitset copy (LEAF_SCAN_BITSET)
+    int64_t ids_off = -1;   // chunk blob offset of the dictId list (bitmap leaves), nb entries
+    int nb = 0;
+  };
+  using LeafKey = std::tuple<size_t, const uint32_t*, int32_t, int32_t, int>;
   struct ChunkOut {
     std::vector<int32_t> blob;
+    std::map<const std::vector<int32_t>*, size_t> remap_off;
+    std::map<LeafKey, LeafMemo> leaf_memo;
     std::vector<ExecPlan::Fix> fixes;
     std::vector<ExecPlan::RoarItem> roar;
     std::vector<ExecPlan::MvItem> mv;
@@ -1908,9 +2058,13 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       }
       for (int g = 0; g < K.num_gcols; ++g) {
         if (!P.gdicts[g].identity) {
-          const auto& rm = P.gdicts[g].remap[s];
-          o.fixes.push_back({size_t(s), 0, K.gcol[g], o.blob.size()});
-          o.blob.insert(o.blob.end(), rm.begin(), rm.end());
+          const std::vector<int32_t>* rm = P.gdicts[g].remap[s].get();
+          auto it = o.remap_off.find(rm);  // one blob copy per distinct dictionary in this chunk
+          if (it == o.remap_off.end()) {
+            it = o.remap_off.emplace(rm, o.blob.size()).first;
+            o.blob.insert(o.blob.end(), rm->begin(), rm->end());
+          }
+          o.fixes.push_back({size_t(s), 0, K.gcol[g], it->second});
         }
       }
       // leaves
@@ -1928,6 +2082,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           if (b.words) return (b.words[id >> 5] >> (id & 31)) & 1u;
           return id >= b.lo && id <= b.hi;
         };
+        const bool bitmap_leaf = P.use_docmask && P.leaf_phys[l] == PH_BITMAP && col.inv_dev.p;
         if (col.is_sorted) {
           // SortedInvertedIndexBasedFilterOperator (additive ranges, merged), clipped to [0, totalRawDocs-1]
           std::vector<int32_t> r;
@@ -1945,43 +2100,62 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           L.nranges = int32_t(r.size() / 2);
           o.fixes.push_back({size_t(s), 1, int(l), o.blob.size()});
           o.blob.insert(o.blob.end(), r.begin(), r.end());
-        } else if (b.words) {
-          bool any = false;
-          const int nw = (col.card + 31) / 32;
-          for (int w = 0; w < nw && !any; ++w) any = b.words[w] != 0;
-          if (!any) { L.mode = LEAF_NONE; continue; }
-          L.mode = LEAF_SCAN_BITSET;
-          o.fixes.push_back({size_t(s), 2, int(l), o.blob.size()});
-          for (int w = 0; w < nw; ++w) o.blob.push_back(int32_t(b.words[w]));
-        } else {
-          L.mode = (b.hi < b.lo) ? LEAF_NONE : LEAF_SCAN_INTERVAL;
+          continue;
         }
-        if (P.use_docmask && L.mode != LEAF_NONE && P.leaf_phys[l] == PH_BITMAP && col.inv_dev.p) {
-          // BitmapBasedFilterOperator (operator/filter/BitmapBasedFilterOperator.java:62-92): OR the roaring bitmaps
-          // of the matching dictIds; NEQ / NOT_IN OR the NON-matching ones and flip over the scanned doc range.
-          const bool neg = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
-          ExecPlan::RoarItem it{s, int(l), neg, o.blob.size(), 0, int((int64_t(seg.total_docs) + 65535) >> 16),
-                                o.mask_words, col.inv_dev.p};
-          auto take = [&](int id) {
-            o.blob.push_back(int32_t(col.inv_off[id]));
-            it.bytes += col.inv_off[id + 1] - col.inv_off[id];
-            ++it.nb;
-          };
-          if (b.words) {  // walk the set (or, negated, the clear) bits of the dictId bitset
+        const bool neg = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
+        auto mit = o.leaf_memo.find(LeafKey(l, b.words, b.lo, b.hi, col.card));
+        if (mit == o.leaf_memo.end()) {
+          LeafMemo m;
+          if (b.words) {
+            bool any = false;
             const int nw = (col.card + 31) / 32;
-            for (int w = 0; w < nw; ++w) {
-              uint32_t x = neg ? ~b.words[w] : b.words[w];
-              if (w == nw - 1 && (col.card & 31)) x &= (1u << (col.card & 31)) - 1u;
-              while (x) {
-                take(w * 32 + __builtin_ctz(x));
-                x &= x - 1u;
-              }
+            for (int w = 0; w < nw && !any; ++w) any = b.words[w] != 0;
+            if (any) {
+              m.mode = LEAF_SCAN_BITSET;
+              m.bits_off = int64_t(o.blob.size());
+              for (int w = 0; w < nw; ++w) o.blob.push_back(int32_t(b.words[w]));
             }
-          } else if (!neg) {
-            for (int id = std::max(0, b.lo); id <= std::min(b.hi, col.card - 1); ++id) take(id);
           } else {
-            for (int id = 0; id < col.card; ++id)
-              if (id < b.lo || id > b.hi) take(id);
+            m.mode = (b.hi < b.lo) ? LEAF_NONE : LEAF_SCAN_INTERVAL;
+          }
+          if (bitmap_leaf && m.mode != LEAF_NONE) {
+            // BitmapBasedFilterOperator (operator/filter/BitmapBasedFilterOperator.java:62-92): OR the roaring bitmaps
+            // of the matching dictIds; NEQ / NOT_IN OR the NON-matching ones and flip over the scanned doc range.  The
+            // list holds dictIds: the device reads each bitmap's offset from the staged file's own header.
+            m.ids_off = int64_t(o.blob.size());
+            auto take = [&](int id) {
+              o.blob.push_back(int32_t(id));
+              ++m.nb;
+            };
+            if (b.words) {  // walk the set (or, negated, the clear) bits of the dictId bitset
+              const int nw = (col.card + 31) / 32;
+              for (int w = 0; w < nw; ++w) {
+                uint32_t x = neg ? ~b.words[w] : b.words[w];
+                if (w == nw - 1 && (col.card & 31)) x &= (1u << (col.card & 31)) - 1u;
+                while (x) {
+                  take(w * 32 + __builtin_ctz(x));
+                  x &= x - 1u;
+                }
+              }
+            } else if (!neg) {
+              for (int id = std::max(0, b.lo); id <= std::min(b.hi, col.card - 1); ++id) take(id);
+            } else {
+              for (int id = 0; id < col.card; ++id)
+                if (id < b.lo || id > b.hi) take(id);
+            }
+          }
+          mit = o.leaf_memo.emplace(LeafKey(l, b.words, b.lo, b.hi, col.card), m).first;
+        }
+        const LeafMemo& m = mit->second;
+        L.mode = m.mode;
+        if (m.mode == LEAF_NONE) continue;
+        if (m.mode == LEAF_SCAN_BITSET) o.fixes.push_back({size_t(s), 2, int(l), size_t(m.bits_off)});
+        if (bitmap_leaf) {
+          ExecPlan::RoarItem it{s, int(l), neg, size_t(m.ids_off), m.nb, int((int64_t(seg.total_docs) + 65535) >> 16),
+                                o.mask_words, col.inv_dev.p};
+          if (s == 0) {  // serialized bytes of the ORed bitmaps: segment 0's selectivity estimate only
+            const int32_t* ids = o.blob.data() + m.ids_off;
+            for (int k = 0; k < m.nb; ++k) it.bytes += col.inv_off[ids[k] + 1] - col.inv_off[ids[k]];
           }
           if (!P.rprog_on) o.mask_words += uint64_t(it.nchunks) * 2048;
           o.maxchunks = std::max(o.maxchunks, it.nchunks);
@@ -1994,8 +2168,9 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       }
     }
   };
-  if (nchunk > 1) ctx->parallel_for(nchunk, plan_chunk);
-  else if (nchunk == 1) plan_chunk(0);
+  if (nchunk > 1 && !P.serial) ctx->parallel_for(nchunk, plan_chunk);
+  else
+    for (int ci = 0; ci < nchunk; ++ci) plan_chunk(ci);
   P.mv_items.clear();
   P.mv_index.assign(n, std::vector<int>(q.leaf_col.size(), -1));
   P.mv_neg.assign(q.leaf_col.size(), 0);
@@ -2276,6 +2451,45 @@ int rprog_slots(const RProg& r) {
   return ns;
 }
 
+// The wave kernel's own plan walk (pgx_roaring_program_wave) keeps the operand stack as 4-bit entries of one 64-bit
+// word and shifts on every binary op unconditionally: only well-formed programs (each NOT / AND / OR has its operands,
+// one result left), at most 16 operands deep and with slot ids below 8 may take it.  Mirrors the device walk.
+bool rprog_wave_ok(const RProg& r, int* slots) {
+  int depth = 0, maxd = 0, ns = 0;
+  std::vector<bool> pure;
+  for (int i = 0; i < r.nops; ++i) {
+    const int op = r.op[i];
+    if (op == RP_LEAF) {
+      const bool top = !pure.empty() && pure.back();
+      const bool f_or = top && i + 1 < r.nops && r.op[i + 1] == RP_OR;
+      const bool f_andnot = top && !f_or && i + 2 < r.nops && r.op[i + 1] == RP_NOT && r.op[i + 2] == RP_AND;
+      if (f_or) {
+        ++i;
+      } else if (f_andnot) {
+        pure.back() = false;
+        i += 2;
+      } else {
+        pure.push_back(true);
+        ++ns;
+        maxd = std::max(maxd, ++depth);
+      }
+    } else if (op == RP_NOT) {
+      if (depth < 1) return false;
+      pure.back() = false;
+    } else if (op == RP_AND || op == RP_OR) {
+      if (depth < 2) return false;
+      --depth;
+      pure.pop_back();
+      pure.back() = false;
+    } else {
+      return false;
+    }
+  }
+  if (depth != 1 || maxd > 16 || ns > 7) return false;
+  if (slots) *slots = ns;
+  return true;
+}
+
 void launch_bitmaps(ExecPlan& P, hipStream_t st) {
   if (P.rchunk) return;  // the query kernels evaluate the bitmap programs per chunk themselves
   if (P.rprog_on) {
@@ -2289,7 +2503,8 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
       int nb = 0;
       for (int k = 0; k < r.nops; ++k)
         if (r.op[k] == RP_LEAF && r.arg[k] >= 0) nb += P.roar[r.arg[k]].nb;
-      const int ns = rprog_slots(r);
+      int ns = 0;
+      if (!rprog_wave_ok(r, &ns) || ns != rprog_slots(r)) wave = false;
       if (nb > 64 || ns > 3) wave = false;
       nslots = std::max(nslots, ns);
     }
@@ -2323,7 +2538,9 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
   }
 }
 
-void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
+// Host half of the argument upload: lays out and fills the pinned arena (blob, KSeg, RDesc, RProg) and allocates the
+// device buffers the plan needs.  No stream work: batched plans build their arenas on planner threads.
+void build_arena(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B) {
   const size_t n = P.ksegs.size();
   B.off_ksegs = align_up(P.blob32.size() * 4, 256);
   B.off_jsegs = align_up(B.off_ksegs + n * sizeof(KSeg), 256);
@@ -2347,7 +2564,7 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
   }
   P.lmask_dev = nullptr;
   if (P.fsm_on) {
-    const int L = P.fsm.num_leaves, S = P.fsm.num_states;
+    const int S = P.fsm.num_states;
     P.lmask_buf = DevBuf(ctx, std::max<uint64_t>(P.lmask_total, 1) * 4);
     P.lmask_dev = P.lmask_buf.as<uint32_t>();
     size_t fi = 0;
@@ -2358,12 +2575,7 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
       P.fsm_segs[fi++].lmask = P.lmask_dev + P.lmask_off[s];
     }
     P.fsm_table = DevBuf(ctx, P.fsm.table.size() * 4);
-    hip_check(hipMemcpyAsync(P.fsm_table.p, P.fsm.table.data(), P.fsm.table.size() * 4, hipMemcpyHostToDevice, st),
-              "automaton tables H2D");
     P.fsm_segbuf = DevBuf(ctx, P.fsm_segs.size() * sizeof(FsmSeg));
-    hip_check(hipMemcpyAsync(P.fsm_segbuf.p, P.fsm_segs.data(), P.fsm_segs.size() * sizeof(FsmSeg),
-                             hipMemcpyHostToDevice, st),
-              "automaton segments H2D");
     const uint64_t ent = std::max<uint64_t>(uint64_t(P.fsm_chunks) * S, 1);
     P.fsm_cnt = DevBuf(ctx, ent * 4);
     P.fsm_stv = DevBuf(ctx, ent * 2);
@@ -2371,10 +2583,11 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
     const uint64_t pe = uint64_t(P.fsm_segs.size()) * P.fsm_T * S;
     P.fsm_pcount = DevBuf(ctx, pe * 8);
     P.fsm_pstate = DevBuf(ctx, pe * 2);
-    (void)L;
   }
+  P.mv_host.clear();
   if (!P.mv_items.empty()) {  // multi-value scan leaves: descriptors + one doc mask per (segment, leaf)
-    std::vector<MvLeaf> items(P.mv_items.size());
+    std::vector<MvLeaf>& items = P.mv_host;
+    items.resize(P.mv_items.size());
     std::vector<int64_t> off(P.mv_items.size());
     int64_t words = 0;
     P.mv_max_words = 0;
@@ -2399,14 +2612,10 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
       m.num_docs = S.num_docs;
       m.lo = uint32_t(L.lo);
       m.span = uint32_t(L.hi) - uint32_t(L.lo);
-      m.neg = 0;
+      m.neg = P.mv_neg.empty() ? 0 : P.mv_neg[it.leaf];
       P.ksegs[it.seg].leaf[it.leaf].bitset = m.mask;  // the query kernel's LEAF_DOCMASK word source
     }
     P.mv_descs = DevBuf(ctx, items.size() * sizeof(MvLeaf));
-    for (size_t i = 0; i < items.size(); ++i) items[i].neg = P.mv_neg.empty() ? 0 : P.mv_neg[P.mv_items[i].leaf];
-    hip_check(hipMemcpyAsync(P.mv_descs.p, items.data(), items.size() * sizeof(MvLeaf), hipMemcpyHostToDevice, st),
-              "multi-value leaf descriptors H2D");
-    hip_check(hipStreamSynchronize(st), "sync");  // the host vector goes out of scope
   }
   if (n) std::memcpy(B.host.bytes() + B.off_ksegs, P.ksegs.data(), n * sizeof(KSeg));
   P.kq.segs = reinterpret_cast<const KSeg*>(B.dev() + B.off_ksegs);
@@ -2426,7 +2635,7 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
       const auto& it = P.roar[i];
       rd[i].mask = P.rprog_on ? nullptr : P.masks_dev + it.mask_off;
       rd[i].inv = static_cast<const uint8_t*>(it.inv);
-      rd[i].offs = reinterpret_cast<const uint32_t*>(base + it.blob_off);
+      rd[i].ids = reinterpret_cast<const uint32_t*>(base + it.blob_off);
       rd[i].nb = it.nb;
       rd[i].nchunks = it.nchunks;
     }
@@ -2437,14 +2646,36 @@ void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
       rp[i].mask = P.masks_dev + uintptr_t(P.rprogs[i].mask);  // word offset -> device pointer
     }
     P.rprog_dev = reinterpret_cast<const RProg*>(B.dev() + B.off_rprog);
-    // Expand the bitmaps now: send the blob (roaring offsets) and the descriptors ahead of the rest of the arena and
-    // launch, so the expansion runs on the GPU while the host plans the query kernels (plan_jit).
+  }
+}
+
+// Stream half: the automaton / multi-value descriptor copies, and -- so the bitmap expansion runs on the GPU while the
+// host plans the query kernels (plan_jit) -- the blob (roaring offsets) and bitmap descriptors ahead of the rest of the
+// arena, then the bitmap launch.
+void send_arena(ExecPlan& P, ExecBuffers& B, hipStream_t st) {
+  if (P.fsm_on) {
+    hip_check(hipMemcpyAsync(P.fsm_table.p, P.fsm.table.data(), P.fsm.table.size() * 4, hipMemcpyHostToDevice, st),
+              "automaton tables H2D");
+    hip_check(hipMemcpyAsync(P.fsm_segbuf.p, P.fsm_segs.data(), P.fsm_segs.size() * sizeof(FsmSeg),
+                             hipMemcpyHostToDevice, st),
+              "automaton segments H2D");
+  }
+  if (!P.mv_host.empty())  // pageable source: the copy completes before the call returns (P keeps it alive anyway)
+    hip_check(hipMemcpyAsync(P.mv_descs.p, P.mv_host.data(), P.mv_host.size() * sizeof(MvLeaf), hipMemcpyHostToDevice,
+                             st),
+              "multi-value leaf descriptors H2D");
+  if (P.rdesc_dev || P.rprog_dev) {
     hip_check(hipMemcpyAsync(B.arena.p, B.host.p, P.blob32.size() * 4, hipMemcpyHostToDevice, st), "blob H2D");
     hip_check(hipMemcpyAsync(B.dev() + B.off_rdesc, B.host.bytes() + B.off_rdesc,
                              B.off_outs - B.off_rdesc, hipMemcpyHostToDevice, st), "bitmap descriptors H2D");
     launch_bitmaps(P, st);
     P.roar_early = !P.rchunk;
   }
+}
+
+void upload_plan(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, hipStream_t st) {
+  build_arena(ctx, P, B);
+  send_arena(P, B, st);
 }
 
 void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, uint64_t dense_out_bytes) {
@@ -3297,12 +3528,14 @@ struct HostProf {
   }
 };
 
-// Long segment lists (C5: 4096 segments) are planned and launched in batches on one stream: the host plans batch k + 1
-// while the GPU runs batch k, instead of planning every segment before the first launch.  Every batch decodes its
-// group keys against global dictionaries built over the WHOLE list (Domain), accumulates into batch 0's dense table
-// and writes its statistics / aggregation planes into batch 0's output block, so the combine stays on the device and
-// the result is read back once.  Aggregation-only and dense group-by plans only (sparse / hash plans size their
-// tables from the whole list); false before anything was launched when the plan does not qualify.
+// Long segment lists (C5: 4096 segments) are planned and launched in batches: every batch is planned on a planner
+// thread of its own (plan_query, the pinned argument arena, the query-kernel arguments) while the calling thread sends
+// and launches the batches in order, so the GPU starts after the first (small) batch is planned and host planning
+// (~1 us per segment single-threaded) overlaps the GPU instead of pacing it.  Every batch decodes its group keys
+// against global dictionaries built over the WHOLE list (Domain), accumulates into batch 0's dense table and writes
+// its statistics / aggregation planes into batch 0's output block, so the combine stays on the device and the result
+// is read back once.  Aggregation-only and dense group-by plans only (sparse / hash plans size their tables from the
+// whole list); false before anything was launched when the plan does not qualify.
 bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                  const pgx_exec_opts* opts, pgx_result* R, hipStream_t st, uint32_t xflags, HostProf& hp) {
   int bs = 512;
@@ -3310,18 +3543,85 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   if (bs <= 0 || n < 2 * bs || !jit_enabled()) return false;
   const size_t L = q.leaf_col.size();
   std::vector<GlobalDict> full;
-  for (const auto& g : q.group_cols) full.push_back(build_global_dict(segs, n, g));
-  // batch 0 is a quarter batch: the GPU idles until it is planned; the rest split evenly
-  std::vector<int> start{0};
-  int first = bs / 4;
+  for (int g = 0; g < int(q.group_cols.size()); ++g) full.push_back(group_dict(q, segs, n, g));
+  hp.mark("b.dicts");
+  // Batch sizes double from a small first batch up to bs: every batch is planned concurrently from t = 0, and batch k
+  // (twice batch k - 1) is ready by the time the GPU has run batches 0 .. k - 1 (~1 us of planning per segment on one
+  // planner thread against ~1.5 us of GPU time per C5 segment).  PGX_BATCH_FIRST tunes the first size.
+  int first = 64;
   if (const char* e = std::getenv("PGX_BATCH_FIRST")) first = std::atoi(e);
   first = std::max(1, std::min(first, bs));
-  start.push_back(first);
-  const int rest = (n - first + bs - 1) / bs;
-  for (int b = 1; b <= rest; ++b) start.push_back(first + int(int64_t(n - first) * b / rest));
+  std::vector<int> start{0};
+  for (int size = first; start.back() < n; size = std::min(bs, 2 * size)) {
+    const int left = n - start.back();
+    start.push_back(start.back() + (left < size + size / 2 ? left : size));  // a short tail joins the last batch
+  }
   const int nb = int(start.size()) - 1;
-  std::vector<std::unique_ptr<ExecPlan>> plans;
-  std::vector<std::unique_ptr<ExecBuffers>> bufs;
+  struct Batch {
+    std::unique_ptr<ExecPlan> P;
+    std::unique_ptr<ExecBuffers> B;
+    bool ready = false, eligible = true;
+    std::exception_ptr err;
+  };
+  std::vector<Batch> bt(nb);
+  std::mutex mu;
+  std::condition_variable cv;
+  int done = 0;
+  const int dev = ctx->device;
+  std::vector<std::string> prof(hp.on ? nb : 0);  // PGX_HOST_PROFILE: each planner's phase marks
+  auto plan_one = [&, dev](int b) {
+    Batch& x = bt[b];
+    HostProf bp;
+    if (bp.on) g_prof_mark = [&bp](const char* w) { bp.mark(w); };
+    try {
+      hip_check(hipSetDevice(dev), "hipSetDevice");  // device buffers and JIT modules belong to the context's device
+      const int s0 = start[b], cnt = start[b + 1] - s0;
+      Domain d;
+      d.g = &full;
+      d.index.resize(cnt);
+      std::iota(d.index.begin(), d.index.end(), s0);
+      x.P = std::make_unique<ExecPlan>();
+      x.P->serial = true;
+      plan_query(ctx, q, segs + s0, cnt, bindings ? bindings + size_t(s0) * L : nullptr, xflags, *x.P, &d);
+      const int gm = x.P->kq.group_mode;
+      x.eligible = !x.P->use_part && (gm == G_NONE || gm == G_DENSE_LDS || gm == G_DENSE_GLOBAL) && x.P->mv_items.empty();
+      if (x.eligible) {
+        x.B = std::make_unique<ExecBuffers>();
+        bp.mark("t.plan");
+        build_arena(ctx, *x.P, *x.B);
+        bp.mark("t.arena");
+        plan_jit(ctx, q, segs + s0, cnt, *x.P, *x.B);
+        bp.mark("t.jit");
+      }
+    } catch (...) {
+      x.err = std::current_exception();
+    }
+    if (bp.on) {
+      prof[b] = bp.line;
+      bp.on = false;
+      g_prof_mark = nullptr;
+    }
+    std::lock_guard<std::mutex> g(mu);
+    x.ready = true;
+    ++done;
+    cv.notify_all();
+  };
+  // the planner tasks reference this frame (plan_one and what it captures are declared above): every submitted task
+  // finishes before run_batched returns or throws
+  struct Drain {
+    std::mutex& mu;
+    std::condition_variable& cv;
+    int& done;
+    int submitted = 0;
+    ~Drain() {
+      std::unique_lock<std::mutex> g(mu);
+      cv.wait(g, [&] { return done == submitted; });
+    }
+  } drain{mu, cv, done};
+  for (int b = 0; b < nb; ++b) {
+    ++drain.submitted;
+    ctx->plan_submit([&plan_one, b] { plan_one(b); });
+  }
   // Two streams: each batch's argument arena and bitmap programs go on the side stream, and the query stream waits
   // for them with an event.  The copies' SDMA latency and the bitmap programs of batch k + 1 then run while batch k's
   // query kernel streams the forward indexes, instead of between the query kernels.  Declared after the buffers:
@@ -3351,50 +3651,52 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   }
   int64_t host_entries = 0, total_raw = 0;
   for (int b = 0; b < nb; ++b) {
-    const int s0 = start[b], cnt = start[b + 1] - s0;
-    Domain d;
-    d.g = &full;
-    d.index.resize(cnt);
-    std::iota(d.index.begin(), d.index.end(), s0);
-    auto P = std::make_unique<ExecPlan>();
-    plan_query(ctx, q, segs + s0, cnt, bindings ? bindings + size_t(s0) * L : nullptr, xflags, *P, &d);
-    const int gm = P->kq.group_mode;
-    if (b == 0 && (P->use_part || !(gm == G_NONE || gm == G_DENSE_LDS || gm == G_DENSE_GLOBAL))) return false;
-    auto B = std::make_unique<ExecBuffers>();
-    upload_plan(ctx, *P, *B, ss);
-    plan_jit(ctx, q, segs + s0, cnt, *P, *B);
+    {
+      std::unique_lock<std::mutex> g(mu);
+      cv.wait(g, [&] { return bt[b].ready; });
+    }
+    hp.mark("b.wait");
+    Batch& x = bt[b];
+    if (x.err) std::rethrow_exception(x.err);
+    if (!x.eligible) {
+      if (b == 0) return false;  // nothing launched yet: the caller plans the whole list at once
+      fail(PGX_ERR_INTERNAL, "batched plans disagree");
+    }
+    ExecPlan& P = *x.P;
+    ExecBuffers& B = *x.B;
+    send_arena(P, B, ss);
     if (b == 0) {
-      alloc_outputs(ctx, *P, *B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
-      reset_outputs(*P, *B, ss);
+      alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
+      reset_outputs(P, B, ss);
     } else {
-      const KQuery& K0 = plans[0]->kq;
-      if (P->kq.group_mode != K0.group_mode || P->dense_slots != plans[0]->dense_slots ||
-          P->kq.num_planes != K0.num_planes)
+      const ExecPlan& P0 = *bt[0].P;
+      const KQuery& K0 = P0.kq;
+      if (P.kq.group_mode != K0.group_mode || P.dense_slots != P0.dense_slots || P.kq.num_planes != K0.num_planes)
         fail(PGX_ERR_INTERNAL, "batched plans disagree");
-      alloc_outputs(ctx, *P, *B, K0.table, plans[0]->dense_slots * uint64_t(K0.num_planes) * 8);
-      reset_outputs(*P, *B, ss, false);
-      P->kq.agg_out = K0.agg_out;  // one output block for the whole query
-      P->kq.stats = K0.stats;
-      P->kq.overflow = K0.overflow;
+      alloc_outputs(ctx, P, B, K0.table, P0.dense_slots * uint64_t(K0.num_planes) * 8);
+      reset_outputs(P, B, ss, false);
+      P.kq.agg_out = K0.agg_out;  // one output block for the whole query
+      P.kq.stats = K0.stats;
+      P.kq.overflow = K0.overflow;
     }
     if (two) {
       hipEvent_t e = evs.make();
       hip_check(hipEventRecord(e, ss), "record");
       hip_check(hipStreamWaitEvent(st, e, 0), "wait");
     }
-    launch_scan(*P, st);
-    host_entries += P->host_entries;
-    total_raw += P->total_raw;
-    plans.push_back(std::move(P));
-    bufs.push_back(std::move(B));
+    launch_scan(P, st);
+    hp.mark("b.launch");
+    host_entries += P.host_entries;
+    total_raw += P.total_raw;
   }
   hp.mark("batches");
-  ExecPlan& P0 = *plans[0];
+  for (int b = 0; b < int(prof.size()); ++b) std::fprintf(stderr, "[pgx plan %d]%s\n", b, prof[b].c_str());
+  ExecPlan& P0 = *bt[0].P;
   P0.host_entries = host_entries;
   P0.total_raw = total_raw;
   if (opts && (opts->flags & PGX_X_KEEP_DENSE_ON_DEVICE)) {
-    unsigned long long* outs = reinterpret_cast<unsigned long long*>(bufs[0]->host.bytes() + bufs[0]->off_outs);
-    hip_check(hipMemcpyAsync(outs, bufs[0]->dev() + bufs[0]->off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
+    unsigned long long* outs = reinterpret_cast<unsigned long long*>(bt[0].B->host.bytes() + bt[0].B->off_outs);
+    hip_check(hipMemcpyAsync(outs, bt[0].B->dev() + bt[0].B->off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
     hip_check(hipStreamSynchronize(st), "sync");
     const unsigned long long* stats = outs + 16;
     R->stats[0] = int64_t(stats[0]);
@@ -3406,7 +3708,7 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
     R->agg_fn = q.agg_fn;
     return true;
   }
-  finish_result(ctx, q, P0, *bufs[0], segs, n, st, R, nullptr);
+  finish_result(ctx, q, P0, *bt[0].B, segs, n, st, R, nullptr);
   hp.mark("finish");
   return true;
 }
@@ -3706,7 +4008,7 @@ void run_multi(pgx_ctx* const* ctxs, int nctx, const pgx_query& q, pgx_segment* 
     if (!part[k].empty()) active.push_back(k);
   const size_t L = q.leaf_col.size();
   std::vector<GlobalDict> gd;
-  for (const auto& g : q.group_cols) gd.push_back(build_global_dict(segs, n, g));
+  for (int g = 0; g < int(q.group_cols.size()); ++g) gd.push_back(group_dict(q, segs, n, g));
   uint64_t slots = 1;
   bool dense = !q.group_cols.empty() && !(xflags & PGX_X_FORCE_HASH);
   for (const auto& g : gd) {
@@ -3979,6 +4281,42 @@ pgx_status pgx_query_compile(pgx_ctx* ctx, const pgx_query_desc* d, pgx_query** 
   });
 }
 
+pgx_status pgx_query_set_key_domain(pgx_query* q, int32_t group_col, int32_t type, int64_t num_values,
+                                    const int64_t* ivals, const double* dvals, const char* const* svals) {
+  return guarded([&] {
+    if (!q) fail(PGX_ERR_INVALID_ARG, "NULL query");
+    if (group_col < 0 || group_col >= int(q->group_cols.size())) fail(PGX_ERR_INVALID_ARG, "group column index");
+    if (num_values < 0 || num_values > INT32_MAX) fail(PGX_ERR_INVALID_ARG, "key domain size");
+    q->key_domain.resize(q->group_cols.size());
+    KeyDomain D;
+    D.type = type;
+    if (num_values == 0) {  // clears the domain: the union of the executed segments' dictionaries again
+      q->key_domain[group_col] = KeyDomain{};
+      return;
+    }
+    if (type == PGX_INT || type == PGX_LONG) {
+      if (!ivals) fail(PGX_ERR_INVALID_ARG, "NULL values");
+      D.iv.assign(ivals, ivals + num_values);
+      for (int64_t i = 1; i < num_values; ++i)
+        if (!(D.iv[i - 1] < D.iv[i])) fail(PGX_ERR_INVALID_ARG, "key domain not sorted and distinct");
+    } else if (type == PGX_FLOAT || type == PGX_DOUBLE) {
+      if (!dvals) fail(PGX_ERR_INVALID_ARG, "NULL values");
+      D.dv.assign(dvals, dvals + num_values);
+      for (int64_t i = 1; i < num_values; ++i)
+        if (!(D.dv[i - 1] < D.dv[i])) fail(PGX_ERR_INVALID_ARG, "key domain not sorted and distinct");
+    } else if (type == PGX_STRING) {
+      if (!svals) fail(PGX_ERR_INVALID_ARG, "NULL values");
+      for (int64_t i = 0; i < num_values; ++i) D.sv.emplace_back(svals[i] ? svals[i] : "");
+      for (int64_t i = 1; i < num_values; ++i)
+        if (!(D.sv[i - 1] < D.sv[i])) fail(PGX_ERR_INVALID_ARG, "key domain not sorted and distinct");
+    } else {
+      fail(PGX_ERR_INVALID_ARG, "key domain type");
+    }
+    D.set = true;
+    q->key_domain[group_col] = std::move(D);
+  });
+}
+
 pgx_status pgx_query_release(pgx_query* q) {
   return guarded([&] { delete q; });
 }
@@ -4248,7 +4586,7 @@ pgx_status pgx_query_dense_slots(const pgx_query* q, pgx_segment* const* segs, i
   return guarded([&] {
     if (!q || !segs || !slots) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     uint64_t prod = 1;
-    for (const auto& g : q->group_cols) prod *= uint64_t(build_global_dict(segs, n, g).card);
+    for (int g = 0; g < int(q->group_cols.size()); ++g) prod *= uint64_t(group_dict(*q, segs, n, g).card);
     *slots = int64_t(prod);
   });
 }
@@ -4490,39 +4828,57 @@ pgx_status pgx_bind_predicates(const pgx_query* q, pgx_segment* const* segs, int
     auto B = std::make_unique<pgx_bindings>();
     const size_t L = q->leaf_col.size();
     B->arr.assign(size_t(n) * L, pgx_leaf_binding{0, -1, nullptr});
-    B->words.reserve(size_t(n) * L);
-    // one resolution per (leaf, distinct dictionary); consecutive segments usually share a dictionary, so each leaf
-    // first compares with the previous segment's column before the map lookup
-    using Key = std::tuple<size_t, uint64_t, int, int, int>;
-    std::map<Key, size_t> memo;
-    std::vector<const StagedColumn*> prev(L, nullptr);
-    std::vector<size_t> prev_at(L, 0);
-    for (int s = 0; s < n; ++s)
-      for (size_t l = 0; l < L; ++l) {
-        const StagedColumn& c = segs[s]->col(q->leaf_col[l]);
-        pgx_leaf_binding& b = B->arr[size_t(s) * L + l];
-        const StagedColumn* p = prev[l];
-        if (p && p->dict_hash == c.dict_hash && p->card == c.card && p->data_type == c.data_type &&
-            p->pad_char == c.pad_char) {
-          b = B->arr[prev_at[l]];
-          continue;
-        }
-        prev[l] = &c;
-        prev_at[l] = size_t(s) * L + l;
-        const Key key = std::make_tuple(l, c.dict_hash, c.card, c.data_type, c.pad_char);
-        auto it = memo.find(key);
-        if (it != memo.end()) {
-          b = B->arr[it->second];
-          continue;
-        }
-        std::vector<uint32_t> w;
-        resolve_binding(c, q->leaf_kind[l], preds[l], b.lo, b.hi, w);
-        if (!w.empty()) {
-          B->words.push_back(std::move(w));
-          b.words = B->words.back().data();
-        }
-        memo.emplace(key, size_t(s) * L + l);
+    // one resolution per (leaf, distinct dictionary) and chunk of segments; consecutive segments usually share a
+    // dictionary, so each leaf first compares with the previous segment's column before the map lookup.  Long segment
+    // lists (C5: 4096) resolve their chunks in parallel on the context's pool; bitsets are owned per chunk (moving a
+    // vector keeps its buffer, so the binding pointers stay valid when the chunks' bitsets are gathered).
+    constexpr int kChunk = 256;
+    const int nchunk = (n + kChunk - 1) / kChunk;
+    std::vector<std::vector<std::vector<uint32_t>>> owned(nchunk);
+    std::vector<std::exception_ptr> errs(nchunk);
+    auto bind_chunk = [&](int ci) {
+      try {
+        using Key = std::tuple<size_t, uint64_t, int, int, int>;
+        std::map<Key, size_t> memo;
+        std::vector<const StagedColumn*> prev(L, nullptr);
+        std::vector<size_t> prev_at(L, 0);
+        for (int s = ci * kChunk; s < std::min(n, (ci + 1) * kChunk); ++s)
+          for (size_t l = 0; l < L; ++l) {
+            const StagedColumn& c = segs[s]->col(q->leaf_col[l]);
+            pgx_leaf_binding& b = B->arr[size_t(s) * L + l];
+            const StagedColumn* p = prev[l];
+            if (p && p->dict_hash == c.dict_hash && p->card == c.card && p->data_type == c.data_type &&
+                p->pad_char == c.pad_char) {
+              b = B->arr[prev_at[l]];
+              continue;
+            }
+            prev[l] = &c;
+            prev_at[l] = size_t(s) * L + l;
+            const Key key = std::make_tuple(l, c.dict_hash, c.card, c.data_type, c.pad_char);
+            auto it = memo.find(key);
+            if (it != memo.end()) {
+              b = B->arr[it->second];
+              continue;
+            }
+            std::vector<uint32_t> w;
+            resolve_binding(c, q->leaf_kind[l], preds[l], b.lo, b.hi, w);
+            if (!w.empty()) {
+              owned[ci].push_back(std::move(w));
+              b.words = owned[ci].back().data();
+            }
+            memo.emplace(key, size_t(s) * L + l);
+          }
+      } catch (...) {
+        errs[ci] = std::current_exception();
       }
+    };
+    if (nchunk > 1 && n >= 1024) segs[0]->ctx->parallel_for(nchunk, bind_chunk);
+    else
+      for (int ci = 0; ci < nchunk; ++ci) bind_chunk(ci);
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+    for (auto& o : owned)
+      for (auto& w : o) B->words.push_back(std::move(w));
     *out = B.release();
   });
 }

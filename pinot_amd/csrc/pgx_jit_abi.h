@@ -14,8 +14,9 @@
 #define PGX_J_MAX_RLEAVES 8  // leaves of one bitmap program (== kRProgMaxLeaves)
 struct JRDesc {
   unsigned int* mask;            // separate-expansion path only: nchunks x 2048 words
-  const unsigned char* inv;      // device copy of <col>.bitmap.inv
-  const unsigned int* offs;      // byte offsets (into inv) of the roaring bitmaps to OR
+  const unsigned char* inv;      // device copy of <col>.bitmap.inv: (card + 1) big-endian int offsets, then the bitmaps
+  const unsigned int* ids;       // dictIds of the roaring bitmaps to OR (bitmap id starts at inv + BE int at inv + 4 id;
+                                 // shared by every segment with the same binding)
   int nb;                        // number of bitmaps
   int nchunks;                   // ceil(total_docs / 65536)
 };

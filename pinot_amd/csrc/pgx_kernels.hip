@@ -525,6 +525,11 @@ __global__ void pgx_compact(const unsigned long long* table, uint64_t slots, int
 // Global-address-space loads: flat loads would share the LDS counter with the mask atomics and serialise them.
 __device__ __forceinline__ uint32_t rd16(const uint8_t* p) { return *(const PGX_GLOBAL uint16_t*)(p); }
 __device__ __forceinline__ uint32_t rd32(const uint8_t* p) { return rd16(p) | (rd16(p + 2) << 16); }
+// Bitmap k of a descriptor: its dictId's entry of the .bitmap.inv header (BE int offsets, 4-byte aligned) locates it.
+__device__ __forceinline__ const uint8_t* rbitmap(const RDesc& D, int k) {
+  const uint32_t id = D.ids[k];
+  return D.inv + __builtin_bswap32(((const PGX_GLOBAL uint32_t*)(D.inv))[id]);
+}
 
 constexpr int kRoarBatch = 256;
 
@@ -538,7 +543,7 @@ __device__ void roar_or_chunk(const RDesc& D, int chunk, uint32_t* m, const uint
     __syncthreads();
     const int b = b0 + tid;
     if (b < D.nb) {
-      const uint8_t* base = D.inv + D.offs[b];
+      const uint8_t* base = rbitmap(D, b);
       const int n = static_cast<int>(rd32(base + 4));
       // keys are sorted and distinct, so a bitmap with a container in every chunk holds chunk c at index c: probe
       // there first (one load for dense bitmaps), then binary-search the rest of the range
@@ -737,7 +742,7 @@ __global__ void __launch_bounds__(256) pgx_roaring_program_wide(const RProg* __r
       int j = 0;
       while (leaf_b0[j + 1] <= b) ++j;  // the leaf this bitmap belongs to (<= 8 leaves)
       const RDesc& D = descs[leaf_desc[j]];
-      const uint8_t* base = D.inv + D.offs[b - leaf_b0[j]];
+      const uint8_t* base = rbitmap(D, b - leaf_b0[j]);
       const int n = static_cast<int>(rd32(base + 4));
       int lo = 0, hi = n - 1, found = -1;
       const int g = min(chunk, n - 1);
@@ -899,7 +904,7 @@ __global__ void __launch_bounds__(kSegRThreads, 8) pgx_roaring_program_seg(const
   uint32_t off = 0;
   if (my_desc >= 0) {
     const RDesc& D = descs[my_desc];
-    base = D.inv + D.offs[tid - my_first];
+    base = rbitmap(D, tid - my_first);
     n = static_cast<int>(rd32(base + 4));
     if (c0 > 0 && n > 0) {  // first container with key >= c0: keys are strictly increasing, so key[c0] == c0 settles it
       if (n > c0 && static_cast<int>(rd16(base + 8 + 4 * c0)) == c0) {
@@ -1136,7 +1141,7 @@ __global__ void __launch_bounds__(64 * WPB, MINW) pgx_roaring_program_wave(const
   uint32_t off = 0;
   if (my_desc >= 0) {
     const RDesc& D = descs[my_desc];
-    base = D.inv + D.offs[lane - my_first];
+    base = rbitmap(D, lane - my_first);
     n = static_cast<int>(rd32(base + 4));
     if (c0 > 0 && n > 0) {
       if (n > c0 && static_cast<int>(rd16(base + 8 + 4 * c0)) == c0) {

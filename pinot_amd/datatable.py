@@ -357,10 +357,18 @@ class DataTable:
 # ---------------------------------------------------------------------------------------------------------------------
 # InstanceResponse <-> DataTable (IntermediateResultsBlock.getDataTable / BrokerReduceService's read)
 # ---------------------------------------------------------------------------------------------------------------------
+def _base_fn(fn: str) -> str:
+    """The function whose intermediate an MV function carries: AggregationFunctionRegistry maps countmv / summv / minmv
+    / maxmv / avgmv to the Count / Sum / Min / Max / Avg functions (AggregationFunctionRegistry.java:76-80)."""
+    from .broker import _MV_BASE
+    return _MV_BASE.get(fn, fn)
+
+
 def _to_object(fn: str, v):
     """The in-process intermediate of one function as the reference's Serializable (query/aggregation/function/*):
     avg (sum, count) -> AvgPair, minmaxrange -> MinMaxRangePair, distinctcount -> IntOpenHashSet, percentile value
     multiset -> DoubleArrayList, HLL registers -> HyperLogLog, count / sum / min / max -> Double."""
+    fn = _base_fn(fn)
     if fn == "avg":
         return AvgPair((float(v[0]), int(v[1])))
     if fn == "minmaxrange":
@@ -381,6 +389,7 @@ def _to_object(fn: str, v):
 
 
 def _from_object(fn: str, o):
+    fn = _base_fn(fn)
     if fn == "avg":
         return (float(o[0]), int(o[1]))
     if fn == "minmaxrange":
@@ -407,8 +416,8 @@ def response_to_datatable(broker_request: dict, resp) -> bytes:
     from .broker import function_name
     aggs = broker_request["aggregations"]
     if resp.aggregation is not None:
-        types = ["LONG" if a["fn"] == "count" else ("DOUBLE" if a["fn"] in ("sum", "min", "max") else "OBJECT")
-                 for a in aggs]
+        types = ["LONG" if _base_fn(a["fn"]) == "count" else
+                 ("DOUBLE" if _base_fn(a["fn"]) in ("sum", "min", "max") else "OBJECT") for a in aggs]
         dt = DataTable([function_name(a) for a in aggs], types)
         dt.rows.append([int(v) if t == "LONG" else (float(v) if t == "DOUBLE" else _to_object(a["fn"], v))
                         for a, t, v in zip(aggs, types, resp.aggregation)])
@@ -418,11 +427,12 @@ def response_to_datatable(broker_request: dict, resp) -> bytes:
             dt.rows.append([function_name(a), {k: _to_object(a["fn"], v) for k, v in m.items()}])
     else:
         dt = DataTable()
-    if resp.aggregation is not None or resp.group_by is not None:
-        dt.metadata[NUM_DOCS_SCANNED] = str(int(resp.stats[0]))
-        dt.metadata[NUM_ENTRIES_SCANNED_IN_FILTER] = str(int(resp.stats[1]))
-        dt.metadata[NUM_ENTRIES_SCANNED_POST_FILTER] = str(int(resp.stats[2]))
-        dt.metadata[TOTAL_DOCS] = str(int(resp.stats[3]))
+    # attachMetadataToDataTable runs for exception-only tables too (IntermediateResultsBlock.java:163-178)
+    st = list(resp.stats) if resp.stats is not None else [0, 0, 0, 0]
+    dt.metadata[NUM_DOCS_SCANNED] = str(int(st[0]))
+    dt.metadata[NUM_ENTRIES_SCANNED_IN_FILTER] = str(int(st[1]))
+    dt.metadata[NUM_ENTRIES_SCANNED_POST_FILTER] = str(int(st[2]))
+    dt.metadata[TOTAL_DOCS] = str(int(st[3]))
     for code, msg in resp.exceptions.items():
         dt.metadata[EXCEPTION_KEY + str(code)] = msg
     return dt.to_bytes()
@@ -436,10 +446,10 @@ def datatable_to_response(broker_request: dict, b: bytes):
     for k, v in dt.metadata.items():
         if k.startswith(EXCEPTION_KEY):
             resp.exceptions[int(k[len(EXCEPTION_KEY):])] = v
-    if not dt.columns:
-        return resp
     resp.stats = [int(dt.metadata.get(k, 0)) for k in (NUM_DOCS_SCANNED, NUM_ENTRIES_SCANNED_IN_FILTER,
                                                        NUM_ENTRIES_SCANNED_POST_FILTER, TOTAL_DOCS)]
+    if not dt.columns:
+        return resp
     aggs = broker_request["aggregations"]
     if dt.columns == ["functionName", "GroupByResultMap"]:
         resp.group_by = [{k: _from_object(a["fn"], v) for k, v in row[1].items()} for a, row in zip(aggs, dt.rows)]

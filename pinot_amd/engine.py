@@ -376,12 +376,13 @@ class GroupKey:
 class AggregationGroupByResult:
     """operator/aggregation/groupby/AggregationGroupByResult.java:56-113 over the columnar pgx result."""
 
-    def __init__(self, keys: List[str], values: List[list], fns: List[str], mode: str, raw_keys=None):
+    def __init__(self, keys: List[str], values: List[list], fns: List[str], mode: str, raw_keys=None, key_parts=None):
         self._keys = keys
         self._values = values  # [group][fn]
         self.fns = fns
         self.storage_mode = mode
         self.raw_keys = raw_keys
+        self.key_parts = key_parts  # [column][group]: each group column's rendered value (a field may hold tabs)
 
     def get_group_key_iterator(self):
         for i, k in enumerate(self._keys):
@@ -452,6 +453,7 @@ class _Query:
         N.check(N.lib().pgx_query_compile(ctx.handle, C.byref(qd), C.byref(h)))
         self.handle = h
         self.group_cols = gcols
+        self.domains = {}  # group column -> (sorted values, data type) of a caller-given key domain
 
     def predicates(self):
         """The leaves' raw predicate values for pgx_bind_predicates (a-4 runs inside the library)."""
@@ -521,6 +523,30 @@ class _Query:
                                           C.byref(opts), C.byref(r)))
         return r
 
+    def set_key_domain(self, g: int, values, data_type: str):
+        """pgx_query_set_key_domain: group column g's key space becomes `values` (sorted distinct, the union of the
+        column's dictionaries over every process's segments), so ranks plan identical keys.  The result's
+        keys for that column then come back as (-1, index into values); `render_key` reads them from here."""
+        L = N.lib()
+        if values is None:
+            N.check(L.pgx_query_set_key_domain(self.handle, g, 0, 0, None, None, None))
+            self.domains.pop(g, None)
+            return
+        t = {"INT": N.PGX_INT, "LONG": N.PGX_LONG, "FLOAT": N.PGX_FLOAT, "DOUBLE": N.PGX_DOUBLE,
+             "STRING": N.PGX_STRING}[data_type]
+        if data_type == "STRING":
+            vals = sorted(set(str(v) for v in values), key=lambda v: v.encode("utf-8"))
+            arr = (C.c_char_p * max(1, len(vals)))(*[v.encode("utf-8") for v in vals])
+            N.check(L.pgx_query_set_key_domain(self.handle, g, t, len(vals), None, None, arr))
+            keep = np.array(vals, dtype=object)
+        elif data_type in ("INT", "LONG"):
+            keep = np.unique(np.asarray(values, dtype=np.int64))
+            N.check(L.pgx_query_set_key_domain(self.handle, g, t, len(keep), keep.ctypes.data, None, None))
+        else:
+            keep = np.unique(np.asarray(values, dtype=np.float64))
+            N.check(L.pgx_query_set_key_domain(self.handle, g, t, len(keep), None, keep.ctypes.data, None))
+        self.domains[g] = (keep, data_type)
+
     def close(self):
         if getattr(self, "handle", None):
             N.lib().pgx_query_release(self.handle)
@@ -543,6 +569,26 @@ class _Bindings:
         if self.h:
             N.lib().pgx_bindings_release(self.h)
             self.h = None
+
+
+def _render_value(data_type: str, v) -> str:
+    """Dictionary.getStringValue of one group value (keys are dictionary values joined by tab)."""
+    if data_type == "STRING":
+        return str(v)
+    if data_type in ("INT", "LONG"):
+        return str(int(v))
+    if data_type == "FLOAT":
+        return _java_double_str(float(np.float32(v)))
+    return _java_double_str(float(v))
+
+
+def render_key(q: _Query, segments: Sequence[IndexSegment], g: int, seg_index: int, dict_id: int) -> str:
+    """Group column g's value of one result key: a segment's dictionary entry, or (seg_index -1) an entry of the
+    query's key domain (pgx_query_set_key_domain)."""
+    if seg_index < 0:
+        vals, dt = q.domains[g]
+        return _render_value(dt, vals[dict_id])
+    return segments[seg_index].column(q.group_cols[g]).string_of(int(dict_id))
 
 
 def decode_result(q: _Query, r, segments: Sequence[IndexSegment], trim: bool = False) -> IntermediateResultsBlock:
@@ -574,8 +620,7 @@ def decode_result(q: _Query, r, segments: Sequence[IndexSegment], trim: bool = F
         si = np.zeros(max(n, 1), dtype=np.int32)
         di = np.zeros(max(n, 1), dtype=np.int32)
         N.check(L.pgx_result_group_keys(r, g, si.ctypes.data, di.ctypes.data))
-        infos = [seg.column(col) for seg in segments]
-        key_parts.append([infos[si[i]].string_of(int(di[i])) for i in range(n)])
+        key_parts.append([render_key(q, segments, g, int(si[i]), int(di[i])) for i in range(n)])
         raw.append(di[:n].copy())
     keys = ["\t".join(p[i] for p in key_parts) for i in range(n)]
     vals = []
@@ -591,7 +636,7 @@ def decode_result(q: _Query, r, segments: Sequence[IndexSegment], trim: bool = F
             vals.append([float(x) for x in v[:n]])
     per_group = [[vals[f][i] for f in range(len(q.fns))] for i in range(n)]
     blk.aggregation_group_by_result = AggregationGroupByResult(keys, per_group, q.fns, _MODES[mode.value],
-                                                               raw_keys=raw)
+                                                               raw_keys=raw, key_parts=key_parts)
     if trim:
         trimmed = []
         for i in range(len(q.fns)):
@@ -632,24 +677,25 @@ def trimmed_maps(q: _Query, r, segments: Sequence[IndexSegment]) -> List[Dict[st
     function (count -> int, avg -> (sum, count), others -> float)."""
     maps = []
     for fn, (si, di, v, c) in zip(q.fns, trim_and_gather(q, r)):
-        infos = [[seg.column(col) for seg in segments] for col in q.group_cols]
         m = {}
         for j in range(len(v)):
-            key = "\t".join(infos[g][si[g, j]].string_of(int(di[g, j])) for g in range(len(q.group_cols)))
+            key = "\t".join(render_key(q, segments, g, int(si[g, j]), int(di[g, j])) for g in range(len(q.group_cols)))
             m[key] = int(c[j]) if fn == "count" else ((float(v[j]), int(c[j])) if fn == "avg" else float(v[j]))
         maps.append(m)
     return maps
 
 
-def _column_values(segments: Sequence[IndexSegment], col: str, si: np.ndarray, di: np.ndarray) -> np.ndarray:
-    """Values of (segment index, dictId) pairs of one group column, vectorised per distinct segment dictionary."""
+def _column_values(segments: Sequence[IndexSegment], col: str, si: np.ndarray, di: np.ndarray,
+                   domain=None) -> np.ndarray:
+    """Values of (segment index, dictId) pairs of one group column, vectorised per distinct segment dictionary;
+    segment index -1 reads the query's key domain for the column (`domain`: (values, data type))."""
     infos = [seg.column(col) for seg in segments]
     strings = infos[0].meta.data_type == "STRING"
     out = np.empty(len(si), dtype=object if strings else np.float64 if infos[0].meta.data_type in ("FLOAT", "DOUBLE")
                    else np.int64)
     for s in np.unique(si):
         m = si == s
-        vals = infos[int(s)].values
+        vals = domain[0] if s < 0 else infos[int(s)].values
         out[m] = (np.asarray(vals, dtype=object) if strings else np.asarray(vals))[di[m]]
     return out.astype(str) if strings else out
 
@@ -666,7 +712,7 @@ def group_partials(q: _Query, r, segments: Sequence[IndexSegment]):
         si = np.zeros(max(n, 1), dtype=np.int32)
         di = np.zeros(max(n, 1), dtype=np.int32)
         N.check(L.pgx_result_group_keys(r, g, si.ctypes.data, di.ctypes.data))
-        cols.append(_column_values(segments, col, si[:n], di[:n]))
+        cols.append(_column_values(segments, col, si[:n], di[:n], q.domains.get(g)))
     nf = len(q.fns)
     vals = np.zeros((nf, max(n, 1)))
     cnts = np.zeros((nf, max(n, 1)), dtype=np.int64)
@@ -678,23 +724,12 @@ def group_partials(q: _Query, r, segments: Sequence[IndexSegment]):
 def render_group_maps(q: _Query, segments: Sequence[IndexSegment], key_cols, vals, cnts, kept) -> List[Dict[str, object]]:
     """Merged (and trimmed: `kept` = group indices per function) groups as the reference's trimmed combine output:
     one {string key: value} map per function, keys rendered like Dictionary.getStringValue (values joined by tab)."""
-    infos = [segments[0].column(col) for col in q.group_cols]
-
-    def render(info, v):
-        dt = info.meta.data_type
-        if dt == "STRING":
-            return str(v)
-        if dt in ("INT", "LONG"):
-            return str(int(v))
-        if dt == "FLOAT":
-            return _java_double_str(float(np.float32(v)))
-        return _java_double_str(float(v))
-
+    types = [segments[0].column(col).meta.data_type for col in q.group_cols]
     maps = []
     for i, fn in enumerate(q.fns):
         m = {}
         for j in kept[i]:
-            key = "\t".join(render(info, c[j]) for info, c in zip(infos, key_cols))
+            key = "\t".join(_render_value(dt, c[j]) for dt, c in zip(types, key_cols))
             m[key] = int(cnts[i, j]) if fn == "count" else (
                 (float(vals[i, j]), int(cnts[i, j])) if fn == "avg" else float(vals[i, j]))
         maps.append(m)

@@ -203,15 +203,16 @@ def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock
                             "filter": request.get("filter")})
         r = hq.execute(segments)
         try:
-            hmap = E.decode_result(hq, r, segments).get_aggregation_group_by_result().as_map()
+            hres = E.decode_result(hq, r, segments).get_aggregation_group_by_result()
         finally:
             N.lib().pgx_result_release(r)
             hq.close()
         dt = _dtype(segments, c)
         per: Dict[str, Dict[object, int]] = {}
-        for key, (cnt,) in hmap.items():
-            f = key.split("\t", ng)  # the value field is last and may itself hold tabs (STRING)
-            g, v = "\t".join(f[:ng]), _parse_value(dt, f[ng])
+        parts = hres.key_parts  # per column: any field, leading or last, may itself hold tabs (STRING values)
+        for gk in hres.get_group_key_iterator():
+            i, cnt = gk.group_id, hres.get_result_for_key(gk, 0)
+            g, v = "\t".join(parts[j][i] for j in range(ng)), _parse_value(dt, parts[ng][i])
             d = per.setdefault(g, {})
             d[v] = d.get(v, 0) + int(cnt)
         hists[c] = {g: sorted(d.items()) for g, d in per.items()}

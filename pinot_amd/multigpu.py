@@ -8,8 +8,10 @@ operator/MCombineGroupByOperator.java:139-233) for partials that live on differe
   * dense group-by: every rank holds the same dense table layout (pgx_query_dense_slots / pgx_query_dense_plane_op:
     plane 0 = int64 doc count, then one plane per function: 0 int64 add, 1 double add, 2 ordered-u64 min,
     3 ordered-u64 max) -> one all-reduce per plane kind, min/max on sign-flipped ordered encodings;
-  * sparse group-by (key spaces too wide for a dense table): groups gathered to rank 0 by key value and merged there
-    (gather_group_partials / merge_group_partials / trim_to_size).
+  * sparse group-by (key spaces too wide for a dense table): groups routed by packed key to an owner rank with one
+    all-to-all and merged on its device (device_sparse_merge); ranks whose results are not device-resident fall back to
+    gathering groups to rank 0 by key value (gather_group_partials / merge_group_partials / trim_to_size).
+Key identity across processes: union_key_domains (one key space per group-by column over every rank's dictionaries).
 """
 from __future__ import annotations
 
@@ -47,6 +49,38 @@ def dictionary_fingerprint(columns_values: Sequence[Sequence]) -> List[int]:
         h.update("\x1f".join(map(str, u.tolist())).encode("utf-8") if u.dtype == object else u.tobytes())
         out.append(int.from_bytes(h.digest(), "little") >> 1)
     return out
+
+
+def union_key_domains(q, segments) -> None:
+    """Cross-process key identity ("a host-side global dictionary per group-by column"): every rank
+    contributes the distinct values of each group-by column over its segments' dictionaries, all ranks build the same
+    sorted union, and the query plans its keys over it (pgx_query_set_key_domain).  Dense slots and packed sparse keys
+    then mean the same group on every GPU whatever dictionaries the ranks hold, so the partials merge by slot (RCCL
+    all-reduce) or by packed key (all-to-all + device merge) -- the value-keyed combine of
+    MCombineGroupByOperator.java:166-191 without moving values.  One all_gather of dictionary values per query shape:
+    segment metadata, not per-row data."""
+    import torch.distributed as dist
+    mine = []
+    for col in q.group_cols:
+        infos = [s.column(col) for s in segments]
+        dt = infos[0].meta.data_type if infos else None
+        if dt == "STRING":
+            u = sorted({str(v) for i in infos for v in i.values})
+        elif dt is None:
+            u = []
+        else:
+            u = np.unique(np.concatenate([np.asarray(i.values, dtype=np.float64 if dt in ("FLOAT", "DOUBLE")
+                                                     else np.int64) for i in infos])).tolist()
+        mine.append((dt, u))
+    allv = [None] * dist.get_world_size()
+    dist.all_gather_object(allv, mine)
+    for g in range(len(q.group_cols)):
+        dts = {p[g][0] for p in allv if p[g][0] is not None}
+        if len(dts) != 1:
+            raise ValueError("group column %s has different types across ranks: %s" % (q.group_cols[g], dts))
+        dt = dts.pop()
+        vals = [v for p in allv for v in p[g][1]]
+        q.set_key_domain(g, vals, dt)
 
 
 def dense_layout_agrees(slots: int, fingerprints: Sequence[int], device=None) -> bool:
@@ -297,7 +331,7 @@ def device_sparse_merge(ctx, q, r, segments, device):
         L.pgx_result_release(merged)
     fns = q.fns
     si, di = si[:m * ncols].reshape(ncols, m), di[:m * ncols].reshape(ncols, m)
-    cols = [E._column_values(segments, col, si[g], di[g]) for g, col in enumerate(q.group_cols)]
+    cols = [E._column_values(segments, col, si[g], di[g], q.domains.get(g)) for g, col in enumerate(q.group_cols)]
     vals, cnts = v[:m * nf].reshape(nf, m), c[:m * nf].reshape(nf, m)
     parts = gather_group_partials(cols, vals, cnts)  # kept groups only, as key values
     if dist.get_rank() != 0:

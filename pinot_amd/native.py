@@ -101,6 +101,8 @@ EXPORTS = {
     "pgx_segment_device_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     "pgx_query_compile": (C.c_int, [C.c_void_p, C.POINTER(QueryDesc), C.POINTER(C.c_void_p)]),
     "pgx_query_release": (C.c_int, [C.c_void_p]),
+    "pgx_query_set_key_domain": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_void_p,
+                                           C.c_void_p]),
     "pgx_execute": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(LeafBinding),
                               C.POINTER(ExecOpts), C.POINTER(C.c_void_p)]),
     "pgx_result_release": (C.c_int, [C.c_void_p]),

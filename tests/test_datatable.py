@@ -40,15 +40,36 @@ def test_hashmap_order_is_bucket_then_insertion():
 
 
 def test_exception_only_table_layout():
-    """DataTable() + addException: no dictionary, no schema, no rows; metadata "Exception<code>" (DataTable.java:856-861)."""
-    resp = B.InstanceResponse(exceptions={200: "boom"})
+    """DataTable() + addException: no dictionary, no schema, no rows; metadata "Exception<code>" (DataTable.java:856-861)
+    plus the four statistics attachMetadataToDataTable always writes (IntermediateResultsBlock.java:163-178), in
+    HashMap order."""
+    resp = B.InstanceResponse(exceptions={200: "boom"}, stats=[5, 6, 7, 8])
     b = D.response_to_datatable(pql.compile(BASIC), resp)
     h = _header(b)
-    meta = struct.pack(">i", 1) + struct.pack(">i", 12) + b"Exception200" + struct.pack(">i", 4) + b"boom"
+    entries = {"numDocsScanned": "5", "numEntriesScannedInFilter": "6", "numEntriesScannedPostFilter": "7",
+               "totalDocs": "8", "Exception200": "boom"}
+    meta = struct.pack(">i", 5) + b"".join(struct.pack(">i", len(k)) + k.encode() + struct.pack(">i", len(entries[k]))
+                                           + entries[k].encode() for k in D.java_hashmap_order(list(entries)))
     assert h == (2, 0, 0, 52, 0, 52, len(meta), 52 + len(meta), 0, 52 + len(meta), 0, 52 + len(meta), 0)
     assert b[52:] == meta
     back = D.datatable_to_response(pql.compile(BASIC), b)
     assert back.exceptions == {200: "boom"} and back.aggregation is None and back.group_by is None
+    assert back.stats == [5, 6, 7, 8]
+
+
+def test_mv_functions_use_their_base_functions_cells():
+    """countmv / summv / minmv / maxmv / avgmv are the Count / Sum / Min / Max / Avg functions
+    (AggregationFunctionRegistry.java:76-80): LONG, DOUBLE cells and an AvgPair object, read back as the same values."""
+    q = pql.compile("SELECT COUNTMV(mv), SUMMV(mv), MINMV(mv), MAXMV(mv), AVGMV(mv) FROM t")
+    resp = B.InstanceResponse(aggregation=[7, 21.0, 1.0, 6.0, (21.0, 7)], stats=[3, 0, 3, 10])
+    b = D.response_to_datatable(q, resp)
+    dt = D.DataTable.from_bytes(b)
+    assert dt.types == ["LONG", "DOUBLE", "DOUBLE", "DOUBLE", "OBJECT"]
+    back = D.datatable_to_response(q, b)
+    assert back.aggregation == [7, 21.0, 1.0, 6.0, (21.0, 7)]
+    assert isinstance(back.aggregation[0], int)
+    red = B.BrokerReduceService().reduce_on_data_table(q, {"x": b, "y": b})
+    assert red == B.BrokerReduceService().reduce_on_data_table(q, {"x": resp, "y": resp})
 
 
 def test_aggregation_table_layout_and_values():

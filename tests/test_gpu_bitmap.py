@@ -102,17 +102,27 @@ def test_mixed_bitmap_and_scan_segments_in_one_query(ctx, segs, text):
         H.assert_values_equal(blk.get_aggregation_result(), o["results"], fns)
 
 
-@pytest.mark.parametrize("mode", ["0", "0chunk", "1"])
-@pytest.mark.parametrize("text", QUERIES[9:])
+# all-bitmap filter whose program ORs more than 64 bitmaps: past the wave kernel's one-bitmap-per-lane limit, so the
+# normal heuristic picks the per-segment walk (pgx_roaring_program_seg)
+WIDE_IN = "SELECT COUNT(*), SUM(m) FROM t WHERE y IN (%s) AND x <> 1" % ", ".join(str(3 * i + 1) for i in range(70))
+
+
+@pytest.mark.parametrize("mode", ["0wave", "0", "0chunk", "0narrow", "1"])
+@pytest.mark.parametrize("text", QUERIES[9:] + [WIDE_IN])
 def test_bitmap_program_in_kernel_vs_separate_pass(ctx, segs, text, mode, monkeypatch):
     """All-bitmap filter sub-trees evaluated per 65536-doc chunk inside the query kernel (LEAF_RCHUNK, PGX_RCHUNK=1)
-    or by the separate expansion pass (PGX_RCHUNK=0): one workgroup per segment walking every bitmap's containers in
-    key order (default), or one workgroup per (segment, chunk) with a container search ("0chunk", PGX_RPROG_SEG=0).
-    All equal the oracle, statistics included, alone and in a multi-segment launch whose workgroups start
-    mid-chunk."""
+    or by the separate expansion pass (PGX_RCHUNK=0): the wave-per-chunk kernel ("0wave", the default for programs of
+    at most 64 bitmaps and 3 mask slots), one workgroup per segment walking every bitmap's containers in key order
+    ("0", PGX_RPROG_WAVE=0), one workgroup per (segment, chunk) with a container search ("0chunk", PGX_RPROG_SEG=0),
+    or the stack kernel ("0narrow", PGX_RPROG_NARROW=1).  All equal the oracle, statistics included, alone and in a
+    multi-segment launch whose workgroups start mid-chunk."""
     from pinot_amd import engine as E
     monkeypatch.setenv("PGX_RCHUNK", mode[0])
+    monkeypatch.setenv("PGX_RPROG_WAVE", "1" if mode == "0wave" else "0")
     monkeypatch.setenv("PGX_RPROG_SEG", "0" if mode == "0chunk" else "1")
+    if mode == "0narrow":
+        monkeypatch.setenv("PGX_RPROG_NARROW", "1")
+        monkeypatch.setenv("PGX_RPROG_SEG", "0")
     inv, scan, oseg = segs
     q = pql.compile(text)
     pm = E.InstancePlanMakerImplV2(ctx)

@@ -218,3 +218,28 @@ def test_fasthll_over_serialized_hll_column(env):
     with pytest.raises(N.PgxError) as ei:
         pm.make_inter_segment_plan(gsegs, pql.compile("SELECT FASTHLL(d) FROM t")).execute()
     assert ei.value.status == N.PGX_ERR_UNSUPPORTED
+
+
+def test_histogram_group_key_with_tab_in_leading_string(env):
+    """A leading STRING group value holding a tab: the histogram sub-query's groups are folded per leading key from
+    the result's per-column key parts, not by re-splitting the joined string (DefaultGroupKeyGenerator joins with tab,
+    so the joined key alone is ambiguous)."""
+    from pinot_amd import engine as E
+    ctx, _, _ = env
+    g0 = np.array(["a\tb", "a", "a\tb", "c", "a", "a\tb", "c", "c\t"] * 50)
+    raw = {"g": g0, "v": (np.arange(len(g0)) % 7).astype(np.int32), "m": np.arange(len(g0), dtype=np.int32)}
+    seg, o = H.build_pair("tabkey", raw)
+    gs = E.IndexSegment(ctx, seg)
+    pm = E.InstancePlanMakerImplV2(ctx)
+    for text in ("SELECT DISTINCTCOUNT(v), PERCENTILE50(v), COUNT(*) FROM t GROUP BY g",
+                 "SELECT DISTINCTCOUNT(v) FROM t WHERE m < 300 GROUP BY g"):
+        q = pql.compile(text)
+        got = pm.make_inter_segment_plan([gs], q).execute().get_aggregation_group_by_result().as_map()
+        exp = O.combine_group_by([O.run_group_by(o, q, literal_filter=False)], q)["merged"]
+        assert set(got) == set(exp)
+        for k in exp:
+            assert got[k][0] == exp[k][0], k
+            if len(exp[k]) > 1:
+                vals, cnts = np.unique(np.asarray(exp[k][1], dtype=np.float64), return_counts=True)
+                assert got[k][1] == [(float(a), int(c)) for a, c in zip(vals, cnts)]
+                assert got[k][2] == exp[k][2]

@@ -341,3 +341,78 @@ def test_trim_to_size_with_global_total():
     kept = multigpu.trim_to_size(["sum"], vals, cnts, 10, total=50000)[0]  # 50000 > 20000: keep the best 5000
     assert len(kept) == 5000 and set(vals[0, kept]) == set(range(7000, 12000))
     assert len(multigpu.trim_to_size(["sum"], vals, cnts, 10, total=15000)[0]) == 12000  # below the threshold: all
+
+
+# ------------------------------------------------------------------------------------------------
+# Cross-process key identity (multigpu.union_key_domains): every rank contributes its group columns' dictionary values,
+# every rank sets the SAME sorted union as the query's key domain (pgx_query_set_key_domain), whatever it holds itself.
+# ------------------------------------------------------------------------------------------------
+class _FakeCol:
+    def __init__(self, values, dt):
+        self.values = values
+        self.meta = type("M", (), {"data_type": dt})()
+
+
+class _FakeSeg:
+    def __init__(self, cols):
+        self.cols = cols
+
+    def column(self, name):
+        return self.cols[name]
+
+
+class _FakeQuery:
+    """Records the domains union_key_domains sets (the library call is the GPU tests' part)."""
+    def __init__(self, group_cols):
+        self.group_cols = group_cols
+        self.set = {}
+
+    def set_key_domain(self, g, values, dt):
+        if dt == "STRING":
+            vals = sorted(set(values), key=lambda v: v.encode("utf-8"))
+        else:
+            vals = np.unique(np.asarray(values, dtype=np.float64 if dt in ("FLOAT", "DOUBLE") else np.int64)).tolist()
+        self.set[g] = (dt, vals)
+
+
+def _domain_segments(rank):
+    segs = []
+    for s in range(2):
+        ints = np.arange(rank * 50 + s * 10, rank * 50 + s * 10 + 60, dtype=np.int64)  # overlapping ranges
+        strs = ["k%d" % (rank * 3 + s + i) for i in range(4)] + ["été", "a\tb"]
+        dbl = np.array([0.5 * rank, 1.25, -3.0 + s])
+        segs.append(_FakeSeg({"i": _FakeCol(ints, "INT"), "s": _FakeCol(strs, "STRING"), "d": _FakeCol(dbl, "DOUBLE")}))
+    return segs
+
+
+def _domain_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fq = _FakeQuery(["i", "s", "d"])
+        multigpu.union_key_domains(fq, _domain_segments(rank) if rank < 2 else [])  # rank 2 holds no segment
+        q.put((rank, fq.set))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_union_key_domains_identical_on_every_rank():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_domain_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1] == res[2]
+    every = _domain_segments(0) + _domain_segments(1)
+    exp_i = sorted({int(v) for s in every for v in s.column("i").values})
+    exp_s = sorted({v for s in every for v in s.column("s").values}, key=lambda v: v.encode("utf-8"))
+    exp_d = sorted({float(v) for s in every for v in s.column("d").values})
+    assert res[0][0] == ("INT", exp_i) and res[0][1] == ("STRING", exp_s) and res[0][2] == ("DOUBLE", exp_d)
+    assert len(exp_i) == 120  # rank 0: 0..69, rank 1: 50..119
