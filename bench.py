@@ -25,6 +25,19 @@ METRIC = "rows/sec for filter+group-by SUM at 1/2/4/8 GPUs; % of HBM roofline"
 CPU_SAMPLE = {"c2": (8, 32_000_000), "c5": (64, 2_000_000), "c3": (8, 16_000_000)}
 
 
+def source_hash():
+    """Hash of the library and kernel sources: stamps PMC traffic files (tools/pmc_traffic.py) so a measurement is only
+    reported for the code it was taken on."""
+    import hashlib
+    h = hashlib.sha1()
+    d = os.path.join(ROOT, "pinot_amd", "csrc")
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".cpp", ".hip", ".h")):
+            h.update(f.encode())
+            h.update(open(os.path.join(d, f), "rb").read())
+    return h.hexdigest()[:16]
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -33,7 +46,7 @@ def parse():
     ap.add_argument("--workload", default=os.environ.get("PGX_WORKLOAD", "c5"))
     ap.add_argument("--rows", type=int, default=0, help="override rows per segment (smoke/debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--profile-iters", type=int, default=0, help="only run K kernel launches (for rocprofv3)")
+    ap.add_argument("--profile-iters", type=int, default=0, help="only run K steps (for rocprofv3 PMC passes)")
     return ap.parse_args()
 
 
@@ -160,7 +173,6 @@ def main():
     q = E._Query(ctx, req)
     segs = data.segments
     seg_arr = (C.c_void_p * len(segs))(*[s.handle.value for s in segs])
-    binds, keep = q.bindings(segs)  # for the untimed profiling / timing calls only; steps bind their own
     L = N.lib()
 
     dense = False
@@ -181,14 +193,6 @@ def main():
             N.check(L.pgx_query_dense_plane_op(q.handle, seg_arr, len(segs), p, C.byref(op)))
             plane_ops.append(op.value)
         dense_t = torch.zeros(nplanes * slots.value, dtype=torch.int64, device="cuda:%d" % local)
-
-    if args.profile_iters:
-        tot, kern = C.c_double(), C.c_double()
-        N.check(L.pgx_execute_timed(ctx.handle, q.handle, seg_arr, len(segs), binds, args.profile_iters,
-                                    C.byref(tot), C.byref(kern), None))
-        if rank == 0:
-            print(json.dumps({"profile_iters": args.profile_iters, "kernel_ms": kern.value}))
-        return
 
     merged = [None]
 
@@ -241,6 +245,14 @@ def main():
                                                    device="cuda:%d" % local)
         return r
 
+    if args.profile_iters:  # exactly K steps and nothing else (PMC passes divide the step kernels' counters by K)
+        for _ in range(args.profile_iters):
+            L.pgx_result_release(step())
+        barrier_sync(world)
+        if rank == 0:
+            print(json.dumps({"profile_steps": args.profile_iters}))
+        return
+
     for _ in range(args.warmup):
         L.pgx_result_release(step())
     barrier_sync(world)
@@ -279,11 +291,20 @@ def main():
     total_rows = rows * (wl.segments * world if wl.scaling == "weak" else wl.segments)
     value = total_rows / (elapsed / args.steps)
 
+    # Kernel time of the SAME step (same plans, batches and streams): every library launch of a few more steps is
+    # bracketed by HIP events on its own stream; the union of the busy intervals is the GPU time a step costs
+    # (pgx_timing_start / pgx_timing_stop).  Run after the timed loop so the events do not perturb it.
+    timing_steps = 5
+    tout = (C.c_double * 3)()
+    tjson = C.create_string_buffer(8192)
+    N.check(L.pgx_timing_start(ctx.handle))
+    for _ in range(timing_steps):
+        L.pgx_result_release(step())
+    N.check(L.pgx_timing_stop(ctx.handle, tout, tjson, len(tjson)))
+    step_kernels = json.loads(tjson.value.decode())
+    kernel_ms = tout[0] / timing_steps
     if rank != 0:
         return
-    tot, kern = C.c_double(), C.c_double()
-    N.check(L.pgx_execute_timed(ctx.handle, q.handle, seg_arr, len(segs), binds, 10, C.byref(tot), C.byref(kern),
-                                None))
     # forward-index bytes of every column the kernel decodes, serialized roaring bytes of every bitmap a
     # bitmap-index leaf ORs (inverted columns, non-RANGE predicates: FilterPlanNode.java:118-132), dictionaries.
     bitmap_leaves = [(lf, np.nonzero(E.leaf_matching_ids(segs[0].column(lf["column"]), lf))[0])
@@ -299,17 +320,20 @@ def main():
         algo_bytes = data.algorithmic_bytes(used, dict_cols, bitmap_leaves)
     # + output_bytes of the final partial table: key + one 8-byte value per function per group
     algo_bytes += ngroups * 8 * (1 + len(req["aggregations"]))
-    # the query-specialised kernel (hiprtc, pgx_jit.cpp) unless PGX_JIT=0 selects the generic interpreter kernel
-    kernel_name = "pgxq (generated per query shape)" if os.environ.get("PGX_JIT", "1") != "0" else "pgx_scan_kernel"
-    if bitmap_leaves:  # the timed span covers the bitmap expansion too (pgx_execute_timed brackets both launches)
-        kernel_name = "pgx_roaring_program + " + kernel_name
-    achieved = algo_bytes / (kern.value * 1e-3) / 1e9
+    # every kernel of the step: the query-specialised kernels (hiprtc, pgx_jit.cpp; PGX_JIT=0 selects the generic
+    # interpreter kernel), bitmap programs, partition / aggregation / trim kernels -- busy union per step
+    kernel_name = "all kernels of the step (busy union): " + ", ".join(
+        "%s x%d" % (k, v[0] // timing_steps) for k, v in sorted(step_kernels["kernels"].items()))
+    ms_step = 1e3 * elapsed / args.steps
+    achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % wl.name)
     if os.path.exists(tf):
         tj = json.load(open(tf))
-        if tj.get("rows") == rows:
-            traffic = tj.get("hbm_bytes_per_launch")  # PMC FETCH/WRITE of the same command (tools/profile_wl.sh)
+        # PMC FETCH/WRITE of the same command (tools/profile_wl.sh), valid only for the kernel sources it was measured
+        # on: a stale file (sources changed since) reports null instead of an old number
+        if tj.get("rows") == rows and tj.get("source_hash") == source_hash():
+            traffic = tj.get("hbm_bytes_per_launch")
     cpu = None
     if world == 1 and not args.no_cpu_baseline and wl.name in CPU_SAMPLE:
         nseg, seg_rows = CPU_SAMPLE[wl.name]
@@ -322,7 +346,7 @@ def main():
         summary = {"local": summary, "merged_over_gpus": merged[0]}
     line = {
         "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": 1e3 * elapsed / args.steps, "higher_is_better": True,
+        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
         "scaling": wl.scaling, "vs_baseline": None, "dtype": "int64",
         "data": "synthetic: device-generated v1 fixed-bit segments (seed %d), dictionaries per SURVEY 8d" % wl.seed,
         "config": {"workload": wl.name + ": " + wl.description, "query": wl.query,
@@ -330,8 +354,14 @@ def main():
                    "rows_total": total_rows, "parallelism": "dp%d (segment sharding)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": kernel_name, "kernel_ms": kern.value, "algorithmic_bytes": algo_bytes,
-                     "host_ms_per_step": 1e3 * elapsed / args.steps - kern.value},
+                     "kernel": kernel_name, "kernel_ms": kernel_ms, "algorithmic_bytes": algo_bytes,
+                     # the same bytes over the whole step (host planning, copies and launch gaps included)
+                     "achieved_per_step": algo_bytes / (ms_step * 1e-3) / 1e9,
+                     "frac_per_step": algo_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "kernel_sum_ms": tout[1] / timing_steps, "kernel_span_ms": tout[2] / timing_steps,
+                     "gpu_idle_ms_per_step": ms_step - kernel_ms,
+                     "kernels_per_step": {k: [v[0] / timing_steps, v[1] / timing_steps]
+                                          for k, v in step_kernels["kernels"].items()}},
         "cpu_baseline": cpu,
         "result": summary, "stats": list(st), "gen_s": t_gen,
     }

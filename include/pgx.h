@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGX_ABI_VERSION 5
+#define PGX_ABI_VERSION 6
 
 typedef enum {
   PGX_OK = 0,
@@ -309,8 +309,18 @@ pgx_status pgx_device_free(pgx_ctx* ctx, void* p);
 pgx_status pgx_copy_to_device(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 pgx_status pgx_copy_to_host(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 
-/* ---- timing (bench): run the query `iters` times back to back, returning per-launch kernel times of
- * the dominant kernel measured with HIP events on the stream it is launched on. */
+/* ---- timing (bench) ---------------------------------------------------------------------------
+ * Kernel time of whole executions (ABI 6): between pgx_timing_start and pgx_timing_stop every kernel the library
+ * launches (on any stream: the context's, the side stream of batched plans, a caller's) is bracketed by HIP events on
+ * its own stream.  pgx_timing_stop waits for the device and returns out[0] = the union of the launches' busy intervals
+ * (concurrent kernels count once: the GPU time the executions cost), out[1] = the summed per-launch durations,
+ * out[2] = the span from the first launch's start to the last one's end, all in ms; json (optional) receives the same
+ * plus per kernel name [launches, summed ms].  One window at a time per process; no reference counterpart. */
+pgx_status pgx_timing_start(pgx_ctx* ctx);
+pgx_status pgx_timing_stop(pgx_ctx* ctx, double out[3], char* json, uint64_t json_cap);
+
+/* Run the query `iters` times back to back as ONE plan over all n segments (one launch per kernel), returning the
+ * average kernel time per iteration measured with HIP events on the stream it is launched on (diagnostics). */
 pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
                              const pgx_leaf_binding* bindings, int32_t iters, double* total_ms,
                              double* kernel_ms, pgx_result** out);

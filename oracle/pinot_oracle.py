@@ -1221,6 +1221,8 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
     gcols = [seg.columns[c] for c in q["group_by"]["columns"]]
     cards = [c.card for c in gcols]
     mode, prod = group_key_mode(cards)
+    if any(c.mv_ids is not None for c in gcols) or any(a["fn"] in MV_FUNCTIONS for a in q["aggregations"]):
+        return _run_group_by_mv(seg, q, docs, scanned, gcols, cards, mode)
     # Raw key = sum_j dictId_j * prod_{i<j} card_i (column 0 least significant), :230-246
     ids = np.stack([c.dict_ids[docs] for c in gcols], axis=1) if len(docs) else np.zeros((0, len(gcols)), np.int64)
     keys = [tuple(int(x) for x in row) for row in ids]
@@ -1306,6 +1308,115 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
     stats = [len(docs), scanned, len(docs) * n_proj, seg.total_raw_docs]
     return {"mode": mode, "map": out, "order": order, "string_key": string_key, "stats": stats,
             "empty": len(docs) == 0}
+
+
+def doc_group_keys(gcols, d: int) -> List[tuple]:
+    """DefaultGroupKeyGenerator.generateKeysForDocId{ArrayBased,LongMapBased,ArrayMapBased}
+    (operator/aggregation/groupby/DefaultGroupKeyGenerator.java:475-608): one key per combination of the doc's values,
+    a single-value column contributing its one dictId, a multi-value column each of its values (duplicates included:
+    a doc whose column holds v twice yields the key twice).  Keys as dictId tuples."""
+    keys = [()]
+    for c in gcols:
+        ids = c.mv_ids[d] if c.mv_ids is not None else [c.dict_ids[d]]
+        keys = [k + (int(i),) for i in ids for k in keys]
+    return keys
+
+
+def _run_group_by_mv(seg: OSegment, q: dict, docs, scanned, gcols, cards, mode) -> dict:
+    """Group-by with multi-value group columns (DefaultGroupByExecutor.java:154-196 -> aggregateGroupByMV) and/or
+    multi-value functions, restated per doc in doc order:
+      COUNT                 += 1 per (doc, key)                       CountAggregationFunction.java:81-90
+      SUM/MIN/MAX/AVG (SV)  the doc's value into each of its keys     Sum/Min/Max/AvgAggregationFunction.aggregateGroupByMV
+      COUNTMV               += number of the doc's values             CountMVAggregationFunction.java:90-102
+      SUMMV / AVGMV         += every value (AVGMV count += 1 each)    SumMVAggregationFunction.java:98-112, AvgMV:113-133
+      MINMV / MAXMV         the holder's value BEFORE the doc is read once; each value below (above) it replaces the
+                            holder, so the doc leaves the LAST such value in its value order, not its extreme
+                            (MinMVAggregationFunction.java:76-91 aggregateGroupBySV, :103-119 aggregateGroupByMV;
+                            MaxMVAggregationFunction.java:85-121).
+    Extended functions (distinctcount / percentile / HLL ...) are not restated here."""
+    uniq, order_seen = {}, []
+    per = []  # (doc, key) pairs in processing order
+    for d in docs.tolist():
+        for k in doc_group_keys(gcols, d):
+            if k not in uniq:
+                uniq[k] = len(uniq)
+                order_seen.append(k)
+            per.append((d, uniq[k]))
+    G = len(uniq)
+    out = {k: [] for k in uniq}
+    for a in q["aggregations"]:
+        fn = a["fn"]
+        if fn == "count":
+            acc = [0] * G
+            for _, g in per:
+                acc[g] += 1
+            vals = acc
+        else:
+            col = seg.columns[a["column"]]
+            mv = fn in MV_FUNCTIONS
+            if mv and col.mv_ids is None:
+                raise ValueError("%s over a single-value column" % fn)
+            if not mv and col.mv_ids is not None:
+                raise ValueError("%s over a multi-value column" % fn)
+            if fn not in ("sum", "min", "max", "avg") and not mv:
+                raise ValueError("%s is not restated for multi-value group-by" % fn)
+
+            def dvals(d):
+                ids = col.mv_ids[d] if mv else [col.dict_ids[d]]
+                return [float(x) for x in col.value_as_double(np.asarray(ids, dtype=np.int64))]
+            if fn in ("sum", "summv"):
+                acc = [0.0] * G
+                for d, g in per:
+                    for v in dvals(d):
+                        acc[g] += v
+                vals = acc
+            elif fn == "countmv":
+                acc = [0] * G
+                for d, g in per:
+                    acc[g] += len(col.mv_ids[d])
+                vals = acc
+            elif fn in ("avg", "avgmv"):
+                acc = [[0.0, 0] for _ in range(G)]
+                for d, g in per:
+                    for v in dvals(d):
+                        acc[g][0] += v
+                        acc[g][1] += 1
+                vals = [(s, c) for s, c in acc]
+            elif fn in ("min", "minmv"):
+                acc = [math.inf] * G
+                for d, g in per:
+                    old = acc[g]
+                    for v in dvals(d):
+                        if v < old:
+                            acc[g] = v
+                vals = acc
+            elif fn in ("max", "maxmv"):
+                acc = [-math.inf] * G
+                for d, g in per:
+                    old = acc[g]
+                    for v in dvals(d):
+                        if v > old:
+                            acc[g] = v
+                vals = acc
+            else:
+                raise ValueError("unsupported function %s" % fn)
+        for k, i in uniq.items():
+            out[k].append(vals[i])
+
+    def raw_key(k):
+        r = 0
+        for j in range(len(k) - 1, -1, -1):
+            r = r * cards[j] + k[j]
+        return r
+
+    def string_key(k):
+        return "\t".join(gcols[j].string_of(k[j]) for j in range(len(k)))
+
+    order = sorted(uniq.keys(), key=raw_key) if mode == "ARRAY_BASED" else None
+    n_proj = len(_projection_columns(q))
+    stats = [len(docs), scanned, len(docs) * n_proj, seg.total_raw_docs]
+    return {"mode": mode, "map": out, "order": order, "string_key": string_key, "stats": stats,
+            "empty": len(docs) == 0, "first_seen": order_seen}
 
 
 # ------------------------------------------------------------------------------------------------

@@ -100,6 +100,61 @@ void hip_check(hipError_t e, const char* what) {
   if (e != hipSuccess) fail(PGX_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// Kernel timing of whole executions (pgx_timing_start / pgx_timing_stop; bench.py's roofline): while a window is open,
+// every kernel the library launches is bracketed by two HIP events on the stream it is launched on (the query stream,
+// the side stream of batched plans, a caller's stream).  At the end of the window the launches' [start, end] intervals
+// give the GPU time an execution really costs: the UNION of busy intervals (concurrent kernels on two streams count
+// once), next to the summed per-launch durations and the span.  Process-wide: one window at a time.
+struct KTimer {
+  std::atomic<bool> on{false};
+  std::mutex mu;
+  struct Rec {
+    hipEvent_t a, b;
+    const char* name;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> spare;
+  hipEvent_t ref = nullptr;
+  hipEvent_t take() {
+    std::lock_guard<std::mutex> g(mu);
+    if (!spare.empty()) {
+      hipEvent_t e = spare.back();
+      spare.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+  void add(hipEvent_t a, hipEvent_t b, const char* name) {
+    std::lock_guard<std::mutex> g(mu);
+    recs.push_back({a, b, name});
+  }
+};
+KTimer g_kt;
+
+struct KScope {
+  hipEvent_t a = nullptr, b = nullptr;
+  hipStream_t st;
+  const char* name;
+  KScope(hipStream_t s, const char* n) : st(s), name(n) {
+    if (!g_kt.on.load(std::memory_order_relaxed)) return;
+    a = g_kt.take();
+    b = g_kt.take();
+    if (a && b && hipEventRecord(a, st) != hipSuccess) a = nullptr;
+  }
+  ~KScope() {
+    if (!a || !b) return;
+    if (hipEventRecord(b, st) == hipSuccess) g_kt.add(a, b, name);
+  }
+};
+// launch `call` (returning hipError_t) on stream `st` as kernel `name`, timed when a timing window is open
+#define PGX_LAUNCH(st, name, call, what) \
+  do {                                   \
+    KScope ks_((st), (name));            \
+    hip_check((call), (what));           \
+  } while (0)
+
 template <typename F>
 pgx_status guarded(F&& f) {
   try {
@@ -2509,7 +2564,7 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
       nslots = std::max(nslots, ns);
     }
     if (wave) {
-      hip_check(pgx_launch_roaring_program_wave(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, nslots, st),
+      PGX_LAUNCH(st, "pgx_roaring_program_wave", pgx_launch_roaring_program_wave(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, nslots, st),
                 "bitmap program launch");
       return;
     }
@@ -2531,10 +2586,10 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
       if (nb > 512) seg_walk = false;
     }
     if (seg_walk) maxleaves = -maxleaves;
-    hip_check(pgx_launch_roaring_program(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, maxleaves, st),
+    PGX_LAUNCH(st, "pgx_roaring_program", pgx_launch_roaring_program(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, maxleaves, st),
               "bitmap program launch");
   } else if (P.rdesc_dev) {
-    hip_check(pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
+    PGX_LAUNCH(st, "pgx_roaring", pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
   }
 }
 
@@ -2720,7 +2775,7 @@ void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table 
   if (init_table && K.group_mode != G_NONE && !P.use_part) {
     const uint64_t slots = (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) ? P.hash_cap : P.dense_slots;
     const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : (K.group_mode == G_HASH64 ? P.hash_cap : 0);
-    hip_check(pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
+    PGX_LAUNCH(st, "pgx_init_planes", pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
   }
 }
 
@@ -3009,7 +3064,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
 
 void launch_fsm(ExecPlan& P, hipStream_t st) {
   if (!P.fsm_on) return;
-  hip_check(pgx_launch_fsm(P.fsm_segbuf.as<FsmSeg>(), int(P.fsm_segs.size()), P.fsm_table.as<uint32_t>(),
+  PGX_LAUNCH(st, "pgx_fsm", pgx_launch_fsm(P.fsm_segbuf.as<FsmSeg>(), int(P.fsm_segs.size()), P.fsm_table.as<uint32_t>(),
                            P.fsm.num_states, P.fsm.num_leaves, P.fsm_chunks, P.fsm_cnt.as<uint32_t>(),
                            P.fsm_stv.as<uint16_t>(), P.fsm_pcount.as<unsigned long long>(), P.fsm_pstate.as<uint16_t>(),
                            P.fsm_T, P.kq.stats, st),
@@ -3019,7 +3074,7 @@ void launch_fsm(ExecPlan& P, hipStream_t st) {
 void launch_scan(ExecPlan& P, hipStream_t st) {
   if (!P.mv_items.empty()) {
     if (P.jit.empty() || !P.jit[0].fn) fail(PGX_ERR_UNSUPPORTED, "multi-value filter needs the query kernels");
-    hip_check(pgx_launch_mv_leaf_mask(P.mv_descs.as<MvLeaf>(), int(P.mv_items.size()), P.mv_max_words, st),
+    PGX_LAUNCH(st, "pgx_mv_leaf_mask", pgx_launch_mv_leaf_mask(P.mv_descs.as<MvLeaf>(), int(P.mv_items.size()), P.mv_max_words, st),
               "multi-value leaf masks");
   }
   if (!P.jit.empty()) {
@@ -3035,7 +3090,7 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
       G.args.part_cap = P.part_cap;
       G.args.part_cstride = kCursorStride;
       void* params[] = {&G.args};
-      hip_check(hipModuleLaunchKernel(static_cast<hipFunction_t>(G.fn), G.grid, 1, 1, G.T, 1, 1, 0, st, params,
+      PGX_LAUNCH(st, "pgxq", hipModuleLaunchKernel(static_cast<hipFunction_t>(G.fn), G.grid, 1, 1, G.T, 1, 1, 0, st, params,
                                       nullptr),
                 "query kernel launch");
     }
@@ -3044,7 +3099,7 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
   }
   if (P.kq.total_tiles == 0) return;
   if (P.rprog_on) fail(PGX_ERR_INTERNAL, "bitmap programs need the query kernels");
-  hip_check(pgx_launch_scan(&P.kq, P.grid, P.tiles_per_wg, P.lds_bytes, st), "scan kernel launch");
+  PGX_LAUNCH(st, "pgx_scan_kernel", pgx_launch_scan(&P.kq, P.grid, P.tiles_per_wg, P.lds_bytes, st), "scan kernel launch");
   launch_fsm(P, st);
 }
 
@@ -3067,7 +3122,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
       PinnedBuf hres(ctx, bytes);
       hip_check(hipMemsetAsync(res.p, 0, 8, st), "memset");
       unsigned long long* rb = devp(res);
-      hip_check(pgx_launch_compact(K.table, slots, K.num_planes, rb, reinterpret_cast<int64_t*>(rb + 32), rb + 32 + cap,
+      PGX_LAUNCH(st, "pgx_compact", pgx_launch_compact(K.table, slots, K.num_planes, rb, reinterpret_cast<int64_t*>(rb + 32), rb + 32 + cap,
                                    cap, st),
                 "compact");
       hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
@@ -3128,7 +3183,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     hip_check(hipMemsetAsync(counter.p, 0, 8, st), "memset");
     const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(slots, uint64_t(std::max<int64_t>(stats[0], 1))));
     DevBuf oslot(ctx, cap * 8), oplanes(ctx, cap * K.num_planes * 8);
-    hip_check(pgx_launch_compact(K.table, slots, K.num_planes, devp(counter), oslot.as<int64_t>(), devp(oplanes), cap,
+    PGX_LAUNCH(st, "pgx_compact", pgx_launch_compact(K.table, slots, K.num_planes, devp(counter), oslot.as<int64_t>(), devp(oplanes), cap,
                                  st),
               "compact");
     unsigned long long cnt = 0;
@@ -3291,7 +3346,7 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
     const uint64_t* recs = reinterpret_cast<const uint64_t*>(P.kq.table);
     const int64_t chunks1 = (N + kPartChunkRecs - 1) / kPartChunkRecs;
     if (chunks1 > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
-    hip_check(pgx_launch_partition(recs, nullptr, nullptr, 1, N, int(chunks1), keymask, 64 - kPart1Bits, kPart1Bits,
+    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(recs, nullptr, nullptr, 1, N, int(chunks1), keymask, 64 - kPart1Bits, kPart1Bits,
                                    PB.out1.as<uint64_t>(), PB.cap1, c1, kCursorStride, tail + 1, st),
               "partition pass 1");
   }
@@ -3302,7 +3357,7 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   if (PB.nbits2) {
     const int64_t chunks2 = (PB.cap1 + kPartChunkRecs - 1) / kPartChunkRecs;
     if (chunks2 * kPart1N > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
-    hip_check(pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, kPart1N, PB.cap1, int(chunks2), keymask,
+    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, kPart1N, PB.cap1, int(chunks2), keymask,
                                    64 - kPart1Bits - PB.nbits2, PB.nbits2, PB.out2.as<uint64_t>(), PB.cap2, c2,
                                    kCursorStride, tail + 2, st),
               "partition pass 2");
@@ -3314,7 +3369,7 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   // count and sum share one LDS add when a partition's count and value sum both fit their bit fields
   const int cbits = bits_for(acap + 1);
   const int pack_shift = (2 * cbits + P.part_vbits <= 64) ? 64 - cbits : 0;
-  hip_check(pgx_launch_part_aggregate(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits, P.part_vbase,
+  PGX_LAUNCH(st, "pgx_part_aggregate", pgx_launch_part_aggregate(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits, P.part_vbase,
                                       P.part_dictid ? P.part_vdict : nullptr, P.part_sum, P.part_min, P.part_max,
                                       pack_shift, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(), PB.ocap, tail,
                                       tail + 3, st),
@@ -3449,7 +3504,7 @@ const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
   DevBuf state(L.ctx, sb * nf), idx(L.ctx, size_t(size) * 8 * nf), keys(L.ctx, size_t(size) * 8 * nf);
   hip_check(hipMemcpyAsync(state.p, init.data(), init.size(), hipMemcpyHostToDevice, st), "trim state H2D");
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((num_groups + 255) / 256, int64_t(L.ctx->num_cus) * 8)));
-  hip_check(pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kinds.data(), nf, state.p,
+  PGX_LAUNCH(st, "pgx_trim", pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kinds.data(), nf, state.p,
                             idx.as<int64_t>(), keys.as<uint64_t>(), size, grid, st),
             "trim launch");
   std::vector<int64_t> ix(size_t(size) * nf);
@@ -3793,7 +3848,7 @@ void run_mv(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, c
     }
   DevBuf idev(ctx, std::max<size_t>(1, items.size()) * sizeof(MvAgg));
   hip_check(hipMemcpy(idev.p, items.data(), items.size() * sizeof(MvAgg), hipMemcpyHostToDevice), "MV items H2D");
-  hip_check(pgx_launch_mv_aggregate(idev.as<MvAgg>(), int(items.size()), max_words, st), "multi-value aggregation");
+  PGX_LAUNCH(st, "pgx_mv_aggregate", pgx_launch_mv_aggregate(idev.as<MvAgg>(), int(items.size()), max_words, st), "multi-value aggregation");
   pgx_result Rs;
   finish_result(ctx, qs, P, B, segs, n, st, &Rs, nullptr);
   std::vector<unsigned long long> res(init.size());
@@ -3918,9 +3973,9 @@ void merge_device_groups(pgx_ctx* ctx, hipStream_t st, const uint64_t* keys, con
   hip_check(hipMemsetAsync(tp + 3 * cap, 0, cap * 8, st), "merge table");    // ordered max
   hip_check(hipMemsetAsync(ctr.p, 0, 16, st), "merge counters");
   unsigned long long* c = ctr.as<unsigned long long>();
-  hip_check(pgx_launch_group_merge(keys, planes, es, ps, n, tkey.as<unsigned long long>(), tp, cap, c + 1, st),
+  PGX_LAUNCH(st, "pgx_group_merge", pgx_launch_group_merge(keys, planes, es, ps, n, tkey.as<unsigned long long>(), tp, cap, c + 1, st),
             "group merge");
-  hip_check(pgx_launch_group_compact(tkey.as<unsigned long long>(), tp, cap, okey.as<uint64_t>(),
+  PGX_LAUNCH(st, "pgx_group_compact", pgx_launch_group_compact(tkey.as<unsigned long long>(), tp, cap, okey.as<uint64_t>(),
                                      oplane.as<uint64_t>(), ocap, c, st),
             "group compact");
   unsigned long long h[2] = {0, 0};
@@ -4100,7 +4155,7 @@ void run_multi(pgx_ctx* const* ctxs, int nctx, const pgx_query& q, pgx_segment* 
                   "dense table peer copy");
         src = stage.as<unsigned long long>();
       }
-      hip_check(pgx_launch_dense_reduce(t0, src, slots, nplanes, ops, st), "dense reduce");
+      PGX_LAUNCH(st, "pgx_dense_reduce", pgx_launch_dense_reduce(t0, src, slots, nplanes, ops, st), "dense reduce");
     }
     std::vector<unsigned long long> host(slots * nplanes);
     hip_check(hipMemcpyAsync(host.data(), t0, tbytes, hipMemcpyDeviceToHost, st), "dense D2H");
@@ -4426,7 +4481,7 @@ pgx_status pgx_result_device_groups(const pgx_result* r, int64_t* n, void* recor
     const auto& L = *r->lazy;
     hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
     hipStream_t st = L.ctx->stream;
-    hip_check(pgx_launch_group_pack(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, r->num_groups,
+    PGX_LAUNCH(st, "pgx_group_pack", pgx_launch_group_pack(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, r->num_groups,
                                     static_cast<uint64_t*>(records), st),
               "group pack");
     hip_check(hipStreamSynchronize(st), "sync");
@@ -4561,7 +4616,7 @@ pgx_status pgx_result_gather(const pgx_result* r, const int64_t* gi, int64_t n, 
       DevBuf di(L.ctx, size_t(n) * 8), out(L.ctx, size_t(n) * 5 * 8);
       std::vector<uint64_t> h(size_t(n) * 5);
       hip_check(hipMemcpyAsync(di.p, gi, size_t(n) * 8, hipMemcpyHostToDevice, st), "gather H2D");
-      hip_check(pgx_launch_group_gather(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, di.as<int64_t>(), n,
+      PGX_LAUNCH(st, "pgx_group_gather", pgx_launch_group_gather(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, di.as<int64_t>(), n,
                                         out.as<uint64_t>(), st),
                 "gather launch");
       hip_check(hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, st), "gather D2H");
@@ -4888,6 +4943,82 @@ const pgx_leaf_binding* pgx_bindings_array(const pgx_bindings* b) { return b ? b
 pgx_status pgx_bindings_release(pgx_bindings* b) {
   delete b;
   return PGX_OK;
+}
+
+pgx_status pgx_timing_start(pgx_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    if (g_kt.on.load()) fail(PGX_ERR_INVALID_ARG, "a timing window is already open");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    hip_check(hipDeviceSynchronize(), "sync");  // every later launch starts after the reference event
+    std::lock_guard<std::mutex> g(g_kt.mu);
+    for (auto& r : g_kt.recs) {
+      g_kt.spare.push_back(r.a);
+      g_kt.spare.push_back(r.b);
+    }
+    g_kt.recs.clear();
+    if (!g_kt.ref) hip_check(hipEventCreate(&g_kt.ref), "event");
+    hip_check(hipEventRecord(g_kt.ref, ctx->stream), "record");
+    hip_check(hipEventSynchronize(g_kt.ref), "sync");
+    g_kt.on = true;
+  });
+}
+
+pgx_status pgx_timing_stop(pgx_ctx* ctx, double out[3], char* json, uint64_t json_cap) {
+  return guarded([&] {
+    if (!ctx || !g_kt.on.load()) fail(PGX_ERR_INVALID_ARG, "no timing window open");
+    g_kt.on = false;
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    hip_check(hipDeviceSynchronize(), "sync");
+    std::lock_guard<std::mutex> g(g_kt.mu);
+    std::vector<std::pair<double, double>> iv;
+    std::map<std::string, std::pair<int, double>> per;
+    for (const auto& r : g_kt.recs) {
+      float a = 0, b = 0;
+      hip_check(hipEventElapsedTime(&a, g_kt.ref, r.a), "elapsed");
+      hip_check(hipEventElapsedTime(&b, g_kt.ref, r.b), "elapsed");
+      iv.emplace_back(a, std::max(a, b));
+      auto& x = per[r.name];
+      ++x.first;
+      x.second += std::max(0.0f, b - a);
+    }
+    std::sort(iv.begin(), iv.end());
+    double busy = 0, sum = 0, cs = 0, ce = -1;
+    for (const auto& x : iv) {
+      sum += x.second - x.first;
+      if (ce < 0 || x.first > ce) {
+        if (ce >= 0) busy += ce - cs;
+        cs = x.first;
+        ce = x.second;
+      } else {
+        ce = std::max(ce, x.second);
+      }
+    }
+    if (ce >= 0) busy += ce - cs;
+    const double span = iv.empty() ? 0.0 : ce - iv.front().first;
+    if (out) {
+      out[0] = busy;
+      out[1] = sum;
+      out[2] = span;
+    }
+    if (json && json_cap) {
+      std::string s = "{";
+      char buf[160];
+      std::snprintf(buf, sizeof buf, "\"busy_ms\": %.6f, \"sum_ms\": %.6f, \"span_ms\": %.6f, \"launches\": %zu, \"kernels\": {",
+                    busy, sum, span, iv.size());
+      s += buf;
+      bool first = true;
+      for (const auto& kv : per) {
+        std::snprintf(buf, sizeof buf, "%s\"%s\": [%d, %.6f]", first ? "" : ", ", kv.first.c_str(), kv.second.first,
+                      kv.second.second);
+        s += buf;
+        first = false;
+      }
+      s += "}}";
+      if (s.size() + 1 > json_cap) fail(PGX_ERR_INVALID_ARG, "json buffer too small");
+      std::memcpy(json, s.c_str(), s.size() + 1);
+    }
+  });
 }
 
 pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,

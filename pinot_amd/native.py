@@ -139,6 +139,8 @@ EXPORTS = {
     "pgx_copy_to_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     "pgx_execute_timed": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(LeafBinding),
                                     C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_void_p)]),
+    "pgx_timing_start": (C.c_int, [C.c_void_p]),
+    "pgx_timing_stop": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_char_p, C.c_uint64]),
 }
 
 
