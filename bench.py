@@ -186,36 +186,53 @@ def main():
         slots = C.c_int64()
         N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
         dense = slots.value <= (1 << 22)
+    # Queries in flight (PGX_INFLIGHT, default 2): step i + 1 is submitted (pgx_execute_async: predicate binding and
+    # host planning on the library's threads, kernels on its own HIP stream) before step i is completed (wait, trim +
+    # read-back, cross-GPU merge), as a server overlaps consecutive queries.  Every step still runs its whole query;
+    # the line also reports the one-query-at-a-time latency (PGX_INFLIGHT=1 gives that timing for every step).
+    inflight = max(1, int(os.environ.get("PGX_INFLIGHT", "2")))
+    streams = [torch.cuda.Stream(device="cuda:%d" % local) for _ in range(inflight)]
     if dense:
         nplanes = 1 + len(req["aggregations"])
         for p in range(nplanes):
             op = C.c_int32()
             N.check(L.pgx_query_dense_plane_op(q.handle, seg_arr, len(segs), p, C.byref(op)))
             plane_ops.append(op.value)
-        dense_t = torch.zeros(nplanes * slots.value, dtype=torch.int64, device="cuda:%d" % local)
+        dense_t = [torch.zeros(nplanes * slots.value, dtype=torch.int64, device="cuda:%d" % local)
+                   for _ in range(inflight)]
 
     merged = [None]
 
-    def step():
-        binds, _owner = q.bindings(segs, seg_arr)  # a-4 per segment, inside the timed step
+    def submit(i):
+        """Start step i: a-4 per segment (pgx_bind_predicates), then the asynchronous execution on stream i."""
+        binds, _owner = q.bindings(segs, seg_arr)  # the library copies the bindings before pgx_execute_async returns
         r = C.c_void_p()
-        if dense and world > 1:
-            opts = N.ExecOpts(0, C.c_void_p(dense_t.data_ptr()), dense_t.numel() * 8, N.PGX_X_KEEP_DENSE_ON_DEVICE)
-            N.check(L.pgx_execute(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
+        hs = streams[i % inflight].cuda_stream
+        if dense:
+            d = dense_t[i % inflight]
+            opts = N.ExecOpts(hs, C.c_void_p(d.data_ptr()), d.numel() * 8, N.PGX_X_KEEP_DENSE_ON_DEVICE)
+        else:
+            opts = N.ExecOpts(hs, None, 0, 0)
+        N.check(L.pgx_execute_async(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
+        return r
+
+    def complete(i, r):
+        """Finish step i: wait, then the combine output (trimToSize, kept groups read back) or the cross-GPU merge."""
+        N.check(L.pgx_result_wait(r, -1))
+        if dense:
+            d = dense_t[i % inflight]
             st = (C.c_int64 * 4)()
             N.check(L.pgx_result_stats(r, st))
             L.pgx_result_release(r)
-            multigpu.merge_dense_planes(dense_t, plane_ops)
-            stats_t = torch.tensor(list(st), dtype=torch.int64, device=dense_t.device)
+            multigpu.merge_dense_planes(d, plane_ops)
+            stats_t = torch.tensor(list(st), dtype=torch.int64, device=d.device)
             torch.distributed.all_reduce(stats_t)
             out = C.c_void_p()
             s4 = (C.c_int64 * 4)(*stats_t.tolist())
-            N.check(L.pgx_result_from_dense(ctx.handle, q.handle, seg_arr, len(segs),
-                                            C.c_void_p(dense_t.data_ptr()), s4, C.byref(out)))
+            N.check(L.pgx_result_from_dense(ctx.handle, q.handle, seg_arr, len(segs), C.c_void_p(d.data_ptr()), s4,
+                                            C.byref(out)))
             E.trim_and_gather(q, out)
             return out
-        opts = N.ExecOpts(0, None, 0, 0)
-        N.check(L.pgx_execute(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
         if req.get("group_by") and world > 1:  # sparse keys
             dev = "cuda:%d" % local
             n = C.c_int64()
@@ -237,33 +254,49 @@ def main():
             E.trim_and_gather(q, r)
         if world > 1 and not req.get("group_by"):  # aggregation-only: combine the scalar partials across GPUs
             vals = []
-            for i in range(len(req["aggregations"])):
+            for k in range(len(req["aggregations"])):
                 v, c = C.c_double(), C.c_int64()
-                N.check(L.pgx_result_agg(r, i, C.byref(v), C.byref(c)))
+                N.check(L.pgx_result_agg(r, k, C.byref(v), C.byref(c)))
                 vals.append((v.value, c.value))
             merged[0] = multigpu.merge_aggregation([a["fn"] for a in req["aggregations"]], vals,
                                                    device="cuda:%d" % local)
         return r
 
+    def run_steps(k, keep_last=False):
+        """k steps with up to `inflight` queries in flight; returns the last step's result when keep_last."""
+        pending = [submit(i) for i in range(min(inflight, k))]
+        last = None
+        for i in range(k):
+            r = complete(i, pending.pop(0))
+            if i + inflight < k:
+                pending.append(submit(i + inflight))
+            if keep_last and i == k - 1:
+                last = r
+            else:
+                L.pgx_result_release(r)
+        return last
+
+    def step():  # one query, nothing in flight beside it (latency; tools)
+        return complete(0, submit(0))
+
     if args.profile_iters:  # exactly K steps and nothing else (PMC passes divide the step kernels' counters by K)
-        for _ in range(args.profile_iters):
-            L.pgx_result_release(step())
+        run_steps(args.profile_iters)
         barrier_sync(world)
         if rank == 0:
             print(json.dumps({"profile_steps": args.profile_iters}))
         return
 
-    for _ in range(args.warmup):
+    run_steps(args.warmup)
+    barrier_sync(world)
+    # one-query-at-a-time latency, untimed for the line's value: a few single steps
+    t_lat = []
+    for _ in range(3):
+        t1 = time.perf_counter()
         L.pgx_result_release(step())
+        t_lat.append(time.perf_counter() - t1)
     barrier_sync(world)
     t0 = time.perf_counter()
-    last = None
-    for i in range(args.steps):
-        r = step()
-        if i == args.steps - 1:
-            last = r
-        else:
-            L.pgx_result_release(r)
+    last = run_steps(args.steps, keep_last=True)
     barrier_sync(world)
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -298,8 +331,7 @@ def main():
     tout = (C.c_double * 3)()
     tjson = C.create_string_buffer(8192)
     N.check(L.pgx_timing_start(ctx.handle))
-    for _ in range(timing_steps):
-        L.pgx_result_release(step())
+    run_steps(timing_steps)
     N.check(L.pgx_timing_stop(ctx.handle, tout, tjson, len(tjson)))
     step_kernels = json.loads(tjson.value.decode())
     kernel_ms = tout[0] / timing_steps
@@ -347,6 +379,7 @@ def main():
     line = {
         "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True,
+        "queries_in_flight": inflight, "single_query_ms": 1e3 * min(t_lat),
         "scaling": wl.scaling, "vs_baseline": None, "dtype": "int64",
         "data": "synthetic: device-generated v1 fixed-bit segments (seed %d), dictionaries per SURVEY 8d" % wl.seed,
         "config": {"workload": wl.name + ": " + wl.description, "query": wl.query,

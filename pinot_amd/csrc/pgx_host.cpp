@@ -4392,6 +4392,12 @@ pgx_status pgx_result_release(pgx_result* r) {
   return guarded([&] { delete r; });  // an async result joins its execution first (~AsyncState)
 }
 
+struct PtrCardHash {
+  size_t operator()(const std::pair<const uint32_t*, int>& k) const {
+    return std::hash<const void*>()(k.first) ^ (size_t(k.second) * 0x9E3779B97F4A7C15ull);
+  }
+};
+
 pgx_status pgx_execute_async(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,
                              const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out) {
   return guarded([&] {
@@ -4405,12 +4411,18 @@ pgx_status pgx_execute_async(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     if (L) {
       A.binds.assign(bindings, bindings + size_t(n) * L);
       A.words.reserve(A.binds.size());
+      // one copy per distinct bitset (segments sharing a dictionary share their bindings' words, pgx_bind_predicates)
+      std::unordered_map<std::pair<const uint32_t*, int>, const uint32_t*, PtrCardHash> copied;
       for (size_t i = 0; i < A.binds.size(); ++i) {
         pgx_leaf_binding& b = A.binds[i];
         if (!b.words) continue;
         const int card = segs[i / L]->col(q->leaf_col[i % L]).card;
-        A.words.emplace_back(b.words, b.words + (card + 31) / 32);
-        b.words = A.words.back().data();
+        auto it = copied.find({b.words, card});
+        if (it == copied.end()) {
+          A.words.emplace_back(b.words, b.words + (card + 31) / 32);
+          it = copied.emplace(std::make_pair(b.words, card), A.words.back().data()).first;
+        }
+        b.words = it->second;
       }
     }
     if (opts) {

@@ -1118,6 +1118,31 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.num_planes = 3;
     shapes.push_back(s);
   }
+  {  // the C5 benchmark shape: SUM(m) over the bitmap program's doc mask GROUP BY gk (card 1000, dense LDS table)
+    JitShape s = base(10, 16, IMG_FOR16, 11);
+    s.cols.resize(5);
+    s.cols[4] = s.cols[0];                 // gk, 10 bits
+    s.cols[3] = s.cols[1];                 // m, 16 bits, FOR16 image
+    s.cols[0] = s.cols[1] = s.cols[2] = JitCol{};
+    s.cols[0].bits = 10;                   // f1, f2, f3: bitmap leaves, not decoded
+    s.cols[1].bits = 7;
+    s.cols[2].bits = 4;
+    s.leaf_col = {0, 1, 2, -1};
+    s.leaf_mode = {LEAF_NONE, LEAF_NONE, LEAF_NONE, LEAF_DOCMASK};
+    s.prog_op = {OP_LEAF, OP_STAT};
+    s.prog_arg = {3, 0};
+    s.agg_kind = {A_SUM};
+    s.agg_col = {3};
+    s.plane_op = {P_ADD_I64, P_ADD_I64};
+    s.num_planes = 2;
+    s.group_mode = G_DENSE_LDS;
+    s.gcol = {4};
+    s.gmul = {1};
+    s.dense_slots = 1000;
+    s.R = 16;
+    s.T = 1024;
+    shapes.push_back(s);
+  }
   shapes.push_back(base(8, 16, IMG_NONE, 0));
   {
     JitShape s = base(10, 16, IMG_F64, 0);
