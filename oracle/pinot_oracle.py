@@ -975,6 +975,15 @@ FN_DEFAULT = {"count": 0.0, "sum": 0.0, "min": math.inf, "max": -math.inf,
 MV_FUNCTIONS = ("countmv", "summv", "minmv", "maxmv", "avgmv")
 EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95",
                  "percentile99", "percentileest50", "percentileest90", "percentileest95", "percentileest99")
+# DistinctCountMV / DistinctCountHLLMV / MinMaxRangeMV / PercentileMV / PercentileestMV (AggregationFunctionFactory.java:
+# 48-58): the single-value function over every value of the selected docs (getMVHashCodeArray for the distinct counts)
+EXT_MV_FUNCTIONS = ("distinctcountmv", "distinctcounthllmv", "minmaxrangemv") + tuple(
+    "percentile%dmv" % p for p in (50, 90, 95, 99)) + tuple("percentileest%dmv" % p for p in (50, 90, 95, 99))
+
+
+def ext_base(fn: str) -> str:
+    """The single-value function an extended multi-value function restates over every value."""
+    return fn[:-2] if fn in EXT_MV_FUNCTIONS else fn
 
 
 # DISTINCTCOUNTHLL: stream-lib 2.7.0 HyperLogLog(log2m = HllConstants.DEFAULT_LOG2M = 8) (third-party, not vendored;
@@ -1100,7 +1109,7 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
         docs, scanned = np.nonzero(filter_mask_vectorized(seg, q.get("filter")))[0], None
     holders = []
     for a in q["aggregations"]:
-        fn = a["fn"]
+        fn = ext_base(a["fn"])
         holders.append([0.0, 0] if fn in ("avg", "avgmv") else set() if fn == "distinctcount" else
                        [0] * (1 << HLL_LOG2M) if fn in ("distinctcounthll", "fasthll") else
                        [math.inf, -math.inf] if fn == "minmaxrange" else _qdigest() if fn.startswith("percentileest")
@@ -1130,10 +1139,15 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
                     holders[k] = [holders[k][0] + (float(np.cumsum(flat)[-1]) if len(flat) else 0.0),
                                   holders[k][1] + len(flat)]
                 continue
-            if col.mv_ids is not None:
-                raise ValueError("%s over a multi-value column" % fn)
+            mvx = fn in EXT_MV_FUNCTIONS
+            if (col.mv_ids is not None) != mvx:
+                raise ValueError("%s over a %s column" % (fn, "single-value" if mvx else "multi-value"))
+            fn = ext_base(fn)
+            # the block's values: one per doc, or every value of every doc (getMVHashCodeArray / getMultiValues)
+            ids = (np.concatenate([col.mv_ids[int(d)] for d in blk]) if len(blk) else np.zeros(0, np.int64)) \
+                if mvx else col.dict_ids[blk]
             if fn in ("distinctcount", "distinctcounthll"):  # getSVHashCodeArray: (int) of each value's hashCode()
-                hc = [java_hash_code(col, int(i)) for i in col.dict_ids[blk]]
+                hc = [java_hash_code(col, int(i)) for i in ids]
                 if fn == "distinctcount":
                     holders[k].update(hc)
                 else:
@@ -1143,12 +1157,12 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
             if fn == "fasthll":  # FastHllAggregationFunction.aggregate: addAll(convertStringToHll(value)) per doc
                 if col.dtype != "STRING":
                     raise ValueError("fasthll over a non-STRING column")
-                for i in col.dict_ids[blk]:
+                for i in ids:
                     hll_add_all(holders[k], hll_from_string(col.dictionary[int(i)]))
                 continue
             if col.dtype == "STRING":  # String[] values where aggregate() requires double[]
                 raise ValueError("%s over a STRING column" % fn)
-            v = col.value_as_double(col.dict_ids[blk])
+            v = col.value_as_double(np.asarray(ids, dtype=np.int64))
             if fn == "sum":  # SumAggregationFunction.aggregate:45-56 (sequential double sum)
                 s = float(np.cumsum(v)[-1]) if len(v) else 0.0
                 holders[k] = holders[k] + s
@@ -1173,6 +1187,7 @@ def run_aggregation(seg: OSegment, q: dict, literal_filter: bool = True) -> dict
                 holders[k].extend(v.tolist())
     results = []
     for k, a in enumerate(q["aggregations"]):
+        a = dict(a, fn=ext_base(a["fn"]))
         if a["fn"] in ("count", "countmv"):
             results.append(int(holders[k]))  # MutableLongValue((long) double)
         elif a["fn"] in ("avg", "avgmv"):
@@ -1221,7 +1236,8 @@ def run_group_by(seg: OSegment, q: dict, literal_filter: bool = True) -> dict:
     gcols = [seg.columns[c] for c in q["group_by"]["columns"]]
     cards = [c.card for c in gcols]
     mode, prod = group_key_mode(cards)
-    if any(c.mv_ids is not None for c in gcols) or any(a["fn"] in MV_FUNCTIONS for a in q["aggregations"]):
+    if any(c.mv_ids is not None for c in gcols) or \
+            any(a["fn"] in MV_FUNCTIONS or a["fn"] in EXT_MV_FUNCTIONS for a in q["aggregations"]):
         return _run_group_by_mv(seg, q, docs, scanned, gcols, cards, mode)
     # Raw key = sum_j dictId_j * prod_{i<j} card_i (column 0 least significant), :230-246
     ids = np.stack([c.dict_ids[docs] for c in gcols], axis=1) if len(docs) else np.zeros((0, len(gcols)), np.int64)
@@ -1353,18 +1369,47 @@ def _run_group_by_mv(seg: OSegment, q: dict, docs, scanned, gcols, cards, mode) 
             vals = acc
         else:
             col = seg.columns[a["column"]]
-            mv = fn in MV_FUNCTIONS
+            mv = fn in MV_FUNCTIONS or fn in EXT_MV_FUNCTIONS
             if mv and col.mv_ids is None:
                 raise ValueError("%s over a single-value column" % fn)
             if not mv and col.mv_ids is not None:
                 raise ValueError("%s over a multi-value column" % fn)
-            if fn not in ("sum", "min", "max", "avg") and not mv:
-                raise ValueError("%s is not restated for multi-value group-by" % fn)
+            fn = ext_base(fn)
+
+            def dids(d):
+                return col.mv_ids[d] if mv else [col.dict_ids[d]]
 
             def dvals(d):
-                ids = col.mv_ids[d] if mv else [col.dict_ids[d]]
-                return [float(x) for x in col.value_as_double(np.asarray(ids, dtype=np.int64))]
-            if fn in ("sum", "summv"):
+                return [float(x) for x in col.value_as_double(np.asarray(dids(d), dtype=np.int64))]
+            if fn in ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange") or fn.startswith("percentile"):
+                # {DistinctCount,DistinctCountHLL,FastHll,MinMaxRange,Percentile,Percentileest}{,MV}
+                # .aggregateGroupByMV: every value of the doc into each of its keys' holders
+                vals = [None] * G
+                for d, g in per:
+                    if fn == "distinctcount":
+                        vals[g] = (vals[g] or set()) | {java_hash_code(col, int(i)) for i in dids(d)}
+                    elif fn == "distinctcounthll":
+                        vals[g] = vals[g] or [0] * (1 << HLL_LOG2M)
+                        for i in dids(d):
+                            hll_offer(vals[g], java_hash_code(col, int(i)))
+                    elif fn == "fasthll":
+                        vals[g] = vals[g] or [0] * (1 << HLL_LOG2M)
+                        for i in dids(d):
+                            hll_add_all(vals[g], hll_from_string(col.dictionary[int(i)]))
+                    elif fn == "minmaxrange":
+                        lo, hi = vals[g] or (math.inf, -math.inf)
+                        for x in dvals(d):
+                            lo, hi = min(lo, x), max(hi, x)
+                        vals[g] = (lo, hi)
+                    elif fn.startswith("percentileest"):
+                        vals[g] = vals[g] or _qdigest()
+                        for x in dvals(d):
+                            vals[g].add(int(x))
+                    else:
+                        vals[g] = (vals[g] or []) + dvals(d)
+                if fn.startswith("percentile") and not fn.startswith("percentileest"):
+                    vals = [sorted(x) for x in vals]
+            elif fn in ("sum", "summv"):
                 acc = [0.0] * G
                 for d, g in per:
                     for v in dvals(d):
@@ -1432,6 +1477,7 @@ def _qdigest():
 
 def combine_two(fn: str, a, b):
     """Legacy combineTwoValues (query/aggregation/function/{Sum,Count,Min,Max,Avg}AggregationFunction.java)."""
+    fn = ext_base(fn)
     if fn in ("count", "countmv", "summv"):
         return a + b
     if fn == "minmv":
@@ -1476,6 +1522,7 @@ def reduce_extended(fn: str, v) -> float:
     """Final value of the extended functions (query/aggregation/function/DistinctCountAggregationFunction.java:136-145,
     MinMaxRangeAggregationFunction.java:129-146, quantile/PercentileUtil.java:40-52: sorted list, element
     (int)(size * p / 100))."""
+    fn = ext_base(fn)
     if fn == "distinctcount":
         return len(v)
     if fn in ("distinctcounthll", "fasthll"):  # {DistinctCountHLL,FastHll}AggregationFunction.reduce: cardinality()
@@ -1525,7 +1572,7 @@ def combine_group_by(parts: List[dict], q: dict) -> dict:
         # PERCENTILE's DoubleArrayList IS Comparable (lexicographic, over values in merge order, which depends on
         # thread timing): that trim is not reproducible, so every group is kept here too (parity unpinned above the
         # threshold; tests stay below it).
-        if len(merged) > threshold and f not in EXT_FUNCTIONS:
+        if len(merged) > threshold and f not in EXT_FUNCTIONS and f not in EXT_MV_FUNCTIONS:
             keyf = (lambda kv: kv[1][0] / kv[1][1] if kv[1][1] else 0.0) if f == "avg" else (lambda kv: kv[1])
             items.sort(key=keyf, reverse=(f != "min"))
             items = items[:size]

@@ -37,11 +37,12 @@ def function_name(agg: dict) -> str:
     minMaxRange_<col>, percentileNN_<col> (query/aggregation/function/CountAggregationFunction.java:118-120,
     SumAggregationFunction.java:207-209, DistinctCountAggregationFunction.java:165, MinMaxRangeAggregationFunction
     .java:170, quantile/PercentileAggregationFunction.java:171)."""
-    if agg["fn"] == "count":
+    fn = base_function(agg["fn"])
+    if fn == "count":  # COUNTMV too: registered as CountAggregationFunction (AggregationFunctionRegistry.java:76)
         return "count_star"
-    if agg["fn"].startswith("percentileest"):  # DigestAggregationFunction.getFunctionName (:161-163)
-        return "percentileEst%s_%s" % (agg["fn"][len("percentileest"):], agg["column"])
-    return "%s_%s" % (_NAMES.get(agg["fn"], agg["fn"]), agg["column"])
+    if fn.startswith("percentileest"):  # DigestAggregationFunction.getFunctionName (:161-163)
+        return "percentileEst%s_%s" % (fn[len("percentileest"):], agg["column"])
+    return "%s_%s" % (_NAMES.get(fn, fn), agg["column"])
 
 
 def java_format_5f(x: float) -> str:
@@ -62,6 +63,12 @@ def java_format_5f(x: float) -> str:
 _MV_BASE = {"countmv": "count", "summv": "sum", "minmv": "min", "maxmv": "max", "avgmv": "avg"}
 
 
+def base_function(fn: str) -> str:
+    """The legacy function class a request key maps to: AggregationFunctionRegistry.java:76-91 registers every *mv key
+    with its single-value class (names, combine and reduce are the base function's)."""
+    return _MV_BASE.get(fn) or X.base_fn(fn)
+
+
 def _combine_two(fn: str, a, b):
     """combineTwoValues of the legacy functions (CountAggregationFunction.java:79-87 long add, SumAggregationFunction
     .java:168-176 double add, MinAggregationFunction.java:112-120, Max..., AvgAggregationFunction.java:116-125 pair add);
@@ -70,7 +77,7 @@ def _combine_two(fn: str, a, b):
         return b
     if b is None:
         return a
-    fn = _MV_BASE.get(fn, fn)
+    fn = base_function(fn)
     if fn in EXT_FUNCTIONS:
         return X.combine_two(fn, a, b)
     if fn == "count":
@@ -87,7 +94,7 @@ def _combine_two(fn: str, a, b):
 def _reduce(fn: str, values: Sequence):
     """AggregationFunction.reduce: count -> long sum; sum -> double sum; min / max over the default +/-inf; avg -> sum /
     count, 0.0 when no docs (AvgAggregationFunction.java:128-143)."""
-    fn = _MV_BASE.get(fn, fn)
+    fn = base_function(fn)
     if fn in EXT_FUNCTIONS:  # combine the intermediates, then the function's final value
         acc = None
         for v in values:
@@ -123,6 +130,7 @@ def _reduce(fn: str, values: Sequence):
 
 def _format(fn: str, v) -> str:
     """Long / Integer (count, distinctcount) -> toString; doubles -> %1.5f (BrokerReduceService.formatValue)."""
+    fn = base_function(fn)
     return str(int(v)) if fn in ("count", "countmv", "distinctcount", "distinctcounthll", "fasthll") \
         or fn.startswith("percentileest") \
         else java_format_5f(float(v))

@@ -55,6 +55,8 @@ extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in
                                            int cstride, unsigned long long* overflow, hipStream_t stream);
 extern "C" hipError_t pgx_launch_mv_leaf_mask(const pgx::MvLeaf* items, int nitems, int max_words, hipStream_t stream);
 extern "C" hipError_t pgx_launch_mv_aggregate(const pgx::MvAgg* items, int nitems, int max_words, hipStream_t stream);
+extern "C" hipError_t pgx_launch_mv_group(const pgx::MvGroupArgs* args, int nsegs, int max_docs, int ordered,
+                                          hipStream_t stream);
 extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
                                                 int nparts, int64_t cap, uint64_t keymask, int keybits, int64_t vbase,
                                                 const int64_t* vdict, int need_sum, int need_min, int need_max, int pack_shift,
@@ -1312,6 +1314,9 @@ struct ExecPlan {
   // selection masks for the multi-value functions (one bit per scanned row, per segment)
   bool want_selmask = false;
   DevBuf sel_buf;
+  // multi-value group-by results: per function, where its count comes from (-1: plane 0, the (doc, key) pairs; -2: its
+  // own value (COUNTMV); p >= 0: plane p (AVGMV's value count))
+  std::vector<int> g_count_plane;
   std::vector<int64_t> sel_off;       // [seg] word offset in sel_buf
   struct DmProg {
     std::vector<int> op, arg;  // RP_*; RP_LEAF arg = query leaf index
@@ -3181,7 +3186,10 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
   } else if (hash) {
     DevBuf counter(ctx, 64);
     hip_check(hipMemsetAsync(counter.p, 0, 8, st), "memset");
-    const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(slots, uint64_t(std::max<int64_t>(stats[0], 1))));
+    // at most one group per selected doc -- except multi-value group keys (several keys per doc: g_count_plane set)
+    const uint64_t cap = P.g_count_plane.empty()
+                             ? std::max<uint64_t>(1, std::min<uint64_t>(slots, uint64_t(std::max<int64_t>(stats[0], 1))))
+                             : slots;
     DevBuf oslot(ctx, cap * 8), oplanes(ctx, cap * K.num_planes * 8);
     PGX_LAUNCH(st, "pgx_compact", pgx_launch_compact(K.table, slots, K.num_planes, devp(counter), oslot.as<int64_t>(), devp(oplanes), cap,
                                  st),
@@ -3243,6 +3251,9 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
       R->g_count[a][oi] = cnt;
       if (K.agg_kind[a] == A_COUNT) R->g_value[a][oi] = double(cnt);
       else R->g_value[a][oi] = decode_plane(K.plane_op[a + 1], K.agg_fp[a], planes[(a + 1) * ng + i], K.agg_kind[a]);
+      const int cp = P.g_count_plane.empty() ? -1 : P.g_count_plane[a];
+      if (cp == -2) R->g_count[a][oi] = int64_t(planes[(a + 1) * ng + i]);
+      else if (cp >= 0) R->g_count[a][oi] = int64_t(planes[uint64_t(cp) * ng + i]);
     }
   }
 }
@@ -3888,6 +3899,245 @@ void run_mv(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, c
   }
 }
 
+// Group-by over multi-value group columns and/or with multi-value functions (DefaultGroupKeyGenerator.java:268-608,
+// DefaultGroupByExecutor.java:154-196).  The single-value part of the query (its filter) runs through the query kernels,
+// which write every scanned row's selection bit; pgx_mv_group then expands each selected doc into its group keys (one
+// per combination of its group columns' values) and applies every function's contribution to each; MINMV / MAXMV,
+// whose reference fold depends on doc order, run in pgx_mv_group_ordered.  Key spaces and result decoding are the
+// single-value ones (dense slots, or 64 / 128-bit hash keys), so finish_result decodes the table as usual.
+void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
+                  uint32_t xflags, pgx_result* R, hipStream_t st) {
+  if (!jit_enabled()) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by needs the query kernels");
+  const int na = int(q.agg_fn.size()), ng = int(q.group_cols.size());
+  if (ng < 1 || ng > kMaxGroupCols) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by: group column count");
+  std::vector<int8_t> mvf(na), fpv(na, 0), cntp(na, -1);
+  int extra = 0;
+  bool ordered = false;
+  for (int a = 0; a < na; ++a) {
+    const int f = q.agg_fn[a];
+    mvf[a] = int8_t(f);  // pgx_agg_fn and MvFnKind share their numbering
+    if (f == PGX_COUNT) continue;
+    const bool mvfn = f >= PGX_COUNTMV;
+    for (int s = 0; s < n; ++s) {
+      const StagedColumn& c = segs[s]->col(q.agg_col[a]);
+      if (c.is_mv != mvfn)
+        fail(PGX_ERR_UNSUPPORTED, std::string(mvfn ? "multi-value function on single-value column "
+                                                   : "single-value aggregation on multi-value column ") + c.name);
+      if (c.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + c.name);
+    }
+    const StagedColumn& c0 = segs[0]->col(q.agg_col[a]);
+    fpv[a] = f != PGX_COUNTMV && (c0.data_type == PGX_FLOAT || c0.data_type == PGX_DOUBLE);
+    if (f == PGX_AVGMV) cntp[a] = int8_t(1 + na + extra++);
+    ordered = ordered || f == PGX_MINMV || f == PGX_MAXMV;
+  }
+  if (na + extra > kMaxAggs) fail(PGX_ERR_UNSUPPORTED, "too many functions for a multi-value group-by");
+
+  // 1. selection bits of the single-value filter
+  pgx_query qs = q;
+  qs.flags |= PGX_Q_NO_STAR_TREE;
+  qs.agg_fn.assign(1, PGX_COUNT);
+  qs.agg_col.assign(1, "");
+  qs.group_cols.clear();
+  qs.key_domain.clear();
+  ExecPlan P;
+  P.want_selmask = true;
+  plan_query(ctx, qs, segs, n, bindings, xflags, P);
+  P.sel_off.assign(n, 0);
+  int64_t words = 0;
+  int max_docs = 0;
+  for (int s = 0; s < n; ++s) {
+    P.sel_off[s] = words;
+    words += (P.ksegs[s].num_docs + 31) / 32 + 1;
+    max_docs = std::max(max_docs, P.ksegs[s].num_docs);
+  }
+  P.sel_buf = DevBuf(ctx, size_t(std::max<int64_t>(words, 1)) * 4);
+  hip_check(hipMemsetAsync(P.sel_buf.p, 0, size_t(std::max<int64_t>(words, 1)) * 4, st), "selection masks");
+  ExecBuffers B;
+  upload_plan(ctx, P, B, st);
+  plan_jit(ctx, qs, segs, n, P, B);
+  if (P.jit.empty() || !P.jit[0].fn) {
+    bool empty = true;  // every segment empty: nothing scanned, no groups
+    for (int s = 0; s < n; ++s) empty = empty && P.ksegs[s].num_docs == 0;
+    if (!empty) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by needs the query kernels");
+  }
+  alloc_outputs(ctx, P, B, nullptr, 0);
+  reset_outputs(P, B, st);
+  launch_scan(P, st);
+
+  // 2. key space: global dictionaries per group column; dense slots, or packed 64 / 128-bit hash keys
+  KQuery& K = P.kq;
+  P.gdicts.clear();
+  P.gbits.clear();
+  uint64_t prod = 1;
+  bool overflow = false;
+  int total_bits = 0;
+  for (int g = 0; g < ng; ++g) {
+    P.gdicts.push_back(group_dict(q, segs, n, g));
+    const int64_t gc = std::max<int64_t>(1, P.gdicts.back().card);
+    if (!overflow && prod > (uint64_t(1) << 62) / uint64_t(gc)) overflow = true;
+    if (!overflow) prod *= uint64_t(gc);
+    P.gbits.push_back(bits_for(gc));
+    total_bits += P.gbits.back();
+  }
+  P.mode_ref = reference_mode(q, segs[0]);
+  K.num_gcols = ng;
+  const uint64_t kDenseMax = uint64_t(1) << 22;
+  if (!overflow && prod <= kDenseMax && !(xflags & PGX_X_FORCE_HASH)) {
+    uint64_t mul = 1;
+    for (int g = 0; g < ng; ++g) {
+      K.gmul[g] = mul;
+      mul *= uint64_t(P.gdicts[g].card);
+    }
+    K.group_mode = G_DENSE_GLOBAL;
+    P.dense_slots = prod;
+  } else if (total_bits <= 126) {
+    int sh = 0;
+    bool hi = false;
+    for (int g = 0; g < ng; ++g) {
+      if (!hi && sh + P.gbits[g] > 63) {
+        hi = true;
+        sh = 0;
+      }
+      K.gshift[g] = sh;
+      K.ghi[g] = hi;
+      sh += P.gbits[g];
+    }
+    K.group_mode = hi ? G_HASH128 : G_HASH64;
+  } else {
+    fail(PGX_ERR_UNSUPPORTED, "group key wider than 126 bits");
+  }
+  const bool dense = K.group_mode == G_DENSE_GLOBAL;
+  if (ordered && !dense) fail(PGX_ERR_UNSUPPORTED, "MINMV / MAXMV under GROUP BY need a dense key space");
+  K.num_aggs = na;
+  K.num_planes = 1 + na + extra;
+  K.plane_op[0] = P_ADD_I64;
+  P.g_count_plane.assign(na, -1);
+  for (int a = 0; a < na; ++a) {
+    const int f = q.agg_fn[a];
+    K.agg_fp[a] = fpv[a];
+    K.agg_kind[a] = f == PGX_COUNT ? A_COUNT : (f == PGX_MIN || f == PGX_MINMV) ? A_MIN
+                  : (f == PGX_MAX || f == PGX_MAXMV) ? A_MAX : (f == PGX_AVG || f == PGX_AVGMV) ? A_AVG : A_SUM;
+    K.plane_op[a + 1] = K.agg_kind[a] == A_MIN ? P_MIN_ORD : K.agg_kind[a] == A_MAX ? P_MAX_ORD
+                      : fpv[a] ? P_ADD_F64 : P_ADD_I64;
+    if (f == PGX_COUNTMV) P.g_count_plane[a] = -2;
+    if (f == PGX_AVGMV) P.g_count_plane[a] = cntp[a];
+  }
+  for (int p = 1 + na; p < K.num_planes; ++p) K.plane_op[p] = P_ADD_I64;
+  std::vector<std::string> proj;  // numEntriesScannedPostFilter: docs x projected columns
+  for (int a = 0; a < na; ++a)
+    if (q.agg_fn[a] != PGX_COUNT && std::find(proj.begin(), proj.end(), q.agg_col[a]) == proj.end())
+      proj.push_back(q.agg_col[a]);
+  for (const auto& g : q.group_cols)
+    if (std::find(proj.begin(), proj.end(), g) == proj.end()) proj.push_back(g);
+  P.n_proj = int(proj.size());
+
+  // 3. per-segment descriptors, remap tables (one device copy per distinct table)
+  std::vector<int32_t> blob;
+  std::map<const std::vector<int32_t>*, size_t> roff;
+  for (int g = 0; g < ng; ++g)
+    if (!P.gdicts[g].identity)
+      for (int s = 0; s < n; ++s) {
+        const std::vector<int32_t>* rm = P.gdicts[g].remap[s].get();
+        if (rm && !roff.count(rm)) {
+          roff[rm] = blob.size();
+          blob.insert(blob.end(), rm->begin(), rm->end());
+        }
+      }
+  DevBuf rdev(ctx, std::max<size_t>(1, blob.size()) * 4);
+  if (!blob.empty())
+    hip_check(hipMemcpyAsync(rdev.p, blob.data(), blob.size() * 4, hipMemcpyHostToDevice, st), "remap H2D");
+  std::vector<MvGroupSeg> hs(n);
+  for (int s = 0; s < n; ++s) {
+    MvGroupSeg& m = hs[s];
+    m = MvGroupSeg{};
+    m.sel = P.sel_buf.as<uint32_t>() + P.sel_off[s];
+    m.num_docs = P.ksegs[s].num_docs;
+    for (int g = 0; g < ng; ++g) {
+      const StagedColumn& c = segs[s]->col(q.group_cols[g]);
+      m.g[g].vals = c.fwd;
+      m.g[g].start = c.is_mv ? c.mv_start.as<const int32_t>() : nullptr;
+      m.g[g].bits = c.bits;
+      if (!P.gdicts[g].identity && P.gdicts[g].remap[s])
+        m.g[g].remap = rdev.as<int32_t>() + roff[P.gdicts[g].remap[s].get()];
+    }
+    for (int a = 0; a < na; ++a) {
+      if (q.agg_fn[a] == PGX_COUNT) continue;
+      const StagedColumn& c = segs[s]->col(q.agg_col[a]);
+      m.a[a].vals = c.fwd;
+      m.a[a].start = c.is_mv ? c.mv_start.as<const int32_t>() : nullptr;
+      m.a[a].dict = c.dict_dev;
+      m.a[a].bits = c.bits;
+    }
+  }
+  DevBuf sdev(ctx, std::max<size_t>(1, hs.size()) * sizeof(MvGroupSeg));
+  hip_check(hipMemcpyAsync(sdev.p, hs.data(), hs.size() * sizeof(MvGroupSeg), hipMemcpyHostToDevice, st), "MV segs");
+
+  // 4. table + launch (hash tables retried bigger on overflow)
+  uint64_t slots = dense ? P.dense_slots : initial_hash_cap(segs, n, P);
+  MvGroupArgs A{};
+  DevBuf adev(ctx, sizeof(MvGroupArgs)), ovf(ctx, 64), ord;
+  for (int attempt = 0;; ++attempt) {
+    B.table = DevBuf(ctx, slots * K.num_planes * 8);
+    K.table = devp(B.table);
+    K.keys = nullptr;
+    K.key_state = nullptr;
+    uint64_t kw = 0;
+    if (!dense) {
+      K.hash_cap = slots;
+      P.hash_cap = slots;
+      kw = K.group_mode == G_HASH128 ? 2 * slots : slots;
+      B.keys = DevBuf(ctx, kw * 8);
+      K.keys = devp(B.keys);
+      if (K.group_mode == G_HASH128) {
+        B.key_state = DevBuf(ctx, slots * 4);
+        K.key_state = B.key_state.as<unsigned int>();
+      }
+    } else {
+      K.dense_slots = slots;
+    }
+    PGX_LAUNCH(st, "pgx_init_planes", pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state,
+                                                             st),
+               "init planes");
+    if (ordered) {
+      const uint64_t bytes = uint64_t(n) * na * slots * 8;
+      if (bytes > (uint64_t(1) << 30)) fail(PGX_ERR_UNSUPPORTED, "MINMV / MAXMV under GROUP BY: key space too large");
+      ord = DevBuf(ctx, bytes);
+    }
+    A.segs = sdev.as<MvGroupSeg>();
+    A.nsegs = n;
+    A.ngcols = ng;
+    A.naggs = na;
+    A.group_mode = K.group_mode;
+    for (int a = 0; a < na; ++a) {
+      A.fn[a] = mvf[a];
+      A.fp[a] = fpv[a];
+      A.cnt_plane[a] = cntp[a];
+    }
+    for (int g = 0; g < ng; ++g) {
+      A.gmul[g] = K.gmul[g];
+      A.gshift[g] = K.gshift[g];
+      A.ghi[g] = K.ghi[g];
+    }
+    A.slots = slots;
+    A.table = K.table;
+    A.keys = K.keys;
+    A.key_state = K.key_state;
+    A.overflow = devp(ovf);
+    A.ord = ordered ? devp(ord) : nullptr;
+    hip_check(hipMemsetAsync(ovf.p, 0, 8, st), "memset");
+    hip_check(hipMemcpyAsync(adev.p, &A, sizeof A, hipMemcpyHostToDevice, st), "MV group args");
+    PGX_LAUNCH(st, "pgx_mv_group", pgx_launch_mv_group(adev.as<MvGroupArgs>(), n, max_docs, ordered ? 1 : 0, st),
+               "multi-value group-by");
+    unsigned long long lost = 0;
+    hip_check(hipMemcpyAsync(&lost, ovf.p, 8, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    if (!lost) break;
+    if (dense || attempt >= 4 || slots >= (uint64_t(1) << 30)) fail(PGX_ERR_OOM, "multi-value group-by hash table");
+    slots *= 4;
+  }
+  finish_result(ctx, q, P, B, segs, n, st, R, nullptr);
+}
+
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                const pgx_exec_opts* opts, pgx_result* R, const Domain* dom = nullptr) {
   HostProf hp;
@@ -3895,12 +4145,21 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   struct Unmark { ~Unmark() { g_prof_mark = nullptr; } } unmark;
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
   const uint32_t xflags = opts ? opts->flags : 0;
-  for (int fn : q.agg_fn)
-    if (fn >= PGX_COUNTMV) {
-      if (dom || (opts && opts->dense_out)) fail(PGX_ERR_UNSUPPORTED, "multi-value functions across devices");
-      run_mv(ctx, q, segs, n, bindings, xflags, R, st);
-      return;
-    }
+  bool mv_group = false;  // a multi-value group column: key expansion per doc
+  for (const auto& g : q.group_cols)
+    for (int s = 0; s < n && !mv_group; ++s) mv_group = segs[s]->col(g).is_mv;
+  bool mv_fn = false;
+  for (int fn : q.agg_fn) mv_fn = mv_fn || fn >= PGX_COUNTMV;
+  if (mv_group || (mv_fn && !q.group_cols.empty())) {
+    if (dom || (opts && opts->dense_out)) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by across devices");
+    run_mv_group(ctx, q, segs, n, bindings, xflags, R, st);
+    return;
+  }
+  if (mv_fn) {
+    if (dom || (opts && opts->dense_out)) fail(PGX_ERR_UNSUPPORTED, "multi-value functions across devices");
+    run_mv(ctx, q, segs, n, bindings, xflags, R, st);
+    return;
+  }
   if (!dom && run_batched(ctx, q, segs, n, bindings, opts, R, st, xflags, hp)) return;
   ExecPlan P;
   plan_query(ctx, q, segs, n, bindings, xflags, P, dom);
@@ -4595,10 +4854,11 @@ pgx_status pgx_result_trim(const pgx_result* r, int32_t fn, int64_t* idx, int64_
       const auto& v = r->g_value[fn];
       const auto& c = r->g_count[fn];
       auto key = [&](int64_t i) -> double {
-        if (f == PGX_AVG) return c[i] ? v[i] / double(c[i]) : 0.0;  // AvgPair compares by ratio
+        if (f == PGX_AVG || f == PGX_AVGMV) return c[i] ? v[i] / double(c[i]) : 0.0;  // AvgPair compares by ratio
         return v[i];
       };
-      auto cmp = [&](int64_t a, int64_t b) { return (f == PGX_MIN) ? key(a) < key(b) : key(a) > key(b); };
+      const bool asc = f == PGX_MIN || f == PGX_MINMV;
+      auto cmp = [&](int64_t a, int64_t b) { return asc ? key(a) < key(b) : key(a) > key(b); };
       order.resize(r->num_groups);
       std::iota(order.begin(), order.end(), 0);
       std::nth_element(order.begin(), order.begin() + size, order.end(), cmp);

@@ -71,6 +71,45 @@ struct MvAgg {
   int32_t pad;
 };
 
+// Group-by with multi-value group columns and/or multi-value functions (DefaultGroupKeyGenerator.java:475-608
+// generateKeysForDocId*, DefaultGroupByExecutor.java:154-196 aggregateGroupByMV): per selected doc, one group key per
+// combination of its group columns' values; every key receives the doc's contribution of every function.
+struct MvGCol {                // one group-by or aggregated column of one segment
+  const uint32_t* vals;        // single-value forward index, or the multi-value values section
+  const int32_t* start;        // multi-value: doc starts (num_docs + 1); null for single-value
+  const int32_t* remap;        // group column: segment dictId -> global id (null: identity)
+  const void* dict;            // aggregated column: int64 / double per dictId
+  int32_t bits;
+  int32_t pad;
+};
+struct MvGroupSeg {
+  const uint32_t* sel;         // selected docs (query kernel selection bits, bit d & 31 of word d >> 5)
+  int32_t num_docs;
+  int32_t pad;
+  MvGCol g[kMaxGroupCols];
+  MvGCol a[kMaxAggs];
+};
+enum MvFnKind : int8_t { MVF_COUNT = 0, MVF_SUM = 1, MVF_MIN = 2, MVF_MAX = 3, MVF_AVG = 4, MVF_COUNTMV = 5,
+                         MVF_SUMMV = 6, MVF_MINMV = 7, MVF_MAXMV = 8, MVF_AVGMV = 9 };
+struct MvGroupArgs {
+  const MvGroupSeg* segs;
+  int32_t nsegs;
+  int32_t ngcols, naggs;
+  int32_t group_mode;          // G_DENSE_GLOBAL, G_HASH64 or G_HASH128
+  int8_t fn[kMaxAggs];         // MvFnKind
+  int8_t fp[kMaxAggs];         // FLOAT / DOUBLE values
+  int8_t cnt_plane[kMaxAggs];  // AVGMV: the plane of its value count (else -1)
+  uint64_t gmul[kMaxGroupCols];
+  int32_t gshift[kMaxGroupCols];
+  int32_t ghi[kMaxGroupCols];
+  uint64_t slots;              // dense slots or hash capacity (power of two)
+  unsigned long long* table;   // planes x slots
+  unsigned long long* keys;    // hash keys (64-bit, or lo / hi pairs)
+  unsigned int* key_state;     // hash128 slot states
+  unsigned long long* overflow;
+  unsigned long long* ord;     // MINMV / MAXMV per-segment holders: [seg][agg][slot] (ordered encodings)
+};
+
 // Statistics automaton over one segment's leaf masks (pgx_kernels.hip pgx_fsm_chunks / pgx_fsm_compose).
 struct FsmSeg {
   const uint32_t* lmask;       // leaf l, row r: bit (r & 31) of word [l * words + (r >> 5)]

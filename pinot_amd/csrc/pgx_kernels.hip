@@ -1407,6 +1407,221 @@ __global__ void __launch_bounds__(256) pgx_mv_aggregate(const MvAgg* __restrict_
 }
 
 // ---------------------------------------------------------------------------------------------
+// Group-by over multi-value group columns and/or with multi-value functions (DefaultGroupKeyGenerator.java:475-608,
+// DefaultGroupByExecutor.java:154-196).  One thread per selected doc: the doc's contribution to every function is
+// folded once (SV: its value; COUNTMV: its value count; SUMMV / AVGMV: sum and count of its values), then every key of
+// the doc -- one per combination of its group columns' values, duplicates included, as generateKeysForDocId* builds
+// them -- receives it (COUNT: 1 per key, CountAggregationFunction.java:81-90; Sum/Min/Max/Avg.aggregateGroupByMV).
+// Keys follow the single-value layouts: dense slot = sum gid_g * mul_g, hash keys gid_g << shift_g.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ int64_t mv_slot64(unsigned long long* keys, uint64_t cap, uint64_t key) {
+  const uint64_t mask = cap - 1;
+  uint64_t h = mix64(key) & mask;
+  for (uint64_t probe = 0; probe < cap; ++probe) {
+    const unsigned long long prev = atomicCAS(keys + h, kEmptyKey, static_cast<unsigned long long>(key));
+    if (prev == kEmptyKey || prev == key) return static_cast<int64_t>(h);
+    h = (h + 1) & mask;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ int64_t mv_slot128(unsigned long long* keys, unsigned int* key_state, uint64_t cap,
+                                              uint64_t klo, uint64_t khi) {
+  const uint64_t mask = cap - 1;
+  uint64_t h = mix64(klo ^ mix64(khi)) & mask;
+  uint64_t probes = 0;
+  while (probes < cap) {
+    const unsigned int st = atomicCAS(key_state + h, 0u, 1u);
+    if (st == 0u) {
+      __hip_atomic_store(keys + 2 * h, klo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(keys + 2 * h + 1, khi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+      atomicExch(key_state + h, 2u);
+      return static_cast<int64_t>(h);
+    }
+    if (st == 2u) {
+      const unsigned long long a = __hip_atomic_load(keys + 2 * h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long b = __hip_atomic_load(keys + 2 * h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (a == klo && b == khi) return static_cast<int64_t>(h);
+      h = (h + 1) & mask;
+      ++probes;
+    }
+  }
+  return -1;
+}
+
+
+// The doc's group keys, in generateKeysForDocId* combination order, one callback per key: f(dense slot or packed lo,
+// packed hi).  Returns false when a multi-value group column holds no value (no key).
+template <typename F>
+__device__ __forceinline__ bool mv_for_each_key(const MvGroupArgs& A, const MvGroupSeg& S, int d, F&& f) {
+  int nv[kMaxGroupCols], base[kMaxGroupCols], idx[kMaxGroupCols];
+  uint32_t sv[kMaxGroupCols];
+#pragma unroll
+  for (int g = 0; g < kMaxGroupCols; ++g) {
+    nv[g] = 1;
+    base[g] = 0;
+    idx[g] = 0;
+    sv[g] = 0;
+    if (g >= A.ngcols) continue;
+    const MvGCol& c = S.g[g];
+    if (c.start) {
+      base[g] = c.start[d];
+      nv[g] = c.start[d + 1] - base[g];
+      if (nv[g] <= 0) return false;
+    } else {
+      sv[g] = mv_value(c.vals, d, c.bits);
+    }
+  }
+  for (;;) {
+    uint64_t lo = 0, hi = 0;
+#pragma unroll
+    for (int g = 0; g < kMaxGroupCols; ++g) {
+      if (g >= A.ngcols) continue;
+      const MvGCol& c = S.g[g];
+      uint32_t id = c.start ? mv_value(c.vals, base[g] + idx[g], c.bits) : sv[g];
+      if (c.remap) id = static_cast<uint32_t>(c.remap[id]);
+      if (A.group_mode == G_DENSE_GLOBAL) lo += static_cast<uint64_t>(id) * A.gmul[g];
+      else if (A.ghi[g]) hi |= static_cast<uint64_t>(id) << A.gshift[g];
+      else lo |= static_cast<uint64_t>(id) << A.gshift[g];
+    }
+    f(lo, hi);
+    int g = 0;  // odometer over the multi-value columns, column 0 fastest
+    for (; g < A.ngcols; ++g) {
+      if (++idx[g] < nv[g]) break;
+      idx[g] = 0;
+    }
+    if (g == A.ngcols) return true;
+  }
+}
+
+__global__ void __launch_bounds__(256) pgx_mv_group(const MvGroupArgs* __restrict__ Ap) {
+  const MvGroupArgs& A = *Ap;
+  const int s = static_cast<int>(blockIdx.y);
+  if (s >= A.nsegs) return;
+  const MvGroupSeg& S = A.segs[s];
+  const int d = static_cast<int>(blockIdx.x) * 256 + static_cast<int>(threadIdx.x);
+  if (d >= S.num_docs || !((S.sel[d >> 5] >> (d & 31)) & 1u)) return;
+  // the doc's contribution per function: enc (plane encoding) and cnt (AVGMV value count)
+  unsigned long long enc[kMaxAggs];
+  long long cnt[kMaxAggs];
+#pragma unroll
+  for (int a = 0; a < kMaxAggs; ++a) {
+    enc[a] = 0;
+    cnt[a] = 0;
+    if (a >= A.naggs) continue;
+    const MvGCol& c = S.a[a];
+    const int fn = A.fn[a];
+    const bool fp = A.fp[a] != 0;
+    if (fn == MVF_COUNT || fn == MVF_MINMV || fn == MVF_MAXMV) continue;  // MINMV / MAXMV: pgx_mv_group_ordered
+    if (fn <= MVF_AVG) {  // single-value column: the doc's value
+      const uint32_t id = mv_value(c.vals, d, c.bits);
+      if (fp) {
+        const double v = static_cast<const double*>(c.dict)[id];
+        enc[a] = (fn == MVF_MIN || fn == MVF_MAX) ? ord_f64(v) : static_cast<unsigned long long>(__double_as_longlong(v));
+      } else {
+        const int64_t v = static_cast<const int64_t*>(c.dict)[id];
+        enc[a] = (fn == MVF_MIN || fn == MVF_MAX) ? ord_i64(v) : static_cast<unsigned long long>(v);
+      }
+      continue;
+    }
+    const int b0 = c.start[d], b1 = c.start[d + 1];
+    cnt[a] = b1 - b0;
+    if (fn == MVF_COUNTMV) {
+      enc[a] = static_cast<unsigned long long>(b1 - b0);
+      continue;
+    }
+    double ds = 0.0;  // SUMMV / AVGMV: the doc's values in order (SumMVAggregationFunction.java:98-112)
+    int64_t is = 0;
+    for (int i = b0; i < b1; ++i) {
+      const uint32_t id = mv_value(c.vals, i, c.bits);
+      if (fp) ds += static_cast<const double*>(c.dict)[id];
+      else is += static_cast<const int64_t*>(c.dict)[id];
+    }
+    enc[a] = fp ? static_cast<unsigned long long>(__double_as_longlong(ds)) : static_cast<unsigned long long>(is);
+  }
+  mv_for_each_key(A, S, d, [&](uint64_t lo, uint64_t hi) {
+    int64_t slot;
+    if (A.group_mode == G_DENSE_GLOBAL) slot = static_cast<int64_t>(lo);
+    else if (A.group_mode == G_HASH64) slot = mv_slot64(A.keys, A.slots, lo);
+    else slot = mv_slot128(A.keys, A.key_state, A.slots, lo, hi);
+    if (slot < 0) {
+      atomicAdd(A.overflow, 1ull);
+      return;
+    }
+    atomicAdd(A.table + slot, 1ull);  // plane 0: (doc, key) pairs = COUNT
+#pragma unroll
+    for (int a = 0; a < kMaxAggs; ++a) {
+      if (a >= A.naggs) continue;
+      const int fn = A.fn[a];
+      unsigned long long* p = A.table + static_cast<uint64_t>(a + 1) * A.slots + slot;
+      const bool fp = A.fp[a] != 0;
+      switch (fn) {
+        case MVF_SUM: case MVF_AVG: case MVF_SUMMV: case MVF_AVGMV:
+          if (fp) atomicAdd(reinterpret_cast<double*>(p), __longlong_as_double(static_cast<long long>(enc[a])));
+          else atomicAdd(p, enc[a]);
+          if (fn == MVF_AVGMV)
+            atomicAdd(A.table + static_cast<uint64_t>(A.cnt_plane[a]) * A.slots + slot,
+                      static_cast<unsigned long long>(cnt[a]));
+          break;
+        case MVF_COUNTMV: atomicAdd(p, enc[a]); break;
+        case MVF_MIN: atomicMin(p, enc[a]); break;
+        case MVF_MAX: atomicMax(p, enc[a]); break;
+        default: break;
+      }
+    }
+  });
+}
+
+// MINMV / MAXMV under GROUP BY (MinMVAggregationFunction.java:76-91 aggregateGroupBySV, :103-119 aggregateGroupByMV;
+// MaxMV alike): the holder's value is read ONCE per (doc, key) and every value of the doc below (above) it replaces the
+// holder, so a doc leaves the LAST such value in its value order -- an order-dependent fold, not a minimum.  One
+// workgroup walks one segment's selected docs in doc order; thread t owns the dense slots s with s % 256 == t and
+// applies the fold to them only, so every key sees its docs in order with no atomics.  Holders are that segment's
+// dictIds (sorted dictionaries: dictId order = value order); the per-segment results merge into the table with the
+// combine's min / max (combineTwoValues).
+__global__ void __launch_bounds__(256) pgx_mv_group_ordered(const MvGroupArgs* __restrict__ Ap) {
+  const MvGroupArgs& A = *Ap;
+  const int s = static_cast<int>(blockIdx.x);
+  if (s >= A.nsegs) return;
+  const MvGroupSeg& S = A.segs[s];
+  const int tid = static_cast<int>(threadIdx.x);
+  int64_t* hold = reinterpret_cast<int64_t*>(A.ord) + static_cast<uint64_t>(s) * A.naggs * A.slots;
+  for (uint64_t sl = tid; sl < A.slots; sl += 256)
+    for (int a = 0; a < A.naggs; ++a) hold[a * A.slots + sl] = A.fn[a] == MVF_MINMV ? INT64_MAX : -1;
+  for (int d = 0; d < S.num_docs; ++d) {
+    if (!((S.sel[d >> 5] >> (d & 31)) & 1u)) continue;
+    mv_for_each_key(A, S, d, [&](uint64_t lo, uint64_t) {
+      if (static_cast<int>(lo & 255u) != tid) return;
+      for (int a = 0; a < A.naggs; ++a) {
+        const int fn = A.fn[a];
+        if (fn != MVF_MINMV && fn != MVF_MAXMV) continue;
+        const MvGCol& c = S.a[a];
+        int64_t* h = hold + a * A.slots + lo;
+        const int64_t old = *h;
+        for (int i = c.start[d]; i < c.start[d + 1]; ++i) {
+          const int64_t id = mv_value(c.vals, i, c.bits);
+          if (fn == MVF_MINMV ? id < old : id > old) *h = id;
+        }
+      }
+    });
+  }
+  for (uint64_t sl = tid; sl < A.slots; sl += 256)
+    for (int a = 0; a < A.naggs; ++a) {
+      const int fn = A.fn[a];
+      if (fn != MVF_MINMV && fn != MVF_MAXMV) continue;
+      const int64_t id = hold[a * A.slots + sl];
+      if (id == INT64_MAX || id < 0) continue;
+      const MvGCol& c = S.a[a];
+      const unsigned long long e = A.fp[a] ? ord_f64(static_cast<const double*>(c.dict)[id])
+                                           : ord_i64(static_cast<const int64_t*>(c.dict)[id]);
+      unsigned long long* p = A.table + static_cast<uint64_t>(a + 1) * A.slots + sl;
+      if (fn == MVF_MINMV) atomicMin(p, e);
+      else atomicMax(p, e);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // High-cardinality group-by (LONG_MAP semantics, DefaultGroupKeyGenerator.java:239-246 / :429-441): the reference
 // probes a Long2IntOpenHashMap per doc; at 10^7 groups a device-wide hash table turns every row into random HBM atomics.
 // Instead the generated scan kernel emits one packed record per selected row (key | value << keybits), two radix
@@ -1950,5 +2165,14 @@ extern "C" hipError_t pgx_launch_mv_aggregate(const pgx::MvAgg* items, int nitem
   hipLaunchKernelGGL(pgx::pgx_mv_aggregate, dim3(static_cast<unsigned>((max_words + 255) / 256),
                                                    static_cast<unsigned>(nitems)),
                      dim3(256), 0, stream, items, nitems);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_mv_group(const pgx::MvGroupArgs* args, int nsegs, int max_docs, int ordered,
+                                          hipStream_t stream) {
+  if (nsegs <= 0 || max_docs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pgx::pgx_mv_group, dim3(static_cast<unsigned>((max_docs + 255) / 256), static_cast<unsigned>(nsegs)),
+                     dim3(256), 0, stream, args);
+  if (ordered) hipLaunchKernelGGL(pgx::pgx_mv_group_ordered, dim3(static_cast<unsigned>(nsegs)), dim3(256), 0, stream, args);
   return hipGetLastError();
 }

@@ -360,8 +360,8 @@ class DataTable:
 def _base_fn(fn: str) -> str:
     """The function whose intermediate an MV function carries: AggregationFunctionRegistry maps countmv / summv / minmv
     / maxmv / avgmv to the Count / Sum / Min / Max / Avg functions (AggregationFunctionRegistry.java:76-80)."""
-    from .broker import _MV_BASE
-    return _MV_BASE.get(fn, fn)
+    from .broker import base_function
+    return base_function(fn)
 
 
 def _to_object(fn: str, v):

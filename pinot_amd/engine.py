@@ -628,9 +628,9 @@ def decode_result(q: _Query, r, segments: Sequence[IndexSegment], trim: bool = F
         v = np.zeros(max(n, 1), dtype=np.float64)
         c = np.zeros(max(n, 1), dtype=np.int64)
         N.check(L.pgx_result_group_values(r, i, v.ctypes.data, c.ctypes.data))
-        if fn == "count":
+        if fn in ("count", "countmv"):
             vals.append([int(x) for x in c[:n]])
-        elif fn == "avg":
+        elif fn in ("avg", "avgmv"):  # AvgPair(sum, count): count = values for AVGMV
             vals.append([(float(a), int(b)) for a, b in zip(v[:n], c[:n])])
         else:
             vals.append([float(x) for x in v[:n]])
@@ -680,7 +680,8 @@ def trimmed_maps(q: _Query, r, segments: Sequence[IndexSegment]) -> List[Dict[st
         m = {}
         for j in range(len(v)):
             key = "\t".join(render_key(q, segments, g, int(si[g, j]), int(di[g, j])) for g in range(len(q.group_cols)))
-            m[key] = int(c[j]) if fn == "count" else ((float(v[j]), int(c[j])) if fn == "avg" else float(v[j]))
+            m[key] = int(c[j]) if fn in ("count", "countmv") else (
+                (float(v[j]), int(c[j])) if fn in ("avg", "avgmv") else float(v[j]))
         maps.append(m)
     return maps
 
@@ -730,8 +731,8 @@ def render_group_maps(q: _Query, segments: Sequence[IndexSegment], key_cols, val
         m = {}
         for j in kept[i]:
             key = "\t".join(_render_value(dt, c[j]) for dt, c in zip(types, key_cols))
-            m[key] = int(cnts[i, j]) if fn == "count" else (
-                (float(vals[i, j]), int(cnts[i, j])) if fn == "avg" else float(vals[i, j]))
+            m[key] = int(cnts[i, j]) if fn in ("count", "countmv") else (
+                (float(vals[i, j]), int(cnts[i, j])) if fn in ("avg", "avgmv") else float(vals[i, j]))
         maps.append(m)
     return maps
 

@@ -31,10 +31,18 @@ from . import engine as E
 from . import hll as HLL
 from . import qdigest as QD
 from . import native as N
-from .pql import EXT_FUNCTIONS
+from .pql import EXT_FUNCTIONS, EXT_MV_FUNCTIONS
 
 
 _HIST_FNS = ("distinctcount", "distinctcounthll", "fasthll")
+
+
+def base_fn(fn: str) -> str:
+    """DISTINCTCOUNTMV, DISTINCTCOUNTHLLMV, MINMAXRANGEMV, PERCENTILEnnMV, PERCENTILEESTnnMV are their single-value
+    functions over every value of a multi-value column (DistinctCountMVAggregationFunction.java aggregate: every value's
+    hash code; MinMaxRangeMV / PercentileMV / PercentileestMV: every value): the ``GROUP BY c`` histogram of a
+    multi-value c counts one entry per value occurrence (pgx_mv_group), which is exactly that multiset."""
+    return fn[:-2] if fn in EXT_MV_FUNCTIONS else fn
 
 
 def has_extended(request: dict) -> bool:
@@ -132,8 +140,8 @@ def _base_request(request: dict):
         if fn == "minmaxrange":
             base += [{"fn": "min", "column": a["column"]}, {"fn": "max", "column": a["column"]}]
             slot.append((len(base) - 2, len(base) - 1))
-        elif fn in _HIST_FNS or fn.startswith("percentile"):
-            slot.append(None)
+        elif fn in _HIST_FNS or fn.startswith("percentile") or fn in EXT_MV_FUNCTIONS:
+            slot.append(None)  # MINMAXRANGEMV too: from the histogram (MINMV / MAXMV fold differently by group)
         else:
             base.append(dict(a))
             slot.append(len(base) - 1)
@@ -147,14 +155,18 @@ def _dtype(segments, col: str) -> str:
 def _hist_columns(request: dict, segments) -> List[str]:
     cols = []
     for a in request["aggregations"]:
-        fn = a["fn"]
+        mv = a["fn"] in EXT_MV_FUNCTIONS
+        fn = base_fn(a["fn"])
         if fn not in _HIST_FNS and fn != "minmaxrange" and not fn.startswith("percentile"):
             continue
+        if segments and bool(segments[0].column(a["column"]).meta.is_mv) != mv:
+            raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a %s column" % (
+                a["fn"], "single-value" if mv else "multi-value"))
         if fn not in _HIST_FNS and _dtype(segments, a["column"]) == "STRING":
             raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "%s over a STRING column" % fn)
         if fn == "fasthll" and _dtype(segments, a["column"]) != "STRING":  # aggregate() requires String[]
             raise N.PgxError(N.PGX_ERR_UNSUPPORTED, "fasthll over a non-STRING column")
-        if fn != "minmaxrange" and a["column"] not in cols:
+        if (fn != "minmaxrange" or mv) and a["column"] not in cols:
             cols.append(a["column"])
     return cols
 
@@ -219,7 +231,10 @@ def _run_group_by(ctx, request, segments, combine) -> E.IntermediateResultsBlock
     aggs = request["aggregations"]
 
     def value(a, s, key, bvals):
-        fn = a["fn"]
+        fn = base_fn(a["fn"])
+        if fn == "minmaxrange" and s is None:  # MINMAXRANGEMV: the extremes of the value multiset
+            h = hists[a["column"]].get(key, [])
+            return (float(h[0][0]), float(h[-1][0])) if h else (math.inf, -math.inf)
         if fn == "minmaxrange":
             return (float(bvals[s[0]]), float(bvals[s[1]]))
         if fn == "distinctcount":
@@ -281,8 +296,11 @@ def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment],
     base_res = bblk.get_aggregation_result()
     out = []
     for a, s in zip(aggs, slot):
-        fn = a["fn"]
-        if fn == "minmaxrange":
+        fn = base_fn(a["fn"])
+        if fn == "minmaxrange" and s is None:  # MINMAXRANGEMV
+            h = hists[a["column"]]
+            out.append((float(h[0][0]), float(h[-1][0])) if h else (math.inf, -math.inf))
+        elif fn == "minmaxrange":
             out.append((float(base_res[s[0]]), float(base_res[s[1]])))
         elif fn == "distinctcount":
             out.append(_hash_set(_dtype(segments, a["column"]), hists[a["column"]]))
@@ -306,6 +324,7 @@ def run(ctx: E.Context, request: dict, segments: Sequence[E.IndexSegment],
 def reduce_value(fn: str, v):
     """Final value of an extended function's (combined) intermediate (DistinctCountAggregationFunction.java:136-145,
     MinMaxRangeAggregationFunction.java:129-146 with DEFAULT_MIN_MAX_RANGE_VALUE = -1, PercentileUtil)."""
+    fn = base_fn(fn)
     if fn == "distinctcount":
         return len(v)
     if fn in ("distinctcounthll", "fasthll"):  # query/aggregation/function/{DistinctCountHLL,FastHll}... reduce
@@ -319,6 +338,7 @@ def reduce_value(fn: str, v):
 
 def combine_two(fn: str, a, b):
     """combineTwoValues: set union, pair extremes, list concatenation (histogram merge)."""
+    fn = base_fn(fn)
     if fn == "distinctcount":
         return set(a) | set(b)
     if fn in ("distinctcounthll", "fasthll"):  # HyperLogLog.addAll

@@ -219,14 +219,14 @@ def trim_to_size(fns: Sequence[str], vals, cnts, top_n: int, total: int = None) 
         if total <= threshold or n <= size:
             out.append(np.arange(n))
             continue
-        if f == "count":
+        if f in ("count", "countmv"):
             score = cnts[i].astype(np.float64)
-        elif f == "avg":
+        elif f in ("avg", "avgmv"):
             c = cnts[i].astype(np.float64)
             score = np.divide(vals[i], c, out=np.zeros(n), where=c != 0)
         else:
             score = vals[i]
-        if f != "min":
+        if f not in ("min", "minmv"):
             score = -score
         out.append(np.argpartition(score, size - 1)[:size])
     return out

@@ -25,6 +25,10 @@ AGG_FUNCTIONS = ("count", "sum", "min", "max", "avg", "countmv", "summv", "minmv
 # distinctcount / minmaxrange / percentileNN (AggregationFunctionFactory.java:84-107): aggregation-only requests
 EXT_FUNCTIONS = ("distinctcount", "distinctcounthll", "fasthll", "minmaxrange", "percentile50", "percentile90", "percentile95",
                  "percentile99", "percentileest50", "percentileest90", "percentileest95", "percentileest99")
+# the same functions over every value of a multi-value column (AggregationFunctionFactory.java:48-58)
+EXT_MV_FUNCTIONS = ("distinctcountmv", "distinctcounthllmv", "minmaxrangemv") + tuple(
+    "percentile%dmv" % p for p in (50, 90, 95, 99)) + tuple("percentileest%dmv" % p for p in (50, 90, 95, 99))
+EXT_FUNCTIONS = EXT_FUNCTIONS + EXT_MV_FUNCTIONS
 
 
 class PqlError(ValueError):
