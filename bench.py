@@ -136,6 +136,66 @@ def cpu_baseline(wl, query, seg_rows, nseg, threads):
             "result_count": int(sum(r["count"] for r in out))}
 
 
+def cpu_baseline_c1(data):
+    """C1 on the C twin (oracle/pinot_oracle_c.c): the whole baseball segment (100k rows), per-row readInt of yearID,
+    the dictId interval of yearID >= 2000 (RangeOfflineDictionaryPredicateEvaluator), LONG_MAP group keys over
+    playerName's dictIds, double SUM(runs); one thread (one segment); best of 20 after 3 warm-ups."""
+    import numpy as np
+    from oracle import c_oracle
+    sd = data.seg_data
+    cols = {}
+    for name in ("yearID", "playerName", "runs"):
+        c = sd.columns[name]
+        fwd = np.frombuffer(bytes(c.fwd_bytes) + b"\0" * 8, dtype=np.uint8)
+        dv = None if c.data_type == "STRING" else np.asarray(c.dictionary_values(), dtype=np.float64)
+        cols[name] = (fwd, c.bits, dv, c.cardinality)
+    years = np.asarray(sd.columns["yearID"].dictionary_values())
+    lo = int(np.searchsorted(years, 2000, side="left"))
+    seg = c_oracle.Segment(sd.total_docs, cols)
+    kw = dict(filter_col="yearID", lo=lo, hi=len(years) - 1, metric="runs", group_cols=("playerName",), threads=1)
+    times, out = [], None
+    for it in range(23):
+        t0 = time.perf_counter()
+        out = c_oracle.run([seg], **kw)
+        if it >= 3:
+            times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {"value": sd.total_docs / best, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": "the whole C1 segment (%d rows, the same bytes the GPU scans), oracle/pinot_oracle_c.c on one "
+                      "thread, best of 20 after 3 warm-ups; %.3f ms per query" % (sd.total_docs, best * 1e3),
+            "result_count": int(out[0]["count"]), "groups": int(out[0]["num_groups"])}
+
+
+def cpu_baseline_c4(data, req):
+    """C4 on the oracle's star-tree restatement (oracle/pinot_oracle.py star_tree_docs: StarTreeIndexOperator's BFS over
+    the OFF_HEAP nodes, then the SUM scan of the selected docs, sum_by_group): the whole C4 segment, one thread, best of
+    3 after 1 warm-up.  Pure Python: a port, not the reference's JIT-compiled Java."""
+    import numpy as np
+    from oracle import pinot_oracle as O
+    sd = data.seg_data
+    cols = {}
+    for name, c in sd.columns.items():
+        d = np.asarray(c.dictionary_values()).astype(np.int64)
+        cols[name] = O.OColumn(name, c.data_type, d, c.dict_ids().astype(np.int64), c.is_sorted, c.has_inverted,
+                               c.bits)
+    os_ = O.OSegment(cols, sd.total_docs, sd.total_raw_docs)
+    metrics = [a["column"] for a in req["aggregations"]]
+    gcols = req["group_by"]["columns"]
+    times, docs = [], None
+    for it in range(4):
+        t0 = time.perf_counter()
+        docs = O.star_tree_docs(os_, sd.star_tree, req, sd.total_raw_docs)
+        O.sum_by_group(os_, docs, metrics, gcols)
+        if it >= 1:
+            times.append(time.perf_counter() - t0)
+    best = min(times)
+    return {"value": sd.total_raw_docs / best, "unit": "raw rows represented/s", "cores": 1, "kind": "port",
+            "sample": "the whole C4 segment (%d raw rows, %d docs incl. star-tree aggregates), star-tree traversal + "
+                      "%d selected docs summed by oracle/pinot_oracle.py on one thread, best of 3 after 1 warm-up; "
+                      "%.3f ms per query" % (sd.total_raw_docs, sd.total_docs, len(docs), best * 1e3),
+            "docs_scanned": int(len(docs))}
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -370,6 +430,10 @@ def main():
     if world == 1 and not args.no_cpu_baseline and wl.name in CPU_SAMPLE:
         nseg, seg_rows = CPU_SAMPLE[wl.name]
         cpu = cpu_baseline(wl, req, min(rows, seg_rows), nseg, 8)
+    elif world == 1 and not args.no_cpu_baseline and wl.name == "c1":
+        cpu = cpu_baseline_c1(data)
+    elif world == 1 and not args.no_cpu_baseline and wl.name == "c4":
+        cpu = cpu_baseline_c4(data, req)
     if merged[0] is not None and req.get("group_by"):
         top = merged[0][0]
         best = sorted(top.items(), key=lambda kv: kv[1], reverse=q.fns[0] != "min")[:3]
