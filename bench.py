@@ -251,6 +251,8 @@ def main():
     # read-back, cross-GPU merge), as a server overlaps consecutive queries.  Every step still runs its whole query;
     # the line also reports the one-query-at-a-time latency (PGX_INFLIGHT=1 gives that timing for every step).
     inflight = max(1, int(os.environ.get("PGX_INFLIGHT", "2")))
+    if world > 1 and req.get("group_by") and not dense:
+        inflight = 1  # sparse cross-GPU merges (all-to-all + device merge) run one query at a time
     streams = [torch.cuda.Stream(device="cuda:%d" % local) for _ in range(inflight)]
     if dense:
         nplanes = 1 + len(req["aggregations"])
