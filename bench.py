@@ -246,11 +246,11 @@ def main():
         slots = C.c_int64()
         N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
         dense = slots.value <= (1 << 22)
-    # Queries in flight (PGX_INFLIGHT, default 2): step i + 1 is submitted (pgx_execute_async: predicate binding and
+    # Queries in flight (PGX_INFLIGHT, default 3): steps i + 1 and i + 2 are submitted (pgx_execute_async: predicate binding and
     # host planning on the library's threads, kernels on its own HIP stream) before step i is completed (wait, trim +
     # read-back, cross-GPU merge), as a server overlaps consecutive queries.  Every step still runs its whole query;
     # the line also reports the one-query-at-a-time latency (PGX_INFLIGHT=1 gives that timing for every step).
-    inflight = max(1, int(os.environ.get("PGX_INFLIGHT", "2")))
+    inflight = max(1, int(os.environ.get("PGX_INFLIGHT", "3")))
     if world > 1 and req.get("group_by") and not dense:
         inflight = 1  # sparse cross-GPU merges (all-to-all + device merge) run one query at a time
     streams = [torch.cuda.Stream(device="cuda:%d" % local) for _ in range(inflight)]
@@ -270,11 +270,12 @@ def main():
         binds, _owner = q.bindings(segs, seg_arr)  # the library copies the bindings before pgx_execute_async returns
         r = C.c_void_p()
         hs = streams[i % inflight].cuda_stream
+        flags = N.PGX_X_THROUGHPUT if inflight > 1 else 0  # queries overlap: one launch per kernel, not batches
         if dense:
             d = dense_t[i % inflight]
-            opts = N.ExecOpts(hs, C.c_void_p(d.data_ptr()), d.numel() * 8, N.PGX_X_KEEP_DENSE_ON_DEVICE)
+            opts = N.ExecOpts(hs, C.c_void_p(d.data_ptr()), d.numel() * 8, N.PGX_X_KEEP_DENSE_ON_DEVICE | flags)
         else:
-            opts = N.ExecOpts(hs, None, 0, 0)
+            opts = N.ExecOpts(hs, None, 0, flags)
         N.check(L.pgx_execute_async(ctx.handle, q.handle, seg_arr, len(segs), binds, C.byref(opts), C.byref(r)))
         return r
 
@@ -338,8 +339,13 @@ def main():
                 L.pgx_result_release(r)
         return last
 
-    def step():  # one query, nothing in flight beside it (latency; tools)
-        return complete(0, submit(0))
+    def step():  # one query, nothing in flight beside it (latency; tools): the batched plan
+        nonlocal inflight
+        saved, inflight = inflight, 1
+        try:
+            return complete(0, submit(0))
+        finally:
+            inflight = saved
 
     if args.profile_iters:  # exactly K steps and nothing else (PMC passes divide the step kernels' counters by K)
         run_steps(args.profile_iters)

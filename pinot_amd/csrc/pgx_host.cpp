@@ -3604,7 +3604,7 @@ struct HostProf {
 // whole list); false before anything was launched when the plan does not qualify.
 bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                  const pgx_exec_opts* opts, pgx_result* R, hipStream_t st, uint32_t xflags, HostProf& hp) {
-  int bs = 512;
+  int bs = (xflags & PGX_X_THROUGHPUT) ? 0 : 512;
   if (const char* e = std::getenv("PGX_BATCH_SEGS")) bs = std::atoi(e);
   if (bs <= 0 || n < 2 * bs || !jit_enabled()) return false;
   const size_t L = q.leaf_col.size();

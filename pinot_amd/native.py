@@ -24,6 +24,7 @@ PGX_MEM_HOST, PGX_MEM_DEVICE = 0, 1
 PGX_X_KEEP_DENSE_ON_DEVICE = 0x1
 PGX_X_FORCE_HASH = 0x2
 PGX_X_NO_PARTITION = 0x4
+PGX_X_THROUGHPUT = 0x8
 PGX_Q_NO_STAR_TREE = 0x1
 ERR_UNSUPPORTED = 2
 PGX_ERR_TIMEOUT = 5
