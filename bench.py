@@ -80,13 +80,15 @@ def barrier_sync(world):
 def cpu_baseline(wl, query, seg_rows, nseg, threads):
     """The oracle's C twin (oracle/pinot_oracle_c.c: one thread per segment, per-row readInt, 10000 / 5000-doc blocks,
     double SUM, hash-map group keys) on a bounded sample of the same workload, generated bit-identically on the host and
-    timed on this host's cores: best of 5 after 2 warm-ups.  Filters with several leaves are evaluated per
-    row on the leaves' dictId sets (the reference's bitmap iterators are not restated in C)."""
+    timed on this host's cores: best of 5 after 2 warm-ups.  C5's leaves read the segments' roaring
+    inverted indexes as the reference's BitmapBasedFilterOperator does (OR of the IN list's bitmaps, the NEQ leaf's
+    flipped bitmap, AND block leapfrogging the OR block's iterator; tests/test_c_oracle_bitmap.py pins it)."""
     import numpy as np
     from oracle import c_oracle
     from pinot_amd import synth
     dicts = {c.name: synth.make_dictionary(c.dict_kind, c.card).astype(np.float64) for c in wl.columns}
     segs = [None] * nseg
+    invs = [{} for _ in range(nseg)]
 
     def gen(s):
         cols = {}
@@ -97,6 +99,9 @@ def cpu_baseline(wl, query, seg_rows, nseg, threads):
             else:
                 fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), seg_rows, c.bits, c.card)
             cols[c.name] = (fwd, c.bits, dicts[c.name], c.card)
+            if c.inverted:  # the .bitmap.inv the GPU segments carry (synth.DeviceSegments._inverted_indexes)
+                invs[s][c.name] = c_oracle.inverted_build(
+                    c_oracle.synth_ids(synth.column_seed(wl.seed, s, ci), seg_rows, c.card), c.card)
         segs[s] = c_oracle.Segment(seg_rows, cols)
 
     ths = [threading.Thread(target=gen, args=(s,)) for s in range(nseg)]
@@ -117,7 +122,7 @@ def cpu_baseline(wl, query, seg_rows, nseg, threads):
             return w
         kw.update(group_cols=("gk",), leaves=[("f1", bits(1000, f1)), ("f2", bits(100, [7])),
                                               ("f3", bits(10, [i for i in range(10) if i != 3]))],
-                  prog=[0, 1, -2, 2, -1])
+                  prog=[0, 1, -2, 2, -1], inverted=invs, excl=[0, 0, 1])
     else:
         return None
     times = []

@@ -27,7 +27,8 @@ class PgoSegQuery(C.Structure):
                 ("entries_scanned", C.c_int64),
                 ("num_groups", C.c_int64), ("g_keys", C.POINTER(C.c_int64)), ("g_sums", C.POINTER(C.c_double)),
                 ("g_counts", C.POINTER(C.c_int64)), ("g_mins", C.POINTER(C.c_double)),
-                ("g_maxs", C.POINTER(C.c_double)), ("g_cap", C.c_int64)]
+                ("g_maxs", C.POINTER(C.c_double)), ("g_cap", C.c_int64),
+                ("leaf_inv", C.POINTER(C.c_void_p)), ("leaf_excl", C.POINTER(C.c_int32))]
 
 
 def lib():
@@ -45,6 +46,9 @@ def lib():
         L.pgo_read_int.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_int64]
         L.pgo_read_int.restype = C.c_int32
         L.pgo_segment_query_size.restype = C.c_int64
+        L.pgo_synth_ids.argtypes = [C.c_uint64, C.c_int64, C.c_uint32, C.c_void_p]
+        L.pgo_inverted_build.argtypes = [C.c_void_p, C.c_int64, C.c_int32, C.c_void_p, C.c_int64]
+        L.pgo_inverted_build.restype = C.c_int64
         assert L.pgo_segment_query_size() == C.sizeof(PgoSegQuery)
         _lib = L
     return _lib
@@ -56,6 +60,23 @@ def synth_fwd(seed, n, bits, card, pair_seed=0, npairs=0):
     nbytes = (n * bits + 7) // 8 + 8
     out = np.zeros(nbytes, dtype=np.uint8)
     lib().pgo_synth_fwd_paired(seed, n, bits, card, out.ctypes.data, nbytes, pair_seed, npairs)
+    return out
+
+
+def synth_ids(seed, n, card):
+    """The synthetic dictIds synth_fwd packs (unpaired columns)."""
+    out = np.empty(n, dtype=np.int32)
+    lib().pgo_synth_ids(seed, n, card, out.ctypes.data)
+    return out
+
+
+def inverted_build(ids, card):
+    """<col>.bitmap.inv bytes of a dictId column (the C twin's writer; tests pin it to pinot_amd.segment's)."""
+    ids = np.ascontiguousarray(ids, dtype=np.int32)
+    L = lib()
+    n = L.pgo_inverted_build(ids.ctypes.data, len(ids), card, None, 0)
+    out = np.empty(n, dtype=np.uint8)
+    L.pgo_inverted_build(ids.ctypes.data, len(ids), card, out.ctypes.data, n)
     return out
 
 
@@ -75,8 +96,10 @@ class Segment:
 
 
 def run(segments, filter_col=None, lo=0, hi=-1, metric="m", group_cols=(), threads=1, collect_groups=False,
-        leaves=None, prog=None):
-    """leaves = [(column, dictId bitset uint32 array)], prog = postfix ints (>= 0 leaf, -1 AND, -2 OR)."""
+        leaves=None, prog=None, inverted=None, excl=None):
+    """leaves = [(column, dictId bitset uint32 array)], prog = postfix ints (>= 0 leaf, -1 AND, -2 OR).
+    inverted = {column: .bitmap.inv bytes (uint8 array)} per segment (a list, one dict per segment): every leaf is then
+    evaluated on the bitmaps (BitmapBasedFilterOperator) instead of per row; excl[l] = 1 marks NEQ / NOT_IN leaves."""
     L = lib()
     qs = (PgoSegQuery * len(segments))()
     keep = []
@@ -108,6 +131,13 @@ def run(segments, filter_col=None, lo=0, hi=-1, metric="m", group_cols=(), threa
             q.leaf_bits = lb
             q.prog_len = len(prog)
             q.prog = pg
+            if inverted is not None:
+                invs = [np.ascontiguousarray(inverted[i][c], dtype=np.uint8) for c, _ in leaves]
+                li = (C.c_void_p * len(leaves))(*[a.ctypes.data for a in invs])
+                le = (C.c_int32 * len(leaves))(*(excl or [0] * len(leaves)))
+                keep += [invs, li, le]
+                q.leaf_inv = li
+                q.leaf_excl = le
         q.metric_col = s.names.index(metric)
         q.num_group_cols = len(group_cols)
         q.group_cols = gc
