@@ -50,9 +50,10 @@ extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const 
 extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
                                        int64_t n_words, uint64_t pair_seed, uint32_t npairs, hipStream_t stream);
 extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
-                                           int nreg, int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
-                                           int nbits, uint64_t* out, int64_t cap, unsigned long long* cursor,
-                                           int cstride, unsigned long long* overflow, hipStream_t stream);
+                                           int in_cstride, int nreg, int reg_div, int64_t in_cap, int chunks_per_reg,
+                                           uint64_t keymask, int shift, int nbits, uint64_t* out, int64_t cap,
+                                           unsigned long long* cursor, int cstride, unsigned long long* overflow,
+                                           hipStream_t stream);
 extern "C" hipError_t pgx_launch_mv_leaf_mask(const pgx::MvLeaf* items, int nitems, int max_words, hipStream_t stream);
 extern "C" hipError_t pgx_launch_mv_aggregate(const pgx::MvAgg* items, int nitems, int max_words, hipStream_t stream);
 extern "C" hipError_t pgx_launch_mv_group(const pgx::MvGroupArgs* args, int nsegs, int max_docs, int ordered,
@@ -1286,6 +1287,9 @@ struct ExecPlan {
   bool part_sum = false, part_min = false, part_max = false;
   bool part_dictid = false;      // records carry the value's dictId (sorted dictionary), values looked up at aggregation
   bool part_fused = false;       // the scan kernel performs the first radix pass (records leave bucketed)
+  bool part_slab = false;        // ... into per-workgroup slabs (value-offset records; pass 2 reads the slabs)
+  int64_t part_nwg = 0;          // slab mode: query-kernel workgroups over all launch groups (slabs per bucket)
+  int64_t part_wg_rows = 0;      // slab mode: most rows one workgroup scans
   const int64_t* part_vdict = nullptr;  // device int64 value per dictId (part_dictid)
   unsigned long long* part_cursor = nullptr;   // fused first pass: bucket cursors, overflow counter, bucket capacity
   unsigned long long* part_overflow = nullptr;
@@ -1980,6 +1984,11 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       P.part_dictid = dictid;
       P.part_fused = dictid || vc < 0;
       if (const char* e = std::getenv("PGX_PART_FUSED")) P.part_fused = P.part_fused && e[0] == '1';
+      // opt-in (PGX_PART_SLAB=1): the scan appends value-offset records straight to its workgroup's slab of each of
+      // the 128 first-pass buckets (LDS cursors, no staging), so pass 1 disappears; measured at C3 the scan's scattered
+      // 8-byte stores (one L2 request each) cost more than the pass they save (busy 17.8 vs 14.7 ms per query)
+      const char* es = std::getenv("PGX_PART_SLAB");
+      P.part_slab = !P.part_fused && es && es[0] == '1';
       P.use_part = true;
       P.part_vcol = vc;
       P.part_keybits = keybits;
@@ -2753,7 +2762,7 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
       B.table = DevBuf(ctx, bytes);
       K.table = devp(B.table);
     }
-  } else if (P.use_part && !P.part_fused) {
+  } else if (P.use_part && !P.part_fused && !P.part_slab) {
     B.table = DevBuf(ctx, std::max<int64_t>(P.rec_total, 1) * 8);  // one key|value record per scanned row
     K.table = devp(B.table);
   } else if (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) {
@@ -2806,11 +2815,16 @@ int jit_occupancy(void* fn, int threads) {
 
 void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
   P.jit.clear();
+  P.part_nwg = 0;
+  P.part_wg_rows = 0;
+  const bool slab = P.part_slab;
+  P.part_slab = false;  // only the query kernels write slabs (the generic kernel writes row-order records)
   const KQuery& K = P.kq;
   if (!jit_enabled()) return;
   if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL || P.use_part)) return;
   const int nc = K.num_qcols;
   if (nc > PGX_J_MAX_COLS) return;
+  P.part_slab = slab;
   const bool grouped = K.group_mode != G_NONE;
   // which columns are decoded, which carry value images
   std::vector<bool> decode(nc, false), want_img(nc, false);
@@ -2970,8 +2984,9 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     if (P.use_part) {
       J.keybits = P.part_keybits;
       J.emit_col = P.part_vcol;
-      J.part_bits = P.part_fused ? kPart1Bits : 0;
+      J.part_bits = (P.part_fused || P.part_slab) ? kPart1Bits : 0;
       J.emit_dictid = P.part_dictid;
+      J.part_slab = P.part_slab;
     }
     J.dense_slots = P.dense_slots;
     J.leafmask = P.fsm_on && P.lmask_off[members[0]] >= 0;
@@ -3062,6 +3077,11 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     G.args.rdesc = P.rdesc_dev;
     G.args.total_tiles = tiles;
     G.args.tiles_per_wg = tpw;
+    if (P.part_slab && tiles > 0) {
+      G.args.part_wg_base = P.part_nwg;
+      P.part_nwg += G.grid;
+      P.part_wg_rows = std::max<int64_t>(P.part_wg_rows, tpw * tile_rows);
+    }
     if (tiles > 0) P.jit.push_back(std::move(G));
   }
   if (P.jit.empty()) P.jit.push_back(ExecPlan::JitGroup{});  // every segment empty: nothing to launch
@@ -3093,7 +3113,8 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
       G.args.part_cursor = P.part_cursor;
       G.args.part_overflow = P.part_overflow;
       G.args.part_cap = P.part_cap;
-      G.args.part_cstride = kCursorStride;
+      G.args.part_cstride = P.part_slab ? 1 : kCursorStride;
+      G.args.part_nwg = P.part_nwg;
       void* params[] = {&G.args};
       PGX_LAUNCH(st, "pgxq", hipModuleLaunchKernel(static_cast<hipFunction_t>(G.fn), G.grid, 1, 1, G.T, 1, 1, 0, st, params,
                                       nullptr),
@@ -3290,8 +3311,15 @@ struct PartBuffers {
   int nbits2 = 7;                       // second pass: 2^nbits2 buckets per first-pass bucket (0: no second pass)
   int64_t cap1 = 0, cap2 = 0, ocap = 0;
   DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[kPart1N] | cursors2[nparts] (kCursorStride apart) | ocount | ovf[3]
+  // slab mode (ExecPlan::part_slab): out1 holds kPart1N x nwg slabs of cap1 records, their counts in scnt; the second
+  // pass always runs (with nbits2 = 0 it only gathers each bucket's slabs into one run)
+  bool slab = false;
+  int64_t nwg = 0;
+  DevBuf scnt;
+  bool pass2() const { return nbits2 > 0 || slab; }
   int64_t nparts() const { return int64_t(1) << (kPart1Bits + nbits2); }
-  size_t ctr_words() const { return size_t(kPart1N + (nbits2 ? nparts() : 0)) * kCursorStride + 4; }
+  size_t ctr_words() const { return size_t(kPart1N + (pass2() ? nparts() : 0)) * kCursorStride + 4; }
+  int64_t out1_recs() const { return slab ? int64_t(kPart1N) * nwg * cap1 : int64_t(kPart1N) * cap1; }
 };
 
 // PGX_PART_DEBUG=1 (tests): start from undersized buckets and one pass, and allow at most one refinement, so the
@@ -3310,11 +3338,17 @@ void part_size(const ExecPlan& P, PartBuffers& PB) {
   PB.nbits2 = 0;
   while (PB.nbits2 < 7 && double(int64_t(1) << (kPart1Bits + PB.nbits2)) * kPartGroupsPerWg < ub) ++PB.nbits2;
   PB.cap1 = N / kPart1N + N / 512 + 65536;
+  PB.slab = P.part_slab;
+  PB.nwg = P.part_nwg;
+  if (PB.slab) {  // a slab holds one workgroup's records of one bucket: binomial around wg_rows / 128
+    const int64_t m = P.part_wg_rows / kPart1N;
+    PB.cap1 = m + m / 8 + 512;
+  }
   const int64_t np = PB.nparts();
   PB.cap2 = N / np + N / np / 4 + 16384;
   if (part_debug()) {
     PB.nbits2 = 0;
-    PB.cap1 = N / 256 + 1;
+    PB.cap1 = PB.slab ? 1 : N / 256 + 1;
     PB.cap2 = 1;
   }
 }
@@ -3322,10 +3356,11 @@ void part_size(const ExecPlan& P, PartBuffers& PB) {
 bool part_alloc(pgx_ctx* ctx, const ExecPlan& P, PartBuffers& PB) {
   const int64_t np = PB.nparts();
   PB.ocap = std::max<int64_t>(1, std::min<int64_t>(P.rec_total, np * 4096));
-  const uint64_t bytes = uint64_t(kPart1N) * PB.cap1 * 8 + (PB.nbits2 ? uint64_t(np) * PB.cap2 * 8 : 0) + uint64_t(PB.ocap) * 40;
+  const uint64_t bytes = uint64_t(PB.out1_recs()) * 8 + (PB.pass2() ? uint64_t(np) * PB.cap2 * 8 : 0) + uint64_t(PB.ocap) * 40;
   if (bytes > kPartMaxBytes) return false;
-  PB.out1 = DevBuf(ctx, size_t(kPart1N) * PB.cap1 * 8);
-  if (PB.nbits2) PB.out2 = DevBuf(ctx, size_t(np) * PB.cap2 * 8);
+  PB.out1 = DevBuf(ctx, size_t(std::max<int64_t>(PB.out1_recs(), 1)) * 8);
+  if (PB.pass2()) PB.out2 = DevBuf(ctx, size_t(np) * PB.cap2 * 8);
+  if (PB.slab) PB.scnt = DevBuf(ctx, size_t(std::max<int64_t>(int64_t(kPart1N) * PB.nwg, 1)) * 8);
   PB.okey = DevBuf(ctx, size_t(PB.ocap) * 8);
   PB.oplane = DevBuf(ctx, size_t(PB.ocap) * 4 * 8);
   PB.ctr = DevBuf(ctx, PB.ctr_words() * 8);
@@ -3337,10 +3372,11 @@ bool part_alloc(pgx_ctx* ctx, const ExecPlan& P, PartBuffers& PB) {
 void part_prepare(ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   unsigned long long* ctr = devp(PB.ctr);
   hip_check(hipMemsetAsync(ctr, 0, PB.ctr_words() * 8, st), "partition counters");
-  P.part_cursor = P.part_fused ? ctr : nullptr;
-  P.part_overflow = P.part_fused ? ctr + PB.ctr_words() - 3 : nullptr;  // overflow[0]: first pass
+  if (PB.slab) hip_check(hipMemsetAsync(PB.scnt.p, 0, size_t(kPart1N) * PB.nwg * 8, st), "slab counters");
+  P.part_cursor = P.part_fused ? ctr : (PB.slab ? devp(PB.scnt) : nullptr);
+  P.part_overflow = (P.part_fused || PB.slab) ? ctr + PB.ctr_words() - 3 : nullptr;  // overflow[0]: first pass
   P.part_cap = PB.cap1;
-  if (P.part_fused) P.kq.table = reinterpret_cast<unsigned long long*>(PB.out1.p);
+  if (P.part_fused || PB.slab) P.kq.table = reinterpret_cast<unsigned long long*>(PB.out1.p);
 }
 
 // After the scan: first pass (unless fused), second pass, aggregation.
@@ -3353,24 +3389,28 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   unsigned long long* tail = ctr + PB.ctr_words() - 4;  // ocount, overflow[3]
   if (N == 0) return;
   const uint64_t keymask = (uint64_t(1) << P.part_keybits) - 1u;
-  if (!P.part_fused) {
+  if (!P.part_fused && !PB.slab) {
     const uint64_t* recs = reinterpret_cast<const uint64_t*>(P.kq.table);
     const int64_t chunks1 = (N + kPartChunkRecs - 1) / kPartChunkRecs;
     if (chunks1 > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
-    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(recs, nullptr, nullptr, 1, N, int(chunks1), keymask, 64 - kPart1Bits, kPart1Bits,
-                                   PB.out1.as<uint64_t>(), PB.cap1, c1, kCursorStride, tail + 1, st),
+    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(recs, nullptr, nullptr, 1, 1, 1, N, int(chunks1), keymask,
+                                   64 - kPart1Bits, kPart1Bits, PB.out1.as<uint64_t>(), PB.cap1, c1, kCursorStride,
+                                   tail + 1, st),
               "partition pass 1");
   }
   const uint64_t* ain = PB.out1.as<uint64_t>();
   const unsigned long long* acnt = c1;
   int64_t acap = PB.cap1;
   int aparts = kPart1N;
-  if (PB.nbits2) {
+  if (PB.pass2()) {
+    // slab mode: region r = slab (bucket r / nwg, workgroup r % nwg), counts in scnt
+    const int64_t nreg = PB.slab ? int64_t(kPart1N) * PB.nwg : kPart1N;
     const int64_t chunks2 = (PB.cap1 + kPartChunkRecs - 1) / kPartChunkRecs;
-    if (chunks2 * kPart1N > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
-    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, kPart1N, PB.cap1, int(chunks2), keymask,
-                                   64 - kPart1Bits - PB.nbits2, PB.nbits2, PB.out2.as<uint64_t>(), PB.cap2, c2,
-                                   kCursorStride, tail + 2, st),
+    if (chunks2 * nreg > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
+    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, PB.slab ? devp(PB.scnt) : c1,
+                                   PB.slab ? 1 : kCursorStride, int(nreg), PB.slab ? int(PB.nwg) : 1, PB.cap1,
+                                   int(chunks2), keymask, 64 - kPart1Bits - PB.nbits2, PB.nbits2,
+                                   PB.out2.as<uint64_t>(), PB.cap2, c2, kCursorStride, tail + 2, st),
               "partition pass 2");
     ain = PB.out2.as<uint64_t>();
     acnt = c2;
@@ -3395,7 +3435,7 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
   for (int attempt = 0; attempt < 12; ++attempt) {
     if (!part_alloc(ctx, P, PB)) return false;
     part_prepare(P, PB, st);
-    if (attempt == 0 || P.part_fused) {  // the fused first pass reruns with the scan (statistics restart with it)
+    if (attempt == 0 || P.part_fused || PB.slab) {  // a fused first pass reruns with the scan (statistics restart too)
       reset_outputs(P, B, st);
       launch_scan(P, st);
     }
@@ -3414,7 +3454,13 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
       return int64_t(m);
     };
     if (tail[1]) {  // a first-pass bucket overflowed: size to the largest (cursors count every record)
-      PB.cap1 = max_cursor(0, kPart1N) + 1024;
+      if (PB.slab) {
+        std::vector<unsigned long long> sc(size_t(kPart1N) * PB.nwg);
+        hip_check(hipMemcpy(sc.data(), PB.scnt.p, sc.size() * 8, hipMemcpyDeviceToHost), "slab counters D2H");
+        PB.cap1 = int64_t(*std::max_element(sc.begin(), sc.end())) + 1024;
+      } else {
+        PB.cap1 = max_cursor(0, kPart1N) + 1024;
+      }
       continue;
     }
     if (tail[2]) {

@@ -241,6 +241,9 @@ struct JitShape {
   // record's value field is the value column's dictId (sorted dictionary) instead of its offset from vbase
   int part_bits = 0;
   bool emit_dictid = false;
+  // with part_bits: each workgroup appends to its own region ("slab") per bucket through LDS cursors, no staging and no
+  // global cursor per sub-step (slab (b, w) at table + (b * part_nwg + part_wg_base + w) * part_cap)
+  bool part_slab = false;
   bool compact = false;   // pack each sub-step's selected rows into consecutive lanes before aggregating (selective)
   bool selmask = false;   // write every row's selection bit (multi-value aggregations read it)
 };

@@ -109,7 +109,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const bool epart = emit && s.part_bits > 0;
   const int pnb = 1 << s.part_bits;
   int pst_off = -1, phist_off = -1;
-  if (epart) {
+  const bool eslab = epart && s.part_slab;
+  if (eslab) {
+    phist_off = lds;
+    lds += pnb * 4;  // per-bucket cursors of this workgroup's slabs
+  } else if (epart) {
     pst_off = lds;
     lds += s.T * s.R * 8;
     phist_off = lds;
@@ -214,7 +218,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   if (s.group_mode == G_DENSE_GLOBAL) e.ln("u64* const tab = A.table;");
   if (scr_off >= 0) e.ln("PgxRScratch& rscr = *(PgxRScratch*)(lds + ", scr_off / 4, ");");
   if (compact) e.ln("u32* const cstg = lds + ", cst_off / 4, " + (tid >> 6) * ", 64 * std::max<size_t>(1, ccols.size()), ";");
-  if (epart) {
+  if (eslab) {
+    e.ln("u32* const phist = lds + ", phist_off / 4, ";");
+    e.ln("for (int i = tid; i < ", pnb, "; i += PT) phist[i] = 0u;");
+    e.ln("__syncthreads();");
+  } else if (epart) {
     e.ln("u64* const pstage = (u64*)(lds + ", pst_off / 4, ");");
     e.ln("u32* const phist = lds + ", phist_off / 4, ";");
     e.ln("u32* const poffs = phist + ", pnb, ";");
@@ -711,7 +719,24 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         e.ln("  ((PGX_G ", ty, "*)(S->lmask + ", l, " * S->lmask_words))[r0 / PR] = (", ty, ")lw", l, ";");
       e.ln("}");
     }
-    if (epart) {
+    if (eslab) {
+      // each record goes straight to this workgroup's slab of its bucket: consecutive records of a bucket land in
+      // consecutive words, so L2 completes the slab's lines before they are written back
+      const std::string KM = std::to_string((1ull << s.keybits) - 1ull) + "ull";
+      const std::string SH = std::to_string(64 - s.part_bits);
+      e.ln("{");
+      e.ln("  PGX_G u64* const pout = (PGX_G u64*)A.table;");
+      e.ln("  const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
+      e.ln("  #pragma unroll");
+      e.ln("  for (int j = 0; j < PR; ++j) {");
+      e.ln("    if (recs[j] != ~0ull) {");
+      e.ln("      const u32 b = (u32)(pgx_part_mix(recs[j] & ", KM, ") >> ", SH, ");");
+      e.ln("      const u32 pos = atomicAdd(&phist[b], 1u);");
+      e.ln("      if (pos < (u32)A.part_cap) pout[((long long)b * A.part_nwg + wsl) * A.part_cap + pos] = recs[j];");
+      e.ln("    }");
+      e.ln("  }");
+      e.ln("}");
+    } else if (epart) {
       const std::string KM = std::to_string((1ull << s.keybits) - 1ull) + "ull";
       const std::string SH = std::to_string(64 - s.part_bits);
       e.ln("{");
@@ -836,6 +861,13 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("  }");
   e.ln("}");
   e.ln("__syncthreads();");
+  if (eslab) {  // slab counts (every record, also past part_cap: the host resizes from the largest)
+    e.ln("for (int i = tid; i < ", pnb, "; i += PT) {");
+    e.ln("  const u32 h = phist[i];");
+    e.ln("  A.part_cursor[((long long)i * A.part_nwg + A.part_wg_base + (long long)blockIdx.x) * A.part_cstride] = h;");
+    e.ln("  if (h > (u32)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
+    e.ln("}");
+  }
   if (!grouped) {
     e.ln("if (tid < ", s.num_planes, ") {");
     e.ind++;
@@ -902,6 +934,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   for (const auto& ops : s.rprog_ops) add(ops);
   k.push_back(s.part_bits);
   k.push_back(s.emit_dictid);
+  k.push_back(s.part_slab);
   k.push_back(s.compact);
   k.push_back(s.selmask);
   return k;
@@ -1247,8 +1280,13 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.cols[1].img = IMG_NONE;  // value image demoted (LDS budget): values from the HBM dictionary
     s.cols[2].remap = true;
     shapes.push_back(s);
-    s.part_bits = 7;           // first radix pass fused, dictId records (the C3 path)
+    s.part_bits = 7;           // first radix pass fused, dictId records
     s.emit_dictid = true;
+    shapes.push_back(s);
+    s.cols[1].img = IMG_FOR16;  // first radix pass fused into per-workgroup slabs, value-offset records (the C3 path)
+    s.cols[2].remap = false;
+    s.emit_dictid = false;
+    s.part_slab = true;
     shapes.push_back(s);
   }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {

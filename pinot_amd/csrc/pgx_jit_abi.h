@@ -69,6 +69,9 @@ struct JArgs {
   unsigned long long* part_overflow; // ... counts buckets that ran past part_cap records
   long long part_cap;                // records per bucket; bucket b's records at table + b * part_cap
   long long part_cstride;
+  long long part_wg_base;            // slab mode: this launch's first workgroup slab and the slabs per bucket; slab
+  long long part_nwg;                // (b, w) holds records at table + (b * part_nwg + w) * part_cap, its count at
+                                     // part_cursor[(b * part_nwg + w) * part_cstride]
 };
 
 #endif  // PGX_JIT_ABI_H_

@@ -1655,13 +1655,15 @@ __device__ __forceinline__ void part_scan128(const int* hist, int* offs, int* to
   if (tid == 63) *total = x;
 }
 
-// Records of region r live at in + in_off[r] (in_off null: r * in_cap), in_cnt[r] of them (in_cnt null: in_cap; else
-// typically the previous pass's cursors, read on the device, so passes chain without a host round trip); region r's
-// partition b goes to out + (r * nb + b) * cap, appended at cursor[(r * nb + b) * cstride] (cursors spread over
-// separate cache lines: every workgroup of a pass reserves its runs there).
+// Records of region r live at in + in_off[r] (in_off null: r * in_cap), in_cnt[r * in_cstride] of them (in_cnt null:
+// in_cap; else typically the previous pass's cursors, read on the device, so passes chain without a host round trip);
+// regions come in groups of reg_div (the scan's per-workgroup slabs of one bucket), and group q's partition b goes to
+// out + (q * nb + b) * cap, appended at cursor[(q * nb + b) * cstride] (cursors spread over separate cache lines: every
+// workgroup of a pass reserves its runs there).
 __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __restrict__ in,
                                                               const int64_t* __restrict__ in_off,
-                                                              const unsigned long long* __restrict__ in_cnt, int nreg,
+                                                              const unsigned long long* __restrict__ in_cnt,
+                                                              int in_cstride, int nreg, int reg_div,
                                                               int64_t in_cap, int chunks_per_reg, uint64_t keymask,
                                                               int shift, int nbits, uint64_t* __restrict__ out,
                                                               int64_t cap, unsigned long long* __restrict__ cursor,
@@ -1669,7 +1671,8 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
   const int r = static_cast<int>(blockIdx.x / chunks_per_reg);
   const int64_t chunk = static_cast<int64_t>(blockIdx.x % chunks_per_reg);
   if (r >= nreg) return;
-  const int64_t n = in_cnt ? min(static_cast<int64_t>(in_cnt[r * cstride]), in_cap) : in_cap;
+  const int64_t n = in_cnt ? min(static_cast<int64_t>(in_cnt[static_cast<int64_t>(r) * in_cstride]), in_cap) : in_cap;
+  const int q = r / reg_div;
   const int64_t c0 = chunk * kPartChunk;
   if (c0 >= n) return;
   const int cn = static_cast<int>(min<int64_t>(kPartChunk, n - c0));
@@ -1699,7 +1702,7 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
   __syncthreads();
   part_scan128(hist, offs, &total, nb, tid);
   if (tid < nb && hist[tid]) {
-    const unsigned long long g = atomicAdd(&cursor[static_cast<int64_t>(r * nb + tid) * cstride],
+    const unsigned long long g = atomicAdd(&cursor[(static_cast<int64_t>(q) * nb + tid) * cstride],
                                            static_cast<unsigned long long>(hist[tid]));
     gpos[tid] = g;
     if (g + hist[tid] > static_cast<unsigned long long>(cap)) atomicAdd(overflow, 1ull);
@@ -1719,7 +1722,7 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
     const unsigned long long p = gpos[b] + static_cast<unsigned long long>(i - offs[b]);
     // plain (not streaming) stores: a bucket run's first and last lines are completed by other workgroups' runs,
     // which L2 merges before write-back
-    if (p < static_cast<unsigned long long>(cap)) dst[(static_cast<int64_t>(r) * nb + b) * cap + static_cast<int64_t>(p)] = v;
+    if (p < static_cast<unsigned long long>(cap)) dst[(static_cast<int64_t>(q) * nb + b) * cap + static_cast<int64_t>(p)] = v;
   }
 }
 
@@ -2048,15 +2051,17 @@ extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, in
 }
 
 extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
-                                           int nreg, int64_t in_cap, int chunks_per_reg, uint64_t keymask, int shift,
-                                           int nbits, uint64_t* out, int64_t cap, unsigned long long* cursor,
-                                           int cstride, unsigned long long* overflow, hipStream_t stream) {
+                                           int in_cstride, int nreg, int reg_div, int64_t in_cap, int chunks_per_reg,
+                                           uint64_t keymask, int shift, int nbits, uint64_t* out, int64_t cap,
+                                           unsigned long long* cursor, int cstride, unsigned long long* overflow,
+                                           hipStream_t stream) {
   const long long blocks = static_cast<long long>(nreg) * chunks_per_reg;
   if (blocks <= 0) return hipSuccess;
-  if (blocks > 0x7FFFFFFFll || nbits > 7 || nbits < 1) return hipErrorInvalidValue;
+  // nbits 0: one partition per region group (gathers the scan's slabs of a bucket into one contiguous run)
+  if (blocks > 0x7FFFFFFFll || nbits > 7 || nbits < 0 || reg_div < 1 || shift < 1 || shift > 63) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pgx::pgx_partition, dim3(static_cast<unsigned>(blocks)), dim3(pgx::kPartThreads), 0, stream, in,
-                     in_off, in_cnt, nreg, in_cap, chunks_per_reg, keymask, shift, nbits, out, cap, cursor, cstride,
-                     overflow);
+                     in_off, in_cnt, in_cstride, nreg, reg_div, in_cap, chunks_per_reg, keymask, shift, nbits, out, cap,
+                     cursor, cstride, overflow);
   return hipGetLastError();
 }
 

@@ -143,12 +143,15 @@ def _expected(raw):
     return out
 
 
+@pytest.mark.parametrize("slab", ["1", "0"])
 @pytest.mark.parametrize("n,card", [(400000, 1000), (1200000, 2000)])
-def test_partitioned_debug_resize_and_fallback(ctx, monkeypatch, n, card):
-    """PGX_PART_DEBUG=1: pass-1 buckets start at 1/4 of their expected size (resize from the measured cursors), one
-    pass of 64 partitions (~n distinct groups overflow the 4096-slot LDS tables: re-split to 128), and at most one
-    re-split: the 1.2M-row case still overflows and falls back to the global hash table.  Both must be exact."""
+def test_partitioned_debug_resize_and_fallback(ctx, monkeypatch, n, card, slab):
+    """PGX_PART_DEBUG=1: pass-1 buckets (slab mode: the scan's one-record slabs) start undersized (resize from the
+    measured counts), one pass of 128 partitions (~n distinct groups overflow the LDS tables: re-split), and at most
+    one re-split: the 1.2M-row case still overflows and falls back to the global hash table.  Both must be exact, with
+    the scan writing per-workgroup slabs (PGX_PART_SLAB=1) or row-order records (0, default)."""
     monkeypatch.setenv("PGX_PART_DEBUG", "1")
+    monkeypatch.setenv("PGX_PART_SLAB", slab)
     gseg, raw = _pairs_segment(ctx, n, card, seed=card)
     q = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY ga, gb")
     got = _map(_execute(ctx, [gseg], q, 0))
@@ -243,15 +246,18 @@ def test_group_partials_split_then_merged_equal_one_launch(ctx):
         H.assert_values_equal(merged[k], v, fns)
 
 
-@pytest.mark.parametrize("fused", ["0", "1"])
+@pytest.mark.parametrize("mode", ["fused", "slab", "rows"])
 @pytest.mark.parametrize("text", [AGGS + " GROUP BY g2, a, c", "SELECT COUNT(*) FROM t WHERE a > 0 GROUP BY a, c",
                                   "SELECT MIN(m), MAX(m) FROM t WHERE b <> %(b1)s GROUP BY c, g2, s, g1"])
-def test_fused_first_pass_equals_oracle(ctx, seg, text, fused, monkeypatch):
-    """PGX_PART_FUSED=1: the scan kernel splits its records 128 ways itself (LDS histogram, per-bucket cursor
-    reservation, bucket-sorted staging) and the records carry the value's dictId (sorted dictionary: MIN / MAX of ids,
-    SUM by lookup while aggregating); =0: row-order records and a separate first pass.  COUNT-only keys always take
-    the fused pass.  Both against the oracle."""
-    monkeypatch.setenv("PGX_PART_FUSED", fused)
+def test_fused_first_pass_equals_oracle(ctx, seg, text, mode, monkeypatch):
+    """The first radix pass three ways.  fused (PGX_PART_FUSED=1): the scan kernel splits its records 128 ways itself
+    (LDS histogram, per-bucket cursor reservation, bucket-sorted staging) and the records carry the value's dictId
+    (sorted dictionary: MIN / MAX of ids, SUM by lookup while aggregating).  slab (PGX_PART_SLAB=1): the scan appends
+    value-offset records to its workgroup's slab of each bucket and the second pass reads the slabs.  rows (default):
+    row-order records and a separate first pass.  COUNT-only keys always take the fused pass.  All
+    against the oracle."""
+    monkeypatch.setenv("PGX_PART_FUSED", "1" if mode == "fused" else "0")
+    monkeypatch.setenv("PGX_PART_SLAB", "0" if mode == "rows" else "1")
     gseg, oseg, fmt = seg
     q = pql.compile(text % fmt)
     blk, st = _run_inner(ctx, gseg, q)
