@@ -70,6 +70,13 @@ extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int6
 extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
                                               const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
 extern "C" size_t pgx_trim_state_bytes(void);
+extern "C" hipError_t pgx_launch_part_aggregate_img(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
+                                                    int nparts, int64_t cap, uint64_t keymask, int keybits,
+                                                    int64_t vbase, const uint32_t* img, int img_words, int img_sh,
+                                                    const int64_t* vdict, int need_min, int need_max, int pack_shift,
+                                                    uint64_t* okey, uint64_t* oplane, int64_t ocap,
+                                                    unsigned long long* ocount, unsigned long long* overflow, int grid,
+                                                    hipStream_t stream);
 extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
                                      int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
                                      uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream);
@@ -1287,10 +1294,13 @@ struct ExecPlan {
   bool part_sum = false, part_min = false, part_max = false;
   bool part_dictid = false;      // records carry the value's dictId (sorted dictionary), values looked up at aggregation
   bool part_fused = false;       // the scan kernel performs the first radix pass (records leave bucketed)
-  bool part_slab = false;        // ... into per-workgroup slabs (value-offset records; pass 2 reads the slabs)
+  bool part_slab = false;        // ... into per-workgroup slabs (dictId records, LDS cursors; pass 2 reads the slabs)
   int64_t part_nwg = 0;          // slab mode: query-kernel workgroups over all launch groups (slabs per bucket)
   int64_t part_wg_rows = 0;      // slab mode: most rows one workgroup scans
   const int64_t* part_vdict = nullptr;  // device int64 value per dictId (part_dictid)
+  const uint32_t* part_img = nullptr;   // slab mode, FOR16 value column: its image, looked up in the aggregation's LDS
+  int part_img_words = 0, part_img_sh = 0;
+  int part_grid = 256;                  // ... its persistent grid: one workgroup per CU (the image fills the LDS)
   unsigned long long* part_cursor = nullptr;   // fused first pass: bucket cursors, overflow counter, bucket capacity
   unsigned long long* part_overflow = nullptr;
   int64_t part_cap = 0;
@@ -1975,20 +1985,32 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       dictid = c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end()) &&
                keybits + bits_for(c0.card) <= 63;
       // opt-in (PGX_PART_FUSED=1): measured at C3, the fused first pass saves 1.7 ms of scan + pass 1, but the
-      // aggregation's per-record dictionary gathers (one 64-B L2 line each) cost 2.3 ms more than offset records
+      // aggregation's per-record dictionary gathers (one 64-B L2 line each) cost 2.3 ms more than offset records.
+      // PGX_PART_SLAB=1: the same fused split, but each workgroup appends to its own slab of every bucket (LDS
+      // cursors, no global cursor round trip per sub-step); the second pass reads the slabs.
       const char* e = std::getenv("PGX_PART_FUSED");
-      dictid = dictid && e && e[0] == '1';
-      if (dictid) P.part_vdict = static_cast<const int64_t*>(c0.dict_dev);
-    }
-    if (ok && keybits + vbits <= 63) {
-      P.part_dictid = dictid;
-      P.part_fused = dictid || vc < 0;
-      if (const char* e = std::getenv("PGX_PART_FUSED")) P.part_fused = P.part_fused && e[0] == '1';
-      // opt-in (PGX_PART_SLAB=1): the scan appends value-offset records straight to its workgroup's slab of each of
-      // the 128 first-pass buckets (LDS cursors, no staging), so pass 1 disappears; measured at C3 the scan's scattered
-      // 8-byte stores (one L2 request each) cost more than the pass they save (busy 17.8 vs 14.7 ms per query)
       const char* es = std::getenv("PGX_PART_SLAB");
-      P.part_slab = !P.part_fused && es && es[0] == '1';
+      P.part_slab = dictid && es && es[0] == '1';
+      dictid = dictid && ((e && e[0] == '1') || P.part_slab);
+      if (dictid) P.part_vdict = static_cast<const int64_t*>(c0.dict_dev);
+      // slab records carry dictIds: with a FOR16 image (<= 65536 values) the aggregation sums through the image in LDS
+      if (P.part_slab && c0.img_kind == IMG_FOR16 && c0.img_dev && c0.img_words >= kImgFor16Blocks &&
+          c0.img_words <= kImgFor16Blocks + 32768) {
+        P.part_img = static_cast<const uint32_t*>(c0.img_dev);
+        P.part_img_words = c0.img_words;
+        P.part_img_sh = c0.img_sh;
+        P.part_grid = ctx->num_cus;
+      }
+    }
+    if (!(ok && keybits + vbits <= 63)) P.part_slab = false;
+    if (ok && keybits + vbits <= 63) {
+      if (vc < 0) {  // COUNT only: records carry no value, the split is always fused
+        const char* es = std::getenv("PGX_PART_SLAB");
+        P.part_slab = es && es[0] == '1';
+      }
+      P.part_dictid = dictid;
+      P.part_fused = (dictid || vc < 0) && !P.part_slab;
+      if (const char* e = std::getenv("PGX_PART_FUSED")) P.part_fused = P.part_fused && e[0] == '1';
       P.use_part = true;
       P.part_vcol = vc;
       P.part_keybits = keybits;
@@ -3304,6 +3326,7 @@ uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {
 // (DefaultGroupKeyGenerator.java:239-343 LONG_MAP / ARRAY_MAP) with a layout that streams HBM instead of probing it.
 // -------------------------------------------------------------------------------------------------
 constexpr int64_t kPartGroupsPerWg = 700;   // groups per pgx_part_aggregate workgroup: LDS table load <= ~1/3 (2048 slots)
+constexpr int64_t kPartGroupsPerWgImg = 400;  // ... pgx_part_aggregate_img (1024 slots beside the value image)
 constexpr uint64_t kPartMaxBytes = uint64_t(96) << 30;  // partition buffers beyond this: fall back to the hash table
 constexpr int kPartChunkRecs = 8192;    // records per pgx_partition workgroup (pgx_kernels.hip kPartChunk)
 
@@ -3329,6 +3352,9 @@ bool part_debug() {
   return e && e[0] == '1';
 }
 
+// second-pass split bits: up to 256 ways for the image aggregation (smaller tables), 128 otherwise
+int part_max_bits2(const ExecPlan& P) { return P.part_img ? 8 : 7; }
+
 void part_size(const ExecPlan& P, PartBuffers& PB) {
   const int64_t N = P.rec_total;
   double ub = double(N);  // groups: at most the rows and the product of the key cardinalities
@@ -3336,7 +3362,8 @@ void part_size(const ExecPlan& P, PartBuffers& PB) {
   for (const auto& g : P.gdicts) prod *= double(g.card);
   ub = std::min(ub, prod);
   PB.nbits2 = 0;
-  while (PB.nbits2 < 7 && double(int64_t(1) << (kPart1Bits + PB.nbits2)) * kPartGroupsPerWg < ub) ++PB.nbits2;
+  const int64_t gpw = P.part_img ? kPartGroupsPerWgImg : kPartGroupsPerWg;
+  while (PB.nbits2 < part_max_bits2(P) && double(int64_t(1) << (kPart1Bits + PB.nbits2)) * gpw < ub) ++PB.nbits2;
   PB.cap1 = N / kPart1N + N / 512 + 65536;
   PB.slab = P.part_slab;
   PB.nwg = P.part_nwg;
@@ -3420,6 +3447,15 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   // count and sum share one LDS add when a partition's count and value sum both fit their bit fields
   const int cbits = bits_for(acap + 1);
   const int pack_shift = (2 * cbits + P.part_vbits <= 64) ? 64 - cbits : 0;
+  if (P.part_img) {
+    PGX_LAUNCH(st, "pgx_part_aggregate_img",
+               pgx_launch_part_aggregate_img(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits,
+                                             P.part_vbase, P.part_img, P.part_img_words, P.part_img_sh, P.part_vdict,
+                                             P.part_min, P.part_max, pack_shift, PB.okey.as<uint64_t>(),
+                                             PB.oplane.as<uint64_t>(), PB.ocap, tail, tail + 3, P.part_grid, st),
+               "partition aggregate (value image)");
+    return;
+  }
   PGX_LAUNCH(st, "pgx_part_aggregate", pgx_launch_part_aggregate(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits, P.part_vbase,
                                       P.part_dictid ? P.part_vdict : nullptr, P.part_sum, P.part_min, P.part_max,
                                       pack_shift, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(), PB.ocap, tail,
@@ -3467,7 +3503,7 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
       PB.cap2 = max_cursor(kPart1N * kCursorStride, PB.nparts()) + 1024;
       continue;
     }
-    if (PB.nbits2 == (part_debug() ? 1 : 7)) return false;  // an LDS table overflowed at the finest split
+    if (PB.nbits2 == (part_debug() ? 1 : part_max_bits2(P))) return false;  // an LDS table overflowed at the finest split
     ++PB.nbits2;
     const int64_t np = PB.nparts();
     PB.cap2 = P.rec_total / np + P.rec_total / np / 4 + (part_debug() ? 1 : 16384);

@@ -104,20 +104,18 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   int stg_off = -1, stg_recs = 0;
   const int stg_pitch = s.R + 2;
   // G_EMIT with part_bits: the sub-step's PT * PR records are split 2^part_bits ways in LDS (histogram, scan, one
-  // global cursor reservation per bucket, bucket-sorted staging) and leave as per-bucket runs: the first radix pass of
-  // the partitioned group-by, fused into the scan
+  // cursor reservation per bucket, bucket-sorted staging) and leave as per-bucket runs: the first radix pass of the
+  // partitioned group-by, fused into the scan.  Cursors: one global cursor per bucket (reserved every sub-step), or
+  // with part_slab this workgroup's own slab of each bucket (an LDS cursor: no global round trip per sub-step)
   const bool epart = emit && s.part_bits > 0;
+  const bool eslab = epart && s.part_slab;
   const int pnb = 1 << s.part_bits;
   int pst_off = -1, phist_off = -1;
-  const bool eslab = epart && s.part_slab;
-  if (eslab) {
-    phist_off = lds;
-    lds += pnb * 4;  // per-bucket cursors of this workgroup's slabs
-  } else if (epart) {
+  if (epart) {
     pst_off = lds;
     lds += s.T * s.R * 8;
     phist_off = lds;
-    lds += pnb * 16 + 16;  // hist (u32), offs (u32), gpos (u64), total
+    lds += pnb * 16 + 16 + (eslab ? pnb * 4 : 0);  // hist (u32), offs (u32), gpos (u64), total[, slab fill (u32)]
   }
   if (emit && !epart) {
     const int waves = s.T / 64;
@@ -218,17 +216,15 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   if (s.group_mode == G_DENSE_GLOBAL) e.ln("u64* const tab = A.table;");
   if (scr_off >= 0) e.ln("PgxRScratch& rscr = *(PgxRScratch*)(lds + ", scr_off / 4, ");");
   if (compact) e.ln("u32* const cstg = lds + ", cst_off / 4, " + (tid >> 6) * ", 64 * std::max<size_t>(1, ccols.size()), ";");
-  if (eslab) {
-    e.ln("u32* const phist = lds + ", phist_off / 4, ";");
-    e.ln("for (int i = tid; i < ", pnb, "; i += PT) phist[i] = 0u;");
-    e.ln("__syncthreads();");
-  } else if (epart) {
+  if (epart) {
     e.ln("u64* const pstage = (u64*)(lds + ", pst_off / 4, ");");
     e.ln("u32* const phist = lds + ", phist_off / 4, ";");
     e.ln("u32* const poffs = phist + ", pnb, ";");
     e.ln("u64* const pgpos = (u64*)(phist + ", 2 * pnb, ");");
     e.ln("u32* const ptotal = phist + ", 4 * pnb, ";");
+    if (eslab) e.ln("u32* const pfill = phist + ", 4 * pnb + 4, ";");
     e.ln("for (int i = tid; i < ", pnb, "; i += PT) phist[i] = 0u;");
+    if (eslab) e.ln("for (int i = tid; i < ", pnb, "; i += PT) pfill[i] = 0u;");
     e.ln("__syncthreads();");
   }
   e.ln("u64 st_docs = 0, st_ent = 0;");
@@ -719,24 +715,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         e.ln("  ((PGX_G ", ty, "*)(S->lmask + ", l, " * S->lmask_words))[r0 / PR] = (", ty, ")lw", l, ";");
       e.ln("}");
     }
-    if (eslab) {
-      // each record goes straight to this workgroup's slab of its bucket: consecutive records of a bucket land in
-      // consecutive words, so L2 completes the slab's lines before they are written back
-      const std::string KM = std::to_string((1ull << s.keybits) - 1ull) + "ull";
-      const std::string SH = std::to_string(64 - s.part_bits);
-      e.ln("{");
-      e.ln("  PGX_G u64* const pout = (PGX_G u64*)A.table;");
-      e.ln("  const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
-      e.ln("  #pragma unroll");
-      e.ln("  for (int j = 0; j < PR; ++j) {");
-      e.ln("    if (recs[j] != ~0ull) {");
-      e.ln("      const u32 b = (u32)(pgx_part_mix(recs[j] & ", KM, ") >> ", SH, ");");
-      e.ln("      const u32 pos = atomicAdd(&phist[b], 1u);");
-      e.ln("      if (pos < (u32)A.part_cap) pout[((long long)b * A.part_nwg + wsl) * A.part_cap + pos] = recs[j];");
-      e.ln("    }");
-      e.ln("  }");
-      e.ln("}");
-    } else if (epart) {
+    if (epart) {
       const std::string KM = std::to_string((1ull << s.keybits) - 1ull) + "ull";
       const std::string SH = std::to_string(64 - s.part_bits);
       e.ln("{");
@@ -750,11 +729,16 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("  pgx_lds_barrier();");
       e.ln("  if (tid < ", pnb, ") {");
       e.ln("    const u32 h = phist[tid];");
-      e.ln("    if (h) {");
-      e.ln("      const u64 g = atomicAdd(A.part_cursor + (long long)tid * A.part_cstride, (u64)h);");
-      e.ln("      pgpos[tid] = g;");
-      e.ln("      if (g + h > (u64)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
-      e.ln("    }");
+      if (eslab) {  // this workgroup's slab of bucket tid: position = fill so far (the kernel end publishes the fill)
+        e.ln("    pgpos[tid] = pfill[tid];");
+        e.ln("    pfill[tid] += h;");
+      } else {
+        e.ln("    if (h) {");
+        e.ln("      const u64 g = atomicAdd(A.part_cursor + (long long)tid * A.part_cstride, (u64)h);");
+        e.ln("      pgpos[tid] = g;");
+        e.ln("      if (g + h > (u64)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
+        e.ln("    }");
+      }
       e.ln("    phist[tid] = 0u;  // ready for the next sub-step (its atomics follow two barriers)");
       e.ln("  }");
       e.ln("  pgx_lds_barrier();");
@@ -764,11 +748,15 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("  pgx_lds_barrier();");
       e.ln("  const int tot = (int)*ptotal;");
       e.ln("  PGX_G u64* const pout = (PGX_G u64*)A.table;");
+      if (eslab) e.ln("  const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
       e.ln("  for (int i = tid; i < tot; i += PT) {");
       e.ln("    const u64 v = pstage[i];");
       e.ln("    const u32 b = (u32)(pgx_part_mix(v & ", KM, ") >> ", SH, ");");
       e.ln("    const u64 pos = pgpos[b] + (u64)(i - (int)poffs[b]);");
-      e.ln("    if (pos < (u64)A.part_cap) pout[(long long)b * A.part_cap + (long long)pos] = v;");
+      if (eslab)
+        e.ln("    if (pos < (u64)A.part_cap) pout[((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)pos] = v;");
+      else
+        e.ln("    if (pos < (u64)A.part_cap) pout[(long long)b * A.part_cap + (long long)pos] = v;");
       e.ln("  }");
       e.ln("  pgx_lds_barrier();");
       e.ln("}");
@@ -861,9 +849,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("  }");
   e.ln("}");
   e.ln("__syncthreads();");
-  if (eslab) {  // slab counts (every record, also past part_cap: the host resizes from the largest)
+  if (eslab) {  // slab fills (every record, also past part_cap: the host resizes from the largest)
     e.ln("for (int i = tid; i < ", pnb, "; i += PT) {");
-    e.ln("  const u32 h = phist[i];");
+    e.ln("  const u32 h = pfill[i];");
     e.ln("  A.part_cursor[((long long)i * A.part_nwg + A.part_wg_base + (long long)blockIdx.x) * A.part_cstride] = h;");
     e.ln("  if (h > (u32)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
     e.ln("}");
@@ -1283,9 +1271,7 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.part_bits = 7;           // first radix pass fused, dictId records
     s.emit_dictid = true;
     shapes.push_back(s);
-    s.cols[1].img = IMG_FOR16;  // first radix pass fused into per-workgroup slabs, value-offset records (the C3 path)
-    s.cols[2].remap = false;
-    s.emit_dictid = false;
+    s.cols[2].remap = false;    // ... into per-workgroup slabs (LDS cursors)
     s.part_slab = true;
     shapes.push_back(s);
   }

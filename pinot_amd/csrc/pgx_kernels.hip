@@ -1638,20 +1638,28 @@ constexpr int kPartPer = 8;                             // records per thread, h
 constexpr int kPartChunk = kPartThreads * kPartPer;     // records per partitioning workgroup (64 KiB LDS staging)
 constexpr uint64_t kNoRecord = ~0ull;
 
-// Exclusive scan of hist[0, nb) (nb <= 128) by wave 0: offs[b] = sum of hist[< b]; *total = sum of all.
-__device__ __forceinline__ void part_scan128(const int* hist, int* offs, int* total, int nb, int tid) {
+constexpr int kPartMaxBuckets = 256;
+
+// Exclusive scan of hist[0, nb) (nb <= 256) by wave 0, four buckets per lane: offs[b] = sum of hist[< b]; *total = sum
+// of all.
+__device__ __forceinline__ void part_scan256(const int* hist, int* offs, int* total, int nb, int tid) {
   if (tid >= 64) return;
-  const int a = 2 * tid < nb ? hist[2 * tid] : 0;
-  const int b = 2 * tid + 1 < nb ? hist[2 * tid + 1] : 0;
-  int x = a + b;
+  int h[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) h[k] = 4 * tid + k < nb ? hist[4 * tid + k] : 0;
+  const int own = h[0] + h[1] + h[2] + h[3];
+  int x = own;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const int y = __shfl_up(x, d, 64);
     if (tid >= d) x += y;
   }
-  const int excl = x - a - b;
-  if (2 * tid < nb) offs[2 * tid] = excl;
-  if (2 * tid + 1 < nb) offs[2 * tid + 1] = excl + a;
+  int run = x - own;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (4 * tid + k < nb) offs[4 * tid + k] = run;
+    run += h[k];
+  }
   if (tid == 63) *total = x;
 }
 
@@ -1678,11 +1686,11 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
   const int cn = static_cast<int>(min<int64_t>(kPartChunk, n - c0));
   const int nb = 1 << nbits;
   __shared__ uint64_t stage[kPartChunk];
-  __shared__ int hist[128], offs[128], total;
-  __shared__ unsigned long long gpos[128];
+  __shared__ int hist[kPartMaxBuckets], offs[kPartMaxBuckets], total;
+  __shared__ unsigned long long gpos[kPartMaxBuckets];
   const int tid = threadIdx.x;
   const uint64_t bmask = static_cast<uint64_t>(nb - 1);
-  if (tid < nb) hist[tid] = 0;
+  for (int i = tid; i < nb; i += kPartThreads) hist[i] = 0;
   const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) +
                                    (in_off ? in_off[r] : static_cast<int64_t>(r) * in_cap) + c0;
   uint64_t rec[kPartPer];
@@ -1700,7 +1708,7 @@ __global__ void __launch_bounds__(kPartThreads) pgx_partition(const uint64_t* __
     rk[k] = bk[k] >= 0 ? atomicAdd(&hist[bk[k]], 1) : 0;
   }
   __syncthreads();
-  part_scan128(hist, offs, &total, nb, tid);
+  part_scan256(hist, offs, &total, nb, tid);
   if (tid < nb && hist[tid]) {
     const unsigned long long g = atomicAdd(&cursor[(static_cast<int64_t>(q) * nb + tid) * cstride],
                                            static_cast<unsigned long long>(hist[tid]));
@@ -1842,6 +1850,119 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
     oplane[2 * ocap + o] = static_cast<unsigned long long>(vlo) ^ 0x8000000000000000ull;
     oplane[3 * ocap + o] = static_cast<unsigned long long>(vhi) ^ 0x8000000000000000ull;
     ++o;
+  }
+}
+
+// Variant for dictId records whose value column has a FOR16 image (sorted dictionary of <= 65536 values): the image
+// (64 block bases + one u16 offset per dictId, 128.25 KiB) lives in LDS beside a 1024-slot table, so SUM looks values
+// up in LDS instead of one L2 request per record.  The image costs one load per workgroup: the grid is persistent
+// (one workgroup per CU walks partitions blockIdx.x, + gridDim.x, ...).  MIN / MAX fold dictIds (sorted dictionary)
+// and map the two extremes through vdict when a group is written.
+constexpr int kAggImgBuckets = 256;
+constexpr int kAggImgSlots = kAggImgBuckets * kAggWays;
+constexpr int kAggImgWords = 64 + 65536 / 2;  // FOR16 image of a 65536-value dictionary, in dwords
+
+template <bool PACK, bool MN, bool MX>
+__global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate_img(const uint64_t* __restrict__ in,
+                                                                      const unsigned long long* __restrict__ in_cnt,
+                                                                      int cstride, int nparts, int64_t cap,
+                                                                      uint64_t keymask, int keybits, int64_t vbase,
+                                                                      const uint32_t* __restrict__ img, int img_words,
+                                                                      int img_sh, const int64_t* __restrict__ vdict,
+                                                                      int pack_shift, uint64_t* __restrict__ okey,
+                                                                      uint64_t* __restrict__ oplane, int64_t ocap,
+                                                                      unsigned long long* __restrict__ ocount,
+                                                                      unsigned long long* __restrict__ overflow) {
+  __shared__ __attribute__((aligned(16))) uint64_t tkey[kAggImgSlots];
+  __shared__ unsigned long long tsum[kAggImgSlots];
+  __shared__ unsigned int tcnt[PACK ? 1 : kAggImgSlots];
+  __shared__ unsigned int tmin[MN ? kAggImgSlots : 1], tmax[MX ? kAggImgSlots : 1];
+  __shared__ __attribute__((aligned(16))) uint32_t simg[kAggImgWords];
+  __shared__ int nfound;
+  __shared__ unsigned long long obase;
+  const int tid = threadIdx.x;
+  const PGX_GLOBAL uint32_t* gi = (const PGX_GLOBAL uint32_t*)img;
+  for (int i = tid; i < img_words; i += kAggThreads) simg[i] = gi[i];
+  const unsigned short* off16 = reinterpret_cast<const unsigned short*>(simg + 64);
+  const PGX_GLOBAL int64_t* vd = (const PGX_GLOBAL int64_t*)vdict;
+  const unsigned long long one = PACK ? (1ull << pack_shift) : 0ull;
+  const unsigned long long smask = PACK ? (1ull << pack_shift) - 1ull : ~0ull;
+  for (int part = blockIdx.x; part < nparts; part += gridDim.x) {
+    for (int i = tid; i < kAggImgSlots; i += kAggThreads) {
+      tkey[i] = kNoRecord;
+      tsum[i] = 0ull;
+      if (!PACK) tcnt[i] = 0u;
+      if (MN) tmin[i] = 0xFFFFFFFFu;
+      if (MX) tmax[i] = 0u;
+    }
+    if (tid == 0) nfound = 0;
+    __syncthreads();
+    const int64_t n = min(static_cast<int64_t>(in_cnt[static_cast<int64_t>(part) * cstride]), cap);
+    const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) + static_cast<int64_t>(part) * cap;
+    bool lost = false;
+    for (int64_t base = 0; base < n; base += kAggThreads * kAggPer) {
+      uint64_t rec[kAggPer];
+#pragma unroll
+      for (int k = 0; k < kAggPer; ++k) {
+        const int64_t i = base + k * kAggThreads + tid;
+        rec[k] = i < n ? __builtin_nontemporal_load(src + i) : kNoRecord;
+      }
+#pragma unroll
+      for (int k = 0; k < kAggPer; ++k) {
+        if (rec[k] == kNoRecord) continue;
+        const uint64_t key = rec[k] & keymask;
+        const unsigned int id = static_cast<unsigned int>(rec[k] >> keybits);
+        const unsigned int sv = simg[id >> img_sh] + static_cast<unsigned int>(off16[id]);  // value - vbase
+        unsigned int bk = static_cast<unsigned int>(part_mix(key)) & (kAggImgBuckets - 1);
+        int slot = -1;
+        for (int t = 0; t < kAggImgBuckets;) {
+          const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(&tkey[bk * kAggWays]);
+          const ulonglong2 a = bp[0], c = bp[1];
+          const int m = a.x == key ? 0 : a.y == key ? 1 : c.x == key ? 2 : c.y == key ? 3 : -1;
+          if (m >= 0) { slot = static_cast<int>(bk) * kAggWays + m; break; }
+          const int e = a.x == kNoRecord ? 0 : a.y == kNoRecord ? 1 : c.x == kNoRecord ? 2 : c.y == kNoRecord ? 3 : -1;
+          if (e >= 0) {
+            const int cand = static_cast<int>(bk) * kAggWays + e;
+            const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[cand]), kNoRecord, key);
+            if (prev == kNoRecord || prev == key) { slot = cand; break; }
+            continue;
+          }
+          bk = (bk + 1) & (kAggImgBuckets - 1);
+          ++t;
+        }
+        if (slot < 0) { lost = true; continue; }
+        if (PACK) {
+          atomicAdd(&tsum[slot], one + sv);
+        } else {
+          atomicAdd(&tcnt[slot], 1u);
+          atomicAdd(&tsum[slot], static_cast<unsigned long long>(sv));
+        }
+        if (MN) atomicMin(&tmin[slot], id);
+        if (MX) atomicMax(&tmax[slot], id);
+      }
+    }
+    if (lost) atomicAdd(overflow, 1ull);
+    __syncthreads();
+    int mine = 0;
+    for (int i = tid; i < kAggImgSlots; i += kAggThreads) mine += tkey[i] != kNoRecord;
+    const int before = atomicAdd(&nfound, mine);
+    __syncthreads();
+    if (tid == 0) obase = atomicAdd(ocount, static_cast<unsigned long long>(nfound));
+    __syncthreads();
+    unsigned long long o = obase + static_cast<unsigned long long>(before);
+    for (int i = tid; i < kAggImgSlots; i += kAggThreads) {
+      if (tkey[i] == kNoRecord) continue;
+      if (o >= static_cast<unsigned long long>(ocap)) { atomicAdd(overflow, 1ull); continue; }
+      okey[o] = tkey[i];
+      const unsigned long long c = PACK ? (tsum[i] >> pack_shift) : tcnt[i];
+      const unsigned long long sm = tsum[i] & smask;
+      oplane[o] = c;
+      oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(sm) + static_cast<int64_t>(c) * vbase);
+      oplane[2 * ocap + o] = static_cast<unsigned long long>(MN ? vd[tmin[i]] : 0) ^ 0x8000000000000000ull;
+      oplane[3 * ocap + o] = static_cast<unsigned long long>(MX ? vd[tmax[i]] : 0) ^ 0x8000000000000000ull;
+      ++o;
+    }
+    __syncthreads();  // the table is re-initialised for the next partition
   }
 }
 
@@ -2058,7 +2179,7 @@ extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in
   const long long blocks = static_cast<long long>(nreg) * chunks_per_reg;
   if (blocks <= 0) return hipSuccess;
   // nbits 0: one partition per region group (gathers the scan's slabs of a bucket into one contiguous run)
-  if (blocks > 0x7FFFFFFFll || nbits > 7 || nbits < 0 || reg_div < 1 || shift < 1 || shift > 63) return hipErrorInvalidValue;
+  if (blocks > 0x7FFFFFFFll || nbits > 8 || nbits < 0 || reg_div < 1 || shift < 1 || shift > 63) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pgx::pgx_partition, dim3(static_cast<unsigned>(blocks)), dim3(pgx::kPartThreads), 0, stream, in,
                      in_off, in_cnt, in_cstride, nreg, reg_div, in_cap, chunks_per_reg, keymask, shift, nbits, out, cap,
                      cursor, cstride, overflow);
@@ -2096,6 +2217,37 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
     PGX_AGG_CASE(7, true, true, true)
   }
 #undef PGX_AGG_CASE
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_part_aggregate_img(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
+                                                    int nparts, int64_t cap, uint64_t keymask, int keybits,
+                                                    int64_t vbase, const uint32_t* img, int img_words, int img_sh,
+                                                    const int64_t* vdict, int need_min, int need_max, int pack_shift,
+                                                    uint64_t* okey, uint64_t* oplane, int64_t ocap,
+                                                    unsigned long long* ocount, unsigned long long* overflow, int grid,
+                                                    hipStream_t stream) {
+  if (nparts <= 0) return hipSuccess;
+  if (img_words > pgx::kAggImgWords || img_words < 64 || grid < 1 || !img || !vdict) return hipErrorInvalidValue;
+  grid = grid < nparts ? grid : nparts;
+  const int sel = (pack_shift ? 4 : 0) | (need_min ? 2 : 0) | (need_max ? 1 : 0);
+#define PGX_AGGI_CASE(K, A, B, C)                                                                                  \
+  case K:                                                                                                          \
+    hipLaunchKernelGGL((pgx::pgx_part_aggregate_img<A, B, C>), dim3(grid), dim3(pgx::kAggThreads), 0, stream, in, \
+                       in_cnt, cstride, nparts, cap, keymask, keybits, vbase, img, img_words, img_sh, vdict,       \
+                       pack_shift, okey, oplane, ocap, ocount, overflow);                                          \
+    break;
+  switch (sel) {
+    PGX_AGGI_CASE(0, false, false, false)
+    PGX_AGGI_CASE(1, false, false, true)
+    PGX_AGGI_CASE(2, false, true, false)
+    PGX_AGGI_CASE(3, false, true, true)
+    PGX_AGGI_CASE(4, true, false, false)
+    PGX_AGGI_CASE(5, true, false, true)
+    PGX_AGGI_CASE(6, true, true, false)
+    PGX_AGGI_CASE(7, true, true, true)
+  }
+#undef PGX_AGGI_CASE
   return hipGetLastError();
 }
 
