@@ -113,14 +113,27 @@ class OColumn:
     has_inverted: bool
     bits: int
     mv_ids: Optional[List[np.ndarray]] = None  # multi-value column: the dictIds of every doc (dict_ids: all values)
+    realtime: bool = False  # mutable dictionary: values in arrival order (realtime/impl/dictionary/*MutableDictionary)
 
     @property
     def card(self) -> int:
         return len(self.dictionary)
 
+    def _parse(self, raw: str):
+        if self.dtype == "STRING":
+            return raw
+        if self.dtype in ("INT", "LONG"):
+            return int(raw)
+        return float(np.float32(float(raw))) if self.dtype == "FLOAT" else float(raw)
+
     def index_of(self, raw: str) -> int:
         """Dictionary.indexOf: binary search returning -(insertion)-1 when absent
-        (segment/index/readers/IntDictionary.java:28-37, StringDictionary.java:37-51)."""
+        (segment/index/readers/IntDictionary.java:28-37, StringDictionary.java:37-51); on a mutable dictionary the
+        arrival-order id or -1 (MutableDictionaryReader.getIndexOfFromBiMap)."""
+        if self.realtime:
+            v = self._parse(raw)
+            hits = [i for i, x in enumerate(self.dictionary.tolist()) if x == v]
+            return hits[0] if hits else -1
         if self.dtype == "STRING":
             keys = list(self.dictionary)
             v = raw
@@ -154,6 +167,28 @@ class OSegment:
     columns: Dict[str, OColumn]
     total_docs: int
     total_raw_docs: int
+
+    @staticmethod
+    def from_realtime(dictionaries: Dict[str, Tuple[str, list]], ids: Dict[str, list], num_docs: int,
+                      inverted: Sequence[str] = ()) -> "OSegment":
+        """A consuming segment as RealtimeSegmentImpl holds it (core/realtime/impl/RealtimeSegmentImpl.java:185-334):
+        per column (data type, arrival-order dictionary values) and the per-doc arrival-order dictIds (a list per doc
+        for a multi-value column); never sorted, inverted per the configured columns
+        (RealtimeColumnDataSource.java:140-152)."""
+        cols = {}
+        for name, (dt, values) in dictionaries.items():
+            dictionary = np.array(values, dtype=object) if dt == "STRING" else np.asarray(
+                values, dtype=np.float64 if dt in ("FLOAT", "DOUBLE") else np.int64)
+            per = ids[name][:num_docs]
+            if per and isinstance(per[0], (list, tuple)):
+                mv = [np.asarray(x, dtype=np.int64) for x in per]
+                flat = np.concatenate(mv)
+                cols[name] = OColumn(name, dt, dictionary, flat, False, name in inverted,
+                                     get_num_of_bits(len(dictionary)), mv, realtime=True)
+            else:
+                cols[name] = OColumn(name, dt, dictionary, np.asarray(per, dtype=np.int64), False, name in inverted,
+                                     get_num_of_bits(len(dictionary)), realtime=True)
+        return OSegment(cols, num_docs, num_docs)
 
     @staticmethod
     def from_raw(raw: Dict[str, np.ndarray], inverted: Sequence[str] = (), dtypes: Dict[str, str] = None,
@@ -223,6 +258,19 @@ def make_evaluator(col: OColumn, leaf: dict) -> Evaluator:
     op = leaf["op"]
     card = col.card
     m = np.zeros(card, dtype=bool)
+    if op == "RANGE" and col.realtime:
+        # RangeRealtimeDictionaryPredicateEvaluator.java:34-75: '*' takes the dictionary's min / max value, then every
+        # dictId whose value lies in the range (MutableDictionary.inRange, e.g. IntMutableDictionary.java:143-174)
+        lower, upper, inc_lo, inc_hi = parse_range(leaf["values"][0])
+        if card:
+            vals = col.dictionary.tolist()
+            lo = min(vals) if lower == "*" else col._parse(lower)
+            hi = max(vals) if upper == "*" else col._parse(upper)
+            for i, v in enumerate(vals):
+                ok = (v >= lo if inc_lo else v > lo) and (v <= hi if inc_hi else v < hi)
+                m[i] = ok
+        ids = np.nonzero(m)[0]
+        return Evaluator(op, m, ids, None, len(ids) == 0)
     if op == "RANGE":
         lower, upper, inc_lo, inc_hi = parse_range(leaf["values"][0])
         # RangeOfflineDictionaryPredicateEvaluator.java:30-65

@@ -311,9 +311,11 @@ def _java_string_sort(values: List[str], width: int, pad: str) -> List[str]:
 
 
 def make_column(name: str, values, data_type: str = None, column_type: str = "DIMENSION",
-                inverted: bool = False, pad: str = DEFAULT_PAD, dictionary=None, dict_ids=None) -> Column:
+                inverted: bool = False, pad: str = DEFAULT_PAD, dictionary=None, dict_ids=None,
+                force_unsorted: bool = False) -> Column:
     """Build a v1 column from raw values (SegmentDictionaryCreator + fwd-index creators).  Either raw `values`, or a
-    pre-built sorted `dictionary` plus `dict_ids` (used by the synthetic generator)."""
+    pre-built sorted `dictionary` plus `dict_ids` (used by the synthetic generator).  force_unsorted: write a fixed-bit
+    forward index even when the ids ascend (realtime snapshots: the realtime data source is never sorted)."""
     if dictionary is None:
         vals = np.asarray(values)
         if data_type is None:
@@ -337,7 +339,7 @@ def make_column(name: str, values, data_type: str = None, column_type: str = "DI
         dict_bytes = np.asarray(dictionary).astype(_DICT_NP[data_type]).tobytes()
     bits = num_bits(card)
     dict_ids = np.asarray(dict_ids, dtype=np.int64)
-    is_sorted = bool(n <= 1 or np.all(np.diff(dict_ids) >= 0))
+    is_sorted = not force_unsorted and bool(n <= 1 or np.all(np.diff(dict_ids) >= 0))
     fwd = sorted_b = None
     if is_sorted:
         first = np.searchsorted(dict_ids, np.arange(card), side="left")
