@@ -2928,6 +2928,11 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       }
     }
     J.R = R;
+    // PGX_NO_IMG=1 (A/B): no value images; SUM / MIN / MAX values are gathered from the dictionary for selected rows
+    // only, which frees the LDS for more workgroups per CU
+    if (const char* e = std::getenv("PGX_NO_IMG"))
+      if (e[0] == '1')
+        for (JitCol& C : J.cols) C.img = IMG_NONE;
     // LDS budget: drop the largest images until everything fits (LEAF_RCHUNK: a budget for three workgroups per CU)
     int64_t rch_bytes = 0;
     if (P.rchunk) {

@@ -246,15 +246,15 @@ class DeviceSegments:
         return any(c.name == name and c.inverted for c in self.wl.columns)
 
     def algorithmic_bytes(self, used_columns: List[str], dict_columns: List[str], bitmap_leaves=()) -> int:
-        """per segment, ceil(N*b/8) per distinct column read + card*width per dictionary used + the
-        serialized bytes of every roaring bitmap a bitmap-index leaf reads (NEQ / NOT_IN read the non-matching ones)."""
-        total = 0
+        """per segment, ceil(N*b/8) per distinct column read + the serialized bytes of every roaring bitmap
+        a bitmap-index leaf reads (NEQ / NOT_IN read the non-matching ones); plus card*width per dictionary used, ONCE:
+        the workload's segments share one dictionary per column, staged once (SharedDict) and read once per query, so
+        crediting it per segment would count 1.07 GB at C5 that no kernel reads."""
+        total = sum(c.card * 4 for c in self.wl.columns if c.name in dict_columns)
         for s in self.seg_ids:
             for c in self.wl.columns:
                 if c.name in used_columns:
                     total += (self.rows * c.bits + 7) // 8
-                if c.name in dict_columns:
-                    total += c.card * 4
             for leaf, ids in bitmap_leaves:
                 off = self.inv_offsets[(s, leaf["column"])]
                 sel = np.zeros(len(off) - 1, dtype=bool)

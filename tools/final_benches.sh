@@ -1,0 +1,9 @@
+#!/bin/bash
+# Round-end bench lines (N=1) for every BASELINE config, with their CPU baselines: gpurun_out/final/<wl>_bench.json
+set -euo pipefail
+OUT=gpurun_out/final
+mkdir -p $OUT
+for wl in c5 c1 c2 c3 c4; do
+  timeout -k 10 300 python bench.py --workload $wl > $OUT/${wl}_bench.json 2> $OUT/${wl}_bench.err
+  echo "$wl done"
+done
