@@ -2927,7 +2927,15 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         C.acc32 = range * 32 < 0xFFFFFFFFull;
       }
     }
+    // PGX_FRAC=1 (A/B): eight rows per lane whatever the widths; columns whose 8 rows are not whole dwords (e.g. a
+    // 10-bit key) load the covering words and shift, so every other column's loads stay contiguous per instruction
+    if (const char* e = std::getenv("PGX_FRAC"))
+      if (e[0] == '1' && R > 8) {
+        R = 8;
+        for (JitCol& C : J.cols) C.frac = C.decode && (8 * C.bits) % 32 != 0;
+      }
     J.R = R;
+    if (const char* e = std::getenv("PGX_LD_X4")) J.ld_x4 = e[0] == '1';
     // PGX_NO_IMG=1 (A/B): no value images; SUM / MIN / MAX values are gathered from the dictionary for selected rows
     // only, which frees the LDS for more workgroups per CU
     if (const char* e = std::getenv("PGX_NO_IMG"))

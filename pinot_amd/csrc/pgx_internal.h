@@ -216,11 +216,13 @@ struct JitCol {
   bool acc32 = false;    // R rows of (value - vbase) always fit a u32 partial sum
   bool fp = false;       // FLOAT/DOUBLE values
   bool remap = false;    // group column with a local->global dictId remap table
+  bool frac = false;     // R * bits is not a multiple of 32: a lane's rows start mid-dword (dword-aligned load of
+                         // the covering words, then a funnel shift by (first row * bits) % 32)
 };
 
 struct JitShape {
   int T = 256;           // threads per workgroup
-  int R = 8;             // rows per lane per sub-step (R * bits % 32 == 0 for every decoded column)
+  int R = 8;             // rows per lane per sub-step (R * bits % 32 == 0 for every decoded column without frac)
   std::vector<JitCol> cols;
   std::vector<int> leaf_col, leaf_mode;   // leaf_col -1: doc-range leaf with no column (star-tree node ranges)
   std::vector<int> prog_op, prog_arg;
@@ -244,6 +246,9 @@ struct JitShape {
   // with part_bits: each workgroup appends to its own region ("slab") per bucket through LDS cursors, no staging and no
   // global cursor per sub-step (slab (b, w) at table + (b * part_nwg + part_wg_base + w) * part_cap)
   bool part_slab = false;
+  // forward-index words of a lane that are not a multiple of 4 / 2 dwords (e.g. 10-bit columns at R = 16: 5 dwords)
+  // load as dword-aligned 16-byte loads plus a remainder instead of one load per dword
+  bool ld_x4 = false;
   bool compact = false;   // pack each sub-step's selected rows into consecutive lanes before aggregating (selective)
   bool selmask = false;   // write every row's selection bit (multi-value aggregations read it)
 };

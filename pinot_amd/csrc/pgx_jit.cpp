@@ -56,7 +56,15 @@ struct Emitter {
   }
 };
 
-int dwords_per(const JitShape& s, int c) { return s.R * s.cols[c].bits / 32; }
+// Words a lane loads per sub-step: R * bits / 32, or for frac columns the words covering R * bits bits that start at
+// any multiple of gcd(R * bits, 32) inside the first word.
+int dwords_per(const JitShape& s, int c) {
+  const int rb = s.R * s.cols[c].bits;
+  if (!s.cols[c].frac) return rb / 32;
+  int g = 32;
+  while (rb % g) g >>= 1;
+  return (rb + 32 - g + 31) / 32;
+}
 bool is_docmask(int mode) { return mode == LEAF_DOCMASK || mode == LEAF_DOCMASK_NOT; }
 
 std::string plane_atomic(int op, const std::string& ptr, const std::string& val) {
@@ -167,6 +175,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const bool any_img = lds > 0 && (tab_off != 0 || s.group_mode != G_DENSE_LDS);
 
   Emitter e;
+  if (s.ld_x4) e.o << "#define PGX_LD_X4 1\n";
   e.o << kAbiSrc << "\n" << kDevSrc << "\n";
   e.ln("#define PT ", s.T);
   e.ln("#define PR ", s.R);
@@ -386,6 +395,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       for (int c = 0; c < ncols; ++c) {
         if (!s.cols[c].decode) continue;
         const int D = dwords_per(s, c);
+        if (s.cols[c].frac)
+          e.ln("if (full || r0 < nd) pgx_ld_u<", D, ">(f", c, " + (((long long)r0 * ", s.cols[c].bits, ") >> 5), &", dst,
+               c, "[", u * D, "]); else pgx_zero<", D, ">(&", dst, c, "[", u * D, "]);");
+        else
         e.ln("if (full || r0 < nd) pgx_ld<", D, ">(f", c, " + (long long)(r0 / PR) * ", D, ", &", dst, c, "[", u * D,
              "]); else pgx_zero<", D, ">(&", dst, c, "[", u * D, "]);");
       }
@@ -476,7 +489,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     for (int c = 0; c < ncols; ++c) {
       if (!s.cols[c].decode) continue;
       e.ln("u32 v", c, "[PR];");
-      e.ln("pgx_unpack<", s.cols[c].bits, ", PR>(&c", c, "[", u * dwords_per(s, c), "], v", c, ");");
+      if (s.cols[c].frac)
+        e.ln("pgx_unpack_frac<", s.cols[c].bits, ", PR, ", dwords_per(s, c), ">(&c", c, "[", u * dwords_per(s, c),
+             "], (u32)(((long long)r0 * ", s.cols[c].bits, ") & 31), v", c, ");");
+      else
+        e.ln("pgx_unpack<", s.cols[c].bits, ", PR>(&c", c, "[", u * dwords_per(s, c), "], v", c, ");");
     }
     for (int l = 0; l < nleaves; ++l) {
       if (s.leaf_mode[l] == LEAF_RANGES) e.ln("const u32 W", l, " = pgx_ranges_bits(rg", l, ", nr", l, ", cur", l, ", r0, PR);");
@@ -904,7 +921,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   std::vector<int64_t> k{device, s.T, s.R, s.group_mode, int64_t(s.dense_slots), s.num_planes, s.keybits, s.emit_col,
                          int64_t(s.cols.size()), s.leafmask};
   for (const JitCol& c : s.cols)
-    k.insert(k.end(), {c.bits, c.decode, c.img, c.img_sh, c.img_words, c.acc32, c.fp, c.remap});
+    k.insert(k.end(), {c.bits, c.decode, c.img, c.img_sh, c.img_words, c.acc32, c.fp, c.remap, c.frac});
   auto add = [&](const auto& v) {
     k.push_back(-int64_t(v.size()) - 1);
     for (auto x : v) k.push_back(int64_t(x));
@@ -923,6 +940,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.part_bits);
   k.push_back(s.emit_dictid);
   k.push_back(s.part_slab);
+  k.push_back(s.ld_x4);
   k.push_back(s.compact);
   k.push_back(s.selmask);
   return k;
@@ -1162,6 +1180,12 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.dense_slots = 1000;
     s.R = 16;
     s.T = 1024;
+    shapes.push_back(s);
+    s.ld_x4 = true;  // gk's 5 words per lane as one dword-aligned 16-byte load + one dword
+    shapes.push_back(s);
+    s.ld_x4 = false;  // R = 8: m's words contiguous per load; gk's 80 bits start mid-dword (frac)
+    s.R = 8;
+    s.cols[4].frac = true;
     shapes.push_back(s);
   }
   shapes.push_back(base(8, 16, IMG_NONE, 0));
