@@ -2936,6 +2936,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       }
     J.R = R;
     if (const char* e = std::getenv("PGX_LD_X4")) J.ld_x4 = e[0] == '1';
+    if (const char* e = std::getenv("PGX_SEL_K")) J.sel_k = std::max(0, std::min(8, std::atoi(e)));
     // PGX_NO_IMG=1 (A/B): no value images; SUM / MIN / MAX values are gathered from the dictionary for selected rows
     // only, which frees the LDS for more workgroups per CU
     if (const char* e = std::getenv("PGX_NO_IMG"))

@@ -249,6 +249,9 @@ struct JitShape {
   // forward-index words of a lane that are not a multiple of 4 / 2 dwords (e.g. 10-bit columns at R = 16: 5 dwords)
   // load as dword-aligned 16-byte loads plus a remainder instead of one load per dword
   bool ld_x4 = false;
+  // dense group-by over sparse selections: the group-table updates of a sub-step run per slot of a lane's first sel_k
+  // selected rows (0: per row)
+  int sel_k = 0;
   bool compact = false;   // pack each sub-step's selected rows into consecutive lanes before aggregating (selective)
   bool selmask = false;   // write every row's selection bit (multi-value aggregations read it)
 };
