@@ -3025,6 +3025,27 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       J.part_slab = P.part_slab;
     }
     J.dense_slots = P.dense_slots;
+    // COUNT + one integer SUM / AVG over a dense LDS table: one packed 64-bit add per row when, for every segment of
+    // the group, its rows fit the count field and rows x value range fit the offset field (flushed per segment);
+    // opt-in: PGX_DENSE_PACK=1
+    if (K.group_mode == G_DENSE_LDS && K.num_planes == 2 && K.num_aggs == 1 &&
+        (K.agg_kind[0] == A_SUM || K.agg_kind[0] == A_AVG) && !P.use_part) {
+      const int c = K.agg_col[0];
+      const char* e = std::getenv("PGX_DENSE_PACK");
+      if (e && e[0] == '1' && c >= 0 && J.cols[c].img != IMG_NONE && !J.cols[c].fp) {
+        int64_t maxdocs = 1;
+        uint64_t vrange = 0;
+        for (int sg : members) {
+          maxdocs = std::max<int64_t>(maxdocs, P.ksegs[sg].num_docs);
+          vrange = std::max<uint64_t>(vrange, P.segcols[sg][c]->vrange);
+        }
+        const int cb = bits_for(maxdocs + 1);
+        const long double sum_max = (long double)maxdocs * (long double)(vrange + 1);
+        int sb = 0;
+        while (sb < 64 && std::ldexp(1.0L, sb) <= sum_max) ++sb;
+        if (cb + sb <= 64) J.dense_pack = 64 - cb;
+      }
+    }
     J.leafmask = P.fsm_on && P.lmask_off[members[0]] >= 0;
     J.compact = P.rchunk && !P.use_part;  // selective bitmap filters: aggregate the selected rows packed
     if (const char* e = std::getenv("PGX_COMPACT")) J.compact = e[0] == '1' && !P.use_part;

@@ -252,6 +252,9 @@ struct JitShape {
   // dense group-by over sparse selections: the group-table updates of a sub-step run per slot of a lane's first sel_k
   // selected rows (0: per row)
   int sel_k = 0;
+  // dense LDS group-by of COUNT + one integer SUM / AVG with a value image: both planes in ONE 64-bit LDS add, the
+  // row count above bit dense_pack (the value offset below), flushed per segment (0: two adds per row)
+  int dense_pack = 0;
   bool compact = false;   // pack each sub-step's selected rows into consecutive lanes before aggregating (selective)
   bool selmask = false;   // write every row's selection bit (multi-value aggregations read it)
 };

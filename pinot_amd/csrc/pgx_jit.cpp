@@ -363,6 +363,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // branch that sparse filters rarely enter).  With 3.7% of rows selected, 16 row-steps per sub-step of which ~15
   // still carry a selected lane become 4 slot-steps.
   const bool dense_g = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL;
+  const bool pack = s.dense_pack > 0 && s.group_mode == G_DENSE_LDS && s.num_planes == 2 && naggs == 1 &&
+                    (s.agg_kind[0] == A_SUM || s.agg_kind[0] == A_AVG) && !s.cols[s.agg_col[0]].fp &&
+                    s.cols[s.agg_col[0]].img != IMG_NONE && !emit;
   bool sel = s.sel_k > 0 && dense_g && !emit && !compact;
   for (int c = 0; c < ncols && sel; ++c) sel = !gcolv[c];
   for (size_t g = 0; g < s.gcol.size() && sel; ++g) sel = !gremap[g];
@@ -680,6 +683,14 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         key += id + " * " + std::to_string(s.gmul[g]) + "u";
       }
       e.ln("const u32 key = ", key.empty() ? "0u" : key, ";");
+      if (pack) {  // count and value offset in one add (the segment flush splits them and adds count * vbase)
+        const int c = s.agg_col[0];
+        e.ln("atomicAdd(&tab[key], (1ull << ", s.dense_pack, ") + (u64)", img_value(s, c, img_off, "v" + std::to_string(c) + "[j]"),
+             ");");
+        e.ind = 6;
+        e.ln("}");
+        return;
+      }
       e.ln("atomicAdd(&tab[key], 1ull);");
       for (int a = 0; a < naggs; ++a) {
         const int k = s.agg_kind[a];
@@ -914,6 +925,20 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("}");
     }
   }
+  if (pack) {  // per-segment flush of the packed table: counts and sums (offset sums + count * this segment's vbase)
+    const int c = s.agg_col[0];
+    const std::string mask = std::to_string((1ull << s.dense_pack) - 1ull) + "ull";
+    e.ln("__syncthreads();");
+    e.ln("for (int i = tid; i < ", s.dense_slots, "; i += PT) {");
+    e.ln("  const u64 x = tab[i];");
+    e.ln("  if (x == 0ull) continue;");
+    e.ln("  const u64 cnt = x >> ", s.dense_pack, ";");
+    e.ln("  atomicAdd(A.table + i, cnt);");
+    e.ln("  atomicAdd(A.table + ", s.dense_slots, " + i, (x & ", mask, ") + cnt * (u64)vb", c, ");");
+    e.ln("  tab[i] = 0ull;");
+    e.ln("}");
+    e.ln("__syncthreads();");
+  }
   e.ln("t = t2;");
   e.ln("++seg;");
   e.ind = 1;
@@ -945,7 +970,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ind--;
     e.ln("}");
   }
-  if (s.group_mode == G_DENSE_LDS) {
+  if (s.group_mode == G_DENSE_LDS && !pack) {
     e.ln("for (int i = tid; i < ", s.dense_slots * s.num_planes, "; i += PT) {");
     e.ind++;
     e.ln("const int p = i / ", s.dense_slots, ";");
@@ -1003,6 +1028,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.part_slab);
   k.push_back(s.ld_x4);
   k.push_back(s.sel_k);
+  k.push_back(s.dense_pack);
   k.push_back(s.compact);
   k.push_back(s.selmask);
   return k;
@@ -1252,6 +1278,9 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.R = 16;         // group-table updates per slot of a lane's first 4 selected rows
     s.cols[4].frac = false;
     s.sel_k = 4;
+    shapes.push_back(s);
+    s.sel_k = 0;      // count and sum in one 64-bit LDS add, flushed per segment
+    s.dense_pack = 40;
     shapes.push_back(s);
   }
   shapes.push_back(base(8, 16, IMG_NONE, 0));
