@@ -1942,6 +1942,8 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   // same INT/LONG column whose dictionary is identical in every segment (one value base), with a value range of at
   // most 32 bits, and key + value fit 63 bits.
   P.use_part = false;
+  P.part_slab = P.part_fused = P.part_dictid = false;
+  P.part_img = nullptr;
   if (K.group_mode == G_HASH64 && jit_enabled() && part_enabled() && !(xflags & PGX_X_NO_PARTITION) &&
       K.num_qcols <= PGX_J_MAX_COLS) {
     int vc = -1;
@@ -2002,7 +2004,10 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         P.part_grid = ctx->num_cus;
       }
     }
-    if (!(ok && keybits + vbits <= 63)) P.part_slab = false;
+    if (!(ok && keybits + vbits <= 63)) {
+      P.part_slab = false;
+      P.part_img = nullptr;
+    }
     if (ok && keybits + vbits <= 63) {
       if (vc < 0) {  // COUNT only: records carry no value, the split is always fused
         const char* es = std::getenv("PGX_PART_SLAB");
@@ -2113,7 +2118,8 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     int64_t ids_off = -1;   // chunk blob offset of the dictId list (bitmap leaves), nb entries
     int nb = 0;
   };
-  using LeafKey = std::tuple<size_t, const uint32_t*, int32_t, int32_t, int>;
+  // keyed by whether the leaf reads the inverted index: a scan-only segment's entry carries no dictId list
+  using LeafKey = std::tuple<size_t, const uint32_t*, int32_t, int32_t, int, bool>;
   struct ChunkOut {
     std::vector<int32_t> blob;
     std::map<const std::vector<int32_t>*, size_t> remap_off;
@@ -2194,7 +2200,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           continue;
         }
         const bool neg = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
-        auto mit = o.leaf_memo.find(LeafKey(l, b.words, b.lo, b.hi, col.card));
+        auto mit = o.leaf_memo.find(LeafKey(l, b.words, b.lo, b.hi, col.card, bitmap_leaf));
         if (mit == o.leaf_memo.end()) {
           LeafMemo m;
           if (b.words) {
@@ -2235,7 +2241,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
                 if (id < b.lo || id > b.hi) take(id);
             }
           }
-          mit = o.leaf_memo.emplace(LeafKey(l, b.words, b.lo, b.hi, col.card), m).first;
+          mit = o.leaf_memo.emplace(LeafKey(l, b.words, b.lo, b.hi, col.card, bitmap_leaf), m).first;
         }
         const LeafMemo& m = mit->second;
         L.mode = m.mode;
@@ -3482,7 +3488,7 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   // count and sum share one LDS add when a partition's count and value sum both fit their bit fields
   const int cbits = bits_for(acap + 1);
   const int pack_shift = (2 * cbits + P.part_vbits <= 64) ? 64 - cbits : 0;
-  if (P.part_img) {
+  if (P.part_img && PB.slab) {  // the image aggregation only on the slab path it was measured on
     PGX_LAUNCH(st, "pgx_part_aggregate_img",
                pgx_launch_part_aggregate_img(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits,
                                              P.part_vbase, P.part_img, P.part_img_words, P.part_img_sh, P.part_vdict,
@@ -3752,8 +3758,18 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   int done = 0;
   const int dev = ctx->device;
   std::vector<std::string> prof(hp.on ? nb : 0);  // PGX_HOST_PROFILE: each planner's phase marks
+  // set when batch 0 turns out ineligible: the tasks not yet started return at once (the caller re-plans the list)
+  std::atomic<bool> cancel{false};
   auto plan_one = [&, dev](int b) {
     Batch& x = bt[b];
+    if (b > 0 && cancel.load(std::memory_order_relaxed)) {
+      std::lock_guard<std::mutex> g(mu);
+      x.eligible = false;
+      x.ready = true;
+      ++done;
+      cv.notify_all();
+      return;
+    }
     HostProf bp;
     if (bp.on) g_prof_mark = [&bp](const char* w) { bp.mark(w); };
     try {
@@ -3842,7 +3858,10 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
     Batch& x = bt[b];
     if (x.err) std::rethrow_exception(x.err);
     if (!x.eligible) {
-      if (b == 0) return false;  // nothing launched yet: the caller plans the whole list at once
+      if (b == 0) {  // nothing launched yet: the caller plans the whole list at once
+        cancel.store(true, std::memory_order_relaxed);
+        return false;
+      }
       fail(PGX_ERR_INTERNAL, "batched plans disagree");
     }
     ExecPlan& P = *x.P;

@@ -81,16 +81,19 @@ def test_bitmap_leaves_match_oracle_and_scan(ctx, segs, text):
         assert blk.get_aggregation_result() == blk_scan.get_aggregation_result()
 
 
-@pytest.mark.parametrize("text", QUERIES[5:])
-def test_mixed_bitmap_and_scan_segments_in_one_query(ctx, segs, text):
+@pytest.mark.parametrize("order", ["isi", "si", "ssi"])
+@pytest.mark.parametrize("text", QUERIES)
+def test_mixed_bitmap_and_scan_segments_in_one_query(ctx, segs, text, order):
     """One launch over an inverted segment (combined bitmap program or per-leaf masks) and a scan-only segment: the
-    combine over both equals the oracle's combine of the two identical segments."""
+    combine over both equals the oracle's combine of the identical segments.  The orders put a scan-only segment first
+    too ("si", "ssi"), so a leaf planned for a scan segment must not be reused for an inverted one that shares its
+    dictionary and binding (EQ / IN / NEQ / NOT_IN single leaves included)."""
     from pinot_amd import engine as E
     inv, scan, oseg = segs
     q = pql.compile(text)
     pm = E.InstancePlanMakerImplV2(ctx)
-    blk = pm.make_inter_segment_plan([inv, scan, inv], q).execute()
-    o = H.oracle_answer([oseg, oseg, oseg], q, literal=True)
+    blk = pm.make_inter_segment_plan([inv if c == "i" else scan for c in order], q).execute()
+    o = H.oracle_answer([oseg] * len(order), q, literal=True)
     fns = [a["fn"] for a in q["aggregations"]]
     if q.get("group_by"):
         m = blk.get_aggregation_group_by_result()
