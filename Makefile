@@ -35,7 +35,11 @@ build/pgx_merge.o: $(CSRC)/pgx_merge.hip
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o build/pgx_trim.o build/pgx_stats.o build/pgx_merge.o
+build/pgx_narrow.o: $(CSRC)/pgx_narrow.hip $(CSRC)/pgx_internal.h $(CSRC)/pgx_jit_abi.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+pinot_amd/libpgx.so: build/pgx_host.o build/pgx_jit.o build/pgx_kernels.o build/pgx_trim.o build/pgx_stats.o build/pgx_merge.o build/pgx_narrow.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
 
 clean:

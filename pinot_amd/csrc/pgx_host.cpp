@@ -77,6 +77,16 @@ extern "C" hipError_t pgx_launch_part_aggregate_img(const uint64_t* in, const un
                                                     uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                     unsigned long long* ocount, unsigned long long* overflow, int grid,
                                                     hipStream_t stream);
+extern "C" hipError_t pgx_launch_narrow_split(const uint32_t* lo, const uint16_t* hi, const unsigned long long* cnt1,
+                                              int nbuckets, int nwg, int64_t cap1, int rb1, int k2, uint32_t* out,
+                                              int64_t cap2, unsigned int* cnt2, unsigned long long* ovf,
+                                              hipStream_t stream);
+extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsigned int* cnt2, int64_t cap2,
+                                                  int nparts, int rb2, int keybits, int64_t vbase, int img_kind,
+                                                  const uint32_t* img, int img_words, int img_sh, const int64_t* vdict,
+                                                  int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
+                                                  uint64_t* oplane, int64_t ocap, unsigned long long* ctr, int grid,
+                                                  hipStream_t stream);
 extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
                                      int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
                                      uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream);
@@ -1304,6 +1314,17 @@ struct ExecPlan {
   unsigned long long* part_cursor = nullptr;   // fused first pass: bucket cursors, overflow counter, bucket capacity
   unsigned long long* part_overflow = nullptr;
   int64_t part_cap = 0;
+  // narrow records (run_narrow, the default for partitioned plans that qualify): the scan writes dictId records split
+  // 256 ways into per-workgroup slabs (part_slab with kNarrow1Bits), u32 in kq.table and bits 32..47 in part_hi
+  bool part_narrow = false;
+  bool narrow_old_slab = false, narrow_old_dictid = false;  // the radix path's choices, restored on fallback
+  int narrow_vd = 0;              // dictId bits of the value column (0: COUNT only)
+  int narrow_k2min = 0;           // second-split bits the record width needs
+  int narrow_img = 0;             // value image in the aggregation's LDS: 0 none, 1 U32, 2 FOR16
+  const uint32_t* narrow_imgp = nullptr;
+  int narrow_img_words = 0, narrow_img_sh = 0;
+  uint64_t narrow_vrange = 0;     // largest value offset (value - vbase)
+  unsigned short* part_hi = nullptr;
   std::vector<int64_t> rec_base; // per segment: index of its row 0 in the record array
   int64_t rec_total = 0;
   struct JitGroup {
@@ -1942,8 +1963,9 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   // same INT/LONG column whose dictionary is identical in every segment (one value base), with a value range of at
   // most 32 bits, and key + value fit 63 bits.
   P.use_part = false;
-  P.part_slab = P.part_fused = P.part_dictid = false;
+  P.part_slab = P.part_fused = P.part_dictid = P.part_narrow = false;
   P.part_img = nullptr;
+  P.part_hi = nullptr;
   if (K.group_mode == G_HASH64 && jit_enabled() && part_enabled() && !(xflags & PGX_X_NO_PARTITION) &&
       K.num_qcols <= PGX_J_MAX_COLS) {
     int vc = -1;
@@ -2024,6 +2046,43 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       P.part_sum = need_sum;
       P.part_min = need_min;
       P.part_max = need_max;
+      // Narrow records (default; PGX_PART_NARROW=0 keeps the 8-byte radix path): the value's dictId rides in a record of
+      // keybits - 8 + dictId bits (<= 48) out of the scan's own 256-way split, then <= 32 bits after the second split,
+      // and the aggregation looks values up in the column's image (FOR16 / U32) in LDS (run_narrow).  Needs a sorted
+      // dictionary (MIN / MAX of dictIds) and, for SUM / AVG, an image that fits beside the aggregation tables.
+      const char* en = std::getenv("PGX_PART_NARROW");
+      if (!(en && en[0] == '0') && !P.part_slab && !P.part_fused && keybits > kNarrow1Bits) {
+        int vd = 0, imgk = 0;
+        bool nok = true;
+        if (vc >= 0) {
+          const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
+          nok = c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end());
+          vd = bits_for(c0.card);
+          if (c0.img_dev && c0.img_kind == IMG_FOR16 && c0.img_words <= kImgFor16Blocks + 32768) imgk = 2;
+          else if (c0.img_dev && c0.img_kind == IMG_U32 && c0.img_words <= kImgFor16Blocks + 32768) imgk = 1;
+          if (need_sum && !imgk) nok = false;
+          if (nok) {
+            P.part_vdict = static_cast<const int64_t*>(c0.dict_dev);
+            P.narrow_imgp = imgk ? static_cast<const uint32_t*>(c0.img_dev) : nullptr;
+            P.narrow_img_words = imgk ? c0.img_words : 0;
+            P.narrow_img_sh = c0.img_sh;
+            P.narrow_vrange = c0.vrange;
+          }
+        }
+        const int rb1 = keybits - kNarrow1Bits;
+        int k2 = std::max(0, rb1 + vd - 32);
+        if (rb1 - k2 > 31) k2 = rb1 - 31;
+        if (nok && rb1 + vd <= 48 && k2 <= kNarrowMaxBits2) {
+          P.narrow_old_slab = P.part_slab;
+          P.narrow_old_dictid = P.part_dictid;
+          P.part_narrow = true;
+          P.part_slab = true;
+          P.part_dictid = vc >= 0;
+          P.narrow_vd = vd;
+          P.narrow_k2min = k2;
+          P.narrow_img = imgk;
+        }
+      }
     }
   }
 
@@ -2985,6 +3044,10 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     J.T = lds <= 20 * 1024 ? 256 : (lds <= 40 * 1024 ? 512 : 1024);
     if (P.rchunk) J.T = 512;  // three 512-thread workgroups per CU, four tiles per chunk
     if (P.use_part) J.T = std::min(J.T, 512);  // record-emitting kernels hold R 64-bit records per lane: 256 VGPRs
+    if (P.part_narrow) {  // the narrow split stages a whole sub-step (T * R records): 32 records per bucket at T = 512
+      J.T = 512;
+      if (const char* e = std::getenv("PGX_NARROW_T")) J.T = std::atoi(e) == 1024 ? 1024 : (std::atoi(e) == 256 ? 256 : 512);
+    }
     for (int l = 0; l < nleaves; ++l) {
       J.leaf_col.push_back(K.leaf_col[l]);
       const int ri = P.roar_index[members[0]][l];
@@ -3026,9 +3089,11 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     if (P.use_part) {
       J.keybits = P.part_keybits;
       J.emit_col = P.part_vcol;
-      J.part_bits = (P.part_fused || P.part_slab) ? kPart1Bits : 0;
+      J.part_bits = P.part_narrow ? kNarrow1Bits : ((P.part_fused || P.part_slab) ? kPart1Bits : 0);
       J.emit_dictid = P.part_dictid;
       J.part_slab = P.part_slab;
+      J.part_narrow = P.part_narrow;
+      J.narrow_vbits = P.part_narrow ? P.narrow_vd : 0;
     }
     J.dense_slots = P.dense_slots;
     // COUNT + one integer SUM / AVG over a dense LDS table: one packed 64-bit add per row when, for every segment of
@@ -3178,6 +3243,7 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
       G.args.part_cap = P.part_cap;
       G.args.part_cstride = P.part_slab ? 1 : kCursorStride;
       G.args.part_nwg = P.part_nwg;
+      G.args.part_hi = P.part_hi;
       void* params[] = {&G.args};
       PGX_LAUNCH(st, "pgxq", hipModuleLaunchKernel(static_cast<hipFunction_t>(G.fn), G.grid, 1, 1, G.T, 1, 1, 0, st, params,
                                       nullptr),
@@ -3550,6 +3616,134 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
     PB.cap2 = P.rec_total / np + P.rec_total / np / 4 + (part_debug() ? 1 : 16384);
   }
   return false;
+}
+
+// -------------------------------------------------------------------------------------------------
+// Narrow partitioned group-by (pgx_narrow.hip): the scan's 256-way split into per-workgroup slabs of u32 (+ u16)
+// dictId records, pgx_narrow_split into 2^(8 + k2) partitions of u32 records, pgx_narrow_aggregate with wavefront-
+// private LDS tables and the value image.  Capacities are sized from the row counts with an 8-sigma margin over the
+// binomial bucket sizes a uniform mix gives; a skewed key distribution that overflows one falls back to the 8-byte
+// radix path (run_partitioned), which sizes from measured counts.
+// -------------------------------------------------------------------------------------------------
+constexpr int kNarrowSlots = 192;  // pgx_narrow.hip kNASlots: one wavefront's table
+constexpr int kNarrowMaxWg = 1024; // pgx_narrow.hip kN2MaxSlabs
+
+struct NarrowBuffers {
+  int k2 = 0, rb1 = 0, rb2 = 0, cshift = 0;
+  bool hib = false;
+  int64_t nwg = 0, cap1 = 0, cap2 = 0, ocap = 0, nparts = 0;
+  DevBuf lo1, hi1, cnt1, rec2, cnt2, okey, oplane, ctr;  // ctr: ocount | overflow scan | split | aggregation
+};
+
+int64_t narrow_cap(double m, int64_t slack) {  // mean + 8 sigma (binomial, p small) + slack, a multiple of 4
+  const int64_t c = int64_t(m + 8.0 * std::sqrt(std::max(m, 1.0))) + slack;
+  return (c + 3) & ~int64_t(3);
+}
+
+bool narrow_size(const ExecPlan& P, NarrowBuffers& NB) {
+  const int K = P.part_keybits;
+  NB.rb1 = K - kNarrow1Bits;
+  NB.hib = NB.rb1 + P.narrow_vd > 32;
+  NB.nwg = P.part_nwg;
+  if (NB.nwg < 1 || NB.nwg > kNarrowMaxWg) return false;
+  // second split: what the record width needs, finer while partitions would average more than 64 groups
+  double ub = double(P.rec_total), prod = 1;
+  for (const auto& g : P.gdicts) prod *= double(g.card);
+  ub = std::min(ub, prod);
+  NB.k2 = P.narrow_k2min;
+  while (NB.k2 < kNarrowMaxBits2 && NB.k2 < NB.rb1 && ub / double(int64_t(1) << (kNarrow1Bits + NB.k2)) > 64.0) ++NB.k2;
+  if (const char* e = std::getenv("PGX_NARROW_K2"))  // tests: coarser partitions, to drive the table-overflow fallback
+    NB.k2 = std::max(P.narrow_k2min, std::min(std::atoi(e), std::min(kNarrowMaxBits2, NB.rb1)));
+  if (NB.k2 > kNarrowMaxBits2 || NB.k2 > NB.rb1) return false;
+  NB.rb2 = NB.rb1 - NB.k2;
+  if (NB.rb2 + P.narrow_vd > 32 || NB.rb2 > 31) return false;
+  NB.nparts = int64_t(1) << (kNarrow1Bits + NB.k2);
+  NB.cap1 = narrow_cap(double(P.part_wg_rows) / (1 << kNarrow1Bits), 64);
+  NB.cap2 = narrow_cap(double(P.rec_total) / double(NB.nparts), 64);
+  if (NB.cap1 * NB.nwg >= (int64_t(1) << 32) || NB.cap2 >= (int64_t(1) << 31)) return false;
+  // count and value-offset sum of one group in one u64: count < 2^cb (a partition holds <= cap2 records)
+  const int cb = bits_for(NB.cap2 + 1);
+  const long double smax = (long double)NB.cap2 * (long double)P.narrow_vrange;
+  int sb = 1;
+  while (sb < 64 && std::ldexp(1.0L, sb) <= smax) ++sb;
+  if (cb + sb > 64 || cb > 62) return false;
+  NB.cshift = 64 - cb;
+  NB.ocap = std::max<int64_t>(1, std::min<int64_t>(P.rec_total, NB.nparts * kNarrowSlots));
+  const uint64_t bytes = uint64_t(kNarrow1Bits == 8 ? 256 : (1 << kNarrow1Bits)) * NB.nwg * NB.cap1 * (NB.hib ? 6 : 4) +
+                         uint64_t(NB.nparts) * NB.cap2 * 4 + uint64_t(NB.ocap) * 40;
+  return bytes <= kPartMaxBytes;
+}
+
+void narrow_alloc(pgx_ctx* ctx, NarrowBuffers& NB) {
+  const int64_t slabs = int64_t(1 << kNarrow1Bits) * NB.nwg;
+  NB.lo1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 4);
+  if (NB.hib) NB.hi1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 2);
+  NB.cnt1 = DevBuf(ctx, size_t(slabs) * 8);
+  NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4);
+  NB.cnt2 = DevBuf(ctx, size_t(NB.nparts) * 4);
+  NB.okey = DevBuf(ctx, size_t(NB.ocap) * 8);
+  NB.oplane = DevBuf(ctx, size_t(NB.ocap) * 4 * 8);
+  NB.ctr = DevBuf(ctx, 4 * 8);
+}
+
+// Before the scan: zero the slab fills (workgroups without tiles publish none) and the counters; point the scan's
+// record outputs at the slabs.
+void narrow_prepare(ExecPlan& P, NarrowBuffers& NB, hipStream_t st) {
+  hip_check(hipMemsetAsync(NB.cnt1.p, 0, size_t(int64_t(1 << kNarrow1Bits) * NB.nwg) * 8, st), "slab counters");
+  hip_check(hipMemsetAsync(NB.ctr.p, 0, 32, st), "narrow counters");
+  P.kq.table = reinterpret_cast<unsigned long long*>(NB.lo1.p);
+  P.part_hi = NB.hib ? NB.hi1.as<unsigned short>() : nullptr;
+  P.part_cursor = devp(NB.cnt1);
+  P.part_overflow = devp(NB.ctr) + 1;
+  P.part_cap = NB.cap1;
+}
+
+// After the scan: the second split and the aggregation.
+void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStream_t st) {
+  if (P.rec_total == 0) return;
+  unsigned long long* ctr = devp(NB.ctr);
+  PGX_LAUNCH(st, "pgx_narrow_split",
+             pgx_launch_narrow_split(NB.lo1.as<uint32_t>(), NB.hib ? NB.hi1.as<uint16_t>() : nullptr, devp(NB.cnt1),
+                                     1 << kNarrow1Bits, int(NB.nwg), NB.cap1, NB.rb1, NB.k2, NB.rec2.as<uint32_t>(),
+                                     NB.cap2, NB.cnt2.as<unsigned int>(), ctr + 2, st),
+             "narrow split");
+  PGX_LAUNCH(st, "pgx_narrow_aggregate",
+             pgx_launch_narrow_aggregate(NB.rec2.as<uint32_t>(), NB.cnt2.as<unsigned int>(), NB.cap2, int(NB.nparts),
+                                         NB.rb2, P.part_keybits, P.part_vbase, P.narrow_img, P.narrow_imgp,
+                                         P.narrow_img_words, P.narrow_img_sh, P.part_vdict, P.part_sum, P.part_min,
+                                         P.part_max, NB.cshift, NB.okey.as<uint64_t>(), NB.oplane.as<uint64_t>(),
+                                         NB.ocap, ctr, ctx->num_cus, st),
+             "narrow aggregate");
+}
+
+// Scan, split and aggregation once.  False (nothing usable produced): a capacity ran over, or the plan does not fit the
+// narrow layout; the caller re-plans the query kernels for the radix path.
+bool run_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hipStream_t st) {
+  alloc_outputs(ctx, P, B, nullptr, 0);
+  if (!narrow_size(P, NB)) return false;
+  narrow_alloc(ctx, NB);
+  narrow_prepare(P, NB, st);
+  reset_outputs(P, B, st);
+  launch_scan(P, st);
+  narrow_enqueue(ctx, P, NB, st);
+  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+  hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
+  unsigned long long* tail = outs + 28;  // spare words of the outputs block: ocount, overflows (part_result reads [28])
+  hip_check(hipMemcpyAsync(tail, NB.ctr.p, 32, hipMemcpyDeviceToHost, st), "D2H");
+  hip_check(hipStreamSynchronize(st), "sync");
+  if (std::getenv("PGX_NARROW_DEBUG"))  // tests: which path ran
+    std::fprintf(stderr, "[pgx narrow] nwg=%lld cap1=%lld k2=%d cap2=%lld groups=%llu ovf=%llu/%llu/%llu\n",
+                 (long long)NB.nwg, (long long)NB.cap1, NB.k2, (long long)NB.cap2, tail[0], tail[1], tail[2], tail[3]);
+  return !tail[1] && !tail[2] && !tail[3];
+}
+
+// The radix path's plan after a narrow attempt gave up: its own slab / dictId choices, 8-byte records.
+void narrow_fallback(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
+  P.part_narrow = false;
+  P.part_slab = P.narrow_old_slab;
+  P.part_dictid = P.narrow_old_dictid;
+  P.part_hi = nullptr;
+  plan_jit(ctx, q, segs, n, P, B);
 }
 
 }  // namespace
@@ -4306,6 +4500,18 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   plan_jit(ctx, q, segs, n, P, B);
   hp.mark("jit");
   if (P.use_part) {
+    if (P.part_narrow) {
+      NarrowBuffers NB;
+      if (run_narrow(ctx, P, B, NB, st)) {
+        PartBuffers PB;
+        PB.okey = std::move(NB.okey);
+        PB.oplane = std::move(NB.oplane);
+        PB.ocap = NB.ocap;
+        part_result(ctx, q, P, B, PB, R);
+        return;
+      }
+      narrow_fallback(ctx, q, segs, n, P, B);
+    }
     PartBuffers PB;
     if (run_partitioned(ctx, P, B, PB, st)) {
       part_result(ctx, q, P, B, PB, R);
@@ -5443,7 +5649,13 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     plan_jit(ctx, *q, segs, n, P, B);
     P.roar_early = false;  // every timed iteration includes the bitmap expansion
     PartBuffers PB;
-    if (P.use_part && !run_partitioned(ctx, P, B, PB, st)) {  // untimed: settles the partition sizes
+    NarrowBuffers NB;
+    bool narrow = false;
+    if (P.use_part && P.part_narrow) {  // untimed: checks the narrow capacities
+      narrow = run_narrow(ctx, P, B, NB, st);
+      if (!narrow) narrow_fallback(ctx, *q, segs, n, P, B);
+    }
+    if (P.use_part && !narrow && !run_partitioned(ctx, P, B, PB, st)) {  // untimed: settles the partition sizes
       P.use_part = false;
       P.jit.clear();
     }
@@ -5458,10 +5670,12 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     hip_check(hipEventRecord(t0, st), "record");
     for (int i = 0; i < iters; ++i) {
       reset_outputs(P, B, st);
-      if (P.use_part) part_prepare(P, PB, st);
+      if (narrow) narrow_prepare(P, NB, st);
+      else if (P.use_part) part_prepare(P, PB, st);
       hip_check(hipEventRecord(ev[2 * i], st), "record");
       launch_scan(P, st);
-      if (P.use_part) part_enqueue(P, PB, st);
+      if (narrow) narrow_enqueue(ctx, P, NB, st);
+      else if (P.use_part) part_enqueue(P, PB, st);
       hip_check(hipEventRecord(ev[2 * i + 1], st), "record");
     }
     hip_check(hipEventRecord(t1, st), "record");
@@ -5483,7 +5697,14 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
       if (P.use_part) {
         unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
         hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
-        hip_check(hipMemcpyAsync(outs + 28, devp(PB.ctr) + PB.ctr_words() - 4, 32, hipMemcpyDeviceToHost, st), "D2H");
+        if (narrow) {
+          hip_check(hipMemcpyAsync(outs + 28, NB.ctr.p, 32, hipMemcpyDeviceToHost, st), "D2H");
+          PB.okey = std::move(NB.okey);
+          PB.oplane = std::move(NB.oplane);
+          PB.ocap = NB.ocap;
+        } else {
+          hip_check(hipMemcpyAsync(outs + 28, devp(PB.ctr) + PB.ctr_words() - 4, 32, hipMemcpyDeviceToHost, st), "D2H");
+        }
         hip_check(hipStreamSynchronize(st), "sync");
         part_result(ctx, *q, P, B, PB, R.get());
       } else {

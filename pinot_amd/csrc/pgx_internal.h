@@ -207,6 +207,32 @@ enum ImgKind : int8_t {
 constexpr int kImgFor16Blocks = 64;
 constexpr int kLdsBudget = 160 * 1024 - 256;  // static LDS of one workgroup, minus the per-plane accumulators
 
+// Narrow partitioned group-by (pgx_host.cpp run_narrow): the packed K-bit group key is mixed by a bijection of
+// [0, 2^K), h = ((((key * c1) & M) ^ (that >> s)) * c2) & M with s = ceil(K / 2) (so one xor-shift inverts itself),
+// and the partitions are h's top bits; h's remaining bits travel in the records and the aggregation rebuilds the key
+// with the inverse.  Shared by the generated scan (pgx_jit.cpp), the split / aggregation kernels and the host.
+constexpr uint64_t kNarrowC1 = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t kNarrowC2 = 0xC2B2AE3D27D4EB4Full;
+constexpr int kNarrow1Bits = 8;      // first split (inside the scan): 256 buckets
+constexpr int kNarrowMaxBits2 = 10;  // second split (pgx_narrow_split): up to 1024 sub-buckets per bucket
+struct NarrowMix {
+  uint64_t mask = 0, c1 = kNarrowC1, c2 = kNarrowC2, ic1 = 0, ic2 = 0;
+  int s = 0;
+};
+inline uint64_t narrow_inverse(uint64_t c) {  // c odd: c * inverse == 1 (mod 2^64), Newton iteration
+  uint64_t x = c;
+  for (int i = 0; i < 6; ++i) x *= 2 - c * x;
+  return x;
+}
+inline NarrowMix narrow_mix(int keybits) {
+  NarrowMix m;
+  m.mask = keybits >= 64 ? ~0ull : (uint64_t(1) << keybits) - 1u;
+  m.s = (keybits + 1) / 2;
+  m.ic1 = narrow_inverse(m.c1);
+  m.ic2 = narrow_inverse(m.c2);
+  return m;
+}
+
 struct JitCol {
   int bits = 0;
   bool decode = false;   // read by a scan leaf, an aggregation or a group key
@@ -257,6 +283,11 @@ struct JitShape {
   int dense_pack = 0;
   bool compact = false;   // pack each sub-step's selected rows into consecutive lanes before aggregating (selective)
   bool selmask = false;   // write every row's selection bit (multi-value aggregations read it)
+  // with part_slab: narrow records (run_narrow).  The key is mixed (NarrowMix), its top part_bits choose the bucket and
+  // the record is the rest of the mix | value dictId << (keybits - part_bits), narrow_vbits wide; it leaves as a u32
+  // (the record's low half) plus, when it is wider than 32 bits, a u16 (bits 32..47) in a second array
+  bool part_narrow = false;
+  int narrow_vbits = 0;
 };
 
 // ----- numEntriesScannedInFilter automaton (pgx_stats.cpp builds it, pgx_kernels.hip pgx_fsm_* runs it) -----

@@ -117,11 +117,24 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // with part_slab this workgroup's own slab of each bucket (an LDS cursor: no global round trip per sub-step)
   const bool epart = emit && s.part_bits > 0;
   const bool eslab = epart && s.part_slab;
+  // narrow records (slab mode only): staged as a u32 array, a u16 array (records wider than 32 bits) and the bucket of
+  // every staged record (u8), instead of 8-byte records
+  const bool enarrow = eslab && s.part_narrow;
+  const int nrb1 = s.keybits - s.part_bits;  // narrow: bits of the key's mix left in the record
+  const bool nhib = enarrow && nrb1 + s.narrow_vbits > 32;
   const int pnb = 1 << s.part_bits;
-  int pst_off = -1, phist_off = -1;
+  int pst_off = -1, phist_off = -1, pstb_off = -1, pstk_off = -1;
   if (epart) {
     pst_off = lds;
-    lds += s.T * s.R * 8;
+    if (enarrow) {
+      lds += s.T * s.R * 4;
+      pstb_off = lds;
+      if (nhib) lds += s.T * s.R * 2;
+      pstk_off = lds;
+      lds += (s.T * s.R + 15) / 16 * 16;
+    } else {
+      lds += s.T * s.R * 8;
+    }
     phist_off = lds;
     lds += pnb * 16 + 16 + (eslab ? pnb * 4 : 0);  // hist (u32), offs (u32), gpos (u64), total[, slab fill (u32)]
   }
@@ -226,7 +239,13 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   if (scr_off >= 0) e.ln("PgxRScratch& rscr = *(PgxRScratch*)(lds + ", scr_off / 4, ");");
   if (compact) e.ln("u32* const cstg = lds + ", cst_off / 4, " + (tid >> 6) * ", 64 * std::max<size_t>(1, ccols.size()), ";");
   if (epart) {
-    e.ln("u64* const pstage = (u64*)(lds + ", pst_off / 4, ");");
+    if (enarrow) {
+      e.ln("u32* const pstA = lds + ", pst_off / 4, ";");
+      if (nhib) e.ln("unsigned short* const pstB = (unsigned short*)(lds + ", pstb_off / 4, ");");
+      e.ln("unsigned char* const pstK = (unsigned char*)(lds + ", pstk_off / 4, ");");
+    } else {
+      e.ln("u64* const pstage = (u64*)(lds + ", pst_off / 4, ");");
+    }
     e.ln("u32* const phist = lds + ", phist_off / 4, ";");
     e.ln("u32* const poffs = phist + ", pnb, ";");
     e.ln("u64* const pgpos = (u64*)(phist + ", 2 * pnb, ");");
@@ -756,7 +775,17 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
           else x = s.cols[s.emit_col].img != IMG_NONE ? img_value(s, s.emit_col, img_off, "v" + ec + "[j]")
                                                       : "(u32)(di" + ec + "[v" + ec + "[j]] - S->vbase[" + ec + "])";
         }
-        e.ln("  rec = (", key, ") | ((u64)(", x, ") << ", s.keybits, ");");
+        if (enarrow) {  // mix the key (NarrowMix), bucket = top part_bits of the mix (bits 56.. of rec), record below
+          const NarrowMix mx = narrow_mix(s.keybits);
+          const std::string M = std::to_string(mx.mask) + "ull";
+          e.ln("  u64 h = ((", key, ") * ", mx.c1, "ull) & ", M, ";");
+          e.ln("  h ^= h >> ", mx.s, ";");
+          e.ln("  h = (h * ", mx.c2, "ull) & ", M, ";");
+          e.ln("  rec = ((h >> ", nrb1, ") << 56) | (h & ", (uint64_t(1) << nrb1) - 1u, "ull) | ((u64)(", x, ") << ", nrb1,
+               ");");
+        } else {
+          e.ln("  rec = (", key, ") | ((u64)(", x, ") << ", s.keybits, ");");
+        }
         e.ln("}");
         e.ln("recs[j] = rec;");
       } else {
@@ -804,7 +833,44 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         e.ln("  ((PGX_G ", ty, "*)(S->lmask + ", l, " * S->lmask_words))[r0 / PR] = (", ty, ")lw", l, ";");
       e.ln("}");
     }
-    if (epart) {
+    if (enarrow) {
+      // Narrow split of this sub-step's PT * PR records 2^part_bits ways: LDS histogram (the atomic returns the record's
+      // rank in its bucket), wave 0 scans it and advances this workgroup's slab fills, records are staged bucket-sorted
+      // and leave as per-bucket runs into the workgroup's own slab of each bucket.  Three barriers per sub-step: the
+      // next sub-step's histogram atomics follow the staging reads of this one's copy-out only through its first
+      // barrier, and the histogram was cleared by wave 0 before the second.
+      e.ln("{");
+      e.ln("  u32 rk[PR];");
+      e.ln("  #pragma unroll");
+      e.ln("  for (int j = 0; j < PR; ++j) rk[j] = recs[j] != ~0ull ? atomicAdd(&phist[(u32)(recs[j] >> 56)], 1u) : 0u;");
+      e.ln("  pgx_lds_barrier();");
+      e.ln("  pgx_narrow_scan<", pnb, ">(phist, poffs, (u32*)pgpos, pfill, ptotal, tid);");
+      e.ln("  pgx_lds_barrier();");
+      e.ln("  #pragma unroll");
+      e.ln("  for (int j = 0; j < PR; ++j)");
+      e.ln("    if (recs[j] != ~0ull) {");
+      e.ln("      const u32 b = (u32)(recs[j] >> 56);");
+      e.ln("      const u32 q = poffs[b] + rk[j];");
+      e.ln("      pstA[q] = (u32)recs[j];");
+      if (nhib) e.ln("      pstB[q] = (unsigned short)(recs[j] >> 32);");
+      e.ln("      pstK[q] = (unsigned char)b;");
+      e.ln("    }");
+      e.ln("  pgx_lds_barrier();");
+      e.ln("  const int tot = (int)*ptotal;");
+      e.ln("  PGX_G u32* const poutA = (PGX_G u32*)A.table;");
+      if (nhib) e.ln("  PGX_G unsigned short* const poutB = (PGX_G unsigned short*)A.part_hi;");
+      e.ln("  const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
+      e.ln("  for (int i = tid; i < tot; i += PT) {");
+      e.ln("    const u32 b = pstK[i];");
+      e.ln("    const u32 pos = ((const u32*)pgpos)[b] + (u32)(i - (int)poffs[b]);");
+      e.ln("    if (pos < (u32)A.part_cap) {");
+      e.ln("      const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)pos;");
+      e.ln("      poutA[o] = pstA[i];");
+      if (nhib) e.ln("      poutB[o] = pstB[i];");
+      e.ln("    }");
+      e.ln("  }");
+      e.ln("}");
+    } else if (epart) {
       const std::string KM = std::to_string((1ull << s.keybits) - 1ull) + "ull";
       const std::string SH = std::to_string(64 - s.part_bits);
       e.ln("{");
@@ -1031,6 +1097,8 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.dense_pack);
   k.push_back(s.compact);
   k.push_back(s.selmask);
+  k.push_back(s.part_narrow);
+  k.push_back(s.narrow_vbits);
   return k;
 }
 
@@ -1392,6 +1460,13 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     shapes.push_back(s);
     s.cols[2].remap = false;    // ... into per-workgroup slabs (LDS cursors)
     s.part_slab = true;
+    shapes.push_back(s);
+    s.part_bits = kNarrow1Bits;  // narrow records: 26 bits of the key's mix + a 16-bit dictId (u32 + u16 arrays)
+    s.part_narrow = true;
+    s.narrow_vbits = 16;
+    shapes.push_back(s);
+    s.emit_col = -1;             // COUNT only: 26-bit records, one u32 array
+    s.narrow_vbits = 0;
     shapes.push_back(s);
   }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {

@@ -72,6 +72,7 @@ struct JArgs {
   long long part_wg_base;            // slab mode: this launch's first workgroup slab and the slabs per bucket; slab
   long long part_nwg;                // (b, w) holds records at table + (b * part_nwg + w) * part_cap, its count at
                                      // part_cursor[(b * part_nwg + w) * part_cstride]
+  unsigned short* part_hi;           // narrow records wider than 32 bits: bits 32..47, same index as the u32 in table
 };
 
 #endif  // PGX_JIT_ABI_H_

@@ -1,0 +1,406 @@
+// Narrow partitioned group-by: the second split and the aggregation (pgx_host.cpp run_narrow).
+//
+// Sparse group keys (LONG_MAP_BASED, DefaultGroupKeyGenerator.java:239-246 / :429-441: the packed raw key probes a
+// Long2IntOpenHashMap per doc; SumAggregationFunction.aggregateGroupBySV, MinAggregationFunction / Max... per doc) are
+// aggregated without a device-wide hash table and without 8-byte records:
+//   1. the generated scan kernel (pgx_jit.cpp, part_narrow) mixes each selected row's key with a bijection of [0, 2^K)
+//      (NarrowMix), splits the rows 256 ways on the mix's top 8 bits inside its LDS and appends to its own slab of each
+//      bucket: K - 8 bits of the mix + the value's dictId, as a u32 (+ a u16 when wider than 32 bits);
+//   2. pgx_narrow_split: one workgroup per bucket reads the bucket's slabs and splits them 2^k2 ways on the next bits of
+//      the mix into partitions of u32 records (the remaining mix bits + the dictId, <= 32 bits by construction);
+//   3. pgx_narrow_aggregate: every wavefront owns a small LDS hash table and aggregates one partition at a time (count
+//      and value sum in one 64-bit LDS add, MIN / MAX over dictIds: numeric dictionaries are sorted, so the extreme
+//      dictId is the extreme value), with the value column's image (FOR16 / U32) in the workgroup's LDS; then rebuilds
+//      each group's packed key from the partition index and the record bits (the mix's inverse) and appends the group.
+// Record bytes per row: 6 written + 6 read + 4 written + 4 read, against 8 B through two radix passes (40 B) before.
+// The output layout (packed key + count / int64 sum / ordered min / ordered max planes) is pgx_part_aggregate's, so the
+// trim, gather, decode and cross-device merges are shared.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pgx_internal.h"
+
+#define PGX_GLOBAL __attribute__((address_space(1)))
+
+namespace pgx {
+namespace {
+
+__device__ __forceinline__ void n_lds_barrier() {  // LDS-only ordering: loads in flight are not drained
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Second split.  Bucket b's records: slab w (one per scan workgroup) holds cnt1[b * nwg + w] records (u32 at
+// lo[(b * nwg + w) * cap1 + i], bits 32.. at hi[same] when hi != null).  A record is r1 | d << rb1 (r1: the mix's low
+// rb1 bits, d: the value's dictId); sub-bucket = r1's top k2 bits; the output record is (r1's low rb1 - k2 bits) |
+// d << (rb1 - k2), appended to partition (b << k2 | sub) at out[part * cap2 + i], its count in cnt2[part].
+// ---------------------------------------------------------------------------------------------------------------------
+constexpr int kN2Threads = 1024;
+constexpr int kN2Per = 16;
+constexpr int kN2Chunk = kN2Threads * kN2Per;  // records per round: 64 KiB of staged u32 records
+constexpr int kN2MaxSub = 1 << kNarrowMaxBits2;
+constexpr int kN2MaxSlabs = 1024;
+
+__global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* __restrict__ lo,
+                                                               const uint16_t* __restrict__ hi,
+                                                               const unsigned long long* __restrict__ cnt1, int nwg,
+                                                               int64_t cap1, int rb1, int k2,
+                                                               uint32_t* __restrict__ out, int64_t cap2,
+                                                               unsigned int* __restrict__ cnt2,
+                                                               unsigned long long* __restrict__ ovf) {
+  __shared__ uint32_t stage[kN2Chunk];
+  __shared__ uint16_t ssub[kN2Chunk];
+  __shared__ uint32_t hist[kN2MaxSub], offs[kN2MaxSub], gpos[kN2MaxSub], fill[kN2MaxSub];
+  __shared__ uint32_t pre[kN2MaxSlabs + 1];
+  __shared__ uint32_t wsum[kN2Threads / 64];
+  __shared__ uint32_t total;
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nsub = 1 << k2;
+  const int rb2 = rb1 - k2;
+  const uint64_t m2 = (uint64_t(1) << rb2) - 1u;
+  for (int i = tid; i < nsub; i += kN2Threads) {
+    hist[i] = 0u;
+    fill[i] = 0u;
+  }
+  // prefix of the slab counts (nwg <= 1024: one per thread)
+  const uint32_t v = tid < nwg ? static_cast<uint32_t>(min(cnt1[static_cast<int64_t>(b) * nwg + tid],
+                                                           static_cast<unsigned long long>(cap1)))
+                               : 0u;
+  uint32_t incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  if (tid < 64) {
+    const uint32_t x = tid < kN2Threads / 64 ? wsum[tid] : 0u;
+    uint32_t xi = x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(xi, d, 64);
+      if (tid >= d) xi += y;
+    }
+    if (tid < kN2Threads / 64) wsum[tid] = xi - x;
+    if (tid == 63) pre[nwg] = xi;
+  }
+  __syncthreads();
+  if (tid < nwg) pre[tid] = wsum[wave] + incl - v;
+  __syncthreads();
+  const uint32_t ntot = pre[nwg];
+  const PGX_GLOBAL uint32_t* glo = (const PGX_GLOBAL uint32_t*)lo + static_cast<int64_t>(b) * nwg * cap1;
+  const PGX_GLOBAL uint16_t* ghi = hi ? (const PGX_GLOBAL uint16_t*)hi + static_cast<int64_t>(b) * nwg * cap1 : nullptr;
+  PGX_GLOBAL uint32_t* gout = (PGX_GLOBAL uint32_t*)out + static_cast<int64_t>(b) * nsub * cap2;
+  int w = 0;  // this thread's slab: positions only grow
+  for (uint32_t c0 = 0; c0 < ntot; c0 += kN2Chunk) {
+    uint32_t xl[kN2Per], xh[kN2Per];
+    // addresses first (LDS prefix walk), then every load in flight, then the split fields
+#pragma unroll
+    for (int k = 0; k < kN2Per; ++k) {
+      const uint32_t pos = c0 + static_cast<uint32_t>(k * kN2Threads + tid);
+      xl[k] = 0u;
+      xh[k] = 0u;
+      if (pos < ntot) {
+        while (pre[w + 1] <= pos) ++w;
+        const int64_t idx = static_cast<int64_t>(w) * cap1 + (pos - pre[w]);
+        xl[k] = __builtin_nontemporal_load(glo + idx);
+        if (ghi) xh[k] = __builtin_nontemporal_load(ghi + idx);
+      }
+    }
+    uint32_t sb[kN2Per], rk[kN2Per];
+#pragma unroll
+    for (int k = 0; k < kN2Per; ++k) {
+      const uint32_t pos = c0 + static_cast<uint32_t>(k * kN2Threads + tid);
+      const uint64_t r1 = static_cast<uint64_t>(xl[k]) | (static_cast<uint64_t>(xh[k]) << 32);
+      sb[k] = pos < ntot ? static_cast<uint32_t>(r1 >> rb2) & static_cast<uint32_t>(nsub - 1) : 0xFFFFFFFFu;
+      xl[k] = static_cast<uint32_t>((r1 & m2) | ((r1 >> rb1) << rb2));
+      rk[k] = sb[k] != 0xFFFFFFFFu ? atomicAdd(&hist[sb[k]], 1u) : 0u;
+    }
+    n_lds_barrier();
+    if (tid < 64) {  // offsets of this round, this workgroup's runs in each partition, histogram cleared
+      constexpr int PER = kN2MaxSub / 64;
+      uint32_t h[PER], x = 0;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int s = tid * PER + q;
+        h[q] = s < nsub ? hist[s] : 0u;
+        x += h[q];
+      }
+      uint32_t xi = x;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(xi, d, 64);
+        if (tid >= d) xi += y;
+      }
+      uint32_t e = xi - x;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int s = tid * PER + q;
+        if (s < nsub) {
+          offs[s] = e;
+          const uint32_t f = fill[s];
+          gpos[s] = f;
+          fill[s] = f + h[q];
+          hist[s] = 0u;
+        }
+        e += h[q];
+      }
+      if (tid == 63) total = xi;
+    }
+    n_lds_barrier();
+#pragma unroll
+    for (int k = 0; k < kN2Per; ++k)
+      if (sb[k] != 0xFFFFFFFFu) {
+        const uint32_t q = offs[sb[k]] + rk[k];
+        stage[q] = xl[k];
+        ssub[q] = static_cast<uint16_t>(sb[k]);
+      }
+    n_lds_barrier();
+    const uint32_t tot = total;
+    for (uint32_t i = tid; i < tot; i += kN2Threads) {
+      const uint32_t s = ssub[i];
+      const uint32_t p = gpos[s] + (i - offs[s]);
+      if (p < static_cast<uint64_t>(cap2)) gout[static_cast<int64_t>(s) * cap2 + p] = stage[i];
+    }
+  }
+  __syncthreads();
+  for (int s = tid; s < nsub; s += kN2Threads) {
+    cnt2[static_cast<int64_t>(b) * nsub + s] = fill[s];
+    if (fill[s] > static_cast<uint64_t>(cap2)) atomicAdd(ovf, 1ull);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------------------------
+// Aggregation.  Wavefront-private open-addressing tables (kNASlots slots: key bits, count << cshift | value sum,
+// min dictId, max dictId); a wavefront takes partitions p = its global index, + all wavefronts, ...; the next 1024
+// records (of this partition or the next) are loaded while the current ones are aggregated.  The workgroup's LDS holds
+// the value image (IMG 1: u32 value - vbase per dictId, 2: FOR16 = 64 u32 block bases + u16 offset per dictId).
+// ctr: [0] groups appended, [3] overflow (a table filled up, or more groups than ocap).
+// ---------------------------------------------------------------------------------------------------------------------
+constexpr int kNAThreads = 512;
+constexpr int kNAWaves = kNAThreads / 64;
+constexpr int kNASlots = 192;
+constexpr int kNAImgWords = 64 + 65536 / 2;
+constexpr uint32_t kNAEmpty = 0xFFFFFFFFu;
+typedef unsigned int na_u32x4 __attribute__((ext_vector_type(4)));
+
+template <int IMG>
+__device__ __forceinline__ uint32_t na_img(const uint32_t* simg, int img_sh, uint32_t d) {
+  if (IMG == 1) return simg[d];
+  if (IMG == 2) return simg[d >> img_sh] + static_cast<uint32_t>(reinterpret_cast<const uint16_t*>(simg + 64)[d]);
+  return 0u;
+}
+
+template <int IMG, bool SUM, bool MN, bool MX>
+__global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
+    const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
+    uint64_t kmask, uint64_t ic1, uint64_t ic2, int ms, int64_t vbase, const uint32_t* __restrict__ img, int img_words,
+    int img_sh, const int64_t* __restrict__ vdict, int cshift, uint64_t* __restrict__ okey,
+    uint64_t* __restrict__ oplane, int64_t ocap, unsigned long long* __restrict__ ctr) {
+  __shared__ __attribute__((aligned(16))) uint32_t simg[IMG ? kNAImgWords : 1];
+  __shared__ uint32_t tkey[kNAWaves * kNASlots];
+  __shared__ unsigned long long tsc[kNAWaves * kNASlots];
+  __shared__ uint32_t tmn[MN ? kNAWaves * kNASlots : 1], tmx[MX ? kNAWaves * kNASlots : 1];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (IMG) {
+    const PGX_GLOBAL uint32_t* gi = (const PGX_GLOBAL uint32_t*)img;
+    for (int i = tid; i < img_words; i += kNAThreads) simg[i] = gi[i];
+  }
+  for (int i = tid; i < kNAWaves * kNASlots; i += kNAThreads) {
+    tkey[i] = kNAEmpty;
+    tsc[i] = 0ull;
+    if (MN) tmn[i] = 0xFFFFFFFFu;
+    if (MX) tmx[i] = 0u;
+  }
+  __syncthreads();  // the only workgroup barrier: wavefronts run independently from here on
+  uint32_t* K = tkey + wave * kNASlots;
+  unsigned long long* S = tsc + wave * kNASlots;
+  uint32_t* N = tmn + (MN ? wave * kNASlots : 0);
+  uint32_t* X = tmx + (MX ? wave * kNASlots : 0);
+  const uint32_t rmask = rb2 >= 32 ? 0xFFFFFFFFu : (1u << rb2) - 1u;
+  const unsigned long long one = 1ull << cshift;
+  const unsigned long long smask = one - 1ull;
+  const int nw = gridDim.x * kNAWaves;
+  const PGX_GLOBAL na_u32x4* src = (const PGX_GLOBAL na_u32x4*)in;
+  const PGX_GLOBAL int64_t* vd = (const PGX_GLOBAL int64_t*)vdict;
+  bool lost = false;
+
+  auto load = [&](int pp, uint32_t i0, uint32_t nn, uint32_t (&buf)[16]) {
+    const int64_t base = (static_cast<int64_t>(pp) * cap2 + i0) >> 2;  // cap2 and i0 are multiples of 4
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t e = static_cast<uint32_t>(q * 256 + lane * 4);
+      na_u32x4 x = {0u, 0u, 0u, 0u};
+      if (i0 + e < nn) x = __builtin_nontemporal_load(src + base + q * 64 + lane);
+      buf[4 * q] = x.x;
+      buf[4 * q + 1] = x.y;
+      buf[4 * q + 2] = x.z;
+      buf[4 * q + 3] = x.w;
+    }
+  };
+  auto flush = [&](int pp) {
+    constexpr int Q = kNASlots / 64;
+    uint32_t has = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) has |= (K[q * 64 + lane] != kNAEmpty ? 1u : 0u) << q;
+    const uint32_t mine = __popc(has);
+    uint32_t incl = mine;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
+    }
+    const uint32_t tot = __shfl(incl, 63, 64);
+    unsigned long long base = 0ull;
+    if (lane == 0 && tot) base = atomicAdd(ctr, static_cast<unsigned long long>(tot));
+    base = __shfl(base, 0, 64);
+    unsigned long long o = base + (incl - mine);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int s = q * 64 + lane;
+      if ((has >> q) & 1u) {
+        if (o < static_cast<unsigned long long>(ocap)) {
+          uint64_t y = ((((static_cast<uint64_t>(pp) << rb2) | K[s]) * ic2) & kmask);
+          y ^= y >> ms;
+          okey[o] = (y * ic1) & kmask;
+          const unsigned long long sc = S[s];
+          const uint64_t c = sc >> cshift;
+          oplane[o] = c;  // plane 0: doc count; planes 1..3: int64 sum, ordered min, ordered max (pgx_part_aggregate)
+          oplane[ocap + o] = static_cast<uint64_t>(static_cast<int64_t>(sc & smask) + static_cast<int64_t>(c) * vbase);
+          int64_t vlo = 0, vhi = 0;
+          if (MN) vlo = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, N[s])) : vd[N[s]];
+          if (MX) vhi = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, X[s])) : vd[X[s]];
+          oplane[2 * ocap + o] = static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull;
+          oplane[3 * ocap + o] = static_cast<uint64_t>(vhi) ^ 0x8000000000000000ull;
+        } else {
+          lost = true;
+        }
+        ++o;
+      }
+      K[s] = kNAEmpty;
+      S[s] = 0ull;
+      if (MN) N[s] = 0xFFFFFFFFu;
+      if (MX) X[s] = 0u;
+    }
+  };
+
+  uint32_t cur[16], nxt[16];
+  int p = blockIdx.x * kNAWaves + wave;
+  uint32_t n = p < nparts ? min(cnt2[p], static_cast<unsigned int>(cap2)) : 0u;
+  uint32_t i0 = 0;
+  if (p < nparts) load(p, 0u, n, cur);
+  while (p < nparts) {
+    int np = p;
+    uint32_t ni0 = i0 + 1024u, nn = n;
+    if (ni0 >= n) {
+      np = p + nw;
+      ni0 = 0u;
+      nn = np < nparts ? min(cnt2[np], static_cast<unsigned int>(cap2)) : 0u;
+    }
+    if (np < nparts) load(np, ni0, nn, nxt);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t e = static_cast<uint32_t>((j >> 2) * 256 + lane * 4 + (j & 3));
+      if (i0 + e >= n) continue;
+      const uint32_t R = cur[j];
+      const uint32_t r2 = R & rmask;
+      const uint32_t d = rb2 >= 32 ? 0u : R >> rb2;
+      uint32_t slot = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNASlots) >> rb2);
+      int found = -1;
+      for (int t = 0; t < kNASlots;) {
+        const uint32_t k = K[slot];
+        if (k == r2) {
+          found = static_cast<int>(slot);
+          break;
+        }
+        if (k == kNAEmpty) {
+          const uint32_t prev = atomicCAS(&K[slot], kNAEmpty, r2);
+          if (prev == kNAEmpty || prev == r2) {
+            found = static_cast<int>(slot);
+            break;
+          }
+          continue;  // another lane took the slot first: look at it again
+        }
+        slot = slot + 1u == static_cast<uint32_t>(kNASlots) ? 0u : slot + 1u;
+        ++t;
+      }
+      if (found < 0) {
+        lost = true;
+        continue;
+      }
+      atomicAdd(&S[found], SUM ? one + na_img<IMG>(simg, img_sh, d) : one);
+      if (MN) atomicMin(&N[found], d);
+      if (MX) atomicMax(&X[found], d);
+    }
+    if (ni0 == 0u) flush(p);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) cur[j] = nxt[j];
+    p = np;
+    i0 = ni0;
+    n = nn;
+  }
+  if (lost) atomicAdd(ctr + 3, 1ull);
+}
+
+}  // namespace
+}  // namespace pgx
+
+extern "C" hipError_t pgx_launch_narrow_split(const uint32_t* lo, const uint16_t* hi, const unsigned long long* cnt1,
+                                              int nbuckets, int nwg, int64_t cap1, int rb1, int k2, uint32_t* out,
+                                              int64_t cap2, unsigned int* cnt2, unsigned long long* ovf,
+                                              hipStream_t stream) {
+  if (nbuckets <= 0) return hipSuccess;
+  if (nwg < 1 || nwg > pgx::kN2MaxSlabs || k2 < 0 || k2 > pgx::kNarrowMaxBits2 || rb1 - k2 < 0 || rb1 > 48 ||
+      cap1 < 1 || cap1 * nwg >= (int64_t(1) << 32) || cap2 < 1 || cap2 >= (int64_t(1) << 32) || !lo || !out || !cnt1 ||
+      !cnt2 || !ovf)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pgx::pgx_narrow_split, dim3(nbuckets), dim3(pgx::kN2Threads), 0, stream, lo, hi, cnt1, nwg, cap1,
+                     rb1, k2, out, cap2, cnt2, ovf);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsigned int* cnt2, int64_t cap2,
+                                                  int nparts, int rb2, int keybits, int64_t vbase, int img_kind,
+                                                  const uint32_t* img, int img_words, int img_sh, const int64_t* vdict,
+                                                  int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
+                                                  uint64_t* oplane, int64_t ocap, unsigned long long* ctr, int grid,
+                                                  hipStream_t stream) {
+  if (nparts <= 0) return hipSuccess;
+  if (rb2 < 0 || rb2 > 31 || keybits < 1 || keybits > 64 || cap2 < 4 || (cap2 & 3) || cshift < 1 || cshift > 63 ||
+      grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 2 ||
+      (img_kind && (!img || img_words < 1 || img_words > pgx::kNAImgWords)) || (need_sum && !img_kind) ||
+      ((need_min || need_max) && !img_kind && !vdict))
+    return hipErrorInvalidValue;
+  const pgx::NarrowMix m = pgx::narrow_mix(keybits);
+  const int sel = img_kind * 8 + (need_sum ? 4 : 0) + (need_min ? 2 : 0) + (need_max ? 1 : 0);
+#define PGX_NA_CASE(C, I, A, B, D)                                                                                   \
+  case C:                                                                                                            \
+    hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D>), dim3(grid), dim3(pgx::kNAThreads), 0, stream, in, cnt2, \
+                       cap2, nparts, rb2, m.mask, m.ic1, m.ic2, m.s, vbase, img, img_words, img_sh, vdict, cshift,   \
+                       okey, oplane, ocap, ctr);                                                                     \
+    break;
+#define PGX_NA_CASES(I)                       \
+  PGX_NA_CASE(I * 8 + 0, I, false, false, false) \
+  PGX_NA_CASE(I * 8 + 1, I, false, false, true)  \
+  PGX_NA_CASE(I * 8 + 2, I, false, true, false)  \
+  PGX_NA_CASE(I * 8 + 3, I, false, true, true)   \
+  PGX_NA_CASE(I * 8 + 4, I, true, false, false)  \
+  PGX_NA_CASE(I * 8 + 5, I, true, false, true)   \
+  PGX_NA_CASE(I * 8 + 6, I, true, true, false)   \
+  PGX_NA_CASE(I * 8 + 7, I, true, true, true)
+  switch (sel) {
+    PGX_NA_CASES(0)
+    PGX_NA_CASES(1)
+    PGX_NA_CASES(2)
+    default:
+      return hipErrorInvalidValue;
+  }
+#undef PGX_NA_CASES
+#undef PGX_NA_CASE
+  return hipGetLastError();
+}

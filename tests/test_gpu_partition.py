@@ -51,9 +51,14 @@ def _execute(ctx, segs, q, flags):
         N.lib().pgx_result_release(r)
 
 
+@pytest.mark.parametrize("mode", ["narrow", "radix"])
 @pytest.mark.parametrize("flt", FILTERS)
 @pytest.mark.parametrize("group", [" GROUP BY g2, a, c", " GROUP BY a, c, g1", " GROUP BY c, g2, s, g1"])
-def test_partitioned_matches_oracle(ctx, seg, flt, group):
+def test_partitioned_matches_oracle(ctx, seg, flt, group, mode, monkeypatch):
+    """Both sparse paths: narrow records (default: the scan's 256-way split, pgx_narrow_split, wavefront tables; the
+    first two key shapes need records wider than 32 bits out of the scan, the u16 array) and the 8-byte radix path
+    (PGX_PART_NARROW=0)."""
+    monkeypatch.setenv("PGX_PART_NARROW", "1" if mode == "narrow" else "0")
     gseg, oseg, fmt = seg
     q = pql.compile(AGGS + (flt % fmt) + group)
     blk, st = _run_inner(ctx, gseg, q)
@@ -152,6 +157,7 @@ def test_partitioned_debug_resize_and_fallback(ctx, monkeypatch, n, card, slab):
     the scan writing per-workgroup slabs (PGX_PART_SLAB=1) or row-order records (0, default)."""
     monkeypatch.setenv("PGX_PART_DEBUG", "1")
     monkeypatch.setenv("PGX_PART_SLAB", slab)
+    monkeypatch.setenv("PGX_PART_NARROW", "0")  # the radix path's own resize / re-split branches
     gseg, raw = _pairs_segment(ctx, n, card, seed=card)
     q = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY ga, gb")
     got = _map(_execute(ctx, [gseg], q, 0))
@@ -268,3 +274,50 @@ def test_fused_first_pass_equals_oracle(ctx, seg, text, mode, monkeypatch):
     fns = [a["fn"] for a in q["aggregations"]]
     for k, v in o["map"].items():
         H.assert_values_equal(m[k], v, fns)
+
+
+@pytest.mark.parametrize("case", ["uniform", "coarse", "skew", "count_only", "min_only"])
+def test_narrow_paths_and_fallback(ctx, monkeypatch, capfd, case):
+    """Narrow records end to end against numpy (every group's count / sum / min / max, exact), including the cases that
+    must leave the narrow layout for the 8-byte radix path: "coarse" (PGX_NARROW_K2=0: 256 partitions of ~1,400 groups
+    overflow the 192-slot wavefront tables) and "skew" (half the rows on one key: its partition outgrows the capacity
+    sized for a uniform mix).  COUNT-only records carry no value (26-bit records, one u32 array)."""
+    from pinot_amd import engine as E
+    rng = np.random.default_rng(99)
+    n, card = 400000, 600
+    dom = np.sort(rng.choice(np.arange(-70000, 70000), size=20000, replace=False)).astype(np.int32)
+    raw = {"ga": rng.integers(0, card, size=n).astype(np.int32),
+           "gb": rng.integers(0, card, size=n).astype(np.int32) * 3,
+           "m": dom[rng.integers(0, len(dom), size=n)]}  # 20,000 values: a value image the aggregation holds in LDS
+    raw["ga"][:card] = np.arange(card)
+    raw["gb"][:card] = np.arange(card) * 3
+    if case == "skew":
+        raw["ga"][card:n // 2 + card] = 7
+        raw["gb"][card:n // 2 + card] = 21
+    if case == "coarse":
+        monkeypatch.setenv("PGX_NARROW_K2", "0")
+    monkeypatch.setenv("PGX_NARROW_DEBUG", "1")  # one "[pgx narrow] ... ovf=a/b/c" line per narrow attempt
+    s, _ = H.build_pair("nw_" + case, raw)
+    gseg = E.IndexSegment(ctx, s)
+    try:
+        text = {"count_only": "SELECT COUNT(*) FROM t GROUP BY ga, gb",
+                "min_only": "SELECT MIN(m) FROM t GROUP BY ga, gb"}.get(case, "SELECT COUNT(*), SUM(m), MIN(m), MAX(m) "
+                                                                           "FROM t GROUP BY ga, gb")
+        q = pql.compile(text)
+        got = _map(_execute(ctx, [gseg], q, 0))
+        exp = _expected(raw)
+        assert len(got) == len(exp)
+        for k, (c, sm, lo, hi) in exp.items():
+            g = got[k]
+            if case == "count_only":
+                assert int(g[0]) == c
+            elif case == "min_only":
+                assert float(g[0]) == lo
+            else:
+                assert (int(g[0]), float(g[1]), float(g[2]), float(g[3])) == (c, sm, lo, hi)
+        lines = [x for x in capfd.readouterr().err.splitlines() if x.startswith("[pgx narrow]")]
+        assert len(lines) == 1, lines  # the narrow path was attempted ...
+        fell_back = not lines[0].endswith("ovf=0/0/0")
+        assert fell_back == (case in ("coarse", "skew")), lines  # ... and kept unless a capacity ran over
+    finally:
+        gseg.destroy()
