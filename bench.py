@@ -247,7 +247,8 @@ def main():
         # one key space on every rank: the union of all ranks' group-column dictionaries, set once per query
         # shape (segment metadata, like staging); dense tables then all-reduce by slot over RCCL, sparse groups merge
         # on the device by packed key
-        multigpu.union_key_domains(q, segs)
+        nccl = os.environ.get("PGX_DIST_BACKEND", "nccl") == "nccl"
+        multigpu.union_key_domains(q, segs, device="cuda:%d" % local if nccl else None)
         slots = C.c_int64()
         N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
         dense = slots.value <= (1 << 22)

@@ -16,6 +16,7 @@ to the Java operators; nothing here computes results on the CPU.
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 import math
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
@@ -130,10 +131,15 @@ def star_skip_dims(seg: SegmentData):
     return [x.strip() for x in v.split(",") if x.strip()]
 
 
+_SEG_UID = itertools.count(1)
+
+
 class IndexSegment:
-    """A segment staged into HBM (Loaders.IndexSegment.load equivalent)."""
+    """A segment staged into HBM (Loaders.IndexSegment.load equivalent).  `uid` identifies the staged segment for the
+    life of the process (caches keyed by segment sets: handles can be reused after a release)."""
 
     def __init__(self, ctx: Context, seg: SegmentData, device_buffers: Optional[Dict[str, int]] = None):
+        self.uid = next(_SEG_UID)
         self.ctx = ctx
         self.data = seg
         self.name = seg.name
@@ -192,6 +198,7 @@ class IndexSegment:
     def from_device(cls, ctx: Context, seg: SegmentData, fwd_device: Dict[str, int]):
         """Stage a segment whose forward indexes already live in HBM (synthetic benchmark data)."""
         self = cls.__new__(cls)
+        self.uid = next(_SEG_UID)
         self.ctx = ctx
         self.data = seg
         self.name = seg.name

@@ -31,70 +31,118 @@ def shard(num_segments: int, world: int, rank: int, scaling: str) -> List[int]:
     return list(range(rank, num_segments, world))
 
 
-def dictionary_fingerprint(columns_values: Sequence[Sequence]) -> List[int]:
-    """Per group-by column: a 63-bit fingerprint of the union of this rank's dictionary values for the column (the
-    rank-local global dictionary build_global_dict builds: sorted distinct values)."""
+def _fingerprint(dt, u) -> int:
+    """63-bit fingerprint of one column's sorted distinct values (and their type)."""
     import hashlib
-    out = []
-    for values in columns_values:
-        parts = [np.asarray(v) for v in values if len(v)]
-        if not parts:
-            u = np.zeros(0)
-        elif parts[0].dtype.kind in "OSU":
-            u = np.array(sorted({str(x) for p in parts for x in p.tolist()}), dtype=object)
-        else:
-            u = np.unique(np.concatenate(parts).astype(np.float64 if parts[0].dtype.kind == "f" else np.int64))
-        h = hashlib.blake2b(digest_size=8)
-        h.update(str(u.dtype).encode())
-        h.update("\x1f".join(map(str, u.tolist())).encode("utf-8") if u.dtype == object else u.tobytes())
-        out.append(int.from_bytes(h.digest(), "little") >> 1)
-    return out
+    h = hashlib.blake2b(digest_size=8)
+    h.update(str(dt).encode())
+    if dt == "STRING":
+        for v in u:
+            b = v.encode("utf-8")
+            h.update(len(b).to_bytes(4, "little"))
+            h.update(b)
+    elif u is not None:
+        h.update(np.ascontiguousarray(u).tobytes())
+    return int.from_bytes(h.digest(), "little") >> 1
 
 
-def union_key_domains(q, segments) -> None:
+def _local_domain(segments, col):
+    """(data type, sorted distinct values) of one group column over this rank's segments' dictionaries."""
+    infos = [s.column(col) for s in segments]
+    dt = infos[0].meta.data_type if infos else None
+    if dt == "STRING":
+        return dt, sorted({str(v) for i in infos for v in i.values}, key=lambda v: v.encode("utf-8"))
+    if dt is None:
+        return None, None
+    kind = np.float64 if dt in ("FLOAT", "DOUBLE") else np.int64
+    return dt, np.unique(np.concatenate([np.asarray(i.values, dtype=kind) for i in infos]))
+
+
+def _gather_bytes(payload: bytes, device) -> List[bytes]:
+    """all_gather of one variable-length byte string per rank as tensors (lengths first, then a padded uint8 tensor)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size()
+    n = torch.tensor([len(payload)], dtype=torch.int64, device=device)
+    ns = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(ns, n)
+    lens = [int(x.item()) for x in ns]
+    cap = max(1, max(lens))
+    buf = torch.zeros(cap, dtype=torch.uint8, device=device)
+    if payload:
+        buf[:len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(device)
+    bufs = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(bufs, buf)
+    return [bytes(b[:k].cpu().numpy().tobytes()) for b, k in zip(bufs, lens)]
+
+
+_DOMAINS = {}  # (group columns, segment uids, world) -> [(data type, values)] of the union
+
+
+def union_key_domains(q, segments, device=None) -> None:
     """Cross-process key identity ("a host-side global dictionary per group-by column"): every rank
     contributes the distinct values of each group-by column over its segments' dictionaries, all ranks build the same
     sorted union, and the query plans its keys over it (pgx_query_set_key_domain).  Dense slots and packed sparse keys
     then mean the same group on every GPU whatever dictionaries the ranks hold, so the partials merge by slot (RCCL
     all-reduce) or by packed key (all-to-all + device merge) -- the value-keyed combine of
-    MCombineGroupByOperator.java:166-191 without moving values.  One all_gather of dictionary values per query shape:
-    segment metadata, not per-row data."""
-    import torch.distributed as dist
-    mine = []
-    for col in q.group_cols:
-        infos = [s.column(col) for s in segments]
-        dt = infos[0].meta.data_type if infos else None
-        if dt == "STRING":
-            u = sorted({str(v) for i in infos for v in i.values})
-        elif dt is None:
-            u = []
-        else:
-            u = np.unique(np.concatenate([np.asarray(i.values, dtype=np.float64 if dt in ("FLOAT", "DOUBLE")
-                                                     else np.int64) for i in infos])).tolist()
-        mine.append((dt, u))
-    allv = [None] * dist.get_world_size()
-    dist.all_gather_object(allv, mine)
-    for g in range(len(q.group_cols)):
-        dts = {p[g][0] for p in allv if p[g][0] is not None}
-        if len(dts) != 1:
-            raise ValueError("group column %s has different types across ranks: %s" % (q.group_cols[g], dts))
-        dt = dts.pop()
-        vals = [v for p in allv for v in p[g][1]]
-        q.set_key_domain(g, vals, dt)
+    MCombineGroupByOperator.java:166-191 without moving values.
 
-
-def dense_layout_agrees(slots: int, fingerprints: Sequence[int], device=None) -> bool:
-    """True iff every rank has the same dense slot count and the same per-column dictionaries, i.e. slot i means the
-    same group on every GPU and the tables can be all-reduced plane by plane.  Otherwise (different value sets across
-    GPUs) the group-by must merge by key VALUE (MCombineGroupByOperator.java:166-191 keys the combine by the value
-    string): the sparse path.  Two tiny all-reduces (MIN and MAX) decide it identically on every rank."""
+    Segment metadata, computed once per (group columns, segment set) and cached: first two all-reduces of per-column
+    fingerprints (MIN, MAX); columns whose dictionaries are the same on every rank (the common case: one table, one
+    schema, shared value domains) need no exchange at all; only the others all-gather their values as byte tensors
+    (`device`: the process group's device, e.g. cuda:N under RCCL; None: CPU, gloo)."""
     import torch
     import torch.distributed as dist
-    t = torch.tensor([int(slots)] + [int(f) for f in fingerprints], dtype=torch.int64, device=device)
-    lo, hi = t.clone(), t.clone()
-    dist.all_reduce(lo, op=dist.ReduceOp.MIN)
-    dist.all_reduce(hi, op=dist.ReduceOp.MAX)
-    return bool(torch.equal(lo, hi))
+    key = (tuple(q.group_cols), tuple(getattr(s, "uid", id(s)) for s in segments), dist.get_world_size())
+    dom = _DOMAINS.get(key)
+    if dom is None:
+        local = [_local_domain(segments, col) for col in q.group_cols]
+        fp = torch.tensor([_fingerprint(dt, u) for dt, u in local], dtype=torch.int64, device=device)
+        lo, hi = fp.clone(), fp.clone()
+        if len(local):
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dom = []
+        for g, (dt, u) in enumerate(local):
+            if dt is not None and int(lo[g]) == int(hi[g]):
+                dom.append((dt, u))
+                continue
+            if dt == "STRING":  # length-prefixed UTF-8 values
+                payload = b"S" + b"".join(len(b).to_bytes(4, "little") + b for b in (v.encode("utf-8") for v in u))
+            elif dt is None:
+                payload = b""
+            else:
+                payload = dt.encode() + b"\0" + np.ascontiguousarray(u).tobytes()
+            parts = _gather_bytes(payload, device)
+            dts, vals = set(), []
+            for p in parts:
+                if not p:
+                    continue
+                if p[:1] == b"S":
+                    dts.add("STRING")
+                    i = 1
+                    while i < len(p):
+                        k = int.from_bytes(p[i:i + 4], "little")
+                        vals.append(p[i + 4:i + 4 + k].decode("utf-8"))
+                        i += 4 + k
+                else:
+                    t, raw = p.split(b"\0", 1)
+                    dts.add(t.decode())
+                    vals.append(np.frombuffer(raw, dtype=np.float64 if t in (b"FLOAT", b"DOUBLE") else np.int64))
+            if not dts:  # no rank holds a segment with this column
+                dom.append((None, None))
+                continue
+            if len(dts) != 1:
+                raise ValueError("group column %s has different types across ranks: %s" % (q.group_cols[g], dts))
+            t = dts.pop()
+            if t == "STRING":
+                dom.append((t, sorted(set(vals), key=lambda v: v.encode("utf-8"))))
+            else:
+                dom.append((t, np.unique(np.concatenate(vals))))
+        _DOMAINS[key] = dom
+    for g, (dt, vals) in enumerate(dom):
+        if dt is not None:
+            q.set_key_domain(g, vals, dt)
 
 
 def merge_dense_planes(t, plane_ops: Sequence[int]) -> None:
@@ -233,7 +281,7 @@ def trim_to_size(fns: Sequence[str], vals, cnts, top_n: int, total: int = None) 
 
 
 # ------------------------------------------------------------------------------------------------
-# Device-side sparse merge (ranks planned the same key space: identical dictionaries, dense_layout_agrees's fingerprint
+# Device-side sparse merge (ranks planned the same key space: identical dictionaries, union_key_domains' fingerprint
 # check).  Every rank's groups stay in HBM as 5-word records (packed key, count, sum, min, max: pgx_result_device_groups),
 # are routed to rank hash(key) mod world with ONE all_to_all_single (RCCL send/recv over xGMI), merged there by the
 # library's device hash merge (pgx_result_merge_groups), trimmed on the device (pgx_result_trim: the key partitions are

@@ -246,11 +246,23 @@ def _dict_worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         segs = _dict_segments(rank)
-        same = multigpu.dictionary_fingerprint([[np.arange(40)]])
-        differ = multigpu.dictionary_fingerprint([[s.columns["g"].dictionary for s in segs]])
-        checks = (multigpu.dense_layout_agrees(40, same),          # identical dictionaries, same slots
-                  multigpu.dense_layout_agrees(40 + rank, same),   # slot counts differ
-                  multigpu.dense_layout_agrees(40, differ))        # same slot count, different values
+        # key spaces: identical dictionaries on both ranks need no exchange (fingerprints agree), differing ones gather
+        # their values; a second call with the same segment set is served from the cache (no collective at all)
+        calls = []
+        real = multigpu._gather_bytes
+        multigpu._gather_bytes = lambda payload, device: calls.append(1) or real(payload, device)
+        same_q, differ_q = _FakeQuery(["g"]), _FakeQuery(["g"])
+        same_segs = [_FakeSeg({"g": _FakeCol(np.arange(40, dtype=np.int64), "INT")})]
+        multigpu.union_key_domains(same_q, same_segs)
+        n_same = len(calls)
+        differ_segs = [_FakeSeg({"g": _FakeCol(np.unique(s.columns["g"].dictionary), "INT")}) for s in segs]
+        multigpu.union_key_domains(differ_q, differ_segs)
+        n_differ = len(calls) - n_same
+        again = _FakeQuery(["g"])
+        multigpu.union_key_domains(again, differ_segs)
+        multigpu._gather_bytes = real
+        checks = (n_same, n_differ, len(calls) - n_same - n_differ, same_q.set[0][1] == list(range(40)),
+                  differ_q.set[0][1] == list(range(47)), again.set == differ_q.set)
         req = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY g")
         fns = [a["fn"] for a in req["aggregations"]]
         local = O.combine_group_by([O.run_group_by(s, req) for s in segs], req)["merged"]
@@ -276,7 +288,7 @@ def test_two_rank_dense_layout_agreement_and_value_keyed_merge():
         p.join(timeout=60)
         assert p.exitcode == 0
     for r in (0, 1):
-        assert res[r][0] == (True, False, False)  # every rank takes the same decision
+        assert res[r][0] == (0, 1, 0, True, True, True)  # same decision and the same union (0..46) on every rank
     cols, vals, cnts = res[0][1]
     req = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY g")
     exp = O.combine_group_by([O.run_group_by(s, req) for r in (0, 1) for s in _dict_segments(r)], req)["merged"]
