@@ -251,7 +251,7 @@ def main():
         multigpu.union_key_domains(q, segs, device="cuda:%d" % local if nccl else None)
         slots = C.c_int64()
         N.check(L.pgx_query_dense_slots(q.handle, seg_arr, len(segs), C.byref(slots)))
-        dense = slots.value <= (1 << 22)
+        dense = 0 <= slots.value <= (1 << 22)  # -1: multi-value group-by, merged by key
     # Queries in flight (PGX_INFLIGHT, default 3): steps i + 1 and i + 2 are submitted (pgx_execute_async: predicate binding and
     # host planning on the library's threads, kernels on its own HIP stream) before step i is completed (wait, trim +
     # read-back, cross-GPU merge), as a server overlaps consecutive queries.  Every step still runs its whole query;

@@ -281,7 +281,9 @@ pgx_status pgx_result_gather(const pgx_result* r, const int64_t* group_index, in
 
 /* Dense-table layout for PGX_X_KEEP_DENSE_ON_DEVICE (multi-GPU RCCL merge):
  * slots = product of group cardinalities; buffer = (1 + num_aggs) planes of slots x 8 bytes.
- * plane 0: int64 doc count; plane 1+i: function i in its accumulator encoding (pgx_result_dense_plane_op). */
+ * plane 0: int64 doc count; plane 1+i: function i in its accumulator encoding (pgx_result_dense_plane_op).
+ * slots = -1: the query has no such table (GROUP BY a multi-value column, or multi-value functions under GROUP BY:
+ * their partials merge by key, pgx_result_group_keys / _values, MCombineGroupByOperator.java:166-191). */
 pgx_status pgx_query_dense_slots(const pgx_query* q, pgx_segment* const* segs, int32_t n, int64_t* slots);
 /* For plane p: 0 = int64 add, 1 = double add, 2 = uint64 ordered-min, 3 = uint64 ordered-max. */
 pgx_status pgx_query_dense_plane_op(const pgx_query* q, pgx_segment* const* segs, int32_t n, int32_t plane, int32_t* op);

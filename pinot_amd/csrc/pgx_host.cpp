@@ -4236,7 +4236,7 @@ void run_mv(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, c
 // whose reference fold depends on doc order, run in pgx_mv_group_ordered.  Key spaces and result decoding are the
 // single-value ones (dense slots, or 64 / 128-bit hash keys), so finish_result decodes the table as usual.
 void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
-                  uint32_t xflags, pgx_result* R, hipStream_t st) {
+                  uint32_t xflags, pgx_result* R, hipStream_t st, const Domain* dom = nullptr) {
   if (!jit_enabled()) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by needs the query kernels");
   const int na = int(q.agg_fn.size()), ng = int(q.group_cols.size());
   if (ng < 1 || ng > kMaxGroupCols) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by: group column count");
@@ -4302,7 +4302,7 @@ void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, in
   bool overflow = false;
   int total_bits = 0;
   for (int g = 0; g < ng; ++g) {
-    P.gdicts.push_back(group_dict(q, segs, n, g));
+    P.gdicts.push_back(dom ? domain_dict(*dom, g, n) : group_dict(q, segs, n, g));
     const int64_t gc = std::max<int64_t>(1, P.gdicts.back().card);
     if (!overflow && prod > (uint64_t(1) << 62) / uint64_t(gc)) overflow = true;
     if (!overflow) prod *= uint64_t(gc);
@@ -4481,12 +4481,13 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   bool mv_fn = false;
   for (int fn : q.agg_fn) mv_fn = mv_fn || fn >= PGX_COUNTMV;
   if (mv_group || (mv_fn && !q.group_cols.empty())) {
-    if (dom || (opts && opts->dense_out)) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by across devices");
-    run_mv_group(ctx, q, segs, n, bindings, xflags, R, st);
+    // across devices the keys come from the shared Domain and the partials merge by key on the host (run_multi,
+    // merge_host_groups); a caller-owned dense table is not offered (pgx_query_dense_slots reports -1)
+    if (opts && opts->dense_out) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by into a caller's dense table");
+    run_mv_group(ctx, q, segs, n, bindings, xflags, R, st, dom);
     return;
   }
-  if (mv_fn) {
-    if (dom || (opts && opts->dense_out)) fail(PGX_ERR_UNSUPPORTED, "multi-value functions across devices");
+  if (mv_fn) {  // aggregation-only: the partials combine per function (combine_partial), on any device count
     run_mv(ctx, q, segs, n, bindings, xflags, R, st);
     return;
   }
@@ -4600,11 +4601,21 @@ void merge_device_groups(pgx_ctx* ctx, hipStream_t st, const uint64_t* keys, con
 }
 
 // Combine of one function's partial (value, count) into an accumulated one (the host-side combineTwoValues).
+// A multi-value group column, or a multi-value function (run_mv / run_mv_group execute these).
+bool query_is_mv(const pgx_query& q, pgx_segment* const* segs, int n) {
+  for (int fn : q.agg_fn)
+    if (fn >= PGX_COUNTMV) return true;
+  for (const auto& g : q.group_cols)
+    for (int s = 0; s < n; ++s)
+      if (segs[s]->col(g).is_mv) return true;
+  return false;
+}
+
 void combine_partial(int fn, double& v, int64_t& c, double v2, int64_t c2) {
-  if (fn == PGX_MIN) v = std::min(v, v2);
-  else if (fn == PGX_MAX) v = std::max(v, v2);
+  if (fn == PGX_MIN || fn == PGX_MINMV) v = std::min(v, v2);  // MinMVAggregationFunction.combineTwoValues: Math.min
+  else if (fn == PGX_MAX || fn == PGX_MAXMV) v = std::max(v, v2);
   else if (fn == PGX_COUNT) v = double(c + c2);
-  else v += v2;  // SUM, AVG sum
+  else v += v2;  // SUM, AVG sum; COUNTMV / SUMMV / AVGMV sums
   c += c2;
 }
 
@@ -4666,7 +4677,7 @@ void run_multi(pgx_ctx* const* ctxs, int nctx, const pgx_query& q, pgx_segment* 
   std::vector<GlobalDict> gd;
   for (int g = 0; g < int(q.group_cols.size()); ++g) gd.push_back(group_dict(q, segs, n, g));
   uint64_t slots = 1;
-  bool dense = !q.group_cols.empty() && !(xflags & PGX_X_FORCE_HASH);
+  bool dense = !q.group_cols.empty() && !(xflags & PGX_X_FORCE_HASH) && !query_is_mv(q, segs, n);
   for (const auto& g : gd) {
     if (slots > (uint64_t(1) << 22) / uint64_t(std::max<int64_t>(g.card, 1))) dense = false;
     else slots *= uint64_t(g.card);
@@ -5254,6 +5265,10 @@ pgx_status pgx_result_gather(const pgx_result* r, const int64_t* gi, int64_t n, 
 pgx_status pgx_query_dense_slots(const pgx_query* q, pgx_segment* const* segs, int32_t n, int64_t* slots) {
   return guarded([&] {
     if (!q || !segs || !slots) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    if (!q->group_cols.empty() && query_is_mv(*q, segs, n)) {  // multi-value group-by: merged by key, never densely
+      *slots = -1;
+      return;
+    }
     uint64_t prod = 1;
     for (int g = 0; g < int(q->group_cols.size()); ++g) prod *= uint64_t(group_dict(*q, segs, n, g).card);
     *slots = int64_t(prod);

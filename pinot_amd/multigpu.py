@@ -180,17 +180,18 @@ def merge_aggregation(fns: Sequence[str], values: Sequence[Tuple[float, int]], d
     when the query has them (they are latency-bound 8-byte messages on xGMI)."""
     import torch
     import torch.distributed as dist
-    adds = [float(x[1]) for x in values] + [float(x[0]) for f, x in zip(fns, values) if f in ("count", "sum", "avg")]
+    adding = ("count", "sum", "avg", "countmv", "summv", "avgmv")
+    adds = [float(x[1]) for x in values] + [float(x[0]) for f, x in zip(fns, values) if f in adding]
     t = torch.tensor(adds, dtype=torch.float64, device=device)
     dist.all_reduce(t)
     counts = [int(v) for v in t[:len(fns)].tolist()]
     sums = iter(t[len(fns):].tolist())
     out = [None] * len(fns)
     for i, f in enumerate(fns):
-        if f in ("count", "sum", "avg"):
+        if f in adding:
             out[i] = (next(sums), counts[i])
     for f, op in (("min", dist.ReduceOp.MIN), ("max", dist.ReduceOp.MAX)):
-        idx = [i for i, g in enumerate(fns) if g == f]
+        idx = [i for i, g in enumerate(fns) if g in (f, f + "mv")]  # MINMV / MAXMV combine like MIN / MAX
         if idx:
             m = torch.tensor([values[i][0] for i in idx], dtype=torch.float64, device=device)
             dist.all_reduce(m, op=op)
@@ -243,11 +244,11 @@ def merge_group_partials(fns: Sequence[str], parts):
     out_v = np.empty((nf, len(starts)))
     out_c = np.add.reduceat(cnts, starts, axis=1)
     for i, f in enumerate(fns):
-        if f == "min":
+        if f in ("min", "minmv"):  # MinMVAggregationFunction.combineTwoValues: Math.min
             out_v[i] = np.minimum.reduceat(vals[i], starts)
-        elif f == "max":
+        elif f in ("max", "maxmv"):
             out_v[i] = np.maximum.reduceat(vals[i], starts)
-        else:  # count (value unused), sum, avg: add
+        else:  # count (value unused), sum, avg and their MV forms: add
             out_v[i] = np.add.reduceat(vals[i], starts)
     return [c[starts] for c in cols], out_v, out_c
 

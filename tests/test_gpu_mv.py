@@ -129,6 +129,42 @@ def test_mv_group_by_combine_matches_oracle(ctx, segs, text):
     _check(blk, o, q)
 
 
+@pytest.fixture(scope="module")
+def two_ctx_segs(ctx):
+    """Three MV segments staged on two contexts (device 0 twice: pgx_execute_multi's per-device runs and merge are the
+    same code for one device as for two), interleaved in the segment list."""
+    from pinot_amd import engine as E
+    c2 = E.Context(0)
+    out = []
+    for i in range(3):
+        seg, oseg = _segment("mvx%d" % i, 60 + i, 30000 + 17 * i, i == 1)
+        out.append((E.IndexSegment(ctx if i % 2 == 0 else c2, seg), oseg))
+    yield out
+    for g, _ in out:
+        g.destroy()
+    c2.close()
+
+
+@pytest.mark.parametrize("text", QUERIES[:6] + GROUP_QUERIES)
+def test_mv_execute_multi_matches_oracle(ctx, two_ctx_segs, text):
+    """MV group-by and MV functions across devices (pgx_execute_multi): every device keys its groups in the union key
+    space of all segments (Domain), the partials merge by key on the host with each function's combineTwoValues
+    (MINMV / MAXMV: Math.min / Math.max, MinMVAggregationFunction.java), equal to the oracle's combine."""
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    q = pql.compile(text)
+    segs = [g for g, _ in two_ctx_segs]
+    qq = E._Query(ctx, q)
+    r = qq.execute_multi(segs)
+    try:
+        blk = E.decode_result(qq, r, segs)
+    finally:
+        N.lib().pgx_result_release(r)
+    o = H.oracle_answer([o for _, o in two_ctx_segs], q, literal=True)
+    assert blk.stats.as_list() == list(o["stats"])
+    _check(blk, o, q)
+
+
 def test_mv_unsupported_shapes_fail_loudly(ctx, segs):
     from pinot_amd import engine as E
     from pinot_amd import native as N
