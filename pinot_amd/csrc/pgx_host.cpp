@@ -4337,7 +4337,6 @@ void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, in
     fail(PGX_ERR_UNSUPPORTED, "group key wider than 126 bits");
   }
   const bool dense = K.group_mode == G_DENSE_GLOBAL;
-  if (ordered && !dense) fail(PGX_ERR_UNSUPPORTED, "MINMV / MAXMV under GROUP BY need a dense key space");
   K.num_aggs = na;
   K.num_planes = 1 + na + extra;
   K.plane_op[0] = P_ADD_I64;

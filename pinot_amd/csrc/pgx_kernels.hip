@@ -1573,13 +1573,36 @@ __global__ void __launch_bounds__(256) pgx_mv_group(const MvGroupArgs* __restric
   });
 }
 
+// Slot of a key pgx_mv_group already inserted (read-only probe; -1 if absent).
+__device__ __forceinline__ int64_t mv_find(const MvGroupArgs& A, uint64_t lo, uint64_t hi) {
+  const uint64_t mask = A.slots - 1;
+  if (A.group_mode == G_HASH64) {
+    uint64_t h = mix64(lo) & mask;
+    for (uint64_t probe = 0; probe < A.slots; ++probe) {
+      const unsigned long long k = A.keys[h];
+      if (k == lo) return static_cast<int64_t>(h);
+      if (k == kEmptyKey) return -1;
+      h = (h + 1) & mask;
+    }
+    return -1;
+  }
+  uint64_t h = mix64(lo ^ mix64(hi)) & mask;
+  for (uint64_t probe = 0; probe < A.slots; ++probe) {
+    if (A.key_state[h] != 2u) return -1;
+    if (A.keys[2 * h] == lo && A.keys[2 * h + 1] == hi) return static_cast<int64_t>(h);
+    h = (h + 1) & mask;
+  }
+  return -1;
+}
+
 // MINMV / MAXMV under GROUP BY (MinMVAggregationFunction.java:76-91 aggregateGroupBySV, :103-119 aggregateGroupByMV;
 // MaxMV alike): the holder's value is read ONCE per (doc, key) and every value of the doc below (above) it replaces the
 // holder, so a doc leaves the LAST such value in its value order -- an order-dependent fold, not a minimum.  One
-// workgroup walks one segment's selected docs in doc order; thread t owns the dense slots s with s % 256 == t and
-// applies the fold to them only, so every key sees its docs in order with no atomics.  Holders are that segment's
-// dictIds (sorted dictionaries: dictId order = value order); the per-segment results merge into the table with the
-// combine's min / max (combineTwoValues).
+// workgroup walks one segment's selected docs in doc order; thread t owns the keys whose dense slot s has
+// s % 256 == t (hash key spaces: whose key hash has that residue; the owner finds the key's slot in the table
+// pgx_mv_group filled) and applies the fold to them only, so every key sees its docs in order with no atomics.  Holders
+// are that segment's dictIds (sorted dictionaries: dictId order = value order); the per-segment results merge into the
+// table with the combine's min / max (combineTwoValues).
 __global__ void __launch_bounds__(256) pgx_mv_group_ordered(const MvGroupArgs* __restrict__ Ap) {
   const MvGroupArgs& A = *Ap;
   const int s = static_cast<int>(blockIdx.x);
@@ -1591,13 +1614,25 @@ __global__ void __launch_bounds__(256) pgx_mv_group_ordered(const MvGroupArgs* _
     for (int a = 0; a < A.naggs; ++a) hold[a * A.slots + sl] = A.fn[a] == MVF_MINMV ? INT64_MAX : -1;
   for (int d = 0; d < S.num_docs; ++d) {
     if (!((S.sel[d >> 5] >> (d & 31)) & 1u)) continue;
-    mv_for_each_key(A, S, d, [&](uint64_t lo, uint64_t) {
-      if (static_cast<int>(lo & 255u) != tid) return;
+    mv_for_each_key(A, S, d, [&](uint64_t lo, uint64_t hi) {
+      uint64_t sl = lo;
+      if (A.group_mode == G_DENSE_GLOBAL) {
+        if (static_cast<int>(lo & 255u) != tid) return;
+      } else {
+        const uint64_t own = A.group_mode == G_HASH64 ? mix64(lo) : mix64(lo ^ mix64(hi));
+        if (static_cast<int>((own >> 40) & 255u) != tid) return;
+        const int64_t f = mv_find(A, lo, hi);
+        if (f < 0) {
+          atomicAdd(A.overflow, 1ull);
+          return;
+        }
+        sl = static_cast<uint64_t>(f);
+      }
       for (int a = 0; a < A.naggs; ++a) {
         const int fn = A.fn[a];
         if (fn != MVF_MINMV && fn != MVF_MAXMV) continue;
         const MvGCol& c = S.a[a];
-        int64_t* h = hold + a * A.slots + lo;
+        int64_t* h = hold + a * A.slots + sl;
         const int64_t old = *h;
         for (int i = c.start[d]; i < c.start[d + 1]; ++i) {
           const int64_t id = mv_value(c.vals, i, c.bits);
