@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define PGX_ABI_VERSION 6
+#define PGX_ABI_VERSION 7  /* 7: pgx_mutable_* (realtime segments in place) */
 
 typedef enum {
   PGX_OK = 0,
@@ -121,6 +121,35 @@ pgx_status pgx_segment_stage(pgx_ctx* ctx, const pgx_segment_desc* desc, pgx_seg
 pgx_status pgx_segment_release(pgx_segment* seg);
 /* HBM bytes held by the staged segment (forward indexes + dictionaries + inverted indexes). */
 pgx_status pgx_segment_device_bytes(const pgx_segment* seg, uint64_t* out);
+
+/* ---- realtime (consuming) segments, in place -----------------------------------------------------
+ * RealtimeSegmentImpl.index (core/realtime/impl/RealtimeSegmentImpl.java:185-334) gives every column value an
+ * arrival-order dictId in a mutable dictionary and appends one dictId per doc (a list per doc for multi-value columns).
+ * A pgx_mutable keeps those dictIds in HBM: pgx_mutable_append sends only the new docs' ids.  The caller owns the
+ * mutable dictionaries; whenever one grew it hands the column's current dictionary SORTED (v1 bytes, as
+ * RealtimeSegmentConverter would write it) with the arrival -> sorted id map (pgx_mutable_set_dictionary, O(card)).
+ * pgx_mutable_snapshot returns the docs indexed so far as a queryable pgx_segment: the forward indexes are re-packed
+ * on the device through the maps (no row crosses PCIe again), unsorted (RealtimeColumnDataSource.isSorted() is false),
+ * and columns with has_inverted keep bitmap-filter semantics (FilterPlanNode, numEntriesScannedInFilter) evaluated by
+ * scanning the dictIds.  Release snapshots with pgx_segment_release; they stay valid after more appends. */
+typedef struct pgx_mutable pgx_mutable;
+typedef struct {
+  const char* name;
+  int32_t data_type;          /* pgx_data_type (multi-value: numeric only) */
+  int32_t is_multi_value;
+  int32_t has_inverted;       /* in the table's invertedIndexColumns */
+} pgx_mutable_column;
+pgx_status pgx_mutable_create(pgx_ctx* ctx, const char* name, int32_t capacity, int32_t num_columns,
+                              const pgx_mutable_column* columns, pgx_mutable** out);
+/* ndocs new docs.  ids[c]: column c's arrival-order dictIds, one per doc, or (multi-value) every value of the new docs
+ * in doc order with counts[c][d] values for doc d (>= 1).  counts may be NULL when no column is multi-value. */
+pgx_status pgx_mutable_append(pgx_mutable* m, int32_t ndocs, const int32_t* const* ids, const int32_t* const* counts);
+pgx_status pgx_mutable_set_dictionary(pgx_mutable* m, int32_t column, int32_t cardinality, const void* dict,
+                                      uint64_t dict_len, int32_t dict_width, int32_t pad_char,
+                                      const int32_t* arrival_to_sorted);
+pgx_status pgx_mutable_snapshot(pgx_mutable* m, pgx_segment** out);
+pgx_status pgx_mutable_num_docs(const pgx_mutable* m, int32_t* out);
+pgx_status pgx_mutable_release(pgx_mutable* m);
 
 /* ---- query ---------------------------------------------------------------------------------- */
 typedef struct {

@@ -77,6 +77,8 @@ extern "C" hipError_t pgx_launch_part_aggregate_img(const uint64_t* in, const un
                                                     uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                     unsigned long long* ocount, unsigned long long* overflow, int grid,
                                                     hipStream_t stream);
+extern "C" hipError_t pgx_launch_pack_remap(uint32_t* out_words, const int32_t* ids, const int32_t* remap,
+                                            int64_t n_rows, int bits, int64_t n_words, hipStream_t stream);
 extern "C" hipError_t pgx_launch_narrow_split(const uint32_t* lo, const uint16_t* hi, const unsigned long long* cnt1,
                                               int nbuckets, int nwg, int64_t cap1, int rb1, int k2, uint32_t* out,
                                               int64_t cap2, unsigned int* cnt2, unsigned long long* ovf,
@@ -654,6 +656,10 @@ void parse_star_tree(pgx_segment& seg) {
   seg.st_ok = true;
 }
 
+void stage_dict(pgx_ctx* ctx, pgx_segment* seg, const std::vector<uint8_t>& dict_host, StagedColumn& c);
+void stage_forward(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c,
+                   int64_t n, uint64_t need);
+
 void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c) {
   c.name = d.name ? d.name : "";
   c.data_type = d.data_type;
@@ -678,6 +684,13 @@ void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool
     const uint8_t* p = static_cast<const uint8_t*>(d.dict);
     dict_host.assign(p, p + d.dict_len);
   }
+  stage_dict(ctx, seg, dict_host, c);
+  stage_forward(ctx, seg, d, device_mem, c, n, need);
+}
+
+// The v1 dictionary bytes of column c (c.name / data_type / card / dict_width / pad_char set): host values, the
+// context-wide shared device copy and value image (SharedDict).
+void stage_dict(pgx_ctx* ctx, pgx_segment* seg, const std::vector<uint8_t>& dict_host, StagedColumn& c) {
   const int width = (c.data_type == PGX_INT || c.data_type == PGX_FLOAT) ? 4
                     : (c.data_type == PGX_STRING)                          ? c.dict_width
                                                                            : 8;
@@ -750,8 +763,10 @@ void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool
     c.dict_dev = sd->dict.p;
     c.img_dev = sd->img.p;
   }
+}
 
-  // ---- forward index ----
+void stage_forward(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c,
+                   int64_t n, uint64_t need) {
   if (d.is_multi_value) {
     // FixedBitMultiValueWriter / FixedBitMultiValueReader (io/*/impl/v1/FixedBitMultiValue*.java): numChunks BE int
     // chunk offsets, a totalNumValues-bit MSB-first bitset marking every doc's first value, then the values fixed-bit.
@@ -4911,6 +4926,208 @@ pgx_status pgx_segment_release(pgx_segment* seg) {
     if (!seg) return;
     pgx_ctx* ctx = seg->ctx;
     delete seg;
+    if (ctx) ctx_unref(ctx);
+  });
+}
+
+// -------------------------------------------------------------------------------------------------
+// Realtime (consuming) segments in place (RealtimeSegmentImpl.java:185-334): per column the docs' arrival-order
+// dictIds live in HBM and grow by appends (only the new rows cross PCIe); a snapshot re-packs them on the device through
+// the arrival -> sorted dictId map of the column's current dictionary (RealtimeSegmentConverter's shape: sorted
+// dictionary, unsorted fixed-bit forward index), so a query costs no host pass over the rows.
+// -------------------------------------------------------------------------------------------------
+struct pgx_mutable {
+  pgx_ctx* ctx = nullptr;
+  std::string name;
+  int32_t capacity = 0;
+  int32_t num_docs = 0;
+  struct Col {
+    std::string name;
+    int data_type = 0;
+    bool mv = false, inverted = false;
+    DevBuf ids;                  // arrival-order dictIds: one per doc (SV) or per value (MV)
+    int64_t ids_cap = 0, nvals = 0;
+    DevBuf starts;               // MV: doc d's values are [starts[d], starts[d + 1]) (capacity + 1)
+    int max_mv = 0;
+    int32_t max_id = -1;         // largest arrival id appended
+    int card = 0, dict_width = 0, pad_char = 0;
+    std::vector<uint8_t> dict;   // sorted v1 dictionary bytes
+    DevBuf remap;                // arrival id -> sorted id
+  };
+  std::vector<Col> cols;
+  std::mutex mu;
+};
+
+pgx_status pgx_mutable_create(pgx_ctx* ctx, const char* name, int32_t capacity, int32_t num_columns,
+                              const pgx_mutable_column* columns, pgx_mutable** out) {
+  return guarded([&] {
+    if (!ctx || !columns || !out || capacity < 1 || num_columns < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    auto m = std::make_unique<pgx_mutable>();
+    m->ctx = ctx;
+    m->name = name ? name : "";
+    m->capacity = capacity;
+    m->cols.resize(num_columns);
+    for (int i = 0; i < num_columns; ++i) {
+      const pgx_mutable_column& d = columns[i];
+      pgx_mutable::Col& c = m->cols[i];
+      c.name = d.name ? d.name : "";
+      c.data_type = d.data_type;
+      c.mv = d.is_multi_value != 0;
+      c.inverted = d.has_inverted != 0;
+      if (c.mv && c.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "multi-value STRING column " + c.name);
+      c.ids_cap = c.mv ? std::max<int64_t>(1024, int64_t(capacity)) : capacity;
+      c.ids = DevBuf(ctx, size_t(c.ids_cap) * 4);
+      if (c.mv) {
+        c.starts = DevBuf(ctx, (size_t(capacity) + 1) * 4);
+        hip_check(hipMemset(c.starts.p, 0, 4), "memset");
+      }
+    }
+    ctx->refs.fetch_add(1);  // released by pgx_mutable_release
+    *out = m.release();
+  });
+}
+
+pgx_status pgx_mutable_append(pgx_mutable* m, int32_t ndocs, const int32_t* const* ids, const int32_t* const* counts) {
+  return guarded([&] {
+    if (!m || !ids || ndocs < 0) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    std::lock_guard<std::mutex> g(m->mu);
+    if (int64_t(m->num_docs) + ndocs > m->capacity) fail(PGX_ERR_INVALID_ARG, "realtime segment " + m->name + " full");
+    if (!ndocs) return;
+    hip_check(hipSetDevice(m->ctx->device), "hipSetDevice");
+    hipStream_t st = m->ctx->stream;
+    for (size_t i = 0; i < m->cols.size(); ++i) {
+      pgx_mutable::Col& c = m->cols[i];
+      if (!ids[i] || (c.mv && (!counts || !counts[i]))) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": no ids");
+      int64_t nv = ndocs;
+      if (c.mv) {  // the new docs' starts, then the values
+        std::vector<int32_t> st_new(ndocs);
+        int64_t at = c.nvals;
+        for (int32_t d = 0; d < ndocs; ++d) {
+          if (counts[i][d] < 1) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": a multi-value doc needs a value");
+          at += counts[i][d];
+          st_new[d] = int32_t(at);
+          c.max_mv = std::max(c.max_mv, counts[i][d]);
+        }
+        if (at > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "column " + c.name + ": too many values");
+        nv = at - c.nvals;
+        hip_check(hipMemcpyAsync(c.starts.as<int32_t>() + m->num_docs + 1, st_new.data(), size_t(ndocs) * 4,
+                                 hipMemcpyHostToDevice, st), "starts H2D");
+        hip_check(hipStreamSynchronize(st), "sync");  // st_new is a stack buffer
+        if (c.nvals + nv > c.ids_cap) {  // grow the value buffer (doubling)
+          int64_t cap = c.ids_cap;
+          while (cap < c.nvals + nv) cap *= 2;
+          DevBuf bigger(m->ctx, size_t(cap) * 4);
+          if (c.nvals)
+            hip_check(hipMemcpyAsync(bigger.p, c.ids.p, size_t(c.nvals) * 4, hipMemcpyDeviceToDevice, st), "grow");
+          hip_check(hipStreamSynchronize(st), "sync");
+          c.ids = std::move(bigger);
+          c.ids_cap = cap;
+        }
+      }
+      for (int64_t k = 0; k < nv; ++k) {
+        if (ids[i][k] < 0) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": negative dictId");
+        c.max_id = std::max(c.max_id, ids[i][k]);
+      }
+      const int64_t at = c.mv ? c.nvals : m->num_docs;
+      hip_check(hipMemcpyAsync(c.ids.as<int32_t>() + at, ids[i], size_t(nv) * 4, hipMemcpyHostToDevice, st), "ids H2D");
+      if (c.mv) c.nvals += nv;
+    }
+    hip_check(hipStreamSynchronize(st), "sync");  // the caller's buffers may go away after the call
+    m->num_docs += ndocs;
+  });
+}
+
+pgx_status pgx_mutable_set_dictionary(pgx_mutable* m, int32_t col, int32_t card, const void* dict, uint64_t dict_len,
+                                      int32_t dict_width, int32_t pad_char, const int32_t* arrival_to_sorted) {
+  return guarded([&] {
+    if (!m || !dict || !arrival_to_sorted || card < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
+    std::lock_guard<std::mutex> g(m->mu);
+    if (col < 0 || col >= int(m->cols.size())) fail(PGX_ERR_INVALID_ARG, "column index");
+    pgx_mutable::Col& c = m->cols[col];
+    const int width = (c.data_type == PGX_INT || c.data_type == PGX_FLOAT) ? 4 : c.data_type == PGX_STRING ? dict_width : 8;
+    if (width < 1 || dict_len < uint64_t(width) * card) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": dictionary short");
+    for (int32_t i = 0; i < card; ++i)
+      if (arrival_to_sorted[i] < 0 || arrival_to_sorted[i] >= card)
+        fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": remap out of range");
+    hip_check(hipSetDevice(m->ctx->device), "hipSetDevice");
+    c.card = card;
+    c.dict_width = width;
+    c.pad_char = pad_char & 0xFF;
+    c.dict.assign(static_cast<const uint8_t*>(dict), static_cast<const uint8_t*>(dict) + uint64_t(width) * card);
+    c.remap = DevBuf(m->ctx, size_t(card) * 4);
+    hip_check(hipMemcpy(c.remap.p, arrival_to_sorted, size_t(card) * 4, hipMemcpyHostToDevice), "remap H2D");
+  });
+}
+
+pgx_status pgx_mutable_snapshot(pgx_mutable* m, pgx_segment** out) {
+  return guarded([&] {
+    if (!m || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> g(m->mu);
+    if (m->num_docs < 1) fail(PGX_ERR_INVALID_ARG, "realtime segment " + m->name + " has no docs");
+    pgx_ctx* ctx = m->ctx;
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t st = ctx->stream;
+    auto seg = std::make_unique<pgx_segment>();
+    seg->ctx = ctx;
+    seg->name = m->name;
+    seg->total_docs = seg->total_raw_docs = m->num_docs;
+    seg->cols.resize(m->cols.size());
+    const int64_t n = m->num_docs;
+    for (size_t i = 0; i < m->cols.size(); ++i) {
+      const pgx_mutable::Col& mc = m->cols[i];
+      StagedColumn& c = seg->cols[i];
+      if (mc.card < 1 || mc.max_id >= mc.card)
+        fail(PGX_ERR_INVALID_ARG, "column " + mc.name + ": dictionary not set for every appended value");
+      c.name = mc.name;
+      c.data_type = mc.data_type;
+      c.card = mc.card;
+      c.bits = bits_for(mc.card);
+      c.dict_width = mc.dict_width;
+      c.pad_char = mc.pad_char;
+      c.is_sorted = false;           // RealtimeColumnDataSource.isSorted(): false
+      c.has_inverted = mc.inverted;  // bitmap-filter semantics; without index bytes the leaf is evaluated by scanning
+      stage_dict(ctx, seg.get(), mc.dict, c);
+      const int64_t rows = mc.mv ? mc.nvals : n;
+      const uint64_t need = padded_fwd_bytes(rows, c.bits);
+      c.fwd_owned = DevBuf(ctx, need);
+      hip_check(hipMemsetAsync(c.fwd_owned.p, 0, need, st), "memset");
+      PGX_LAUNCH(st, "pgx_pack_remap", pgx_launch_pack_remap(c.fwd_owned.as<uint32_t>(), mc.ids.as<int32_t>(),
+                                                              mc.remap.as<int32_t>(), rows, c.bits,
+                                                              int64_t((uint64_t(rows) * c.bits + 31) / 32), st),
+                 "realtime forward index");
+      c.fwd = c.fwd_owned.as<const uint32_t>();
+      seg->device_bytes += need;
+      if (mc.mv) {
+        c.is_mv = true;
+        c.total_entries = mc.nvals;
+        c.max_mv = mc.max_mv;
+        c.mv_start = DevBuf(ctx, (size_t(n) + 1) * 4);
+        hip_check(hipMemcpyAsync(c.mv_start.p, mc.starts.p, (size_t(n) + 1) * 4, hipMemcpyDeviceToDevice, st),
+                  "starts copy");
+        seg->device_bytes += (size_t(n) + 1) * 4;
+      }
+      seg->by_name[c.name] = int(i);
+      seg->names.push_back(c.name);
+    }
+    hip_check(hipStreamSynchronize(st), "sync");
+    ctx->refs.fetch_add(1);  // released by pgx_segment_release
+    *out = seg.release();
+  });
+}
+
+pgx_status pgx_mutable_num_docs(const pgx_mutable* m, int32_t* out) {
+  return guarded([&] {
+    if (!m || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    *out = m->num_docs;
+  });
+}
+
+pgx_status pgx_mutable_release(pgx_mutable* m) {
+  return guarded([&] {
+    if (!m) return;
+    pgx_ctx* ctx = m->ctx;
+    delete m;
     if (ctx) ctx_unref(ctx);
   });
 }

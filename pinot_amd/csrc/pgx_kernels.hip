@@ -2045,6 +2045,26 @@ __global__ void pgx_synth_kernel(uint32_t* out_words, int64_t n_rows, int bits, 
 }
 
 
+// Realtime snapshot (pgx_mutable_snapshot): the fixed-bit forward index of dictIds remap[ids[r]] (arrival-order ids
+// through the arrival -> sorted map; remap null: ids as they are), packed MSB-first big-endian like pgx_synth_kernel:
+// one thread per 32-bit word, the rows that overlap it.
+__global__ void pgx_pack_remap_kernel(uint32_t* out_words, const int32_t* __restrict__ ids,
+                                      const int32_t* __restrict__ remap, int64_t n_rows, int bits, int64_t n_words) {
+  for (int64_t w = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; w < n_words; w += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t bit0 = w * 32;
+    const int64_t r_first = bit0 / bits;
+    const int64_t r_last = (bit0 + 31) / bits;
+    uint32_t word = 0;
+    for (int64_t r = r_first; r <= r_last && r < n_rows; ++r) {
+      const int32_t a = ids[r];
+      const uint64_t v = static_cast<uint32_t>(remap ? remap[a] : a);
+      const int64_t sh = 32 - (r * bits - bit0) - bits;
+      word |= static_cast<uint32_t>((sh >= 0 ? v << sh : v >> (-sh)) & 0xFFFFFFFFull);
+    }
+    out_words[w] = bswap32(word);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // numEntriesScannedInFilter automaton (pgx_stats.cpp): the reference's iterator algebra restated as a finite automaton
 // over each row's leaf-membership bits.  Pass 1: one thread per (1024-row chunk, start state) runs the chunk; pass 2:
@@ -2194,6 +2214,16 @@ extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int 
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(pgx::pgx_synth_kernel, dim3(grid), dim3(256), 0, stream, out_words, n_rows, bits, card, seed,
                      n_words, pair_seed, npairs);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_pack_remap(uint32_t* out_words, const int32_t* ids, const int32_t* remap,
+                                            int64_t n_rows, int bits, int64_t n_words, hipStream_t stream) {
+  if (n_words <= 0) return hipSuccess;
+  if (bits < 1 || bits > 32 || !out_words || (n_rows > 0 && !ids)) return hipErrorInvalidValue;
+  const int grid = static_cast<int>(std::min<int64_t>((n_words + 255) / 256, 65536));
+  hipLaunchKernelGGL(pgx::pgx_pack_remap_kernel, dim3(grid), dim3(256), 0, stream, out_words, ids, remap, n_rows, bits,
+                     n_words);
   return hipGetLastError();
 }
 

@@ -195,6 +195,18 @@ class IndexSegment:
         del keep  # the library copied every host buffer during staging
 
     @classmethod
+    def from_handle(cls, ctx: Context, seg: SegmentData, handle):
+        """Wrap a segment the library staged itself (pgx_mutable_snapshot); `seg` carries the column metadata."""
+        self = cls.__new__(cls)
+        self.uid = next(_SEG_UID)
+        self.ctx = ctx
+        self.data = seg
+        self.name = seg.name
+        self._cols = {}
+        self.handle = handle
+        return self
+
+    @classmethod
     def from_device(cls, ctx: Context, seg: SegmentData, fwd_device: Dict[str, int]):
         """Stage a segment whose forward indexes already live in HBM (synthetic benchmark data)."""
         self = cls.__new__(cls)

@@ -77,6 +77,11 @@ class Predicate(C.Structure):
                 ("upper_inclusive", C.c_int32)]
 
 
+class MutableColumn(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("data_type", C.c_int32), ("is_multi_value", C.c_int32),
+                ("has_inverted", C.c_int32)]
+
+
 class ExecOpts(C.Structure):
     _fields_ = [("stream", C.c_uint64), ("dense_out", C.c_void_p), ("dense_out_bytes", C.c_uint64),
                 ("flags", C.c_uint32)]
@@ -141,6 +146,14 @@ EXPORTS = {
     "pgx_execute_timed": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32, C.POINTER(LeafBinding),
                                     C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_void_p)]),
     "pgx_timing_start": (C.c_int, [C.c_void_p]),
+    "pgx_mutable_create": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int32, C.c_int32, C.POINTER(MutableColumn),
+                                     C.POINTER(C.c_void_p)]),
+    "pgx_mutable_append": (C.c_int, [C.c_void_p, C.c_int32, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "pgx_mutable_set_dictionary": (C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_uint64, C.c_int32,
+                                             C.c_int32, C.c_void_p]),
+    "pgx_mutable_snapshot": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
+    "pgx_mutable_num_docs": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    "pgx_mutable_release": (C.c_int, [C.c_void_p]),
     "pgx_timing_stop": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_char_p, C.c_uint64]),
 }
 

@@ -9,13 +9,15 @@ indexed so far (docIdSearchableOffset).  Its data source reports isSorted() fals
 configured columns (realtime/impl/datasource/RealtimeColumnDataSource.java:140-152), and RANGE predicates are evaluated
 by scanning the mutable dictionary (RangeRealtimeDictionaryPredicateEvaluator.java:34-75).
 
-Here :class:`RealtimeSegment` keeps the same host structures (arrival-order dictionaries, per-doc dictIds, per-dictId
-doc lists) and stages a snapshot of the docs indexed so far for the GPU path the way RealtimeSegmentConverter turns a
-consuming segment into an immutable one: each dictionary sorted, the dictIds remapped, a fixed-bit forward index (never
-a sorted one: the realtime data source is unsorted) and the bitmap inverted index of the configured columns.  The
-value sets every predicate selects are the realtime evaluators' (``oracle.pinot_oracle`` restates both and the tests
-compare them), so a query answers exactly what the reference answers on the consuming segment.  The snapshot is cached
-until the next :meth:`RealtimeSegment.index`.
+Here :class:`RealtimeSegment` keeps the same host structures (arrival-order dictionaries, per-doc dictIds) and, for the
+GPU path, a native mutable segment (pgx_mutable_*, include/pgx.h): every doc's arrival-order dictIds live in HBM and
+only the docs indexed since the last query cross PCIe (O(new rows)); when a dictionary grew, its sorted form and the
+arrival -> sorted id map go down (O(cardinality)); the library re-packs the forward indexes on the device into the
+shape RealtimeSegmentConverter gives an immutable segment (sorted dictionaries, unsorted fixed-bit forward indexes) and
+keeps the configured inverted columns' bitmap-filter semantics, evaluated by scanning.  No host pass over the rows per
+query.  The value sets every predicate selects are the realtime evaluators' (``oracle.pinot_oracle`` restates both and
+the tests compare them), so a query answers exactly what the reference answers on the consuming segment.
+:meth:`RealtimeSegment.snapshot` still builds the whole converter-shaped v1 segment on the host (the CPU tests use it).
 """
 from typing import Dict, List, Sequence, Tuple
 
@@ -145,13 +147,119 @@ class RealtimeSegment:
         self._snap = S.make_segment(self.name, cols)
         return self._snap
 
+    def _sorted_dictionary(self, c: str):
+        """(sorted v1 dictionary bytes, entry width, arrival -> sorted id map, sorted values) of column c's mutable
+        dictionary: SegmentDictionaryCreator's order (numbers ascending; strings by Java compareTo of the '\\0'-padded
+        values, so padded and raw order agree)."""
+        t = self.schema[c][0]
+        vals = self.dictionaries[c].values
+        if t == "STRING":
+            width = max([1] + [len(v.encode("utf-8")) for v in vals])
+            order = sorted(range(len(vals)), key=lambda i: [ord(ch) for ch in vals[i]])
+            svals = [vals[i] for i in order]
+            data = b"".join(v.encode("utf-8") + S.DEFAULT_PAD.encode() * (width - len(v.encode("utf-8"))) for v in svals)
+        else:
+            arr = np.asarray(vals, dtype=_NP[t])
+            order = np.argsort(arr, kind="stable")
+            svals = arr[order]
+            data = svals.astype(S._DICT_NP[t]).tobytes()
+            width = int(S._DICT_NP[t][-1])
+        remap = np.empty(len(vals), dtype=np.int32)
+        remap[np.asarray(order, dtype=np.int64)] = np.arange(len(vals), dtype=np.int32)
+        return data, width, remap, svals
+
     def device_segment(self, ctx):
-        """The snapshot staged into HBM (engine.IndexSegment), restaged only after new rows arrive."""
+        """The docs indexed so far as a queryable segment in HBM (engine.IndexSegment over pgx_mutable_snapshot).  Only
+        the docs indexed since the previous call are sent, and a dictionary only when it grew; the snapshot is re-made
+        only when something changed."""
+        import ctypes as C
+
         from pinot_amd import engine as E
-        snap = self.snapshot()
-        if getattr(self, "_dev", None) is None or self._dev_for is not snap:
+        from pinot_amd import native as N
+        L = N.lib()
+        n = self.num_docs_indexed
+        if n == 0:
+            raise ValueError("realtime segment %s has no docs yet" % self.name)
+        names = list(self.schema)
+        if getattr(self, "_mut", None) is None or self._mut_ctx is not ctx:
+            self._release_device()
+            cols = (N.MutableColumn * len(names))()
+            keep = []
+            for i, c in enumerate(names):
+                t, sv, _ = self.schema[c]
+                b = c.encode()
+                keep.append(b)
+                cols[i].name = b
+                cols[i].data_type = {"INT": N.PGX_INT, "LONG": N.PGX_LONG, "FLOAT": N.PGX_FLOAT, "DOUBLE": N.PGX_DOUBLE,
+                                     "STRING": N.PGX_STRING}[t]
+                cols[i].is_multi_value = int(not sv)
+                cols[i].has_inverted = int(c in self.inverted)
+            h = C.c_void_p()
+            N.check(L.pgx_mutable_create(ctx.handle, self.name.encode(), self.capacity, len(names), cols, C.byref(h)))
+            self._mut, self._mut_ctx, self._synced = h, ctx, 0
+            self._dict_card = {c: 0 for c in names}
+        changed = False
+        if self._synced < n:  # the new docs' arrival-order dictIds (and value counts of multi-value columns)
+            lo = self._synced
+            arrs, counts = [], []
+            for c in names:
+                ids = self._ids[c][lo:n]
+                if self.schema[c][1]:
+                    arrs.append(np.asarray(ids, dtype=np.int32))
+                    counts.append(None)
+                else:
+                    arrs.append(np.asarray([x for doc in ids for x in doc], dtype=np.int32))
+                    counts.append(np.asarray([len(doc) for doc in ids], dtype=np.int32))
+            idp = (C.c_void_p * len(names))(*[a.ctypes.data for a in arrs])
+            cnp = (C.c_void_p * len(names))(*[x.ctypes.data if x is not None else None for x in counts])
+            N.check(L.pgx_mutable_append(self._mut, n - lo, idp, cnp))
+            self.docs_sent = getattr(self, "docs_sent", 0) + (n - lo)  # every doc crosses PCIe once
+            self._synced = n
+            changed = True
+        for i, c in enumerate(names):  # dictionaries that grew: sorted form + arrival -> sorted map
+            card = self.dictionaries[c].length()
+            if card != self._dict_card[c]:
+                data, width, remap, _ = self._sorted_dictionary(c)
+                N.check(L.pgx_mutable_set_dictionary(self._mut, i, card, data, len(data), width, 0, remap.ctypes.data))
+                self._dict_card[c] = card
+                changed = True
+        if getattr(self, "_dev", None) is None or changed:
             if getattr(self, "_dev", None) is not None:
                 self._dev.destroy()
-            self._dev = E.IndexSegment(ctx, snap)
-            self._dev_for = snap
+            h = C.c_void_p()
+            N.check(L.pgx_mutable_snapshot(self._mut, C.byref(h)))
+            self._dev = E.IndexSegment.from_handle(ctx, self._metadata(), h)
         return self._dev
+
+    def _metadata(self) -> S.SegmentData:
+        """Column metadata of the snapshot for the host side of the engine (types, sorted dictionaries for key rendering
+        and predicate values); the bytes themselves live in the library."""
+        n = self.num_docs_indexed
+        seg = S.SegmentData(self.name, n, n)
+        for c, (t, sv, ft) in self.schema.items():
+            data, width, _, _ = self._sorted_dictionary(c)
+            card = self.dictionaries[c].length()
+            ct = {"METRIC": "METRIC", "TIME": "TIME"}.get(ft, "DIMENSION")
+            col = S.Column(c, t, ct, card, S.num_bits(card), n, n, False, c in self.inverted, data, width, None, None,
+                           None, S.DEFAULT_PAD)
+            if not sv:
+                col.is_mv = True
+                col.total_entries = sum(len(x) for x in self._ids[c])
+                col.max_mv = self.max_mv[c]
+            seg.columns[c] = col
+        return seg
+
+    def _release_device(self):
+        from pinot_amd import native as N
+        if getattr(self, "_dev", None) is not None:
+            self._dev.destroy()
+            self._dev = None
+        if getattr(self, "_mut", None) is not None:
+            N.lib().pgx_mutable_release(self._mut)
+            self._mut = None
+
+    def __del__(self):
+        try:
+            self._release_device()
+        except Exception:
+            pass

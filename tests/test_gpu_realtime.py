@@ -80,6 +80,8 @@ def test_queries_follow_ingestion(ctx):
         blk, _ = _run_inner(ctx, rt.device_segment(ctx), q)
         res = blk.get_aggregation_result()
         assert int(res[0]) == stop and int(res[1]) == sum(r["met"] for r in seen)
+        # in place: each doc's dictIds crossed to the device once, at the first query after it arrived (pgx_mutable)
+        assert rt.docs_sent == stop
 
 
 def test_consuming_beside_immutable(ctx):
