@@ -96,9 +96,9 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
   const PGX_GLOBAL uint16_t* ghi = hi ? (const PGX_GLOBAL uint16_t*)hi + static_cast<int64_t>(b) * nwg * cap1 : nullptr;
   PGX_GLOBAL uint32_t* gout = (PGX_GLOBAL uint32_t*)out + static_cast<int64_t>(b) * nsub * cap2;
   int w = 0;  // this thread's slab: positions only grow
-  for (uint32_t c0 = 0; c0 < ntot; c0 += kN2Chunk) {
-    uint32_t xl[kN2Per], xh[kN2Per];
-    // addresses first (LDS prefix walk), then every load in flight, then the split fields
+  uint32_t xl[kN2Per], xh[kN2Per];
+  // the records of round c0 into xl / xh: addresses from the LDS prefix walk, every load in flight before any use
+  auto load = [&](uint32_t c0) {
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k) {
       const uint32_t pos = c0 + static_cast<uint32_t>(k * kN2Threads + tid);
@@ -111,15 +111,23 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
         if (ghi) xh[k] = __builtin_nontemporal_load(ghi + idx);
       }
     }
-    uint32_t sb[kN2Per], rk[kN2Per];
+  };
+  if (ntot) load(0u);
+  for (uint32_t c0 = 0; c0 < ntot; c0 += kN2Chunk) {
+    // split fields of this round; pk = sub-bucket | rank << 16 (a round holds 16384 records), ~0: no record
+    uint32_t r2[kN2Per], pk[kN2Per];
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k) {
       const uint32_t pos = c0 + static_cast<uint32_t>(k * kN2Threads + tid);
       const uint64_t r1 = static_cast<uint64_t>(xl[k]) | (static_cast<uint64_t>(xh[k]) << 32);
-      sb[k] = pos < ntot ? static_cast<uint32_t>(r1 >> rb2) & static_cast<uint32_t>(nsub - 1) : 0xFFFFFFFFu;
-      xl[k] = static_cast<uint32_t>((r1 & m2) | ((r1 >> rb1) << rb2));
-      rk[k] = sb[k] != 0xFFFFFFFFu ? atomicAdd(&hist[sb[k]], 1u) : 0u;
+      r2[k] = static_cast<uint32_t>((r1 & m2) | ((r1 >> rb1) << rb2));
+      pk[k] = 0xFFFFFFFFu;
+      if (pos < ntot) {
+        const uint32_t sb = static_cast<uint32_t>(r1 >> rb2) & static_cast<uint32_t>(nsub - 1);
+        pk[k] = sb | (atomicAdd(&hist[sb], 1u) << 16);
+      }
     }
+    if (c0 + kN2Chunk < ntot) load(c0 + kN2Chunk);  // the next round's loads overlap this round's split
     n_lds_barrier();
     if (tid < 64) {  // offsets of this round, this workgroup's runs in each partition, histogram cleared
       constexpr int PER = kN2MaxSub / 64;
@@ -154,10 +162,11 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
     n_lds_barrier();
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k)
-      if (sb[k] != 0xFFFFFFFFu) {
-        const uint32_t q = offs[sb[k]] + rk[k];
-        stage[q] = xl[k];
-        ssub[q] = static_cast<uint16_t>(sb[k]);
+      if (pk[k] != 0xFFFFFFFFu) {
+        const uint32_t sb = pk[k] & 0xFFFFu;
+        const uint32_t q = offs[sb] + (pk[k] >> 16);
+        stage[q] = r2[k];
+        ssub[q] = static_cast<uint16_t>(sb);
       }
     n_lds_barrier();
     const uint32_t tot = total;

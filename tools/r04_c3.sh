@@ -21,7 +21,8 @@ $T 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04/c3/prof -o c3 -- pytho
   --profile-iters 3 > gpurun_out/r04/c3/prof.log 2>&1 || { tail -20 gpurun_out/r04/c3/prof.log; exit 1; }
 find gpurun_out/r04/c3/prof -name "*kernel_stats.csv" | head -3
 $T 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_bitmap.py tests/test_gpu_dense_pack.py tests/test_gpu_c5_headline.py \
+  tests/test_gpu_realtime.py tests/test_gpu_mv.py tests/test_gpu_bitmap.py tests/test_gpu_dense_pack.py \
+  tests/test_gpu_c5_headline.py \
   > gpurun_out/r04/new_tests.log 2>&1
 rc=$?
 tail -5 gpurun_out/r04/new_tests.log
