@@ -284,7 +284,7 @@ def test_narrow_paths_and_fallback(ctx, monkeypatch, capfd, case):
     sized for a uniform mix).  COUNT-only records carry no value (26-bit records, one u32 array)."""
     from pinot_amd import engine as E
     rng = np.random.default_rng(99)
-    n, card = 400000, 600
+    n, card = 400000, 3000  # 3000 x 3000 keys > 2^22: a sparse (LONG_MAP) plan
     dom = np.sort(rng.choice(np.arange(-70000, 70000), size=20000, replace=False)).astype(np.int32)
     raw = {"ga": rng.integers(0, card, size=n).astype(np.int32),
            "gb": rng.integers(0, card, size=n).astype(np.int32) * 3,
