@@ -1332,7 +1332,8 @@ struct ExecPlan {
   // narrow records (run_narrow, the default for partitioned plans that qualify): the scan writes dictId records split
   // 256 ways into per-workgroup slabs (part_slab with kNarrow1Bits), u32 in kq.table and bits 32..47 in part_hi
   bool part_narrow = false;
-  bool narrow_old_slab = false, narrow_old_dictid = false;  // the radix path's choices, restored on fallback
+  bool narrow_old_slab = false, narrow_old_dictid = false, narrow_old_fused = false;  // the radix path's choices,
+                                                                                       // restored on fallback
   int narrow_vd = 0;              // dictId bits of the value column (0: COUNT only)
   int narrow_k2min = 0;           // second-split bits the record width needs
   int narrow_img = 0;             // value image in the aggregation's LDS: 0 none, 1 U32, 2 FOR16
@@ -2066,7 +2067,10 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       // and the aggregation looks values up in the column's image (FOR16 / U32) in LDS (run_narrow).  Needs a sorted
       // dictionary (MIN / MAX of dictIds) and, for SUM / AVG, an image that fits beside the aggregation tables.
       const char* en = std::getenv("PGX_PART_NARROW");
-      if (!(en && en[0] == '0') && !P.part_slab && !P.part_fused && keybits > kNarrow1Bits) {
+      const char* es2 = std::getenv("PGX_PART_SLAB");
+      const char* ef2 = std::getenv("PGX_PART_FUSED");
+      const bool forced = (es2 && es2[0] == '1') || (ef2 && ef2[0] == '1');  // the radix variants asked for by name
+      if (!(en && en[0] == '0') && !forced && keybits > kNarrow1Bits) {
         int vd = 0, imgk = 0;
         bool nok = true;
         if (vc >= 0) {
@@ -2090,7 +2094,9 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         if (nok && rb1 + vd <= 48 && k2 <= kNarrowMaxBits2) {
           P.narrow_old_slab = P.part_slab;
           P.narrow_old_dictid = P.part_dictid;
+          P.narrow_old_fused = P.part_fused;
           P.part_narrow = true;
+          P.part_fused = false;
           P.part_slab = true;
           P.part_dictid = vc >= 0;
           P.narrow_vd = vd;
@@ -3674,7 +3680,9 @@ bool narrow_size(const ExecPlan& P, NarrowBuffers& NB) {
   if (NB.rb2 + P.narrow_vd > 32 || NB.rb2 > 31) return false;
   NB.nparts = int64_t(1) << (kNarrow1Bits + NB.k2);
   NB.cap1 = narrow_cap(double(P.part_wg_rows) / (1 << kNarrow1Bits), 64);
-  NB.cap2 = narrow_cap(double(P.rec_total) / double(NB.nparts), 64);
+  // a partition holds whole groups, so its record count varies more than a binomial: start at 1.5x the mean (C3: ~6
+  // sigma of the group-clumped spread) and resize from the measured fills if that is not enough (run_narrow)
+  NB.cap2 = narrow_cap(1.5 * double(P.rec_total) / double(NB.nparts), 64);
   if (NB.cap1 * NB.nwg >= (int64_t(1) << 32) || NB.cap2 >= (int64_t(1) << 31)) return false;
   // count and value-offset sum of one group in one u64: count < 2^cb (a partition holds <= cap2 records)
   const int cb = bits_for(NB.cap2 + 1);
@@ -3737,19 +3745,56 @@ bool run_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hi
   alloc_outputs(ctx, P, B, nullptr, 0);
   if (!narrow_size(P, NB)) return false;
   narrow_alloc(ctx, NB);
-  narrow_prepare(P, NB, st);
-  reset_outputs(P, B, st);
-  launch_scan(P, st);
-  narrow_enqueue(ctx, P, NB, st);
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
-  hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
   unsigned long long* tail = outs + 28;  // spare words of the outputs block: ocount, overflows (part_result reads [28])
-  hip_check(hipMemcpyAsync(tail, NB.ctr.p, 32, hipMemcpyDeviceToHost, st), "D2H");
-  hip_check(hipStreamSynchronize(st), "sync");
+  bool scan = true, ok = false;
+  int attempt = 0;
+  for (; attempt < 4 && !ok; ++attempt) {
+    if (scan) {
+      narrow_prepare(P, NB, st);
+      reset_outputs(P, B, st);
+      launch_scan(P, st);
+    } else {
+      hip_check(hipMemsetAsync(NB.ctr.p, 0, 8, st), "group counter");
+      hip_check(hipMemsetAsync(devp(NB.ctr) + 2, 0, 16, st), "overflow counters");
+    }
+    narrow_enqueue(ctx, P, NB, st);
+    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
+    hip_check(hipMemcpyAsync(tail, NB.ctr.p, 32, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    ok = !tail[1] && !tail[2] && !tail[3];
+    if (ok || (tail[3] && !tail[1] && !tail[2])) break;  // done, or a wavefront table overflowed: no resize helps
+    // a capacity ran over (keys clump: a partition holds whole groups): resize to the measured fills and rerun what
+    // depends on it -- the split and the aggregation, and the scan only if a slab overflowed
+    if (tail[1]) {
+      std::vector<unsigned long long> c(size_t(1 << kNarrow1Bits) * NB.nwg);
+      hip_check(hipMemcpy(c.data(), NB.cnt1.p, c.size() * 8, hipMemcpyDeviceToHost), "slab fills D2H");
+      NB.cap1 = narrow_cap(double(*std::max_element(c.begin(), c.end())), 64);
+      const int64_t slabs = int64_t(1 << kNarrow1Bits) * NB.nwg;
+      if (NB.cap1 * NB.nwg >= (int64_t(1) << 32) || uint64_t(slabs) * NB.cap1 * 6 > kPartMaxBytes) break;
+      NB.lo1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 4);
+      if (NB.hib) NB.hi1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 2);
+      scan = true;
+      continue;  // the split's fills are void: it read truncated slabs
+    }
+    std::vector<unsigned int> c2(size_t(NB.nparts));
+    hip_check(hipMemcpy(c2.data(), NB.cnt2.p, c2.size() * 4, hipMemcpyDeviceToHost), "partition fills D2H");
+    NB.cap2 = narrow_cap(double(*std::max_element(c2.begin(), c2.end())), 64);
+    if (NB.cap2 >= (int64_t(1) << 31) || uint64_t(NB.nparts) * NB.cap2 * 4 > kPartMaxBytes) break;
+    const int cb = bits_for(NB.cap2 + 1);
+    const long double smax = (long double)NB.cap2 * (long double)P.narrow_vrange;
+    int sb = 1;
+    while (sb < 64 && std::ldexp(1.0L, sb) <= smax) ++sb;
+    if (cb + sb > 64 || cb > 62) break;
+    NB.cshift = 64 - cb;
+    NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4);
+    scan = false;
+  }
   if (std::getenv("PGX_NARROW_DEBUG"))  // tests: which path ran
-    std::fprintf(stderr, "[pgx narrow] nwg=%lld cap1=%lld k2=%d cap2=%lld groups=%llu ovf=%llu/%llu/%llu\n",
-                 (long long)NB.nwg, (long long)NB.cap1, NB.k2, (long long)NB.cap2, tail[0], tail[1], tail[2], tail[3]);
-  return !tail[1] && !tail[2] && !tail[3];
+    std::fprintf(stderr, "[pgx narrow] nwg=%lld cap1=%lld k2=%d cap2=%lld groups=%llu ovf=%llu/%llu/%llu attempts=%d ok=%d\n",
+                 (long long)NB.nwg, (long long)NB.cap1, NB.k2, (long long)NB.cap2, tail[0], tail[1], tail[2], tail[3],
+                 attempt + (ok ? 1 : 0), int(ok));
+  return ok;
 }
 
 // The radix path's plan after a narrow attempt gave up: its own slab / dictId choices, 8-byte records.
@@ -3757,6 +3802,7 @@ void narrow_fallback(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs,
   P.part_narrow = false;
   P.part_slab = P.narrow_old_slab;
   P.part_dictid = P.narrow_old_dictid;
+  P.part_fused = P.narrow_old_fused;
   P.part_hi = nullptr;
   plan_jit(ctx, q, segs, n, P, B);
 }

@@ -1612,6 +1612,7 @@ __global__ void __launch_bounds__(256) pgx_mv_group_ordered(const MvGroupArgs* _
   int64_t* hold = reinterpret_cast<int64_t*>(A.ord) + static_cast<uint64_t>(s) * A.naggs * A.slots;
   for (uint64_t sl = tid; sl < A.slots; sl += 256)
     for (int a = 0; a < A.naggs; ++a) hold[a * A.slots + sl] = A.fn[a] == MVF_MINMV ? INT64_MAX : -1;
+  __syncthreads();  // hash key spaces: a slot's owner is not the thread that initialised it
   for (int d = 0; d < S.num_docs; ++d) {
     if (!((S.sel[d >> 5] >> (d & 31)) & 1u)) continue;
     mv_for_each_key(A, S, d, [&](uint64_t lo, uint64_t hi) {
@@ -1641,6 +1642,7 @@ __global__ void __launch_bounds__(256) pgx_mv_group_ordered(const MvGroupArgs* _
       }
     });
   }
+  __syncthreads();  // ... nor the thread that flushes it
   for (uint64_t sl = tid; sl < A.slots; sl += 256)
     for (int a = 0; a < A.naggs; ++a) {
       const int fn = A.fn[a];

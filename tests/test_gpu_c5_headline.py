@@ -71,9 +71,18 @@ def _check(got_map, st, sums, counts, nseg, rows):
     assert list(st) == [docs, 0, docs * NPROJ, nseg * rows]
 
 
-def test_c5_throughput_inflight_vs_oracle(ctx):
-    import torch
+def _hip_streams(k):
+    """k HIP streams of this process (the HIP runtime libpgx uses), as handles for pgx_exec_opts.stream."""
+    hip = C.CDLL("libamdhip64.so")
+    out = []
+    for _ in range(k):
+        s = C.c_void_p()
+        assert hip.hipStreamCreate(C.byref(s)) == 0
+        out.append(s)
+    return hip, out
 
+
+def test_c5_throughput_inflight_vs_oracle(ctx):
     from pinot_amd import engine as E
     from pinot_amd import native as N
     L = N.lib()
@@ -85,11 +94,11 @@ def test_c5_throughput_inflight_vs_oracle(ctx):
         q = E._Query(ctx, req)
         segs = data.segments
         seg_arr = (C.c_void_p * nseg)(*[s.handle.value for s in segs])
-        streams = [torch.cuda.Stream(device="cuda:0") for _ in range(3)]
+        hip, streams = _hip_streams(3)
         pending = []
         for i in range(3):  # as bench.py submit(): bind, then execute asynchronously on stream i, three in flight
             binds, owner = q.bindings(segs, seg_arr)
-            opts = N.ExecOpts(streams[i].cuda_stream, None, 0, N.PGX_X_THROUGHPUT)
+            opts = N.ExecOpts(streams[i].value, None, 0, N.PGX_X_THROUGHPUT)
             r = C.c_void_p()
             N.check(L.pgx_execute_async(ctx.handle, q.handle, seg_arr, nseg, binds, C.byref(opts), C.byref(r)))
             pending.append((r, owner))
@@ -101,6 +110,8 @@ def test_c5_throughput_inflight_vs_oracle(ctx):
             _check(blk.get_aggregation_group_by_result().as_map(), blk.stats.as_list(), sums, counts, nseg, rows)
             L.pgx_result_release(r)
         q.close()
+        for s in streams:
+            hip.hipStreamDestroy(s)
     finally:
         data.free()
 

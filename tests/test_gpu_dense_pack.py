@@ -82,7 +82,7 @@ def test_dense_pack_matches_oracle(ctx, segs, text, rows, variant, monkeypatch, 
     pm = E.InstancePlanMakerImplV2(ctx)
     op = pm.make_inner_segment_plan(seg, q).run()
     m = op.next_block().get_aggregation_group_by_result().as_map()
-    o = H.oracle_answer([oseg], q)
+    o = H.oracle_answer([oseg], q, literal=True)
     fns = [a["fn"] for a in q["aggregations"]]
     assert op.get_execution_statistics().as_list() == list(o["stats"])
     assert set(m) == set(o["map"])
@@ -92,7 +92,7 @@ def test_dense_pack_matches_oracle(ctx, segs, text, rows, variant, monkeypatch, 
     # both segments: one launch whose members differ in size (the pack decision covers the largest member)
     monkeypatch.delenv("PGX_JIT_DUMP")
     blk = pm.make_inter_segment_plan([segs[60000][0], segs[70000][0]], q).execute()
-    o2 = H.oracle_answer([segs[60000][1], segs[70000][1]], q)
+    o2 = H.oracle_answer([segs[60000][1], segs[70000][1]], q, literal=True)
     m2 = blk.get_aggregation_group_by_result().as_map()
     assert set(m2) == set(o2["map"])
     for k, v in o2["map"].items():
