@@ -860,13 +860,28 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("  PGX_G u32* const poutA = (PGX_G u32*)A.table;");
       if (nhib) e.ln("  PGX_G unsigned short* const poutB = (PGX_G unsigned short*)A.part_hi;");
       e.ln("  const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
-      e.ln("  for (int i = tid; i < tot; i += PT) {");
-      e.ln("    const u32 b = pstK[i];");
-      e.ln("    const u32 pos = ((const u32*)pgpos)[b] + (u32)(i - (int)poffs[b]);");
-      e.ln("    if (pos < (u32)A.part_cap) {");
-      e.ln("      const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)pos;");
-      e.ln("      poutA[o] = pstA[i];");
-      if (nhib) e.ln("      poutB[o] = pstB[i];");
+      // copy-out in halves of PR / 2 records per thread: every LDS read of a half issued before its stores
+      e.ln("  #pragma unroll");
+      e.ln("  for (int hh = 0; hh < 2; ++hh) {");
+      e.ln("    u32 cb[PR / 2], ca[PR / 2];");
+      if (nhib) e.ln("    u32 cbh[PR / 2];");
+      e.ln("    #pragma unroll");
+      e.ln("    for (int k = 0; k < PR / 2; ++k) {");
+      e.ln("      const int i = (hh * (PR / 2) + k) * PT + tid;");
+      e.ln("      cb[k] = i < tot ? (u32)pstK[i] : 0u;");
+      e.ln("      ca[k] = i < tot ? pstA[i] : 0u;");
+      if (nhib) e.ln("      cbh[k] = i < tot ? (u32)pstB[i] : 0u;");
+      e.ln("    }");
+      e.ln("    #pragma unroll");
+      e.ln("    for (int k = 0; k < PR / 2; ++k) {");
+      e.ln("      const int i = (hh * (PR / 2) + k) * PT + tid;");
+      e.ln("      if (i >= tot) continue;");
+      e.ln("      const u32 pos = ((const u32*)pgpos)[cb[k]] + (u32)(i - (int)poffs[cb[k]]);");
+      e.ln("      if (pos < (u32)A.part_cap) {");
+      e.ln("        const long long o = ((long long)cb[k] * A.part_nwg + wsl) * A.part_cap + (long long)pos;");
+      e.ln("        poutA[o] = ca[k];");
+      if (nhib) e.ln("        poutB[o] = (unsigned short)cbh[k];");
+      e.ln("      }");
       e.ln("    }");
       e.ln("  }");
       e.ln("}");

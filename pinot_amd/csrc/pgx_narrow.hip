@@ -38,11 +38,18 @@ __device__ __forceinline__ void n_lds_barrier() {  // LDS-only ordering: loads i
 // d << (rb1 - k2), appended to partition (b << k2 | sub) at out[part * cap2 + i], its count in cnt2[part].
 // ---------------------------------------------------------------------------------------------------------------------
 constexpr int kN2Threads = 1024;
+constexpr int kN2Waves = kN2Threads / 64;
 constexpr int kN2Per = 16;
 constexpr int kN2Chunk = kN2Threads * kN2Per;  // records per round: 64 KiB of staged u32 records
 constexpr int kN2MaxSub = 1 << kNarrowMaxBits2;
 constexpr int kN2MaxSlabs = 1024;
 
+// Rounds walk the bucket's slabs in order: round (w, c0) holds records [c0, c0 + kN2Chunk) of slab w, so a record's
+// address is plain arithmetic (no per-record slab search).  Per round: the split fields and the LDS histogram (the
+// atomic returns the record's rank in its sub-bucket), an exclusive scan of the
+// histogram by all 16 waves (64 sub-buckets each, conflict-free), the records staged sub-bucket-sorted, the next
+// round's loads issued, and the copy-out of per-partition runs with the LDS reads of 8 records issued before their
+// stores.
 __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* __restrict__ lo,
                                                                const uint16_t* __restrict__ hi,
                                                                const unsigned long long* __restrict__ cnt1, int nwg,
@@ -53,67 +60,47 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
   __shared__ uint32_t stage[kN2Chunk];
   __shared__ uint16_t ssub[kN2Chunk];
   __shared__ uint32_t hist[kN2MaxSub], offs[kN2MaxSub], gpos[kN2MaxSub], fill[kN2MaxSub];
-  __shared__ uint32_t pre[kN2MaxSlabs + 1];
-  __shared__ uint32_t wsum[kN2Threads / 64];
-  __shared__ uint32_t total;
+  __shared__ uint32_t scnt[kN2MaxSlabs];
+  __shared__ uint32_t wsum[kN2Waves];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nsub = 1 << k2;
   const int rb2 = rb1 - k2;
   const uint64_t m2 = (uint64_t(1) << rb2) - 1u;
-  for (int i = tid; i < nsub; i += kN2Threads) {
+  for (int i = tid; i < kN2MaxSub; i += kN2Threads) {
     hist[i] = 0u;
     fill[i] = 0u;
   }
-  // prefix of the slab counts (nwg <= 1024: one per thread)
-  const uint32_t v = tid < nwg ? static_cast<uint32_t>(min(cnt1[static_cast<int64_t>(b) * nwg + tid],
-                                                           static_cast<unsigned long long>(cap1)))
-                               : 0u;
-  uint32_t incl = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) wsum[wave] = incl;
+  for (int i = tid; i < nwg; i += kN2Threads)
+    scnt[i] = static_cast<uint32_t>(min(cnt1[static_cast<int64_t>(b) * nwg + i], static_cast<unsigned long long>(cap1)));
   __syncthreads();
-  if (tid < 64) {
-    const uint32_t x = tid < kN2Threads / 64 ? wsum[tid] : 0u;
-    uint32_t xi = x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(xi, d, 64);
-      if (tid >= d) xi += y;
-    }
-    if (tid < kN2Threads / 64) wsum[tid] = xi - x;
-    if (tid == 63) pre[nwg] = xi;
-  }
-  __syncthreads();
-  if (tid < nwg) pre[tid] = wsum[wave] + incl - v;
-  __syncthreads();
-  const uint32_t ntot = pre[nwg];
   const PGX_GLOBAL uint32_t* glo = (const PGX_GLOBAL uint32_t*)lo + static_cast<int64_t>(b) * nwg * cap1;
   const PGX_GLOBAL uint16_t* ghi = hi ? (const PGX_GLOBAL uint16_t*)hi + static_cast<int64_t>(b) * nwg * cap1 : nullptr;
   PGX_GLOBAL uint32_t* gout = (PGX_GLOBAL uint32_t*)out + static_cast<int64_t>(b) * nsub * cap2;
-  int w = 0;  // this thread's slab: positions only grow
+  // the first round at or after (w, c0): slabs with no records left are skipped (uniform: every thread walks alike)
+  auto next_round = [&](int& w, uint32_t& c0) {
+    while (w < nwg && c0 >= scnt[w]) {
+      ++w;
+      c0 = 0u;
+    }
+  };
   uint32_t xl[kN2Per], xh[kN2Per];
-  // the records of round c0 into xl / xh: addresses from the LDS prefix walk, every load in flight before any use
-  auto load = [&](uint32_t c0) {
+  auto load = [&](int w, uint32_t c0) {
+    const uint32_t n = scnt[w];
+    const PGX_GLOBAL uint32_t* sl = glo + static_cast<int64_t>(w) * cap1;
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k) {
       const uint32_t pos = c0 + static_cast<uint32_t>(k * kN2Threads + tid);
-      xl[k] = 0u;
-      xh[k] = 0u;
-      if (pos < ntot) {
-        while (pre[w + 1] <= pos) ++w;
-        const int64_t idx = static_cast<int64_t>(w) * cap1 + (pos - pre[w]);
-        xl[k] = __builtin_nontemporal_load(glo + idx);
-        if (ghi) xh[k] = __builtin_nontemporal_load(ghi + idx);
-      }
+      xl[k] = pos < n ? __builtin_nontemporal_load(sl + pos) : 0u;
+      xh[k] = (ghi && pos < n) ? __builtin_nontemporal_load(ghi + static_cast<int64_t>(w) * cap1 + pos) : 0u;
     }
   };
-  if (ntot) load(0u);
-  for (uint32_t c0 = 0; c0 < ntot; c0 += kN2Chunk) {
+  int w = 0;
+  uint32_t c0 = 0u;
+  next_round(w, c0);
+  if (w < nwg) load(w, c0);
+  while (w < nwg) {
+    const uint32_t n = scnt[w];
     // split fields of this round; pk = sub-bucket | rank << 16 (a round holds 16384 records), ~0: no record
     uint32_t r2[kN2Per], pk[kN2Per];
 #pragma unroll
@@ -122,43 +109,34 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
       const uint64_t r1 = static_cast<uint64_t>(xl[k]) | (static_cast<uint64_t>(xh[k]) << 32);
       r2[k] = static_cast<uint32_t>((r1 & m2) | ((r1 >> rb1) << rb2));
       pk[k] = 0xFFFFFFFFu;
-      if (pos < ntot) {
+      if (pos < n) {
         const uint32_t sb = static_cast<uint32_t>(r1 >> rb2) & static_cast<uint32_t>(nsub - 1);
         pk[k] = sb | (atomicAdd(&hist[sb], 1u) << 16);
       }
     }
-    if (c0 + kN2Chunk < ntot) load(c0 + kN2Chunk);  // the next round's loads overlap this round's split
+    int nw2 = w;
+    uint32_t nc0 = c0 + kN2Chunk;
+    next_round(nw2, nc0);
     n_lds_barrier();
-    if (tid < 64) {  // offsets of this round, this workgroup's runs in each partition, histogram cleared
-      constexpr int PER = kN2MaxSub / 64;
-      uint32_t h[PER], x = 0;
+    // exclusive scan of hist[0, kN2MaxSub): wave v owns sub-buckets [64 v, 64 v + 64), one per lane
+    const int sidx = wave * 64 + lane;
+    const uint32_t h = hist[sidx];
+    uint32_t incl = h;
 #pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int s = tid * PER + q;
-        h[q] = s < nsub ? hist[s] : 0u;
-        x += h[q];
-      }
-      uint32_t xi = x;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(xi, d, 64);
-        if (tid >= d) xi += y;
-      }
-      uint32_t e = xi - x;
-#pragma unroll
-      for (int q = 0; q < PER; ++q) {
-        const int s = tid * PER + q;
-        if (s < nsub) {
-          offs[s] = e;
-          const uint32_t f = fill[s];
-          gpos[s] = f;
-          fill[s] = f + h[q];
-          hist[s] = 0u;
-        }
-        e += h[q];
-      }
-      if (tid == 63) total = xi;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= d) incl += y;
     }
+    if (lane == 63) wsum[wave] = incl;
+    n_lds_barrier();
+    uint32_t before = 0;
+#pragma unroll
+    for (int v = 0; v < kN2Waves; ++v) before += v < wave ? wsum[v] : 0u;
+    offs[sidx] = before + incl - h;
+    const uint32_t f = fill[sidx];
+    gpos[sidx] = f;
+    fill[sidx] = f + h;
+    hist[sidx] = 0u;
     n_lds_barrier();
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k)
@@ -168,13 +146,31 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
         stage[q] = r2[k];
         ssub[q] = static_cast<uint16_t>(sb);
       }
+    if (nw2 < nwg) load(nw2, nc0);  // the next round's loads overlap this round's copy-out
     n_lds_barrier();
-    const uint32_t tot = total;
-    for (uint32_t i = tid; i < tot; i += kN2Threads) {
-      const uint32_t s = ssub[i];
-      const uint32_t p = gpos[s] + (i - offs[s]);
-      if (p < static_cast<uint64_t>(cap2)) gout[static_cast<int64_t>(s) * cap2 + p] = stage[i];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int v = 0; v < kN2Waves; ++v) tot += wsum[v];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {  // two halves of 8 records (registers: the next round's loads are in flight)
+      uint32_t cs[kN2Per / 2], cv[kN2Per / 2];
+#pragma unroll
+      for (int k = 0; k < kN2Per / 2; ++k) {
+        const uint32_t i = static_cast<uint32_t>((hh * kN2Per / 2 + k) * kN2Threads + tid);
+        cs[k] = i < tot ? ssub[i] : 0u;
+        cv[k] = i < tot ? stage[i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < kN2Per / 2; ++k) {
+        const uint32_t i = static_cast<uint32_t>((hh * kN2Per / 2 + k) * kN2Threads + tid);
+        if (i >= tot) continue;
+        const uint32_t p = gpos[cs[k]] + (i - offs[cs[k]]);
+        if (p < static_cast<uint64_t>(cap2)) gout[static_cast<int64_t>(cs[k]) * cap2 + p] = cv[k];
+      }
     }
+    w = nw2;
+    c0 = nc0;
+    n_lds_barrier();  // wsum and the staging are reused by the next round
   }
   __syncthreads();
   for (int s = tid; s < nsub; s += kN2Threads) {
@@ -184,15 +180,21 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
 }
 
 // ---------------------------------------------------------------------------------------------------------------------
-// Aggregation.  Wavefront-private open-addressing tables (kNASlots slots: key bits, count << cshift | value sum,
-// min dictId, max dictId); a wavefront takes partitions p = its global index, + all wavefronts, ...; the next 1024
-// records (of this partition or the next) are loaded while the current ones are aggregated.  The workgroup's LDS holds
-// the value image (IMG 1: u32 value - vbase per dictId, 2: FOR16 = 64 u32 block bases + u16 offset per dictId).
+// Aggregation.  Wavefront-private open-addressing tables of kNABuckets 4-way buckets (16 contiguous bytes of keys,
+// read with ONE ds_read_b128): key bits, count << cshift | value sum, min dictId, max dictId.  A wavefront takes
+// partitions p = its global index, + all wavefronts, ...; the next 1024 records (of this partition or the next) are
+// loaded while the current ones are aggregated.  Records are resolved 8 at a time: the 8 home buckets and the 8 values
+// are read back to back (one LDS round trip for all), a key found in its home bucket -- every record of a group but
+// its first, unless the bucket overflowed -- goes straight to the fire-and-forget LDS atomics, and only the others take
+// the probing loop (insert by CAS, then neighbouring buckets).  The workgroup's LDS holds the value image (IMG 1: u32
+// value - vbase per dictId, 2: FOR16 = 64 u32 block bases + u16 offset per dictId).
 // ctr: [0] groups appended, [3] overflow (a table filled up, or more groups than ocap).
 // ---------------------------------------------------------------------------------------------------------------------
 constexpr int kNAThreads = 512;
 constexpr int kNAWaves = kNAThreads / 64;
-constexpr int kNASlots = 192;
+constexpr int kNAWays = 4;
+constexpr int kNABuckets = 48;
+constexpr int kNASlots = kNABuckets * kNAWays;  // 192
 constexpr int kNAImgWords = 64 + 65536 / 2;
 constexpr uint32_t kNAEmpty = 0xFFFFFFFFu;
 typedef unsigned int na_u32x4 __attribute__((ext_vector_type(4)));
@@ -204,6 +206,10 @@ __device__ __forceinline__ uint32_t na_img(const uint32_t* simg, int img_sh, uin
   return 0u;
 }
 
+__device__ __forceinline__ int na_way(const na_u32x4 k, uint32_t key) {
+  return k.x == key ? 0 : k.y == key ? 1 : k.z == key ? 2 : k.w == key ? 3 : -1;
+}
+
 template <int IMG, bool SUM, bool MN, bool MX>
 __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
     const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
@@ -211,7 +217,7 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
     int img_sh, const int64_t* __restrict__ vdict, int cshift, uint64_t* __restrict__ okey,
     uint64_t* __restrict__ oplane, int64_t ocap, unsigned long long* __restrict__ ctr) {
   __shared__ __attribute__((aligned(16))) uint32_t simg[IMG ? kNAImgWords : 1];
-  __shared__ uint32_t tkey[kNAWaves * kNASlots];
+  __shared__ __attribute__((aligned(16))) uint32_t tkey[kNAWaves * kNASlots];
   __shared__ unsigned long long tsc[kNAWaves * kNASlots];
   __shared__ uint32_t tmn[MN ? kNAWaves * kNASlots : 1], tmx[MX ? kNAWaves * kNASlots : 1];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -251,6 +257,23 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
       buf[4 * q + 2] = x.z;
       buf[4 * q + 3] = x.w;
     }
+  };
+  // slot of key r2 whose home bucket b did not hold it: empty ways are claimed by CAS, then the next buckets
+  auto probe = [&](uint32_t r2, uint32_t b) -> int {
+    for (int t = 0; t < kNABuckets;) {
+      const na_u32x4 k = *reinterpret_cast<const na_u32x4*>(K + b * kNAWays);
+      const int m = na_way(k, r2);
+      if (m >= 0) return static_cast<int>(b) * kNAWays + m;
+      const int e = k.x == kNAEmpty ? 0 : k.y == kNAEmpty ? 1 : k.z == kNAEmpty ? 2 : k.w == kNAEmpty ? 3 : -1;
+      if (e >= 0) {
+        const uint32_t prev = atomicCAS(&K[b * kNAWays + e], kNAEmpty, r2);
+        if (prev == kNAEmpty || prev == r2) return static_cast<int>(b) * kNAWays + e;
+        continue;  // another lane took that way first: look at the bucket again
+      }
+      b = b + 1u == static_cast<uint32_t>(kNABuckets) ? 0u : b + 1u;
+      ++t;
+    }
+    return -1;
   };
   auto flush = [&](int pp) {
     constexpr int Q = kNASlots / 64;
@@ -313,38 +336,37 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
     }
     if (np < nparts) load(np, ni0, nn, nxt);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const uint32_t e = static_cast<uint32_t>((j >> 2) * 256 + lane * 4 + (j & 3));
-      if (i0 + e >= n) continue;
-      const uint32_t R = cur[j];
-      const uint32_t r2 = R & rmask;
-      const uint32_t d = rb2 >= 32 ? 0u : R >> rb2;
-      uint32_t slot = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNASlots) >> rb2);
-      int found = -1;
-      for (int t = 0; t < kNASlots;) {
-        const uint32_t k = K[slot];
-        if (k == r2) {
-          found = static_cast<int>(slot);
-          break;
-        }
-        if (k == kNAEmpty) {
-          const uint32_t prev = atomicCAS(&K[slot], kNAEmpty, r2);
-          if (prev == kNAEmpty || prev == r2) {
-            found = static_cast<int>(slot);
-            break;
-          }
-          continue;  // another lane took the slot first: look at it again
-        }
-        slot = slot + 1u == static_cast<uint32_t>(kNASlots) ? 0u : slot + 1u;
-        ++t;
+    for (int h = 0; h < 2; ++h) {  // two halves of 8 records: home buckets and values read back to back
+      na_u32x4 kb[8];
+      uint32_t val[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int jj = h * 8 + j;
+        const uint32_t R = cur[jj];
+        const uint32_t r2 = R & rmask;
+        const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2);
+        kb[j] = *reinterpret_cast<const na_u32x4*>(K + b * kNAWays);
+        val[j] = SUM ? na_img<IMG>(simg, img_sh, rb2 >= 32 ? 0u : R >> rb2) : 0u;
       }
-      if (found < 0) {
-        lost = true;
-        continue;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int jj = h * 8 + j;
+        const uint32_t e = static_cast<uint32_t>((jj >> 2) * 256 + lane * 4 + (jj & 3));
+        if (i0 + e >= n) continue;
+        const uint32_t R = cur[jj];
+        const uint32_t r2 = R & rmask;
+        const uint32_t d = rb2 >= 32 ? 0u : R >> rb2;
+        const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2);
+        const int m = na_way(kb[j], r2);
+        int slot = m >= 0 ? static_cast<int>(b) * kNAWays + m : probe(r2, b);
+        if (slot < 0) {
+          lost = true;
+          continue;
+        }
+        atomicAdd(&S[slot], SUM ? one + val[j] : one);
+        if (MN) atomicMin(&N[slot], d);
+        if (MX) atomicMax(&X[slot], d);
       }
-      atomicAdd(&S[found], SUM ? one + na_img<IMG>(simg, img_sh, d) : one);
-      if (MN) atomicMin(&N[found], d);
-      if (MX) atomicMax(&X[found], d);
     }
     if (ni0 == 0u) flush(p);
 #pragma unroll
