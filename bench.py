@@ -369,10 +369,18 @@ def main():
         L.pgx_result_release(step())
         t_lat.append(time.perf_counter() - t1)
     barrier_sync(world)
+    prof = None
+    if os.environ.get("PGX_BENCH_CPROFILE"):  # host-overhead hunting: Python profile of the timed steps (not for lines)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     last = run_steps(args.steps, keep_last=True)
     barrier_sync(world)
     elapsed = time.perf_counter() - t0
+    if prof is not None:
+        prof.disable()
+        prof.dump_stats(os.environ["PGX_BENCH_CPROFILE"])
     if world > 1:
         import torch.distributed as dist
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda:%d" % local)
