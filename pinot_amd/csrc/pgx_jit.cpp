@@ -1434,6 +1434,30 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.selmask = true;
     shapes.push_back(s);
   }
+  {  // the C5 bench shape: the bitmap program's doc mask as one leaf, dense LDS group-by of gk, packed COUNT + SUM(m)
+     // through the FOR16 image
+    JitShape s = base(10, 16, IMG_FOR16, 11);
+    s.cols[1].img_words = 64 + 32768;
+    s.cols.push_back(JitCol{});
+    s.cols[2].bits = 10;
+    s.cols[2].decode = false;
+    s.leaf_col = {2, 2, 2, -1};
+    s.leaf_mode = {LEAF_NONE, LEAF_NONE, LEAF_NONE, LEAF_DOCMASK};
+    s.prog_op = {OP_LEAF, OP_STAT};
+    s.prog_arg = {3, 0};
+    s.R = 16;
+    s.T = 1024;
+    s.group_mode = G_DENSE_LDS;
+    s.gcol = {0};
+    s.gmul = {1};
+    s.dense_slots = 1000;
+    s.agg_kind = {A_SUM};
+    s.agg_col = {1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64};
+    s.num_planes = 2;
+    s.dense_pack = 40;
+    shapes.push_back(s);
+  }
   for (int R : {8, 16, 32}) {  // statistics automaton input: every leaf's predicate bits written per lane
     JitShape s = base(R == 8 ? 8 : (R == 16 ? 10 : 7), 16, IMG_FOR16, 11);
     s.cols.push_back(JitCol{});
