@@ -136,7 +136,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       lds += s.T * s.R * 8;
     }
     phist_off = lds;
-    lds += pnb * 16 + 16 + (eslab ? pnb * 4 : 0);  // hist (u32), offs (u32), gpos (u64), total[, slab fill (u32)]
+    // hist (u32), offs (u32), gpos (u64), total[, slab fill (u32) | narrow: the second hist buffer]
+    lds += pnb * 16 + 16 + (eslab ? pnb * 4 : 0);
   }
   if (emit && !epart) {
     const int waves = s.T / 64;
@@ -253,6 +254,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     if (eslab) e.ln("u32* const pfill = phist + ", 4 * pnb + 4, ";");
     e.ln("for (int i = tid; i < ", pnb, "; i += PT) phist[i] = 0u;");
     if (eslab) e.ln("for (int i = tid; i < ", pnb, "; i += PT) pfill[i] = 0u;");
+    if (enarrow) {  // the second histogram buffer sits where slab mode keeps pfill; fills live in registers
+      e.ln("u32 nfill[", std::max(1, pnb / 64), "] = {};");
+      e.ln("int pbuf = 0;");
+    }
     e.ln("__syncthreads();");
   }
   e.ln("u64 st_docs = 0, st_ent = 0;");
@@ -840,12 +845,13 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       // next sub-step's histogram atomics follow the staging reads of this one's copy-out only through its first
       // barrier, and the histogram was cleared by wave 0 before the second.
       e.ln("{");
+      e.ln("  u32* const ph = pbuf ? pfill : phist;  // this sub-step's histogram buffer");
       e.ln("  u32 rk[PR];");
       e.ln("  #pragma unroll");
-      e.ln("  for (int j = 0; j < PR; ++j) rk[j] = recs[j] != ~0ull ? atomicAdd(&phist[(u32)(recs[j] >> 56)], 1u) : 0u;");
+      e.ln("  for (int j = 0; j < PR; ++j) rk[j] = recs[j] != ~0ull ? atomicAdd(&ph[(u32)(recs[j] >> 56)], 1u) : 0u;");
       e.ln("  pgx_lds_barrier();");
-      e.ln("  pgx_narrow_scan<", pnb, ">(phist, poffs, (u32*)pgpos, pfill, ptotal, tid);");
-      e.ln("  pgx_lds_barrier();");
+      e.ln("  const int tot = (int)pgx_narrow_scan2<", pnb, ">(ph, poffs, (u32*)pgpos, nfill, pbuf ? phist : pfill, tid);");
+      e.ln("  pbuf ^= 1;");
       e.ln("  #pragma unroll");
       e.ln("  for (int j = 0; j < PR; ++j)");
       e.ln("    if (recs[j] != ~0ull) {");
@@ -856,7 +862,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("      pstK[q] = (unsigned char)b;");
       e.ln("    }");
       e.ln("  pgx_lds_barrier();");
-      e.ln("  const int tot = (int)*ptotal;");
       e.ln("  PGX_G u32* const poutA = (PGX_G u32*)A.table;");
       if (nhib) e.ln("  PGX_G unsigned short* const poutB = (PGX_G unsigned short*)A.part_hi;");
       e.ln("  const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
@@ -1033,7 +1038,18 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("  }");
   e.ln("}");
   e.ln("__syncthreads();");
-  if (eslab) {  // slab fills (every record, also past part_cap: the host resizes from the largest)
+  if (enarrow) {  // slab fills from wavefront 0's registers (every wavefront holds the same)
+    e.ln("if ((tid >> 6) == 0) {");
+    e.ln("  #pragma unroll");
+    e.ln("  for (int q = 0; q < ", std::max(1, pnb / 64), "; ++q) {");
+    e.ln("    const int i = q * 64 + lane;");
+    e.ln("    if (i >= ", pnb, ") continue;");
+    e.ln("    const u32 h = nfill[q];");
+    e.ln("    A.part_cursor[((long long)i * A.part_nwg + A.part_wg_base + (long long)blockIdx.x) * A.part_cstride] = h;");
+    e.ln("    if (h > (u32)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
+    e.ln("  }");
+    e.ln("}");
+  } else if (eslab) {  // slab fills (every record, also past part_cap: the host resizes from the largest)
     e.ln("for (int i = tid; i < ", pnb, "; i += PT) {");
     e.ln("  const u32 h = pfill[i];");
     e.ln("  A.part_cursor[((long long)i * A.part_nwg + A.part_wg_base + (long long)blockIdx.x) * A.part_cstride] = h;");

@@ -45,11 +45,14 @@ constexpr int kN2MaxSub = 1 << kNarrowMaxBits2;
 constexpr int kN2MaxSlabs = 1024;
 
 // Rounds walk the bucket's slabs in order: round (w, c0) holds records [c0, c0 + kN2Chunk) of slab w, so a record's
-// address is plain arithmetic (no per-record slab search).  Per round: the split fields and the LDS histogram (the
-// atomic returns the record's rank in its sub-bucket), an exclusive scan of the
-// histogram by all 16 waves (64 sub-buckets each, conflict-free), the records staged sub-bucket-sorted, the next
-// round's loads issued, and the copy-out of per-partition runs with the LDS reads of 8 records issued before their
-// stores.
+// address is plain arithmetic (no per-record slab search).  Two barriers per round:
+//   split fields + LDS histogram of this round's buffer (the atomic returns the record's rank in its sub-bucket)
+//   | B1 | every wavefront scans the whole histogram itself (no single-wave phase: the same offsets, the same slab fills
+//   kept in registers by every wavefront, written to LDS redundantly), stages its records sub-bucket-sorted and issues
+//   the next round's loads; wavefront 0 clears the OTHER histogram buffer for the next round
+//   | B2 | copy-out of per-partition runs, the LDS reads of 8 records issued before their stores.
+// The staging, offsets and positions of round r are rewritten only after B1 of round r + 1, which every wavefront
+// passes after its copy-out of round r.
 __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* __restrict__ lo,
                                                                const uint16_t* __restrict__ hi,
                                                                const unsigned long long* __restrict__ cnt1, int nwg,
@@ -59,18 +62,18 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
                                                                unsigned long long* __restrict__ ovf) {
   __shared__ uint32_t stage[kN2Chunk];
   __shared__ uint16_t ssub[kN2Chunk];
-  __shared__ uint32_t hist[kN2MaxSub], offs[kN2MaxSub], gpos[kN2MaxSub], fill[kN2MaxSub];
+  __shared__ uint32_t hist[2][kN2MaxSub], offs[kN2MaxSub], gpos[kN2MaxSub];
   __shared__ uint32_t scnt[kN2MaxSlabs];
-  __shared__ uint32_t wsum[kN2Waves];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nsub = 1 << k2;
   const int rb2 = rb1 - k2;
   const uint64_t m2 = (uint64_t(1) << rb2) - 1u;
-  for (int i = tid; i < kN2MaxSub; i += kN2Threads) {
-    hist[i] = 0u;
-    fill[i] = 0u;
-  }
+  constexpr int PER = kN2MaxSub / 64;  // sub-buckets q * 64 + lane of every lane
+  uint32_t fill[PER];
+#pragma unroll
+  for (int q = 0; q < PER; ++q) fill[q] = 0u;
+  for (int i = tid; i < 2 * kN2MaxSub; i += kN2Threads) (&hist[0][0])[i] = 0u;
   for (int i = tid; i < nwg; i += kN2Threads)
     scnt[i] = static_cast<uint32_t>(min(cnt1[static_cast<int64_t>(b) * nwg + i], static_cast<unsigned long long>(cap1)));
   __syncthreads();
@@ -95,12 +98,13 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
       xh[k] = (ghi && pos < n) ? __builtin_nontemporal_load(ghi + static_cast<int64_t>(w) * cap1 + pos) : 0u;
     }
   };
-  int w = 0;
+  int w = 0, buf = 0;
   uint32_t c0 = 0u;
   next_round(w, c0);
   if (w < nwg) load(w, c0);
   while (w < nwg) {
     const uint32_t n = scnt[w];
+    uint32_t* const H = hist[buf];
     // split fields of this round; pk = sub-bucket | rank << 16 (a round holds 16384 records), ~0: no record
     uint32_t r2[kN2Per], pk[kN2Per];
 #pragma unroll
@@ -111,33 +115,32 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
       pk[k] = 0xFFFFFFFFu;
       if (pos < n) {
         const uint32_t sb = static_cast<uint32_t>(r1 >> rb2) & static_cast<uint32_t>(nsub - 1);
-        pk[k] = sb | (atomicAdd(&hist[sb], 1u) << 16);
+        pk[k] = sb | (atomicAdd(&H[sb], 1u) << 16);
       }
     }
     int nw2 = w;
     uint32_t nc0 = c0 + kN2Chunk;
     next_round(nw2, nc0);
-    n_lds_barrier();
-    // exclusive scan of hist[0, kN2MaxSub): wave v owns sub-buckets [64 v, 64 v + 64), one per lane
-    const int sidx = wave * 64 + lane;
-    const uint32_t h = hist[sidx];
-    uint32_t incl = h;
+    n_lds_barrier();  // B1
+    uint32_t carry = 0;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = __shfl_up(incl, d, 64);
-      if (lane >= d) incl += y;
+    for (int q = 0; q < PER; ++q) {
+      const int s = q * 64 + lane;
+      const uint32_t h = H[s];
+      uint32_t incl = h;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+      }
+      offs[s] = carry + incl - h;
+      gpos[s] = fill[q];
+      fill[q] += h;
+      carry += __shfl(incl, 63, 64);
     }
-    if (lane == 63) wsum[wave] = incl;
-    n_lds_barrier();
-    uint32_t before = 0;
-#pragma unroll
-    for (int v = 0; v < kN2Waves; ++v) before += v < wave ? wsum[v] : 0u;
-    offs[sidx] = before + incl - h;
-    const uint32_t f = fill[sidx];
-    gpos[sidx] = f;
-    fill[sidx] = f + h;
-    hist[sidx] = 0u;
-    n_lds_barrier();
+    const uint32_t tot = carry;
+    if (wave == 0)
+      for (int s = lane; s < kN2MaxSub; s += 64) hist[buf ^ 1][s] = 0u;
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k)
       if (pk[k] != 0xFFFFFFFFu) {
@@ -147,10 +150,7 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
         ssub[q] = static_cast<uint16_t>(sb);
       }
     if (nw2 < nwg) load(nw2, nc0);  // the next round's loads overlap this round's copy-out
-    n_lds_barrier();
-    uint32_t tot = 0;
-#pragma unroll
-    for (int v = 0; v < kN2Waves; ++v) tot += wsum[v];
+    n_lds_barrier();  // B2
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {  // two halves of 8 records (registers: the next round's loads are in flight)
       uint32_t cs[kN2Per / 2], cv[kN2Per / 2];
@@ -170,12 +170,17 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
     }
     w = nw2;
     c0 = nc0;
-    n_lds_barrier();  // wsum and the staging are reused by the next round
+    buf ^= 1;
   }
-  __syncthreads();
-  for (int s = tid; s < nsub; s += kN2Threads) {
-    cnt2[static_cast<int64_t>(b) * nsub + s] = fill[s];
-    if (fill[s] > static_cast<uint64_t>(cap2)) atomicAdd(ovf, 1ull);
+  // every wavefront holds the same fills: wavefront 0 publishes them
+  if (wave == 0) {
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      const int s = q * 64 + lane;
+      if (s >= nsub) continue;
+      cnt2[static_cast<int64_t>(b) * nsub + s] = fill[q];
+      if (fill[q] > static_cast<uint64_t>(cap2)) atomicAdd(ovf, 1ull);
+    }
   }
 }
 
@@ -275,12 +280,55 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
     }
     return -1;
   };
-  auto flush = [&](int pp) {
-    constexpr int Q = kNASlots / 64;
-    uint32_t has = 0;
+  // A finished partition: its groups move to registers (<= 3 slots per lane), the table is cleared, and one lane
+  // reserves the output rows; the rows are written at the NEXT partition's end (flush_end), so the reservation's round
+  // trip to L2 overlaps the next partition's records instead of stalling the wavefront.
+  constexpr int Q = kNASlots / 64;
+  uint32_t fk[Q], fn_[Q], fx[Q], fhas = 0, fexcl = 0;
+  unsigned long long fsc[Q], fbase = 0ull;
+  int fp = -1;
+  auto flush_end = [&]() {
+    if (fp < 0) return;
+    const unsigned long long base = __shfl(fbase, 0, 64);
+    unsigned long long o = base + fexcl;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) has |= (K[q * 64 + lane] != kNAEmpty ? 1u : 0u) << q;
-    const uint32_t mine = __popc(has);
+    for (int q = 0; q < Q; ++q) {
+      if (!((fhas >> q) & 1u)) continue;
+      if (o < static_cast<unsigned long long>(ocap)) {
+        uint64_t y = ((((static_cast<uint64_t>(fp) << rb2) | fk[q]) * ic2) & kmask);
+        y ^= y >> ms;
+        okey[o] = (y * ic1) & kmask;
+        const uint64_t c = fsc[q] >> cshift;
+        oplane[o] = c;  // plane 0: doc count; planes 1..3: int64 sum, ordered min, ordered max (pgx_part_aggregate)
+        oplane[ocap + o] = static_cast<uint64_t>(static_cast<int64_t>(fsc[q] & smask) + static_cast<int64_t>(c) * vbase);
+        int64_t vlo = 0, vhi = 0;
+        if (MN) vlo = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, fn_[q])) : vd[fn_[q]];
+        if (MX) vhi = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, fx[q])) : vd[fx[q]];
+        oplane[2 * ocap + o] = static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull;
+        oplane[3 * ocap + o] = static_cast<uint64_t>(vhi) ^ 0x8000000000000000ull;
+      } else {
+        lost = true;
+      }
+      ++o;
+    }
+    fp = -1;
+  };
+  auto flush_begin = [&](int pp) {
+    fhas = 0;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int s = q * 64 + lane;
+      fk[q] = K[s];
+      fsc[q] = S[s];
+      fn_[q] = MN ? N[s] : 0u;
+      fx[q] = MX ? X[s] : 0u;
+      fhas |= (fk[q] != kNAEmpty ? 1u : 0u) << q;
+      K[s] = kNAEmpty;
+      S[s] = 0ull;
+      if (MN) N[s] = 0xFFFFFFFFu;
+      if (MX) X[s] = 0u;
+    }
+    const uint32_t mine = __popc(fhas);
     uint32_t incl = mine;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
@@ -288,53 +336,32 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
       if (lane >= d) incl += y;
     }
     const uint32_t tot = __shfl(incl, 63, 64);
-    unsigned long long base = 0ull;
-    if (lane == 0 && tot) base = atomicAdd(ctr, static_cast<unsigned long long>(tot));
-    base = __shfl(base, 0, 64);
-    unsigned long long o = base + (incl - mine);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int s = q * 64 + lane;
-      if ((has >> q) & 1u) {
-        if (o < static_cast<unsigned long long>(ocap)) {
-          uint64_t y = ((((static_cast<uint64_t>(pp) << rb2) | K[s]) * ic2) & kmask);
-          y ^= y >> ms;
-          okey[o] = (y * ic1) & kmask;
-          const unsigned long long sc = S[s];
-          const uint64_t c = sc >> cshift;
-          oplane[o] = c;  // plane 0: doc count; planes 1..3: int64 sum, ordered min, ordered max (pgx_part_aggregate)
-          oplane[ocap + o] = static_cast<uint64_t>(static_cast<int64_t>(sc & smask) + static_cast<int64_t>(c) * vbase);
-          int64_t vlo = 0, vhi = 0;
-          if (MN) vlo = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, N[s])) : vd[N[s]];
-          if (MX) vhi = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, X[s])) : vd[X[s]];
-          oplane[2 * ocap + o] = static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull;
-          oplane[3 * ocap + o] = static_cast<uint64_t>(vhi) ^ 0x8000000000000000ull;
-        } else {
-          lost = true;
-        }
-        ++o;
-      }
-      K[s] = kNAEmpty;
-      S[s] = 0ull;
-      if (MN) N[s] = 0xFFFFFFFFu;
-      if (MX) X[s] = 0u;
-    }
+    fexcl = incl - mine;
+    fbase = 0ull;
+    if (lane == 0 && tot) fbase = atomicAdd(ctr, static_cast<unsigned long long>(tot));
+    fp = pp;
   };
 
-  uint32_t cur[16], nxt[16];
-  int p = blockIdx.x * kNAWaves + wave;
-  uint32_t n = p < nparts ? min(cnt2[p], static_cast<unsigned int>(cap2)) : 0u;
-  uint32_t i0 = 0;
-  if (p < nparts) load(p, 0u, n, cur);
-  while (p < nparts) {
-    int np = p;
-    uint32_t ni0 = i0 + 1024u, nn = n;
-    if (ni0 >= n) {
-      np = p + nw;
-      ni0 = 0u;
-      nn = np < nparts ? min(cnt2[np], static_cast<unsigned int>(cap2)) : 0u;
-    }
-    if (np < nparts) load(np, ni0, nn, nxt);
+  // three batches of 1024 records in registers: the one being aggregated and the next two, loaded ahead
+  struct Pos {
+    int p;
+    uint32_t i0, n;
+  };
+  auto count = [&](int pp) { return pp < nparts ? min(cnt2[pp], static_cast<unsigned int>(cap2)) : 0u; };
+  auto advance = [&](Pos a) -> Pos {
+    if (a.i0 + 1024u < a.n) return Pos{a.p, a.i0 + 1024u, a.n};
+    const int np = a.p + nw;
+    return Pos{np, 0u, count(np)};
+  };
+  uint32_t b0[16], b1[16], b2[16];
+  Pos c{static_cast<int>(blockIdx.x) * kNAWaves + wave, 0u, 0u};
+  c.n = count(c.p);
+  if (c.p < nparts) load(c.p, c.i0, c.n, b0);
+  Pos d = advance(c);
+  if (d.p < nparts) load(d.p, d.i0, d.n, b1);
+  while (c.p < nparts) {
+    const Pos e = advance(d);
+    if (e.p < nparts) load(e.p, e.i0, e.n, b2);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {  // two halves of 8 records: home buckets and values read back to back
       na_u32x4 kb[8];
@@ -342,7 +369,7 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int jj = h * 8 + j;
-        const uint32_t R = cur[jj];
+        const uint32_t R = b0[jj];
         const uint32_t r2 = R & rmask;
         const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2);
         kb[j] = *reinterpret_cast<const na_u32x4*>(K + b * kNAWays);
@@ -351,30 +378,36 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int jj = h * 8 + j;
-        const uint32_t e = static_cast<uint32_t>((jj >> 2) * 256 + lane * 4 + (jj & 3));
-        if (i0 + e >= n) continue;
-        const uint32_t R = cur[jj];
+        const uint32_t ei = static_cast<uint32_t>((jj >> 2) * 256 + lane * 4 + (jj & 3));
+        if (c.i0 + ei >= c.n) continue;
+        const uint32_t R = b0[jj];
         const uint32_t r2 = R & rmask;
-        const uint32_t d = rb2 >= 32 ? 0u : R >> rb2;
+        const uint32_t dd = rb2 >= 32 ? 0u : R >> rb2;
         const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2);
         const int m = na_way(kb[j], r2);
-        int slot = m >= 0 ? static_cast<int>(b) * kNAWays + m : probe(r2, b);
+        const int slot = m >= 0 ? static_cast<int>(b) * kNAWays + m : probe(r2, b);
         if (slot < 0) {
           lost = true;
           continue;
         }
         atomicAdd(&S[slot], SUM ? one + val[j] : one);
-        if (MN) atomicMin(&N[slot], d);
-        if (MX) atomicMax(&X[slot], d);
+        if (MN) atomicMin(&N[slot], dd);
+        if (MX) atomicMax(&X[slot], dd);
       }
     }
-    if (ni0 == 0u) flush(p);
+    if (d.p != c.p) {  // partition c.p is complete
+      flush_end();
+      flush_begin(c.p);
+    }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) cur[j] = nxt[j];
-    p = np;
-    i0 = ni0;
-    n = nn;
+    for (int j = 0; j < 16; ++j) {
+      b0[j] = b1[j];
+      b1[j] = b2[j];
+    }
+    c = d;
+    d = e;
   }
+  flush_end();
   if (lost) atomicAdd(ctr + 3, 1ull);
 }
 
