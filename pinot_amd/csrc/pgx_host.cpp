@@ -3068,6 +3068,12 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     if (P.part_narrow) {  // the narrow split stages a whole sub-step (T * R records): 32 records per bucket at T = 512
       J.T = 512;
       if (const char* e = std::getenv("PGX_NARROW_T")) J.T = std::atoi(e) == 1024 ? 1024 : (std::atoi(e) == 256 ? 256 : 512);
+      if (const char* e = std::getenv("PGX_NARROW_R"))  // A/B: rows per lane (8: fractional loads of odd widths)
+        if (std::atoi(e) == 8 && J.R > 8) {
+          J.R = 8;
+          for (JitCol& C : J.cols) C.frac = C.decode && (8 * C.bits) % 32 != 0;
+        }
+      if (const char* e = std::getenv("PGX_NARROW_TL")) J.TL = std::max(J.R, std::min(32, std::atoi(e)));
     }
     for (int l = 0; l < nleaves; ++l) {
       J.leaf_col.push_back(K.leaf_col[l]);
@@ -3150,7 +3156,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     G.fn = jit_function(J, ctx->device, &lds_bytes, &err);
     if (!G.fn) fail(PGX_ERR_INTERNAL, "query kernel compile: " + err);
     // per-segment arguments
-    const int64_t tile_rows = int64_t(J.T) * 32;
+    const int64_t tile_rows = int64_t(J.T) * J.TL;
     int64_t tiles = 0;
     for (int s : members) {
       const KSeg& S = P.ksegs[s];

@@ -249,6 +249,7 @@ struct JitCol {
 struct JitShape {
   int T = 256;           // threads per workgroup
   int R = 8;             // rows per lane per sub-step (R * bits % 32 == 0 for every decoded column without frac)
+  int TL = 32;           // rows per lane per tile (a multiple of R): the rows whose raw words are loaded one tile ahead
   std::vector<JitCol> cols;
   std::vector<int> leaf_col, leaf_mode;   // leaf_col -1: doc-range leaf with no column (star-tree node ranges)
   std::vector<int> prog_op, prog_arg;

@@ -90,7 +90,7 @@ std::string img_value(const JitShape& s, int c, const std::vector<int>& img_off,
 
 std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const int ncols = int(s.cols.size());
-  const int U = 32 / s.R;
+  const int U = s.TL / s.R;
   const bool emit = s.group_mode == G_EMIT;
   const bool grouped = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL || emit;
   // ---- LDS layout: images, then the dense group table ----
@@ -193,6 +193,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.o << kAbiSrc << "\n" << kDevSrc << "\n";
   e.ln("#define PT ", s.T);
   e.ln("#define PR ", s.R);
+  e.ln("#define PTL ", s.TL);
   e.ln("extern \"C\" __global__ void __launch_bounds__(PT) pgxq(const JArgs A) {");
   e.ind = 1;
   if (lds > 0) {
@@ -334,7 +335,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       case LEAF_RANGES:
         e.ln("const PGX_G int* __restrict__ rg", l, " = (const PGX_G int*)S->lranges[", l, "];");
         e.ln("const int nr", l, " = S->lnr[", l, "];");
-        e.ln("int cur", l, " = pgx_ranges_seek(rg", l, ", nr", l, ", (int)((tl ? (long long)tl[t - tile0] : (t - tile0)) * (PT * 32)));");
+        e.ln("int cur", l, " = pgx_ranges_seek(rg", l, ", nr", l, ", (int)((tl ? (long long)tl[t - tile0] : (t - tile0)) * (PT * PTL)));");
         break;
       default:
         break;
@@ -431,8 +432,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   auto emit_loads = [&](const std::string& tile, const std::string& dst) {
     e.ln("{");
     e.ind++;
-    e.ln("const int rb = (int)((tl ? (long long)tl[", tile, " - tile0] : (", tile, " - tile0)) * (PT * 32));");
-    e.ln("const bool full = rb + PT * 32 <= nd;");
+    e.ln("const int rb = (int)((tl ? (long long)tl[", tile, " - tile0] : (", tile, " - tile0)) * (PT * PTL));");
+    e.ln("const bool full = rb + PT * PTL <= nd;");
     for (int u = 0; u < U; ++u) {
       e.ln("{");
       e.ind++;
@@ -479,9 +480,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     }
   e.ln("if (tt + 1 < t2) ");
   emit_loads("tt + 1", "n");
-  e.ln("const int rb = (int)((tl ? (long long)tl[tt - tile0] : (tt - tile0)) * (PT * 32));");
+  e.ln("const int rb = (int)((tl ? (long long)tl[tt - tile0] : (tt - tile0)) * (PT * PTL));");
   if (scr_off >= 0) {
-    // a tile (PT * 32 rows) lies inside one 65536-doc chunk: build that chunk's program masks when it changes (the next
+    // a tile (PT * PTL rows) lies inside one 65536-doc chunk: build that chunk's program masks when it changes (the next
     // tile's forward-index loads are already in flight)
     e.ln("if ((rb >> 16) != rc_cur) {");
     e.ln("  rc_cur = rb >> 16;");
@@ -973,7 +974,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   }
   e.ind = 3;
   e.ln("};");
-  e.ln("if (rb + PT * 32 <= nd) body(pgx_bool<true>{}); else body(pgx_bool<false>{});");
+  e.ln("if (rb + PT * PTL <= nd) body(pgx_bool<true>{}); else body(pgx_bool<false>{});");
   e.ind = 2;
   e.ln("}");
   // per-segment flush of the lane accumulators (values depend on this segment's dictionaries)
@@ -1101,7 +1102,7 @@ std::map<std::pair<int, std::string>, JitEntry> g_jit_cache;
 // Every field of a shape that the generated source depends on, flattened: the per-query lookup key (generating the
 // source text to find a cached kernel cost ~14 us per query).
 std::vector<int64_t> shape_key(const JitShape& s, int device) {
-  std::vector<int64_t> k{device, s.T, s.R, s.group_mode, int64_t(s.dense_slots), s.num_planes, s.keybits, s.emit_col,
+  std::vector<int64_t> k{device, s.T, s.R, s.TL, s.group_mode, int64_t(s.dense_slots), s.num_planes, s.keybits, s.emit_col,
                          int64_t(s.cols.size()), s.leafmask};
   for (const JitCol& c : s.cols)
     k.insert(k.end(), {c.bits, c.decode, c.img, c.img_sh, c.img_words, c.acc32, c.fp, c.remap, c.frac});
@@ -1520,7 +1521,18 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.part_narrow = true;
     s.narrow_vbits = 16;
     shapes.push_back(s);
-    s.emit_col = -1;             // COUNT only: 26-bit records, one u32 array
+    {  // eight rows per lane (fractional loads of the 14-bit column), 1024 threads: the same records per sub-step
+      JitShape t = s;
+      t.R = 8;
+      t.T = 1024;
+      for (JitCol& C : t.cols) C.frac = C.decode && (8 * C.bits) % 32 != 0;
+      shapes.push_back(t);
+      t.TL = 16;  // half tiles: half the raw words in flight per lane
+      shapes.push_back(t);
+      t.T = 512;
+      shapes.push_back(t);
+    }
+    s.emit_col = -1;            // COUNT only: 26-bit records, one u32 array
     s.narrow_vbits = 0;
     shapes.push_back(s);
   }

@@ -172,17 +172,26 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restric
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+  // Once `ties` threshold groups are taken the rest are dropped without touching the tie cursor: a MIN threshold can
+  // tie millions of groups, and one atomic per wave on one address then costs more than the whole pass.  The cursor
+  // is read first (a stale value only costs an atomic) and a wave that saw it full stops reading it.
+  bool ties_full = ties <= 0;
   for (int64_t b = static_cast<int64_t>(blockIdx.x) * 256 + (threadIdx.x & ~63); b < n; b += stride) {
     const int64_t i = b + lane;
     const bool valid = i < n;
     const uint64_t key = valid ? trim_key(pl, ocap, i, kind) : 0ull;
     const bool eq = valid && key == thr;
     const unsigned long long em = __ballot(eq);
-    long long tbase = 0;
-    if (em) {
-      if (lane == __ffsll(static_cast<long long>(em)) - 1)
-        tbase = static_cast<long long>(atomicAdd(&st->n_tie, static_cast<unsigned long long>(__popcll(em))));
-      tbase = __shfl(tbase, __ffsll(static_cast<long long>(em)) - 1, 64);
+    long long tbase = ties;
+    if (em && !ties_full) {
+      const int ld = __ffsll(static_cast<long long>(em)) - 1;
+      if (lane == ld) {
+        const unsigned long long seen = __hip_atomic_load(&st->n_tie, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (seen < static_cast<unsigned long long>(ties))
+          tbase = static_cast<long long>(atomicAdd(&st->n_tie, static_cast<unsigned long long>(__popcll(em))));
+      }
+      tbase = __shfl(tbase, ld, 64);
+      ties_full = tbase + __popcll(em) >= ties;
     }
     const bool take = (valid && key > thr) || (eq && tbase + __popcll(em & below) < ties);
     const unsigned long long tm = __ballot(take);
