@@ -155,13 +155,19 @@ __global__ void pgx_trim_step(TrimState* __restrict__ sts) {
   for (int b = 0; b < 256; ++b) st->hist[b] = 0u;
 }
 
-// Function slot y writes its selection to idx / keys + y * cap.  Cursor reservations are wave-aggregated (one atomic
-// per wave and kind): at a MIN threshold tens of thousands of groups can tie, and per-lane atomics on one address
-// serialise.
+// Function slot y writes its selection to idx / keys + y * cap.  A workgroup scans one contiguous range of groups.
+// Groups above the threshold key are taken at once (wave-aggregated reservations: at most k of them exist).  Threshold
+// ties are listed in the workgroup's LDS and reserved with ONE atomic per workgroup at the end: a MIN or MAX threshold
+// can tie tens of thousands of groups, and one device-scope atomic per wave on one address serialises at ~11 ns each.
+// A workgroup whose range holds more than kTieCap ties reserves the rest per wave as it finds them.
+constexpr int kTieCap = 2048;
 __global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restrict__ oplane, int64_t ocap, int64_t n,
                                                        const TrimKinds K, TrimState* __restrict__ sts,
                                                        int64_t* __restrict__ idx, uint64_t* __restrict__ keys,
                                                        int64_t cap) {
+  __shared__ uint32_t tbuf[kTieCap];
+  __shared__ unsigned int tcnt;
+  __shared__ long long ttake, tsel;
   TrimState* st = sts + blockIdx.y;
   const int kind = K.kind[blockIdx.y];
   idx += static_cast<int64_t>(blockIdx.y) * cap;
@@ -171,41 +177,64 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restric
   const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)oplane;
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
-  const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
-  // Once `ties` threshold groups are taken the rest are dropped without touching the tie cursor: a MIN threshold can
-  // tie millions of groups, and one atomic per wave on one address then costs more than the whole pass.  The cursor
-  // is read first (a stale value only costs an atomic) and a wave that saw it full stops reading it.
-  bool ties_full = ties <= 0;
-  for (int64_t b = static_cast<int64_t>(blockIdx.x) * 256 + (threadIdx.x & ~63); b < n; b += stride) {
+  const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * chunk;
+  const int64_t hi = lo + chunk < n ? lo + chunk : n;
+  if (threadIdx.x == 0) tcnt = 0u;
+  __syncthreads();
+  // wave-aggregated reservation of `mask` lanes on cursor c; returns this lane's slot
+  auto reserve = [&](unsigned long long* c, unsigned long long mask) -> unsigned long long {
+    const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(c, static_cast<unsigned long long>(__popcll(mask)));
+    return __shfl(base, leader, 64) + __popcll(mask & below);
+  };
+  for (int64_t b = lo + (threadIdx.x & ~63); b < hi; b += 256) {
     const int64_t i = b + lane;
-    const bool valid = i < n;
+    const bool valid = i < hi;
     const uint64_t key = valid ? trim_key(pl, ocap, i, kind) : 0ull;
     const bool eq = valid && key == thr;
     const unsigned long long em = __ballot(eq);
-    long long tbase = ties;
-    if (em && !ties_full) {
+    bool take = valid && key > thr;
+    if (em) {
       const int ld = __ffsll(static_cast<long long>(em)) - 1;
-      if (lane == ld) {
-        const unsigned long long seen = __hip_atomic_load(&st->n_tie, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (seen < static_cast<unsigned long long>(ties))
-          tbase = static_cast<long long>(atomicAdd(&st->n_tie, static_cast<unsigned long long>(__popcll(em))));
+      unsigned int r0 = 0u;
+      if (lane == ld) r0 = atomicAdd(&tcnt, static_cast<unsigned int>(__popcll(em)));
+      const unsigned int r = __shfl(r0, ld, 64) + static_cast<unsigned int>(__popcll(em & below));
+      if (eq && r < static_cast<unsigned int>(kTieCap)) tbuf[r] = static_cast<uint32_t>(i - lo);
+      const unsigned long long om = __ballot(eq && r >= static_cast<unsigned int>(kTieCap));
+      if (om) {  // LDS list full: this wave reserves its overflowing ties itself
+        const unsigned long long t = reserve(&st->n_tie, om);
+        take = take || (eq && r >= static_cast<unsigned int>(kTieCap) && static_cast<long long>(t) < ties);
       }
-      tbase = __shfl(tbase, ld, 64);
-      ties_full = tbase + __popcll(em) >= ties;
     }
-    const bool take = (valid && key > thr) || (eq && tbase + __popcll(em & below) < ties);
     const unsigned long long tm = __ballot(take);
     if (!tm) continue;
-    unsigned long long sbase = 0;
-    const int leader = __ffsll(static_cast<long long>(tm)) - 1;
-    if (lane == leader) sbase = atomicAdd(&st->n_sel, static_cast<unsigned long long>(__popcll(tm)));
-    sbase = __shfl(sbase, leader, 64);
-    if (take) {
-      const unsigned long long p = sbase + __popcll(tm & below);
-      if (p < static_cast<unsigned long long>(cap)) {
-        idx[p] = i;
-        keys[p] = key;
-      }
+    const unsigned long long p = reserve(&st->n_sel, tm);
+    if (take && p < static_cast<unsigned long long>(cap)) {
+      idx[p] = i;
+      keys[p] = key;
+    }
+  }
+  __syncthreads();
+  const unsigned int nt = tcnt < static_cast<unsigned int>(kTieCap) ? tcnt : static_cast<unsigned int>(kTieCap);
+  if (threadIdx.x == 0) {
+    long long tk = 0, sb = 0;
+    if (nt) {
+      const long long t0 = static_cast<long long>(atomicAdd(&st->n_tie, static_cast<unsigned long long>(nt)));
+      tk = ties - t0;
+      tk = tk < 0 ? 0 : (tk > nt ? nt : tk);
+      if (tk) sb = static_cast<long long>(atomicAdd(&st->n_sel, static_cast<unsigned long long>(tk)));
+    }
+    ttake = tk;
+    tsel = sb;
+  }
+  __syncthreads();
+  for (long long j = threadIdx.x; j < ttake; j += 256) {
+    const long long p = tsel + j;
+    if (p < cap) {
+      idx[p] = lo + tbuf[j];
+      keys[p] = thr;
     }
   }
 }
