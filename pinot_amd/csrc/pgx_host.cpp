@@ -3065,15 +3065,21 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     J.T = lds <= 20 * 1024 ? 256 : (lds <= 40 * 1024 ? 512 : 1024);
     if (P.rchunk) J.T = 512;  // three 512-thread workgroups per CU, four tiles per chunk
     if (P.use_part) J.T = std::min(J.T, 512);  // record-emitting kernels hold R 64-bit records per lane: 256 VGPRs
-    if (P.part_narrow) {  // the narrow split stages a whole sub-step (T * R records): 32 records per bucket at T = 512
+    if (P.part_narrow) {
+      // the narrow split's LDS rings (pgx_jit.cpp) want ~16 records per bucket per sub-step (T * R = 4096: a ring of
+      // 64 holds the unflushed unit plus the sub-step's records with a wide margin): 512 threads, eight rows per lane
+      // (fractional loads of widths that need it), half tiles (16 rows per lane) so the raw words of the next tile stay
+      // in registers without spilling.  PGX_NARROW_T / _R / _TL: A/B knobs.
       J.T = 512;
+      int nr = 8, ntl = 16;
       if (const char* e = std::getenv("PGX_NARROW_T")) J.T = std::atoi(e) == 1024 ? 1024 : (std::atoi(e) == 256 ? 256 : 512);
-      if (const char* e = std::getenv("PGX_NARROW_R"))  // A/B: rows per lane (8: fractional loads of odd widths)
-        if (std::atoi(e) == 8 && J.R > 8) {
-          J.R = 8;
-          for (JitCol& C : J.cols) C.frac = C.decode && (8 * C.bits) % 32 != 0;
-        }
-      if (const char* e = std::getenv("PGX_NARROW_TL")) J.TL = std::max(J.R, std::min(32, std::atoi(e)));
+      if (const char* e = std::getenv("PGX_NARROW_R")) nr = std::atoi(e) == 16 ? 16 : 8;
+      if (const char* e = std::getenv("PGX_NARROW_TL")) ntl = std::atoi(e) == 32 ? 32 : 16;
+      if (nr < J.R) {
+        J.R = nr;
+        for (JitCol& C : J.cols) C.frac = C.decode && (nr * C.bits) % 32 != 0;
+      }
+      J.TL = std::max(J.R, ntl);
     }
     for (int l = 0; l < nleaves; ++l) {
       J.leaf_col.push_back(K.leaf_col[l]);
@@ -3662,9 +3668,11 @@ struct NarrowBuffers {
   DevBuf lo1, hi1, cnt1, rec2, cnt2, okey, oplane, ctr;  // ctr: ocount | overflow scan | split | aggregation
 };
 
-int64_t narrow_cap(double m, int64_t slack) {  // mean + 8 sigma (binomial, p small) + slack, a multiple of 4
+// mean + 8 sigma (binomial, p small) + slack, a multiple of 32: slabs then start on 128-byte lines (u32 records) and
+// 64-byte lines (u16), so the scan's whole 32-record units are whole lines
+int64_t narrow_cap(double m, int64_t slack) {
   const int64_t c = int64_t(m + 8.0 * std::sqrt(std::max(m, 1.0))) + slack;
-  return (c + 3) & ~int64_t(3);
+  return (c + 31) & ~int64_t(31);
 }
 
 bool narrow_size(const ExecPlan& P, NarrowBuffers& NB) {

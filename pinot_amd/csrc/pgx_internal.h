@@ -214,6 +214,7 @@ constexpr int kLdsBudget = 160 * 1024 - 256;  // static LDS of one workgroup, mi
 constexpr uint64_t kNarrowC1 = 0x9E3779B97F4A7C15ull;
 constexpr uint64_t kNarrowC2 = 0xC2B2AE3D27D4EB4Full;
 constexpr int kNarrow1Bits = 8;      // first split (inside the scan): 256 buckets
+constexpr int kNarrowRing = 64;      // scan: per-bucket LDS ring of records (two 32-record units)
 constexpr int kNarrowMaxBits2 = 10;  // second split (pgx_narrow_split): up to 1024 sub-buckets per bucket
 struct NarrowMix {
   uint64_t mask = 0, c1 = kNarrowC1, c2 = kNarrowC2, ic1 = 0, ic2 = 0;

@@ -117,26 +117,28 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // with part_slab this workgroup's own slab of each bucket (an LDS cursor: no global round trip per sub-step)
   const bool epart = emit && s.part_bits > 0;
   const bool eslab = epart && s.part_slab;
-  // narrow records (slab mode only): staged as a u32 array, a u16 array (records wider than 32 bits) and the bucket of
-  // every staged record (u8), instead of 8-byte records
+  // narrow records (slab mode only): a u32 array and a u16 array (records wider than 32 bits), written through
+  // per-bucket LDS rings so that only whole 32-record units leave (128-B u32 / 64-B u16 lines, see the sub-step below)
   const bool enarrow = eslab && s.part_narrow;
   const int nrb1 = s.keybits - s.part_bits;  // narrow: bits of the key's mix left in the record
   const bool nhib = enarrow && nrb1 + s.narrow_vbits > 32;
   const int pnb = 1 << s.part_bits;
-  int pst_off = -1, phist_off = -1, pstb_off = -1, pstk_off = -1;
-  if (epart) {
+  // (narrow: pnb = 256 and T a multiple of 256 -- plan_jit's choices; four owner wavefronts hold one bucket per lane)
+  int pst_off = -1, phist_off = -1, nring_off = -1, nringb_off = -1, nst_off = -1;
+  if (enarrow) {
+    nring_off = lds;
+    lds += pnb * kNarrowRing * 4;
+    nringb_off = lds;
+    if (nhib) lds += pnb * kNarrowRing * 2;
+    // cursors[256], unflushed-unit starts[2][256], ring-valid-from[2][256], unit lists (u16 bucket, u32 position)
+    // [4][128] each, list counts[4]
+    nst_off = lds;
+    lds += pnb * 4 * 5 + 4 * 128 * 2 + 4 * 128 * 4 + 16;
+  } else if (epart) {
     pst_off = lds;
-    if (enarrow) {
-      lds += s.T * s.R * 4;
-      pstb_off = lds;
-      if (nhib) lds += s.T * s.R * 2;
-      pstk_off = lds;
-      lds += (s.T * s.R + 15) / 16 * 16;
-    } else {
-      lds += s.T * s.R * 8;
-    }
+    lds += s.T * s.R * 8;
     phist_off = lds;
-    // hist (u32), offs (u32), gpos (u64), total[, slab fill (u32) | narrow: the second hist buffer]
+    // hist (u32), offs (u32), gpos (u64), total[, slab fill (u32)]
     lds += pnb * 16 + 16 + (eslab ? pnb * 4 : 0);
   }
   if (emit && !epart) {
@@ -240,14 +242,23 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   if (s.group_mode == G_DENSE_GLOBAL) e.ln("u64* const tab = A.table;");
   if (scr_off >= 0) e.ln("PgxRScratch& rscr = *(PgxRScratch*)(lds + ", scr_off / 4, ");");
   if (compact) e.ln("u32* const cstg = lds + ", cst_off / 4, " + (tid >> 6) * ", 64 * std::max<size_t>(1, ccols.size()), ";");
-  if (epart) {
-    if (enarrow) {
-      e.ln("u32* const pstA = lds + ", pst_off / 4, ";");
-      if (nhib) e.ln("unsigned short* const pstB = (unsigned short*)(lds + ", pstb_off / 4, ");");
-      e.ln("unsigned char* const pstK = (unsigned char*)(lds + ", pstk_off / 4, ");");
-    } else {
-      e.ln("u64* const pstage = (u64*)(lds + ", pst_off / 4, ");");
-    }
+  if (enarrow) {
+    e.ln("u32* const ringA = lds + ", nring_off / 4, ";");
+    if (nhib) e.ln("unsigned short* const ringB = (unsigned short*)(lds + ", nringb_off / 4, ");");
+    e.ln("u32* const ncur = lds + ", nst_off / 4, ";");
+    e.ln("u32* const nU = ncur + 256;");
+    e.ln("u32* const nV = ncur + 768;");
+    e.ln("unsigned short* const nlb = (unsigned short*)(ncur + 1280);");
+    e.ln("u32* const nlp = ncur + 1536;");
+    e.ln("u32* const nlc = ncur + 2048;");
+    e.ln("for (int i = tid; i < 1280; i += PT) ncur[i] = 0u;");
+    e.ln("int npar = 0;");
+    e.ln("PGX_G u32* const poutA = (PGX_G u32*)A.table;");
+    if (nhib) e.ln("PGX_G unsigned short* const poutB = (PGX_G unsigned short*)A.part_hi;");
+    e.ln("const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
+    e.ln("__syncthreads();");
+  } else if (epart) {
+    e.ln("u64* const pstage = (u64*)(lds + ", pst_off / 4, ");");
     e.ln("u32* const phist = lds + ", phist_off / 4, ";");
     e.ln("u32* const poffs = phist + ", pnb, ";");
     e.ln("u64* const pgpos = (u64*)(phist + ", 2 * pnb, ");");
@@ -255,10 +266,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     if (eslab) e.ln("u32* const pfill = phist + ", 4 * pnb + 4, ";");
     e.ln("for (int i = tid; i < ", pnb, "; i += PT) phist[i] = 0u;");
     if (eslab) e.ln("for (int i = tid; i < ", pnb, "; i += PT) pfill[i] = 0u;");
-    if (enarrow) {  // the second histogram buffer sits where slab mode keeps pfill; fills live in registers
-      e.ln("u32 nfill[", std::max(1, pnb / 64), "] = {};");
-      e.ln("int pbuf = 0;");
-    }
     e.ln("__syncthreads();");
   }
   e.ln("u64 st_docs = 0, st_ent = 0;");
@@ -840,56 +847,73 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("}");
     }
     if (enarrow) {
-      // Narrow split of this sub-step's PT * PR records 2^part_bits ways: LDS histogram (the atomic returns the record's
-      // rank in its bucket), wave 0 scans it and advances this workgroup's slab fills, records are staged bucket-sorted
-      // and leave as per-bucket runs into the workgroup's own slab of each bucket.  Three barriers per sub-step: the
-      // next sub-step's histogram atomics follow the staging reads of this one's copy-out only through its first
-      // barrier, and the histogram was cleared by wave 0 before the second.
+      // Narrow split of this sub-step's records 256 ways through per-bucket LDS rings (software write combining).
+      // Bucket b's records go to this workgroup's slab of b at consecutive positions (an LDS cursor per bucket: the
+      // atomic returns the position); a record is held in the ring slot (position mod kNarrowRing) until its 32-record
+      // unit is complete, and whole units leave as one 128-B u32 line (+ one 64-B u16 line) each, written by 32
+      // consecutive lanes.  Stores of partial units would leave as separate partial-line writes (the L2 does not
+      // merge them across sub-steps).  Per sub-step: positions (atomics) | A | four owner wavefronts (a bucket per
+      // lane) list the units that complete, every lane writes its records into the rings | B | every wavefront
+      // writes listed units.  The ring holds positions [U, U + kNarrowRing) (U: first unflushed unit); a record
+      // beyond that (a key-skewed sub-step) is stored straight to the slab, and the ring's copy of positions below V
+      // (ring-valid-from) is ignored.  Two buffers of U and V: the owners write the next sub-step's while this one's
+      // are read.
+      const std::string NR = std::to_string(kNarrowRing);
       e.ln("{");
-      e.ln("  u32* const ph = pbuf ? pfill : phist;  // this sub-step's histogram buffer");
-      e.ln("  u32 rk[PR];");
+      e.ln("  u32 pp[PR];");
       e.ln("  #pragma unroll");
-      e.ln("  for (int j = 0; j < PR; ++j) rk[j] = recs[j] != ~0ull ? atomicAdd(&ph[(u32)(recs[j] >> 56)], 1u) : 0u;");
+      e.ln("  for (int j = 0; j < PR; ++j) pp[j] = recs[j] != ~0ull ? atomicAdd(&ncur[(u32)(recs[j] >> 56)], 1u) : 0u;");
       e.ln("  pgx_lds_barrier();");
-      e.ln("  const int tot = (int)pgx_narrow_scan2<", pnb, ">(ph, poffs, (u32*)pgpos, nfill, pbuf ? phist : pfill, tid);");
-      e.ln("  pbuf ^= 1;");
+      e.ln("  const u32* const Ucur = nU + npar * 256;");
+      e.ln("  const u32* const Vcur = nV + npar * 256;");
+      e.ln("  if (tid < 256) {");
+      e.ln("    const u32 en = ncur[tid], u0 = Ucur[tid], v0 = Vcur[tid];");
+      e.ln("    const u32 lim = u0 + ", NR, "u;");
+      e.ln("    const u32 nu = (((en < lim) ? en : lim) - u0) >> 5;");
+      e.ln("    nU[(npar ^ 1) * 256 + tid] = en & ~31u;");
+      e.ln("    nV[(npar ^ 1) * 256 + tid] = en > lim ? en : v0;");
+      e.ln("    u32 incl = nu;");
+      e.ln("    #pragma unroll");
+      e.ln("    for (int d = 1; d < 64; d <<= 1) {");
+      e.ln("      const u32 y = __shfl_up(incl, d, 64);");
+      e.ln("      if (lane >= d) incl += y;");
+      e.ln("    }");
+      e.ln("    const int w = tid >> 6;");
+      e.ln("    for (u32 q = 0, k = incl - nu; q < nu; ++q, ++k) {");
+      e.ln("      nlb[w * 128 + k] = (unsigned short)tid;");
+      e.ln("      nlp[w * 128 + k] = u0 + 32u * q;");
+      e.ln("    }");
+      e.ln("    if (lane == 63) nlc[w] = incl;");
+      e.ln("  }");
       e.ln("  #pragma unroll");
       e.ln("  for (int j = 0; j < PR; ++j)");
       e.ln("    if (recs[j] != ~0ull) {");
       e.ln("      const u32 b = (u32)(recs[j] >> 56);");
-      e.ln("      const u32 q = poffs[b] + rk[j];");
-      e.ln("      pstA[q] = (u32)recs[j];");
-      if (nhib) e.ln("      pstB[q] = (unsigned short)(recs[j] >> 32);");
-      e.ln("      pstK[q] = (unsigned char)b;");
+      e.ln("      const u32 pos = pp[j];");
+      e.ln("      if (pos < Ucur[b] + ", NR, "u) {");
+      e.ln("        ringA[b * ", NR, "u + (pos & ", kNarrowRing - 1, "u)] = (u32)recs[j];");
+      if (nhib) e.ln("        ringB[b * ", NR, "u + (pos & ", kNarrowRing - 1, "u)] = (unsigned short)(recs[j] >> 32);");
+      e.ln("      } else if (pos < (u32)A.part_cap) {  // past the ring (key skew): straight to the slab");
+      e.ln("        const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)pos;");
+      e.ln("        poutA[o] = (u32)recs[j];");
+      if (nhib) e.ln("        poutB[o] = (unsigned short)(recs[j] >> 32);");
+      e.ln("      }");
       e.ln("    }");
       e.ln("  pgx_lds_barrier();");
-      e.ln("  PGX_G u32* const poutA = (PGX_G u32*)A.table;");
-      if (nhib) e.ln("  PGX_G unsigned short* const poutB = (PGX_G unsigned short*)A.part_hi;");
-      e.ln("  const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
-      // copy-out in halves of PR / 2 records per thread: every LDS read of a half issued before its stores
-      e.ln("  #pragma unroll");
-      e.ln("  for (int hh = 0; hh < 2; ++hh) {");
-      e.ln("    u32 cb[PR / 2], ca[PR / 2];");
-      if (nhib) e.ln("    u32 cbh[PR / 2];");
-      e.ln("    #pragma unroll");
-      e.ln("    for (int k = 0; k < PR / 2; ++k) {");
-      e.ln("      const int i = (hh * (PR / 2) + k) * PT + tid;");
-      e.ln("      cb[k] = i < tot ? (u32)pstK[i] : 0u;");
-      e.ln("      ca[k] = i < tot ? pstA[i] : 0u;");
-      if (nhib) e.ln("      cbh[k] = i < tot ? (u32)pstB[i] : 0u;");
-      e.ln("    }");
-      e.ln("    #pragma unroll");
-      e.ln("    for (int k = 0; k < PR / 2; ++k) {");
-      e.ln("      const int i = (hh * (PR / 2) + k) * PT + tid;");
-      e.ln("      if (i >= tot) continue;");
-      e.ln("      const u32 pos = ((const u32*)pgpos)[cb[k]] + (u32)(i - (int)poffs[cb[k]]);");
-      e.ln("      if (pos < (u32)A.part_cap) {");
-      e.ln("        const long long o = ((long long)cb[k] * A.part_nwg + wsl) * A.part_cap + (long long)pos;");
-      e.ln("        poutA[o] = ca[k];");
-      if (nhib) e.ln("        poutB[o] = (unsigned short)cbh[k];");
+      e.ln("  {");
+      e.ln("    const int w = tid >> 6, l = w & 3;");
+      e.ln("    const int cnt = (int)nlc[l];");
+      e.ln("    for (int k = (w >> 2) * 2 + (lane >> 5); k < cnt; k += 2 * (PT / 256)) {");
+      e.ln("      const u32 b = nlb[l * 128 + k];");
+      e.ln("      const u32 i = nlp[l * 128 + k] + (u32)(lane & 31);");
+      e.ln("      if (i >= Vcur[b] && i < (u32)A.part_cap) {");
+      e.ln("        const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)i;");
+      e.ln("        poutA[o] = ringA[b * ", NR, "u + (i & ", kNarrowRing - 1, "u)];");
+      if (nhib) e.ln("        poutB[o] = ringB[b * ", NR, "u + (i & ", kNarrowRing - 1, "u)];");
       e.ln("      }");
       e.ln("    }");
       e.ln("  }");
+      e.ln("  npar ^= 1;");
       e.ln("}");
     } else if (epart) {
       const std::string KM = std::to_string((1ull << s.keybits) - 1ull) + "ull";
@@ -1039,16 +1063,21 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("  }");
   e.ln("}");
   e.ln("__syncthreads();");
-  if (enarrow) {  // slab fills from wavefront 0's registers (every wavefront holds the same)
-    e.ln("if ((tid >> 6) == 0) {");
-    e.ln("  #pragma unroll");
-    e.ln("  for (int q = 0; q < ", std::max(1, pnb / 64), "; ++q) {");
-    e.ln("    const int i = q * 64 + lane;");
-    e.ln("    if (i >= ", pnb, ") continue;");
-    e.ln("    const u32 h = nfill[q];");
-    e.ln("    A.part_cursor[((long long)i * A.part_nwg + A.part_wg_base + (long long)blockIdx.x) * A.part_cstride] = h;");
-    e.ln("    if (h > (u32)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
+  if (enarrow) {  // the rings' last partial units, then the slab fills (every record, also past part_cap)
+    const std::string NR = std::to_string(kNarrowRing);
+    e.ln("for (int x = tid; x < 256 * 32; x += PT) {");
+    e.ln("  const u32 b = (u32)x >> 5;");
+    e.ln("  const u32 i = nU[npar * 256 + b] + ((u32)x & 31u);");
+    e.ln("  if (i < ncur[b] && i >= nV[npar * 256 + b] && i < (u32)A.part_cap) {");
+    e.ln("    const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)i;");
+    e.ln("    poutA[o] = ringA[b * ", NR, "u + (i & ", kNarrowRing - 1, "u)];");
+    if (nhib) e.ln("    poutB[o] = ringB[b * ", NR, "u + (i & ", kNarrowRing - 1, "u)];");
     e.ln("  }");
+    e.ln("}");
+    e.ln("for (int i = tid; i < 256; i += PT) {");
+    e.ln("  const u32 h = ncur[i];");
+    e.ln("  A.part_cursor[((long long)i * A.part_nwg + wsl) * A.part_cstride] = h;");
+    e.ln("  if (h > (u32)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
     e.ln("}");
   } else if (eslab) {  // slab fills (every record, also past part_cap: the host resizes from the largest)
     e.ln("for (int i = tid; i < ", pnb, "; i += PT) {");
