@@ -39,20 +39,26 @@ __device__ __forceinline__ void n_lds_barrier() {  // LDS-only ordering: loads i
 // ---------------------------------------------------------------------------------------------------------------------
 constexpr int kN2Threads = 1024;
 constexpr int kN2Waves = kN2Threads / 64;
-constexpr int kN2Per = 16;
-constexpr int kN2Chunk = kN2Threads * kN2Per;  // records per round: 64 KiB of staged u32 records
+constexpr int kN2Per = 8;
+constexpr int kN2Chunk = kN2Threads * kN2Per;  // records per round
 constexpr int kN2MaxSub = 1 << kNarrowMaxBits2;
 constexpr int kN2MaxSlabs = 1024;
+constexpr int kN2RingWords = 32768;             // 128 KiB of LDS rings: 32768 >> k2 records per sub-bucket
+constexpr int kN2Unit = 16;                     // records per unit: one 64-byte line segment
+constexpr int kN2ListCap = kN2Chunk / kN2Unit + kN2MaxSub;  // units that can complete in one round
 
+// Software write combining, as in the scan (pgx_jit.cpp narrow sub-step): sub-bucket s's records take consecutive
+// positions of partition (b << k2 | s) (an LDS cursor per sub-bucket: the atomic returns the position) and wait in the
+// sub-bucket's LDS ring (position mod ring) until their 16-record unit is complete; whole units leave as 64 contiguous
+// bytes written by 16 consecutive lanes.  Partial-unit stores would leave as separate partial-line writes.
 // Rounds walk the bucket's slabs in order: round (w, c0) holds records [c0, c0 + kN2Chunk) of slab w, so a record's
-// address is plain arithmetic (no per-record slab search).  Two barriers per round:
-//   split fields + LDS histogram of this round's buffer (the atomic returns the record's rank in its sub-bucket)
-//   | B1 | every wavefront scans the whole histogram itself (no single-wave phase: the same offsets, the same slab fills
-//   kept in registers by every wavefront, written to LDS redundantly), stages its records sub-bucket-sorted and issues
-//   the next round's loads; wavefront 0 clears the OTHER histogram buffer for the next round
-//   | B2 | copy-out of per-partition runs, the LDS reads of 8 records issued before their stores.
-// The staging, offsets and positions of round r are rewritten only after B1 of round r + 1, which every wavefront
-// passes after its copy-out of round r.
+// address is plain arithmetic; the loads of the next two rounds are in flight.  Per round:
+//   split fields, positions (LDS atomics)
+//   | A | owner lanes (one per sub-bucket) list the units that complete (one LDS atomic per wavefront reserves list
+//   space), every lane writes its records into the rings (a record past its ring -- key skew -- goes straight out)
+//   | B | the listed units are written out, four per wavefront instruction.
+// U (first unflushed position, a unit boundary) and V (ring-valid-from: positions below it were stored straight out)
+// are double-buffered so the owners write the next round's while this round's are read.
 __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* __restrict__ lo,
                                                                const uint16_t* __restrict__ hi,
                                                                const unsigned long long* __restrict__ cnt1, int nwg,
@@ -60,127 +66,148 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
                                                                uint32_t* __restrict__ out, int64_t cap2,
                                                                unsigned int* __restrict__ cnt2,
                                                                unsigned long long* __restrict__ ovf) {
-  __shared__ uint32_t stage[kN2Chunk];
-  __shared__ uint16_t ssub[kN2Chunk];
-  __shared__ uint32_t hist[2][kN2MaxSub], offs[kN2MaxSub], gpos[kN2MaxSub];
-  __shared__ uint32_t scnt[kN2MaxSlabs];
+  __shared__ uint32_t ring[kN2RingWords];
+  __shared__ uint32_t cur[kN2MaxSub], Ub[2][kN2MaxSub], Vb[2][kN2MaxSub];
+  __shared__ uint16_t lsub[kN2ListCap];
+  __shared__ uint32_t lpos[kN2ListCap];
+  __shared__ uint32_t lcnt[2];
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nsub = 1 << k2;
   const int rb2 = rb1 - k2;
+  const int rlog = 15 - k2;
+  const uint32_t rmask = (1u << rlog) - 1u;
   const uint64_t m2 = (uint64_t(1) << rb2) - 1u;
-  constexpr int PER = kN2MaxSub / 64;  // sub-buckets q * 64 + lane of every lane
-  uint32_t fill[PER];
-#pragma unroll
-  for (int q = 0; q < PER; ++q) fill[q] = 0u;
-  for (int i = tid; i < 2 * kN2MaxSub; i += kN2Threads) (&hist[0][0])[i] = 0u;
-  for (int i = tid; i < nwg; i += kN2Threads)
-    scnt[i] = static_cast<uint32_t>(min(cnt1[static_cast<int64_t>(b) * nwg + i], static_cast<unsigned long long>(cap1)));
+  const uint32_t ucap = static_cast<uint32_t>(cap2 < 0xFFFFFFFFll ? cap2 : 0xFFFFFFFFll);
+  for (int i = tid; i < nsub; i += kN2Threads) {
+    cur[i] = 0u;
+    Ub[0][i] = 0u;
+    Vb[0][i] = 0u;
+  }
+  if (tid < 2) lcnt[tid] = 0u;
   __syncthreads();
+  const unsigned long long* const c1 = cnt1 + static_cast<int64_t>(b) * nwg;
+  auto scount = [&](int w) -> uint32_t {  // records of slab w (uniform)
+    const unsigned long long c = c1[w];
+    return static_cast<uint32_t>(c < static_cast<unsigned long long>(cap1) ? c : static_cast<unsigned long long>(cap1));
+  };
   const PGX_GLOBAL uint32_t* glo = (const PGX_GLOBAL uint32_t*)lo + static_cast<int64_t>(b) * nwg * cap1;
   const PGX_GLOBAL uint16_t* ghi = hi ? (const PGX_GLOBAL uint16_t*)hi + static_cast<int64_t>(b) * nwg * cap1 : nullptr;
   PGX_GLOBAL uint32_t* gout = (PGX_GLOBAL uint32_t*)out + static_cast<int64_t>(b) * nsub * cap2;
-  // the first round at or after (w, c0): slabs with no records left are skipped (uniform: every thread walks alike)
-  auto next_round = [&](int& w, uint32_t& c0) {
-    while (w < nwg && c0 >= scnt[w]) {
-      ++w;
-      c0 = 0u;
-    }
+  struct Rd {
+    int w;
+    uint32_t c0, n;
   };
-  uint32_t xl[kN2Per], xh[kN2Per];
-  auto load = [&](int w, uint32_t c0) {
-    const uint32_t n = scnt[w];
-    const PGX_GLOBAL uint32_t* sl = glo + static_cast<int64_t>(w) * cap1;
+  // the round after r (or the first at or after (w, 0)): slabs with no records left are skipped
+  auto advance = [&](Rd r) -> Rd {
+    r.c0 += kN2Chunk;
+    while (r.w < nwg && r.c0 >= r.n) {
+      ++r.w;
+      r.c0 = 0u;
+      r.n = r.w < nwg ? scount(r.w) : 0u;
+    }
+    return r;
+  };
+  auto load = [&](Rd r, uint32_t (&xl)[kN2Per], uint32_t (&xh)[kN2Per]) {
+    const PGX_GLOBAL uint32_t* sl = glo + static_cast<int64_t>(r.w) * cap1;
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k) {
-      const uint32_t pos = c0 + static_cast<uint32_t>(k * kN2Threads + tid);
-      xl[k] = pos < n ? __builtin_nontemporal_load(sl + pos) : 0u;
-      xh[k] = (ghi && pos < n) ? __builtin_nontemporal_load(ghi + static_cast<int64_t>(w) * cap1 + pos) : 0u;
+      const uint32_t pos = r.c0 + static_cast<uint32_t>(k * kN2Threads + tid);
+      xl[k] = pos < r.n ? __builtin_nontemporal_load(sl + pos) : 0u;
+      xh[k] = (ghi && pos < r.n) ? __builtin_nontemporal_load(ghi + static_cast<int64_t>(r.w) * cap1 + pos) : 0u;
     }
   };
-  int w = 0, buf = 0;
-  uint32_t c0 = 0u;
-  next_round(w, c0);
-  if (w < nwg) load(w, c0);
-  while (w < nwg) {
-    const uint32_t n = scnt[w];
-    uint32_t* const H = hist[buf];
-    // split fields of this round; pk = sub-bucket | rank << 16 (a round holds 16384 records), ~0: no record
-    uint32_t r2[kN2Per], pk[kN2Per];
+  uint32_t l0[kN2Per], h0[kN2Per], l1[kN2Per], h1[kN2Per], l2[kN2Per], h2[kN2Per];
+  Rd r0{0, 0u - static_cast<uint32_t>(kN2Chunk), nwg > 0 ? scount(0) : 0u};
+  r0 = advance(r0);
+  if (r0.w < nwg) load(r0, l0, h0);
+  Rd r1 = advance(r0);
+  if (r1.w < nwg) load(r1, l1, h1);
+  int par = 0;
+  while (r0.w < nwg) {
+    const Rd r2n = advance(r1);
+    if (r2n.w < nwg) load(r2n, l2, h2);
+    // split fields and positions
+    uint32_t rec[kN2Per], sbp[kN2Per];  // sbp: sub-bucket | valid << 31
+    uint32_t pp[kN2Per];
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k) {
-      const uint32_t pos = c0 + static_cast<uint32_t>(k * kN2Threads + tid);
-      const uint64_t r1 = static_cast<uint64_t>(xl[k]) | (static_cast<uint64_t>(xh[k]) << 32);
-      r2[k] = static_cast<uint32_t>((r1 & m2) | ((r1 >> rb1) << rb2));
-      pk[k] = 0xFFFFFFFFu;
-      if (pos < n) {
-        const uint32_t sb = static_cast<uint32_t>(r1 >> rb2) & static_cast<uint32_t>(nsub - 1);
-        pk[k] = sb | (atomicAdd(&H[sb], 1u) << 16);
+      const uint32_t pos = r0.c0 + static_cast<uint32_t>(k * kN2Threads + tid);
+      const uint64_t x = static_cast<uint64_t>(l0[k]) | (static_cast<uint64_t>(h0[k]) << 32);
+      rec[k] = static_cast<uint32_t>((x & m2) | ((x >> rb1) << rb2));
+      const uint32_t sb = static_cast<uint32_t>(x >> rb2) & static_cast<uint32_t>(nsub - 1);
+      sbp[k] = pos < r0.n ? (sb | 0x80000000u) : 0u;
+      pp[k] = pos < r0.n ? atomicAdd(&cur[sb], 1u) : 0u;
+    }
+    n_lds_barrier();  // A
+    const uint32_t* const Uc = Ub[par];
+    const uint32_t* const Vc = Vb[par];
+    if (wave * 64 < nsub) {  // owner lanes: sub-bucket tid
+      uint32_t nu = 0u, en = 0u, u0 = 0u, v0 = 0u;
+      if (tid < nsub) {
+        en = cur[tid];
+        u0 = Uc[tid];
+        v0 = Vc[tid];
+        const uint32_t lim = u0 + (1u << rlog);
+        nu = ((en < lim ? en : lim) - u0) / kN2Unit;
+        Ub[par ^ 1][tid] = en & ~static_cast<uint32_t>(kN2Unit - 1);
+        Vb[par ^ 1][tid] = en > lim ? en : v0;
       }
-    }
-    int nw2 = w;
-    uint32_t nc0 = c0 + kN2Chunk;
-    next_round(nw2, nc0);
-    n_lds_barrier();  // B1
-    uint32_t carry = 0;
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int s = q * 64 + lane;
-      const uint32_t h = H[s];
-      uint32_t incl = h;
+      uint32_t incl = nu;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(incl, d, 64);
         if (lane >= d) incl += y;
       }
-      offs[s] = carry + incl - h;
-      gpos[s] = fill[q];
-      fill[q] += h;
-      carry += __shfl(incl, 63, 64);
-    }
-    const uint32_t tot = carry;
-    if (wave == 0)
-      for (int s = lane; s < kN2MaxSub; s += 64) hist[buf ^ 1][s] = 0u;
-#pragma unroll
-    for (int k = 0; k < kN2Per; ++k)
-      if (pk[k] != 0xFFFFFFFFu) {
-        const uint32_t sb = pk[k] & 0xFFFFu;
-        const uint32_t q = offs[sb] + (pk[k] >> 16);
-        stage[q] = r2[k];
-        ssub[q] = static_cast<uint16_t>(sb);
-      }
-    if (nw2 < nwg) load(nw2, nc0);  // the next round's loads overlap this round's copy-out
-    n_lds_barrier();  // B2
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {  // two halves of 8 records (registers: the next round's loads are in flight)
-      uint32_t cs[kN2Per / 2], cv[kN2Per / 2];
-#pragma unroll
-      for (int k = 0; k < kN2Per / 2; ++k) {
-        const uint32_t i = static_cast<uint32_t>((hh * kN2Per / 2 + k) * kN2Threads + tid);
-        cs[k] = i < tot ? ssub[i] : 0u;
-        cv[k] = i < tot ? stage[i] : 0u;
-      }
-#pragma unroll
-      for (int k = 0; k < kN2Per / 2; ++k) {
-        const uint32_t i = static_cast<uint32_t>((hh * kN2Per / 2 + k) * kN2Threads + tid);
-        if (i >= tot) continue;
-        const uint32_t p = gpos[cs[k]] + (i - offs[cs[k]]);
-        if (p < static_cast<uint64_t>(cap2)) gout[static_cast<int64_t>(cs[k]) * cap2 + p] = cv[k];
+      const uint32_t tot = __shfl(incl, 63, 64);
+      uint32_t base = 0u;
+      if (lane == 0 && tot) base = atomicAdd(&lcnt[par], tot);
+      base = __shfl(base, 0, 64);
+      for (uint32_t q = 0, k = base + incl - nu; q < nu; ++q, ++k) {
+        lsub[k] = static_cast<uint16_t>(tid);
+        lpos[k] = u0 + q * kN2Unit;
       }
     }
-    w = nw2;
-    c0 = nc0;
-    buf ^= 1;
+    if (tid == 0) lcnt[par ^ 1] = 0u;  // the next round's list (its reservations follow barrier B)
+#pragma unroll
+    for (int k = 0; k < kN2Per; ++k) {
+      if (!sbp[k]) continue;
+      const uint32_t sb = sbp[k] & 0x7FFFFFFFu;
+      const uint32_t pos = pp[k];
+      if (pos < Uc[sb] + (1u << rlog)) ring[(sb << rlog) + (pos & rmask)] = rec[k];
+      else if (pos < ucap) gout[static_cast<int64_t>(sb) * cap2 + pos] = rec[k];  // past the ring: straight out
+    }
+    n_lds_barrier();  // B
+    {
+      const uint32_t n = lcnt[par];
+      for (uint32_t u = static_cast<uint32_t>(wave * 4 + (lane >> 4)); u < n; u += kN2Waves * 4) {
+        const uint32_t sb = lsub[u];
+        const uint32_t i = lpos[u] + static_cast<uint32_t>(lane & 15);
+        if (i >= Vc[sb] && i < ucap) gout[static_cast<int64_t>(sb) * cap2 + i] = ring[(sb << rlog) + (i & rmask)];
+      }
+    }
+    par ^= 1;
+#pragma unroll
+    for (int k = 0; k < kN2Per; ++k) {
+      l0[k] = l1[k];
+      h0[k] = h1[k];
+      l1[k] = l2[k];
+      h1[k] = h2[k];
+    }
+    r0 = r1;
+    r1 = r2n;
   }
-  // every wavefront holds the same fills: wavefront 0 publishes them
-  if (wave == 0) {
-#pragma unroll
-    for (int q = 0; q < PER; ++q) {
-      const int s = q * 64 + lane;
-      if (s >= nsub) continue;
-      cnt2[static_cast<int64_t>(b) * nsub + s] = fill[q];
-      if (fill[q] > static_cast<uint64_t>(cap2)) atomicAdd(ovf, 1ull);
-    }
+  __syncthreads();
+  // the rings' last partial units, then the partition fills (every record, also past cap2)
+  for (int x = tid; x < nsub * kN2Unit; x += kN2Threads) {
+    const int sb = x / kN2Unit;
+    const uint32_t i = Ub[par][sb] + static_cast<uint32_t>(x % kN2Unit);
+    if (i < cur[sb] && i >= Vb[par][sb] && i < ucap)
+      gout[static_cast<int64_t>(sb) * cap2 + i] = ring[(sb << rlog) + (i & rmask)];
+  }
+  for (int sb = tid; sb < nsub; sb += kN2Threads) {
+    cnt2[static_cast<int64_t>(b) * nsub + sb] = cur[sb];
+    if (cur[sb] > ucap) atomicAdd(ovf, 1ull);
   }
 }
 
