@@ -913,12 +913,12 @@ struct pgx_bindings {
   std::vector<std::vector<uint32_t>> words;  // owned bitsets (arr[i].words points into these)
 };
 
-// pgx_execute_async: the query runs on a host thread of its own (planning, the launches on the context's stream, the
-// read-back); the submitting thread returns at once.  The inputs the caller owns only for the duration of the call (the
-// segment list, the bindings and their bitsets, the options) are copied here first.
+// pgx_execute_async: the query runs on a worker thread of the library's pool (planning, the launches on the context's
+// stream, the read-back); the submitting thread returns at once.  The inputs the caller owns only for the duration of
+// the call (the segment list, the bindings and their bitsets, the options) are copied here first.  The pool's threads
+// live for the whole process (a thread per query cost ~20-40 us of creation and join per query: C1-sized queries).
 struct AsyncState {
-  std::thread th;
-  std::mutex m, join_mu;
+  std::mutex m;
   std::condition_variable cv;
   bool done = false;
   pgx_status status = PGX_OK;
@@ -928,11 +928,47 @@ struct AsyncState {
   std::vector<std::vector<uint32_t>> words;
   pgx_exec_opts opts{};
   bool has_opts = false;
-  void join() {
-    std::lock_guard<std::mutex> g(join_mu);
-    if (th.joinable()) th.join();
+  void join() {  // until the worker has finished with this state
+    std::unique_lock<std::mutex> g(m);
+    cv.wait(g, [&] { return done; });
   }
   ~AsyncState() { join(); }
+};
+
+class AsyncPool {
+ public:
+  static AsyncPool& get() {
+    static AsyncPool* p = new AsyncPool(kThreads);  // never destroyed: workers may be blocked at process exit
+    return *p;
+  }
+  void submit(std::function<void()> f) {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      q_.push_back(std::move(f));
+    }
+    cv_.notify_one();
+  }
+
+ private:
+  static constexpr int kThreads = 8;  // queries in flight per process (bench: 3; one per device under execute_multi)
+  explicit AsyncPool(int n) {
+    for (int i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
+  }
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return !q_.empty(); });
+        f = std::move(q_.front());
+        q_.pop_front();
+      }
+      f();
+    }
+  }
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::deque<std::function<void()>> q_;
 };
 
 struct pgx_result {
@@ -5318,7 +5354,7 @@ pgx_status pgx_execute_async(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
       A.has_opts = true;
     }
     pgx_result* r = R.get();
-    A.th = std::thread([ctx, q, r] {
+    AsyncPool::get().submit([ctx, q, r] {
       AsyncState& S = *r->async;
       const pgx_status st = guarded([&] {
         hip_check(hipSetDevice(ctx->device), "hipSetDevice");

@@ -126,6 +126,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // (narrow: pnb = 256 and T a multiple of 256 -- plan_jit's choices; four owner wavefronts hold one bucket per lane)
   int pst_off = -1, phist_off = -1, nring_off = -1, nringb_off = -1, nst_off = -1;
   if (enarrow) {
+    lds = (lds + 15) & ~15;  // 16-byte ring reads and writes
     nring_off = lds;
     lds += pnb * kNarrowRing * 4;
     nringb_off = lds;
@@ -900,16 +901,28 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("      }");
       e.ln("    }");
       e.ln("  pgx_lds_barrier();");
+      // eight lanes per unit, 16 bytes each (u32: 8 x 4 records; u16: the first 4 lanes x 8 records); a unit
+      // holding positions below V (after a skewed sub-step) goes record by record
       e.ln("  {");
-      e.ln("    const int w = tid >> 6, l = w & 3;");
+      e.ln("    const int w = tid >> 6, l = w & 3, g = lane & 7;");
       e.ln("    const int cnt = (int)nlc[l];");
-      e.ln("    for (int k = (w >> 2) * 2 + (lane >> 5); k < cnt; k += 2 * (PT / 256)) {");
+      e.ln("    for (int k = (w >> 2) * 8 + (lane >> 3); k < cnt; k += 8 * (PT / 256)) {");
       e.ln("      const u32 b = nlb[l * 128 + k];");
-      e.ln("      const u32 i = nlp[l * 128 + k] + (u32)(lane & 31);");
-      e.ln("      if (i >= Vcur[b] && i < (u32)A.part_cap) {");
-      e.ln("        const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)i;");
-      e.ln("        poutA[o] = ringA[b * ", NR, "u + (i & ", kNarrowRing - 1, "u)];");
-      if (nhib) e.ln("        poutB[o] = ringB[b * ", NR, "u + (i & ", kNarrowRing - 1, "u)];");
+      e.ln("      const u32 u = nlp[l * 128 + k];");
+      e.ln("      if (u >= (u32)A.part_cap) continue;");
+      e.ln("      const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)u;");
+      e.ln("      const u32 rs = b * ", NR, "u + (u & ", kNarrowRing - 1, "u);");
+      e.ln("      if (u >= Vcur[b]) {");
+      e.ln("        *(PGX_G pgx_u32x4*)(poutA + o + 4 * g) = *(const pgx_u32x4*)(ringA + rs + 4 * g);");
+      if (nhib)
+        e.ln("        if (g < 4) *(PGX_G pgx_u32x4*)(poutB + o + 8 * g) = *(const pgx_u32x4*)(ringB + rs + 8 * g);");
+      e.ln("      } else {");
+      e.ln("        for (int q = 0; q < 4; ++q) {");
+      e.ln("          const u32 x = 4 * g + q;");
+      e.ln("          if (u + x < Vcur[b]) continue;");
+      e.ln("          poutA[o + x] = ringA[rs + x];");
+      if (nhib) e.ln("          poutB[o + x] = ringB[rs + x];");
+      e.ln("        }");
       e.ln("      }");
       e.ln("    }");
       e.ln("  }");

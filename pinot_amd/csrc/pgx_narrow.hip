@@ -37,6 +37,7 @@ __device__ __forceinline__ void n_lds_barrier() {  // LDS-only ordering: loads i
 // rb1 bits, d: the value's dictId); sub-bucket = r1's top k2 bits; the output record is (r1's low rb1 - k2 bits) |
 // d << (rb1 - k2), appended to partition (b << k2 | sub) at out[part * cap2 + i], its count in cnt2[part].
 // ---------------------------------------------------------------------------------------------------------------------
+typedef unsigned int na_u32x4 __attribute__((ext_vector_type(4)));
 constexpr int kN2Threads = 1024;
 constexpr int kN2Waves = kN2Threads / 64;
 constexpr int kN2Per = 8;
@@ -66,7 +67,7 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
                                                                uint32_t* __restrict__ out, int64_t cap2,
                                                                unsigned int* __restrict__ cnt2,
                                                                unsigned long long* __restrict__ ovf) {
-  __shared__ uint32_t ring[kN2RingWords];
+  __shared__ __attribute__((aligned(16))) uint32_t ring[kN2RingWords];
   __shared__ uint32_t cur[kN2MaxSub], Ub[2][kN2MaxSub], Vb[2][kN2MaxSub];
   __shared__ uint16_t lsub[kN2ListCap];
   __shared__ uint32_t lpos[kN2ListCap];
@@ -178,12 +179,21 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
       else if (pos < ucap) gout[static_cast<int64_t>(sb) * cap2 + pos] = rec[k];  // past the ring: straight out
     }
     n_lds_barrier();  // B
-    {
+    {  // four lanes per unit, 16 bytes each; a unit holding positions below V goes record by record
       const uint32_t n = lcnt[par];
-      for (uint32_t u = static_cast<uint32_t>(wave * 4 + (lane >> 4)); u < n; u += kN2Waves * 4) {
+      const int g = lane & 3;
+      for (uint32_t u = static_cast<uint32_t>(wave * 16 + (lane >> 2)); u < n; u += kN2Waves * 16) {
         const uint32_t sb = lsub[u];
-        const uint32_t i = lpos[u] + static_cast<uint32_t>(lane & 15);
-        if (i >= Vc[sb] && i < ucap) gout[static_cast<int64_t>(sb) * cap2 + i] = ring[(sb << rlog) + (i & rmask)];
+        const uint32_t p0 = lpos[u];
+        if (p0 >= ucap) continue;
+        PGX_GLOBAL uint32_t* const dst = gout + static_cast<int64_t>(sb) * cap2 + p0 + 4 * g;
+        const uint32_t* const rs = ring + (sb << rlog) + (p0 & rmask) + 4 * g;
+        if (p0 >= Vc[sb]) {
+          *(PGX_GLOBAL na_u32x4*)dst = *(const na_u32x4*)rs;
+        } else {
+          for (int q = 0; q < 4; ++q)
+            if (p0 + 4 * g + q >= Vc[sb]) dst[q] = rs[q];
+        }
       }
     }
     par ^= 1;
@@ -229,7 +239,6 @@ constexpr int kNABuckets = 48;
 constexpr int kNASlots = kNABuckets * kNAWays;  // 192
 constexpr int kNAImgWords = 64 + 65536 / 2;
 constexpr uint32_t kNAEmpty = 0xFFFFFFFFu;
-typedef unsigned int na_u32x4 __attribute__((ext_vector_type(4)));
 
 template <int IMG>
 __device__ __forceinline__ uint32_t na_img(const uint32_t* simg, int img_sh, uint32_t d) {
@@ -402,6 +411,7 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
         kb[j] = *reinterpret_cast<const na_u32x4*>(K + b * kNAWays);
         val[j] = SUM ? na_img<IMG>(simg, img_sh, rb2 >= 32 ? 0u : R >> rb2) : 0u;
       }
+      uint32_t miss = 0u;  // records of this half whose key is not in its home bucket (yet)
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int jj = h * 8 + j;
@@ -412,12 +422,37 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
         const uint32_t dd = rb2 >= 32 ? 0u : R >> rb2;
         const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2);
         const int m = na_way(kb[j], r2);
-        const int slot = m >= 0 ? static_cast<int>(b) * kNAWays + m : probe(r2, b);
+        if (m < 0) {
+          miss |= 1u << j;
+          continue;
+        }
+        const int slot = static_cast<int>(b) * kNAWays + m;
+        atomicAdd(&S[slot], SUM ? one + val[j] : one);
+        if (MN) atomicMin(&N[slot], dd);
+        if (MX) atomicMax(&X[slot], dd);
+      }
+      // The misses (a group's first record, ~1 in 60 at C3: some lane of the wave misses at most j) probe together:
+      // each pass resolves every lane's next missed record, so the wave pays one probe chain per pass instead of
+      // one per j that any lane missed.
+      while (__ballot(miss != 0u)) {
+        if (!miss) continue;
+        const int js = __builtin_ctz(miss);
+        miss &= miss - 1u;
+        uint32_t R = 0u, v = 0u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (j == js) {
+            R = b0[h * 8 + j];
+            v = val[j];
+          }
+        const uint32_t r2 = R & rmask;
+        const uint32_t dd = rb2 >= 32 ? 0u : R >> rb2;
+        const int slot = probe(r2, static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2));
         if (slot < 0) {
           lost = true;
           continue;
         }
-        atomicAdd(&S[slot], SUM ? one + val[j] : one);
+        atomicAdd(&S[slot], SUM ? one + v : one);
         if (MN) atomicMin(&N[slot], dd);
         if (MX) atomicMax(&X[slot], dd);
       }
