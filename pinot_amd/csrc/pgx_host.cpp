@@ -522,8 +522,11 @@ struct StagedColumn {
   int max_mv = 0;
 };
 
+std::atomic<uint64_t> g_segment_uid{1};
+
 struct pgx_segment {
   pgx_ctx* ctx = nullptr;
+  uint64_t uid = g_segment_uid.fetch_add(1);  // never reused: keys the plan cache (a freed address may be reused)
   std::string name;
   int32_t total_docs = 0, total_raw_docs = 0;
   std::vector<StagedColumn> cols;
@@ -4578,6 +4581,176 @@ void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, in
   finish_result(ctx, q, P, B, segs, n, st, R, nullptr);
 }
 
+// After the launches of a non-partitioned plan: with PGX_X_KEEP_DENSE_ON_DEVICE the caller's dense table stays on the
+// device (statistics only); otherwise the result is read back (finish_result).
+void complete_scan(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, pgx_segment* const* segs, int n,
+                   const pgx_exec_opts* opts, hipStream_t st, pgx_result* R) {
+  if (opts && (opts->flags & PGX_X_KEEP_DENSE_ON_DEVICE)) {
+    unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    const unsigned long long* stats = outs + 16;
+    R->stats[0] = int64_t(stats[0]);
+    R->stats[1] = int64_t(stats[1]) + P.host_entries;
+    R->stats[2] = int64_t(stats[0]) * P.n_proj;
+    R->stats[3] = P.total_raw;
+    R->group_by = true;
+    R->num_aggs = P.kq.num_aggs;
+    R->agg_fn = q.agg_fn;
+    return;
+  }
+  finish_result(ctx, q, P, B, segs, n, st, R, nullptr);
+}
+
+// -------------------------------------------------------------------------------------------------
+// Plan cache: a server runs the same query shape over the same segments again and again (and the bench's steps do).
+// Planning a 4,096-segment query costs ~2.5-3 ms of host time (predicate leaves, bitmap programs and chunk descriptors,
+// key spaces, the argument arena, per-segment kernel descriptors: p.* / upload / j.sig / jit phases of
+// PGX_HOST_PROFILE) before the first launch.  A plan whose state is the argument arena and the bitmap masks (dense or
+// aggregation-only, no partitioned / hash / multi-value / automaton buffers) is kept after its execution, with its
+// device arena, keyed by the query, the segment list (unique segment ids), the bindings' content, the planning flags and
+// the PGX_* environment.  A later execution with the same key replays it: arena and descriptors re-sent, launches,
+// read-back -- no planning.  An entry serves one execution at a time (the bench keeps three in flight: up to
+// kPlanCacheMax entries per query).  Entries hold a context reference; they go with their query
+// (pgx_query_release), their context (pgx_ctx_destroy) or by eviction.  PGX_PLAN_CACHE=0 turns the cache off.
+// -------------------------------------------------------------------------------------------------
+}  // namespace
+extern "C" char** environ;
+namespace {
+
+struct PlanEntry {
+  pgx_ctx* ctx = nullptr;
+  std::vector<uint64_t> uids;
+  uint64_t key = 0;
+  std::unique_ptr<ExecPlan> P;
+  std::unique_ptr<ExecBuffers> B;
+  bool busy = false;
+  uint64_t stamp = 0;
+  ~PlanEntry() {
+    B.reset();
+    P.reset();
+    if (ctx) ctx_unref(ctx);
+  }
+};
+constexpr size_t kPlanCacheMax = 4;
+std::mutex g_pc_mu;
+std::unordered_map<const pgx_query*, std::vector<std::shared_ptr<PlanEntry>>> g_pc;
+uint64_t g_pc_clock = 0;
+
+bool plan_cache_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("PGX_PLAN_CACHE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// FNV-1a over the planning inputs that are not the segment list: context, planning flags, the PGX_* environment (A/B
+// knobs select plans), every binding's range and its bitset's content (bitsets shared by segments hashed once).
+uint64_t plan_key(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
+                  uint32_t xflags) {
+  uint64_t h = 1469598103934665603ull;
+  auto mix = [&](uint64_t x) {
+    for (int i = 0; i < 8; ++i) {
+      h ^= (x >> (8 * i)) & 0xFF;
+      h *= 1099511628211ull;
+    }
+  };
+  mix(reinterpret_cast<uintptr_t>(ctx));
+  mix(uint64_t(n));
+  mix(xflags & ~(PGX_X_THROUGHPUT | PGX_X_KEEP_DENSE_ON_DEVICE));
+  for (char** e = environ; *e; ++e)
+    if (std::strncmp(*e, "PGX_", 4) == 0)
+      for (const char* c = *e; *c; ++c) mix(uint8_t(*c));
+  const size_t L = q.leaf_col.size();
+  if (!L || !bindings) return h;
+  std::unordered_map<const uint32_t*, uint64_t> seen;
+  for (int s = 0; s < n; ++s)
+    for (size_t l = 0; l < L; ++l) {
+      const pgx_leaf_binding& b = bindings[size_t(s) * L + l];
+      mix((uint64_t(uint32_t(b.lo)) << 32) | uint32_t(b.hi));
+      if (!b.words) continue;
+      const int card = segs[s]->col(q.leaf_col[l]).card;
+      auto it = seen.find(b.words);
+      if (it == seen.end()) {
+        uint64_t w = 1469598103934665603ull;
+        for (int i = 0; i < (card + 31) / 32; ++i) w = (w ^ b.words[i]) * 1099511628211ull;
+        it = seen.emplace(b.words, w ^ uint64_t(card)).first;
+      }
+      mix(it->second);
+    }
+  return h;
+}
+
+std::shared_ptr<PlanEntry> plan_cache_acquire(const pgx_query* q, const std::vector<uint64_t>& uids, uint64_t key) {
+  std::lock_guard<std::mutex> g(g_pc_mu);
+  auto it = g_pc.find(q);
+  if (it == g_pc.end()) return nullptr;
+  for (auto& e : it->second)
+    if (!e->busy && e->key == key && e->uids == uids) {
+      e->busy = true;
+      e->stamp = ++g_pc_clock;
+      return e;
+    }
+  return nullptr;
+}
+
+void plan_cache_release(const std::shared_ptr<PlanEntry>& e) {
+  std::lock_guard<std::mutex> g(g_pc_mu);
+  e->busy = false;
+}
+
+// after a successful execution of a cacheable plan: keep it (the oldest idle entry makes room)
+void plan_cache_insert(const pgx_query* q, pgx_ctx* ctx, std::vector<uint64_t> uids, uint64_t key,
+                       std::unique_ptr<ExecPlan> P, std::unique_ptr<ExecBuffers> B) {
+  auto e = std::make_shared<PlanEntry>();
+  ctx->refs.fetch_add(1);
+  e->ctx = ctx;
+  e->uids = std::move(uids);
+  e->key = key;
+  e->P = std::move(P);
+  e->B = std::move(B);
+  std::shared_ptr<PlanEntry> evicted;  // destroyed outside the lock (frees device memory)
+  std::lock_guard<std::mutex> g(g_pc_mu);
+  auto& v = g_pc[q];
+  if (v.size() >= kPlanCacheMax) {
+    int old = -1;
+    for (size_t i = 0; i < v.size(); ++i)
+      if (!v[i]->busy && (old < 0 || v[i]->stamp < v[size_t(old)]->stamp)) old = int(i);
+    if (old < 0) return;  // every entry busy: not kept
+    evicted = std::move(v[size_t(old)]);
+    v.erase(v.begin() + old);
+  }
+  e->stamp = ++g_pc_clock;
+  v.push_back(std::move(e));
+}
+
+// drop a query's entries (query released) or a context's (context destroyed); busy entries stay alive with the
+// execution that holds them
+void plan_cache_purge(const pgx_query* q, const pgx_ctx* ctx) {
+  std::vector<std::shared_ptr<PlanEntry>> drop;
+  {
+    std::lock_guard<std::mutex> g(g_pc_mu);
+    for (auto it = g_pc.begin(); it != g_pc.end();) {
+      auto& v = it->second;
+      for (size_t i = 0; i < v.size();) {
+        if ((q && it->first == q) || (ctx && v[i]->ctx == ctx)) {
+          drop.push_back(std::move(v[i]));
+          v.erase(v.begin() + long(i));
+        } else {
+          ++i;
+        }
+      }
+      it = v.empty() ? g_pc.erase(it) : std::next(it);
+    }
+  }
+}
+
+bool plan_cacheable(const ExecPlan& P) {
+  return !P.use_part && P.kq.group_mode != G_HASH64 && P.kq.group_mode != G_HASH128 && P.mv_items.empty() &&
+         !P.fsm_on && !P.mv_masks.p && !P.sel_buf.p && !P.lmask_buf.p && !P.jit.empty();
+}
+
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                const pgx_exec_opts* opts, pgx_result* R, const Domain* dom = nullptr) {
   HostProf hp;
@@ -4601,11 +4774,39 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     run_mv(ctx, q, segs, n, bindings, xflags, R, st);
     return;
   }
+  // plan cache (single-device plans without a caller key domain)
+  const bool cache = !dom && plan_cache_on() && n > 0;
+  std::vector<uint64_t> uids;
+  uint64_t pkey = 0;
+  if (cache) {
+    uids.resize(size_t(n));
+    for (int s = 0; s < n; ++s) uids[size_t(s)] = segs[s]->uid;
+    pkey = plan_key(ctx, q, segs, n, bindings, xflags);
+    if (auto e = plan_cache_acquire(&q, uids, pkey)) {
+      struct Rel {
+        const std::shared_ptr<PlanEntry>& e;
+        ~Rel() { plan_cache_release(e); }
+      } rel{e};
+      hp.mark("cached");
+      ExecPlan& P = *e->P;
+      ExecBuffers& B = *e->B;
+      send_arena(P, B, st);
+      alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
+      reset_outputs(P, B, st);
+      launch_scan(P, st);
+      hp.mark("launch");
+      complete_scan(ctx, q, P, B, segs, n, opts, st, R);
+      hp.mark("finish");
+      return;
+    }
+  }
   if (!dom && run_batched(ctx, q, segs, n, bindings, opts, R, st, xflags, hp)) return;
-  ExecPlan P;
+  auto Pp = std::make_unique<ExecPlan>();
+  auto Bp = std::make_unique<ExecBuffers>();
+  ExecPlan& P = *Pp;
   plan_query(ctx, q, segs, n, bindings, xflags, P, dom);
   hp.mark("plan");
-  ExecBuffers B;
+  ExecBuffers& B = *Bp;
   upload_plan(ctx, P, B, st);
   hp.mark("upload");
   plan_jit(ctx, q, segs, n, P, B);
@@ -4646,22 +4847,9 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     P.hash_cap *= 4;  // table full: grow and rerun
     if (attempt == 5) fail(PGX_ERR_OOM, "group-by hash table overflow");
   }
-  if (opts && (opts->flags & PGX_X_KEEP_DENSE_ON_DEVICE)) {
-    unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
-    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
-    hip_check(hipStreamSynchronize(st), "sync");
-    const unsigned long long* stats = outs + 16;
-    R->stats[0] = int64_t(stats[0]);
-    R->stats[1] = int64_t(stats[1]) + P.host_entries;
-    R->stats[2] = int64_t(stats[0]) * P.n_proj;
-    R->stats[3] = P.total_raw;
-    R->group_by = true;
-    R->num_aggs = P.kq.num_aggs;
-    R->agg_fn = q.agg_fn;
-    return;
-  }
-  finish_result(ctx, q, P, B, segs, n, st, R, nullptr);
+  complete_scan(ctx, q, P, B, segs, n, opts, st, R);
   hp.mark("finish");
+  if (cache && plan_cacheable(P)) plan_cache_insert(&q, ctx, std::move(uids), pkey, std::move(Pp), std::move(Bp));
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -4984,6 +5172,7 @@ void ctx_unref(pgx_ctx* ctx) {
 pgx_status pgx_ctx_destroy(pgx_ctx* ctx) {
   return guarded([&] {
     if (!ctx) return;
+    plan_cache_purge(nullptr, ctx);  // cached plans hold context references
     ctx_unref(ctx);
   });
 }
@@ -5265,6 +5454,7 @@ pgx_status pgx_query_set_key_domain(pgx_query* q, int32_t group_col, int32_t typ
   return guarded([&] {
     if (!q) fail(PGX_ERR_INVALID_ARG, "NULL query");
     if (group_col < 0 || group_col >= int(q->group_cols.size())) fail(PGX_ERR_INVALID_ARG, "group column index");
+    plan_cache_purge(q, nullptr);  // plans decode keys against the domain
     if (num_values < 0 || num_values > INT32_MAX) fail(PGX_ERR_INVALID_ARG, "key domain size");
     q->key_domain.resize(q->group_cols.size());
     KeyDomain D;
@@ -5297,7 +5487,10 @@ pgx_status pgx_query_set_key_domain(pgx_query* q, int32_t group_col, int32_t typ
 }
 
 pgx_status pgx_query_release(pgx_query* q) {
-  return guarded([&] { delete q; });
+  return guarded([&] {
+    plan_cache_purge(q, nullptr);
+    delete q;
+  });
 }
 
 pgx_status pgx_execute(pgx_ctx* ctx, const pgx_query* q, pgx_segment* const* segs, int32_t n,

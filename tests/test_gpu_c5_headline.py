@@ -155,3 +155,38 @@ def test_c5_full_size_shard_linearity(ctx):
         q.close()
     finally:
         data.free()
+
+
+def test_plan_cache_replays_vs_oracle(ctx, monkeypatch, capfd):
+    """The plan cache (pgx_host.cpp run_query): a second execution of the same query over the same segments replays the
+    first one's plan (the host-profile line carries the "cached" mark) with the same result, statistics included; the
+    throughput flag does not change the key; a different segment list (a subset) plans afresh.  Oracle as above."""
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    monkeypatch.setenv("PGX_HOST_PROFILE", "1")
+    nseg, rows = 48, 65536 + 999
+    seg_ids = list(range(nseg))
+    data = synth.DeviceSegments(ctx, WL, seg_ids, rows=rows)
+    try:
+        req = pql.compile(WL.query)
+        q = E._Query(ctx, req)
+        segs = data.segments
+        sums, counts = _oracle(seg_ids, rows, req)
+        for k, flags in enumerate([0, 0, N.PGX_X_THROUGHPUT]):
+            r = q.execute(segs, flags=flags)
+            blk = E.decode_result(q, r, segs)
+            _check(blk.get_aggregation_group_by_result().as_map(), blk.stats.as_list(), sums, counts, nseg, rows)
+            N.lib().pgx_result_release(r)
+            lines = [x for x in capfd.readouterr().err.splitlines() if x.startswith("[pgx host us]")]
+            assert lines and (" cached=" in lines[-1]) == (k > 0), lines
+        sub = segs[:20]
+        r = q.execute(sub)
+        blk = E.decode_result(q, r, sub)
+        s2, c2 = _oracle(seg_ids[:20], rows, req)
+        _check(blk.get_aggregation_group_by_result().as_map(), blk.stats.as_list(), s2, c2, 20, rows)
+        N.lib().pgx_result_release(r)
+        lines = [x for x in capfd.readouterr().err.splitlines() if x.startswith("[pgx host us]")]
+        assert lines and " cached=" not in lines[-1], lines
+        q.close()
+    finally:
+        data.free()
