@@ -2926,13 +2926,17 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
   }
 }
 
-void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table = true) {
-  // (re)sends the whole argument arena with initialised output planes
+void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table = true, bool outs_only = false) {
+  // (re)sends the whole argument arena with initialised output planes; outs_only: the arena's descriptors are already
+  // on the device (a cached plan's replay: kernels write only the outputs block), send the outputs block alone
   KQuery& K = P.kq;
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
   std::memset(outs, 0, kOutsBytes);
   for (int p = 1; p < K.num_planes; ++p) outs[p] = (K.plane_op[p] == P_MIN_ORD) ? ~0ull : 0ull;
-  hip_check(hipMemcpyAsync(B.arena.p, B.host.p, B.size, hipMemcpyHostToDevice, st), "argument arena H2D");
+  if (outs_only)
+    hip_check(hipMemcpyAsync(B.dev() + B.off_outs, outs, kOutsBytes, hipMemcpyHostToDevice, st), "outputs H2D");
+  else
+    hip_check(hipMemcpyAsync(B.arena.p, B.host.p, B.size, hipMemcpyHostToDevice, st), "argument arena H2D");
   if (init_table && K.group_mode != G_NONE && !P.use_part) {
     const uint64_t slots = (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) ? P.hash_cap : P.dense_slots;
     const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : (K.group_mode == G_HASH64 ? P.hash_cap : 0);
@@ -4645,39 +4649,51 @@ bool plan_cache_on() {
   return on;
 }
 
-// FNV-1a over the planning inputs that are not the segment list: context, planning flags, the PGX_* environment (A/B
-// knobs select plans), every binding's range and its bitset's content (bitsets shared by segments hashed once).
+// Hash of the planning inputs that are not the segment list: context, planning flags, the PGX_* environment (A/B knobs
+// select plans), every binding's range and its bitset's content (a bitset shared by consecutive segments -- one
+// dictionary -- is hashed once).  64-bit multiply-xorshift steps: ~12k bindings at C5.
 uint64_t plan_key(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                   uint32_t xflags) {
-  uint64_t h = 1469598103934665603ull;
+  uint64_t h = 0x9E3779B97F4A7C15ull;
   auto mix = [&](uint64_t x) {
-    for (int i = 0; i < 8; ++i) {
-      h ^= (x >> (8 * i)) & 0xFF;
-      h *= 1099511628211ull;
-    }
+    h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 31;
   };
   mix(reinterpret_cast<uintptr_t>(ctx));
   mix(uint64_t(n));
   mix(xflags & ~(PGX_X_THROUGHPUT | PGX_X_KEEP_DENSE_ON_DEVICE));
   for (char** e = environ; *e; ++e)
-    if (std::strncmp(*e, "PGX_", 4) == 0)
-      for (const char* c = *e; *c; ++c) mix(uint8_t(*c));
+    if (std::strncmp(*e, "PGX_", 4) == 0) {
+      uint64_t w = 0;
+      int k = 0;
+      for (const char* c = *e; *c; ++c) {
+        w = (w << 8) | uint8_t(*c);
+        if (++k == 8) {
+          mix(w);
+          w = 0;
+          k = 0;
+        }
+      }
+      mix(w ^ (uint64_t(k) << 56));
+    }
   const size_t L = q.leaf_col.size();
   if (!L || !bindings) return h;
-  std::unordered_map<const uint32_t*, uint64_t> seen;
+  std::vector<const uint32_t*> last_ptr(L, nullptr);
+  std::vector<uint64_t> last_hash(L, 0);
   for (int s = 0; s < n; ++s)
     for (size_t l = 0; l < L; ++l) {
       const pgx_leaf_binding& b = bindings[size_t(s) * L + l];
       mix((uint64_t(uint32_t(b.lo)) << 32) | uint32_t(b.hi));
       if (!b.words) continue;
-      const int card = segs[s]->col(q.leaf_col[l]).card;
-      auto it = seen.find(b.words);
-      if (it == seen.end()) {
-        uint64_t w = 1469598103934665603ull;
-        for (int i = 0; i < (card + 31) / 32; ++i) w = (w ^ b.words[i]) * 1099511628211ull;
-        it = seen.emplace(b.words, w ^ uint64_t(card)).first;
+      if (b.words != last_ptr[l]) {  // (a bitset pointer is one dictionary's: pgx_bind_predicates shares them)
+        const int card = segs[s]->col(q.leaf_col[l]).card;
+        uint64_t w = uint64_t(card) * 0x9E3779B97F4A7C15ull;
+        for (int i = 0; i < (card + 31) / 32; ++i) w = (w ^ b.words[i]) * 0xBF58476D1CE4E5B9ull;
+        last_ptr[l] = b.words;
+        last_hash[l] = w;
       }
-      mix(it->second);
+      mix(last_hash[l]);
     }
   return h;
 }
@@ -4693,6 +4709,25 @@ std::shared_ptr<PlanEntry> plan_cache_acquire(const pgx_query* q, const std::vec
       return e;
     }
   return nullptr;
+}
+
+// A long segment list is first run batched (the GPU starts after the first batch is planned); the second execution of
+// the same key plans the whole list at once so that the plan is kept (recent keys remembered here).
+bool plan_cache_seen_before(const pgx_query* q, uint64_t key, const std::vector<uint64_t>& uids) {
+  static uint64_t recent[32] = {};
+  static int next = 0;
+  uint64_t h = key ^ reinterpret_cast<uintptr_t>(q);
+  for (uint64_t u : uids) h = (h ^ u) * 0x100000001B3ull;
+  h |= 1;  // 0 marks an empty slot
+  std::lock_guard<std::mutex> g(g_pc_mu);
+  for (uint64_t& r : recent)
+    if (r == h) {
+      r = 0;
+      return true;
+    }
+  recent[next] = h;
+  next = (next + 1) % 32;
+  return false;
 }
 
 void plan_cache_release(const std::shared_ptr<PlanEntry>& e) {
@@ -4758,6 +4793,33 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   struct Unmark { ~Unmark() { g_prof_mark = nullptr; } } unmark;
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
   const uint32_t xflags = opts ? opts->flags : 0;
+  // plan cache (single-device plans without a caller key domain; only plain plans are ever kept, so a hit is one)
+  const bool cache = !dom && plan_cache_on() && n > 0;
+  std::vector<uint64_t> uids;
+  uint64_t pkey = 0;
+  if (cache) {
+    uids.resize(size_t(n));
+    for (int s = 0; s < n; ++s) uids[size_t(s)] = segs[s]->uid;
+    pkey = plan_key(ctx, q, segs, n, bindings, xflags);
+    if (auto e = plan_cache_acquire(&q, uids, pkey)) {
+      struct Rel {
+        const std::shared_ptr<PlanEntry>& e;
+        ~Rel() { plan_cache_release(e); }
+      } rel{e};
+      hp.mark("cached");
+      ExecPlan& P = *e->P;
+      ExecBuffers& B = *e->B;
+      // the device arena (descriptors, bitmap-program descriptors, blob) is as the first execution sent it; the
+      // bitmap programs run again from launch_scan
+      alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
+      reset_outputs(P, B, st, true, true);
+      launch_scan(P, st);
+      hp.mark("launch");
+      complete_scan(ctx, q, P, B, segs, n, opts, st, R);
+      hp.mark("finish");
+      return;
+    }
+  }
   bool mv_group = false;  // a multi-value group column: key expansion per doc
   for (const auto& g : q.group_cols)
     for (int s = 0; s < n && !mv_group; ++s) mv_group = segs[s]->col(g).is_mv;
@@ -4774,33 +4836,8 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     run_mv(ctx, q, segs, n, bindings, xflags, R, st);
     return;
   }
-  // plan cache (single-device plans without a caller key domain)
-  const bool cache = !dom && plan_cache_on() && n > 0;
-  std::vector<uint64_t> uids;
-  uint64_t pkey = 0;
-  if (cache) {
-    uids.resize(size_t(n));
-    for (int s = 0; s < n; ++s) uids[size_t(s)] = segs[s]->uid;
-    pkey = plan_key(ctx, q, segs, n, bindings, xflags);
-    if (auto e = plan_cache_acquire(&q, uids, pkey)) {
-      struct Rel {
-        const std::shared_ptr<PlanEntry>& e;
-        ~Rel() { plan_cache_release(e); }
-      } rel{e};
-      hp.mark("cached");
-      ExecPlan& P = *e->P;
-      ExecBuffers& B = *e->B;
-      send_arena(P, B, st);
-      alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
-      reset_outputs(P, B, st);
-      launch_scan(P, st);
-      hp.mark("launch");
-      complete_scan(ctx, q, P, B, segs, n, opts, st, R);
-      hp.mark("finish");
-      return;
-    }
-  }
-  if (!dom && run_batched(ctx, q, segs, n, bindings, opts, R, st, xflags, hp)) return;
+  const bool again = cache && plan_cache_seen_before(&q, pkey, uids);
+  if (!dom && !again && run_batched(ctx, q, segs, n, bindings, opts, R, st, xflags, hp)) return;
   auto Pp = std::make_unique<ExecPlan>();
   auto Bp = std::make_unique<ExecBuffers>();
   ExecPlan& P = *Pp;

@@ -190,3 +190,33 @@ def test_plan_cache_replays_vs_oracle(ctx, monkeypatch, capfd):
         q.close()
     finally:
         data.free()
+
+
+def test_plan_cache_batched_list_promotes(ctx, monkeypatch, capfd):
+    """A list long enough to be planned in batches (>= 2 x 512 segments, flags 0): the first execution runs batched,
+    the second plans the whole list at once and keeps the plan, the third replays it (host-profile marks: "b.dicts"
+    for batched, "cached" for a replay).  Every result equals the oracle's."""
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    monkeypatch.setenv("PGX_HOST_PROFILE", "1")
+    nseg, rows = 1100, 4096 + 17
+    seg_ids = list(range(nseg))
+    data = synth.DeviceSegments(ctx, WL, seg_ids, rows=rows)
+    try:
+        req = pql.compile(WL.query)
+        q = E._Query(ctx, req)
+        segs = data.segments
+        sums, counts = _oracle(seg_ids, rows, req)
+        marks = []
+        for _ in range(3):
+            r = q.execute(segs)
+            blk = E.decode_result(q, r, segs)
+            _check(blk.get_aggregation_group_by_result().as_map(), blk.stats.as_list(), sums, counts, nseg, rows)
+            N.lib().pgx_result_release(r)
+            lines = [x for x in capfd.readouterr().err.splitlines() if x.startswith("[pgx host us]")]
+            assert lines, "no host profile line"
+            marks.append((" b.dicts=" in lines[-1], " cached=" in lines[-1]))
+        assert marks == [(True, False), (False, False), (False, True)], marks
+        q.close()
+    finally:
+        data.free()
