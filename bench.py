@@ -1,6 +1,6 @@
 """Benchmark of the MI355X segment query hot path (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c2|c3|c1|c4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c2|c3|c1|c4|c6]
   (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
 The default workload is c5, BASELINE configs[4] -- the metric's own shape: bitmap inverted-index AND/OR filter +
@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "rows/sec for filter+group-by SUM at 1/2/4/8 GPUs; % of HBM roofline"
 # bounded CPU-baseline samples (segments, rows per segment): ~10-30 s of single-core work over 8 threads in total
-CPU_SAMPLE = {"c2": (8, 32_000_000), "c5": (64, 2_000_000), "c3": (8, 16_000_000)}
+CPU_SAMPLE = {"c2": (8, 32_000_000), "c5": (64, 2_000_000), "c3": (8, 16_000_000), "c6": (8, 8_000_000)}
 
 
 def source_hash():
@@ -123,6 +123,14 @@ def cpu_baseline(wl, query, seg_rows, nseg, threads):
         kw.update(group_cols=("gk",), leaves=[("f1", bits(1000, f1)), ("f2", bits(100, [7])),
                                               ("f3", bits(10, [i for i in range(10) if i != 3]))],
                   prog=[0, 1, -2, 2, -1], inverted=invs, excl=[0, 0, 1])
+    elif wl.name == "c6":  # ten range leaves ORed, as dictId bitsets: w_i < C6_CUT
+        leaves = []
+        for k, c in enumerate(wl.columns[:10]):
+            w = np.zeros((c.card + 31) // 32, dtype=np.uint32)
+            for i in range(synth.C6_CUT[k % 3]):
+                w[i >> 5] |= np.uint32(1 << (i & 31))
+            leaves.append((c.name, w))
+        kw.update(group_cols=("gk",), leaves=leaves, prog=[0] + [x for i in range(1, 10) for x in (i, -2)])
     else:
         return None
     times = []

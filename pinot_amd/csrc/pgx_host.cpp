@@ -3064,6 +3064,35 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         for (JitCol& C : J.cols) C.frac = C.decode && (8 * C.bits) % 32 != 0;
       }
     J.R = R;
+    // Registers for the raw words of the next tile (loaded one tile ahead, so held twice): sum over the decoded columns
+    // of the dwords one sub-step of R rows takes, times the sub-steps per tile.  A query over many columns (C6: twelve)
+    // at 32 rows per lane per tile needs ~250 VGPRs for them alone and spills at the 1024-thread workgroups an LDS image
+    // asks for: take eight rows per lane (fractional loads of odd widths) and fewer rows per lane per tile until the
+    // double-buffered words fit kTileWordBudget.  C2 / C5 shapes (two or three columns) keep 32 rows per lane per tile.
+    {
+      constexpr int kTileWordBudget = 64;
+      auto words = [&](int r) {
+        int w = 0;
+        for (const JitCol& C : J.cols) {
+          if (!C.decode) continue;
+          const int rb = r * C.bits;
+          if (rb % 32 == 0) {
+            w += rb / 32;
+          } else {
+            int g = 32;
+            while (rb % g) g >>= 1;
+            w += (rb + 32 - g + 31) / 32;
+          }
+        }
+        return w;
+      };
+      if (J.R > 8 && 2 * words(J.R) > kTileWordBudget) {
+        J.R = 8;
+        for (JitCol& C : J.cols) C.frac = C.decode && (8 * C.bits) % 32 != 0;
+      }
+      const int w = words(J.R);
+      while (J.TL > J.R && 2 * (J.TL / J.R) * w > kTileWordBudget) J.TL /= 2;
+    }
     if (const char* e = std::getenv("PGX_LD_X4")) J.ld_x4 = e[0] == '1';
     if (const char* e = std::getenv("PGX_SEL_K")) J.sel_k = std::max(0, std::min(8, std::atoi(e)));
     // PGX_NO_IMG=1 (A/B): no value images; SUM / MIN / MAX values are gathered from the dictionary for selected rows

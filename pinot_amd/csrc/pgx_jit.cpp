@@ -1578,6 +1578,39 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.narrow_vbits = 0;
     shapes.push_back(s);
   }
+  {  // twelve columns (the C6 "wide" shape): ten filter leaves ANDed, a 10-bit dense group column, SUM of a 16-bit one
+    JitShape s = base(8, 16, IMG_U32, 0);
+    for (int c = 2; c < 12; ++c) {
+      JitCol C;
+      C.bits = c == 11 ? 10 : 8 + 2 * (c % 3);
+      C.decode = true;
+      s.cols.push_back(C);
+    }
+    s.leaf_col.clear();
+    s.leaf_mode.clear();
+    s.prog_op.clear();
+    s.prog_arg.clear();
+    for (int l = 0; l < 10; ++l) {
+      s.leaf_col.push_back(l == 0 ? 0 : l + 1);
+      s.leaf_mode.push_back(LEAF_SCAN_INTERVAL);
+      s.prog_op.push_back(OP_LEAF);
+      s.prog_arg.push_back(l);
+      if (l) {
+        s.prog_op.push_back(OP_AND);
+        s.prog_arg.push_back(0);
+      }
+    }
+    s.R = 16;
+    s.group_mode = G_DENSE_LDS;
+    s.gcol = {11};
+    s.gmul = {1};
+    s.dense_slots = 1024;
+    s.agg_kind = {A_SUM};
+    s.agg_col = {1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64};
+    s.num_planes = 2;
+    shapes.push_back(s);
+  }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {
     JitShape s = base(8, 16, IMG_U32, 0);
     s.cols.push_back(JitCol{});

@@ -4,7 +4,7 @@
 #ifndef PGX_JIT_ABI_H_
 #define PGX_JIT_ABI_H_
 
-#define PGX_J_MAX_COLS 8     // distinct columns one generated kernel reads
+#define PGX_J_MAX_COLS 16    // distinct columns one generated kernel reads (== kMaxQCols)
 #define PGX_J_MAX_LEAVES 16  // filter leaves (== kMaxLeaves)
 #define PGX_J_MAX_AGGS 8     // aggregation functions (== kMaxAggs)
 

@@ -183,3 +183,61 @@ def test_c5_eight_segments(ctx, rchunk, monkeypatch):
         assert st[0] == int(counts.sum()) and st[1] == 0 and st[3] == 8 * wl.rows
     finally:
         data.free()
+
+
+def test_c6_twelve_columns_in_query_kernel(ctx):
+    """C6: ten range leaves (ORed) + group column + metric = twelve columns, more than round 3's eight-column query
+    kernels took (they ran on the interpreter kernel).  The step runs the generated kernel (kernel names of pgx_timing), and
+    the group map + ExecutionStatistics equal the vectorised oracle over the regenerated columns."""
+    import json
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    L = N.lib()
+    wl = synth.WORKLOADS["c6"]
+    rows = 3_000_000 + 123
+    seg_ids = [0, 1]
+    data = synth.DeviceSegments(ctx, wl, seg_ids, rows=rows)
+    try:
+        q = pql.compile(wl.query)
+        N.check(L.pgx_timing_start(ctx.handle))
+        blk = E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(data.segments, q).execute()
+        out = (C.c_double * 3)()
+        js = C.create_string_buffer(8192)
+        N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
+        kernels = json.loads(js.value.decode())["kernels"]
+        assert "pgxq" in kernels and "pgx_scan_kernel" not in kernels, kernels
+        got = blk.get_aggregation_group_by_result().as_map()
+        st = blk.stats.as_list()
+        mvals = synth.make_dictionary("metric", 65536).astype(np.float64)
+        sums = np.zeros(1000)
+        counts = np.zeros(1000, dtype=np.int64)
+        for s in seg_ids:
+            ids = {c.name: c_oracle.synth_ids(synth.column_seed(wl.seed, s, ci), rows, c.card)
+                   for ci, c in enumerate(wl.columns)}
+            sel = np.zeros(rows, dtype=bool)
+            for k, c in enumerate(wl.columns[:10]):
+                sel |= ids[c.name] < synth.C6_CUT[k % 3]
+            sums += np.bincount(ids["gk"][sel], weights=mvals[ids["m"][sel]], minlength=1000)
+            counts += np.bincount(ids["gk"][sel], minlength=1000)
+        exp = {str(g): [float(sums[g])] for g in range(1000) if counts[g]}
+        assert set(got) == set(exp)
+        for k, v in exp.items():
+            H.assert_values_equal(got[k], v, ["sum"])
+        # numEntriesScannedInFilter from the C twin's iterator restatement (OR of scan leaves) over the same columns
+        leaves = []
+        for k, c in enumerate(wl.columns[:10]):
+            w = np.zeros((c.card + 31) // 32, dtype=np.uint32)
+            for i in range(synth.C6_CUT[k % 3]):
+                w[i >> 5] |= np.uint32(1 << (i & 31))
+            leaves.append((c.name, w))
+        osegs = [c_oracle.Segment(rows, {c.name: (c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), rows, c.bits,
+                                                                     c.card), c.bits,
+                                                     synth.make_dictionary(c.dict_kind, c.card).astype(np.float64),
+                                                     c.card)
+                                         for ci, c in enumerate(wl.columns)}) for s in seg_ids]
+        res = c_oracle.run(osegs, metric="m", group_cols=("gk",), threads=2, leaves=leaves,
+                           prog=[0] + [x for i in range(1, 10) for x in (i, -2)])
+        assert sum(r["count"] for r in res) == int(counts.sum())
+        assert st == [int(counts.sum()), sum(r["entries"] for r in res), 2 * int(counts.sum()), 2 * rows]
+    finally:
+        data.free()
