@@ -65,8 +65,8 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream);
 extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
-                                      void* states,
-                                      int64_t* idx, uint64_t* keys, int64_t cap, int grid, hipStream_t stream);
+                                      void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
+                                      const unsigned long long* prange, hipStream_t stream);
 extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
                                               const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
 extern "C" size_t pgx_trim_state_bytes(void);
@@ -87,8 +87,8 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
                                                   int nparts, int rb2, int keybits, int64_t vbase, int img_kind,
                                                   const uint32_t* img, int img_words, int img_sh, const int64_t* vdict,
                                                   int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
-                                                  uint64_t* oplane, int64_t ocap, unsigned long long* ctr, int grid,
-                                                  hipStream_t stream);
+                                                  uint64_t* oplane, int64_t ocap, unsigned long long* ctr,
+                                                  unsigned long long* prange, int grid, hipStream_t stream);
 extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
                                      int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
                                      uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream);
@@ -993,6 +993,7 @@ struct pgx_result {
   struct Lazy {
     pgx_ctx* ctx = nullptr;      // holds a context reference (the result may outlive the caller's handle)
     DevBuf okey, oplane;         // packed keys; planes [count, sum, min, max] x ocap
+    DevBuf prange;               // trim-key ranges per kind (pgx_narrow_aggregate), or none: the trim's range pass
     int64_t ocap = 0;
     std::vector<int> gshift, gbits;
     std::vector<std::vector<int32_t>> rep_seg, rep_id;  // [col][global id]
@@ -1002,6 +1003,7 @@ struct pgx_result {
     ~Lazy() {
       okey.reset();
       oplane.reset();
+      prange.reset();
       if (ctx) ctx_unref(ctx);
     }
   };
@@ -3546,6 +3548,7 @@ struct PartBuffers {
   int nbits2 = 7;                       // second pass: 2^nbits2 buckets per first-pass bucket (0: no second pass)
   int64_t cap1 = 0, cap2 = 0, ocap = 0;
   DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[kPart1N] | cursors2[nparts] (kCursorStride apart) | ocount | ovf[3]
+  DevBuf prange;                         // trim-key ranges of the groups (narrow aggregation), or none
   // slab mode (ExecPlan::part_slab): out1 holds kPart1N x nwg slabs of cap1 records, their counts in scnt; the second
   // pass always runs (with nbits2 = 0 it only gathers each bucket's slabs into one run)
   bool slab = false;
@@ -3738,6 +3741,7 @@ struct NarrowBuffers {
   bool hib = false;
   int64_t nwg = 0, cap1 = 0, cap2 = 0, ocap = 0, nparts = 0;
   DevBuf lo1, hi1, cnt1, rec2, cnt2, okey, oplane, ctr;  // ctr: ocount | overflow scan | split | aggregation
+  DevBuf prange;  // trim-key ranges: [kind] smallest, [4 + kind] largest (pgx_trim.hip)
 };
 
 // mean + 8 sigma (binomial, p small) + slack, a multiple of 32: slabs then start on 128-byte lines (u32 records) and
@@ -3793,6 +3797,7 @@ void narrow_alloc(pgx_ctx* ctx, NarrowBuffers& NB) {
   NB.okey = DevBuf(ctx, size_t(NB.ocap) * 8);
   NB.oplane = DevBuf(ctx, size_t(NB.ocap) * 4 * 8);
   NB.ctr = DevBuf(ctx, 4 * 8);
+  NB.prange = DevBuf(ctx, 8 * 8);
 }
 
 // Before the scan: zero the slab fills (workgroups without tiles publish none) and the counters; point the scan's
@@ -3810,6 +3815,8 @@ void narrow_prepare(ExecPlan& P, NarrowBuffers& NB, hipStream_t st) {
 // After the scan: the second split and the aggregation.
 void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStream_t st) {
   if (P.rec_total == 0) return;
+  hip_check(hipMemsetAsync(NB.prange.p, 0xFF, 32, st), "range minima");
+  hip_check(hipMemsetAsync(static_cast<uint8_t*>(NB.prange.p) + 32, 0, 32, st), "range maxima");
   unsigned long long* ctr = devp(NB.ctr);
   PGX_LAUNCH(st, "pgx_narrow_split",
              pgx_launch_narrow_split(NB.lo1.as<uint32_t>(), NB.hib ? NB.hi1.as<uint16_t>() : nullptr, devp(NB.cnt1),
@@ -3821,7 +3828,7 @@ void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStrea
                                          NB.rb2, P.part_keybits, P.part_vbase, P.narrow_img, P.narrow_imgp,
                                          P.narrow_img_words, P.narrow_img_sh, P.part_vdict, P.part_sum, P.part_min,
                                          P.part_max, NB.cshift, NB.okey.as<uint64_t>(), NB.oplane.as<uint64_t>(),
-                                         NB.ocap, ctr, ctx->num_cus, st),
+                                         NB.ocap, ctr, devp(NB.prange), ctx->num_cus, st),
              "narrow aggregate");
 }
 
@@ -3980,7 +3987,8 @@ const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
   hip_check(hipMemcpyAsync(state.p, init.data(), init.size(), hipMemcpyHostToDevice, st), "trim state H2D");
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((num_groups + 255) / 256, int64_t(L.ctx->num_cus) * 8)));
   PGX_LAUNCH(st, "pgx_trim", pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kinds.data(), nf, state.p,
-                            idx.as<int64_t>(), keys.as<uint64_t>(), size, grid, st),
+                            idx.as<int64_t>(), keys.as<uint64_t>(), size, grid,
+                            L.prange.p ? devp(L.prange) : nullptr, st),
             "trim launch");
   std::vector<int64_t> ix(size_t(size) * nf);
   std::vector<uint64_t> ky(size_t(size) * nf);
@@ -4021,6 +4029,7 @@ void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, 
   auto L = std::make_unique<pgx_result::Lazy>();
   L->okey = std::move(PB.okey);
   L->oplane = std::move(PB.oplane);
+  L->prange = std::move(PB.prange);
   L->ocap = PB.ocap;
   for (int g = 0; g < K.num_gcols; ++g) {
     L->gshift.push_back(K.gshift[g]);
@@ -4884,6 +4893,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
         PartBuffers PB;
         PB.okey = std::move(NB.okey);
         PB.oplane = std::move(NB.oplane);
+        PB.prange = std::move(NB.prange);
         PB.ocap = NB.ocap;
         part_result(ctx, q, P, B, PB, R);
         return;

@@ -240,6 +240,10 @@ constexpr int kNASlots = kNABuckets * kNAWays;  // 192
 constexpr int kNAImgWords = 64 + 65536 / 2;
 constexpr uint32_t kNAEmpty = 0xFFFFFFFFu;
 
+__device__ __forceinline__ unsigned long long oplane_sum_key(int64_t sum) {  // trim_key(SUM)
+  return static_cast<unsigned long long>(sum) ^ 0x8000000000000000ull;
+}
+
 template <int IMG>
 __device__ __forceinline__ uint32_t na_img(const uint32_t* simg, int img_sh, uint32_t d) {
   if (IMG == 1) return simg[d];
@@ -256,7 +260,8 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
     const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
     uint64_t kmask, uint64_t ic1, uint64_t ic2, int ms, int64_t vbase, const uint32_t* __restrict__ img, int img_words,
     int img_sh, const int64_t* __restrict__ vdict, int cshift, uint64_t* __restrict__ okey,
-    uint64_t* __restrict__ oplane, int64_t ocap, unsigned long long* __restrict__ ctr) {
+    uint64_t* __restrict__ oplane, int64_t ocap, unsigned long long* __restrict__ ctr,
+    unsigned long long* __restrict__ prange) {
   __shared__ __attribute__((aligned(16))) uint32_t simg[IMG ? kNAImgWords : 1];
   __shared__ __attribute__((aligned(16))) uint32_t tkey[kNAWaves * kNASlots];
   __shared__ unsigned long long tsc[kNAWaves * kNASlots];
@@ -323,6 +328,13 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
   uint32_t fk[Q], fn_[Q], fx[Q], fhas = 0, fexcl = 0;
   unsigned long long fsc[Q], fbase = 0ull;
   int fp = -1;
+  // trim-key ranges of the written groups (pgx_trim.hip trim_key: COUNT, SUM, MIN, MAX), so the trim skips its range
+  // pass: [kind] smallest, [4 + kind] largest
+  unsigned long long rlo[4] = {~0ull, ~0ull, ~0ull, ~0ull}, rhi[4] = {0ull, 0ull, 0ull, 0ull};
+  auto note = [&](int k, unsigned long long x) {
+    rlo[k] = x < rlo[k] ? x : rlo[k];
+    rhi[k] = x > rhi[k] ? x : rhi[k];
+  };
   auto flush_end = [&]() {
     if (fp < 0) return;
     const unsigned long long base = __shfl(fbase, 0, 64);
@@ -342,6 +354,10 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
         if (MX) vhi = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, fx[q])) : vd[fx[q]];
         oplane[2 * ocap + o] = static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull;
         oplane[3 * ocap + o] = static_cast<uint64_t>(vhi) ^ 0x8000000000000000ull;
+        note(0, c);
+        note(1, oplane_sum_key(static_cast<int64_t>(fsc[q] & smask) + static_cast<int64_t>(c) * vbase));
+        note(2, ~(static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull));
+        note(3, static_cast<uint64_t>(vhi) ^ 0x8000000000000000ull);
       } else {
         lost = true;
       }
@@ -471,6 +487,22 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
   }
   flush_end();
   if (lost) atomicAdd(ctr + 3, 1ull);
+  if (prange) {  // wavefront minimum / maximum, then one atomic per wavefront and kind
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      unsigned long long a = rlo[k], b = rhi[k];
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long x = __shfl_xor(a, d, 64), y = __shfl_xor(b, d, 64);
+        a = x < a ? x : a;
+        b = y > b ? y : b;
+      }
+      if (lane == 0 && a <= b) {
+        atomicMin(prange + k, a);
+        atomicMax(prange + 4 + k, b);
+      }
+    }
+  }
 }
 
 }  // namespace
@@ -494,8 +526,8 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
                                                   int nparts, int rb2, int keybits, int64_t vbase, int img_kind,
                                                   const uint32_t* img, int img_words, int img_sh, const int64_t* vdict,
                                                   int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
-                                                  uint64_t* oplane, int64_t ocap, unsigned long long* ctr, int grid,
-                                                  hipStream_t stream) {
+                                                  uint64_t* oplane, int64_t ocap, unsigned long long* ctr,
+                                                  unsigned long long* prange, int grid, hipStream_t stream) {
   if (nparts <= 0) return hipSuccess;
   if (rb2 < 0 || rb2 > 31 || keybits < 1 || keybits > 64 || cap2 < 4 || (cap2 & 3) || cshift < 1 || cshift > 63 ||
       grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 2 ||
@@ -508,7 +540,7 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
   case C:                                                                                                            \
     hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D>), dim3(grid), dim3(pgx::kNAThreads), 0, stream, in, cnt2, \
                        cap2, nparts, rb2, m.mask, m.ic1, m.ic2, m.s, vbase, img, img_words, img_sh, vdict, cshift,   \
-                       okey, oplane, ocap, ctr);                                                                     \
+                       okey, oplane, ocap, ctr, prange);                                                             \
     break;
 #define PGX_NA_CASES(I)                       \
   PGX_NA_CASE(I * 8 + 0, I, false, false, false) \

@@ -4,7 +4,7 @@
 // The reference trims the combined map when it holds more than 20 x max(topN, 1000) groups: per aggregation function
 // a MinMaxPriorityQueue keeps the 5 x max(topN, 1000) best values, largest first, smallest first for MIN functions
 // (query/aggregation/groupby/AggregationGroupByOperatorService.java:64-76, :284-440; the comparator looks at the value
-// only).  Here the same selection is a radix select over a 64-bit order key per group (8 passes of 8 bits, each a
+// only).  Here the same selection is a radix select over a 64-bit order key per group (passes of 11-bit digits, each a
 // histogram of the groups still matching the selected prefix), then one compaction pass that keeps every group above
 // the threshold key and as many threshold ties as fit.  Which of several tied groups at the threshold survive is
 // arbitrary, as in the reference (heap order; parity unpinned); the kept values are exact.
@@ -31,8 +31,11 @@ struct TrimState {
   unsigned long long n_tie;    //                                                  (40)
   unsigned long long kmin;     // key range of the groups                          (48)
   unsigned long long kmax;     //                                                  (56)
-  unsigned int hist[256];      //                                                  (64)
+  unsigned int hist[2048];     //                                                  (64)
 };
+constexpr int kTrimDigit = 11;             // bits per histogram pass
+constexpr int kTrimBins = 1 << kTrimDigit;
+constexpr int kTrimPasses = (64 + kTrimDigit - 1) / kTrimDigit;
 
 constexpr int kTrimMaxFns = 8;
 struct TrimKinds {             // function slot -> trim key kind
@@ -95,6 +98,17 @@ __global__ void __launch_bounds__(256) pgx_trim_range(const uint64_t* __restrict
   }
 }
 
+// Key ranges computed by the kernel that wrote the planes (pgx_narrow_aggregate): prange[k] = smallest and
+// prange[4 + k] = largest trim key of kind k (COUNT / SUM / MIN / MAX), so the range pass need not re-read the planes.
+__global__ void pgx_trim_seed(const unsigned long long* __restrict__ prange, const TrimKinds K,
+                              TrimState* __restrict__ sts) {
+  if (threadIdx.x != 0) return;
+  TrimState* st = sts + blockIdx.x;
+  const int kind = K.kind[blockIdx.x];
+  st->kmin = prange[kind];
+  st->kmax = prange[4 + kind];
+}
+
 // One lane per function: fix the bits above the highest differing bit, first digit just below them.
 __global__ void pgx_trim_begin(TrimState* __restrict__ sts) {
   if (threadIdx.x != 0) return;
@@ -109,7 +123,7 @@ __global__ void pgx_trim_begin(TrimState* __restrict__ sts) {
   const int hb = 64 - __clzll(static_cast<long long>(x));  // bits [0, hb) vary
   st->mask = hb == 64 ? 0ull : ~((1ull << hb) - 1ull);
   st->prefix = st->kmin & st->mask;
-  st->shift = hb > 8 ? hb - 8 : 0;
+  st->shift = hb > kTrimDigit ? hb - kTrimDigit : 0;
   st->done = 0;
 }
 
@@ -117,42 +131,63 @@ __global__ void __launch_bounds__(256) pgx_trim_hist(const uint64_t* __restrict_
                                                      const TrimKinds K, TrimState* __restrict__ sts) {
   TrimState* st = sts + blockIdx.y;
   if (st->done) return;
-  __shared__ unsigned int lh[256];
+  __shared__ unsigned int lh[kTrimBins];
   const int tid = threadIdx.x;
   const int kind = K.kind[blockIdx.y];
-  lh[tid] = 0u;
+  for (int b = tid; b < kTrimBins; b += 256) lh[b] = 0u;
   __syncthreads();
   const unsigned long long prefix = st->prefix, mask = st->mask;
   const int shift = st->shift;
   const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)oplane;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
     const uint64_t key = trim_key(pl, ocap, i, kind);
-    if ((key & mask) == prefix) atomicAdd(&lh[(key >> shift) & 255u], 1u);
+    if ((key & mask) == prefix) atomicAdd(&lh[(key >> shift) & (kTrimBins - 1u)], 1u);
   }
   __syncthreads();
-  if (lh[tid]) atomicAdd(&st->hist[tid], lh[tid]);
+  for (int b = tid; b < kTrimBins; b += 256)
+    if (lh[b]) atomicAdd(&st->hist[b], lh[b]);
 }
 
-// One lane per function: fix the next digit of the threshold from the histogram (the largest digit d whose bins >= d
-// hold at least k groups), then clear the histogram for the next pass.  Digits may overlap bits fixed before (the
-// last one ends at bit 0): those bits are equal in every key matching the prefix, so OR-ing them in changes nothing.
+// One wavefront per function: fix the next digit of the threshold from the histogram (the largest digit d whose bins
+// >= d hold at least k groups), then clear the histogram for the next pass.  Lane l holds bins [32 l, 32 l + 32).
+// Digits may overlap bits fixed before (the last one ends at bit 0): those bits are equal in every key matching the
+// prefix, so OR-ing them in changes nothing.
 __global__ void pgx_trim_step(TrimState* __restrict__ sts) {
-  if (threadIdx.x != 0) return;
   TrimState* st = sts + blockIdx.x;
   if (st->done) return;
-  long long above = 0;
-  int d = 255;
-  for (; d > 0; --d) {
-    const long long h = st->hist[d];
-    if (above + h >= st->k) break;
-    above += h;
+  const int lane = threadIdx.x;
+  constexpr int kPer = kTrimBins / 64;
+  long long mine = 0;
+  for (int i = 0; i < kPer; ++i) mine += st->hist[lane * kPer + i];
+  // suffix sums over lanes: S(l) = bins of lanes >= l
+  long long suf = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const long long y = __shfl_down(suf, d, 64);
+    if (lane + d < 64) suf += y;
   }
-  st->prefix |= static_cast<unsigned long long>(d) << st->shift;
-  st->mask |= 255ull << st->shift;
-  st->k -= above;
-  if (st->shift == 0) st->done = 1;
-  else st->shift = st->shift > 8 ? st->shift - 8 : 0;
-  for (int b = 0; b < 256; ++b) st->hist[b] = 0u;
+  const long long k = st->k;
+  // the highest lane whose suffix reaches k holds the threshold digit (lane 0 if none: every group is kept)
+  const unsigned long long reach = __ballot(suf >= k);
+  const int L = reach ? 63 - __clzll(static_cast<long long>(reach)) : 0;
+  const long long above_lane = __shfl(suf - mine, L, 64);  // bins of lanes > L
+  if (lane == L) {
+    long long above = above_lane;
+    int d = L * kPer + kPer - 1;
+    for (; d > L * kPer; --d) {
+      const long long h = st->hist[d];
+      if (above + h >= k) break;
+      above += h;
+    }
+    if (!reach) d = 0;
+    st->prefix |= static_cast<unsigned long long>(d) << st->shift;
+    st->mask |= static_cast<unsigned long long>(kTrimBins - 1) << st->shift;
+    st->k -= above;
+    if (st->shift == 0) st->done = 1;
+    else st->shift = st->shift > kTrimDigit ? st->shift - kTrimDigit : 0;
+  }
+  __syncthreads();
+  for (int i = 0; i < kPer; ++i) st->hist[lane * kPer + i] = 0u;
 }
 
 // Function slot y writes its selection to idx / keys + y * cap.  A workgroup scans one contiguous range of groups.
@@ -259,15 +294,20 @@ __global__ void __launch_bounds__(256) pgx_group_gather(const uint64_t* __restri
 // a function's threshold is complete return at once.
 extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
                                       void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
-                                      hipStream_t stream) {
+                                      const unsigned long long* prange, hipStream_t stream) {
   if (nf < 1 || nf > pgx::kTrimMaxFns) return hipErrorInvalidValue;
   pgx::TrimKinds K{};
-  for (int f = 0; f < nf; ++f) K.kind[f] = kinds[f];
+  bool seeded = prange != nullptr;
+  for (int f = 0; f < nf; ++f) {
+    K.kind[f] = kinds[f];
+    seeded = seeded && kinds[f] != pgx::TK_AVG;  // AVG keys are ratios: their range needs the pass
+  }
   pgx::TrimState* st = static_cast<pgx::TrimState*>(states);
   const dim3 g(grid, nf);
-  hipLaunchKernelGGL(pgx::pgx_trim_range, g, dim3(256), 0, stream, oplane, ocap, n, K, st);
+  if (seeded) hipLaunchKernelGGL(pgx::pgx_trim_seed, dim3(nf), dim3(64), 0, stream, prange, K, st);
+  else hipLaunchKernelGGL(pgx::pgx_trim_range, g, dim3(256), 0, stream, oplane, ocap, n, K, st);
   hipLaunchKernelGGL(pgx::pgx_trim_begin, dim3(nf), dim3(64), 0, stream, st);
-  for (int pass = 0; pass < 8; ++pass) {
+  for (int pass = 0; pass < pgx::kTrimPasses; ++pass) {
     hipLaunchKernelGGL(pgx::pgx_trim_hist, g, dim3(256), 0, stream, oplane, ocap, n, K, st);
     hipLaunchKernelGGL(pgx::pgx_trim_step, dim3(nf), dim3(64), 0, stream, st);
   }
