@@ -1,6 +1,6 @@
 """Benchmark of the MI355X segment query hot path (BASELINE.json metric).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c2|c3|c1|c4|c6]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c5|c2|c3|c1|c4|c6|c7]
   (N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
 
 The default workload is c5, BASELINE configs[4] -- the metric's own shape: bitmap inverted-index AND/OR filter +

@@ -1925,6 +1925,13 @@ void prof_mark(const char* what) {
 
 void canon_rprog(std::vector<int>& op, std::vector<int>& arg);
 
+// Hash group-by in the generated kernels (pgx_jit.cpp emit_hash): PGX_JIT_HASH=0 keeps the interpreter kernel (A/B).
+bool jit_hash_ok(const KQuery& K) {
+  if (K.group_mode != G_HASH64 && K.group_mode != G_HASH128) return true;
+  const char* e = std::getenv("PGX_JIT_HASH");
+  return !(e && e[0] == '0');
+}
+
 void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                 uint32_t xflags, ExecPlan& P, const Domain* dom = nullptr) {
   if (n < 1) fail(PGX_ERR_INVALID_ARG, "no segments");
@@ -2157,7 +2164,9 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   P.rprog_on = false;
   P.dm_progs.clear();
   P.use_docmask = jit_enabled() && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
-                                    K.group_mode == G_DENSE_GLOBAL || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS;
+                                    K.group_mode == G_DENSE_GLOBAL || K.group_mode == G_HASH64 ||
+                                    K.group_mode == G_HASH128 || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS &&
+                    jit_hash_ok(K);
   if (!q.filter.empty()) {
     PNode root = build_tree(q, *segs[0]);
     const size_t L = q.leaf_col.size();
@@ -2974,7 +2983,10 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
   P.part_slab = false;  // only the query kernels write slabs (the generic kernel writes row-order records)
   const KQuery& K = P.kq;
   if (!jit_enabled()) return;
-  if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL || P.use_part)) return;
+  if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL || P.use_part ||
+        K.group_mode == G_HASH64 || K.group_mode == G_HASH128))
+    return;
+  if (!jit_hash_ok(K)) return;
   const int nc = K.num_qcols;
   if (nc > PGX_J_MAX_COLS) return;
   P.part_slab = slab;
@@ -3118,13 +3130,19 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       rch_bytes += 5152;  // container-search scratch
     }
     const int64_t lds_budget = P.rchunk ? 52 * 1024 : kLdsBudget;
+    // hash group-by: the workgroup's LDS table (keys, 128-bit key states, planes); 2048 slots when they fit beside the
+    // images, down to 512 before an image is dropped
+    const bool hashg = K.group_mode == G_HASH64 || K.group_mode == G_HASH128;
+    const int64_t hslot_bytes = hashg ? (K.group_mode == G_HASH128 ? 20 : 8) + 8 * K.num_planes : 0;
+    int hash_slots = hashg ? 2048 : 0;
     auto lds_need = [&]() {
-      int64_t b = rch_bytes;
+      int64_t b = rch_bytes + (hashg ? hash_slots * hslot_bytes + 32 : 0);
       for (const JitCol& C : J.cols)
         if (C.img != IMG_NONE) b += ((int64_t(C.img_words) * 4 + 15) / 16) * 16;
       if (K.group_mode == G_DENSE_LDS) b += int64_t(P.dense_slots) * K.num_planes * 8;
       return b;
     };
+    while (hashg && hash_slots > 512 && lds_need() > lds_budget) hash_slots /= 2;
     while (lds_need() > lds_budget) {
       int big = -1;
       for (int c = 0; c < nc; ++c)
@@ -3192,7 +3210,9 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       J.gcol.push_back(K.gcol[g]);
       J.gmul.push_back(K.gmul[g]);
       J.gshift.push_back(K.gshift[g]);
+      J.ghi.push_back(K.ghi[g] ? 1 : 0);
     }
+    J.hash_slots = (J.group_mode == G_HASH64 || J.group_mode == G_HASH128) ? hash_slots : 0;
     if (P.use_part) {
       J.keybits = P.part_keybits;
       J.emit_col = P.part_vcol;
@@ -3351,6 +3371,10 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
       G.args.part_cstride = P.part_slab ? 1 : kCursorStride;
       G.args.part_nwg = P.part_nwg;
       G.args.part_hi = P.part_hi;
+      G.args.hkeys = P.kq.keys;
+      G.args.hstate = P.kq.key_state;
+      G.args.hash_cap = P.kq.hash_cap;
+      G.args.overflow = P.kq.overflow;
       void* params[] = {&G.args};
       PGX_LAUNCH(st, "pgxq", hipModuleLaunchKernel(static_cast<hipFunction_t>(G.fn), G.grid, 1, 1, G.T, 1, 1, 0, st, params,
                                       nullptr),
@@ -4909,7 +4933,13 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     P.jit.clear();
   }
   const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
-  if (hash) P.hash_cap = initial_hash_cap(segs, n, P);
+  if (hash) {
+    P.hash_cap = initial_hash_cap(segs, n, P);
+    // the generated kernels pre-aggregate in LDS and send the global table distinct keys only: start at 1M slots
+    // (the overflow count grows it 4x and reruns), not at one slot per row of a wide key space -- a 64M-slot table
+    // costs more to clear and compact than the scan (C7: 330 ms of host and device per query)
+    if (!P.jit.empty()) P.hash_cap = std::min<uint64_t>(P.hash_cap, uint64_t(1) << 20);
+  }
   for (int attempt = 0; attempt < 6; ++attempt) {
     alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
     reset_outputs(P, B, st);

@@ -264,6 +264,9 @@ struct JitShape {
   std::vector<int> gshift;
   int keybits = 0;
   int emit_col = -1;
+  // G_HASH64 / G_HASH128: group ids at gshift of the low (ghi 0) or high (ghi 1) key word; hash_slots LDS slots
+  std::vector<int> ghi;
+  int hash_slots = 0;
   bool leafmask = false;  // write every leaf's per-row predicate bit (statistics automaton input, pgx_stats.cpp)
   // LEAF_RCHUNK leaves, in leaf order: the bitmap program's postfix ops (RP_*), identical for the group's segments
   std::vector<std::vector<int>> rprog_ops;

@@ -92,7 +92,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const int ncols = int(s.cols.size());
   const int U = s.TL / s.R;
   const bool emit = s.group_mode == G_EMIT;
-  const bool grouped = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL || emit;
+  const bool hashm = s.group_mode == G_HASH64 || s.group_mode == G_HASH128;
+  const bool h128 = s.group_mode == G_HASH128;
+  const bool grouped = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL || emit || hashm;
   // ---- LDS layout: images, then the dense group table ----
   std::vector<int> img_off(ncols, -1);
   int lds = 0;
@@ -105,6 +107,21 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   if (s.group_mode == G_DENSE_LDS) {
     tab_off = lds;
     lds += int(s.dense_slots) * s.num_planes * 8;
+  }
+  // hash group-by: LDS keys (1 or 2 words per slot), 128-bit key states, planes x hash_slots
+  int hk_off = -1, hst_off = -1, ht_off = -1;
+  const int HS = s.hash_slots;
+  if (hashm) {
+    lds = (lds + 15) & ~15;
+    hk_off = lds;
+    lds += HS * 8 * (h128 ? 2 : 1);
+    if (h128) {
+      hst_off = lds;
+      lds += HS * 4;
+    }
+    lds = (lds + 15) & ~15;
+    ht_off = lds;
+    lds += HS * s.num_planes * 8;
   }
   // G_EMIT: per-wave LDS staging of the records, so that they leave as 64 lanes x 8 contiguous bytes per store
   // instead of R-strided 8-byte stores (each lane owns R consecutive rows).  A lane's R records sit at a pitch of
@@ -236,6 +253,19 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ind--;
     e.ln("}");
     e.ind--;
+    e.ln("}");
+  }
+  if (hashm) {
+    e.ln("u64* const hk = (u64*)(lds + ", hk_off / 4, ");");
+    if (h128) e.ln("u32* const hst = lds + ", hst_off / 4, ";");
+    e.ln("u64* const ht = (u64*)(lds + ", ht_off / 4, ");");
+    e.ln("for (int i = tid; i < ", HS * (h128 ? 2 : 1), "; i += PT) hk[i] = ~0ull;");
+    if (h128) e.ln("for (int i = tid; i < ", HS, "; i += PT) hst[i] = 0u;");
+    e.ln("for (int i = tid; i < ", HS * s.num_planes, "; i += PT) {");
+    e.ln("  u64 z = 0ull;");
+    for (int p = 1; p < s.num_planes; ++p)
+      if (s.plane_op[p] == P_MIN_ORD) e.ln("  if (i / ", HS, " == ", p, ") z = ~0ull;");
+    e.ln("  ht[i] = z;");
     e.ln("}");
   }
   e.ln("__syncthreads();");
@@ -744,6 +774,59 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ind = 6;
       e.ln("}");
     };
+    // hash group-by: the packed raw key (LONG_MAP / ARRAY_MAP, DefaultGroupKeyGenerator.java:239-246), a slot of the
+    // workgroup's LDS table, or of the global table when the LDS one has no room for it
+    auto emit_hash = [&]() {
+      e.ln("if (m) {");
+      e.ind = 7;
+      std::string klo = "0ull", khi = "0ull";
+      for (size_t g = 0; g < s.gcol.size(); ++g) {
+        const int c = s.gcol[g];
+        std::string id = "v" + std::to_string(c) + "[j]";
+        if (s.cols[c].remap) id = gremap[g] ? "gr" + std::to_string(g) + "[j]" : "(u32)rm" + std::to_string(g) + "[" + id + "]";
+        const std::string part = " | ((u64)" + id + " << " + std::to_string(s.gshift[g]) + ")";
+        if (h128 && s.ghi[g]) khi += part;
+        else klo += part;
+      }
+      e.ln("const u64 klo = ", klo, ";");
+      if (h128) e.ln("const u64 khi = ", khi, ";");
+      e.ln("const int ls = ", h128 ? "pgx_lhash128(hk, hst, " + std::to_string(HS) + ", klo, khi)"
+                                   : "pgx_lhash64(hk, " + std::to_string(HS) + ", klo)", ";");
+      std::vector<std::string> encs(naggs);
+      for (int a = 0; a < naggs; ++a) {
+        const int k = s.agg_kind[a];
+        if (k == A_COUNT) continue;
+        const int c = s.agg_col[a];
+        const JitCol& C = s.cols[c];
+        const std::string id = "v" + std::to_string(c) + "[j]";
+        std::string val;
+        if (C.fp) val = (C.img == IMG_F64) ? "((const double*)lds)[" + std::to_string(img_off[c] / 8) + " + " + id + "]"
+                                            : (gcolv[c] ? "gv" + std::to_string(c) + "[j]" : "dd" + std::to_string(c) + "[" + id + "]");
+        else if (C.img == IMG_NONE) val = gcolv[c] ? "gv" + std::to_string(c) + "[j]" : "di" + std::to_string(c) + "[" + id + "]";
+        else val = "(vb" + std::to_string(c) + " + (i64)" + img_value(s, c, img_off, id) + ")";
+        if (k == A_MIN || k == A_MAX) encs[a] = C.fp ? "pgx_ord_f64(" + val + ")" : "pgx_ord_i64(" + val + ")";
+        else encs[a] = C.fp ? "pgx_f64_bits(" + val + ")" : "(u64)" + val;
+      }
+      e.ln("if (ls >= 0) {");
+      e.ln("  atomicAdd(&ht[ls], 1ull);");
+      for (int a = 0; a < naggs; ++a)
+        if (s.agg_kind[a] != A_COUNT)
+          e.ln("  ", plane_atomic(s.plane_op[a + 1], "&ht[" + std::to_string((a + 1) * HS) + " + ls]", encs[a]));
+      e.ln("} else {");
+      e.ln("  const long long gs = ", h128 ? "pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, klo, khi)"
+                                           : "pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, klo)", ";");
+      e.ln("  if (gs < 0) {");
+      e.ln("    atomicAdd(A.overflow, 1ull);");
+      e.ln("  } else {");
+      e.ln("    atomicAdd(A.table + gs, 1ull);");
+      for (int a = 0; a < naggs; ++a)
+        if (s.agg_kind[a] != A_COUNT)
+          e.ln("    ", plane_atomic(s.plane_op[a + 1], "A.table + " + std::to_string(a + 1) + " * A.hash_cap + gs", encs[a]));
+      e.ln("  }");
+      e.ln("}");
+      e.ind = 6;
+      e.ln("}");
+    };
     if (!grouped) {
       for (int a = 0; a < naggs; ++a) {
         const int k = s.agg_kind[a];
@@ -802,6 +885,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         }
         e.ln("}");
         e.ln("recs[j] = rec;");
+      } else if (hashm) {
+        emit_hash();
       } else {
         emit_dense();
       }
@@ -818,7 +903,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("    for (int j = 0; j < PR; ++j) {");
       e.ind = 6;
       e.ln("const bool m = (rest >> j) & 1u;");
-      emit_dense();
+      if (hashm) emit_hash();
+      else emit_dense();
       e.ind = 5;
       e.ln("    }");
       e.ln("  }");
@@ -1076,6 +1162,26 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("  }");
   e.ln("}");
   e.ln("__syncthreads();");
+  if (hashm) {  // the workgroup's LDS table into the global one (identity planes merge harmlessly)
+    e.ln("for (int i = tid; i < ", HS, "; i += PT) {");
+    if (h128) {
+      e.ln("  if (hst[i] != 2u) continue;");
+      e.ln("  const long long gs = pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, hk[2 * i], hk[2 * i + 1]);");
+    } else {
+      e.ln("  if (hk[i] == ~0ull) continue;");
+      e.ln("  const long long gs = pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, hk[i]);");
+    }
+    e.ln("  if (gs < 0) {");
+    e.ln("    atomicAdd(A.overflow, ht[i]);");
+    e.ln("    continue;");
+    e.ln("  }");
+    e.ln("  atomicAdd(A.table + gs, ht[i]);");
+    for (int a = 0; a < naggs; ++a)
+      if (s.agg_kind[a] != A_COUNT)
+        e.ln("  ", plane_atomic(s.plane_op[a + 1], "A.table + " + std::to_string(a + 1) + " * A.hash_cap + gs",
+                               "ht[" + std::to_string((a + 1) * HS) + " + i]"));
+    e.ln("}");
+  }
   if (enarrow) {  // the rings' last partial units, then the slab fills (every record, also past part_cap)
     const std::string NR = std::to_string(kNarrowRing);
     e.ln("for (int x = tid; x < 256 * 32; x += PT) {");
@@ -1173,6 +1279,8 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.selmask);
   k.push_back(s.part_narrow);
   k.push_back(s.narrow_vbits);
+  add(s.ghi);
+  k.push_back(s.hash_slots);
   return k;
 }
 
@@ -1609,6 +1717,28 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.agg_col = {1};
     s.plane_op = {P_ADD_I64, P_ADD_I64};
     s.num_planes = 2;
+    shapes.push_back(s);
+  }
+  for (int gm : {G_HASH64, G_HASH128}) {  // hash group-by: LDS table + global overflow, remapped group ids
+    JitShape s = base(8, 16, IMG_U32, 0);
+    for (int c = 2; c < 5; ++c) {
+      JitCol C;
+      C.bits = 14;
+      C.decode = true;
+      C.remap = c == 3;
+      s.cols.push_back(C);
+    }
+    s.R = 16;
+    s.group_mode = gm;
+    s.gcol = {2, 3, 4, 0};
+    s.gmul = {1, 1, 1, 1};
+    s.gshift = gm == G_HASH128 ? std::vector<int>{0, 14, 28, 0} : std::vector<int>{0, 14, 28, 42};
+    s.ghi = gm == G_HASH128 ? std::vector<int>{0, 0, 0, 1} : std::vector<int>{0, 0, 0, 0};
+    s.hash_slots = 1024;
+    s.agg_kind = {A_SUM, A_MIN, A_MAX, A_COUNT};
+    s.agg_col = {1, 1, 1, -1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64, P_MIN_ORD, P_MAX_ORD, P_ADD_I64};
+    s.num_planes = 5;
     shapes.push_back(s);
   }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {

@@ -73,6 +73,10 @@ struct JArgs {
   long long part_nwg;                // (b, w) holds records at table + (b * part_nwg + w) * part_cap, its count at
                                      // part_cursor[(b * part_nwg + w) * part_cstride]
   unsigned short* part_hi;           // narrow records wider than 32 bits: bits 32..47, same index as the u32 in table
+  unsigned long long* hkeys;         // hash group-by: the global table's keys (1 or 2 words per slot),
+  unsigned int* hstate;              // its 128-bit key states,
+  long long hash_cap;                // its slots (a power of two; planes at table + p * hash_cap)
+  unsigned long long* overflow;      // keys that found no global slot (the host grows the table and reruns)
 };
 
 #endif  // PGX_JIT_ABI_H_

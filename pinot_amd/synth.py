@@ -103,6 +103,14 @@ WORKLOADS: Dict[str, Workload] = {
                    "SELECT SUM(m) FROM T WHERE " + " OR ".join(
                        "w%d < %d" % (i, C6_CUT[i % 3]) for i in range(10))
                    + " GROUP BY gk TOP 10", 6, "weak"),
+    # C7: an ARRAY_MAP group key (five 14-bit columns: 70 bits > 64, DefaultGroupKeyGenerator.java:167-186) over 1024
+    # distinct combinations (paired columns), the shape that ran on the interpreter kernel before (VERDICT r03
+    # missing #3); not a BASELINE config
+    "c7": Workload("c7", "ARRAY_MAP group-by: five 14-bit group columns (70-bit keys, 1024 distinct combinations), "
+                   "sum(m) over a 4096-value metric: 4 x 125M rows",
+                   4, 125_000_000,
+                   [ColSpec("h%d" % i, 16384, paired=True) for i in range(5)] + [ColSpec("m", 4096, "metric")],
+                   "SELECT SUM(m) FROM T GROUP BY h0, h1, h2, h3, h4 TOP 10", 7, "weak", npairs=1024),
 }
 
 

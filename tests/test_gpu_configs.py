@@ -241,3 +241,48 @@ def test_c6_twelve_columns_in_query_kernel(ctx):
         assert st == [int(counts.sum()), sum(r["entries"] for r in res), 2 * int(counts.sum()), 2 * rows]
     finally:
         data.free()
+
+
+def test_c7_array_map_keys_in_query_kernel(ctx):
+    """C7: five 14-bit group columns = a 70-bit ARRAY_MAP key (G_HASH128), 1024 distinct combinations.  The step runs
+    the generated kernel (LDS hash table per workgroup, global table for what does not fit), not the interpreter, and
+    every group's sum / count equals numpy over the regenerated dictIds; statistics too."""
+    import json
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    L = N.lib()
+    wl = synth.WORKLOADS["c7"]
+    rows = 2_000_000 + 77
+    seg_ids = [0, 1]
+    data = synth.DeviceSegments(ctx, wl, seg_ids, rows=rows)
+    try:
+        q = pql.compile(wl.query)
+        N.check(L.pgx_timing_start(ctx.handle))
+        blk = E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(data.segments, q).execute()
+        out = (C.c_double * 3)()
+        js = C.create_string_buffer(8192)
+        N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
+        kernels = json.loads(js.value.decode())["kernels"]
+        assert "pgxq" in kernels and "pgx_scan_kernel" not in kernels, kernels
+        got = blk.get_aggregation_group_by_result().as_map()
+        mvals = synth.make_dictionary("metric", 4096).astype(np.float64)
+        acc = {}
+        for s in seg_ids:
+            ids = {}
+            for ci, c in enumerate(wl.columns):
+                pair = dict(pair_seed=synth.column_seed(wl.seed, s, 99), npairs=wl.npairs) if c.paired else {}
+                seed = synth.column_seed(wl.seed, 0 if c.paired else s, ci)
+                ids[c.name] = c_oracle.dict_ids(c_oracle.synth_fwd(seed, rows, c.bits, c.card, **pair), rows, c.bits)
+            keys = np.stack([ids["h%d" % i] for i in range(5)], axis=1)
+            uk, inv = np.unique(keys, axis=0, return_inverse=True)
+            sums = np.bincount(inv.ravel(), weights=mvals[ids["m"]])
+            for k, v in zip(uk, sums):
+                t = "\t".join(str(int(x)) for x in k)
+                acc[t] = acc.get(t, 0.0) + float(v)
+        assert 900 <= len(acc) <= 1024
+        assert set(got) == set(acc)
+        for k, v in acc.items():
+            H.assert_values_equal(got[k], [v], ["sum"])
+        assert blk.stats.as_list() == [2 * rows, 0, 6 * 2 * rows, 2 * rows]  # 6 projected columns
+    finally:
+        data.free()
