@@ -3213,6 +3213,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       J.ghi.push_back(K.ghi[g] ? 1 : 0);
     }
     J.hash_slots = (J.group_mode == G_HASH64 || J.group_mode == G_HASH128) ? hash_slots : 0;
+    if (const char* e = std::getenv("PGX_HASH_BATCH")) J.hash_batch = e[0] == '1';  // A/B (off by default)
     if (P.use_part) {
       J.keybits = P.part_keybits;
       J.emit_col = P.part_vcol;

@@ -267,6 +267,8 @@ struct JitShape {
   // G_HASH64 / G_HASH128: group ids at gshift of the low (ghi 0) or high (ghi 1) key word; hash_slots LDS slots
   std::vector<int> ghi;
   int hash_slots = 0;
+  bool hash_batch = false;  // hash group-by: every row's home-slot read of a sub-step issued before any is resolved
+                            // (PGX_HASH_BATCH=1; measured slower at C7: 8.1 vs 5.1 ms, register pressure)
   bool leafmask = false;  // write every leaf's per-row predicate bit (statistics automaton input, pgx_stats.cpp)
   // LEAF_RCHUNK leaves, in leaf order: the bitmap program's postfix ops (RP_*), identical for the group's segments
   std::vector<std::vector<int>> rprog_ops;

@@ -593,6 +593,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
           e.ln("u32 p", a, " = 0u;");
       }
     if (emit) e.ln("u64 recs[PR];");
+    const bool hbatch = hashm && s.hash_batch;
+    if (hbatch) {
+      e.ln("u32 hm = 0u, hq[PR], hsv[PR];");
+      e.ln(h128 ? "pgx_u32x4 hkv[PR];" : "u64 hkv[PR];");
+    }
     if (split) e.ln("u32 msk = 0u;");
     if (s.selmask) e.ln("u32 smk = 0u;");
     if (s.leafmask)
@@ -776,8 +781,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     };
     // hash group-by: the packed raw key (LONG_MAP / ARRAY_MAP, DefaultGroupKeyGenerator.java:239-246), a slot of the
     // workgroup's LDS table, or of the global table when the LDS one has no room for it
-    auto emit_hash = [&]() {
-      e.ln("if (m) {");
+    auto emit_hash = [&](bool resolve) {
+      e.ln(resolve ? "if ((hm >> j) & 1u) {" : "if (m) {");
       e.ind = 7;
       std::string klo = "0ull", khi = "0ull";
       for (size_t g = 0; g < s.gcol.size(); ++g) {
@@ -790,8 +795,30 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       }
       e.ln("const u64 klo = ", klo, ";");
       if (h128) e.ln("const u64 khi = ", khi, ";");
-      e.ln("const int ls = ", h128 ? "pgx_lhash128(hk, hst, " + std::to_string(HS) + ", klo, khi)"
-                                   : "pgx_lhash64(hk, " + std::to_string(HS) + ", klo)", ";");
+      if (hbatch && !resolve) {  // pass 1: the home slot's state and key, read back to back for every row
+        e.ln("const int h = (int)(", h128 ? "pgx_mix64(klo ^ pgx_mix64(khi))" : "pgx_mix64(klo)", " & ", HS - 1, "ull);");
+        e.ln("hq[j] = (u32)h;");
+        if (h128) {
+          e.ln("hsv[j] = hst[h];");
+          e.ln("hkv[j] = *(const pgx_u32x4*)(hk + 2 * h);");
+        } else {
+          e.ln("hkv[j] = hk[h];");
+        }
+        e.ln("hm |= 1u << j;");
+        e.ind = 6;
+        e.ln("}");
+        return;
+      }
+      if (hbatch) {  // pass 2: a home slot that held the key needs no probe
+        if (h128)
+          e.ln("const int ls = (hsv[j] == 2u && (((u64)hkv[j].y << 32) | hkv[j].x) == klo && (((u64)hkv[j].w << 32) | hkv[j].z) == khi) ? (int)hq[j] : pgx_lhash128(hk, hst, ",
+               HS, ", klo, khi);");
+        else
+          e.ln("const int ls = hkv[j] == klo ? (int)hq[j] : pgx_lhash64(hk, ", HS, ", klo);");
+      } else {
+        e.ln("const int ls = ", h128 ? "pgx_lhash128(hk, hst, " + std::to_string(HS) + ", klo, khi)"
+                                     : "pgx_lhash64(hk, " + std::to_string(HS) + ", klo)", ";");
+      }
       std::vector<std::string> encs(naggs);
       for (int a = 0; a < naggs; ++a) {
         const int k = s.agg_kind[a];
@@ -886,13 +913,21 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         e.ln("}");
         e.ln("recs[j] = rec;");
       } else if (hashm) {
-        emit_hash();
+        emit_hash(false);
       } else {
         emit_dense();
       }
     }
     e.ind = 5;
     e.ln("}");
+    if (hbatch) {  // pass 2 of the batched hash updates
+      e.ln("#pragma unroll");
+      e.ln("for (int j = 0; j < PR; ++j) {");
+      e.ind = 6;
+      emit_hash(true);
+      e.ind = 5;
+      e.ln("}");
+    }
     if (sel) {  // rows past a lane's first sel_k selected ones: the per-row loop, entered only if some lane has them
       e.ln("{");
       e.ln("  u32 rest = msk;");
@@ -903,7 +938,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("    for (int j = 0; j < PR; ++j) {");
       e.ind = 6;
       e.ln("const bool m = (rest >> j) & 1u;");
-      if (hashm) emit_hash();
+      if (hashm) emit_hash(false);
       else emit_dense();
       e.ind = 5;
       e.ln("    }");
@@ -1281,6 +1316,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.narrow_vbits);
   add(s.ghi);
   k.push_back(s.hash_slots);
+  k.push_back(s.hash_batch);
   return k;
 }
 
