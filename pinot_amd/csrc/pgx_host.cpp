@@ -2773,7 +2773,8 @@ void build_arena(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B) {
   B.off_jsegs = align_up(B.off_ksegs + n * sizeof(KSeg), 256);
   P.star_tile_cap = 0;
   for (int s = 0; s < int(n); ++s)
-    if (!P.star.empty() && P.star[s].on) P.star_tile_cap += size_t(P.ksegs[s].num_docs) / 8192 + 2;
+    // tiles of at least 256 threads x 8 rows (plan_jit may shrink rows per lane per tile to 8 for wide queries)
+    if (!P.star.empty() && P.star[s].on) P.star_tile_cap += size_t(P.ksegs[s].num_docs) / 2048 + 2;
   B.off_tiles = align_up(B.off_jsegs + n * sizeof(JSeg), 256);
   B.off_rdesc = align_up(B.off_tiles + P.star_tile_cap * 4, 256);
   B.off_rprog = align_up(B.off_rdesc + P.roar.size() * sizeof(RDesc), 256);

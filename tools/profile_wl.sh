@@ -24,4 +24,5 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$KRX" -d 
 ROWS=$(python3 -c "import json; print(json.load(open('$OUT/bench.json'))['config']['rows_per_segment'])")
 python3 tools/pmc_traffic.py $OUT/pmc_fetch/${WL}_counter_collection.csv,$OUT/pmc_write/${WL}_counter_collection.csv \
   "$KLIST" $WL $ROWS $OUT/traffic_$WL.json $PSTEPS
+python3 tools/reconcile.py $OUT/trace/${WL}_kernel_trace.csv $OUT/bench.json $OUT/reconcile_$WL.json > /dev/null || true
 rm -f $OUT/pmc_fetch/*_counter_collection.csv $OUT/pmc_write/*_counter_collection.csv $OUT/trace/*_kernel_trace.csv
