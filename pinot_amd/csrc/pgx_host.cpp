@@ -3228,8 +3228,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     // COUNT + one integer SUM / AVG over a dense LDS table: one packed 64-bit add per row when, for every segment of
     // the group, its rows fit the count field and rows x value range fit the offset field (flushed per segment);
     // PGX_DENSE_PACK=0 keeps two adds
-    if (K.group_mode == G_DENSE_LDS && K.num_planes == 2 && K.num_aggs == 1 &&
-        (K.agg_kind[0] == A_SUM || K.agg_kind[0] == A_AVG) && !P.use_part) {
+    if ((K.group_mode == G_DENSE_LDS || K.group_mode == G_HASH64 || K.group_mode == G_HASH128) &&
+        K.num_planes == 2 && K.num_aggs == 1 && (K.agg_kind[0] == A_SUM || K.agg_kind[0] == A_AVG) && !P.use_part) {
       const int c = K.agg_col[0];
       const char* e = std::getenv("PGX_DENSE_PACK");
       if (!(e && e[0] == '0') && c >= 0 && J.cols[c].img != IMG_NONE && !J.cols[c].fp) {

@@ -429,6 +429,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const bool pack = s.dense_pack > 0 && s.group_mode == G_DENSE_LDS && s.num_planes == 2 && naggs == 1 &&
                     (s.agg_kind[0] == A_SUM || s.agg_kind[0] == A_AVG) && !s.cols[s.agg_col[0]].fp &&
                     s.cols[s.agg_col[0]].img != IMG_NONE && !emit;
+  // the same packed count + value-offset add in the LDS hash table (flushed per segment into the global table)
+  const bool hpack = s.dense_pack > 0 && hashm && s.num_planes == 2 && naggs == 1 &&
+                     (s.agg_kind[0] == A_SUM || s.agg_kind[0] == A_AVG) && !s.cols[s.agg_col[0]].fp &&
+                     s.cols[s.agg_col[0]].img != IMG_NONE;
   bool sel = s.sel_k > 0 && dense_g && !emit && !compact;
   for (int c = 0; c < ncols && sel; ++c) sel = !gcolv[c];
   for (size_t g = 0; g < s.gcol.size() && sel; ++g) sel = !gremap[g];
@@ -835,10 +839,16 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         else encs[a] = C.fp ? "pgx_f64_bits(" + val + ")" : "(u64)" + val;
       }
       e.ln("if (ls >= 0) {");
-      e.ln("  atomicAdd(&ht[ls], 1ull);");
-      for (int a = 0; a < naggs; ++a)
-        if (s.agg_kind[a] != A_COUNT)
-          e.ln("  ", plane_atomic(s.plane_op[a + 1], "&ht[" + std::to_string((a + 1) * HS) + " + ls]", encs[a]));
+      if (hpack) {
+        const int c = s.agg_col[0];
+        e.ln("  atomicAdd(&ht[ls], (1ull << ", s.dense_pack, ") + (u64)", img_value(s, c, img_off, "v" + std::to_string(c) + "[j]"),
+             ");");
+      } else {
+        e.ln("  atomicAdd(&ht[ls], 1ull);");
+        for (int a = 0; a < naggs; ++a)
+          if (s.agg_kind[a] != A_COUNT)
+            e.ln("  ", plane_atomic(s.plane_op[a + 1], "&ht[" + std::to_string((a + 1) * HS) + " + ls]", encs[a]));
+      }
       e.ln("} else {");
       e.ln("  const long long gs = ", h128 ? "pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, klo, khi)"
                                            : "pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, klo)", ";");
@@ -1170,6 +1180,26 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("}");
     }
   }
+  if (hpack) {  // per-segment flush of the packed LDS hash planes into the global table (the keys stay)
+    const int c = s.agg_col[0];
+    const std::string mask = std::to_string((1ull << s.dense_pack) - 1ull) + "ull";
+    e.ln("__syncthreads();");
+    e.ln("for (int i = tid; i < ", HS, "; i += PT) {");
+    e.ln("  const u64 x = ht[i];");
+    e.ln("  if (x == 0ull) continue;");
+    e.ln("  const long long gs = ", h128 ? "pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, hk[2 * i], hk[2 * i + 1])"
+                                         : "pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, hk[i])", ";");
+    e.ln("  const u64 cnt = x >> ", s.dense_pack, ";");
+    e.ln("  if (gs < 0) {");
+    e.ln("    atomicAdd(A.overflow, cnt);");
+    e.ln("  } else {");
+    e.ln("    atomicAdd(A.table + gs, cnt);");
+    e.ln("    atomicAdd(A.table + A.hash_cap + gs, (x & ", mask, ") + cnt * (u64)vb", c, ");");
+    e.ln("  }");
+    e.ln("  ht[i] = 0ull;");
+    e.ln("}");
+    e.ln("__syncthreads();");
+  }
   if (pack) {  // per-segment flush of the packed table: counts and sums (offset sums + count * this segment's vbase)
     const int c = s.agg_col[0];
     const std::string mask = std::to_string((1ull << s.dense_pack) - 1ull) + "ull";
@@ -1197,7 +1227,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("  }");
   e.ln("}");
   e.ln("__syncthreads();");
-  if (hashm) {  // the workgroup's LDS table into the global one (identity planes merge harmlessly)
+  if (hashm && !hpack) {  // the workgroup's LDS table into the global one (identity planes merge harmlessly)
     e.ln("for (int i = tid; i < ", HS, "; i += PT) {");
     if (h128) {
       e.ln("  if (hst[i] != 2u) continue;");
@@ -1775,6 +1805,12 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.agg_col = {1, 1, 1, -1};
     s.plane_op = {P_ADD_I64, P_ADD_I64, P_MIN_ORD, P_MAX_ORD, P_ADD_I64};
     s.num_planes = 5;
+    shapes.push_back(s);
+    s.agg_kind = {A_SUM};  // packed count + value offset in one LDS add, flushed per segment
+    s.agg_col = {1};
+    s.plane_op = {P_ADD_I64, P_ADD_I64};
+    s.num_planes = 2;
+    s.dense_pack = 40;
     shapes.push_back(s);
   }
   for (int gm : {G_DENSE_LDS, G_DENSE_GLOBAL}) {
