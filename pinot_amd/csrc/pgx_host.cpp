@@ -523,6 +523,8 @@ struct StagedColumn {
 };
 
 std::atomic<uint64_t> g_segment_uid{1};
+std::atomic<uint64_t> g_segment_frees{0};  // segments freed so far: a plan-cache entry whose segment pointers match
+                                           // and no segment was freed since it was kept needs no uid comparison
 
 struct pgx_segment {
   pgx_ctx* ctx = nullptr;
@@ -4689,6 +4691,8 @@ namespace {
 struct PlanEntry {
   pgx_ctx* ctx = nullptr;
   std::vector<uint64_t> uids;
+  std::vector<pgx_segment*> ptrs;  // the segment list as passed, and g_segment_frees when last matched
+  uint64_t gen = 0;
   uint64_t key = 0;
   std::unique_ptr<ExecPlan> P;
   std::unique_ptr<ExecBuffers> B;
@@ -4762,16 +4766,25 @@ uint64_t plan_key(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, in
   return h;
 }
 
-std::shared_ptr<PlanEntry> plan_cache_acquire(const pgx_query* q, const std::vector<uint64_t>& uids, uint64_t key) {
+std::shared_ptr<PlanEntry> plan_cache_acquire(const pgx_query* q, pgx_segment* const* segs, int n, uint64_t key) {
+  const uint64_t gen = g_segment_frees.load();
   std::lock_guard<std::mutex> g(g_pc_mu);
   auto it = g_pc.find(q);
   if (it == g_pc.end()) return nullptr;
-  for (auto& e : it->second)
-    if (!e->busy && e->key == key && e->uids == uids) {
-      e->busy = true;
-      e->stamp = ++g_pc_clock;
-      return e;
+  for (auto& e : it->second) {
+    if (e->busy || e->key != key || e->ptrs.size() != size_t(n) ||
+        std::memcmp(e->ptrs.data(), segs, sizeof(pgx_segment*) * size_t(n)) != 0)
+      continue;
+    if (e->gen != gen) {  // a segment was freed since: the same addresses may hold other segments
+      bool same = true;
+      for (int s = 0; s < n && same; ++s) same = segs[s]->uid == e->uids[size_t(s)];
+      if (!same) continue;
+      e->gen = gen;
     }
+    e->busy = true;
+    e->stamp = ++g_pc_clock;
+    return e;
+  }
   return nullptr;
 }
 
@@ -4800,11 +4813,13 @@ void plan_cache_release(const std::shared_ptr<PlanEntry>& e) {
 }
 
 // after a successful execution of a cacheable plan: keep it (the oldest idle entry makes room)
-void plan_cache_insert(const pgx_query* q, pgx_ctx* ctx, std::vector<uint64_t> uids, uint64_t key,
-                       std::unique_ptr<ExecPlan> P, std::unique_ptr<ExecBuffers> B) {
+void plan_cache_insert(const pgx_query* q, pgx_ctx* ctx, pgx_segment* const* segs, int n, std::vector<uint64_t> uids,
+                       uint64_t key, std::unique_ptr<ExecPlan> P, std::unique_ptr<ExecBuffers> B) {
   auto e = std::make_shared<PlanEntry>();
   ctx->refs.fetch_add(1);
   e->ctx = ctx;
+  e->gen = g_segment_frees.load();
+  e->ptrs.assign(segs, segs + n);
   e->uids = std::move(uids);
   e->key = key;
   e->P = std::move(P);
@@ -4862,10 +4877,8 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   std::vector<uint64_t> uids;
   uint64_t pkey = 0;
   if (cache) {
-    uids.resize(size_t(n));
-    for (int s = 0; s < n; ++s) uids[size_t(s)] = segs[s]->uid;
     pkey = plan_key(ctx, q, segs, n, bindings, xflags);
-    if (auto e = plan_cache_acquire(&q, uids, pkey)) {
+    if (auto e = plan_cache_acquire(&q, segs, n, pkey)) {
       struct Rel {
         const std::shared_ptr<PlanEntry>& e;
         ~Rel() { plan_cache_release(e); }
@@ -4899,6 +4912,10 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   if (mv_fn) {  // aggregation-only: the partials combine per function (combine_partial), on any device count
     run_mv(ctx, q, segs, n, bindings, xflags, R, st);
     return;
+  }
+  if (cache) {
+    uids.resize(size_t(n));
+    for (int s = 0; s < n; ++s) uids[size_t(s)] = segs[s]->uid;
   }
   const bool again = cache && plan_cache_seen_before(&q, pkey, uids);
   if (!dom && !again && run_batched(ctx, q, segs, n, bindings, opts, R, st, xflags, hp)) return;
@@ -4957,7 +4974,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   }
   complete_scan(ctx, q, P, B, segs, n, opts, st, R);
   hp.mark("finish");
-  if (cache && plan_cacheable(P)) plan_cache_insert(&q, ctx, std::move(uids), pkey, std::move(Pp), std::move(Bp));
+  if (cache && plan_cacheable(P)) plan_cache_insert(&q, ctx, segs, n, std::move(uids), pkey, std::move(Pp), std::move(Bp));
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -5319,6 +5336,7 @@ pgx_status pgx_segment_release(pgx_segment* seg) {
     if (!seg) return;
     pgx_ctx* ctx = seg->ctx;
     delete seg;
+    g_segment_frees.fetch_add(1);
     if (ctx) ctx_unref(ctx);
   });
 }
