@@ -303,7 +303,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // value images already in LDS (segments sharing one dictionary share one image: not restaged per segment)
   for (int c = 0; c < ncols; ++c)
     if (s.cols[c].img != IMG_NONE) e.ln("const void* imgp", c, " = nullptr;");
-  e.ln("int seg = pgx_find_seg(A.segs, A.num_segs, tb);");
+  e.ln("int seg = __builtin_amdgcn_readfirstlane(pgx_find_seg(A.segs, A.num_segs, tb));  // workgroup-uniform");
   e.ln("long long t = tb;");
   e.ln("while (t < te) {");
   e.ind = 2;
@@ -352,7 +352,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   };
   // per-segment pointers and leaf parameters
   for (int c = 0; c < ncols; ++c)
-    if (s.cols[c].decode) e.ln("const u32* __restrict__ f", c, " = S->fwd[", c, "];");
+    if (s.cols[c].decode) e.ln("const u32* __restrict__ f", c, " = pgx_sgpr(S->fwd[", c, "]);");
   const int nleaves = int(s.leaf_col.size());
   for (int l = 0; l < nleaves; ++l) {
     switch (s.leaf_mode[l]) {
@@ -474,7 +474,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   auto emit_loads = [&](const std::string& tile, const std::string& dst) {
     e.ln("{");
     e.ind++;
-    e.ln("const int rb = (int)((tl ? (long long)tl[", tile, " - tile0] : (", tile, " - tile0)) * (PT * PTL));");
+    e.ln("rbn = (int)((tl ? (long long)tl[", tile, " - tile0] : (", tile, " - tile0)) * (PT * PTL));");
+    e.ln("const int rb = rbn;");
     e.ln("const bool full = rb + PT * PTL <= nd;");
     for (int u = 0; u < U; ++u) {
       e.ln("{");
@@ -503,6 +504,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     if (s.cols[c].decode) e.ln("u32 n", c, "[", U * dwords_per(s, c), "];");
   for (int l = 0; l < nleaves; ++l)
     if (is_docmask(s.leaf_mode[l])) e.ln("u32 nq", l, "[", U, "];");
+  // first row of the tile whose raw words are in flight: carried into the next iteration, so the loop body never
+  // reloads the tile list after issuing the prefetch (that load's wait would also wait for the prefetch)
+  e.ln("int rbn;");
   emit_loads("t", "n");
   emit_images();
   e.ln("for (long long tt = t; tt < t2; ++tt) {");
@@ -520,9 +524,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("#pragma unroll");
       e.ln("for (int i = 0; i < ", U, "; ++i) cq", l, "[i] = nq", l, "[i];");
     }
+  e.ln("const int rb = rbn;");
   e.ln("if (tt + 1 < t2) ");
   emit_loads("tt + 1", "n");
-  e.ln("const int rb = (int)((tl ? (long long)tl[tt - tile0] : (tt - tile0)) * (PT * PTL));");
   if (scr_off >= 0) {
     // a tile (PT * PTL rows) lies inside one 65536-doc chunk: build that chunk's program masks when it changes (the next
     // tile's forward-index loads are already in flight)
