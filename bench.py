@@ -22,7 +22,8 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "rows/sec for filter+group-by SUM at 1/2/4/8 GPUs; % of HBM roofline"
 # bounded CPU-baseline samples (segments, rows per segment): ~10-30 s of single-core work over 8 threads in total
-CPU_SAMPLE = {"c2": (8, 32_000_000), "c5": (64, 2_000_000), "c3": (8, 16_000_000), "c6": (8, 8_000_000)}
+CPU_SAMPLE = {"c2": (8, 32_000_000), "c5": (64, 2_000_000), "c3": (8, 16_000_000), "c3d": (8, 16_000_000),
+              "c6": (8, 8_000_000)}
 
 
 def source_hash():
@@ -98,7 +99,9 @@ def cpu_baseline(wl, query, seg_rows, nseg, threads):
                                          pair_seed=synth.column_seed(wl.seed, s, 99), npairs=wl.npairs)
             else:
                 fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), seg_rows, c.bits, c.card)
-            cols[c.name] = (fwd, c.bits, dicts[c.name], c.card)
+            dv = (synth.make_dictionary(c.dict_kind, c.card, s).astype(np.float64) if c.dict_kind == "metric_seg"
+                  else dicts[c.name])
+            cols[c.name] = (fwd, c.bits, dv, c.card)
             if c.inverted:  # the .bitmap.inv the GPU segments carry (synth.DeviceSegments._inverted_indexes)
                 invs[s][c.name] = c_oracle.inverted_build(
                     c_oracle.synth_ids(synth.column_seed(wl.seed, s, ci), seg_rows, c.card), c.card)
@@ -110,7 +113,7 @@ def cpu_baseline(wl, query, seg_rows, nseg, threads):
     kw = {"threads": threads, "metric": "m"}
     if wl.name == "c2":
         kw.update(filter_col="dA", lo=64, hi=191)
-    elif wl.name == "c3":
+    elif wl.name in ("c3", "c3d"):
         kw.update(group_cols=("g1", "g2"))
     elif wl.name == "c5":  # (f1 IN (...) OR f2 = 7) AND f3 <> 3 GROUP BY gk: leaves as dictId bitsets
         f1 = [int(v) for v in query["filter"]["children"][0]["children"][0]["values"]]

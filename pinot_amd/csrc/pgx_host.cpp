@@ -2050,18 +2050,26 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     for (int g = 0; g < K.num_gcols; ++g) keybits = std::max(keybits, K.gshift[g] + P.gbits[g]);
     int vbits = 0;
     int64_t vbase = 0;
+    bool same_dict = true;  // one dictionary in every segment: records may carry the dictId (narrow path)
     if (ok && vc >= 0) {
+      // Value records carry value - vbase with ONE query-wide vbase (the smallest value of any segment's dictionary):
+      // each segment's records are rebased by (its image base - vbase) in the scan (JSeg.emit_rebase), so segments
+      // with their own dictionaries (SegmentDictionaryCreator builds one per segment) share the radix path.
       const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
-      ok = (c0.data_type == PGX_INT || c0.data_type == PGX_LONG) && !c0.ivals.empty();
-      for (int s = 1; s < n && ok; ++s) {
+      int64_t vmin = 0, vmax = 0;
+      for (int s = 0; s < n && ok; ++s) {
         const StagedColumn& c = segs[s]->col(P.qcols[vc]);
-        ok = c.dict_hash == c0.dict_hash && c.card == c0.card && c.data_type == c0.data_type;
+        ok = (c.data_type == PGX_INT || c.data_type == PGX_LONG) && !c.ivals.empty() && c.data_type == c0.data_type;
+        if (!ok) break;
+        const int64_t lo = *std::min_element(c.ivals.begin(), c.ivals.end());
+        const int64_t hi = *std::max_element(c.ivals.begin(), c.ivals.end());
+        vmin = s ? std::min(vmin, lo) : lo;
+        vmax = s ? std::max(vmax, hi) : hi;
+        same_dict = same_dict && c.dict_hash == c0.dict_hash && c.card == c0.card;
       }
       if (ok) {
-        const int64_t vmin = *std::min_element(c0.ivals.begin(), c0.ivals.end());
-        const int64_t vmax = *std::max_element(c0.ivals.begin(), c0.ivals.end());
         const uint64_t range = uint64_t(vmax) - uint64_t(vmin);
-        ok = range <= 0xFFFFFFFFull && c0.vbase == vmin;
+        ok = range <= 0xFFFFFFFFull;
         vbase = vmin;
         vbits = ok ? bits_for(int64_t(range) + 1) : 64;
       }
@@ -2072,7 +2080,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     bool dictid = false;
     if (ok && vc >= 0) {
       const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
-      dictid = c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end()) &&
+      dictid = same_dict && c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end()) &&
                keybits + bits_for(c0.card) <= 63;
       // opt-in (PGX_PART_FUSED=1): measured at C3, the fused first pass saves 1.7 ms of scan + pass 1, but the
       // aggregation's per-record dictionary gathers (one 64-B L2 line each) cost 2.3 ms more than offset records.
@@ -2125,7 +2133,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         bool nok = true;
         if (vc >= 0) {
           const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
-          nok = c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end());
+          nok = same_dict && c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end());
           vd = bits_for(c0.card);
           if (c0.img_dev && c0.img_kind == IMG_FOR16 && c0.img_words <= kImgFor16Blocks + 32768) imgk = 2;
           else if (c0.img_dev && c0.img_kind == IMG_U32 && c0.img_words <= kImgFor16Blocks + 32768) imgk = 1;
@@ -3301,6 +3309,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         js.img_words[c] = J.cols[c].img != IMG_NONE ? col.img_words : 0;
         js.vbase[c] = col.vbase;
       }
+      js.emit_rebase = (P.use_part && P.part_vcol >= 0) ? P.segcols[s][P.part_vcol]->vbase - P.part_vbase : 0;
       if (P.rprog_on)
         for (size_t k = 0; k < P.dm_progs.size(); ++k)
           js.lbits[nleaves + k] = P.rchunk ? reinterpret_cast<const uint32_t*>(P.rprog_dev + s * P.dm_progs.size() + k)
@@ -5366,7 +5375,7 @@ struct pgx_mutable {
     DevBuf remap;                // arrival id -> sorted id
   };
   std::vector<Col> cols;
-  std::mutex mu;
+  mutable std::mutex mu;
 };
 
 pgx_status pgx_mutable_create(pgx_ctx* ctx, const char* name, int32_t capacity, int32_t num_columns,
@@ -5405,29 +5414,46 @@ pgx_status pgx_mutable_append(pgx_mutable* m, int32_t ndocs, const int32_t* cons
     std::lock_guard<std::mutex> g(m->mu);
     if (int64_t(m->num_docs) + ndocs > m->capacity) fail(PGX_ERR_INVALID_ARG, "realtime segment " + m->name + " full");
     if (!ndocs) return;
-    hip_check(hipSetDevice(m->ctx->device), "hipSetDevice");
-    hipStream_t st = m->ctx->stream;
-    for (size_t i = 0; i < m->cols.size(); ++i) {
-      pgx_mutable::Col& c = m->cols[i];
+    // Validate every column before any device or host state changes: a rejected batch leaves nvals, starts, max_id
+    // and num_docs exactly as they were (no half-appended multi-value column).
+    const size_t ncols = m->cols.size();
+    std::vector<int64_t> nv(ncols, ndocs);
+    std::vector<int32_t> top(ncols, -1), mvmax(ncols, 0);
+    for (size_t i = 0; i < ncols; ++i) {
+      const pgx_mutable::Col& c = m->cols[i];
       if (!ids[i] || (c.mv && (!counts || !counts[i]))) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": no ids");
-      int64_t nv = ndocs;
-      if (c.mv) {  // the new docs' starts, then the values
-        std::vector<int32_t> st_new(ndocs);
+      if (c.mv) {
         int64_t at = c.nvals;
         for (int32_t d = 0; d < ndocs; ++d) {
           if (counts[i][d] < 1) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": a multi-value doc needs a value");
           at += counts[i][d];
-          st_new[d] = int32_t(at);
-          c.max_mv = std::max(c.max_mv, counts[i][d]);
+          mvmax[i] = std::max(mvmax[i], counts[i][d]);
         }
         if (at > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "column " + c.name + ": too many values");
-        nv = at - c.nvals;
+        nv[i] = at - c.nvals;
+      }
+      for (int64_t k = 0; k < nv[i]; ++k) {
+        if (ids[i][k] < 0) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": negative dictId");
+        top[i] = std::max(top[i], ids[i][k]);
+      }
+    }
+    hip_check(hipSetDevice(m->ctx->device), "hipSetDevice");
+    hipStream_t st = m->ctx->stream;
+    for (size_t i = 0; i < ncols; ++i) {
+      pgx_mutable::Col& c = m->cols[i];
+      if (c.mv) {  // the new docs' starts, then the values
+        std::vector<int32_t> st_new(ndocs);
+        int64_t at = c.nvals;
+        for (int32_t d = 0; d < ndocs; ++d) {
+          at += counts[i][d];
+          st_new[d] = int32_t(at);
+        }
         hip_check(hipMemcpyAsync(c.starts.as<int32_t>() + m->num_docs + 1, st_new.data(), size_t(ndocs) * 4,
                                  hipMemcpyHostToDevice, st), "starts H2D");
         hip_check(hipStreamSynchronize(st), "sync");  // st_new is a stack buffer
-        if (c.nvals + nv > c.ids_cap) {  // grow the value buffer (doubling)
+        if (c.nvals + nv[i] > c.ids_cap) {  // grow the value buffer (doubling)
           int64_t cap = c.ids_cap;
-          while (cap < c.nvals + nv) cap *= 2;
+          while (cap < c.nvals + nv[i]) cap *= 2;
           DevBuf bigger(m->ctx, size_t(cap) * 4);
           if (c.nvals)
             hip_check(hipMemcpyAsync(bigger.p, c.ids.p, size_t(c.nvals) * 4, hipMemcpyDeviceToDevice, st), "grow");
@@ -5436,15 +5462,19 @@ pgx_status pgx_mutable_append(pgx_mutable* m, int32_t ndocs, const int32_t* cons
           c.ids_cap = cap;
         }
       }
-      for (int64_t k = 0; k < nv; ++k) {
-        if (ids[i][k] < 0) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": negative dictId");
-        c.max_id = std::max(c.max_id, ids[i][k]);
-      }
       const int64_t at = c.mv ? c.nvals : m->num_docs;
-      hip_check(hipMemcpyAsync(c.ids.as<int32_t>() + at, ids[i], size_t(nv) * 4, hipMemcpyHostToDevice, st), "ids H2D");
-      if (c.mv) c.nvals += nv;
+      hip_check(hipMemcpyAsync(c.ids.as<int32_t>() + at, ids[i], size_t(nv[i]) * 4, hipMemcpyHostToDevice, st),
+                "ids H2D");
     }
     hip_check(hipStreamSynchronize(st), "sync");  // the caller's buffers may go away after the call
+    for (size_t i = 0; i < ncols; ++i) {  // commit: every column was accepted
+      pgx_mutable::Col& c = m->cols[i];
+      c.max_id = std::max(c.max_id, top[i]);
+      if (c.mv) {
+        c.nvals += nv[i];
+        c.max_mv = std::max(c.max_mv, mvmax[i]);
+      }
+    }
     m->num_docs += ndocs;
   });
 }
@@ -5530,6 +5560,7 @@ pgx_status pgx_mutable_snapshot(pgx_mutable* m, pgx_segment** out) {
 pgx_status pgx_mutable_num_docs(const pgx_mutable* m, int32_t* out) {
   return guarded([&] {
     if (!m || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    std::lock_guard<std::mutex> g(m->mu);  // appends write num_docs under the same lock
     *out = m->num_docs;
   });
 }

@@ -208,16 +208,18 @@ constexpr int kImgFor16Blocks = 64;
 constexpr int kLdsBudget = 160 * 1024 - 256;  // static LDS of one workgroup, minus the per-plane accumulators
 
 // Narrow partitioned group-by (pgx_host.cpp run_narrow): the packed K-bit group key is mixed by a bijection of
-// [0, 2^K), h = ((((key * c1) & M) ^ (that >> s)) * c2) & M with s = ceil(K / 2) (so one xor-shift inverts itself),
-// and the partitions are h's top bits; h's remaining bits travel in the records and the aggregation rebuilds the key
-// with the inverse.  Shared by the generated scan (pgx_jit.cpp), the split / aggregation kernels and the host.
-constexpr uint64_t kNarrowC1 = 0x9E3779B97F4A7C15ull;
-constexpr uint64_t kNarrowC2 = 0xC2B2AE3D27D4EB4Full;
+// [0, 2^K), h = ((key * c1) & M) ^ (that >> s) with s = ceil(K / 2) (so the xor-shift inverts itself), and the
+// partitions are h's top bits (the multiply carries every key bit into them); the xor-shift folds those well-mixed top
+// bits into the low bits that choose a record's slot in the aggregation tables.  h's remaining bits travel in the
+// records and the aggregation rebuilds the key with the inverse.  c1 has 32 bits: the scan's multiply of a key of up
+// to 64 bits is three 32-bit multiplies (round 4 used two full 64-bit multiplies, eight, for the same partitions).
+// Shared by the generated scan (pgx_jit.cpp), the split / aggregation kernels and the host.
+constexpr uint64_t kNarrowC1 = 0x9E3779B1ull;
 constexpr int kNarrow1Bits = 8;      // first split (inside the scan): 256 buckets
 constexpr int kNarrowRing = 64;      // scan: per-bucket LDS ring of records (two 32-record units)
 constexpr int kNarrowMaxBits2 = 10;  // second split (pgx_narrow_split): up to 1024 sub-buckets per bucket
 struct NarrowMix {
-  uint64_t mask = 0, c1 = kNarrowC1, c2 = kNarrowC2, ic1 = 0, ic2 = 0;
+  uint64_t mask = 0, c1 = kNarrowC1, ic1 = 0;
   int s = 0;
 };
 inline uint64_t narrow_inverse(uint64_t c) {  // c odd: c * inverse == 1 (mod 2^64), Newton iteration
@@ -230,7 +232,6 @@ inline NarrowMix narrow_mix(int keybits) {
   m.mask = keybits >= 64 ? ~0ull : (uint64_t(1) << keybits) - 1u;
   m.s = (keybits + 1) / 2;
   m.ic1 = narrow_inverse(m.c1);
-  m.ic2 = narrow_inverse(m.c2);
   return m;
 }
 

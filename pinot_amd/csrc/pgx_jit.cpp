@@ -910,15 +910,15 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         if (s.emit_col >= 0) {
           const std::string ec = std::to_string(s.emit_col);
           if (s.emit_dictid) x = "v" + ec + "[j]";  // the value's dictId (sorted dictionary): looked up at aggregation
-          else x = s.cols[s.emit_col].img != IMG_NONE ? img_value(s, s.emit_col, img_off, "v" + ec + "[j]")
-                                                      : "(u32)(di" + ec + "[v" + ec + "[j]] - S->vbase[" + ec + "])";
+          else x = s.cols[s.emit_col].img != IMG_NONE
+                       ? "(u32)(" + img_value(s, s.emit_col, img_off, "v" + ec + "[j]") + " + (u32)S->emit_rebase)"
+                       : "(u32)(di" + ec + "[v" + ec + "[j]] - S->vbase[" + ec + "] + S->emit_rebase)";
         }
         if (enarrow) {  // mix the key (NarrowMix), bucket = top part_bits of the mix (bits 56.. of rec), record below
           const NarrowMix mx = narrow_mix(s.keybits);
           const std::string M = std::to_string(mx.mask) + "ull";
           e.ln("  u64 h = ((", key, ") * ", mx.c1, "ull) & ", M, ";");
           e.ln("  h ^= h >> ", mx.s, ";");
-          e.ln("  h = (h * ", mx.c2, "ull) & ", M, ";");
           e.ln("  rec = ((h >> ", nrb1, ") << 56) | (h & ", (uint64_t(1) << nrb1) - 1u, "ull) | ((u64)(", x, ") << ", nrb1,
                ");");
         } else {

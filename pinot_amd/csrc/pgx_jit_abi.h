@@ -53,6 +53,7 @@ struct JSeg {
   unsigned int* lmask;                           // statistics automaton: leaf l's predicate bit of row r goes to bit
   long long lmask_words;                         // (r & 31) of word [l * lmask_words + (r >> 5)]
   unsigned int* selmask;                         // selection bit of row r: bit (r & 31) of word r >> 5 (MV functions)
+  long long emit_rebase;                         // G_EMIT value records: this segment's vbase - the query's vbase
 };
 
 struct JArgs {

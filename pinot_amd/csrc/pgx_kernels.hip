@@ -194,10 +194,16 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return x;
 }
 
+// Probe chains are bounded (kGlobalMaxProbes): at the load factors the host plans (<= 1/2) a longer chain means the
+// table is (nearly) full, so the lane reports overflow at once and the host regrows the table and reruns, instead of
+// walking the whole table with one device atomic per slot.
+constexpr uint64_t kGlobalMaxProbes = 512;
+
 __device__ __forceinline__ int64_t hash_slot64(const KQuery& Q, uint64_t key) {
   const uint64_t mask = Q.hash_cap - 1;
+  const uint64_t lim = Q.hash_cap < kGlobalMaxProbes ? Q.hash_cap : kGlobalMaxProbes;
   uint64_t h = mix64(key) & mask;
-  for (uint64_t probe = 0; probe < Q.hash_cap; ++probe) {
+  for (uint64_t probe = 0; probe < lim; ++probe) {
     unsigned long long prev = atomicCAS(Q.keys + h, kEmptyKey, static_cast<unsigned long long>(key));
     if (prev == kEmptyKey || prev == key) return static_cast<int64_t>(h);
     h = (h + 1) & mask;
@@ -207,10 +213,11 @@ __device__ __forceinline__ int64_t hash_slot64(const KQuery& Q, uint64_t key) {
 
 __device__ __forceinline__ int64_t hash_slot128(const KQuery& Q, uint64_t klo, uint64_t khi) {
   const uint64_t mask = Q.hash_cap - 1;
+  const uint64_t lim = Q.hash_cap < kGlobalMaxProbes ? Q.hash_cap : kGlobalMaxProbes;
   uint64_t h = mix64(klo ^ mix64(khi)) & mask;
   uint64_t probes = 0;
   // Every loop iteration makes progress for every lane (no divergent spin on another lane's write).
-  while (probes < Q.hash_cap) {
+  while (probes < lim) {
     unsigned int st = atomicCAS(Q.key_state + h, 0u, 1u);
     if (st == 0u) {
       __hip_atomic_store(Q.keys + 2 * h, klo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1416,8 +1423,9 @@ __global__ void __launch_bounds__(256) pgx_mv_aggregate(const MvAgg* __restrict_
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int64_t mv_slot64(unsigned long long* keys, uint64_t cap, uint64_t key) {
   const uint64_t mask = cap - 1;
+  const uint64_t lim = cap < kGlobalMaxProbes ? cap : kGlobalMaxProbes;
   uint64_t h = mix64(key) & mask;
-  for (uint64_t probe = 0; probe < cap; ++probe) {
+  for (uint64_t probe = 0; probe < lim; ++probe) {
     const unsigned long long prev = atomicCAS(keys + h, kEmptyKey, static_cast<unsigned long long>(key));
     if (prev == kEmptyKey || prev == key) return static_cast<int64_t>(h);
     h = (h + 1) & mask;
@@ -1428,9 +1436,10 @@ __device__ __forceinline__ int64_t mv_slot64(unsigned long long* keys, uint64_t 
 __device__ __forceinline__ int64_t mv_slot128(unsigned long long* keys, unsigned int* key_state, uint64_t cap,
                                               uint64_t klo, uint64_t khi) {
   const uint64_t mask = cap - 1;
+  const uint64_t lim = cap < kGlobalMaxProbes ? cap : kGlobalMaxProbes;
   uint64_t h = mix64(klo ^ mix64(khi)) & mask;
   uint64_t probes = 0;
-  while (probes < cap) {
+  while (probes < lim) {
     const unsigned int st = atomicCAS(key_state + h, 0u, 1u);
     if (st == 0u) {
       __hip_atomic_store(keys + 2 * h, klo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -258,7 +258,7 @@ __device__ __forceinline__ int na_way(const na_u32x4 k, uint32_t key) {
 template <int IMG, bool SUM, bool MN, bool MX>
 __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
     const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
-    uint64_t kmask, uint64_t ic1, uint64_t ic2, int ms, int64_t vbase, const uint32_t* __restrict__ img, int img_words,
+    uint64_t kmask, uint64_t ic1, int ms, int64_t vbase, const uint32_t* __restrict__ img, int img_words,
     int img_sh, const int64_t* __restrict__ vdict, int cshift, uint64_t* __restrict__ okey,
     uint64_t* __restrict__ oplane, int64_t ocap, unsigned long long* __restrict__ ctr,
     unsigned long long* __restrict__ prange) {
@@ -343,7 +343,7 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
     for (int q = 0; q < Q; ++q) {
       if (!((fhas >> q) & 1u)) continue;
       if (o < static_cast<unsigned long long>(ocap)) {
-        uint64_t y = ((((static_cast<uint64_t>(fp) << rb2) | fk[q]) * ic2) & kmask);
+        uint64_t y = (static_cast<uint64_t>(fp) << rb2) | fk[q];
         y ^= y >> ms;
         okey[o] = (y * ic1) & kmask;
         const uint64_t c = fsc[q] >> cshift;
@@ -539,7 +539,7 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
 #define PGX_NA_CASE(C, I, A, B, D)                                                                                   \
   case C:                                                                                                            \
     hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D>), dim3(grid), dim3(pgx::kNAThreads), 0, stream, in, cnt2, \
-                       cap2, nparts, rb2, m.mask, m.ic1, m.ic2, m.s, vbase, img, img_words, img_sh, vdict, cshift,   \
+                       cap2, nparts, rb2, m.mask, m.ic1, m.s, vbase, img, img_words, img_sh, vdict, cshift,   \
                        okey, oplane, ocap, ctr, prange);                                                             \
     break;
 #define PGX_NA_CASES(I)                       \

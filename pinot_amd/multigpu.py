@@ -76,7 +76,48 @@ def _gather_bytes(payload: bytes, device) -> List[bytes]:
     return [bytes(b[:k].cpu().numpy().tobytes()) for b, k in zip(bufs, lens)]
 
 
-_DOMAINS = {}  # (group columns, segment uids, world) -> [(data type, values)] of the union
+_DOMAINS = None  # OrderedDict: this rank's local key -> (global fingerprint, [(data type, values)] of the union)
+_DOMAINS_CAP = 32
+
+
+def _h63(obj) -> int:
+    import hashlib
+    return int.from_bytes(hashlib.blake2b(repr(obj).encode(), digest_size=8).digest(), "little") >> 1
+
+
+def _domain_cache_probe(local_key, device):
+    """Collective hit-or-miss decision of the union-domain cache.  Every rank all-gathers (hash of its local key, the
+    global fingerprint stored with its cached entry or -1).  The union depends on EVERY rank's segments, so an entry is
+    used only when every rank holds one, all of them were stored under the same global fingerprint, and that
+    fingerprint equals the hash of the local keys gathered now.  The decision is a function of the gathered tensor
+    alone, so every rank takes the same branch and the collectives of the miss path stay in step (a rank whose segment
+    set changed while another's did not makes every rank recompute).  Returns (entry or None, global fingerprint)."""
+    import collections
+
+    import torch
+    import torch.distributed as dist
+    global _DOMAINS
+    if _DOMAINS is None:
+        _DOMAINS = collections.OrderedDict()
+    h = _h63(local_key)
+    ent = _DOMAINS.get(local_key)
+    mine = torch.tensor([h, ent[0] if ent is not None else -1], dtype=torch.int64, device=device)
+    parts = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, mine)
+    rows = [tuple(int(v) for v in p.tolist()) for p in parts]
+    g = _h63(tuple(r[0] for r in rows))
+    hit = all(r[1] == g for r in rows)
+    if hit:
+        _DOMAINS.move_to_end(local_key)
+        return ent[1], g
+    return None, g
+
+
+def _domain_cache_store(local_key, g, dom) -> None:
+    _DOMAINS[local_key] = (g, dom)
+    _DOMAINS.move_to_end(local_key)
+    while len(_DOMAINS) > _DOMAINS_CAP:  # LRU bound: realtime snapshots get new uids every query
+        _DOMAINS.popitem(last=False)
 
 
 def union_key_domains(q, segments, device=None) -> None:
@@ -87,14 +128,15 @@ def union_key_domains(q, segments, device=None) -> None:
     all-reduce) or by packed key (all-to-all + device merge) -- the value-keyed combine of
     MCombineGroupByOperator.java:166-191 without moving values.
 
-    Segment metadata, computed once per (group columns, segment set) and cached: first two all-reduces of per-column
+    Cached per (group columns, every rank's segment set): one all-gather of 16 bytes per rank decides, on every rank
+    alike, whether the cached union still holds (_domain_cache_probe).  On a miss: two all-reduces of per-column
     fingerprints (MIN, MAX); columns whose dictionaries are the same on every rank (the common case: one table, one
     schema, shared value domains) need no exchange at all; only the others all-gather their values as byte tensors
     (`device`: the process group's device, e.g. cuda:N under RCCL; None: CPU, gloo)."""
     import torch
     import torch.distributed as dist
     key = (tuple(q.group_cols), tuple(getattr(s, "uid", id(s)) for s in segments), dist.get_world_size())
-    dom = _DOMAINS.get(key)
+    dom, gfp = _domain_cache_probe(key, device)
     if dom is None:
         local = [_local_domain(segments, col) for col in q.group_cols]
         fp = torch.tensor([_fingerprint(dt, u) for dt, u in local], dtype=torch.int64, device=device)
@@ -139,7 +181,7 @@ def union_key_domains(q, segments, device=None) -> None:
                 dom.append((t, sorted(set(vals), key=lambda v: v.encode("utf-8"))))
             else:
                 dom.append((t, np.unique(np.concatenate(vals))))
-        _DOMAINS[key] = dom
+        _domain_cache_store(key, gfp, dom)
     for g, (dt, vals) in enumerate(dom):
         if dt is not None:
             q.set_key_domain(g, vals, dt)

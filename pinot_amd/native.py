@@ -7,6 +7,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PGX_LIB", os.path.join(_HERE, "libpgx.so"))
 
 
+PGX_ERR_INVALID_ARG = 1
 PGX_ERR_UNSUPPORTED = 2  # pgx.h pgx_status: the caller falls back to the Java operators
 
 

@@ -53,17 +53,19 @@ class _Table:
 
     def __init__(self, dims: np.ndarray, mets: np.ndarray):
         self.blocks = [(0, dims, mets)]
+        self.starts = [0]  # block start rows, ascending (kept beside the blocks: no per-lookup rebuild)
         self.n = len(dims)
 
     def append(self, d: np.ndarray, m: np.ndarray) -> int:
         start = self.n
         self.blocks.append((start, d, m))
+        self.starts.append(start)
         self.n += len(d)
         return start
 
     def rows(self, a, b):
         import bisect
-        i = bisect.bisect_right([blk[0] for blk in self.blocks], a) - 1
+        i = bisect.bisect_right(self.starts, a) - 1
         s0, d, m = self.blocks[i]
         assert b - s0 <= len(d), "range spans two blocks"
         return d[a - s0:b - s0], m[a - s0:b - s0]

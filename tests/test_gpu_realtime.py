@@ -112,3 +112,38 @@ def test_consuming_beside_immutable(ctx):
                 H.assert_values_equal(m[k], v, fns)
         else:
             H.assert_values_equal(r.get_aggregation_result(), o["results"], fns)
+
+
+def test_rejected_append_changes_nothing(ctx):
+    """pgx_mutable_append validates every column before touching any state.  A batch whose multi-value
+    column (tags, index 3) is valid but whose later column (met, index 4) holds a negative dictId is rejected, and the
+    consuming segment afterwards answers exactly as if the batch had never been offered."""
+    import ctypes as C
+
+    from pinot_amd import native as N
+    rng = np.random.default_rng(33)
+    rt = RealtimeSegment("rt_bad", SCHEMA, capacity=100000, inverted=["dim"])
+    rows = _rows(rng, 3000)
+    for r in rows[:2000]:
+        rt.index(r)
+    rt.device_segment(ctx)  # the first 2000 docs are in HBM
+    L = N.lib()
+    k = 5
+    arrs = []
+    for c in SCHEMA:
+        if c == "tags":
+            arrs.append((np.zeros(2 * k, dtype=np.int32), np.full(k, 2, dtype=np.int32)))
+        elif c == "met":
+            arrs.append((np.full(k, -1, dtype=np.int32), None))
+        else:
+            arrs.append((np.zeros(k, dtype=np.int32), None))
+    idp = (C.c_void_p * len(arrs))(*[a.ctypes.data for a, _ in arrs])
+    cnp = (C.c_void_p * len(arrs))(*[x.ctypes.data if x is not None else None for _, x in arrs])
+    assert L.pgx_mutable_append(rt._mut, k, idp, cnp) == N.PGX_ERR_INVALID_ARG
+    nd = C.c_int32()
+    N.check(L.pgx_mutable_num_docs(rt._mut, C.byref(nd)))
+    assert nd.value == 2000
+    for r in rows[2000:]:  # the valid rows that follow land right after the first 2000
+        rt.index(r)
+    for text in QUERIES:
+        _check(ctx, rt, text)

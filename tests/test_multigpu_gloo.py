@@ -387,6 +387,55 @@ class _FakeQuery:
         self.set[g] = (dt, vals)
 
 
+def _cache_worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+        real = multigpu._gather_bytes
+        multigpu._gather_bytes = lambda payload, device: calls.append(1) or real(payload, device)
+        a = _FakeSeg({"g": _FakeCol(np.arange(rank * 5, rank * 5 + 20, dtype=np.int64), "INT")})
+        a.uid = 1000 + rank
+        seen = []
+        for step in range(4):
+            segs = [a]
+            if rank == 1 and step >= 2:  # only rank 1's segment set changes (a new segment, e.g. a realtime snapshot)
+                b = _FakeSeg({"g": _FakeCol(np.arange(100, 103, dtype=np.int64), "INT")})
+                b.uid = 2000 + step  # a fresh uid per step: never a cache hit on rank 1's side
+                segs = [a, b]
+            fq = _FakeQuery(["g"])
+            before = len(calls)
+            multigpu.union_key_domains(fq, segs)
+            seen.append((len(calls) - before, fq.set[0][1]))
+        multigpu._gather_bytes = real
+        q.put((rank, seen))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_union_domain_cache_decides_collectively():
+    """one rank's segment set changes while the other's does not.  Every rank must miss together
+    (the same collectives run on both: no hang, no pairing with the next collective) and see the new union."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cache_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res[0] == res[1]
+    base = list(range(0, 25))
+    grown = base + [100, 101, 102]
+    # step 0: miss (differing dictionaries gather), 1: hit, 2 and 3: rank 1 changed -> both ranks gather again
+    assert [c for c, _ in res[0]] == [1, 0, 1, 1]
+    assert [v for _, v in res[0]] == [base, base, grown, grown]
+
+
 def _domain_segments(rank):
     segs = []
     for s in range(2):
