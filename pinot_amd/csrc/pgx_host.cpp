@@ -60,7 +60,7 @@ extern "C" hipError_t pgx_launch_mv_group(const pgx::MvGroupArgs* args, int nseg
                                           hipStream_t stream);
 extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
                                                 int nparts, int64_t cap, uint64_t keymask, int keybits, int64_t vbase,
-                                                const int64_t* vdict, int need_sum, int need_min, int need_max, int pack_shift,
+                                                int need_sum, int need_min, int need_max, int pack_shift,
                                                 uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream);
@@ -70,13 +70,6 @@ extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int6
 extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
                                               const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
 extern "C" size_t pgx_trim_state_bytes(void);
-extern "C" hipError_t pgx_launch_part_aggregate_img(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
-                                                    int nparts, int64_t cap, uint64_t keymask, int keybits,
-                                                    int64_t vbase, const uint32_t* img, int img_words, int img_sh,
-                                                    const int64_t* vdict, int need_min, int need_max, int pack_shift,
-                                                    uint64_t* okey, uint64_t* oplane, int64_t ocap,
-                                                    unsigned long long* ocount, unsigned long long* overflow, int grid,
-                                                    hipStream_t stream);
 extern "C" hipError_t pgx_launch_pack_remap(uint32_t* out_words, const int32_t* ids, const int32_t* remap,
                                             int64_t n_rows, int bits, int64_t n_words, hipStream_t stream);
 extern "C" hipError_t pgx_launch_narrow_split(const uint32_t* lo, const uint16_t* hi, const unsigned long long* cnt1,
@@ -908,6 +901,7 @@ struct pgx_query {
   std::vector<int> leaf_kind;
   uint32_t flags = 0;
   std::vector<KeyDomain> key_domain;  // [group column]
+  Knobs kn;                           // the PGX_* environment when the query was compiled (read_knobs)
 };
 
 // =================================================================================================
@@ -1354,6 +1348,7 @@ struct ExecPlan {
   size_t lds_bytes = 0;
   // query-specialised kernels (pgx_jit.cpp): one launch per group of segments sharing a shape
   // partitioned group-by (G_HASH64 keys, one integer value column; run_partitioned)
+  Knobs kn;  // the query's (plan_query copies them in: partition sizing and launches read them from the plan)
   bool use_part = false;
   int part_vcol = -1;            // query column slot of the aggregated value (-1: COUNT only)
   int part_keybits = 0;
@@ -1361,22 +1356,16 @@ struct ExecPlan {
   int64_t part_vbase = 0;
   bool part_sum = false, part_min = false, part_max = false;
   bool part_dictid = false;      // records carry the value's dictId (sorted dictionary), values looked up at aggregation
-  bool part_fused = false;       // the scan kernel performs the first radix pass (records leave bucketed)
   bool part_slab = false;        // ... into per-workgroup slabs (dictId records, LDS cursors; pass 2 reads the slabs)
   int64_t part_nwg = 0;          // slab mode: query-kernel workgroups over all launch groups (slabs per bucket)
   int64_t part_wg_rows = 0;      // slab mode: most rows one workgroup scans
   const int64_t* part_vdict = nullptr;  // device int64 value per dictId (part_dictid)
-  const uint32_t* part_img = nullptr;   // slab mode, FOR16 value column: its image, looked up in the aggregation's LDS
-  int part_img_words = 0, part_img_sh = 0;
-  int part_grid = 256;                  // ... its persistent grid: one workgroup per CU (the image fills the LDS)
   unsigned long long* part_cursor = nullptr;   // fused first pass: bucket cursors, overflow counter, bucket capacity
   unsigned long long* part_overflow = nullptr;
   int64_t part_cap = 0;
   // narrow records (run_narrow, the default for partitioned plans that qualify): the scan writes dictId records split
   // 256 ways into per-workgroup slabs (part_slab with kNarrow1Bits), u32 in kq.table and bits 32..47 in part_hi
   bool part_narrow = false;
-  bool narrow_old_slab = false, narrow_old_dictid = false, narrow_old_fused = false;  // the radix path's choices,
-                                                                                       // restored on fallback
   int narrow_vd = 0;              // dictId bits of the value column (0: COUNT only)
   int narrow_k2min = 0;           // second-split bits the record width needs
   int narrow_img = 0;             // value image in the aggregation's LDS: 0 none, 1 U32, 2 FOR16
@@ -1436,15 +1425,40 @@ struct ExecPlan {
 // forced with PGX_RCHUNK=1 (measured slower at C5 so far: the per-chunk container search stalls its workgroup).
 constexpr double kRchunkMaxSel = 0.0;
 
-bool jit_enabled() {
-  const char* e = std::getenv("PGX_JIT");
-  return !(e && e[0] == '0');
+}  // namespace
+
+Knobs pgx::read_knobs() {
+  Knobs k;
+  auto env = [](const char* name) -> std::string {
+    const char* e = std::getenv(name);
+    return e ? std::string(e) : std::string();
+  };
+  const std::string jit = env("PGX_JIT"), nar = env("PGX_PART_NARROW"), rc = env("PGX_RCHUNK"), rp = env("PGX_RPROG");
+  const std::string bs = env("PGX_BATCH_SEGS"), dbg = env("PGX_DEBUG");
+  k.jit = !(jit.size() && jit[0] == '0');
+  k.narrow = !(nar.size() && nar[0] == '0');
+  if (rc.size()) k.rchunk = rc[0] == '1' ? 1 : 0;
+  if (rp == "off") k.rprog = RPROG_OFF;
+  else if (rp == "wave") k.rprog = RPROG_WAVE;
+  else if (rp == "seg") k.rprog = RPROG_SEG;
+  else if (rp == "chunk") k.rprog = RPROG_CHUNK;
+  else if (rp == "stack") k.rprog = RPROG_STACK;
+  if (bs.size()) k.batch_segs = std::atoi(bs.c_str());
+  size_t i = 0;
+  while (i < dbg.size()) {
+    size_t j = dbg.find(',', i);
+    if (j == std::string::npos) j = dbg.size();
+    const std::string o = dbg.substr(i, j - i);
+    if (o == "part_small") k.part_small = true;
+    else if (o == "narrow_log") k.narrow_log = true;
+    else if (o == "host_profile") k.host_profile = true;
+    else if (o.rfind("narrow_k2=", 0) == 0) k.narrow_k2 = std::atoi(o.c_str() + 10);
+    i = j + 1;
+  }
+  return k;
 }
 
-bool part_enabled() {
-  const char* e = std::getenv("PGX_PART");
-  return !(e && e[0] == '0');
-}
+namespace {
 
 int qslot(ExecPlan& P, const std::string& name) {
   for (size_t i = 0; i < P.qcols.size(); ++i)
@@ -1927,12 +1941,6 @@ void prof_mark(const char* what) {
 
 void canon_rprog(std::vector<int>& op, std::vector<int>& arg);
 
-// Hash group-by in the generated kernels (pgx_jit.cpp emit_hash): PGX_JIT_HASH=0 keeps the interpreter kernel (A/B).
-bool jit_hash_ok(const KQuery& K) {
-  if (K.group_mode != G_HASH64 && K.group_mode != G_HASH128) return true;
-  const char* e = std::getenv("PGX_JIT_HASH");
-  return !(e && e[0] == '0');
-}
 
 void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                 uint32_t xflags, ExecPlan& P, const Domain* dom = nullptr) {
@@ -1940,6 +1948,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   if (q.agg_fn.size() > size_t(kMaxAggs)) fail(PGX_ERR_UNSUPPORTED, "too many aggregation functions");
   if (q.group_cols.size() > size_t(kMaxGroupCols)) fail(PGX_ERR_UNSUPPORTED, "too many group-by columns");
   if (q.leaf_col.size() > size_t(kMaxLeaves)) fail(PGX_ERR_UNSUPPORTED, "too many filter leaves");
+  P.kn = q.kn;
   KQuery& K = P.kq;
   // query column slots
   for (size_t l = 0; l < q.leaf_col.size(); ++l) K.leaf_col[l] = int8_t(qslot(P, q.leaf_col[l]));
@@ -2029,10 +2038,9 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   // same INT/LONG column whose dictionary is identical in every segment (one value base), with a value range of at
   // most 32 bits, and key + value fit 63 bits.
   P.use_part = false;
-  P.part_slab = P.part_fused = P.part_dictid = P.part_narrow = false;
-  P.part_img = nullptr;
+  P.part_slab = P.part_dictid = P.part_narrow = false;
   P.part_hi = nullptr;
-  if (K.group_mode == G_HASH64 && jit_enabled() && part_enabled() && !(xflags & PGX_X_NO_PARTITION) &&
+  if (K.group_mode == G_HASH64 && q.kn.jit && !(xflags & PGX_X_NO_PARTITION) &&
       K.num_qcols <= PGX_J_MAX_COLS) {
     int vc = -1;
     bool ok = true;
@@ -2074,44 +2082,9 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         vbits = ok ? bits_for(int64_t(range) + 1) : 64;
       }
     }
-    // records may carry the dictId instead of the value offset when the dictionary is sorted (numeric dictionaries are:
-    // SegmentDictionaryCreator), so MIN / MAX of ids are MIN / MAX of values and SUM looks values up while aggregating;
-    // the scan then needs no value image, which leaves its LDS to the fused first radix pass
-    bool dictid = false;
-    if (ok && vc >= 0) {
-      const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
-      dictid = same_dict && c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end()) &&
-               keybits + bits_for(c0.card) <= 63;
-      // opt-in (PGX_PART_FUSED=1): measured at C3, the fused first pass saves 1.7 ms of scan + pass 1, but the
-      // aggregation's per-record dictionary gathers (one 64-B L2 line each) cost 2.3 ms more than offset records.
-      // PGX_PART_SLAB=1: the same fused split, but each workgroup appends to its own slab of every bucket (LDS
-      // cursors, no global cursor round trip per sub-step); the second pass reads the slabs.
-      const char* e = std::getenv("PGX_PART_FUSED");
-      const char* es = std::getenv("PGX_PART_SLAB");
-      P.part_slab = dictid && es && es[0] == '1';
-      dictid = dictid && ((e && e[0] == '1') || P.part_slab);
-      if (dictid) P.part_vdict = static_cast<const int64_t*>(c0.dict_dev);
-      // slab records carry dictIds: with a FOR16 image (<= 65536 values) the aggregation sums through the image in LDS
-      if (P.part_slab && c0.img_kind == IMG_FOR16 && c0.img_dev && c0.img_words >= kImgFor16Blocks &&
-          c0.img_words <= kImgFor16Blocks + 32768) {
-        P.part_img = static_cast<const uint32_t*>(c0.img_dev);
-        P.part_img_words = c0.img_words;
-        P.part_img_sh = c0.img_sh;
-        P.part_grid = ctx->num_cus;
-      }
-    }
-    if (!(ok && keybits + vbits <= 63)) {
-      P.part_slab = false;
-      P.part_img = nullptr;
-    }
+    // The 8-byte radix path's records carry value offsets (round 3's dictId records with a fused first pass or
+    // per-workgroup slabs measured slower at C3 and were removed in round 5)
     if (ok && keybits + vbits <= 63) {
-      if (vc < 0) {  // COUNT only: records carry no value, the split is always fused
-        const char* es = std::getenv("PGX_PART_SLAB");
-        P.part_slab = es && es[0] == '1';
-      }
-      P.part_dictid = dictid;
-      P.part_fused = (dictid || vc < 0) && !P.part_slab;
-      if (const char* e = std::getenv("PGX_PART_FUSED")) P.part_fused = P.part_fused && e[0] == '1';
       P.use_part = true;
       P.part_vcol = vc;
       P.part_keybits = keybits;
@@ -2124,11 +2097,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       // keybits - 8 + dictId bits (<= 48) out of the scan's own 256-way split, then <= 32 bits after the second split,
       // and the aggregation looks values up in the column's image (FOR16 / U32) in LDS (run_narrow).  Needs a sorted
       // dictionary (MIN / MAX of dictIds) and, for SUM / AVG, an image that fits beside the aggregation tables.
-      const char* en = std::getenv("PGX_PART_NARROW");
-      const char* es2 = std::getenv("PGX_PART_SLAB");
-      const char* ef2 = std::getenv("PGX_PART_FUSED");
-      const bool forced = (es2 && es2[0] == '1') || (ef2 && ef2[0] == '1');  // the radix variants asked for by name
-      if (!(en && en[0] == '0') && !forced && keybits > kNarrow1Bits) {
+      if (q.kn.narrow && keybits > kNarrow1Bits) {
         int vd = 0, imgk = 0;
         bool nok = true;
         if (vc >= 0) {
@@ -2150,11 +2119,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         int k2 = std::max(0, rb1 + vd - 32);
         if (rb1 - k2 > 31) k2 = rb1 - 31;
         if (nok && rb1 + vd <= 48 && k2 <= kNarrowMaxBits2) {
-          P.narrow_old_slab = P.part_slab;
-          P.narrow_old_dictid = P.part_dictid;
-          P.narrow_old_fused = P.part_fused;
           P.part_narrow = true;
-          P.part_fused = false;
           P.part_slab = true;
           P.part_dictid = vc >= 0;
           P.narrow_vd = vd;
@@ -2173,14 +2138,13 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   P.fsm_on = false;
   P.rprog_on = false;
   P.dm_progs.clear();
-  P.use_docmask = jit_enabled() && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
-                                    K.group_mode == G_DENSE_GLOBAL || K.group_mode == G_HASH64 ||
-                                    K.group_mode == G_HASH128 || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS &&
-                    jit_hash_ok(K);
+  P.use_docmask = q.kn.jit && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
+                                K.group_mode == G_DENSE_GLOBAL || K.group_mode == G_HASH64 ||
+                                K.group_mode == G_HASH128 || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS;
   if (!q.filter.empty()) {
     PNode root = build_tree(q, *segs[0]);
     const size_t L = q.leaf_col.size();
-    bool fuse = P.use_docmask && stats_closed_form(root, q, segs, n, bindings) && !std::getenv("PGX_NO_RPROG");
+    bool fuse = P.use_docmask && stats_closed_form(root, q, segs, n, bindings) && q.kn.rprog != RPROG_OFF;
     for (int s = 0; s < n && fuse; ++s) {
       if (star_fit(q, *segs[s])) fuse = false;
       for (size_t l = 0; l < L && fuse; ++l) {
@@ -2471,7 +2435,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       if (!st.empty()) est = std::min(est, st.back());  // the programs are ANDed or ORed into the tree: a bound
     }
     P.rchunk = est <= kRchunkMaxSel;
-    if (const char* e = std::getenv("PGX_RCHUNK")) P.rchunk = e[0] == '1';
+    if (q.kn.rchunk >= 0) P.rchunk = q.kn.rchunk == 1;
     for (int s = 0; s < n && P.rchunk; ++s)
       if (star_fit(q, *segs[s])) P.rchunk = false;
   }
@@ -2732,9 +2696,9 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
   if (P.rprog_on) {
     const int np = int(P.rprogs.size());
     // wave-per-chunk kernel when every program has <= 64 bitmaps (one lane each) and <= 3 mask slots
-    bool wave = true;
+    const int rk = P.kn.rprog;  // PGX_RPROG: wave | seg | chunk | stack (default: the first that fits)
+    bool wave = rk == RPROG_AUTO || rk == RPROG_WAVE;
     int nslots = 1;
-    if (const char* e = std::getenv("PGX_RPROG_WAVE")) wave = e[0] == '1';
     for (size_t i = 0; i < P.rprogs.size() && wave; ++i) {
       const RProg& r = P.rprogs[i];
       int nb = 0;
@@ -2750,16 +2714,15 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
                 "bitmap program launch");
       return;
     }
-    int maxleaves = 0;  // leaf masks the wide kernel keeps in LDS (PGX_RPROG_NARROW=1: the stack kernel)
+    int maxleaves = 0;  // leaf masks the wide kernel keeps in LDS (PGX_RPROG=stack: the stack kernel)
     for (const auto& dp : P.dm_progs) {
       int nl = 0;
       for (int8_t o : dp.op) nl += o == RP_LEAF;
       maxleaves = std::max(maxleaves, nl);
     }
-    if (std::getenv("PGX_RPROG_NARROW")) maxleaves = 0;
-    // per-segment container walk when every program's bitmaps fit one lane each (PGX_RPROG_SEG=0: per-chunk kernels)
-    bool seg_walk = maxleaves >= 1;
-    if (const char* e = std::getenv("PGX_RPROG_SEG")) seg_walk = seg_walk && e[0] == '1';
+    if (rk == RPROG_STACK) maxleaves = 0;
+    // per-segment container walk when every program's bitmaps fit one lane each (PGX_RPROG=chunk: per-chunk kernels)
+    bool seg_walk = maxleaves >= 1 && rk != RPROG_CHUNK && rk != RPROG_STACK;
     for (size_t i = 0; i < P.rprogs.size() && seg_walk; ++i) {
       int nb = 0;
       const RProg& r = P.rprogs[i];
@@ -2931,7 +2894,7 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
       B.table = DevBuf(ctx, bytes);
       K.table = devp(B.table);
     }
-  } else if (P.use_part && !P.part_fused && !P.part_slab) {
+  } else if (P.use_part && !P.part_slab) {
     B.table = DevBuf(ctx, std::max<int64_t>(P.rec_total, 1) * 8);  // one key|value record per scanned row
     K.table = devp(B.table);
   } else if (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) {
@@ -2993,11 +2956,10 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
   const bool slab = P.part_slab;
   P.part_slab = false;  // only the query kernels write slabs (the generic kernel writes row-order records)
   const KQuery& K = P.kq;
-  if (!jit_enabled()) return;
+  if (!P.kn.jit) return;
   if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL || P.use_part ||
         K.group_mode == G_HASH64 || K.group_mode == G_HASH128))
     return;
-  if (!jit_hash_ok(K)) return;
   const int nc = K.num_qcols;
   if (nc > PGX_J_MAX_COLS) return;
   P.part_slab = slab;
@@ -3081,13 +3043,6 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         C.acc32 = range * 32 < 0xFFFFFFFFull;
       }
     }
-    // PGX_FRAC=1 (A/B): eight rows per lane whatever the widths; columns whose 8 rows are not whole dwords (e.g. a
-    // 10-bit key) load the covering words and shift, so every other column's loads stay contiguous per instruction
-    if (const char* e = std::getenv("PGX_FRAC"))
-      if (e[0] == '1' && R > 8) {
-        R = 8;
-        for (JitCol& C : J.cols) C.frac = C.decode && (8 * C.bits) % 32 != 0;
-      }
     J.R = R;
     // Registers for the raw words of the next tile (loaded one tile ahead, so held twice): sum over the decoded columns
     // of the dwords one sub-step of R rows takes, times the sub-steps per tile.  A query over many columns (C6: twelve)
@@ -3118,13 +3073,6 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       const int w = words(J.R);
       while (J.TL > J.R && 2 * (J.TL / J.R) * w > kTileWordBudget) J.TL /= 2;
     }
-    if (const char* e = std::getenv("PGX_LD_X4")) J.ld_x4 = e[0] == '1';
-    if (const char* e = std::getenv("PGX_SEL_K")) J.sel_k = std::max(0, std::min(8, std::atoi(e)));
-    // PGX_NO_IMG=1 (A/B): no value images; SUM / MIN / MAX values are gathered from the dictionary for selected rows
-    // only, which frees the LDS for more workgroups per CU
-    if (const char* e = std::getenv("PGX_NO_IMG"))
-      if (e[0] == '1')
-        for (JitCol& C : J.cols) C.img = IMG_NONE;
     // LDS budget: drop the largest images until everything fits (LEAF_RCHUNK: a budget for three workgroups per CU)
     int64_t rch_bytes = 0;
     if (P.rchunk) {
@@ -3172,12 +3120,9 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       // the narrow split's LDS rings (pgx_jit.cpp) want ~16 records per bucket per sub-step (T * R = 4096: a ring of
       // 64 holds the unflushed unit plus the sub-step's records with a wide margin): 512 threads, eight rows per lane
       // (fractional loads of widths that need it), half tiles (16 rows per lane) so the raw words of the next tile stay
-      // in registers without spilling.  PGX_NARROW_T / _R / _TL: A/B knobs.
+      // in registers without spilling (1024 threads and 16 or 32 rows per lane measured slower).
       J.T = 512;
-      int nr = 8, ntl = 16;
-      if (const char* e = std::getenv("PGX_NARROW_T")) J.T = std::atoi(e) == 1024 ? 1024 : (std::atoi(e) == 256 ? 256 : 512);
-      if (const char* e = std::getenv("PGX_NARROW_R")) nr = std::atoi(e) == 16 ? 16 : 8;
-      if (const char* e = std::getenv("PGX_NARROW_TL")) ntl = std::atoi(e) == 32 ? 32 : 16;
+      const int nr = 8, ntl = 16;
       if (nr < J.R) {
         J.R = nr;
         for (JitCol& C : J.cols) C.frac = C.decode && (nr * C.bits) % 32 != 0;
@@ -3224,11 +3169,10 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       J.ghi.push_back(K.ghi[g] ? 1 : 0);
     }
     J.hash_slots = (J.group_mode == G_HASH64 || J.group_mode == G_HASH128) ? hash_slots : 0;
-    if (const char* e = std::getenv("PGX_HASH_BATCH")) J.hash_batch = e[0] == '1';  // A/B (off by default)
     if (P.use_part) {
       J.keybits = P.part_keybits;
       J.emit_col = P.part_vcol;
-      J.part_bits = P.part_narrow ? kNarrow1Bits : ((P.part_fused || P.part_slab) ? kPart1Bits : 0);
+      J.part_bits = P.part_narrow ? kNarrow1Bits : 0;
       J.emit_dictid = P.part_dictid;
       J.part_slab = P.part_slab;
       J.part_narrow = P.part_narrow;
@@ -3236,13 +3180,11 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     }
     J.dense_slots = P.dense_slots;
     // COUNT + one integer SUM / AVG over a dense LDS table: one packed 64-bit add per row when, for every segment of
-    // the group, its rows fit the count field and rows x value range fit the offset field (flushed per segment);
-    // PGX_DENSE_PACK=0 keeps two adds
+    // the group, its rows fit the count field and rows x value range fit the offset field (flushed per segment)
     if ((K.group_mode == G_DENSE_LDS || K.group_mode == G_HASH64 || K.group_mode == G_HASH128) &&
         K.num_planes == 2 && K.num_aggs == 1 && (K.agg_kind[0] == A_SUM || K.agg_kind[0] == A_AVG) && !P.use_part) {
       const int c = K.agg_col[0];
-      const char* e = std::getenv("PGX_DENSE_PACK");
-      if (!(e && e[0] == '0') && c >= 0 && J.cols[c].img != IMG_NONE && !J.cols[c].fp) {
+      if (c >= 0 && J.cols[c].img != IMG_NONE && !J.cols[c].fp) {
         int64_t maxdocs = 1;
         uint64_t vrange = 0;
         for (int sg : members) {
@@ -3258,7 +3200,6 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     }
     J.leafmask = P.fsm_on && P.lmask_off[members[0]] >= 0;
     J.compact = P.rchunk && !P.use_part;  // selective bitmap filters: aggregate the selected rows packed
-    if (const char* e = std::getenv("PGX_COMPACT")) J.compact = e[0] == '1' && !P.use_part;
     J.selmask = P.want_selmask;
 
     ExecPlan::JitGroup G;
@@ -3577,7 +3518,6 @@ uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {
 // (DefaultGroupKeyGenerator.java:239-343 LONG_MAP / ARRAY_MAP) with a layout that streams HBM instead of probing it.
 // -------------------------------------------------------------------------------------------------
 constexpr int64_t kPartGroupsPerWg = 700;   // groups per pgx_part_aggregate workgroup: LDS table load <= ~1/3 (2048 slots)
-constexpr int64_t kPartGroupsPerWgImg = 400;  // ... pgx_part_aggregate_img (1024 slots beside the value image)
 constexpr uint64_t kPartMaxBytes = uint64_t(96) << 30;  // partition buffers beyond this: fall back to the hash table
 constexpr int kPartChunkRecs = 8192;    // records per pgx_partition workgroup (pgx_kernels.hip kPartChunk)
 
@@ -3586,26 +3526,18 @@ struct PartBuffers {
   int64_t cap1 = 0, cap2 = 0, ocap = 0;
   DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[kPart1N] | cursors2[nparts] (kCursorStride apart) | ocount | ovf[3]
   DevBuf prange;                         // trim-key ranges of the groups (narrow aggregation), or none
-  // slab mode (ExecPlan::part_slab): out1 holds kPart1N x nwg slabs of cap1 records, their counts in scnt; the second
-  // pass always runs (with nbits2 = 0 it only gathers each bucket's slabs into one run)
-  bool slab = false;
-  int64_t nwg = 0;
-  DevBuf scnt;
-  bool pass2() const { return nbits2 > 0 || slab; }
+  bool pass2() const { return nbits2 > 0; }
   int64_t nparts() const { return int64_t(1) << (kPart1Bits + nbits2); }
   size_t ctr_words() const { return size_t(kPart1N + (pass2() ? nparts() : 0)) * kCursorStride + 4; }
-  int64_t out1_recs() const { return slab ? int64_t(kPart1N) * nwg * cap1 : int64_t(kPart1N) * cap1; }
+  int64_t out1_recs() const { return int64_t(kPart1N) * cap1; }
 };
 
-// PGX_PART_DEBUG=1 (tests): start from undersized buckets and one pass, and allow at most one refinement, so the
+// PGX_DEBUG=part_small (tests): start from undersized buckets and one pass, and allow at most one refinement, so the
 // resize, re-split and hash-table fallback branches run at small row counts.
-bool part_debug() {
-  const char* e = std::getenv("PGX_PART_DEBUG");
-  return e && e[0] == '1';
-}
+bool part_debug(const ExecPlan& P) { return P.kn.part_small; }
 
-// second-pass split bits: up to 256 ways for the image aggregation (smaller tables), 128 otherwise
-int part_max_bits2(const ExecPlan& P) { return P.part_img ? 8 : 7; }
+// second-pass split bits: up to 128 ways
+int part_max_bits2(const ExecPlan&) { return 7; }
 
 void part_size(const ExecPlan& P, PartBuffers& PB) {
   const int64_t N = P.rec_total;
@@ -3614,20 +3546,14 @@ void part_size(const ExecPlan& P, PartBuffers& PB) {
   for (const auto& g : P.gdicts) prod *= double(g.card);
   ub = std::min(ub, prod);
   PB.nbits2 = 0;
-  const int64_t gpw = P.part_img ? kPartGroupsPerWgImg : kPartGroupsPerWg;
-  while (PB.nbits2 < part_max_bits2(P) && double(int64_t(1) << (kPart1Bits + PB.nbits2)) * gpw < ub) ++PB.nbits2;
+  while (PB.nbits2 < part_max_bits2(P) && double(int64_t(1) << (kPart1Bits + PB.nbits2)) * kPartGroupsPerWg < ub)
+    ++PB.nbits2;
   PB.cap1 = N / kPart1N + N / 512 + 65536;
-  PB.slab = P.part_slab;
-  PB.nwg = P.part_nwg;
-  if (PB.slab) {  // a slab holds one workgroup's records of one bucket: binomial around wg_rows / 128
-    const int64_t m = P.part_wg_rows / kPart1N;
-    PB.cap1 = m + m / 8 + 512;
-  }
   const int64_t np = PB.nparts();
   PB.cap2 = N / np + N / np / 4 + 16384;
-  if (part_debug()) {
+  if (part_debug(P)) {
     PB.nbits2 = 0;
-    PB.cap1 = PB.slab ? 1 : N / 256 + 1;
+    PB.cap1 = N / 256 + 1;
     PB.cap2 = 1;
   }
 }
@@ -3639,26 +3565,22 @@ bool part_alloc(pgx_ctx* ctx, const ExecPlan& P, PartBuffers& PB) {
   if (bytes > kPartMaxBytes) return false;
   PB.out1 = DevBuf(ctx, size_t(std::max<int64_t>(PB.out1_recs(), 1)) * 8);
   if (PB.pass2()) PB.out2 = DevBuf(ctx, size_t(np) * PB.cap2 * 8);
-  if (PB.slab) PB.scnt = DevBuf(ctx, size_t(std::max<int64_t>(int64_t(kPart1N) * PB.nwg, 1)) * 8);
   PB.okey = DevBuf(ctx, size_t(PB.ocap) * 8);
   PB.oplane = DevBuf(ctx, size_t(PB.ocap) * 4 * 8);
   PB.ctr = DevBuf(ctx, PB.ctr_words() * 8);
   return true;
 }
 
-// Before the scan: zero the cursors and counters; with the fused first pass the scan kernel appends its bucketed
-// records to out1 through the first-pass cursors.
+// Before the scan: zero the cursors and counters (the scan writes row-order records into the plan's record array).
 void part_prepare(ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   unsigned long long* ctr = devp(PB.ctr);
   hip_check(hipMemsetAsync(ctr, 0, PB.ctr_words() * 8, st), "partition counters");
-  if (PB.slab) hip_check(hipMemsetAsync(PB.scnt.p, 0, size_t(kPart1N) * PB.nwg * 8, st), "slab counters");
-  P.part_cursor = P.part_fused ? ctr : (PB.slab ? devp(PB.scnt) : nullptr);
-  P.part_overflow = (P.part_fused || PB.slab) ? ctr + PB.ctr_words() - 3 : nullptr;  // overflow[0]: first pass
+  P.part_cursor = nullptr;
+  P.part_overflow = nullptr;
   P.part_cap = PB.cap1;
-  if (P.part_fused || PB.slab) P.kq.table = reinterpret_cast<unsigned long long*>(PB.out1.p);
 }
 
-// After the scan: first pass (unless fused), second pass, aggregation.
+// After the scan: first pass, second pass, aggregation.
 void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   const int64_t N = P.rec_total;
   unsigned long long* ctr = devp(PB.ctr);
@@ -3668,7 +3590,7 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   unsigned long long* tail = ctr + PB.ctr_words() - 4;  // ocount, overflow[3]
   if (N == 0) return;
   const uint64_t keymask = (uint64_t(1) << P.part_keybits) - 1u;
-  if (!P.part_fused && !PB.slab) {
+  {
     const uint64_t* recs = reinterpret_cast<const uint64_t*>(P.kq.table);
     const int64_t chunks1 = (N + kPartChunkRecs - 1) / kPartChunkRecs;
     if (chunks1 > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
@@ -3682,12 +3604,11 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   int64_t acap = PB.cap1;
   int aparts = kPart1N;
   if (PB.pass2()) {
-    // slab mode: region r = slab (bucket r / nwg, workgroup r % nwg), counts in scnt
-    const int64_t nreg = PB.slab ? int64_t(kPart1N) * PB.nwg : kPart1N;
+    const int64_t nreg = kPart1N;
     const int64_t chunks2 = (PB.cap1 + kPartChunkRecs - 1) / kPartChunkRecs;
     if (chunks2 * nreg > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
-    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, PB.slab ? devp(PB.scnt) : c1,
-                                   PB.slab ? 1 : kCursorStride, int(nreg), PB.slab ? int(PB.nwg) : 1, PB.cap1,
+    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, kCursorStride, int(nreg),
+                                   1, PB.cap1,
                                    int(chunks2), keymask, 64 - kPart1Bits - PB.nbits2, PB.nbits2,
                                    PB.out2.as<uint64_t>(), PB.cap2, c2, kCursorStride, tail + 2, st),
               "partition pass 2");
@@ -3699,17 +3620,8 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   // count and sum share one LDS add when a partition's count and value sum both fit their bit fields
   const int cbits = bits_for(acap + 1);
   const int pack_shift = (2 * cbits + P.part_vbits <= 64) ? 64 - cbits : 0;
-  if (P.part_img && PB.slab) {  // the image aggregation only on the slab path it was measured on
-    PGX_LAUNCH(st, "pgx_part_aggregate_img",
-               pgx_launch_part_aggregate_img(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits,
-                                             P.part_vbase, P.part_img, P.part_img_words, P.part_img_sh, P.part_vdict,
-                                             P.part_min, P.part_max, pack_shift, PB.okey.as<uint64_t>(),
-                                             PB.oplane.as<uint64_t>(), PB.ocap, tail, tail + 3, P.part_grid, st),
-               "partition aggregate (value image)");
-    return;
-  }
   PGX_LAUNCH(st, "pgx_part_aggregate", pgx_launch_part_aggregate(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits, P.part_vbase,
-                                      P.part_dictid ? P.part_vdict : nullptr, P.part_sum, P.part_min, P.part_max,
+                                      P.part_sum, P.part_min, P.part_max,
                                       pack_shift, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(), PB.ocap, tail,
                                       tail + 3, st),
             "partition aggregate");
@@ -3723,7 +3635,7 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
   for (int attempt = 0; attempt < 12; ++attempt) {
     if (!part_alloc(ctx, P, PB)) return false;
     part_prepare(P, PB, st);
-    if (attempt == 0 || P.part_fused || PB.slab) {  // a fused first pass reruns with the scan (statistics restart too)
+    if (attempt == 0) {
       reset_outputs(P, B, st);
       launch_scan(P, st);
     }
@@ -3742,23 +3654,17 @@ bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB,
       return int64_t(m);
     };
     if (tail[1]) {  // a first-pass bucket overflowed: size to the largest (cursors count every record)
-      if (PB.slab) {
-        std::vector<unsigned long long> sc(size_t(kPart1N) * PB.nwg);
-        hip_check(hipMemcpy(sc.data(), PB.scnt.p, sc.size() * 8, hipMemcpyDeviceToHost), "slab counters D2H");
-        PB.cap1 = int64_t(*std::max_element(sc.begin(), sc.end())) + 1024;
-      } else {
-        PB.cap1 = max_cursor(0, kPart1N) + 1024;
-      }
+      PB.cap1 = max_cursor(0, kPart1N) + 1024;
       continue;
     }
     if (tail[2]) {
       PB.cap2 = max_cursor(kPart1N * kCursorStride, PB.nparts()) + 1024;
       continue;
     }
-    if (PB.nbits2 == (part_debug() ? 1 : part_max_bits2(P))) return false;  // an LDS table overflowed at the finest split
+    if (PB.nbits2 == (part_debug(P) ? 1 : part_max_bits2(P))) return false;  // an LDS table overflowed at the finest split
     ++PB.nbits2;
     const int64_t np = PB.nparts();
-    PB.cap2 = P.rec_total / np + P.rec_total / np / 4 + (part_debug() ? 1 : 16384);
+    PB.cap2 = P.rec_total / np + P.rec_total / np / 4 + (part_debug(P) ? 1 : 16384);
   }
   return false;
 }
@@ -3800,8 +3706,8 @@ bool narrow_size(const ExecPlan& P, NarrowBuffers& NB) {
   ub = std::min(ub, prod);
   NB.k2 = P.narrow_k2min;
   while (NB.k2 < kNarrowMaxBits2 && NB.k2 < NB.rb1 && ub / double(int64_t(1) << (kNarrow1Bits + NB.k2)) > 64.0) ++NB.k2;
-  if (const char* e = std::getenv("PGX_NARROW_K2"))  // tests: coarser partitions, to drive the table-overflow fallback
-    NB.k2 = std::max(P.narrow_k2min, std::min(std::atoi(e), std::min(kNarrowMaxBits2, NB.rb1)));
+  if (P.kn.narrow_k2 >= 0)  // tests (PGX_DEBUG=narrow_k2=N): coarser partitions, to drive the table-overflow fallback
+    NB.k2 = std::max(P.narrow_k2min, std::min(P.kn.narrow_k2, std::min(kNarrowMaxBits2, NB.rb1)));
   if (NB.k2 > kNarrowMaxBits2 || NB.k2 > NB.rb1) return false;
   NB.rb2 = NB.rb1 - NB.k2;
   if (NB.rb2 + P.narrow_vd > 32 || NB.rb2 > 31) return false;
@@ -3920,19 +3826,18 @@ bool run_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hi
     NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4);
     scan = false;
   }
-  if (std::getenv("PGX_NARROW_DEBUG"))  // tests: which path ran
+  if (P.kn.narrow_log)  // tests (PGX_DEBUG=narrow_log): which path ran
     std::fprintf(stderr, "[pgx narrow] nwg=%lld cap1=%lld k2=%d cap2=%lld groups=%llu ovf=%llu/%llu/%llu attempts=%d ok=%d\n",
                  (long long)NB.nwg, (long long)NB.cap1, NB.k2, (long long)NB.cap2, tail[0], tail[1], tail[2], tail[3],
                  attempt + (ok ? 1 : 0), int(ok));
   return ok;
 }
 
-// The radix path's plan after a narrow attempt gave up: its own slab / dictId choices, 8-byte records.
+// The radix path's plan after a narrow attempt gave up: row-order 8-byte value records.
 void narrow_fallback(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
   P.part_narrow = false;
-  P.part_slab = P.narrow_old_slab;
-  P.part_dictid = P.narrow_old_dictid;
-  P.part_fused = P.narrow_old_fused;
+  P.part_slab = false;
+  P.part_dictid = false;
   P.part_hi = nullptr;
   plan_jit(ctx, q, segs, n, P, B);
 }
@@ -4080,14 +3985,12 @@ void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, 
   R->lazy = std::move(L);
 }
 
-// PGX_HOST_PROFILE=1: per-phase host wall time of every pgx_execute on stderr (host overhead hunting).
+// PGX_DEBUG=host_profile: per-phase host wall time of every pgx_execute on stderr (host overhead hunting).
 struct HostProf {
   bool on = false;
   std::chrono::steady_clock::time_point t0, last;
   std::string line;
-  HostProf() {
-    const char* e = std::getenv("PGX_HOST_PROFILE");
-    on = e && e[0] == '1';
+  explicit HostProf(bool enable) : on(enable) {  // PGX_DEBUG=host_profile
     if (on) t0 = last = std::chrono::steady_clock::now();
   }
   void mark(const char* what) {
@@ -4115,18 +4018,16 @@ struct HostProf {
 bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                  const pgx_exec_opts* opts, pgx_result* R, hipStream_t st, uint32_t xflags, HostProf& hp) {
   int bs = (xflags & PGX_X_THROUGHPUT) ? 0 : 512;
-  if (const char* e = std::getenv("PGX_BATCH_SEGS")) bs = std::atoi(e);
-  if (bs <= 0 || n < 2 * bs || !jit_enabled()) return false;
+  if (q.kn.batch_segs >= 0) bs = q.kn.batch_segs;
+  if (bs <= 0 || n < 2 * bs || !q.kn.jit) return false;
   const size_t L = q.leaf_col.size();
   std::vector<GlobalDict> full;
   for (int g = 0; g < int(q.group_cols.size()); ++g) full.push_back(group_dict(q, segs, n, g));
   hp.mark("b.dicts");
   // Batch sizes double from a small first batch up to bs: every batch is planned concurrently from t = 0, and batch k
   // (twice batch k - 1) is ready by the time the GPU has run batches 0 .. k - 1 (~1 us of planning per segment on one
-  // planner thread against ~1.5 us of GPU time per C5 segment).  PGX_BATCH_FIRST tunes the first size.
-  int first = 64;
-  if (const char* e = std::getenv("PGX_BATCH_FIRST")) first = std::atoi(e);
-  first = std::max(1, std::min(first, bs));
+  // planner thread against ~1.5 us of GPU time per C5 segment).
+  const int first = std::max(1, std::min(64, bs));
   std::vector<int> start{0};
   for (int size = first; start.back() < n; size = std::min(bs, 2 * size)) {
     const int left = n - start.back();
@@ -4144,7 +4045,7 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   std::condition_variable cv;
   int done = 0;
   const int dev = ctx->device;
-  std::vector<std::string> prof(hp.on ? nb : 0);  // PGX_HOST_PROFILE: each planner's phase marks
+  std::vector<std::string> prof(hp.on ? nb : 0);  // PGX_DEBUG=host_profile: each planner's phase marks
   // set when batch 0 turns out ineligible: the tasks not yet started return at once (the caller re-plans the list)
   std::atomic<bool> cancel{false};
   auto plan_one = [&, dev](int b) {
@@ -4157,7 +4058,7 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
       cv.notify_all();
       return;
     }
-    HostProf bp;
+    HostProf bp(hp.on);
     if (bp.on) g_prof_mark = [&bp](const char* w) { bp.mark(w); };
     try {
       hip_check(hipSetDevice(dev), "hipSetDevice");  // device buffers and JIT modules belong to the context's device
@@ -4212,8 +4113,8 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   // for them with an event.  The copies' SDMA latency and the bitmap programs of batch k + 1 then run while batch k's
   // query kernel streams the forward indexes, instead of between the query kernels.  Declared after the buffers:
   // on any exit both streams drain before the buffers return to the pool.
-  const bool two = std::getenv("PGX_BATCH_ONE_STREAM") == nullptr;
-  hipStream_t ss = two ? ctx->side : st;
+  const bool two = true;
+  hipStream_t ss = ctx->side;
   struct Events {
     hipStream_t a, b;
     std::vector<hipEvent_t> ev;
@@ -4309,7 +4210,7 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
 void run_mv(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
             uint32_t xflags, pgx_result* R, hipStream_t st) {
   if (!q.group_cols.empty()) fail(PGX_ERR_UNSUPPORTED, "multi-value functions with GROUP BY");
-  if (!jit_enabled()) fail(PGX_ERR_UNSUPPORTED, "multi-value functions need the query kernels");
+  if (!q.kn.jit) fail(PGX_ERR_UNSUPPORTED, "multi-value functions need the query kernels");
   pgx_query qs = q;
   qs.flags |= PGX_Q_NO_STAR_TREE;  // every raw row gets its selection bit
   qs.agg_fn.clear();
@@ -4430,7 +4331,7 @@ void run_mv(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, c
 // single-value ones (dense slots, or 64 / 128-bit hash keys), so finish_result decodes the table as usual.
 void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                   uint32_t xflags, pgx_result* R, hipStream_t st, const Domain* dom = nullptr) {
-  if (!jit_enabled()) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by needs the query kernels");
+  if (!q.kn.jit) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by needs the query kernels");
   const int na = int(q.agg_fn.size()), ng = int(q.group_cols.size());
   if (ng < 1 || ng > kMaxGroupCols) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by: group column count");
   std::vector<int8_t> mvf(na), fpv(na, 0), cntp(na, -1);
@@ -4685,18 +4586,14 @@ void complete_scan(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
 // Plan cache: a server runs the same query shape over the same segments again and again (and the bench's steps do).
 // Planning a 4,096-segment query costs ~2.5-3 ms of host time (predicate leaves, bitmap programs and chunk descriptors,
 // key spaces, the argument arena, per-segment kernel descriptors: p.* / upload / j.sig / jit phases of
-// PGX_HOST_PROFILE) before the first launch.  A plan whose state is the argument arena and the bitmap masks (dense or
+// PGX_DEBUG=host_profile) before the first launch.  A plan whose state is the argument arena and the bitmap masks (dense or
 // aggregation-only, no partitioned / hash / multi-value / automaton buffers) is kept after its execution, with its
-// device arena, keyed by the query, the segment list (unique segment ids), the bindings' content, the planning flags and
-// the PGX_* environment.  A later execution with the same key replays it: arena and descriptors re-sent, launches,
+// device arena, keyed by the query (which holds its PGX_* knobs), the segment list (unique segment ids), the bindings'
+// content and the planning flags.  A later execution with the same key replays it: arena and descriptors re-sent, launches,
 // read-back -- no planning.  An entry serves one execution at a time (the bench keeps three in flight: up to
 // kPlanCacheMax entries per query).  Entries hold a context reference; they go with their query
 // (pgx_query_release), their context (pgx_ctx_destroy) or by eviction.  PGX_PLAN_CACHE=0 turns the cache off.
 // -------------------------------------------------------------------------------------------------
-}  // namespace
-extern "C" char** environ;
-namespace {
-
 struct PlanEntry {
   pgx_ctx* ctx = nullptr;
   std::vector<uint64_t> uids;
@@ -4726,8 +4623,8 @@ bool plan_cache_on() {
   return on;
 }
 
-// Hash of the planning inputs that are not the segment list: context, planning flags, the PGX_* environment (A/B knobs
-// select plans), every binding's range and its bitset's content (a bitset shared by consecutive segments -- one
+// Hash of the planning inputs that are not the segment list: context, planning flags, every binding's range and its
+// bitset's content (the PGX_* knobs are the query's own, fixed at compile time: entries are kept per query) (a bitset shared by consecutive segments -- one
 // dictionary -- is hashed once).  64-bit multiply-xorshift steps: ~12k bindings at C5.
 uint64_t plan_key(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                   uint32_t xflags) {
@@ -4740,20 +4637,6 @@ uint64_t plan_key(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, in
   mix(reinterpret_cast<uintptr_t>(ctx));
   mix(uint64_t(n));
   mix(xflags & ~(PGX_X_THROUGHPUT | PGX_X_KEEP_DENSE_ON_DEVICE));
-  for (char** e = environ; *e; ++e)
-    if (std::strncmp(*e, "PGX_", 4) == 0) {
-      uint64_t w = 0;
-      int k = 0;
-      for (const char* c = *e; *c; ++c) {
-        w = (w << 8) | uint8_t(*c);
-        if (++k == 8) {
-          mix(w);
-          w = 0;
-          k = 0;
-        }
-      }
-      mix(w ^ (uint64_t(k) << 56));
-    }
   const size_t L = q.leaf_col.size();
   if (!L || !bindings) return h;
   std::vector<const uint32_t*> last_ptr(L, nullptr);
@@ -4876,7 +4759,7 @@ bool plan_cacheable(const ExecPlan& P) {
 
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
                const pgx_exec_opts* opts, pgx_result* R, const Domain* dom = nullptr) {
-  HostProf hp;
+  HostProf hp(q.kn.host_profile);
   if (hp.on) g_prof_mark = [&hp](const char* w) { hp.mark(w); };
   struct Unmark { ~Unmark() { g_prof_mark = nullptr; } } unmark;
   hipStream_t st = (opts && opts->stream) ? reinterpret_cast<hipStream_t>(opts->stream) : ctx->stream;
@@ -4961,11 +4844,13 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     P.jit.clear();
   }
   const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
+  uint64_t hash_est = 0;
   if (hash) {
-    P.hash_cap = initial_hash_cap(segs, n, P);
-    // the generated kernels pre-aggregate in LDS and send the global table distinct keys only: start at 1M slots
-    // (the overflow count grows it 4x and reruns), not at one slot per row of a wide key space -- a 64M-slot table
-    // costs more to clear and compact than the scan (C7: 330 ms of host and device per query)
+    P.hash_cap = hash_est = initial_hash_cap(segs, n, P);
+    // the generated kernels pre-aggregate in LDS and send the global table distinct keys only: start at 1M slots, not
+    // at one slot per row of a wide key space -- a 64M-slot table costs more to clear and compact than the scan (C7:
+    // 330 ms of host and device per query).  An overflow reruns at the row-count estimate at once (C3-sized group
+    // counts: one short failed pass -- every lane stops probing at the first overflow -- then one full pass)
     if (!P.jit.empty()) P.hash_cap = std::min<uint64_t>(P.hash_cap, uint64_t(1) << 20);
   }
   for (int attempt = 0; attempt < 6; ++attempt) {
@@ -4978,7 +4863,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
     hip_check(hipStreamSynchronize(st), "sync");
     if (outs[24] == 0) break;
-    P.hash_cap *= 4;  // table full: grow and rerun
+    P.hash_cap = std::max(P.hash_cap * 4, hash_est);  // table full: grow and rerun
     if (attempt == 5) fail(PGX_ERR_OOM, "group-by hash table overflow");
   }
   complete_scan(ctx, q, P, B, segs, n, opts, st, R);
@@ -5602,6 +5487,7 @@ pgx_status pgx_query_compile(pgx_ctx* ctx, const pgx_query_desc* d, pgx_query** 
       q->leaf_kind.push_back(d->leaves[l].kind);
     }
     q->flags = d->flags;
+    q->kn = read_knobs();
     *out = q.release();
   });
 }

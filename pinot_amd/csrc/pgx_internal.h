@@ -218,6 +218,31 @@ constexpr uint64_t kNarrowC1 = 0x9E3779B1ull;
 constexpr int kNarrow1Bits = 8;      // first split (inside the scan): 256 buckets
 constexpr int kNarrowRing = 64;      // scan: per-bucket LDS ring of records (two 32-record units)
 constexpr int kNarrowMaxBits2 = 10;  // second split (pgx_narrow_split): up to 1024 sub-buckets per bucket
+// Environment knobs (A/B switches and test hooks), read ONCE per query by pgx_query_compile and kept with the query:
+// planning and execution read them from there, never from the environment (no per-query walk of environ, no race
+// with a setenv on another thread).  The whole set:
+//   PGX_JIT=0          the generic interpreter kernel instead of the generated (hiprtc) kernels, everywhere (A/B)
+//   PGX_PART_NARROW=0  sparse group-by through the 8-byte radix path instead of the narrow records
+//   PGX_RCHUNK=0|1     bitmap programs evaluated by the separate pass / inside the query kernels (default: planner)
+//   PGX_RPROG=off|wave|seg|chunk|stack   bitmap-program kernel (off: no program fusion; default: planner)
+//   PGX_BATCH_SEGS=N   segments per batch of a long segment list on its first execution (0: one launch)
+//   PGX_DEBUG=opt,...  part_small (radix buckets start undersized), narrow_k2=N (coarser narrow partitions),
+//                      narrow_log (which sparse path ran, on stderr), host_profile (planning phases on stderr)
+// and, outside the query: PGX_PLAN_CACHE=0 (process-wide), PGX_JIT_CACHE=<dir> / PGX_JIT_DUMP=<dir> (the compiler).
+enum RProgKind { RPROG_AUTO = -1, RPROG_OFF = 0, RPROG_WAVE = 1, RPROG_SEG = 2, RPROG_CHUNK = 3, RPROG_STACK = 4 };
+struct Knobs {
+  bool jit = true;
+  bool narrow = true;
+  int rchunk = -1;          // -1: planner's choice
+  int rprog = RPROG_AUTO;
+  int batch_segs = -1;      // -1: default (512; 0 with PGX_X_THROUGHPUT)
+  bool part_small = false;  // PGX_DEBUG part_small
+  int narrow_k2 = -1;       // PGX_DEBUG narrow_k2=N
+  bool narrow_log = false;  // PGX_DEBUG narrow_log
+  bool host_profile = false;
+};
+Knobs read_knobs();
+
 struct NarrowMix {
   uint64_t mask = 0, c1 = kNarrowC1, ic1 = 0;
   int s = 0;
@@ -268,8 +293,6 @@ struct JitShape {
   // G_HASH64 / G_HASH128: group ids at gshift of the low (ghi 0) or high (ghi 1) key word; hash_slots LDS slots
   std::vector<int> ghi;
   int hash_slots = 0;
-  bool hash_batch = false;  // hash group-by: every row's home-slot read of a sub-step issued before any is resolved
-                            // (PGX_HASH_BATCH=1; measured slower at C7: 8.1 vs 5.1 ms, register pressure)
   bool leafmask = false;  // write every leaf's per-row predicate bit (statistics automaton input, pgx_stats.cpp)
   // LEAF_RCHUNK leaves, in leaf order: the bitmap program's postfix ops (RP_*), identical for the group's segments
   std::vector<std::vector<int>> rprog_ops;
@@ -280,12 +303,6 @@ struct JitShape {
   // with part_bits: each workgroup appends to its own region ("slab") per bucket through LDS cursors, no staging and no
   // global cursor per sub-step (slab (b, w) at table + (b * part_nwg + part_wg_base + w) * part_cap)
   bool part_slab = false;
-  // forward-index words of a lane that are not a multiple of 4 / 2 dwords (e.g. 10-bit columns at R = 16: 5 dwords)
-  // load as dword-aligned 16-byte loads plus a remainder instead of one load per dword
-  bool ld_x4 = false;
-  // dense group-by over sparse selections: the group-table updates of a sub-step run per slot of a lane's first sel_k
-  // selected rows (0: per row)
-  int sel_k = 0;
   // dense LDS group-by of COUNT + one integer SUM / AVG with a value image: both planes in ONE 64-bit LDS add, the
   // row count above bit dense_pack (the value offset below), flushed per segment (0: two adds per row)
   int dense_pack = 0;

@@ -128,20 +128,17 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // R + 2 words (conflict-free 16-byte LDS writes); rounds of stg_recs records when the budget is tight.
   int stg_off = -1, stg_recs = 0;
   const int stg_pitch = s.R + 2;
-  // G_EMIT with part_bits: the sub-step's PT * PR records are split 2^part_bits ways in LDS (histogram, scan, one
-  // cursor reservation per bucket, bucket-sorted staging) and leave as per-bucket runs: the first radix pass of the
-  // partitioned group-by, fused into the scan.  Cursors: one global cursor per bucket (reserved every sub-step), or
-  // with part_slab this workgroup's own slab of each bucket (an LDS cursor: no global round trip per sub-step)
+  // G_EMIT with part_bits (narrow records only: part_slab and part_narrow): the sub-step's records are split
+  // 2^part_bits ways into this workgroup's slab of each bucket, a u32 array and a u16 array (records wider than 32
+  // bits), written through per-bucket LDS rings so that only whole 32-record units leave (128-B u32 / 64-B u16 lines,
+  // see the sub-step below).  Without part_bits the records leave in row order (the 8-byte radix path).
   const bool epart = emit && s.part_bits > 0;
-  const bool eslab = epart && s.part_slab;
-  // narrow records (slab mode only): a u32 array and a u16 array (records wider than 32 bits), written through
-  // per-bucket LDS rings so that only whole 32-record units leave (128-B u32 / 64-B u16 lines, see the sub-step below)
-  const bool enarrow = eslab && s.part_narrow;
+  const bool enarrow = epart && s.part_slab && s.part_narrow;
   const int nrb1 = s.keybits - s.part_bits;  // narrow: bits of the key's mix left in the record
   const bool nhib = enarrow && nrb1 + s.narrow_vbits > 32;
   const int pnb = 1 << s.part_bits;
   // (narrow: pnb = 256 and T a multiple of 256 -- plan_jit's choices; four owner wavefronts hold one bucket per lane)
-  int pst_off = -1, phist_off = -1, nring_off = -1, nringb_off = -1, nst_off = -1;
+  int nring_off = -1, nringb_off = -1, nst_off = -1;
   if (enarrow) {
     lds = (lds + 15) & ~15;  // 16-byte ring reads and writes
     nring_off = lds;
@@ -152,12 +149,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     // [4][128] each, list counts[4]
     nst_off = lds;
     lds += pnb * 4 * 5 + 4 * 128 * 2 + 4 * 128 * 4 + 16;
-  } else if (epart) {
-    pst_off = lds;
-    lds += s.T * s.R * 8;
-    phist_off = lds;
-    // hist (u32), offs (u32), gpos (u64), total[, slab fill (u32)]
-    lds += pnb * 16 + 16 + (eslab ? pnb * 4 : 0);
   }
   if (emit && !epart) {
     const int waves = s.T / 64;
@@ -209,7 +200,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const bool any_img = lds > 0 && (tab_off != 0 || s.group_mode != G_DENSE_LDS);
 
   Emitter e;
-  if (s.ld_x4) e.o << "#define PGX_LD_X4 1\n";
   e.o << kAbiSrc << "\n" << kDevSrc << "\n";
   e.ln("#define PT ", s.T);
   e.ln("#define PR ", s.R);
@@ -287,16 +277,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ln("PGX_G u32* const poutA = (PGX_G u32*)A.table;");
     if (nhib) e.ln("PGX_G unsigned short* const poutB = (PGX_G unsigned short*)A.part_hi;");
     e.ln("const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
-    e.ln("__syncthreads();");
-  } else if (epart) {
-    e.ln("u64* const pstage = (u64*)(lds + ", pst_off / 4, ");");
-    e.ln("u32* const phist = lds + ", phist_off / 4, ";");
-    e.ln("u32* const poffs = phist + ", pnb, ";");
-    e.ln("u64* const pgpos = (u64*)(phist + ", 2 * pnb, ");");
-    e.ln("u32* const ptotal = phist + ", 4 * pnb, ";");
-    if (eslab) e.ln("u32* const pfill = phist + ", 4 * pnb + 4, ";");
-    e.ln("for (int i = tid; i < ", pnb, "; i += PT) phist[i] = 0u;");
-    if (eslab) e.ln("for (int i = tid; i < ", pnb, "; i += PT) pfill[i] = 0u;");
     e.ln("__syncthreads();");
   }
   e.ln("u64 st_docs = 0, st_ent = 0;");
@@ -420,12 +400,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       for (size_t g = 0; g < s.gcol.size(); ++g)
         if (s.cols[s.gcol[g]].remap) gremap[g] = split = true;
   }
-  // sel_k > 0 (dense group-by, values from LDS images): after the filter pass, each lane moves its first sel_k selected
-  // rows' group ids and values into slots (compare + select, no dynamic register indexing) and the group-table updates
-  // run once per slot instead of once per row; rows past the sel_k-th of a lane take the per-row loop (a wave-uniform
-  // branch that sparse filters rarely enter).  With 3.7% of rows selected, 16 row-steps per sub-step of which ~15
-  // still carry a selected lane become 4 slot-steps.
-  const bool dense_g = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL;
   const bool pack = s.dense_pack > 0 && s.group_mode == G_DENSE_LDS && s.num_planes == 2 && naggs == 1 &&
                     (s.agg_kind[0] == A_SUM || s.agg_kind[0] == A_AVG) && !s.cols[s.agg_col[0]].fp &&
                     s.cols[s.agg_col[0]].img != IMG_NONE && !emit;
@@ -433,18 +407,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const bool hpack = s.dense_pack > 0 && hashm && s.num_planes == 2 && naggs == 1 &&
                      (s.agg_kind[0] == A_SUM || s.agg_kind[0] == A_AVG) && !s.cols[s.agg_col[0]].fp &&
                      s.cols[s.agg_col[0]].img != IMG_NONE;
-  bool sel = s.sel_k > 0 && dense_g && !emit && !compact;
-  for (int c = 0; c < ncols && sel; ++c) sel = !gcolv[c];
-  for (size_t g = 0; g < s.gcol.size() && sel; ++g) sel = !gremap[g];
-  std::vector<int> selcols;  // columns whose values the slots carry: group columns, then aggregated columns
-  if (sel) {
-    split = true;
-    for (int c : s.gcol)
-      if (std::find(selcols.begin(), selcols.end(), c) == selcols.end()) selcols.push_back(c);
-    for (int a = 0; a < naggs; ++a)
-      if (s.agg_kind[a] != A_COUNT && std::find(selcols.begin(), selcols.end(), s.agg_col[a]) == selcols.end())
-        selcols.push_back(s.agg_col[a]);
-  }
   for (int c = 0; c < ncols; ++c) {
     if (need_vb[c]) e.ln("const i64 vb", c, " = S->vbase[", c, "];");
     if (need_dict[c]) {
@@ -601,11 +563,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
           e.ln("u32 p", a, " = 0u;");
       }
     if (emit) e.ln("u64 recs[PR];");
-    const bool hbatch = hashm && s.hash_batch;
-    if (hbatch) {
-      e.ln("u32 hm = 0u, hq[PR], hsv[PR];");
-      e.ln(h128 ? "pgx_u32x4 hkv[PR];" : "u64 hkv[PR];");
-    }
     if (split) e.ln("u32 msk = 0u;");
     if (s.selmask) e.ln("u32 smk = 0u;");
     if (s.leafmask)
@@ -698,29 +655,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
                            "[v", c, "[0]] : 0};");
       for (size_t g = 0; g < s.gcol.size(); ++g)
         if (gremap[g]) e.ln("u32 gr", g, "[1] = {m ? (u32)rm", g, "[v", s.gcol[g], "[0]] : 0u};");
-    } else if (sel) {
-      e.ln("msk |= (u32)m << j;");
-      e.ind = 5;
-      e.ln("}");
-      const int K = s.sel_k;
-      for (int c : selcols) e.ln("u32 sv", c, "[", K, "] = {};");
-      e.ln("#pragma unroll");
-      e.ln("for (int j = 0; j < PR; ++j) {");
-      e.ln("  const u32 rank = __popc(msk & ((1u << j) - 1u));  // selected rows before row j");
-      e.ln("  const bool mj = (msk >> j) & 1u;");
-      e.ln("  #pragma unroll");
-      e.ln("  for (int q = 0; q < ", K, "; ++q)");
-      e.ln("    if (mj && rank == (u32)q) {");
-      for (int c : selcols) e.ln("      sv", c, "[q] = v", c, "[j];");
-      e.ln("    }");
-      e.ln("}");
-      e.ln("const u32 nsel = __popc(msk);");
-      e.ln("#pragma unroll");
-      e.ln("for (int q = 0; q < ", K, "; ++q) {");
-      e.ind = 6;
-      e.ln("const bool m = (u32)q < nsel;");
-      e.ln("const int j = 0;");
-      for (int c : selcols) e.ln("const u32 v", c, "[1] = {sv", c, "[q]};");
     } else if (split) {
       e.ln("msk |= (u32)m << j;");
       e.ind = 5;
@@ -745,7 +679,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ind = 6;
       e.ln("const bool m = (msk >> j) & 1u;");
     }
-    // dense group-by update of the row (j, m) in scope (sel mode: emitted for the slots and for the overflow rows)
+    // dense group-by update of the row (j, m) in scope
     auto emit_dense = [&]() {
       // dense group-by: key = sum_g id_g * mul_g (column 0 least significant, DefaultGroupKeyGenerator.java:230-237)
       e.ln("if (m) {");
@@ -789,8 +723,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     };
     // hash group-by: the packed raw key (LONG_MAP / ARRAY_MAP, DefaultGroupKeyGenerator.java:239-246), a slot of the
     // workgroup's LDS table, or of the global table when the LDS one has no room for it
-    auto emit_hash = [&](bool resolve) {
-      e.ln(resolve ? "if ((hm >> j) & 1u) {" : "if (m) {");
+    auto emit_hash = [&]() {
+      e.ln("if (m) {");
       e.ind = 7;
       std::string klo = "0ull", khi = "0ull";
       for (size_t g = 0; g < s.gcol.size(); ++g) {
@@ -803,30 +737,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       }
       e.ln("const u64 klo = ", klo, ";");
       if (h128) e.ln("const u64 khi = ", khi, ";");
-      if (hbatch && !resolve) {  // pass 1: the home slot's state and key, read back to back for every row
-        e.ln("const int h = (int)(", h128 ? "pgx_mix64(klo ^ pgx_mix64(khi))" : "pgx_mix64(klo)", " & ", HS - 1, "ull);");
-        e.ln("hq[j] = (u32)h;");
-        if (h128) {
-          e.ln("hsv[j] = hst[h];");
-          e.ln("hkv[j] = *(const pgx_u32x4*)(hk + 2 * h);");
-        } else {
-          e.ln("hkv[j] = hk[h];");
-        }
-        e.ln("hm |= 1u << j;");
-        e.ind = 6;
-        e.ln("}");
-        return;
-      }
-      if (hbatch) {  // pass 2: a home slot that held the key needs no probe
-        if (h128)
-          e.ln("const int ls = (hsv[j] == 2u && (((u64)hkv[j].y << 32) | hkv[j].x) == klo && (((u64)hkv[j].w << 32) | hkv[j].z) == khi) ? (int)hq[j] : pgx_lhash128(hk, hst, ",
-               HS, ", klo, khi);");
-        else
-          e.ln("const int ls = hkv[j] == klo ? (int)hq[j] : pgx_lhash64(hk, ", HS, ", klo);");
-      } else {
         e.ln("const int ls = ", h128 ? "pgx_lhash128(hk, hst, " + std::to_string(HS) + ", klo, khi)"
                                      : "pgx_lhash64(hk, " + std::to_string(HS) + ", klo)", ";");
-      }
       std::vector<std::string> encs(naggs);
       for (int a = 0; a < naggs; ++a) {
         const int k = s.agg_kind[a];
@@ -854,8 +766,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
             e.ln("  ", plane_atomic(s.plane_op[a + 1], "&ht[" + std::to_string((a + 1) * HS) + " + ls]", encs[a]));
       }
       e.ln("} else {");
-      e.ln("  const long long gs = ", h128 ? "pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, klo, khi)"
-                                           : "pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, klo)", ";");
+      e.ln("  const long long gs = ", h128 ? "pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, klo, khi, A.overflow)"
+                                           : "pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, klo, A.overflow)", ";");
       e.ln("  if (gs < 0) {");
       e.ln("    atomicAdd(A.overflow, 1ull);");
       e.ln("  } else {");
@@ -927,38 +839,13 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         e.ln("}");
         e.ln("recs[j] = rec;");
       } else if (hashm) {
-        emit_hash(false);
+        emit_hash();
       } else {
         emit_dense();
       }
     }
     e.ind = 5;
     e.ln("}");
-    if (hbatch) {  // pass 2 of the batched hash updates
-      e.ln("#pragma unroll");
-      e.ln("for (int j = 0; j < PR; ++j) {");
-      e.ind = 6;
-      emit_hash(true);
-      e.ind = 5;
-      e.ln("}");
-    }
-    if (sel) {  // rows past a lane's first sel_k selected ones: the per-row loop, entered only if some lane has them
-      e.ln("{");
-      e.ln("  u32 rest = msk;");
-      e.ln("  #pragma unroll");
-      e.ln("  for (int q = 0; q < ", s.sel_k, "; ++q) rest &= rest - 1u;");
-      e.ln("  if (__ballot(rest != 0u)) {");
-      e.ln("    #pragma unroll");
-      e.ln("    for (int j = 0; j < PR; ++j) {");
-      e.ind = 6;
-      e.ln("const bool m = (rest >> j) & 1u;");
-      if (hashm) emit_hash(false);
-      else emit_dense();
-      e.ind = 5;
-      e.ln("    }");
-      e.ln("  }");
-      e.ln("}");
-    }
     if (compact) {
       e.ln("  pgx_wave_lds_sync();");
       e.ln("}");
@@ -1063,51 +950,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("  }");
       e.ln("  npar ^= 1;");
       e.ln("}");
-    } else if (epart) {
-      const std::string KM = std::to_string((1ull << s.keybits) - 1ull) + "ull";
-      const std::string SH = std::to_string(64 - s.part_bits);
-      e.ln("{");
-      e.ln("  u32 rk[PR];");
-      e.ln("  #pragma unroll");
-      e.ln("  for (int j = 0; j < PR; ++j)");
-      e.ln("    rk[j] = recs[j] != ~0ull ? atomicAdd(&phist[(u32)(pgx_part_mix(recs[j] & ", KM, ") >> ", SH,
-           ")], 1u) : 0u;");
-      e.ln("  pgx_lds_barrier();");
-      e.ln("  pgx_scan_buckets<", pnb, ">(phist, poffs, ptotal, tid);");
-      e.ln("  pgx_lds_barrier();");
-      e.ln("  if (tid < ", pnb, ") {");
-      e.ln("    const u32 h = phist[tid];");
-      if (eslab) {  // this workgroup's slab of bucket tid: position = fill so far (the kernel end publishes the fill)
-        e.ln("    pgpos[tid] = pfill[tid];");
-        e.ln("    pfill[tid] += h;");
-      } else {
-        e.ln("    if (h) {");
-        e.ln("      const u64 g = atomicAdd(A.part_cursor + (long long)tid * A.part_cstride, (u64)h);");
-        e.ln("      pgpos[tid] = g;");
-        e.ln("      if (g + h > (u64)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
-        e.ln("    }");
-      }
-      e.ln("    phist[tid] = 0u;  // ready for the next sub-step (its atomics follow two barriers)");
-      e.ln("  }");
-      e.ln("  pgx_lds_barrier();");
-      e.ln("  #pragma unroll");
-      e.ln("  for (int j = 0; j < PR; ++j)");
-      e.ln("    if (recs[j] != ~0ull) pstage[poffs[(u32)(pgx_part_mix(recs[j] & ", KM, ") >> ", SH, ")] + rk[j]] = recs[j];");
-      e.ln("  pgx_lds_barrier();");
-      e.ln("  const int tot = (int)*ptotal;");
-      e.ln("  PGX_G u64* const pout = (PGX_G u64*)A.table;");
-      if (eslab) e.ln("  const long long wsl = A.part_wg_base + (long long)blockIdx.x;");
-      e.ln("  for (int i = tid; i < tot; i += PT) {");
-      e.ln("    const u64 v = pstage[i];");
-      e.ln("    const u32 b = (u32)(pgx_part_mix(v & ", KM, ") >> ", SH, ");");
-      e.ln("    const u64 pos = pgpos[b] + (u64)(i - (int)poffs[b]);");
-      if (eslab)
-        e.ln("    if (pos < (u64)A.part_cap) pout[((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)pos] = v;");
-      else
-        e.ln("    if (pos < (u64)A.part_cap) pout[(long long)b * A.part_cap + (long long)pos] = v;");
-      e.ln("  }");
-      e.ln("  pgx_lds_barrier();");
-      e.ln("}");
     } else if (emit && stg_recs) {
       const int L = stg_recs / s.R;  // lanes whose records fill one round
       int lg = 0;
@@ -1191,8 +1033,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ln("for (int i = tid; i < ", HS, "; i += PT) {");
     e.ln("  const u64 x = ht[i];");
     e.ln("  if (x == 0ull) continue;");
-    e.ln("  const long long gs = ", h128 ? "pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, hk[2 * i], hk[2 * i + 1])"
-                                         : "pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, hk[i])", ";");
+    e.ln("  const long long gs = ", h128 ? "pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, hk[2 * i], hk[2 * i + 1], A.overflow)"
+                                         : "pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, hk[i], A.overflow)", ";");
     e.ln("  const u64 cnt = x >> ", s.dense_pack, ";");
     e.ln("  if (gs < 0) {");
     e.ln("    atomicAdd(A.overflow, cnt);");
@@ -1235,10 +1077,10 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ln("for (int i = tid; i < ", HS, "; i += PT) {");
     if (h128) {
       e.ln("  if (hst[i] != 2u) continue;");
-      e.ln("  const long long gs = pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, hk[2 * i], hk[2 * i + 1]);");
+      e.ln("  const long long gs = pgx_ghash128((PGX_G unsigned long long*)A.hkeys, (PGX_G unsigned int*)A.hstate, A.hash_cap, hk[2 * i], hk[2 * i + 1], A.overflow);");
     } else {
       e.ln("  if (hk[i] == ~0ull) continue;");
-      e.ln("  const long long gs = pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, hk[i]);");
+      e.ln("  const long long gs = pgx_ghash64((PGX_G unsigned long long*)A.hkeys, A.hash_cap, hk[i], A.overflow);");
     }
     e.ln("  if (gs < 0) {");
     e.ln("    atomicAdd(A.overflow, ht[i]);");
@@ -1265,12 +1107,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ln("for (int i = tid; i < 256; i += PT) {");
     e.ln("  const u32 h = ncur[i];");
     e.ln("  A.part_cursor[((long long)i * A.part_nwg + wsl) * A.part_cstride] = h;");
-    e.ln("  if (h > (u32)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
-    e.ln("}");
-  } else if (eslab) {  // slab fills (every record, also past part_cap: the host resizes from the largest)
-    e.ln("for (int i = tid; i < ", pnb, "; i += PT) {");
-    e.ln("  const u32 h = pfill[i];");
-    e.ln("  A.part_cursor[((long long)i * A.part_nwg + A.part_wg_base + (long long)blockIdx.x) * A.part_cstride] = h;");
     e.ln("  if (h > (u32)A.part_cap) atomicAdd(A.part_overflow, 1ull);");
     e.ln("}");
   }
@@ -1341,8 +1177,6 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.part_bits);
   k.push_back(s.emit_dictid);
   k.push_back(s.part_slab);
-  k.push_back(s.ld_x4);
-  k.push_back(s.sel_k);
   k.push_back(s.dense_pack);
   k.push_back(s.compact);
   k.push_back(s.selmask);
@@ -1350,7 +1184,6 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.narrow_vbits);
   add(s.ghi);
   k.push_back(s.hash_slots);
-  k.push_back(s.hash_batch);
   return k;
 }
 
@@ -1504,14 +1337,14 @@ extern "C" int pgx_jit_compile_check(const char* source, char* log, unsigned lon
     if (n) hiprtcGetProgramLog(prog, &l[0]);
     std::snprintf(log, log_cap, "%s", l.c_str());
   }
-  // debugging: PGX_JIT_CODE=<path> keeps the code object of the last compile (for llvm-objdump)
+  // debugging: with PGX_JIT_DUMP=<dir>, <dir>/last_check.co keeps the code object of the last compile (llvm-objdump)
   if (rc == HIPRTC_SUCCESS)
-    if (const char* path = std::getenv("PGX_JIT_CODE")) {
+    if (const char* dir = std::getenv("PGX_JIT_DUMP")) {
       size_t cs = 0;
       hiprtcGetCodeSize(prog, &cs);
       std::string code(cs, '\0');
       hiprtcGetCode(prog, &code[0]);
-      if (FILE* f = std::fopen(path, "wb")) {
+      if (FILE* f = std::fopen((std::string(dir) + "/last_check.co").c_str(), "wb")) {
         std::fwrite(code.data(), 1, cs, f);
         std::fclose(f);
       }
@@ -1589,17 +1422,11 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.R = 16;
     s.T = 1024;
     shapes.push_back(s);
-    s.ld_x4 = true;  // gk's 5 words per lane as one dword-aligned 16-byte load + one dword
-    shapes.push_back(s);
-    s.ld_x4 = false;  // R = 8: m's words contiguous per load; gk's 80 bits start mid-dword (frac)
-    s.R = 8;
+    s.R = 8;  // m's words contiguous per load; gk's 80 bits start mid-dword (frac)
     s.cols[4].frac = true;
     shapes.push_back(s);
-    s.R = 16;         // group-table updates per slot of a lane's first 4 selected rows
+    s.R = 16;  // count and sum in one 64-bit LDS add, flushed per segment
     s.cols[4].frac = false;
-    s.sel_k = 4;
-    shapes.push_back(s);
-    s.sel_k = 0;      // count and sum in one 64-bit LDS add, flushed per segment
     s.dense_pack = 40;
     shapes.push_back(s);
   }
@@ -1731,13 +1558,10 @@ extern "C" int pgx_jit_selftest(int* n_total, char* log, unsigned long log_cap) 
     s.cols[1].img = IMG_NONE;  // value image demoted (LDS budget): values from the HBM dictionary
     s.cols[2].remap = true;
     shapes.push_back(s);
-    s.part_bits = 7;           // first radix pass fused, dictId records
-    s.emit_dictid = true;
-    shapes.push_back(s);
-    s.cols[2].remap = false;    // ... into per-workgroup slabs (LDS cursors)
+    s.emit_dictid = true;       // narrow records: 26 bits of the key's mix + a 16-bit dictId (u32 + u16 arrays)
+    s.cols[2].remap = false;
     s.part_slab = true;
-    shapes.push_back(s);
-    s.part_bits = kNarrow1Bits;  // narrow records: 26 bits of the key's mix + a 16-bit dictId (u32 + u16 arrays)
+    s.part_bits = kNarrow1Bits;
     s.part_narrow = true;
     s.narrow_vbits = 16;
     shapes.push_back(s);

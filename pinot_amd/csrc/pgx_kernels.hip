@@ -197,7 +197,7 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 // Probe chains are bounded (kGlobalMaxProbes): at the load factors the host plans (<= 1/2) a longer chain means the
 // table is (nearly) full, so the lane reports overflow at once and the host regrows the table and reruns, instead of
 // walking the whole table with one device atomic per slot.
-constexpr uint64_t kGlobalMaxProbes = 512;
+constexpr uint64_t kGlobalMaxProbes = 64;
 
 __device__ __forceinline__ int64_t hash_slot64(const KQuery& Q, uint64_t key) {
   const uint64_t mask = Q.hash_cap - 1;
@@ -1792,12 +1792,11 @@ constexpr int kAggSlots = kAggBuckets * kAggWays;
 constexpr int kAggThreads = 1024;
 constexpr int kAggPer = 8;
 
-template <bool PACK, bool MN, bool MX, bool IDV>
+template <bool PACK, bool MN, bool MX>
 __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t* __restrict__ in,
                                                                   const unsigned long long* __restrict__ in_cnt,
                                                                   int cstride, int64_t cap, uint64_t keymask,
-                                                                  int keybits, int64_t vbase,
-                                                                  const int64_t* __restrict__ vdict, int pack_shift,
+                                                                  int keybits, int64_t vbase, int pack_shift,
                                                                   uint64_t* __restrict__ okey,
                                                                   uint64_t* __restrict__ oplane, int64_t ocap,
                                                                   unsigned long long* __restrict__ ocount,
@@ -1822,7 +1821,6 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
   const int64_t n = min(static_cast<int64_t>(in_cnt[static_cast<int64_t>(part) * cstride]), cap);
   const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) + static_cast<int64_t>(part) * cap;
   const unsigned long long one = PACK ? (1ull << pack_shift) : 0ull;
-  const PGX_GLOBAL int64_t* vd = (const PGX_GLOBAL int64_t*)vdict;  // dictId records: value = vd[id] (sorted dictionary)
   bool lost = false;
   for (int64_t base = 0; base < n; base += kAggThreads * kAggPer) {
     uint64_t rec[kAggPer];
@@ -1831,17 +1829,14 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
       const int64_t i = base + k * kAggThreads + tid;
       rec[k] = i < n ? __builtin_nontemporal_load(src + i) : kNoRecord;
     }
-    unsigned int sv[kAggPer];  // the values to sum: the record's offset, or (dictId records) gathered, all in flight
+    unsigned int sv[kAggPer];  // the values to sum: the records' offsets
 #pragma unroll
-    for (int k = 0; k < kAggPer; ++k) {
-      const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);
-      sv[k] = IDV ? (rec[k] != kNoRecord ? static_cast<unsigned int>(vd[v] - vbase) : 0u) : v;
-    }
+    for (int k = 0; k < kAggPer; ++k) sv[k] = static_cast<unsigned int>(rec[k] >> keybits);
 #pragma unroll
     for (int k = 0; k < kAggPer; ++k) {
       if (rec[k] == kNoRecord) continue;
       const uint64_t key = rec[k] & keymask;
-      const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);  // value offset, or dictId (vd)
+      const unsigned int v = static_cast<unsigned int>(rec[k] >> keybits);  // value offset
       unsigned int bk = static_cast<unsigned int>(part_mix(key)) & (kAggBuckets - 1);
       int slot = -1;
       for (int t = 0; t < kAggBuckets;) {
@@ -1891,126 +1886,14 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
     oplane[o] = c;  // plane 0: doc count
     // planes 1..3: sum (int64 incl. vbase * count), min, max (ordered encodings of the int64 value)
     oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(sm) + static_cast<int64_t>(c) * vbase);
-    const int64_t vlo = IDV ? (MN ? vd[lo] : 0) : vbase + static_cast<int64_t>(lo);  // min / max of dictIds -> values
-    const int64_t vhi = IDV ? (MX ? vd[hi] : 0) : vbase + static_cast<int64_t>(hi);
+    const int64_t vlo = vbase + static_cast<int64_t>(lo);
+    const int64_t vhi = vbase + static_cast<int64_t>(hi);
     oplane[2 * ocap + o] = static_cast<unsigned long long>(vlo) ^ 0x8000000000000000ull;
     oplane[3 * ocap + o] = static_cast<unsigned long long>(vhi) ^ 0x8000000000000000ull;
     ++o;
   }
 }
 
-// Variant for dictId records whose value column has a FOR16 image (sorted dictionary of <= 65536 values): the image
-// (64 block bases + one u16 offset per dictId, 128.25 KiB) lives in LDS beside a 1024-slot table, so SUM looks values
-// up in LDS instead of one L2 request per record.  The image costs one load per workgroup: the grid is persistent
-// (one workgroup per CU walks partitions blockIdx.x, + gridDim.x, ...).  MIN / MAX fold dictIds (sorted dictionary)
-// and map the two extremes through vdict when a group is written.
-constexpr int kAggImgBuckets = 256;
-constexpr int kAggImgSlots = kAggImgBuckets * kAggWays;
-constexpr int kAggImgWords = 64 + 65536 / 2;  // FOR16 image of a 65536-value dictionary, in dwords
-
-template <bool PACK, bool MN, bool MX>
-__global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate_img(const uint64_t* __restrict__ in,
-                                                                      const unsigned long long* __restrict__ in_cnt,
-                                                                      int cstride, int nparts, int64_t cap,
-                                                                      uint64_t keymask, int keybits, int64_t vbase,
-                                                                      const uint32_t* __restrict__ img, int img_words,
-                                                                      int img_sh, const int64_t* __restrict__ vdict,
-                                                                      int pack_shift, uint64_t* __restrict__ okey,
-                                                                      uint64_t* __restrict__ oplane, int64_t ocap,
-                                                                      unsigned long long* __restrict__ ocount,
-                                                                      unsigned long long* __restrict__ overflow) {
-  __shared__ __attribute__((aligned(16))) uint64_t tkey[kAggImgSlots];
-  __shared__ unsigned long long tsum[kAggImgSlots];
-  __shared__ unsigned int tcnt[PACK ? 1 : kAggImgSlots];
-  __shared__ unsigned int tmin[MN ? kAggImgSlots : 1], tmax[MX ? kAggImgSlots : 1];
-  __shared__ __attribute__((aligned(16))) uint32_t simg[kAggImgWords];
-  __shared__ int nfound;
-  __shared__ unsigned long long obase;
-  const int tid = threadIdx.x;
-  const PGX_GLOBAL uint32_t* gi = (const PGX_GLOBAL uint32_t*)img;
-  for (int i = tid; i < img_words; i += kAggThreads) simg[i] = gi[i];
-  const unsigned short* off16 = reinterpret_cast<const unsigned short*>(simg + 64);
-  const PGX_GLOBAL int64_t* vd = (const PGX_GLOBAL int64_t*)vdict;
-  const unsigned long long one = PACK ? (1ull << pack_shift) : 0ull;
-  const unsigned long long smask = PACK ? (1ull << pack_shift) - 1ull : ~0ull;
-  for (int part = blockIdx.x; part < nparts; part += gridDim.x) {
-    for (int i = tid; i < kAggImgSlots; i += kAggThreads) {
-      tkey[i] = kNoRecord;
-      tsum[i] = 0ull;
-      if (!PACK) tcnt[i] = 0u;
-      if (MN) tmin[i] = 0xFFFFFFFFu;
-      if (MX) tmax[i] = 0u;
-    }
-    if (tid == 0) nfound = 0;
-    __syncthreads();
-    const int64_t n = min(static_cast<int64_t>(in_cnt[static_cast<int64_t>(part) * cstride]), cap);
-    const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) + static_cast<int64_t>(part) * cap;
-    bool lost = false;
-    for (int64_t base = 0; base < n; base += kAggThreads * kAggPer) {
-      uint64_t rec[kAggPer];
-#pragma unroll
-      for (int k = 0; k < kAggPer; ++k) {
-        const int64_t i = base + k * kAggThreads + tid;
-        rec[k] = i < n ? __builtin_nontemporal_load(src + i) : kNoRecord;
-      }
-#pragma unroll
-      for (int k = 0; k < kAggPer; ++k) {
-        if (rec[k] == kNoRecord) continue;
-        const uint64_t key = rec[k] & keymask;
-        const unsigned int id = static_cast<unsigned int>(rec[k] >> keybits);
-        const unsigned int sv = simg[id >> img_sh] + static_cast<unsigned int>(off16[id]);  // value - vbase
-        unsigned int bk = static_cast<unsigned int>(part_mix(key)) & (kAggImgBuckets - 1);
-        int slot = -1;
-        for (int t = 0; t < kAggImgBuckets;) {
-          const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(&tkey[bk * kAggWays]);
-          const ulonglong2 a = bp[0], c = bp[1];
-          const int m = a.x == key ? 0 : a.y == key ? 1 : c.x == key ? 2 : c.y == key ? 3 : -1;
-          if (m >= 0) { slot = static_cast<int>(bk) * kAggWays + m; break; }
-          const int e = a.x == kNoRecord ? 0 : a.y == kNoRecord ? 1 : c.x == kNoRecord ? 2 : c.y == kNoRecord ? 3 : -1;
-          if (e >= 0) {
-            const int cand = static_cast<int>(bk) * kAggWays + e;
-            const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[cand]), kNoRecord, key);
-            if (prev == kNoRecord || prev == key) { slot = cand; break; }
-            continue;
-          }
-          bk = (bk + 1) & (kAggImgBuckets - 1);
-          ++t;
-        }
-        if (slot < 0) { lost = true; continue; }
-        if (PACK) {
-          atomicAdd(&tsum[slot], one + sv);
-        } else {
-          atomicAdd(&tcnt[slot], 1u);
-          atomicAdd(&tsum[slot], static_cast<unsigned long long>(sv));
-        }
-        if (MN) atomicMin(&tmin[slot], id);
-        if (MX) atomicMax(&tmax[slot], id);
-      }
-    }
-    if (lost) atomicAdd(overflow, 1ull);
-    __syncthreads();
-    int mine = 0;
-    for (int i = tid; i < kAggImgSlots; i += kAggThreads) mine += tkey[i] != kNoRecord;
-    const int before = atomicAdd(&nfound, mine);
-    __syncthreads();
-    if (tid == 0) obase = atomicAdd(ocount, static_cast<unsigned long long>(nfound));
-    __syncthreads();
-    unsigned long long o = obase + static_cast<unsigned long long>(before);
-    for (int i = tid; i < kAggImgSlots; i += kAggThreads) {
-      if (tkey[i] == kNoRecord) continue;
-      if (o >= static_cast<unsigned long long>(ocap)) { atomicAdd(overflow, 1ull); continue; }
-      okey[o] = tkey[i];
-      const unsigned long long c = PACK ? (tsum[i] >> pack_shift) : tcnt[i];
-      const unsigned long long sm = tsum[i] & smask;
-      oplane[o] = c;
-      oplane[ocap + o] = static_cast<unsigned long long>(static_cast<int64_t>(sm) + static_cast<int64_t>(c) * vbase);
-      oplane[2 * ocap + o] = static_cast<unsigned long long>(MN ? vd[tmin[i]] : 0) ^ 0x8000000000000000ull;
-      oplane[3 * ocap + o] = static_cast<unsigned long long>(MX ? vd[tmax[i]] : 0) ^ 0x8000000000000000ull;
-      ++o;
-    }
-    __syncthreads();  // the table is re-initialised for the next partition
-  }
-}
 
 // ---------------------------------------------------------------------------------------------
 // Synthetic forward-index generator (benchmarks): dictId(row) = splitmix64(seed ^ row*golden) % card, packed
@@ -2264,23 +2147,18 @@ extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in
 
 extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
                                                 int nparts, int64_t cap, uint64_t keymask, int keybits, int64_t vbase,
-                                                const int64_t* vdict, int need_sum, int need_min, int need_max, int pack_shift,
+                                                int need_sum, int need_min, int need_max, int pack_shift,
                                                 uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream) {
   (void)need_sum;  // sums are always accumulated (one add)
   if (nparts <= 0) return hipSuccess;
   const int sel = (pack_shift ? 4 : 0) | (need_min ? 2 : 0) | (need_max ? 1 : 0);
-#define PGX_AGG_CASE(K, A, B, C)                                                                                   \
-  case K:                                                                                                           \
-    if (vdict)                                                                                                      \
-      hipLaunchKernelGGL((pgx::pgx_part_aggregate<A, B, C, true>), dim3(nparts), dim3(pgx::kAggThreads), 0, stream, \
-                         in, in_cnt, cstride, cap, keymask, keybits, vbase, vdict, pack_shift, okey, oplane, ocap,  \
-                         ocount, overflow);                                                                         \
-    else                                                                                                            \
-      hipLaunchKernelGGL((pgx::pgx_part_aggregate<A, B, C, false>), dim3(nparts), dim3(pgx::kAggThreads), 0,       \
-                         stream, in, in_cnt, cstride, cap, keymask, keybits, vbase, vdict, pack_shift, okey, oplane,\
-                         ocap, ocount, overflow);                                                                   \
+#define PGX_AGG_CASE(K, A, B, C)                                                                                    \
+  case K:                                                                                                            \
+    hipLaunchKernelGGL((pgx::pgx_part_aggregate<A, B, C>), dim3(nparts), dim3(pgx::kAggThreads), 0, stream, in,     \
+                       in_cnt, cstride, cap, keymask, keybits, vbase, pack_shift, okey, oplane, ocap, ocount,       \
+                       overflow);                                                                                   \
     break;
   switch (sel) {
     PGX_AGG_CASE(0, false, false, false)
@@ -2293,37 +2171,6 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
     PGX_AGG_CASE(7, true, true, true)
   }
 #undef PGX_AGG_CASE
-  return hipGetLastError();
-}
-
-extern "C" hipError_t pgx_launch_part_aggregate_img(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
-                                                    int nparts, int64_t cap, uint64_t keymask, int keybits,
-                                                    int64_t vbase, const uint32_t* img, int img_words, int img_sh,
-                                                    const int64_t* vdict, int need_min, int need_max, int pack_shift,
-                                                    uint64_t* okey, uint64_t* oplane, int64_t ocap,
-                                                    unsigned long long* ocount, unsigned long long* overflow, int grid,
-                                                    hipStream_t stream) {
-  if (nparts <= 0) return hipSuccess;
-  if (img_words > pgx::kAggImgWords || img_words < 64 || grid < 1 || !img || !vdict) return hipErrorInvalidValue;
-  grid = grid < nparts ? grid : nparts;
-  const int sel = (pack_shift ? 4 : 0) | (need_min ? 2 : 0) | (need_max ? 1 : 0);
-#define PGX_AGGI_CASE(K, A, B, C)                                                                                  \
-  case K:                                                                                                          \
-    hipLaunchKernelGGL((pgx::pgx_part_aggregate_img<A, B, C>), dim3(grid), dim3(pgx::kAggThreads), 0, stream, in, \
-                       in_cnt, cstride, nparts, cap, keymask, keybits, vbase, img, img_words, img_sh, vdict,       \
-                       pack_shift, okey, oplane, ocap, ocount, overflow);                                          \
-    break;
-  switch (sel) {
-    PGX_AGGI_CASE(0, false, false, false)
-    PGX_AGGI_CASE(1, false, false, true)
-    PGX_AGGI_CASE(2, false, true, false)
-    PGX_AGGI_CASE(3, false, true, true)
-    PGX_AGGI_CASE(4, true, false, false)
-    PGX_AGGI_CASE(5, true, false, true)
-    PGX_AGGI_CASE(6, true, true, false)
-    PGX_AGGI_CASE(7, true, true, true)
-  }
-#undef PGX_AGGI_CASE
   return hipGetLastError();
 }
 
@@ -2348,7 +2195,6 @@ extern "C" hipError_t pgx_launch_roaring_program_wave(const pgx::RProg* progs, c
   if (nprogs <= 0 || maxchunks <= 0) return hipSuccess;
   // ~8192 waves (four rounds of 256 CUs x 8 resident), at most one per chunk
   int parts = std::max(1, std::min(maxchunks, (8192 + nprogs - 1) / nprogs));
-  if (const char* e = std::getenv("PGX_RPROG_PARTS")) parts = std::max(1, std::atoi(e));
   const long long waves = static_cast<long long>(nprogs) * parts;
   // waves per SIMD the LDS allows (NS x 8 KiB per wave) bound the registers: 1 slot -> 4, 2 -> 2, 3 -> 1
 #define PGX_WAVE_LAUNCH(NS, WPB, MINW)                                                                             \
@@ -2369,8 +2215,7 @@ extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const 
   if (maxleaves < 0 && -maxleaves <= pgx::kRProgMaxLeaves) {  // per-segment walk (host: every program <= 512 bitmaps)
     // at least ~2048 workgroups (two full rounds at 4 resident per CU on 256 CUs), at most 8 parts per segment
     int parts = std::max(1, std::min(std::min(maxchunks, 8), (2048 + nprogs - 1) / nprogs));
-    if (const char* e = std::getenv("PGX_RPROG_PARTS")) parts = std::max(1, std::atoi(e));
-    hipLaunchKernelGGL(pgx::pgx_roaring_program_seg, dim3(static_cast<unsigned>(nprogs * parts)),
+      hipLaunchKernelGGL(pgx::pgx_roaring_program_seg, dim3(static_cast<unsigned>(nprogs * parts)),
                        dim3(pgx::kSegRThreads), static_cast<size_t>(-maxleaves) * 2048 * 4, stream, progs, descs,
                        nprogs, parts);
     return hipGetLastError();

@@ -83,14 +83,13 @@ def test_batched_equals_oracle_and_unbatched(ctx, segs, text, monkeypatch):
 @pytest.mark.parametrize("rchunk", ["0", "1"])
 @pytest.mark.parametrize("text", QUERIES)
 def test_compacted_selected_rows_equal_oracle(ctx, segs, text, rchunk, monkeypatch):
-    """PGX_COMPACT=1: each sub-step's selected rows are packed into consecutive lanes (wave prefix + LDS staging)
-    before the value gathers / image lookups, group-key remaps and table atomics; with bitmap programs evaluated in the
-    kernel (PGX_RCHUNK=1) or by the separate pass.  The segments' dictionaries differ, so remapped group keys are
+    """Bitmap programs evaluated in the query kernel (PGX_RCHUNK=1, which also packs each sub-step's selected rows into
+    consecutive lanes -- wave prefix + LDS staging -- before the value gathers / image lookups, group-key remaps and
+    table atomics) or by the separate pass (PGX_RCHUNK=0).  The segments' dictionaries differ, so remapped group keys are
     gathered in the packed domain too."""
     gsegs, osegs = segs
     q = pql.compile(text)
     fns = [a["fn"] for a in q["aggregations"]]
-    monkeypatch.setenv("PGX_COMPACT", "1")
     monkeypatch.setenv("PGX_RCHUNK", rchunk)
     got, st = _answer(ctx, gsegs, q)
     o = H.oracle_answer(osegs, q, literal=True)

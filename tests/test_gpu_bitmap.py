@@ -116,16 +116,12 @@ def test_bitmap_program_in_kernel_vs_separate_pass(ctx, segs, text, mode, monkey
     """All-bitmap filter sub-trees evaluated per 65536-doc chunk inside the query kernel (LEAF_RCHUNK, PGX_RCHUNK=1)
     or by the separate expansion pass (PGX_RCHUNK=0): the wave-per-chunk kernel ("0wave", the default for programs of
     at most 64 bitmaps and 3 mask slots), one workgroup per segment walking every bitmap's containers in key order
-    ("0", PGX_RPROG_WAVE=0), one workgroup per (segment, chunk) with a container search ("0chunk", PGX_RPROG_SEG=0),
-    or the stack kernel ("0narrow", PGX_RPROG_NARROW=1).  All equal the oracle, statistics included, alone and in a
+    ("0", PGX_RPROG=seg), one workgroup per (segment, chunk) with a container search ("0chunk", PGX_RPROG=chunk),
+    or the stack kernel ("0narrow", PGX_RPROG=stack).  All equal the oracle, statistics included, alone and in a
     multi-segment launch whose workgroups start mid-chunk."""
     from pinot_amd import engine as E
     monkeypatch.setenv("PGX_RCHUNK", mode[0])
-    monkeypatch.setenv("PGX_RPROG_WAVE", "1" if mode == "0wave" else "0")
-    monkeypatch.setenv("PGX_RPROG_SEG", "0" if mode == "0chunk" else "1")
-    if mode == "0narrow":
-        monkeypatch.setenv("PGX_RPROG_NARROW", "1")
-        monkeypatch.setenv("PGX_RPROG_SEG", "0")
+    monkeypatch.setenv("PGX_RPROG", {"0wave": "wave", "0": "seg", "0chunk": "chunk", "0narrow": "stack", "1": "wave"}[mode])
     inv, scan, oseg = segs
     q = pql.compile(text)
     pm = E.InstancePlanMakerImplV2(ctx)

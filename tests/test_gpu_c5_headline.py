@@ -163,7 +163,7 @@ def test_plan_cache_replays_vs_oracle(ctx, monkeypatch, capfd):
     throughput flag does not change the key; a different segment list (a subset) plans afresh.  Oracle as above."""
     from pinot_amd import engine as E
     from pinot_amd import native as N
-    monkeypatch.setenv("PGX_HOST_PROFILE", "1")
+    monkeypatch.setenv("PGX_DEBUG", "host_profile")
     nseg, rows = 48, 65536 + 999
     seg_ids = list(range(nseg))
     data = synth.DeviceSegments(ctx, WL, seg_ids, rows=rows)
@@ -198,7 +198,7 @@ def test_plan_cache_batched_list_promotes(ctx, monkeypatch, capfd):
     for batched, "cached" for a replay).  Every result equals the oracle's."""
     from pinot_amd import engine as E
     from pinot_amd import native as N
-    monkeypatch.setenv("PGX_HOST_PROFILE", "1")
+    monkeypatch.setenv("PGX_DEBUG", "host_profile")
     nseg, rows = 1100, 4096 + 17
     seg_ids = list(range(nseg))
     data = synth.DeviceSegments(ctx, WL, seg_ids, rows=rows)

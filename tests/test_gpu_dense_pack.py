@@ -1,13 +1,11 @@
 """GPU parity of the packed dense group-by update (count and value offset in ONE 64-bit LDS add, flushed per segment
-as count and offset sum + count x that segment's vbase; pgx_jit.cpp `pack`, default on, PGX_DENSE_PACK=0 restores two
-adds).  Semantics: DefaultGroupByExecutor.aggregateColumn -> SumAggregationFunction.aggregateGroupBySV /
+as count and offset sum + count x that segment's vbase; pgx_jit.cpp `pack`, whenever the fields fit).  Semantics: DefaultGroupByExecutor.aggregateColumn -> SumAggregationFunction.aggregateGroupBySV /
 AvgAggregationFunction.aggregateGroupBySV.
 
 Cases the default C5 plan does not reach:
 * negative values (vbase < 0: the flush adds count x vbase in wrapping u64 arithmetic),
 * the field boundary: the host packs only when bits(rows + 1) + bits(rows x (range + 1)) <= 64, so with a 2^32 - 1 value
-  range a 60,000-row segment packs and a 70,000-row one falls back to two adds,
-* pack combined with the per-lane slots (PGX_SEL_K) and with wave compaction (PGX_COMPACT).
+  range a 60,000-row segment packs and a 70,000-row one falls back to two adds.
 Every answer is compared with the CPU oracle, bit-exactly (all sums are integers below 2^53)."""
 import glob
 import os
@@ -64,16 +62,11 @@ def _pack_bits(rows, vrange):
     return cb + sb
 
 
-@pytest.mark.parametrize("variant", ["pack", "nopack", "selk2", "compact"])
+@pytest.mark.parametrize("variant", ["pack"])
 @pytest.mark.parametrize("rows", [60000, 70000])
 @pytest.mark.parametrize("text", QUERIES)
 def test_dense_pack_matches_oracle(ctx, segs, text, rows, variant, monkeypatch, tmp_path):
     from pinot_amd import engine as E
-    monkeypatch.setenv("PGX_DENSE_PACK", "0" if variant == "nopack" else "1")
-    if variant == "selk2":
-        monkeypatch.setenv("PGX_SEL_K", "2")
-    if variant == "compact":
-        monkeypatch.setenv("PGX_COMPACT", "1")
     one = tmp_path / "one"
     one.mkdir()
     monkeypatch.setenv("PGX_JIT_DUMP", str(one))

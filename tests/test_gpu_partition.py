@@ -1,7 +1,7 @@
 """GPU parity of the partitioned sparse group-by (pgx_host.cpp run_partitioned: record-emitting query kernel, two
 radix passes, per-partition LDS aggregation) for LONG_MAP-sized key spaces: against the oracle, against the global
 hash-table path (PGX_X_NO_PARTITION), across segments with different group dictionaries, and through its resize /
-re-split / fallback branches (PGX_PART_DEBUG=1 starts from undersized buckets and a single pass)."""
+re-split / fallback branches (PGX_DEBUG=part_small starts from undersized buckets and a single pass)."""
 import numpy as np
 import pytest
 
@@ -148,15 +148,12 @@ def _expected(raw):
     return out
 
 
-@pytest.mark.parametrize("slab", ["1", "0"])
 @pytest.mark.parametrize("n,card", [(400000, 1000), (1200000, 2000)])
-def test_partitioned_debug_resize_and_fallback(ctx, monkeypatch, n, card, slab):
-    """PGX_PART_DEBUG=1: pass-1 buckets (slab mode: the scan's one-record slabs) start undersized (resize from the
-    measured counts), one pass of 128 partitions (~n distinct groups overflow the LDS tables: re-split), and at most
-    one re-split: the 1.2M-row case still overflows and falls back to the global hash table.  Both must be exact, with
-    the scan writing per-workgroup slabs (PGX_PART_SLAB=1) or row-order records (0, default)."""
-    monkeypatch.setenv("PGX_PART_DEBUG", "1")
-    monkeypatch.setenv("PGX_PART_SLAB", slab)
+def test_partitioned_debug_resize_and_fallback(ctx, monkeypatch, n, card):
+    """PGX_DEBUG=part_small: pass-1 buckets start undersized (resize from the measured counts), one pass of 128
+    partitions (~n distinct groups overflow the LDS tables: re-split), and at most one re-split: the 1.2M-row case
+    still overflows and falls back to the global hash table.  Both must be exact."""
+    monkeypatch.setenv("PGX_DEBUG", "part_small")
     monkeypatch.setenv("PGX_PART_NARROW", "0")  # the radix path's own resize / re-split branches
     gseg, raw = _pairs_segment(ctx, n, card, seed=card)
     q = pql.compile("SELECT COUNT(*), SUM(m), MIN(m), MAX(m) FROM t GROUP BY ga, gb")
@@ -252,18 +249,12 @@ def test_group_partials_split_then_merged_equal_one_launch(ctx):
         H.assert_values_equal(merged[k], v, fns)
 
 
-@pytest.mark.parametrize("mode", ["fused", "slab", "rows"])
 @pytest.mark.parametrize("text", [AGGS + " GROUP BY g2, a, c", "SELECT COUNT(*) FROM t WHERE a > 0 GROUP BY a, c",
                                   "SELECT MIN(m), MAX(m) FROM t WHERE b <> %(b1)s GROUP BY c, g2, s, g1"])
-def test_fused_first_pass_equals_oracle(ctx, seg, text, mode, monkeypatch):
-    """The first radix pass three ways.  fused (PGX_PART_FUSED=1): the scan kernel splits its records 128 ways itself
-    (LDS histogram, per-bucket cursor reservation, bucket-sorted staging) and the records carry the value's dictId
-    (sorted dictionary: MIN / MAX of ids, SUM by lookup while aggregating).  slab (PGX_PART_SLAB=1): the scan appends
-    value-offset records to its workgroup's slab of each bucket and the second pass reads the slabs.  rows (default):
-    row-order records and a separate first pass.  COUNT-only keys always take the fused pass.  All
-    against the oracle."""
-    monkeypatch.setenv("PGX_PART_FUSED", "1" if mode == "fused" else "0")
-    monkeypatch.setenv("PGX_PART_SLAB", "0" if mode == "rows" else "1")
+def test_radix_row_records_equal_oracle(ctx, seg, text, monkeypatch):
+    """The 8-byte radix path (PGX_PART_NARROW=0): row-order value records, two radix passes, LDS aggregation; COUNT-only
+    keys and MIN / MAX-only functions included.  Against the oracle."""
+    monkeypatch.setenv("PGX_PART_NARROW", "0")
     gseg, oseg, fmt = seg
     q = pql.compile(text % fmt)
     blk, st = _run_inner(ctx, gseg, q)
@@ -279,7 +270,7 @@ def test_fused_first_pass_equals_oracle(ctx, seg, text, mode, monkeypatch):
 @pytest.mark.parametrize("case", ["uniform", "coarse", "skew", "count_only", "min_only"])
 def test_narrow_paths_and_fallback(ctx, monkeypatch, capfd, case):
     """Narrow records end to end against numpy (every group's count / sum / min / max, exact), including the cases that
-    must change course: "coarse" (PGX_NARROW_K2=0: 256 partitions of ~1,500 groups overflow the 192-slot wavefront
+    must change course: "coarse" (PGX_DEBUG=narrow_k2=0: 256 partitions of ~1,500 groups overflow the 192-slot wavefront
     tables: the 8-byte radix path takes over) and "skew" (half the rows on one key: its slab and partition outgrow the
     capacities sized for a uniform mix, which are resized from the measured fills and the affected passes rerun).  COUNT-only records carry no value (26-bit records, one u32 array)."""
     from pinot_amd import engine as E
@@ -294,9 +285,8 @@ def test_narrow_paths_and_fallback(ctx, monkeypatch, capfd, case):
     if case == "skew":
         raw["ga"][card:n // 2 + card] = 7
         raw["gb"][card:n // 2 + card] = 21
-    if case == "coarse":
-        monkeypatch.setenv("PGX_NARROW_K2", "0")
-    monkeypatch.setenv("PGX_NARROW_DEBUG", "1")  # one "[pgx narrow] ... ovf=a/b/c" line per narrow attempt
+    # narrow_log: one "[pgx narrow] ... ovf=a/b/c" line per narrow attempt
+    monkeypatch.setenv("PGX_DEBUG", "narrow_log,narrow_k2=0" if case == "coarse" else "narrow_log")
     s, _ = H.build_pair("nw_" + case, raw)
     gseg = E.IndexSegment(ctx, s)
     try:
