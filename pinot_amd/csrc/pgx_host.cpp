@@ -1337,6 +1337,20 @@ struct ExecPlan {
   uint64_t mask_words = 0;
   const RDesc* rdesc_dev = nullptr;
   bool roar_early = false;  // the expansion was launched by upload_plan (before the query kernels are planned)
+  // a lone query's replay (plan cache, no PGX_X_THROUGHPUT): bitmap programs and query kernel in two halves, the second
+  // half's programs on the side stream beside the first half's query kernel (launch_scan)
+  bool split2 = false;
+  hipStream_t ctx_side = nullptr;
+  struct Ev {
+    hipEvent_t e = nullptr;
+    hipEvent_t get() {
+      if (!e) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
+      return e;
+    }
+    ~Ev() {
+      if (e) (void)hipEventDestroy(e);
+    }
+  } ev_pre, ev_half;
   int roar_maxchunks = 0;
   uint32_t* masks_dev = nullptr;
   int n_proj = 0;
@@ -2691,10 +2705,13 @@ bool rprog_wave_ok(const RProg& r, int* slots) {
   return true;
 }
 
-void launch_bitmaps(ExecPlan& P, hipStream_t st) {
+// Bitmap programs [p0, p1) (default: all of them).
+void launch_bitmaps(ExecPlan& P, hipStream_t st, int p0 = 0, int p1 = -1) {
   if (P.rchunk) return;  // the query kernels evaluate the bitmap programs per chunk themselves
   if (P.rprog_on) {
-    const int np = int(P.rprogs.size());
+    if (p1 < 0) p1 = int(P.rprogs.size());
+    const int np = p1 - p0;
+    const RProg* progs = P.rprog_dev + p0;
     // wave-per-chunk kernel when every program has <= 64 bitmaps (one lane each) and <= 3 mask slots
     const int rk = P.kn.rprog;  // PGX_RPROG: wave | seg | chunk | stack (default: the first that fits)
     bool wave = rk == RPROG_AUTO || rk == RPROG_WAVE;
@@ -2710,7 +2727,7 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
       nslots = std::max(nslots, ns);
     }
     if (wave) {
-      PGX_LAUNCH(st, "pgx_roaring_program_wave", pgx_launch_roaring_program_wave(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, nslots, st),
+      PGX_LAUNCH(st, "pgx_roaring_program_wave", pgx_launch_roaring_program_wave(progs, P.rdesc_dev, np, P.roar_maxchunks, nslots, st),
                 "bitmap program launch");
       return;
     }
@@ -2731,7 +2748,7 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st) {
       if (nb > 512) seg_walk = false;
     }
     if (seg_walk) maxleaves = -maxleaves;
-    PGX_LAUNCH(st, "pgx_roaring_program", pgx_launch_roaring_program(P.rprog_dev, P.rdesc_dev, np, P.roar_maxchunks, maxleaves, st),
+    PGX_LAUNCH(st, "pgx_roaring_program", pgx_launch_roaring_program(progs, P.rdesc_dev, np, P.roar_maxchunks, maxleaves, st),
               "bitmap program launch");
   } else if (P.rdesc_dev) {
     PGX_LAUNCH(st, "pgx_roaring", pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
@@ -3312,6 +3329,48 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
               "multi-value leaf masks");
   }
   if (!P.jit.empty()) {
+    // a lone query's replay: bitmap programs and query kernel in two halves of the segment list, the second half's
+    // programs on the side stream, so they run beside the first half's query kernel instead of before it
+    const bool two = P.split2 && P.rdesc_dev && P.rprog_on && !P.roar_early && !P.rchunk && P.jit.size() == 1 &&
+                     P.jit[0].fn && !P.fsm_on && P.mv_items.empty() && P.jit[0].segs.size() >= 64 &&
+                     P.jit[0].segs.size() == P.ksegs.size() && !P.dm_progs.empty() &&
+                     P.rprogs.size() == P.ksegs.size() * P.dm_progs.size() && P.ctx_side && !P.use_part;
+    if (two) {
+      ExecPlan::JitGroup& G = P.jit[0];
+      const int n = int(G.segs.size()), h = n / 2;
+      const int ph = h * int(P.dm_progs.size());
+      hip_check(hipEventRecord(P.ev_pre.get(), st), "event");
+      hip_check(hipStreamWaitEvent(P.ctx_side, P.ev_pre.get(), 0), "event wait");
+      launch_bitmaps(P, st, 0, ph);
+      launch_bitmaps(P, P.ctx_side, ph, int(P.rprogs.size()));
+      hip_check(hipEventRecord(P.ev_half.get(), P.ctx_side), "event");
+      const long long tiles = G.args.total_tiles, th = G.segs[h].tile_begin;
+      for (int half = 0; half < 2; ++half) {
+        if (half) hip_check(hipStreamWaitEvent(st, P.ev_half.get(), 0), "event wait");
+        JArgs a = G.args;
+        a.agg_out = P.kq.agg_out;
+        a.stats = P.kq.stats;
+        a.table = P.kq.table;
+        a.hkeys = P.kq.keys;
+        a.hstate = P.kq.key_state;
+        a.hash_cap = P.kq.hash_cap;
+        a.overflow = P.kq.overflow;
+        a.segs = G.args.segs + (half ? h : 0);
+        a.num_segs = half ? n - h : h;
+        a.tile_base = half ? th : 0;
+        a.total_tiles = half ? tiles : th;
+        // the whole persistent grid for each half (the plan's tiles per workgroup were sized for all the tiles)
+        const long long span = half ? tiles - th : th;
+        const long long tph = std::max<long long>(1, (span + G.grid - 1) / G.grid);
+        a.tiles_per_wg = tph;
+        const int grid = int(std::max<long long>(1, (span + tph - 1) / tph));
+        void* params[] = {&a};
+        PGX_LAUNCH(st, "pgxq", hipModuleLaunchKernel(static_cast<hipFunction_t>(G.fn), grid, 1, 1, G.T, 1, 1, 0, st,
+                                                     params, nullptr),
+                   "query kernel launch");
+      }
+      return;
+    }
     if (P.rdesc_dev && !P.roar_early) launch_bitmaps(P, st);
     P.roar_early = false;  // relaunches (hash-table retries, timed iterations) expand again
     for (auto& G : P.jit) {
@@ -4782,7 +4841,10 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
       // bitmap programs run again from launch_scan
       alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
       reset_outputs(P, B, st, true, true);
+      P.split2 = !(xflags & PGX_X_THROUGHPUT);
+      P.ctx_side = ctx->side;
       launch_scan(P, st);
+      P.split2 = false;
       hp.mark("launch");
       complete_scan(ctx, q, P, B, segs, n, opts, st, R);
       hp.mark("finish");

@@ -214,7 +214,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   e.ln("__shared__ u64 s_acc[", s.num_planes, "];");
   e.ln("const int tid = threadIdx.x;");
   e.ln("const int lane = tid & 63;");
-  e.ln("const long long tb = (long long)blockIdx.x * A.tiles_per_wg;");
+  e.ln("const long long tb = A.tile_base + (long long)blockIdx.x * A.tiles_per_wg;");
   e.ln("const long long te = (tb + A.tiles_per_wg < A.total_tiles) ? tb + A.tiles_per_wg : A.total_tiles;");
   e.ln("if (tb >= te) return;");
   // accumulator init
@@ -432,6 +432,47 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       }
     }
   }
+  // Mask-gated loads: when every filter leaf is a doc-mask leaf (a bitmap program's mask, an MV leaf's mask: no scan
+  // leaf reads a column) and the program selects only rows whose mask bit `gate` is set, a row with a clear bit is
+  // never selected and its forward-index words matter to nothing (not the filter, not the statistics, not any group or
+  // value).  The gate leaf's mask words then load one tile earlier than the columns, and a lane whose rows are all
+  // clear does not load their words: the row-selective read of the reference's projection
+  // (DataFetcher.fetchSingleDictIds over the filtered docIds), at the granularity of a lane's dwords.
+  int gate = -1;
+  {
+    bool all_masks = !s.prog_op.empty();
+    for (size_t pc = 0; pc < s.prog_op.size() && all_masks; ++pc)
+      if (s.prog_op[pc] == OP_LEAF && !is_docmask(s.leaf_mode[s.prog_arg[pc]])) all_masks = false;
+    std::vector<std::vector<int>> impl;  // per stack entry: the doc-mask leaves every selected row has set
+    for (size_t pc = 0; pc < s.prog_op.size() && all_masks; ++pc) {
+      const int op = s.prog_op[pc], arg = s.prog_arg[pc];
+      if (op == OP_LEAF) {
+        impl.push_back(s.leaf_mode[arg] == LEAF_DOCMASK ? std::vector<int>{arg} : std::vector<int>{});
+      } else if (op == OP_AND || op == OP_OR) {
+        std::vector<int> acc = impl.back();
+        impl.pop_back();
+        for (int k = 1; k < arg; ++k) {
+          std::vector<int> x = impl.back(), y;
+          impl.pop_back();
+          if (op == OP_AND) {
+            y = acc;
+            y.insert(y.end(), x.begin(), x.end());
+          } else {
+            for (int l : acc)
+              if (std::find(x.begin(), x.end(), l) != x.end()) y.push_back(l);
+          }
+          acc = y;
+        }
+        impl.push_back(acc);
+      } else if (op == OP_TRUE) {
+        impl.push_back({});
+      }
+    }
+    if (all_masks && impl.size() == 1 && !impl[0].empty() && !compact) gate = impl[0][0];
+  }
+  auto gate_bits = [&](const std::string& w) {  // the lane's PR bits of gate word w (r0 in scope)
+    return s.R == 32 ? w : "((" + w + " >> (r0 & 31)) & " + std::to_string((1u << s.R) - 1u) + "u)";
+  };
   // software-pipelined tile loop: raw words of tile tt+1 are loaded while tile tt is computed
   auto emit_loads = [&](const std::string& tile, const std::string& dst) {
     e.ln("{");
@@ -443,22 +484,37 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("{");
       e.ind++;
       e.ln("const int r0 = rb + ", u * s.R, " * PT + tid * PR;");
+      const std::string cond =
+          gate >= 0 ? "(full || r0 < nd) && " + gate_bits("ga[" + std::to_string(u) + "]") + " != 0u" : "full || r0 < nd";
       for (int c = 0; c < ncols; ++c) {
         if (!s.cols[c].decode) continue;
         const int D = dwords_per(s, c);
         if (s.cols[c].frac)
-          e.ln("if (full || r0 < nd) pgx_ld_u<", D, ">(f", c, " + (((long long)r0 * ", s.cols[c].bits, ") >> 5), &", dst,
+          e.ln("if (", cond, ") pgx_ld_u<", D, ">(f", c, " + (((long long)r0 * ", s.cols[c].bits, ") >> 5), &", dst,
                c, "[", u * D, "]); else pgx_zero<", D, ">(&", dst, c, "[", u * D, "]);");
         else
-        e.ln("if (full || r0 < nd) pgx_ld<", D, ">(f", c, " + (long long)(r0 / PR) * ", D, ", &", dst, c, "[", u * D,
+        e.ln("if (", cond, ") pgx_ld<", D, ">(f", c, " + (long long)(r0 / PR) * ", D, ", &", dst, c, "[", u * D,
              "]); else pgx_zero<", D, ">(&", dst, c, "[", u * D, "]);");
       }
       for (int l = 0; l < nleaves; ++l)
-        if (is_docmask(s.leaf_mode[l]))
+        if (l == gate) e.ln(dst, "q", l, "[", u, "] = ga[", u, "];");
+        else if (is_docmask(s.leaf_mode[l]))
           e.ln(dst, "q", l, "[", u, "] = (full || r0 < nd) ? dm", l, "[r0 >> 5] : 0u;");
       e.ind--;
       e.ln("}");
     }
+    e.ind--;
+    e.ln("}");
+  };
+  // gate words of one tile (gate >= 0): into ga for the tile whose columns load next, gn for the one after
+  auto emit_gate_loads = [&](const std::string& tile, const std::string& dst) {
+    e.ln("{");
+    e.ind++;
+    e.ln("const int rb = (int)((tl ? (long long)tl[", tile, " - tile0] : (", tile, " - tile0)) * (PT * PTL));");
+    e.ln("const bool full = rb + PT * PTL <= nd;");
+    for (int u = 0; u < U; ++u)
+      e.ln("{ const int r0 = rb + ", u * s.R, " * PT + tid * PR; ", dst, "[", u, "] = (full || r0 < nd) ? dm", gate,
+           "[r0 >> 5] : 0u; }");
     e.ind--;
     e.ln("}");
   };
@@ -469,7 +525,15 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   // first row of the tile whose raw words are in flight: carried into the next iteration, so the loop body never
   // reloads the tile list after issuing the prefetch (that load's wait would also wait for the prefetch)
   e.ln("int rbn;");
+  if (gate >= 0) {
+    e.ln("u32 ga[", U, "], gn[", U, "];");
+    emit_gate_loads("t", "ga");
+  }
   emit_loads("t", "n");
+  if (gate >= 0) {
+    e.ln("if (t + 1 < t2)");
+    emit_gate_loads("t + 1", "gn");
+  }
   emit_images();
   e.ln("for (long long tt = t; tt < t2; ++tt) {");
   e.ind = 3;
@@ -487,8 +551,20 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("for (int i = 0; i < ", U, "; ++i) cq", l, "[i] = nq", l, "[i];");
     }
   e.ln("const int rb = rbn;");
-  e.ln("if (tt + 1 < t2) ");
-  emit_loads("tt + 1", "n");
+  if (gate >= 0) {  // the next tile's gate words arrived during the previous tile; the one after that's load now
+    e.ln("if (tt + 1 < t2) {");
+    e.ind++;
+    e.ln("#pragma unroll");
+    e.ln("for (int i = 0; i < ", U, "; ++i) ga[i] = gn[i];");
+    emit_loads("tt + 1", "n");
+    e.ln("if (tt + 2 < t2)");
+    emit_gate_loads("tt + 2", "gn");
+    e.ind--;
+    e.ln("}");
+  } else {
+    e.ln("if (tt + 1 < t2) ");
+    emit_loads("tt + 1", "n");
+  }
   if (scr_off >= 0) {
     // a tile (PT * PTL rows) lies inside one 65536-doc chunk: build that chunk's program masks when it changes (the next
     // tile's forward-index loads are already in flight)

@@ -78,6 +78,7 @@ struct JArgs {
   unsigned int* hstate;              // its 128-bit key states,
   long long hash_cap;                // its slots (a power of two; planes at table + p * hash_cap)
   unsigned long long* overflow;      // keys that found no global slot (the host grows the table and reruns)
+  long long tile_base;               // first tile of this launch (a plan launched in two halves: the second half's)
 };
 
 #endif  // PGX_JIT_ABI_H_

@@ -160,11 +160,13 @@ def test_c5_full_size_shard_linearity(ctx):
 def test_plan_cache_replays_vs_oracle(ctx, monkeypatch, capfd):
     """The plan cache (pgx_host.cpp run_query): a second execution of the same query over the same segments replays the
     first one's plan (the host-profile line carries the "cached" mark) with the same result, statistics included; the
-    throughput flag does not change the key; a different segment list (a subset) plans afresh.  Oracle as above."""
+    throughput flag does not change the key; a different segment list (a subset) plans afresh.  The replay without the
+    throughput flag launches the bitmap programs and the query kernel in two halves (the second half's programs on the
+    side stream beside the first half's query kernel).  Oracle as above."""
     from pinot_amd import engine as E
     from pinot_amd import native as N
     monkeypatch.setenv("PGX_DEBUG", "host_profile")
-    nseg, rows = 48, 65536 + 999
+    nseg, rows = 96, 65536 + 999  # >= 64 segments: a replay without the throughput flag runs in two halves
     seg_ids = list(range(nseg))
     data = synth.DeviceSegments(ctx, WL, seg_ids, rows=rows)
     try:
