@@ -42,6 +42,8 @@ extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t
 extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
                                          unsigned long long* counter, int64_t* out_slot,
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
+extern "C" hipError_t pgx_launch_gather_keys(const unsigned long long* keys, const int64_t* slot, int64_t n, int kw,
+                                             unsigned long long* out, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring_program_wave(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
                                                       int maxchunks, int nslots, hipStream_t stream);
@@ -992,7 +994,8 @@ struct pgx_result {
     DevBuf prange;               // trim-key ranges per kind (pgx_narrow_aggregate), or none: the trim's range pass
     int64_t ocap = 0;
     std::vector<int> gshift, gbits;
-    std::vector<std::vector<int32_t>> rep_seg, rep_id;  // [col][global id]
+    using Reps = std::shared_ptr<const std::vector<std::vector<int32_t>>>;
+    Reps rep_seg, rep_id;  // [col][global id] (shared with a kept plan: every replay's result reads the same tables)
     std::vector<int> agg_kind;
     std::vector<std::vector<int64_t>> trims;  // per function: the device-selected trim, best first
     int64_t trim_size = 0;                    // the size those selections were made for
@@ -1380,6 +1383,7 @@ struct ExecPlan {
   // narrow records (run_narrow, the default for partitioned plans that qualify): the scan writes dictId records split
   // 256 ways into per-workgroup slabs (part_slab with kNarrow1Bits), u32 in kq.table and bits 32..47 in part_hi
   bool part_narrow = false;
+  std::shared_ptr<const std::vector<std::vector<int32_t>>> lazy_rep_seg, lazy_rep_id;  // part_result's key tables
   int narrow_vd = 0;              // dictId bits of the value column (0: COUNT only)
   int narrow_k2min = 0;           // second-split bits the record width needs
   int narrow_img = 0;             // value image in the aggregation's LDS: 0 none, 1 U32, 2 FOR16
@@ -1451,6 +1455,7 @@ Knobs pgx::read_knobs() {
   const std::string bs = env("PGX_BATCH_SEGS"), dbg = env("PGX_DEBUG");
   k.jit = !(jit.size() && jit[0] == '0');
   k.narrow = !(nar.size() && nar[0] == '0');
+  k.narrow_direct = nar == "direct";
   if (rc.size()) k.rchunk = rc[0] == '1' ? 1 : 0;
   if (rp == "off") k.rprog = RPROG_OFF;
   else if (rp == "wave") k.rprog = RPROG_WAVE;
@@ -2072,6 +2077,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     for (int g = 0; g < K.num_gcols; ++g) keybits = std::max(keybits, K.gshift[g] + P.gbits[g]);
     int vbits = 0;
     int64_t vbase = 0;
+    uint64_t vrange = 0;
     bool same_dict = true;  // one dictionary in every segment: records may carry the dictId (narrow path)
     if (ok && vc >= 0) {
       // Value records carry value - vbase with ONE query-wide vbase (the smallest value of any segment's dictionary):
@@ -2093,6 +2099,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         const uint64_t range = uint64_t(vmax) - uint64_t(vmin);
         ok = range <= 0xFFFFFFFFull;
         vbase = vmin;
+        vrange = range;
         vbits = ok ? bits_for(int64_t(range) + 1) : 64;
       }
     }
@@ -2112,7 +2119,16 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       // and the aggregation looks values up in the column's image (FOR16 / U32) in LDS (run_narrow).  Needs a sorted
       // dictionary (MIN / MAX of dictIds) and, for SUM / AVG, an image that fits beside the aggregation tables.
       if (q.kn.narrow && keybits > kNarrow1Bits) {
-        int vd = 0, imgk = 0;
+        // Value field: the dictId looked up in an LDS image of the column (one sorted dictionary in every segment, an
+        // image that fits the LDS), or the value offset itself (value - vbase, rebased per segment like the radix
+        // records: per-segment dictionaries, no image, and no LDS spent on one -- PGX_PART_NARROW=direct prefers it)
+        const int rb1 = keybits - kNarrow1Bits;
+        auto fits = [&](int vd, int& k2) {
+          k2 = std::max(0, rb1 + vd - 32);
+          if (rb1 - k2 > 31) k2 = rb1 - 31;
+          return rb1 + vd <= 48 && k2 <= kNarrowMaxBits2;
+        };
+        int vd = 0, imgk = 0, k2 = 0;
         bool nok = true;
         if (vc >= 0) {
           const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
@@ -2121,21 +2137,32 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           if (c0.img_dev && c0.img_kind == IMG_FOR16 && c0.img_words <= kImgFor16Blocks + 32768) imgk = 2;
           else if (c0.img_dev && c0.img_kind == IMG_U32 && c0.img_words <= kImgFor16Blocks + 32768) imgk = 1;
           if (need_sum && !imgk) nok = false;
-          if (nok) {
+          nok = nok && fits(vd, k2);
+          int k2d = 0;
+          if ((!nok || q.kn.narrow_direct) && vbits <= 32 && fits(vbits, k2d)) {
+            nok = true;
+            imgk = 3;
+            vd = vbits;
+            k2 = k2d;
+            P.part_vdict = nullptr;
+            P.narrow_imgp = nullptr;
+            P.narrow_img_words = 0;
+            P.narrow_img_sh = 0;
+            P.narrow_vrange = vrange;
+          } else if (nok) {
             P.part_vdict = static_cast<const int64_t*>(c0.dict_dev);
             P.narrow_imgp = imgk ? static_cast<const uint32_t*>(c0.img_dev) : nullptr;
             P.narrow_img_words = imgk ? c0.img_words : 0;
             P.narrow_img_sh = c0.img_sh;
             P.narrow_vrange = c0.vrange;
           }
+        } else {
+          nok = fits(0, k2);
         }
-        const int rb1 = keybits - kNarrow1Bits;
-        int k2 = std::max(0, rb1 + vd - 32);
-        if (rb1 - k2 > 31) k2 = rb1 - 31;
-        if (nok && rb1 + vd <= 48 && k2 <= kNarrowMaxBits2) {
+        if (nok) {
           P.part_narrow = true;
           P.part_slab = true;
-          P.part_dictid = vc >= 0;
+          P.part_dictid = vc >= 0 && imgk != 3;
           P.narrow_vd = vd;
           P.narrow_k2min = k2;
           P.narrow_img = imgk;
@@ -3470,6 +3497,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     }
     return;
   }
+  std::vector<unsigned long long> keys_lo, keys_hi;
   if (dense_host_override) {
     for (uint64_t s = 0; s < slots; ++s)
       if (dense_host_override[s]) slot_ids.push_back(int64_t(s));
@@ -3493,26 +3521,29 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     hip_check(hipStreamSynchronize(st), "sync");
     ng = std::min<uint64_t>(cnt, cap);
     slot_ids.resize(ng);
-    std::vector<unsigned long long> pl(cap * K.num_planes);
-    if (ng) {
-      hip_check(hipMemcpy(slot_ids.data(), oslot.p, ng * 8, hipMemcpyDeviceToHost), "D2H");
-      hip_check(hipMemcpy(pl.data(), oplanes.p, cap * K.num_planes * 8, hipMemcpyDeviceToHost), "D2H");
-    }
     planes.resize(ng * K.num_planes);
-    for (int p = 0; p < K.num_planes; ++p)
-      for (uint64_t i = 0; i < ng; ++i) planes[p * ng + i] = pl[p * cap + i];
-  }
-  // keys
-  std::vector<unsigned long long> keys_lo, keys_hi;
-  if (hash && ng) {
-    const uint64_t kw = (K.group_mode == G_HASH128) ? 2 : 1;
-    std::vector<unsigned long long> all(slots * kw);
-    hip_check(hipMemcpy(all.data(), K.keys, slots * kw * 8, hipMemcpyDeviceToHost), "keys D2H");
-    keys_lo.resize(ng);
-    keys_hi.resize(ng, 0);
-    for (uint64_t i = 0; i < ng; ++i) {
-      keys_lo[i] = all[uint64_t(slot_ids[i]) * kw];
-      if (kw == 2) keys_hi[i] = all[uint64_t(slot_ids[i]) * 2 + 1];
+    std::vector<unsigned long long> gk;
+    if (ng) {  // only the ng live groups travel: their slots, planes and (gathered on the device) keys
+      const uint64_t kw = (K.group_mode == G_HASH128) ? 2 : 1;
+      DevBuf okeys(ctx, ng * kw * 8);
+      PGX_LAUNCH(st, "pgx_gather_keys",
+                 pgx_launch_gather_keys(K.keys, oslot.as<int64_t>(), int64_t(ng), int(kw),
+                                        reinterpret_cast<unsigned long long*>(okeys.p), st),
+                 "gather keys");
+      gk.resize(ng * kw);
+      hip_check(hipMemcpyAsync(slot_ids.data(), oslot.p, ng * 8, hipMemcpyDeviceToHost, st), "D2H");
+      for (int p = 0; p < K.num_planes; ++p)
+        hip_check(hipMemcpyAsync(planes.data() + p * ng, static_cast<char*>(oplanes.p) + p * cap * 8, ng * 8,
+                                 hipMemcpyDeviceToHost, st),
+                  "D2H");
+      hip_check(hipMemcpyAsync(gk.data(), okeys.p, ng * kw * 8, hipMemcpyDeviceToHost, st), "keys D2H");
+      hip_check(hipStreamSynchronize(st), "sync");
+      keys_lo.resize(ng);
+      keys_hi.resize(ng, 0);
+      for (uint64_t i = 0; i < ng; ++i) {
+        keys_lo[i] = gk[i * kw];
+        if (kw == 2) keys_hi[i] = gk[i * 2 + 1];
+      }
     }
   }
   // ARRAY_BASED iteration order is ascending raw key (DefaultGroupKeyGenerator.java:613-644): sort dense slots.
@@ -3830,7 +3861,9 @@ void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStrea
                                          NB.rb2, P.part_keybits, P.part_vbase, P.narrow_img, P.narrow_imgp,
                                          P.narrow_img_words, P.narrow_img_sh, P.part_vdict, P.part_sum, P.part_min,
                                          P.part_max, NB.cshift, NB.okey.as<uint64_t>(), NB.oplane.as<uint64_t>(),
-                                         NB.ocap, ctr, devp(NB.prange), ctx->num_cus, st),
+                                         NB.ocap, ctr, devp(NB.prange),
+                                         // an LDS image allows one workgroup per CU; the tables alone, four
+                                         ctx->num_cus * (P.narrow_img == 3 ? 4 : 1), st),
              "narrow aggregate");
 }
 
@@ -3838,7 +3871,12 @@ void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStrea
 // narrow layout; the caller re-plans the query kernels for the radix path.
 bool run_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hipStream_t st) {
   alloc_outputs(ctx, P, B, nullptr, 0);
-  if (!narrow_size(P, NB)) return false;
+  if (!narrow_size(P, NB)) {
+    if (P.kn.narrow_log)
+      std::fprintf(stderr, "[pgx narrow] layout does not fit: nwg=%lld keybits=%d vd=%d k2=%d cap1=%lld cap2=%lld\n",
+                   (long long)NB.nwg, P.part_keybits, P.narrow_vd, NB.k2, (long long)NB.cap1, (long long)NB.cap2);
+    return false;
+  }
   narrow_alloc(ctx, NB);
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
   unsigned long long* tail = outs + 28;  // spare words of the outputs block: ocount, overflows (part_result reads [28])
@@ -3892,6 +3930,25 @@ bool run_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hi
   return ok;
 }
 
+// A kept narrow plan again (plan cache): the slabs and partitions are the first run's, the group outputs (handed to
+// that run's result) are allocated anew.  False if a capacity ran over (the caller plans afresh).
+bool replay_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hipStream_t st) {
+  alloc_outputs(ctx, P, B, nullptr, 0);
+  NB.okey = DevBuf(ctx, size_t(NB.ocap) * 8);
+  NB.oplane = DevBuf(ctx, size_t(NB.ocap) * 4 * 8);
+  NB.prange = DevBuf(ctx, 8 * 8);
+  narrow_prepare(P, NB, st);
+  reset_outputs(P, B, st);
+  launch_scan(P, st);
+  narrow_enqueue(ctx, P, NB, st);
+  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+  unsigned long long* tail = outs + 28;
+  hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
+  hip_check(hipMemcpyAsync(tail, NB.ctr.p, 32, hipMemcpyDeviceToHost, st), "D2H");
+  hip_check(hipStreamSynchronize(st), "sync");
+  return !tail[1] && !tail[2] && !tail[3];
+}
+
 // The radix path's plan after a narrow attempt gave up: row-order 8-byte value records.
 void narrow_fallback(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
   P.part_narrow = false;
@@ -3913,8 +3970,8 @@ void pgx_result::decode_lazy(const uint64_t* keys, const uint64_t* planes, int64
     const uint64_t mask = (uint64_t(1) << L.gbits[g]) - 1u;
     for (int64_t i = 0; i < n; ++i) {
       const uint64_t gid = (keys[i] >> L.gshift[g]) & mask;
-      if (seg_index) seg_index[g * out_stride + i] = L.rep_seg[g][gid];
-      if (dict_id) dict_id[g * out_stride + i] = L.rep_id[g][gid];
+      if (seg_index) seg_index[g * out_stride + i] = (*L.rep_seg)[g][gid];
+      if (dict_id) dict_id[g * out_stride + i] = (*L.rep_id)[g][gid];
     }
   }
   for (int a = 0; a < int(L.agg_kind.size()); ++a) {
@@ -4032,12 +4089,22 @@ void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, 
   L->oplane = std::move(PB.oplane);
   L->prange = std::move(PB.prange);
   L->ocap = PB.ocap;
+  if (!P.lazy_rep_seg) {  // the key tables move to shared storage once (a kept plan's replays share them)
+    auto rs = std::make_shared<std::vector<std::vector<int32_t>>>();
+    auto ri = std::make_shared<std::vector<std::vector<int32_t>>>();
+    for (int g = 0; g < K.num_gcols; ++g) {
+      rs->push_back(std::move(P.gdicts[g].rep_seg));
+      ri->push_back(std::move(P.gdicts[g].rep_id));
+    }
+    P.lazy_rep_seg = std::move(rs);
+    P.lazy_rep_id = std::move(ri);
+  }
   for (int g = 0; g < K.num_gcols; ++g) {
     L->gshift.push_back(K.gshift[g]);
     L->gbits.push_back(P.gbits[g]);
-    L->rep_seg.push_back(std::move(P.gdicts[g].rep_seg));
-    L->rep_id.push_back(std::move(P.gdicts[g].rep_id));
   }
+  L->rep_seg = P.lazy_rep_seg;
+  L->rep_id = P.lazy_rep_id;
   for (int a = 0; a < K.num_aggs; ++a) L->agg_kind.push_back(K.agg_kind[a]);
   ctx->refs.fetch_add(1);
   L->ctx = ctx;
@@ -4661,9 +4728,11 @@ struct PlanEntry {
   uint64_t key = 0;
   std::unique_ptr<ExecPlan> P;
   std::unique_ptr<ExecBuffers> B;
+  std::unique_ptr<NarrowBuffers> NB;  // a narrow partitioned plan's slabs and partitions (sized by its first run)
   bool busy = false;
   uint64_t stamp = 0;
   ~PlanEntry() {
+    NB.reset();
     B.reset();
     P.reset();
     if (ctx) ctx_unref(ctx);
@@ -4765,7 +4834,8 @@ void plan_cache_release(const std::shared_ptr<PlanEntry>& e) {
 
 // after a successful execution of a cacheable plan: keep it (the oldest idle entry makes room)
 void plan_cache_insert(const pgx_query* q, pgx_ctx* ctx, pgx_segment* const* segs, int n, std::vector<uint64_t> uids,
-                       uint64_t key, std::unique_ptr<ExecPlan> P, std::unique_ptr<ExecBuffers> B) {
+                       uint64_t key, std::unique_ptr<ExecPlan> P, std::unique_ptr<ExecBuffers> B,
+                       std::unique_ptr<NarrowBuffers> NB = nullptr) {
   auto e = std::make_shared<PlanEntry>();
   ctx->refs.fetch_add(1);
   e->ctx = ctx;
@@ -4775,6 +4845,7 @@ void plan_cache_insert(const pgx_query* q, pgx_ctx* ctx, pgx_segment* const* seg
   e->key = key;
   e->P = std::move(P);
   e->B = std::move(B);
+  e->NB = std::move(NB);
   std::shared_ptr<PlanEntry> evicted;  // destroyed outside the lock (frees device memory)
   std::lock_guard<std::mutex> g(g_pc_mu);
   auto& v = g_pc[q];
@@ -4811,9 +4882,12 @@ void plan_cache_purge(const pgx_query* q, const pgx_ctx* ctx) {
   }
 }
 
+// Plain plans, and narrow partitioned plans (kept with their slabs and partitions: the same segments and bindings
+// give the same fills, so the first run's capacities hold; a replay that overflows anyway plans afresh)
 bool plan_cacheable(const ExecPlan& P) {
-  return !P.use_part && P.kq.group_mode != G_HASH64 && P.kq.group_mode != G_HASH128 && P.mv_items.empty() &&
-         !P.fsm_on && !P.mv_masks.p && !P.sel_buf.p && !P.lmask_buf.p && !P.jit.empty();
+  const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
+  return (P.use_part ? P.part_narrow : !hash) && P.mv_items.empty() && !P.fsm_on && !P.mv_masks.p && !P.sel_buf.p &&
+         !P.lmask_buf.p && !P.jit.empty();
 }
 
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
@@ -4837,6 +4911,20 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
       hp.mark("cached");
       ExecPlan& P = *e->P;
       ExecBuffers& B = *e->B;
+      if (P.use_part) {  // narrow partitioned: scan, split and aggregation into the kept slabs and partitions
+        if (e->NB && replay_narrow(ctx, P, B, *e->NB, st)) {
+          hp.mark("launch");
+          PartBuffers PB;
+          PB.okey = std::move(e->NB->okey);
+          PB.oplane = std::move(e->NB->oplane);
+          PB.prange = std::move(e->NB->prange);
+          PB.ocap = e->NB->ocap;
+          part_result(ctx, q, P, B, PB, R);
+          hp.mark("finish");
+          return;
+        }
+        e->key = ~e->key;  // (cannot happen: same inputs, same fills) never matched again; plan afresh below
+      }
       // the device arena (descriptors, bitmap-program descriptors, blob) is as the first execution sent it; the
       // bitmap programs run again from launch_scan
       alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
@@ -4893,6 +4981,10 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
         PB.prange = std::move(NB.prange);
         PB.ocap = NB.ocap;
         part_result(ctx, q, P, B, PB, R);
+        hp.mark("finish");
+        if (cache && plan_cacheable(P))
+          plan_cache_insert(&q, ctx, segs, n, std::move(uids), pkey, std::move(Pp), std::move(Bp),
+                            std::make_unique<NarrowBuffers>(std::move(NB)));
         return;
       }
       narrow_fallback(ctx, q, segs, n, P, B);

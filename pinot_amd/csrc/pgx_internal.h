@@ -222,7 +222,8 @@ constexpr int kNarrowMaxBits2 = 10;  // second split (pgx_narrow_split): up to 1
 // planning and execution read them from there, never from the environment (no per-query walk of environ, no race
 // with a setenv on another thread).  The whole set:
 //   PGX_JIT=0          the generic interpreter kernel instead of the generated (hiprtc) kernels, everywhere (A/B)
-//   PGX_PART_NARROW=0  sparse group-by through the 8-byte radix path instead of the narrow records
+//   PGX_PART_NARROW=0  sparse group-by through the 8-byte radix path instead of the narrow records; =direct: narrow
+//                      records carry value offsets wherever they fit (default: dictIds + LDS image when there is one)
 //   PGX_RCHUNK=0|1     bitmap programs evaluated by the separate pass / inside the query kernels (default: planner)
 //   PGX_RPROG=off|wave|seg|chunk|stack   bitmap-program kernel (off: no program fusion; default: planner)
 //   PGX_BATCH_SEGS=N   segments per batch of a long segment list on its first execution (0: one launch)
@@ -233,6 +234,7 @@ enum RProgKind { RPROG_AUTO = -1, RPROG_OFF = 0, RPROG_WAVE = 1, RPROG_SEG = 2, 
 struct Knobs {
   bool jit = true;
   bool narrow = true;
+  bool narrow_direct = false;  // PGX_PART_NARROW=direct
   int rchunk = -1;          // -1: planner's choice
   int rprog = RPROG_AUTO;
   int batch_segs = -1;      // -1: default (512; 0 with PGX_X_THROUGHPUT)

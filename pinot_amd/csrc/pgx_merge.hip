@@ -98,6 +98,17 @@ __global__ void __launch_bounds__(256) pgx_group_compact(const unsigned long lon
   }
 }
 
+// Hash-table keys of the compacted slots (kw words per key): the host reads back only the live groups' keys.
+__global__ void __launch_bounds__(256) pgx_gather_keys(const unsigned long long* __restrict__ keys,
+                                                       const int64_t* __restrict__ slot, int64_t n, int kw,
+                                                       unsigned long long* __restrict__ out) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t s = slot[i];
+    for (int w = 0; w < kw; ++w) out[i * kw + w] = keys[s * kw + w];
+  }
+}
+
 // Columnar groups (okey, oplane[p * ocap + i]) -> records of 5 words (key, count, sum, min, max) for an exchange.
 __global__ void __launch_bounds__(256) pgx_group_pack(const uint64_t* __restrict__ okey,
                                                       const uint64_t* __restrict__ opl, int64_t ocap, int64_t n,
@@ -119,6 +130,15 @@ extern "C" hipError_t pgx_launch_dense_reduce(unsigned long long* dst, const uns
   if (nplanes > 32) return hipErrorInvalidValue;
   const unsigned grid = static_cast<unsigned>(n / 256 + 1 < 16384 ? n / 256 + 1 : 16384);
   hipLaunchKernelGGL(pgx::pgx_dense_reduce, dim3(grid), dim3(256), 0, stream, dst, src, slots, nplanes, ops);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_gather_keys(const unsigned long long* keys, const int64_t* slot, int64_t n, int kw,
+                                             unsigned long long* out, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  if (kw < 1 || kw > 2) return hipErrorInvalidValue;
+  const unsigned grid = static_cast<unsigned>(n / 256 + 1 < 16384 ? n / 256 + 1 : 16384);
+  hipLaunchKernelGGL(pgx::pgx_gather_keys, dim3(grid), dim3(256), 0, stream, keys, slot, n, kw, out);
   return hipGetLastError();
 }
 

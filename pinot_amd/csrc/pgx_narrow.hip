@@ -228,8 +228,10 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
 // loaded while the current ones are aggregated.  Records are resolved 8 at a time: the 8 home buckets and the 8 values
 // are read back to back (one LDS round trip for all), a key found in its home bucket -- every record of a group but
 // its first, unless the bucket overflowed -- goes straight to the fire-and-forget LDS atomics, and only the others take
-// the probing loop (insert by CAS, then neighbouring buckets).  The workgroup's LDS holds the value image (IMG 1: u32
-// value - vbase per dictId, 2: FOR16 = 64 u32 block bases + u16 offset per dictId).
+// the probing loop (insert by CAS, then neighbouring buckets).  The record's value field is a dictId whose value the
+// workgroup's LDS image holds (IMG 1: u32 value - vbase per dictId, 2: FOR16 = 64 u32 block bases + u16 offset per
+// dictId), or the dictId of a MIN / MAX-only column looked up in vdict at the flush (IMG 0), or the value offset itself
+// (IMG 3: value - vbase; no image, so the LDS holds only the tables and more wavefronts fit a CU).
 // ctr: [0] groups appended, [3] overflow (a table filled up, or more groups than ocap).
 // ---------------------------------------------------------------------------------------------------------------------
 constexpr int kNAThreads = 512;
@@ -248,6 +250,7 @@ template <int IMG>
 __device__ __forceinline__ uint32_t na_img(const uint32_t* simg, int img_sh, uint32_t d) {
   if (IMG == 1) return simg[d];
   if (IMG == 2) return simg[d >> img_sh] + static_cast<uint32_t>(reinterpret_cast<const uint16_t*>(simg + 64)[d]);
+  if (IMG == 3) return d;
   return 0u;
 }
 
@@ -256,19 +259,20 @@ __device__ __forceinline__ int na_way(const na_u32x4 k, uint32_t key) {
 }
 
 template <int IMG, bool SUM, bool MN, bool MX>
-__global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
+__global__ void __launch_bounds__(kNAThreads) __attribute__((amdgpu_waves_per_eu(IMG == 3 ? 4 : 1))) pgx_narrow_aggregate(
     const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
     uint64_t kmask, uint64_t ic1, int ms, int64_t vbase, const uint32_t* __restrict__ img, int img_words,
     int img_sh, const int64_t* __restrict__ vdict, int cshift, uint64_t* __restrict__ okey,
     uint64_t* __restrict__ oplane, int64_t ocap, unsigned long long* __restrict__ ctr,
     unsigned long long* __restrict__ prange) {
-  __shared__ __attribute__((aligned(16))) uint32_t simg[IMG ? kNAImgWords : 1];
+  constexpr bool LIMG = IMG == 1 || IMG == 2;  // an image in LDS
+  __shared__ __attribute__((aligned(16))) uint32_t simg[LIMG ? kNAImgWords : 1];
   __shared__ __attribute__((aligned(16))) uint32_t tkey[kNAWaves * kNASlots];
   __shared__ unsigned long long tsc[kNAWaves * kNASlots];
   __shared__ uint32_t tmn[MN ? kNAWaves * kNASlots : 1], tmx[MX ? kNAWaves * kNASlots : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (IMG) {
+  if (LIMG) {
     const PGX_GLOBAL uint32_t* gi = (const PGX_GLOBAL uint32_t*)img;
     for (int i = tid; i < img_words; i += kNAThreads) simg[i] = gi[i];
   }
@@ -405,32 +409,40 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
     const int np = a.p + nw;
     return Pos{np, 0u, count(np)};
   };
-  uint32_t b0[16], b1[16], b2[16];
+  // (without an image: two batches and groups of 4 records, so 128 VGPRs hold a wavefront and a SIMD runs four)
+  constexpr int HB = LIMG ? 8 : 4;  // records resolved together
+  uint32_t b0[16], b1[16], b2[LIMG ? 16 : 1];
   Pos c{static_cast<int>(blockIdx.x) * kNAWaves + wave, 0u, 0u};
   c.n = count(c.p);
   if (c.p < nparts) load(c.p, c.i0, c.n, b0);
   Pos d = advance(c);
-  if (d.p < nparts) load(d.p, d.i0, d.n, b1);
+  if constexpr (LIMG) {
+    if (d.p < nparts) load(d.p, d.i0, d.n, b1);
+  }
   while (c.p < nparts) {
     const Pos e = advance(d);
-    if (e.p < nparts) load(e.p, e.i0, e.n, b2);
+    if constexpr (LIMG) {
+      if (e.p < nparts) load(e.p, e.i0, e.n, b2);
+    } else {
+      if (d.p < nparts) load(d.p, d.i0, d.n, b1);
+    }
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {  // two halves of 8 records: home buckets and values read back to back
-      na_u32x4 kb[8];
-      uint32_t val[8];
+    for (int h = 0; h < 16 / HB; ++h) {  // groups of HB records: home buckets and values read back to back
+      na_u32x4 kb[HB];
+      uint32_t val[HB];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int jj = h * 8 + j;
+      for (int j = 0; j < HB; ++j) {
+        const int jj = h * HB + j;
         const uint32_t R = b0[jj];
         const uint32_t r2 = R & rmask;
         const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2);
         kb[j] = *reinterpret_cast<const na_u32x4*>(K + b * kNAWays);
         val[j] = SUM ? na_img<IMG>(simg, img_sh, rb2 >= 32 ? 0u : R >> rb2) : 0u;
       }
-      uint32_t miss = 0u;  // records of this half whose key is not in its home bucket (yet)
+      uint32_t miss = 0u;  // records of this group whose key is not in its home bucket (yet)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int jj = h * 8 + j;
+      for (int j = 0; j < HB; ++j) {
+        const int jj = h * HB + j;
         const uint32_t ei = static_cast<uint32_t>((jj >> 2) * 256 + lane * 4 + (jj & 3));
         if (c.i0 + ei >= c.n) continue;
         const uint32_t R = b0[jj];
@@ -456,9 +468,9 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
         miss &= miss - 1u;
         uint32_t R = 0u, v = 0u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < HB; ++j)
           if (j == js) {
-            R = b0[h * 8 + j];
+            R = b0[h * HB + j];
             v = val[j];
           }
         const uint32_t r2 = R & rmask;
@@ -480,7 +492,7 @@ __global__ void __launch_bounds__(kNAThreads) pgx_narrow_aggregate(
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       b0[j] = b1[j];
-      b1[j] = b2[j];
+      if constexpr (LIMG) b1[j] = b2[j];
     }
     c = d;
     d = e;
@@ -530,8 +542,8 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
                                                   unsigned long long* prange, int grid, hipStream_t stream) {
   if (nparts <= 0) return hipSuccess;
   if (rb2 < 0 || rb2 > 31 || keybits < 1 || keybits > 64 || cap2 < 4 || (cap2 & 3) || cshift < 1 || cshift > 63 ||
-      grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 2 ||
-      (img_kind && (!img || img_words < 1 || img_words > pgx::kNAImgWords)) || (need_sum && !img_kind) ||
+      grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 3 ||
+      ((img_kind == 1 || img_kind == 2) && (!img || img_words < 1 || img_words > pgx::kNAImgWords)) || (need_sum && !img_kind) ||
       ((need_min || need_max) && !img_kind && !vdict))
     return hipErrorInvalidValue;
   const pgx::NarrowMix m = pgx::narrow_mix(keybits);
@@ -555,6 +567,7 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
     PGX_NA_CASES(0)
     PGX_NA_CASES(1)
     PGX_NA_CASES(2)
+    PGX_NA_CASES(3)
     default:
       return hipErrorInvalidValue;
   }
