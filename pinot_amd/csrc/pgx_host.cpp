@@ -3949,6 +3949,23 @@ bool replay_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB,
   return !tail[1] && !tail[2] && !tail[3];
 }
 
+// A kept radix plan again (plan cache): buckets and partitions as the first run sized them, the group outputs anew.
+bool replay_part(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB, hipStream_t st) {
+  alloc_outputs(ctx, P, B, nullptr, 0);
+  PB.okey = DevBuf(ctx, size_t(PB.ocap) * 8);
+  PB.oplane = DevBuf(ctx, size_t(PB.ocap) * 4 * 8);
+  part_prepare(P, PB, st);
+  reset_outputs(P, B, st);
+  launch_scan(P, st);
+  part_enqueue(P, PB, st);
+  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+  unsigned long long* tail = outs + 28;
+  hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
+  hip_check(hipMemcpyAsync(tail, devp(PB.ctr) + PB.ctr_words() - 4, 32, hipMemcpyDeviceToHost, st), "D2H");
+  hip_check(hipStreamSynchronize(st), "sync");
+  return !tail[1] && !tail[2] && !tail[3];
+}
+
 // The radix path's plan after a narrow attempt gave up: row-order 8-byte value records.
 void narrow_fallback(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
   P.part_narrow = false;
@@ -4729,10 +4746,12 @@ struct PlanEntry {
   std::unique_ptr<ExecPlan> P;
   std::unique_ptr<ExecBuffers> B;
   std::unique_ptr<NarrowBuffers> NB;  // a narrow partitioned plan's slabs and partitions (sized by its first run)
+  std::unique_ptr<PartBuffers> PB;    // a radix partitioned plan's buckets and partitions (same)
   bool busy = false;
   uint64_t stamp = 0;
   ~PlanEntry() {
     NB.reset();
+    PB.reset();
     B.reset();
     P.reset();
     if (ctx) ctx_unref(ctx);
@@ -4835,7 +4854,7 @@ void plan_cache_release(const std::shared_ptr<PlanEntry>& e) {
 // after a successful execution of a cacheable plan: keep it (the oldest idle entry makes room)
 void plan_cache_insert(const pgx_query* q, pgx_ctx* ctx, pgx_segment* const* segs, int n, std::vector<uint64_t> uids,
                        uint64_t key, std::unique_ptr<ExecPlan> P, std::unique_ptr<ExecBuffers> B,
-                       std::unique_ptr<NarrowBuffers> NB = nullptr) {
+                       std::unique_ptr<NarrowBuffers> NB = nullptr, std::unique_ptr<PartBuffers> PB = nullptr) {
   auto e = std::make_shared<PlanEntry>();
   ctx->refs.fetch_add(1);
   e->ctx = ctx;
@@ -4846,6 +4865,7 @@ void plan_cache_insert(const pgx_query* q, pgx_ctx* ctx, pgx_segment* const* seg
   e->P = std::move(P);
   e->B = std::move(B);
   e->NB = std::move(NB);
+  e->PB = std::move(PB);
   std::shared_ptr<PlanEntry> evicted;  // destroyed outside the lock (frees device memory)
   std::lock_guard<std::mutex> g(g_pc_mu);
   auto& v = g_pc[q];
@@ -4882,11 +4902,11 @@ void plan_cache_purge(const pgx_query* q, const pgx_ctx* ctx) {
   }
 }
 
-// Plain plans, and narrow partitioned plans (kept with their slabs and partitions: the same segments and bindings
+// Plain plans, and partitioned plans (kept with their slabs / buckets and partitions: the same segments and bindings
 // give the same fills, so the first run's capacities hold; a replay that overflows anyway plans afresh)
 bool plan_cacheable(const ExecPlan& P) {
   const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
-  return (P.use_part ? P.part_narrow : !hash) && P.mv_items.empty() && !P.fsm_on && !P.mv_masks.p && !P.sel_buf.p &&
+  return (P.use_part || !hash) && P.mv_items.empty() && !P.fsm_on && !P.mv_masks.p && !P.sel_buf.p &&
          !P.lmask_buf.p && !P.jit.empty();
 }
 
@@ -4911,14 +4931,23 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
       hp.mark("cached");
       ExecPlan& P = *e->P;
       ExecBuffers& B = *e->B;
-      if (P.use_part) {  // narrow partitioned: scan, split and aggregation into the kept slabs and partitions
+      if (P.use_part) {  // partitioned: scan, splits and aggregation into the kept slabs / buckets and partitions
+        PartBuffers PB;
+        bool ok = false;
         if (e->NB && replay_narrow(ctx, P, B, *e->NB, st)) {
-          hp.mark("launch");
-          PartBuffers PB;
           PB.okey = std::move(e->NB->okey);
           PB.oplane = std::move(e->NB->oplane);
           PB.prange = std::move(e->NB->prange);
           PB.ocap = e->NB->ocap;
+          ok = true;
+        } else if (e->PB && replay_part(ctx, P, B, *e->PB, st)) {
+          PB.okey = std::move(e->PB->okey);
+          PB.oplane = std::move(e->PB->oplane);
+          PB.ocap = e->PB->ocap;
+          ok = true;
+        }
+        if (ok) {
+          hp.mark("launch");
           part_result(ctx, q, P, B, PB, R);
           hp.mark("finish");
           return;
@@ -4992,6 +5021,11 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     PartBuffers PB;
     if (run_partitioned(ctx, P, B, PB, st)) {
       part_result(ctx, q, P, B, PB, R);
+      hp.mark("finish");
+      if (cache && plan_cacheable(P)) {
+        auto kept = std::make_unique<PartBuffers>(std::move(PB));
+        plan_cache_insert(&q, ctx, segs, n, std::move(uids), pkey, std::move(Pp), std::move(Bp), nullptr, std::move(kept));
+      }
       return;
     }
     P.use_part = false;  // groups too many or too skewed for the partitions: global hash table, generic kernel

@@ -368,14 +368,16 @@ def test_partitioned_per_segment_metric_dictionaries(ctx, metric):
     assert blk.stats.as_list() == list(o["stats"])
 
 
-def test_narrow_plan_cache_replays(ctx, seg, monkeypatch, capfd):
-    """A narrow partitioned plan is kept with its slabs and partitions (pgx_host.cpp plan_cacheable, replay_narrow): the
-    second and third executions of the same query over the same segment replay it (the host-profile line's "cached"
-    mark; no second narrow sizing run), and every result -- decoded only after all three ran, so each result's group
-    outputs are its own and the shared key tables outlive the replays -- equals the oracle's."""
+@pytest.mark.parametrize("mode", ["narrow", "radix"])
+def test_partitioned_plan_cache_replays(ctx, seg, mode, monkeypatch, capfd):
+    """A partitioned plan is kept with its slabs / buckets and partitions (pgx_host.cpp plan_cacheable, replay_narrow,
+    replay_part): the second and third executions of the same query over the same segment replay it (the host-profile
+    line's "cached" mark; no second narrow sizing run), and every result -- decoded only after all three ran, so each
+    result's group outputs are its own and the shared key tables outlive the replays -- equals the oracle's."""
     from pinot_amd import engine as E
     from pinot_amd import native as N
     monkeypatch.setenv("PGX_DEBUG", "host_profile,narrow_log")
+    monkeypatch.setenv("PGX_PART_NARROW", "1" if mode == "narrow" else "0")
     gseg, oseg, fmt = seg
     q = pql.compile(AGGS + " WHERE a > 100 GROUP BY g2, a, c")
     o = H.oracle_answer([oseg], q, literal=True)
@@ -389,7 +391,7 @@ def test_narrow_plan_cache_replays(ctx, seg, monkeypatch, capfd):
         assert lines, err
         marks.append(" cached=" in lines[-1])
     assert marks == [False, True, True]
-    assert narrow_runs == 1
+    assert narrow_runs == (1 if mode == "narrow" else 0)
     fns = [a["fn"] for a in q["aggregations"]]
     for r in results:
         blk = E.decode_result(qq, r, [gseg])
