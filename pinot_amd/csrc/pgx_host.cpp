@@ -68,7 +68,8 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
                                                 hipStream_t stream);
 extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
                                       void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
-                                      const unsigned long long* prange, hipStream_t stream);
+                                      const unsigned long long* prange, int64_t* cidx, uint64_t* ckey, int64_t ccap,
+                                      hipStream_t stream);
 extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
                                               const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
 extern "C" size_t pgx_trim_state_bytes(void);
@@ -4061,9 +4062,13 @@ const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
   DevBuf state(L.ctx, sb * nf), idx(L.ctx, size_t(size) * 8 * nf), keys(L.ctx, size_t(size) * 8 * nf);
   hip_check(hipMemcpyAsync(state.p, init.data(), init.size(), hipMemcpyHostToDevice, st), "trim state H2D");
   const int grid = int(std::max<int64_t>(1, std::min<int64_t>((num_groups + 255) / 256, int64_t(L.ctx->num_cus) * 8)));
+  // candidate lists after the first digit (pgx_trim_cand): room for 32x the groups wanted, at least 1M (a MAX
+  // threshold's bin at C3 holds a few 100k groups), at most every group
+  const int64_t ccap = std::min<int64_t>(num_groups, std::max<int64_t>(int64_t(1) << 20, 32 * size));
+  DevBuf cidx(L.ctx, size_t(std::max<int64_t>(ccap, 1)) * 8 * nf), ckey(L.ctx, size_t(std::max<int64_t>(ccap, 1)) * 8 * nf);
   PGX_LAUNCH(st, "pgx_trim", pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kinds.data(), nf, state.p,
                             idx.as<int64_t>(), keys.as<uint64_t>(), size, grid,
-                            L.prange.p ? devp(L.prange) : nullptr, st),
+                            L.prange.p ? devp(L.prange) : nullptr, cidx.as<int64_t>(), ckey.as<uint64_t>(), ccap, st),
             "trim launch");
   std::vector<int64_t> ix(size_t(size) * nf);
   std::vector<uint64_t> ky(size_t(size) * nf);

@@ -6,7 +6,9 @@
 // (query/aggregation/groupby/AggregationGroupByOperatorService.java:64-76, :284-440; the comparator looks at the value
 // only).  Here the same selection is a radix select over a 64-bit order key per group (passes of 11-bit digits, each a
 // histogram of the groups still matching the selected prefix), then one compaction pass that keeps every group above
-// the threshold key and as many threshold ties as fit.  Which of several tied groups at the threshold survive is
+// the threshold key and as many threshold ties as fit.  After the first digit the groups at or above the threshold's
+// bin -- the only ones the later passes and the selection can keep -- are copied out (index + key) once, and the later
+// passes read that short list instead of the planes (two full reads of a plane per function instead of up to eight).  Which of several tied groups at the threshold survive is
 // arbitrary, as in the reference (heap order; parity unpinned); the kept values are exact.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -32,6 +34,7 @@ struct TrimState {
   unsigned long long kmin;     // key range of the groups                          (48)
   unsigned long long kmax;     //                                                  (56)
   unsigned int hist[2048];     //                                                  (64)
+  unsigned long long n_cand;   // groups copied to the candidate list (pgx_trim_cand)
 };
 constexpr int kTrimDigit = 11;             // bits per histogram pass
 constexpr int kTrimBins = 1 << kTrimDigit;
@@ -41,6 +44,19 @@ constexpr int kTrimMaxFns = 8;
 struct TrimKinds {             // function slot -> trim key kind
   int kind[kTrimMaxFns];
 };
+
+// Where a pass reads its groups: the planes (trim_key of group i), or -- once pgx_trim_cand has run and its list fit --
+// function y's candidate list (cidx / ckey + y * ccap: the group's index and key).
+struct TrimSrc {
+  const uint64_t* oplane;
+  int64_t ocap, n;
+  const int64_t* cidx;
+  const uint64_t* ckey;
+  int64_t ccap;
+};
+__device__ __forceinline__ bool trim_use_cand(const TrimState* st, const TrimSrc& S) {
+  return st->n_cand - 1ull < static_cast<unsigned long long>(S.ccap);  // 0 < n_cand <= ccap
+}
 
 // Larger key = better group.
 __device__ __forceinline__ uint64_t trim_key(const PGX_GLOBAL uint64_t* pl, int64_t ocap, int64_t i, int kind) {
@@ -127,10 +143,13 @@ __global__ void pgx_trim_begin(TrimState* __restrict__ sts) {
   st->done = 0;
 }
 
-__global__ void __launch_bounds__(256) pgx_trim_hist(const uint64_t* __restrict__ oplane, int64_t ocap, int64_t n,
-                                                     const TrimKinds K, TrimState* __restrict__ sts) {
+__global__ void __launch_bounds__(256) pgx_trim_hist(const TrimSrc S, const TrimKinds K, TrimState* __restrict__ sts) {
   TrimState* st = sts + blockIdx.y;
   if (st->done) return;
+  const bool cand = trim_use_cand(st, S);
+  const int64_t n = cand ? static_cast<int64_t>(st->n_cand) : S.n;
+  if (static_cast<int64_t>(blockIdx.x) * 256 >= n) return;  // (a short candidate list: most workgroups idle)
+  const PGX_GLOBAL uint64_t* ck = (const PGX_GLOBAL uint64_t*)S.ckey + static_cast<int64_t>(blockIdx.y) * S.ccap;
   __shared__ unsigned int lh[kTrimBins];
   const int tid = threadIdx.x;
   const int kind = K.kind[blockIdx.y];
@@ -138,14 +157,73 @@ __global__ void __launch_bounds__(256) pgx_trim_hist(const uint64_t* __restrict_
   __syncthreads();
   const unsigned long long prefix = st->prefix, mask = st->mask;
   const int shift = st->shift;
-  const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)oplane;
+  const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)S.oplane;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
-    const uint64_t key = trim_key(pl, ocap, i, kind);
+    const uint64_t key = cand ? ck[i] : trim_key(pl, S.ocap, i, kind);
     if ((key & mask) == prefix) atomicAdd(&lh[(key >> shift) & (kTrimBins - 1u)], 1u);
   }
   __syncthreads();
   for (int b = tid; b < kTrimBins; b += 256)
     if (lh[b]) atomicAdd(&st->hist[b], lh[b]);
+}
+
+// After the first digit: every group at or above the threshold's bin (key >= prefix: the bits below the fixed ones are
+// zero in prefix) to function y's candidate list.  A workgroup scans one contiguous range and lists its candidates in
+// LDS, reserving list space with ONE device atomic per flush (a few per workgroup): a wavefront atomic per 64 groups on
+// one address would serialise (~11 ns each, ~10^5 of them at C3).  A list that would run past ccap is abandoned
+// (n_cand > ccap: the later passes read the planes).
+constexpr int kCandLds = 2048;
+__global__ void __launch_bounds__(256) pgx_trim_cand(const TrimSrc S, const TrimKinds K, TrimState* __restrict__ sts,
+                                                     int64_t* __restrict__ cidx, uint64_t* __restrict__ ckey) {
+  __shared__ uint32_t lidx[kCandLds];
+  __shared__ uint64_t lkey[kCandLds];
+  __shared__ unsigned int lcnt;
+  __shared__ unsigned long long gbase;
+  TrimState* st = sts + blockIdx.y;
+  if (st->done) return;  // threshold complete after one digit: the selection reads the planes once
+  const int kind = K.kind[blockIdx.y];
+  const unsigned long long prefix = st->prefix;
+  const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)S.oplane;
+  cidx += static_cast<int64_t>(blockIdx.y) * S.ccap;
+  ckey += static_cast<int64_t>(blockIdx.y) * S.ccap;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int64_t chunk = (S.n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * chunk;
+  const int64_t hi = lo + chunk < S.n ? lo + chunk : S.n;
+  if (tid == 0) lcnt = 0u;
+  __syncthreads();
+  for (int64_t b = lo; b < hi; b += 256) {
+    const int64_t i = b + tid;
+    const uint64_t key = i < hi ? trim_key(pl, S.ocap, i, kind) : 0ull;
+    const bool in = i < hi && key >= prefix;
+    const unsigned long long m = __ballot(in);
+    if (m) {
+      const int leader = __ffsll(static_cast<long long>(m)) - 1;
+      unsigned int r0 = 0u;
+      if (lane == leader) r0 = atomicAdd(&lcnt, static_cast<unsigned int>(__popcll(m)));
+      const unsigned int r = __shfl(r0, leader, 64) + static_cast<unsigned int>(__popcll(m & ((1ull << lane) - 1ull)));
+      if (in) {  // r < kCandLds: the list is flushed while it has room for a whole round
+        lidx[r] = static_cast<uint32_t>(i - lo);
+        lkey[r] = key;
+      }
+    }
+    __syncthreads();
+    const unsigned int nl = lcnt;
+    if (nl > static_cast<unsigned int>(kCandLds - 256) || b + 256 >= hi) {  // (uniform)
+      if (tid == 0 && nl) gbase = atomicAdd(&st->n_cand, static_cast<unsigned long long>(nl));
+      __syncthreads();
+      for (unsigned int j = tid; j < nl; j += 256) {
+        const unsigned long long p = gbase + j;
+        if (p < static_cast<unsigned long long>(S.ccap)) {
+          cidx[p] = lo + lidx[j];
+          ckey[p] = lkey[j];
+        }
+      }
+      __syncthreads();
+      if (tid == 0) lcnt = 0u;
+      __syncthreads();
+    }
+  }
 }
 
 // One wavefront per function: fix the next digit of the threshold from the histogram (the largest digit d whose bins
@@ -196,8 +274,7 @@ __global__ void pgx_trim_step(TrimState* __restrict__ sts) {
 // can tie tens of thousands of groups, and one device-scope atomic per wave on one address serialises at ~11 ns each.
 // A workgroup whose range holds more than kTieCap ties reserves the rest per wave as it finds them.
 constexpr int kTieCap = 2048;
-__global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restrict__ oplane, int64_t ocap, int64_t n,
-                                                       const TrimKinds K, TrimState* __restrict__ sts,
+__global__ void __launch_bounds__(256) pgx_trim_select(const TrimSrc S, const TrimKinds K, TrimState* __restrict__ sts,
                                                        int64_t* __restrict__ idx, uint64_t* __restrict__ keys,
                                                        int64_t cap) {
   __shared__ uint32_t tbuf[kTieCap];
@@ -209,7 +286,12 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restric
   keys += static_cast<int64_t>(blockIdx.y) * cap;
   const unsigned long long thr = st->prefix;
   const long long ties = st->k;
-  const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)oplane;
+  const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)S.oplane;
+  const bool cand = trim_use_cand(st, S);
+  const int64_t n = cand ? static_cast<int64_t>(st->n_cand) : S.n;
+  const PGX_GLOBAL uint64_t* ck = (const PGX_GLOBAL uint64_t*)S.ckey + static_cast<int64_t>(blockIdx.y) * S.ccap;
+  const PGX_GLOBAL int64_t* ci = (const PGX_GLOBAL int64_t*)S.cidx + static_cast<int64_t>(blockIdx.y) * S.ccap;
+  auto orig = [&](int64_t i) -> int64_t { return cand ? ci[i] : i; };  // the group's index in the planes
   const int lane = threadIdx.x & 63;
   const unsigned long long below = (1ull << lane) - 1ull;
   const int64_t chunk = (n + gridDim.x - 1) / gridDim.x;
@@ -227,7 +309,7 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restric
   for (int64_t b = lo + (threadIdx.x & ~63); b < hi; b += 256) {
     const int64_t i = b + lane;
     const bool valid = i < hi;
-    const uint64_t key = valid ? trim_key(pl, ocap, i, kind) : 0ull;
+    const uint64_t key = valid ? (cand ? ck[i] : trim_key(pl, S.ocap, i, kind)) : 0ull;
     const bool eq = valid && key == thr;
     const unsigned long long em = __ballot(eq);
     bool take = valid && key > thr;
@@ -247,7 +329,7 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restric
     if (!tm) continue;
     const unsigned long long p = reserve(&st->n_sel, tm);
     if (take && p < static_cast<unsigned long long>(cap)) {
-      idx[p] = i;
+      idx[p] = orig(i);
       keys[p] = key;
     }
   }
@@ -268,7 +350,7 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const uint64_t* __restric
   for (long long j = threadIdx.x; j < ttake; j += 256) {
     const long long p = tsel + j;
     if (p < cap) {
-      idx[p] = lo + tbuf[j];
+      idx[p] = orig(lo + tbuf[j]);
       keys[p] = thr;
     }
   }
@@ -294,8 +376,10 @@ __global__ void __launch_bounds__(256) pgx_group_gather(const uint64_t* __restri
 // a function's threshold is complete return at once.
 extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
                                       void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
-                                      const unsigned long long* prange, hipStream_t stream) {
-  if (nf < 1 || nf > pgx::kTrimMaxFns) return hipErrorInvalidValue;
+                                      const unsigned long long* prange, int64_t* cidx, uint64_t* ckey, int64_t ccap,
+                                      hipStream_t stream) {
+  if (nf < 1 || nf > pgx::kTrimMaxFns || ccap < 0 || (ccap > 0 && (!cidx || !ckey))) return hipErrorInvalidValue;
+  const pgx::TrimSrc S{oplane, ocap, n, cidx, ckey, ccap};
   pgx::TrimKinds K{};
   bool seeded = prange != nullptr;
   for (int f = 0; f < nf; ++f) {
@@ -308,10 +392,11 @@ extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int6
   else hipLaunchKernelGGL(pgx::pgx_trim_range, g, dim3(256), 0, stream, oplane, ocap, n, K, st);
   hipLaunchKernelGGL(pgx::pgx_trim_begin, dim3(nf), dim3(64), 0, stream, st);
   for (int pass = 0; pass < pgx::kTrimPasses; ++pass) {
-    hipLaunchKernelGGL(pgx::pgx_trim_hist, g, dim3(256), 0, stream, oplane, ocap, n, K, st);
+    hipLaunchKernelGGL(pgx::pgx_trim_hist, g, dim3(256), 0, stream, S, K, st);
     hipLaunchKernelGGL(pgx::pgx_trim_step, dim3(nf), dim3(64), 0, stream, st);
+    if (pass == 0 && ccap > 0) hipLaunchKernelGGL(pgx::pgx_trim_cand, g, dim3(256), 0, stream, S, K, st, cidx, ckey);
   }
-  hipLaunchKernelGGL(pgx::pgx_trim_select, g, dim3(256), 0, stream, oplane, ocap, n, K, st, idx, keys, cap);
+  hipLaunchKernelGGL(pgx::pgx_trim_select, g, dim3(256), 0, stream, S, K, st, idx, keys, cap);
   return hipGetLastError();
 }
 
