@@ -235,7 +235,7 @@ typedef struct {
 #define PGX_X_KEEP_DENSE_ON_DEVICE 0x1u /* leave the dense table in dense_out; do not compact to host */
 #define PGX_X_FORCE_HASH 0x2u           /* testing: use the hash group-by path even for small key spaces */
 #define PGX_X_NO_PARTITION 0x4u         /* testing: sparse group-by through the global hash table, not the partitioned
-                                           record path (pgx_host.cpp run_partitioned) */
+                                           record path (pgx_part.cpp run_partitioned) */
 #define PGX_X_THROUGHPUT 0x8u           /* the caller keeps several queries in flight (pgx_execute_async): plan every
                                            segment into one launch per kernel instead of the batched pipeline, whose
                                            early start only shortens a lone query's latency (ABI 6) */

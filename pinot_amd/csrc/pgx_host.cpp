@@ -2,2620 +2,13 @@
 //
 // Segment staging (Loaders / ColumnIndexContainer), per-query physical planning (FilterPlanNode's operator choice,
 // the AND/OR algebra as a postfix program, DefaultGroupKeyGenerator's key space), launch of the fused HIP kernel and
-// decoding of the combined result (MCombine*Operator + AggregationGroupByOperatorService.trimToSize).
+// decoding of the combined result (MCombine*Operator + AggregationGroupByOperatorService.trimToSize).  The partitioned
+// sparse group-by runtime is pgx_part.cpp; the shared types are pgx_host.h.
 // Reference paths are relative to pinot-core/src/main/java/com/linkedin/pinot/core/.
-#include <hip/hip_runtime.h>
+#include "pgx_host.h"
 
-#include <algorithm>
-#include <atomic>
-#include <chrono>
-#include <condition_variable>
-#include <exception>
-#include <functional>
-#include <thread>
-#include <cctype>
-#include <cerrno>
-#include <cmath>
-#include <tuple>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <deque>
-#include <limits>
-#include <map>
-#include <memory>
-#include <mutex>
-#include <numeric>
-#include <string>
-#include <unordered_map>
-#include <vector>
 
-#include "../../include/pgx.h"
-#include "pgx_internal.h"
-#include "pgx_jit_abi.h"
-
-extern "C" hipError_t pgx_launch_scan(const pgx::KQuery* q, int grid, int64_t tiles_per_wg, size_t lds_bytes,
-                                      hipStream_t stream);
-extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t slots, int num_planes,
-                                             const pgx::KQuery* q, unsigned long long* keys, uint64_t key_words,
-                                             unsigned int* key_state, hipStream_t stream);
-extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
-                                         unsigned long long* counter, int64_t* out_slot,
-                                         unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
-extern "C" hipError_t pgx_launch_gather_keys(const unsigned long long* keys, const int64_t* slot, int64_t n, int kw,
-                                             unsigned long long* out, hipStream_t stream);
-extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
-extern "C" hipError_t pgx_launch_roaring_program_wave(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
-                                                      int maxchunks, int nslots, hipStream_t stream);
-extern "C" hipError_t pgx_launch_roaring_program(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
-                                                 int maxchunks, int maxleaves, hipStream_t stream);
-extern "C" hipError_t pgx_launch_synth(uint32_t* out_words, int64_t n_rows, int bits, uint32_t card, uint64_t seed,
-                                       int64_t n_words, uint64_t pair_seed, uint32_t npairs, hipStream_t stream);
-extern "C" hipError_t pgx_launch_partition(const uint64_t* in, const int64_t* in_off, const unsigned long long* in_cnt,
-                                           int in_cstride, int nreg, int reg_div, int64_t in_cap, int chunks_per_reg,
-                                           uint64_t keymask, int shift, int nbits, uint64_t* out, int64_t cap,
-                                           unsigned long long* cursor, int cstride, unsigned long long* overflow,
-                                           hipStream_t stream);
-extern "C" hipError_t pgx_launch_mv_leaf_mask(const pgx::MvLeaf* items, int nitems, int max_words, hipStream_t stream);
-extern "C" hipError_t pgx_launch_mv_aggregate(const pgx::MvAgg* items, int nitems, int max_words, hipStream_t stream);
-extern "C" hipError_t pgx_launch_mv_group(const pgx::MvGroupArgs* args, int nsegs, int max_docs, int ordered,
-                                          hipStream_t stream);
-extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
-                                                int nparts, int64_t cap, uint64_t keymask, int keybits, int64_t vbase,
-                                                int need_sum, int need_min, int need_max, int pack_shift,
-                                                uint64_t* okey, uint64_t* oplane, int64_t ocap,
-                                                unsigned long long* ocount, unsigned long long* overflow,
-                                                hipStream_t stream);
-extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
-                                      void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
-                                      const unsigned long long* prange, int64_t* cidx, uint64_t* ckey, int64_t ccap,
-                                      hipStream_t stream);
-extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
-                                              const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
-extern "C" size_t pgx_trim_state_bytes(void);
-extern "C" hipError_t pgx_launch_pack_remap(uint32_t* out_words, const int32_t* ids, const int32_t* remap,
-                                            int64_t n_rows, int bits, int64_t n_words, hipStream_t stream);
-extern "C" hipError_t pgx_launch_narrow_split(const uint32_t* lo, const uint16_t* hi, const unsigned long long* cnt1,
-                                              int nbuckets, int nwg, int64_t cap1, int rb1, int k2, uint32_t* out,
-                                              int64_t cap2, unsigned int* cnt2, unsigned long long* ovf,
-                                              hipStream_t stream);
-extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsigned int* cnt2, int64_t cap2,
-                                                  int nparts, int rb2, int keybits, int64_t vbase, int img_kind,
-                                                  const uint32_t* img, int img_words, int img_sh, const int64_t* vdict,
-                                                  int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
-                                                  uint64_t* oplane, int64_t ocap, unsigned long long* ctr,
-                                                  unsigned long long* prange, int grid, hipStream_t stream);
-extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
-                                     int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
-                                     uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream);
-extern "C" hipError_t pgx_launch_dense_reduce(unsigned long long* dst, const unsigned long long* src, uint64_t slots,
-                                              int nplanes, uint64_t ops, hipStream_t stream);
-extern "C" hipError_t pgx_launch_group_merge(const uint64_t* key, const uint64_t* pl, int64_t es, int64_t ps,
-                                             int64_t n, unsigned long long* tkey, unsigned long long* tpl,
-                                             uint64_t cap, unsigned long long* overflow, hipStream_t stream);
-extern "C" hipError_t pgx_launch_group_pack(const uint64_t* okey, const uint64_t* opl, int64_t ocap, int64_t n,
-                                            uint64_t* rec, hipStream_t stream);
-extern "C" hipError_t pgx_launch_group_compact(const unsigned long long* tkey, const unsigned long long* tpl,
-                                               uint64_t cap, uint64_t* okey, uint64_t* opl, int64_t ocap,
-                                               unsigned long long* counter, hipStream_t stream);
-struct pgx_ctx;
-extern "C" void ctx_unref(pgx_ctx* ctx);
-
-using namespace pgx;
-
-namespace {
-
-thread_local std::string g_last_error;
-
-struct PgxError {
-  pgx_status status;
-  std::string msg;
-};
-
-[[noreturn]] void fail(pgx_status s, const std::string& m) { throw PgxError{s, m}; }
-
-void hip_check(hipError_t e, const char* what) {
-  if (e != hipSuccess) fail(PGX_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-// Kernel timing of whole executions (pgx_timing_start / pgx_timing_stop; bench.py's roofline): while a window is open,
-// every kernel the library launches is bracketed by two HIP events on the stream it is launched on (the query stream,
-// the side stream of batched plans, a caller's stream).  At the end of the window the launches' [start, end] intervals
-// give the GPU time an execution really costs: the UNION of busy intervals (concurrent kernels on two streams count
-// once), next to the summed per-launch durations and the span.  Process-wide: one window at a time.
-struct KTimer {
-  std::atomic<bool> on{false};
-  std::mutex mu;
-  struct Rec {
-    hipEvent_t a, b;
-    const char* name;
-  };
-  std::vector<Rec> recs;
-  std::vector<hipEvent_t> spare;
-  hipEvent_t ref = nullptr;
-  hipEvent_t take() {
-    std::lock_guard<std::mutex> g(mu);
-    if (!spare.empty()) {
-      hipEvent_t e = spare.back();
-      spare.pop_back();
-      return e;
-    }
-    hipEvent_t e = nullptr;
-    if (hipEventCreate(&e) != hipSuccess) return nullptr;
-    return e;
-  }
-  void add(hipEvent_t a, hipEvent_t b, const char* name) {
-    std::lock_guard<std::mutex> g(mu);
-    recs.push_back({a, b, name});
-  }
-};
-KTimer g_kt;
-
-struct KScope {
-  hipEvent_t a = nullptr, b = nullptr;
-  hipStream_t st;
-  const char* name;
-  KScope(hipStream_t s, const char* n) : st(s), name(n) {
-    if (!g_kt.on.load(std::memory_order_relaxed)) return;
-    a = g_kt.take();
-    b = g_kt.take();
-    if (a && b && hipEventRecord(a, st) != hipSuccess) a = nullptr;
-  }
-  ~KScope() {
-    if (!a || !b) return;
-    if (hipEventRecord(b, st) == hipSuccess) g_kt.add(a, b, name);
-  }
-};
-// launch `call` (returning hipError_t) on stream `st` as kernel `name`, timed when a timing window is open
-#define PGX_LAUNCH(st, name, call, what) \
-  do {                                   \
-    KScope ks_((st), (name));            \
-    hip_check((call), (what));           \
-  } while (0)
-
-template <typename F>
-pgx_status guarded(F&& f) {
-  try {
-    f();
-    return PGX_OK;
-  } catch (const PgxError& e) {
-    g_last_error = e.msg;
-    return e.status;
-  } catch (const std::bad_alloc&) {
-    g_last_error = "host out of memory";
-    return PGX_ERR_OOM;
-  } catch (const std::exception& e) {
-    g_last_error = e.what();
-    return PGX_ERR_INTERNAL;
-  }
-}
-
-inline uint32_t be32(const uint8_t* p) {
-  return (uint32_t(p[0]) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | uint32_t(p[3]);
-}
-inline uint64_t be64(const uint8_t* p) { return (uint64_t(be32(p)) << 32) | be32(p + 4); }
-
-uint64_t fnv1a(const void* data, size_t n, uint64_t h = 1469598103934665603ull) {
-  const uint8_t* p = static_cast<const uint8_t*>(data);
-  for (size_t i = 0; i < n; ++i) {
-    h ^= p[i];
-    h *= 1099511628211ull;
-  }
-  return h;
-}
-
-// Padded size of a fixed-bit forward index on device: whole tiles (each lane reads exactly `bits` dwords).
-uint64_t padded_fwd_bytes(int64_t total_docs, int bits) {
-  const int64_t tiles = (total_docs + kTileRows - 1) / kTileRows;
-  return static_cast<uint64_t>(std::max<int64_t>(tiles, 1)) * (kTileRows / 8) * bits + 64;
-}
-
-}  // namespace
-
-// =================================================================================================
-// Context
-// =================================================================================================
-// Host worker pool of a context: per-segment query planning of large segment lists runs on it (C5: 4096 segments).
-// run(n, f) calls f(i) for i in [0, n) on the workers and the caller; the first exception is rethrown to the caller.
-struct WorkerPool {
-  std::vector<std::thread> th;
-  std::mutex m;
-  std::condition_variable cv, done_cv;
-  const std::function<void(int)>* job = nullptr;
-  int njobs = 0, pending = 0;
-  std::atomic<int> next{0};
-  uint64_t gen = 0;
-  bool stop = false;
-  std::exception_ptr err;
-
-  void work() {
-    for (int i; (i = next.fetch_add(1)) < njobs;) {
-      try {
-        (*job)(i);
-      } catch (...) {
-        std::lock_guard<std::mutex> g(m);
-        if (!err) err = std::current_exception();
-      }
-    }
-  }
-  void start(int nthreads) {
-    for (int t = 0; t < nthreads; ++t)
-      th.emplace_back([this] {
-        uint64_t seen = 0;
-        for (;;) {
-          {
-            std::unique_lock<std::mutex> g(m);
-            cv.wait(g, [&] { return stop || gen != seen; });
-            if (stop) return;
-            seen = gen;
-          }
-          work();
-          std::lock_guard<std::mutex> g(m);
-          if (--pending == 0) done_cv.notify_all();
-        }
-      });
-  }
-  std::mutex run_mu;  // one job at a time: concurrent pgx_execute calls on one context take turns here
-  void run(int n, const std::function<void(int)>& f) {
-    std::lock_guard<std::mutex> one(run_mu);
-    std::unique_lock<std::mutex> g(m);
-    job = &f;
-    njobs = n;
-    next = 0;
-    err = nullptr;
-    pending = int(th.size());
-    ++gen;
-    cv.notify_all();
-    g.unlock();
-    work();
-    g.lock();
-    done_cv.wait(g, [&] { return pending == 0; });
-    job = nullptr;
-    if (err) std::rethrow_exception(err);
-  }
-  ~WorkerPool() {
-    {
-      std::lock_guard<std::mutex> g(m);
-      stop = true;
-    }
-    cv.notify_all();
-    for (auto& t : th) t.join();
-  }
-};
-
-// Persistent host threads for independent tasks (batched plans: every batch of a long segment list is planned on its own
-// thread while the submitting thread launches the batches in order).  Unlike WorkerPool (one parallel loop at a time,
-// the caller blocks), submit() returns at once.
-struct TaskTeam {
-  std::vector<std::thread> th;
-  std::mutex m;
-  std::condition_variable cv;
-  std::deque<std::function<void()>> q;
-  bool stop = false;
-  void start(int n) {
-    for (int t = 0; t < n; ++t)
-      th.emplace_back([this] {
-        for (;;) {
-          std::function<void()> f;
-          {
-            std::unique_lock<std::mutex> g(m);
-            cv.wait(g, [&] { return stop || !q.empty(); });
-            if (q.empty()) return;  // stop, nothing left
-            f = std::move(q.front());
-            q.pop_front();
-          }
-          f();  // tasks catch their own exceptions
-        }
-      });
-  }
-  void submit(std::function<void()> f) {
-    {
-      std::lock_guard<std::mutex> g(m);
-      q.push_back(std::move(f));
-    }
-    cv.notify_one();
-  }
-  ~TaskTeam() {
-    {
-      std::lock_guard<std::mutex> g(m);
-      stop = true;
-    }
-    cv.notify_all();
-    for (auto& t : th) t.join();
-  }
-};
-
-struct DevBuf;
-struct SharedDict;
-
-struct pgx_ctx {
-  std::atomic<int> refs{1};  // the caller's handle + one per staged segment
-  // Numeric dictionaries (and their LDS value images) staged once per context and shared by every segment holding
-  // the same dictionary (key: content hash; content compared on a hit): segments of one table usually share value
-  // domains, so thousands of segments then read one L2-resident table instead of thousands of private copies.
-  std::mutex dict_mu;
-  std::unordered_map<uint64_t, std::weak_ptr<SharedDict>> dicts;
-  WorkerPool pool;           // started lazily (first large query)
-  std::once_flag pool_once;
-  TaskTeam plan_team;        // batched plans (run_batched), started lazily
-  std::once_flag plan_once;
-  void plan_submit(std::function<void()> f) {
-    std::call_once(plan_once, [this] {
-      const unsigned hc = std::thread::hardware_concurrency();
-      plan_team.start(int(std::min<unsigned>(8, hc > 2 ? hc - 2 : 1)));
-    });
-    plan_team.submit(std::move(f));
-  }
-  void parallel_for(int n, const std::function<void(int)>& f) {
-    std::call_once(pool_once, [this] {
-      const unsigned hc = std::thread::hardware_concurrency();
-      pool.start(int(std::min<unsigned>(15, hc > 1 ? hc - 1 : 1)));  // + the caller: 16 (the box's CPU share)
-    });
-    pool.run(n, f);
-  }
-  int device = 0;
-  int num_cus = 256;
-  hipStream_t stream = nullptr;
-  hipStream_t side = nullptr;  // batched queries: argument uploads + bitmap programs run ahead of the query kernels
-  std::mutex mu;
-  // Pinned host blocks for the per-query argument arena (one H2D copy per query) and result read-back.
-  std::multimap<size_t, void*> pinned_free;
-  std::unordered_map<void*, size_t> pinned_live;
-
-  void* pinned_alloc(size_t bytes) {
-    bytes = std::max<size_t>(4096, (bytes + 4095) & ~size_t(4095));
-    std::lock_guard<std::mutex> g(mu);
-    auto it = pinned_free.lower_bound(bytes);
-    if (it != pinned_free.end() && it->first <= bytes * 4) {
-      void* p = it->second;
-      pinned_live[p] = it->first;
-      pinned_free.erase(it);
-      return p;
-    }
-    void* p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) fail(PGX_ERR_OOM, "hipHostMalloc failed");
-    pinned_live[p] = bytes;
-    return p;
-  }
-  void pinned_release(void* p) {
-    if (!p) return;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = pinned_live.find(p);
-    if (it == pinned_live.end()) return;
-    pinned_free.emplace(it->second, p);
-    pinned_live.erase(it);
-  }
-  // Simple size-bucketed device memory pool (avoids hipMalloc/hipFree on the query path).
-  std::multimap<size_t, void*> free_blocks;
-  std::unordered_map<void*, size_t> live;
-
-  void* alloc(size_t bytes) {
-    bytes = std::max<size_t>(256, (bytes + 255) & ~size_t(255));
-    std::lock_guard<std::mutex> g(mu);
-    auto it = free_blocks.lower_bound(bytes);
-    if (it != free_blocks.end() && it->first <= bytes * 2) {
-      void* p = it->second;
-      live[p] = it->first;
-      free_blocks.erase(it);
-      return p;
-    }
-    void* p = nullptr;
-    hipError_t e = hipMalloc(&p, bytes);
-    if (e != hipSuccess) {
-      // release cached blocks and retry once
-      for (auto& kv : free_blocks) (void)hipFree(kv.second);
-      free_blocks.clear();
-      e = hipMalloc(&p, bytes);
-      if (e != hipSuccess) fail(PGX_ERR_OOM, "hipMalloc(" + std::to_string(bytes) + ") failed");
-    }
-    live[p] = bytes;
-    return p;
-  }
-  void release(void* p) {
-    if (!p) return;
-    std::lock_guard<std::mutex> g(mu);
-    auto it = live.find(p);
-    if (it == live.end()) return;
-    free_blocks.emplace(it->second, p);
-    live.erase(it);
-  }
-};
-
-struct PinnedBuf {
-  pgx_ctx* ctx = nullptr;
-  void* p = nullptr;
-  PinnedBuf() = default;
-  PinnedBuf(pgx_ctx* c, size_t n) : ctx(c), p(c->pinned_alloc(n)) {}
-  PinnedBuf(const PinnedBuf&) = delete;
-  PinnedBuf& operator=(const PinnedBuf&) = delete;
-  PinnedBuf(PinnedBuf&& o) noexcept : ctx(o.ctx), p(o.p) { o.p = nullptr; }
-  PinnedBuf& operator=(PinnedBuf&& o) noexcept {
-    reset();
-    ctx = o.ctx;
-    p = o.p;
-    o.p = nullptr;
-    return *this;
-  }
-  ~PinnedBuf() { reset(); }
-  void reset() {
-    if (p && ctx) ctx->pinned_release(p);
-    p = nullptr;
-  }
-  uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
-};
-
-struct DevBuf {
-  pgx_ctx* ctx = nullptr;
-  void* p = nullptr;
-  DevBuf() = default;
-  DevBuf(pgx_ctx* c, size_t n) : ctx(c), p(c->alloc(n)) {}
-  DevBuf(const DevBuf&) = delete;
-  DevBuf& operator=(const DevBuf&) = delete;
-  DevBuf(DevBuf&& o) noexcept : ctx(o.ctx), p(o.p) { o.p = nullptr; }
-  DevBuf& operator=(DevBuf&& o) noexcept {
-    reset();
-    ctx = o.ctx;
-    p = o.p;
-    o.p = nullptr;
-    return *this;
-  }
-  ~DevBuf() { reset(); }
-  void reset() {
-    if (p && ctx) ctx->release(p);
-    p = nullptr;
-  }
-  template <typename T>
-  T* as() const { return static_cast<T*>(p); }
-};
-
-struct SharedDict {
-  int data_type = 0;
-  std::vector<uint64_t> enc;  // int64 / double bits per dictId (the device copy's content)
-  DevBuf dict;
-  DevBuf img;
-  int img_kind = 0, img_sh = 0, img_words = 0;
-  int64_t vbase = 0;
-  uint64_t vrange = 0;
-};
-
-// =================================================================================================
-// Segments
-// =================================================================================================
-struct StagedColumn {
-  std::string name;
-  int data_type = 0;
-  int card = 0;
-  int bits = 0;
-  bool is_sorted = false;
-  int dict_width = 0;
-  bool has_inverted = false;
-  // device
-  const uint32_t* fwd = nullptr;  // packed fixed-bit (padded)
-  DevBuf fwd_owned;
-  const void* dict_dev = nullptr;  // int64 / double values per dictId (shared->dict)
-  std::shared_ptr<SharedDict> shared;  // the context-wide copy of this dictionary and its value image
-  // host
-  std::vector<int32_t> sorted_first, sorted_last;  // sorted columns: inclusive doc range per dictId
-  std::vector<int64_t> ivals;                      // numeric dictionary values (INT/LONG)
-  std::vector<double> dvals;                       // FLOAT/DOUBLE dictionary values
-  std::vector<std::string> svals;                  // STRING dictionary values (unpadded)
-  int pad_char = 0;                                // STRING padding byte
-  uint64_t dict_hash = 0;
-  std::vector<uint8_t> inv;                        // bitmap inverted index bytes (host)
-  std::vector<uint32_t> inv_off;                   // (card+1) byte offsets of the per-dictId roaring bitmaps
-  DevBuf inv_dev;                                  // device copy (expanded by pgx_roaring_expand); null if unusable
-  // LDS value image (pgx_jit.cpp): the dictionary re-encoded so a whole column's values fit one workgroup's LDS
-  int img_kind = IMG_NONE;
-  int img_sh = 0;
-  int img_words = 0;
-  int64_t vbase = 0;       // integer images hold value - vbase
-  uint64_t vrange = 0;     // max(value) - vbase
-  const void* img_dev = nullptr;  // shared->img
-  // multi-value columns (<col>.mv.fwd): fwd holds the raw value section; doc d owns values [mv_start[d], mv_start[d+1])
-  bool is_mv = false;
-  int64_t total_entries = 0;
-  DevBuf mv_start;
-  int max_mv = 0;
-};
-
-std::atomic<uint64_t> g_segment_uid{1};
-std::atomic<uint64_t> g_segment_frees{0};  // segments freed so far: a plan-cache entry whose segment pointers match
-                                           // and no segment was freed since it was kept needs no uid comparison
-
-struct pgx_segment {
-  pgx_ctx* ctx = nullptr;
-  uint64_t uid = g_segment_uid.fetch_add(1);  // never reused: keys the plan cache (a freed address may be reused)
-  std::string name;
-  int32_t total_docs = 0, total_raw_docs = 0;
-  std::vector<StagedColumn> cols;
-  std::unordered_map<std::string, int> by_name;
-  std::vector<uint8_t> star_tree;
-  // OFF_HEAP star tree (core/startree/StarTreeOffHeap.java:95-150, StarTreeIndexNodeOffHeap.java): BFS nodes of
-  // {dimName, dimValue, startDoc, endDoc (exclusive), aggDocId, childStart, childEnd}, children sorted by value.
-  struct StarNode { int32_t dim, value, start, end, agg, cbeg, cend; };
-  bool st_ok = false;
-  std::vector<StarNode> st_nodes;
-  std::vector<std::string> st_dim_name;          // dimension index -> column name
-  std::vector<std::string> st_skip;              // star.tree.skip.materialization.for.dimensions
-  uint64_t device_bytes = 0;
-
-  std::vector<std::string> names;  // column names, contiguous: planning looks columns up per segment and query column
-  const StagedColumn& col(const std::string& n) const {
-    if (names.size() <= 24) {  // a short scan over one or two cache lines beats hashing the name
-      for (size_t i = 0; i < names.size(); ++i)
-        if (names[i].size() == n.size() && std::memcmp(names[i].data(), n.data(), n.size()) == 0) return cols[i];
-      fail(PGX_ERR_INVALID_ARG, "segment " + name + " has no column " + n);
-    }
-    auto it = by_name.find(n);
-    if (it == by_name.end()) fail(PGX_ERR_INVALID_ARG, "segment " + name + " has no column " + n);
-    return cols[it->second];
-  }
-};
-
-namespace {
-
-// Re-encode a numeric dictionary into an LDS image (DESIGN.md "LDS value images"): the sum of a column over a scan
-// is a per-row dictionary lookup (ImmutableDictionaryReader.readValues), which from HBM/L2 is a random 8-byte gather
-// per row.  The image makes it an LDS read.  INT/LONG: u32 (value - min) when the card fits 144 KiB, else 64 block
-// bases + u16 offsets (frame of reference; exact, checked per block).  FLOAT/DOUBLE: doubles when they fit.
-void build_value_image(pgx_ctx* ctx, StagedColumn& c, SharedDict& sd) {
-  const int64_t card = c.card;
-  const int64_t kMax = 144 * 1024;
-  std::vector<uint32_t> img;
-  if (c.data_type == PGX_INT || c.data_type == PGX_LONG) {
-    const int64_t vmin = *std::min_element(c.ivals.begin(), c.ivals.end());
-    const int64_t vmax = *std::max_element(c.ivals.begin(), c.ivals.end());
-    const uint64_t range = uint64_t(vmax) - uint64_t(vmin);
-    if (range > 0xFFFFFFFFull) return;
-    c.vbase = vmin;
-    c.vrange = range;
-    if (card * 4 <= kMax) {
-      img.resize(card);
-      for (int64_t i = 0; i < card; ++i) img[i] = uint32_t(uint64_t(c.ivals[i]) - uint64_t(vmin));
-      c.img_kind = IMG_U32;
-    } else if (card * 2 + 4 * kImgFor16Blocks <= kMax) {
-      int sh = 0;
-      while ((card + (int64_t(1) << sh) - 1) >> sh > 32) ++sh;  // <= 32 blocks: base reads are bank-conflict free
-      bool ok = false;
-      std::vector<uint32_t> base;
-      for (int tries = 0; tries < 2 && !ok; ++tries, --sh) {
-        if (sh < 0 || ((card + (int64_t(1) << sh) - 1) >> sh) > kImgFor16Blocks) break;
-        const int64_t nblk = (card + (int64_t(1) << sh) - 1) >> sh;
-        base.assign(kImgFor16Blocks, 0);
-        ok = true;
-        for (int64_t b = 0; b < nblk && ok; ++b) {
-          uint64_t lo = ~0ull, hi = 0;
-          for (int64_t i = b << sh; i < std::min(card, (b + 1) << sh); ++i) {
-            const uint64_t x = uint64_t(c.ivals[i]) - uint64_t(vmin);
-            lo = std::min(lo, x);
-            hi = std::max(hi, x);
-          }
-          if (hi - lo > 0xFFFF) ok = false;
-          base[b] = uint32_t(lo);
-        }
-        if (ok) c.img_sh = sh;
-      }
-      if (!ok) return;
-      img.assign(kImgFor16Blocks + (card + 1) / 2, 0);
-      std::copy(base.begin(), base.end(), img.begin());
-      uint16_t* off = reinterpret_cast<uint16_t*>(img.data() + kImgFor16Blocks);
-      for (int64_t i = 0; i < card; ++i)
-        off[i] = uint16_t(uint64_t(c.ivals[i]) - uint64_t(vmin) - base[i >> c.img_sh]);
-      c.img_kind = IMG_FOR16;
-    } else {
-      return;
-    }
-  } else if (c.data_type == PGX_FLOAT || c.data_type == PGX_DOUBLE) {
-    if (card * 8 > kMax) return;
-    img.resize(card * 2);
-    std::memcpy(img.data(), c.dvals.data(), card * 8);
-    c.img_kind = IMG_F64;
-  } else {
-    return;
-  }
-  c.img_words = int(img.size());
-  img.resize((img.size() + 3) & ~size_t(3), 0);  // whole 16-B chunks for the LDS staging copy
-  sd.img = DevBuf(ctx, img.size() * 4);
-  hip_check(hipMemcpy(sd.img.p, img.data(), img.size() * 4, hipMemcpyHostToDevice), "image H2D");
-}
-
-// StarTreeSerDe.writeTreeOffHeapFormat (core/startree/StarTreeSerDe.java:183-328), native (LE) byte order: u64 magic,
-// i32 version, i32 header size, i32 #dims, #dims x {i32 index, i32 len, bytes}, i32 #nodes, #nodes x 7 x i32.
-// Other star-tree formats (the Java-serialised ON_HEAP tree) leave st_ok false: queries then scan the raw docs.
-void parse_star_tree(pgx_segment& seg) {
-  const std::vector<uint8_t>& b = seg.star_tree;
-  auto rd32 = [&](size_t o) {
-    if (o + 4 > b.size()) fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": star tree truncated");
-    int32_t x;
-    std::memcpy(&x, &b[o], 4);
-    return x;
-  };
-  if (b.size() < 24) return;
-  uint64_t magic;
-  std::memcpy(&magic, b.data(), 8);
-  if (magic != 0xBADDA55B00DAD00Dull) return;
-  size_t o = 16;
-  const int nd = rd32(o);
-  o += 4;
-  if (nd < 0 || nd > 4096) fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": bad star tree header");
-  seg.st_dim_name.assign(nd, "");
-  for (int i = 0; i < nd; ++i) {
-    const int idx = rd32(o), len = rd32(o + 4);
-    if (idx < 0 || idx >= nd || len < 0 || o + 8 + size_t(len) > b.size())
-      fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": bad star tree dimension map");
-    seg.st_dim_name[idx].assign(reinterpret_cast<const char*>(&b[o + 8]), size_t(len));
-    o += 8 + size_t(len);
-  }
-  const int nn = rd32(o);
-  o += 4;
-  if (nn < 1 || o + size_t(nn) * 28 > b.size()) fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": bad star tree");
-  seg.st_nodes.resize(nn);
-  std::memcpy(seg.st_nodes.data(), &b[o], size_t(nn) * 28);
-  for (const auto& x : seg.st_nodes)
-    if ((x.cbeg != -1 && (x.cbeg < 1 || x.cend < x.cbeg || x.cend >= nn)) || x.dim >= nd)
-      fail(PGX_ERR_INVALID_ARG, "segment " + seg.name + ": star tree node out of range");
-  seg.st_ok = true;
-}
-
-void stage_dict(pgx_ctx* ctx, pgx_segment* seg, const std::vector<uint8_t>& dict_host, StagedColumn& c);
-void stage_forward(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c,
-                   int64_t n, uint64_t need);
-
-void stage_column(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c) {
-  c.name = d.name ? d.name : "";
-  c.data_type = d.data_type;
-  c.card = d.cardinality;
-  c.bits = d.bits_per_element;
-  c.is_sorted = d.is_sorted != 0;
-  c.dict_width = d.dict_width;
-  c.pad_char = d.pad_char & 0xFF;
-  if (c.card < 1) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": cardinality < 1");
-  if (c.bits < 1 || c.bits > 32) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": bitsPerElement out of [1,32]");
-  if (c.card > 1 && (c.bits < 32) && (int64_t(c.card) - 1) >> c.bits)
-    fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": cardinality does not fit bitsPerElement");
-  const int64_t n = seg->total_docs;
-  const uint64_t need = padded_fwd_bytes(n, c.bits);
-
-  // ---- dictionary (host copy always; device copy for numeric columns) ----
-  std::vector<uint8_t> dict_host;
-  if (device_mem) {
-    dict_host.resize(d.dict_len);
-    if (d.dict_len) hip_check(hipMemcpy(dict_host.data(), d.dict, d.dict_len, hipMemcpyDeviceToHost), "dict D2H");
-  } else {
-    const uint8_t* p = static_cast<const uint8_t*>(d.dict);
-    dict_host.assign(p, p + d.dict_len);
-  }
-  stage_dict(ctx, seg, dict_host, c);
-  stage_forward(ctx, seg, d, device_mem, c, n, need);
-}
-
-// The v1 dictionary bytes of column c (c.name / data_type / card / dict_width / pad_char set): host values, the
-// context-wide shared device copy and value image (SharedDict).
-void stage_dict(pgx_ctx* ctx, pgx_segment* seg, const std::vector<uint8_t>& dict_host, StagedColumn& c) {
-  const int width = (c.data_type == PGX_INT || c.data_type == PGX_FLOAT) ? 4
-                    : (c.data_type == PGX_STRING)                          ? c.dict_width
-                                                                           : 8;
-  if (width <= 0 || dict_host.size() < uint64_t(width) * c.card)
-    fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": dictionary too short");
-  c.dict_hash = fnv1a(dict_host.data(), uint64_t(width) * c.card, fnv1a(&c.data_type, sizeof(int)));
-  if (c.data_type == PGX_STRING) {
-    c.svals.resize(c.card);
-    for (int i = 0; i < c.card; ++i) {
-      const char* s = reinterpret_cast<const char*>(dict_host.data()) + size_t(i) * width;
-      size_t len = width;
-      // StringDictionary.get: truncate at the first padding char (metadata; '\0' default, '%' legacy)
-      for (size_t k = 0; k < size_t(width); ++k)
-        if (s[k] == char(c.pad_char)) { len = k; break; }
-      c.svals[i].assign(s, len);
-    }
-  } else {
-    std::vector<uint64_t> enc(c.card);
-    if (c.data_type == PGX_INT || c.data_type == PGX_LONG) {
-      c.ivals.resize(c.card);
-      for (int i = 0; i < c.card; ++i) {
-        int64_t v = (c.data_type == PGX_INT) ? int64_t(int32_t(be32(&dict_host[size_t(i) * 4])))
-                                             : int64_t(be64(&dict_host[size_t(i) * 8]));
-        c.ivals[i] = v;
-        enc[i] = uint64_t(v);
-      }
-    } else {
-      c.dvals.resize(c.card);
-      for (int i = 0; i < c.card; ++i) {
-        double v;
-        if (c.data_type == PGX_FLOAT) {
-          uint32_t b = be32(&dict_host[size_t(i) * 4]);
-          float f;
-          std::memcpy(&f, &b, 4);
-          v = double(f);  // (double) widening as FloatDictionary.getDoubleValue
-        } else {
-          uint64_t b = be64(&dict_host[size_t(i) * 8]);
-          std::memcpy(&v, &b, 8);
-        }
-        c.dvals[i] = v;
-        std::memcpy(&enc[i], &v, 8);
-      }
-    }
-    std::lock_guard<std::mutex> g(ctx->dict_mu);
-    auto& slot = ctx->dicts[c.dict_hash];
-    std::shared_ptr<SharedDict> sd = slot.lock();
-    if (sd && (sd->data_type != c.data_type || sd->enc != enc)) sd = nullptr;  // hash collision: a private copy
-    if (!sd) {
-      sd = std::make_shared<SharedDict>();
-      sd->data_type = c.data_type;
-      sd->dict = DevBuf(ctx, enc.size() * 8);
-      hip_check(hipMemcpy(sd->dict.p, enc.data(), enc.size() * 8, hipMemcpyHostToDevice), "dict H2D");
-      build_value_image(ctx, c, *sd);
-      sd->img_kind = c.img_kind;
-      sd->img_sh = c.img_sh;
-      sd->img_words = c.img_words;
-      sd->vbase = c.vbase;
-      sd->vrange = c.vrange;
-      sd->enc = std::move(enc);
-      if (!slot.lock()) slot = sd;
-      seg->device_bytes += sd->enc.size() * 8 + (sd->img.p ? size_t(sd->img_words) * 4 : 0);
-    } else {
-      c.img_kind = sd->img_kind;
-      c.img_sh = sd->img_sh;
-      c.img_words = sd->img_words;
-      c.vbase = sd->vbase;
-      c.vrange = sd->vrange;
-    }
-    c.shared = sd;
-    c.dict_dev = sd->dict.p;
-    c.img_dev = sd->img.p;
-  }
-}
-
-void stage_forward(pgx_ctx* ctx, pgx_segment* seg, const pgx_column_desc& d, bool device_mem, StagedColumn& c,
-                   int64_t n, uint64_t need) {
-  if (d.is_multi_value) {
-    // FixedBitMultiValueWriter / FixedBitMultiValueReader (io/*/impl/v1/FixedBitMultiValue*.java): numChunks BE int
-    // chunk offsets, a totalNumValues-bit MSB-first bitset marking every doc's first value, then the values fixed-bit.
-    // docsPerChunk = ceil(2048 / (float)(totalNumValues / numDocs)) with the integer division of the reference.
-    c.is_mv = true;
-    c.is_sorted = false;
-    const int64_t tv = d.total_entries;
-    if (tv < n || n < 1) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": totalNumberOfEntries < docs");
-    c.total_entries = tv;
-    const float avg = float(tv / n);
-    const int64_t dpc = int64_t(std::ceil(2048.0f / avg));
-    const int64_t nchunks = (n + dpc - 1) / dpc;
-    const uint64_t head = uint64_t(nchunks) * 4, bs = uint64_t(tv + 7) / 8, raw = (uint64_t(tv) * c.bits + 7) / 8;
-    if (d.fwd_len < head + bs + raw) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": multi-value index short");
-    std::vector<uint8_t> f(head + bs + raw);
-    if (device_mem) hip_check(hipMemcpy(f.data(), d.fwd, f.size(), hipMemcpyDeviceToHost), "mv fwd D2H");
-    else std::memcpy(f.data(), d.fwd, f.size());
-    std::vector<int32_t> start;
-    start.reserve(size_t(n) + 1);
-    for (int64_t i = 0; i < tv; ++i)
-      if ((f[head + size_t(i >> 3)] >> (7 - (i & 7))) & 1u) start.push_back(int32_t(i));
-    if (int64_t(start.size()) != n || start[0] != 0)
-      fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": multi-value doc bitset does not mark one start per doc");
-    for (int64_t k = 0; k < nchunks; ++k)
-      if (int64_t(be32(&f[size_t(k) * 4])) != start[size_t(k * dpc)])
-        fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": multi-value chunk offset mismatch");
-    start.push_back(int32_t(tv));
-    for (int64_t dd = 0; dd < n; ++dd) c.max_mv = std::max<int>(c.max_mv, start[dd + 1] - start[dd]);
-    c.mv_start = DevBuf(ctx, start.size() * 4);
-    hip_check(hipMemcpy(c.mv_start.p, start.data(), start.size() * 4, hipMemcpyHostToDevice), "mv starts H2D");
-    const uint64_t vneed = padded_fwd_bytes(tv, c.bits);
-    c.fwd_owned = DevBuf(ctx, vneed);
-    hip_check(hipMemset(c.fwd_owned.p, 0, vneed), "memset");
-    hip_check(hipMemcpy(c.fwd_owned.p, f.data() + head + bs, raw, hipMemcpyHostToDevice), "mv values H2D");
-    c.fwd = c.fwd_owned.as<const uint32_t>();
-    seg->device_bytes += vneed + start.size() * 4;
-  } else if (c.is_sorted) {
-    // Sorted SV column: card x (start,end) BE int pairs (SortedForwardIndexReader / SortedInvertedIndexReader).
-    std::vector<uint8_t> pairs(d.sorted_len);
-    if (d.sorted_len < uint64_t(c.card) * 8) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": sorted index short");
-    if (device_mem) hip_check(hipMemcpy(pairs.data(), d.sorted_pairs, d.sorted_len, hipMemcpyDeviceToHost), "D2H");
-    else std::memcpy(pairs.data(), d.sorted_pairs, d.sorted_len);
-    c.sorted_first.resize(c.card);
-    c.sorted_last.resize(c.card);
-    for (int i = 0; i < c.card; ++i) {
-      c.sorted_first[i] = int32_t(be32(&pairs[size_t(i) * 8]));
-      c.sorted_last[i] = int32_t(be32(&pairs[size_t(i) * 8 + 4]));
-    }
-    // Materialise a packed fixed-bit view on device so group-by / value reads use the same unpack path.
-    std::vector<uint8_t> packed(need, 0);
-    for (int id = 0; id < c.card; ++id) {
-      for (int64_t r = std::max<int32_t>(0, c.sorted_first[id]); r <= c.sorted_last[id] && r < n; ++r) {
-        const int64_t bit0 = r * c.bits;
-        for (int k = 0; k < c.bits; ++k) {
-          if ((uint32_t(id) >> (c.bits - 1 - k)) & 1u) {
-            const int64_t bit = bit0 + k;
-            packed[bit >> 3] |= uint8_t(0x80u >> (bit & 7));
-          }
-        }
-      }
-    }
-    c.fwd_owned = DevBuf(ctx, need);
-    hip_check(hipMemcpy(c.fwd_owned.p, packed.data(), need, hipMemcpyHostToDevice), "fwd H2D");
-    c.fwd = c.fwd_owned.as<const uint32_t>();
-    seg->device_bytes += need;
-  } else {
-    const uint64_t file_bytes = (uint64_t(n) * c.bits + 7) / 8;
-    if (d.fwd_len < file_bytes) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": forward index short");
-    if (device_mem && d.fwd_len >= need && (reinterpret_cast<uintptr_t>(d.fwd) & 15) == 0) {
-      c.fwd = static_cast<const uint32_t*>(d.fwd);  // referenced in place (caller keeps it alive)
-    } else {
-      c.fwd_owned = DevBuf(ctx, need);
-      hip_check(hipMemset(c.fwd_owned.p, 0, need), "memset");
-      hip_check(hipMemcpy(c.fwd_owned.p, d.fwd, file_bytes, device_mem ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice),
-                "fwd copy");
-      c.fwd = c.fwd_owned.as<const uint32_t>();
-      seg->device_bytes += need;
-    }
-  }
-  if (d.inv && d.inv_len) {
-    // <col>.bitmap.inv: (card+1) BE int offsets, then concatenated portable roaring bitmaps
-    // (segment/creator/impl/inv/HeapBitmapInvertedIndexCreator.java:74-81, BitmapInvertedIndexReader.java:91-117)
-    const uint8_t* p = static_cast<const uint8_t*>(d.inv);
-    c.inv.assign(p, p + d.inv_len);
-    c.has_inverted = true;
-    if (d.inv_len < uint64_t(c.card + 1) * 4) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": inverted index short");
-    c.inv_off.resize(c.card + 1);
-    bool device_ok = true;
-    for (int i = 0; i <= c.card; ++i) {
-      c.inv_off[i] = be32(p + 4 * size_t(i));
-      if (c.inv_off[i] > d.inv_len || (i && c.inv_off[i] < c.inv_off[i - 1]))
-        fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": inverted index offsets out of order");
-      // The device expansion reads RoaringBitmap 0.5.10's portable no-run format (cookie 12346), all the reference
-      // writes (no runOptimize); anything else keeps this column on the dictId-bitset scan path.
-      if (i < c.card) {
-        const uint32_t o = c.inv_off[i];
-        if ((o & 1u) || uint64_t(o) + 8 > d.inv_len) device_ok = false;
-        else if ((uint32_t(p[o]) | uint32_t(p[o + 1]) << 8 | uint32_t(p[o + 2]) << 16 | uint32_t(p[o + 3]) << 24) != 12346u)
-          device_ok = false;
-      }
-    }
-    if (device_ok) {
-      c.inv_dev = DevBuf(ctx, d.inv_len + 16);
-      hip_check(hipMemcpy(c.inv_dev.p, p, d.inv_len, hipMemcpyHostToDevice), "inverted index H2D");
-      seg->device_bytes += d.inv_len;
-    }
-  }
-  if (c.is_sorted) c.has_inverted = true;  // ColumnDataSourceImpl: sorted columns report an inverted index
-}
-
-}  // namespace
-
-// =================================================================================================
-// Query
-// =================================================================================================
-// A caller-given key space for one group-by column (pgx_query_set_key_domain): the sorted distinct values of the column
-// over every process's segments, so that every rank plans the same dense slots / packed keys.
-struct KeyDomain {
-  bool set = false;
-  int type = PGX_INT;                 // PGX_INT / PGX_LONG -> iv, PGX_FLOAT / PGX_DOUBLE -> dv, PGX_STRING -> sv
-  std::vector<int64_t> iv;
-  std::vector<double> dv;
-  std::vector<std::string> sv;
-  int64_t size() const { return type == PGX_STRING ? int64_t(sv.size()) : (iv.empty() ? int64_t(dv.size()) : int64_t(iv.size())); }
-};
-
-struct pgx_query {
-  std::vector<int> agg_fn;
-  std::vector<std::string> agg_col;  // "" for COUNT(*)
-  std::vector<std::string> group_cols;
-  int top_n = 10;
-  std::vector<pgx_filter_node> filter;
-  std::vector<std::string> leaf_col;
-  std::vector<int> leaf_kind;
-  uint32_t flags = 0;
-  std::vector<KeyDomain> key_domain;  // [group column]
-  Knobs kn;                           // the PGX_* environment when the query was compiled (read_knobs)
-};
-
-// =================================================================================================
-// Result
-// =================================================================================================
-struct pgx_bindings {
-  std::vector<pgx_leaf_binding> arr;
-  std::vector<std::vector<uint32_t>> words;  // owned bitsets (arr[i].words points into these)
-};
-
-// pgx_execute_async: the query runs on a worker thread of the library's pool (planning, the launches on the context's
-// stream, the read-back); the submitting thread returns at once.  The inputs the caller owns only for the duration of
-// the call (the segment list, the bindings and their bitsets, the options) are copied here first.  The pool's threads
-// live for the whole process (a thread per query cost ~20-40 us of creation and join per query: C1-sized queries).
-struct AsyncState {
-  std::mutex m;
-  std::condition_variable cv;
-  bool done = false;
-  pgx_status status = PGX_OK;
-  std::string msg;
-  std::vector<pgx_segment*> segs;
-  std::vector<pgx_leaf_binding> binds;
-  std::vector<std::vector<uint32_t>> words;
-  pgx_exec_opts opts{};
-  bool has_opts = false;
-  void join() {  // until the worker has finished with this state
-    std::unique_lock<std::mutex> g(m);
-    cv.wait(g, [&] { return done; });
-  }
-  ~AsyncState() { join(); }
-};
-
-class AsyncPool {
- public:
-  static AsyncPool& get() {
-    static AsyncPool* p = new AsyncPool(kThreads);  // never destroyed: workers may be blocked at process exit
-    return *p;
-  }
-  void submit(std::function<void()> f) {
-    {
-      std::lock_guard<std::mutex> g(m_);
-      q_.push_back(std::move(f));
-    }
-    cv_.notify_one();
-  }
-
- private:
-  static constexpr int kThreads = 8;  // queries in flight per process (bench: 3; one per device under execute_multi)
-  explicit AsyncPool(int n) {
-    for (int i = 0; i < n; ++i) std::thread([this] { loop(); }).detach();
-  }
-  void loop() {
-    for (;;) {
-      std::function<void()> f;
-      {
-        std::unique_lock<std::mutex> g(m_);
-        cv_.wait(g, [&] { return !q_.empty(); });
-        f = std::move(q_.front());
-        q_.pop_front();
-      }
-      f();
-    }
-  }
-  std::mutex m_;
-  std::condition_variable cv_;
-  std::deque<std::function<void()>> q_;
-};
-
-struct pgx_result {
-  int64_t stats[4] = {0, 0, 0, 0};
-  int num_aggs = 0;
-  std::vector<int> agg_fn;
-  bool group_by = false;
-  int top_n = 10;
-  int mode = 0;
-  // aggregation-only
-  std::vector<double> agg_value;
-  std::vector<int64_t> agg_count;
-  // group-by (columnar)
-  int64_t num_groups = 0;
-  std::vector<std::vector<int32_t>> key_seg, key_id;  // [col][group]
-  std::vector<std::vector<double>> g_value;          // [fn][group]
-  std::vector<std::vector<int64_t>> g_count;         // [fn][group]
-  // Partitioned group-by (run_partitioned): the groups stay in device memory until an accessor needs them.
-  struct Lazy {
-    pgx_ctx* ctx = nullptr;      // holds a context reference (the result may outlive the caller's handle)
-    DevBuf okey, oplane;         // packed keys; planes [count, sum, min, max] x ocap
-    DevBuf prange;               // trim-key ranges per kind (pgx_narrow_aggregate), or none: the trim's range pass
-    int64_t ocap = 0;
-    std::vector<int> gshift, gbits;
-    using Reps = std::shared_ptr<const std::vector<std::vector<int32_t>>>;
-    Reps rep_seg, rep_id;  // [col][global id] (shared with a kept plan: every replay's result reads the same tables)
-    std::vector<int> agg_kind;
-    std::vector<std::vector<int64_t>> trims;  // per function: the device-selected trim, best first
-    int64_t trim_size = 0;                    // the size those selections were made for
-    ~Lazy() {
-      okey.reset();
-      oplane.reset();
-      prange.reset();
-      if (ctx) ctx_unref(ctx);
-    }
-  };
-  std::unique_ptr<Lazy> lazy;
-  std::unique_ptr<AsyncState> async;  // declared last: destroyed (joined) before the fields its thread writes
-  void ready() const;                 // waits for an async execution; throws its error
-  void materialize();
-  const std::vector<int64_t>& device_trim(int fn, int64_t size);
-  void decode_lazy(const uint64_t* keys, const uint64_t* planes, int64_t n, int64_t out_stride, int32_t* seg_index,
-                   int32_t* dict_id, double* value, int64_t* count) const;
-};
-
-namespace {
-
-// ----- physical filter plan (FilterPlanNode.constructPhysicalOperator + reorder, plan/FilterPlanNode.java:77-170) -----
-enum PhysKind { PH_SORTED = 0, PH_AND = 1, PH_BITMAP = 2, PH_SCAN = 3, PH_OR = 4 };
-
-struct PNode {
-  int op;  // PGX_F_LEAF / AND / OR
-  int leaf = -1;
-  int phys = PH_SCAN;
-  std::vector<PNode> kids;
-};
-
-PNode build_tree(const pgx_query& q, const pgx_segment& seg0) {
-  std::vector<PNode> st;
-  for (const auto& n : q.filter) {
-    if (n.op == PGX_F_LEAF) {
-      if (n.arg < 0 || n.arg >= int(q.leaf_col.size())) fail(PGX_ERR_INVALID_ARG, "filter leaf index out of range");
-      PNode p;
-      p.op = PGX_F_LEAF;
-      p.leaf = n.arg;
-      const StagedColumn& c = seg0.col(q.leaf_col[n.arg]);
-      if (c.has_inverted && q.leaf_kind[n.arg] != PGX_PRED_RANGE) p.phys = c.is_sorted ? PH_SORTED : PH_BITMAP;
-      else p.phys = PH_SCAN;
-      st.push_back(std::move(p));
-    } else if (n.op == PGX_F_AND || n.op == PGX_F_OR) {
-      if (n.arg < 1 || n.arg > int(st.size())) fail(PGX_ERR_INVALID_ARG, "filter node arity");
-      PNode p;
-      p.op = n.op;
-      p.phys = n.op == PGX_F_AND ? PH_AND : PH_OR;
-      p.kids.assign(std::make_move_iterator(st.end() - n.arg), std::make_move_iterator(st.end()));
-      st.erase(st.end() - n.arg, st.end());
-      std::stable_sort(p.kids.begin(), p.kids.end(), [](const PNode& a, const PNode& b) { return a.phys < b.phys; });
-      st.push_back(std::move(p));
-    } else {
-      fail(PGX_ERR_INVALID_ARG, "bad filter op");
-    }
-  }
-  if (st.size() != 1) fail(PGX_ERR_INVALID_ARG, "filter postfix does not reduce to one tree");
-  return std::move(st.back());
-}
-
-// Emit the device program.  Evaluation order follows AndBlockDocIdSet.fastIterator (operator/docidsets/
-// AndBlockDocIdSet.java:146-229): sorted ranges and bitmaps first, then every scan child tested against the running
-// candidate set (applyAnd) -- an OP_STAT before each scan child records numEntriesScannedInFilter.  host_scan_leaves
-// counts scan leaves whose entries equal the whole scan range (a root scan leaf; scan children of a root OR, which
-// OrDocIdIterator advances doc by doc, operator/dociditerators/OrDocIdIterator.java:100-139).
-void emit(const PNode& n, std::vector<int8_t>& op, std::vector<int8_t>& arg, bool root, bool stats_inside,
-          int& host_scan_leaves) {
-  if (n.op == PGX_F_LEAF) {
-    op.push_back(OP_LEAF);
-    arg.push_back(int8_t(n.leaf));
-    if (root && n.phys == PH_SCAN) host_scan_leaves += 1;
-    return;
-  }
-  if (n.op == PGX_F_OR) {
-    for (size_t i = 0; i < n.kids.size(); ++i) {
-      const PNode& k = n.kids[i];
-      if (root && k.op == PGX_F_LEAF && k.phys == PH_SCAN) host_scan_leaves += 1;
-      emit(k, op, arg, false, false, host_scan_leaves);
-      if (i > 0) { op.push_back(OP_OR); arg.push_back(2); }
-    }
-    return;
-  }
-  // AND: index-based children first, then scans with statistics, then nested operators.
-  int pushed = 0;
-  auto fold = [&]() {
-    if (pushed > 1) { op.push_back(OP_AND); arg.push_back(2); }
-  };
-  for (const PNode& k : n.kids)
-    if (k.op == PGX_F_LEAF && (k.phys == PH_SORTED || k.phys == PH_BITMAP)) {
-      emit(k, op, arg, false, false, host_scan_leaves);
-      ++pushed;
-      fold();
-    }
-  const bool fast = pushed > 0;
-  for (const PNode& k : n.kids)
-    if (k.op == PGX_F_LEAF && k.phys == PH_SCAN) {
-      if (fast || pushed > 0) { op.push_back(OP_STAT); arg.push_back(0); }
-      else if (root) host_scan_leaves += 1;  // first scan of an all-scan AND walks the whole range
-      emit(k, op, arg, false, false, host_scan_leaves);
-      ++pushed;
-      fold();
-    }
-  for (const PNode& k : n.kids)
-    if (k.op != PGX_F_LEAF) {
-      emit(k, op, arg, false, stats_inside, host_scan_leaves);
-      ++pushed;
-      fold();
-    }
-}
-
-unsigned long long* devp(const DevBuf& b) { return b.as<unsigned long long>(); }
-
-double decode_plane(int op, bool fp, unsigned long long x, int fn) {
-  if (op == P_ADD_I64) return double(int64_t(x));
-  if (op == P_ADD_F64) {
-    double d;
-    std::memcpy(&d, &x, 8);
-    return d;
-  }
-  // ordered min/max
-  if (op == P_MIN_ORD && x == ~0ull) return std::numeric_limits<double>::infinity();
-  if (op == P_MAX_ORD && x == 0ull) return -std::numeric_limits<double>::infinity();
-  if (!fp) return double(int64_t(x ^ 0x8000000000000000ull));
-  uint64_t b = (x & 0x8000000000000000ull) ? (x & ~0x8000000000000000ull) : ~x;
-  double d;
-  std::memcpy(&d, &b, 8);
-  (void)fn;
-  return d;
-}
-
-// Global key identity for one group-by column over the executed segments (per-segment dictIds -> union
-// dictionary ids).  Identity when every segment holds the same dictionary bytes.
-struct GlobalDict {
-  int64_t card = 0;
-  bool identity = true;
-  // [seg][local] -> global; segments with byte-identical dictionaries share one table (and one blob copy)
-  std::vector<std::shared_ptr<const std::vector<int32_t>>> remap;
-  // [global] -> a (segment, local id) holding the value; rep_seg -1: the caller's key domain, rep_id = domain index
-  std::vector<int32_t> rep_seg, rep_id;
-};
-
-GlobalDict build_global_dict(pgx_segment* const* segs, int n, const std::string& col) {
-  GlobalDict g;
-  const StagedColumn& c0 = segs[0]->col(col);
-  // every segment holds the same dictionary?  (long lists: chunks on the context's pool -- the loop is bound by cache
-  // misses on the segments' column records, ~45 ns per segment)
-  std::atomic<bool> same{true};
-  auto check = [&](int lo, int hi) {
-    for (int s = lo; s < hi && same.load(std::memory_order_relaxed); ++s) {
-      const StagedColumn& c = segs[s]->col(col);
-      if (!(c.dict_hash == c0.dict_hash && c.card == c0.card && c.data_type == c0.data_type)) same = false;
-    }
-  };
-  constexpr int kChunk = 256;
-  if (n >= 4 * kChunk) segs[0]->ctx->parallel_for((n + kChunk - 1) / kChunk, [&](int i) {
-      check(std::max(1, i * kChunk), std::min(n, (i + 1) * kChunk));
-    });
-  else
-    check(1, n);
-  if (same) {
-    g.card = c0.card;
-    g.identity = true;
-    g.rep_seg.assign(g.card, 0);
-    g.rep_id.resize(g.card);
-    std::iota(g.rep_id.begin(), g.rep_id.end(), 0);
-    return g;
-  }
-  g.identity = false;
-  g.remap.resize(n);
-  // k-way merge of the sorted dictionaries by value, one representative segment per distinct dictionary
-  struct Item { int seg; int id; };
-  std::vector<Item> all;
-  std::map<std::pair<uint64_t, int>, int> first;  // (dict hash, card) -> representative segment
-  std::vector<int> rep(n);
-  std::vector<std::vector<int32_t>> tabs(n);
-  for (int s = 0; s < n; ++s) {
-    const StagedColumn& c = segs[s]->col(col);
-    if (c.data_type != c0.data_type) fail(PGX_ERR_INVALID_ARG, "column " + col + " has different types");
-    auto it = first.emplace(std::make_pair(c.dict_hash, c.card), s).first;
-    rep[s] = it->second;
-    if (rep[s] != s) continue;
-    tabs[s].resize(c.card);
-    for (int i = 0; i < c.card; ++i) all.push_back({s, i});
-  }
-  auto less = [&](const Item& a, const Item& b) {
-    const StagedColumn& ca = segs[a.seg]->col(col);
-    const StagedColumn& cb = segs[b.seg]->col(col);
-    if (c0.data_type == PGX_STRING) return ca.svals[a.id] < cb.svals[b.id];
-    if (c0.data_type == PGX_INT || c0.data_type == PGX_LONG) return ca.ivals[a.id] < cb.ivals[b.id];
-    return ca.dvals[a.id] < cb.dvals[b.id];
-  };
-  std::stable_sort(all.begin(), all.end(), less);
-  int64_t gid = -1;
-  for (size_t i = 0; i < all.size(); ++i) {
-    if (i == 0 || less(all[i - 1], all[i])) {
-      ++gid;
-      g.rep_seg.push_back(all[i].seg);
-      g.rep_id.push_back(all[i].id);
-    }
-    tabs[all[i].seg][all[i].id] = int32_t(gid);
-  }
-  std::vector<std::shared_ptr<const std::vector<int32_t>>> shared(n);
-  for (int s = 0; s < n; ++s) {
-    if (rep[s] == s) shared[s] = std::make_shared<const std::vector<int32_t>>(std::move(tabs[s]));
-    g.remap[s] = shared[rep[s]];
-  }
-  g.card = gid + 1;
-  return g;
-}
-
-// Key space from the caller's domain (pgx_query_set_key_domain): each distinct segment dictionary is remapped by value
-// into the domain's sorted values; a value outside the domain is a caller error.
-GlobalDict domain_global_dict(const KeyDomain& D, pgx_segment* const* segs, int n, const std::string& col) {
-  GlobalDict g;
-  g.card = D.size();
-  g.identity = false;
-  g.remap.resize(n);
-  g.rep_seg.assign(size_t(g.card), -1);
-  g.rep_id.resize(size_t(g.card));
-  std::iota(g.rep_id.begin(), g.rep_id.end(), 0);
-  std::map<std::pair<uint64_t, int>, std::shared_ptr<const std::vector<int32_t>>> memo;
-  bool ident = true;
-  for (int s = 0; s < n; ++s) {
-    const StagedColumn& c = segs[s]->col(col);
-    const bool str = c.data_type == PGX_STRING, integral = c.data_type == PGX_INT || c.data_type == PGX_LONG;
-    if (str != (D.type == PGX_STRING) || integral != (D.type == PGX_INT || D.type == PGX_LONG))
-      fail(PGX_ERR_INVALID_ARG, "key domain type differs from column " + col);
-    auto& m = memo[std::make_pair(c.dict_hash, c.card)];
-    if (!m) {
-      std::vector<int32_t> t(c.card);
-      for (int i = 0; i < c.card; ++i) {
-        int64_t pos;
-        if (str) pos = std::lower_bound(D.sv.begin(), D.sv.end(), c.svals[i]) - D.sv.begin();
-        else if (integral) pos = std::lower_bound(D.iv.begin(), D.iv.end(), c.ivals[i]) - D.iv.begin();
-        else pos = std::lower_bound(D.dv.begin(), D.dv.end(), c.dvals[i]) - D.dv.begin();
-        const bool hit = pos < g.card && (str ? D.sv[pos] == c.svals[i]
-                                              : integral ? D.iv[pos] == c.ivals[i] : D.dv[pos] == c.dvals[i]);
-        if (!hit) fail(PGX_ERR_INVALID_ARG, "a value of column " + col + " is not in its key domain");
-        t[i] = int32_t(pos);
-        ident = ident && pos == i;
-      }
-      ident = ident && c.card == g.card;
-      m = std::make_shared<const std::vector<int32_t>>(std::move(t));
-    }
-    g.remap[s] = m;
-  }
-  if (ident) {  // every segment holds exactly the domain: no remap tables (rep_seg stays -1: keys are domain indices)
-    g.identity = true;
-    g.remap.clear();
-  }
-  return g;
-}
-
-// The key space of group-by column g: the caller's domain when one is set, else the union of the segments' dictionaries.
-GlobalDict group_dict(const pgx_query& q, pgx_segment* const* segs, int n, int g) {
-  if (size_t(g) < q.key_domain.size() && q.key_domain[g].set)
-    return domain_global_dict(q.key_domain[g], segs, n, q.group_cols[g]);
-  return build_global_dict(segs, n, q.group_cols[g]);
-}
-
-// Reference storage mode of a single segment (DefaultGroupKeyGenerator.java:167-186): 0 ARRAY_BASED, 1 LONG_MAP_BASED,
-// 2 ARRAY_MAP_BASED.
-int reference_mode(const pgx_query& q, const pgx_segment* seg) {
-  int64_t p1 = 1;
-  bool ov = false;
-  for (const auto& g : q.group_cols) {
-    const int64_t cc = seg->col(g).card;
-    if (!ov && p1 > std::numeric_limits<int64_t>::max() / cc) ov = true;
-    else if (!ov) p1 *= cc;
-  }
-  return ov ? 2 : (p1 > 10000 ? 1 : 0);
-}
-
-// Key identity of a query whose segments run on several devices (pgx_execute_multi): the global dictionaries are built
-// once over ALL segments, and each device's plan takes its segments' rows of them, so a packed key or dense slot
-// means the same group on every device and the per-device partials merge without a remap.
-struct Domain {
-  const std::vector<GlobalDict>* g = nullptr;  // per group column, over the full segment list
-  std::vector<int> index;                      // this device's segment i -> position in the full list
-};
-
-GlobalDict domain_dict(const Domain& d, int col, int n) {
-  const GlobalDict& full = (*d.g)[col];
-  GlobalDict r;
-  r.card = full.card;
-  r.identity = full.identity;
-  r.rep_seg = full.rep_seg;  // positions in the FULL segment list: the merged result is decoded against it
-  r.rep_id = full.rep_id;
-  if (!full.identity) {
-    r.remap.resize(n);
-    for (int s = 0; s < n; ++s) r.remap[s] = full.remap[d.index[s]];
-  }
-  return r;
-}
-
-int bits_for(int64_t card) {
-  int b = 1;
-  while ((int64_t(1) << b) < card) ++b;
-  return b;
-}
-
-constexpr int kPart1Bits = 7;           // partitioned group-by, first pass: 128 buckets (top bits of the mix)
-constexpr int kPart1N = 1 << kPart1Bits;
-constexpr int kCursorStride = 16;       // u64 words between partition cursors: one 128-B line each
-
-struct ExecPlan {
-  bool serial = false;            // planned on a planner thread: no nested parallel_for on the context's pool
-  KQuery kq{};
-  std::vector<KSeg> ksegs;
-  std::vector<int32_t> blob32;   // ranges / remaps / bitsets, uploaded as one buffer
-  struct Fix { size_t seg; int kind; int slot; size_t off; };  // pointer fixups into blob32
-  std::vector<Fix> fixes;
-  std::vector<std::string> qcols;
-  std::vector<GlobalDict> gdicts;
-  std::vector<int> gbits;
-  int64_t host_entries = 0;
-  int64_t total_raw = 0;
-  // bitmap inverted-index leaves expanded on device for the query kernels (a-7)
-  bool use_docmask = false;
-  std::vector<int> leaf_phys;                      // physical operator kind per leaf (FilterPlanNode choice)
-  struct RoarItem {
-    int seg, leaf;
-    bool neg;
-    size_t blob_off;
-    int nb, nchunks;
-    uint64_t mask_off;
-    const void* inv;
-    uint64_t bytes = 0;  // serialized bytes of its bitmaps (selectivity estimate)
-  };
-  std::vector<RoarItem> roar;
-  std::vector<std::vector<int>> roar_index;        // [seg][leaf] -> index into roar or -1
-  std::vector<std::vector<const StagedColumn*>> segcols;  // [seg][query column slot]
-  // star-tree segments (a-18): a per-segment filter program over the query's leaves plus doc-range leaves
-  struct StarPlan {
-    bool on = false;
-    std::vector<int> op, arg;                      // postfix program (OP_*)
-    std::vector<std::pair<size_t, int>> ranges;    // extra range leaves: (blob offset, number of [a,b] pairs)
-  };
-  std::vector<StarPlan> star;
-  std::vector<std::vector<int32_t>> star_tiles;   // per star segment: local tile ids intersecting its ranges
-  size_t star_tile_cap = 0;                       // arena int32 slots reserved for them
-  uint64_t mask_words = 0;
-  const RDesc* rdesc_dev = nullptr;
-  bool roar_early = false;  // the expansion was launched by upload_plan (before the query kernels are planned)
-  // a lone query's replay (plan cache, no PGX_X_THROUGHPUT): bitmap programs and query kernel in two halves, the second
-  // half's programs on the side stream beside the first half's query kernel (launch_scan)
-  bool split2 = false;
-  hipStream_t ctx_side = nullptr;
-  struct Ev {
-    hipEvent_t e = nullptr;
-    hipEvent_t get() {
-      if (!e) hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event");
-      return e;
-    }
-    ~Ev() {
-      if (e) (void)hipEventDestroy(e);
-    }
-  } ev_pre, ev_half;
-  int roar_maxchunks = 0;
-  uint32_t* masks_dev = nullptr;
-  int n_proj = 0;
-  int mode_ref = 0;
-  uint64_t dense_slots = 0;
-  uint64_t hash_cap = 0;
-  int grid = 0;
-  int64_t tiles_per_wg = 0;
-  size_t lds_bytes = 0;
-  // query-specialised kernels (pgx_jit.cpp): one launch per group of segments sharing a shape
-  // partitioned group-by (G_HASH64 keys, one integer value column; run_partitioned)
-  Knobs kn;  // the query's (plan_query copies them in: partition sizing and launches read them from the plan)
-  bool use_part = false;
-  int part_vcol = -1;            // query column slot of the aggregated value (-1: COUNT only)
-  int part_keybits = 0;
-  int part_vbits = 0;
-  int64_t part_vbase = 0;
-  bool part_sum = false, part_min = false, part_max = false;
-  bool part_dictid = false;      // records carry the value's dictId (sorted dictionary), values looked up at aggregation
-  bool part_slab = false;        // ... into per-workgroup slabs (dictId records, LDS cursors; pass 2 reads the slabs)
-  int64_t part_nwg = 0;          // slab mode: query-kernel workgroups over all launch groups (slabs per bucket)
-  int64_t part_wg_rows = 0;      // slab mode: most rows one workgroup scans
-  const int64_t* part_vdict = nullptr;  // device int64 value per dictId (part_dictid)
-  unsigned long long* part_cursor = nullptr;   // fused first pass: bucket cursors, overflow counter, bucket capacity
-  unsigned long long* part_overflow = nullptr;
-  int64_t part_cap = 0;
-  // narrow records (run_narrow, the default for partitioned plans that qualify): the scan writes dictId records split
-  // 256 ways into per-workgroup slabs (part_slab with kNarrow1Bits), u32 in kq.table and bits 32..47 in part_hi
-  bool part_narrow = false;
-  std::shared_ptr<const std::vector<std::vector<int32_t>>> lazy_rep_seg, lazy_rep_id;  // part_result's key tables
-  int narrow_vd = 0;              // dictId bits of the value column (0: COUNT only)
-  int narrow_k2min = 0;           // second-split bits the record width needs
-  int narrow_img = 0;             // value image in the aggregation's LDS: 0 none, 1 U32, 2 FOR16
-  const uint32_t* narrow_imgp = nullptr;
-  int narrow_img_words = 0, narrow_img_sh = 0;
-  uint64_t narrow_vrange = 0;     // largest value offset (value - vbase)
-  unsigned short* part_hi = nullptr;
-  std::vector<int64_t> rec_base; // per segment: index of its row 0 in the record array
-  int64_t rec_total = 0;
-  struct JitGroup {
-    void* fn = nullptr;
-    int T = 256;
-    int grid = 1;
-    JArgs args{};
-    std::vector<JSeg> segs;
-  };
-  std::vector<JitGroup> jit;
-  // bitmap sub-trees evaluated by pgx_roaring_program into one mask each (JIT leaf L + k for program k)
-  bool rprog_on = false;
-  bool rchunk = false;   // ... evaluated per chunk inside the query kernels (LEAF_RCHUNK), not by a separate pass
-  // multi-value scan leaves (pgx_mv_leaf_mask writes one doc mask per (segment, leaf), read as LEAF_DOCMASK)
-  struct MvItem { int seg, leaf; };
-  std::vector<MvItem> mv_items;
-  std::vector<int> mv_neg;                 // [leaf] NEQ / NOT_IN
-  std::vector<std::vector<int>> mv_index;  // [seg][leaf] -> index into mv_items or -1
-  DevBuf mv_masks, mv_descs;
-  std::vector<MvLeaf> mv_host;             // their descriptors (host copy, sent by send_arena)
-  int mv_max_words = 0;
-  // selection masks for the multi-value functions (one bit per scanned row, per segment)
-  bool want_selmask = false;
-  DevBuf sel_buf;
-  // multi-value group-by results: per function, where its count comes from (-1: plane 0, the (doc, key) pairs; -2: its
-  // own value (COUNTMV); p >= 0: plane p (AVGMV's value count))
-  std::vector<int> g_count_plane;
-  std::vector<int64_t> sel_off;       // [seg] word offset in sel_buf
-  struct DmProg {
-    std::vector<int> op, arg;  // RP_*; RP_LEAF arg = query leaf index
-  };
-  std::vector<DmProg> dm_progs;
-  std::vector<RProg> rprogs;              // [seg * nprogs + k]
-  const RProg* rprog_dev = nullptr;
-  // numEntriesScannedInFilter automaton (pgx_stats.cpp) for filter trees whose statistic has no closed form
-  bool fsm_on = false;
-  FsmPlan fsm;
-  std::vector<int64_t> sorted_span;     // [seg * L + leaf] -> (first << 32 | last) doc of a sorted leaf (0 = empty)
-  std::vector<int64_t> lmask_off;       // [seg] word offset of its leaf masks (-1: no automaton for this segment)
-  std::vector<int64_t> lmask_words;     // [seg] words per leaf
-  uint64_t lmask_total = 0;
-  uint32_t* lmask_dev = nullptr;
-  std::vector<FsmSeg> fsm_segs;
-  int64_t fsm_chunks = 0;
-  DevBuf fsm_table, fsm_segbuf, fsm_cnt, fsm_stv, fsm_pcount, fsm_pstate, lmask_buf;
-  int fsm_T = 1;
-};
-
-// Estimated filter selectivity below which bitmap programs run inside the query kernels (LEAF_RCHUNK).  0: only when
-// forced with PGX_RCHUNK=1 (measured slower at C5 so far: the per-chunk container search stalls its workgroup).
-constexpr double kRchunkMaxSel = 0.0;
-
-}  // namespace
-
-Knobs pgx::read_knobs() {
-  Knobs k;
-  auto env = [](const char* name) -> std::string {
-    const char* e = std::getenv(name);
-    return e ? std::string(e) : std::string();
-  };
-  const std::string jit = env("PGX_JIT"), nar = env("PGX_PART_NARROW"), rc = env("PGX_RCHUNK"), rp = env("PGX_RPROG");
-  const std::string bs = env("PGX_BATCH_SEGS"), dbg = env("PGX_DEBUG");
-  k.jit = !(jit.size() && jit[0] == '0');
-  k.narrow = !(nar.size() && nar[0] == '0');
-  k.narrow_direct = nar == "direct";
-  if (rc.size()) k.rchunk = rc[0] == '1' ? 1 : 0;
-  if (rp == "off") k.rprog = RPROG_OFF;
-  else if (rp == "wave") k.rprog = RPROG_WAVE;
-  else if (rp == "seg") k.rprog = RPROG_SEG;
-  else if (rp == "chunk") k.rprog = RPROG_CHUNK;
-  else if (rp == "stack") k.rprog = RPROG_STACK;
-  if (bs.size()) k.batch_segs = std::atoi(bs.c_str());
-  size_t i = 0;
-  while (i < dbg.size()) {
-    size_t j = dbg.find(',', i);
-    if (j == std::string::npos) j = dbg.size();
-    const std::string o = dbg.substr(i, j - i);
-    if (o == "part_small") k.part_small = true;
-    else if (o == "narrow_log") k.narrow_log = true;
-    else if (o == "host_profile") k.host_profile = true;
-    else if (o.rfind("narrow_k2=", 0) == 0) k.narrow_k2 = std::atoi(o.c_str() + 10);
-    i = j + 1;
-  }
-  return k;
-}
-
-namespace {
-
-int qslot(ExecPlan& P, const std::string& name) {
-  for (size_t i = 0; i < P.qcols.size(); ++i)
-    if (P.qcols[i] == name) return int(i);
-  if (P.qcols.size() >= size_t(kMaxQCols)) fail(PGX_ERR_UNSUPPORTED, "query touches too many columns");
-  P.qcols.push_back(name);
-  return int(P.qcols.size() - 1);
-}
-
-// RequestUtils.isFitForStarTreeIndex (pinot-common/.../common/utils/request/RequestUtils.java:128-220): aggregations
-// only SUM, filter a single predicate or an AND of predicates on distinct star-tree dimensions.
-bool star_fit(const pgx_query& q, const pgx_segment& seg) {
-  if (!seg.st_ok || (q.flags & PGX_Q_NO_STAR_TREE) || q.agg_fn.empty()) return false;
-  // group-by and predicate columns must be materialised (:149-163, :195-198, :209-211): a skipped dimension holds the
-  // star value in every aggregated doc, so only a raw scan answers for it
-  auto skipped = [&](const std::string& c) {
-    return std::find(seg.st_skip.begin(), seg.st_skip.end(), c) != seg.st_skip.end();
-  };
-  for (const auto& g : q.group_cols)
-    if (skipped(g)) return false;
-  for (const auto& c : q.leaf_col)
-    if (skipped(c)) return false;
-  for (int fn : q.agg_fn)
-    if (fn != PGX_SUM) return false;
-  const size_t nl = q.leaf_col.size();
-  if (!q.filter.empty()) {
-    if (q.filter.size() == 1) {
-      if (q.filter[0].op != PGX_F_LEAF) return false;
-    } else {
-      if (q.filter.back().op != PGX_F_AND || q.filter.back().arg != int(nl) || q.filter.size() != nl + 1) return false;
-      for (size_t i = 0; i + 1 < q.filter.size(); ++i)
-        if (q.filter[i].op != PGX_F_LEAF) return false;
-    }
-  }
-  for (size_t i = 0; i < nl; ++i) {
-    if (std::find(seg.st_dim_name.begin(), seg.st_dim_name.end(), q.leaf_col[i]) == seg.st_dim_name.end()) return false;
-    for (size_t j = 0; j < i; ++j)
-      if (q.leaf_col[j] == q.leaf_col[i]) return false;
-  }
-  return true;
-}
-
-// StarTreeIndexOperator (operator/filter/StarTreeIndexOperator.java:134-478) for one segment: BFS from the root; at a
-// node splitting on a predicate column follow the children of the matching dictIds; on a group-by column (or with no
-// star child) follow every non-star child; otherwise take the star child.  An entry matches at a leaf, or once no
-// predicate / group-by column remains and the node has an aggregated doc.  Matched entries become: the aggregated doc
-// (nothing left to apply), the node's doc range, or the range AND the remaining predicates (createChildOperator).
-// The result is expressed as a filter program: OR(exact ranges, range_m AND preds(m) for each remaining-set m).
-void plan_star_segment(const pgx_query& q, const pgx_segment& seg, const KSeg& S, const pgx_leaf_binding* b,
-                       const std::vector<int>& leaf_phys, std::vector<int32_t>& blob, ExecPlan::StarPlan& sp) {
-  const auto& nodes = seg.st_nodes;
-  const int nl = int(q.leaf_col.size());
-  const int ng = int(q.group_cols.size());
-  sp.on = true;
-  sp.op.clear();
-  sp.arg.clear();
-  sp.ranges.clear();
-  bool empty = false;
-  for (int l = 0; l < nl; ++l)
-    if (S.leaf[l].mode == LEAF_NONE) empty = true;  // PredicateEvaluator.alwaysFalse -> emptyResult
-  std::map<uint32_t, std::vector<std::pair<int32_t, int32_t>>> groups;  // remaining-predicate mask -> [a, b] ranges
-  std::vector<std::pair<int32_t, int32_t>>& exact = groups[0];
-  if (!empty) {
-    std::vector<int> dim_leaf(seg.st_dim_name.size(), -1), dim_group(seg.st_dim_name.size(), -1);
-    for (size_t d = 0; d < seg.st_dim_name.size(); ++d) {
-      for (int l = 0; l < nl; ++l)
-        if (q.leaf_col[l] == seg.st_dim_name[d]) dim_leaf[d] = l;
-      for (int g = 0; g < ng; ++g)
-        if (q.group_cols[g] == seg.st_dim_name[d]) dim_group[d] = g;
-    }
-    auto matches = [&](int l, int id) -> bool {
-      const pgx_leaf_binding& x = b[l];
-      if (x.words) return (x.words[id >> 5] >> (id & 31)) & 1u;
-      return id >= x.lo && id <= x.hi;
-    };
-    struct Entry { int node; uint32_t pred, gb; };
-    std::deque<Entry> queue;
-    queue.push_back({0, nl ? (uint32_t(1) << nl) - 1u : 0u, ng ? (uint32_t(1) << ng) - 1u : 0u});
-    const int32_t num_raw = seg.total_raw_docs;
-    while (!queue.empty()) {
-      const Entry e = queue.front();
-      queue.pop_front();
-      const auto& cur = nodes[e.node];
-      const bool leaf = cur.cbeg == -1;
-      if (leaf || (e.pred == 0 && e.gb == 0 && cur.agg >= num_raw)) {
-        const bool agg_ok = cur.agg >= num_raw;
-        if (e.pred == 0) {
-          if (agg_ok && e.gb == 0) exact.push_back({cur.agg, cur.agg});
-          else if (cur.end > cur.start) exact.push_back({cur.start, cur.end - 1});
-        } else if (cur.end > cur.start) {
-          groups[e.pred].push_back({cur.start, cur.end - 1});
-        }
-        continue;
-      }
-      const int cdim = nodes[cur.cbeg].dim;  // StarTreeIndexNodeOffHeap.getChildDimensionName: first child's dimension
-      const int l = (cdim >= 0 && cdim < int(dim_leaf.size())) ? dim_leaf[cdim] : -1;
-      const int g = (cdim >= 0 && cdim < int(dim_group.size())) ? dim_group[cdim] : -1;
-      Entry ne{0, e.pred, e.gb};
-      if (l >= 0) {
-        ne.pred &= ~(uint32_t(1) << l);
-        if (g >= 0) ne.gb &= ~(uint32_t(1) << g);
-        // children sorted by value: each matching dictId is a binary search (getChildForDimensionValue)
-        const int card = seg.col(q.leaf_col[l]).card;
-        for (int id = 0; id < card; ++id) {
-          if (!matches(l, id)) continue;
-          int lo = cur.cbeg, hi = cur.cend;
-          while (lo <= hi) {
-            const int mid = lo + ((hi - lo) >> 1);
-            if (nodes[mid].value == id) { ne.node = mid; queue.push_back(ne); break; }
-            if (nodes[mid].value < id) lo = mid + 1; else hi = mid - 1;
-          }
-        }
-      } else {
-        const bool has_star = nodes[cur.cbeg].value == -1;
-        if (g >= 0 || !has_star) {
-          for (int c = cur.cbeg; c <= cur.cend; ++c) {
-            if (nodes[c].value == -1) continue;
-            if (g >= 0) ne.gb &= ~(uint32_t(1) << g);
-            ne.node = c;
-            queue.push_back(ne);
-          }
-        } else {
-          ne.node = cur.cbeg;
-          queue.push_back(ne);
-        }
-      }
-    }
-  }
-  // ranges -> blob (sorted, merged), program
-  auto put_ranges = [&](std::vector<std::pair<int32_t, int32_t>>& r) {
-    std::sort(r.begin(), r.end());
-    std::vector<int32_t> m;
-    for (const auto& x : r) {
-      if (!m.empty() && x.first <= m.back() + 1) m.back() = std::max(m.back(), x.second);
-      else { m.push_back(x.first); m.push_back(x.second); }
-    }
-    sp.ranges.push_back({blob.size(), int(m.size() / 2)});
-    blob.insert(blob.end(), m.begin(), m.end());
-    return nl + int(sp.ranges.size()) - 1;  // leaf index of this range leaf
-  };
-  int terms = 0;
-  for (auto& kv : groups) {
-    if (kv.second.empty()) continue;
-    const int rl = put_ranges(kv.second);
-    sp.op.push_back(OP_LEAF);
-    sp.arg.push_back(rl);
-    for (int pass = 0; pass < 2; ++pass)  // index-based children first, then scans (AndBlockDocIdSet)
-      for (int l = 0; l < nl; ++l) {
-        if (!((kv.first >> l) & 1u)) continue;
-        const bool scan = leaf_phys[l] == PH_SCAN;
-        if (scan != (pass == 1)) continue;
-        if (scan) { sp.op.push_back(OP_STAT); sp.arg.push_back(0); }
-        sp.op.push_back(OP_LEAF);
-        sp.arg.push_back(l);
-        sp.op.push_back(OP_AND);
-        sp.arg.push_back(2);
-      }
-    ++terms;
-  }
-  if (terms == 0) {
-    std::vector<std::pair<int32_t, int32_t>> none;
-    const int rl = put_ranges(none);
-    sp.op.push_back(OP_LEAF);
-    sp.arg.push_back(rl);
-    terms = 1;
-  }
-  if (terms > 1) { sp.op.push_back(OP_OR); sp.arg.push_back(terms); }
-}
-
-// Does numEntriesScannedInFilter have a closed form the query kernels compute on the fly?  Yes for: no scan leaf at
-// all (0); a root scan leaf or a root OR of leaves (SVScanDocIdIterator.next walks its whole [start, end] range,
-// OrDocIdIterator.next re-targets a child right after each of its matches); a root AND of leaves with at least one
-// sorted / bitmap leaf (AndBlockDocIdSet.fastIterator: each scan's applyAnd tests the running answer -- OP_STAT
-// popcounts -- unless its evaluator is alwaysFalse, SVScanDocIdIterator.java:133-135).  Every other tree goes through
-// the statistics automaton (pgx_stats.cpp).
-bool has_scan_leaf(const PNode& n) {
-  if (n.op == PGX_F_LEAF) return n.phys == PH_SCAN;
-  for (const PNode& k : n.kids)
-    if (has_scan_leaf(k)) return true;
-  return false;
-}
-
-bool binding_empty(const pgx_leaf_binding& b, int card) {
-  if (b.words) {
-    const int nw = (card + 31) / 32;
-    for (int w = 0; w < nw; ++w)
-      if (b.words[w]) return false;
-    return true;
-  }
-  return b.hi < b.lo;
-}
-
-bool stats_closed_form(const PNode& root, const pgx_query& q, pgx_segment* const* segs, int n,
-                       const pgx_leaf_binding* bindings) {
-  if (!has_scan_leaf(root)) return true;
-  if (root.op == PGX_F_LEAF) return true;
-  for (const PNode& k : root.kids)
-    if (k.op != PGX_F_LEAF) return false;
-  if (root.op == PGX_F_OR) return true;
-  bool index = false;
-  for (const PNode& k : root.kids) index |= k.phys == PH_SORTED || k.phys == PH_BITMAP;
-  if (!index) return false;
-  const size_t L = q.leaf_col.size();
-  for (const PNode& k : root.kids)
-    if (k.phys == PH_SCAN)
-      for (int s = 0; s < n; ++s)
-        if (binding_empty(bindings[size_t(s) * L + k.leaf], segs[s]->col(q.leaf_col[k.leaf]).card)) return false;
-  return true;
-}
-
-// Bitmap sub-trees: a node whose leaves are all bitmap inverted-index leaves (and the bitmap / all-bitmap children of
-// any AND / OR) is evaluated per 65536-doc chunk by pgx_roaring_program into ONE doc mask.
-struct FusePlan {
-  std::map<const PNode*, int> full;   // node evaluated whole by program k
-  std::map<const PNode*, int> group;  // AND / OR whose all-bitmap children are program k
-  std::vector<ExecPlan::DmProg> progs;
-};
-
-bool all_bitmap(const PNode& n) {
-  if (n.op == PGX_F_LEAF) return n.phys == PH_BITMAP;
-  for (const PNode& k : n.kids)
-    if (!all_bitmap(k)) return false;
-  return true;
-}
-
-void bitmap_prog(const PNode& n, const pgx_query& q, ExecPlan::DmProg& p) {
-  if (n.op == PGX_F_LEAF) {
-    p.op.push_back(RP_LEAF);
-    p.arg.push_back(n.leaf);
-    // BitmapBasedFilterOperator NEQ / NOT_IN: OR of the non-matching bitmaps, then flip (BitmapDocIdSet.java:60-73)
-    if (q.leaf_kind[n.leaf] == PGX_PRED_NEQ || q.leaf_kind[n.leaf] == PGX_PRED_NOT_IN) {
-      p.op.push_back(RP_NOT);
-      p.arg.push_back(0);
-    }
-    return;
-  }
-  for (size_t i = 0; i < n.kids.size(); ++i) {
-    bitmap_prog(n.kids[i], q, p);
-    if (i > 0) {
-      p.op.push_back(n.op == PGX_F_AND ? RP_AND : RP_OR);
-      p.arg.push_back(0);
-    }
-  }
-}
-
-void plan_fuse(const PNode& n, const pgx_query& q, FusePlan& F) {
-  if (n.op == PGX_F_LEAF) {
-    if (n.phys == PH_BITMAP) {
-      F.full[&n] = int(F.progs.size());
-      F.progs.emplace_back();
-      bitmap_prog(n, q, F.progs.back());
-    }
-    return;
-  }
-  if (all_bitmap(n)) {
-    F.full[&n] = int(F.progs.size());
-    F.progs.emplace_back();
-    bitmap_prog(n, q, F.progs.back());
-    return;
-  }
-  std::vector<const PNode*> fk;
-  for (const PNode& k : n.kids) {
-    if (all_bitmap(k)) fk.push_back(&k);
-    else plan_fuse(k, q, F);
-  }
-  if (fk.empty()) return;
-  ExecPlan::DmProg p;
-  for (size_t i = 0; i < fk.size(); ++i) {
-    bitmap_prog(*fk[i], q, p);
-    if (i > 0) {
-      p.op.push_back(n.op == PGX_F_AND ? RP_AND : RP_OR);
-      p.arg.push_back(0);
-    }
-  }
-  F.group[&n] = int(F.progs.size());
-  F.progs.push_back(std::move(p));
-}
-
-int prog_depth(const ExecPlan::DmProg& p) {
-  int d = 0, mx = 0;
-  for (int op : p.op) {
-    if (op == RP_LEAF) mx = std::max(mx, ++d);
-    else if (op == RP_AND || op == RP_OR) --d;
-  }
-  return mx;
-}
-
-// emit() with bitmap programs: a fused node is one doc-mask leaf (query leaf L + k); an AND / OR puts its fused group
-// where its bitmap children were (AND: after the sorted ranges, before the scan children and their OP_STATs).
-void emit_fused(const PNode& n, const FusePlan& F, int L, std::vector<int8_t>& op, std::vector<int8_t>& arg, bool root,
-                int& host_scan_leaves) {
-  auto f = F.full.find(&n);
-  if (f != F.full.end()) {
-    op.push_back(OP_LEAF);
-    arg.push_back(int8_t(L + f->second));
-    return;
-  }
-  if (n.op == PGX_F_LEAF) {
-    op.push_back(OP_LEAF);
-    arg.push_back(int8_t(n.leaf));
-    if (root && n.phys == PH_SCAN) host_scan_leaves += 1;
-    return;
-  }
-  auto g = F.group.find(&n);
-  int pushed = 0;
-  auto fold = [&](int opc) {
-    if (pushed > 1) { op.push_back(int8_t(opc)); arg.push_back(2); }
-  };
-  if (n.op == PGX_F_OR) {
-    for (const PNode& k : n.kids) {
-      if (all_bitmap(k)) continue;
-      if (root && k.op == PGX_F_LEAF && k.phys == PH_SCAN) host_scan_leaves += 1;
-      emit_fused(k, F, L, op, arg, false, host_scan_leaves);
-      ++pushed;
-      fold(OP_OR);
-    }
-    if (g != F.group.end()) {
-      op.push_back(OP_LEAF);
-      arg.push_back(int8_t(L + g->second));
-      ++pushed;
-      fold(OP_OR);
-    }
-    return;
-  }
-  for (const PNode& k : n.kids)
-    if (k.op == PGX_F_LEAF && k.phys == PH_SORTED) {
-      emit_fused(k, F, L, op, arg, false, host_scan_leaves);
-      ++pushed;
-      fold(OP_AND);
-    }
-  if (g != F.group.end()) {
-    op.push_back(OP_LEAF);
-    arg.push_back(int8_t(L + g->second));
-    ++pushed;
-    fold(OP_AND);
-  }
-  const bool fast = pushed > 0;
-  for (const PNode& k : n.kids)
-    if (k.op == PGX_F_LEAF && k.phys == PH_SCAN) {
-      if (fast || pushed > 0) { op.push_back(OP_STAT); arg.push_back(0); }
-      else if (root) host_scan_leaves += 1;
-      emit_fused(k, F, L, op, arg, false, host_scan_leaves);
-      ++pushed;
-      fold(OP_AND);
-    }
-  for (const PNode& k : n.kids)
-    if (k.op != PGX_F_LEAF && !all_bitmap(k)) {
-      emit_fused(k, F, L, op, arg, false, host_scan_leaves);
-      ++pushed;
-      fold(OP_AND);
-    }
-}
-
-FsmTreeNode fsm_tree(const PNode& n) {
-  FsmTreeNode t;
-  t.op = n.op == PGX_F_LEAF ? 0 : (n.op == PGX_F_AND ? 1 : 2);
-  t.leaf = n.leaf;
-  t.phys = n.phys;
-  for (const PNode& k : n.kids) t.kids.push_back(fsm_tree(k));
-  return t;
-}
-
-
-// ----- a-4: predicate values -> dictId space (per segment, memoised per distinct dictionary) -----
-
-namespace {
-
-std::string trim_ws(const std::string& v) {
-  size_t a = 0, b = v.size();
-  while (a < b && (unsigned char)v[a] <= ' ') ++a;
-  while (b > a && (unsigned char)v[b - 1] <= ' ') --b;
-  return v.substr(a, b - a);
-}
-
-// Dictionary.indexOf (segment/index/readers/{Int,Long,Float,Double,String}Dictionary.java): binary search, -(insertion
-// point) - 1 when absent.
-int dict_index_of(const StagedColumn& c, const std::string& raw) {
-  auto search = [&](auto less, auto eq) {
-    int lo = 0, hi = c.card - 1;
-    while (lo <= hi) {
-      const int mid = (lo + hi) >> 1;
-      if (eq(mid)) return mid;
-      if (less(mid)) lo = mid + 1;
-      else hi = mid - 1;
-    }
-    return -(lo + 1);
-  };
-  switch (c.data_type) {
-    case PGX_INT:
-    case PGX_LONG: {  // Integer.parseInt / Long.parseLong: optional sign, digits only
-      const char* s = raw.c_str();
-      char* end = nullptr;
-      errno = 0;
-      const long long v = std::strtoll(s, &end, 10);
-      const bool ok = !raw.empty() && *end == '\0' && errno == 0 && !std::isspace((unsigned char)raw[0]) &&
-                      (c.data_type == PGX_LONG || (v >= INT32_MIN && v <= INT32_MAX));
-      if (!ok) fail(PGX_ERR_INVALID_ARG, "NumberFormatException: For input string: \"" + raw + "\"");
-      return search([&](int i) { return c.ivals[i] < v; }, [&](int i) { return c.ivals[i] == v; });
-    }
-    case PGX_FLOAT:
-    case PGX_DOUBLE: {  // Float.parseFloat / Double.parseDouble: surrounding whitespace and a trailing f/F/d/D allowed
-      std::string t = trim_ws(raw);
-      if (!t.empty() && std::strchr("fFdD", t.back())) t.pop_back();
-      char* end = nullptr;
-      const double d = c.data_type == PGX_FLOAT ? double(std::strtof(t.c_str(), &end)) : std::strtod(t.c_str(), &end);
-      if (t.empty() || *end != '\0') fail(PGX_ERR_INVALID_ARG, "NumberFormatException: For input string: \"" + raw + "\"");
-      return search([&](int i) { return c.dvals[i] < d; }, [&](int i) { return c.dvals[i] == d; });
-    }
-    default: {  // StringDictionary.indexOf: pad the lookup to the entry width unless it is at least that long
-      const size_t w = size_t(c.dict_width);
-      const char pad = char(c.pad_char);
-      const std::string key = raw.size() >= w ? raw : raw + std::string(w - raw.size(), pad);
-      auto entry = [&](int i) {
-        const std::string& v = c.svals[i];
-        return v.size() >= w ? v : v + std::string(w - v.size(), pad);
-      };
-      return search([&](int i) { return entry(i) < key; }, [&](int i) { return entry(i) == key; });
-    }
-  }
-}
-
-void resolve_binding(const StagedColumn& c, int kind, const pgx_predicate& p, int32_t& lo, int32_t& hi,
-                     std::vector<uint32_t>& words) {
-  const int card = c.card;
-  auto val = [&](int i) { return std::string(p.values[i] ? p.values[i] : ""); };
-  words.clear();
-  lo = 0;
-  hi = -1;
-  if (kind == PGX_PRED_RANGE) {  // RangeOfflineDictionaryPredicateEvaluator.java:30-65
-    if (p.num_values != 2) fail(PGX_ERR_INVALID_ARG, "RANGE needs (lower, upper)");
-    const std::string a = val(0), b = val(1);
-    int start = a == "*" ? 0 : dict_index_of(c, a);
-    int end = b == "*" ? card - 1 : dict_index_of(c, b);
-    if (start < 0) start = -(start + 1);
-    else if (!p.lower_inclusive && a != "*") start += 1;
-    if (end < 0) end = -(end + 1) - 1;
-    else if (!p.upper_inclusive && b != "*") end -= 1;
-    if (end >= start) {
-      lo = start;
-      hi = end;
-    }
-    return;
-  }
-  if (kind == PGX_PRED_EQ) {  // EqualsPredicateEvaluator.java:28-42
-    if (p.num_values < 1) fail(PGX_ERR_INVALID_ARG, "EQ needs a value");
-    const int i = dict_index_of(c, val(0));
-    if (i >= 0) lo = hi = i;
-    return;
-  }
-  std::vector<uint8_t> m(card, kind == PGX_PRED_IN ? 0 : 1);  // In / NotIn / NotEquals evaluators
-  for (int k = 0; k < p.num_values; ++k) {
-    const int i = dict_index_of(c, val(k));
-    if (i >= 0) m[i] = kind == PGX_PRED_IN ? 1 : 0;
-  }
-  int first = -1, last = -1, cnt = 0;
-  for (int i = 0; i < card; ++i)
-    if (m[i]) {
-      if (first < 0) first = i;
-      last = i;
-      ++cnt;
-    }
-  if (cnt == 0) return;
-  if (last - first + 1 == cnt) {
-    lo = first;
-    hi = last;
-    return;
-  }
-  words.assign((card + 31) / 32, 0u);
-  for (int i = 0; i < card; ++i)
-    if (m[i]) words[i >> 5] |= 1u << (i & 31);
-}
-
-}  // namespace
-
-// PGX_HOST_PROFILE=1: sub-phase marks of the planner (appended to the running pgx_execute's profile line).
-thread_local std::function<void(const char*)> g_prof_mark;
-void prof_mark(const char* what) {
-  if (g_prof_mark) g_prof_mark(what);
-}
-
-void canon_rprog(std::vector<int>& op, std::vector<int>& arg);
-
-
-void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
-                uint32_t xflags, ExecPlan& P, const Domain* dom = nullptr) {
-  if (n < 1) fail(PGX_ERR_INVALID_ARG, "no segments");
-  if (q.agg_fn.size() > size_t(kMaxAggs)) fail(PGX_ERR_UNSUPPORTED, "too many aggregation functions");
-  if (q.group_cols.size() > size_t(kMaxGroupCols)) fail(PGX_ERR_UNSUPPORTED, "too many group-by columns");
-  if (q.leaf_col.size() > size_t(kMaxLeaves)) fail(PGX_ERR_UNSUPPORTED, "too many filter leaves");
-  P.kn = q.kn;
-  KQuery& K = P.kq;
-  // query column slots
-  for (size_t l = 0; l < q.leaf_col.size(); ++l) K.leaf_col[l] = int8_t(qslot(P, q.leaf_col[l]));
-  K.num_aggs = int(q.agg_fn.size());
-  K.num_planes = K.num_aggs + 1;
-  K.plane_op[0] = P_ADD_I64;
-  std::vector<std::string> proj;
-  for (int a = 0; a < K.num_aggs; ++a) {
-    const int fn = q.agg_fn[a];
-    K.agg_kind[a] = int8_t(fn);
-    if (fn == PGX_COUNT) {
-      K.agg_col[a] = -1;
-      K.agg_fp[a] = 0;
-      K.plane_op[a + 1] = P_ADD_I64;
-      continue;
-    }
-    const StagedColumn& c = segs[0]->col(q.agg_col[a]);
-    if (c.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + c.name);
-    if (fn >= PGX_COUNTMV) fail(PGX_ERR_INTERNAL, "multi-value function in the single-value plan");
-    for (int s = 0; s < n; ++s)
-      if (segs[s]->col(q.agg_col[a]).is_mv)
-        fail(PGX_ERR_UNSUPPORTED, "single-value aggregation on multi-value column " + c.name);
-    const bool fp = c.data_type == PGX_FLOAT || c.data_type == PGX_DOUBLE;
-    K.agg_col[a] = int8_t(qslot(P, q.agg_col[a]));
-    K.agg_fp[a] = fp;
-    K.plane_op[a + 1] = (fn == PGX_MIN) ? P_MIN_ORD : (fn == PGX_MAX) ? P_MAX_ORD : (fp ? P_ADD_F64 : P_ADD_I64);
-    if (std::find(proj.begin(), proj.end(), q.agg_col[a]) == proj.end()) proj.push_back(q.agg_col[a]);
-  }
-  for (const auto& g : q.group_cols)
-    if (std::find(proj.begin(), proj.end(), g) == proj.end()) proj.push_back(g);
-  P.n_proj = int(proj.size());
-
-  // group-by key space
-  K.num_gcols = int(q.group_cols.size());
-  K.group_mode = G_NONE;
-  if (K.num_gcols) {
-    uint64_t prod = 1;
-    bool overflow = false;
-    int total_bits = 0;
-    P.gdicts.clear();
-    for (int g = 0; g < K.num_gcols; ++g) {
-      for (int s = 0; s < n; ++s)
-        if (segs[s]->col(q.group_cols[g]).is_mv)
-          fail(PGX_ERR_UNSUPPORTED, "GROUP BY on multi-value column " + q.group_cols[g]);
-      K.gcol[g] = int8_t(qslot(P, q.group_cols[g]));
-      P.gdicts.push_back(dom ? domain_dict(*dom, g, n) : group_dict(q, segs, n, g));
-      const int64_t gc = P.gdicts.back().card;
-      if (!overflow && prod > (uint64_t(1) << 62) / uint64_t(gc)) overflow = true;
-      if (!overflow) prod *= uint64_t(gc);
-      P.gbits.push_back(bits_for(gc));
-      total_bits += P.gbits.back();
-    }
-    P.mode_ref = reference_mode(q, segs[0]);
-    const uint64_t kDenseMax = uint64_t(1) << 22;
-    if (!overflow && prod <= kDenseMax && !(xflags & PGX_X_FORCE_HASH)) {
-      uint64_t mul = 1;
-      for (int g = 0; g < K.num_gcols; ++g) {  // column 0 least significant (DefaultGroupKeyGenerator.java:230-237)
-        K.gmul[g] = mul;
-        mul *= uint64_t(P.gdicts[g].card);
-      }
-      P.dense_slots = prod;
-      const size_t lds = size_t(prod) * K.num_planes * 8;
-      K.group_mode = (lds <= 48 * 1024) ? G_DENSE_LDS : G_DENSE_GLOBAL;
-      if (K.group_mode == G_DENSE_LDS) P.lds_bytes = lds;
-    } else if (total_bits <= 126) {
-      int sh = 0;
-      bool hi = false;
-      for (int g = 0; g < K.num_gcols; ++g) {
-        if (!hi && sh + P.gbits[g] > 63) {
-          hi = true;
-          sh = 0;
-        }
-        K.gshift[g] = sh;
-        K.ghi[g] = hi;
-        sh += P.gbits[g];
-      }
-      K.group_mode = hi ? G_HASH128 : G_HASH64;
-    } else {
-      fail(PGX_ERR_UNSUPPORTED, "group key wider than 126 bits");
-    }
-  }
-  K.num_qcols = int(P.qcols.size());
-  prof_mark("p.keys");
-
-  // Partitioned group-by: sparse 64-bit keys go through record-emitting query kernels, radix partitioning and LDS
-  // aggregation (run_partitioned) instead of one global hash table.  Eligible when every non-COUNT function reads the
-  // same INT/LONG column whose dictionary is identical in every segment (one value base), with a value range of at
-  // most 32 bits, and key + value fit 63 bits.
-  P.use_part = false;
-  P.part_slab = P.part_dictid = P.part_narrow = false;
-  P.part_hi = nullptr;
-  if (K.group_mode == G_HASH64 && q.kn.jit && !(xflags & PGX_X_NO_PARTITION) &&
-      K.num_qcols <= PGX_J_MAX_COLS) {
-    int vc = -1;
-    bool ok = true;
-    bool need_sum = false, need_min = false, need_max = false;
-    for (int a = 0; a < K.num_aggs && ok; ++a) {
-      const int k = K.agg_kind[a];
-      if (k == A_COUNT) continue;
-      if (K.agg_fp[a] || (vc >= 0 && vc != K.agg_col[a])) ok = false;
-      vc = K.agg_col[a];
-      need_sum |= k == A_SUM || k == A_AVG;
-      need_min |= k == A_MIN;
-      need_max |= k == A_MAX;
-    }
-    int keybits = 0;
-    for (int g = 0; g < K.num_gcols; ++g) keybits = std::max(keybits, K.gshift[g] + P.gbits[g]);
-    int vbits = 0;
-    int64_t vbase = 0;
-    uint64_t vrange = 0;
-    bool same_dict = true;  // one dictionary in every segment: records may carry the dictId (narrow path)
-    if (ok && vc >= 0) {
-      // Value records carry value - vbase with ONE query-wide vbase (the smallest value of any segment's dictionary):
-      // each segment's records are rebased by (its image base - vbase) in the scan (JSeg.emit_rebase), so segments
-      // with their own dictionaries (SegmentDictionaryCreator builds one per segment) share the radix path.
-      const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
-      int64_t vmin = 0, vmax = 0;
-      for (int s = 0; s < n && ok; ++s) {
-        const StagedColumn& c = segs[s]->col(P.qcols[vc]);
-        ok = (c.data_type == PGX_INT || c.data_type == PGX_LONG) && !c.ivals.empty() && c.data_type == c0.data_type;
-        if (!ok) break;
-        const int64_t lo = *std::min_element(c.ivals.begin(), c.ivals.end());
-        const int64_t hi = *std::max_element(c.ivals.begin(), c.ivals.end());
-        vmin = s ? std::min(vmin, lo) : lo;
-        vmax = s ? std::max(vmax, hi) : hi;
-        same_dict = same_dict && c.dict_hash == c0.dict_hash && c.card == c0.card;
-      }
-      if (ok) {
-        const uint64_t range = uint64_t(vmax) - uint64_t(vmin);
-        ok = range <= 0xFFFFFFFFull;
-        vbase = vmin;
-        vrange = range;
-        vbits = ok ? bits_for(int64_t(range) + 1) : 64;
-      }
-    }
-    // The 8-byte radix path's records carry value offsets (round 3's dictId records with a fused first pass or
-    // per-workgroup slabs measured slower at C3 and were removed in round 5)
-    if (ok && keybits + vbits <= 63) {
-      P.use_part = true;
-      P.part_vcol = vc;
-      P.part_keybits = keybits;
-      P.part_vbits = vbits;
-      P.part_vbase = vbase;
-      P.part_sum = need_sum;
-      P.part_min = need_min;
-      P.part_max = need_max;
-      // Narrow records (default; PGX_PART_NARROW=0 keeps the 8-byte radix path): the value's dictId rides in a record of
-      // keybits - 8 + dictId bits (<= 48) out of the scan's own 256-way split, then <= 32 bits after the second split,
-      // and the aggregation looks values up in the column's image (FOR16 / U32) in LDS (run_narrow).  Needs a sorted
-      // dictionary (MIN / MAX of dictIds) and, for SUM / AVG, an image that fits beside the aggregation tables.
-      if (q.kn.narrow && keybits > kNarrow1Bits) {
-        // Value field: the dictId looked up in an LDS image of the column (one sorted dictionary in every segment, an
-        // image that fits the LDS), or the value offset itself (value - vbase, rebased per segment like the radix
-        // records: per-segment dictionaries, no image, and no LDS spent on one -- PGX_PART_NARROW=direct prefers it)
-        const int rb1 = keybits - kNarrow1Bits;
-        auto fits = [&](int vd, int& k2) {
-          k2 = std::max(0, rb1 + vd - 32);
-          if (rb1 - k2 > 31) k2 = rb1 - 31;
-          return rb1 + vd <= 48 && k2 <= kNarrowMaxBits2;
-        };
-        int vd = 0, imgk = 0, k2 = 0;
-        bool nok = true;
-        if (vc >= 0) {
-          const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
-          nok = same_dict && c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end());
-          vd = bits_for(c0.card);
-          if (c0.img_dev && c0.img_kind == IMG_FOR16 && c0.img_words <= kImgFor16Blocks + 32768) imgk = 2;
-          else if (c0.img_dev && c0.img_kind == IMG_U32 && c0.img_words <= kImgFor16Blocks + 32768) imgk = 1;
-          if (need_sum && !imgk) nok = false;
-          nok = nok && fits(vd, k2);
-          int k2d = 0;
-          if ((!nok || q.kn.narrow_direct) && vbits <= 32 && fits(vbits, k2d)) {
-            nok = true;
-            imgk = 3;
-            vd = vbits;
-            k2 = k2d;
-            P.part_vdict = nullptr;
-            P.narrow_imgp = nullptr;
-            P.narrow_img_words = 0;
-            P.narrow_img_sh = 0;
-            P.narrow_vrange = vrange;
-          } else if (nok) {
-            P.part_vdict = static_cast<const int64_t*>(c0.dict_dev);
-            P.narrow_imgp = imgk ? static_cast<const uint32_t*>(c0.img_dev) : nullptr;
-            P.narrow_img_words = imgk ? c0.img_words : 0;
-            P.narrow_img_sh = c0.img_sh;
-            P.narrow_vrange = c0.vrange;
-          }
-        } else {
-          nok = fits(0, k2);
-        }
-        if (nok) {
-          P.part_narrow = true;
-          P.part_slab = true;
-          P.part_dictid = vc >= 0 && imgk != 3;
-          P.narrow_vd = vd;
-          P.narrow_k2min = k2;
-          P.narrow_img = imgk;
-        }
-      }
-    }
-  }
-
-  // filter program
-  P.host_entries = 0;
-  int host_scan_leaves = 0;
-  std::vector<int8_t> pop, parg;
-  PNode froot;
-  P.fsm_on = false;
-  P.rprog_on = false;
-  P.dm_progs.clear();
-  P.use_docmask = q.kn.jit && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
-                                K.group_mode == G_DENSE_GLOBAL || K.group_mode == G_HASH64 ||
-                                K.group_mode == G_HASH128 || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS;
-  if (!q.filter.empty()) {
-    PNode root = build_tree(q, *segs[0]);
-    const size_t L = q.leaf_col.size();
-    bool fuse = P.use_docmask && stats_closed_form(root, q, segs, n, bindings) && q.kn.rprog != RPROG_OFF;
-    for (int s = 0; s < n && fuse; ++s) {
-      if (star_fit(q, *segs[s])) fuse = false;
-      for (size_t l = 0; l < L && fuse; ++l) {
-        const StagedColumn& c = segs[s]->col(q.leaf_col[l]);
-        const bool bitmap = c.has_inverted && !c.is_sorted && q.leaf_kind[l] != PGX_PRED_RANGE;
-        if (bitmap != (!segs[0]->col(q.leaf_col[l]).is_sorted && segs[0]->col(q.leaf_col[l]).has_inverted &&
-                       q.leaf_kind[l] != PGX_PRED_RANGE))
-          fuse = false;  // index kinds differ across segments
-        else if (bitmap && !c.inv_dev.p && !binding_empty(bindings[size_t(s) * L + l], c.card))
-          fuse = false;
-      }
-    }
-    prof_mark("p.fusechk");
-    FusePlan F;
-    if (fuse) {
-      plan_fuse(root, q, F);
-      if (F.progs.empty() || L + F.progs.size() > size_t(PGX_J_MAX_LEAVES)) fuse = false;
-      for (const auto& p : F.progs)
-        if (prog_depth(p) > 4 || p.op.size() > size_t(kMaxRProg)) fuse = false;
-    }
-    if (fuse) {
-      emit_fused(root, F, int(L), pop, parg, true, host_scan_leaves);
-      P.rprog_on = true;
-      P.dm_progs = F.progs;
-      for (auto& p : P.dm_progs) canon_rprog(p.op, p.arg);
-    } else {
-      emit(root, pop, parg, true, false, host_scan_leaves);
-    }
-    if (!stats_closed_form(root, q, segs, n, bindings)) {
-      // the automaton counts every entry: no OP_STAT popcounts, no whole-range host terms
-      P.fsm_on = true;
-      host_scan_leaves = 0;
-      std::vector<int8_t> o2, a2;
-      for (size_t i = 0; i < pop.size(); ++i)
-        if (pop[i] != OP_STAT) {
-          o2.push_back(pop[i]);
-          a2.push_back(parg[i]);
-        }
-      pop.swap(o2);
-      parg.swap(a2);
-      froot = root;
-    }
-    P.leaf_phys.assign(q.leaf_col.size(), PH_SCAN);
-    std::vector<const PNode*> todo{&root};
-    while (!todo.empty()) {
-      const PNode* x = todo.back();
-      todo.pop_back();
-      if (x->op == PGX_F_LEAF) P.leaf_phys[x->leaf] = x->phys;
-      for (const PNode& k : x->kids) todo.push_back(&k);
-    }
-  }
-  P.roar.clear();
-  P.roar_index.assign(n, std::vector<int>(q.leaf_col.size(), -1));
-  P.mask_words = 0;
-  P.roar_maxchunks = 0;
-  if (pop.size() > size_t(kMaxProg)) fail(PGX_ERR_UNSUPPORTED, "filter program too long");
-  K.prog_len = int(pop.size());
-  for (size_t i = 0; i < pop.size(); ++i) {
-    K.prog_op[i] = pop[i];
-    K.prog_arg[i] = parg[i];
-  }
-
-  prof_mark("p.head");
-  // per-segment descriptors: planned in chunks of segments (in parallel for long segment lists); each chunk keeps its
-  // blob words, pointer fixups and bitmap items with chunk-local offsets, concatenated in segment order afterwards.
-  P.ksegs.assign(n, KSeg{});
-  P.segcols.assign(n, {});
-  P.sorted_span.assign(size_t(n) * q.leaf_col.size(), 0);
-  // Per distinct (leaf, binding, cardinality) in a chunk: the leaf mode, ONE blob copy of its dictId bitset and ONE list
-  // of the dictIds whose bitmaps a bitmap leaf ORs.  Segments sharing a dictionary share their bindings
-  // (pgx_bind_predicates), so a chunk usually resolves each leaf once, whatever its segment count.
-  struct LeafMemo {
-    int8_t mode = LEAF_NONE;
-    int64_t bits_off = -1;  // chunk blob offset of the bitset copy (LEAF_SCAN_BITSET)
-    int64_t ids_off = -1;   // chunk blob offset of the dictId list (bitmap leaves), nb entries
-    int nb = 0;
-  };
-  // keyed by whether the leaf reads the inverted index: a scan-only segment's entry carries no dictId list
-  using LeafKey = std::tuple<size_t, const uint32_t*, int32_t, int32_t, int, bool>;
-  struct ChunkOut {
-    std::vector<int32_t> blob;
-    std::map<const std::vector<int32_t>*, size_t> remap_off;
-    std::map<LeafKey, LeafMemo> leaf_memo;
-    std::vector<ExecPlan::Fix> fixes;
-    std::vector<ExecPlan::RoarItem> roar;
-    std::vector<ExecPlan::MvItem> mv;
-    int64_t total_raw = 0, host_entries = 0;
-    uint64_t mask_words = 0;
-    int maxchunks = 0;
-  };
-  const int kSegsPerChunk = 64;
-  const int nchunk = (n + kSegsPerChunk - 1) / kSegsPerChunk;
-  std::vector<ChunkOut> chunks(nchunk);
-  auto plan_chunk = [&](int ci) {
-    ChunkOut& o = chunks[ci];
-    for (int s = ci * kSegsPerChunk; s < std::min(n, (ci + 1) * kSegsPerChunk); ++s) {
-      const pgx_segment& seg = *segs[s];
-      KSeg& S = P.ksegs[s];
-      S.num_docs = seg.total_raw_docs;  // MatchEntireSegment / FilterPlanNode scan range [0, totalRawDocs)
-      S.num_tiles = int32_t((int64_t(S.num_docs) + kTileRows - 1) / kTileRows);
-      o.total_raw += seg.total_raw_docs;
-      o.host_entries += int64_t(host_scan_leaves) * seg.total_raw_docs;
-      auto& segcols = P.segcols[s];
-      segcols.resize(P.qcols.size());
-      for (size_t c = 0; c < P.qcols.size(); ++c) {
-        const StagedColumn& col = seg.col(P.qcols[c]);
-        segcols[c] = &col;
-        S.fwd[c] = col.fwd;
-        S.bits[c] = int8_t(col.bits);
-        S.dict[c] = col.dict_dev;
-        S.remap[c] = nullptr;
-      }
-      for (int g = 0; g < K.num_gcols; ++g) {
-        if (!P.gdicts[g].identity) {
-          const std::vector<int32_t>* rm = P.gdicts[g].remap[s].get();
-          auto it = o.remap_off.find(rm);  // one blob copy per distinct dictionary in this chunk
-          if (it == o.remap_off.end()) {
-            it = o.remap_off.emplace(rm, o.blob.size()).first;
-            o.blob.insert(o.blob.end(), rm->begin(), rm->end());
-          }
-          o.fixes.push_back({size_t(s), 0, K.gcol[g], it->second});
-        }
-      }
-      // leaves
-      for (size_t l = 0; l < q.leaf_col.size(); ++l) {
-        const StagedColumn& col = *segcols[K.leaf_col[l]];
-        const pgx_leaf_binding& b = bindings[size_t(s) * q.leaf_col.size() + l];
-        KLeaf& L = S.leaf[l];
-        L.lo = b.lo;
-        L.hi = b.hi;
-        L.bitset = nullptr;
-        L.ranges = nullptr;
-        L.nranges = 0;
-        // matching dictIds
-        auto matches = [&](int id) -> bool {
-          if (b.words) return (b.words[id >> 5] >> (id & 31)) & 1u;
-          return id >= b.lo && id <= b.hi;
-        };
-        const bool bitmap_leaf = P.use_docmask && P.leaf_phys[l] == PH_BITMAP && col.inv_dev.p;
-        if (col.is_sorted) {
-          // SortedInvertedIndexBasedFilterOperator (additive ranges, merged), clipped to [0, totalRawDocs-1]
-          std::vector<int32_t> r;
-          for (int id = 0; id < col.card; ++id) {
-            if (!matches(id)) continue;
-            int32_t a = std::max(col.sorted_first[id], 0);
-            int32_t e = std::min(col.sorted_last[id], seg.total_raw_docs - 1);
-            if (e < a) continue;
-            if (!r.empty() && a <= r.back() + 1) r.back() = std::max(r.back(), e);
-            else { r.push_back(a); r.push_back(e); }
-          }
-          if (r.empty()) { L.mode = LEAF_NONE; continue; }
-          P.sorted_span[size_t(s) * q.leaf_col.size() + l] = (int64_t(r.front()) << 32) | int64_t(uint32_t(r.back()));
-          L.mode = LEAF_RANGES;
-          L.nranges = int32_t(r.size() / 2);
-          o.fixes.push_back({size_t(s), 1, int(l), o.blob.size()});
-          o.blob.insert(o.blob.end(), r.begin(), r.end());
-          continue;
-        }
-        const bool neg = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
-        auto mit = o.leaf_memo.find(LeafKey(l, b.words, b.lo, b.hi, col.card, bitmap_leaf));
-        if (mit == o.leaf_memo.end()) {
-          LeafMemo m;
-          if (b.words) {
-            bool any = false;
-            const int nw = (col.card + 31) / 32;
-            for (int w = 0; w < nw && !any; ++w) any = b.words[w] != 0;
-            if (any) {
-              m.mode = LEAF_SCAN_BITSET;
-              m.bits_off = int64_t(o.blob.size());
-              for (int w = 0; w < nw; ++w) o.blob.push_back(int32_t(b.words[w]));
-            }
-          } else {
-            m.mode = (b.hi < b.lo) ? LEAF_NONE : LEAF_SCAN_INTERVAL;
-          }
-          if (bitmap_leaf && m.mode != LEAF_NONE) {
-            // BitmapBasedFilterOperator (operator/filter/BitmapBasedFilterOperator.java:62-92): OR the roaring bitmaps
-            // of the matching dictIds; NEQ / NOT_IN OR the NON-matching ones and flip over the scanned doc range.  The
-            // list holds dictIds: the device reads each bitmap's offset from the staged file's own header.
-            m.ids_off = int64_t(o.blob.size());
-            auto take = [&](int id) {
-              o.blob.push_back(int32_t(id));
-              ++m.nb;
-            };
-            if (b.words) {  // walk the set (or, negated, the clear) bits of the dictId bitset
-              const int nw = (col.card + 31) / 32;
-              for (int w = 0; w < nw; ++w) {
-                uint32_t x = neg ? ~b.words[w] : b.words[w];
-                if (w == nw - 1 && (col.card & 31)) x &= (1u << (col.card & 31)) - 1u;
-                while (x) {
-                  take(w * 32 + __builtin_ctz(x));
-                  x &= x - 1u;
-                }
-              }
-            } else if (!neg) {
-              for (int id = std::max(0, b.lo); id <= std::min(b.hi, col.card - 1); ++id) take(id);
-            } else {
-              for (int id = 0; id < col.card; ++id)
-                if (id < b.lo || id > b.hi) take(id);
-            }
-          }
-          mit = o.leaf_memo.emplace(LeafKey(l, b.words, b.lo, b.hi, col.card, bitmap_leaf), m).first;
-        }
-        const LeafMemo& m = mit->second;
-        L.mode = m.mode;
-        if (m.mode == LEAF_NONE) continue;
-        if (m.mode == LEAF_SCAN_BITSET) o.fixes.push_back({size_t(s), 2, int(l), size_t(m.bits_off)});
-        if (bitmap_leaf) {
-          ExecPlan::RoarItem it{s, int(l), neg, size_t(m.ids_off), m.nb, int((int64_t(seg.total_docs) + 65535) >> 16),
-                                o.mask_words, col.inv_dev.p};
-          if (s == 0) {  // serialized bytes of the ORed bitmaps: segment 0's selectivity estimate only
-            const int32_t* ids = o.blob.data() + m.ids_off;
-            for (int k = 0; k < m.nb; ++k) it.bytes += col.inv_off[ids[k] + 1] - col.inv_off[ids[k]];
-          }
-          if (!P.rprog_on) o.mask_words += uint64_t(it.nchunks) * 2048;
-          o.maxchunks = std::max(o.maxchunks, it.nchunks);
-          o.roar.push_back(it);
-        } else if (col.is_mv && L.mode != LEAF_NONE) {
-          // MVScanDocIdIterator: the query kernel reads the doc mask pgx_mv_leaf_mask derives from the values
-          if (!P.use_docmask) fail(PGX_ERR_UNSUPPORTED, "multi-value filter needs the query kernels");
-          o.mv.push_back({s, int(l)});
-        }
-      }
-    }
-  };
-  if (nchunk > 1 && !P.serial) ctx->parallel_for(nchunk, plan_chunk);
-  else
-    for (int ci = 0; ci < nchunk; ++ci) plan_chunk(ci);
-  P.mv_items.clear();
-  P.mv_index.assign(n, std::vector<int>(q.leaf_col.size(), -1));
-  P.mv_neg.assign(q.leaf_col.size(), 0);
-  for (size_t l = 0; l < q.leaf_col.size(); ++l)
-    P.mv_neg[l] = q.leaf_kind[l] == PGX_PRED_NEQ || q.leaf_kind[l] == PGX_PRED_NOT_IN;
-  for (ChunkOut& o : chunks)
-    for (const auto& it : o.mv) {
-      P.mv_index[it.seg][it.leaf] = int(P.mv_items.size());
-      P.mv_items.push_back(it);
-    }
-  int64_t tiles = 0;
-  P.total_raw = 0;
-  for (int s = 0; s < n; ++s) {
-    P.ksegs[s].tile_begin = tiles;
-    tiles += P.ksegs[s].num_tiles;
-  }
-  prof_mark("p.chunks");
-  for (ChunkOut& o : chunks) {
-    const size_t base = P.blob32.size();
-    const uint64_t mbase = P.mask_words;
-    P.blob32.insert(P.blob32.end(), o.blob.begin(), o.blob.end());
-    for (auto f : o.fixes) {
-      f.off += base;
-      P.fixes.push_back(f);
-    }
-    for (auto it : o.roar) {
-      it.blob_off += base;
-      it.mask_off += mbase;
-      P.roar_index[it.seg][it.leaf] = int(P.roar.size());
-      P.roar.push_back(it);
-    }
-    P.mask_words += o.mask_words;
-    P.roar_maxchunks = std::max(P.roar_maxchunks, o.maxchunks);
-    P.total_raw += o.total_raw;
-    P.host_entries += o.host_entries;
-  }
-  // Bitmap programs inside the query kernels (LEAF_RCHUNK) when the filter is selective: the kernel then needs no
-  // value image (selected rows gather their values from the dictionary in HBM/L2), leaving LDS for the chunk masks and
-  // several workgroups per CU.  Selectivity estimate: segment 0's leaves, 2 serialized bytes per doc (array
-  // containers), AND / OR / NOT as independent events.  PGX_RCHUNK=0/1 forces the choice.
-  P.rchunk = false;
-  if (P.rprog_on && !P.use_part) {
-    double est = 1.0;
-    const double nd0 = std::max(1, segs[0]->total_raw_docs);
-    for (const auto& dp : P.dm_progs) {
-      std::vector<double> st;
-      for (size_t i = 0; i < dp.op.size(); ++i) {
-        if (dp.op[i] == RP_LEAF) {
-          const int ri = P.roar_index[0][dp.arg[i]];
-          double f = ri >= 0 ? std::min(1.0, double(P.roar[ri].bytes) / 2.0 / nd0) : 0.0;
-          if (ri >= 0 && P.roar[ri].neg) f = 1.0 - f;
-          st.push_back(f);
-        } else if (dp.op[i] == RP_NOT) {
-          st.back() = 1.0 - st.back();
-        } else {
-          const double b = st.back();
-          st.pop_back();
-          st.back() = dp.op[i] == RP_AND ? st.back() * b : st.back() + b - st.back() * b;
-        }
-      }
-      if (!st.empty()) est = std::min(est, st.back());  // the programs are ANDed or ORed into the tree: a bound
-    }
-    P.rchunk = est <= kRchunkMaxSel;
-    if (q.kn.rchunk >= 0) P.rchunk = q.kn.rchunk == 1;
-    for (int s = 0; s < n && P.rchunk; ++s)
-      if (star_fit(q, *segs[s])) P.rchunk = false;
-  }
-  // per (segment, bitmap program): the program over that segment's leaf descriptors and its output mask
-  P.rprogs.clear();
-  if (P.rprog_on) {
-    const size_t np = P.dm_progs.size();
-    P.rprogs.resize(size_t(n) * np);
-    for (int s = 0; s < n; ++s) {
-      const int nchunks = int((int64_t(segs[s]->total_docs) + 65535) >> 16);
-      P.roar_maxchunks = std::max(P.roar_maxchunks, nchunks);
-      for (size_t k = 0; k < np; ++k) {
-        const auto& dp = P.dm_progs[k];
-        RProg& r = P.rprogs[size_t(s) * np + k];
-        r = RProg{};
-        r.nchunks = nchunks;
-        r.num_docs = P.ksegs[s].num_docs;
-        r.mask = reinterpret_cast<uint32_t*>(uintptr_t(P.mask_words));  // word offset until the buffer exists
-        if (!P.rchunk) P.mask_words += uint64_t(nchunks) * 2048;
-        int o = 0, nl = 0;
-        for (size_t i = 0; i < dp.op.size(); ++i) {
-          if (dp.op[i] == RP_LEAF) {
-            const int ri = P.roar_index[s][dp.arg[i]];
-            r.op[o] = RP_LEAF;
-            r.arg[o++] = int16_t(ri);
-            if (nl < PGX_J_MAX_RLEAVES) r.ldesc[nl] = int16_t(ri);
-            ++nl;
-            // a leaf without matching dictIds (alwaysFalse) is empty, negated or not
-            if (ri < 0 && i + 1 < dp.op.size() && dp.op[i + 1] == RP_NOT) ++i;
-          } else {
-            r.op[o] = int8_t(dp.op[i]);
-            r.arg[o++] = 0;
-          }
-        }
-        r.nops = o;
-      }
-    }
-  }
-  prof_mark("p.merge");
-  // star-tree segments (query kernels only: the per-segment program needs the generated kernels)
-  P.star.assign(n, ExecPlan::StarPlan{});
-  if (P.use_docmask && !P.use_part && int(q.leaf_col.size()) + 8 <= PGX_J_MAX_LEAVES) {
-    tiles = 0;
-    for (int s = 0; s < n; ++s) {
-      KSeg& S = P.ksegs[s];
-      if (star_fit(q, *segs[s])) {
-        plan_star_segment(q, *segs[s], S, bindings + size_t(s) * q.leaf_col.size(), P.leaf_phys, P.blob32, P.star[s]);
-        if (int(q.leaf_col.size() + P.star[s].ranges.size()) > PGX_J_MAX_LEAVES) {
-          P.star[s] = ExecPlan::StarPlan{};
-        } else {
-          // StarTreeIndexOperator reaches aggregated docs: scan [0, totalDocs); no root scan leaf
-          P.host_entries -= int64_t(host_scan_leaves) * segs[s]->total_raw_docs;
-          S.num_docs = segs[s]->total_docs;
-        }
-      }
-      S.tile_begin = tiles;
-      S.num_tiles = int32_t((int64_t(S.num_docs) + kTileRows - 1) / kTileRows);
-      tiles += S.num_tiles;
-    }
-  }
-  K.total_tiles = tiles;
-  K.num_segs = n;
-  P.lmask_off.assign(n, -1);
-  P.lmask_words.assign(n, 0);
-  P.lmask_total = 0;
-  P.fsm_segs.clear();
-  P.fsm_chunks = 0;
-  if (P.fsm_on) {
-    const int L = int(q.leaf_col.size());
-    std::vector<FsmSegInfo> infos;
-    std::vector<int> fsegs;
-    for (int s = 0; s < n; ++s) {
-      if (!P.star.empty() && P.star[s].on) continue;  // star-tree plans count their own statistic
-      FsmSegInfo si;
-      si.num_docs = P.ksegs[s].num_docs;
-      si.sorted_first.assign(L, 0);
-      si.sorted_last.assign(L, 0);
-      for (int l = 0; l < L; ++l) {
-        const int64_t sp = P.sorted_span[size_t(s) * L + l];
-        if (sp) {
-          si.sorted_first[l] = sp >> 32;
-          si.sorted_last[l] = int32_t(uint32_t(sp));
-        }
-        if (P.ksegs[s].leaf[l].mode == LEAF_NONE && P.leaf_phys[l] == PH_SCAN) si.always_false |= 1u << l;
-      }
-      infos.push_back(std::move(si));
-      fsegs.push_back(s);
-    }
-    std::string err;
-    if (!fsegs.empty() && !fsm_build(fsm_tree(froot), L, infos, P.fsm, &err)) fail(PGX_ERR_UNSUPPORTED, err);
-    for (size_t i = 0; i < fsegs.size(); ++i) {
-      const int s = fsegs[i];
-      const int64_t nd = P.ksegs[s].num_docs;
-      P.lmask_words[s] = (nd + 31) / 32 + 1;
-      P.lmask_off[s] = int64_t(P.lmask_total);
-      P.lmask_total += uint64_t(P.lmask_words[s]) * L;
-      FsmSeg g{};
-      g.words = P.lmask_words[s];
-      g.num_docs = int32_t(nd);
-      g.chunk0 = P.fsm_chunks;
-      P.fsm_chunks += (nd + kFsmChunkRows - 1) / kFsmChunkRows;
-      const auto& iv = P.fsm.seg_intervals[i];
-      if (iv.size() > size_t(kFsmMaxIntervals)) fail(PGX_ERR_INTERNAL, "statistics automaton intervals");
-      g.nint = int32_t(iv.size());
-      for (size_t k = 0; k < iv.size(); ++k) {
-        g.ibeg[k] = iv[k].first;
-        g.itab[k] = iv[k].second;
-      }
-      P.fsm_segs.push_back(g);
-    }
-    if (P.fsm_segs.empty()) P.fsm_on = false;
-  }
-  P.rec_base.assign(n, 0);
-  P.rec_total = 0;
-  for (int s = 0; s < n; ++s) {
-    P.rec_base[s] = P.rec_total;
-    P.rec_total += P.ksegs[s].num_docs;
-  }
-
-  // grid: persistent, contiguous tile ranges per workgroup
-  const int cus = ctx->num_cus;
-  const int wgs_per_cu = (K.group_mode == G_NONE) ? 8 : 4;
-  const int64_t max_grid = int64_t(cus) * wgs_per_cu;
-  P.tiles_per_wg = std::max<int64_t>(1, (tiles + max_grid - 1) / max_grid);
-  P.grid = int(std::max<int64_t>(1, (tiles + P.tiles_per_wg - 1) / P.tiles_per_wg));
-}
-
-// Per-query device arguments live in ONE arena, written on the host into pinned memory and sent with ONE copy:
-//   [blob (ranges / bitsets / remaps) | KSeg x n | JSeg x n | outputs (agg planes, stats, overflow)]
-constexpr size_t kOutsBytes = 256;  // agg planes [0, 72), stats [128, 144), overflow [192, 200)
-struct ExecBuffers {
-  DevBuf arena;
-  PinnedBuf host;
-  size_t off_ksegs = 0, off_jsegs = 0, off_tiles = 0, off_rdesc = 0, off_rprog = 0, off_outs = 0, size = 0;
-  DevBuf table, keys, key_state, masks;
-  uint8_t* dev() const { return arena.as<uint8_t>(); }
-};
-
+namespace pgxh {
 size_t align_up(size_t x, size_t a) { return (x + a - 1) & ~(a - 1); }
 
 // Bitmap inverted-index leaves: one mask per (segment, leaf) (pgx_roaring_expand), or one mask per (segment, bitmap
@@ -2956,7 +349,7 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
   }
 }
 
-void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table = true, bool outs_only = false) {
+void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table, bool outs_only) {
   // (re)sends the whole argument arena with initialised output planes; outs_only: the arena's descriptors are already
   // on the device (a cached plan's replay: kernels write only the outputs block), send the outputs block alone
   KQuery& K = P.kq;
@@ -3599,539 +992,11 @@ uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {
   return cap;
 }
 
-// -------------------------------------------------------------------------------------------------
-// Partitioned group-by (DESIGN.md "Sparse group-by").  The query kernel writes one 8-byte record per scanned row,
-// key | (value - vbase) << keybits (~0: row not selected).  Two radix passes on independent bits of a 64-bit mix of
-// the key (128 buckets, then 2^nbits2 per bucket) split the records into partitions whose groups fit one workgroup's
-// LDS hash table; pgx_part_aggregate aggregates each partition and appends its groups.  Each pass reads the previous
-// pass's cursors on the device, so the chain runs without a host round trip until the final counters.
-// Replaces, for sparse keys, the reference's per-segment MAP-based group-key holders
-// (DefaultGroupKeyGenerator.java:239-343 LONG_MAP / ARRAY_MAP) with a layout that streams HBM instead of probing it.
-// -------------------------------------------------------------------------------------------------
-constexpr int64_t kPartGroupsPerWg = 700;   // groups per pgx_part_aggregate workgroup: LDS table load <= ~1/3 (2048 slots)
-constexpr uint64_t kPartMaxBytes = uint64_t(96) << 30;  // partition buffers beyond this: fall back to the hash table
-constexpr int kPartChunkRecs = 8192;    // records per pgx_partition workgroup (pgx_kernels.hip kPartChunk)
 
-struct PartBuffers {
-  int nbits2 = 7;                       // second pass: 2^nbits2 buckets per first-pass bucket (0: no second pass)
-  int64_t cap1 = 0, cap2 = 0, ocap = 0;
-  DevBuf out1, out2, okey, oplane, ctr;  // ctr: cursors1[kPart1N] | cursors2[nparts] (kCursorStride apart) | ocount | ovf[3]
-  DevBuf prange;                         // trim-key ranges of the groups (narrow aggregation), or none
-  bool pass2() const { return nbits2 > 0; }
-  int64_t nparts() const { return int64_t(1) << (kPart1Bits + nbits2); }
-  size_t ctr_words() const { return size_t(kPart1N + (pass2() ? nparts() : 0)) * kCursorStride + 4; }
-  int64_t out1_recs() const { return int64_t(kPart1N) * cap1; }
-};
+}  // namespace pgxh
 
-// PGX_DEBUG=part_small (tests): start from undersized buckets and one pass, and allow at most one refinement, so the
-// resize, re-split and hash-table fallback branches run at small row counts.
-bool part_debug(const ExecPlan& P) { return P.kn.part_small; }
+namespace pgxh {
 
-// second-pass split bits: up to 128 ways
-int part_max_bits2(const ExecPlan&) { return 7; }
-
-void part_size(const ExecPlan& P, PartBuffers& PB) {
-  const int64_t N = P.rec_total;
-  double ub = double(N);  // groups: at most the rows and the product of the key cardinalities
-  double prod = 1;
-  for (const auto& g : P.gdicts) prod *= double(g.card);
-  ub = std::min(ub, prod);
-  PB.nbits2 = 0;
-  while (PB.nbits2 < part_max_bits2(P) && double(int64_t(1) << (kPart1Bits + PB.nbits2)) * kPartGroupsPerWg < ub)
-    ++PB.nbits2;
-  PB.cap1 = N / kPart1N + N / 512 + 65536;
-  const int64_t np = PB.nparts();
-  PB.cap2 = N / np + N / np / 4 + 16384;
-  if (part_debug(P)) {
-    PB.nbits2 = 0;
-    PB.cap1 = N / 256 + 1;
-    PB.cap2 = 1;
-  }
-}
-
-bool part_alloc(pgx_ctx* ctx, const ExecPlan& P, PartBuffers& PB) {
-  const int64_t np = PB.nparts();
-  PB.ocap = std::max<int64_t>(1, std::min<int64_t>(P.rec_total, np * 4096));
-  const uint64_t bytes = uint64_t(PB.out1_recs()) * 8 + (PB.pass2() ? uint64_t(np) * PB.cap2 * 8 : 0) + uint64_t(PB.ocap) * 40;
-  if (bytes > kPartMaxBytes) return false;
-  PB.out1 = DevBuf(ctx, size_t(std::max<int64_t>(PB.out1_recs(), 1)) * 8);
-  if (PB.pass2()) PB.out2 = DevBuf(ctx, size_t(np) * PB.cap2 * 8);
-  PB.okey = DevBuf(ctx, size_t(PB.ocap) * 8);
-  PB.oplane = DevBuf(ctx, size_t(PB.ocap) * 4 * 8);
-  PB.ctr = DevBuf(ctx, PB.ctr_words() * 8);
-  return true;
-}
-
-// Before the scan: zero the cursors and counters (the scan writes row-order records into the plan's record array).
-void part_prepare(ExecPlan& P, PartBuffers& PB, hipStream_t st) {
-  unsigned long long* ctr = devp(PB.ctr);
-  hip_check(hipMemsetAsync(ctr, 0, PB.ctr_words() * 8, st), "partition counters");
-  P.part_cursor = nullptr;
-  P.part_overflow = nullptr;
-  P.part_cap = PB.cap1;
-}
-
-// After the scan: first pass, second pass, aggregation.
-void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
-  const int64_t N = P.rec_total;
-  unsigned long long* ctr = devp(PB.ctr);
-  const int64_t np = PB.nparts();
-  unsigned long long* c1 = ctr;
-  unsigned long long* c2 = ctr + kPart1N * kCursorStride;
-  unsigned long long* tail = ctr + PB.ctr_words() - 4;  // ocount, overflow[3]
-  if (N == 0) return;
-  const uint64_t keymask = (uint64_t(1) << P.part_keybits) - 1u;
-  {
-    const uint64_t* recs = reinterpret_cast<const uint64_t*>(P.kq.table);
-    const int64_t chunks1 = (N + kPartChunkRecs - 1) / kPartChunkRecs;
-    if (chunks1 > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
-    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(recs, nullptr, nullptr, 1, 1, 1, N, int(chunks1), keymask,
-                                   64 - kPart1Bits, kPart1Bits, PB.out1.as<uint64_t>(), PB.cap1, c1, kCursorStride,
-                                   tail + 1, st),
-              "partition pass 1");
-  }
-  const uint64_t* ain = PB.out1.as<uint64_t>();
-  const unsigned long long* acnt = c1;
-  int64_t acap = PB.cap1;
-  int aparts = kPart1N;
-  if (PB.pass2()) {
-    const int64_t nreg = kPart1N;
-    const int64_t chunks2 = (PB.cap1 + kPartChunkRecs - 1) / kPartChunkRecs;
-    if (chunks2 * nreg > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "too many rows for one partitioned group-by");
-    PGX_LAUNCH(st, "pgx_partition", pgx_launch_partition(PB.out1.as<uint64_t>(), nullptr, c1, kCursorStride, int(nreg),
-                                   1, PB.cap1,
-                                   int(chunks2), keymask, 64 - kPart1Bits - PB.nbits2, PB.nbits2,
-                                   PB.out2.as<uint64_t>(), PB.cap2, c2, kCursorStride, tail + 2, st),
-              "partition pass 2");
-    ain = PB.out2.as<uint64_t>();
-    acnt = c2;
-    acap = PB.cap2;
-    aparts = int(np);
-  }
-  // count and sum share one LDS add when a partition's count and value sum both fit their bit fields
-  const int cbits = bits_for(acap + 1);
-  const int pack_shift = (2 * cbits + P.part_vbits <= 64) ? 64 - cbits : 0;
-  PGX_LAUNCH(st, "pgx_part_aggregate", pgx_launch_part_aggregate(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits, P.part_vbase,
-                                      P.part_sum, P.part_min, P.part_max,
-                                      pack_shift, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(), PB.ocap, tail,
-                                      tail + 3, st),
-            "partition aggregate");
-}
-
-// Scan (records), partition passes and aggregation; grows the buffers to the measured bucket sizes when a pass
-// overflowed.  False: the groups do not fit the partitioned layout (the caller uses the global hash table).
-bool run_partitioned(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB, hipStream_t st) {
-  alloc_outputs(ctx, P, B, nullptr, 0);
-  part_size(P, PB);
-  for (int attempt = 0; attempt < 12; ++attempt) {
-    if (!part_alloc(ctx, P, PB)) return false;
-    part_prepare(P, PB, st);
-    if (attempt == 0) {
-      reset_outputs(P, B, st);
-      launch_scan(P, st);
-    }
-    part_enqueue(P, PB, st);
-    unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
-    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
-    unsigned long long* tail = outs + 28;  // spare words of the outputs block
-    hip_check(hipMemcpyAsync(tail, devp(PB.ctr) + PB.ctr_words() - 4, 32, hipMemcpyDeviceToHost, st), "D2H");
-    hip_check(hipStreamSynchronize(st), "sync");
-    if (!tail[1] && !tail[2] && !tail[3]) return true;
-    std::vector<unsigned long long> c(PB.ctr_words());
-    hip_check(hipMemcpy(c.data(), PB.ctr.p, c.size() * 8, hipMemcpyDeviceToHost), "counters D2H");
-    auto max_cursor = [&](size_t first, int64_t count) {
-      unsigned long long m = 0;
-      for (int64_t i = 0; i < count; ++i) m = std::max(m, c[first + size_t(i) * kCursorStride]);
-      return int64_t(m);
-    };
-    if (tail[1]) {  // a first-pass bucket overflowed: size to the largest (cursors count every record)
-      PB.cap1 = max_cursor(0, kPart1N) + 1024;
-      continue;
-    }
-    if (tail[2]) {
-      PB.cap2 = max_cursor(kPart1N * kCursorStride, PB.nparts()) + 1024;
-      continue;
-    }
-    if (PB.nbits2 == (part_debug(P) ? 1 : part_max_bits2(P))) return false;  // an LDS table overflowed at the finest split
-    ++PB.nbits2;
-    const int64_t np = PB.nparts();
-    PB.cap2 = P.rec_total / np + P.rec_total / np / 4 + (part_debug(P) ? 1 : 16384);
-  }
-  return false;
-}
-
-// -------------------------------------------------------------------------------------------------
-// Narrow partitioned group-by (pgx_narrow.hip): the scan's 256-way split into per-workgroup slabs of u32 (+ u16)
-// dictId records, pgx_narrow_split into 2^(8 + k2) partitions of u32 records, pgx_narrow_aggregate with wavefront-
-// private LDS tables and the value image.  Capacities are sized from the row counts with an 8-sigma margin over the
-// binomial bucket sizes a uniform mix gives; a skewed key distribution that overflows one falls back to the 8-byte
-// radix path (run_partitioned), which sizes from measured counts.
-// -------------------------------------------------------------------------------------------------
-constexpr int kNarrowSlots = 192;  // pgx_narrow.hip kNASlots: one wavefront's table
-constexpr int kNarrowMaxWg = 1024; // pgx_narrow.hip kN2MaxSlabs
-
-struct NarrowBuffers {
-  int k2 = 0, rb1 = 0, rb2 = 0, cshift = 0;
-  bool hib = false;
-  int64_t nwg = 0, cap1 = 0, cap2 = 0, ocap = 0, nparts = 0;
-  DevBuf lo1, hi1, cnt1, rec2, cnt2, okey, oplane, ctr;  // ctr: ocount | overflow scan | split | aggregation
-  DevBuf prange;  // trim-key ranges: [kind] smallest, [4 + kind] largest (pgx_trim.hip)
-};
-
-// mean + 8 sigma (binomial, p small) + slack, a multiple of 32: slabs then start on 128-byte lines (u32 records) and
-// 64-byte lines (u16), so the scan's whole 32-record units are whole lines
-int64_t narrow_cap(double m, int64_t slack) {
-  const int64_t c = int64_t(m + 8.0 * std::sqrt(std::max(m, 1.0))) + slack;
-  return (c + 31) & ~int64_t(31);
-}
-
-bool narrow_size(const ExecPlan& P, NarrowBuffers& NB) {
-  const int K = P.part_keybits;
-  NB.rb1 = K - kNarrow1Bits;
-  NB.hib = NB.rb1 + P.narrow_vd > 32;
-  NB.nwg = P.part_nwg;
-  if (NB.nwg < 1 || NB.nwg > kNarrowMaxWg) return false;
-  // second split: what the record width needs, finer while partitions would average more than 64 groups
-  double ub = double(P.rec_total), prod = 1;
-  for (const auto& g : P.gdicts) prod *= double(g.card);
-  ub = std::min(ub, prod);
-  NB.k2 = P.narrow_k2min;
-  while (NB.k2 < kNarrowMaxBits2 && NB.k2 < NB.rb1 && ub / double(int64_t(1) << (kNarrow1Bits + NB.k2)) > 64.0) ++NB.k2;
-  if (P.kn.narrow_k2 >= 0)  // tests (PGX_DEBUG=narrow_k2=N): coarser partitions, to drive the table-overflow fallback
-    NB.k2 = std::max(P.narrow_k2min, std::min(P.kn.narrow_k2, std::min(kNarrowMaxBits2, NB.rb1)));
-  if (NB.k2 > kNarrowMaxBits2 || NB.k2 > NB.rb1) return false;
-  NB.rb2 = NB.rb1 - NB.k2;
-  if (NB.rb2 + P.narrow_vd > 32 || NB.rb2 > 31) return false;
-  NB.nparts = int64_t(1) << (kNarrow1Bits + NB.k2);
-  NB.cap1 = narrow_cap(double(P.part_wg_rows) / (1 << kNarrow1Bits), 64);
-  // a partition holds whole groups, so its record count varies more than a binomial: start at 1.5x the mean (C3: ~6
-  // sigma of the group-clumped spread) and resize from the measured fills if that is not enough (run_narrow)
-  NB.cap2 = narrow_cap(1.5 * double(P.rec_total) / double(NB.nparts), 64);
-  if (NB.cap1 * NB.nwg >= (int64_t(1) << 32) || NB.cap2 >= (int64_t(1) << 31)) return false;
-  // count and value-offset sum of one group in one u64: count < 2^cb (a partition holds <= cap2 records)
-  const int cb = bits_for(NB.cap2 + 1);
-  const long double smax = (long double)NB.cap2 * (long double)P.narrow_vrange;
-  int sb = 1;
-  while (sb < 64 && std::ldexp(1.0L, sb) <= smax) ++sb;
-  if (cb + sb > 64 || cb > 62) return false;
-  NB.cshift = 64 - cb;
-  NB.ocap = std::max<int64_t>(1, std::min<int64_t>(P.rec_total, NB.nparts * kNarrowSlots));
-  const uint64_t bytes = uint64_t(kNarrow1Bits == 8 ? 256 : (1 << kNarrow1Bits)) * NB.nwg * NB.cap1 * (NB.hib ? 6 : 4) +
-                         uint64_t(NB.nparts) * NB.cap2 * 4 + uint64_t(NB.ocap) * 40;
-  return bytes <= kPartMaxBytes;
-}
-
-void narrow_alloc(pgx_ctx* ctx, NarrowBuffers& NB) {
-  const int64_t slabs = int64_t(1 << kNarrow1Bits) * NB.nwg;
-  NB.lo1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 4);
-  if (NB.hib) NB.hi1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 2);
-  NB.cnt1 = DevBuf(ctx, size_t(slabs) * 8);
-  NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4);
-  NB.cnt2 = DevBuf(ctx, size_t(NB.nparts) * 4);
-  NB.okey = DevBuf(ctx, size_t(NB.ocap) * 8);
-  NB.oplane = DevBuf(ctx, size_t(NB.ocap) * 4 * 8);
-  NB.ctr = DevBuf(ctx, 4 * 8);
-  NB.prange = DevBuf(ctx, 8 * 8);
-}
-
-// Before the scan: zero the slab fills (workgroups without tiles publish none) and the counters; point the scan's
-// record outputs at the slabs.
-void narrow_prepare(ExecPlan& P, NarrowBuffers& NB, hipStream_t st) {
-  hip_check(hipMemsetAsync(NB.cnt1.p, 0, size_t(int64_t(1 << kNarrow1Bits) * NB.nwg) * 8, st), "slab counters");
-  hip_check(hipMemsetAsync(NB.ctr.p, 0, 32, st), "narrow counters");
-  P.kq.table = reinterpret_cast<unsigned long long*>(NB.lo1.p);
-  P.part_hi = NB.hib ? NB.hi1.as<unsigned short>() : nullptr;
-  P.part_cursor = devp(NB.cnt1);
-  P.part_overflow = devp(NB.ctr) + 1;
-  P.part_cap = NB.cap1;
-}
-
-// After the scan: the second split and the aggregation.
-void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStream_t st) {
-  if (P.rec_total == 0) return;
-  hip_check(hipMemsetAsync(NB.prange.p, 0xFF, 32, st), "range minima");
-  hip_check(hipMemsetAsync(static_cast<uint8_t*>(NB.prange.p) + 32, 0, 32, st), "range maxima");
-  unsigned long long* ctr = devp(NB.ctr);
-  PGX_LAUNCH(st, "pgx_narrow_split",
-             pgx_launch_narrow_split(NB.lo1.as<uint32_t>(), NB.hib ? NB.hi1.as<uint16_t>() : nullptr, devp(NB.cnt1),
-                                     1 << kNarrow1Bits, int(NB.nwg), NB.cap1, NB.rb1, NB.k2, NB.rec2.as<uint32_t>(),
-                                     NB.cap2, NB.cnt2.as<unsigned int>(), ctr + 2, st),
-             "narrow split");
-  PGX_LAUNCH(st, "pgx_narrow_aggregate",
-             pgx_launch_narrow_aggregate(NB.rec2.as<uint32_t>(), NB.cnt2.as<unsigned int>(), NB.cap2, int(NB.nparts),
-                                         NB.rb2, P.part_keybits, P.part_vbase, P.narrow_img, P.narrow_imgp,
-                                         P.narrow_img_words, P.narrow_img_sh, P.part_vdict, P.part_sum, P.part_min,
-                                         P.part_max, NB.cshift, NB.okey.as<uint64_t>(), NB.oplane.as<uint64_t>(),
-                                         NB.ocap, ctr, devp(NB.prange),
-                                         // an LDS image allows one workgroup per CU; the tables alone, four
-                                         ctx->num_cus * (P.narrow_img == 3 ? 4 : 1), st),
-             "narrow aggregate");
-}
-
-// Scan, split and aggregation once.  False (nothing usable produced): a capacity ran over, or the plan does not fit the
-// narrow layout; the caller re-plans the query kernels for the radix path.
-bool run_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hipStream_t st) {
-  alloc_outputs(ctx, P, B, nullptr, 0);
-  if (!narrow_size(P, NB)) {
-    if (P.kn.narrow_log)
-      std::fprintf(stderr, "[pgx narrow] layout does not fit: nwg=%lld keybits=%d vd=%d k2=%d cap1=%lld cap2=%lld\n",
-                   (long long)NB.nwg, P.part_keybits, P.narrow_vd, NB.k2, (long long)NB.cap1, (long long)NB.cap2);
-    return false;
-  }
-  narrow_alloc(ctx, NB);
-  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
-  unsigned long long* tail = outs + 28;  // spare words of the outputs block: ocount, overflows (part_result reads [28])
-  bool scan = true, ok = false;
-  int attempt = 0;
-  for (; attempt < 4 && !ok; ++attempt) {
-    if (scan) {
-      narrow_prepare(P, NB, st);
-      reset_outputs(P, B, st);
-      launch_scan(P, st);
-    } else {
-      hip_check(hipMemsetAsync(NB.ctr.p, 0, 8, st), "group counter");
-      hip_check(hipMemsetAsync(devp(NB.ctr) + 2, 0, 16, st), "overflow counters");
-    }
-    narrow_enqueue(ctx, P, NB, st);
-    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
-    hip_check(hipMemcpyAsync(tail, NB.ctr.p, 32, hipMemcpyDeviceToHost, st), "D2H");
-    hip_check(hipStreamSynchronize(st), "sync");
-    ok = !tail[1] && !tail[2] && !tail[3];
-    if (ok || (tail[3] && !tail[1] && !tail[2])) break;  // done, or a wavefront table overflowed: no resize helps
-    // a capacity ran over (keys clump: a partition holds whole groups): resize to the measured fills and rerun what
-    // depends on it -- the split and the aggregation, and the scan only if a slab overflowed
-    if (tail[1]) {
-      std::vector<unsigned long long> c(size_t(1 << kNarrow1Bits) * NB.nwg);
-      hip_check(hipMemcpy(c.data(), NB.cnt1.p, c.size() * 8, hipMemcpyDeviceToHost), "slab fills D2H");
-      NB.cap1 = narrow_cap(double(*std::max_element(c.begin(), c.end())), 64);
-      const int64_t slabs = int64_t(1 << kNarrow1Bits) * NB.nwg;
-      if (NB.cap1 * NB.nwg >= (int64_t(1) << 32) || uint64_t(slabs) * NB.cap1 * 6 > kPartMaxBytes) break;
-      NB.lo1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 4);
-      if (NB.hib) NB.hi1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 2);
-      scan = true;
-      continue;  // the split's fills are void: it read truncated slabs
-    }
-    std::vector<unsigned int> c2(size_t(NB.nparts));
-    hip_check(hipMemcpy(c2.data(), NB.cnt2.p, c2.size() * 4, hipMemcpyDeviceToHost), "partition fills D2H");
-    NB.cap2 = narrow_cap(double(*std::max_element(c2.begin(), c2.end())), 64);
-    if (NB.cap2 >= (int64_t(1) << 31) || uint64_t(NB.nparts) * NB.cap2 * 4 > kPartMaxBytes) break;
-    const int cb = bits_for(NB.cap2 + 1);
-    const long double smax = (long double)NB.cap2 * (long double)P.narrow_vrange;
-    int sb = 1;
-    while (sb < 64 && std::ldexp(1.0L, sb) <= smax) ++sb;
-    if (cb + sb > 64 || cb > 62) break;
-    NB.cshift = 64 - cb;
-    NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4);
-    scan = false;
-  }
-  if (P.kn.narrow_log)  // tests (PGX_DEBUG=narrow_log): which path ran
-    std::fprintf(stderr, "[pgx narrow] nwg=%lld cap1=%lld k2=%d cap2=%lld groups=%llu ovf=%llu/%llu/%llu attempts=%d ok=%d\n",
-                 (long long)NB.nwg, (long long)NB.cap1, NB.k2, (long long)NB.cap2, tail[0], tail[1], tail[2], tail[3],
-                 attempt + (ok ? 1 : 0), int(ok));
-  return ok;
-}
-
-// A kept narrow plan again (plan cache): the slabs and partitions are the first run's, the group outputs (handed to
-// that run's result) are allocated anew.  False if a capacity ran over (the caller plans afresh).
-bool replay_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hipStream_t st) {
-  alloc_outputs(ctx, P, B, nullptr, 0);
-  NB.okey = DevBuf(ctx, size_t(NB.ocap) * 8);
-  NB.oplane = DevBuf(ctx, size_t(NB.ocap) * 4 * 8);
-  NB.prange = DevBuf(ctx, 8 * 8);
-  narrow_prepare(P, NB, st);
-  reset_outputs(P, B, st);
-  launch_scan(P, st);
-  narrow_enqueue(ctx, P, NB, st);
-  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
-  unsigned long long* tail = outs + 28;
-  hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
-  hip_check(hipMemcpyAsync(tail, NB.ctr.p, 32, hipMemcpyDeviceToHost, st), "D2H");
-  hip_check(hipStreamSynchronize(st), "sync");
-  return !tail[1] && !tail[2] && !tail[3];
-}
-
-// A kept radix plan again (plan cache): buckets and partitions as the first run sized them, the group outputs anew.
-bool replay_part(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB, hipStream_t st) {
-  alloc_outputs(ctx, P, B, nullptr, 0);
-  PB.okey = DevBuf(ctx, size_t(PB.ocap) * 8);
-  PB.oplane = DevBuf(ctx, size_t(PB.ocap) * 4 * 8);
-  part_prepare(P, PB, st);
-  reset_outputs(P, B, st);
-  launch_scan(P, st);
-  part_enqueue(P, PB, st);
-  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
-  unsigned long long* tail = outs + 28;
-  hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
-  hip_check(hipMemcpyAsync(tail, devp(PB.ctr) + PB.ctr_words() - 4, 32, hipMemcpyDeviceToHost, st), "D2H");
-  hip_check(hipStreamSynchronize(st), "sync");
-  return !tail[1] && !tail[2] && !tail[3];
-}
-
-// The radix path's plan after a narrow attempt gave up: row-order 8-byte value records.
-void narrow_fallback(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
-  P.part_narrow = false;
-  P.part_slab = false;
-  P.part_dictid = false;
-  P.part_hi = nullptr;
-  plan_jit(ctx, q, segs, n, P, B);
-}
-
-}  // namespace
-
-// Decode n groups of a device-resident result (packed keys; planes p at planes[p * n], p = 0 count, 1 int64 sum,
-// 2 ordered min, 3 ordered max: pgx_part_aggregate) into column / function-major outputs of stride out_stride.
-void pgx_result::decode_lazy(const uint64_t* keys, const uint64_t* planes, int64_t n, int64_t out_stride,
-                             int32_t* seg_index, int32_t* dict_id, double* value, int64_t* count) const {
-  const Lazy& L = *lazy;
-  const int ncols = int(L.gshift.size());
-  for (int g = 0; g < ncols; ++g) {
-    const uint64_t mask = (uint64_t(1) << L.gbits[g]) - 1u;
-    for (int64_t i = 0; i < n; ++i) {
-      const uint64_t gid = (keys[i] >> L.gshift[g]) & mask;
-      if (seg_index) seg_index[g * out_stride + i] = (*L.rep_seg)[g][gid];
-      if (dict_id) dict_id[g * out_stride + i] = (*L.rep_id)[g][gid];
-    }
-  }
-  for (int a = 0; a < int(L.agg_kind.size()); ++a) {
-    const int k = L.agg_kind[a];
-    const int p = k == A_COUNT ? 0 : (k == A_MIN ? 2 : (k == A_MAX ? 3 : 1));
-    const int op = k == A_MIN ? P_MIN_ORD : (k == A_MAX ? P_MAX_ORD : P_ADD_I64);
-    for (int64_t i = 0; i < n; ++i) {
-      if (count) count[a * out_stride + i] = int64_t(planes[i]);
-      if (value) value[a * out_stride + i] = decode_plane(op, false, planes[size_t(p) * n + i], k);
-    }
-  }
-}
-
-// Read the partitioned group-by's groups back and decode them into the columnar host result.
-void pgx_result::materialize() {
-  if (!lazy) return;
-  const int64_t ng = num_groups;
-  hip_check(hipSetDevice(lazy->ctx->device), "hipSetDevice");
-  std::vector<uint64_t> keys(ng), pl(size_t(4) * ng);
-  if (ng) {
-    hip_check(hipMemcpy(keys.data(), lazy->okey.p, ng * 8, hipMemcpyDeviceToHost), "group keys D2H");
-    for (int p = 0; p < 4; ++p)
-      hip_check(hipMemcpy(pl.data() + p * ng, lazy->oplane.as<uint64_t>() + p * lazy->ocap, ng * 8,
-                          hipMemcpyDeviceToHost),
-                "group planes D2H");
-  }
-  const int ncols = int(lazy->gshift.size()), na = int(lazy->agg_kind.size());
-  std::vector<int32_t> seg(size_t(ncols) * ng), id(size_t(ncols) * ng);
-  std::vector<double> val(size_t(na) * ng);
-  std::vector<int64_t> cnt(size_t(na) * ng);
-  decode_lazy(keys.data(), pl.data(), ng, ng, seg.data(), id.data(), val.data(), cnt.data());
-  key_seg.assign(ncols, {});
-  key_id.assign(ncols, {});
-  for (int g = 0; g < ncols; ++g) {
-    key_seg[g].assign(seg.begin() + g * ng, seg.begin() + (g + 1) * ng);
-    key_id[g].assign(id.begin() + g * ng, id.begin() + (g + 1) * ng);
-  }
-  g_value.assign(na, {});
-  g_count.assign(na, {});
-  for (int a = 0; a < na; ++a) {
-    g_value[a].assign(val.begin() + a * ng, val.begin() + (a + 1) * ng);
-    g_count[a].assign(cnt.begin() + a * ng, cnt.begin() + (a + 1) * ng);
-  }
-  lazy.reset();
-}
-
-// Combine trim of a device-resident result (pgx_trim.hip): indices of the `size` best groups for function fn, best
-// first (ties in index order).  The first call selects for EVERY function of the result in one set of launches (one
-// range pass, <= 8 histogram passes, one select, all functions side by side) and keeps the selections.
-const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
-  Lazy& L = *lazy;
-  const int nf = int(L.agg_kind.size());
-  if (int(L.trims.size()) < nf) L.trims.resize(nf);
-  if (!L.trims[fn].empty() && L.trim_size == size) return L.trims[fn];
-  hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
-  hipStream_t st = L.ctx->stream;
-  std::vector<int> kinds(nf);
-  for (int f = 0; f < nf; ++f) {
-    const int k = L.agg_kind[f];
-    kinds[f] = k == A_COUNT ? 0 : k == A_SUM ? 1 : k == A_MIN ? 2 : k == A_MAX ? 3 : 4;
-  }
-  const size_t sb = pgx_trim_state_bytes();
-  std::vector<uint8_t> init(sb * nf, 0);
-  const int64_t want = size;
-  const uint64_t kmin0 = ~0ull;
-  for (int f = 0; f < nf; ++f) {
-    std::memcpy(init.data() + f * sb + 16, &want, 8);   // TrimState.k
-    std::memcpy(init.data() + f * sb + 48, &kmin0, 8);  // TrimState.kmin
-  }
-  DevBuf state(L.ctx, sb * nf), idx(L.ctx, size_t(size) * 8 * nf), keys(L.ctx, size_t(size) * 8 * nf);
-  hip_check(hipMemcpyAsync(state.p, init.data(), init.size(), hipMemcpyHostToDevice, st), "trim state H2D");
-  const int grid = int(std::max<int64_t>(1, std::min<int64_t>((num_groups + 255) / 256, int64_t(L.ctx->num_cus) * 8)));
-  // candidate lists after the first digit (pgx_trim_cand): room for 32x the groups wanted, at least 1M (a MAX
-  // threshold's bin at C3 holds a few 100k groups), at most every group
-  const int64_t ccap = std::min<int64_t>(num_groups, std::max<int64_t>(int64_t(1) << 20, 32 * size));
-  DevBuf cidx(L.ctx, size_t(std::max<int64_t>(ccap, 1)) * 8 * nf), ckey(L.ctx, size_t(std::max<int64_t>(ccap, 1)) * 8 * nf);
-  PGX_LAUNCH(st, "pgx_trim", pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kinds.data(), nf, state.p,
-                            idx.as<int64_t>(), keys.as<uint64_t>(), size, grid,
-                            L.prange.p ? devp(L.prange) : nullptr, cidx.as<int64_t>(), ckey.as<uint64_t>(), ccap, st),
-            "trim launch");
-  std::vector<int64_t> ix(size_t(size) * nf);
-  std::vector<uint64_t> ky(size_t(size) * nf);
-  hip_check(hipMemcpyAsync(ix.data(), idx.p, ix.size() * 8, hipMemcpyDeviceToHost, st), "trim D2H");
-  hip_check(hipMemcpyAsync(ky.data(), keys.p, ky.size() * 8, hipMemcpyDeviceToHost, st), "trim D2H");
-  hip_check(hipStreamSynchronize(st), "sync");
-  L.trim_size = size;
-  for (int f = 0; f < nf; ++f) {
-    const int64_t* fi = ix.data() + size_t(f) * size;
-    const uint64_t* fk = ky.data() + size_t(f) * size;
-    std::vector<int64_t> order(size);
-    std::iota(order.begin(), order.end(), 0);
-    std::sort(order.begin(), order.end(),
-              [&](int64_t a, int64_t b) { return fk[a] != fk[b] ? fk[a] > fk[b] : fi[a] < fi[b]; });
-    std::vector<int64_t>& out = L.trims[f];
-    out.resize(size);
-    for (int64_t i = 0; i < size; ++i) out[i] = fi[order[i]];
-  }
-  return L.trims[fn];
-}
-
-namespace {
-
-void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, PartBuffers& PB, pgx_result* R) {
-  const unsigned long long* outs = reinterpret_cast<const unsigned long long*>(B.host.bytes() + B.off_outs);
-  const unsigned long long* stats = outs + 16;
-  const KQuery& K = P.kq;
-  R->stats[0] = int64_t(stats[0]);
-  R->stats[1] = int64_t(stats[1]) + P.host_entries;
-  R->stats[2] = int64_t(stats[0]) * P.n_proj;
-  R->stats[3] = P.total_raw;
-  R->num_aggs = K.num_aggs;
-  R->agg_fn = q.agg_fn;
-  R->top_n = q.top_n;
-  R->group_by = true;
-  R->mode = P.mode_ref;
-  R->num_groups = int64_t(std::min<unsigned long long>(outs[28], uint64_t(PB.ocap)));
-  auto L = std::make_unique<pgx_result::Lazy>();
-  L->okey = std::move(PB.okey);
-  L->oplane = std::move(PB.oplane);
-  L->prange = std::move(PB.prange);
-  L->ocap = PB.ocap;
-  if (!P.lazy_rep_seg) {  // the key tables move to shared storage once (a kept plan's replays share them)
-    auto rs = std::make_shared<std::vector<std::vector<int32_t>>>();
-    auto ri = std::make_shared<std::vector<std::vector<int32_t>>>();
-    for (int g = 0; g < K.num_gcols; ++g) {
-      rs->push_back(std::move(P.gdicts[g].rep_seg));
-      ri->push_back(std::move(P.gdicts[g].rep_id));
-    }
-    P.lazy_rep_seg = std::move(rs);
-    P.lazy_rep_id = std::move(ri);
-  }
-  for (int g = 0; g < K.num_gcols; ++g) {
-    L->gshift.push_back(K.gshift[g]);
-    L->gbits.push_back(P.gbits[g]);
-  }
-  L->rep_seg = P.lazy_rep_seg;
-  L->rep_id = P.lazy_rep_id;
-  for (int a = 0; a < K.num_aggs; ++a) L->agg_kind.push_back(K.agg_kind[a]);
-  ctx->refs.fetch_add(1);
-  L->ctx = ctx;
-  R->lazy = std::move(L);
-}
 
 // PGX_DEBUG=host_profile: per-phase host wall time of every pgx_execute on stderr (host overhead hunting).
 struct HostProf {
@@ -4351,364 +1216,6 @@ bool run_batched(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int
   return true;
 }
 
-// Multi-value functions (Count/Sum/Min/Max/AvgMVAggregationFunction, operator/aggregation/function/*MV*.java),
-// aggregation-only: the single-value part of the query (its filter and SV functions, or COUNT(*) alone) runs through
-// the query kernels, which also write every scanned row's selection bit; pgx_mv_aggregate then folds every value of
-// every selected doc of each MV column (count, int64 / f64 sum, min / max over the sorted dictionary's ids).
-void run_mv(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
-            uint32_t xflags, pgx_result* R, hipStream_t st) {
-  if (!q.group_cols.empty()) fail(PGX_ERR_UNSUPPORTED, "multi-value functions with GROUP BY");
-  if (!q.kn.jit) fail(PGX_ERR_UNSUPPORTED, "multi-value functions need the query kernels");
-  pgx_query qs = q;
-  qs.flags |= PGX_Q_NO_STAR_TREE;  // every raw row gets its selection bit
-  qs.agg_fn.clear();
-  qs.agg_col.clear();
-  std::vector<int> sv_pos(q.agg_fn.size(), -1), mv_pos(q.agg_fn.size(), -1);
-  std::vector<std::string> mv_cols;
-  for (size_t a = 0; a < q.agg_fn.size(); ++a) {
-    if (q.agg_fn[a] >= PGX_COUNTMV) {
-      const std::string& c = q.agg_col[a];
-      for (int s = 0; s < n; ++s) {
-        const StagedColumn& col = segs[s]->col(c);
-        if (!col.is_mv) fail(PGX_ERR_UNSUPPORTED, "multi-value function on single-value column " + c);
-        if (col.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + c);
-      }
-      auto it = std::find(mv_cols.begin(), mv_cols.end(), c);
-      mv_pos[a] = int(it - mv_cols.begin());
-      if (it == mv_cols.end()) mv_cols.push_back(c);
-    } else {
-      sv_pos[a] = int(qs.agg_fn.size());
-      qs.agg_fn.push_back(q.agg_fn[a]);
-      qs.agg_col.push_back(q.agg_col[a]);
-    }
-  }
-  if (qs.agg_fn.empty()) {
-    qs.agg_fn.push_back(PGX_COUNT);
-    qs.agg_col.push_back("");
-  }
-  ExecPlan P;
-  P.want_selmask = true;
-  plan_query(ctx, qs, segs, n, bindings, xflags, P);
-  P.sel_off.assign(n, 0);
-  int64_t words = 0;
-  int max_words = 0;
-  for (int s = 0; s < n; ++s) {
-    P.sel_off[s] = words;
-    const int w = (P.ksegs[s].num_docs + 31) / 32 + 1;
-    words += w;
-    max_words = std::max(max_words, w);
-  }
-  P.sel_buf = DevBuf(ctx, size_t(std::max<int64_t>(words, 1)) * 4);
-  hip_check(hipMemsetAsync(P.sel_buf.p, 0, size_t(std::max<int64_t>(words, 1)) * 4, st), "selection masks");
-  ExecBuffers B;
-  upload_plan(ctx, P, B, st);
-  plan_jit(ctx, qs, segs, n, P, B);
-  if (P.jit.empty()) fail(PGX_ERR_UNSUPPORTED, "multi-value functions need the query kernels");
-  alloc_outputs(ctx, P, B, nullptr, 0);
-  reset_outputs(P, B, st);
-  launch_scan(P, st);
-  // one item per (segment, MV column); outputs [count, sum, ordered min, ordered max] per column
-  std::vector<unsigned long long> init(mv_cols.size() * 4, 0ull);
-  for (size_t k = 0; k < mv_cols.size(); ++k) init[4 * k + 2] = ~0ull;
-  DevBuf outs(ctx, init.size() * 8);
-  hip_check(hipMemcpy(outs.p, init.data(), init.size() * 8, hipMemcpyHostToDevice), "MV outputs init");
-  std::vector<MvAgg> items;
-  std::vector<int> fp(mv_cols.size(), 0);
-  for (size_t k = 0; k < mv_cols.size(); ++k)
-    for (int s = 0; s < n; ++s) {
-      const StagedColumn& col = segs[s]->col(mv_cols[k]);
-      fp[k] = col.data_type == PGX_FLOAT || col.data_type == PGX_DOUBLE;
-      MvAgg m{};
-      m.vals = col.fwd;
-      m.start = col.mv_start.as<const int32_t>();
-      m.sel = P.sel_buf.as<uint32_t>() + P.sel_off[s];
-      m.dict = col.dict_dev;
-      m.out = outs.as<unsigned long long>() + 4 * k;
-      m.bits = col.bits;
-      m.num_docs = P.ksegs[s].num_docs;
-      m.fp = fp[k];
-      items.push_back(m);
-    }
-  DevBuf idev(ctx, std::max<size_t>(1, items.size()) * sizeof(MvAgg));
-  hip_check(hipMemcpy(idev.p, items.data(), items.size() * sizeof(MvAgg), hipMemcpyHostToDevice), "MV items H2D");
-  PGX_LAUNCH(st, "pgx_mv_aggregate", pgx_launch_mv_aggregate(idev.as<MvAgg>(), int(items.size()), max_words, st), "multi-value aggregation");
-  pgx_result Rs;
-  finish_result(ctx, qs, P, B, segs, n, st, &Rs, nullptr);
-  std::vector<unsigned long long> res(init.size());
-  hip_check(hipMemcpy(res.data(), outs.p, res.size() * 8, hipMemcpyDeviceToHost), "MV outputs D2H");
-  // assemble in the request's order; numEntriesScannedPostFilter counts the MV columns among the projected ones
-  int extra = 0;
-  for (const auto& c : mv_cols)
-    if (std::find(qs.agg_col.begin(), qs.agg_col.end(), c) == qs.agg_col.end()) ++extra;
-  for (int i = 0; i < 4; ++i) R->stats[i] = Rs.stats[i];
-  R->stats[2] = Rs.stats[0] * (P.n_proj + extra);
-  R->num_aggs = int(q.agg_fn.size());
-  R->agg_fn = q.agg_fn;
-  R->top_n = q.top_n;
-  R->group_by = false;
-  R->mode = Rs.mode;
-  R->agg_value.assign(q.agg_fn.size(), 0.0);
-  R->agg_count.assign(q.agg_fn.size(), 0);
-  for (size_t a = 0; a < q.agg_fn.size(); ++a) {
-    if (sv_pos[a] >= 0) {
-      R->agg_value[a] = Rs.agg_value[sv_pos[a]];
-      R->agg_count[a] = Rs.agg_count[sv_pos[a]];
-      continue;
-    }
-    const int k = mv_pos[a];
-    const unsigned long long* o = &res[4 * size_t(k)];
-    const int64_t cnt = int64_t(o[0]);
-    double sum;
-    if (fp[k]) std::memcpy(&sum, &o[1], 8);
-    else sum = double(int64_t(o[1]));
-    R->agg_count[a] = cnt;
-    switch (q.agg_fn[a]) {
-      case PGX_COUNTMV: R->agg_value[a] = double(cnt); break;
-      case PGX_MINMV: R->agg_value[a] = decode_plane(P_MIN_ORD, fp[k], o[2], PGX_MIN); break;
-      case PGX_MAXMV: R->agg_value[a] = decode_plane(P_MAX_ORD, fp[k], o[3], PGX_MAX); break;
-      default: R->agg_value[a] = sum; break;  // SUMMV; AVGMV: (sum, value count) like AvgPair
-    }
-  }
-}
-
-// Group-by over multi-value group columns and/or with multi-value functions (DefaultGroupKeyGenerator.java:268-608,
-// DefaultGroupByExecutor.java:154-196).  The single-value part of the query (its filter) runs through the query kernels,
-// which write every scanned row's selection bit; pgx_mv_group then expands each selected doc into its group keys (one
-// per combination of its group columns' values) and applies every function's contribution to each; MINMV / MAXMV,
-// whose reference fold depends on doc order, run in pgx_mv_group_ordered.  Key spaces and result decoding are the
-// single-value ones (dense slots, or 64 / 128-bit hash keys), so finish_result decodes the table as usual.
-void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
-                  uint32_t xflags, pgx_result* R, hipStream_t st, const Domain* dom = nullptr) {
-  if (!q.kn.jit) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by needs the query kernels");
-  const int na = int(q.agg_fn.size()), ng = int(q.group_cols.size());
-  if (ng < 1 || ng > kMaxGroupCols) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by: group column count");
-  std::vector<int8_t> mvf(na), fpv(na, 0), cntp(na, -1);
-  int extra = 0;
-  bool ordered = false;
-  for (int a = 0; a < na; ++a) {
-    const int f = q.agg_fn[a];
-    mvf[a] = int8_t(f);  // pgx_agg_fn and MvFnKind share their numbering
-    if (f == PGX_COUNT) continue;
-    const bool mvfn = f >= PGX_COUNTMV;
-    for (int s = 0; s < n; ++s) {
-      const StagedColumn& c = segs[s]->col(q.agg_col[a]);
-      if (c.is_mv != mvfn)
-        fail(PGX_ERR_UNSUPPORTED, std::string(mvfn ? "multi-value function on single-value column "
-                                                   : "single-value aggregation on multi-value column ") + c.name);
-      if (c.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "numeric aggregation on STRING column " + c.name);
-    }
-    const StagedColumn& c0 = segs[0]->col(q.agg_col[a]);
-    fpv[a] = f != PGX_COUNTMV && (c0.data_type == PGX_FLOAT || c0.data_type == PGX_DOUBLE);
-    if (f == PGX_AVGMV) cntp[a] = int8_t(1 + na + extra++);
-    ordered = ordered || f == PGX_MINMV || f == PGX_MAXMV;
-  }
-  if (na + extra > kMaxAggs) fail(PGX_ERR_UNSUPPORTED, "too many functions for a multi-value group-by");
-
-  // 1. selection bits of the single-value filter
-  pgx_query qs = q;
-  qs.flags |= PGX_Q_NO_STAR_TREE;
-  qs.agg_fn.assign(1, PGX_COUNT);
-  qs.agg_col.assign(1, "");
-  qs.group_cols.clear();
-  qs.key_domain.clear();
-  ExecPlan P;
-  P.want_selmask = true;
-  plan_query(ctx, qs, segs, n, bindings, xflags, P);
-  P.sel_off.assign(n, 0);
-  int64_t words = 0;
-  int max_docs = 0;
-  for (int s = 0; s < n; ++s) {
-    P.sel_off[s] = words;
-    words += (P.ksegs[s].num_docs + 31) / 32 + 1;
-    max_docs = std::max(max_docs, P.ksegs[s].num_docs);
-  }
-  P.sel_buf = DevBuf(ctx, size_t(std::max<int64_t>(words, 1)) * 4);
-  hip_check(hipMemsetAsync(P.sel_buf.p, 0, size_t(std::max<int64_t>(words, 1)) * 4, st), "selection masks");
-  ExecBuffers B;
-  upload_plan(ctx, P, B, st);
-  plan_jit(ctx, qs, segs, n, P, B);
-  if (P.jit.empty() || !P.jit[0].fn) {
-    bool empty = true;  // every segment empty: nothing scanned, no groups
-    for (int s = 0; s < n; ++s) empty = empty && P.ksegs[s].num_docs == 0;
-    if (!empty) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by needs the query kernels");
-  }
-  alloc_outputs(ctx, P, B, nullptr, 0);
-  reset_outputs(P, B, st);
-  launch_scan(P, st);
-
-  // 2. key space: global dictionaries per group column; dense slots, or packed 64 / 128-bit hash keys
-  KQuery& K = P.kq;
-  P.gdicts.clear();
-  P.gbits.clear();
-  uint64_t prod = 1;
-  bool overflow = false;
-  int total_bits = 0;
-  for (int g = 0; g < ng; ++g) {
-    P.gdicts.push_back(dom ? domain_dict(*dom, g, n) : group_dict(q, segs, n, g));
-    const int64_t gc = std::max<int64_t>(1, P.gdicts.back().card);
-    if (!overflow && prod > (uint64_t(1) << 62) / uint64_t(gc)) overflow = true;
-    if (!overflow) prod *= uint64_t(gc);
-    P.gbits.push_back(bits_for(gc));
-    total_bits += P.gbits.back();
-  }
-  P.mode_ref = reference_mode(q, segs[0]);
-  K.num_gcols = ng;
-  const uint64_t kDenseMax = uint64_t(1) << 22;
-  if (!overflow && prod <= kDenseMax && !(xflags & PGX_X_FORCE_HASH)) {
-    uint64_t mul = 1;
-    for (int g = 0; g < ng; ++g) {
-      K.gmul[g] = mul;
-      mul *= uint64_t(P.gdicts[g].card);
-    }
-    K.group_mode = G_DENSE_GLOBAL;
-    P.dense_slots = prod;
-  } else if (total_bits <= 126) {
-    int sh = 0;
-    bool hi = false;
-    for (int g = 0; g < ng; ++g) {
-      if (!hi && sh + P.gbits[g] > 63) {
-        hi = true;
-        sh = 0;
-      }
-      K.gshift[g] = sh;
-      K.ghi[g] = hi;
-      sh += P.gbits[g];
-    }
-    K.group_mode = hi ? G_HASH128 : G_HASH64;
-  } else {
-    fail(PGX_ERR_UNSUPPORTED, "group key wider than 126 bits");
-  }
-  const bool dense = K.group_mode == G_DENSE_GLOBAL;
-  K.num_aggs = na;
-  K.num_planes = 1 + na + extra;
-  K.plane_op[0] = P_ADD_I64;
-  P.g_count_plane.assign(na, -1);
-  for (int a = 0; a < na; ++a) {
-    const int f = q.agg_fn[a];
-    K.agg_fp[a] = fpv[a];
-    K.agg_kind[a] = f == PGX_COUNT ? A_COUNT : (f == PGX_MIN || f == PGX_MINMV) ? A_MIN
-                  : (f == PGX_MAX || f == PGX_MAXMV) ? A_MAX : (f == PGX_AVG || f == PGX_AVGMV) ? A_AVG : A_SUM;
-    K.plane_op[a + 1] = K.agg_kind[a] == A_MIN ? P_MIN_ORD : K.agg_kind[a] == A_MAX ? P_MAX_ORD
-                      : fpv[a] ? P_ADD_F64 : P_ADD_I64;
-    if (f == PGX_COUNTMV) P.g_count_plane[a] = -2;
-    if (f == PGX_AVGMV) P.g_count_plane[a] = cntp[a];
-  }
-  for (int p = 1 + na; p < K.num_planes; ++p) K.plane_op[p] = P_ADD_I64;
-  std::vector<std::string> proj;  // numEntriesScannedPostFilter: docs x projected columns
-  for (int a = 0; a < na; ++a)
-    if (q.agg_fn[a] != PGX_COUNT && std::find(proj.begin(), proj.end(), q.agg_col[a]) == proj.end())
-      proj.push_back(q.agg_col[a]);
-  for (const auto& g : q.group_cols)
-    if (std::find(proj.begin(), proj.end(), g) == proj.end()) proj.push_back(g);
-  P.n_proj = int(proj.size());
-
-  // 3. per-segment descriptors, remap tables (one device copy per distinct table)
-  std::vector<int32_t> blob;
-  std::map<const std::vector<int32_t>*, size_t> roff;
-  for (int g = 0; g < ng; ++g)
-    if (!P.gdicts[g].identity)
-      for (int s = 0; s < n; ++s) {
-        const std::vector<int32_t>* rm = P.gdicts[g].remap[s].get();
-        if (rm && !roff.count(rm)) {
-          roff[rm] = blob.size();
-          blob.insert(blob.end(), rm->begin(), rm->end());
-        }
-      }
-  DevBuf rdev(ctx, std::max<size_t>(1, blob.size()) * 4);
-  if (!blob.empty())
-    hip_check(hipMemcpyAsync(rdev.p, blob.data(), blob.size() * 4, hipMemcpyHostToDevice, st), "remap H2D");
-  std::vector<MvGroupSeg> hs(n);
-  for (int s = 0; s < n; ++s) {
-    MvGroupSeg& m = hs[s];
-    m = MvGroupSeg{};
-    m.sel = P.sel_buf.as<uint32_t>() + P.sel_off[s];
-    m.num_docs = P.ksegs[s].num_docs;
-    for (int g = 0; g < ng; ++g) {
-      const StagedColumn& c = segs[s]->col(q.group_cols[g]);
-      m.g[g].vals = c.fwd;
-      m.g[g].start = c.is_mv ? c.mv_start.as<const int32_t>() : nullptr;
-      m.g[g].bits = c.bits;
-      if (!P.gdicts[g].identity && P.gdicts[g].remap[s])
-        m.g[g].remap = rdev.as<int32_t>() + roff[P.gdicts[g].remap[s].get()];
-    }
-    for (int a = 0; a < na; ++a) {
-      if (q.agg_fn[a] == PGX_COUNT) continue;
-      const StagedColumn& c = segs[s]->col(q.agg_col[a]);
-      m.a[a].vals = c.fwd;
-      m.a[a].start = c.is_mv ? c.mv_start.as<const int32_t>() : nullptr;
-      m.a[a].dict = c.dict_dev;
-      m.a[a].bits = c.bits;
-    }
-  }
-  DevBuf sdev(ctx, std::max<size_t>(1, hs.size()) * sizeof(MvGroupSeg));
-  hip_check(hipMemcpyAsync(sdev.p, hs.data(), hs.size() * sizeof(MvGroupSeg), hipMemcpyHostToDevice, st), "MV segs");
-
-  // 4. table + launch (hash tables retried bigger on overflow)
-  uint64_t slots = dense ? P.dense_slots : initial_hash_cap(segs, n, P);
-  MvGroupArgs A{};
-  DevBuf adev(ctx, sizeof(MvGroupArgs)), ovf(ctx, 64), ord;
-  for (int attempt = 0;; ++attempt) {
-    B.table = DevBuf(ctx, slots * K.num_planes * 8);
-    K.table = devp(B.table);
-    K.keys = nullptr;
-    K.key_state = nullptr;
-    uint64_t kw = 0;
-    if (!dense) {
-      K.hash_cap = slots;
-      P.hash_cap = slots;
-      kw = K.group_mode == G_HASH128 ? 2 * slots : slots;
-      B.keys = DevBuf(ctx, kw * 8);
-      K.keys = devp(B.keys);
-      if (K.group_mode == G_HASH128) {
-        B.key_state = DevBuf(ctx, slots * 4);
-        K.key_state = B.key_state.as<unsigned int>();
-      }
-    } else {
-      K.dense_slots = slots;
-    }
-    PGX_LAUNCH(st, "pgx_init_planes", pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state,
-                                                             st),
-               "init planes");
-    if (ordered) {
-      const uint64_t bytes = uint64_t(n) * na * slots * 8;
-      if (bytes > (uint64_t(1) << 30)) fail(PGX_ERR_UNSUPPORTED, "MINMV / MAXMV under GROUP BY: key space too large");
-      ord = DevBuf(ctx, bytes);
-    }
-    A.segs = sdev.as<MvGroupSeg>();
-    A.nsegs = n;
-    A.ngcols = ng;
-    A.naggs = na;
-    A.group_mode = K.group_mode;
-    for (int a = 0; a < na; ++a) {
-      A.fn[a] = mvf[a];
-      A.fp[a] = fpv[a];
-      A.cnt_plane[a] = cntp[a];
-    }
-    for (int g = 0; g < ng; ++g) {
-      A.gmul[g] = K.gmul[g];
-      A.gshift[g] = K.gshift[g];
-      A.ghi[g] = K.ghi[g];
-    }
-    A.slots = slots;
-    A.table = K.table;
-    A.keys = K.keys;
-    A.key_state = K.key_state;
-    A.overflow = devp(ovf);
-    A.ord = ordered ? devp(ord) : nullptr;
-    hip_check(hipMemsetAsync(ovf.p, 0, 8, st), "memset");
-    hip_check(hipMemcpyAsync(adev.p, &A, sizeof A, hipMemcpyHostToDevice, st), "MV group args");
-    PGX_LAUNCH(st, "pgx_mv_group", pgx_launch_mv_group(adev.as<MvGroupArgs>(), n, max_docs, ordered ? 1 : 0, st),
-               "multi-value group-by");
-    unsigned long long lost = 0;
-    hip_check(hipMemcpyAsync(&lost, ovf.p, 8, hipMemcpyDeviceToHost, st), "D2H");
-    hip_check(hipStreamSynchronize(st), "sync");
-    if (!lost) break;
-    if (dense || attempt >= 4 || slots >= (uint64_t(1) << 30)) fail(PGX_ERR_OOM, "multi-value group-by hash table");
-    slots *= 4;
-  }
-  finish_result(ctx, q, P, B, segs, n, st, R, nullptr);
-}
-
 // After the launches of a non-partitioned plan: with PGX_X_KEEP_DENSE_ON_DEVICE the caller's dense table stays on the
 // device (statistics only); otherwise the result is read back (finish_result).
 void complete_scan(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, pgx_segment* const* segs, int n,
@@ -4730,193 +1237,8 @@ void complete_scan(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
   finish_result(ctx, q, P, B, segs, n, st, R, nullptr);
 }
 
-// -------------------------------------------------------------------------------------------------
-// Plan cache: a server runs the same query shape over the same segments again and again (and the bench's steps do).
-// Planning a 4,096-segment query costs ~2.5-3 ms of host time (predicate leaves, bitmap programs and chunk descriptors,
-// key spaces, the argument arena, per-segment kernel descriptors: p.* / upload / j.sig / jit phases of
-// PGX_DEBUG=host_profile) before the first launch.  A plan whose state is the argument arena and the bitmap masks (dense or
-// aggregation-only, no partitioned / hash / multi-value / automaton buffers) is kept after its execution, with its
-// device arena, keyed by the query (which holds its PGX_* knobs), the segment list (unique segment ids), the bindings'
-// content and the planning flags.  A later execution with the same key replays it: arena and descriptors re-sent, launches,
-// read-back -- no planning.  An entry serves one execution at a time (the bench keeps three in flight: up to
-// kPlanCacheMax entries per query).  Entries hold a context reference; they go with their query
-// (pgx_query_release), their context (pgx_ctx_destroy) or by eviction.  PGX_PLAN_CACHE=0 turns the cache off.
-// -------------------------------------------------------------------------------------------------
-struct PlanEntry {
-  pgx_ctx* ctx = nullptr;
-  std::vector<uint64_t> uids;
-  std::vector<pgx_segment*> ptrs;  // the segment list as passed, and g_segment_frees when last matched
-  uint64_t gen = 0;
-  uint64_t key = 0;
-  std::unique_ptr<ExecPlan> P;
-  std::unique_ptr<ExecBuffers> B;
-  std::unique_ptr<NarrowBuffers> NB;  // a narrow partitioned plan's slabs and partitions (sized by its first run)
-  std::unique_ptr<PartBuffers> PB;    // a radix partitioned plan's buckets and partitions (same)
-  bool busy = false;
-  uint64_t stamp = 0;
-  ~PlanEntry() {
-    NB.reset();
-    PB.reset();
-    B.reset();
-    P.reset();
-    if (ctx) ctx_unref(ctx);
-  }
-};
-constexpr size_t kPlanCacheMax = 4;
-std::mutex g_pc_mu;
-std::unordered_map<const pgx_query*, std::vector<std::shared_ptr<PlanEntry>>> g_pc;
-uint64_t g_pc_clock = 0;
-
-bool plan_cache_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("PGX_PLAN_CACHE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// Hash of the planning inputs that are not the segment list: context, planning flags, every binding's range and its
-// bitset's content (the PGX_* knobs are the query's own, fixed at compile time: entries are kept per query) (a bitset shared by consecutive segments -- one
-// dictionary -- is hashed once).  64-bit multiply-xorshift steps: ~12k bindings at C5.
-uint64_t plan_key(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
-                  uint32_t xflags) {
-  uint64_t h = 0x9E3779B97F4A7C15ull;
-  auto mix = [&](uint64_t x) {
-    h ^= x + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
-    h *= 0xBF58476D1CE4E5B9ull;
-    h ^= h >> 31;
-  };
-  mix(reinterpret_cast<uintptr_t>(ctx));
-  mix(uint64_t(n));
-  mix(xflags & ~(PGX_X_THROUGHPUT | PGX_X_KEEP_DENSE_ON_DEVICE));
-  const size_t L = q.leaf_col.size();
-  if (!L || !bindings) return h;
-  std::vector<const uint32_t*> last_ptr(L, nullptr);
-  std::vector<uint64_t> last_hash(L, 0);
-  for (int s = 0; s < n; ++s)
-    for (size_t l = 0; l < L; ++l) {
-      const pgx_leaf_binding& b = bindings[size_t(s) * L + l];
-      mix((uint64_t(uint32_t(b.lo)) << 32) | uint32_t(b.hi));
-      if (!b.words) continue;
-      if (b.words != last_ptr[l]) {  // (a bitset pointer is one dictionary's: pgx_bind_predicates shares them)
-        const int card = segs[s]->col(q.leaf_col[l]).card;
-        uint64_t w = uint64_t(card) * 0x9E3779B97F4A7C15ull;
-        for (int i = 0; i < (card + 31) / 32; ++i) w = (w ^ b.words[i]) * 0xBF58476D1CE4E5B9ull;
-        last_ptr[l] = b.words;
-        last_hash[l] = w;
-      }
-      mix(last_hash[l]);
-    }
-  return h;
-}
-
-std::shared_ptr<PlanEntry> plan_cache_acquire(const pgx_query* q, pgx_segment* const* segs, int n, uint64_t key) {
-  const uint64_t gen = g_segment_frees.load();
-  std::lock_guard<std::mutex> g(g_pc_mu);
-  auto it = g_pc.find(q);
-  if (it == g_pc.end()) return nullptr;
-  for (auto& e : it->second) {
-    if (e->busy || e->key != key || e->ptrs.size() != size_t(n) ||
-        std::memcmp(e->ptrs.data(), segs, sizeof(pgx_segment*) * size_t(n)) != 0)
-      continue;
-    if (e->gen != gen) {  // a segment was freed since: the same addresses may hold other segments
-      bool same = true;
-      for (int s = 0; s < n && same; ++s) same = segs[s]->uid == e->uids[size_t(s)];
-      if (!same) continue;
-      e->gen = gen;
-    }
-    e->busy = true;
-    e->stamp = ++g_pc_clock;
-    return e;
-  }
-  return nullptr;
-}
-
-// A long segment list is first run batched (the GPU starts after the first batch is planned); the second execution of
-// the same key plans the whole list at once so that the plan is kept (recent keys remembered here).
-bool plan_cache_seen_before(const pgx_query* q, uint64_t key, const std::vector<uint64_t>& uids) {
-  static uint64_t recent[32] = {};
-  static int next = 0;
-  uint64_t h = key ^ reinterpret_cast<uintptr_t>(q);
-  for (uint64_t u : uids) h = (h ^ u) * 0x100000001B3ull;
-  h |= 1;  // 0 marks an empty slot
-  std::lock_guard<std::mutex> g(g_pc_mu);
-  for (uint64_t& r : recent)
-    if (r == h) {
-      r = 0;
-      return true;
-    }
-  recent[next] = h;
-  next = (next + 1) % 32;
-  return false;
-}
-
-void plan_cache_release(const std::shared_ptr<PlanEntry>& e) {
-  std::lock_guard<std::mutex> g(g_pc_mu);
-  e->busy = false;
-}
-
-// after a successful execution of a cacheable plan: keep it (the oldest idle entry makes room)
-void plan_cache_insert(const pgx_query* q, pgx_ctx* ctx, pgx_segment* const* segs, int n, std::vector<uint64_t> uids,
-                       uint64_t key, std::unique_ptr<ExecPlan> P, std::unique_ptr<ExecBuffers> B,
-                       std::unique_ptr<NarrowBuffers> NB = nullptr, std::unique_ptr<PartBuffers> PB = nullptr) {
-  auto e = std::make_shared<PlanEntry>();
-  ctx->refs.fetch_add(1);
-  e->ctx = ctx;
-  e->gen = g_segment_frees.load();
-  e->ptrs.assign(segs, segs + n);
-  e->uids = std::move(uids);
-  e->key = key;
-  e->P = std::move(P);
-  e->B = std::move(B);
-  e->NB = std::move(NB);
-  e->PB = std::move(PB);
-  std::shared_ptr<PlanEntry> evicted;  // destroyed outside the lock (frees device memory)
-  std::lock_guard<std::mutex> g(g_pc_mu);
-  auto& v = g_pc[q];
-  if (v.size() >= kPlanCacheMax) {
-    int old = -1;
-    for (size_t i = 0; i < v.size(); ++i)
-      if (!v[i]->busy && (old < 0 || v[i]->stamp < v[size_t(old)]->stamp)) old = int(i);
-    if (old < 0) return;  // every entry busy: not kept
-    evicted = std::move(v[size_t(old)]);
-    v.erase(v.begin() + old);
-  }
-  e->stamp = ++g_pc_clock;
-  v.push_back(std::move(e));
-}
-
-// drop a query's entries (query released) or a context's (context destroyed); busy entries stay alive with the
-// execution that holds them
-void plan_cache_purge(const pgx_query* q, const pgx_ctx* ctx) {
-  std::vector<std::shared_ptr<PlanEntry>> drop;
-  {
-    std::lock_guard<std::mutex> g(g_pc_mu);
-    for (auto it = g_pc.begin(); it != g_pc.end();) {
-      auto& v = it->second;
-      for (size_t i = 0; i < v.size();) {
-        if ((q && it->first == q) || (ctx && v[i]->ctx == ctx)) {
-          drop.push_back(std::move(v[i]));
-          v.erase(v.begin() + long(i));
-        } else {
-          ++i;
-        }
-      }
-      it = v.empty() ? g_pc.erase(it) : std::next(it);
-    }
-  }
-}
-
-// Plain plans, and partitioned plans (kept with their slabs / buckets and partitions: the same segments and bindings
-// give the same fills, so the first run's capacities hold; a replay that overflows anyway plans afresh)
-bool plan_cacheable(const ExecPlan& P) {
-  const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
-  return (P.use_part || !hash) && P.mv_items.empty() && !P.fsm_on && !P.mv_masks.p && !P.sel_buf.p &&
-         !P.lmask_buf.p && !P.jit.empty();
-}
-
 void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, const pgx_leaf_binding* bindings,
-               const pgx_exec_opts* opts, pgx_result* R, const Domain* dom = nullptr) {
+               const pgx_exec_opts* opts, pgx_result* R, const Domain* dom) {
   HostProf hp(q.kn.host_profile);
   if (hp.on) g_prof_mark = [&hp](const char* w) { hp.mark(w); };
   struct Unmark { ~Unmark() { g_prof_mark = nullptr; } } unmark;
@@ -5064,272 +1386,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   if (cache && plan_cacheable(P)) plan_cache_insert(&q, ctx, segs, n, std::move(uids), pkey, std::move(Pp), std::move(Bp));
 }
 
-// -------------------------------------------------------------------------------------------------
-// Merging group-by partials of different devices (MCombineGroupByOperator.java:166-191 semantics: equal
-// keys combine with each function's combineTwoValues).
-// -------------------------------------------------------------------------------------------------
-// Sparse groups resident in device memory (packed keys; planes count / int64 sum / ordered min / ordered max: group i
-// key keys[i * es], plane p planes[p * ps + i * es]) -> one device-resident result decoded with `like`'s key tables
-// (pgx_merge.hip).
-void merge_device_groups(pgx_ctx* ctx, hipStream_t st, const uint64_t* keys, const uint64_t* planes, int64_t es,
-                         int64_t ps, int64_t n, const pgx_result::Lazy& like, pgx_result* R) {
-  uint64_t cap = 1024;
-  while (cap < uint64_t(std::max<int64_t>(n, 1)) * 2) cap <<= 1;
-  DevBuf tkey(ctx, cap * 8), tpl(ctx, cap * 4 * 8), ctr(ctx, 64);
-  const int64_t ocap = std::max<int64_t>(n, 1);
-  DevBuf okey(ctx, size_t(ocap) * 8), oplane(ctx, size_t(ocap) * 4 * 8);
-  unsigned long long* tp = tpl.as<unsigned long long>();
-  hip_check(hipMemsetAsync(tkey.p, 0xFF, cap * 8, st), "merge table");
-  hip_check(hipMemsetAsync(tp, 0, cap * 2 * 8, st), "merge table");          // count, sum
-  hip_check(hipMemsetAsync(tp + 2 * cap, 0xFF, cap * 8, st), "merge table"); // ordered min
-  hip_check(hipMemsetAsync(tp + 3 * cap, 0, cap * 8, st), "merge table");    // ordered max
-  hip_check(hipMemsetAsync(ctr.p, 0, 16, st), "merge counters");
-  unsigned long long* c = ctr.as<unsigned long long>();
-  PGX_LAUNCH(st, "pgx_group_merge", pgx_launch_group_merge(keys, planes, es, ps, n, tkey.as<unsigned long long>(), tp, cap, c + 1, st),
-            "group merge");
-  PGX_LAUNCH(st, "pgx_group_compact", pgx_launch_group_compact(tkey.as<unsigned long long>(), tp, cap, okey.as<uint64_t>(),
-                                     oplane.as<uint64_t>(), ocap, c, st),
-            "group compact");
-  unsigned long long h[2] = {0, 0};
-  hip_check(hipMemcpyAsync(h, c, 16, hipMemcpyDeviceToHost, st), "merge counters D2H");
-  hip_check(hipStreamSynchronize(st), "sync");
-  if (h[1]) fail(PGX_ERR_INTERNAL, "group merge table overflow");
-  R->group_by = true;
-  R->num_groups = int64_t(std::min<unsigned long long>(h[0], uint64_t(ocap)));
-  auto L = std::make_unique<pgx_result::Lazy>();
-  L->okey = std::move(okey);
-  L->oplane = std::move(oplane);
-  L->ocap = ocap;
-  L->gshift = like.gshift;
-  L->gbits = like.gbits;
-  L->rep_seg = like.rep_seg;
-  L->rep_id = like.rep_id;
-  L->agg_kind = like.agg_kind;
-  ctx->refs.fetch_add(1);
-  L->ctx = ctx;
-  R->lazy = std::move(L);
-}
-
-// Combine of one function's partial (value, count) into an accumulated one (the host-side combineTwoValues).
-// A multi-value group column, or a multi-value function (run_mv / run_mv_group execute these).
-bool query_is_mv(const pgx_query& q, pgx_segment* const* segs, int n) {
-  for (int fn : q.agg_fn)
-    if (fn >= PGX_COUNTMV) return true;
-  for (const auto& g : q.group_cols)
-    for (int s = 0; s < n; ++s)
-      if (segs[s]->col(g).is_mv) return true;
-  return false;
-}
-
-void combine_partial(int fn, double& v, int64_t& c, double v2, int64_t c2) {
-  if (fn == PGX_MIN || fn == PGX_MINMV) v = std::min(v, v2);  // MinMVAggregationFunction.combineTwoValues: Math.min
-  else if (fn == PGX_MAX || fn == PGX_MAXMV) v = std::max(v, v2);
-  else if (fn == PGX_COUNT) v = double(c + c2);
-  else v += v2;  // SUM, AVG sum; COUNTMV / SUMMV / AVGMV sums
-  c += c2;
-}
-
-// Host merge of materialised group-by results whose keys come from one Domain (equal global ids <=> equal
-// (rep segment, rep dictId) pairs, so the pairs key the merge).
-void merge_host_groups(std::vector<std::unique_ptr<pgx_result>>& parts, pgx_result* R) {
-  const int ncols = int(parts[0]->key_seg.size()), na = parts[0]->num_aggs;
-  std::unordered_map<std::string, int64_t> where;
-  R->key_seg.assign(ncols, {});
-  R->key_id.assign(ncols, {});
-  R->g_value.assign(na, {});
-  R->g_count.assign(na, {});
-  std::string k(size_t(ncols) * 8, '\0');
-  for (auto& p : parts) {
-    for (int64_t i = 0; i < p->num_groups; ++i) {
-      for (int g = 0; g < ncols; ++g) {
-        std::memcpy(&k[size_t(g) * 8], &p->key_seg[g][i], 4);
-        std::memcpy(&k[size_t(g) * 8 + 4], &p->key_id[g][i], 4);
-      }
-      auto it = where.find(k);
-      if (it == where.end()) {
-        where.emplace(k, R->num_groups);
-        for (int g = 0; g < ncols; ++g) {
-          R->key_seg[g].push_back(p->key_seg[g][i]);
-          R->key_id[g].push_back(p->key_id[g][i]);
-        }
-        for (int a = 0; a < na; ++a) {
-          R->g_value[a].push_back(p->g_value[a][i]);
-          R->g_count[a].push_back(p->g_count[a][i]);
-        }
-        ++R->num_groups;
-      } else {
-        for (int a = 0; a < na; ++a)
-          combine_partial(R->agg_fn[a], R->g_value[a][it->second], R->g_count[a][it->second], p->g_value[a][i],
-                          p->g_count[a][i]);
-      }
-    }
-  }
-}
-
-// pgx_execute_multi: the segments run where they are staged (one thread per context, concurrently), then the partials
-// merge on the first context's device: aggregation-only on the host; dense tables over the shared key space are copied
-// to that device (hipMemcpyPeerAsync, xGMI between GPUs) and reduced plane by plane; sparse groups still in device
-// memory are copied there and merged by pgx_group_merge; anything else merges on the host by key.
-void run_multi(pgx_ctx* const* ctxs, int nctx, const pgx_query& q, pgx_segment* const* segs, int n,
-               const pgx_leaf_binding* bindings, uint32_t xflags, pgx_result* R) {
-  if (n < 1) fail(PGX_ERR_INVALID_ARG, "no segments");
-  std::vector<std::vector<int>> part(nctx);
-  for (int i = 0; i < n; ++i) {
-    int k = 0;
-    while (k < nctx && segs[i]->ctx != ctxs[k]) ++k;
-    if (k == nctx) fail(PGX_ERR_INVALID_ARG, "segment " + segs[i]->name + " is not staged on any of the contexts");
-    part[k].push_back(i);
-  }
-  std::vector<int> active;
-  for (int k = 0; k < nctx; ++k)
-    if (!part[k].empty()) active.push_back(k);
-  const size_t L = q.leaf_col.size();
-  std::vector<GlobalDict> gd;
-  for (int g = 0; g < int(q.group_cols.size()); ++g) gd.push_back(group_dict(q, segs, n, g));
-  uint64_t slots = 1;
-  bool dense = !q.group_cols.empty() && !(xflags & PGX_X_FORCE_HASH) && !query_is_mv(q, segs, n);
-  for (const auto& g : gd) {
-    if (slots > (uint64_t(1) << 22) / uint64_t(std::max<int64_t>(g.card, 1))) dense = false;
-    else slots *= uint64_t(g.card);
-  }
-  const int nplanes = 1 + int(q.agg_fn.size());
-  const int na = int(q.agg_fn.size());
-  uint64_t ops = 0;  // dense plane ops, 2 bits per plane (pgx_query_dense_plane_op)
-  for (int a = 0; a < na; ++a) {
-    const int fn = q.agg_fn[a];
-    int op = P_ADD_I64;
-    if (fn != PGX_COUNT) {
-      const StagedColumn& c = segs[0]->col(q.agg_col[a]);
-      const bool fp = c.data_type == PGX_FLOAT || c.data_type == PGX_DOUBLE;
-      op = fn == PGX_MIN ? P_MIN_ORD : fn == PGX_MAX ? P_MAX_ORD : (fp ? P_ADD_F64 : P_ADD_I64);
-    }
-    ops |= uint64_t(op) << (2 * (a + 1));
-  }
-  const int na_ctx = int(active.size());
-  std::vector<Domain> dom(na_ctx);
-  std::vector<std::vector<pgx_segment*>> sub(na_ctx);
-  std::vector<std::vector<pgx_leaf_binding>> sb(na_ctx);
-  std::vector<std::unique_ptr<pgx_result>> res(na_ctx);
-  std::vector<DevBuf> tables(na_ctx);
-  std::vector<std::exception_ptr> errs(na_ctx);
-  const uint64_t tbytes = slots * uint64_t(nplanes) * 8;
-  for (int j = 0; j < na_ctx; ++j) {
-    const int k = active[j];
-    dom[j].g = &gd;
-    dom[j].index = part[k];
-    for (int i : part[k]) {
-      sub[j].push_back(segs[i]);
-      if (L) sb[j].insert(sb[j].end(), bindings + size_t(i) * L, bindings + size_t(i + 1) * L);
-    }
-    res[j] = std::make_unique<pgx_result>();
-  }
-  auto run_one = [&](int j) {
-    pgx_ctx* c = ctxs[active[j]];
-    hip_check(hipSetDevice(c->device), "hipSetDevice");
-    pgx_exec_opts o{};
-    o.flags = xflags & ~uint32_t(PGX_X_KEEP_DENSE_ON_DEVICE);
-    if (dense) {
-      tables[j] = DevBuf(c, tbytes);
-      o.dense_out = tables[j].p;
-      o.dense_out_bytes = tbytes;
-      o.flags |= PGX_X_KEEP_DENSE_ON_DEVICE;
-    }
-    run_query(c, q, sub[j].data(), int(sub[j].size()), L ? sb[j].data() : nullptr, &o, res[j].get(), &dom[j]);
-  };
-  {
-    std::vector<std::thread> th;
-    for (int j = 1; j < na_ctx; ++j)
-      th.emplace_back([&, j] {
-        try {
-          run_one(j);
-        } catch (...) {
-          errs[j] = std::current_exception();
-        }
-      });
-    try {
-      run_one(0);
-    } catch (...) {
-      errs[0] = std::current_exception();
-    }
-    for (auto& t : th) t.join();
-    for (auto& e : errs)
-      if (e) std::rethrow_exception(e);
-  }
-  pgx_ctx* c0 = ctxs[active[0]];
-  hip_check(hipSetDevice(c0->device), "hipSetDevice");
-  hipStream_t st = c0->stream;
-  int64_t stats[4] = {0, 0, 0, 0};
-  for (auto& r : res)
-    for (int i = 0; i < 4; ++i) stats[i] += r->stats[i];
-  if (q.group_cols.empty()) {
-    *R = std::move(*res[0]);
-    for (int j = 1; j < na_ctx; ++j)
-      for (int a = 0; a < na; ++a)
-        combine_partial(q.agg_fn[a], R->agg_value[a], R->agg_count[a], res[j]->agg_value[a], res[j]->agg_count[a]);
-  } else if (dense) {
-    unsigned long long* t0 = tables[0].as<unsigned long long>();
-    DevBuf stage;
-    for (int j = 1; j < na_ctx; ++j) {
-      const unsigned long long* src = tables[j].as<unsigned long long>();
-      if (tables[j].ctx->device != c0->device) {
-        if (!stage.p) stage = DevBuf(c0, tbytes);
-        hip_check(hipMemcpyPeerAsync(stage.p, c0->device, tables[j].p, tables[j].ctx->device, tbytes, st),
-                  "dense table peer copy");
-        src = stage.as<unsigned long long>();
-      }
-      PGX_LAUNCH(st, "pgx_dense_reduce", pgx_launch_dense_reduce(t0, src, slots, nplanes, ops, st), "dense reduce");
-    }
-    std::vector<unsigned long long> host(slots * nplanes);
-    hip_check(hipMemcpyAsync(host.data(), t0, tbytes, hipMemcpyDeviceToHost, st), "dense D2H");
-    hip_check(hipStreamSynchronize(st), "sync");
-    ExecPlan P;
-    std::vector<pgx_leaf_binding> none(sub[0].size() * L, pgx_leaf_binding{0, -1, nullptr});
-    plan_query(c0, q, sub[0].data(), int(sub[0].size()), none.data(), xflags, P, &dom[0]);
-    ExecBuffers B;
-    B.host = PinnedBuf(c0, kOutsBytes);
-    B.off_outs = 0;
-    std::memset(B.host.p, 0, kOutsBytes);
-    reinterpret_cast<unsigned long long*>(B.host.p)[16] = static_cast<unsigned long long>(stats[0]);
-    finish_result(c0, q, P, B, sub[0].data(), int(sub[0].size()), st, R, host.data());
-  } else {
-    bool all_lazy = true;
-    for (auto& r : res) all_lazy = all_lazy && r->lazy;
-    *R = pgx_result();
-    R->num_aggs = na;
-    R->agg_fn = q.agg_fn;
-    R->group_by = true;
-    if (all_lazy) {
-      int64_t total = 0;
-      for (auto& r : res) total += r->num_groups;
-      DevBuf keys(c0, size_t(std::max<int64_t>(total, 1)) * 8), pl(c0, size_t(std::max<int64_t>(total, 1)) * 32);
-      int64_t off = 0;
-      for (auto& r : res) {
-        const auto& Lz = *r->lazy;
-        const int64_t ng = r->num_groups;
-        if (!ng) continue;
-        hip_check(hipMemcpyPeerAsync(keys.as<uint64_t>() + off, c0->device, Lz.okey.p, Lz.ctx->device, ng * 8, st),
-                  "group keys peer copy");
-        for (int p = 0; p < 4; ++p)
-          hip_check(hipMemcpyPeerAsync(pl.as<uint64_t>() + p * total + off, c0->device,
-                                       Lz.oplane.as<uint64_t>() + p * Lz.ocap, Lz.ctx->device, ng * 8, st),
-                    "group planes peer copy");
-        off += ng;
-      }
-      merge_device_groups(c0, st, keys.as<uint64_t>(), pl.as<uint64_t>(), 1, total, total, *res[0]->lazy, R);
-    } else {
-      for (auto& r : res) r->materialize();
-      merge_host_groups(res, R);
-    }
-  }
-  for (int i = 0; i < 4; ++i) R->stats[i] = stats[i];
-  R->num_aggs = na;
-  R->agg_fn = q.agg_fn;
-  R->top_n = q.top_n;
-  R->group_by = !q.group_cols.empty();
-  if (R->group_by) R->mode = reference_mode(q, segs[0]);
-}
-
-}  // namespace
+}  // namespace pgxh
 
 void pgx_result::ready() const {
   if (!async) return;
@@ -5424,230 +1481,6 @@ pgx_status pgx_segment_release(pgx_segment* seg) {
     pgx_ctx* ctx = seg->ctx;
     delete seg;
     g_segment_frees.fetch_add(1);
-    if (ctx) ctx_unref(ctx);
-  });
-}
-
-// -------------------------------------------------------------------------------------------------
-// Realtime (consuming) segments in place (RealtimeSegmentImpl.java:185-334): per column the docs' arrival-order
-// dictIds live in HBM and grow by appends (only the new rows cross PCIe); a snapshot re-packs them on the device through
-// the arrival -> sorted dictId map of the column's current dictionary (RealtimeSegmentConverter's shape: sorted
-// dictionary, unsorted fixed-bit forward index), so a query costs no host pass over the rows.
-// -------------------------------------------------------------------------------------------------
-struct pgx_mutable {
-  pgx_ctx* ctx = nullptr;
-  std::string name;
-  int32_t capacity = 0;
-  int32_t num_docs = 0;
-  struct Col {
-    std::string name;
-    int data_type = 0;
-    bool mv = false, inverted = false;
-    DevBuf ids;                  // arrival-order dictIds: one per doc (SV) or per value (MV)
-    int64_t ids_cap = 0, nvals = 0;
-    DevBuf starts;               // MV: doc d's values are [starts[d], starts[d + 1]) (capacity + 1)
-    int max_mv = 0;
-    int32_t max_id = -1;         // largest arrival id appended
-    int card = 0, dict_width = 0, pad_char = 0;
-    std::vector<uint8_t> dict;   // sorted v1 dictionary bytes
-    DevBuf remap;                // arrival id -> sorted id
-  };
-  std::vector<Col> cols;
-  mutable std::mutex mu;
-};
-
-pgx_status pgx_mutable_create(pgx_ctx* ctx, const char* name, int32_t capacity, int32_t num_columns,
-                              const pgx_mutable_column* columns, pgx_mutable** out) {
-  return guarded([&] {
-    if (!ctx || !columns || !out || capacity < 1 || num_columns < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
-    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-    auto m = std::make_unique<pgx_mutable>();
-    m->ctx = ctx;
-    m->name = name ? name : "";
-    m->capacity = capacity;
-    m->cols.resize(num_columns);
-    for (int i = 0; i < num_columns; ++i) {
-      const pgx_mutable_column& d = columns[i];
-      pgx_mutable::Col& c = m->cols[i];
-      c.name = d.name ? d.name : "";
-      c.data_type = d.data_type;
-      c.mv = d.is_multi_value != 0;
-      c.inverted = d.has_inverted != 0;
-      if (c.mv && c.data_type == PGX_STRING) fail(PGX_ERR_UNSUPPORTED, "multi-value STRING column " + c.name);
-      c.ids_cap = c.mv ? std::max<int64_t>(1024, int64_t(capacity)) : capacity;
-      c.ids = DevBuf(ctx, size_t(c.ids_cap) * 4);
-      if (c.mv) {
-        c.starts = DevBuf(ctx, (size_t(capacity) + 1) * 4);
-        hip_check(hipMemset(c.starts.p, 0, 4), "memset");
-      }
-    }
-    ctx->refs.fetch_add(1);  // released by pgx_mutable_release
-    *out = m.release();
-  });
-}
-
-pgx_status pgx_mutable_append(pgx_mutable* m, int32_t ndocs, const int32_t* const* ids, const int32_t* const* counts) {
-  return guarded([&] {
-    if (!m || !ids || ndocs < 0) fail(PGX_ERR_INVALID_ARG, "bad argument");
-    std::lock_guard<std::mutex> g(m->mu);
-    if (int64_t(m->num_docs) + ndocs > m->capacity) fail(PGX_ERR_INVALID_ARG, "realtime segment " + m->name + " full");
-    if (!ndocs) return;
-    // Validate every column before any device or host state changes: a rejected batch leaves nvals, starts, max_id
-    // and num_docs exactly as they were (no half-appended multi-value column).
-    const size_t ncols = m->cols.size();
-    std::vector<int64_t> nv(ncols, ndocs);
-    std::vector<int32_t> top(ncols, -1), mvmax(ncols, 0);
-    for (size_t i = 0; i < ncols; ++i) {
-      const pgx_mutable::Col& c = m->cols[i];
-      if (!ids[i] || (c.mv && (!counts || !counts[i]))) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": no ids");
-      if (c.mv) {
-        int64_t at = c.nvals;
-        for (int32_t d = 0; d < ndocs; ++d) {
-          if (counts[i][d] < 1) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": a multi-value doc needs a value");
-          at += counts[i][d];
-          mvmax[i] = std::max(mvmax[i], counts[i][d]);
-        }
-        if (at > 0x7FFFFFFF) fail(PGX_ERR_UNSUPPORTED, "column " + c.name + ": too many values");
-        nv[i] = at - c.nvals;
-      }
-      for (int64_t k = 0; k < nv[i]; ++k) {
-        if (ids[i][k] < 0) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": negative dictId");
-        top[i] = std::max(top[i], ids[i][k]);
-      }
-    }
-    hip_check(hipSetDevice(m->ctx->device), "hipSetDevice");
-    hipStream_t st = m->ctx->stream;
-    for (size_t i = 0; i < ncols; ++i) {
-      pgx_mutable::Col& c = m->cols[i];
-      if (c.mv) {  // the new docs' starts, then the values
-        std::vector<int32_t> st_new(ndocs);
-        int64_t at = c.nvals;
-        for (int32_t d = 0; d < ndocs; ++d) {
-          at += counts[i][d];
-          st_new[d] = int32_t(at);
-        }
-        hip_check(hipMemcpyAsync(c.starts.as<int32_t>() + m->num_docs + 1, st_new.data(), size_t(ndocs) * 4,
-                                 hipMemcpyHostToDevice, st), "starts H2D");
-        hip_check(hipStreamSynchronize(st), "sync");  // st_new is a stack buffer
-        if (c.nvals + nv[i] > c.ids_cap) {  // grow the value buffer (doubling)
-          int64_t cap = c.ids_cap;
-          while (cap < c.nvals + nv[i]) cap *= 2;
-          DevBuf bigger(m->ctx, size_t(cap) * 4);
-          if (c.nvals)
-            hip_check(hipMemcpyAsync(bigger.p, c.ids.p, size_t(c.nvals) * 4, hipMemcpyDeviceToDevice, st), "grow");
-          hip_check(hipStreamSynchronize(st), "sync");
-          c.ids = std::move(bigger);
-          c.ids_cap = cap;
-        }
-      }
-      const int64_t at = c.mv ? c.nvals : m->num_docs;
-      hip_check(hipMemcpyAsync(c.ids.as<int32_t>() + at, ids[i], size_t(nv[i]) * 4, hipMemcpyHostToDevice, st),
-                "ids H2D");
-    }
-    hip_check(hipStreamSynchronize(st), "sync");  // the caller's buffers may go away after the call
-    for (size_t i = 0; i < ncols; ++i) {  // commit: every column was accepted
-      pgx_mutable::Col& c = m->cols[i];
-      c.max_id = std::max(c.max_id, top[i]);
-      if (c.mv) {
-        c.nvals += nv[i];
-        c.max_mv = std::max(c.max_mv, mvmax[i]);
-      }
-    }
-    m->num_docs += ndocs;
-  });
-}
-
-pgx_status pgx_mutable_set_dictionary(pgx_mutable* m, int32_t col, int32_t card, const void* dict, uint64_t dict_len,
-                                      int32_t dict_width, int32_t pad_char, const int32_t* arrival_to_sorted) {
-  return guarded([&] {
-    if (!m || !dict || !arrival_to_sorted || card < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
-    std::lock_guard<std::mutex> g(m->mu);
-    if (col < 0 || col >= int(m->cols.size())) fail(PGX_ERR_INVALID_ARG, "column index");
-    pgx_mutable::Col& c = m->cols[col];
-    const int width = (c.data_type == PGX_INT || c.data_type == PGX_FLOAT) ? 4 : c.data_type == PGX_STRING ? dict_width : 8;
-    if (width < 1 || dict_len < uint64_t(width) * card) fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": dictionary short");
-    for (int32_t i = 0; i < card; ++i)
-      if (arrival_to_sorted[i] < 0 || arrival_to_sorted[i] >= card)
-        fail(PGX_ERR_INVALID_ARG, "column " + c.name + ": remap out of range");
-    hip_check(hipSetDevice(m->ctx->device), "hipSetDevice");
-    c.card = card;
-    c.dict_width = width;
-    c.pad_char = pad_char & 0xFF;
-    c.dict.assign(static_cast<const uint8_t*>(dict), static_cast<const uint8_t*>(dict) + uint64_t(width) * card);
-    c.remap = DevBuf(m->ctx, size_t(card) * 4);
-    hip_check(hipMemcpy(c.remap.p, arrival_to_sorted, size_t(card) * 4, hipMemcpyHostToDevice), "remap H2D");
-  });
-}
-
-pgx_status pgx_mutable_snapshot(pgx_mutable* m, pgx_segment** out) {
-  return guarded([&] {
-    if (!m || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
-    std::lock_guard<std::mutex> g(m->mu);
-    if (m->num_docs < 1) fail(PGX_ERR_INVALID_ARG, "realtime segment " + m->name + " has no docs");
-    pgx_ctx* ctx = m->ctx;
-    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-    hipStream_t st = ctx->stream;
-    auto seg = std::make_unique<pgx_segment>();
-    seg->ctx = ctx;
-    seg->name = m->name;
-    seg->total_docs = seg->total_raw_docs = m->num_docs;
-    seg->cols.resize(m->cols.size());
-    const int64_t n = m->num_docs;
-    for (size_t i = 0; i < m->cols.size(); ++i) {
-      const pgx_mutable::Col& mc = m->cols[i];
-      StagedColumn& c = seg->cols[i];
-      if (mc.card < 1 || mc.max_id >= mc.card)
-        fail(PGX_ERR_INVALID_ARG, "column " + mc.name + ": dictionary not set for every appended value");
-      c.name = mc.name;
-      c.data_type = mc.data_type;
-      c.card = mc.card;
-      c.bits = bits_for(mc.card);
-      c.dict_width = mc.dict_width;
-      c.pad_char = mc.pad_char;
-      c.is_sorted = false;           // RealtimeColumnDataSource.isSorted(): false
-      c.has_inverted = mc.inverted;  // bitmap-filter semantics; without index bytes the leaf is evaluated by scanning
-      stage_dict(ctx, seg.get(), mc.dict, c);
-      const int64_t rows = mc.mv ? mc.nvals : n;
-      const uint64_t need = padded_fwd_bytes(rows, c.bits);
-      c.fwd_owned = DevBuf(ctx, need);
-      hip_check(hipMemsetAsync(c.fwd_owned.p, 0, need, st), "memset");
-      PGX_LAUNCH(st, "pgx_pack_remap", pgx_launch_pack_remap(c.fwd_owned.as<uint32_t>(), mc.ids.as<int32_t>(),
-                                                              mc.remap.as<int32_t>(), rows, c.bits,
-                                                              int64_t((uint64_t(rows) * c.bits + 31) / 32), st),
-                 "realtime forward index");
-      c.fwd = c.fwd_owned.as<const uint32_t>();
-      seg->device_bytes += need;
-      if (mc.mv) {
-        c.is_mv = true;
-        c.total_entries = mc.nvals;
-        c.max_mv = mc.max_mv;
-        c.mv_start = DevBuf(ctx, (size_t(n) + 1) * 4);
-        hip_check(hipMemcpyAsync(c.mv_start.p, mc.starts.p, (size_t(n) + 1) * 4, hipMemcpyDeviceToDevice, st),
-                  "starts copy");
-        seg->device_bytes += (size_t(n) + 1) * 4;
-      }
-      seg->by_name[c.name] = int(i);
-      seg->names.push_back(c.name);
-    }
-    hip_check(hipStreamSynchronize(st), "sync");
-    ctx->refs.fetch_add(1);  // released by pgx_segment_release
-    *out = seg.release();
-  });
-}
-
-pgx_status pgx_mutable_num_docs(const pgx_mutable* m, int32_t* out) {
-  return guarded([&] {
-    if (!m || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
-    std::lock_guard<std::mutex> g(m->mu);  // appends write num_docs under the same lock
-    *out = m->num_docs;
-  });
-}
-
-pgx_status pgx_mutable_release(pgx_mutable* m) {
-  return guarded([&] {
-    if (!m) return;
-    pgx_ctx* ctx = m->ctx;
-    delete m;
     if (ctx) ctx_unref(ctx);
   });
 }
@@ -6056,193 +1889,6 @@ pgx_status pgx_result_from_dense(pgx_ctx* ctx, const pgx_query* q, pgx_segment* 
     R->stats[2] = stats[2];
     R->stats[3] = stats[3];
     *out = R.release();
-  });
-}
-
-pgx_status pgx_device_alloc(pgx_ctx* ctx, uint64_t bytes, void** out) {
-  return guarded([&] {
-    if (!ctx || !out) fail(PGX_ERR_INVALID_ARG, "NULL argument");
-    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-    void* p = nullptr;
-    if (hipMalloc(&p, std::max<uint64_t>(bytes, 256)) != hipSuccess) fail(PGX_ERR_OOM, "hipMalloc failed");
-    *out = p;
-  });
-}
-
-pgx_status pgx_device_free(pgx_ctx* ctx, void* p) {
-  return guarded([&] {
-    if (!ctx) fail(PGX_ERR_INVALID_ARG, "NULL argument");
-    if (p) hip_check(hipFree(p), "hipFree");
-  });
-}
-
-pgx_status pgx_copy_to_device(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
-  return guarded([&] {
-    if (!ctx || !dst || !src) fail(PGX_ERR_INVALID_ARG, "NULL argument");
-    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-    hip_check(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice), "H2D");
-  });
-}
-
-pgx_status pgx_copy_to_host(pgx_ctx* ctx, void* dst, const void* src, uint64_t bytes) {
-  return guarded([&] {
-    if (!ctx || (bytes && (!dst || !src))) fail(PGX_ERR_INVALID_ARG, "NULL argument");
-    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-    hip_check(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost), "D2H");
-  });
-}
-
-pgx_status pgx_synth_column_paired(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
-                                   uint64_t seed, uint64_t pair_seed, uint32_t npairs) {
-  return guarded([&] {
-    if (!ctx || !device_fwd) fail(PGX_ERR_INVALID_ARG, "NULL argument");
-    if (bits < 1 || bits > 32 || card < 1) fail(PGX_ERR_INVALID_ARG, "bits/card");
-    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-    const int64_t n_words = int64_t(padded_fwd_bytes(n_rows, bits) / 4);
-    hip_check(pgx_launch_synth(static_cast<uint32_t*>(device_fwd), n_rows, bits, uint32_t(card), seed, n_words, pair_seed, npairs,
-                               ctx->stream),
-              "synth launch");
-    hip_check(hipStreamSynchronize(ctx->stream), "sync");
-  });
-}
-
-pgx_status pgx_synth_column(pgx_ctx* ctx, void* device_fwd, int64_t n_rows, int32_t bits, int32_t card,
-                            uint64_t seed) {
-  return pgx_synth_column_paired(ctx, device_fwd, n_rows, bits, card, seed, 0, 0);
-}
-
-// ---- segment-creation helpers (benchmark data and fixtures; not on the query path) ----------------------------------
-
-// dictId(row) = splitmix64(seed ^ row * 0x9E3779B97F4A7C15) % card: the same sequence pgx_synth_column packs on device.
-pgx_status pgx_synth_dict_ids(uint64_t seed, int64_t n_rows, int32_t card, int32_t* out) {
-  return guarded([&] {
-    if (!out || n_rows < 0 || card < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
-    for (int64_t r = 0; r < n_rows; ++r) {
-      uint64_t x = seed ^ (static_cast<uint64_t>(r) * 0x9E3779B97F4A7C15ull);
-      x += 0x9E3779B97F4A7C15ull;
-      x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-      x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-      x ^= x >> 31;
-      out[r] = static_cast<int32_t>(x % static_cast<uint64_t>(card));
-    }
-  });
-}
-
-// <col>.bitmap.inv of a column (segment/creator/impl/inv/HeapBitmapInvertedIndexCreator.java:42-81): (card+1) BE int
-// offsets, then per dictId the RoaringBitmap 0.5.10 portable serialisation of its doc ids (cookie 12346, no run
-// containers; array containers up to 4096 docs, bitmap containers above).  out == NULL (or cap too small) only
-// reports the size in *len.
-// Segment creation: FixedBitSingleValueWriter's packing (MSB-first, big-endian, no padding between values), 64 bits
-// at a time.  out holds ceil(n * bits / 8) bytes.
-pgx_status pgx_pack_fixed_bit(const int32_t* ids, int64_t n, int32_t bits, uint8_t* out) {
-  return guarded([&] {
-    if (bits < 1 || bits > 32 || n < 0 || (n && (!ids || !out))) fail(PGX_ERR_INVALID_ARG, "bad argument");
-    const uint64_t nbytes = (uint64_t(n) * uint64_t(bits) + 7) / 8;
-    uint64_t acc = 0;  // pending bits, left-aligned count `have`
-    int have = 0;
-    uint64_t o = 0;
-    const uint64_t mask = bits == 32 ? 0xFFFFFFFFull : ((uint64_t(1) << bits) - 1);
-    for (int64_t i = 0; i < n; ++i) {
-      const uint64_t v = uint64_t(uint32_t(ids[i])) & mask;
-      if (have + bits <= 64) {
-        acc |= v << (64 - have - bits);
-        have += bits;
-      } else {
-        const int fit = 64 - have;
-        acc |= v >> (bits - fit);
-        for (int b = 0; b < 8; ++b) out[o++] = uint8_t(acc >> (56 - 8 * b));
-        acc = v << (64 - (bits - fit));
-        have = bits - fit;
-      }
-      if (have == 64) {
-        for (int b = 0; b < 8; ++b) out[o++] = uint8_t(acc >> (56 - 8 * b));
-        acc = 0;
-        have = 0;
-      }
-    }
-    for (int b = 0; o < nbytes; ++b) out[o++] = uint8_t(acc >> (56 - 8 * b));
-  });
-}
-
-pgx_status pgx_inverted_index_build(const int32_t* ids, int64_t n, int32_t card, uint8_t* out, uint64_t cap,
-                                    uint64_t* len) {
-  return guarded([&] {
-    if (!ids || !len || n < 0 || card < 1) fail(PGX_ERR_INVALID_ARG, "bad argument");
-    // counting sort of doc ids by dictId
-    std::vector<int64_t> start(size_t(card) + 1, 0);
-    for (int64_t i = 0; i < n; ++i) {
-      if (ids[i] < 0 || ids[i] >= card) fail(PGX_ERR_INVALID_ARG, "dictId out of range");
-      ++start[size_t(ids[i]) + 1];
-    }
-    for (int32_t v = 0; v < card; ++v) start[v + 1] += start[v];
-    std::vector<int32_t> docs(static_cast<size_t>(n));
-    {
-      std::vector<int64_t> pos(start.begin(), start.end() - 1);
-      for (int64_t i = 0; i < n; ++i) docs[size_t(pos[ids[i]]++)] = int32_t(i);
-    }
-    // sizes
-    auto bitmap_bytes = [&](int32_t v, std::vector<std::pair<int, int>>* conts) {
-      uint64_t b = 8;
-      const int64_t a = start[v], e = start[v + 1];
-      int64_t i = a;
-      while (i < e) {
-        const int key = docs[size_t(i)] >> 16;
-        int64_t j = i;
-        while (j < e && (docs[size_t(j)] >> 16) == key) ++j;
-        const int c = int(j - i);
-        b += 8 + (c > 4096 ? 8192 : 2 * uint64_t(c));
-        if (conts) conts->push_back({key, c});
-        i = j;
-      }
-      return b;
-    };
-    uint64_t total = 4 * (uint64_t(card) + 1);
-    for (int32_t v = 0; v < card; ++v) total += bitmap_bytes(v, nullptr);
-    *len = total;
-    if (!out || cap < total) return;
-    if (total > 0x7FFFFFFFull) fail(PGX_ERR_UNSUPPORTED, "inverted index over 2 GiB");
-    auto put32be = [&](uint64_t o, uint32_t x) {
-      out[o] = uint8_t(x >> 24); out[o + 1] = uint8_t(x >> 16); out[o + 2] = uint8_t(x >> 8); out[o + 3] = uint8_t(x);
-    };
-    auto put32le = [&](uint64_t o, uint32_t x) { std::memcpy(out + o, &x, 4); };
-    auto put16le = [&](uint64_t o, uint16_t x) { std::memcpy(out + o, &x, 2); };
-    uint64_t o = 4 * (uint64_t(card) + 1);
-    std::vector<std::pair<int, int>> conts;
-    for (int32_t v = 0; v < card; ++v) {
-      put32be(4 * uint64_t(v), uint32_t(o));
-      conts.clear();
-      bitmap_bytes(v, &conts);
-      const uint64_t b0 = o;
-      const int nc = int(conts.size());
-      put32le(o, 12346u);
-      put32le(o + 4, uint32_t(nc));
-      uint64_t payload = 8 + 8 * uint64_t(nc);
-      for (int k = 0; k < nc; ++k) {
-        put16le(o + 8 + 4 * k, uint16_t(conts[k].first));
-        put16le(o + 8 + 4 * k + 2, uint16_t(conts[k].second - 1));
-        put32le(o + 8 + 4 * uint64_t(nc) + 4 * k, uint32_t(payload));
-        payload += conts[k].second > 4096 ? 8192 : 2 * uint64_t(conts[k].second);
-      }
-      uint64_t p = o + 8 + 8 * uint64_t(nc);
-      int64_t i = start[v];
-      for (int k = 0; k < nc; ++k) {
-        const int c = conts[k].second;
-        if (c > 4096) {
-          std::memset(out + p, 0, 8192);
-          for (int t = 0; t < c; ++t) {
-            const uint32_t lo = uint32_t(docs[size_t(i + t)]) & 0xFFFFu;
-            out[p + (lo >> 3)] |= uint8_t(1u << (lo & 7));
-          }
-          p += 8192;
-        } else {
-          for (int t = 0; t < c; ++t) put16le(p + 2 * uint64_t(t), uint16_t(uint32_t(docs[size_t(i + t)]) & 0xFFFFu));
-          p += 2 * uint64_t(c);
-        }
-        i += c;
-      }
-      o = b0 + (p - b0);
-    }
-    put32be(4 * uint64_t(card), uint32_t(o));
   });
 }
 

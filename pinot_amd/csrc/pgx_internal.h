@@ -197,7 +197,7 @@ struct KQuery {
 
 namespace pgx {
 
-// Value images staged in LDS for aggregated columns (built once per column at staging time, pgx_host.cpp).
+// Value images staged in LDS for aggregated columns (built once per column at staging time, pgx_stage.cpp).
 enum ImgKind : int8_t {
   IMG_NONE = 0,   // no image: values are gathered from the HBM value table (int64 / double per dictId)
   IMG_U32 = 1,    // u32 (value - vbase) per dictId
@@ -207,7 +207,7 @@ enum ImgKind : int8_t {
 constexpr int kImgFor16Blocks = 64;
 constexpr int kLdsBudget = 160 * 1024 - 256;  // static LDS of one workgroup, minus the per-plane accumulators
 
-// Narrow partitioned group-by (pgx_host.cpp run_narrow): the packed K-bit group key is mixed by a bijection of
+// Narrow partitioned group-by (pgx_part.cpp run_narrow): the packed K-bit group key is mixed by a bijection of
 // [0, 2^K), h = ((key * c1) & M) ^ (that >> s) with s = ceil(K / 2) (so the xor-shift inverts itself), and the
 // partitions are h's top bits (the multiply carries every key bit into them); the xor-shift folds those well-mixed top
 // bits into the low bits that choose a record's slot in the aggregation tables.  h's remaining bits travel in the

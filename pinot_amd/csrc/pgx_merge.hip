@@ -16,7 +16,7 @@
 
 namespace pgx {
 
-constexpr unsigned long long kMergeEmpty = ~0ull;  // packed keys use < 64 bits (pgx_host.cpp part_keybits <= 63)
+constexpr unsigned long long kMergeEmpty = ~0ull;  // packed keys use < 64 bits (pgx_plan.cpp part_keybits <= 63)
 
 __device__ __forceinline__ uint64_t merge_mix(uint64_t x) {
   x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;

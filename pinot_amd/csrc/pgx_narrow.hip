@@ -1,4 +1,4 @@
-// Narrow partitioned group-by: the second split and the aggregation (pgx_host.cpp run_narrow).
+// Narrow partitioned group-by: the second split and the aggregation (pgx_part.cpp run_narrow).
 //
 // Sparse group keys (LONG_MAP_BASED, DefaultGroupKeyGenerator.java:239-246 / :429-441: the packed raw key probes a
 // Long2IntOpenHashMap per doc; SumAggregationFunction.aggregateGroupBySV, MinAggregationFunction / Max... per doc) are

@@ -1,5 +1,5 @@
 // Combine trim on the device for group-by results that stay in HBM (the partitioned sparse
-// group-by, pgx_host.cpp run_partitioned), and the gather of selected groups.
+// group-by, pgx_part.cpp run_partitioned), and the gather of selected groups.
 //
 // The reference trims the combined map when it holds more than 20 x max(topN, 1000) groups: per aggregation function
 // a MinMaxPriorityQueue keeps the 5 x max(topN, 1000) best values, largest first, smallest first for MIN functions
@@ -21,7 +21,7 @@ namespace pgx {
 // 2 ordered min, 3 ordered max.
 enum TrimKind : int { TK_COUNT = 0, TK_SUM = 1, TK_MIN = 2, TK_MAX = 3, TK_AVG = 4 };
 
-// Layout shared with pgx_host.cpp (device_trims writes k, kmin = ~0 and zeros before the launch).  One state per
+// Layout shared with pgx_part.cpp (device_trim writes k, kmin = ~0 and zeros before the launch).  One state per
 // function: every kernel below takes an array of states and the function slot is blockIdx.y.
 struct TrimState {
   unsigned long long prefix;   // selected high bits of the threshold key          (offset 0)
@@ -371,7 +371,7 @@ __global__ void __launch_bounds__(256) pgx_group_gather(const uint64_t* __restri
 
 }  // namespace pgx
 
-// Host launchers (pgx_host.cpp).  The nf state blocks are prepared by the caller: k = groups wanted, kmin = ~0,
+// Host launchers (pgx_part.cpp device_trim).  The nf state blocks are prepared by the caller: k = groups wanted, kmin = ~0,
 // everything else zero.  kinds[f]: TrimKind of function slot f.  At most 8 histogram passes (8-bit digits); passes after
 // a function's threshold is complete return at once.
 extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,

@@ -109,7 +109,7 @@ WORKLOADS: Dict[str, Workload] = {
     # C6: a query over twelve columns (ten filter leaves): more than the eight columns round 3's query kernels took,
     # the shape that ran on the interpreter kernel before (VERDICT r03 missing #3); not a BASELINE config
     # (an OR of scan leaves: its numEntriesScannedInFilter has a closed form the kernel counts, where an AND of scan
-    # leaves needs the statistics automaton, pgx_host.cpp stats_closed_form)
+    # leaves needs the statistics automaton, pgx_plan.cpp stats_closed_form)
     "c6": Workload("c6", "12-column scan (ten range leaves ORed over 8/10/12-bit columns, ~34% of rows selected), "
                    "group by gk (card 1000), sum(m): 4 x 125M rows",
                    4, 125_000_000,

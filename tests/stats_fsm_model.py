@@ -1,5 +1,5 @@
 """Test infrastructure: the per-row "sweep" model of numEntriesScannedInFilter that libpgx's statistics automaton
-(pgx_host.cpp FilterStatsFsm, pgx_kernels.hip pgx_fsm_*) is built from, restated in Python so it can be checked against
+(pgx_stats.cpp fsm_build, pgx_kernels.hip pgx_fsm_*) is built from, restated in Python so it can be checked against
 the oracle's literal iterator algebra (oracle/pinot_oracle.py filter_docs) on random filter trees.
 
 Every iterator of the reference filter algebra (SVScanDocIdIterator, Bitmap/Sorted/RangelessBitmapDocIdIterator,

@@ -1,4 +1,4 @@
-"""GPU parity of the partitioned sparse group-by (pgx_host.cpp run_partitioned: record-emitting query kernel, two
+"""GPU parity of the partitioned sparse group-by (pgx_part.cpp run_partitioned: record-emitting query kernel, two
 radix passes, per-partition LDS aggregation) for LONG_MAP-sized key spaces: against the oracle, against the global
 hash-table path (PGX_X_NO_PARTITION), across segments with different group dictionaries, and through its resize /
 re-split / fallback branches (PGX_DEBUG=part_small starts from undersized buckets and a single pass)."""
@@ -370,7 +370,7 @@ def test_partitioned_per_segment_metric_dictionaries(ctx, metric):
 
 @pytest.mark.parametrize("mode", ["narrow", "radix"])
 def test_partitioned_plan_cache_replays(ctx, seg, mode, monkeypatch, capfd):
-    """A partitioned plan is kept with its slabs / buckets and partitions (pgx_host.cpp plan_cacheable, replay_narrow,
+    """A partitioned plan is kept with its slabs / buckets and partitions (pgx_plan_cache.cpp plan_cacheable, pgx_part.cpp replay_narrow,
     replay_part): the second and third executions of the same query over the same segment replay it (the host-profile
     line's "cached" mark; no second narrow sizing run), and every result -- decoded only after all three ran, so each
     result's group outputs are its own and the shared key tables outlive the replays -- equals the oracle's."""
