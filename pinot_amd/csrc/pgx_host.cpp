@@ -833,9 +833,15 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
   const uint64_t slots = hash ? P.hash_cap : P.dense_slots;
   std::vector<int64_t> slot_ids;
   std::vector<unsigned long long> planes;  // [plane][group]
+  std::vector<unsigned long long> keys_lo, keys_hi;  // hash keys of the groups
   uint64_t ng = 0;
+  // first guess of the group count: the plan's previous execution's (a kept plan replays the same query), else <= 64k
+  auto guess = [&](uint64_t limit) {
+    const uint64_t g = P.last_groups ? std::max<uint64_t>(256, P.last_groups + P.last_groups / 4) : (uint64_t(1) << 16);
+    return std::max<uint64_t>(1, std::min<uint64_t>(limit, g));
+  };
   if (dense_dev) {
-    uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(slots, uint64_t(1) << 16));
+    uint64_t cap = guess(slots);
     for (;;) {
       const size_t bytes = 256 + size_t(cap) * 8 * (1 + K.num_planes);
       DevBuf res(ctx, bytes);
@@ -848,9 +854,10 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
       hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
       hip_check(hipMemcpyAsync(hres.p, res.p, bytes, hipMemcpyDeviceToHost, st), "groups D2H");
       hip_check(hipStreamSynchronize(st), "sync");
+      prof_mark("f.sync");
       const unsigned long long* h = reinterpret_cast<const unsigned long long*>(hres.p);
       const uint64_t cnt = h[0];
-      if (cnt > cap) {  // more groups than the first guess: once more at the exact size
+      if (cnt > cap) {  // more groups than the guess: once more at the exact size
         cap = cnt;
         continue;
       }
@@ -861,9 +868,55 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
         std::memcpy(planes.data() + p * ng, h + 32 + cap + p * cap, ng * 8);
       break;
     }
+    P.last_groups = ng;
+  } else if (hash && K.num_gcols > 0) {
+    // compaction, key gather and read-back of the live groups in ONE round trip at the guessed size (the gather reads
+    // the group count on the device); again at the exact size if the guess was short
+    // (the outputs block travels with the groups; at most one group per slot)
+    const uint64_t cap_max = std::max<uint64_t>(1, slots);
+    const uint64_t kw = (K.group_mode == G_HASH128) ? 2 : 1;
+    uint64_t cap = guess(cap_max);
+    for (;;) {
+      const size_t bytes = 256 + size_t(cap) * 8 * (1 + K.num_planes + kw);
+      DevBuf res(ctx, bytes);
+      PinnedBuf hres(ctx, bytes);
+      unsigned long long* rb = devp(res);
+      int64_t* oslot = reinterpret_cast<int64_t*>(rb + 32);
+      unsigned long long* oplanes = rb + 32 + cap;
+      unsigned long long* okeys = rb + 32 + cap * (1 + K.num_planes);
+      hip_check(hipMemsetAsync(rb, 0, 8, st), "memset");
+      PGX_LAUNCH(st, "pgx_compact", pgx_launch_compact(K.table, slots, K.num_planes, rb, oslot, oplanes, cap, st),
+                 "compact");
+      PGX_LAUNCH(st, "pgx_gather_keys", pgx_launch_gather_keys(K.keys, oslot, rb, int64_t(cap), int(kw), okeys, st),
+                 "gather keys");
+      hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
+      hip_check(hipMemcpyAsync(hres.p, res.p, bytes, hipMemcpyDeviceToHost, st), "groups D2H");
+      hip_check(hipStreamSynchronize(st), "sync");
+      prof_mark("f.sync");
+      const unsigned long long* h = reinterpret_cast<const unsigned long long*>(hres.p);
+      const uint64_t cnt = std::min<uint64_t>(h[0], cap_max);
+      if (cnt > cap) {
+        cap = cnt;
+        continue;
+      }
+      ng = cnt;
+      slot_ids.assign(reinterpret_cast<const int64_t*>(h + 32), reinterpret_cast<const int64_t*>(h + 32) + ng);
+      planes.resize(ng * K.num_planes);
+      for (int p = 0; p < K.num_planes; ++p) std::memcpy(planes.data() + p * ng, h + 32 + cap + p * cap, ng * 8);
+      const unsigned long long* gk = h + 32 + cap * (1 + K.num_planes);
+      keys_lo.resize(ng);
+      keys_hi.resize(ng, 0);
+      for (uint64_t i = 0; i < ng; ++i) {
+        keys_lo[i] = gk[i * kw];
+        if (kw == 2) keys_hi[i] = gk[i * 2 + 1];
+      }
+      break;
+    }
+    P.last_groups = ng;
   } else if (!dense_host_override) {  // one read-back of every output plane and statistic
     hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
     hip_check(hipStreamSynchronize(st), "sync");
+    prof_mark("f.sync");
   }
   const unsigned long long* stats = outs + 16;
   R->stats[0] = int64_t(stats[0]);
@@ -891,7 +944,6 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     }
     return;
   }
-  std::vector<unsigned long long> keys_lo, keys_hi;
   if (dense_host_override) {
     for (uint64_t s = 0; s < slots; ++s)
       if (dense_host_override[s]) slot_ids.push_back(int64_t(s));
@@ -899,51 +951,22 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     planes.resize(ng * K.num_planes);
     for (int p = 0; p < K.num_planes; ++p)
       for (uint64_t i = 0; i < ng; ++i) planes[p * ng + i] = dense_host_override[p * slots + slot_ids[i]];
-  } else if (hash) {
-    DevBuf counter(ctx, 64);
-    hip_check(hipMemsetAsync(counter.p, 0, 8, st), "memset");
-    // at most one group per selected doc -- except multi-value group keys (several keys per doc: g_count_plane set)
-    const uint64_t cap = P.g_count_plane.empty()
-                             ? std::max<uint64_t>(1, std::min<uint64_t>(slots, uint64_t(std::max<int64_t>(stats[0], 1))))
-                             : slots;
-    DevBuf oslot(ctx, cap * 8), oplanes(ctx, cap * K.num_planes * 8);
-    PGX_LAUNCH(st, "pgx_compact", pgx_launch_compact(K.table, slots, K.num_planes, devp(counter), oslot.as<int64_t>(), devp(oplanes), cap,
-                                 st),
-              "compact");
-    unsigned long long cnt = 0;
-    hip_check(hipMemcpyAsync(&cnt, counter.p, 8, hipMemcpyDeviceToHost, st), "D2H");
-    hip_check(hipStreamSynchronize(st), "sync");
-    ng = std::min<uint64_t>(cnt, cap);
-    slot_ids.resize(ng);
-    planes.resize(ng * K.num_planes);
-    std::vector<unsigned long long> gk;
-    if (ng) {  // only the ng live groups travel: their slots, planes and (gathered on the device) keys
-      const uint64_t kw = (K.group_mode == G_HASH128) ? 2 : 1;
-      DevBuf okeys(ctx, ng * kw * 8);
-      PGX_LAUNCH(st, "pgx_gather_keys",
-                 pgx_launch_gather_keys(K.keys, oslot.as<int64_t>(), int64_t(ng), int(kw),
-                                        reinterpret_cast<unsigned long long*>(okeys.p), st),
-                 "gather keys");
-      gk.resize(ng * kw);
-      hip_check(hipMemcpyAsync(slot_ids.data(), oslot.p, ng * 8, hipMemcpyDeviceToHost, st), "D2H");
-      for (int p = 0; p < K.num_planes; ++p)
-        hip_check(hipMemcpyAsync(planes.data() + p * ng, static_cast<char*>(oplanes.p) + p * cap * 8, ng * 8,
-                                 hipMemcpyDeviceToHost, st),
-                  "D2H");
-      hip_check(hipMemcpyAsync(gk.data(), okeys.p, ng * kw * 8, hipMemcpyDeviceToHost, st), "keys D2H");
-      hip_check(hipStreamSynchronize(st), "sync");
-      keys_lo.resize(ng);
-      keys_hi.resize(ng, 0);
-      for (uint64_t i = 0; i < ng; ++i) {
-        keys_lo[i] = gk[i * kw];
-        if (kw == 2) keys_hi[i] = gk[i * 2 + 1];
-      }
-    }
   }
+  prof_mark("f.groups");
   // ARRAY_BASED iteration order is ascending raw key (DefaultGroupKeyGenerator.java:613-644): sort dense slots.
   std::vector<uint64_t> order(ng);
   std::iota(order.begin(), order.end(), 0);
-  if (!hash) std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return slot_ids[a] < slot_ids[b]; });
+  if (!hash && ng > 1) {
+    if (slots <= 64 * ng + 65536) {  // slot ids are distinct and < slots: place them (one pass over the slot range)
+      std::vector<int64_t> at(slots, -1);
+      for (uint64_t i = 0; i < ng; ++i) at[uint64_t(slot_ids[i])] = int64_t(i);
+      uint64_t k = 0;
+      for (uint64_t s = 0; s < slots; ++s)
+        if (at[s] >= 0) order[k++] = uint64_t(at[s]);
+    } else {
+      std::sort(order.begin(), order.end(), [&](uint64_t a, uint64_t b) { return slot_ids[a] < slot_ids[b]; });
+    }
+  }
   R->num_groups = int64_t(ng);
   R->key_seg.assign(K.num_gcols, std::vector<int32_t>(ng));
   R->key_id.assign(K.num_gcols, std::vector<int32_t>(ng));
@@ -952,7 +975,10 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     for (int g = 0; g < K.num_gcols; ++g) {
       int64_t gid;
       if (!hash) {
-        gid = int64_t((uint64_t(slot_ids[i]) / K.gmul[g]) % uint64_t(P.gdicts[g].card));
+        const uint64_t sl = uint64_t(slot_ids[i]);
+        if (K.num_gcols == 1) gid = int64_t(sl);  // one column: the slot is the id
+        else if (slots <= 0xFFFFFFFFull) gid = int64_t((uint32_t(sl) / uint32_t(K.gmul[g])) % uint32_t(P.gdicts[g].card));
+        else gid = int64_t((sl / K.gmul[g]) % uint64_t(P.gdicts[g].card));
       } else {
         const unsigned long long w = K.ghi[g] ? keys_hi[i] : keys_lo[i];
         gid = int64_t((w >> K.gshift[g]) & ((1ull << P.gbits[g]) - 1ull));
@@ -975,6 +1001,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
       else if (cp >= 0) R->g_count[a][oi] = int64_t(planes[uint64_t(cp) * ng + i]);
     }
   }
+  prof_mark("f.decode");
 }
 
 uint64_t initial_hash_cap(pgx_segment* const* segs, int n, const ExecPlan& P) {

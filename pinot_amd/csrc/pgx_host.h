@@ -42,8 +42,9 @@ extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t
 extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
                                          unsigned long long* counter, int64_t* out_slot,
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
-extern "C" hipError_t pgx_launch_gather_keys(const unsigned long long* keys, const int64_t* slot, int64_t n, int kw,
-                                             unsigned long long* out, hipStream_t stream);
+extern "C" hipError_t pgx_launch_gather_keys(const unsigned long long* keys, const int64_t* slot,
+                                             const unsigned long long* n_dev, int64_t n, int kw, unsigned long long* out,
+                                             hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring(const pgx::RDesc* descs, int npairs, int maxchunks, hipStream_t stream);
 extern "C" hipError_t pgx_launch_roaring_program_wave(const pgx::RProg* progs, const pgx::RDesc* descs, int nprogs,
                                                       int maxchunks, int nslots, hipStream_t stream);
@@ -813,6 +814,7 @@ struct ExecPlan {
   // narrow records (run_narrow, the default for partitioned plans that qualify): the scan writes dictId records split
   // 256 ways into per-workgroup slabs (part_slab with kNarrow1Bits), u32 in kq.table and bits 32..47 in part_hi
   bool part_narrow = false;
+  uint64_t last_groups = 0;  // groups of this plan's previous execution (finish_result's first read-back size)
   std::shared_ptr<const std::vector<std::vector<int32_t>>> lazy_rep_seg, lazy_rep_id;  // part_result's key tables
   int narrow_vd = 0;              // dictId bits of the value column (0: COUNT only)
   int narrow_k2min = 0;           // second-split bits the record width needs
