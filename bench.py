@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--rows", type=int, default=0, help="override rows per segment (smoke/debug only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--profile-iters", type=int, default=0, help="only run K steps (for rocprofv3 PMC passes)")
+    ap.add_argument("--no-partition", action="store_true",
+                    help="sparse group-by through the global hash table (PGX_X_NO_PARTITION), not the partitioned path")
     return ap.parse_args()
 
 
@@ -288,6 +290,8 @@ def main():
         r = C.c_void_p()
         hs = streams[i % inflight].cuda_stream
         flags = N.PGX_X_THROUGHPUT if inflight > 1 else 0  # queries overlap: one launch per kernel, not batches
+        if args.no_partition:
+            flags |= N.PGX_X_NO_PARTITION
         if dense:
             d = dense_t[i % inflight]
             opts = N.ExecOpts(hs, C.c_void_p(d.data_ptr()), d.numel() * 8, N.PGX_X_KEEP_DENSE_ON_DEVICE | flags)
@@ -453,7 +457,7 @@ def main():
     achieved = algo_bytes / (kernel_ms * 1e-3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "traffic_%s.json" % wl.name)
-    if os.path.exists(tf):
+    if os.path.exists(tf) and not args.no_partition:  # (the traffic files are the default execution's)
         tj = json.load(open(tf))
         # PMC FETCH/WRITE of the same command (tools/profile_wl.sh), valid only for the kernel sources it was measured
         # on: a stale file (sources changed since) reports null instead of an old number
@@ -481,7 +485,8 @@ def main():
         "data": "synthetic: device-generated v1 fixed-bit segments (seed %d), dictionaries per SURVEY 8d" % wl.seed,
         "config": {"workload": wl.name + ": " + wl.description, "query": wl.query,
                    "rows_per_segment": rows, "segments": len(segs) * (world if wl.scaling == "weak" else 1),
-                   "rows_total": total_rows, "parallelism": "dp%d (segment sharding)" % world},
+                   "rows_total": total_rows, "parallelism": "dp%d (segment sharding)" % world,
+                   **({"exec": "PGX_X_NO_PARTITION (global hash table)"} if args.no_partition else {})},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel_name, "kernel_ms": kernel_ms, "algorithmic_bytes": algo_bytes,

@@ -1393,7 +1393,8 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     // at one slot per row of a wide key space -- a 64M-slot table costs more to clear and compact than the scan (C7:
     // 330 ms of host and device per query).  An overflow reruns at the row-count estimate at once (C3-sized group
     // counts: one short failed pass -- every lane stops probing at the first overflow -- then one full pass)
-    if (!P.jit.empty()) P.hash_cap = std::min<uint64_t>(P.hash_cap, uint64_t(1) << 20);
+    if (!P.jit.empty())
+      P.hash_cap = std::min<uint64_t>(P.hash_cap, std::max<uint64_t>(uint64_t(1) << 20, q.hash_cap_hint.load()));
   }
   for (int attempt = 0; attempt < 6; ++attempt) {
     alloc_outputs(ctx, P, B, opts ? opts->dense_out : nullptr, opts ? opts->dense_out_bytes : 0);
@@ -1408,6 +1409,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     P.hash_cap = std::max(P.hash_cap * 4, hash_est);  // table full: grow and rerun
     if (attempt == 5) fail(PGX_ERR_OOM, "group-by hash table overflow");
   }
+  if (hash && P.hash_cap > q.hash_cap_hint.load()) q.hash_cap_hint.store(P.hash_cap);
   complete_scan(ctx, q, P, B, segs, n, opts, st, R);
   hp.mark("finish");
   if (cache && plan_cacheable(P)) plan_cache_insert(&q, ctx, segs, n, std::move(uids), pkey, std::move(Pp), std::move(Bp));

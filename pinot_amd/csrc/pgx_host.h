@@ -1,7 +1,8 @@
 // libpgx host side: what its translation units share.  pgx_host.cpp holds the C ABI of include/pgx.h and query execution
 // (launches, result read-back, batched and cached runs); pgx_plan.cpp the per-query planning; pgx_stage.cpp segment
 // staging; pgx_part.cpp the partitioned sparse group-by runtime and the device-resident results it produces;
-// pgx_plan_cache.cpp, pgx_mv.cpp, pgx_multi.cpp, pgx_realtime.cpp and pgx_fixtures.cpp as their names say.  Context, segment, query, result and plan types live here.
+// pgx_plan_cache.cpp, pgx_mv.cpp, pgx_multi.cpp, pgx_realtime.cpp and pgx_fixtures.cpp as their names say.  Context,
+// segment, query, result and plan types live here.
 // Reference paths are relative to pinot-core/src/main/java/com/linkedin/pinot/core/.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -579,6 +580,20 @@ struct pgx_query {
   uint32_t flags = 0;
   std::vector<KeyDomain> key_domain;  // [group column]
   Knobs kn;                           // the PGX_* environment when the query was compiled (read_knobs)
+  // global hash-table size the query's last execution needed (run_query starts there instead of at 1M slots and
+  // overflowing once more): a start size only, never a result input
+  struct Hint {  // an atomic that copies by value (a query is copied for its multi-value part, pgx_mv.cpp)
+    mutable std::atomic<uint64_t> v{0};
+    Hint() = default;
+    Hint(const Hint& o) : v(o.v.load()) {}
+    Hint& operator=(const Hint& o) {
+      v.store(o.v.load());
+      return *this;
+    }
+    uint64_t load() const { return v.load(); }
+    void store(uint64_t x) const { v.store(x); }
+  };
+  Hint hash_cap_hint;
 };
 
 // =================================================================================================
