@@ -1354,6 +1354,14 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
   hp.mark("upload");
   plan_jit(ctx, q, segs, n, P, B);
   hp.mark("jit");
+  if (P.use_part && P.part_cols.size() > 1) {  // several value columns: one pipeline run per column, joined by key
+    if (run_value_columns(ctx, q, segs, n, P, B, st, R)) {
+      hp.mark("finish");
+      return;
+    }
+    P.use_part = false;
+    P.jit.clear();
+  }
   if (P.use_part) {
     if (P.part_narrow) {
       NarrowBuffers NB;
@@ -1703,6 +1711,7 @@ pgx_status pgx_result_device_groups(const pgx_result* r, int64_t* n, void* recor
     if (!r || !n) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     r->ready();
     if (!r->group_by || !r->lazy) fail(PGX_ERR_UNSUPPORTED, "the groups of this result are not in device memory");
+    if (r->lazy->nplanes != 4) fail(PGX_ERR_UNSUPPORTED, "group records hold one value column");
     *n = r->num_groups;
     if (!records || !r->num_groups) return;
     const auto& L = *r->lazy;
@@ -1841,11 +1850,11 @@ pgx_status pgx_result_gather(const pgx_result* r, const int64_t* gi, int64_t n, 
       const auto& L = *r->lazy;
       hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
       hipStream_t st = L.ctx->stream;
-      DevBuf di(L.ctx, size_t(n) * 8), out(L.ctx, size_t(n) * 5 * 8);
-      std::vector<uint64_t> h(size_t(n) * 5);
+      DevBuf di(L.ctx, size_t(n) * 8), out(L.ctx, size_t(n) * (1 + L.nplanes) * 8);
+      std::vector<uint64_t> h(size_t(n) * (1 + L.nplanes));
       hip_check(hipMemcpyAsync(di.p, gi, size_t(n) * 8, hipMemcpyHostToDevice, st), "gather H2D");
-      PGX_LAUNCH(st, "pgx_group_gather", pgx_launch_group_gather(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, di.as<int64_t>(), n,
-                                        out.as<uint64_t>(), st),
+      PGX_LAUNCH(st, "pgx_group_gather", pgx_launch_group_gather(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, L.nplanes,
+                                        di.as<int64_t>(), n, out.as<uint64_t>(), st),
                 "gather launch");
       hip_check(hipMemcpyAsync(h.data(), out.p, h.size() * 8, hipMemcpyDeviceToHost, st), "gather D2H");
       hip_check(hipStreamSynchronize(st), "sync");
@@ -2082,6 +2091,10 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
     PartBuffers PB;
     NarrowBuffers NB;
     bool narrow = false;
+    if (P.use_part && P.part_cols.size() > 1) {  // (several value columns: timed through the global hash table)
+      P.use_part = false;
+      P.jit.clear();
+    }
     if (P.use_part && P.part_narrow) {  // untimed: checks the narrow capacities
       narrow = run_narrow(ctx, P, B, NB, st);
       if (!narrow) narrow_fallback(ctx, *q, segs, n, P, B);

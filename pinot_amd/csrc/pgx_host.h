@@ -68,11 +68,12 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
                                                 uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream);
-extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
+extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds,
+                                      const int* planes, int nf,
                                       void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
                                       const unsigned long long* prange, int64_t* cidx, uint64_t* ckey, int64_t ccap,
                                       hipStream_t stream);
-extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
+extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap, int nplanes,
                                               const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream);
 extern "C" size_t pgx_trim_state_bytes(void);
 extern "C" hipError_t pgx_launch_pack_remap(uint32_t* out_words, const int32_t* ids, const int32_t* remap,
@@ -92,6 +93,10 @@ extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const u
                                      uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream);
 extern "C" hipError_t pgx_launch_dense_reduce(unsigned long long* dst, const unsigned long long* src, uint64_t slots,
                                               int nplanes, uint64_t ops, hipStream_t stream);
+extern "C" hipError_t pgx_launch_join(const uint64_t* okey0, int64_t n0, const uint64_t* okey, const uint64_t* opl,
+                                      int64_t ocap, int64_t n, unsigned long long* tkey, int64_t* tidx, uint64_t cap,
+                                      uint64_t* comb, int64_t ccap, int base, unsigned long long* miss,
+                                      hipStream_t stream);
 extern "C" hipError_t pgx_launch_group_merge(const uint64_t* key, const uint64_t* pl, int64_t es, int64_t ps,
                                              int64_t n, unsigned long long* tkey, unsigned long long* tpl,
                                              uint64_t cap, unsigned long long* overflow, hipStream_t stream);
@@ -680,7 +685,9 @@ struct pgx_result {
   // Partitioned group-by (run_partitioned): the groups stay in device memory until an accessor needs them.
   struct Lazy {
     pgx_ctx* ctx = nullptr;      // holds a context reference (the result may outlive the caller's handle)
-    DevBuf okey, oplane;         // packed keys; planes [count, sum, min, max] x ocap
+    DevBuf okey, oplane;         // packed keys; planes x ocap: count, then sum, min, max per value column
+    int nplanes = 4;             // 1 + 3 x value columns
+    std::vector<int> agg_plane;  // per function: the plane its value is decoded from (COUNT: 0)
     DevBuf prange;               // trim-key ranges per kind (pgx_narrow_aggregate), or none: the trim's range pass
     int64_t ocap = 0;
     std::vector<int> gshift, gbits;
@@ -838,6 +845,33 @@ struct ExecPlan {
   int narrow_img_words = 0, narrow_img_sh = 0;
   uint64_t narrow_vrange = 0;     // largest value offset (value - vbase)
   unsigned short* part_hi = nullptr;
+  // One value column's partitioned-path settings (the fields above from part_vcol to narrow_vrange).  A query whose
+  // functions read several value columns runs the pipeline once per column (pgx_part.cpp run_value_columns) and joins
+  // the passes' groups by key; part_cols[0] is loaded into the fields above at planning.
+  struct PartCol {
+    int vcol = -1, vbits = 0;
+    int64_t vbase = 0;
+    bool sum = false, mn = false, mx = false, dictid = false, slab = false, narrow = false;
+    const int64_t* vdict = nullptr;
+    int vd = 0, k2min = 0, img = 0, img_words = 0, img_sh = 0;
+    const uint32_t* imgp = nullptr;
+    uint64_t vrange = 0;
+  };
+  std::vector<PartCol> part_cols;
+  PartCol save_part_col() const {
+    PartCol c;
+    c.vcol = part_vcol, c.vbits = part_vbits, c.vbase = part_vbase;
+    c.sum = part_sum, c.mn = part_min, c.mx = part_max, c.dictid = part_dictid, c.slab = part_slab, c.narrow = part_narrow;
+    c.vdict = part_vdict, c.vd = narrow_vd, c.k2min = narrow_k2min, c.img = narrow_img, c.img_words = narrow_img_words;
+    c.img_sh = narrow_img_sh, c.imgp = narrow_imgp, c.vrange = narrow_vrange;
+    return c;
+  }
+  void load_part_col(const PartCol& c) {
+    part_vcol = c.vcol, part_vbits = c.vbits, part_vbase = c.vbase;
+    part_sum = c.sum, part_min = c.mn, part_max = c.mx, part_dictid = c.dictid, part_slab = c.slab, part_narrow = c.narrow;
+    part_vdict = c.vdict, narrow_vd = c.vd, narrow_k2min = c.k2min, narrow_img = c.img, narrow_img_words = c.img_words;
+    narrow_img_sh = c.img_sh, narrow_imgp = c.imgp, narrow_vrange = c.vrange;
+  }
   std::vector<int64_t> rec_base; // per segment: index of its row 0 in the record array
   int64_t rec_total = 0;
   struct JitGroup {
@@ -914,6 +948,7 @@ struct PartBuffers {
   int64_t out1_recs() const { return int64_t(kPart1N) * cap1; }
 };
 
+constexpr int kPartMaxValueCols = 4;  // value columns of one partitioned plan (one pipeline run each)
 constexpr int kNarrowSlots = 192;  // pgx_narrow.hip kNASlots: one wavefront's table
 constexpr int kNarrowMaxWg = 1024; // pgx_narrow.hip kN2MaxSlabs
 
@@ -1017,4 +1052,6 @@ bool run_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hi
 bool replay_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hipStream_t st);
 void narrow_fallback(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B);
 void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, PartBuffers& PB, pgx_result* R);
+bool run_value_columns(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B,
+                       hipStream_t st, pgx_result* R);
 }  // namespace pgxh

@@ -112,6 +112,58 @@ __global__ void __launch_bounds__(256) pgx_gather_keys(const unsigned long long*
   }
 }
 
+// Joining the passes of a partitioned plan over several value columns (pgx_part.cpp run_value_columns): every pass
+// finds the same groups (the filter and the keys are the same) in its own order.  pgx_join_build puts the first pass's
+// keys in an open-addressing table (key -> index in the first pass); pgx_join_scatter looks up each group of a later
+// pass and writes its sum / min / max planes into the combined planes at the first pass's index.  A key the table does
+// not hold counts in *miss (cannot happen: the host fails the query if it does).
+__global__ void __launch_bounds__(256) pgx_join_build(const uint64_t* __restrict__ okey, int64_t n,
+                                                      unsigned long long* __restrict__ tkey,
+                                                      int64_t* __restrict__ tidx, uint64_t cap) {
+  const uint64_t mask = cap - 1;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const unsigned long long k = okey[i];
+    uint64_t h = merge_mix(k) & mask;
+    for (uint64_t probe = 0; probe < cap; ++probe) {
+      if (atomicCAS(tkey + h, kMergeEmpty, k) == kMergeEmpty) {  // keys are distinct: a free slot, never our key
+        tidx[h] = i;
+        break;
+      }
+      h = (h + 1) & mask;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) pgx_join_scatter(const uint64_t* __restrict__ okey,
+                                                        const uint64_t* __restrict__ opl, int64_t ocap, int64_t n,
+                                                        const unsigned long long* __restrict__ tkey,
+                                                        const int64_t* __restrict__ tidx, uint64_t cap,
+                                                        uint64_t* __restrict__ comb, int64_t ccap, int base,
+                                                        unsigned long long* __restrict__ miss) {
+  const uint64_t mask = cap - 1;
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const unsigned long long k = okey[i];
+    uint64_t h = merge_mix(k) & mask;
+    int64_t j = -1;
+    for (uint64_t probe = 0; probe < cap; ++probe) {
+      const unsigned long long t = tkey[h];
+      if (t == k) {
+        j = tidx[h];
+        break;
+      }
+      if (t == kMergeEmpty) break;
+      h = (h + 1) & mask;
+    }
+    if (j < 0) {
+      atomicAdd(miss, 1ull);
+      continue;
+    }
+    for (int p = 0; p < 3; ++p) comb[(base + p) * ccap + j] = opl[(1 + p) * ocap + i];  // sum, min, max
+  }
+}
+
 // Columnar groups (okey, oplane[p * ocap + i]) -> records of 5 words (key, count, sum, min, max) for an exchange.
 __global__ void __launch_bounds__(256) pgx_group_pack(const uint64_t* __restrict__ okey,
                                                       const uint64_t* __restrict__ opl, int64_t ocap, int64_t n,
@@ -143,6 +195,26 @@ extern "C" hipError_t pgx_launch_gather_keys(const unsigned long long* keys, con
   if (kw < 1 || kw > 2) return hipErrorInvalidValue;
   const unsigned grid = static_cast<unsigned>(n / 256 + 1 < 16384 ? n / 256 + 1 : 16384);
   hipLaunchKernelGGL(pgx::pgx_gather_keys, dim3(grid), dim3(256), 0, stream, keys, slot, n_dev, n, kw, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_join(const uint64_t* okey0, int64_t n0, const uint64_t* okey, const uint64_t* opl,
+                                      int64_t ocap, int64_t n, unsigned long long* tkey, int64_t* tidx, uint64_t cap,
+                                      uint64_t* comb, int64_t ccap, int base, unsigned long long* miss,
+                                      hipStream_t stream) {
+  // okey0 != null: build the table from the first pass's n0 keys; else scatter a later pass's n groups
+  if (cap == 0 || (cap & (cap - 1)) != 0 || !tkey || !tidx) return hipErrorInvalidValue;
+  if (okey0) {
+    if (n0 <= 0) return hipSuccess;
+    const unsigned grid = static_cast<unsigned>(n0 / 256 + 1 < 16384 ? n0 / 256 + 1 : 16384);
+    hipLaunchKernelGGL(pgx::pgx_join_build, dim3(grid), dim3(256), 0, stream, okey0, n0, tkey, tidx, cap);
+    return hipGetLastError();
+  }
+  if (n <= 0) return hipSuccess;
+  if (!okey || !opl || !comb || !miss || base < 1) return hipErrorInvalidValue;
+  const unsigned grid = static_cast<unsigned>(n / 256 + 1 < 16384 ? n / 256 + 1 : 16384);
+  hipLaunchKernelGGL(pgx::pgx_join_scatter, dim3(grid), dim3(256), 0, stream, okey, opl, ocap, n, tkey, tidx, cap, comb,
+                     ccap, base, miss);
   return hipGetLastError();
 }
 

@@ -396,9 +396,93 @@ void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, 
   L->rep_seg = P.lazy_rep_seg;
   L->rep_id = P.lazy_rep_id;
   for (int a = 0; a < K.num_aggs; ++a) L->agg_kind.push_back(K.agg_kind[a]);
+  // planes: count, then sum / min / max per value column in part_cols order (one column: the kernels' own layout)
+  L->nplanes = 1 + 3 * std::max<int>(1, int(P.part_cols.size()));
+  for (int a = 0; a < K.num_aggs; ++a) {
+    const int k = K.agg_kind[a];
+    int c = 0;
+    for (size_t i = 0; i < P.part_cols.size(); ++i)
+      if (P.part_cols[i].vcol == K.agg_col[a]) c = int(i);
+    L->agg_plane.push_back(k == A_COUNT ? 0 : 1 + 3 * c + (k == A_MIN ? 1 : (k == A_MAX ? 2 : 0)));
+  }
   ctx->refs.fetch_add(1);
   L->ctx = ctx;
   R->lazy = std::move(L);
+}
+
+// A partitioned plan over several value columns (SELECT SUM(a), MAX(b) ... GROUP BY sparse keys): the pipeline runs
+// once per column -- the emitted value and its record layout re-planned between passes (plan_jit), the key columns and
+// the filter the same -- and every later pass's sum / min / max planes are joined into the first pass's group order by
+// key on the device (pgx_merge.hip pgx_join_*).  The result carries 1 + 3 x columns planes.  False: a pass could not
+// run partitioned (the caller takes the global hash table for the whole query).
+bool run_value_columns(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B,
+                       hipStream_t st, pgx_result* R) {
+  const int V = int(P.part_cols.size());
+  const int NP = 1 + 3 * V;
+  DevBuf okey0, comb, tkey, tidx, miss(ctx, 64);
+  int64_t ng0 = 0, ccap = 1;
+  uint64_t tcap = 1024;
+  hip_check(hipMemsetAsync(miss.p, 0, 8, st), "join miss counter");
+  for (int v = 0; v < V; ++v) {
+    if (v > 0) {
+      P.load_part_col(P.part_cols[size_t(v)]);
+      plan_jit(ctx, q, segs, n, P, B);
+    }
+    PartBuffers PB;
+    bool ok = false;
+    if (P.part_narrow) {
+      NarrowBuffers NB;
+      if (run_narrow(ctx, P, B, NB, st)) {
+        PB.okey = std::move(NB.okey);
+        PB.oplane = std::move(NB.oplane);
+        PB.ocap = NB.ocap;
+        ok = true;
+      } else {
+        narrow_fallback(ctx, q, segs, n, P, B);
+      }
+    }
+    if (!ok && !run_partitioned(ctx, P, B, PB, st)) return false;
+    const unsigned long long* outs = reinterpret_cast<const unsigned long long*>(B.host.bytes() + B.off_outs);
+    const int64_t ng = int64_t(std::min<unsigned long long>(outs[28], uint64_t(PB.ocap)));
+    if (v == 0) {
+      ng0 = ng;
+      ccap = std::max<int64_t>(ng0, 1);
+      okey0 = std::move(PB.okey);
+      comb = DevBuf(ctx, size_t(ccap) * NP * 8);
+      for (int p = 0; p < 4; ++p)
+        if (ng0)
+          hip_check(hipMemcpyAsync(comb.as<uint64_t>() + p * ccap, PB.oplane.as<uint64_t>() + p * PB.ocap, ng0 * 8,
+                                   hipMemcpyDeviceToDevice, st),
+                    "first pass planes");
+      while (tcap < uint64_t(ng0) * 2) tcap <<= 1;
+      tkey = DevBuf(ctx, tcap * 8);
+      tidx = DevBuf(ctx, tcap * 8);
+      hip_check(hipMemsetAsync(tkey.p, 0xFF, tcap * 8, st), "join table");
+      PGX_LAUNCH(st, "pgx_join", pgx_launch_join(okey0.as<uint64_t>(), ng0, nullptr, nullptr, 0, 0, devp(tkey),
+                                                 tidx.as<int64_t>(), tcap, nullptr, 0, 0, nullptr, st),
+                 "join build");
+    } else {
+      if (ng != ng0) fail(PGX_ERR_INTERNAL, "value-column passes found different group counts");
+      PGX_LAUNCH(st, "pgx_join", pgx_launch_join(nullptr, 0, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(), PB.ocap,
+                                                 ng, devp(tkey), tidx.as<int64_t>(), tcap, comb.as<uint64_t>(), ccap,
+                                                 1 + 3 * v, devp(miss), st),
+                 "join scatter");
+      hip_check(hipStreamSynchronize(st), "sync");  // PB's buffers go out of scope: the scatter has read them
+    }
+  }
+  unsigned long long nmiss = 0;
+  hip_check(hipMemcpyAsync(&nmiss, miss.p, 8, hipMemcpyDeviceToHost, st), "D2H");
+  hip_check(hipStreamSynchronize(st), "sync");
+  if (nmiss) fail(PGX_ERR_INTERNAL, "value-column passes found different groups");
+  unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
+  outs[28] = uint64_t(ng0);
+  PartBuffers PR;
+  PR.okey = std::move(okey0);
+  PR.oplane = std::move(comb);
+  PR.ocap = ccap;
+  P.load_part_col(P.part_cols[0]);
+  part_result(ctx, q, P, B, PR, R);
+  return true;
 }
 
 }  // namespace pgxh
@@ -419,7 +503,7 @@ void pgx_result::decode_lazy(const uint64_t* keys, const uint64_t* planes, int64
   }
   for (int a = 0; a < int(L.agg_kind.size()); ++a) {
     const int k = L.agg_kind[a];
-    const int p = k == A_COUNT ? 0 : (k == A_MIN ? 2 : (k == A_MAX ? 3 : 1));
+    const int p = L.agg_plane[size_t(a)];
     const int op = k == A_MIN ? P_MIN_ORD : (k == A_MAX ? P_MAX_ORD : P_ADD_I64);
     for (int64_t i = 0; i < n; ++i) {
       if (count) count[a * out_stride + i] = int64_t(planes[i]);
@@ -433,10 +517,10 @@ void pgx_result::materialize() {
   if (!lazy) return;
   const int64_t ng = num_groups;
   hip_check(hipSetDevice(lazy->ctx->device), "hipSetDevice");
-  std::vector<uint64_t> keys(ng), pl(size_t(4) * ng);
+  std::vector<uint64_t> keys(ng), pl(size_t(lazy->nplanes) * ng);
   if (ng) {
     hip_check(hipMemcpy(keys.data(), lazy->okey.p, ng * 8, hipMemcpyDeviceToHost), "group keys D2H");
-    for (int p = 0; p < 4; ++p)
+    for (int p = 0; p < lazy->nplanes; ++p)
       hip_check(hipMemcpy(pl.data() + p * ng, lazy->oplane.as<uint64_t>() + p * lazy->ocap, ng * 8,
                           hipMemcpyDeviceToHost),
                 "group planes D2H");
@@ -471,10 +555,11 @@ const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
   if (!L.trims[fn].empty() && L.trim_size == size) return L.trims[fn];
   hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
   hipStream_t st = L.ctx->stream;
-  std::vector<int> kinds(nf);
+  std::vector<int> kinds(nf), planes(nf);
   for (int f = 0; f < nf; ++f) {
     const int k = L.agg_kind[f];
     kinds[f] = k == A_COUNT ? 0 : k == A_SUM ? 1 : k == A_MIN ? 2 : k == A_MAX ? 3 : 4;
+    planes[f] = L.agg_plane[size_t(f)];
   }
   const size_t sb = pgx_trim_state_bytes();
   std::vector<uint8_t> init(sb * nf, 0);
@@ -491,7 +576,7 @@ const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
   // threshold's bin at C3 holds a few 100k groups), at most every group
   const int64_t ccap = std::min<int64_t>(num_groups, std::max<int64_t>(int64_t(1) << 20, 32 * size));
   DevBuf cidx(L.ctx, size_t(std::max<int64_t>(ccap, 1)) * 8 * nf), ckey(L.ctx, size_t(std::max<int64_t>(ccap, 1)) * 8 * nf);
-  PGX_LAUNCH(st, "pgx_trim", pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kinds.data(), nf, state.p,
+  PGX_LAUNCH(st, "pgx_trim", pgx_launch_trim(L.oplane.as<uint64_t>(), L.ocap, num_groups, kinds.data(), planes.data(), nf, state.p,
                             idx.as<int64_t>(), keys.as<uint64_t>(), size, grid,
                             L.prange.p ? devp(L.prange) : nullptr, cidx.as<int64_t>(), ckey.as<uint64_t>(), ccap, st),
             "trim launch");

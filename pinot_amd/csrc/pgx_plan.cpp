@@ -863,60 +863,67 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   prof_mark("p.keys");
 
   // Partitioned group-by: sparse 64-bit keys go through record-emitting query kernels, radix partitioning and LDS
-  // aggregation (run_partitioned) instead of one global hash table.  Eligible when every non-COUNT function reads the
-  // same INT/LONG column whose dictionary is identical in every segment (one value base), with a value range of at
-  // most 32 bits, and key + value fit 63 bits.
+  // aggregation (run_partitioned / run_narrow) instead of one global hash table.  Eligible when every non-COUNT function
+  // reads an INT/LONG column (at most kPartMaxValueCols of them: one pipeline run per column, the passes' groups joined
+  // by key) whose values span at most 32 bits, and key + value offset fit 63 bits.
   P.use_part = false;
   P.part_slab = P.part_dictid = P.part_narrow = false;
   P.part_hi = nullptr;
+  P.part_cols.clear();
   if (K.group_mode == G_HASH64 && q.kn.jit && !(xflags & PGX_X_NO_PARTITION) &&
       K.num_qcols <= PGX_J_MAX_COLS) {
-    int vc = -1;
+    std::vector<int> vcols;
     bool ok = true;
-    bool need_sum = false, need_min = false, need_max = false;
     for (int a = 0; a < K.num_aggs && ok; ++a) {
-      const int k = K.agg_kind[a];
-      if (k == A_COUNT) continue;
-      if (K.agg_fp[a] || (vc >= 0 && vc != K.agg_col[a])) ok = false;
-      vc = K.agg_col[a];
-      need_sum |= k == A_SUM || k == A_AVG;
-      need_min |= k == A_MIN;
-      need_max |= k == A_MAX;
+      if (K.agg_kind[a] == A_COUNT) continue;
+      if (K.agg_fp[a]) ok = false;
+      if (std::find(vcols.begin(), vcols.end(), K.agg_col[a]) == vcols.end()) vcols.push_back(K.agg_col[a]);
     }
+    if (int(vcols.size()) > kPartMaxValueCols) ok = false;
     int keybits = 0;
     for (int g = 0; g < K.num_gcols; ++g) keybits = std::max(keybits, K.gshift[g] + P.gbits[g]);
-    int vbits = 0;
-    int64_t vbase = 0;
-    uint64_t vrange = 0;
-    bool same_dict = true;  // one dictionary in every segment: records may carry the dictId (narrow path)
-    if (ok && vc >= 0) {
-      // Value records carry value - vbase with ONE query-wide vbase (the smallest value of any segment's dictionary):
-      // each segment's records are rebased by (its image base - vbase) in the scan (JSeg.emit_rebase), so segments
-      // with their own dictionaries (SegmentDictionaryCreator builds one per segment) share the radix path.
-      const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
-      int64_t vmin = 0, vmax = 0;
-      for (int s = 0; s < n && ok; ++s) {
-        const StagedColumn& c = segs[s]->col(P.qcols[vc]);
-        ok = (c.data_type == PGX_INT || c.data_type == PGX_LONG) && !c.ivals.empty() && c.data_type == c0.data_type;
-        if (!ok) break;
-        const int64_t lo = *std::min_element(c.ivals.begin(), c.ivals.end());
-        const int64_t hi = *std::max_element(c.ivals.begin(), c.ivals.end());
-        vmin = s ? std::min(vmin, lo) : lo;
-        vmax = s ? std::max(vmax, hi) : hi;
-        same_dict = same_dict && c.dict_hash == c0.dict_hash && c.card == c0.card;
+    // one value column's settings into P (part_vcol ... narrow_vrange); false if the column does not qualify
+    auto config = [&](int vc) -> bool {
+      P.part_slab = P.part_dictid = P.part_narrow = false;
+      bool need_sum = false, need_min = false, need_max = false;
+      for (int a = 0; a < K.num_aggs; ++a) {
+        if (K.agg_kind[a] == A_COUNT || K.agg_col[a] != vc) continue;
+        need_sum |= K.agg_kind[a] == A_SUM || K.agg_kind[a] == A_AVG;
+        need_min |= K.agg_kind[a] == A_MIN;
+        need_max |= K.agg_kind[a] == A_MAX;
       }
-      if (ok) {
-        const uint64_t range = uint64_t(vmax) - uint64_t(vmin);
-        ok = range <= 0xFFFFFFFFull;
-        vbase = vmin;
-        vrange = range;
-        vbits = ok ? bits_for(int64_t(range) + 1) : 64;
+      bool cok = true;
+      int vbits = 0;
+      int64_t vbase = 0;
+      uint64_t vrange = 0;
+      bool same_dict = true;  // one dictionary in every segment: records may carry the dictId (narrow path)
+      if (vc >= 0) {
+        // Value records carry value - vbase with ONE query-wide vbase (the smallest value of any segment's
+        // dictionary): each segment's records are rebased by (its image base - vbase) in the scan (JSeg.emit_rebase),
+        // so segments with their own dictionaries (SegmentDictionaryCreator builds one per segment) share the path.
+        const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
+        int64_t vmin = 0, vmax = 0;
+        for (int s = 0; s < n && cok; ++s) {
+          const StagedColumn& c = segs[s]->col(P.qcols[vc]);
+          cok = (c.data_type == PGX_INT || c.data_type == PGX_LONG) && !c.ivals.empty() && c.data_type == c0.data_type;
+          if (!cok) break;
+          const int64_t lo = *std::min_element(c.ivals.begin(), c.ivals.end());
+          const int64_t hi = *std::max_element(c.ivals.begin(), c.ivals.end());
+          vmin = s ? std::min(vmin, lo) : lo;
+          vmax = s ? std::max(vmax, hi) : hi;
+          same_dict = same_dict && c.dict_hash == c0.dict_hash && c.card == c0.card;
+        }
+        if (cok) {
+          const uint64_t range = uint64_t(vmax) - uint64_t(vmin);
+          cok = range <= 0xFFFFFFFFull;
+          vbase = vmin;
+          vrange = range;
+          vbits = cok ? bits_for(int64_t(range) + 1) : 64;
+        }
       }
-    }
-    // The 8-byte radix path's records carry value offsets (round 3's dictId records with a fused first pass or
-    // per-workgroup slabs measured slower at C3 and were removed in round 5)
-    if (ok && keybits + vbits <= 63) {
-      P.use_part = true;
+      // The 8-byte radix path's records carry value offsets (round 3's dictId records with a fused first pass or
+      // per-workgroup slabs measured slower at C3 and were removed in round 5)
+      if (!cok || keybits + vbits > 63) return false;
       P.part_vcol = vc;
       P.part_keybits = keybits;
       P.part_vbits = vbits;
@@ -924,6 +931,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       P.part_sum = need_sum;
       P.part_min = need_min;
       P.part_max = need_max;
+      P.part_vdict = nullptr;
       // Narrow records (default; PGX_PART_NARROW=0 keeps the 8-byte radix path): the value's dictId rides in a record of
       // keybits - 8 + dictId bits (<= 48) out of the scan's own 256-way split, then <= 32 bits after the second split,
       // and the aggregation looks values up in the column's image (FOR16 / U32) in LDS (run_narrow).  Needs a sorted
@@ -954,7 +962,6 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
             imgk = 3;
             vd = vbits;
             k2 = k2d;
-            P.part_vdict = nullptr;
             P.narrow_imgp = nullptr;
             P.narrow_img_words = 0;
             P.narrow_img_sh = 0;
@@ -978,6 +985,19 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           P.narrow_img = imgk;
         }
       }
+      return true;
+    };
+    if (vcols.empty()) vcols.push_back(-1);  // COUNT only
+    for (size_t i = 0; i < vcols.size() && ok; ++i) {
+      ok = config(vcols[i]);
+      if (ok) P.part_cols.push_back(P.save_part_col());
+    }
+    if (ok) {
+      P.use_part = true;
+      P.load_part_col(P.part_cols[0]);
+    } else {
+      P.part_cols.clear();
+      P.part_slab = P.part_dictid = P.part_narrow = false;
     }
   }
 

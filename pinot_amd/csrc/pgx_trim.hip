@@ -41,8 +41,9 @@ constexpr int kTrimBins = 1 << kTrimDigit;
 constexpr int kTrimPasses = (64 + kTrimDigit - 1) / kTrimDigit;
 
 constexpr int kTrimMaxFns = 8;
-struct TrimKinds {             // function slot -> trim key kind
+struct TrimKinds {             // function slot -> trim key kind, and the plane holding its value (sum plane for AVG)
   int kind[kTrimMaxFns];
+  int plane[kTrimMaxFns];
 };
 
 // Where a pass reads its groups: the planes (trim_key of group i), or -- once pgx_trim_cand has run and its list fit --
@@ -58,20 +59,22 @@ __device__ __forceinline__ bool trim_use_cand(const TrimState* st, const TrimSrc
   return st->n_cand - 1ull < static_cast<unsigned long long>(S.ccap);  // 0 < n_cand <= ccap
 }
 
-// Larger key = better group.
-__device__ __forceinline__ uint64_t trim_key(const PGX_GLOBAL uint64_t* pl, int64_t ocap, int64_t i, int kind) {
+// Larger key = better group.  Plane 0 is the count; `plane` the function's value plane.
+__device__ __forceinline__ uint64_t trim_key(const PGX_GLOBAL uint64_t* pl, int64_t ocap, int64_t i, int kind,
+                                             int plane) {
+  const PGX_GLOBAL uint64_t* v = pl + static_cast<int64_t>(plane) * ocap;
   switch (kind) {
     case TK_COUNT:
       return pl[i];
     case TK_SUM:
-      return pl[ocap + i] ^ 0x8000000000000000ull;
+      return v[i] ^ 0x8000000000000000ull;
     case TK_MIN:
-      return ~pl[2 * ocap + i];
+      return ~v[i];
     case TK_MAX:
-      return pl[3 * ocap + i];
+      return v[i];
     default: {  // AVG: the ratio sum / count as an ordered double (AvgPair compares by value)
       const uint64_t c = pl[i];
-      const double d = c ? static_cast<double>(static_cast<int64_t>(pl[ocap + i])) / static_cast<double>(c) : 0.0;
+      const double d = c ? static_cast<double>(static_cast<int64_t>(v[i])) / static_cast<double>(c) : 0.0;
       const uint64_t b = static_cast<uint64_t>(__double_as_longlong(d));
       return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
     }
@@ -84,12 +87,12 @@ __global__ void __launch_bounds__(256) pgx_trim_range(const uint64_t* __restrict
                                                       const TrimKinds K, TrimState* __restrict__ sts) {
   __shared__ unsigned long long wmin[4], wmax[4];
   TrimState* st = sts + blockIdx.y;
-  const int kind = K.kind[blockIdx.y];
+  const int kind = K.kind[blockIdx.y], plane = K.plane[blockIdx.y];
   const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)oplane;
   unsigned long long lo = ~0ull, hi = 0ull;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * 256) {
-    const uint64_t key = trim_key(pl, ocap, i, kind);
+    const uint64_t key = trim_key(pl, ocap, i, kind, plane);
     lo = key < lo ? key : lo;
     hi = key > hi ? key : hi;
   }
@@ -152,14 +155,14 @@ __global__ void __launch_bounds__(256) pgx_trim_hist(const TrimSrc S, const Trim
   const PGX_GLOBAL uint64_t* ck = (const PGX_GLOBAL uint64_t*)S.ckey + static_cast<int64_t>(blockIdx.y) * S.ccap;
   __shared__ unsigned int lh[kTrimBins];
   const int tid = threadIdx.x;
-  const int kind = K.kind[blockIdx.y];
+  const int kind = K.kind[blockIdx.y], plane = K.plane[blockIdx.y];
   for (int b = tid; b < kTrimBins; b += 256) lh[b] = 0u;
   __syncthreads();
   const unsigned long long prefix = st->prefix, mask = st->mask;
   const int shift = st->shift;
   const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)S.oplane;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + tid; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
-    const uint64_t key = cand ? ck[i] : trim_key(pl, S.ocap, i, kind);
+    const uint64_t key = cand ? ck[i] : trim_key(pl, S.ocap, i, kind, plane);
     if ((key & mask) == prefix) atomicAdd(&lh[(key >> shift) & (kTrimBins - 1u)], 1u);
   }
   __syncthreads();
@@ -181,7 +184,7 @@ __global__ void __launch_bounds__(256) pgx_trim_cand(const TrimSrc S, const Trim
   __shared__ unsigned long long gbase;
   TrimState* st = sts + blockIdx.y;
   if (st->done) return;  // threshold complete after one digit: the selection reads the planes once
-  const int kind = K.kind[blockIdx.y];
+  const int kind = K.kind[blockIdx.y], plane = K.plane[blockIdx.y];
   const unsigned long long prefix = st->prefix;
   const PGX_GLOBAL uint64_t* pl = (const PGX_GLOBAL uint64_t*)S.oplane;
   cidx += static_cast<int64_t>(blockIdx.y) * S.ccap;
@@ -194,7 +197,7 @@ __global__ void __launch_bounds__(256) pgx_trim_cand(const TrimSrc S, const Trim
   __syncthreads();
   for (int64_t b = lo; b < hi; b += 256) {
     const int64_t i = b + tid;
-    const uint64_t key = i < hi ? trim_key(pl, S.ocap, i, kind) : 0ull;
+    const uint64_t key = i < hi ? trim_key(pl, S.ocap, i, kind, plane) : 0ull;
     const bool in = i < hi && key >= prefix;
     const unsigned long long m = __ballot(in);
     if (m) {
@@ -281,7 +284,7 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const TrimSrc S, const Tr
   __shared__ unsigned int tcnt;
   __shared__ long long ttake, tsel;
   TrimState* st = sts + blockIdx.y;
-  const int kind = K.kind[blockIdx.y];
+  const int kind = K.kind[blockIdx.y], plane = K.plane[blockIdx.y];
   idx += static_cast<int64_t>(blockIdx.y) * cap;
   keys += static_cast<int64_t>(blockIdx.y) * cap;
   const unsigned long long thr = st->prefix;
@@ -309,7 +312,7 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const TrimSrc S, const Tr
   for (int64_t b = lo + (threadIdx.x & ~63); b < hi; b += 256) {
     const int64_t i = b + lane;
     const bool valid = i < hi;
-    const uint64_t key = valid ? (cand ? ck[i] : trim_key(pl, S.ocap, i, kind)) : 0ull;
+    const uint64_t key = valid ? (cand ? ck[i] : trim_key(pl, S.ocap, i, kind, plane)) : 0ull;
     const bool eq = valid && key == thr;
     const unsigned long long em = __ballot(eq);
     bool take = valid && key > thr;
@@ -356,17 +359,16 @@ __global__ void __launch_bounds__(256) pgx_trim_select(const TrimSrc S, const Tr
   }
 }
 
-// Gather selected groups: out[0, m) packed keys, then planes 0..3 (m words each).
+// Gather selected groups: out[0, m) packed keys, then planes 0 .. nplanes-1 (m words each).
 __global__ void __launch_bounds__(256) pgx_group_gather(const uint64_t* __restrict__ okey,
                                                         const uint64_t* __restrict__ oplane, int64_t ocap,
-                                                        const int64_t* __restrict__ idx, int64_t m,
+                                                        int nplanes, const int64_t* __restrict__ idx, int64_t m,
                                                         uint64_t* __restrict__ out) {
   const int64_t j = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
   if (j >= m) return;
   const int64_t i = idx[j];
   out[j] = okey[i];
-#pragma unroll
-  for (int p = 0; p < 4; ++p) out[(p + 1) * m + j] = oplane[p * ocap + i];
+  for (int p = 0; p < nplanes; ++p) out[(p + 1) * m + j] = oplane[p * ocap + i];
 }
 
 }  // namespace pgx
@@ -374,7 +376,8 @@ __global__ void __launch_bounds__(256) pgx_group_gather(const uint64_t* __restri
 // Host launchers (pgx_part.cpp device_trim).  The nf state blocks are prepared by the caller: k = groups wanted, kmin = ~0,
 // everything else zero.  kinds[f]: TrimKind of function slot f.  At most 8 histogram passes (8-bit digits); passes after
 // a function's threshold is complete return at once.
-extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds, int nf,
+extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds,
+                                      const int* planes, int nf,
                                       void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
                                       const unsigned long long* prange, int64_t* cidx, uint64_t* ckey, int64_t ccap,
                                       hipStream_t stream) {
@@ -384,6 +387,7 @@ extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int6
   bool seeded = prange != nullptr;
   for (int f = 0; f < nf; ++f) {
     K.kind[f] = kinds[f];
+    K.plane[f] = planes[f];
     seeded = seeded && kinds[f] != pgx::TK_AVG;  // AVG keys are ratios: their range needs the pass
   }
   pgx::TrimState* st = static_cast<pgx::TrimState*>(states);
@@ -400,11 +404,12 @@ extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int6
   return hipGetLastError();
 }
 
-extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap,
+extern "C" hipError_t pgx_launch_group_gather(const uint64_t* okey, const uint64_t* oplane, int64_t ocap, int nplanes,
                                               const int64_t* idx, int64_t m, uint64_t* out, hipStream_t stream) {
   if (m <= 0) return hipSuccess;
+  if (nplanes < 1 || nplanes > 1 + 3 * 8) return hipErrorInvalidValue;
   hipLaunchKernelGGL(pgx::pgx_group_gather, dim3(static_cast<unsigned>((m + 255) / 256)), dim3(256), 0, stream, okey,
-                     oplane, ocap, idx, m, out);
+                     oplane, ocap, nplanes, idx, m, out);
   return hipGetLastError();
 }
 

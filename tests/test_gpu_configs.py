@@ -70,7 +70,7 @@ def _c3_gpu_groups(ctx, data, seg_idx, flags=0):
     return key[o], vals[:, o], cnts[0, o]
 
 
-def _c3_twin(wl, s):
+def _c3_twin(wl, s, metric="m"):
     dicts = {c.name: synth.make_dictionary(c.dict_kind, c.card, s).astype(np.float64) for c in wl.columns}
     cols = {}
     for ci, c in enumerate(wl.columns):
@@ -80,7 +80,7 @@ def _c3_twin(wl, s):
         else:
             fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), wl.rows, c.bits, c.card)
         cols[c.name] = (fwd, c.bits, dicts[c.name], c.card)
-    r = c_oracle.run([c_oracle.Segment(wl.rows, cols)], metric="m", group_cols=("g1", "g2"), collect_groups=True)[0]
+    r = c_oracle.run([c_oracle.Segment(wl.rows, cols)], metric=metric, group_cols=("g1", "g2"), collect_groups=True)[0]
     keys, sums, counts, mins, maxs = r["groups"]
     o = np.argsort(keys)
     return keys[o], sums[o], counts[o], mins[o], maxs[o]
@@ -119,6 +119,36 @@ def test_c3_hash_fallback_over_a_million_groups(ctx, c3):
     assert np.array_equal(keys, tk) and np.array_equal(cnt, tc)
     assert np.array_equal(vals[0], ts) and np.array_equal(vals[1], tmin) and np.array_equal(vals[2], tmax)
     assert took < 60, took
+
+
+def test_c3m2_two_value_columns_vs_c_twin(ctx):
+    """c3m2: C3's keys with SUM(m), SUM(m2), MAX(m) -- two value columns.  The partitioned pipeline runs once per column
+    and the second pass's planes are joined into the first pass's groups by key on the device (pgx_part.cpp
+    run_value_columns); one full 125M-row segment, every group == the C twin's (run once per metric column)."""
+    import ctypes as C
+    import json
+
+    from pinot_amd import native as N
+    L = N.lib()
+    wl = synth.WORKLOADS["c3m2"]
+    data = synth.DeviceSegments(ctx, wl, [0])
+    try:
+        N.check(L.pgx_timing_start(ctx.handle))
+        keys, vals, cnt = _c3_gpu_groups(ctx, data, [0])
+        out = (C.c_double * 3)()
+        js = C.create_string_buffer(8192)
+        N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
+        kernels = json.loads(js.value.decode())["kernels"]
+        assert "pgx_join" in kernels and "pgx_scan_kernel" not in kernels, kernels
+    finally:
+        data.free()
+    tk, ts, tc, tmin, tmax = _c3_twin(wl, 0, "m")
+    tk2, ts2, tc2, _, _ = _c3_twin(wl, 0, "m2")
+    assert len(keys) == len(tk) > 10_000_000 and np.array_equal(tk, tk2)
+    assert np.array_equal(keys, tk) and np.array_equal(cnt, tc)
+    assert np.array_equal(vals[0], ts)    # SUM(m)
+    assert np.array_equal(vals[1], ts2)   # SUM(m2)
+    assert np.array_equal(vals[2], tmax)  # MAX(m)
 
 
 def test_c3d_per_segment_dictionaries_vs_c_twin(ctx):

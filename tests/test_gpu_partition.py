@@ -124,7 +124,8 @@ def _pairs_segment(ctx, n, card, seed):
     rng = np.random.default_rng(seed)
     raw = {"ga": rng.integers(0, card, size=n).astype(np.int32),
            "gb": rng.integers(0, card, size=n).astype(np.int32) * 3,
-           "m": rng.integers(-5000, 5000, size=n).astype(np.int32)}
+           "m": rng.integers(-5000, 5000, size=n).astype(np.int32),
+           "m2": (rng.integers(0, 3000, size=n) * 7 - 9000).astype(np.int32)}
     raw["ga"][:card] = np.arange(card)
     raw["gb"][:card] = np.arange(card) * 3
     raw["m"][:2] = [-5000, 4999]
@@ -402,3 +403,72 @@ def test_partitioned_plan_cache_replays(ctx, seg, mode, monkeypatch, capfd):
         assert blk.stats.as_list() == list(o["stats"])
         N.lib().pgx_result_release(r)
     qq.close()
+
+
+MULTI_AGGS = "SELECT COUNT(*), SUM(m), MIN(m), MAX(b), SUM(c), AVG(b), MIN(s) FROM t"
+
+
+def _kernels_of(ctx, fn):
+    """Run fn() inside a kernel-timing window; returns (fn's value, kernel names that ran)."""
+    import ctypes as C
+    import json
+
+    from pinot_amd import native as N
+    L = N.lib()
+    N.check(L.pgx_timing_start(ctx.handle))
+    v = fn()
+    out = (C.c_double * 3)()
+    js = C.create_string_buffer(16384)
+    N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
+    return v, set(json.loads(js.value.decode())["kernels"])
+
+
+@pytest.mark.parametrize("mode", ["narrow", "radix"])
+@pytest.mark.parametrize("group", [" GROUP BY g2, a, c", " GROUP BY a, c, g1"])
+def test_partitioned_several_value_columns(ctx, seg, group, mode, monkeypatch):
+    """Functions over four value columns (m, b, c, s) with sparse keys: one partitioned pipeline run per column, the
+    later passes' planes joined into the first pass's groups by key on the device (pgx_part.cpp run_value_columns,
+    pgx_merge.hip pgx_join_*), not the global hash table.  Every group and function == the oracle's; statistics too."""
+    monkeypatch.setenv("PGX_PART_NARROW", "1" if mode == "narrow" else "0")
+    gseg, oseg, fmt = seg
+    q = pql.compile(MULTI_AGGS + " WHERE a > 40" + group)
+    (blk, st), kernels = _kernels_of(ctx, lambda: _run_inner(ctx, gseg, q))
+    assert "pgx_join" in kernels, kernels
+    assert ("pgx_narrow_aggregate" if mode == "narrow" else "pgx_part_aggregate") in kernels, kernels
+    o = H.oracle_answer([oseg], q, literal=True)
+    assert st.as_list() == list(o["stats"])
+    m = _map(blk)
+    assert set(m) == set(o["map"])
+    fns = [a["fn"] for a in q["aggregations"]]
+    for k, v in o["map"].items():
+        H.assert_values_equal(m[k], v, fns)
+
+
+def test_several_value_columns_trim_on_device(ctx):
+    """Combine trim over > 20,000 groups of a two-column result (planes: count, then sum / min / max per column): the
+    5,000 best groups of every function, each carrying its own untrimmed value (the trim's key reads the function's
+    own plane)."""
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    gseg, raw = _pairs_segment(ctx, 300000, 3000, seed=78)  # 9M-slot key space: sparse (partitioned) keys
+    raw2 = dict(raw)
+    exp_m = _expected(raw)
+    raw2["m"] = raw["m2"]
+    exp_m2 = _expected(raw2)
+    assert len(exp_m) > 20000
+    q = pql.compile("SELECT SUM(m), MAX(m2), MIN(m2), MIN(m), COUNT(*) FROM t GROUP BY ga, gb")
+    qq = E._Query(ctx, q)
+    r, kernels = _kernels_of(ctx, lambda: qq.execute([gseg]))
+    assert "pgx_join" in kernels, kernels
+    try:
+        maps = E.trimmed_maps(qq, r, [gseg])
+    finally:
+        N.lib().pgx_result_release(r)
+    for i, (fn, exp, col) in enumerate([("sum", exp_m, 1), ("max", exp_m2, 3), ("min", exp_m2, 2), ("min", exp_m, 2),
+                                        ("count", exp_m, 0)]):
+        m = maps[i]
+        assert len(m) == 5000
+        got = sorted(m.values(), reverse=(fn != "min"))
+        assert got == _trim_expect(exp, fn), (i, fn)
+        for k, v in m.items():
+            assert v == exp[k][col], (i, fn, k, v, exp[k])
