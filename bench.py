@@ -23,6 +23,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICRO
 METRIC = "rows/sec for filter+group-by SUM at 1/2/4/8 GPUs; % of HBM roofline"
 # bounded CPU-baseline samples (segments, rows per segment): ~10-30 s of single-core work over 8 threads in total
 CPU_SAMPLE = {"c2": (8, 32_000_000), "c5": (64, 2_000_000), "c3": (8, 16_000_000), "c3d": (8, 16_000_000),
+              "c3f": (8, 16_000_000),
               "c6": (8, 8_000_000)}
 
 
@@ -101,8 +102,8 @@ def cpu_baseline(wl, query, seg_rows, nseg, threads):
                                          pair_seed=synth.column_seed(wl.seed, s, 99), npairs=wl.npairs)
             else:
                 fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), seg_rows, c.bits, c.card)
-            dv = (synth.make_dictionary(c.dict_kind, c.card, s).astype(np.float64) if c.dict_kind == "metric_seg"
-                  else dicts[c.name])
+            dv = (synth.make_dictionary(c.dict_kind, c.card, s).astype(np.float64)
+                  if c.dict_kind in ("metric_seg", "metric_f64_seg") else dicts[c.name])
             cols[c.name] = (fwd, c.bits, dv, c.card)
             if c.inverted:  # the .bitmap.inv the GPU segments carry (synth.DeviceSegments._inverted_indexes)
                 invs[s][c.name] = c_oracle.inverted_build(
@@ -115,7 +116,7 @@ def cpu_baseline(wl, query, seg_rows, nseg, threads):
     kw = {"threads": threads, "metric": "m"}
     if wl.name == "c2":
         kw.update(filter_col="dA", lo=64, hi=191)
-    elif wl.name in ("c3", "c3d"):
+    elif wl.name in ("c3", "c3d", "c3f"):
         kw.update(group_cols=("g1", "g2"))
     elif wl.name == "c5":  # (f1 IN (...) OR f2 = 7) AND f3 <> 3 GROUP BY gk: leaves as dictId bitsets
         f1 = [int(v) for v in query["filter"]["children"][0]["children"][0]["values"]]

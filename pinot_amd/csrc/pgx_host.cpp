@@ -688,7 +688,9 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         js.img_words[c] = J.cols[c].img != IMG_NONE ? col.img_words : 0;
         js.vbase[c] = col.vbase;
       }
-      js.emit_rebase = (P.use_part && P.part_vcol >= 0) ? P.segcols[s][P.part_vcol]->vbase - P.part_vbase : 0;
+      js.emit_rebase = !(P.use_part && P.part_vcol >= 0) ? 0
+                       : P.part_fp ? P.part_fbase[size_t(s)]  // the segment's dictionary in the concatenation
+                                   : P.segcols[s][P.part_vcol]->vbase - P.part_vbase;
       if (P.rprog_on)
         for (size_t k = 0; k < P.dm_progs.size(); ++k)
           js.lbits[nleaves + k] = P.rchunk ? reinterpret_cast<const uint32_t*>(P.rprog_dev + s * P.dm_progs.size() + k)
@@ -1712,6 +1714,8 @@ pgx_status pgx_result_device_groups(const pgx_result* r, int64_t* n, void* recor
     r->ready();
     if (!r->group_by || !r->lazy) fail(PGX_ERR_UNSUPPORTED, "the groups of this result are not in device memory");
     if (r->lazy->nplanes != 4) fail(PGX_ERR_UNSUPPORTED, "group records hold one value column");
+    for (bool f : r->lazy->agg_fp)
+      if (f) fail(PGX_ERR_UNSUPPORTED, "group records hold integer sums");
     *n = r->num_groups;
     if (!records || !r->num_groups) return;
     const auto& L = *r->lazy;

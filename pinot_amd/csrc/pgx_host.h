@@ -68,6 +68,11 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
                                                 uint64_t* okey, uint64_t* oplane, int64_t ocap,
                                                 unsigned long long* ocount, unsigned long long* overflow,
                                                 hipStream_t stream);
+extern "C" hipError_t pgx_launch_part_aggregate_f64(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
+                                                    int nparts, int64_t cap, uint64_t keymask, int keybits,
+                                                    const double* fdict, int need_min, int need_max, uint64_t* okey,
+                                                    uint64_t* oplane, int64_t ocap, unsigned long long* ocount,
+                                                    unsigned long long* overflow, hipStream_t stream);
 extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int64_t n, const int* kinds,
                                       const int* planes, int nf,
                                       void* states, int64_t* idx, uint64_t* keys, int64_t cap, int grid,
@@ -688,6 +693,7 @@ struct pgx_result {
     DevBuf okey, oplane;         // packed keys; planes x ocap: count, then sum, min, max per value column
     int nplanes = 4;             // 1 + 3 x value columns
     std::vector<int> agg_plane;  // per function: the plane its value is decoded from (COUNT: 0)
+    std::vector<bool> agg_fp;    // per function: a FLOAT / DOUBLE column (f64 sum, ordered-f64 min / max)
     DevBuf prange;               // trim-key ranges per kind (pgx_narrow_aggregate), or none: the trim's range pass
     int64_t ocap = 0;
     std::vector<int> gshift, gbits;
@@ -845,6 +851,12 @@ struct ExecPlan {
   int narrow_img_words = 0, narrow_img_sh = 0;
   uint64_t narrow_vrange = 0;     // largest value offset (value - vbase)
   unsigned short* part_hi = nullptr;
+  // FLOAT / DOUBLE value column: records carry an index into the concatenation of the segments' dictionaries
+  // (part_fdict; segment s's dictionary starts at part_fbase[s]), summed in f64 by pgx_part_aggregate_f64
+  bool part_fp = false;
+  const double* part_fdict = nullptr;
+  std::vector<int64_t> part_fbase;
+  std::vector<DevBuf> part_fdict_bufs;  // owns the concatenated dictionaries (one per FLOAT / DOUBLE value column)
   // One value column's partitioned-path settings (the fields above from part_vcol to narrow_vrange).  A query whose
   // functions read several value columns runs the pipeline once per column (pgx_part.cpp run_value_columns) and joins
   // the passes' groups by key; part_cols[0] is loaded into the fields above at planning.
@@ -856,6 +868,9 @@ struct ExecPlan {
     int vd = 0, k2min = 0, img = 0, img_words = 0, img_sh = 0;
     const uint32_t* imgp = nullptr;
     uint64_t vrange = 0;
+    bool fp = false;
+    const double* fdict = nullptr;
+    std::vector<int64_t> fbase;
   };
   std::vector<PartCol> part_cols;
   PartCol save_part_col() const {
@@ -864,6 +879,7 @@ struct ExecPlan {
     c.sum = part_sum, c.mn = part_min, c.mx = part_max, c.dictid = part_dictid, c.slab = part_slab, c.narrow = part_narrow;
     c.vdict = part_vdict, c.vd = narrow_vd, c.k2min = narrow_k2min, c.img = narrow_img, c.img_words = narrow_img_words;
     c.img_sh = narrow_img_sh, c.imgp = narrow_imgp, c.vrange = narrow_vrange;
+    c.fp = part_fp, c.fdict = part_fdict, c.fbase = part_fbase;
     return c;
   }
   void load_part_col(const PartCol& c) {
@@ -871,6 +887,7 @@ struct ExecPlan {
     part_sum = c.sum, part_min = c.mn, part_max = c.mx, part_dictid = c.dictid, part_slab = c.slab, part_narrow = c.narrow;
     part_vdict = c.vdict, narrow_vd = c.vd, narrow_k2min = c.k2min, narrow_img = c.img, narrow_img_words = c.img_words;
     narrow_img_sh = c.img_sh, narrow_imgp = c.imgp, narrow_vrange = c.vrange;
+    part_fp = c.fp, part_fdict = c.fdict, part_fbase = c.fbase;
   }
   std::vector<int64_t> rec_base; // per segment: index of its row 0 in the record array
   int64_t rec_total = 0;

@@ -897,7 +897,9 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         std::string x = "0u";
         if (s.emit_col >= 0) {
           const std::string ec = std::to_string(s.emit_col);
-          if (s.emit_dictid) x = "v" + ec + "[j]";  // the value's dictId (sorted dictionary): looked up at aggregation
+          // the value's dictId, looked up at aggregation (narrow: the sorted dictionary, rebase 0; FLOAT / DOUBLE: the
+          // segment's place in the concatenated dictionaries)
+          if (s.emit_dictid) x = "(u32)(v" + ec + "[j] + (u32)S->emit_rebase)";
           else x = s.cols[s.emit_col].img != IMG_NONE
                        ? "(u32)(" + img_value(s, s.emit_col, img_off, "v" + ec + "[j]") + " + (u32)S->emit_rebase)"
                        : "(u32)(di" + ec + "[v" + ec + "[j]] - S->vbase[" + ec + "] + S->emit_rebase)";

@@ -1901,6 +1901,104 @@ __global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate(const uint64_t
 }
 
 
+// FLOAT / DOUBLE value column (SumAggregationFunction / Min / Max over a double dictionary): the record's value field
+// is an index into the query's concatenation of the segments' dictionaries (fdict, each segment's records rebased to
+// its dictionary's place by the scan), looked up here -- the dictionaries are small and L2-resident.  Per slot: count,
+// f64 sum (LDS f64 add), ordered-u64 min / max of the value (64-bit LDS min / max).  Planes as pgx_part_aggregate's
+// with the sum as f64 bits and the ordered encodings of doubles.
+template <bool MN, bool MX>
+__global__ void __launch_bounds__(kAggThreads) pgx_part_aggregate_f64(const uint64_t* __restrict__ in,
+                                                                      const unsigned long long* __restrict__ in_cnt,
+                                                                      int cstride, int64_t cap, uint64_t keymask,
+                                                                      int keybits, const double* __restrict__ fdict,
+                                                                      uint64_t* __restrict__ okey,
+                                                                      uint64_t* __restrict__ oplane, int64_t ocap,
+                                                                      unsigned long long* __restrict__ ocount,
+                                                                      unsigned long long* __restrict__ overflow) {
+  __shared__ __attribute__((aligned(16))) uint64_t tkey[kAggSlots];
+  __shared__ double tsum[kAggSlots];
+  __shared__ unsigned int tcnt[kAggSlots];
+  __shared__ unsigned long long tmin[MN ? kAggSlots : 1], tmax[MX ? kAggSlots : 1];
+  __shared__ int nfound;
+  __shared__ unsigned long long obase;
+  const int tid = threadIdx.x;
+  const int part = blockIdx.x;
+  for (int i = tid; i < kAggSlots; i += kAggThreads) {
+    tkey[i] = kNoRecord;
+    tsum[i] = 0.0;
+    tcnt[i] = 0u;
+    if (MN) tmin[i] = ~0ull;
+    if (MX) tmax[i] = 0ull;
+  }
+  if (tid == 0) nfound = 0;
+  __syncthreads();
+  const int64_t n = min(static_cast<int64_t>(in_cnt[static_cast<int64_t>(part) * cstride]), cap);
+  const PGX_GLOBAL uint64_t* src = (const PGX_GLOBAL uint64_t*)(in) + static_cast<int64_t>(part) * cap;
+  const PGX_GLOBAL double* fd = (const PGX_GLOBAL double*)fdict;
+  bool lost = false;
+  for (int64_t base = 0; base < n; base += kAggThreads * kAggPer) {
+    uint64_t rec[kAggPer];
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) {
+      const int64_t i = base + k * kAggThreads + tid;
+      rec[k] = i < n ? __builtin_nontemporal_load(src + i) : kNoRecord;
+    }
+    double val[kAggPer];
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) val[k] = rec[k] != kNoRecord ? fd[rec[k] >> keybits] : 0.0;
+#pragma unroll
+    for (int k = 0; k < kAggPer; ++k) {
+      if (rec[k] == kNoRecord) continue;
+      const uint64_t key = rec[k] & keymask;
+      unsigned int bk = static_cast<unsigned int>(part_mix(key)) & (kAggBuckets - 1);
+      int slot = -1;
+      for (int t = 0; t < kAggBuckets;) {
+        const ulonglong2* bp = reinterpret_cast<const ulonglong2*>(&tkey[bk * kAggWays]);
+        const ulonglong2 a = bp[0], c = bp[1];
+        const int m = a.x == key ? 0 : a.y == key ? 1 : c.x == key ? 2 : c.y == key ? 3 : -1;
+        if (m >= 0) { slot = static_cast<int>(bk) * kAggWays + m; break; }
+        const int e = a.x == kNoRecord ? 0 : a.y == kNoRecord ? 1 : c.x == kNoRecord ? 2 : c.y == kNoRecord ? 3 : -1;
+        if (e >= 0) {
+          const int cand = static_cast<int>(bk) * kAggWays + e;
+          const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&tkey[cand]), kNoRecord, key);
+          if (prev == kNoRecord || prev == key) { slot = cand; break; }
+          continue;
+        }
+        bk = (bk + 1) & (kAggBuckets - 1);
+        ++t;
+      }
+      if (slot < 0) { lost = true; continue; }
+      atomicAdd(&tcnt[slot], 1u);
+      atomicAdd(&tsum[slot], val[k]);
+      if (MN || MX) {
+        const uint64_t b = static_cast<uint64_t>(__double_as_longlong(val[k]));
+        const unsigned long long o = (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+        if (MN) atomicMin(&tmin[slot], o);
+        if (MX) atomicMax(&tmax[slot], o);
+      }
+    }
+  }
+  if (lost) atomicAdd(overflow, 1ull);
+  __syncthreads();
+  int mine = 0;
+  for (int i = tid; i < kAggSlots; i += kAggThreads) mine += tkey[i] != kNoRecord;
+  const int before = atomicAdd(&nfound, mine);
+  __syncthreads();
+  if (tid == 0) obase = atomicAdd(ocount, static_cast<unsigned long long>(nfound));
+  __syncthreads();
+  unsigned long long o = obase + static_cast<unsigned long long>(before);
+  for (int i = tid; i < kAggSlots; i += kAggThreads) {
+    if (tkey[i] == kNoRecord) continue;
+    if (o >= static_cast<unsigned long long>(ocap)) { atomicAdd(overflow, 1ull); continue; }
+    okey[o] = tkey[i];
+    oplane[o] = tcnt[i];
+    oplane[ocap + o] = static_cast<unsigned long long>(__double_as_longlong(tsum[i]));
+    oplane[2 * ocap + o] = MN ? tmin[i] : ~0ull;
+    oplane[3 * ocap + o] = MX ? tmax[i] : 0ull;
+    ++o;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // Synthetic forward-index generator (benchmarks): dictId(row) = splitmix64(seed ^ row*golden) % card, packed
 // MSB-first big-endian.  One thread writes one 32-bit big-endian word = the 32 rows' bits that fall in it.
@@ -2177,6 +2275,29 @@ extern "C" hipError_t pgx_launch_part_aggregate(const uint64_t* in, const unsign
     PGX_AGG_CASE(7, true, true, true)
   }
 #undef PGX_AGG_CASE
+  return hipGetLastError();
+}
+
+extern "C" hipError_t pgx_launch_part_aggregate_f64(const uint64_t* in, const unsigned long long* in_cnt, int cstride,
+                                                    int nparts, int64_t cap, uint64_t keymask, int keybits,
+                                                    const double* fdict, int need_min, int need_max, uint64_t* okey,
+                                                    uint64_t* oplane, int64_t ocap, unsigned long long* ocount,
+                                                    unsigned long long* overflow, hipStream_t stream) {
+  if (nparts <= 0) return hipSuccess;
+  if (!fdict || keybits < 1 || keybits > 63) return hipErrorInvalidValue;
+  const int sel = (need_min ? 2 : 0) | (need_max ? 1 : 0);
+#define PGX_AGGF_CASE(K, B, C)                                                                                      \
+  case K:                                                                                                            \
+    hipLaunchKernelGGL((pgx::pgx_part_aggregate_f64<B, C>), dim3(nparts), dim3(pgx::kAggThreads), 0, stream, in,    \
+                       in_cnt, cstride, cap, keymask, keybits, fdict, okey, oplane, ocap, ocount, overflow);         \
+    break;
+  switch (sel) {
+    PGX_AGGF_CASE(0, false, false)
+    PGX_AGGF_CASE(1, false, true)
+    PGX_AGGF_CASE(2, true, false)
+    PGX_AGGF_CASE(3, true, true)
+  }
+#undef PGX_AGGF_CASE
   return hipGetLastError();
 }
 

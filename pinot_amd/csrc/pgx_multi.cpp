@@ -47,6 +47,7 @@ void merge_device_groups(pgx_ctx* ctx, hipStream_t st, const uint64_t* keys, con
   L->rep_id = like.rep_id;
   L->agg_kind = like.agg_kind;
   L->agg_plane = like.agg_plane;  // (merged results hold the 4-plane layout: count, sum, min, max)
+  L->agg_fp = like.agg_fp;
   L->nplanes = 4;
   ctx->refs.fetch_add(1);
   L->ctx = ctx;
@@ -236,7 +237,11 @@ void run_multi(pgx_ctx* const* ctxs, int nctx, const pgx_query& q, pgx_segment* 
     finish_result(c0, q, P, B, sub[0].data(), int(sub[0].size()), st, R, host.data());
   } else {
     bool all_lazy = true;
-    for (auto& r : res) all_lazy = all_lazy && r->lazy && r->lazy->nplanes == 4;
+    for (auto& r : res) {
+      all_lazy = all_lazy && r->lazy && r->lazy->nplanes == 4;
+      if (all_lazy)
+        for (bool f : r->lazy->agg_fp) all_lazy = all_lazy && !f;  // (the device merge adds integer sums)
+    }
     *R = pgx_result();
     R->num_aggs = na;
     R->agg_fn = q.agg_fn;

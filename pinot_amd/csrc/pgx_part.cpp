@@ -105,11 +105,18 @@ void part_enqueue(const ExecPlan& P, PartBuffers& PB, hipStream_t st) {
   // count and sum share one LDS add when a partition's count and value sum both fit their bit fields
   const int cbits = bits_for(acap + 1);
   const int pack_shift = (2 * cbits + P.part_vbits <= 64) ? 64 - cbits : 0;
-  PGX_LAUNCH(st, "pgx_part_aggregate", pgx_launch_part_aggregate(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits, P.part_vbase,
-                                      P.part_sum, P.part_min, P.part_max,
-                                      pack_shift, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(), PB.ocap, tail,
-                                      tail + 3, st),
-            "partition aggregate");
+  if (P.part_fp)
+    PGX_LAUNCH(st, "pgx_part_aggregate_f64",
+               pgx_launch_part_aggregate_f64(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits,
+                                             P.part_fdict, P.part_min, P.part_max, PB.okey.as<uint64_t>(),
+                                             PB.oplane.as<uint64_t>(), PB.ocap, tail, tail + 3, st),
+               "partition aggregate (f64)");
+  else
+    PGX_LAUNCH(st, "pgx_part_aggregate", pgx_launch_part_aggregate(ain, acnt, kCursorStride, aparts, acap, keymask, P.part_keybits, P.part_vbase,
+                                        P.part_sum, P.part_min, P.part_max,
+                                        pack_shift, PB.okey.as<uint64_t>(), PB.oplane.as<uint64_t>(), PB.ocap, tail,
+                                        tail + 3, st),
+              "partition aggregate");
 }
 
 // Scan (records), partition passes and aggregation; grows the buffers to the measured bucket sizes when a pass
@@ -404,6 +411,7 @@ void part_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B, 
     for (size_t i = 0; i < P.part_cols.size(); ++i)
       if (P.part_cols[i].vcol == K.agg_col[a]) c = int(i);
     L->agg_plane.push_back(k == A_COUNT ? 0 : 1 + 3 * c + (k == A_MIN ? 1 : (k == A_MAX ? 2 : 0)));
+    L->agg_fp.push_back(k != A_COUNT && K.agg_fp[a]);
   }
   ctx->refs.fetch_add(1);
   L->ctx = ctx;
@@ -504,10 +512,11 @@ void pgx_result::decode_lazy(const uint64_t* keys, const uint64_t* planes, int64
   for (int a = 0; a < int(L.agg_kind.size()); ++a) {
     const int k = L.agg_kind[a];
     const int p = L.agg_plane[size_t(a)];
-    const int op = k == A_MIN ? P_MIN_ORD : (k == A_MAX ? P_MAX_ORD : P_ADD_I64);
+    const bool fp = !L.agg_fp.empty() && L.agg_fp[size_t(a)];
+    const int op = k == A_MIN ? P_MIN_ORD : (k == A_MAX ? P_MAX_ORD : (fp ? P_ADD_F64 : P_ADD_I64));
     for (int64_t i = 0; i < n; ++i) {
       if (count) count[a * out_stride + i] = int64_t(planes[i]);
-      if (value) value[a * out_stride + i] = decode_plane(op, false, planes[size_t(p) * n + i], k);
+      if (value) value[a * out_stride + i] = decode_plane(op, fp, planes[size_t(p) * n + i], k);
     }
   }
 }
@@ -558,7 +567,8 @@ const std::vector<int64_t>& pgx_result::device_trim(int fn, int64_t size) {
   std::vector<int> kinds(nf), planes(nf);
   for (int f = 0; f < nf; ++f) {
     const int k = L.agg_kind[f];
-    kinds[f] = k == A_COUNT ? 0 : k == A_SUM ? 1 : k == A_MIN ? 2 : k == A_MAX ? 3 : 4;
+    const bool fp = !L.agg_fp.empty() && L.agg_fp[size_t(f)];
+    kinds[f] = k == A_COUNT ? 0 : k == A_SUM ? (fp ? 5 : 1) : k == A_MIN ? 2 : k == A_MAX ? 3 : (fp ? 6 : 4);
     planes[f] = L.agg_plane[size_t(f)];
   }
   const size_t sb = pgx_trim_state_bytes();

@@ -876,7 +876,6 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     bool ok = true;
     for (int a = 0; a < K.num_aggs && ok; ++a) {
       if (K.agg_kind[a] == A_COUNT) continue;
-      if (K.agg_fp[a]) ok = false;
       if (std::find(vcols.begin(), vcols.end(), K.agg_col[a]) == vcols.end()) vcols.push_back(K.agg_col[a]);
     }
     if (int(vcols.size()) > kPartMaxValueCols) ok = false;
@@ -884,13 +883,56 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     for (int g = 0; g < K.num_gcols; ++g) keybits = std::max(keybits, K.gshift[g] + P.gbits[g]);
     // one value column's settings into P (part_vcol ... narrow_vrange); false if the column does not qualify
     auto config = [&](int vc) -> bool {
-      P.part_slab = P.part_dictid = P.part_narrow = false;
+      P.part_slab = P.part_dictid = P.part_narrow = P.part_fp = false;
+      P.part_fdict = nullptr;
+      P.part_fbase.clear();
       bool need_sum = false, need_min = false, need_max = false;
       for (int a = 0; a < K.num_aggs; ++a) {
         if (K.agg_kind[a] == A_COUNT || K.agg_col[a] != vc) continue;
         need_sum |= K.agg_kind[a] == A_SUM || K.agg_kind[a] == A_AVG;
         need_min |= K.agg_kind[a] == A_MIN;
         need_max |= K.agg_kind[a] == A_MAX;
+      }
+      if (vc >= 0) {
+        const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
+        if (c0.data_type == PGX_FLOAT || c0.data_type == PGX_DOUBLE) {
+          // FLOAT / DOUBLE: the records carry the value's index in the concatenation of the segments' dictionaries
+          // (segments holding the same dictionary share one copy), 8-byte radix records, f64 aggregation
+          std::vector<double> all;
+          std::vector<int64_t> fbase(size_t(n), 0);
+          std::unordered_map<uint64_t, int64_t> seen;
+          for (int s = 0; s < n; ++s) {
+            const StagedColumn& c = segs[s]->col(P.qcols[vc]);
+            if (c.data_type != c0.data_type || c.dvals.empty() || int64_t(c.dvals.size()) != int64_t(c.card)) return false;
+            const uint64_t dk = c.dict_hash ^ (uint64_t(c.card) << 40);
+            auto it = seen.find(dk);
+            if (it != seen.end()) {
+              fbase[size_t(s)] = it->second;
+              continue;
+            }
+            fbase[size_t(s)] = int64_t(all.size());
+            seen.emplace(dk, int64_t(all.size()));
+            all.insert(all.end(), c.dvals.begin(), c.dvals.end());
+          }
+          const int vbits = bits_for(int64_t(all.size()));
+          if (keybits + vbits > 63 || all.size() > (size_t(1) << 31)) return false;
+          DevBuf buf(ctx, all.size() * 8);
+          hip_check(hipMemcpy(buf.p, all.data(), all.size() * 8, hipMemcpyHostToDevice), "value dictionaries H2D");
+          P.part_fp = true;
+          P.part_fdict = buf.as<double>();
+          P.part_fbase = std::move(fbase);
+          P.part_fdict_bufs.push_back(std::move(buf));
+          P.part_vcol = vc;
+          P.part_keybits = keybits;
+          P.part_vbits = vbits;
+          P.part_vbase = 0;
+          P.part_sum = need_sum;
+          P.part_min = need_min;
+          P.part_max = need_max;
+          P.part_dictid = true;  // (the index, rebased per segment: JSeg.emit_rebase)
+          P.part_vdict = nullptr;
+          return true;
+        }
       }
       bool cok = true;
       int vbits = 0;
@@ -997,7 +1039,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       P.load_part_col(P.part_cols[0]);
     } else {
       P.part_cols.clear();
-      P.part_slab = P.part_dictid = P.part_narrow = false;
+      P.part_slab = P.part_dictid = P.part_narrow = P.part_fp = false;
     }
   }
 

@@ -19,7 +19,7 @@ namespace pgx {
 
 // Plane layout of a partitioned result (pgx_part_aggregate): oplane[p * ocap + g], p = 0 count, 1 int64 sum,
 // 2 ordered min, 3 ordered max.
-enum TrimKind : int { TK_COUNT = 0, TK_SUM = 1, TK_MIN = 2, TK_MAX = 3, TK_AVG = 4 };
+enum TrimKind : int { TK_COUNT = 0, TK_SUM = 1, TK_MIN = 2, TK_MAX = 3, TK_AVG = 4, TK_SUMF = 5, TK_AVGF = 6 };
 
 // Layout shared with pgx_part.cpp (device_trim writes k, kmin = ~0 and zeros before the launch).  One state per
 // function: every kernel below takes an array of states and the function slot is blockIdx.y.
@@ -72,9 +72,15 @@ __device__ __forceinline__ uint64_t trim_key(const PGX_GLOBAL uint64_t* pl, int6
       return ~v[i];
     case TK_MAX:
       return v[i];
+    case TK_SUMF: {  // f64 sum bits -> ordered
+      const uint64_t b = v[i];
+      return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+    }
     default: {  // AVG: the ratio sum / count as an ordered double (AvgPair compares by value)
       const uint64_t c = pl[i];
-      const double d = c ? static_cast<double>(static_cast<int64_t>(v[i])) / static_cast<double>(c) : 0.0;
+      const double s = kind == TK_AVGF ? __longlong_as_double(static_cast<long long>(v[i]))
+                                       : static_cast<double>(static_cast<int64_t>(v[i]));
+      const double d = c ? s / static_cast<double>(c) : 0.0;
       const uint64_t b = static_cast<uint64_t>(__double_as_longlong(d));
       return (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
     }
@@ -388,7 +394,7 @@ extern "C" hipError_t pgx_launch_trim(const uint64_t* oplane, int64_t ocap, int6
   for (int f = 0; f < nf; ++f) {
     K.kind[f] = kinds[f];
     K.plane[f] = planes[f];
-    seeded = seeded && kinds[f] != pgx::TK_AVG;  // AVG keys are ratios: their range needs the pass
+    seeded = seeded && kinds[f] != pgx::TK_AVG && kinds[f] < pgx::TK_SUMF;  // ratios / f64: their range needs the pass
   }
   pgx::TrimState* st = static_cast<pgx::TrimState*>(states);
   const dim3 g(grid, nf);

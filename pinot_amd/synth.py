@@ -8,6 +8,7 @@ baseline and for full-size spot checks.  Dictionaries are small and built on the
     "ids"    dict[i] = i                                    (dimension columns)
     "metric" dict[i] = 16*i + splitmix64(0xD1C7 ^ i) % 16    (sorted, distinct, in [0, 2^20) for card <= 65536)
     "metric_seg"  the same shape with a per-segment jitter seed: every segment has its own dictionary (c3d)
+    "metric_f64_seg"  metric_seg / 8 as a DOUBLE dictionary (exact in binary; c3f)
 """
 from __future__ import annotations
 
@@ -40,11 +41,12 @@ def make_dictionary(kind: str, card: int, seg: int = 0) -> np.ndarray:
     i = np.arange(card, dtype=np.uint64)
     if kind == "ids":
         return i.astype(np.int64)
-    if kind in ("metric", "metric_seg"):
-        salt = np.uint64(0xD1C7 + (0x10001 * (seg + 1) if kind == "metric_seg" else 0))
+    if kind in ("metric", "metric_seg", "metric_f64_seg"):
+        salt = np.uint64(0xD1C7 + (0x10001 * (seg + 1) if kind != "metric" else 0))
         with np.errstate(over="ignore"):
             jitter = splitmix64_np(salt ^ i) % np.uint64(16)
-        return (i * np.uint64(16) + jitter).astype(np.int64)
+        v = (i * np.uint64(16) + jitter).astype(np.int64)
+        return v / 8.0 if kind == "metric_f64_seg" else v
     raise ValueError(kind)
 
 
@@ -92,6 +94,12 @@ WORKLOADS: Dict[str, Workload] = {
                     "segment: 1B rows (8 x 125M), group by g1 x g2 (2^24 pairs), sum/min/max(m)",
                     8, 125_000_000, [ColSpec("g1", 10000, paired=True), ColSpec("g2", 1_000_000, paired=True),
                                      ColSpec("m", 65536, "metric_seg")],
+                    "SELECT SUM(m), MIN(m), MAX(m) FROM T GROUP BY g1, g2 TOP 10", 3, "weak", npairs=1 << 24),
+    # C3 with a DOUBLE metric, its own dictionary in every segment: f64 aggregation of the concatenated dictionaries
+    "c3f": Workload("c3f", "C3 (BASELINE configs[2] shape) with a DOUBLE metric (a dictionary per segment): 1B rows "
+                    "(8 x 125M), group by g1 x g2 (2^24 pairs), sum/min/max(m)",
+                    8, 125_000_000, [ColSpec("g1", 10000, paired=True), ColSpec("g2", 1_000_000, paired=True),
+                                     ColSpec("m", 65536, "metric_f64_seg")],
                     "SELECT SUM(m), MIN(m), MAX(m) FROM T GROUP BY g1, g2 TOP 10", 3, "weak", npairs=1 << 24),
     # C3 with two metrics (SUM(m), SUM(m2)): two value columns, the generated hash kernels' shape at C3 cardinality
     "c3m2": Workload("c3m2", "C3 keys with two metric columns: 1B rows (8 x 125M), group by g1 x g2 (2^24 pairs), "
@@ -245,13 +253,14 @@ class DeviceSegments:
                     N.check(L.pgx_synth_column(ctx.handle, p, self.rows, c.bits, c.card,
                                                column_seed(wl.seed, s, ci)))
                 fwd_dev[c.name] = (p.value, nbytes)
-                dict_bytes = dicts[c.name].astype(">i4").tobytes()
+                f64 = c.dict_kind == "metric_f64_seg"
+                dict_bytes = dicts[c.name].astype(">f8" if f64 else ">i4").tobytes()
                 inv_bytes = inv.pop((s, ci), None)
                 if inv_bytes is not None:
                     self.inv_offsets[(s, c.name)] = np.frombuffer(inv_bytes, dtype=">u4", count=c.card + 1).astype(
                         np.int64)
-                cols.append(Column(c.name, "INT", "DIMENSION", c.card, c.bits, self.rows, self.rows, False,
-                                   inv_bytes is not None, dict_bytes, 4, None, None, inv_bytes))
+                cols.append(Column(c.name, "DOUBLE" if f64 else "INT", "DIMENSION", c.card, c.bits, self.rows, self.rows,
+                                   False, inv_bytes is not None, dict_bytes, 8 if f64 else 4, None, None, inv_bytes))
             seg = SegmentData("%s_%d" % (wl.name, s), self.rows, self.rows, {c.name: c for c in cols})
             self.segments.append(IndexSegment.from_device(ctx, seg, fwd_dev))
 
@@ -287,9 +296,12 @@ class DeviceSegments:
         a bitmap-index leaf reads (NEQ / NOT_IN read the non-matching ones); plus card*width per dictionary used, ONCE:
         the workload's segments share one dictionary per column, staged once (SharedDict) and read once per query, so
         crediting it per segment would count 1.07 GB at C5 that no kernel reads."""
-        total = sum(c.card * 4 for c in self.wl.columns if c.name in dict_columns and c.dict_kind != "metric_seg")
+        per_seg = ("metric_seg", "metric_f64_seg")
+        width = {"metric_f64_seg": 8}
+        total = sum(c.card * 4 for c in self.wl.columns if c.name in dict_columns and c.dict_kind not in per_seg)
         for s in self.seg_ids:
-            total += sum(c.card * 4 for c in self.wl.columns if c.name in dict_columns and c.dict_kind == "metric_seg")
+            total += sum(c.card * width.get(c.dict_kind, 4) for c in self.wl.columns
+                         if c.name in dict_columns and c.dict_kind in per_seg)
             for c in self.wl.columns:
                 if c.name in used_columns:
                     total += (self.rows * c.bits + 7) // 8

@@ -188,6 +188,43 @@ def test_c3d_per_segment_dictionaries_vs_c_twin(ctx):
     assert np.array_equal(cnt, np.add.reduceat(tc, st))
 
 
+def test_c3f_double_metric_vs_c_twin(ctx):
+    """c3f: C3's keys and query over a DOUBLE metric whose dictionary differs per segment.  The records carry the
+    value's index in the concatenation of the two segments' dictionaries and the aggregation sums in f64
+    (pgx_part_aggregate_f64); two full 125M-row segments, every group of their combine == the C twin's groups of both,
+    merged (values are multiples of 1/8 below 2^17: the sums are exact in any order)."""
+    import ctypes as C
+    import json
+
+    from pinot_amd import native as N
+    L = N.lib()
+    wl = synth.WORKLOADS["c3f"]
+    data = synth.DeviceSegments(ctx, wl, [0, 1])
+    try:
+        N.check(L.pgx_timing_start(ctx.handle))
+        keys, vals, cnt = _c3_gpu_groups(ctx, data, [0, 1])
+        out = (C.c_double * 3)()
+        js = C.create_string_buffer(8192)
+        N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
+        kernels = json.loads(js.value.decode())["kernels"]
+        assert "pgx_part_aggregate_f64" in kernels and "pgx_scan_kernel" not in kernels, kernels
+    finally:
+        data.free()
+    parts = [_c3_twin(wl, s) for s in (0, 1)]
+    k = np.concatenate([p[0] for p in parts])
+    o = np.argsort(k, kind="stable")
+    k = k[o]
+    ts, tc, tmin, tmax = (np.concatenate([p[i] for p in parts])[o] for i in (1, 2, 3, 4))
+    first = np.ones(len(k), dtype=bool)
+    first[1:] = k[1:] != k[:-1]
+    st = np.nonzero(first)[0]
+    assert np.array_equal(keys, k[st])
+    assert np.array_equal(vals[0], np.add.reduceat(ts, st))
+    assert np.array_equal(vals[1], np.minimum.reduceat(tmin, st))
+    assert np.array_equal(vals[2], np.maximum.reduceat(tmax, st))
+    assert np.array_equal(cnt, np.add.reduceat(tc, st))
+
+
 def test_c3_combine_linearity(ctx, c3):
     k01, v01, c01 = _c3_gpu_groups(ctx, c3, [0, 1])
     parts = [_c3_gpu_groups(ctx, c3, [i]) for i in (0, 1)]

@@ -126,10 +126,11 @@ def _pairs_segment(ctx, n, card, seed):
            "gb": rng.integers(0, card, size=n).astype(np.int32) * 3,
            "m": rng.integers(-5000, 5000, size=n).astype(np.int32),
            "m2": (rng.integers(0, 3000, size=n) * 7 - 9000).astype(np.int32)}
+    raw["md"] = raw["m2"] / 4.0 + 0.25  # DOUBLE, exact in binary
     raw["ga"][:card] = np.arange(card)
     raw["gb"][:card] = np.arange(card) * 3
     raw["m"][:2] = [-5000, 4999]
-    s, _ = H.build_pair("pp%d" % seed, raw)
+    s, _ = H.build_pair("pp%d" % seed, raw, types={"md": "DOUBLE"})
     return E.IndexSegment(ctx, s), raw
 
 
@@ -321,7 +322,8 @@ def test_partitioned_per_segment_metric_dictionaries(ctx, metric):
     """VERDICT r4 missing #1: every segment builds its own metric dictionary (SegmentDictionaryCreator builds one per
     segment), so no two segments share a value image.  Integer metrics take a partitioned path with value offsets
     rebased per segment (JSeg.emit_rebase: one query-wide value base), not the global hash table -- the narrow records
-    when the offsets fit them, else the 8-byte radix records; a DOUBLE metric takes the generated hash kernels.  Groups (LONG_MAP key space > 2^22) and every function == the oracle's combine."""
+    when the offsets fit them, else the 8-byte radix records; a DOUBLE metric's records carry its index in the
+    concatenation of the segments' dictionaries, aggregated in f64.  Groups (LONG_MAP key space > 2^22) and every function == the oracle's combine."""
     import ctypes as C
     import json
 
@@ -353,8 +355,8 @@ def test_partitioned_per_segment_metric_dictionaries(ctx, metric):
     js = C.create_string_buffer(8192)
     N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
     kernels = json.loads(js.value.decode())["kernels"]
-    if metric == "double":
-        assert "pgx_part_aggregate" not in kernels and "pgxq" in kernels, kernels
+    if metric == "double":  # the concatenated dictionaries, f64 aggregation (pgx_part_aggregate_f64)
+        assert "pgx_part_aggregate_f64" in kernels, kernels
     elif metric == "int_own_dict":  # value offsets fit the narrow records (no shared image: IMG 3, direct values)
         assert "pgx_narrow_aggregate" in kernels and "pgx_part_aggregate" not in kernels, kernels
     else:  # 32-bit value offsets: too wide for the narrow records, the 8-byte radix path
@@ -472,3 +474,76 @@ def test_several_value_columns_trim_on_device(ctx):
         assert got == _trim_expect(exp, fn), (i, fn)
         for k, v in m.items():
             assert v == exp[k][col], (i, fn, k, v, exp[k])
+
+
+def test_partitioned_double_and_int_value_columns(ctx):
+    """A DOUBLE metric with its own dictionary in every segment beside an INT metric: the DOUBLE column's records
+    carry its index in the concatenated dictionaries (JSeg.emit_rebase = the segment's place), aggregated in f64
+    (pgx_part_aggregate_f64); the INT column runs its own pass and the two join by key.  Every group == the oracle's
+    (f64 sums to 1e-12 relative: the device adds in another order), statistics too."""
+    from pinot_amd import engine as E
+    rng = np.random.default_rng(91)
+    gsegs, osegs = [], []
+    for i in range(3):
+        n = 6000 + 700 * i
+        raw = {"k": (rng.integers(0, 2500, size=n) * 5).astype(np.int32),
+               "x": np.array(["w%d" % v for v in rng.integers(0, 1800, size=n)]),
+               "d": rng.integers(-30000, 30000, size=n) / 16.0 + 0.5 * i,
+               "m": rng.integers(-7000, 7000, size=n).astype(np.int32)}
+        sg, og = H.build_pair("pdm%d" % i, raw, types={"d": "DOUBLE"})
+        gsegs.append(E.IndexSegment(ctx, sg))
+        osegs.append(og)
+    q = pql.compile("SELECT SUM(d), MIN(d), MAX(d), AVG(d), SUM(m), COUNT(*) FROM t WHERE k > 90 GROUP BY x, k")
+    blk, kernels = _kernels_of(ctx, lambda: E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute())
+    assert "pgx_part_aggregate_f64" in kernels and "pgx_join" in kernels, kernels
+    o = H.oracle_answer(osegs, q, literal=True)
+    m = blk.get_aggregation_group_by_result().as_map()
+    assert 10000 < len(o["map"]) < 20000
+    assert set(m) == set(o["map"])
+    fns = [a["fn"] for a in q["aggregations"]]
+    for k, v in o["map"].items():
+        H.assert_values_equal(m[k], v, fns, rel=1e-12)
+    assert blk.stats.as_list() == list(o["stats"])
+
+
+def test_double_value_column_trim_on_device(ctx):
+    """Combine trim over > 20,000 groups of a DOUBLE metric on the partitioned path: SUM / AVG keys read the f64 sum
+    plane (TK_SUMF / TK_AVGF), MIN / MAX the ordered-f64 planes; the 5,000 best of each, every kept group with its own
+    value."""
+    from pinot_amd import engine as E
+    from pinot_amd import native as N
+    gseg, raw = _pairs_segment(ctx, 300000, 3000, seed=79)
+    raw2 = dict(raw)
+    raw2["m"] = raw["md"]
+    key = raw["ga"].astype(np.int64) * (1 << 32) + raw["gb"].astype(np.int64)
+    u, inv = np.unique(key, return_inverse=True)
+    cnt = np.bincount(inv)
+    sm = np.bincount(inv, weights=raw["md"])
+    mx = np.full(len(u), -np.inf)
+    np.maximum.at(mx, inv, raw["md"])
+    exp = {"%d\t%d" % (k >> 32, k & 0xFFFFFFFF): (int(cnt[i]), float(sm[i]), 0.0, float(mx[i]))
+           for i, k in enumerate(u.tolist())}
+    assert len(exp) > 20000
+    q = pql.compile("SELECT SUM(md), MAX(md), AVG(md) FROM t GROUP BY ga, gb")
+    qq = E._Query(ctx, q)
+    r, kernels = _kernels_of(ctx, lambda: qq.execute([gseg]))
+    assert "pgx_part_aggregate_f64" in kernels, kernels
+    try:
+        maps = E.trimmed_maps(qq, r, [gseg])
+    finally:
+        N.lib().pgx_result_release(r)
+    for i, fn in enumerate(["sum", "max", "avg"]):
+        m = maps[i]
+        assert len(m) == 5000
+        if fn == "avg":
+            got = sorted((s_ / c for s_, c in m.values()), reverse=True)
+        else:
+            got = sorted(m.values(), reverse=True)
+        want = _trim_expect(exp, fn)
+        assert np.allclose(got, want, rtol=1e-12, atol=0), fn
+        for k, v in m.items():
+            e = exp[k]
+            if fn == "sum":
+                assert abs(v - e[1]) <= 1e-9 * max(1.0, abs(e[1])), (k, v, e)
+            elif fn == "max":
+                assert v == e[3], (k, v, e)
