@@ -70,17 +70,18 @@ def _c3_gpu_groups(ctx, data, seg_idx, flags=0):
     return key[o], vals[:, o], cnts[0, o]
 
 
-def _c3_twin(wl, s, metric="m"):
+def _c3_twin(wl, s, metric="m", rows=None):
+    rows = rows or wl.rows
     dicts = {c.name: synth.make_dictionary(c.dict_kind, c.card, s).astype(np.float64) for c in wl.columns}
     cols = {}
     for ci, c in enumerate(wl.columns):
         if c.paired:
-            fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, 0, ci), wl.rows, c.bits, c.card,
+            fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, 0, ci), rows, c.bits, c.card,
                                      pair_seed=synth.column_seed(wl.seed, s, 99), npairs=wl.npairs)
         else:
-            fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), wl.rows, c.bits, c.card)
+            fwd = c_oracle.synth_fwd(synth.column_seed(wl.seed, s, ci), rows, c.bits, c.card)
         cols[c.name] = (fwd, c.bits, dicts[c.name], c.card)
-    r = c_oracle.run([c_oracle.Segment(wl.rows, cols)], metric=metric, group_cols=("g1", "g2"), collect_groups=True)[0]
+    r = c_oracle.run([c_oracle.Segment(rows, cols)], metric=metric, group_cols=("g1", "g2"), collect_groups=True)[0]
     keys, sums, counts, mins, maxs = r["groups"]
     o = np.argsort(keys)
     return keys[o], sums[o], counts[o], mins[o], maxs[o]
@@ -124,14 +125,15 @@ def test_c3_hash_fallback_over_a_million_groups(ctx, c3):
 def test_c3m2_two_value_columns_vs_c_twin(ctx):
     """c3m2: C3's keys with SUM(m), SUM(m2), MAX(m) -- two value columns.  The partitioned pipeline runs once per column
     and the second pass's planes are joined into the first pass's groups by key on the device (pgx_part.cpp
-    run_value_columns); one full 125M-row segment, every group == the C twin's (run once per metric column)."""
+    run_value_columns); one 40M-row segment (~15.7M groups), every group == the C twin's (run once per metric column)."""
     import ctypes as C
     import json
 
     from pinot_amd import native as N
     L = N.lib()
     wl = synth.WORKLOADS["c3m2"]
-    data = synth.DeviceSegments(ctx, wl, [0])
+    rows = 40_000_000  # ~15.7M of the 2^24 pairs occur: the C3 group-count regime at a third of the twin's time
+    data = synth.DeviceSegments(ctx, wl, [0], rows=rows)
     try:
         N.check(L.pgx_timing_start(ctx.handle))
         keys, vals, cnt = _c3_gpu_groups(ctx, data, [0])
@@ -142,8 +144,8 @@ def test_c3m2_two_value_columns_vs_c_twin(ctx):
         assert "pgx_join" in kernels and "pgx_scan_kernel" not in kernels, kernels
     finally:
         data.free()
-    tk, ts, tc, tmin, tmax = _c3_twin(wl, 0, "m")
-    tk2, ts2, tc2, _, _ = _c3_twin(wl, 0, "m2")
+    tk, ts, tc, tmin, tmax = _c3_twin(wl, 0, "m", rows)
+    tk2, ts2, tc2, _, _ = _c3_twin(wl, 0, "m2", rows)
     assert len(keys) == len(tk) > 10_000_000 and np.array_equal(tk, tk2)
     assert np.array_equal(keys, tk) and np.array_equal(cnt, tc)
     assert np.array_equal(vals[0], ts)    # SUM(m)
@@ -191,7 +193,7 @@ def test_c3d_per_segment_dictionaries_vs_c_twin(ctx):
 def test_c3f_double_metric_vs_c_twin(ctx):
     """c3f: C3's keys and query over a DOUBLE metric whose dictionary differs per segment.  The records carry the
     value's index in the concatenation of the two segments' dictionaries and the aggregation sums in f64
-    (pgx_part_aggregate_f64); two full 125M-row segments, every group of their combine == the C twin's groups of both,
+    (pgx_part_aggregate_f64); two 40M-row segments, every group of their combine == the C twin's groups of both,
     merged (values are multiples of 1/8 below 2^17: the sums are exact in any order)."""
     import ctypes as C
     import json
@@ -199,7 +201,8 @@ def test_c3f_double_metric_vs_c_twin(ctx):
     from pinot_amd import native as N
     L = N.lib()
     wl = synth.WORKLOADS["c3f"]
-    data = synth.DeviceSegments(ctx, wl, [0, 1])
+    rows = 40_000_000
+    data = synth.DeviceSegments(ctx, wl, [0, 1], rows=rows)
     try:
         N.check(L.pgx_timing_start(ctx.handle))
         keys, vals, cnt = _c3_gpu_groups(ctx, data, [0, 1])
@@ -210,7 +213,7 @@ def test_c3f_double_metric_vs_c_twin(ctx):
         assert "pgx_part_aggregate_f64" in kernels and "pgx_scan_kernel" not in kernels, kernels
     finally:
         data.free()
-    parts = [_c3_twin(wl, s) for s in (0, 1)]
+    parts = [_c3_twin(wl, s, "m", rows) for s in (0, 1)]
     k = np.concatenate([p[0] for p in parts])
     o = np.argsort(k, kind="stable")
     k = k[o]
