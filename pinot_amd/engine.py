@@ -759,6 +759,45 @@ def render_group_maps(q: _Query, segments: Sequence[IndexSegment], key_cols, val
 # ------------------------------------------------------------------------------------------------
 # Operators / plan nodes / plan maker
 # ------------------------------------------------------------------------------------------------
+# Shape limits of ONE library query (pinot_amd/csrc/pgx_internal.h:12-15: kMaxAggs, kMaxQCols).  The reference has
+# none (AggregationFunctionFactory builds any number of functions; FilterPlanNode.java:62-170 any number of columns), so
+# a request past them runs as several library queries over slices of its functions (_GpuOperator._run_slices).
+MAX_AGGS = 8
+MAX_COLS = 16
+_EXT_BASE_SLOTS = {"minmaxrange": 2}  # extended.py _base_request: MIN + MAX; histogram functions add no slot
+
+
+def agg_slices(request: dict, max_aggs: int = MAX_AGGS, max_cols: int = MAX_COLS) -> List[List[int]]:
+    """Consecutive slices of the request's function indices such that each slice, with the request's filter and GROUP
+    BY, fits one library query: at most `max_aggs` aggregation slots (an extended slice's base query holds COUNT(*)
+    plus the slots extended.py's _base_request gives; AVGMV keeps a second plane for its value count, pgx_mv.cpp:158)
+    and at most `max_cols` distinct columns (filter leaves, group columns, aggregated columns).  One slice when the
+    request fits as it is; a single function past the limits on its own stays one slice (the library refuses it)."""
+    from .pql import EXT_FUNCTIONS, EXT_MV_FUNCTIONS
+    aggs = request["aggregations"]
+    _, leaves = _flatten_filter(request.get("filter"))
+    fixed = {lf["column"] for lf in leaves} | set((request.get("group_by") or {}).get("columns", []))
+
+    def slots(idx):
+        fns = [aggs[i]["fn"] for i in idx]
+        if any(f in EXT_FUNCTIONS or f in EXT_MV_FUNCTIONS for f in fns):
+            return 1 + sum(_EXT_BASE_SLOTS.get(f, 0 if (f in EXT_FUNCTIONS or f in EXT_MV_FUNCTIONS) else 1)
+                           for f in fns)
+        return len(fns) + sum(1 for f in fns if f == "avgmv")
+
+    def ncols(idx):
+        return len(fixed | {aggs[i]["column"] for i in idx if aggs[i]["column"] != "*"})
+
+    out, cur = [], []
+    for i in range(len(aggs)):
+        if cur and (slots(cur + [i]) > max_aggs or ncols(cur + [i]) > max_cols):
+            out.append(cur)
+            cur = []
+        cur.append(i)
+    out.append(cur)
+    return out
+
+
 class _GpuOperator:
     """Gpu{Aggregation,AggregationGroupBy}Operator: returns exactly one IntermediateResultsBlock (blockId 0), then None
     (operator/aggregation/groupby/AggregationGroupByOperator.java:81-85)."""
@@ -780,6 +819,12 @@ class _GpuOperator:
     def next_block(self):
         if self._done:
             return None
+        slices = agg_slices(self.request)
+        if len(slices) > 1:
+            blk = self._run_slices(slices)
+            self._stats = blk.stats
+            self._done = True
+            return blk
         from . import extended
         if extended.has_extended(self.request):  # decomposed into GPU sub-queries on the host (extended.py)
             blk = extended.run(self.ctx, self.request, self.segments, combine=self.combine)
@@ -802,6 +847,48 @@ class _GpuOperator:
         return blk
 
     nextBlock = next_block
+
+    def _run_slices(self, slices: List[List[int]], use_star_tree: bool = True) -> IntermediateResultsBlock:
+        """A request past one library query's shape limits (agg_slices): one operator per slice of its functions,
+        same filter and GROUP BY, results concatenated in function order.  Every function's result (and, at the
+        combine, its trimmed map: AggregationGroupByOperatorService.trimToSize runs per function) depends on the
+        filter and the group keys only, so the slices' results are the whole request's."""
+        aggs = self.request["aggregations"]
+        blocks = []
+        for s in slices:
+            sub = dict(self.request, aggregations=[aggs[i] for i in s])
+            if not use_star_tree:
+                sub["debug_options"] = dict(self.request.get("debug_options") or {}, useStarTree="false")
+            blocks.append(type(self)(self.ctx, sub, self.segments, self.combine).next_block())
+        docs = {b.stats.num_docs_scanned for b in blocks}
+        if len(docs) > 1 and use_star_tree:
+            # a slice answered from the star-tree and another from the raw docs: the reference plans the request as a
+            # whole, and the star-tree only serves it when every function qualifies (StarTreeUtils), so all raw
+            return self._run_slices(slices, use_star_tree=False)
+        from .extended import _projection_count
+        st0 = blocks[0].stats
+        stats = ExecutionStatistics(st0.num_docs_scanned, st0.num_entries_scanned_in_filter,
+                                    st0.num_docs_scanned * _projection_count(self.request), st0.num_total_raw_docs)
+        fns = [a["fn"] for a in aggs]
+        if not self.request.get("group_by"):
+            res = [v for b in blocks for v in b.get_aggregation_result()]
+            return IntermediateResultsBlock(aggregation_result=res, stats=stats)
+        out = IntermediateResultsBlock(stats=stats)
+        gbs = [b.get_aggregation_group_by_result() for b in blocks]
+        if all(g is not None for g in gbs):
+            first = gbs[0]
+            keys = [k.string_key for k in first.get_group_key_iterator()]
+            maps = [g.as_map() for g in gbs]
+            if any(len(g) != len(keys) or any(k not in g for k in keys) for g in maps[1:]):
+                raise N.PgxError(N.PGX_ERR_INTERNAL, "aggregation slices found different groups")
+            per_group = [[v for g in maps for v in g[k]] for k in keys]
+            out.aggregation_group_by_result = AggregationGroupByResult(
+                keys, per_group, fns, first.storage_mode, raw_keys=first.raw_keys, key_parts=first.key_parts)
+        elif any(g is not None for g in gbs):
+            raise N.PgxError(N.PGX_ERR_INTERNAL, "aggregation slices found different groups")
+        if self.combine:
+            out.trimmed = [m for b in blocks for m in b.trimmed]
+        return out
 
     def get_execution_statistics(self) -> ExecutionStatistics:
         return self._stats

@@ -29,6 +29,7 @@ PGX_X_THROUGHPUT = 0x8
 PGX_Q_NO_STAR_TREE = 0x1
 ERR_UNSUPPORTED = 2
 PGX_ERR_TIMEOUT = 5
+PGX_ERR_INTERNAL = 6
 
 
 class CtxOpts(C.Structure):

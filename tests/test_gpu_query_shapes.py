@@ -1,0 +1,95 @@
+"""GPU parity of requests past one library query's shape limits (engine.agg_slices / _GpuOperator._run_slices):
+more than kMaxAggs (8) functions, and more than kMaxQCols (16) distinct columns, which the reference plans like any
+other request (AggregationFunctionFactory, FilterPlanNode.java:62-170 have no such limits).  The operator runs one
+library query per slice of the functions and concatenates; results, trimmed maps and ExecutionStatistics are checked
+against the oracle's combine over three segments with different dictionaries."""
+import numpy as np
+import pytest
+
+from pinot_amd import pql
+from tests import helpers as H
+
+pytestmark = pytest.mark.gpu
+
+NCOLS = 18
+
+
+@pytest.fixture(scope="module")
+def env():
+    from pinot_amd import engine as E
+    ctx = E.Context(0)
+    rng = np.random.default_rng(29)
+    gsegs, osegs = [], []
+    for i in range(3):
+        n = 30000 + 7000 * i
+        raw = {"c%d" % c: rng.integers(-(40 + 13 * c), 60 + 17 * c + 5 * i, n).astype(np.int32) for c in range(NCOLS)}
+        raw["c13"] = rng.integers(0, 12 + i, n).astype(np.int32)  # group columns: a few hundred groups
+        raw["c14"] = rng.integers(0, 30, n).astype(np.int32) * 3
+        s, o = H.build_pair("shape%d" % i, raw)
+        gsegs.append(E.IndexSegment(ctx, s))
+        osegs.append(o)
+    yield ctx, gsegs, osegs
+    ctx.close()
+
+
+_FNS = ["sum", "min", "max", "avg", "count", "sum", "min", "max", "sum", "avg", "max", "min"]
+_AGG12 = ", ".join("%s(%s)" % (f.upper(), "*" if f == "count" else "c%d" % c) for c, f in enumerate(_FNS))
+QUERIES = [
+    # 12 functions over 11 columns + 1 filter column: two slices (8 + 4)
+    "SELECT %s FROM t WHERE c11 < 40" % _AGG12,
+    # 12 functions grouped by two columns: two slices, groups joined by key
+    "SELECT %s FROM t WHERE c12 > -20 GROUP BY c13, c14 TOP 10" % _AGG12,
+    # 18 distinct columns (10 filter, 2 group, 6 aggregated) with 6 functions: sliced by columns (4 + 2)
+    "SELECT SUM(c0), MAX(c1), MIN(c2), SUM(c3), AVG(c4), SUM(c5) FROM t WHERE c6 < 90 AND c7 > -80 AND c8 < 150 "
+    "AND c9 > -100 AND c10 < 200 AND c11 < 50 AND (c12 > -30 OR c15 < 20) AND c16 > -200 AND c17 < 300 "
+    "GROUP BY c13, c14 TOP 10",
+    "SELECT SUM(c0), MAX(c1), MIN(c2), SUM(c3), AVG(c4), SUM(c5), MAX(c6), SUM(c7), MIN(c8), SUM(c9), MAX(c10), "
+    "SUM(c16), MIN(c17) FROM t WHERE c11 < 50 AND (c12 > -30 OR c15 < 20)",
+    # no row selected: the defaults of every slice
+    "SELECT %s FROM t WHERE c11 = 123456" % _AGG12,
+]
+
+
+@pytest.mark.parametrize("text", QUERIES)
+def test_sliced_request_matches_oracle(env, text):
+    from pinot_amd import engine as E
+    ctx, gsegs, osegs = env
+    q = pql.compile(text)
+    assert len(E.agg_slices(q)) > 1
+    fns = [a["fn"] for a in q["aggregations"]]
+    blk = E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute()
+    o = H.oracle_answer(osegs, q, literal=False)
+    if q.get("group_by"):
+        m = blk.get_aggregation_group_by_result().as_map()
+        assert set(m) == set(o["map"]) and m
+        for k, v in o["map"].items():
+            H.assert_values_equal(m[k], v, fns)
+        assert len(blk.trimmed) == len(fns)
+        for i, f in enumerate(fns):
+            assert set(blk.trimmed[i]) == set(o["trimmed"][i])
+            for k, v in o["trimmed"][i].items():
+                H.assert_values_equal([blk.trimmed[i][k]], [v], [f])
+    else:
+        H.assert_values_equal(blk.get_aggregation_result(), o["results"], fns)
+    st = blk.stats.as_list()
+    assert st[0] == o["stats"][0] and st[2] == o["stats"][2] and st[3] == o["stats"][3]
+    assert st[1] == H.literal_entries(osegs, q)
+
+
+def test_sliced_inner_segment_plan(env):
+    """The per-segment plan (no combine): the group-by result joined by key, null when no group is selected."""
+    from pinot_amd import engine as E
+    ctx, gsegs, osegs = env
+    q = pql.compile(QUERIES[1])
+    fns = [a["fn"] for a in q["aggregations"]]
+    blk = E.InstancePlanMakerImplV2(ctx).make_inner_segment_plan(gsegs[1], q).run().next_block()
+    o = H.oracle_answer([osegs[1]], q)
+    gr = blk.get_aggregation_group_by_result()
+    m = gr.as_map()
+    assert set(m) == set(o["map"])
+    for k, v in o["map"].items():
+        H.assert_values_equal(m[k], v, fns)
+    assert gr.storage_mode == o["mode"]
+    q0 = pql.compile("SELECT %s FROM t WHERE c11 = 123456 GROUP BY c13" % _AGG12)
+    blk0 = E.InstancePlanMakerImplV2(ctx).make_inner_segment_plan(gsegs[0], q0).run().next_block()
+    assert blk0.get_aggregation_group_by_result() is None
