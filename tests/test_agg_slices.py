@@ -84,3 +84,33 @@ def test_slices_no_group_selected():
     q = pql.compile("SELECT %s FROM t WHERE f > 3 GROUP BY g" % aggs)
     blk = _FakeOp(None, q, [], combine=False).next_block()
     assert blk.get_aggregation_group_by_result() is None
+
+
+class _StarOp(_FakeOp):
+    """Slices whose functions all qualify for the star-tree scan fewer docs unless useStarTree=false."""
+    runs = []
+
+    def next_block(self):
+        if len(E.agg_slices(self.request)) > 1:
+            return E._GpuOperator.next_block(self)
+        star = str((self.request.get("debug_options") or {}).get("useStarTree", "true")) != "false"
+        qualifies = all(a["fn"] == "sum" for a in self.request["aggregations"])
+        docs = 10 if star and qualifies else 100
+        _StarOp.runs.append(docs)
+        return E.IntermediateResultsBlock(aggregation_result=[docs] * len(self.request["aggregations"]),
+                                          stats=E.ExecutionStatistics(docs, 0, 0, 1000))
+
+
+def test_slices_rerun_on_raw_docs_when_star_tree_disagrees():
+    # the first slice qualifies for the star-tree, the second does not: the request runs on the raw docs throughout
+    aggs = ", ".join(["SUM(m)"] * 8 + ["MIN(m)"])
+    q = pql.compile("SELECT %s FROM t" % aggs)
+    _StarOp.runs = []
+    blk = _StarOp(None, q, [], combine=True).next_block()
+    assert _StarOp.runs == [10, 100, 100, 100]
+    assert blk.get_aggregation_result() == [100] * 9 and blk.stats.num_docs_scanned == 100
+    # every slice qualifies: no re-run
+    _StarOp.runs = []
+    q = pql.compile("SELECT %s FROM t" % ", ".join(["SUM(m)"] * 10))
+    blk = _StarOp(None, q, [], combine=True).next_block()
+    assert _StarOp.runs == [10, 10] and blk.stats.num_docs_scanned == 10
