@@ -93,3 +93,39 @@ def test_sliced_inner_segment_plan(env):
     q0 = pql.compile("SELECT %s FROM t WHERE c11 = 123456 GROUP BY c13" % _AGG12)
     blk0 = E.InstancePlanMakerImplV2(ctx).make_inner_segment_plan(gsegs[0], q0).run().next_block()
     assert blk0.get_aggregation_group_by_result() is None
+
+
+def test_sliced_star_tree_request():
+    """Star-tree segment: ten SUMs (every slice served from the star tree: numDocsScanned = the tree's docs), and
+    eight SUMs + MIN (the MIN slice cannot use the tree, so the whole request runs on the raw docs, as the reference
+    plans it: RequestUtils.isFitForStarTreeIndex over all functions)."""
+    from oracle import pinot_oracle as O
+    from pinot_amd import engine as E
+    from pinot_amd import startree as ST
+    from tests.test_startree import METRICS, make_raw, oseg_of
+    ctx = E.Context(0)
+    try:
+        dims, mets = make_raw(40000, seed=5)
+        seg = ST.make_star_tree_segment("stshape", dims, mets, max_leaf_records=500)
+        gseg, os_ = E.IndexSegment(ctx, seg), oseg_of(seg)
+        flt = "where d1 = 2"
+        raw_docs = np.nonzero(O.filter_mask_vectorized(os_, pql.compile("select sum(m1) from T " + flt)["filter"]))[0]
+        exp = O.sum_by_group(os_, raw_docs, METRICS, ["d2"])
+        sums = ", ".join("sum(m%d)" % (1 + i % 2) for i in range(10))
+        q = pql.compile("select %s from T %s group by d2" % (sums, flt))
+        assert len(E.agg_slices(q)) == 2
+        op = E.InstancePlanMakerImplV2(ctx).make_inner_segment_plan(gseg, q).run()
+        m = op.next_block().get_aggregation_group_by_result().as_map()
+        assert {k: v for k, v in m.items()} == {k: [v[i % 2] for i in range(10)] for k, v in exp.items()}
+        st = op.get_execution_statistics().as_list()
+        assert st[0] == len(O.star_tree_docs(os_, seg.star_tree, q, seg.total_raw_docs)) < len(raw_docs)
+        mixed = ", ".join(["sum(m1)"] * 8 + ["min(m2)"])
+        q2 = pql.compile("select %s from T %s group by d2" % (mixed, flt))
+        op2 = E.InstancePlanMakerImplV2(ctx).make_inner_segment_plan(gseg, q2).run()
+        m2 = op2.next_block().get_aggregation_group_by_result().as_map()
+        assert set(m2) == set(exp)
+        for k, v in m2.items():
+            assert v[:8] == [exp[k][0]] * 8
+        assert op2.get_execution_statistics().as_list()[0] == len(raw_docs)
+    finally:
+        ctx.close()
