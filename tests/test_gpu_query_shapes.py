@@ -129,3 +129,31 @@ def test_sliced_star_tree_request():
         assert op2.get_execution_statistics().as_list()[0] == len(raw_docs)
     finally:
         ctx.close()
+
+
+MV_QUERIES = [
+    "SELECT COUNTMV(tags), SUMMV(tags), MINMV(tags), MAXMV(tags), AVGMV(tags), COUNTMV(vals), SUMMV(vals), "
+    "MINMV(vals), MAXMV(vals), AVGMV(vals), SUM(m) FROM t WHERE d > 10",
+    "SELECT SUMMV(vals), COUNTMV(vals), AVGMV(vals), MINMV(vals), MAXMV(vals), AVGMV(tags), SUMMV(tags), COUNT(*), "
+    "MAX(m) FROM t GROUP BY d",
+]
+
+
+@pytest.mark.parametrize("text", MV_QUERIES)
+def test_sliced_multi_value_request(text):
+    """Multi-value functions past the limits (AVGMV keeps a second plane for its value count, pgx_mv.cpp:158), over two
+    segments of test_gpu_mv's shape, combined, against the oracle (statistics with the literal filter algebra)."""
+    from pinot_amd import engine as E
+    from tests.test_gpu_mv import _check, _segment
+    ctx = E.Context(0)
+    try:
+        pairs = [_segment("mvshape%d" % i, 70 + i, 30000 + 11 * i, i == 1) for i in range(2)]
+        gsegs = [E.IndexSegment(ctx, s) for s, _ in pairs]
+        q = pql.compile(text)
+        assert len(E.agg_slices(q)) > 1
+        blk = E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute()
+        o = H.oracle_answer([o for _, o in pairs], q, literal=True)
+        assert blk.stats.as_list() == list(o["stats"])
+        _check(blk, o, q)
+    finally:
+        ctx.close()
