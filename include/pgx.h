@@ -33,7 +33,8 @@
 extern "C" {
 #endif
 
-#define PGX_ABI_VERSION 7  /* 7: pgx_mutable_* (realtime segments in place) */
+#define PGX_ABI_VERSION 8  /* 7: pgx_mutable_* (realtime segments in place); 8: pgx_result_record_words, records of
+                              * every device-resident layout (several value columns, f64 sums) */
 
 typedef enum {
   PGX_OK = 0,
@@ -268,14 +269,19 @@ pgx_status pgx_execute_multi(pgx_ctx* const* ctxs, int32_t nctx, const pgx_query
                              int32_t n, const pgx_leaf_binding* bindings, const pgx_exec_opts* opts, pgx_result** out);
 
 /* Cross-process merge of sparse group-by results (one process per GPU; the caller exchanges the groups, e.g. an RCCL
- * all-to-all by key hash).  A group travels as a record of 5 uint64: packed group key, doc count, int64 sum, ordered
- * min, ordered max (the layout of the partitioned sparse group-by).  pgx_result_device_groups: *n = the number of
- * groups of a result whose groups stay in device memory (PGX_ERR_UNSUPPORTED otherwise) and, when records is
- * non-NULL, the records written to that device buffer (n x 40 bytes, on the result's device).
- * pgx_result_merge_groups: merge n records (equal keys combine) into a device-resident result decoded with `like`'s
- * key tables -- valid when every source planned the same key space (identical dictionaries on all ranks); stats
- * (may be NULL: like's) become the result's ExecutionStatistics. */
+ * all-to-all by key hash).  A group travels as a record of W uint64 (pgx_result_record_words: W = 1 + planes):
+ * packed group key, doc count, then per value column sum, ordered min, ordered max (the layout of the partitioned
+ * sparse group-by; an INT / LONG column's sum is int64, a FLOAT / DOUBLE column's the f64 bits).  One value column:
+ * W = 5.  pgx_result_device_groups: *n = the number of groups of a result whose groups stay in device memory
+ * (PGX_ERR_UNSUPPORTED otherwise) and, when records is non-NULL, the records written to that device buffer
+ * (n x W x 8 bytes, on the result's device).  pgx_result_merge_groups: merge n records of like's layout (equal keys
+ * combine: counts and integer sums add, f64 sums add in f64 -- in arbitrary order, so within rounding of the
+ * reference's sequential order -- minima and maxima take the extreme) into a device-resident result decoded with
+ * `like`'s key tables -- valid when every source planned the same key space (identical dictionaries on all ranks);
+ * stats (may be NULL: like's) become the result's ExecutionStatistics.  Replaces the cross-server half of
+ * MCombineGroupByOperator.java:139-233 (per-function combineTwoValues over equal keys). */
 pgx_status pgx_result_device_groups(const pgx_result* r, int64_t* n, void* records);
+pgx_status pgx_result_record_words(const pgx_result* r, int32_t* words);
 pgx_status pgx_result_merge_groups(pgx_ctx* ctx, const pgx_result* like, const void* records, int64_t n,
                                    const int64_t stats[4], pgx_result** out);
 

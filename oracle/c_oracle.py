@@ -28,7 +28,8 @@ class PgoSegQuery(C.Structure):
                 ("num_groups", C.c_int64), ("g_keys", C.POINTER(C.c_int64)), ("g_sums", C.POINTER(C.c_double)),
                 ("g_counts", C.POINTER(C.c_int64)), ("g_mins", C.POINTER(C.c_double)),
                 ("g_maxs", C.POINTER(C.c_double)), ("g_cap", C.c_int64),
-                ("leaf_inv", C.POINTER(C.c_void_p)), ("leaf_excl", C.POINTER(C.c_int32))]
+                ("leaf_inv", C.POINTER(C.c_void_p)), ("leaf_excl", C.POINTER(C.c_int32)),
+                ("key_part", C.c_int32), ("key_parts", C.c_int32)]
 
 
 def lib():
@@ -40,6 +41,8 @@ def lib():
         L.pgo_synth_fwd.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_uint32, C.c_void_p, C.c_int64]
         L.pgo_synth_fwd_paired.argtypes = [C.c_uint64, C.c_int64, C.c_int, C.c_uint32, C.c_void_p, C.c_int64,
                                            C.c_uint64, C.c_uint32]
+        L.pgo_synth_fwd_range.argtypes = [C.c_uint64, C.c_int64, C.c_int64, C.c_int, C.c_uint32, C.c_void_p,
+                                          C.c_uint64, C.c_uint32]
         L.pgo_synth_value.argtypes = [C.c_uint64, C.c_int64, C.c_uint32]
         L.pgo_synth_value.restype = C.c_uint32
         L.pgo_run.argtypes = [C.POINTER(PgoSegQuery), C.c_int, C.c_int]
@@ -59,7 +62,16 @@ def synth_fwd(seed, n, bits, card, pair_seed=0, npairs=0):
     npairs > 0 to pgx_synth_column_paired)."""
     nbytes = (n * bits + 7) // 8 + 8
     out = np.zeros(nbytes, dtype=np.uint8)
-    lib().pgo_synth_fwd_paired(seed, n, bits, card, out.ctypes.data, nbytes, pair_seed, npairs)
+    L = lib()
+    if n < (1 << 22):
+        L.pgo_synth_fwd_paired(seed, n, bits, card, out.ctypes.data, nbytes, pair_seed, npairs)
+        return out
+    from concurrent.futures import ThreadPoolExecutor  # row ranges of a multiple of 8 rows touch disjoint bytes
+    T = test_threads()
+    step = (n // T + 7) & ~7
+    with ThreadPoolExecutor(T) as ex:
+        list(ex.map(lambda r0: L.pgo_synth_fwd_range(seed, r0, min(n, r0 + step), bits, card, out.ctypes.data,
+                                                     pair_seed, npairs), range(0, n, step)))
     return out
 
 
@@ -95,13 +107,22 @@ class Segment:
         self.columns = columns
 
 
+def test_threads():
+    """Host threads for the C twin in tests: the GPU box shows the whole machine's CPUs but grants 16."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def run(segments, filter_col=None, lo=0, hi=-1, metric="m", group_cols=(), threads=1, collect_groups=False,
-        leaves=None, prog=None, inverted=None, excl=None):
+        leaves=None, prog=None, inverted=None, excl=None, key_parts=1):
     """leaves = [(column, dictId bitset uint32 array)], prog = postfix ints (>= 0 leaf, -1 AND, -2 OR).
     inverted = {column: .bitmap.inv bytes (uint8 array)} per segment (a list, one dict per segment): every leaf is then
-    evaluated on the bitmaps (BitmapBasedFilterOperator) instead of per row; excl[l] = 1 marks NEQ / NOT_IN leaves."""
+    evaluated on the bitmaps (BitmapBasedFilterOperator) instead of per row; excl[l] = 1 marks NEQ / NOT_IN leaves.
+    key_parts > 1 (LONG_MAP group-by with collect_groups, tests only): every segment runs as key_parts tasks, each
+    aggregating the groups of one hash part of the key space; the parts' groups are disjoint and are concatenated (in
+    part order), and count / entries come from part 0 (every part scans every doc)."""
     L = lib()
-    qs = (PgoSegQuery * len(segments))()
+    P = max(1, int(key_parts))
+    qs = (PgoSegQuery * (len(segments) * P))()
     keep = []
     for i, s in enumerate(segments):
         cols = (PgoCol * len(s.names))()
@@ -114,53 +135,68 @@ def run(segments, filter_col=None, lo=0, hi=-1, metric="m", group_cols=(), threa
             cols[j].card = card
         gc = (C.c_int32 * max(1, len(group_cols)))(*[s.names.index(g) for g in group_cols])
         keep += [cols, gc]
-        q = qs[i]
-        q.num_docs = s.num_docs
-        q.num_cols = len(s.names)
-        q.cols = cols
-        q.filter_col = s.names.index(filter_col) if filter_col else -1
-        q.lo, q.hi = lo, hi
-        if leaves:
-            lc = (C.c_int32 * len(leaves))(*[s.names.index(c) for c, _ in leaves])
-            bits = [np.ascontiguousarray(b, dtype=np.uint32) for _, b in leaves]
-            lb = (C.POINTER(C.c_uint32) * len(leaves))(*[b.ctypes.data_as(C.POINTER(C.c_uint32)) for b in bits])
-            pg = (C.c_int32 * len(prog))(*prog)
-            keep += [lc, bits, lb, pg]
-            q.num_leaves = len(leaves)
-            q.leaf_col = lc
-            q.leaf_bits = lb
-            q.prog_len = len(prog)
-            q.prog = pg
-            if inverted is not None:
-                invs = [np.ascontiguousarray(inverted[i][c], dtype=np.uint8) for c, _ in leaves]
-                li = (C.c_void_p * len(leaves))(*[a.ctypes.data for a in invs])
-                le = (C.c_int32 * len(leaves))(*(excl or [0] * len(leaves)))
-                keep += [invs, li, le]
-                q.leaf_inv = li
-                q.leaf_excl = le
-        q.metric_col = s.names.index(metric)
-        q.num_group_cols = len(group_cols)
-        q.group_cols = gc
-        if collect_groups:
-            cap = s.num_docs
-            arrs = (np.zeros(cap, np.int64), np.zeros(cap, np.float64), np.zeros(cap, np.int64),
-                    np.zeros(cap, np.float64), np.zeros(cap, np.float64))
-            keep.append(arrs)
-            q.g_keys = arrs[0].ctypes.data_as(C.POINTER(C.c_int64))
-            q.g_sums = arrs[1].ctypes.data_as(C.POINTER(C.c_double))
-            q.g_counts = arrs[2].ctypes.data_as(C.POINTER(C.c_int64))
-            q.g_mins = arrs[3].ctypes.data_as(C.POINTER(C.c_double))
-            q.g_maxs = arrs[4].ctypes.data_as(C.POINTER(C.c_double))
-            q.g_cap = cap
-    L.pgo_run(qs, len(segments), threads)
+        for part in range(P):
+            q = qs[i * P + part]
+            q.key_part, q.key_parts = part, P
+            q.num_docs = s.num_docs
+            q.num_cols = len(s.names)
+            q.cols = cols
+            q.filter_col = s.names.index(filter_col) if filter_col else -1
+            q.lo, q.hi = lo, hi
+            if leaves:
+                lc = (C.c_int32 * len(leaves))(*[s.names.index(c) for c, _ in leaves])
+                bits = [np.ascontiguousarray(b, dtype=np.uint32) for _, b in leaves]
+                lb = (C.POINTER(C.c_uint32) * len(leaves))(*[b.ctypes.data_as(C.POINTER(C.c_uint32)) for b in bits])
+                pg = (C.c_int32 * len(prog))(*prog)
+                keep += [lc, bits, lb, pg]
+                q.num_leaves = len(leaves)
+                q.leaf_col = lc
+                q.leaf_bits = lb
+                q.prog_len = len(prog)
+                q.prog = pg
+                if inverted is not None:
+                    invs = [np.ascontiguousarray(inverted[i][c], dtype=np.uint8) for c, _ in leaves]
+                    li = (C.c_void_p * len(leaves))(*[a.ctypes.data for a in invs])
+                    le = (C.c_int32 * len(leaves))(*(excl or [0] * len(leaves)))
+                    keep += [invs, li, le]
+                    q.leaf_inv = li
+                    q.leaf_excl = le
+            q.metric_col = s.names.index(metric)
+            q.num_group_cols = len(group_cols)
+            q.group_cols = gc
+            if collect_groups:
+                _attach_groups(q, s.num_docs if P == 1 else s.num_docs // P + s.num_docs // (4 * P) + 65536, keep)
+    L.pgo_run(qs, len(qs), threads)
+    if collect_groups and P > 1:  # a part whose groups overflowed its guess: rerun it alone with the exact capacity
+        redo = [k for k in range(len(qs)) if qs[k].num_groups > qs[k].g_cap]
+        for k in redo:
+            _attach_groups(qs[k], qs[k].num_groups, keep)
+            L.pgo_run(C.byref(qs[k]), 1, 1)
     out = []
     for i in range(len(segments)):
-        q = qs[i]
+        q = qs[i * P]
         r = {"count": q.count, "sum": q.sum, "min": q.vmin, "max": q.vmax, "entries": q.entries_scanned,
-             "num_groups": q.num_groups}
+             "num_groups": sum(qs[i * P + p].num_groups for p in range(P))}
         if collect_groups:
-            ng = q.num_groups
-            r["groups"] = tuple(np.ctypeslib.as_array(p, shape=(ng,)).copy()
-                                for p in (q.g_keys, q.g_sums, q.g_counts, q.g_mins, q.g_maxs))
+            parts = []
+            for p in range(P):
+                qp = qs[i * P + p]
+                ng = qp.num_groups
+                parts.append(tuple(np.ctypeslib.as_array(a, shape=(ng,)).copy() if ng else np.zeros(0, dt)
+                                   for a, dt in zip((qp.g_keys, qp.g_sums, qp.g_counts, qp.g_mins, qp.g_maxs),
+                                                    (np.int64, np.float64, np.int64, np.float64, np.float64))))
+            r["groups"] = tuple(np.concatenate([pt[j] for pt in parts]) for j in range(5)) if P > 1 else parts[0]
         out.append(r)
     return out
+
+
+def _attach_groups(q, cap, keep):
+    arrs = (np.zeros(cap, np.int64), np.zeros(cap, np.float64), np.zeros(cap, np.int64),
+            np.zeros(cap, np.float64), np.zeros(cap, np.float64))
+    keep.append(arrs)
+    q.g_keys = arrs[0].ctypes.data_as(C.POINTER(C.c_int64))
+    q.g_sums = arrs[1].ctypes.data_as(C.POINTER(C.c_double))
+    q.g_counts = arrs[2].ctypes.data_as(C.POINTER(C.c_int64))
+    q.g_mins = arrs[3].ctypes.data_as(C.POINTER(C.c_double))
+    q.g_maxs = arrs[4].ctypes.data_as(C.POINTER(C.c_double))
+    q.g_cap = cap

@@ -61,6 +61,19 @@ void pgo_synth_fwd_paired(uint64_t seed, int64_t n, int bits, uint32_t card, uin
   }
 }
 
+/* Rows [r0, r1) of the same stream into a zeroed buffer; r0 a multiple of 8, so ranges touch disjoint bytes and may be
+   written by separate threads. */
+void pgo_synth_fwd_range(uint64_t seed, int64_t r0, int64_t r1, int bits, uint32_t card, uint8_t* out,
+                         uint64_t pair_seed, uint32_t npairs) {
+  for (int64_t r = r0; r < r1; ++r) {
+    const int64_t src = npairs ? (int64_t)pgo_synth_value(pair_seed, r, npairs) : r;
+    uint32_t v = pgo_synth_value(seed, src, card);
+    int64_t bit = r * bits;
+    for (int k = bits - 1; k >= 0; --k, ++bit)
+      if ((v >> k) & 1u) out[bit >> 3] |= (uint8_t)(0x80u >> (bit & 7));
+  }
+}
+
 void pgo_synth_fwd(uint64_t seed, int64_t n, int bits, uint32_t card, uint8_t* out, int64_t out_len) {
   pgo_synth_fwd_paired(seed, n, bits, card, out, out_len, 0, 0);
 }
@@ -137,6 +150,10 @@ typedef struct {
      then one portable roaring bitmap per dictId); leaf_excl[l] = 1 for NEQ / NOT_IN leaves */
   const uint8_t* const* leaf_inv;
   const int32_t* leaf_excl;
+  /* test speed-up, not a reference structure: with key_parts > 1 a LONG_MAP group-by aggregates only the docs whose
+     raw key hashes to key_part (mix64(key) >> 40 mod key_parts); the parts of one segment run as separate tasks and
+     hold disjoint groups, each in doc order, so their union is the segment's group map */
+  int32_t key_part, key_parts;
 } pgo_segment_query;
 
 static int row_matches(const pgo_segment_query* q, int64_t d) {
@@ -805,6 +822,8 @@ static void run_segment(pgo_segment_query* q) {
         }
         if (array_based) {
           gkeys[i] = (int32_t)raw;
+        } else if (q->key_parts > 1 && (int32_t)((mix64((uint64_t)raw) >> 40) % (uint64_t)q->key_parts) != q->key_part) {
+          gkeys[i] = -1;
         } else {
           int32_t id = lmap_get_or_add(&map, raw);
           if (id >= mcap) {
@@ -827,6 +846,7 @@ static void run_segment(pgo_segment_query* q) {
       double* H_ = array_based ? dmax : mmax;
       for (int i = 0; i < n; ++i) {  /* per doc in doc order (Sum/Min/MaxAggregationFunction.aggregateGroupBySV) */
         const int32_t k = gkeys[i];
+        if (k < 0) continue;
         S_[k] += values[i];
         C_[k] += 1;
         if (values[i] < L_[k]) L_[k] = values[i];

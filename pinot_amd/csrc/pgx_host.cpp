@@ -1713,18 +1713,24 @@ pgx_status pgx_result_device_groups(const pgx_result* r, int64_t* n, void* recor
     if (!r || !n) fail(PGX_ERR_INVALID_ARG, "NULL argument");
     r->ready();
     if (!r->group_by || !r->lazy) fail(PGX_ERR_UNSUPPORTED, "the groups of this result are not in device memory");
-    if (r->lazy->nplanes != 4) fail(PGX_ERR_UNSUPPORTED, "group records hold one value column");
-    for (bool f : r->lazy->agg_fp)
-      if (f) fail(PGX_ERR_UNSUPPORTED, "group records hold integer sums");
     *n = r->num_groups;
     if (!records || !r->num_groups) return;
     const auto& L = *r->lazy;
     hip_check(hipSetDevice(L.ctx->device), "hipSetDevice");
     hipStream_t st = L.ctx->stream;
-    PGX_LAUNCH(st, "pgx_group_pack", pgx_launch_group_pack(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap, r->num_groups,
-                                    static_cast<uint64_t*>(records), st),
+    PGX_LAUNCH(st, "pgx_group_pack", pgx_launch_group_pack(L.okey.as<uint64_t>(), L.oplane.as<uint64_t>(), L.ocap,
+                                                           r->num_groups, L.nplanes, static_cast<uint64_t*>(records), st),
               "group pack");
     hip_check(hipStreamSynchronize(st), "sync");
+  });
+}
+
+pgx_status pgx_result_record_words(const pgx_result* r, int32_t* words) {
+  return guarded([&] {
+    if (!r || !words) fail(PGX_ERR_INVALID_ARG, "NULL argument");
+    r->ready();
+    if (!r->group_by || !r->lazy) fail(PGX_ERR_UNSUPPORTED, "the groups of this result are not in device memory");
+    *words = 1 + r->lazy->nplanes;
   });
 }
 
@@ -1737,7 +1743,7 @@ pgx_status pgx_result_merge_groups(pgx_ctx* ctx, const pgx_result* like, const v
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     auto R = std::make_unique<pgx_result>();
     const uint64_t* rec = static_cast<const uint64_t*>(records);
-    merge_device_groups(ctx, ctx->stream, rec, rec + 1, 5, 1, n, *like->lazy, R.get());
+    merge_device_groups(ctx, ctx->stream, rec, rec + 1, 1 + like->lazy->nplanes, 1, n, *like->lazy, R.get());
     R->num_aggs = like->num_aggs;
     R->agg_fn = like->agg_fn;
     R->top_n = like->top_n;

@@ -104,11 +104,12 @@ extern "C" hipError_t pgx_launch_join(const uint64_t* okey0, int64_t n0, const u
                                       hipStream_t stream);
 extern "C" hipError_t pgx_launch_group_merge(const uint64_t* key, const uint64_t* pl, int64_t es, int64_t ps,
                                              int64_t n, unsigned long long* tkey, unsigned long long* tpl,
-                                             uint64_t cap, unsigned long long* overflow, hipStream_t stream);
+                                             uint64_t cap, int nplanes, uint64_t ops, unsigned long long* overflow,
+                                             hipStream_t stream);
 extern "C" hipError_t pgx_launch_group_pack(const uint64_t* okey, const uint64_t* opl, int64_t ocap, int64_t n,
-                                            uint64_t* rec, hipStream_t stream);
+                                            int nplanes, uint64_t* rec, hipStream_t stream);
 extern "C" hipError_t pgx_launch_group_compact(const unsigned long long* tkey, const unsigned long long* tpl,
-                                               uint64_t cap, uint64_t* okey, uint64_t* opl, int64_t ocap,
+                                               uint64_t cap, int nplanes, uint64_t* okey, uint64_t* opl, int64_t ocap,
                                                unsigned long long* counter, hipStream_t stream);
 struct pgx_ctx;
 extern "C" void ctx_unref(pgx_ctx* ctx);

@@ -6,11 +6,13 @@
 // * pgx_dense_reduce: dst op= src over dense tables of the same layout (slot s = the same group on every device: the
 //   plan's key space is the union dictionary of ALL segments of the query), one plane op per plane.  Streams both
 //   tables once (16 B read + 8 B written per slot and plane), HBM-bound.
-// * pgx_group_merge: sparse groups (packed key + planes count / int64 sum / ordered min / ordered max, the layout
-//   pgx_part_aggregate writes) from any number of devices, copied side by side into one buffer, are inserted into an
-//   open-addressing table in HBM (linear probing on a 64-bit mix of the key, one CAS per new key, then one atomic per
-//   plane), and pgx_group_compact appends the occupied slots to okey / oplane again (wave-aggregated cursor).  A group
-//   moves 40 B in, ~5 random 8-B atomics, 40 B out: bound by the atomics' 64-B granules, not by arithmetic.
+// * pgx_group_merge: sparse groups (packed key + planes: count, then per value column sum / ordered min / ordered max,
+//   the layout pgx_part_aggregate / pgx_narrow_aggregate / pgx_part_aggregate_f64 and the several-column join write;
+//   a FLOAT / DOUBLE column's sum plane holds f64 bits) from any number of devices, copied side by side into one
+//   buffer, are inserted into an open-addressing table in HBM (linear probing on a 64-bit mix of the key, one CAS per
+//   new key, then one atomic per plane with the plane's op: int64 add, f64 add, ordered min, ordered max), and
+//   pgx_group_compact appends the occupied slots to okey / oplane again (wave-aggregated cursor).  A group of P planes
+//   moves 8 (1 + P) B in, P + 1 random 8-B atomics, 8 (1 + P) B out: bound by the atomics' 64-B granules.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -42,14 +44,15 @@ __global__ void pgx_dense_reduce(unsigned long long* __restrict__ dst, const uns
   }
 }
 
-// Table: tkey[cap] (kMergeEmpty = free), tpl[p * cap + slot] for p = 0 count, 1 sum, 2 min (init ~0), 3 max (init 0).
-// Input group i: key[i * es], plane p at pl[p * ps + i * es] (columnar: es = 1, ps = n; records of 5 words: key = rec,
-// pl = rec + 1, es = 5, ps = 1).  A group whose probe sequence finds no slot counts in *overflow.
+// Table: tkey[cap] (kMergeEmpty = free), tpl[p * cap + slot] for the planes p < nplanes (min planes start at ~0, the
+// others at 0).  ops: 2 bits per plane (PlaneOp: 0 int64 add, 1 f64 add, 2 ordered min, 3 ordered max).  Input group i:
+// key[i * es], plane p at pl[p * ps + i * es] (columnar: es = 1, ps = n; records of 1 + nplanes words: key = rec,
+// pl = rec + 1, es = 1 + nplanes, ps = 1).  A group whose probe sequence finds no slot counts in *overflow.
 __global__ void __launch_bounds__(256) pgx_group_merge(const uint64_t* __restrict__ key,
                                                        const uint64_t* __restrict__ pl, int64_t es, int64_t ps,
                                                        int64_t n, unsigned long long* __restrict__ tkey,
-                                                       unsigned long long* __restrict__ tpl, uint64_t cap,
-                                                       unsigned long long* __restrict__ overflow) {
+                                                       unsigned long long* __restrict__ tpl, uint64_t cap, int nplanes,
+                                                       uint64_t ops, unsigned long long* __restrict__ overflow) {
   const uint64_t mask = cap - 1;  // cap is a power of two
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -69,17 +72,23 @@ __global__ void __launch_bounds__(256) pgx_group_merge(const uint64_t* __restric
       continue;
     }
     const uint64_t* g = pl + i * es;
-    atomicAdd(tpl + slot, static_cast<unsigned long long>(g[0]));
-    atomicAdd(tpl + cap + slot, static_cast<unsigned long long>(g[ps]));
-    atomicMin(tpl + 2 * cap + slot, static_cast<unsigned long long>(g[2 * ps]));
-    atomicMax(tpl + 3 * cap + slot, static_cast<unsigned long long>(g[3 * ps]));
+    for (int p = 0; p < nplanes; ++p) {
+      const unsigned long long x = static_cast<unsigned long long>(g[p * ps]);
+      unsigned long long* t = tpl + p * cap + slot;
+      const int op = static_cast<int>((ops >> (2 * p)) & 3u);
+      if (op == 0) atomicAdd(t, x);
+      else if (op == 1) atomicAdd(reinterpret_cast<double*>(t), __longlong_as_double(static_cast<long long>(x)));
+      else if (op == 2) atomicMin(t, x);
+      else atomicMax(t, x);
+    }
   }
 }
 
 __global__ void __launch_bounds__(256) pgx_group_compact(const unsigned long long* __restrict__ tkey,
                                                          const unsigned long long* __restrict__ tpl, uint64_t cap,
-                                                         uint64_t* __restrict__ okey, uint64_t* __restrict__ opl,
-                                                         int64_t ocap, unsigned long long* __restrict__ counter) {
+                                                         int nplanes, uint64_t* __restrict__ okey,
+                                                         uint64_t* __restrict__ opl, int64_t ocap,
+                                                         unsigned long long* __restrict__ counter) {
   const int lane = threadIdx.x & 63;
   for (uint64_t base = blockIdx.x * static_cast<uint64_t>(blockDim.x) + (threadIdx.x & ~63u); base < cap;
        base += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
@@ -94,7 +103,7 @@ __global__ void __launch_bounds__(256) pgx_group_compact(const unsigned long lon
     const unsigned long long j = o + __popcll(bal & ((1ull << lane) - 1ull));
     if (j >= static_cast<unsigned long long>(ocap)) continue;  // the host sized ocap from the table; cannot happen
     okey[j] = tkey[s];
-    for (int p = 0; p < 4; ++p) opl[p * ocap + j] = tpl[p * cap + s];
+    for (int p = 0; p < nplanes; ++p) opl[p * ocap + j] = tpl[p * cap + s];
   }
 }
 
@@ -164,15 +173,15 @@ __global__ void __launch_bounds__(256) pgx_join_scatter(const uint64_t* __restri
   }
 }
 
-// Columnar groups (okey, oplane[p * ocap + i]) -> records of 5 words (key, count, sum, min, max) for an exchange.
+// Columnar groups (okey, oplane[p * ocap + i]) -> records of 1 + nplanes words (key, then the planes) for an exchange.
 __global__ void __launch_bounds__(256) pgx_group_pack(const uint64_t* __restrict__ okey,
                                                       const uint64_t* __restrict__ opl, int64_t ocap, int64_t n,
-                                                      uint64_t* __restrict__ rec) {
+                                                      int nplanes, uint64_t* __restrict__ rec) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
        i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    uint64_t* r = rec + 5 * i;
+    uint64_t* r = rec + (1 + nplanes) * i;
     r[0] = okey[i];
-    for (int p = 0; p < 4; ++p) r[1 + p] = opl[p * ocap + i];
+    for (int p = 0; p < nplanes; ++p) r[1 + p] = opl[p * ocap + i];
   }
 }
 
@@ -220,30 +229,33 @@ extern "C" hipError_t pgx_launch_join(const uint64_t* okey0, int64_t n0, const u
 
 extern "C" hipError_t pgx_launch_group_merge(const uint64_t* key, const uint64_t* pl, int64_t es, int64_t ps,
                                              int64_t n, unsigned long long* tkey, unsigned long long* tpl,
-                                             uint64_t cap, unsigned long long* overflow, hipStream_t stream) {
+                                             uint64_t cap, int nplanes, uint64_t ops, unsigned long long* overflow,
+                                             hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  if (cap == 0 || (cap & (cap - 1)) != 0) return hipErrorInvalidValue;
+  if (cap == 0 || (cap & (cap - 1)) != 0 || nplanes < 1 || nplanes > 32) return hipErrorInvalidValue;
   const int64_t g = (n + 255) / 256;
   hipLaunchKernelGGL(pgx::pgx_group_merge, dim3(static_cast<unsigned>(g < 65536 ? g : 65536)), dim3(256), 0, stream,
-                     key, pl, es, ps, n, tkey, tpl, cap, overflow);
+                     key, pl, es, ps, n, tkey, tpl, cap, nplanes, ops, overflow);
   return hipGetLastError();
 }
 
 extern "C" hipError_t pgx_launch_group_pack(const uint64_t* okey, const uint64_t* opl, int64_t ocap, int64_t n,
-                                            uint64_t* rec, hipStream_t stream) {
+                                            int nplanes, uint64_t* rec, hipStream_t stream) {
   if (n <= 0) return hipSuccess;
+  if (nplanes < 1 || nplanes > 32) return hipErrorInvalidValue;
   const int64_t g = (n + 255) / 256;
   hipLaunchKernelGGL(pgx::pgx_group_pack, dim3(static_cast<unsigned>(g < 65536 ? g : 65536)), dim3(256), 0, stream,
-                     okey, opl, ocap, n, rec);
+                     okey, opl, ocap, n, nplanes, rec);
   return hipGetLastError();
 }
 
 extern "C" hipError_t pgx_launch_group_compact(const unsigned long long* tkey, const unsigned long long* tpl,
-                                               uint64_t cap, uint64_t* okey, uint64_t* opl, int64_t ocap,
+                                               uint64_t cap, int nplanes, uint64_t* okey, uint64_t* opl, int64_t ocap,
                                                unsigned long long* counter, hipStream_t stream) {
   if (cap == 0) return hipSuccess;
+  if (nplanes < 1 || nplanes > 32) return hipErrorInvalidValue;
   const uint64_t g = (cap + 255) / 256;
   hipLaunchKernelGGL(pgx::pgx_group_compact, dim3(static_cast<unsigned>(g < 65536 ? g : 65536)), dim3(256), 0, stream,
-                     tkey, tpl, cap, okey, opl, ocap, counter);
+                     tkey, tpl, cap, nplanes, okey, opl, ocap, counter);
   return hipGetLastError();
 }

@@ -9,27 +9,44 @@ namespace pgxh {
 // Merging group-by partials of different devices (MCombineGroupByOperator.java:166-191 semantics: equal
 // keys combine with each function's combineTwoValues).
 // -------------------------------------------------------------------------------------------------
-// Sparse groups resident in device memory (packed keys; planes count / int64 sum / ordered min / ordered max: group i
-// key keys[i * es], plane p planes[p * ps + i * es]) -> one device-resident result decoded with `like`'s key tables
+// The merge op of every plane of a device-resident result (count, then sum / min / max per value column): PlaneOp,
+// 2 bits per plane.  A FLOAT / DOUBLE column's sum plane holds f64 bits (pgx_part_aggregate_f64), so it adds as f64.
+uint64_t lazy_plane_ops(const pgx_result::Lazy& L) {
+  uint64_t ops = uint64_t(P_ADD_I64);
+  for (int p = 1; p < L.nplanes; ++p) {
+    const int c = (p - 1) / 3, r = (p - 1) % 3;
+    bool fp = false;
+    for (size_t a = 0; a < L.agg_plane.size(); ++a)
+      if (L.agg_plane[a] >= 1 + 3 * c && L.agg_plane[a] <= 3 + 3 * c && L.agg_fp[a]) fp = true;
+    const int op = r == 0 ? (fp ? P_ADD_F64 : P_ADD_I64) : (r == 1 ? P_MIN_ORD : P_MAX_ORD);
+    ops |= uint64_t(op) << (2 * p);
+  }
+  return ops;
+}
+
+// Sparse groups resident in device memory (packed keys; like.nplanes planes: group i key keys[i * es], plane p
+// planes[p * ps + i * es]) -> one device-resident result of like's layout, decoded with `like`'s key tables
 // (pgx_merge.hip).
 void merge_device_groups(pgx_ctx* ctx, hipStream_t st, const uint64_t* keys, const uint64_t* planes, int64_t es,
                          int64_t ps, int64_t n, const pgx_result::Lazy& like, pgx_result* R) {
+  const int NP = like.nplanes;
+  const uint64_t ops = lazy_plane_ops(like);
   uint64_t cap = 1024;
   while (cap < uint64_t(std::max<int64_t>(n, 1)) * 2) cap <<= 1;
-  DevBuf tkey(ctx, cap * 8), tpl(ctx, cap * 4 * 8), ctr(ctx, 64);
+  DevBuf tkey(ctx, cap * 8), tpl(ctx, cap * NP * 8), ctr(ctx, 64);
   const int64_t ocap = std::max<int64_t>(n, 1);
-  DevBuf okey(ctx, size_t(ocap) * 8), oplane(ctx, size_t(ocap) * 4 * 8);
+  DevBuf okey(ctx, size_t(ocap) * 8), oplane(ctx, size_t(ocap) * NP * 8);
   unsigned long long* tp = tpl.as<unsigned long long>();
   hip_check(hipMemsetAsync(tkey.p, 0xFF, cap * 8, st), "merge table");
-  hip_check(hipMemsetAsync(tp, 0, cap * 2 * 8, st), "merge table");          // count, sum
-  hip_check(hipMemsetAsync(tp + 2 * cap, 0xFF, cap * 8, st), "merge table"); // ordered min
-  hip_check(hipMemsetAsync(tp + 3 * cap, 0, cap * 8, st), "merge table");    // ordered max
+  for (int p = 0; p < NP; ++p)  // ordered-min planes start at the largest encoding, the others at 0 (0.0 for f64)
+    hip_check(hipMemsetAsync(tp + p * cap, ((ops >> (2 * p)) & 3u) == P_MIN_ORD ? 0xFF : 0, cap * 8, st), "merge table");
   hip_check(hipMemsetAsync(ctr.p, 0, 16, st), "merge counters");
   unsigned long long* c = ctr.as<unsigned long long>();
-  PGX_LAUNCH(st, "pgx_group_merge", pgx_launch_group_merge(keys, planes, es, ps, n, tkey.as<unsigned long long>(), tp, cap, c + 1, st),
+  PGX_LAUNCH(st, "pgx_group_merge", pgx_launch_group_merge(keys, planes, es, ps, n, tkey.as<unsigned long long>(), tp, cap,
+                                                           NP, ops, c + 1, st),
             "group merge");
-  PGX_LAUNCH(st, "pgx_group_compact", pgx_launch_group_compact(tkey.as<unsigned long long>(), tp, cap, okey.as<uint64_t>(),
-                                     oplane.as<uint64_t>(), ocap, c, st),
+  PGX_LAUNCH(st, "pgx_group_compact", pgx_launch_group_compact(tkey.as<unsigned long long>(), tp, cap, NP,
+                                                               okey.as<uint64_t>(), oplane.as<uint64_t>(), ocap, c, st),
             "group compact");
   unsigned long long h[2] = {0, 0};
   hip_check(hipMemcpyAsync(h, c, 16, hipMemcpyDeviceToHost, st), "merge counters D2H");
@@ -46,9 +63,9 @@ void merge_device_groups(pgx_ctx* ctx, hipStream_t st, const uint64_t* keys, con
   L->rep_seg = like.rep_seg;
   L->rep_id = like.rep_id;
   L->agg_kind = like.agg_kind;
-  L->agg_plane = like.agg_plane;  // (merged results hold the 4-plane layout: count, sum, min, max)
+  L->agg_plane = like.agg_plane;
   L->agg_fp = like.agg_fp;
-  L->nplanes = 4;
+  L->nplanes = NP;
   ctx->refs.fetch_add(1);
   L->ctx = ctx;
   R->lazy = std::move(L);
@@ -236,20 +253,19 @@ void run_multi(pgx_ctx* const* ctxs, int nctx, const pgx_query& q, pgx_segment* 
     reinterpret_cast<unsigned long long*>(B.host.p)[16] = static_cast<unsigned long long>(stats[0]);
     finish_result(c0, q, P, B, sub[0].data(), int(sub[0].size()), st, R, host.data());
   } else {
-    bool all_lazy = true;
-    for (auto& r : res) {
-      all_lazy = all_lazy && r->lazy && r->lazy->nplanes == 4;
-      if (all_lazy)
-        for (bool f : r->lazy->agg_fp) all_lazy = all_lazy && !f;  // (the device merge adds integer sums)
-    }
+    bool all_lazy = true;  // every context's groups in device memory, in one plane layout
+    for (auto& r : res)
+      all_lazy = all_lazy && r->lazy && r->lazy->nplanes == res[0]->lazy->nplanes &&
+                 r->lazy->agg_plane == res[0]->lazy->agg_plane && r->lazy->agg_fp == res[0]->lazy->agg_fp;
     *R = pgx_result();
     R->num_aggs = na;
     R->agg_fn = q.agg_fn;
     R->group_by = true;
     if (all_lazy) {
+      const int NP = res[0]->lazy->nplanes;
       int64_t total = 0;
       for (auto& r : res) total += r->num_groups;
-      DevBuf keys(c0, size_t(std::max<int64_t>(total, 1)) * 8), pl(c0, size_t(std::max<int64_t>(total, 1)) * 32);
+      DevBuf keys(c0, size_t(std::max<int64_t>(total, 1)) * 8), pl(c0, size_t(std::max<int64_t>(total, 1)) * 8 * NP);
       int64_t off = 0;
       for (auto& r : res) {
         const auto& Lz = *r->lazy;
@@ -257,7 +273,7 @@ void run_multi(pgx_ctx* const* ctxs, int nctx, const pgx_query& q, pgx_segment* 
         if (!ng) continue;
         hip_check(hipMemcpyPeerAsync(keys.as<uint64_t>() + off, c0->device, Lz.okey.p, Lz.ctx->device, ng * 8, st),
                   "group keys peer copy");
-        for (int p = 0; p < 4; ++p)
+        for (int p = 0; p < NP; ++p)
           hip_check(hipMemcpyPeerAsync(pl.as<uint64_t>() + p * total + off, c0->device,
                                        Lz.oplane.as<uint64_t>() + p * Lz.ocap, Lz.ctx->device, ng * 8, st),
                     "group planes peer copy");

@@ -449,7 +449,10 @@ bool run_value_columns(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* seg
         narrow_fallback(ctx, q, segs, n, P, B);
       }
     }
-    if (!ok && !run_partitioned(ctx, P, B, PB, st)) return false;
+    if (!ok && !run_partitioned(ctx, P, B, PB, st)) {
+      if (v > 0) P.load_part_col(P.part_cols[0]);  // the caller's global-hash fallback plans from column 0's state
+      return false;
+    }
     const unsigned long long* outs = reinterpret_cast<const unsigned long long*>(B.host.bytes() + B.off_outs);
     const int64_t ng = int64_t(std::min<unsigned long long>(outs[28], uint64_t(PB.ocap)));
     if (v == 0) {

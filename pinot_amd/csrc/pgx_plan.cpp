@@ -2,6 +2,7 @@
 // programs fused from inverted-index leaves, predicate values to dictId ranges, group key spaces
 // (DefaultGroupKeyGenerator), the partitioned-path choice, and the per-segment kernel descriptors (plan_query).
 // Reference paths are relative to pinot-core/src/main/java/com/linkedin/pinot/core/.
+#include <cstring>
 #include "pgx_host.h"
 
 namespace pgxh {
@@ -898,20 +899,38 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         if (c0.data_type == PGX_FLOAT || c0.data_type == PGX_DOUBLE) {
           // FLOAT / DOUBLE: the records carry the value's index in the concatenation of the segments' dictionaries
           // (segments holding the same dictionary share one copy), 8-byte radix records, f64 aggregation
+          // a dictionary is shared only when its values equal an earlier segment's (the hash picks the candidate);
+          // the concatenation is sized before it is built, within the partition buffers' budget
           std::vector<double> all;
           std::vector<int64_t> fbase(size_t(n), 0);
-          std::unordered_map<uint64_t, int64_t> seen;
+          std::unordered_multimap<uint64_t, int> seen;  // dictionary hash -> first segment holding those values
+          std::vector<int> first_of(size_t(n), -1);
+          uint64_t total = 0;
           for (int s = 0; s < n; ++s) {
             const StagedColumn& c = segs[s]->col(P.qcols[vc]);
             if (c.data_type != c0.data_type || c.dvals.empty() || int64_t(c.dvals.size()) != int64_t(c.card)) return false;
             const uint64_t dk = c.dict_hash ^ (uint64_t(c.card) << 40);
-            auto it = seen.find(dk);
-            if (it != seen.end()) {
-              fbase[size_t(s)] = it->second;
+            auto range = seen.equal_range(dk);
+            for (auto it = range.first; it != range.second && first_of[size_t(s)] < 0; ++it) {
+              const StagedColumn& o = segs[it->second]->col(P.qcols[vc]);
+              if (o.dvals.size() == c.dvals.size() &&
+                  std::memcmp(o.dvals.data(), c.dvals.data(), c.dvals.size() * sizeof(double)) == 0)
+                first_of[size_t(s)] = it->second;
+            }
+            if (first_of[size_t(s)] >= 0) continue;
+            first_of[size_t(s)] = s;
+            seen.emplace(dk, s);
+            total += c.dvals.size();
+            if (total > (uint64_t(1) << 31) || total * 8 > kPartMaxBytes) return false;
+          }
+          all.reserve(size_t(total));
+          for (int s = 0; s < n; ++s) {
+            if (first_of[size_t(s)] != s) {
+              fbase[size_t(s)] = fbase[size_t(first_of[size_t(s)])];
               continue;
             }
+            const StagedColumn& c = segs[s]->col(P.qcols[vc]);
             fbase[size_t(s)] = int64_t(all.size());
-            seen.emplace(dk, int64_t(all.size()));
             all.insert(all.end(), c.dvals.begin(), c.dvals.end());
           }
           const int vbits = bits_for(int64_t(all.size()));

@@ -781,8 +781,8 @@ def agg_slices(request: dict, max_aggs: int = MAX_AGGS, max_cols: int = MAX_COLS
     def slots(idx):
         fns = [aggs[i]["fn"] for i in idx]
         if any(f in EXT_FUNCTIONS or f in EXT_MV_FUNCTIONS for f in fns):
-            return 1 + sum(_EXT_BASE_SLOTS.get(f, 0 if (f in EXT_FUNCTIONS or f in EXT_MV_FUNCTIONS) else 1)
-                           for f in fns)
+            return 1 + sum(_EXT_BASE_SLOTS.get(f, 0 if (f in EXT_FUNCTIONS or f in EXT_MV_FUNCTIONS) else
+                                               (2 if f == "avgmv" else 1)) for f in fns)
         return len(fns) + sum(1 for f in fns if f == "avgmv")
 
     def ncols(idx):
@@ -860,7 +860,9 @@ class _GpuOperator:
             if not use_star_tree:
                 sub["debug_options"] = dict(self.request.get("debug_options") or {}, useStarTree="false")
             blocks.append(type(self)(self.ctx, sub, self.segments, self.combine).next_block())
-        docs = {b.stats.num_docs_scanned for b in blocks}
+        # a slice's block served by the star-tree differs from a raw-docs block in docs scanned or in entries scanned
+        # in filter (a filter matching nothing scans the same 0 docs either way)
+        docs = {(b.stats.num_docs_scanned, b.stats.num_entries_scanned_in_filter) for b in blocks}
         if len(docs) > 1 and use_star_tree:
             # a slice answered from the star-tree and another from the raw docs: the reference plans the request as a
             # whole, and the star-tree only serves it when every function qualifies (StarTreeUtils), so all raw

@@ -325,7 +325,8 @@ def trim_to_size(fns: Sequence[str], vals, cnts, top_n: int, total: int = None) 
 
 # ------------------------------------------------------------------------------------------------
 # Device-side sparse merge (ranks planned the same key space: identical dictionaries, union_key_domains' fingerprint
-# check).  Every rank's groups stay in HBM as 5-word records (packed key, count, sum, min, max: pgx_result_device_groups),
+# check).  Every rank's groups stay in HBM as records of 1 + planes words (packed key, count, then sum, min, max per value
+# column: pgx_result_device_groups / pgx_result_record_words; f64 sums of FLOAT / DOUBLE columns merge as f64),
 # are routed to rank hash(key) mod world with ONE all_to_all_single (RCCL send/recv over xGMI), merged there by the
 # library's device hash merge (pgx_result_merge_groups), trimmed on the device (pgx_result_trim: the key partitions are
 # disjoint, so the union of the per-partition top-K holds the global top-K), and only the kept groups -- as VALUES --
@@ -350,7 +351,7 @@ def _all_to_all(out, inp, out_splits, in_splits):
 
 
 def exchange_group_records(recs, world: int):
-    """all_to_all of [n, 5] int64 group records by destination rank: returns this rank's [m, 5] records."""
+    """all_to_all of [n, W] int64 group records by destination rank: returns this rank's [m, W] records."""
     import torch
     import torch.distributed as dist
     dest = group_destination(recs[:, 0], world)
@@ -365,7 +366,7 @@ def exchange_group_records(recs, world: int):
     else:
         dist.all_to_all_single(recv, send)
     in_splits, out_splits = send.tolist(), recv.tolist()
-    out = torch.empty((sum(out_splits), 5), dtype=torch.int64, device=recs.device)
+    out = torch.empty((sum(out_splits), recs.shape[1]), dtype=torch.int64, device=recs.device)
     _all_to_all(out, recs, out_splits, in_splits)
     return out
 
@@ -383,8 +384,10 @@ def device_sparse_merge(ctx, q, r, segments, device):
     L = N.lib()
     world = dist.get_world_size()
     n = C.c_int64()
+    w = C.c_int32()
     N.check(L.pgx_result_device_groups(r, C.byref(n), None))
-    recs = torch.empty((max(n.value, 1), 5), dtype=torch.int64, device=device)
+    N.check(L.pgx_result_record_words(r, C.byref(w)))
+    recs = torch.empty((max(n.value, 1), w.value), dtype=torch.int64, device=device)
     N.check(L.pgx_result_device_groups(r, C.byref(n), C.c_void_p(recs.data_ptr())))
     mine = exchange_group_records(recs[:n.value], world)
     st = (C.c_int64 * 4)()

@@ -142,6 +142,7 @@ EXPORTS = {
     "pgx_execute_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int32, C.c_void_p, C.POINTER(C.c_void_p), C.c_int32,
                                     C.POINTER(LeafBinding), C.POINTER(ExecOpts), C.POINTER(C.c_void_p)]),
     "pgx_result_device_groups": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64), C.c_void_p]),
+    "pgx_result_record_words": (C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     "pgx_result_merge_groups": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
                                           C.POINTER(C.c_void_p)]),
     "pgx_copy_to_host": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),

@@ -99,13 +99,15 @@ def _lexsort(d: np.ndarray, order: Sequence[int]) -> np.ndarray:
 
 def build(dim_ids: np.ndarray, metrics: np.ndarray, cards: Sequence[int], max_leaf_records: int = DEFAULT_MAX_LEAF_RECORDS,
           split_order: Optional[Sequence[int]] = None, skip: Optional[Sequence[int]] = None,
-          skip_cardinality: int = DEFAULT_SKIP_MATERIALIZATION_CARDINALITY):
+          skip_cardinality: int = DEFAULT_SKIP_MATERIALIZATION_CARDINALITY, dense_limit: int = 1 << 22):
     """dim_ids: (N, D) int dictIds (no star values); metrics: (N, M) int64.
     Returns (tree_root, all_dims (T, D) with ALL=-1 for star, all_metrics (T, M), split_order, num_raw, skip).
 
     skipMaterializationForDimensions (OffHeapStarTreeBuilder.build :308-322): by default every dimension whose
     cardinality exceeds the threshold (computeDefaultDimensionsToSkipMaterialization :557-565); they leave the default
-    split order, and the star-node rows hold ALL for them (uniqueCombinations :738-745)."""
+    split order, and the star-node rows hold ALL for them (uniqueCombinations :738-745).
+    dense_limit: a range's distinct combinations are counted in a dense table when their key span is at most
+    max(dense_limit, 2 x rows) (0: always sort; the output is the same either way)."""
     n, ndim = dim_ids.shape
     skip = set(skip) if skip else {k for k in range(ndim) if cards[k] > skip_cardinality}
     if split_order is None:
@@ -137,16 +139,31 @@ def build(dim_ids: np.ndarray, metrics: np.ndarray, cards: Sequence[int], max_le
     tab = _Table(np.ascontiguousarray(dim_ids[perm]).astype(np.int32), np.ascontiguousarray(metrics[perm]).astype(np.int64))
     root = Node(ALL, ALL, 0)
 
-    def unique_combinations(a, b, split_dim):
+    def unique_combinations(a, b, split_dim, dense_limit=dense_limit):
         d, m = tab.rows(a, b)
         d = d.copy()
         d[:, split_dim] = ALL
         for k in skip:
             d[:, k] = ALL
-        o, key = order_rows(d)
-        d, m = d[o], m[o]
         if len(d) == 0:
             return d, m
+        if span < (1 << 62):
+            # the distinct sort keys of the range span few values (the prefix dims are constant): count them in a dense
+            # table -- the same combinations in the same ascending-key order as sort + reduceat, in O(rows + span)
+            key = sort_key(d)
+            lo = int(key.min())
+            width = int(key.max()) - lo + 1
+            mabs = int(np.abs(m).max(initial=0))
+            if dense_limit > 0 and width <= max(dense_limit, 2 * len(d)) and mabs * len(d) < (1 << 53):
+                off = key - lo
+                rep = np.empty(width, dtype=np.int64)
+                rep[off] = np.arange(len(d))  # any row of a key: its dims are the combination
+                present = np.flatnonzero(np.bincount(off, minlength=width))
+                sums = np.stack([np.bincount(off, weights=m[:, j], minlength=width)[present]
+                                 for j in range(m.shape[1])], axis=1) if m.shape[1] else np.zeros((len(present), 0))
+                return d[rep[present]], np.rint(sums).astype(np.int64)
+        o, key = order_rows(d)
+        d, m = d[o], m[o]
         brk = np.ones(len(d), dtype=bool)
         brk[1:] = (key[1:] != key[:-1]) if key is not None else np.any(d[1:] != d[:-1], axis=1)
         starts = np.nonzero(brk)[0]
@@ -254,7 +271,7 @@ def parse(buf: bytes):
 def make_star_tree_segment(name: str, dims: Dict[str, np.ndarray], metrics: Dict[str, np.ndarray],
                            max_leaf_records: int = DEFAULT_MAX_LEAF_RECORDS, inverted: Sequence[str] = (),
                            skip_materialization: Optional[Sequence[str]] = None,
-                           skip_cardinality: int = DEFAULT_SKIP_MATERIALIZATION_CARDINALITY):
+                           skip_cardinality: int = DEFAULT_SKIP_MATERIALIZATION_CARDINALITY, dense_limit: int = 1 << 22):
     """Build a v1 star-tree segment from raw INT dimension and metric values (SegmentIndexCreationDriverImpl.buildStarTree,
     :193-289): docs = raw docs in star-tree order, then the aggregated docs; star dimension values are the INT default
     null (Integer.MIN_VALUE), which therefore sits in every dimension dictionary."""
@@ -273,7 +290,7 @@ def make_star_tree_segment(name: str, dims: Dict[str, np.ndarray], metrics: Dict
     mets = np.stack([np.asarray(metrics[k], dtype=np.int64) for k in mnames], axis=1)
     skip_idx = [dnames.index(k) for k in skip_materialization] if skip_materialization else None
     root, all_d, all_m, order, nraw, skipped = build(dim_ids, mets, cards, max_leaf_records, skip=skip_idx,
-                                                     skip_cardinality=skip_cardinality)
+                                                     skip_cardinality=skip_cardinality, dense_limit=dense_limit)
     total = len(all_d)
     cols = []
     for i, k in enumerate(dnames):

@@ -146,6 +146,28 @@ C4_TEST_ROWS = 10_000_000
 C4_QUERY = "SELECT SUM(m1), SUM(m2), SUM(m3) FROM T WHERE d2 = 3 AND d4 IN (1, 2, 3) GROUP BY d1 TOP 10"
 
 
+def c4_raw_rows(rows: int, seed: int = 4):
+    """C4's raw rows: every dimension uniform over its cardinality (independently), metrics uniform in [0, 2^16).
+    The rows come out already in the builder's sort order (split order = cardinality descending: d6 .. d1): the
+    combined dimension key is drawn as the order statistics of `rows` uniform draws (cumulative exponential gaps), so
+    the multiset of rows is distributed exactly as independent draws, and the builder's initial sort of 100M rows is
+    a linear pass over sorted input."""
+    rng = np.random.default_rng(seed)
+    span = 1
+    for c in C4_CARDS:
+        span *= c
+    gaps = rng.exponential(1.0, rows + 1)
+    u = np.cumsum(gaps)
+    key = np.minimum((u[:rows] * (span / u[rows])).astype(np.int64), span - 1)
+    del gaps, u
+    dims = {}
+    for i, c in enumerate(C4_CARDS):  # d1 (the least significant digit of the sort order) first
+        dims["d%d" % (i + 1)] = (key % c).astype(np.int32)
+        key //= c
+    mets = {"m%d" % (i + 1): rng.integers(0, 1 << 16, rows).astype(np.int32) for i in range(3)}
+    return dims, mets
+
+
 class StarTreeSegments:
     """One C4 star-tree segment staged from host bytes (synthetic, seed 4)."""
 
@@ -156,9 +178,7 @@ class StarTreeSegments:
         import time
         self.rows = rows or C4_ROWS
         t0 = time.time()
-        rng = np.random.default_rng(seed)
-        dims = {"d%d" % (i + 1): rng.integers(0, c, self.rows) for i, c in enumerate(C4_CARDS)}
-        mets = {"m%d" % (i + 1): rng.integers(0, 1 << 16, self.rows) for i in range(3)}
+        dims, mets = c4_raw_rows(self.rows, seed)
         print("[c4] building the star tree over %d raw rows" % self.rows, file=sys.stderr, flush=True)
         self.seg_data = ST.make_star_tree_segment("c4_0", dims, mets, max_leaf_records=ST.DEFAULT_MAX_LEAF_RECORDS)
         del dims, mets

@@ -36,6 +36,14 @@ def test_avgmv_value_count_plane():
     assert E.agg_slices(pql.compile("SELECT %s FROM t" % aggs)) == [[0, 1, 2, 3], [4]]
 
 
+def test_avgmv_beside_an_extended_function():
+    # an extended slice keeps AVGMV in its base query, whose value-count plane is a slot too:
+    # DISTINCTCOUNT + 7 x AVGMV needs 1 (base COUNT(*)) + 0 + 7 x 2 slots, so no slice may hold more than 3 AVGMV
+    aggs = ", ".join(["DISTINCTCOUNT(d)"] + ["AVGMV(v)"] * 7)
+    sl = E.agg_slices(pql.compile("SELECT %s FROM t GROUP BY g" % aggs))
+    assert sl == [[0, 1, 2, 3], [4, 5, 6, 7]]  # 1 + 0 + 3 x 2 = 7, then 4 x 2 = 8
+
+
 def _value(a, key):
     return (len(a["fn"]) * 1000 + sum(map(ord, a["column"]))) * (1 + sum(map(ord, key)))
 
@@ -87,18 +95,22 @@ def test_slices_no_group_selected():
 
 
 class _StarOp(_FakeOp):
-    """Slices whose functions all qualify for the star-tree scan fewer docs unless useStarTree=false."""
+    """Slices whose functions all qualify for the star-tree scan fewer docs unless useStarTree=false (with
+    `empty`, a filter matching nothing: both scan 0 docs, but only the raw docs count entries scanned in filter)."""
     runs = []
+    empty = False
 
     def next_block(self):
         if len(E.agg_slices(self.request)) > 1:
             return E._GpuOperator.next_block(self)
         star = str((self.request.get("debug_options") or {}).get("useStarTree", "true")) != "false"
         qualifies = all(a["fn"] == "sum" for a in self.request["aggregations"])
-        docs = 10 if star and qualifies else 100
-        _StarOp.runs.append(docs)
+        on_tree = star and qualifies
+        docs = 0 if _StarOp.empty else (10 if on_tree else 100)
+        entries = 0 if on_tree else 1000
+        _StarOp.runs.append(docs if not _StarOp.empty else entries)
         return E.IntermediateResultsBlock(aggregation_result=[docs] * len(self.request["aggregations"]),
-                                          stats=E.ExecutionStatistics(docs, 0, 0, 1000))
+                                          stats=E.ExecutionStatistics(docs, entries, 0, 1000))
 
 
 def test_slices_rerun_on_raw_docs_when_star_tree_disagrees():
@@ -114,3 +126,17 @@ def test_slices_rerun_on_raw_docs_when_star_tree_disagrees():
     q = pql.compile("SELECT %s FROM t" % ", ".join(["SUM(m)"] * 10))
     blk = _StarOp(None, q, [], combine=True).next_block()
     assert _StarOp.runs == [10, 10] and blk.stats.num_docs_scanned == 10
+
+
+def test_slices_rerun_when_only_entries_scanned_differ():
+    # a filter that matches nothing scans 0 docs on the tree and on the raw docs; the entries scanned in
+    # filter still tell the star-tree slice from the raw one, and the request re-runs on the raw docs
+    aggs = ", ".join(["SUM(m)"] * 8 + ["MIN(m)"])
+    q = pql.compile("SELECT %s FROM t WHERE d = 3" % aggs)
+    _StarOp.runs, _StarOp.empty = [], True
+    try:
+        blk = _StarOp(None, q, [], combine=True).next_block()
+    finally:
+        _StarOp.empty = False
+    assert _StarOp.runs == [0, 1000, 1000, 1000]
+    assert blk.stats.num_entries_scanned_in_filter == 1000

@@ -12,7 +12,8 @@ tests run exactly that:
   over all segments: the vectorised filter `(f1 IN ... OR f2 = 7) AND f3 <> 3` and per-gk sums over the
   regenerated (bit-identical) dictIds, MCombineGroupByOperator.java:139-233.
 * `test_c5_full_size_shard_linearity`: the bench's own 4,096 x 2M-row result equals the merge of 8 disjoint shard
-  results (combine linearity: every function is a sum or count here), and two of those shards equal the oracle.
+  results (combine linearity: every function is a sum or count here), and the first shard (512 segments) equals the
+  oracle.
 """
 import concurrent.futures as CF
 import ctypes as C
@@ -149,7 +150,7 @@ def test_c5_full_size_shard_linearity(ctx):
         for k, v in fmap.items():
             assert v[0] == acc[k], k  # integer sums below 2^53: exact in any order
         assert list(ast) == fst
-        for ids, m, st in shard_maps[:2]:
+        for ids, m, st in shard_maps[:1]:  # one shard (512 segments) against the oracle; the rest by linearity
             sums, counts = _oracle(ids, rows, req)
             _check(m, st, sums, counts, len(ids), rows)
         q.close()

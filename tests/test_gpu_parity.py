@@ -117,7 +117,8 @@ def test_query_executor_two_segments(ctx):
 def _rand_segment(rng, n, cards, name, sorted_col=None, dtypes=None):
     raw = {}
     for c, card in cards.items():
-        dom = np.sort(rng.choice(np.arange(-(1 << 30), 1 << 30, dtype=np.int64), size=card, replace=False))
+        # distinct values in [-2^30, 2^30), drawn without materialising the 2^31-value population
+        dom = np.sort(rng.choice(1 << 31, size=card, replace=False).astype(np.int64) - (1 << 30))
         ids = rng.integers(0, card, size=n)
         if n >= card:
             ids[:card] = np.arange(card)

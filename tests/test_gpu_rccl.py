@@ -45,6 +45,9 @@ def _free_port():
 
 def _worker(port, q):
     import ctypes as C
+    import sys
+    import time
+    from datetime import timedelta
 
     import torch
     import torch.distributed as dist
@@ -53,19 +56,30 @@ def _worker(port, q):
     from pinot_amd import multigpu, pql
     from pinot_amd import native as N
     from tests import helpers as H
+    t0 = time.time()
+    phases = {}
+
+    def phase(name):  # each phase's end time, on stderr as it happens: a slow bring-up names itself
+        phases[name] = round(time.time() - t0, 3)
+        print("[rccl child] %s at %.2f s" % (name, phases[name]), file=sys.stderr, flush=True)
+
+    phase("imports")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev, timeout=timedelta(seconds=60))
+    phase("init_process_group")
     try:
-        out = {"backend": dist.get_backend()}
+        out = {"backend": dist.get_backend(), "phases": phases}
         L = N.lib()
         ctx = E.Context(0)
         segs = [E.IndexSegment(ctx, H.build_pair("rc%d" % i, _raw(i))[0]) for i in range(3)]
+        phase("segments")
         arr = (C.c_void_p * len(segs))(*[s.handle.value for s in segs])
         # byte-tensor all-gather over RCCL (the differing-dictionary branch of union_key_domains)
         payload = b"INT\0" + np.arange(17, dtype=np.int64).tobytes()
         out["gather"] = multigpu._gather_bytes(payload, "cuda:0") == [payload]
+        phase("all_gather")
         # dense: key domains (fingerprint all-reduces + the cache's all-gather), planes all-reduced on the device
         qd = E._Query(ctx, pql.compile(DENSE_QUERY))
         multigpu.union_key_domains(qd, segs, device="cuda:0")
@@ -94,6 +108,7 @@ def _worker(port, q):
         blk = E.decode_result(qd, rd, segs)
         L.pgx_result_release(rd)
         out["dense"] = (blk.get_aggregation_group_by_result().as_map(), list(s4))
+        phase("dense")
         # aggregation-only: per-function partials all-reduced
         qa = E._Query(ctx, pql.compile(AGG_QUERY))
         r = qa.execute(segs)
@@ -104,6 +119,7 @@ def _worker(port, q):
             vals.append((v.value, c.value))
         L.pgx_result_release(r)
         out["agg"] = multigpu.merge_aggregation(qa.fns, vals, device="cuda:0")
+        phase("aggregation")
         # sparse: device-resident groups, all_to_all_single, device merge + trim, kept groups gathered
         qs = E._Query(ctx, pql.compile(SPARSE_QUERY))
         multigpu.union_key_domains(qs, segs, device="cuda:0")
@@ -113,6 +129,7 @@ def _worker(port, q):
         maps, total, stats = multigpu.device_sparse_merge(ctx, qs, r, segs, "cuda:0")
         L.pgx_result_release(r)
         out["sparse"] = (maps, total, stats)
+        phase("sparse")
         ctx.close()
         q.put(out)
     except Exception as e:  # report instead of hanging the parent
@@ -135,9 +152,15 @@ def test_rccl_merges_match_oracle_combine():
     q = mpc.Queue()
     p = mpc.Process(target=_worker, args=(_free_port(), q))
     p.start()
-    res = q.get(timeout=240)
-    p.join(timeout=60)
+    try:
+        res = q.get(timeout=120)  # the child prints each phase's time on stderr: a hang names its phase
+        p.join(timeout=30)
+    finally:
+        if p.is_alive():
+            p.kill()
+            p.join(timeout=10)
     assert isinstance(res, dict), res
+    print("rccl child phases (s):", res["phases"])
     assert p.exitcode == 0
     assert res["backend"] == "nccl" and res["gather"] and res["resident"]
     osegs = [H.build_pair("orc%d" % i, _raw(i))[1] for i in range(3)]

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
     missing = [s for s in declared_symbols() if not hasattr(lib, s)]
     assert not missing, missing
     lib.pgx_abi_version.restype = ctypes.c_int32
-    assert lib.pgx_abi_version() == 7
+    assert lib.pgx_abi_version() == 8
 
 
 def test_binding_table_matches_header():

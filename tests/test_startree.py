@@ -132,3 +132,17 @@ def test_skip_materialization_dimension():
         raw_docs = np.nonzero(O.filter_mask_vectorized(os_, q.get("filter")))[0]
         docs = O.star_tree_docs(os_, seg.star_tree, q, seg.total_raw_docs)
         assert O.sum_by_group(os_, docs, METRICS, []) == O.sum_by_group(os_, raw_docs, METRICS, [])
+
+
+@pytest.mark.parametrize("leaf", [500, 60])
+def test_dense_combination_count_equals_sort_path(leaf):
+    """The builder's dense-table unique combinations (a range whose key span is small) give the segment the sort +
+    reduceat path gives: the same OFF_HEAP tree bytes, and every column's dictionary and dictIds."""
+    dims, mets = make_raw(20000)
+    a = ST.make_star_tree_segment("st", dims, mets, max_leaf_records=leaf)
+    b = ST.make_star_tree_segment("st", dims, mets, max_leaf_records=leaf, dense_limit=0)
+    assert a.star_tree == b.star_tree and a.total_docs == b.total_docs
+    for name in a.columns:
+        assert np.array_equal(np.asarray(a.columns[name].dictionary_values()),
+                              np.asarray(b.columns[name].dictionary_values()))
+        assert np.array_equal(a.columns[name].dict_ids(), b.columns[name].dict_ids())
