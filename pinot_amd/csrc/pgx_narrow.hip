@@ -234,23 +234,36 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
 // (IMG 3: value - vbase; no image, so the LDS holds only the tables and more wavefronts fit a CU).
 // ctr: [0] groups appended, [3] overflow (a table filled up, or more groups than ocap).
 // ---------------------------------------------------------------------------------------------------------------------
-constexpr int kNAThreads = 512;
-constexpr int kNAWaves = kNAThreads / 64;
 constexpr int kNAWays = 4;
 constexpr int kNABuckets = 48;
 constexpr int kNASlots = kNABuckets * kNAWays;  // 192
 constexpr int kNAImgWords = 64 + 65536 / 2;
+// IMG 4 (packed frame of reference): 1024-thread workgroups, so 16 wavefront tables (60 KiB) sit beside the image
+constexpr int kNAImg4Words = (160 * 1024 - 16 * kNASlots * 20 - 1024) / 4;
 constexpr uint32_t kNAEmpty = 0xFFFFFFFFu;
+template <int IMG>
+constexpr int na_threads() {
+  return IMG == 4 ? 1024 : 512;
+}
 
 __device__ __forceinline__ unsigned long long oplane_sum_key(int64_t sum) {  // trim_key(SUM)
   return static_cast<unsigned long long>(sum) ^ 0x8000000000000000ull;
 }
 
+// IMG 4: img_sh packs the block shift (bits 0-4), the offset width b (bits 5-9) and the number of block bases (bits
+// 10..): the image is nblk u32 bases, then the b-bit offsets packed LSB-first into dwords (plus one pad dword).
 template <int IMG>
 __device__ __forceinline__ uint32_t na_img(const uint32_t* simg, int img_sh, uint32_t d) {
   if (IMG == 1) return simg[d];
   if (IMG == 2) return simg[d >> img_sh] + static_cast<uint32_t>(reinterpret_cast<const uint16_t*>(simg + 64)[d]);
   if (IMG == 3) return d;
+  if (IMG == 4) {
+    const int sh = img_sh & 31, b = (img_sh >> 5) & 31, nb = img_sh >> 10;
+    const uint32_t bp = d * static_cast<uint32_t>(b);
+    const uint32_t* pk = simg + nb + (bp >> 5);
+    const uint32_t off = __builtin_amdgcn_alignbit(pk[1], pk[0], bp & 31u) & ((1u << b) - 1u);
+    return simg[d >> sh] + off;
+  }
   return 0u;
 }
 
@@ -259,14 +272,18 @@ __device__ __forceinline__ int na_way(const na_u32x4 k, uint32_t key) {
 }
 
 template <int IMG, bool SUM, bool MN, bool MX>
-__global__ void __launch_bounds__(kNAThreads) __attribute__((amdgpu_waves_per_eu(IMG == 3 ? 4 : 1))) pgx_narrow_aggregate(
+__global__ void __launch_bounds__(na_threads<IMG>()) __attribute__((amdgpu_waves_per_eu(IMG >= 3 ? 4 : 1)))
+pgx_narrow_aggregate(
     const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
     uint64_t kmask, uint64_t ic1, int ms, int64_t vbase, const uint32_t* __restrict__ img, int img_words,
     int img_sh, const int64_t* __restrict__ vdict, int cshift, uint64_t* __restrict__ okey,
     uint64_t* __restrict__ oplane, int64_t ocap, unsigned long long* __restrict__ ctr,
     unsigned long long* __restrict__ prange) {
-  constexpr bool LIMG = IMG == 1 || IMG == 2;  // an image in LDS
-  __shared__ __attribute__((aligned(16))) uint32_t simg[LIMG ? kNAImgWords : 1];
+  constexpr int kNAThreads = na_threads<IMG>();
+  constexpr int kNAWaves = kNAThreads / 64;
+  constexpr bool LIMG = IMG == 1 || IMG == 2 || IMG == 4;  // an image in LDS
+  constexpr bool BIG = IMG == 1 || IMG == 2;               // 512 threads, two waves per SIMD: wider batches
+  __shared__ __attribute__((aligned(16))) uint32_t simg[LIMG ? (IMG == 4 ? kNAImg4Words : kNAImgWords) : 1];
   __shared__ __attribute__((aligned(16))) uint32_t tkey[kNAWaves * kNASlots];
   __shared__ unsigned long long tsc[kNAWaves * kNASlots];
   __shared__ uint32_t tmn[MN ? kNAWaves * kNASlots : 1], tmx[MX ? kNAWaves * kNASlots : 1];
@@ -409,19 +426,20 @@ __global__ void __launch_bounds__(kNAThreads) __attribute__((amdgpu_waves_per_eu
     const int np = a.p + nw;
     return Pos{np, 0u, count(np)};
   };
-  // (without an image: two batches and groups of 4 records, so 128 VGPRs hold a wavefront and a SIMD runs four)
-  constexpr int HB = LIMG ? 8 : 4;  // records resolved together
-  uint32_t b0[16], b1[16], b2[LIMG ? 16 : 1];
+  // (four waves per SIMD -- no image, or the packed image of 1024-thread workgroups: two batches and groups of 4
+  // records, so 128 VGPRs hold a wavefront)
+  constexpr int HB = BIG ? 8 : 4;  // records resolved together
+  uint32_t b0[16], b1[16], b2[BIG ? 16 : 1];
   Pos c{static_cast<int>(blockIdx.x) * kNAWaves + wave, 0u, 0u};
   c.n = count(c.p);
   if (c.p < nparts) load(c.p, c.i0, c.n, b0);
   Pos d = advance(c);
-  if constexpr (LIMG) {
+  if constexpr (BIG) {
     if (d.p < nparts) load(d.p, d.i0, d.n, b1);
   }
   while (c.p < nparts) {
     const Pos e = advance(d);
-    if constexpr (LIMG) {
+    if constexpr (BIG) {
       if (e.p < nparts) load(e.p, e.i0, e.n, b2);
     } else {
       if (d.p < nparts) load(d.p, d.i0, d.n, b1);
@@ -492,7 +510,7 @@ __global__ void __launch_bounds__(kNAThreads) __attribute__((amdgpu_waves_per_eu
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       b0[j] = b1[j];
-      if constexpr (LIMG) b1[j] = b2[j];
+      if constexpr (BIG) b1[j] = b2[j];
     }
     c = d;
     d = e;
@@ -542,15 +560,17 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
                                                   unsigned long long* prange, int grid, hipStream_t stream) {
   if (nparts <= 0) return hipSuccess;
   if (rb2 < 0 || rb2 > 31 || keybits < 1 || keybits > 64 || cap2 < 4 || (cap2 & 3) || cshift < 1 || cshift > 63 ||
-      grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 3 ||
-      ((img_kind == 1 || img_kind == 2) && (!img || img_words < 1 || img_words > pgx::kNAImgWords)) || (need_sum && !img_kind) ||
+      grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 4 ||
+      ((img_kind == 1 || img_kind == 2) && (!img || img_words < 1 || img_words > pgx::kNAImgWords)) ||
+      (img_kind == 4 && (!img || img_words < 1 || img_words > pgx::kNAImg4Words)) || (need_sum && !img_kind) ||
       ((need_min || need_max) && !img_kind && !vdict))
     return hipErrorInvalidValue;
   const pgx::NarrowMix m = pgx::narrow_mix(keybits);
   const int sel = img_kind * 8 + (need_sum ? 4 : 0) + (need_min ? 2 : 0) + (need_max ? 1 : 0);
 #define PGX_NA_CASE(C, I, A, B, D)                                                                                   \
   case C:                                                                                                            \
-    hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D>), dim3(grid), dim3(pgx::kNAThreads), 0, stream, in, cnt2, \
+    hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D>), dim3(grid), dim3(pgx::na_threads<I>()), 0, stream, in, \
+                       cnt2,                                                                                          \
                        cap2, nparts, rb2, m.mask, m.ic1, m.s, vbase, img, img_words, img_sh, vdict, cshift,   \
                        okey, oplane, ocap, ctr, prange);                                                             \
     break;
@@ -568,6 +588,7 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
     PGX_NA_CASES(1)
     PGX_NA_CASES(2)
     PGX_NA_CASES(3)
+    PGX_NA_CASES(4)
     default:
       return hipErrorInvalidValue;
   }
