@@ -45,7 +45,7 @@ build/pgx_narrow.o: $(CSRC)/pgx_narrow.hip $(CSRC)/pgx_internal.h $(CSRC)/pgx_ji
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 pinot_amd/libpgx.so: build/pgx_host.o build/pgx_part.o build/pgx_multi.o build/pgx_realtime.o build/pgx_fixtures.o build/pgx_stage.o build/pgx_mv.o build/pgx_plan_cache.o build/pgx_plan.o build/pgx_jit.o build/pgx_kernels.o build/pgx_trim.o build/pgx_stats.o build/pgx_merge.o build/pgx_narrow.o
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC $^ -o $@ -L/opt/rocm/lib -lhiprtc -Wl,-rpath,/opt/rocm/lib -Wl,--no-undefined
 
 clean:
 	rm -rf build pinot_amd/libpgx.so

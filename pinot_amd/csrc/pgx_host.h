@@ -92,7 +92,9 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
                                                   const uint32_t* img, int img_words, int img_sh, const int64_t* vdict,
                                                   int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
                                                   uint64_t* oplane, int64_t ocap, unsigned long long* ctr,
-                                                  unsigned long long* prange, int grid, hipStream_t stream);
+                                                  unsigned long long* prange, int grid, uint64_t* scratch,
+                                                  int64_t scratch_words, hipStream_t stream);
+extern "C" int64_t pgx_narrow_scratch_words(int nparts, int img_kind, int grid);
 extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
                                      int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
                                      uint16_t* pstate, int T, unsigned long long* stats, hipStream_t stream);
@@ -490,7 +492,12 @@ struct SharedDict {
   int img_kind = 0, img_sh = 0, img_words = 0;
   int64_t vbase = 0;
   uint64_t vrange = 0;
+  // the narrow aggregation's packed image (pgx_narrow.hip IMG 4), built on first use: pk_state 0 untried, 1 built,
+  // -1 does not fit (guarded by the context's dict_mu)
+  DevBuf pk_img;
+  int pk_state = 0, pk_sh = 0, pk_words = 0;
 };
+constexpr int kNarrowImg4Words = (160 * 1024 - 16 * 192 * 20 - 1024) / 4;  // pgx_narrow.hip kNAImg4Words
 
 // =================================================================================================
 // Segments
@@ -976,6 +983,8 @@ struct NarrowBuffers {
   int64_t nwg = 0, cap1 = 0, cap2 = 0, ocap = 0, nparts = 0;
   DevBuf lo1, hi1, cnt1, rec2, cnt2, okey, oplane, ctr;  // ctr: ocount | overflow scan | split | aggregation
   DevBuf prange;  // trim-key ranges: [kind] smallest, [4 + kind] largest (pgx_trim.hip)
+  DevBuf agg_scratch;  // the aggregation's per-wavefront output regions (pgx_narrow_scratch_words)
+  int64_t agg_scratch_words = 0;
 };
 
 inline unsigned long long* devp(const DevBuf& b) { return b.as<unsigned long long>(); }
@@ -983,6 +992,7 @@ inline unsigned long long* devp(const DevBuf& b) { return b.as<unsigned long lon
 
 namespace pgxh {
 // ---- pgx_host.cpp: planning and execution pieces the partitioned runtime drives --------------------------------
+bool packed_value_image(pgx_ctx* ctx, SharedDict& sd, const std::vector<int64_t>& ivals);  // pgx_stage.cpp
 void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, uint64_t dense_out_bytes);
 void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table = true, bool outs_only = false);
 void launch_scan(ExecPlan& P, hipStream_t st);

@@ -502,24 +502,55 @@ __global__ void pgx_init_planes(unsigned long long* table, uint64_t slots, int n
     for (uint64_t i = t0; i < slots; i += step) key_state[i] = 0u;
 }
 
+// Exclusive prefix of `mine` over the workgroup's 256 threads and ONE device atomic per call: *base = the counter's
+// old value (visible to every thread after the call).  Every thread of the workgroup must call it.
+__device__ __forceinline__ unsigned int block_reserve(unsigned int* scan, unsigned long long* base, unsigned int mine,
+                                                     unsigned long long* counter) {
+  const int tid = threadIdx.x;
+  scan[tid] = mine;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {  // Hillis-Steele inclusive scan
+    const unsigned int y = tid >= d ? scan[tid - d] : 0u;
+    __syncthreads();
+    scan[tid] += y;
+    __syncthreads();
+  }
+  if (tid == 255) *base = scan[255] ? atomicAdd(counter, static_cast<unsigned long long>(scan[255])) : 0ull;
+  __syncthreads();
+  return scan[tid] - mine;
+}
+
 // Emit occupied slots: out_slot[i] = slot index, out_planes[p*cap_out + i] = plane value.
-__global__ void pgx_compact(const unsigned long long* table, uint64_t slots, int num_planes,
-                            unsigned long long* counter, int64_t* out_slot, unsigned long long* out_planes,
-                            uint64_t cap_out) {
-  // one counter reservation per wavefront (a device atomic per occupied slot serialises on the counter: 16.7M groups
-  // ~ 24 ms), lanes in slot order within the wavefront
-  const int lane = threadIdx.x & 63;
-  for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); b < slots; b += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t s = b + lane;
-    const bool live = s < slots && table[s] != 0;
-    const unsigned long long m = __ballot(live);
-    if (!m) continue;
-    unsigned long long base = 0;
-    if (lane == 0) base = atomicAdd(counter, static_cast<unsigned long long>(__popcll(m)));
-    const unsigned long long i = __shfl(base, 0, 64) + __popcll(m & ((1ull << lane) - 1ull));
-    if (!live || i >= cap_out) continue;
-    out_slot[i] = static_cast<int64_t>(s);
-    for (int p = 0; p < num_planes; ++p) out_planes[p * cap_out + i] = table[p * slots + s];
+// One counter reservation per workgroup tile of 256 x 16 slots (block_reserve): a device atomic per occupied slot
+// serialises on the counter (16.7M groups ~ 24 ms), and even one per wavefront costs ~11 ns each at one L2 address.
+__global__ void __launch_bounds__(256) pgx_compact(const unsigned long long* table, uint64_t slots, int num_planes,
+                                                   unsigned long long* counter, int64_t* out_slot,
+                                                   unsigned long long* out_planes, uint64_t cap_out) {
+  __shared__ unsigned int scan[256];
+  __shared__ unsigned long long base;
+  constexpr int K = 16;
+  for (uint64_t t0 = blockIdx.x * (uint64_t)(256 * K); t0 < slots; t0 += (uint64_t)gridDim.x * 256 * K) {
+    unsigned int live = 0, mine = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t s = t0 + k * 256 + threadIdx.x;
+      const bool l = s < slots && table[s] != 0;
+      live |= (l ? 1u : 0u) << k;
+      mine += l;
+    }
+    const unsigned int excl = block_reserve(scan, &base, mine, counter);
+    unsigned long long i = base + excl;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (!((live >> k) & 1u)) continue;
+      const uint64_t s = t0 + k * 256 + threadIdx.x;
+      if (i < cap_out) {
+        out_slot[i] = static_cast<int64_t>(s);
+        for (int p = 0; p < num_planes; ++p) out_planes[p * cap_out + i] = table[p * slots + s];
+      }
+      ++i;
+    }
+    __syncthreads();  // base / scan are reused by the next tile
   }
 }
 
@@ -2199,7 +2230,7 @@ extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t
 extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
                                          unsigned long long* counter, int64_t* out_slot,
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream) {
-  int grid = static_cast<int>(std::min<uint64_t>((slots + 255) / 256, 8192));
+  int grid = static_cast<int>(std::min<uint64_t>((slots + 4095) / 4096, 4096));
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(pgx::pgx_compact, dim3(grid), dim3(256), 0, stream, table, slots, num_planes, counter, out_slot,
                      out_planes, cap_out);

@@ -89,21 +89,43 @@ __global__ void __launch_bounds__(256) pgx_group_compact(const unsigned long lon
                                                          int nplanes, uint64_t* __restrict__ okey,
                                                          uint64_t* __restrict__ opl, int64_t ocap,
                                                          unsigned long long* __restrict__ counter) {
-  const int lane = threadIdx.x & 63;
-  for (uint64_t base = blockIdx.x * static_cast<uint64_t>(blockDim.x) + (threadIdx.x & ~63u); base < cap;
-       base += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
-    const uint64_t s = base + static_cast<uint64_t>(lane);
-    const bool live = s < cap && tkey[s] != kMergeEmpty;
-    const unsigned long long bal = __ballot(live);
-    if (!bal) continue;
-    unsigned long long o = 0;
-    if (lane == 0) o = atomicAdd(counter, static_cast<unsigned long long>(__popcll(bal)));
-    o = __shfl(o, 0);
-    if (!live) continue;
-    const unsigned long long j = o + __popcll(bal & ((1ull << lane) - 1ull));
-    if (j >= static_cast<unsigned long long>(ocap)) continue;  // the host sized ocap from the table; cannot happen
-    okey[j] = tkey[s];
-    for (int p = 0; p < nplanes; ++p) opl[p * ocap + j] = tpl[p * cap + s];
+  // one counter reservation per workgroup tile of 256 x 16 slots: one per wavefront serialised ~500K device atomics on
+  // one address for a 33M-slot merge table (~11 ns each)
+  __shared__ unsigned int scan[256];
+  __shared__ unsigned long long base;
+  constexpr int K = 16;
+  const int tid = threadIdx.x;
+  for (uint64_t t0 = blockIdx.x * static_cast<uint64_t>(256 * K); t0 < cap; t0 += static_cast<uint64_t>(gridDim.x) * 256 * K) {
+    unsigned int live = 0, mine = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint64_t s = t0 + k * 256 + tid;
+      const bool l = s < cap && tkey[s] != kMergeEmpty;
+      live |= (l ? 1u : 0u) << k;
+      mine += l;
+    }
+    scan[tid] = mine;
+    __syncthreads();
+    for (int d = 1; d < 256; d <<= 1) {
+      const unsigned int y = tid >= d ? scan[tid - d] : 0u;
+      __syncthreads();
+      scan[tid] += y;
+      __syncthreads();
+    }
+    if (tid == 255) base = scan[255] ? atomicAdd(counter, static_cast<unsigned long long>(scan[255])) : 0ull;
+    __syncthreads();
+    unsigned long long j = base + scan[tid] - mine;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (!((live >> k) & 1u)) continue;
+      const uint64_t s = t0 + k * 256 + tid;
+      if (j < static_cast<unsigned long long>(ocap)) {  // the host sized ocap from the table; cannot run over
+        okey[j] = tkey[s];
+        for (int p = 0; p < nplanes; ++p) opl[p * ocap + j] = tpl[p * cap + s];
+      }
+      ++j;
+    }
+    __syncthreads();  // scan / base are reused by the next tile
   }
 }
 
@@ -254,8 +276,8 @@ extern "C" hipError_t pgx_launch_group_compact(const unsigned long long* tkey, c
                                                unsigned long long* counter, hipStream_t stream) {
   if (cap == 0) return hipSuccess;
   if (nplanes < 1 || nplanes > 32) return hipErrorInvalidValue;
-  const uint64_t g = (cap + 255) / 256;
-  hipLaunchKernelGGL(pgx::pgx_group_compact, dim3(static_cast<unsigned>(g < 65536 ? g : 65536)), dim3(256), 0, stream,
+  const uint64_t g = (cap + 4095) / 4096;
+  hipLaunchKernelGGL(pgx::pgx_group_compact, dim3(static_cast<unsigned>(g < 4096 ? g : 4096)), dim3(256), 0, stream,
                      tkey, tpl, cap, nplanes, okey, opl, ocap, counter);
   return hipGetLastError();
 }

@@ -276,9 +276,9 @@ __global__ void __launch_bounds__(na_threads<IMG>()) __attribute__((amdgpu_waves
 pgx_narrow_aggregate(
     const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
     uint64_t kmask, uint64_t ic1, int ms, int64_t vbase, const uint32_t* __restrict__ img, int img_words,
-    int img_sh, const int64_t* __restrict__ vdict, int cshift, uint64_t* __restrict__ okey,
-    uint64_t* __restrict__ oplane, int64_t ocap, unsigned long long* __restrict__ ctr,
-    unsigned long long* __restrict__ prange) {
+    int img_sh, const int64_t* __restrict__ vdict, int cshift, uint64_t* __restrict__ rkey,
+    uint64_t* __restrict__ rplane, int64_t wcap, int64_t rstride, unsigned long long* __restrict__ wcount,
+    unsigned long long* __restrict__ ctr, unsigned long long* __restrict__ prange) {
   constexpr int kNAThreads = na_threads<IMG>();
   constexpr int kNAWaves = kNAThreads / 64;
   constexpr bool LIMG = IMG == 1 || IMG == 2 || IMG == 4;  // an image in LDS
@@ -305,6 +305,11 @@ pgx_narrow_aggregate(
   uint32_t* N = tmn + (MN ? wave * kNASlots : 0);
   uint32_t* X = tmx + (MX ? wave * kNASlots : 0);
   const uint32_t rmask = rb2 >= 32 ? 0xFFFFFFFFu : (1u << rb2) - 1u;
+  // home bucket of key bits r2 < 2^rb2: (r2 * kNABuckets) >> rb2, as one 32-bit high multiply
+  const int hsh = rb2 >= 1 ? 32 - rb2 : 31;
+  auto home = [&](uint32_t r2) -> uint32_t {
+    return rb2 >= 1 ? __umulhi(r2 << hsh, static_cast<uint32_t>(kNABuckets)) : 0u;
+  };
   const unsigned long long one = 1ull << cshift;
   const unsigned long long smask = one - 1ull;
   const int nw = gridDim.x * kNAWaves;
@@ -342,13 +347,19 @@ pgx_narrow_aggregate(
     }
     return -1;
   };
-  // A finished partition: its groups move to registers (<= 3 slots per lane), the table is cleared, and one lane
-  // reserves the output rows; the rows are written at the NEXT partition's end (flush_end), so the reservation's round
-  // trip to L2 overlaps the next partition's records instead of stalling the wavefront.
+  // A finished partition: its groups move to registers (<= 3 slots per lane) and the table is cleared; the rows are
+  // written at the NEXT partition's end (flush_end), into this wavefront's own region of the scratch output (wcap rows:
+  // its partitions times the table size, so it cannot run over).  No output row is reserved with a device atomic: one
+  // counter for every partition's reservation serialised 2^18 atomics at C3 (~11 ns each at one L2 address, ~2.9 ms);
+  // pgx_narrow_compact packs the regions afterwards.
   constexpr int Q = kNASlots / 64;
   uint32_t fk[Q], fn_[Q], fx[Q], fhas = 0, fexcl = 0;
-  unsigned long long fsc[Q], fbase = 0ull;
+  unsigned long long fbase = 0ull, cursor = 0ull;  // (wave-uniform) rows this wavefront has written
+  unsigned long long fsc[Q];
   int fp = -1;
+  const int64_t gw = static_cast<int64_t>(blockIdx.x) * kNAWaves + wave;
+  uint64_t* const wkey = rkey + gw * wcap;
+  uint64_t* const wpl = rplane + gw * wcap;
   // trim-key ranges of the written groups (pgx_trim.hip trim_key: COUNT, SUM, MIN, MAX), so the trim skips its range
   // pass: [kind] smallest, [4 + kind] largest
   unsigned long long rlo[4] = {~0ull, ~0ull, ~0ull, ~0ull}, rhi[4] = {0ull, 0ull, 0ull, 0ull};
@@ -358,23 +369,22 @@ pgx_narrow_aggregate(
   };
   auto flush_end = [&]() {
     if (fp < 0) return;
-    const unsigned long long base = __shfl(fbase, 0, 64);
-    unsigned long long o = base + fexcl;
+    unsigned long long o = fbase + fexcl;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       if (!((fhas >> q) & 1u)) continue;
-      if (o < static_cast<unsigned long long>(ocap)) {
+      if (o < static_cast<unsigned long long>(wcap)) {
         uint64_t y = (static_cast<uint64_t>(fp) << rb2) | fk[q];
         y ^= y >> ms;
-        okey[o] = (y * ic1) & kmask;
+        wkey[o] = (y * ic1) & kmask;
         const uint64_t c = fsc[q] >> cshift;
-        oplane[o] = c;  // plane 0: doc count; planes 1..3: int64 sum, ordered min, ordered max (pgx_part_aggregate)
-        oplane[ocap + o] = static_cast<uint64_t>(static_cast<int64_t>(fsc[q] & smask) + static_cast<int64_t>(c) * vbase);
+        wpl[o] = c;  // plane 0: doc count; planes 1..3: int64 sum, ordered min, ordered max (pgx_part_aggregate)
+        wpl[rstride + o] = static_cast<uint64_t>(static_cast<int64_t>(fsc[q] & smask) + static_cast<int64_t>(c) * vbase);
         int64_t vlo = 0, vhi = 0;
         if (MN) vlo = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, fn_[q])) : vd[fn_[q]];
         if (MX) vhi = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, fx[q])) : vd[fx[q]];
-        oplane[2 * ocap + o] = static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull;
-        oplane[3 * ocap + o] = static_cast<uint64_t>(vhi) ^ 0x8000000000000000ull;
+        wpl[2 * rstride + o] = static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull;
+        wpl[3 * rstride + o] = static_cast<uint64_t>(vhi) ^ 0x8000000000000000ull;
         note(0, c);
         note(1, oplane_sum_key(static_cast<int64_t>(fsc[q] & smask) + static_cast<int64_t>(c) * vbase));
         note(2, ~(static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull));
@@ -410,8 +420,8 @@ pgx_narrow_aggregate(
     }
     const uint32_t tot = __shfl(incl, 63, 64);
     fexcl = incl - mine;
-    fbase = 0ull;
-    if (lane == 0 && tot) fbase = atomicAdd(ctr, static_cast<unsigned long long>(tot));
+    fbase = cursor;
+    cursor += tot;
     fp = pp;
   };
 
@@ -444,6 +454,7 @@ pgx_narrow_aggregate(
     } else {
       if (d.p < nparts) load(d.p, d.i0, d.n, b1);
     }
+    const bool full = c.i0 + 1024u <= c.n;  // every record of the batch is the partition's
 #pragma unroll
     for (int h = 0; h < 16 / HB; ++h) {  // groups of HB records: home buckets and values read back to back
       na_u32x4 kb[HB];
@@ -453,7 +464,7 @@ pgx_narrow_aggregate(
         const int jj = h * HB + j;
         const uint32_t R = b0[jj];
         const uint32_t r2 = R & rmask;
-        const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2);
+        const uint32_t b = home(r2);
         kb[j] = *reinterpret_cast<const na_u32x4*>(K + b * kNAWays);
         val[j] = SUM ? na_img<IMG>(simg, img_sh, rb2 >= 32 ? 0u : R >> rb2) : 0u;
       }
@@ -462,16 +473,14 @@ pgx_narrow_aggregate(
       for (int j = 0; j < HB; ++j) {
         const int jj = h * HB + j;
         const uint32_t ei = static_cast<uint32_t>((jj >> 2) * 256 + lane * 4 + (jj & 3));
-        if (c.i0 + ei >= c.n) continue;
+        const bool valid = full || c.i0 + ei < c.n;  // (full: a wave-uniform flag, no per-record compare)
         const uint32_t R = b0[jj];
         const uint32_t r2 = R & rmask;
         const uint32_t dd = rb2 >= 32 ? 0u : R >> rb2;
-        const uint32_t b = static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2);
+        const uint32_t b = home(r2);
         const int m = na_way(kb[j], r2);
-        if (m < 0) {
-          miss |= 1u << j;
-          continue;
-        }
+        if (valid && m < 0) miss |= 1u << j;
+        if (!valid || m < 0) continue;
         const int slot = static_cast<int>(b) * kNAWays + m;
         atomicAdd(&S[slot], SUM ? one + val[j] : one);
         if (MN) atomicMin(&N[slot], dd);
@@ -493,7 +502,7 @@ pgx_narrow_aggregate(
           }
         const uint32_t r2 = R & rmask;
         const uint32_t dd = rb2 >= 32 ? 0u : R >> rb2;
-        const int slot = probe(r2, static_cast<uint32_t>((static_cast<uint64_t>(r2) * kNABuckets) >> rb2));
+        const int slot = probe(r2, home(r2));
         if (slot < 0) {
           lost = true;
           continue;
@@ -516,6 +525,7 @@ pgx_narrow_aggregate(
     d = e;
   }
   flush_end();
+  if (lane == 0) wcount[gw] = cursor;
   if (lost) atomicAdd(ctr + 3, 1ull);
   if (prange) {  // wavefront minimum / maximum, then one atomic per wavefront and kind
 #pragma unroll
@@ -535,8 +545,59 @@ pgx_narrow_aggregate(
   }
 }
 
+// The wavefronts' output regions -> one compact group list (okey, oplane[p * ocap + i]).  Workgroup w copies region w to
+// the rows after every earlier region's (an exclusive sum over wcount, recomputed by each workgroup: nw <= 8192 reads);
+// workgroup 0 publishes the total in ctr[0] and counts an overflow of ocap in ctr[3].
+__global__ void __launch_bounds__(256) pgx_narrow_compact(const uint64_t* __restrict__ rkey,
+                                                          const uint64_t* __restrict__ rplane, int64_t wcap,
+                                                          int64_t rstride, const unsigned long long* __restrict__ wcount,
+                                                          int nw, uint64_t* __restrict__ okey,
+                                                          uint64_t* __restrict__ oplane, int64_t ocap,
+                                                          unsigned long long* __restrict__ ctr) {
+  __shared__ unsigned long long part[256];
+  const int w = blockIdx.x, tid = threadIdx.x;
+  const int upto = w == 0 ? nw : w;  // workgroup 0 sums every region (the total), the others the earlier ones
+  unsigned long long s = 0;
+  for (int i = tid; i < upto; i += 256) s += wcount[i];
+  part[tid] = s;
+  __syncthreads();
+  for (int d = 128; d > 0; d >>= 1) {
+    if (tid < d) part[tid] += part[tid + d];
+    __syncthreads();
+  }
+  const unsigned long long sum = part[0];
+  __syncthreads();
+  unsigned long long off = 0;
+  if (w == 0) {
+    if (tid == 0) {
+      ctr[0] = sum;
+      if (sum > static_cast<unsigned long long>(ocap)) atomicAdd(ctr + 3, 1ull);
+    }
+  } else {
+    off = sum;
+  }
+  const unsigned long long n = wcount[w];
+  const uint64_t* sk = rkey + static_cast<int64_t>(w) * wcap;
+  const uint64_t* sp = rplane + static_cast<int64_t>(w) * wcap;
+  for (unsigned long long i = tid; i < n; i += 256) {
+    const unsigned long long o = off + i;
+    if (o >= static_cast<unsigned long long>(ocap)) break;
+    okey[o] = sk[i];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) oplane[p * ocap + static_cast<int64_t>(o)] = sp[p * rstride + static_cast<int64_t>(i)];
+  }
+}
+
 }  // namespace
 }  // namespace pgx
+
+// Scratch of the narrow aggregation (pgx_launch_narrow_aggregate): per wavefront, an output region of its partitions x
+// the table size (key + 4 planes), and its row count.
+extern "C" int64_t pgx_narrow_scratch_words(int nparts, int img_kind, int grid) {
+  const int64_t nw = int64_t(grid) * (img_kind == 4 ? 16 : 8);
+  const int64_t wcap = (int64_t(nparts) + nw - 1) / nw * pgx::kNASlots;
+  return nw * wcap * 5 + nw;
+}
 
 extern "C" hipError_t pgx_launch_narrow_split(const uint32_t* lo, const uint16_t* hi, const unsigned long long* cnt1,
                                               int nbuckets, int nwg, int64_t cap1, int rb1, int k2, uint32_t* out,
@@ -557,8 +618,16 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
                                                   const uint32_t* img, int img_words, int img_sh, const int64_t* vdict,
                                                   int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
                                                   uint64_t* oplane, int64_t ocap, unsigned long long* ctr,
-                                                  unsigned long long* prange, int grid, hipStream_t stream) {
+                                                  unsigned long long* prange, int grid, uint64_t* scratch,
+                                                  int64_t scratch_words, hipStream_t stream) {
   if (nparts <= 0) return hipSuccess;
+  if (!scratch || scratch_words < pgx_narrow_scratch_words(nparts, img_kind, grid)) return hipErrorInvalidValue;
+  const int nw = grid * (img_kind == 4 ? 16 : 8);
+  const int64_t wcap = (int64_t(nparts) + nw - 1) / nw * pgx::kNASlots;
+  const int64_t rstride = int64_t(nw) * wcap;
+  uint64_t* rkey = scratch;
+  uint64_t* rplane = scratch + rstride;
+  unsigned long long* wcount = reinterpret_cast<unsigned long long*>(scratch + 5 * rstride);
   if (rb2 < 0 || rb2 > 31 || keybits < 1 || keybits > 64 || cap2 < 4 || (cap2 & 3) || cshift < 1 || cshift > 63 ||
       grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 4 ||
       ((img_kind == 1 || img_kind == 2) && (!img || img_words < 1 || img_words > pgx::kNAImgWords)) ||
@@ -572,7 +641,7 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
     hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D>), dim3(grid), dim3(pgx::na_threads<I>()), 0, stream, in, \
                        cnt2,                                                                                          \
                        cap2, nparts, rb2, m.mask, m.ic1, m.s, vbase, img, img_words, img_sh, vdict, cshift,   \
-                       okey, oplane, ocap, ctr, prange);                                                             \
+                       rkey, rplane, wcap, rstride, wcount, ctr, prange);                                            \
     break;
 #define PGX_NA_CASES(I)                       \
   PGX_NA_CASE(I * 8 + 0, I, false, false, false) \
@@ -594,5 +663,9 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
   }
 #undef PGX_NA_CASES
 #undef PGX_NA_CASE
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pgx::pgx_narrow_compact, dim3(nw), dim3(256), 0, stream, rkey, rplane, wcap, rstride, wcount, nw,
+                     okey, oplane, ocap, ctr);
   return hipGetLastError();
 }

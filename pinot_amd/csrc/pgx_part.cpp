@@ -208,7 +208,10 @@ bool narrow_size(const ExecPlan& P, NarrowBuffers& NB) {
   NB.cshift = 64 - cb;
   NB.ocap = std::max<int64_t>(1, std::min<int64_t>(P.rec_total, NB.nparts * kNarrowSlots));
   const uint64_t bytes = uint64_t(kNarrow1Bits == 8 ? 256 : (1 << kNarrow1Bits)) * NB.nwg * NB.cap1 * (NB.hib ? 6 : 4) +
-                         uint64_t(NB.nparts) * NB.cap2 * 4 + uint64_t(NB.ocap) * 40;
+                         uint64_t(NB.nparts) * NB.cap2 * 4 + uint64_t(NB.ocap) * 40 +
+                         // the aggregation's per-wavefront output regions (pgx_narrow_scratch_words; wavefront
+                         // rounding bounded by 4096 wavefronts' tables)
+                         (uint64_t(NB.nparts) + 4096) * kNarrowSlots * 40;
   return bytes <= kPartMaxBytes;
 }
 
@@ -243,6 +246,13 @@ void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStrea
   hip_check(hipMemsetAsync(NB.prange.p, 0xFF, 32, st), "range minima");
   hip_check(hipMemsetAsync(static_cast<uint8_t*>(NB.prange.p) + 32, 0, 32, st), "range maxima");
   unsigned long long* ctr = devp(NB.ctr);
+  // an LDS image allows one workgroup per CU (512 threads; 1024 for the packed image), the tables alone four
+  const int agg_grid = ctx->num_cus * (P.narrow_img == 3 ? 4 : 1);
+  const int64_t sw = pgx_narrow_scratch_words(int(NB.nparts), P.narrow_img, agg_grid);
+  if (NB.agg_scratch_words < sw) {
+    NB.agg_scratch = DevBuf(ctx, size_t(sw) * 8);
+    NB.agg_scratch_words = sw;
+  }
   PGX_LAUNCH(st, "pgx_narrow_split",
              pgx_launch_narrow_split(NB.lo1.as<uint32_t>(), NB.hib ? NB.hi1.as<uint16_t>() : nullptr, devp(NB.cnt1),
                                      1 << kNarrow1Bits, int(NB.nwg), NB.cap1, NB.rb1, NB.k2, NB.rec2.as<uint32_t>(),
@@ -253,9 +263,8 @@ void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStrea
                                          NB.rb2, P.part_keybits, P.part_vbase, P.narrow_img, P.narrow_imgp,
                                          P.narrow_img_words, P.narrow_img_sh, P.part_vdict, P.part_sum, P.part_min,
                                          P.part_max, NB.cshift, NB.okey.as<uint64_t>(), NB.oplane.as<uint64_t>(),
-                                         NB.ocap, ctr, devp(NB.prange),
-                                         // an LDS image allows one workgroup per CU; the tables alone, four
-                                         ctx->num_cus * (P.narrow_img == 3 ? 4 : 1), st),
+                                         NB.ocap, ctr, devp(NB.prange), agg_grid, NB.agg_scratch.as<uint64_t>(),
+                                         NB.agg_scratch_words, st),
              "narrow aggregate");
 }
 

@@ -1033,6 +1033,13 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
             P.narrow_img_words = imgk ? c0.img_words : 0;
             P.narrow_img_sh = c0.img_sh;
             P.narrow_vrange = c0.vrange;
+            // the packed image, when it fits beside sixteen tables: 1024-thread aggregation workgroups (IMG 4)
+            if (imgk && c0.shared && packed_value_image(ctx, *c0.shared, c0.ivals)) {
+              imgk = 4;
+              P.narrow_imgp = c0.shared->pk_img.as<uint32_t>();
+              P.narrow_img_words = c0.shared->pk_words;
+              P.narrow_img_sh = c0.shared->pk_sh;
+            }
           }
         } else {
           nok = fits(0, k2);

@@ -70,6 +70,53 @@ void build_value_image(pgx_ctx* ctx, StagedColumn& c, SharedDict& sd) {
   hip_check(hipMemcpy(sd.img.p, img.data(), img.size() * 4, hipMemcpyHostToDevice), "image H2D");
 }
 
+// The narrow aggregation's packed frame-of-reference image (pgx_narrow.hip IMG 4): per block of 2^sh dictIds a u32 base
+// (value - vbase), then every dictId's offset from its block's base in b bits, packed LSB-first into dwords (+ 1 pad
+// dword for the two-dword read of the last offset).  The block shift is the one giving the smallest image; built only
+// if it fits beside sixteen wavefront tables (kNarrowImg4Words), so the aggregation runs 1024-thread workgroups (four
+// wavefronts per SIMD) where the 128 KiB FOR16 image allowed 512.  Exact: b covers every block's span.
+bool packed_value_image(pgx_ctx* ctx, SharedDict& sd, const std::vector<int64_t>& ivals) {
+  std::lock_guard<std::mutex> g(ctx->dict_mu);
+  if (sd.pk_state) return sd.pk_state > 0;
+  sd.pk_state = -1;
+  const int64_t card = int64_t(ivals.size());
+  if (!card || !std::is_sorted(ivals.begin(), ivals.end())) return false;
+  int best_sh = -1, best_b = 0;
+  int64_t best_words = 0;
+  for (int sh = 0; sh <= 16; ++sh) {
+    const int64_t nblk = (card + (int64_t(1) << sh) - 1) >> sh;
+    uint64_t span = 0;
+    for (int64_t b = 0; b < nblk; ++b) {  // sorted: a block's span is its last value minus its first
+      const int64_t lo = ivals[size_t(b << sh)], hi = ivals[size_t(std::min(card, (b + 1) << sh) - 1)];
+      span = std::max<uint64_t>(span, uint64_t(hi) - uint64_t(lo));
+    }
+    int bits = 1;
+    while (bits < 32 && (uint64_t(1) << bits) <= span) ++bits;
+    if (bits > 16) continue;
+    const int64_t words = nblk + (card * bits + 31) / 32 + 1;
+    if (best_sh < 0 || words < best_words) best_sh = sh, best_b = bits, best_words = words;
+  }
+  if (best_sh < 0 || best_words > kNarrowImg4Words) return false;
+  const int64_t nblk = (card + (int64_t(1) << best_sh) - 1) >> best_sh;
+  std::vector<uint32_t> img(size_t(best_words), 0u);
+  for (int64_t b = 0; b < nblk; ++b) img[size_t(b)] = uint32_t(uint64_t(ivals[size_t(b << best_sh)]) - uint64_t(sd.vbase));
+  for (int64_t i = 0; i < card; ++i) {
+    const uint64_t off = uint64_t(ivals[size_t(i)]) - uint64_t(ivals[size_t((i >> best_sh) << best_sh)]);
+    const uint64_t pos = uint64_t(i) * uint64_t(best_b);
+    const size_t w = size_t(nblk + int64_t(pos >> 5));
+    const int o = int(pos & 31);
+    img[w] |= uint32_t(off << o);
+    if (o + best_b > 32) img[w + 1] |= uint32_t(off >> (32 - o));
+  }
+  img.resize((img.size() + 3) & ~size_t(3), 0u);  // whole 16-B chunks
+  sd.pk_img = DevBuf(ctx, img.size() * 4);
+  hip_check(hipMemcpy(sd.pk_img.p, img.data(), img.size() * 4, hipMemcpyHostToDevice), "packed image H2D");
+  sd.pk_sh = best_sh | (best_b << 5) | int(nblk << 10);
+  sd.pk_words = int(best_words);
+  sd.pk_state = 1;
+  return true;
+}
+
 // StarTreeSerDe.writeTreeOffHeapFormat (core/startree/StarTreeSerDe.java:183-328), native (LE) byte order: u64 magic,
 // i32 version, i32 header size, i32 #dims, #dims x {i32 index, i32 len, bytes}, i32 #nodes, #nodes x 7 x i32.
 // Other star-tree formats (the Java-serialised ON_HEAP tree) leave st_ok false: queries then scan the raw docs.
