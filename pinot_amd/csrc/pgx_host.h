@@ -85,7 +85,7 @@ extern "C" hipError_t pgx_launch_pack_remap(uint32_t* out_words, const int32_t* 
                                             int64_t n_rows, int bits, int64_t n_words, hipStream_t stream);
 extern "C" hipError_t pgx_launch_narrow_split(const uint32_t* lo, const uint16_t* hi, const unsigned long long* cnt1,
                                               int nbuckets, int nwg, int64_t cap1, int rb1, int k2, uint32_t* out,
-                                              int64_t cap2, unsigned int* cnt2, unsigned long long* ovf,
+                                              int64_t cap2, unsigned int* cnt2, unsigned long long* ovf, int wide,
                                               hipStream_t stream);
 extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsigned int* cnt2, int64_t cap2,
                                                   int nparts, int rb2, int keybits, int64_t vbase, int img_kind,
@@ -93,7 +93,7 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
                                                   int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
                                                   uint64_t* oplane, int64_t ocap, unsigned long long* ctr,
                                                   unsigned long long* prange, int grid, uint64_t* scratch,
-                                                  int64_t scratch_words, hipStream_t stream);
+                                                  int64_t scratch_words, int wide, hipStream_t stream);
 extern "C" int64_t pgx_narrow_scratch_words(int nparts, int img_kind, int grid);
 extern "C" hipError_t pgx_launch_fsm(const pgx::FsmSeg* segs, int nsegs, const uint32_t* table, int S, int L,
                                      int64_t total_chunks, uint32_t* cnt, uint16_t* stv, unsigned long long* pcount,
@@ -854,7 +854,8 @@ struct ExecPlan {
   std::shared_ptr<const std::vector<std::vector<int32_t>>> lazy_rep_seg, lazy_rep_id;  // part_result's key tables
   int narrow_vd = 0;              // dictId bits of the value column (0: COUNT only)
   int narrow_k2min = 0;           // second-split bits the record width needs
-  int narrow_img = 0;             // value image in the aggregation's LDS: 0 none, 1 U32, 2 FOR16
+  int narrow_img = 0;             // value image in the aggregation's LDS: 0 none, 1 U32, 2 FOR16, 3 value offsets, 4 packed
+  bool narrow_wide = false;       // second-stage records of 64 bits (value offsets too wide for 32-bit records)
   const uint32_t* narrow_imgp = nullptr;
   int narrow_img_words = 0, narrow_img_sh = 0;
   uint64_t narrow_vrange = 0;     // largest value offset (value - vbase)
@@ -874,6 +875,7 @@ struct ExecPlan {
     bool sum = false, mn = false, mx = false, dictid = false, slab = false, narrow = false;
     const int64_t* vdict = nullptr;
     int vd = 0, k2min = 0, img = 0, img_words = 0, img_sh = 0;
+    bool wide = false;
     const uint32_t* imgp = nullptr;
     uint64_t vrange = 0;
     bool fp = false;
@@ -886,7 +888,7 @@ struct ExecPlan {
     c.vcol = part_vcol, c.vbits = part_vbits, c.vbase = part_vbase;
     c.sum = part_sum, c.mn = part_min, c.mx = part_max, c.dictid = part_dictid, c.slab = part_slab, c.narrow = part_narrow;
     c.vdict = part_vdict, c.vd = narrow_vd, c.k2min = narrow_k2min, c.img = narrow_img, c.img_words = narrow_img_words;
-    c.img_sh = narrow_img_sh, c.imgp = narrow_imgp, c.vrange = narrow_vrange;
+    c.img_sh = narrow_img_sh, c.imgp = narrow_imgp, c.vrange = narrow_vrange, c.wide = narrow_wide;
     c.fp = part_fp, c.fdict = part_fdict, c.fbase = part_fbase;
     return c;
   }
@@ -894,7 +896,7 @@ struct ExecPlan {
     part_vcol = c.vcol, part_vbits = c.vbits, part_vbase = c.vbase;
     part_sum = c.sum, part_min = c.mn, part_max = c.mx, part_dictid = c.dictid, part_slab = c.slab, part_narrow = c.narrow;
     part_vdict = c.vdict, narrow_vd = c.vd, narrow_k2min = c.k2min, narrow_img = c.img, narrow_img_words = c.img_words;
-    narrow_img_sh = c.img_sh, narrow_imgp = c.imgp, narrow_vrange = c.vrange;
+    narrow_img_sh = c.img_sh, narrow_imgp = c.imgp, narrow_vrange = c.vrange, narrow_wide = c.wide;
     part_fp = c.fp, part_fdict = c.fdict, part_fbase = c.fbase;
   }
   std::vector<int64_t> rec_base; // per segment: index of its row 0 in the record array
@@ -980,6 +982,7 @@ constexpr int kNarrowMaxWg = 1024; // pgx_narrow.hip kN2MaxSlabs
 struct NarrowBuffers {
   int k2 = 0, rb1 = 0, rb2 = 0, cshift = 0;
   bool hib = false;
+  int w2 = 1;  // u32 words per second-stage record (2: ExecPlan::narrow_wide)
   int64_t nwg = 0, cap1 = 0, cap2 = 0, ocap = 0, nparts = 0;
   DevBuf lo1, hi1, cnt1, rec2, cnt2, okey, oplane, ctr;  // ctr: ocount | overflow scan | split | aggregation
   DevBuf prange;  // trim-key ranges: [kind] smallest, [4 + kind] largest (pgx_trim.hip)

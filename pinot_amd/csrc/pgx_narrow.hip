@@ -60,6 +60,9 @@ constexpr int kN2ListCap = kN2Chunk / kN2Unit + kN2MaxSub;  // units that can co
 //   | B | the listed units are written out, four per wavefront instruction.
 // U (first unflushed position, a unit boundary) and V (ring-valid-from: positions below it were stored straight out)
 // are double-buffered so the owners write the next round's while this round's are read.
+// W: u32 words per output record -- 1, or 2 when the remaining key bits and the value field need more than 32 bits
+// (value offsets of per-segment dictionaries, c3d): the rings then hold kN2RingWords / 2 records and a 64-byte unit 8.
+template <int W>
 __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* __restrict__ lo,
                                                                const uint16_t* __restrict__ hi,
                                                                const unsigned long long* __restrict__ cnt1, int nwg,
@@ -76,7 +79,8 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nsub = 1 << k2;
   const int rb2 = rb1 - k2;
-  const int rlog = 15 - k2;
+  constexpr int UR = kN2Unit / W;  // records per 64-byte unit
+  const int rlog = (W == 2 ? 14 : 15) - k2;  // ring records per sub-bucket: 2^rlog
   const uint32_t rmask = (1u << rlog) - 1u;
   const uint64_t m2 = (uint64_t(1) << rb2) - 1u;
   const uint32_t ucap = static_cast<uint32_t>(cap2 < 0xFFFFFFFFll ? cap2 : 0xFFFFFFFFll);
@@ -94,7 +98,20 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
   };
   const PGX_GLOBAL uint32_t* glo = (const PGX_GLOBAL uint32_t*)lo + static_cast<int64_t>(b) * nwg * cap1;
   const PGX_GLOBAL uint16_t* ghi = hi ? (const PGX_GLOBAL uint16_t*)hi + static_cast<int64_t>(b) * nwg * cap1 : nullptr;
-  PGX_GLOBAL uint32_t* gout = (PGX_GLOBAL uint32_t*)out + static_cast<int64_t>(b) * nsub * cap2;
+  PGX_GLOBAL uint32_t* gout = (PGX_GLOBAL uint32_t*)out + static_cast<int64_t>(b) * nsub * cap2 * W;
+  // record i of sub-bucket sb: words [(sb * cap2 + i) * W, + W) of gout; ring slot (sb << rlog) + (i & rmask) likewise
+  auto put_out = [&](uint32_t sb, uint32_t i, uint64_t r) {
+    const int64_t at = (static_cast<int64_t>(sb) * cap2 + i) * W;
+    if (W == 2) *(PGX_GLOBAL uint64_t*)(gout + at) = r;
+    else gout[at] = static_cast<uint32_t>(r);
+  };
+  auto put_ring = [&](uint32_t slot, uint64_t r) {
+    if (W == 2) *reinterpret_cast<uint64_t*>(ring + 2 * slot) = r;
+    else ring[slot] = static_cast<uint32_t>(r);
+  };
+  auto get_ring = [&](uint32_t slot) -> uint64_t {
+    return W == 2 ? *reinterpret_cast<const uint64_t*>(ring + 2 * slot) : static_cast<uint64_t>(ring[slot]);
+  };
   struct Rd {
     int w;
     uint32_t c0, n;
@@ -129,13 +146,14 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
     const Rd r2n = advance(r1);
     if (r2n.w < nwg) load(r2n, l2, h2);
     // split fields and positions
-    uint32_t rec[kN2Per], sbp[kN2Per];  // sbp: sub-bucket | valid << 31
+    uint64_t rec[kN2Per];
+    uint32_t sbp[kN2Per];  // sbp: sub-bucket | valid << 31
     uint32_t pp[kN2Per];
 #pragma unroll
     for (int k = 0; k < kN2Per; ++k) {
       const uint32_t pos = r0.c0 + static_cast<uint32_t>(k * kN2Threads + tid);
       const uint64_t x = static_cast<uint64_t>(l0[k]) | (static_cast<uint64_t>(h0[k]) << 32);
-      rec[k] = static_cast<uint32_t>((x & m2) | ((x >> rb1) << rb2));
+      rec[k] = (x & m2) | ((x >> rb1) << rb2);
       const uint32_t sb = static_cast<uint32_t>(x >> rb2) & static_cast<uint32_t>(nsub - 1);
       sbp[k] = pos < r0.n ? (sb | 0x80000000u) : 0u;
       pp[k] = pos < r0.n ? atomicAdd(&cur[sb], 1u) : 0u;
@@ -150,8 +168,8 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
         u0 = Uc[tid];
         v0 = Vc[tid];
         const uint32_t lim = u0 + (1u << rlog);
-        nu = ((en < lim ? en : lim) - u0) / kN2Unit;
-        Ub[par ^ 1][tid] = en & ~static_cast<uint32_t>(kN2Unit - 1);
+        nu = ((en < lim ? en : lim) - u0) / UR;
+        Ub[par ^ 1][tid] = en & ~static_cast<uint32_t>(UR - 1);
         Vb[par ^ 1][tid] = en > lim ? en : v0;
       }
       uint32_t incl = nu;
@@ -166,7 +184,7 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
       base = __shfl(base, 0, 64);
       for (uint32_t q = 0, k = base + incl - nu; q < nu; ++q, ++k) {
         lsub[k] = static_cast<uint16_t>(tid);
-        lpos[k] = u0 + q * kN2Unit;
+        lpos[k] = u0 + q * UR;
       }
     }
     if (tid == 0) lcnt[par ^ 1] = 0u;  // the next round's list (its reservations follow barrier B)
@@ -175,8 +193,8 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
       if (!sbp[k]) continue;
       const uint32_t sb = sbp[k] & 0x7FFFFFFFu;
       const uint32_t pos = pp[k];
-      if (pos < Uc[sb] + (1u << rlog)) ring[(sb << rlog) + (pos & rmask)] = rec[k];
-      else if (pos < ucap) gout[static_cast<int64_t>(sb) * cap2 + pos] = rec[k];  // past the ring: straight out
+      if (pos < Uc[sb] + (1u << rlog)) put_ring((sb << rlog) + (pos & rmask), rec[k]);
+      else if (pos < ucap) put_out(sb, pos, rec[k]);  // past the ring: straight out
     }
     n_lds_barrier();  // B
     {  // four lanes per unit, 16 bytes each; a unit holding positions below V goes record by record
@@ -186,13 +204,14 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
         const uint32_t sb = lsub[u];
         const uint32_t p0 = lpos[u];
         if (p0 >= ucap) continue;
-        PGX_GLOBAL uint32_t* const dst = gout + static_cast<int64_t>(sb) * cap2 + p0 + 4 * g;
-        const uint32_t* const rs = ring + (sb << rlog) + (p0 & rmask) + 4 * g;
+        PGX_GLOBAL uint32_t* const dst = gout + (static_cast<int64_t>(sb) * cap2 + p0) * W + 4 * g;
+        const uint32_t* const rs = ring + ((sb << rlog) + (p0 & rmask)) * W + 4 * g;
         if (p0 >= Vc[sb]) {
           *(PGX_GLOBAL na_u32x4*)dst = *(const na_u32x4*)rs;
-        } else {
-          for (int q = 0; q < 4; ++q)
-            if (p0 + 4 * g + q >= Vc[sb]) dst[q] = rs[q];
+        } else {  // this lane's 4 / W records, each only if it was not stored straight out
+          for (int q = 0; q < 4 / W; ++q)
+            if (p0 + (4 / W) * g + q >= Vc[sb])
+              for (int w = 0; w < W; ++w) dst[q * W + w] = rs[q * W + w];
         }
       }
     }
@@ -209,11 +228,10 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
   }
   __syncthreads();
   // the rings' last partial units, then the partition fills (every record, also past cap2)
-  for (int x = tid; x < nsub * kN2Unit; x += kN2Threads) {
-    const int sb = x / kN2Unit;
-    const uint32_t i = Ub[par][sb] + static_cast<uint32_t>(x % kN2Unit);
-    if (i < cur[sb] && i >= Vb[par][sb] && i < ucap)
-      gout[static_cast<int64_t>(sb) * cap2 + i] = ring[(sb << rlog) + (i & rmask)];
+  for (int x = tid; x < nsub * UR; x += kN2Threads) {
+    const int sb = x / UR;
+    const uint32_t i = Ub[par][sb] + static_cast<uint32_t>(x % UR);
+    if (i < cur[sb] && i >= Vb[par][sb] && i < ucap) put_out(sb, i, get_ring((sb << rlog) + (i & rmask)));
   }
   for (int sb = tid; sb < nsub; sb += kN2Threads) {
     cnt2[static_cast<int64_t>(b) * nsub + sb] = cur[sb];
@@ -271,7 +289,9 @@ __device__ __forceinline__ int na_way(const na_u32x4 k, uint32_t key) {
   return k.x == key ? 0 : k.y == key ? 1 : k.z == key ? 2 : k.w == key ? 3 : -1;
 }
 
-template <int IMG, bool SUM, bool MN, bool MX>
+// W: u32 words per record (pgx_narrow_split<W>); W = 2 carries value offsets wider than the 32-bit record leaves room
+// for (IMG 3 only): 512 records per batch instead of 1024, the same 4 KiB per wavefront.
+template <int IMG, bool SUM, bool MN, bool MX, int W>
 __global__ void __launch_bounds__(na_threads<IMG>()) __attribute__((amdgpu_waves_per_eu(IMG >= 3 ? 4 : 1)))
 pgx_narrow_aggregate(
     const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
@@ -283,6 +303,8 @@ pgx_narrow_aggregate(
   constexpr int kNAWaves = kNAThreads / 64;
   constexpr bool LIMG = IMG == 1 || IMG == 2 || IMG == 4;  // an image in LDS
   constexpr bool BIG = IMG == 1 || IMG == 2;               // 512 threads, two waves per SIMD: wider batches
+  constexpr int NR = 16 / W;                               // records per lane per batch
+  constexpr uint32_t BATCH = 64u * NR;
   __shared__ __attribute__((aligned(16))) uint32_t simg[LIMG ? (IMG == 4 ? kNAImg4Words : kNAImgWords) : 1];
   __shared__ __attribute__((aligned(16))) uint32_t tkey[kNAWaves * kNASlots];
   __shared__ unsigned long long tsc[kNAWaves * kNASlots];
@@ -318,10 +340,10 @@ pgx_narrow_aggregate(
   bool lost = false;
 
   auto load = [&](int pp, uint32_t i0, uint32_t nn, uint32_t (&buf)[16]) {
-    const int64_t base = (static_cast<int64_t>(pp) * cap2 + i0) >> 2;  // cap2 and i0 are multiples of 4
+    const int64_t base = ((static_cast<int64_t>(pp) * cap2 + i0) * W) >> 2;  // cap2 and i0 are multiples of 4
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint32_t e = static_cast<uint32_t>(q * 256 + lane * 4);
+      const uint32_t e = static_cast<uint32_t>(q * (256 / W) + lane * (4 / W));
       na_u32x4 x = {0u, 0u, 0u, 0u};
       if (i0 + e < nn) x = __builtin_nontemporal_load(src + base + q * 64 + lane);
       buf[4 * q] = x.x;
@@ -432,7 +454,7 @@ pgx_narrow_aggregate(
   };
   auto count = [&](int pp) { return pp < nparts ? min(cnt2[pp], static_cast<unsigned int>(cap2)) : 0u; };
   auto advance = [&](Pos a) -> Pos {
-    if (a.i0 + 1024u < a.n) return Pos{a.p, a.i0 + 1024u, a.n};
+    if (a.i0 + BATCH < a.n) return Pos{a.p, a.i0 + BATCH, a.n};
     const int np = a.p + nw;
     return Pos{np, 0u, count(np)};
   };
@@ -454,29 +476,37 @@ pgx_narrow_aggregate(
     } else {
       if (d.p < nparts) load(d.p, d.i0, d.n, b1);
     }
-    const bool full = c.i0 + 1024u <= c.n;  // every record of the batch is the partition's
+    const bool full = c.i0 + BATCH <= c.n;  // every record of the batch is the partition's
+    auto rec = [&](int jj) -> uint64_t {  // record jj of this lane's batch
+      return W == 1 ? static_cast<uint64_t>(b0[jj])
+                    : static_cast<uint64_t>(b0[2 * jj]) | (static_cast<uint64_t>(b0[2 * jj + 1]) << 32);
+    };
+    auto field = [&](uint64_t R) -> uint32_t {  // the value field: dictId or value offset
+      return rb2 >= 32 && W == 1 ? 0u : static_cast<uint32_t>(R >> rb2);
+    };
 #pragma unroll
-    for (int h = 0; h < 16 / HB; ++h) {  // groups of HB records: home buckets and values read back to back
+    for (int h = 0; h < NR / HB; ++h) {  // groups of HB records: home buckets and values read back to back
       na_u32x4 kb[HB];
       uint32_t val[HB];
 #pragma unroll
       for (int j = 0; j < HB; ++j) {
         const int jj = h * HB + j;
-        const uint32_t R = b0[jj];
-        const uint32_t r2 = R & rmask;
+        const uint64_t R = rec(jj);
+        const uint32_t r2 = static_cast<uint32_t>(R) & rmask;
         const uint32_t b = home(r2);
         kb[j] = *reinterpret_cast<const na_u32x4*>(K + b * kNAWays);
-        val[j] = SUM ? na_img<IMG>(simg, img_sh, rb2 >= 32 ? 0u : R >> rb2) : 0u;
+        val[j] = SUM ? na_img<IMG>(simg, img_sh, field(R)) : 0u;
       }
       uint32_t miss = 0u;  // records of this group whose key is not in its home bucket (yet)
 #pragma unroll
       for (int j = 0; j < HB; ++j) {
         const int jj = h * HB + j;
-        const uint32_t ei = static_cast<uint32_t>((jj >> 2) * 256 + lane * 4 + (jj & 3));
+        const uint32_t ei = W == 1 ? static_cast<uint32_t>((jj >> 2) * 256 + lane * 4 + (jj & 3))
+                                   : static_cast<uint32_t>((jj >> 1) * 128 + lane * 2 + (jj & 1));
         const bool valid = full || c.i0 + ei < c.n;  // (full: a wave-uniform flag, no per-record compare)
-        const uint32_t R = b0[jj];
-        const uint32_t r2 = R & rmask;
-        const uint32_t dd = rb2 >= 32 ? 0u : R >> rb2;
+        const uint64_t R = rec(jj);
+        const uint32_t r2 = static_cast<uint32_t>(R) & rmask;
+        const uint32_t dd = field(R);
         const uint32_t b = home(r2);
         const int m = na_way(kb[j], r2);
         if (valid && m < 0) miss |= 1u << j;
@@ -493,15 +523,16 @@ pgx_narrow_aggregate(
         if (!miss) continue;
         const int js = __builtin_ctz(miss);
         miss &= miss - 1u;
-        uint32_t R = 0u, v = 0u;
+        uint64_t R = 0u;
+        uint32_t v = 0u;
 #pragma unroll
         for (int j = 0; j < HB; ++j)
           if (j == js) {
-            R = b0[h * HB + j];
+            R = rec(h * HB + j);
             v = val[j];
           }
-        const uint32_t r2 = R & rmask;
-        const uint32_t dd = rb2 >= 32 ? 0u : R >> rb2;
+        const uint32_t r2 = static_cast<uint32_t>(R) & rmask;
+        const uint32_t dd = field(R);
         const int slot = probe(r2, home(r2));
         if (slot < 0) {
           lost = true;
@@ -601,15 +632,19 @@ extern "C" int64_t pgx_narrow_scratch_words(int nparts, int img_kind, int grid) 
 
 extern "C" hipError_t pgx_launch_narrow_split(const uint32_t* lo, const uint16_t* hi, const unsigned long long* cnt1,
                                               int nbuckets, int nwg, int64_t cap1, int rb1, int k2, uint32_t* out,
-                                              int64_t cap2, unsigned int* cnt2, unsigned long long* ovf,
+                                              int64_t cap2, unsigned int* cnt2, unsigned long long* ovf, int wide,
                                               hipStream_t stream) {
   if (nbuckets <= 0) return hipSuccess;
   if (nwg < 1 || nwg > pgx::kN2MaxSlabs || k2 < 0 || k2 > pgx::kNarrowMaxBits2 || rb1 - k2 < 0 || rb1 > 48 ||
       cap1 < 1 || cap1 * nwg >= (int64_t(1) << 32) || cap2 < 1 || cap2 >= (int64_t(1) << 32) || !lo || !out || !cnt1 ||
       !cnt2 || !ovf)
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pgx::pgx_narrow_split, dim3(nbuckets), dim3(pgx::kN2Threads), 0, stream, lo, hi, cnt1, nwg, cap1,
-                     rb1, k2, out, cap2, cnt2, ovf);
+  if (wide)
+    hipLaunchKernelGGL(pgx::pgx_narrow_split<2>, dim3(nbuckets), dim3(pgx::kN2Threads), 0, stream, lo, hi, cnt1, nwg,
+                       cap1, rb1, k2, out, cap2, cnt2, ovf);
+  else
+    hipLaunchKernelGGL(pgx::pgx_narrow_split<1>, dim3(nbuckets), dim3(pgx::kN2Threads), 0, stream, lo, hi, cnt1, nwg,
+                       cap1, rb1, k2, out, cap2, cnt2, ovf);
   return hipGetLastError();
 }
 
@@ -619,7 +654,7 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
                                                   int need_sum, int need_min, int need_max, int cshift, uint64_t* okey,
                                                   uint64_t* oplane, int64_t ocap, unsigned long long* ctr,
                                                   unsigned long long* prange, int grid, uint64_t* scratch,
-                                                  int64_t scratch_words, hipStream_t stream) {
+                                                  int64_t scratch_words, int wide, hipStream_t stream) {
   if (nparts <= 0) return hipSuccess;
   if (!scratch || scratch_words < pgx_narrow_scratch_words(nparts, img_kind, grid)) return hipErrorInvalidValue;
   const int nw = grid * (img_kind == 4 ? 16 : 8);
@@ -632,13 +667,13 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
       grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 4 ||
       ((img_kind == 1 || img_kind == 2) && (!img || img_words < 1 || img_words > pgx::kNAImgWords)) ||
       (img_kind == 4 && (!img || img_words < 1 || img_words > pgx::kNAImg4Words)) || (need_sum && !img_kind) ||
-      ((need_min || need_max) && !img_kind && !vdict))
+      ((need_min || need_max) && !img_kind && !vdict) || (wide && img_kind != 3))
     return hipErrorInvalidValue;
   const pgx::NarrowMix m = pgx::narrow_mix(keybits);
-  const int sel = img_kind * 8 + (need_sum ? 4 : 0) + (need_min ? 2 : 0) + (need_max ? 1 : 0);
+  const int sel = (wide ? 5 : img_kind) * 8 + (need_sum ? 4 : 0) + (need_min ? 2 : 0) + (need_max ? 1 : 0);
 #define PGX_NA_CASE(C, I, A, B, D)                                                                                   \
   case C:                                                                                                            \
-    hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D>), dim3(grid), dim3(pgx::na_threads<I>()), 0, stream, in, \
+    hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D, 1>), dim3(grid), dim3(pgx::na_threads<I>()), 0, stream, in, \
                        cnt2,                                                                                          \
                        cap2, nparts, rb2, m.mask, m.ic1, m.s, vbase, img, img_words, img_sh, vdict, cshift,   \
                        rkey, rplane, wcap, rstride, wcount, ctr, prange);                                            \
@@ -658,6 +693,21 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
     PGX_NA_CASES(2)
     PGX_NA_CASES(3)
     PGX_NA_CASES(4)
+#define PGX_NA_CASE_W(C, A, B, D)                                                                                    \
+  case C:                                                                                                            \
+    hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<3, A, B, D, 2>), dim3(grid), dim3(pgx::na_threads<3>()), 0, stream, \
+                       in, cnt2, cap2, nparts, rb2, m.mask, m.ic1, m.s, vbase, img, img_words, img_sh, vdict, cshift,  \
+                       rkey, rplane, wcap, rstride, wcount, ctr, prange);                                            \
+    break;
+    PGX_NA_CASE_W(40, false, false, false)
+    PGX_NA_CASE_W(41, false, false, true)
+    PGX_NA_CASE_W(42, false, true, false)
+    PGX_NA_CASE_W(43, false, true, true)
+    PGX_NA_CASE_W(44, true, false, false)
+    PGX_NA_CASE_W(45, true, false, true)
+    PGX_NA_CASE_W(46, true, true, false)
+    PGX_NA_CASE_W(47, true, true, true)
+#undef PGX_NA_CASE_W
     default:
       return hipErrorInvalidValue;
   }

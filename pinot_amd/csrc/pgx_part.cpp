@@ -192,7 +192,8 @@ bool narrow_size(const ExecPlan& P, NarrowBuffers& NB) {
     NB.k2 = std::max(P.narrow_k2min, std::min(P.kn.narrow_k2, std::min(kNarrowMaxBits2, NB.rb1)));
   if (NB.k2 > kNarrowMaxBits2 || NB.k2 > NB.rb1) return false;
   NB.rb2 = NB.rb1 - NB.k2;
-  if (NB.rb2 + P.narrow_vd > 32 || NB.rb2 > 31) return false;
+  NB.w2 = P.narrow_wide ? 2 : 1;
+  if (NB.rb2 + P.narrow_vd > 32 * NB.w2 || NB.rb2 > 31) return false;
   NB.nparts = int64_t(1) << (kNarrow1Bits + NB.k2);
   NB.cap1 = narrow_cap(double(P.part_wg_rows) / (1 << kNarrow1Bits), 64);
   // a partition holds whole groups, so its record count varies more than a binomial: start at 1.5x the mean (C3: ~6
@@ -208,7 +209,7 @@ bool narrow_size(const ExecPlan& P, NarrowBuffers& NB) {
   NB.cshift = 64 - cb;
   NB.ocap = std::max<int64_t>(1, std::min<int64_t>(P.rec_total, NB.nparts * kNarrowSlots));
   const uint64_t bytes = uint64_t(kNarrow1Bits == 8 ? 256 : (1 << kNarrow1Bits)) * NB.nwg * NB.cap1 * (NB.hib ? 6 : 4) +
-                         uint64_t(NB.nparts) * NB.cap2 * 4 + uint64_t(NB.ocap) * 40 +
+                         uint64_t(NB.nparts) * NB.cap2 * 4 * NB.w2 + uint64_t(NB.ocap) * 40 +
                          // the aggregation's per-wavefront output regions (pgx_narrow_scratch_words; wavefront
                          // rounding bounded by 4096 wavefronts' tables)
                          (uint64_t(NB.nparts) + 4096) * kNarrowSlots * 40;
@@ -220,7 +221,7 @@ void narrow_alloc(pgx_ctx* ctx, NarrowBuffers& NB) {
   NB.lo1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 4);
   if (NB.hib) NB.hi1 = DevBuf(ctx, size_t(slabs * NB.cap1) * 2);
   NB.cnt1 = DevBuf(ctx, size_t(slabs) * 8);
-  NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4);
+  NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4 * NB.w2);
   NB.cnt2 = DevBuf(ctx, size_t(NB.nparts) * 4);
   NB.okey = DevBuf(ctx, size_t(NB.ocap) * 8);
   NB.oplane = DevBuf(ctx, size_t(NB.ocap) * 4 * 8);
@@ -256,7 +257,7 @@ void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStrea
   PGX_LAUNCH(st, "pgx_narrow_split",
              pgx_launch_narrow_split(NB.lo1.as<uint32_t>(), NB.hib ? NB.hi1.as<uint16_t>() : nullptr, devp(NB.cnt1),
                                      1 << kNarrow1Bits, int(NB.nwg), NB.cap1, NB.rb1, NB.k2, NB.rec2.as<uint32_t>(),
-                                     NB.cap2, NB.cnt2.as<unsigned int>(), ctr + 2, st),
+                                     NB.cap2, NB.cnt2.as<unsigned int>(), ctr + 2, NB.w2 == 2, st),
              "narrow split");
   PGX_LAUNCH(st, "pgx_narrow_aggregate",
              pgx_launch_narrow_aggregate(NB.rec2.as<uint32_t>(), NB.cnt2.as<unsigned int>(), NB.cap2, int(NB.nparts),
@@ -264,7 +265,7 @@ void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStrea
                                          P.narrow_img_words, P.narrow_img_sh, P.part_vdict, P.part_sum, P.part_min,
                                          P.part_max, NB.cshift, NB.okey.as<uint64_t>(), NB.oplane.as<uint64_t>(),
                                          NB.ocap, ctr, devp(NB.prange), agg_grid, NB.agg_scratch.as<uint64_t>(),
-                                         NB.agg_scratch_words, st),
+                                         NB.agg_scratch_words, NB.w2 == 2, st),
              "narrow aggregate");
 }
 
@@ -314,14 +315,14 @@ bool run_narrow(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, NarrowBuffers& NB, hi
     std::vector<unsigned int> c2(size_t(NB.nparts));
     hip_check(hipMemcpy(c2.data(), NB.cnt2.p, c2.size() * 4, hipMemcpyDeviceToHost), "partition fills D2H");
     NB.cap2 = narrow_cap(double(*std::max_element(c2.begin(), c2.end())), 64);
-    if (NB.cap2 >= (int64_t(1) << 31) || uint64_t(NB.nparts) * NB.cap2 * 4 > kPartMaxBytes) break;
+    if (NB.cap2 >= (int64_t(1) << 31) || uint64_t(NB.nparts) * NB.cap2 * 4 * NB.w2 > kPartMaxBytes) break;
     const int cb = bits_for(NB.cap2 + 1);
     const long double smax = (long double)NB.cap2 * (long double)P.narrow_vrange;
     int sb = 1;
     while (sb < 64 && std::ldexp(1.0L, sb) <= smax) ++sb;
     if (cb + sb > 64 || cb > 62) break;
     NB.cshift = 64 - cb;
-    NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4);
+    NB.rec2 = DevBuf(ctx, size_t(NB.nparts * NB.cap2) * 4 * NB.w2);
     scan = false;
   }
   if (P.kn.narrow_log)  // tests (PGX_DEBUG=narrow_log): which path ran

@@ -1007,8 +1007,14 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           if (rb1 - k2 > 31) k2 = rb1 - 31;
           return rb1 + vd <= 48 && k2 <= kNarrowMaxBits2;
         };
+        // value offsets too wide for a 32-bit second-stage record (c3d: 16 key bits + 20 offset bits): 64-bit second-
+        // stage records instead of the 8-byte radix path's two full passes
+        auto fits_wide = [&](int vd, int& k2) {
+          k2 = std::max(0, rb1 - 31);
+          return rb1 + vd <= 48 && vd <= 32 && k2 <= kNarrowMaxBits2;
+        };
         int vd = 0, imgk = 0, k2 = 0;
-        bool nok = true;
+        bool nok = true, wide = false;
         if (vc >= 0) {
           const StagedColumn& c0 = segs[0]->col(P.qcols[vc]);
           nok = same_dict && c0.dict_dev != nullptr && std::is_sorted(c0.ivals.begin(), c0.ivals.end());
@@ -1018,7 +1024,18 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           if (need_sum && !imgk) nok = false;
           nok = nok && fits(vd, k2);
           int k2d = 0;
-          if ((!nok || q.kn.narrow_direct) && vbits <= 32 && fits(vbits, k2d)) {
+          const bool direct = vbits <= 32 && fits(vbits, k2d);
+          // value-offset records are made in the scan, from the column's LDS image beside the scan's record rings
+          // (256 buckets x kNarrowRing records x 6 B): a per-segment image larger than the rest of the LDS (c3d's
+          // 128 KiB FOR16 images) keeps the 8-byte radix path
+          int64_t scan_img = 0;
+          for (int s = 0; s < n; ++s) {
+            const StagedColumn& c = segs[s]->col(P.qcols[vc]);
+            if (c.img_kind != IMG_NONE) scan_img = std::max<int64_t>(scan_img, int64_t(c.img_words) * 4);
+          }
+          const bool scan_fits = scan_img + (int64_t(1) << kNarrow1Bits) * kNarrowRing * 6 + 16 * 1024 <= 160 * 1024;
+          if ((!nok || q.kn.narrow_direct) && scan_fits && (direct || (vbits <= 32 && fits_wide(vbits, k2d)))) {
+            wide = !direct;
             nok = true;
             imgk = 3;
             vd = vbits;
@@ -1051,6 +1068,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           P.narrow_vd = vd;
           P.narrow_k2min = k2;
           P.narrow_img = imgk;
+          P.narrow_wide = wide;
         }
       }
       return true;

@@ -93,7 +93,7 @@ def main():
     fn.restype = C.c_int
     fn.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int64, C.c_int, C.c_void_p,
                    C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
-                   C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_void_p]
+                   C.c_int64, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_int64, C.c_int, C.c_void_p]
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     grid = ncu * (4 if args.img == 3 else 1)
     L.pgx_narrow_scratch_words.restype = C.c_int64
@@ -106,7 +106,7 @@ def main():
         ctr.zero_()
         rc = fn(recs.data_ptr(), cnt2.data_ptr(), cap2, P, rb2, 34, 0, args.img, img.data_ptr(), img.numel(), img_sh,
                 vdict.data_ptr(), args.sum, mm, mm, cshift, okey.data_ptr(), oplane.data_ptr(), ocap, ctr.data_ptr(),
-                prange.data_ptr(), grid, scratch.data_ptr(), sw, C.c_void_p(st.cuda_stream))
+                prange.data_ptr(), grid, scratch.data_ptr(), sw, 0, C.c_void_p(st.cuda_stream))
         assert rc == 0, rc
 
     launch()
