@@ -335,14 +335,14 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
   } else if (P.use_part && !P.part_slab) {
     B.table = DevBuf(ctx, std::max<int64_t>(P.rec_total, 1) * 8);  // one key|value record per scanned row
     K.table = devp(B.table);
-  } else if (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) {
+  } else if (hash_mode(K.group_mode)) {
     K.hash_cap = P.hash_cap;
     B.table = DevBuf(ctx, P.hash_cap * K.num_planes * 8);
     K.table = devp(B.table);
-    const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : P.hash_cap;
+    const uint64_t kw = uint64_t(K.key_words) * P.hash_cap;
     B.keys = DevBuf(ctx, kw * 8);
     K.keys = devp(B.keys);
-    if (K.group_mode == G_HASH128) {
+    if (K.group_mode != G_HASH64) {
       B.key_state = DevBuf(ctx, P.hash_cap * 4);
       K.key_state = B.key_state.as<unsigned int>();
     }
@@ -361,8 +361,8 @@ void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table,
   else
     hip_check(hipMemcpyAsync(B.arena.p, B.host.p, B.size, hipMemcpyHostToDevice, st), "argument arena H2D");
   if (init_table && K.group_mode != G_NONE && !P.use_part) {
-    const uint64_t slots = (K.group_mode == G_HASH64 || K.group_mode == G_HASH128) ? P.hash_cap : P.dense_slots;
-    const uint64_t kw = (K.group_mode == G_HASH128) ? 2 * P.hash_cap : (K.group_mode == G_HASH64 ? P.hash_cap : 0);
+    const uint64_t slots = hash_mode(K.group_mode) ? P.hash_cap : P.dense_slots;
+    const uint64_t kw = hash_mode(K.group_mode) ? uint64_t(K.key_words) * P.hash_cap : 0;
     PGX_LAUNCH(st, "pgx_init_planes", pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
   }
 }
@@ -396,7 +396,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
   const KQuery& K = P.kq;
   if (!P.kn.jit) return;
   if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL || P.use_part ||
-        K.group_mode == G_HASH64 || K.group_mode == G_HASH128))
+        hash_mode(K.group_mode)))
     return;
   const int nc = K.num_qcols;
   if (nc > PGX_J_MAX_COLS) return;
@@ -829,13 +829,13 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
                    hipStream_t st, pgx_result* R, const unsigned long long* dense_host_override) {
   KQuery& K = P.kq;
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
-  const bool hash = K.group_mode == G_HASH64 || K.group_mode == G_HASH128;
+  const bool hash = hash_mode(K.group_mode);
   const bool dense_dev = K.num_gcols > 0 && !hash && !dense_host_override;
   // group-by compaction (occupied slots -> columnar), read back together with the outputs block: ONE sync
   const uint64_t slots = hash ? P.hash_cap : P.dense_slots;
   std::vector<int64_t> slot_ids;
   std::vector<unsigned long long> planes;  // [plane][group]
-  std::vector<unsigned long long> keys_lo, keys_hi;  // hash keys of the groups
+  std::vector<unsigned long long> gkeys;  // hash keys of the groups: key_words words each
   uint64_t ng = 0;
   // first guess of the group count: the plan's previous execution's (a kept plan replays the same query), else <= 64k
   auto guess = [&](uint64_t limit) {
@@ -876,7 +876,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     // the group count on the device); again at the exact size if the guess was short
     // (the outputs block travels with the groups; at most one group per slot)
     const uint64_t cap_max = std::max<uint64_t>(1, slots);
-    const uint64_t kw = (K.group_mode == G_HASH128) ? 2 : 1;
+    const uint64_t kw = uint64_t(K.key_words);
     uint64_t cap = guess(cap_max);
     for (;;) {
       const size_t bytes = 256 + size_t(cap) * 8 * (1 + K.num_planes + kw);
@@ -906,12 +906,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
       planes.resize(ng * K.num_planes);
       for (int p = 0; p < K.num_planes; ++p) std::memcpy(planes.data() + p * ng, h + 32 + cap + p * cap, ng * 8);
       const unsigned long long* gk = h + 32 + cap * (1 + K.num_planes);
-      keys_lo.resize(ng);
-      keys_hi.resize(ng, 0);
-      for (uint64_t i = 0; i < ng; ++i) {
-        keys_lo[i] = gk[i * kw];
-        if (kw == 2) keys_hi[i] = gk[i * 2 + 1];
-      }
+      gkeys.assign(gk, gk + ng * kw);
       break;
     }
     P.last_groups = ng;
@@ -982,7 +977,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
         else if (slots <= 0xFFFFFFFFull) gid = int64_t((uint32_t(sl) / uint32_t(K.gmul[g])) % uint32_t(P.gdicts[g].card));
         else gid = int64_t((sl / K.gmul[g]) % uint64_t(P.gdicts[g].card));
       } else {
-        const unsigned long long w = K.ghi[g] ? keys_hi[i] : keys_lo[i];
+        const unsigned long long w = gkeys[i * uint64_t(K.key_words) + uint64_t(K.ghi[g])];
         gid = int64_t((w >> K.gshift[g]) & ((1ull << P.gbits[g]) - 1ull));
       }
       R->key_seg[g][oi] = P.gdicts[g].rep_seg[gid];
@@ -1395,7 +1390,7 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     P.use_part = false;  // groups too many or too skewed for the partitions: global hash table, generic kernel
     P.jit.clear();
   }
-  const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
+  const bool hash = hash_mode(P.kq.group_mode);
   uint64_t hash_est = 0;
   if (hash) {
     P.hash_cap = hash_est = initial_hash_cap(segs, n, P);
@@ -2113,7 +2108,7 @@ pgx_status pgx_execute_timed(pgx_ctx* ctx, const pgx_query* q, pgx_segment* cons
       P.use_part = false;
       P.jit.clear();
     }
-    const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
+    const bool hash = hash_mode(P.kq.group_mode);
     if (hash && !P.use_part) P.hash_cap = initial_hash_cap(segs, n, P);
     if (!P.use_part) alloc_outputs(ctx, P, B, nullptr, 0);
     std::vector<hipEvent_t> ev(2 * iters);

@@ -12,7 +12,7 @@ constexpr int kBlock = 256;            // threads per workgroup
 constexpr int kMaxQCols = 16;          // distinct columns a query touches
 constexpr int kMaxLeaves = 16;
 constexpr int kMaxAggs = 8;
-constexpr int kMaxGroupCols = 10;
+constexpr int kMaxGroupCols = 16;
 constexpr int kMaxProg = 64;
 constexpr int kStackDepth = 8;
 constexpr uint64_t kEmptyKey = ~0ull;
@@ -127,7 +127,10 @@ enum AggKind : int8_t { A_COUNT = 0, A_SUM = 1, A_MIN = 2, A_MAX = 3, A_AVG = 4 
 enum PlaneOp : int8_t { P_ADD_I64 = 0, P_ADD_F64 = 1, P_MIN_ORD = 2, P_MAX_ORD = 3 };
 
 enum GroupMode : int8_t { G_NONE = 0, G_DENSE_LDS = 1, G_DENSE_GLOBAL = 2, G_HASH64 = 3, G_HASH128 = 4,
-                          G_EMIT = 5 /* query kernels: emit key|value records for the partitioned group-by */ };
+                          G_EMIT = 5 /* query kernels: emit key|value records for the partitioned group-by */,
+                          G_HASHW = 6 /* keys of 3-4 64-bit words (ARRAY_MAP keys over 126 bits): generic kernel */ };
+constexpr int kMaxKeyWords = 4;
+inline bool hash_mode(int gm) { return gm == G_HASH64 || gm == G_HASH128 || gm == G_HASHW; }
 
 struct KLeaf {
   int32_t lo, hi;
@@ -174,15 +177,16 @@ struct KQuery {
   int8_t gcol[kMaxGroupCols];
   uint64_t gmul[kMaxGroupCols];  // dense: mixed-radix multiplier; hash: bit shift
   int32_t gshift[kMaxGroupCols];
-  int32_t ghi[kMaxGroupCols];    // 128-bit keys: field goes to the high word
+  int32_t ghi[kMaxGroupCols];    // 128-bit / wide keys: the 64-bit word the field goes to (0 = low)
+  int32_t key_words;             // hash keys: 64-bit words per key (1, 2, or up to kMaxKeyWords for G_HASHW)
   uint64_t dense_slots;          // dense key space
   uint64_t hash_cap;             // power of two
   // outputs
   unsigned long long* agg_out;   // aggregation-only: num_planes accumulators (plane encodings)
   unsigned long long* stats;     // [0] docs matched, [1] entries scanned in filter (kernel part)
   unsigned long long* table;     // dense: planes x dense_slots ; hash: planes x hash_cap
-  unsigned long long* keys;      // hash: hash_cap (64-bit) or 2*hash_cap (128-bit: lo, hi)
-  unsigned int* key_state;       // hash128: 0 empty, 1 busy, 2 ready
+  unsigned long long* keys;      // hash: key_words * hash_cap (word w of slot s at keys[s * key_words + w])
+  unsigned int* key_state;       // hash128 / wide: 0 empty, 1 busy, 2 ready
   unsigned long long* overflow;  // hash insert failures (table full) -> host retries bigger
 };
 

@@ -238,6 +238,39 @@ __device__ __forceinline__ int64_t hash_slot128(const KQuery& Q, uint64_t klo, u
   return -1;
 }
 
+// Keys of W 64-bit words (G_HASHW, ARRAY_MAP keys over 126 bits): the 128-bit protocol with W words per slot.
+template <int W>
+__device__ __forceinline__ int64_t hash_slotw(const KQuery& Q, const uint64_t (&k)[W]) {
+  const uint64_t mask = Q.hash_cap - 1;
+  const uint64_t lim = Q.hash_cap < kGlobalMaxProbes ? Q.hash_cap : kGlobalMaxProbes;
+  uint64_t hv = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w) hv = mix64(hv ^ k[w]);
+  uint64_t h = hv & mask;
+  uint64_t probes = 0;
+  while (probes < lim) {
+    unsigned int st = atomicCAS(Q.key_state + h, 0u, 1u);
+    if (st == 0u) {
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        __hip_atomic_store(Q.keys + W * h + w, k[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+      atomicExch(Q.key_state + h, 2u);
+      return static_cast<int64_t>(h);
+    }
+    if (st == 2u) {
+      bool same = true;
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+        same = same && __hip_atomic_load(Q.keys + W * h + w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == k[w];
+      if (same) return static_cast<int64_t>(h);
+      h = (h + 1) & mask;
+      ++probes;
+    }
+  }
+  return -1;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Plane updates (LDS or global; the pointer's address space is known at each call site)
 // ---------------------------------------------------------------------------------------------
@@ -386,7 +419,7 @@ __global__ void __launch_bounds__(kBlock) pgx_scan_kernel(const KQuery Q, int64_
 #pragma unroll
         for (int j = 0; j < 32; ++j) khi[j] = 0;
       }
-      for (int g = 0; g < Q.num_gcols; ++g) {
+      for (int g = 0; g < (GM == G_HASHW ? 0 : Q.num_gcols); ++g) {
         const int c = Q.gcol[g];
         uint32_t v[32];
         decode_dyn(S.bits[c], S.fwd[c], lane_chunk, v);
@@ -413,6 +446,48 @@ __global__ void __launch_bounds__(kBlock) pgx_scan_kernel(const KQuery Q, int64_
       }
       // Resolve hash slots in place (klo becomes the slot index).
       uint32_t live = mask;
+      if constexpr (GM == G_HASHW) {
+        // keys of 3-4 words: 8 rows at a time (their words in registers), each column decoded once per chunk
+        for (int j0 = 0; j0 < 32; j0 += 8) {
+          if (!((mask >> j0) & 0xFFu)) continue;
+          uint64_t kw[8][kMaxKeyWords];
+#pragma unroll
+          for (int r = 0; r < 8; ++r)
+#pragma unroll
+            for (int w = 0; w < kMaxKeyWords; ++w) kw[r][w] = 0;
+          for (int g = 0; g < Q.num_gcols; ++g) {
+            const int c = Q.gcol[g];
+            uint32_t v[32];
+            decode_dyn(S.bits[c], S.fwd[c], lane_chunk, v);
+            const int32_t* rm = S.remap[c];
+            const int sh = Q.gshift[g], wd = Q.ghi[g];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              uint32_t x = v[j0 + r];
+              if (rm && ((mask >> (j0 + r)) & 1u)) x = static_cast<uint32_t>(rm[x]);
+#pragma unroll
+              for (int w = 0; w < kMaxKeyWords; ++w)
+                if (w == wd) kw[r][w] |= static_cast<uint64_t>(x) << sh;
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int j = j0 + r;
+            if (!((mask >> j) & 1u)) continue;
+            int64_t sl;
+            if (Q.key_words == 3) {
+              const uint64_t k3[3] = {kw[r][0], kw[r][1], kw[r][2]};
+              sl = hash_slotw<3>(Q, k3);
+            } else {
+              const uint64_t k4[4] = {kw[r][0], kw[r][1], kw[r][2], kw[r][3]};
+              sl = hash_slotw<4>(Q, k4);
+            }
+            if (sl < 0) live &= ~(1u << j);
+            klo[j] = static_cast<uint64_t>(sl);
+          }
+        }
+        if (live != mask) atomicAdd(Q.overflow, static_cast<unsigned long long>(__popc(mask & ~live)));
+      }
       if constexpr (GM == G_HASH64 || GM == G_HASH128) {
 #pragma unroll
         for (int j = 0; j < 32; ++j) {
@@ -426,7 +501,7 @@ __global__ void __launch_bounds__(kBlock) pgx_scan_kernel(const KQuery Q, int64_
         }
         if (live != mask) atomicAdd(Q.overflow, static_cast<unsigned long long>(__popc(mask & ~live)));
       }
-      const uint64_t stride = (GM == G_DENSE_LDS || GM == G_DENSE_GLOBAL) ? Q.dense_slots : Q.hash_cap;
+      const uint64_t stride = (GM == G_DENSE_LDS || GM == G_DENSE_GLOBAL) ? Q.dense_slots : Q.hash_cap;  // (HASHW too)
 #pragma unroll
       for (int j = 0; j < 32; ++j)
         if ((live >> j) & 1u) {
@@ -2207,6 +2282,11 @@ extern "C" hipError_t pgx_launch_scan(const pgx::KQuery* q, int grid, int64_t ti
       break;
     case pgx::G_HASH128:
       hipLaunchKernelGGL(pgx::pgx_scan_kernel<pgx::G_HASH128>, dim3(grid), dim3(pgx::kBlock), lds_bytes, stream, *q,
+                         tiles_per_wg);
+      break;
+    case pgx::G_HASHW:
+      if (q->key_words < 3 || q->key_words > pgx::kMaxKeyWords) return hipErrorInvalidValue;
+      hipLaunchKernelGGL(pgx::pgx_scan_kernel<pgx::G_HASHW>, dim3(grid), dim3(pgx::kBlock), lds_bytes, stream, *q,
                          tiles_per_wg);
       break;
     default:

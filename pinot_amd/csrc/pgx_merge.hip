@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256) pgx_group_compact(const unsigned long lon
   }
 }
 
-// Hash-table keys of the compacted slots (kw words per key): the host reads back only the live groups' keys.  n_dev
+// Hash-table keys of the compacted slots (kw <= 4 words per key): the host reads back only the live groups' keys.  n_dev
 // (optional): the compaction's group counter -- min(*n_dev, n) keys are gathered.
 __global__ void __launch_bounds__(256) pgx_gather_keys(const unsigned long long* __restrict__ keys,
                                                        const int64_t* __restrict__ slot,
@@ -223,7 +223,7 @@ extern "C" hipError_t pgx_launch_gather_keys(const unsigned long long* keys, con
                                              const unsigned long long* n_dev, int64_t n, int kw, unsigned long long* out,
                                              hipStream_t stream) {
   if (n <= 0) return hipSuccess;
-  if (kw < 1 || kw > 2) return hipErrorInvalidValue;
+  if (kw < 1 || kw > 4) return hipErrorInvalidValue;
   const unsigned grid = static_cast<unsigned>(n / 256 + 1 < 16384 ? n / 256 + 1 : 16384);
   hipLaunchKernelGGL(pgx::pgx_gather_keys, dim3(grid), dim3(256), 0, stream, keys, slot, n_dev, n, kw, out);
   return hipGetLastError();

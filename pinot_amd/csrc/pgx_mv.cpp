@@ -228,8 +228,9 @@ void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, in
       sh += P.gbits[g];
     }
     K.group_mode = hi ? G_HASH128 : G_HASH64;
+    K.key_words = hi ? 2 : 1;
   } else {
-    fail(PGX_ERR_UNSUPPORTED, "group key wider than 126 bits");
+    fail(PGX_ERR_UNSUPPORTED, "multi-value group-by: group key wider than 126 bits");
   }
   const bool dense = K.group_mode == G_DENSE_GLOBAL;
   K.num_aggs = na;

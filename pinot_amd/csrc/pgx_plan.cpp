@@ -843,21 +843,23 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
       const size_t lds = size_t(prod) * K.num_planes * 8;
       K.group_mode = (lds <= 48 * 1024) ? G_DENSE_LDS : G_DENSE_GLOBAL;
       if (K.group_mode == G_DENSE_LDS) P.lds_bytes = lds;
-    } else if (total_bits <= 126) {
-      int sh = 0;
-      bool hi = false;
+    } else {
+      // LONG_MAP / ARRAY_MAP keys: the columns' id fields packed into 64-bit words, a field never straddling two
+      // words (63 bits per word).  Wider than two words (DefaultGroupKeyGenerator.java:168-173: ARRAY_MAP takes any
+      // key width): up to kMaxKeyWords words on the generic kernel (G_HASHW).
+      int sh = 0, w = 0;
       for (int g = 0; g < K.num_gcols; ++g) {
-        if (!hi && sh + P.gbits[g] > 63) {
-          hi = true;
+        if (sh + P.gbits[g] > 63) {
+          ++w;
           sh = 0;
         }
         K.gshift[g] = sh;
-        K.ghi[g] = hi;
+        K.ghi[g] = w;
         sh += P.gbits[g];
       }
-      K.group_mode = hi ? G_HASH128 : G_HASH64;
-    } else {
-      fail(PGX_ERR_UNSUPPORTED, "group key wider than 126 bits");
+      if (w + 1 > kMaxKeyWords) fail(PGX_ERR_UNSUPPORTED, "group key wider than 252 bits");
+      K.key_words = w + 1;
+      K.group_mode = w == 0 ? G_HASH64 : (w == 1 ? G_HASH128 : G_HASHW);
     }
   }
   K.num_qcols = int(P.qcols.size());
@@ -1098,6 +1100,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   P.use_docmask = q.kn.jit && (K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS ||
                                 K.group_mode == G_DENSE_GLOBAL || K.group_mode == G_HASH64 ||
                                 K.group_mode == G_HASH128 || P.use_part) && K.num_qcols <= PGX_J_MAX_COLS;
+  // (G_HASHW keys stay on the generic kernel: the generated kernels hold two key words)
   if (!q.filter.empty()) {
     PNode root = build_tree(q, *segs[0]);
     const size_t L = q.leaf_col.size();

@@ -163,7 +163,7 @@ void plan_cache_purge(const pgx_query* q, const pgx_ctx* ctx) {
 // Plain plans, and partitioned plans (kept with their slabs / buckets and partitions: the same segments and bindings
 // give the same fills, so the first run's capacities hold; a replay that overflows anyway plans afresh)
 bool plan_cacheable(const ExecPlan& P) {
-  const bool hash = P.kq.group_mode == G_HASH64 || P.kq.group_mode == G_HASH128;
+  const bool hash = hash_mode(P.kq.group_mode);
   return (P.use_part || !hash) && P.part_cols.size() <= 1 && P.mv_items.empty() && !P.fsm_on && !P.mv_masks.p && !P.sel_buf.p &&
          !P.lmask_buf.p && !P.jit.empty();
 }
