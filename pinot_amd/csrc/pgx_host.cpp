@@ -396,8 +396,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
   const KQuery& K = P.kq;
   if (!P.kn.jit) return;
   if (!(K.group_mode == G_NONE || K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL || P.use_part ||
-        hash_mode(K.group_mode)))
-    return;
+        K.group_mode == G_HASH64 || K.group_mode == G_HASH128))
+    return;  // (G_HASHW: keys of 3-4 words stay on the generic kernel)
   const int nc = K.num_qcols;
   if (nc > PGX_J_MAX_COLS) return;
   P.part_slab = slab;
@@ -623,12 +623,17 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         K.num_planes == 2 && K.num_aggs == 1 && (K.agg_kind[0] == A_SUM || K.agg_kind[0] == A_AVG) && !P.use_part) {
       const int c = K.agg_col[0];
       if (c >= 0 && J.cols[c].img != IMG_NONE && !J.cols[c].fp) {
-        int64_t maxdocs = 1;
+        int64_t maxdocs = 1, ntiles = 0;
         uint64_t vrange = 0;
+        const int64_t trows = int64_t(J.T) * J.TL;
         for (int sg : members) {
           maxdocs = std::max<int64_t>(maxdocs, P.ksegs[sg].num_docs);
           vrange = std::max<uint64_t>(vrange, P.segcols[sg][c]->vrange);
+          ntiles += (int64_t(P.ksegs[sg].num_docs) + trows - 1) / trows;
         }
+        // a workgroup flushes its table at every segment switch and walks at most ceil(tiles / CUs) tiles (the
+        // persistent grid has at least one workgroup per CU): the rows one flush covers are bounded by both
+        maxdocs = std::min<int64_t>(maxdocs, (ntiles + cus - 1) / cus * trows);
         const int cb = bits_for(maxdocs + 1);
         const long double sum_max = (long double)maxdocs * (long double)(vrange + 1);
         int sb = 0;
