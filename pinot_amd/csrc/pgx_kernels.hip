@@ -596,7 +596,27 @@ __device__ __forceinline__ unsigned int block_reserve(unsigned int* scan, unsign
 }
 
 // Emit occupied slots: out_slot[i] = slot index, out_planes[p*cap_out + i] = plane value.
-// One counter reservation per workgroup tile of 256 x 16 slots (block_reserve): a device atomic per occupied slot
+// Small tables (dense key spaces, <= 2^20 slots): one counter reservation per wavefront, lanes in slot order.
+__global__ void pgx_compact_wave(const unsigned long long* table, uint64_t slots, int num_planes,
+                                 unsigned long long* counter, int64_t* out_slot, unsigned long long* out_planes,
+                                 uint64_t cap_out) {
+  const int lane = threadIdx.x & 63;
+  for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); b < slots;
+       b += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t s = b + lane;
+    const bool live = s < slots && table[s] != 0;
+    const unsigned long long m = __ballot(live);
+    if (!m) continue;
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(counter, static_cast<unsigned long long>(__popcll(m)));
+    const unsigned long long i = __shfl(base, 0, 64) + __popcll(m & ((1ull << lane) - 1ull));
+    if (!live || i >= cap_out) continue;
+    out_slot[i] = static_cast<int64_t>(s);
+    for (int p = 0; p < num_planes; ++p) out_planes[p * cap_out + i] = table[p * slots + s];
+  }
+}
+
+// Large tables (hash tables, up to 2^27 slots): one counter reservation per workgroup tile of 256 x 16 slots (block_reserve): a device atomic per occupied slot
 // serialises on the counter (16.7M groups ~ 24 ms), and even one per wavefront costs ~11 ns each at one L2 address.
 __global__ void __launch_bounds__(256) pgx_compact(const unsigned long long* table, uint64_t slots, int num_planes,
                                                    unsigned long long* counter, int64_t* out_slot,
@@ -2310,6 +2330,12 @@ extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t
 extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
                                          unsigned long long* counter, int64_t* out_slot,
                                          unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream) {
+  if (slots <= (uint64_t(1) << 20)) {
+    const int grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>((slots + 255) / 256, 4096)));
+    hipLaunchKernelGGL(pgx::pgx_compact_wave, dim3(grid), dim3(256), 0, stream, table, slots, num_planes, counter,
+                       out_slot, out_planes, cap_out);
+    return hipGetLastError();
+  }
   int grid = static_cast<int>(std::min<uint64_t>((slots + 4095) / 4096, 4096));
   if (grid < 1) grid = 1;
   hipLaunchKernelGGL(pgx::pgx_compact, dim3(grid), dim3(256), 0, stream, table, slots, num_planes, counter, out_slot,
