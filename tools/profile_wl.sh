@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 WL=$1; STEPS=$2; shift 2
 PSTEPS=${PGX_PMC_STEPS:-4}
 KRX=${PGX_PMC_REGEX:-pgxq|pgx_roaring|pgx_part|pgx_narrow|pgx_trim|pgx_init|pgx_compact|pgx_group|pgx_fsm|pgx_mv|pgx_join|pgx_gather}
-KLIST=${PGX_PMC_KERNELS:-pgxq+pgx_roaring+pgx_partition+pgx_part_aggregate+pgx_narrow_split+pgx_narrow_aggregate+pgx_trim+pgx_init+pgx_compact+pgx_group+pgx_join+pgx_gather}
+KLIST=${PGX_PMC_KERNELS:-pgxq+pgx_roaring+pgx_partition+pgx_part_aggregate+pgx_narrow_split+pgx_narrow_aggregate+pgx_narrow_compact+pgx_trim+pgx_init+pgx_compact+pgx_group+pgx_join+pgx_gather}
 OUT=gpurun_out/prof_$WL
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/trace -o $WL --output-format csv -- \
