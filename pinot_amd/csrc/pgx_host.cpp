@@ -133,43 +133,50 @@ void launch_bitmaps(ExecPlan& P, hipStream_t st, int p0 = 0, int p1 = -1) {
     if (p1 < 0) p1 = int(P.rprogs.size());
     const int np = p1 - p0;
     const RProg* progs = P.rprog_dev + p0;
-    // wave-per-chunk kernel when every program has <= 64 bitmaps (one lane each) and <= 3 mask slots
-    const int rk = P.kn.rprog;  // PGX_RPROG: wave | seg | chunk | stack (default: the first that fits)
-    bool wave = rk == RPROG_AUTO || rk == RPROG_WAVE;
-    int nslots = 1;
-    for (size_t i = 0; i < P.rprogs.size() && wave; ++i) {
-      const RProg& r = P.rprogs[i];
-      int nb = 0;
-      for (int k = 0; k < r.nops; ++k)
-        if (r.op[k] == RP_LEAF && r.arg[k] >= 0) nb += P.roar[r.arg[k]].nb;
-      int ns = 0;
-      if (!rprog_wave_ok(r, &ns) || ns != rprog_slots(r)) wave = false;
-      if (nb > 64 || ns > 3) wave = false;
-      nslots = std::max(nslots, ns);
+    if (P.rp_kind < 0) {  // once per plan: the choice depends on the programs only
+      // wave-per-chunk kernel when every program has <= 64 bitmaps (one lane each) and <= 3 mask slots
+      const int rk = P.kn.rprog;  // PGX_RPROG: wave | seg | chunk | stack (default: the first that fits)
+      bool wave = rk == RPROG_AUTO || rk == RPROG_WAVE;
+      int nslots = 1;
+      for (size_t i = 0; i < P.rprogs.size() && wave; ++i) {
+        const RProg& r = P.rprogs[i];
+        int nb = 0;
+        for (int k = 0; k < r.nops; ++k)
+          if (r.op[k] == RP_LEAF && r.arg[k] >= 0) nb += P.roar[r.arg[k]].nb;
+        int ns = 0;
+        if (!rprog_wave_ok(r, &ns) || ns != rprog_slots(r)) wave = false;
+        if (nb > 64 || ns > 3) wave = false;
+        nslots = std::max(nslots, ns);
+      }
+      int maxleaves = 0;  // leaf masks the wide kernel keeps in LDS (PGX_RPROG=stack: the stack kernel)
+      if (!wave) {
+        for (const auto& dp : P.dm_progs) {
+          int nl = 0;
+          for (int8_t o : dp.op) nl += o == RP_LEAF;
+          maxleaves = std::max(maxleaves, nl);
+        }
+        if (rk == RPROG_STACK) maxleaves = 0;
+        // per-segment container walk when every program's bitmaps fit one lane each (PGX_RPROG=chunk: per-chunk kernels)
+        bool seg_walk = maxleaves >= 1 && rk != RPROG_CHUNK && rk != RPROG_STACK;
+        for (size_t i = 0; i < P.rprogs.size() && seg_walk; ++i) {
+          int nb = 0;
+          const RProg& r = P.rprogs[i];
+          for (int k = 0; k < r.nops; ++k)
+            if (r.op[k] == RP_LEAF && r.arg[k] >= 0) nb += P.roar[r.arg[k]].nb;
+          if (nb > 512) seg_walk = false;
+        }
+        if (seg_walk) maxleaves = -maxleaves;
+      }
+      P.rp_kind = wave ? 0 : 1;
+      P.rp_nslots = nslots;
+      P.rp_maxleaves = maxleaves;
     }
-    if (wave) {
-      PGX_LAUNCH(st, "pgx_roaring_program_wave", pgx_launch_roaring_program_wave(progs, P.rdesc_dev, np, P.roar_maxchunks, nslots, st),
+    if (P.rp_kind == 0) {
+      PGX_LAUNCH(st, "pgx_roaring_program_wave", pgx_launch_roaring_program_wave(progs, P.rdesc_dev, np, P.roar_maxchunks, P.rp_nslots, st),
                 "bitmap program launch");
       return;
     }
-    int maxleaves = 0;  // leaf masks the wide kernel keeps in LDS (PGX_RPROG=stack: the stack kernel)
-    for (const auto& dp : P.dm_progs) {
-      int nl = 0;
-      for (int8_t o : dp.op) nl += o == RP_LEAF;
-      maxleaves = std::max(maxleaves, nl);
-    }
-    if (rk == RPROG_STACK) maxleaves = 0;
-    // per-segment container walk when every program's bitmaps fit one lane each (PGX_RPROG=chunk: per-chunk kernels)
-    bool seg_walk = maxleaves >= 1 && rk != RPROG_CHUNK && rk != RPROG_STACK;
-    for (size_t i = 0; i < P.rprogs.size() && seg_walk; ++i) {
-      int nb = 0;
-      const RProg& r = P.rprogs[i];
-      for (int k = 0; k < r.nops; ++k)
-        if (r.op[k] == RP_LEAF && r.arg[k] >= 0) nb += P.roar[r.arg[k]].nb;
-      if (nb > 512) seg_walk = false;
-    }
-    if (seg_walk) maxleaves = -maxleaves;
-    PGX_LAUNCH(st, "pgx_roaring_program", pgx_launch_roaring_program(progs, P.rdesc_dev, np, P.roar_maxchunks, maxleaves, st),
+    PGX_LAUNCH(st, "pgx_roaring_program", pgx_launch_roaring_program(progs, P.rdesc_dev, np, P.roar_maxchunks, P.rp_maxleaves, st),
               "bitmap program launch");
   } else if (P.rdesc_dev) {
     PGX_LAUNCH(st, "pgx_roaring", pgx_launch_roaring(P.rdesc_dev, int(P.roar.size()), P.roar_maxchunks, st), "bitmap expansion launch");
@@ -190,7 +197,13 @@ void build_arena(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B) {
   B.off_rdesc = align_up(B.off_tiles + P.star_tile_cap * 4, 256);
   B.off_rprog = align_up(B.off_rdesc + P.roar.size() * sizeof(RDesc), 256);
   B.off_outs = align_up(B.off_rprog + P.rprogs.size() * sizeof(RProg), 256);
-  B.size = B.off_outs + kOutsBytes;
+  const KQuery& K0 = P.kq;
+  const uint64_t tbl = (K0.group_mode == G_DENSE_LDS || K0.group_mode == G_DENSE_GLOBAL) && !P.use_part
+                           ? P.dense_slots * uint64_t(K0.num_planes) * 8
+                           : 0;
+  B.tbl_bytes = tbl <= kArenaTableMax ? size_t(tbl) : 0;
+  B.tbl_live = false;
+  B.size = B.off_outs + kOutsBytes + B.tbl_bytes;
   B.arena = DevBuf(ctx, B.size);
   B.host = PinnedBuf(ctx, B.size);
   if (!P.blob32.empty()) std::memcpy(B.host.bytes(), P.blob32.data(), P.blob32.size() * 4);
@@ -322,12 +335,16 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
   K.table = nullptr;
   K.keys = nullptr;
   K.key_state = nullptr;
+  B.tbl_live = false;
   if (K.group_mode == G_DENSE_LDS || K.group_mode == G_DENSE_GLOBAL) {
     K.dense_slots = P.dense_slots;
     const uint64_t bytes = P.dense_slots * K.num_planes * 8;
     if (dense_out) {
       if (dense_out_bytes < bytes) fail(PGX_ERR_INVALID_ARG, "dense_out too small");
       K.table = static_cast<unsigned long long*>(dense_out);
+    } else if (bytes && B.tbl_bytes == bytes) {
+      K.table = reinterpret_cast<unsigned long long*>(B.dev() + B.off_outs + kOutsBytes);
+      B.tbl_live = true;
     } else {
       B.table = DevBuf(ctx, bytes);
       K.table = devp(B.table);
@@ -356,11 +373,20 @@ void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table,
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
   std::memset(outs, 0, kOutsBytes);
   for (int p = 1; p < K.num_planes; ++p) outs[p] = (K.plane_op[p] == P_MIN_ORD) ? ~0ull : 0ull;
+  const bool tbl = B.tbl_live && init_table;  // the in-arena dense table travels with the outputs block
+  if (tbl) {
+    unsigned long long* t = outs + kOutsBytes / 8;
+    const uint64_t slots = P.dense_slots;
+    for (int p = 0; p < K.num_planes; ++p)
+      std::fill(t + p * slots, t + (p + 1) * slots, (K.plane_op[p] == P_MIN_ORD) ? ~0ull : 0ull);
+  }
   if (outs_only)
-    hip_check(hipMemcpyAsync(B.dev() + B.off_outs, outs, kOutsBytes, hipMemcpyHostToDevice, st), "outputs H2D");
+    hip_check(hipMemcpyAsync(B.dev() + B.off_outs, outs, kOutsBytes + (tbl ? B.tbl_bytes : 0), hipMemcpyHostToDevice,
+                             st),
+              "outputs H2D");
   else
     hip_check(hipMemcpyAsync(B.arena.p, B.host.p, B.size, hipMemcpyHostToDevice, st), "argument arena H2D");
-  if (init_table && K.group_mode != G_NONE && !P.use_part) {
+  if (init_table && K.group_mode != G_NONE && !P.use_part && !B.tbl_live) {
     const uint64_t slots = hash_mode(K.group_mode) ? P.hash_cap : P.dense_slots;
     const uint64_t kw = hash_mode(K.group_mode) ? uint64_t(K.key_words) * P.hash_cap : 0;
     PGX_LAUNCH(st, "pgx_init_planes", pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
@@ -835,6 +861,14 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
   KQuery& K = P.kq;
   unsigned long long* outs = reinterpret_cast<unsigned long long*>(B.host.bytes() + B.off_outs);
   const bool hash = hash_mode(K.group_mode);
+  if (!dense_host_override && B.tbl_live && K.num_gcols > 0 && !hash) {
+    // in-arena dense table: outputs and table in ONE read-back, occupied slots found on the host
+    hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes + B.tbl_bytes, hipMemcpyDeviceToHost, st),
+              "outputs + table D2H");
+    hip_check(hipStreamSynchronize(st), "sync");
+    prof_mark("f.sync");
+    dense_host_override = outs + kOutsBytes / 8;
+  }
   const bool dense_dev = K.num_gcols > 0 && !hash && !dense_host_override;
   // group-by compaction (occupied slots -> columnar), read back together with the outputs block: ONE sync
   const uint64_t slots = hash ? P.hash_cap : P.dense_slots;

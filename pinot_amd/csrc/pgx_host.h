@@ -932,6 +932,9 @@ struct ExecPlan {
   };
   std::vector<DmProg> dm_progs;
   std::vector<RProg> rprogs;              // [seg * nprogs + k]
+  // bitmap-program kernel choice, decided once per plan (launch_bitmaps; a replay must not walk 4096 programs again):
+  // -1 undecided, 0 the wave kernel (rp_nslots mask slots), 1 the wide kernel (rp_maxleaves)
+  int rp_kind = -1, rp_nslots = 1, rp_maxleaves = 0;
   const RProg* rprog_dev = nullptr;
   // numEntriesScannedInFilter automaton (pgx_stats.cpp) for filter trees whose statistic has no closed form
   bool fsm_on = false;
@@ -952,10 +955,15 @@ struct ExecPlan {
 constexpr double kRchunkMaxSel = 0.0;
 
 constexpr size_t kOutsBytes = 256;  // agg planes [0, 72), stats [128, 144), overflow [192, 200)
+// Dense group tables up to this size live in the argument arena right after the outputs block: the arena copy
+// initialises them and ONE read-back returns outputs and table (no init or compaction kernel; C1 / C4 latency)
+constexpr size_t kArenaTableMax = 64 * 1024;
 struct ExecBuffers {
   DevBuf arena;
   PinnedBuf host;
   size_t off_ksegs = 0, off_jsegs = 0, off_tiles = 0, off_rdesc = 0, off_rprog = 0, off_outs = 0, size = 0;
+  size_t tbl_bytes = 0;  // in-arena dense table at off_outs + kOutsBytes (0: none)
+  bool tbl_live = false;  // this execution's table is the in-arena one (alloc_outputs)
   DevBuf table, keys, key_state, masks;
   uint8_t* dev() const { return arena.as<uint8_t>(); }
 };

@@ -1401,6 +1401,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
   }
   // per (segment, bitmap program): the program over that segment's leaf descriptors and its output mask
   P.rprogs.clear();
+  P.rp_kind = -1;
   if (P.rprog_on) {
     const size_t np = P.dm_progs.size();
     P.rprogs.resize(size_t(n) * np);
