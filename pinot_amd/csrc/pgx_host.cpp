@@ -720,7 +720,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         js.vbase[c] = col.vbase;
       }
       js.emit_rebase = !(P.use_part && P.part_vcol >= 0) ? 0
-                       : P.part_fp ? P.part_fbase[size_t(s)]  // the segment's dictionary in the concatenation
+                       : (P.part_fp || (P.part_narrow && P.narrow_img == 5))
+                           ? P.part_fbase[size_t(s)]  // the segment's dictionary in the concatenation / value table
                                    : P.segcols[s][P.part_vcol]->vbase - P.part_vbase;
       if (P.rprog_on)
         for (size_t k = 0; k < P.dm_progs.size(); ++k)

@@ -239,6 +239,7 @@ struct Knobs {
   bool jit = true;
   bool narrow = true;
   bool narrow_direct = false;  // PGX_PART_NARROW=direct
+  bool narrow_gather = false;  // PGX_PART_NARROW=gather (tests): value-table records (IMG 5) where they fit
   int rchunk = -1;          // -1: planner's choice
   int rprog = RPROG_AUTO;
   int batch_segs = -1;      // -1: default (512; 0 with PGX_X_THROUGHPUT)

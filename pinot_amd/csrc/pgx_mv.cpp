@@ -219,7 +219,8 @@ void run_mv_group(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, in
     int sh = 0;
     bool hi = false;
     for (int g = 0; g < ng; ++g) {
-      if (!hi && sh + P.gbits[g] > 63) {
+      if (sh + P.gbits[g] > 63) {  // a field never straddles two words; each word keeps <= 63 bits
+        if (hi) fail(PGX_ERR_UNSUPPORTED, "multi-value group-by: group key needs more than two 63-bit words");
         hi = true;
         sh = 0;
       }

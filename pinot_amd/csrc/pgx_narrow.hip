@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "pgx_internal.h"
 
 #define PGX_GLOBAL __attribute__((address_space(1)))
@@ -249,7 +251,11 @@ __global__ void __launch_bounds__(kN2Threads) pgx_narrow_split(const uint32_t* _
 // the probing loop (insert by CAS, then neighbouring buckets).  The record's value field is a dictId whose value the
 // workgroup's LDS image holds (IMG 1: u32 value - vbase per dictId, 2: FOR16 = 64 u32 block bases + u16 offset per
 // dictId), or the dictId of a MIN / MAX-only column looked up in vdict at the flush (IMG 0), or the value offset itself
-// (IMG 3: value - vbase; no image, so the LDS holds only the tables and more wavefronts fit a CU).
+// (IMG 3: value - vbase; no image, so the LDS holds only the tables and more wavefronts fit a CU), or the value's index
+// in a table of the query's distinct dictionaries in global memory (L2-resident; segments with their own dictionaries,
+// c3d / c3f): IMG 5 gathers value - vbase (u32) and then aggregates as IMG 3, IMG 6 gathers the double and keeps count,
+// f64 sum (LDS f64 add) and ordered-f64 min / max per slot (pgx_part_aggregate_f64's planes).  The gathers of batch i + 1
+// are issued while batch i is aggregated.
 // ctr: [0] groups appended, [3] overflow (a table filled up, or more groups than ocap).
 // ---------------------------------------------------------------------------------------------------------------------
 constexpr int kNAWays = 4;
@@ -274,7 +280,7 @@ template <int IMG>
 __device__ __forceinline__ uint32_t na_img(const uint32_t* simg, int img_sh, uint32_t d) {
   if (IMG == 1) return simg[d];
   if (IMG == 2) return simg[d >> img_sh] + static_cast<uint32_t>(reinterpret_cast<const uint16_t*>(simg + 64)[d]);
-  if (IMG == 3) return d;
+  if (IMG == 3 || IMG == 5) return d;
   if (IMG == 4) {
     const int sh = img_sh & 31, b = (img_sh >> 5) & 31, nb = img_sh >> 10;
     const uint32_t bp = d * static_cast<uint32_t>(b);
@@ -292,7 +298,7 @@ __device__ __forceinline__ int na_way(const na_u32x4 k, uint32_t key) {
 // W: u32 words per record (pgx_narrow_split<W>); W = 2 carries value offsets wider than the 32-bit record leaves room
 // for (IMG 3 only): 512 records per batch instead of 1024, the same 4 KiB per wavefront.
 template <int IMG, bool SUM, bool MN, bool MX, int W>
-__global__ void __launch_bounds__(na_threads<IMG>()) __attribute__((amdgpu_waves_per_eu(IMG >= 3 ? 4 : 1)))
+__global__ void __launch_bounds__(na_threads<IMG>()) __attribute__((amdgpu_waves_per_eu(IMG >= 5 ? 2 : (IMG >= 3 ? 4 : 1))))
 pgx_narrow_aggregate(
     const uint32_t* __restrict__ in, const unsigned int* __restrict__ cnt2, int64_t cap2, int nparts, int rb2,
     uint64_t kmask, uint64_t ic1, int ms, int64_t vbase, const uint32_t* __restrict__ img, int img_words,
@@ -303,12 +309,21 @@ pgx_narrow_aggregate(
   constexpr int kNAWaves = kNAThreads / 64;
   constexpr bool LIMG = IMG == 1 || IMG == 2 || IMG == 4;  // an image in LDS
   constexpr bool BIG = IMG == 1 || IMG == 2;               // 512 threads, two waves per SIMD: wider batches
-  constexpr int NR = 16 / W;                               // records per lane per batch
+  constexpr bool GATHER = IMG >= 5;                         // values gathered from a global table (img)
+  constexpr bool F64 = IMG == 6;                            // ... doubles: count, f64 sum, ordered-f64 min / max
+  constexpr bool PIPE3 = BIG || GATHER;                     // three batches in registers
+  constexpr int LQ = 4;                                    // 16-byte loads per lane per batch (GATHER in half
+                                                           // batches at four waves per SIMD measured slower)
+  constexpr int BW = 4 * LQ;                               // u32 words per lane per batch
+  constexpr int NR = BW / W;                               // records per lane per batch
   constexpr uint32_t BATCH = 64u * NR;
+  typedef typename std::conditional<F64, unsigned long long, uint32_t>::type MT;  // min / max slot type
+  typedef typename std::conditional<F64, double, uint32_t>::type GT;              // gathered value type
   __shared__ __attribute__((aligned(16))) uint32_t simg[LIMG ? (IMG == 4 ? kNAImg4Words : kNAImgWords) : 1];
   __shared__ __attribute__((aligned(16))) uint32_t tkey[kNAWaves * kNASlots];
   __shared__ unsigned long long tsc[kNAWaves * kNASlots];
-  __shared__ uint32_t tmn[MN ? kNAWaves * kNASlots : 1], tmx[MX ? kNAWaves * kNASlots : 1];
+  __shared__ uint32_t tcn[F64 ? kNAWaves * kNASlots : 1];
+  __shared__ MT tmn[MN ? kNAWaves * kNASlots : 1], tmx[MX ? kNAWaves * kNASlots : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (LIMG) {
@@ -317,15 +332,18 @@ pgx_narrow_aggregate(
   }
   for (int i = tid; i < kNAWaves * kNASlots; i += kNAThreads) {
     tkey[i] = kNAEmpty;
-    tsc[i] = 0ull;
-    if (MN) tmn[i] = 0xFFFFFFFFu;
-    if (MX) tmx[i] = 0u;
+    tsc[i] = 0ull;  // (F64: the bits of 0.0)
+    if (F64) tcn[i] = 0u;
+    if (MN) tmn[i] = static_cast<MT>(~0ull);
+    if (MX) tmx[i] = static_cast<MT>(0);
   }
   __syncthreads();  // the only workgroup barrier: wavefronts run independently from here on
   uint32_t* K = tkey + wave * kNASlots;
   unsigned long long* S = tsc + wave * kNASlots;
-  uint32_t* N = tmn + (MN ? wave * kNASlots : 0);
-  uint32_t* X = tmx + (MX ? wave * kNASlots : 0);
+  MT* N = tmn + (MN ? wave * kNASlots : 0);
+  MT* X = tmx + (MX ? wave * kNASlots : 0);
+  uint32_t* C = tcn + (F64 ? wave * kNASlots : 0);
+  const PGX_GLOBAL GT* gtab = (const PGX_GLOBAL GT*)img;  // GATHER: the value table
   const uint32_t rmask = rb2 >= 32 ? 0xFFFFFFFFu : (1u << rb2) - 1u;
   // home bucket of key bits r2 < 2^rb2: (r2 * kNABuckets) >> rb2, as one 32-bit high multiply
   const int hsh = rb2 >= 1 ? 32 - rb2 : 31;
@@ -339,10 +357,10 @@ pgx_narrow_aggregate(
   const PGX_GLOBAL int64_t* vd = (const PGX_GLOBAL int64_t*)vdict;
   bool lost = false;
 
-  auto load = [&](int pp, uint32_t i0, uint32_t nn, uint32_t (&buf)[16]) {
+  auto load = [&](int pp, uint32_t i0, uint32_t nn, uint32_t (&buf)[BW]) {
     const int64_t base = ((static_cast<int64_t>(pp) * cap2 + i0) * W) >> 2;  // cap2 and i0 are multiples of 4
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < LQ; ++q) {
       const uint32_t e = static_cast<uint32_t>(q * (256 / W) + lane * (4 / W));
       na_u32x4 x = {0u, 0u, 0u, 0u};
       if (i0 + e < nn) x = __builtin_nontemporal_load(src + base + q * 64 + lane);
@@ -375,7 +393,8 @@ pgx_narrow_aggregate(
   // counter for every partition's reservation serialised 2^18 atomics at C3 (~11 ns each at one L2 address, ~2.9 ms);
   // pgx_narrow_compact packs the regions afterwards.
   constexpr int Q = kNASlots / 64;
-  uint32_t fk[Q], fn_[Q], fx[Q], fhas = 0, fexcl = 0;
+  uint32_t fk[Q], fcn[F64 ? Q : 1], fhas = 0, fexcl = 0;
+  MT fn_[Q], fx[Q];
   unsigned long long fbase = 0ull, cursor = 0ull;  // (wave-uniform) rows this wavefront has written
   unsigned long long fsc[Q];
   int fp = -1;
@@ -399,12 +418,22 @@ pgx_narrow_aggregate(
         uint64_t y = (static_cast<uint64_t>(fp) << rb2) | fk[q];
         y ^= y >> ms;
         wkey[o] = (y * ic1) & kmask;
+        if constexpr (F64) {  // planes as pgx_part_aggregate_f64: count, f64 sum bits, ordered min / max
+          wpl[o] = fcn[q];
+          wpl[rstride + o] = fsc[q];
+          wpl[2 * rstride + o] = MN ? static_cast<uint64_t>(fn_[q]) : ~0ull;
+          wpl[3 * rstride + o] = MX ? static_cast<uint64_t>(fx[q]) : 0ull;
+          ++o;
+          continue;
+        }
         const uint64_t c = fsc[q] >> cshift;
         wpl[o] = c;  // plane 0: doc count; planes 1..3: int64 sum, ordered min, ordered max (pgx_part_aggregate)
         wpl[rstride + o] = static_cast<uint64_t>(static_cast<int64_t>(fsc[q] & smask) + static_cast<int64_t>(c) * vbase);
         int64_t vlo = 0, vhi = 0;
-        if (MN) vlo = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, fn_[q])) : vd[fn_[q]];
-        if (MX) vhi = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, fx[q])) : vd[fx[q]];
+        if (MN) vlo = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, static_cast<uint32_t>(fn_[q])))
+                          : vd[static_cast<uint32_t>(fn_[q])];
+        if (MX) vhi = IMG ? vbase + static_cast<int64_t>(na_img<IMG>(simg, img_sh, static_cast<uint32_t>(fx[q])))
+                          : vd[static_cast<uint32_t>(fx[q])];
         wpl[2 * rstride + o] = static_cast<uint64_t>(vlo) ^ 0x8000000000000000ull;
         wpl[3 * rstride + o] = static_cast<uint64_t>(vhi) ^ 0x8000000000000000ull;
         note(0, c);
@@ -425,13 +454,17 @@ pgx_narrow_aggregate(
       const int s = q * 64 + lane;
       fk[q] = K[s];
       fsc[q] = S[s];
-      fn_[q] = MN ? N[s] : 0u;
-      fx[q] = MX ? X[s] : 0u;
+      if constexpr (F64) {
+        fcn[q] = C[s];
+        C[s] = 0u;
+      }
+      fn_[q] = MN ? N[s] : static_cast<MT>(0);
+      fx[q] = MX ? X[s] : static_cast<MT>(0);
       fhas |= (fk[q] != kNAEmpty ? 1u : 0u) << q;
       K[s] = kNAEmpty;
       S[s] = 0ull;
-      if (MN) N[s] = 0xFFFFFFFFu;
-      if (MX) X[s] = 0u;
+      if (MN) N[s] = static_cast<MT>(~0ull);
+      if (MX) X[s] = static_cast<MT>(0);
     }
     const uint32_t mine = __popc(fhas);
     uint32_t incl = mine;
@@ -461,28 +494,60 @@ pgx_narrow_aggregate(
   // (four waves per SIMD -- no image, or the packed image of 1024-thread workgroups: two batches and groups of 4
   // records, so 128 VGPRs hold a wavefront)
   constexpr int HB = BIG ? 8 : 4;  // records resolved together
-  uint32_t b0[16], b1[16], b2[BIG ? 16 : 1];
+  uint32_t b0[BW], b1[BW], b2[PIPE3 ? BW : 1];
+  GT g0[GATHER ? NR : 1], g1[GATHER ? NR : 1];  // GATHER: the values of batches b0 and b1
+  auto field = [&](uint64_t R) -> uint32_t {  // the value field: dictId, value offset or table index
+    return rb2 >= 32 && W == 1 ? 0u : static_cast<uint32_t>(R >> rb2);
+  };
+  auto recb = [&](const uint32_t (&buf)[BW], int jj) -> uint64_t {
+    return W == 1 ? static_cast<uint64_t>(buf[jj])
+                  : static_cast<uint64_t>(buf[2 * jj]) | (static_cast<uint64_t>(buf[2 * jj + 1]) << 32);
+  };
+  auto gather = [&](const uint32_t (&buf)[BW], GT (&g)[GATHER ? NR : 1]) {
+    if constexpr (GATHER) {
+#pragma unroll
+      for (int jj = 0; jj < NR; ++jj) {
+        // a batch's last 16-byte load may hold up to three stale words past the partition's records: their index is
+        // clamped into the table (the records themselves are never aggregated)
+        const uint32_t ix = field(recb(buf, jj));
+        g[jj] = gtab[ix < static_cast<uint32_t>(img_words) ? ix : 0u];
+      }
+    }
+  };
   Pos c{static_cast<int>(blockIdx.x) * kNAWaves + wave, 0u, 0u};
   c.n = count(c.p);
   if (c.p < nparts) load(c.p, c.i0, c.n, b0);
   Pos d = advance(c);
-  if constexpr (BIG) {
+  if constexpr (PIPE3) {
     if (d.p < nparts) load(d.p, d.i0, d.n, b1);
   }
+  if (c.p < nparts) gather(b0, g0);
   while (c.p < nparts) {
     const Pos e = advance(d);
-    if constexpr (BIG) {
+    if constexpr (PIPE3) {
       if (e.p < nparts) load(e.p, e.i0, e.n, b2);
     } else {
       if (d.p < nparts) load(d.p, d.i0, d.n, b1);
     }
+    if (d.p < nparts) gather(b1, g1);
     const bool full = c.i0 + BATCH <= c.n;  // every record of the batch is the partition's
-    auto rec = [&](int jj) -> uint64_t {  // record jj of this lane's batch
-      return W == 1 ? static_cast<uint64_t>(b0[jj])
-                    : static_cast<uint64_t>(b0[2 * jj]) | (static_cast<uint64_t>(b0[2 * jj + 1]) << 32);
-    };
-    auto field = [&](uint64_t R) -> uint32_t {  // the value field: dictId or value offset
-      return rb2 >= 32 && W == 1 ? 0u : static_cast<uint32_t>(R >> rb2);
+    auto rec = [&](int jj) -> uint64_t { return recb(b0, jj); };  // record jj of this lane's batch
+    // one record into slot: count (+ value), min / max
+    auto accumulate = [&](int slot, uint32_t v, uint32_t dd, GT gv) {
+      if constexpr (F64) {
+        atomicAdd(&C[slot], 1u);
+        if (SUM) atomicAdd(reinterpret_cast<double*>(&S[slot]), gv);
+        if (MN || MX) {
+          const uint64_t b = static_cast<uint64_t>(__double_as_longlong(gv));
+          const unsigned long long o = (b & 0x8000000000000000ull) ? ~b : (b | 0x8000000000000000ull);
+          if (MN) atomicMin(&N[slot], o);
+          if (MX) atomicMax(&X[slot], o);
+        }
+      } else {
+        atomicAdd(&S[slot], SUM ? one + v : one);
+        if (MN) atomicMin(&N[slot], dd);
+        if (MX) atomicMax(&X[slot], dd);
+      }
     };
 #pragma unroll
     for (int h = 0; h < NR / HB; ++h) {  // groups of HB records: home buckets and values read back to back
@@ -495,7 +560,9 @@ pgx_narrow_aggregate(
         const uint32_t r2 = static_cast<uint32_t>(R) & rmask;
         const uint32_t b = home(r2);
         kb[j] = *reinterpret_cast<const na_u32x4*>(K + b * kNAWays);
-        val[j] = SUM ? na_img<IMG>(simg, img_sh, field(R)) : 0u;
+        if constexpr (GATHER && !F64) val[j] = g0[jj];
+        else if constexpr (!GATHER) val[j] = SUM ? na_img<IMG>(simg, img_sh, field(R)) : 0u;
+        else val[j] = 0u;
       }
       uint32_t miss = 0u;  // records of this group whose key is not in its home bucket (yet)
 #pragma unroll
@@ -506,15 +573,12 @@ pgx_narrow_aggregate(
         const bool valid = full || c.i0 + ei < c.n;  // (full: a wave-uniform flag, no per-record compare)
         const uint64_t R = rec(jj);
         const uint32_t r2 = static_cast<uint32_t>(R) & rmask;
-        const uint32_t dd = field(R);
+        const uint32_t dd = GATHER && !F64 ? val[j] : field(R);
         const uint32_t b = home(r2);
         const int m = na_way(kb[j], r2);
         if (valid && m < 0) miss |= 1u << j;
         if (!valid || m < 0) continue;
-        const int slot = static_cast<int>(b) * kNAWays + m;
-        atomicAdd(&S[slot], SUM ? one + val[j] : one);
-        if (MN) atomicMin(&N[slot], dd);
-        if (MX) atomicMax(&X[slot], dd);
+        accumulate(static_cast<int>(b) * kNAWays + m, val[j], dd, g0[GATHER ? jj : 0]);
       }
       // The misses (a group's first record, ~1 in 60 at C3: some lane of the wave misses at most j) probe together:
       // each pass resolves every lane's next missed record, so the wave pays one probe chain per pass instead of
@@ -525,22 +589,22 @@ pgx_narrow_aggregate(
         miss &= miss - 1u;
         uint64_t R = 0u;
         uint32_t v = 0u;
+        GT gv = GT(0);
 #pragma unroll
         for (int j = 0; j < HB; ++j)
           if (j == js) {
             R = rec(h * HB + j);
             v = val[j];
+            gv = g0[GATHER ? h * HB + j : 0];
           }
         const uint32_t r2 = static_cast<uint32_t>(R) & rmask;
-        const uint32_t dd = field(R);
+        const uint32_t dd = GATHER && !F64 ? v : field(R);
         const int slot = probe(r2, home(r2));
         if (slot < 0) {
           lost = true;
           continue;
         }
-        atomicAdd(&S[slot], SUM ? one + v : one);
-        if (MN) atomicMin(&N[slot], dd);
-        if (MX) atomicMax(&X[slot], dd);
+        accumulate(slot, v, dd, gv);
       }
     }
     if (d.p != c.p) {  // partition c.p is complete
@@ -548,9 +612,13 @@ pgx_narrow_aggregate(
       flush_begin(c.p);
     }
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < BW; ++j) {
       b0[j] = b1[j];
-      if constexpr (BIG) b1[j] = b2[j];
+      if constexpr (PIPE3) b1[j] = b2[j];
+    }
+    if constexpr (GATHER) {
+#pragma unroll
+      for (int j = 0; j < NR; ++j) g0[j] = g1[j];
     }
     c = d;
     d = e;
@@ -664,13 +732,18 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
   uint64_t* rplane = scratch + rstride;
   unsigned long long* wcount = reinterpret_cast<unsigned long long*>(scratch + 5 * rstride);
   if (rb2 < 0 || rb2 > 31 || keybits < 1 || keybits > 64 || cap2 < 4 || (cap2 & 3) || cshift < 1 || cshift > 63 ||
-      grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 4 ||
+      grid < 1 || !in || !cnt2 || !okey || !oplane || !ctr || img_kind < 0 || img_kind > 6 ||
       ((img_kind == 1 || img_kind == 2) && (!img || img_words < 1 || img_words > pgx::kNAImgWords)) ||
-      (img_kind == 4 && (!img || img_words < 1 || img_words > pgx::kNAImg4Words)) || (need_sum && !img_kind) ||
-      ((need_min || need_max) && !img_kind && !vdict) || (wide && img_kind != 3))
+      (img_kind == 4 && (!img || img_words < 1 || img_words > pgx::kNAImg4Words)) ||
+      (img_kind >= 5 && (!img || img_words < 1)) || (need_sum && !img_kind) ||
+      ((need_min || need_max) && !img_kind && !vdict) || (wide && img_kind != 3 && img_kind < 5) ||
+      (img_kind == 6 && prange))
     return hipErrorInvalidValue;
   const pgx::NarrowMix m = pgx::narrow_mix(keybits);
-  const int sel = (wide ? 5 : img_kind) * 8 + (need_sum ? 4 : 0) + (need_min ? 2 : 0) + (need_max ? 1 : 0);
+  // kernel: image kinds 0-4 (32-bit records), 5 = IMG 3 on 64-bit records, 6 / 7 = IMG 5 on 32 / 64-bit records,
+  // 8 / 9 = IMG 6 on 32 / 64-bit records
+  const int kk = img_kind <= 4 ? (wide ? 5 : img_kind) : (img_kind == 5 ? 6 : 8) + (wide ? 1 : 0);
+  const int sel = kk * 8 + (need_sum ? 4 : 0) + (need_min ? 2 : 0) + (need_max ? 1 : 0);
 #define PGX_NA_CASE(C, I, A, B, D)                                                                                   \
   case C:                                                                                                            \
     hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D, 1>), dim3(grid), dim3(pgx::na_threads<I>()), 0, stream, in, \
@@ -693,21 +766,28 @@ extern "C" hipError_t pgx_launch_narrow_aggregate(const uint32_t* in, const unsi
     PGX_NA_CASES(2)
     PGX_NA_CASES(3)
     PGX_NA_CASES(4)
-#define PGX_NA_CASE_W(C, A, B, D)                                                                                    \
+#define PGX_NA_CASE_IW(C, I, Wd, A, B, D)                                                                            \
   case C:                                                                                                            \
-    hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<3, A, B, D, 2>), dim3(grid), dim3(pgx::na_threads<3>()), 0, stream, \
+    hipLaunchKernelGGL((pgx::pgx_narrow_aggregate<I, A, B, D, Wd>), dim3(grid), dim3(pgx::na_threads<I>()), 0, stream, \
                        in, cnt2, cap2, nparts, rb2, m.mask, m.ic1, m.s, vbase, img, img_words, img_sh, vdict, cshift,  \
                        rkey, rplane, wcap, rstride, wcount, ctr, prange);                                            \
     break;
-    PGX_NA_CASE_W(40, false, false, false)
-    PGX_NA_CASE_W(41, false, false, true)
-    PGX_NA_CASE_W(42, false, true, false)
-    PGX_NA_CASE_W(43, false, true, true)
-    PGX_NA_CASE_W(44, true, false, false)
-    PGX_NA_CASE_W(45, true, false, true)
-    PGX_NA_CASE_W(46, true, true, false)
-    PGX_NA_CASE_W(47, true, true, true)
-#undef PGX_NA_CASE_W
+#define PGX_NA_CASES_IW(K, I, Wd)                          \
+  PGX_NA_CASE_IW(K * 8 + 0, I, Wd, false, false, false) \
+  PGX_NA_CASE_IW(K * 8 + 1, I, Wd, false, false, true)  \
+  PGX_NA_CASE_IW(K * 8 + 2, I, Wd, false, true, false)  \
+  PGX_NA_CASE_IW(K * 8 + 3, I, Wd, false, true, true)   \
+  PGX_NA_CASE_IW(K * 8 + 4, I, Wd, true, false, false)  \
+  PGX_NA_CASE_IW(K * 8 + 5, I, Wd, true, false, true)   \
+  PGX_NA_CASE_IW(K * 8 + 6, I, Wd, true, true, false)   \
+  PGX_NA_CASE_IW(K * 8 + 7, I, Wd, true, true, true)
+    PGX_NA_CASES_IW(5, 3, 2)
+    PGX_NA_CASES_IW(6, 5, 1)
+    PGX_NA_CASES_IW(7, 5, 2)
+    PGX_NA_CASES_IW(8, 6, 1)
+    PGX_NA_CASES_IW(9, 6, 2)
+#undef PGX_NA_CASES_IW
+#undef PGX_NA_CASE_IW
     default:
       return hipErrorInvalidValue;
   }

@@ -244,10 +244,14 @@ void narrow_prepare(ExecPlan& P, NarrowBuffers& NB, hipStream_t st) {
 // After the scan: the second split and the aggregation.
 void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStream_t st) {
   if (P.rec_total == 0) return;
-  hip_check(hipMemsetAsync(NB.prange.p, 0xFF, 32, st), "range minima");
-  hip_check(hipMemsetAsync(static_cast<uint8_t*>(NB.prange.p) + 32, 0, 32, st), "range maxima");
+  if (P.narrow_img == 6) NB.prange = DevBuf();  // f64 planes: the trim finds its key ranges itself
+  if (NB.prange.p) {
+    hip_check(hipMemsetAsync(NB.prange.p, 0xFF, 32, st), "range minima");
+    hip_check(hipMemsetAsync(static_cast<uint8_t*>(NB.prange.p) + 32, 0, 32, st), "range maxima");
+  }
   unsigned long long* ctr = devp(NB.ctr);
-  // an LDS image allows one workgroup per CU (512 threads; 1024 for the packed image), the tables alone four
+  // an LDS image allows one workgroup per CU (512 threads; 1024 for the packed image), the tables alone four (gathered
+  // values: one, two waves per SIMD for the registers of three batches and their values in flight)
   const int agg_grid = ctx->num_cus * (P.narrow_img == 3 ? 4 : 1);
   const int64_t sw = pgx_narrow_scratch_words(int(NB.nparts), P.narrow_img, agg_grid);
   if (NB.agg_scratch_words < sw) {
@@ -264,7 +268,7 @@ void narrow_enqueue(pgx_ctx* ctx, const ExecPlan& P, NarrowBuffers& NB, hipStrea
                                          NB.rb2, P.part_keybits, P.part_vbase, P.narrow_img, P.narrow_imgp,
                                          P.narrow_img_words, P.narrow_img_sh, P.part_vdict, P.part_sum, P.part_min,
                                          P.part_max, NB.cshift, NB.okey.as<uint64_t>(), NB.oplane.as<uint64_t>(),
-                                         NB.ocap, ctr, devp(NB.prange), agg_grid, NB.agg_scratch.as<uint64_t>(),
+                                         NB.ocap, ctr, NB.prange.p ? devp(NB.prange) : nullptr, agg_grid, NB.agg_scratch.as<uint64_t>(),
                                          NB.agg_scratch_words, NB.w2 == 2, st),
              "narrow aggregate");
 }
@@ -372,7 +376,7 @@ bool replay_part(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, PartBuffers& PB, hip
 void narrow_fallback(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n, ExecPlan& P, ExecBuffers& B) {
   P.part_narrow = false;
   P.part_slab = false;
-  P.part_dictid = false;
+  P.part_dictid = P.part_fp;  // FLOAT / DOUBLE radix records carry the value's index too
   P.part_hi = nullptr;
   plan_jit(ctx, q, segs, n, P, B);
 }

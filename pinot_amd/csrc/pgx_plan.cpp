@@ -269,6 +269,7 @@ Knobs pgx::read_knobs() {
   k.jit = !(jit.size() && jit[0] == '0');
   k.narrow = !(nar.size() && nar[0] == '0');
   k.narrow_direct = nar == "direct";
+  k.narrow_gather = nar == "gather";
   if (rc.size()) k.rchunk = rc[0] == '1' ? 1 : 0;
   if (rp == "off") k.rprog = RPROG_OFF;
   else if (rp == "wave") k.rprog = RPROG_WAVE;
@@ -885,8 +886,45 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
     int keybits = 0;
     for (int g = 0; g < K.num_gcols; ++g) keybits = std::max(keybits, K.gshift[g] + P.gbits[g]);
     // one value column's settings into P (part_vcol ... narrow_vrange); false if the column does not qualify
+    // narrow record widths (pgx_narrow.hip): the scan's records hold rb1 = keybits - 8 key bits + a vd-bit value field
+    // (<= 48 bits); the second split's k2 bits leave rb1 - k2 key bits beside the field in 32 (or, wide, 64) bits
+    const int rb1 = keybits - kNarrow1Bits;
+    auto fits = [&](int vd, int& k2) {
+      k2 = std::max(0, rb1 + vd - 32);
+      if (rb1 - k2 > 31) k2 = rb1 - 31;
+      return rb1 + vd <= 48 && k2 <= kNarrowMaxBits2;
+    };
+    auto fits_wide = [&](int vd, int& k2) {
+      k2 = std::max(0, rb1 - 31);
+      return rb1 + vd <= 48 && vd <= 32 && k2 <= kNarrowMaxBits2;
+    };
+    // narrow records whose value field indexes a table of the query's distinct dictionaries in global memory (IMG 5:
+    // value - vbase as u32, IMG 6: doubles), gathered by the aggregation: per-segment dictionaries too large for the
+    // scan's LDS beside its rings
+    auto narrow_gather = [&](int img, int vd, const void* table, uint64_t entries) -> bool {
+      if (!q.kn.narrow || keybits <= kNarrow1Bits) return false;
+      int k2 = 0;
+      bool wide = false;
+      if (!fits(vd, k2)) {
+        if (!fits_wide(vd, k2)) return false;
+        wide = true;
+      }
+      P.part_narrow = true;
+      P.part_slab = true;
+      P.part_dictid = true;  // the scan emits dictId + the segment's place in the table (JSeg.emit_rebase)
+      P.narrow_vd = vd;
+      P.narrow_k2min = k2;
+      P.narrow_img = img;
+      P.narrow_wide = wide;
+      P.narrow_imgp = static_cast<const uint32_t*>(table);
+      P.narrow_img_words = int(std::min<uint64_t>(entries, 0x7FFFFFFF));
+      P.narrow_img_sh = 0;
+      return true;
+    };
     auto config = [&](int vc) -> bool {
       P.part_slab = P.part_dictid = P.part_narrow = P.part_fp = false;
+      P.narrow_img = 0;
+      P.narrow_wide = false;
       P.part_fdict = nullptr;
       P.part_fbase.clear();
       bool need_sum = false, need_min = false, need_max = false;
@@ -952,6 +990,8 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
           P.part_max = need_max;
           P.part_dictid = true;  // (the index, rebased per segment: JSeg.emit_rebase)
           P.part_vdict = nullptr;
+          P.narrow_vrange = 0;
+          narrow_gather(6, vbits, P.part_fdict, all.size());  // narrow records when they fit, else the radix path
           return true;
         }
       }
@@ -1003,18 +1043,7 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
         // Value field: the dictId looked up in an LDS image of the column (one sorted dictionary in every segment, an
         // image that fits the LDS), or the value offset itself (value - vbase, rebased per segment like the radix
         // records: per-segment dictionaries, no image, and no LDS spent on one -- PGX_PART_NARROW=direct prefers it)
-        const int rb1 = keybits - kNarrow1Bits;
-        auto fits = [&](int vd, int& k2) {
-          k2 = std::max(0, rb1 + vd - 32);
-          if (rb1 - k2 > 31) k2 = rb1 - 31;
-          return rb1 + vd <= 48 && k2 <= kNarrowMaxBits2;
-        };
-        // value offsets too wide for a 32-bit second-stage record (c3d: 16 key bits + 20 offset bits): 64-bit second-
-        // stage records instead of the 8-byte radix path's two full passes
-        auto fits_wide = [&](int vd, int& k2) {
-          k2 = std::max(0, rb1 - 31);
-          return rb1 + vd <= 48 && vd <= 32 && k2 <= kNarrowMaxBits2;
-        };
+        // (value offsets too wide for a 32-bit second-stage record take 64-bit ones: fits_wide)
         int vd = 0, imgk = 0, k2 = 0;
         bool nok = true, wide = false;
         if (vc >= 0) {
@@ -1036,7 +1065,9 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
             if (c.img_kind != IMG_NONE) scan_img = std::max<int64_t>(scan_img, int64_t(c.img_words) * 4);
           }
           const bool scan_fits = scan_img + (int64_t(1) << kNarrow1Bits) * kNarrowRing * 6 + 16 * 1024 <= 160 * 1024;
-          if ((!nok || q.kn.narrow_direct) && scan_fits && (direct || (vbits <= 32 && fits_wide(vbits, k2d)))) {
+          if (q.kn.narrow_gather) nok = false;
+          if (!q.kn.narrow_gather && (!nok || q.kn.narrow_direct) && scan_fits &&
+              (direct || (vbits <= 32 && fits_wide(vbits, k2d)))) {
             wide = !direct;
             nok = true;
             imgk = 3;
@@ -1058,6 +1089,50 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
               P.narrow_imgp = c0.shared->pk_img.as<uint32_t>();
               P.narrow_img_words = c0.shared->pk_words;
               P.narrow_img_sh = c0.shared->pk_sh;
+            }
+          } else if (vbits <= 32 && q.kn.narrow_gather) {
+            // (measured at c3d: 13.98 ms per step against 13.83 on the 8-byte radix path, whose records carry the value
+            // offsets the scan makes from each segment's image -- so the gather is the tests' option, not the default)
+            // per-segment dictionaries whose value offsets the scan cannot make (no room for the image beside its
+            // rings): the records carry the dictId's index in a u32 table of every distinct dictionary's value - vbase
+            // (IMG 5), gathered by the aggregation from L2
+            std::vector<uint32_t> all;
+            std::vector<int64_t> fbase(size_t(n), 0);
+            std::unordered_multimap<uint64_t, int> seen;
+            std::vector<int> first_of(size_t(n), -1);
+            uint64_t total = 0;
+            bool tok = true;
+            for (int s = 0; s < n && tok; ++s) {
+              const StagedColumn& c = segs[s]->col(P.qcols[vc]);
+              if (int64_t(c.ivals.size()) != int64_t(c.card)) tok = false;
+              const uint64_t dk = c.dict_hash ^ (uint64_t(c.card) << 40);
+              auto range = seen.equal_range(dk);
+              for (auto it = range.first; it != range.second && first_of[size_t(s)] < 0; ++it)
+                if (segs[it->second]->col(P.qcols[vc]).ivals == c.ivals) first_of[size_t(s)] = it->second;
+              if (first_of[size_t(s)] >= 0) continue;
+              first_of[size_t(s)] = s;
+              seen.emplace(dk, s);
+              total += c.ivals.size();
+              if (total > (uint64_t(1) << 31) || total * 4 > kPartMaxBytes / 8) tok = false;
+            }
+            if (tok && total > 0) {
+              all.reserve(size_t(total));
+              for (int s = 0; s < n; ++s) {
+                if (first_of[size_t(s)] != s) {
+                  fbase[size_t(s)] = fbase[size_t(first_of[size_t(s)])];
+                  continue;
+                }
+                fbase[size_t(s)] = int64_t(all.size());
+                for (int64_t v : segs[s]->col(P.qcols[vc]).ivals) all.push_back(uint32_t(uint64_t(v) - uint64_t(vbase)));
+              }
+              DevBuf buf(ctx, all.size() * 4);
+              hip_check(hipMemcpy(buf.p, all.data(), all.size() * 4, hipMemcpyHostToDevice), "value table H2D");
+              if (narrow_gather(5, bits_for(int64_t(all.size())), buf.p, all.size())) {
+                P.narrow_vrange = vrange;
+                P.part_fbase = std::move(fbase);
+                P.part_fdict_bufs.push_back(std::move(buf));
+                return true;
+              }
             }
           }
         } else {

@@ -185,7 +185,8 @@ def test_c3d_per_segment_dictionaries_vs_c_twin(ctx):
         N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
         kernels = json.loads(js.value.decode())["kernels"]
         # value offsets rebased per segment on the 8-byte radix records: the scan that would make narrow value-offset
-        # records needs each segment's 128 KiB image beside its record rings, more than the LDS holds
+        # records needs each segment's 128 KiB image beside its record rings, more than the LDS holds (narrow records
+        # with the values gathered from a global table, PGX_PART_NARROW=gather, measured no faster at c3d)
         assert "pgx_part_aggregate" in kernels and "pgx_scan_kernel" not in kernels, kernels
     finally:
         data.free()
@@ -208,8 +209,8 @@ def test_c3d_per_segment_dictionaries_vs_c_twin(ctx):
 
 def test_c3f_double_metric_vs_c_twin(ctx):
     """c3f: C3's keys and query over a DOUBLE metric whose dictionary differs per segment.  The records carry the
-    value's index in the concatenation of the two segments' dictionaries and the aggregation sums in f64
-    (pgx_part_aggregate_f64); two 40M-row segments, every group of their combine == the C twin's groups of both,
+    value's index in the concatenation of the two segments' dictionaries and the aggregation gathers the doubles and
+    sums in f64 (narrow records, IMG 6); two 40M-row segments, every group of their combine == the C twin's groups of both,
     merged (values are multiples of 1/8 below 2^17: the sums are exact in any order)."""
     import ctypes as C
     import json
@@ -226,7 +227,8 @@ def test_c3f_double_metric_vs_c_twin(ctx):
         js = C.create_string_buffer(8192)
         N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
         kernels = json.loads(js.value.decode())["kernels"]
-        assert "pgx_part_aggregate_f64" in kernels and "pgx_scan_kernel" not in kernels, kernels
+        # narrow records, the doubles gathered from the concatenated dictionaries by the aggregation (IMG 6)
+        assert "pgx_narrow_aggregate" in kernels and "pgx_part_aggregate_f64" not in kernels, kernels
     finally:
         data.free()
     parts = [_c3_twin(wl, s, "m", rows) for s in (0, 1)]

@@ -51,14 +51,16 @@ def _execute(ctx, segs, q, flags):
         N.lib().pgx_result_release(r)
 
 
-@pytest.mark.parametrize("mode", ["narrow", "direct", "radix"])
+@pytest.mark.parametrize("mode", ["narrow", "direct", "gather", "radix"])
 @pytest.mark.parametrize("flt", FILTERS)
 @pytest.mark.parametrize("group", [" GROUP BY g2, a, c", " GROUP BY a, c, g1", " GROUP BY c, g2, s, g1"])
 def test_partitioned_matches_oracle(ctx, seg, flt, group, mode, monkeypatch):
     """Both sparse paths: narrow records (default: the scan's 256-way split, pgx_narrow_split, wavefront tables; the
     first two key shapes need records wider than 32 bits out of the scan, the u16 array; "direct": the records carry
-    value offsets instead of dictIds, PGX_PART_NARROW=direct) and the 8-byte radix path (PGX_PART_NARROW=0)."""
-    monkeypatch.setenv("PGX_PART_NARROW", {"narrow": "1", "direct": "direct", "radix": "0"}[mode])
+    value offsets instead of dictIds, PGX_PART_NARROW=direct; "gather": the records carry the dictId's index in a
+    global table of value offsets, gathered by the aggregation, PGX_PART_NARROW=gather) and the 8-byte radix path
+    (PGX_PART_NARROW=0)."""
+    monkeypatch.setenv("PGX_PART_NARROW", {"narrow": "1", "direct": "direct", "gather": "gather", "radix": "0"}[mode])
     gseg, oseg, fmt = seg
     q = pql.compile(AGGS + (flt % fmt) + group)
     blk, st = _run_inner(ctx, gseg, q)
@@ -317,8 +319,9 @@ def test_narrow_paths_and_fallback(ctx, monkeypatch, capfd, case):
         gseg.destroy()
 
 
-@pytest.mark.parametrize("metric", ["int_own_dict", "long_own_dict", "double", "double_uniform"])
-def test_partitioned_per_segment_metric_dictionaries(ctx, metric):
+@pytest.mark.parametrize("metric", ["int_own_dict", "int_gather", "long_own_dict", "double", "double_uniform",
+                                    "double_radix"])
+def test_partitioned_per_segment_metric_dictionaries(ctx, metric, monkeypatch):
     """VERDICT r4 missing #1: every segment builds its own metric dictionary (SegmentDictionaryCreator builds one per
     segment), so no two segments share a value image.  Integer metrics take a partitioned path with value offsets
     rebased per segment (JSeg.emit_rebase: one query-wide value base), not the global hash table -- the narrow records
@@ -326,7 +329,13 @@ def test_partitioned_per_segment_metric_dictionaries(ctx, metric):
     concatenation of the segments' dictionaries, aggregated in f64.  Groups (LONG_MAP key space > 2^22) and every function == the oracle's combine.
     "double_uniform" (ADVICE r5): non-dyadic doubles, whose f64 sums depend on the addition order -- the device adds
     with LDS atomics in arbitrary order, the reference in doc order -- so SUM / AVG are asserted to north_star's 1e-9
-    relative (COUNT / MIN / MAX stay exact)."""
+    relative (COUNT / MIN / MAX stay exact).  "int_gather": the integer records carry the dictId's index in a global
+    table of every segment's value offsets (IMG 5, PGX_PART_NARROW=gather); DOUBLE metrics run the narrow records with
+    the doubles gathered from the concatenated dictionaries (IMG 6), "double_radix" the 8-byte radix records."""
+    if metric == "int_gather":
+        monkeypatch.setenv("PGX_PART_NARROW", "gather")
+    elif metric == "double_radix":
+        monkeypatch.setenv("PGX_PART_NARROW", "0")
     import ctypes as C
     import json
 
@@ -340,7 +349,7 @@ def test_partitioned_per_segment_metric_dictionaries(ctx, metric):
         if metric == "double":
             m = rng.integers(-40000, 40000, size=n) / 8.0 + 0.125 * i
             types = {"m": "DOUBLE"}
-        elif metric == "double_uniform":
+        elif metric in ("double_uniform", "double_radix"):
             m = rng.uniform(-5000.0, 5000.0, size=n)
             types = {"m": "DOUBLE"}
         elif metric == "long_own_dict":
@@ -361,8 +370,10 @@ def test_partitioned_per_segment_metric_dictionaries(ctx, metric):
     js = C.create_string_buffer(8192)
     N.check(L.pgx_timing_stop(ctx.handle, out, js, len(js)))
     kernels = json.loads(js.value.decode())["kernels"]
-    if metric.startswith("double"):  # the concatenated dictionaries, f64 aggregation (pgx_part_aggregate_f64)
+    if metric == "double_radix":  # the concatenated dictionaries, f64 aggregation on the radix path
         assert "pgx_part_aggregate_f64" in kernels, kernels
+    elif metric.startswith("double"):  # narrow records, the doubles gathered by the aggregation (IMG 6)
+        assert "pgx_narrow_aggregate" in kernels and "pgx_part_aggregate_f64" not in kernels, kernels
     else:  # value offsets on the narrow records (no shared image: IMG 3, direct values) -- 32-bit offsets of LONG
         # values ride 64-bit second-stage records (narrow_wide) instead of the 8-byte radix path
         assert "pgx_narrow_aggregate" in kernels and "pgx_part_aggregate" not in kernels, kernels
@@ -481,12 +492,16 @@ def test_several_value_columns_trim_on_device(ctx):
             assert v == exp[k][col], (i, fn, k, v, exp[k])
 
 
-def test_partitioned_double_and_int_value_columns(ctx):
+@pytest.mark.parametrize("mode", ["narrow", "radix"])
+def test_partitioned_double_and_int_value_columns(ctx, mode, monkeypatch):
     """A DOUBLE metric with its own dictionary in every segment beside an INT metric: the DOUBLE column's records
     carry its index in the concatenated dictionaries (JSeg.emit_rebase = the segment's place), aggregated in f64
     (pgx_part_aggregate_f64); the INT column runs its own pass and the two join by key.  Every group == the oracle's
-    (f64 sums to 1e-12 relative: the device adds in another order), statistics too."""
+    (f64 sums to 1e-12 relative: the device adds in another order), statistics too.  Narrow records (the doubles
+    gathered by the aggregation) or the 8-byte radix records (PGX_PART_NARROW=0)."""
     from pinot_amd import engine as E
+    if mode == "radix":
+        monkeypatch.setenv("PGX_PART_NARROW", "0")
     rng = np.random.default_rng(91)
     gsegs, osegs = [], []
     for i in range(3):
@@ -500,7 +515,8 @@ def test_partitioned_double_and_int_value_columns(ctx):
         osegs.append(og)
     q = pql.compile("SELECT SUM(d), MIN(d), MAX(d), AVG(d), SUM(m), COUNT(*) FROM t WHERE k > 90 GROUP BY x, k")
     blk, kernels = _kernels_of(ctx, lambda: E.InstancePlanMakerImplV2(ctx).make_inter_segment_plan(gsegs, q).execute())
-    assert "pgx_part_aggregate_f64" in kernels and "pgx_join" in kernels, kernels
+    agg = "pgx_narrow_aggregate" if mode == "narrow" else "pgx_part_aggregate_f64"
+    assert agg in kernels and "pgx_join" in kernels, kernels
     o = H.oracle_answer(osegs, q, literal=True)
     m = blk.get_aggregation_group_by_result().as_map()
     assert 10000 < len(o["map"]) < 20000
@@ -511,12 +527,16 @@ def test_partitioned_double_and_int_value_columns(ctx):
     assert blk.stats.as_list() == list(o["stats"])
 
 
-def test_double_value_column_trim_on_device(ctx):
+@pytest.mark.parametrize("mode", ["narrow", "radix"])
+def test_double_value_column_trim_on_device(ctx, mode, monkeypatch):
     """Combine trim over > 20,000 groups of a DOUBLE metric on the partitioned path: SUM / AVG keys read the f64 sum
     plane (TK_SUMF / TK_AVGF), MIN / MAX the ordered-f64 planes; the 5,000 best of each, every kept group with its own
-    value."""
+    value.  Narrow records with gathered doubles (no key ranges from the aggregation: the trim finds them) or the radix
+    path."""
     from pinot_amd import engine as E
     from pinot_amd import native as N
+    if mode == "radix":
+        monkeypatch.setenv("PGX_PART_NARROW", "0")
     gseg, raw = _pairs_segment(ctx, 300000, 3000, seed=79)
     raw2 = dict(raw)
     raw2["m"] = raw["md"]
@@ -532,7 +552,7 @@ def test_double_value_column_trim_on_device(ctx):
     q = pql.compile("SELECT SUM(md), MAX(md), AVG(md) FROM t GROUP BY ga, gb")
     qq = E._Query(ctx, q)
     r, kernels = _kernels_of(ctx, lambda: qq.execute([gseg]))
-    assert "pgx_part_aggregate_f64" in kernels, kernels
+    assert ("pgx_narrow_aggregate" if mode == "narrow" else "pgx_part_aggregate_f64") in kernels, kernels
     try:
         maps = E.trimmed_maps(qq, r, [gseg])
     finally:
