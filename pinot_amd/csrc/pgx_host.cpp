@@ -792,7 +792,7 @@ void launch_scan(ExecPlan& P, hipStream_t st) {
                      P.rprogs.size() == P.ksegs.size() * P.dm_progs.size() && P.ctx_side && !P.use_part;
     if (two) {
       ExecPlan::JitGroup& G = P.jit[0];
-      const int n = int(G.segs.size()), h = n / 2;
+      const int n = int(G.segs.size()), h = std::max(1, n / P.kn.lone_head);
       const int ph = h * int(P.dm_progs.size());
       hip_check(hipEventRecord(P.ev_pre.get(), st), "event");
       hip_check(hipStreamWaitEvent(P.ctx_side, P.ev_pre.get(), 0), "event wait");

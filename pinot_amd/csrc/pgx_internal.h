@@ -243,6 +243,7 @@ struct Knobs {
   int rchunk = -1;          // -1: planner's choice
   int rprog = RPROG_AUTO;
   int batch_segs = -1;      // -1: default (512; 0 with PGX_X_THROUGHPUT)
+  int lone_head = 2;        // PGX_DEBUG head=N: a lone replay's first part is 1/N of the segments (A/B)
   bool part_small = false;  // PGX_DEBUG part_small
   int narrow_k2 = -1;       // PGX_DEBUG narrow_k2=N
   bool narrow_log = false;  // PGX_DEBUG narrow_log
