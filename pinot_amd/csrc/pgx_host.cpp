@@ -585,7 +585,9 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       // 64 holds the unflushed unit plus the sub-step's records with a wide margin): 512 threads, eight rows per lane
       // (fractional loads of widths that need it), half tiles (16 rows per lane) so the raw words of the next tile stay
       // in registers without spilling (1024 threads and 16 or 32 rows per lane measured slower).
-      J.T = 512;
+      // (PGX_DEBUG nunit=16: 16-record units in 32-record rings, 256 threads -- ~8 records per bucket per sub-step
+      // -- so two workgroups share a CU)
+      J.T = P.kn.narrow_unit == 16 ? 256 : 512;
       const int nr = 8, ntl = 16;
       if (nr < J.R) {
         J.R = nr;
@@ -641,6 +643,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       J.part_slab = P.part_slab;
       J.part_narrow = P.part_narrow;
       J.narrow_vbits = P.part_narrow ? P.narrow_vd : 0;
+      J.narrow_unit = P.kn.narrow_unit;
     }
     J.dense_slots = P.dense_slots;
     // COUNT + one integer SUM / AVG over a dense LDS table: one packed 64-bit add per row when, for every segment of

@@ -220,7 +220,7 @@ constexpr int kLdsBudget = 160 * 1024 - 256;  // static LDS of one workgroup, mi
 // Shared by the generated scan (pgx_jit.cpp), the split / aggregation kernels and the host.
 constexpr uint64_t kNarrowC1 = 0x9E3779B1ull;
 constexpr int kNarrow1Bits = 8;      // first split (inside the scan): 256 buckets
-constexpr int kNarrowRing = 64;      // scan: per-bucket LDS ring of records (two 32-record units)
+constexpr int kNarrowRing = 64;      // scan: per-bucket LDS ring of records (two 32-record units; the largest ring)
 constexpr int kNarrowMaxBits2 = 10;  // second split (pgx_narrow_split): up to 1024 sub-buckets per bucket
 // Environment knobs (A/B switches and test hooks), read ONCE per query by pgx_query_compile and kept with the query:
 // planning and execution read them from there, never from the environment (no per-query walk of environ, no race
@@ -243,6 +243,7 @@ struct Knobs {
   int rchunk = -1;          // -1: planner's choice
   int rprog = RPROG_AUTO;
   int batch_segs = -1;      // -1: default (512; 0 with PGX_X_THROUGHPUT)
+  int narrow_unit = 32;     // PGX_DEBUG nunit=16: 16-record units (32-record rings: two scan workgroups per CU)
   int lone_head = 2;        // PGX_DEBUG head=N: a lone replay's first part is 1/N of the segments (A/B)
   bool part_small = false;  // PGX_DEBUG part_small
   int narrow_k2 = -1;       // PGX_DEBUG narrow_k2=N
@@ -321,6 +322,7 @@ struct JitShape {
   // (the record's low half) plus, when it is wider than 32 bits, a u16 (bits 32..47) in a second array
   bool part_narrow = false;
   int narrow_vbits = 0;
+  int narrow_unit = 32;   // records per unit that leaves the scan's rings (ring: two units per bucket)
 };
 
 // ----- numEntriesScannedInFilter automaton (pgx_stats.cpp builds it, pgx_kernels.hip pgx_fsm_* runs it) -----

@@ -137,14 +137,15 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const int nrb1 = s.keybits - s.part_bits;  // narrow: bits of the key's mix left in the record
   const bool nhib = enarrow && nrb1 + s.narrow_vbits > 32;
   const int pnb = 1 << s.part_bits;
+  const int NU = s.narrow_unit, NRG = 2 * s.narrow_unit;  // narrow: records per unit, ring records per bucket
   // (narrow: pnb = 256 and T a multiple of 256 -- plan_jit's choices; four owner wavefronts hold one bucket per lane)
   int nring_off = -1, nringb_off = -1, nst_off = -1;
   if (enarrow) {
     lds = (lds + 15) & ~15;  // 16-byte ring reads and writes
     nring_off = lds;
-    lds += pnb * kNarrowRing * 4;
+    lds += pnb * NRG * 4;
     nringb_off = lds;
-    if (nhib) lds += pnb * kNarrowRing * 2;
+    if (nhib) lds += pnb * NRG * 2;
     // cursors[256], unflushed-unit starts[2][256], ring-valid-from[2][256], unit lists (u16 bucket, u32 position)
     // [4][128] each, list counts[4]
     nst_off = lds;
@@ -959,7 +960,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       // beyond that (a key-skewed sub-step) is stored straight to the slab, and the ring's copy of positions below V
       // (ring-valid-from) is ignored.  Two buffers of U and V: the owners write the next sub-step's while this one's
       // are read.
-      const std::string NR = std::to_string(kNarrowRing);
+      const std::string NR = std::to_string(NRG), NUs = std::to_string(NU);
       e.ln("{");
       e.ln("  u32 pp[PR];");
       e.ln("  #pragma unroll");
@@ -970,8 +971,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("  if (tid < 256) {");
       e.ln("    const u32 en = ncur[tid], u0 = Ucur[tid], v0 = Vcur[tid];");
       e.ln("    const u32 lim = u0 + ", NR, "u;");
-      e.ln("    const u32 nu = (((en < lim) ? en : lim) - u0) >> 5;");
-      e.ln("    nU[(npar ^ 1) * 256 + tid] = en & ~31u;");
+      e.ln("    const u32 nu = (((en < lim) ? en : lim) - u0) / ", NUs, "u;");
+      e.ln("    nU[(npar ^ 1) * 256 + tid] = en & ~", NU - 1, "u;");
       e.ln("    nV[(npar ^ 1) * 256 + tid] = en > lim ? en : v0;");
       e.ln("    u32 incl = nu;");
       e.ln("    #pragma unroll");
@@ -982,7 +983,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("    const int w = tid >> 6;");
       e.ln("    for (u32 q = 0, k = incl - nu; q < nu; ++q, ++k) {");
       e.ln("      nlb[w * 128 + k] = (unsigned short)tid;");
-      e.ln("      nlp[w * 128 + k] = u0 + 32u * q;");
+      e.ln("      nlp[w * 128 + k] = u0 + ", NUs, "u * q;");
       e.ln("    }");
       e.ln("    if (lane == 63) nlc[w] = incl;");
       e.ln("  }");
@@ -992,8 +993,8 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("      const u32 b = (u32)(recs[j] >> 56);");
       e.ln("      const u32 pos = pp[j];");
       e.ln("      if (pos < Ucur[b] + ", NR, "u) {");
-      e.ln("        ringA[b * ", NR, "u + (pos & ", kNarrowRing - 1, "u)] = (u32)recs[j];");
-      if (nhib) e.ln("        ringB[b * ", NR, "u + (pos & ", kNarrowRing - 1, "u)] = (unsigned short)(recs[j] >> 32);");
+      e.ln("        ringA[b * ", NR, "u + (pos & ", NRG - 1, "u)] = (u32)recs[j];");
+      if (nhib) e.ln("        ringB[b * ", NR, "u + (pos & ", NRG - 1, "u)] = (unsigned short)(recs[j] >> 32);");
       e.ln("      } else if (pos < (u32)A.part_cap) {  // past the ring (key skew): straight to the slab");
       e.ln("        const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)pos;");
       e.ln("        poutA[o] = (u32)recs[j];");
@@ -1001,21 +1002,22 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       e.ln("      }");
       e.ln("    }");
       e.ln("  pgx_lds_barrier();");
-      // eight lanes per unit, 16 bytes each (u32: 8 x 4 records; u16: the first 4 lanes x 8 records); a unit
-      // holding positions below V (after a skewed sub-step) goes record by record
+      // NU / 4 lanes per unit, 16 bytes each (u32: 4 records per lane; u16: the first NU / 8 lanes x 8 records); a
+      // unit holding positions below V (after a skewed sub-step) goes record by record
+      const int LPU = NU / 4, UPW = 64 / LPU;  // lanes per unit, units per wavefront instruction
       e.ln("  {");
-      e.ln("    const int w = tid >> 6, l = w & 3, g = lane & 7;");
+      e.ln("    const int w = tid >> 6, l = w & 3, g = lane & ", LPU - 1, ";");
       e.ln("    const int cnt = (int)nlc[l];");
-      e.ln("    for (int k = (w >> 2) * 8 + (lane >> 3); k < cnt; k += 8 * (PT / 256)) {");
+      e.ln("    for (int k = (w >> 2) * ", UPW, " + (lane / ", LPU, "); k < cnt; k += ", UPW, " * (PT / 256)) {");
       e.ln("      const u32 b = nlb[l * 128 + k];");
       e.ln("      const u32 u = nlp[l * 128 + k];");
       e.ln("      if (u >= (u32)A.part_cap) continue;");
       e.ln("      const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)u;");
-      e.ln("      const u32 rs = b * ", NR, "u + (u & ", kNarrowRing - 1, "u);");
+      e.ln("      const u32 rs = b * ", NR, "u + (u & ", NRG - 1, "u);");
       e.ln("      if (u >= Vcur[b]) {");
       e.ln("        *(PGX_G pgx_u32x4*)(poutA + o + 4 * g) = *(const pgx_u32x4*)(ringA + rs + 4 * g);");
       if (nhib)
-        e.ln("        if (g < 4) *(PGX_G pgx_u32x4*)(poutB + o + 8 * g) = *(const pgx_u32x4*)(ringB + rs + 8 * g);");
+        e.ln("        if (g < ", NU / 8, ") *(PGX_G pgx_u32x4*)(poutB + o + 8 * g) = *(const pgx_u32x4*)(ringB + rs + 8 * g);");
       e.ln("      } else {");
       e.ln("        for (int q = 0; q < 4; ++q) {");
       e.ln("          const u32 x = 4 * g + q;");
@@ -1172,14 +1174,14 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ln("}");
   }
   if (enarrow) {  // the rings' last partial units, then the slab fills (every record, also past part_cap)
-    const std::string NR = std::to_string(kNarrowRing);
-    e.ln("for (int x = tid; x < 256 * 32; x += PT) {");
-    e.ln("  const u32 b = (u32)x >> 5;");
-    e.ln("  const u32 i = nU[npar * 256 + b] + ((u32)x & 31u);");
+    const std::string NR = std::to_string(NRG);
+    e.ln("for (int x = tid; x < 256 * ", NU, "; x += PT) {");
+    e.ln("  const u32 b = (u32)x / ", NU, "u;");
+    e.ln("  const u32 i = nU[npar * 256 + b] + ((u32)x & ", NU - 1, "u);");
     e.ln("  if (i < ncur[b] && i >= nV[npar * 256 + b] && i < (u32)A.part_cap) {");
     e.ln("    const long long o = ((long long)b * A.part_nwg + wsl) * A.part_cap + (long long)i;");
-    e.ln("    poutA[o] = ringA[b * ", NR, "u + (i & ", kNarrowRing - 1, "u)];");
-    if (nhib) e.ln("    poutB[o] = ringB[b * ", NR, "u + (i & ", kNarrowRing - 1, "u)];");
+    e.ln("    poutA[o] = ringA[b * ", NR, "u + (i & ", NRG - 1, "u)];");
+    if (nhib) e.ln("    poutB[o] = ringB[b * ", NR, "u + (i & ", NRG - 1, "u)];");
     e.ln("  }");
     e.ln("}");
     e.ln("for (int i = tid; i < 256; i += PT) {");
@@ -1260,6 +1262,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.selmask);
   k.push_back(s.part_narrow);
   k.push_back(s.narrow_vbits);
+  k.push_back(s.narrow_unit);
   add(s.ghi);
   k.push_back(s.hash_slots);
   return k;

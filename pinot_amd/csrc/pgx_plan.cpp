@@ -286,6 +286,7 @@ Knobs pgx::read_knobs() {
     else if (o == "narrow_log") k.narrow_log = true;
     else if (o == "host_profile") k.host_profile = true;
     else if (o.rfind("narrow_k2=", 0) == 0) k.narrow_k2 = std::atoi(o.c_str() + 10);
+    else if (o == "nunit=16") k.narrow_unit = 16;
     else if (o.rfind("head=", 0) == 0) k.lone_head = std::max(2, std::atoi(o.c_str() + 5));
     i = j + 1;
   }
@@ -1065,7 +1066,8 @@ void plan_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int 
             const StagedColumn& c = segs[s]->col(P.qcols[vc]);
             if (c.img_kind != IMG_NONE) scan_img = std::max<int64_t>(scan_img, int64_t(c.img_words) * 4);
           }
-          const bool scan_fits = scan_img + (int64_t(1) << kNarrow1Bits) * kNarrowRing * 6 + 16 * 1024 <= 160 * 1024;
+          const bool scan_fits =
+              scan_img + (int64_t(1) << kNarrow1Bits) * (2 * q.kn.narrow_unit) * 6 + 16 * 1024 <= 160 * 1024;
           if (q.kn.narrow_gather) nok = false;
           if (!q.kn.narrow_gather && (!nok || q.kn.narrow_direct) && scan_fits &&
               (direct || (vbits <= 32 && fits_wide(vbits, k2d)))) {
