@@ -644,6 +644,7 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       J.part_narrow = P.part_narrow;
       J.narrow_vbits = P.part_narrow ? P.narrow_vd : 0;
       J.narrow_unit = P.kn.narrow_unit;
+      J.prefetch2 = P.part_narrow && P.kn.prefetch2;
     }
     J.dense_slots = P.dense_slots;
     // COUNT + one integer SUM / AVG over a dense LDS table: one packed 64-bit add per row when, for every segment of
@@ -1454,6 +1455,9 @@ void run_query(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n
     hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "D2H");
     hip_check(hipStreamSynchronize(st), "sync");
     if (outs[24] == 0) break;
+    if (P.kn.narrow_log)  // (PGX_DEBUG=narrow_log: which path ran, and why)
+      std::fprintf(stderr, "[pgx hash] overflow %llu at %llu slots (attempt %d)\n", outs[24],
+                   (unsigned long long)P.hash_cap, attempt);
     P.hash_cap = std::max(P.hash_cap * 4, hash_est);  // table full: grow and rerun
     if (attempt == 5) fail(PGX_ERR_OOM, "group-by hash table overflow");
   }

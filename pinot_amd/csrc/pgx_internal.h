@@ -243,6 +243,7 @@ struct Knobs {
   int rchunk = -1;          // -1: planner's choice
   int rprog = RPROG_AUTO;
   int batch_segs = -1;      // -1: default (512; 0 with PGX_X_THROUGHPUT)
+  bool prefetch2 = false;   // PGX_DEBUG pf2: narrow scans load two tiles ahead (A/B)
   int narrow_unit = 32;     // PGX_DEBUG nunit=16: 16-record units (32-record rings: two scan workgroups per CU)
   int lone_head = 2;        // PGX_DEBUG head=N: a lone replay's first part is 1/N of the segments (A/B)
   bool part_small = false;  // PGX_DEBUG part_small
@@ -323,6 +324,7 @@ struct JitShape {
   bool part_narrow = false;
   int narrow_vbits = 0;
   int narrow_unit = 32;   // records per unit that leaves the scan's rings (ring: two units per bucket)
+  bool prefetch2 = false; // raw words of tiles tt+1 AND tt+2 in flight (no gate leaf): twice the bytes in flight
 };
 
 // ----- numEntriesScannedInFilter automaton (pgx_stats.cpp builds it, pgx_kernels.hip pgx_fsm_* runs it) -----

@@ -475,11 +475,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     return s.R == 32 ? w : "((" + w + " >> (r0 & 31)) & " + std::to_string((1u << s.R) - 1u) + "u)";
   };
   // software-pipelined tile loop: raw words of tile tt+1 are loaded while tile tt is computed
-  auto emit_loads = [&](const std::string& tile, const std::string& dst) {
+  auto emit_loads = [&](const std::string& tile, const std::string& dst, const std::string& rbv = "rbn") {
     e.ln("{");
     e.ind++;
-    e.ln("rbn = (int)((tl ? (long long)tl[", tile, " - tile0] : (", tile, " - tile0)) * (PT * PTL));");
-    e.ln("const int rb = rbn;");
+    e.ln(rbv, " = (int)((tl ? (long long)tl[", tile, " - tile0] : (", tile, " - tile0)) * (PT * PTL));");
+    e.ln("const int rb = ", rbv, ";");
     e.ln("const bool full = rb + PT * PTL <= nd;");
     for (int u = 0; u < U; ++u) {
       e.ln("{");
@@ -519,10 +519,18 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ind--;
     e.ln("}");
   };
+  // (prefetch2, no gate leaf: a second buffer set m* holds tile tt+2)
+  const bool pf2 = s.prefetch2 && gate < 0;
   for (int c = 0; c < ncols; ++c)
-    if (s.cols[c].decode) e.ln("u32 n", c, "[", U * dwords_per(s, c), "];");
+    if (s.cols[c].decode) {
+      e.ln("u32 n", c, "[", U * dwords_per(s, c), "];");
+      if (pf2) e.ln("u32 m", c, "[", U * dwords_per(s, c), "];");
+    }
   for (int l = 0; l < nleaves; ++l)
-    if (is_docmask(s.leaf_mode[l])) e.ln("u32 nq", l, "[", U, "];");
+    if (is_docmask(s.leaf_mode[l])) {
+      e.ln("u32 nq", l, "[", U, "];");
+      if (pf2) e.ln("u32 mq", l, "[", U, "];");
+    }
   // first row of the tile whose raw words are in flight: carried into the next iteration, so the loop body never
   // reloads the tile list after issuing the prefetch (that load's wait would also wait for the prefetch)
   e.ln("int rbn;");
@@ -531,6 +539,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     emit_gate_loads("t", "ga");
   }
   emit_loads("t", "n");
+  if (pf2) {
+    e.ln("int rbm = 0;");
+    e.ln("if (t + 1 < t2)");
+    emit_loads("t + 1", "m", "rbm");
+  }
   if (gate >= 0) {
     e.ln("if (t + 1 < t2)");
     emit_gate_loads("t + 1", "gn");
@@ -562,6 +575,20 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     emit_gate_loads("tt + 2", "gn");
     e.ind--;
     e.ln("}");
+  } else if (pf2) {  // tile tt+1's words moved up; tile tt+2's load now
+    for (int c = 0; c < ncols; ++c) {
+      if (!s.cols[c].decode) continue;
+      e.ln("#pragma unroll");
+      e.ln("for (int i = 0; i < ", U * dwords_per(s, c), "; ++i) n", c, "[i] = m", c, "[i];");
+    }
+    for (int l = 0; l < nleaves; ++l)
+      if (is_docmask(s.leaf_mode[l])) {
+        e.ln("#pragma unroll");
+        e.ln("for (int i = 0; i < ", U, "; ++i) nq", l, "[i] = mq", l, "[i];");
+      }
+    e.ln("rbn = rbm;");
+    e.ln("if (tt + 2 < t2) ");
+    emit_loads("tt + 2", "m", "rbm");
   } else {
     e.ln("if (tt + 1 < t2) ");
     emit_loads("tt + 1", "n");
@@ -1263,6 +1290,7 @@ std::vector<int64_t> shape_key(const JitShape& s, int device) {
   k.push_back(s.part_narrow);
   k.push_back(s.narrow_vbits);
   k.push_back(s.narrow_unit);
+  k.push_back(s.prefetch2);
   add(s.ghi);
   k.push_back(s.hash_slots);
   return k;
