@@ -537,6 +537,8 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
       const int w = words(J.R);
       while (J.TL > J.R && 2 * (J.TL / J.R) * w > kTileWordBudget) J.TL /= 2;
     }
+    if (P.kn.no_img && !P.use_part)
+      for (JitCol& C : J.cols) C.img = IMG_NONE;
     // LDS budget: drop the largest images until everything fits (LEAF_RCHUNK: a budget for three workgroups per CU)
     int64_t rch_bytes = 0;
     if (P.rchunk) {

@@ -243,6 +243,7 @@ struct Knobs {
   int rchunk = -1;          // -1: planner's choice
   int rprog = RPROG_AUTO;
   int batch_segs = -1;      // -1: default (512; 0 with PGX_X_THROUGHPUT)
+  bool no_img = false;      // PGX_DEBUG noimg: query kernels gather values from the dictionaries, no LDS images (A/B)
   bool prefetch2 = false;   // PGX_DEBUG pf2: narrow scans load two tiles ahead (A/B)
   int narrow_unit = 32;     // PGX_DEBUG nunit=16: 16-record units (32-record rings: two scan workgroups per CU)
   int lone_head = 2;        // PGX_DEBUG head=N: a lone replay's first part is 1/N of the segments (A/B)

@@ -288,6 +288,7 @@ Knobs pgx::read_knobs() {
     else if (o.rfind("narrow_k2=", 0) == 0) k.narrow_k2 = std::atoi(o.c_str() + 10);
     else if (o == "nunit=16") k.narrow_unit = 16;
     else if (o == "pf2") k.prefetch2 = true;
+    else if (o == "noimg") k.no_img = true;
     else if (o.rfind("head=", 0) == 0) k.lone_head = std::max(2, std::atoi(o.c_str() + 5));
     i = j + 1;
   }
