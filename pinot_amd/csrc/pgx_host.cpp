@@ -346,14 +346,22 @@ void alloc_outputs(pgx_ctx* ctx, ExecPlan& P, ExecBuffers& B, void* dense_out, u
       K.table = reinterpret_cast<unsigned long long*>(B.dev() + B.off_outs + kOutsBytes);
       B.tbl_live = true;
     } else {
-      B.table = DevBuf(ctx, bytes);
+      if (!B.table.p || B.table_bytes != bytes) {  // (a kept plan reuses its table: clean after a resetting compaction)
+        B.table = DevBuf(ctx, bytes);
+        B.table_bytes = bytes;
+        B.table_clean = false;
+      }
       K.table = devp(B.table);
     }
   } else if (P.use_part && !P.part_slab) {
+    B.table_bytes = 0;
+    B.table_clean = false;
     B.table = DevBuf(ctx, std::max<int64_t>(P.rec_total, 1) * 8);  // one key|value record per scanned row
     K.table = devp(B.table);
   } else if (hash_mode(K.group_mode)) {
     K.hash_cap = P.hash_cap;
+    B.table_bytes = 0;
+    B.table_clean = false;
     B.table = DevBuf(ctx, P.hash_cap * K.num_planes * 8);
     K.table = devp(B.table);
     const uint64_t kw = uint64_t(K.key_words) * P.hash_cap;
@@ -389,7 +397,10 @@ void reset_outputs(ExecPlan& P, ExecBuffers& B, hipStream_t st, bool init_table,
   if (init_table && K.group_mode != G_NONE && !P.use_part && !B.tbl_live) {
     const uint64_t slots = hash_mode(K.group_mode) ? P.hash_cap : P.dense_slots;
     const uint64_t kw = hash_mode(K.group_mode) ? uint64_t(K.key_words) * P.hash_cap : 0;
-    PGX_LAUNCH(st, "pgx_init_planes", pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
+    const bool clean = !hash_mode(K.group_mode) && B.table_clean && B.table.p && K.table == devp(B.table);
+    if (!clean)
+      PGX_LAUNCH(st, "pgx_init_planes", pgx_launch_init_planes(K.table, slots, K.num_planes, &K, K.keys, kw, K.key_state, st), "init planes");
+    B.table_clean = false;  // this execution's kernels accumulate into it
   }
 }
 
@@ -889,15 +900,22 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
     return std::max<uint64_t>(1, std::min<uint64_t>(limit, g));
   };
   if (dense_dev) {
-    uint64_t cap = guess(slots);
+    // a table of the plan's own of up to 64K slots is read whole, so the compaction can put it back clean (below)
+    const bool own = B.table.p && K.table == devp(B.table);
+    uint64_t cap = own && slots <= 65536 ? slots : guess(slots);
     for (;;) {
       const size_t bytes = 256 + size_t(cap) * 8 * (1 + K.num_planes);
       DevBuf res(ctx, bytes);
       PinnedBuf hres(ctx, bytes);
       hip_check(hipMemsetAsync(res.p, 0, 8, st), "memset");
       unsigned long long* rb = devp(res);
+      // the plan's own table, read whole: put its slots back to their initial values for the next execution
+      const bool reset = own && cap >= slots && slots <= (uint64_t(1) << 20) && K.num_planes <= 32;
+      uint32_t min_mask = 0;
+      for (int p = 0; p < K.num_planes; ++p)
+        if (K.plane_op[p] == P_MIN_ORD) min_mask |= 1u << p;
       PGX_LAUNCH(st, "pgx_compact", pgx_launch_compact(K.table, slots, K.num_planes, rb, reinterpret_cast<int64_t*>(rb + 32), rb + 32 + cap,
-                                   cap, st),
+                                   cap, reset ? 1 : 0, min_mask, st),
                 "compact");
       hip_check(hipMemcpyAsync(outs, B.dev() + B.off_outs, kOutsBytes, hipMemcpyDeviceToHost, st), "outputs D2H");
       hip_check(hipMemcpyAsync(hres.p, res.p, bytes, hipMemcpyDeviceToHost, st), "groups D2H");
@@ -909,6 +927,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
         cap = cnt;
         continue;
       }
+      B.table_clean = reset;
       ng = cnt;
       slot_ids.assign(reinterpret_cast<const int64_t*>(h + 32), reinterpret_cast<const int64_t*>(h + 32) + ng);
       planes.resize(ng * K.num_planes);
@@ -933,7 +952,7 @@ void finish_result(pgx_ctx* ctx, const pgx_query& q, ExecPlan& P, ExecBuffers& B
       unsigned long long* oplanes = rb + 32 + cap;
       unsigned long long* okeys = rb + 32 + cap * (1 + K.num_planes);
       hip_check(hipMemsetAsync(rb, 0, 8, st), "memset");
-      PGX_LAUNCH(st, "pgx_compact", pgx_launch_compact(K.table, slots, K.num_planes, rb, oslot, oplanes, cap, st),
+      PGX_LAUNCH(st, "pgx_compact", pgx_launch_compact(K.table, slots, K.num_planes, rb, oslot, oplanes, cap, 0, 0u, st),
                  "compact");
       PGX_LAUNCH(st, "pgx_gather_keys", pgx_launch_gather_keys(K.keys, oslot, rb, int64_t(cap), int(kw), okeys, st),
                  "gather keys");

@@ -40,9 +40,10 @@ extern "C" hipError_t pgx_launch_scan(const pgx::KQuery* q, int grid, int64_t ti
 extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t slots, int num_planes,
                                              const pgx::KQuery* q, unsigned long long* keys, uint64_t key_words,
                                              unsigned int* key_state, hipStream_t stream);
-extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
+extern "C" hipError_t pgx_launch_compact(unsigned long long* table, uint64_t slots, int num_planes,
                                          unsigned long long* counter, int64_t* out_slot,
-                                         unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream);
+                                         unsigned long long* out_planes, uint64_t cap_out, int reset,
+                                         uint32_t min_mask, hipStream_t stream);
 extern "C" hipError_t pgx_launch_gather_keys(const unsigned long long* keys, const int64_t* slot,
                                              const unsigned long long* n_dev, int64_t n, int kw, unsigned long long* out,
                                              hipStream_t stream);
@@ -965,6 +966,8 @@ struct ExecBuffers {
   size_t tbl_bytes = 0;  // in-arena dense table at off_outs + kOutsBytes (0: none)
   bool tbl_live = false;  // this execution's table is the in-arena one (alloc_outputs)
   DevBuf table, keys, key_state, masks;
+  uint64_t table_bytes = 0;  // dense table: size of `table`, kept across executions of a kept plan
+  bool table_clean = false;  // ... and its slots are at their initial values (the last compaction reset them)
   uint8_t* dev() const { return arena.as<uint8_t>(); }
 };
 

@@ -597,9 +597,11 @@ __device__ __forceinline__ unsigned int block_reserve(unsigned int* scan, unsign
 
 // Emit occupied slots: out_slot[i] = slot index, out_planes[p*cap_out + i] = plane value.
 // Small tables (dense key spaces, <= 2^20 slots): one counter reservation per wavefront, lanes in slot order.
-__global__ void pgx_compact_wave(const unsigned long long* table, uint64_t slots, int num_planes,
+// reset: every occupied slot is put back to its planes' initial values (ordered-min planes, bit p of min_mask: ~0; the
+// others 0) once read, so the next execution of a kept plan finds the table clean (no pgx_init_planes).
+__global__ void pgx_compact_wave(unsigned long long* table, uint64_t slots, int num_planes,
                                  unsigned long long* counter, int64_t* out_slot, unsigned long long* out_planes,
-                                 uint64_t cap_out) {
+                                 uint64_t cap_out, int reset, uint32_t min_mask) {
   const int lane = threadIdx.x & 63;
   for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); b < slots;
        b += (uint64_t)gridDim.x * blockDim.x) {
@@ -610,9 +612,13 @@ __global__ void pgx_compact_wave(const unsigned long long* table, uint64_t slots
     unsigned long long base = 0;
     if (lane == 0) base = atomicAdd(counter, static_cast<unsigned long long>(__popcll(m)));
     const unsigned long long i = __shfl(base, 0, 64) + __popcll(m & ((1ull << lane) - 1ull));
-    if (!live || i >= cap_out) continue;
-    out_slot[i] = static_cast<int64_t>(s);
-    for (int p = 0; p < num_planes; ++p) out_planes[p * cap_out + i] = table[p * slots + s];
+    if (!live) continue;
+    if (i < cap_out) {
+      out_slot[i] = static_cast<int64_t>(s);
+      for (int p = 0; p < num_planes; ++p) out_planes[p * cap_out + i] = table[p * slots + s];
+    }
+    if (reset)
+      for (int p = 0; p < num_planes; ++p) table[p * slots + s] = ((min_mask >> p) & 1u) ? ~0ull : 0ull;
   }
 }
 
@@ -2327,13 +2333,15 @@ extern "C" hipError_t pgx_launch_init_planes(unsigned long long* table, uint64_t
   return hipGetLastError();
 }
 
-extern "C" hipError_t pgx_launch_compact(const unsigned long long* table, uint64_t slots, int num_planes,
+extern "C" hipError_t pgx_launch_compact(unsigned long long* table, uint64_t slots, int num_planes,
                                          unsigned long long* counter, int64_t* out_slot,
-                                         unsigned long long* out_planes, uint64_t cap_out, hipStream_t stream) {
+                                         unsigned long long* out_planes, uint64_t cap_out, int reset,
+                                         uint32_t min_mask, hipStream_t stream) {
+  if (reset && (slots > (uint64_t(1) << 20) || cap_out < slots || num_planes > 32)) return hipErrorInvalidValue;
   if (slots <= (uint64_t(1) << 20)) {
     const int grid = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>((slots + 255) / 256, 4096)));
     hipLaunchKernelGGL(pgx::pgx_compact_wave, dim3(grid), dim3(256), 0, stream, table, slots, num_planes, counter,
-                       out_slot, out_planes, cap_out);
+                       out_slot, out_planes, cap_out, reset, min_mask);
     return hipGetLastError();
   }
   int grid = static_cast<int>(std::min<uint64_t>((slots + 4095) / 4096, 4096));

@@ -674,18 +674,26 @@ def trim_and_gather(q: _Query, r):
     L = N.lib()
     ncols, nf = len(q.group_cols), len(q.fns)
     out = []
+    total = C.c_int64(0)
+    N.check(L.pgx_result_num_groups(r, C.byref(total)))
+    shared = None  # every function keeps every group (the trim rule depends on the group count only): one gather
     for i in range(nf):
-        cap = C.c_int64(0)
-        N.check(L.pgx_result_trim(r, i, None, C.byref(cap)))
-        n = cap.value
-        idx = np.zeros(max(n, 1), dtype=np.int64)
-        N.check(L.pgx_result_trim(r, i, idx.ctypes.data, C.byref(cap)))
-        si = np.zeros(max(n * ncols, 1), dtype=np.int32)
-        di = np.zeros(max(n * ncols, 1), dtype=np.int32)
-        v = np.zeros(max(n * nf, 1), dtype=np.float64)
-        c = np.zeros(max(n * nf, 1), dtype=np.int64)
-        N.check(L.pgx_result_gather(r, idx.ctypes.data, n, si.ctypes.data, di.ctypes.data, v.ctypes.data,
-                                    c.ctypes.data))
+        if shared is None:
+            cap = C.c_int64(0)
+            N.check(L.pgx_result_trim(r, i, None, C.byref(cap)))
+            n = cap.value
+            idx = np.empty(max(n, 1), dtype=np.int64)
+            N.check(L.pgx_result_trim(r, i, idx.ctypes.data, C.byref(cap)))
+            si = np.empty(max(n * ncols, 1), dtype=np.int32)
+            di = np.empty(max(n * ncols, 1), dtype=np.int32)
+            v = np.empty(max(n * nf, 1), dtype=np.float64)
+            c = np.empty(max(n * nf, 1), dtype=np.int64)
+            N.check(L.pgx_result_gather(r, idx.ctypes.data, n, si.ctypes.data, di.ctypes.data, v.ctypes.data,
+                                        c.ctypes.data))
+            if n == total.value:
+                shared = (n, si, di, v, c)
+        else:
+            n, si, di, v, c = shared
         out.append((si[:n * ncols].reshape(ncols, n), di[:n * ncols].reshape(ncols, n), v[i * n:(i + 1) * n],
                     c[i * n:(i + 1) * n]))
     return out
