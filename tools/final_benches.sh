@@ -6,5 +6,5 @@ OUT=gpurun_out/final
 mkdir -p $OUT
 for wl in c5 c1 c2 c3 c4 c6 c7 c3d c3m2 c3f; do
   timeout -k 10 300 python bench.py --workload $wl > $OUT/${wl}_bench.json 2> $OUT/${wl}_bench.err
-  echo "$wl done: $(python tools/bench_summary.py $OUT/${wl}_bench.json | head -1)"
+  echo "$wl done: $(python tools/bench_summary.py $OUT/${wl}_bench.json)"
 done
