@@ -841,8 +841,6 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
       }
       e.ln("const u64 klo = ", klo, ";");
       if (h128) e.ln("const u64 khi = ", khi, ";");
-        e.ln("const int ls = ", h128 ? "pgx_lhash128(hk, hst, " + std::to_string(HS) + ", klo, khi)"
-                                     : "pgx_lhash64(hk, " + std::to_string(HS) + ", klo)", ";");
       std::vector<std::string> encs(naggs);
       for (int a = 0; a < naggs; ++a) {
         const int k = s.agg_kind[a];
@@ -858,11 +856,22 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
         if (k == A_MIN || k == A_MAX) encs[a] = C.fp ? "pgx_ord_f64(" + val + ")" : "pgx_ord_i64(" + val + ")";
         else encs[a] = C.fp ? "pgx_f64_bits(" + val + ")" : "(u64)" + val;
       }
-      e.ln("if (ls >= 0) {");
+      // the values (LDS image reads) are read before the probe, so their round trip overlaps the probe's
+      for (int a = 0; a < naggs; ++a)
+        if (s.agg_kind[a] != A_COUNT) {
+          e.ln("const u64 ev", a, " = ", encs[a], ";");
+          encs[a] = "ev" + std::to_string(a);
+        }
       if (hpack) {
         const int c = s.agg_col[0];
-        e.ln("  atomicAdd(&ht[ls], (1ull << ", s.dense_pack, ") + (u64)", img_value(s, c, img_off, "v" + std::to_string(c) + "[j]"),
-             ");");
+        e.ln("const u64 hv = (1ull << ", s.dense_pack, ") + (u64)", img_value(s, c, img_off, "v" + std::to_string(c) + "[j]"),
+             ";");
+      }
+      e.ln("const int ls = ", h128 ? "pgx_lhash128(hk, hst, " + std::to_string(HS) + ", klo, khi)"
+                                   : "pgx_lhash64(hk, " + std::to_string(HS) + ", klo)", ";");
+      e.ln("if (ls >= 0) {");
+      if (hpack) {
+        e.ln("  atomicAdd(&ht[ls], hv);");
       } else {
         e.ln("  atomicAdd(&ht[ls], 1ull);");
         for (int a = 0; a < naggs; ++a)
