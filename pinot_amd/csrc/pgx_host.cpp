@@ -569,10 +569,16 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
     // hash group-by: the workgroup's LDS table (keys, 128-bit key states, planes); 2048 slots when they fit beside the
     // images, down to 512 before an image is dropped
     const bool hashg = K.group_mode == G_HASH64 || K.group_mode == G_HASH128;
-    const int64_t hslot_bytes = hashg ? (K.group_mode == G_HASH128 ? 20 : 8) + 8 * K.num_planes : 0;
-    int hash_slots = hashg ? 2048 : 0;
+    // a packed count + sum table (COUNT + one integer SUM / AVG over an image: dense_pack below, pgx_jit.cpp hpack)
+    // holds one plane per slot: 4096 slots then fit beside a 16 KiB image (load 1/4 at C7's 1024 groups: shorter probes)
+    bool hp1 = hashg && K.num_planes == 2 && K.num_aggs == 1 && (K.agg_kind[0] == A_SUM || K.agg_kind[0] == A_AVG) &&
+               K.agg_col[0] >= 0 && !K.agg_fp[0] && J.cols[K.agg_col[0]].img != IMG_NONE;
+    auto hslot_bytes = [&]() -> int64_t {
+      return hashg ? (K.group_mode == G_HASH128 ? 20 : 8) + 8 * (hp1 ? 1 : K.num_planes) : 0;
+    };
+    int hash_slots = hashg ? (hp1 ? 4096 : 2048) : 0;
     auto lds_need = [&]() {
-      int64_t b = rch_bytes + (hashg ? hash_slots * hslot_bytes + 32 : 0);
+      int64_t b = rch_bytes + (hashg ? hash_slots * hslot_bytes() + 32 : 0);
       for (const JitCol& C : J.cols)
         if (C.img != IMG_NONE) b += ((int64_t(C.img_words) * 4 + 15) / 16) * 16;
       if (K.group_mode == G_DENSE_LDS) b += int64_t(P.dense_slots) * K.num_planes * 8;
@@ -588,6 +594,10 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         return;  // the dense LDS table alone does not fit: generic kernel
       }
       J.cols[big].img = IMG_NONE;
+    }
+    if (hp1 && J.cols[K.agg_col[0]].img == IMG_NONE) {  // the image went: no packed table, two planes per slot
+      hp1 = false;
+      while (hash_slots > 512 && lds_need() > lds_budget) hash_slots /= 2;
     }
     const int64_t lds = lds_need();
     J.T = lds <= 20 * 1024 ? 256 : (lds <= 40 * 1024 ? 512 : 1024);
@@ -683,6 +693,11 @@ void plan_jit(pgx_ctx* ctx, const pgx_query& q, pgx_segment* const* segs, int n,
         while (sb < 64 && std::ldexp(1.0L, sb) <= sum_max) ++sb;
         if (cb + sb <= 64) J.dense_pack = 64 - cb;
       }
+    }
+    if (hp1 && !J.dense_pack && hashg) {  // the packed add does not fit after all: two planes per slot
+      hp1 = false;
+      while (hash_slots > 512 && lds_need() > lds_budget) hash_slots /= 2;
+      J.hash_slots = hash_slots;
     }
     J.leafmask = P.fsm_on && P.lmask_off[members[0]] >= 0;
     J.compact = P.rchunk && !P.use_part;  // selective bitmap filters: aggregate the selected rows packed

@@ -94,6 +94,11 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const bool emit = s.group_mode == G_EMIT;
   const bool hashm = s.group_mode == G_HASH64 || s.group_mode == G_HASH128;
   const bool h128 = s.group_mode == G_HASH128;
+  // packed count + value-offset add in the LDS hash table (flushed per segment into the global table): one plane
+  const bool hpack = s.dense_pack > 0 && hashm && s.num_planes == 2 && s.agg_kind.size() == 1 &&
+                     (s.agg_kind[0] == A_SUM || s.agg_kind[0] == A_AVG) && !s.cols[s.agg_col[0]].fp &&
+                     s.cols[s.agg_col[0]].img != IMG_NONE;
+  const int htp = hpack ? 1 : s.num_planes;  // LDS hash planes
   const bool grouped = s.group_mode == G_DENSE_LDS || s.group_mode == G_DENSE_GLOBAL || emit || hashm;
   // ---- LDS layout: images, then the dense group table ----
   std::vector<int> img_off(ncols, -1);
@@ -121,7 +126,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     }
     lds = (lds + 15) & ~15;
     ht_off = lds;
-    lds += HS * s.num_planes * 8;
+    lds += HS * htp * 8;
   }
   // G_EMIT: per-wave LDS staging of the records, so that they leave as 64 lanes x 8 contiguous bytes per store
   // instead of R-strided 8-byte stores (each lane owns R consecutive rows).  A lane's R records sit at a pitch of
@@ -252,7 +257,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
     e.ln("u64* const ht = (u64*)(lds + ", ht_off / 4, ");");
     e.ln("for (int i = tid; i < ", HS * (h128 ? 2 : 1), "; i += PT) hk[i] = ~0ull;");
     if (h128) e.ln("for (int i = tid; i < ", HS, "; i += PT) hst[i] = 0u;");
-    e.ln("for (int i = tid; i < ", HS * s.num_planes, "; i += PT) {");
+    e.ln("for (int i = tid; i < ", HS * htp, "; i += PT) {");
     e.ln("  u64 z = 0ull;");
     for (int p = 1; p < s.num_planes; ++p)
       if (s.plane_op[p] == P_MIN_ORD) e.ln("  if (i / ", HS, " == ", p, ") z = ~0ull;");
@@ -404,10 +409,7 @@ std::string jit_source(const JitShape& s, int* lds_bytes_out) {
   const bool pack = s.dense_pack > 0 && s.group_mode == G_DENSE_LDS && s.num_planes == 2 && naggs == 1 &&
                     (s.agg_kind[0] == A_SUM || s.agg_kind[0] == A_AVG) && !s.cols[s.agg_col[0]].fp &&
                     s.cols[s.agg_col[0]].img != IMG_NONE && !emit;
-  // the same packed count + value-offset add in the LDS hash table (flushed per segment into the global table)
-  const bool hpack = s.dense_pack > 0 && hashm && s.num_planes == 2 && naggs == 1 &&
-                     (s.agg_kind[0] == A_SUM || s.agg_kind[0] == A_AVG) && !s.cols[s.agg_col[0]].fp &&
-                     s.cols[s.agg_col[0]].img != IMG_NONE;
+  // (hpack: the same packed count + value-offset add in the LDS hash table, decided above)
   for (int c = 0; c < ncols; ++c) {
     if (need_vb[c]) e.ln("const i64 vb", c, " = S->vbase[", c, "];");
     if (need_dict[c]) {
