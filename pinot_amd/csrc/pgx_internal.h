@@ -227,12 +227,16 @@ constexpr int kNarrowMaxBits2 = 10;  // second split (pgx_narrow_split): up to 1
 // with a setenv on another thread).  The whole set:
 //   PGX_JIT=0          the generic interpreter kernel instead of the generated (hiprtc) kernels, everywhere (A/B)
 //   PGX_PART_NARROW=0  sparse group-by through the 8-byte radix path instead of the narrow records; =direct: narrow
-//                      records carry value offsets wherever they fit (default: dictIds + LDS image when there is one)
+//                      records carry value offsets wherever they fit (default: dictIds + LDS image when there is one);
+//                      =gather: integer records carry the dictId's index in a global value table (IMG 5, tests)
 //   PGX_RCHUNK=0|1     bitmap programs evaluated by the separate pass / inside the query kernels (default: planner)
 //   PGX_RPROG=off|wave|seg|chunk|stack   bitmap-program kernel (off: no program fusion; default: planner)
 //   PGX_BATCH_SEGS=N   segments per batch of a long segment list on its first execution (0: one launch)
 //   PGX_DEBUG=opt,...  part_small (radix buckets start undersized), narrow_k2=N (coarser narrow partitions),
-//                      narrow_log (which sparse path ran, on stderr), host_profile (planning phases on stderr)
+//                      narrow_log (which sparse path ran, hash-table regrowth; on stderr), host_profile (planning phases
+//                      on stderr); A/B switches measured slower and kept off: nunit=16 (16-record narrow
+//                      scan units), pf2 (narrow scans load two tiles ahead), noimg (no LDS value images in the query
+//                      kernels), head=N (a lone replay's first part is 1/N of the segments)
 // and, outside the query: PGX_PLAN_CACHE=0 (process-wide), PGX_JIT_CACHE=<dir> / PGX_JIT_DUMP=<dir> (the compiler).
 enum RProgKind { RPROG_AUTO = -1, RPROG_OFF = 0, RPROG_WAVE = 1, RPROG_SEG = 2, RPROG_CHUNK = 3, RPROG_STACK = 4 };
 struct Knobs {
